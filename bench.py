@@ -1,0 +1,152 @@
+"""Benchmark: config C of BASELINE.json on MI355X.
+
+A step is one BSP round of the hot path (HyParView handlers + timers,
+Plumtree broadcast, message route) over every node of a 2^20-node overlay
+(steady state after a doubling bootstrap; a broadcast from node 0 every 10
+rounds).  Prints ONE JSON line (rank 0).  See DESIGN.md section 5.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0           # MI355X HBM3E spec (MI355X_MICROARCH.md)
+S_NODE = 416                    # algorithmic state bytes per processed node
+S_MSG = 64                      # message record bytes
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=50)
+    p.add_argument("--warmup", type=int, default=10)
+    p.add_argument("--nodes", type=int, default=1 << 20)
+    p.add_argument("--seed", type=int, default=1)
+    p.add_argument("--settle", type=int, default=60, help="untimed rounds after bootstrap")
+    p.add_argument("--cpu-sample-nodes", type=int, default=1 << 16)
+    p.add_argument("--cpu-sample-rounds", type=int, default=40)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    return p.parse_args()
+
+
+def cpu_baseline(args):
+    """The CPU oracle (port of the reference handlers, 1 thread) on a bounded
+    sample of the same workload: 2^16 nodes, same bootstrap, timed rounds
+    with the same broadcast cadence."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from _oracle import Oracle
+    from partisan_amd import workloads as W
+    from partisan_amd.sim import default_config
+
+    n = args.cpu_sample_nodes
+    o = Oracle(default_config(n_nodes=n, seed=args.seed))
+    o.run_schedule(W.doubling_join(n, args.seed), 40)
+    k = 0
+    t0 = time.perf_counter()
+    msgs = 0
+    for r in range(args.cpu_sample_rounds):
+        if r % 10 == 0:
+            o.broadcast(0, k)
+            k += 1
+        st = o.step(1)
+        msgs += int(st["emitted"].sum())
+    dt = time.perf_counter() - t0
+    return {"value": n * args.cpu_sample_rounds / dt, "unit": "node-rounds/s", "cores": 1,
+            "kind": "port",
+            "msgs_per_sec": msgs / dt,
+            "sample": f"oracle/psim_oracle.c, {n} nodes, {args.cpu_sample_rounds} steady-state "
+                      f"rounds after a doubling bootstrap, broadcast every 10 rounds, 1 thread"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo")
+    from partisan_amd import Simulator
+    from partisan_amd import workloads as W
+    from partisan_amd.sim import default_config
+
+    n = args.nodes
+    cfg = default_config(n_nodes=n, seed=args.seed + rank)
+    cfg.device = int(os.environ.get("LOCAL_RANK", "0"))
+    sim = Simulator(cfg)
+    boot = W.doubling_join(n, args.seed + rank)
+    sim.run_schedule(boot, boot[-1][0] + 1 + args.settle)
+
+    state = {"k": 0}
+
+    def round_events(i):
+        if i % 10 == 0:
+            sim.broadcast(0, state["k"] % 0x10000)
+            state["k"] += 1
+
+    for i in range(args.warmup):
+        round_events(i)
+        sim.step(1)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    stats = []
+    kt = {}
+    for i in range(args.steps):
+        round_events(args.warmup + i)
+        stats.append(sim.step(1))
+        for name, (ms, cnt) in sim.kernel_times().items():
+            a, b = kt.get(name, (0.0, 0))
+            kt[name] = (a + ms, b + cnt)
+    t1 = time.perf_counter()
+    st = np.concatenate(stats)
+    dt = t1 - t0
+    if world > 1:
+        import torch
+        t = torch.tensor([dt], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    msgs = int(st["emitted"].sum())
+    node_rounds = n * args.steps * world
+    # roofline of the dominant kernel (consume): algorithmic bytes per launch
+    proc = int(st["nodes_processed"].sum())
+    deliv = int(st["delivered"].sum())
+    alg_bytes = proc * 2 * S_NODE + deliv * S_MSG + msgs * (S_MSG + 4)
+    c_ms, c_n = kt.get("consume", (0.0, 0))
+    per_launch_bytes = alg_bytes / max(1, c_n)
+    per_launch_s = (c_ms / 1e3) / max(1, c_n)
+    achieved = per_launch_bytes / per_launch_s / 1e9 if per_launch_s > 0 else 0.0
+    out = {
+        "metric": "simulated node-rounds/sec (+ msgs/sec), 1M-node HyParView+Plumtree",
+        "value": node_rounds / dt,
+        "unit": "node-rounds/s",
+        "msgs_per_sec": msgs * world / dt,
+        "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": dt / args.steps * 1e3,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "u32", "data": "synthetic",
+        "config": {"workload": "C: HyParView+Plumtree, doubling bootstrap, steady state, "
+                               "broadcast from node 0 every 10 rounds",
+                   "nodes": n, "seed": args.seed, "parallelism": "replicas" if world > 1 else "1 GPU"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "kernel": "k_consume", "alg_bytes_per_launch": per_launch_bytes,
+                     "avg_launch_ms": per_launch_s * 1e3},
+        "kernel_ms_per_step": {k: v[0] / args.steps for k, v in kt.items()},
+        "overflow": int(st["overflow"].sum()),
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(args)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

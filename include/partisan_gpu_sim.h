@@ -1,0 +1,194 @@
+/*
+ * partisan_gpu_sim.h -- C ABI of the MI355X overlay simulator.
+ *
+ * This is the drop-in boundary for the hot path named in BASELINE.json
+ * `north_star`: partisan's HyParView membership manager and Plumtree
+ * broadcast, simulated one BSP round at a time with all node state resident
+ * in HBM.  The Erlang host keeps partisan's callback surfaces and drives this
+ * library through a NIF shim (erlang/c_src/partisan_gpu_sim_nif.c); Python
+ * drives it through ctypes (partisan_amd/_lib.py).
+ *
+ * Each entry point replaces one reference interface (cited as file:line under
+ * /root/reference, read-only):
+ *
+ *   psim_create / psim_destroy
+ *       partisan_hyparview_peer_service_manager:init/1          (:289-354)
+ *       partisan_plumtree_broadcast:init/1                      (:251-264)
+ *       config keys of partisan_config:init/0                   (partisan_config.erl:102-145)
+ *   psim_join
+ *       partisan_peer_service:join/1 -> hyparview join/1,
+ *       handle_cast({join, Peer})                               (hyparview:225-226, :500-515)
+ *   psim_crash
+ *       connection death -> handle_info({'EXIT', ...})          (hyparview:609-654)
+ *   psim_set_partition / psim_clear_partition
+ *       inject_partition/2, resolve_partition/1                 (hyparview:244-250, :1731-1797)
+ *       (modelled as a network partition)
+ *   psim_broadcast
+ *       partisan_plumtree_broadcast:broadcast/2 with the default
+ *       partisan_plumtree_backend handler                       (plumtree:176-178, backend:179-200)
+ *   psim_step
+ *       one BSP round of every node's timers and inbox:
+ *       hyparview handle_message/2 (:693-1166), handle_info timers (:542-607),
+ *       plumtree handle_cast/2 (:282-336), lazy_tick (:341-345)
+ *   psim_get_nodes
+ *       debug getters active/0, passive/0 (hyparview:261-281),
+ *       plumtree debug_get_peers/2,3 (:222-231), broadcast_members/0 (:188-195)
+ *
+ * Conventions: every function returns 0 on success or a negative PSIM_E*
+ * code; psim_strerror() names it.  No exceptions or aborts cross the ABI.
+ * A handle is thread-compatible (not thread-safe): the NIF shim serialises
+ * calls per handle and runs psim_step on a dirty CPU scheduler.
+ * The library owns all device memory; the caller owns every host buffer.
+ */
+#ifndef PARTISAN_GPU_SIM_H
+#define PARTISAN_GPU_SIM_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PSIM_ABI_VERSION 1
+
+/* error codes */
+#define PSIM_OK 0
+#define PSIM_EINVAL -1      /* bad argument / config                 */
+#define PSIM_ENOMEM -2      /* device or host allocation failed       */
+#define PSIM_EDEVICE -3     /* HIP runtime error                      */
+#define PSIM_ESTATE -4      /* call not valid in the current state    */
+#define PSIM_ERANGE -5      /* node id out of range                   */
+#define PSIM_ECOMM -6       /* RCCL / transport error                 */
+#define PSIM_EUNSUPPORTED -7
+
+/* message types (the record `type` field; also stats indices) */
+enum psim_msg_type {
+    PSIM_MSG_JOIN = 0,              /* {join, Peer, Tag, Epoch}                  hyparview:703  */
+    PSIM_MSG_FORWARD_JOIN = 1,      /* {forward_join, Peer, Tag, Epoch, TTL, S}  hyparview:808  */
+    PSIM_MSG_NEIGHBOR = 2,          /* {neighbor, Peer, Tag, DisconnectId, _}    hyparview:774  */
+    PSIM_MSG_DISCONNECT = 3,        /* {disconnect, Peer, DisconnectId}          hyparview:926  */
+    PSIM_MSG_NEIGHBOR_REQUEST = 4,  /* {neighbor_request, Peer, high, ...}       hyparview:975  */
+    PSIM_MSG_NEIGHBOR_ACCEPTED = 5, /* {neighbor_accepted, Peer, Tag, Id, Ex}    hyparview:1070 */
+    PSIM_MSG_NEIGHBOR_REJECTED = 6, /* {neighbor_rejected, Peer, Ex}             hyparview:1056 */
+    PSIM_MSG_SHUFFLE = 7,           /* {shuffle, Exchange, TTL, Sender}          hyparview:1095 */
+    PSIM_MSG_SHUFFLE_REPLY = 8,     /* {shuffle_reply, Exchange, Sender}         hyparview:1091 */
+    PSIM_MSG_PT_BROADCAST = 9,      /* {broadcast, Id, M, Mod, Round, Root, From} plumtree:288 */
+    PSIM_MSG_PT_PRUNE = 10,         /* {prune, Root, From}                       plumtree:294  */
+    PSIM_MSG_PT_IHAVE = 11,         /* {i_have, Id, Mod, Round, Root, From}      plumtree:299  */
+    PSIM_MSG_PT_IGNORED_IHAVE = 12, /* {ignored_i_have, ...}                     plumtree:304  */
+    PSIM_MSG_PT_GRAFT = 13,         /* {graft, Id, Mod, Round, Root, From}       plumtree:308  */
+    PSIM_MSG_NTYPES = 16
+};
+
+/* Plumtree peer identities: an atom name is the bare node id; a node_spec
+ * map (myself(), From, Root) has this bit set.  Erlang term order puts every
+ * atom before every map, which is exactly unsigned order of the encoding.
+ * See SURVEY.md App. A Q6 and plumtree:662-663. */
+#define PSIM_MAP_BIT 0x80000000u
+#define PSIM_NONE 0xFFFFFFFFu
+
+/* capacities of the fixed-size per-node tables */
+#define PSIM_ACTIVE_CAP 8
+#define PSIM_PASSIVE_CAP 32
+#define PSIM_IDMAP_CAP 32   /* sent_message_map / recv_message_map slots */
+#define PSIM_PT_MEMBERS_CAP 8
+#define PSIM_PT_SET_CAP 16
+#define PSIM_PT_OUT_CAP 32
+#define PSIM_EXCHANGE_CAP 8
+
+typedef struct psim_config {
+    uint32_t abi_version;        /* must be PSIM_ABI_VERSION */
+    uint32_t n_nodes;            /* global node-id space [0, n_nodes) */
+    uint64_t seed;               /* Philox key (partisan_config random_seed) */
+    /* HyParView keys, partisan_config.erl:102-145 (init/0 defaults) */
+    uint32_t max_active_size;    /* 6, includes self */
+    uint32_t min_active_size;    /* 3 */
+    uint32_t max_passive_size;   /* 30 */
+    uint32_t arwl;               /* 5 */
+    uint32_t prwl;               /* 30 */
+    uint32_t k_active;           /* 3  (hyparview:1560) */
+    uint32_t k_passive;          /* 4  (hyparview:1564) */
+    uint32_t shuffle_period;     /* rounds; passive_view_shuffle_period 10000 ms */
+    uint32_t promotion_period;   /* rounds; RANDOM_PROMOTION_INTERVAL 5000 ms */
+    uint32_t random_promotion;   /* 1 */
+    uint32_t persist_epoch;      /* 0: epoch restarts at 1 (no partisan_data_dir) */
+    /* Plumtree */
+    uint32_t plumtree;           /* 1: run the broadcast layer */
+    uint32_t lazy_tick_period;   /* rounds; DEFAULT_LAZY_TICK_PERIOD 1000 ms */
+    /* execution */
+    int32_t device;              /* HIP device ordinal, -1 = current */
+    uint32_t n_shards;           /* node-range shards of this process (virtual shards), 1 */
+    uint32_t shard_rank;         /* RCCL rank (multi-process), 0 */
+    uint32_t shard_world;        /* RCCL world size, 1 */
+    const void *comm_id;         /* ncclUniqueId bytes when shard_world > 1, else NULL */
+    uint64_t max_msgs_per_round; /* 0 = auto */
+    uint32_t reserved[8];
+} psim_config;
+
+typedef struct psim_round_stats {
+    uint64_t round;                          /* round number just executed */
+    uint64_t emitted[PSIM_MSG_NTYPES];       /* messages sent (successful sends) by type */
+    uint64_t delivered[PSIM_MSG_NTYPES];     /* messages processed by a live recipient */
+    uint64_t dropped;                        /* messages whose recipient was down */
+    uint64_t nodes_up;
+    uint64_t nodes_processed;                /* nodes with inbox, timer or event work */
+    uint64_t exits;                          /* EXIT events handled */
+    uint64_t send_fail;                      /* sends refused: no connection */
+    uint64_t first_deliveries;               /* plumtree merge() == true this round */
+    uint64_t overflow;                       /* fixed-table overflows (must be 0 in parity runs) */
+    uint64_t digest;                         /* sum of per-message hashes of emitted messages */
+    uint64_t state_bytes;                    /* algorithmic state bytes read+written */
+    uint64_t reserved[4];
+} psim_round_stats;
+
+/* Canonical per-node view (inspection; unused slots zero). */
+typedef struct psim_node_view {
+    uint32_t up, epoch, start_round, pt_root;
+    uint64_t rng_ctr;
+    uint32_t act_n, pas_n;
+    uint32_t act[PSIM_ACTIVE_CAP];           /* sets:to_list order, self included */
+    uint32_t pas[PSIM_PASSIVE_CAP];          /* sets:to_list order */
+    uint32_t sent_n, sent_head, recv_n, recv_head;
+    uint32_t sent_peer[PSIM_IDMAP_CAP], sent_id[PSIM_IDMAP_CAP];
+    uint32_t recv_peer[PSIM_IDMAP_CAP], recv_id[PSIM_IDMAP_CAP];
+    uint32_t pt_all_n, pt_common_n, pt_eager_n, pt_lazy_n, pt_out_n, pt_pad;
+    uint32_t pt_all[PSIM_PT_MEMBERS_CAP], pt_common[PSIM_PT_MEMBERS_CAP];
+    uint32_t pt_eager[PSIM_PT_SET_CAP], pt_lazy[PSIM_PT_SET_CAP];
+    uint32_t pt_out_peer[PSIM_PT_OUT_CAP], pt_out_msg[PSIM_PT_OUT_CAP], pt_out_round[PSIM_PT_OUT_CAP];
+    uint32_t have, trk_round, trk_hop, pad1;
+} psim_node_view;
+
+typedef struct psim_handle psim_handle;
+
+void psim_default_config(psim_config *cfg);
+int psim_create(const psim_config *cfg, psim_handle **out);
+void psim_destroy(psim_handle *h);
+const char *psim_strerror(int code);
+int psim_abi_version(void);
+
+/* Events take effect at the start of the next round. */
+int psim_join(psim_handle *h, const uint32_t *nodes, const uint32_t *contacts, size_t n);
+int psim_crash(psim_handle *h, const uint32_t *nodes, size_t n);
+int psim_set_partition(psim_handle *h, const uint8_t *group, size_t n);
+int psim_clear_partition(psim_handle *h);
+int psim_broadcast(psim_handle *h, uint32_t root, uint32_t msg_id);
+
+/* Run n_rounds BSP rounds; stats (may be NULL) receives one entry per round. */
+int psim_step(psim_handle *h, uint32_t n_rounds, psim_round_stats *stats);
+
+/* Inspection: views of nodes [first, first+count) into caller buffers. */
+int psim_get_nodes(psim_handle *h, uint32_t first, uint32_t count, psim_node_view *out);
+int psim_get_round(psim_handle *h, uint64_t *round);
+/* Per-kernel device time (ms) accumulated over the last psim_step call:
+ * names[i] is a static string; returns the number of entries. */
+int psim_kernel_times(psim_handle *h, const char **names, double *ms, uint64_t *launches, int cap);
+
+/* RCCL bootstrap for multi-process sharding (rank 0 creates, all pass it in cfg). */
+int psim_comm_id_size(void);
+int psim_get_comm_id(void *buf, size_t cap);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PARTISAN_GPU_SIM_H */

@@ -1,0 +1,1009 @@
+/*
+ * oracle/psim_oracle.c -- TEST INFRASTRUCTURE ONLY.  Not part of the product.
+ *
+ * A deliberately plain, single-threaded CPU restatement of partisan's
+ * HyParView peer-service manager and Plumtree broadcast under the BSP round
+ * model R0.  Only tests/, __graft_entry__.smoke() and
+ * bench.py's cpu_baseline leg may load it, and only as the checker.  The
+ * product (libpartisan_gpu_sim.so) never links or calls it.
+ *
+ * Style: views are kept as lists in sets:to_list/1 order and every handler is
+ * written as a transliteration of the Erlang clause it cites, with the
+ * list operations (--, lists:usort, lists:sublist(shuffle(...))) spelled out.
+ * The GPU engine (partisan_amd/csrc/psim_engine.hip) is an independent
+ * data-oriented implementation of the same model; the parity tests compare the
+ * two bit for bit.
+ *
+ * PARITY UNPINNED against the Erlang reference: /root/reference holds no
+ * golden vectors for this path and no Erlang VM
+ * exists in this image, so the reference cannot be run to produce any.  This
+ * oracle is pinned only by the reference's behavioural invariants
+ * (test/partisan_SUITE.erl:2044-2108 connectivity + symmetry,
+ *  :2024-2041 crashed node leaves every view, :1955-1994 delivery), which
+ * tests/test_oracle.py checks, and by line-by-line citation.
+ *
+ * Exported symbols mirror include/partisan_gpu_sim.h with an `orc_` prefix.
+ */
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../include/partisan_gpu_sim.h"
+
+/* ------------------------------------------------------------------ RNG -- */
+/* Philox4x32-10 (Salmon et al. 2011).  key = seed, counter = (draw#, node,
+ * stream).  One 58-bit value per draw, the width of OTP's exsplus
+ * (partisan_config.erl:154-170 seeds exsplus; the harness installs a
+ * Philox-backed rand alg handler with bits=58). */
+static void philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0,
+                   uint32_t k1, uint32_t out[4]) {
+    for (int i = 0; i < 10; i++) {
+        uint64_t p0 = (uint64_t)0xD2511F53u * c0;
+        uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
+        uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
+        uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+        c0 = n0;
+        c1 = (uint32_t)p1;
+        c2 = n2;
+        c3 = (uint32_t)p0;
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+    out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
+}
+
+#define STREAM_HYPARVIEW 0u
+#define TWO58 ((uint64_t)1 << 58)
+
+typedef struct node {
+    uint32_t up, epoch, start_round, join_contact;
+    uint64_t rng;
+    uint32_t act[PSIM_ACTIVE_CAP]; uint32_t act_n;
+    uint32_t pas[PSIM_PASSIVE_CAP]; uint32_t pas_n;
+    uint32_t sent_peer[PSIM_IDMAP_CAP], sent_id[PSIM_IDMAP_CAP], sent_n, sent_head;
+    uint32_t recv_peer[PSIM_IDMAP_CAP], recv_id[PSIM_IDMAP_CAP], recv_n, recv_head;
+    uint32_t pt_all[PSIM_PT_MEMBERS_CAP], pt_all_n;
+    uint32_t pt_common[PSIM_PT_MEMBERS_CAP], pt_common_n;
+    uint32_t pt_root;
+    uint32_t pt_eager[PSIM_PT_SET_CAP], pt_eager_n;
+    uint32_t pt_lazy[PSIM_PT_SET_CAP], pt_lazy_n;
+    uint32_t out_peer[PSIM_PT_OUT_CAP], out_msg[PSIM_PT_OUT_CAP], out_round[PSIM_PT_OUT_CAP], out_n;
+    uint32_t have, trk_round, trk_hop;
+} node;
+
+typedef struct omsg {
+    uint32_t dst, src, seq;
+    uint32_t type, ttl, nex;
+    uint32_t a0, a1, a2;
+    uint32_t ex[PSIM_EXCHANGE_CAP];
+} omsg;
+
+typedef struct msgvec { omsg *v; size_t n, cap; } msgvec;
+
+struct psim_handle {
+    psim_config cfg;
+    uint32_t N;
+    node *nodes;
+    uint8_t *part, *crashed_now;
+    uint64_t round;
+    msgvec inbox, out;              /* inbox sorted by (dst, src, seq) */
+    size_t *in_beg;                 /* N+1 offsets into inbox */
+    /* pending events */
+    uint32_t *pend_crash; size_t pend_crash_n, pend_crash_cap;
+    uint32_t *pend_join, *pend_contact; size_t pend_join_n, pend_join_cap;
+    uint8_t *pend_part; int pend_part_set, pend_part_clear;
+    int pend_bcast; uint32_t pend_root, pend_msg;
+    uint32_t bcast_root;            /* single-root restriction */
+    uint32_t origin_node, origin_msg; int origin_now;
+    uint32_t tracked_msg;
+    psim_round_stats *st;           /* stats of the round being executed */
+};
+
+/* per-node execution context */
+typedef struct ctx {
+    struct psim_handle *h;
+    node *s;
+    uint32_t me;
+    uint32_t seq;
+} ctx;
+
+static uint64_t draw58(ctx *c) {
+    uint32_t o[4];
+    uint64_t k = c->s->rng++;
+    philox((uint32_t)k, (uint32_t)(k >> 32), c->me, STREAM_HYPARVIEW, (uint32_t)c->h->cfg.seed,
+           (uint32_t)(c->h->cfg.seed >> 32), o);
+    return ((((uint64_t)o[1]) << 32) | o[0]) >> 6;
+}
+
+/* rand:uniform/1 for a 58-bit alg handler (OTP rand.erl ?uniform_range):
+ * V < N -> V+1; else I = V rem N, accept when V - I =< 2^58 - N. */
+static uint32_t uniform_n(ctx *c, uint32_t n) {
+    for (;;) {
+        uint64_t v = draw58(c);
+        if (v < n) return (uint32_t)v + 1;
+        uint64_t i = v % n;
+        if (v - i <= TWO58 - n) return (uint32_t)i + 1;
+    }
+}
+
+/* rand:uniform/0 as a sort key: (V bsr 5) * 2^-53 -- the 53-bit integer is an
+ * order-preserving stand-in for the float. */
+static uint64_t uniform_key(ctx *c) { return draw58(c) >> 5; }
+
+/* ------------------------------------------------------- sets v1 order -- */
+/* OTP sets (v1) with <= 80 elements: 16 buckets, element prepended in its
+ * bucket, to_list yields bucket 1..16, oldest first.
+ * bucket16() stands in for erlang:phash(NodeSpec, 16): see DESIGN.md. */
+static uint32_t bucket16(uint32_t id) {
+    uint32_t h = id;
+    h ^= h >> 16; h *= 0x85EBCA6Bu; h ^= h >> 13; h *= 0xC2B2AE35u; h ^= h >> 16;
+    return h & 15u;
+}
+
+static int list_member(const uint32_t *l, uint32_t n, uint32_t e) {
+    for (uint32_t i = 0; i < n; i++)
+        if (l[i] == e) return 1;
+    return 0;
+}
+
+/* sets:add_element/2 */
+static void set_add(uint32_t *l, uint32_t *n, uint32_t e) {
+    if (list_member(l, *n, e)) return;
+    uint32_t b = bucket16(e), pos = *n;
+    for (uint32_t i = 0; i < *n; i++)
+        if (bucket16(l[i]) > b) { pos = i; break; }
+    for (uint32_t i = *n; i > pos; i--) l[i] = l[i - 1];
+    l[pos] = e;
+    (*n)++;
+}
+
+/* sets:del_element/2 */
+static void set_del(uint32_t *l, uint32_t *n, uint32_t e) {
+    uint32_t j = 0;
+    for (uint32_t i = 0; i < *n; i++)
+        if (l[i] != e) l[j++] = l[i];
+    for (uint32_t i = j; i < *n; i++) l[i] = 0;
+    *n = j;
+}
+
+/* List -- Omit (elements unique, so a filter) */
+static uint32_t list_subtract(const uint32_t *l, uint32_t n, const uint32_t *omit, uint32_t no,
+                              uint32_t *out) {
+    uint32_t k = 0;
+    for (uint32_t i = 0; i < n; i++)
+        if (!list_member(omit, no, l[i])) out[k++] = l[i];
+    return k;
+}
+
+static int cmp_u32(const void *a, const void *b) {
+    uint32_t x = *(const uint32_t *)a, y = *(const uint32_t *)b;
+    return x < y ? -1 : x > y;
+}
+
+/* lists:usort/1 over node ids (term order of the harness node_specs = id order) */
+static uint32_t usort(uint32_t *l, uint32_t n) {
+    if (n == 0) return 0;
+    qsort(l, n, sizeof(uint32_t), cmp_u32);
+    uint32_t k = 1;
+    for (uint32_t i = 1; i < n; i++)
+        if (l[i] != l[k - 1]) l[k++] = l[i];
+    return k;
+}
+
+/* select_random/2, hyparview:1346-1356: index = rand:uniform(length(List)),
+ * no draw when the list is empty (uniform(0) raises before drawing). */
+static uint32_t select_random(ctx *c, const uint32_t *view, uint32_t n, const uint32_t *omit,
+                              uint32_t no) {
+    uint32_t tmp[PSIM_PASSIVE_CAP];
+    uint32_t k = list_subtract(view, n, omit, no, tmp);
+    if (k == 0) return PSIM_NONE;
+    return tmp[uniform_n(c, k) - 1];
+}
+
+/* select_random_sublist/2 + shuffle/1, hyparview:1359-1361, :1586-1587:
+ * one rand:uniform() key per element in to_list order, lists:sort of
+ * {Key, Elem} tuples, then lists:sublist(.., K). */
+static uint32_t select_random_sublist(ctx *c, const uint32_t *view, uint32_t n, uint32_t k,
+                                      uint32_t *out) {
+    uint64_t key[PSIM_PASSIVE_CAP];
+    uint32_t el[PSIM_PASSIVE_CAP];
+    for (uint32_t i = 0; i < n; i++) { key[i] = uniform_key(c); el[i] = view[i]; }
+    for (uint32_t i = 1; i < n; i++) {       /* insertion sort by (key, elem) */
+        uint64_t kk = key[i]; uint32_t ee = el[i]; int j = (int)i - 1;
+        while (j >= 0 && (key[j] > kk || (key[j] == kk && el[j] > ee))) {
+            key[j + 1] = key[j]; el[j + 1] = el[j]; j--;
+        }
+        key[j + 1] = kk; el[j + 1] = ee;
+    }
+    uint32_t m = n < k ? n : k;
+    for (uint32_t i = 0; i < m; i++) out[i] = el[i];
+    return m;
+}
+
+/* ------------------------------------------------------------ emission -- */
+static uint64_t mix64(uint64_t z) {
+    z ^= z >> 30; z *= 0xBF58476D1CE4E5B9ull;
+    z ^= z >> 27; z *= 0x94D049BB133111EBull;
+    z ^= z >> 31;
+    return z;
+}
+
+static uint64_t msg_hash(const omsg *m) {
+    uint64_t h = 0x9E3779B97F4A7C15ull ^ (((uint64_t)m->dst << 32) | m->src);
+    h = mix64(h ^ (((uint64_t)m->seq << 32) | (m->type << 16) | (m->ttl << 8) | m->nex));
+    h = mix64(h ^ (((uint64_t)m->a0 << 32) | m->a1));
+    h = mix64(h ^ m->a2);
+    for (uint32_t i = 0; i < m->nex; i++) h = mix64(h ^ (((uint64_t)m->ex[i] << 32) | i));
+    return h;
+}
+
+static void vec_push(msgvec *v, const omsg *m) {
+    if (v->n == v->cap) {
+        v->cap = v->cap ? v->cap * 2 : 1024;
+        v->v = (omsg *)realloc(v->v, v->cap * sizeof(omsg));
+    }
+    v->v[v->n++] = *m;
+}
+
+static void emit(ctx *c, uint32_t dst, uint32_t type, uint32_t ttl, uint32_t a0, uint32_t a1,
+                 uint32_t a2, const uint32_t *ex, uint32_t nex) {
+    omsg m;
+    memset(&m, 0, sizeof m);
+    m.dst = dst; m.src = c->me; m.seq = c->seq++;
+    m.type = type; m.ttl = ttl; m.nex = nex;
+    m.a0 = a0; m.a1 = a1; m.a2 = a2;
+    for (uint32_t i = 0; i < nex; i++) m.ex[i] = ex[i];
+    vec_push(&c->h->out, &m);
+    c->h->st->emitted[type]++;
+    c->h->st->digest += msg_hash(&m);
+}
+
+/* maybe_connect + find: the connection attempt succeeds iff the peer's
+ * manager is running and no network partition separates the two
+ * (partisan_util.erl:75-134; partition model DESIGN.md). */
+static int connect_ok(ctx *c, uint32_t dst) {
+    struct psim_handle *h = c->h;
+    if (dst >= h->N || dst == c->me) return 0;
+    return h->nodes[dst].up && h->part[dst] == h->part[c->me];
+}
+
+/* do_send_message/3 after maybe_connect (hyparview:1274-1343): on success
+ * partisan_util:dispatch_pid/1 draws rand:uniform(1) (util:190-195). */
+static int hv_send(ctx *c, uint32_t dst, uint32_t type, uint32_t ttl, uint32_t a0, uint32_t a1,
+                   const uint32_t *ex, uint32_t nex) {
+    if (!connect_ok(c, dst)) { c->h->st->send_fail++; return 0; }
+    (void)uniform_n(c, 1);
+    emit(c, dst, type, ttl, a0, a1, 0, ex, nex);
+    return 1;
+}
+
+/* ----------------------------------------------------- disconnect ids -- */
+#define ID(e, n) (((uint32_t)(e) << 20) | (uint32_t)(n))
+#define ID_E(id) ((id) >> 20)
+#define ID_C(id) ((id) & 0xFFFFFu)
+
+static int map_find(const uint32_t *peer, uint32_t n, uint32_t p) {
+    for (uint32_t i = 0; i < n; i++)
+        if (peer[i] == p) return (int)i;
+    return -1;
+}
+
+/* dict:store/3 into a fixed table; when full the oldest slot is replaced
+ * (counted as overflow). */
+static void map_store(ctx *c, uint32_t *peer, uint32_t *id, uint32_t *n, uint32_t *head,
+                      uint32_t p, uint32_t v) {
+    int i = map_find(peer, *n, p);
+    if (i >= 0) { id[i] = v; return; }
+    if (*n < PSIM_IDMAP_CAP) { peer[*n] = p; id[*n] = v; (*n)++; return; }
+    c->h->st->overflow++;
+    peer[*head] = p; id[*head] = v;
+    *head = (*head + 1) % PSIM_IDMAP_CAP;
+}
+
+/* get_current_id/2, hyparview:1622-1630 */
+static uint32_t current_id(ctx *c, uint32_t p) {
+    int i = map_find(c->s->recv_peer, c->s->recv_n, p);
+    return i >= 0 ? c->s->recv_id[i] : ID(1, 0);
+}
+
+/* get_next_id/3, hyparview:1633-1639 */
+static uint32_t next_id(ctx *c, uint32_t p) {
+    int i = map_find(c->s->sent_peer, c->s->sent_n, p);
+    if (i >= 0 && ID_E(c->s->sent_id[i]) == c->s->epoch) return c->s->sent_id[i] + 1;
+    return ID(c->s->epoch, 1);
+}
+
+/* is_addable/3 integer-epoch clause, hyparview:1670-1676 */
+static int addable_epoch(ctx *c, uint32_t pe, uint32_t p) {
+    int i = map_find(c->s->sent_peer, c->s->sent_n, p);
+    if (i < 0) return 1;
+    return pe >= ID_E(c->s->sent_id[i]);
+}
+
+/* is_addable/3 disconnect-id clause, hyparview:1656-1669 */
+static int addable_id(ctx *c, uint32_t d, uint32_t p) {
+    int i = map_find(c->s->sent_peer, c->s->sent_n, p);
+    if (i < 0) return 1;
+    uint32_t e = ID_E(c->s->sent_id[i]), n = ID_C(c->s->sent_id[i]);
+    if (ID_E(d) > e) return 1;
+    if (ID_E(d) == e) return ID_C(d) >= n;
+    return 0;
+}
+
+/* is_valid_disconnect/3, hyparview:1642-1653 */
+static int valid_disconnect(ctx *c, uint32_t p, uint32_t d) {
+    int i = map_find(c->s->recv_peer, c->s->recv_n, p);
+    if (i < 0) return 1;
+    uint32_t e = ID_E(c->s->recv_id[i]), n = ID_C(c->s->recv_id[i]);
+    if (ID_E(d) > e) return 1;
+    return ID_C(d) > n;
+}
+
+/* ------------------------------------------------------ view updates -- */
+/* add_to_passive_view/2, hyparview:1423-1448 */
+static void add_to_passive(ctx *c, uint32_t p) {
+    node *s = c->s;
+    if (p == c->me || list_member(s->act, s->act_n, p) || list_member(s->pas, s->pas_n, p)) return;
+    if (s->pas_n >= c->h->cfg.max_passive_size) {
+        uint32_t omit[1] = {c->me};
+        uint32_t r = select_random(c, s->pas, s->pas_n, omit, 1);
+        if (r != PSIM_NONE) set_del(s->pas, &s->pas_n, r);
+    }
+    set_add(s->pas, &s->pas_n, p);
+}
+
+/* drop_random_element_from_active_view/1, hyparview:1467-1512 (no reservations) */
+static void drop_random_active(ctx *c) {
+    node *s = c->s;
+    uint32_t omit[1] = {c->me};
+    uint32_t p = select_random(c, s->act, s->act_n, omit, 1);
+    if (p == PSIM_NONE) return;
+    set_del(s->act, &s->act_n, p);
+    add_to_passive(c, p);
+    uint32_t nid = next_id(c, p);
+    map_store(c, s->sent_peer, s->sent_id, &s->sent_n, &s->sent_head, p, nid);
+    hv_send(c, p, PSIM_MSG_DISCONNECT, 0, nid, 0, NULL, 0);
+}
+
+/* add_to_active_view/3, hyparview:1371-1420 (tag/reserved ignored) */
+static void add_to_active(ctx *c, uint32_t p) {
+    node *s = c->s;
+    if (p == c->me || list_member(s->act, s->act_n, p)) return;
+    set_del(s->pas, &s->pas_n, p);
+    if (s->act_n >= c->h->cfg.max_active_size) drop_random_active(c);
+    set_add(s->act, &s->act_n, p);
+}
+
+/* [Myself] ++ select_random_sublist(Active, k_active) ++
+ * select_random_sublist(Passive, k_passive), then lists:usort
+ * (hyparview:577-586, :989-998, :1689-1698) */
+static uint32_t build_exchange(ctx *c, uint32_t *ex) {
+    node *s = c->s;
+    uint32_t e[1 + PSIM_ACTIVE_CAP + PSIM_PASSIVE_CAP];
+    uint32_t n = 0;
+    e[n++] = c->me;
+    n += select_random_sublist(c, s->act, s->act_n, c->h->cfg.k_active, e + n);
+    n += select_random_sublist(c, s->pas, s->pas_n, c->h->cfg.k_passive, e + n);
+    n = usort(e, n);
+    for (uint32_t i = 0; i < n; i++) ex[i] = e[i];
+    return n;
+}
+
+/* merge_exchange/2, hyparview:1590-1595 */
+static void merge_exchange(ctx *c, const uint32_t *ex, uint32_t nex) {
+    node *s = c->s;
+    uint32_t omit[1 + PSIM_ACTIVE_CAP], add[PSIM_EXCHANGE_CAP];
+    omit[0] = c->me;
+    for (uint32_t i = 0; i < s->act_n; i++) omit[1 + i] = s->act[i];
+    uint32_t k = list_subtract(ex, nex, omit, 1 + s->act_n, add);
+    k = usort(add, k);
+    for (uint32_t i = 0; i < k; i++) add_to_passive(c, add[i]);
+}
+
+/* move_peer_from_passive_to_active/2, hyparview:1679-1709 */
+static void move_to_active(ctx *c, uint32_t p) {
+    if (p == PSIM_NONE) return;
+    uint32_t ex[PSIM_EXCHANGE_CAP];
+    uint32_t nex = build_exchange(c, ex);
+    hv_send(c, p, PSIM_MSG_NEIGHBOR_REQUEST, 0, current_id(c, p), 0, ex, nex);
+}
+
+/* --------------------------------------------------------- plumtree -- */
+static void pt_set_add(uint32_t *l, uint32_t *n, uint32_t cap, uint32_t e, ctx *c) {
+    uint32_t i = 0;
+    while (i < *n && l[i] < e) i++;
+    if (i < *n && l[i] == e) return;
+    if (*n >= cap) { c->h->st->overflow++; return; }
+    for (uint32_t j = *n; j > i; j--) l[j] = l[j - 1];
+    l[i] = e;
+    (*n)++;
+}
+
+static void pt_set_del(uint32_t *l, uint32_t *n, uint32_t e) { set_del(l, n, e); }
+
+/* notify/1 (hyparview:1598-1599) -> partisan_peer_service:decode/1
+ * (peer_service.erl:117-119) -> plumtree update/1 -> handle_cast({update,..})
+ * (plumtree:314-336), reset_peers/4 (:652-659), neighbors_down/2 (:404-423). */
+static void notify(ctx *c) {
+    node *s = c->s;
+    if (!c->h->cfg.plumtree) return;
+    uint32_t cur[PSIM_ACTIVE_CAP], ncur = s->act_n;
+    for (uint32_t i = 0; i < ncur; i++) cur[i] = s->act[i];        /* atom names */
+    ncur = usort(cur, ncur);
+    uint32_t newm[PSIM_ACTIVE_CAP], rem[PSIM_PT_MEMBERS_CAP];
+    uint32_t nnew = list_subtract(cur, ncur, s->pt_all, s->pt_all_n, newm);
+    uint32_t nrem = list_subtract(s->pt_all, s->pt_all_n, cur, ncur, rem);
+    if (nnew > 0) {
+        /* EagerPeers = ordsets:union(EagerPeers0, New); reset_peers(Current, ..) */
+        uint32_t u[PSIM_PT_MEMBERS_CAP + PSIM_ACTIVE_CAP], nu = 0;
+        for (uint32_t i = 0; i < s->pt_common_n; i++) u[nu++] = s->pt_common[i];
+        for (uint32_t i = 0; i < nnew; i++) u[nu++] = newm[i];
+        nu = usort(u, nu);
+        nu = list_subtract(u, nu, rem, nrem, u);   /* neighbors_down applied below anyway */
+        memset(s->pt_common, 0, sizeof s->pt_common);
+        for (uint32_t i = 0; i < nu; i++) s->pt_common[i] = u[i];
+        s->pt_common_n = nu;
+        /* del_element(myself(), ..) removes nothing: myself() is a map (Q6) */
+        s->pt_root = PSIM_NONE;
+        memset(s->pt_eager, 0, sizeof s->pt_eager); s->pt_eager_n = 0;
+        memset(s->pt_lazy, 0, sizeof s->pt_lazy); s->pt_lazy_n = 0;
+        memset(s->pt_all, 0, sizeof s->pt_all);
+        for (uint32_t i = 0; i < ncur; i++) s->pt_all[i] = cur[i];
+        s->pt_all_n = ncur;
+    }
+    /* neighbors_down(Removed, ..) */
+    for (uint32_t i = 0; i < nrem; i++) {
+        pt_set_del(s->pt_common, &s->pt_common_n, rem[i]);
+        if (s->pt_root != PSIM_NONE) {
+            pt_set_del(s->pt_eager, &s->pt_eager_n, rem[i]);
+            pt_set_del(s->pt_lazy, &s->pt_lazy_n, rem[i]);
+        }
+        uint32_t j = 0;
+        for (uint32_t k = 0; k < s->out_n; k++)
+            if (s->out_peer[k] != rem[i]) {
+                s->out_peer[j] = s->out_peer[k]; s->out_msg[j] = s->out_msg[k];
+                s->out_round[j] = s->out_round[k]; j++;
+            }
+        for (uint32_t k = j; k < s->out_n; k++) s->out_peer[k] = s->out_msg[k] = s->out_round[k] = 0;
+        s->out_n = j;
+    }
+}
+
+/* all_peers/3 (plumtree:627-631): the per-root set or the common default */
+static void pt_get(ctx *c, uint32_t root, uint32_t *eg, uint32_t *ne, uint32_t *lz, uint32_t *nl) {
+    node *s = c->s;
+    if (s->pt_root != PSIM_NONE && s->pt_root == root) {
+        *ne = s->pt_eager_n; memcpy(eg, s->pt_eager, sizeof s->pt_eager);
+        *nl = s->pt_lazy_n; memcpy(lz, s->pt_lazy, sizeof s->pt_lazy);
+    } else {
+        memset(eg, 0, sizeof s->pt_eager); memset(lz, 0, sizeof s->pt_lazy);
+        *ne = s->pt_common_n;
+        for (uint32_t i = 0; i < s->pt_common_n; i++) eg[i] = s->pt_common[i];
+        *nl = 0;                                   /* common_lazys is always [] */
+    }
+}
+
+/* update_peers/5 + set_peers/4 (plumtree:593-609) */
+static void pt_update(ctx *c, uint32_t from, uint32_t root, int to_eager) {
+    node *s = c->s;
+    uint32_t eg[PSIM_PT_SET_CAP], lz[PSIM_PT_SET_CAP], ne, nl;
+    pt_get(c, root, eg, &ne, lz, &nl);
+    if (to_eager) { pt_set_add(eg, &ne, PSIM_PT_SET_CAP, from, c); pt_set_del(lz, &nl, from); }
+    else { pt_set_del(eg, &ne, from); pt_set_add(lz, &nl, PSIM_PT_SET_CAP, from, c); }
+    if (s->pt_root != PSIM_NONE && s->pt_root != root) { c->h->st->overflow++; return; }
+    s->pt_root = root;
+    memcpy(s->pt_eager, eg, sizeof eg); s->pt_eager_n = ne;
+    memcpy(s->pt_lazy, lz, sizeof lz); s->pt_lazy_n = nl;
+}
+
+/* send/3 (plumtree:633-638) -> cast_message -> forward_message: succeeds only
+ * over an existing connection of this node's manager. */
+static void pt_send(ctx *c, uint32_t ident, uint32_t type, uint32_t msg, uint32_t rnd,
+                    uint32_t root) {
+    uint32_t id = ident & ~PSIM_MAP_BIT;
+    node *s = c->s;
+    if (id == c->me || !list_member(s->act, s->act_n, id) || !c->h->nodes[id].up ||
+        c->h->part[id] != c->h->part[c->me]) {
+        c->h->st->send_fail++;
+        return;
+    }
+    emit(c, id, type, 0, msg, rnd, root, NULL, 0);
+}
+
+/* add_outstanding/6 (plumtree:574-579): ordset keyed by peer, then {Id,..,Round,Root} */
+static void pt_add_out(ctx *c, uint32_t peer, uint32_t msg, uint32_t rnd) {
+    node *s = c->s;
+    uint32_t i = 0;
+    while (i < s->out_n &&
+           (s->out_peer[i] < peer || (s->out_peer[i] == peer && s->out_msg[i] < msg) ||
+            (s->out_peer[i] == peer && s->out_msg[i] == msg && s->out_round[i] < rnd)))
+        i++;
+    if (i < s->out_n && s->out_peer[i] == peer && s->out_msg[i] == msg && s->out_round[i] == rnd)
+        return;
+    if (s->out_n >= PSIM_PT_OUT_CAP) { c->h->st->overflow++; return; }
+    for (uint32_t j = s->out_n; j > i; j--) {
+        s->out_peer[j] = s->out_peer[j - 1]; s->out_msg[j] = s->out_msg[j - 1];
+        s->out_round[j] = s->out_round[j - 1];
+    }
+    s->out_peer[i] = peer; s->out_msg[i] = msg; s->out_round[i] = rnd;
+    s->out_n++;
+}
+
+/* ack_outstanding/6 (plumtree:562-567) */
+static void pt_ack_out(ctx *c, uint32_t peer, uint32_t msg, uint32_t rnd) {
+    node *s = c->s;
+    for (uint32_t i = 0; i < s->out_n; i++)
+        if (s->out_peer[i] == peer && s->out_msg[i] == msg && s->out_round[i] == rnd) {
+            for (uint32_t j = i; j + 1 < s->out_n; j++) {
+                s->out_peer[j] = s->out_peer[j + 1]; s->out_msg[j] = s->out_msg[j + 1];
+                s->out_round[j] = s->out_round[j + 1];
+            }
+            s->out_n--;
+            s->out_peer[s->out_n] = s->out_msg[s->out_n] = s->out_round[s->out_n] = 0;
+            return;
+        }
+}
+
+static int pt_have(ctx *c, uint32_t msg) { return (c->s->have >> (msg & 31u)) & 1u; }
+
+/* eager_push/7 + schedule_lazy_push/6 (plumtree:428-441) */
+static void pt_push(ctx *c, uint32_t msg, uint32_t rnd, uint32_t root, uint32_t from) {
+    uint32_t eg[PSIM_PT_SET_CAP], lz[PSIM_PT_SET_CAP], ne, nl;
+    pt_get(c, root, eg, &ne, lz, &nl);
+    pt_set_del(eg, &ne, from);                    /* all_filtered_peers/4 */
+    for (uint32_t i = 0; i < ne; i++) pt_send(c, eg[i], PSIM_MSG_PT_BROADCAST, msg, rnd, root);
+    pt_get(c, root, eg, &ne, lz, &nl);
+    pt_set_del(lz, &nl, from);
+    for (uint32_t i = 0; i < nl; i++) pt_add_out(c, lz[i], msg, rnd);
+}
+
+static void pt_handle(ctx *c, const omsg *m) {
+    node *s = c->s;
+    uint32_t from = m->src | PSIM_MAP_BIT, root = m->a2, msg = m->a0, rnd = m->a1;
+    switch (m->type) {
+    case PSIM_MSG_PT_BROADCAST: {                 /* plumtree:288-293, :368-378 */
+        int valid = !pt_have(c, msg);             /* plumtree_backend merge/2 :87-96 */
+        if (valid) {
+            s->have |= 1u << (msg & 31u);
+            c->h->st->first_deliveries++;
+            if (msg == c->h->tracked_msg) { s->trk_round = (uint32_t)c->h->round; s->trk_hop = rnd + 1; }
+            pt_update(c, from, root, 1);
+            pt_push(c, msg, rnd + 1, root, from);
+        } else {
+            pt_update(c, from, root, 0);
+            pt_send(c, from, PSIM_MSG_PT_PRUNE, 0, 0, root);
+        }
+        break;
+    }
+    case PSIM_MSG_PT_PRUNE:                       /* plumtree:294-298 */
+        pt_update(c, from, root, 0);
+        break;
+    case PSIM_MSG_PT_IHAVE:                       /* plumtree:299-303, :380-386 */
+        if (pt_have(c, msg)) {
+            pt_send(c, from, PSIM_MSG_PT_IGNORED_IHAVE, msg, rnd, root);
+        } else {
+            pt_send(c, from, PSIM_MSG_PT_GRAFT, msg, rnd, root);
+            pt_update(c, from, root, 1);
+        }
+        break;
+    case PSIM_MSG_PT_IGNORED_IHAVE:               /* plumtree:304-307 */
+        pt_ack_out(c, from, msg, rnd);
+        break;
+    case PSIM_MSG_PT_GRAFT:                       /* plumtree:308-313, :388-402 */
+        if (pt_have(c, msg)) {                    /* backend graft/1 :105-108, :153-159 */
+            pt_update(c, from, root, 1);
+            pt_send(c, from, PSIM_MSG_PT_BROADCAST, msg, rnd, root);
+        }
+        break;
+    default:
+        break;
+    }
+}
+
+/* ------------------------------------------------------- hyparview -- */
+static void hv_handle(ctx *c, const omsg *m) {
+    struct psim_handle *h = c->h;
+    node *s = c->s;
+    uint32_t me = c->me;
+    switch (m->type) {
+    case PSIM_MSG_JOIN: {                         /* hyparview:703-771 */
+        uint32_t p = m->src, pe = m->a0;
+        if (addable_epoch(c, pe, p) && !list_member(s->act, s->act_n, p)) {
+            if (connect_ok(c, p)) {
+                add_to_active(c, p);
+                hv_send(c, p, PSIM_MSG_NEIGHBOR, 0, current_id(c, p), 0, NULL, 0);
+                uint32_t omit[2] = {me, p}, peers[PSIM_ACTIVE_CAP];
+                uint32_t np = list_subtract(s->act, s->act_n, omit, 2, peers);
+                for (uint32_t i = 0; i < np; i++)
+                    hv_send(c, peers[i], PSIM_MSG_FORWARD_JOIN, h->cfg.arwl, p, pe, NULL, 0);
+                notify(c);
+            }
+        }
+        break;
+    }
+    case PSIM_MSG_NEIGHBOR: {                     /* hyparview:774-805 */
+        uint32_t p = m->src;
+        if (addable_id(c, m->a0, p) && connect_ok(c, p)) add_to_active(c, p);
+        notify(c);
+        break;
+    }
+    case PSIM_MSG_FORWARD_JOIN: {                 /* hyparview:808-923 */
+        uint32_t p = m->a0, pe = m->a1, ttl = m->ttl, sender = m->src;
+        if (ttl == 0 || s->act_n == 1) {
+            if (addable_epoch(c, pe, p) && !list_member(s->act, s->act_n, p) && connect_ok(c, p)) {
+                add_to_active(c, p);
+                hv_send(c, p, PSIM_MSG_NEIGHBOR, 0, current_id(c, p), 0, NULL, 0);
+            }
+        } else {
+            uint32_t act0[PSIM_ACTIVE_CAP], n0 = s->act_n;
+            memcpy(act0, s->act, sizeof act0);
+            if (ttl == h->cfg.prwl) add_to_passive(c, p);
+            uint32_t omit[3] = {sender, me, p};
+            uint32_t r = select_random(c, act0, n0, omit, 3);
+            if (r == PSIM_NONE) {
+                if (addable_epoch(c, pe, p) && !list_member(act0, n0, p) && connect_ok(c, p)) {
+                    add_to_active(c, p);
+                    hv_send(c, p, PSIM_MSG_NEIGHBOR, 0, current_id(c, p), 0, NULL, 0);
+                }
+            } else {
+                hv_send(c, r, PSIM_MSG_FORWARD_JOIN, ttl - 1, p, pe, NULL, 0);
+            }
+        }
+        notify(c);
+        break;
+    }
+    case PSIM_MSG_DISCONNECT: {                   /* hyparview:926-972 */
+        uint32_t p = m->src, d = m->a0;
+        if (!valid_disconnect(c, p, d)) break;
+        uint32_t pas0[PSIM_PASSIVE_CAP], np0 = s->pas_n;
+        memcpy(pas0, s->pas, sizeof pas0);
+        set_del(s->act, &s->act_n, p);
+        add_to_passive(c, p);
+        map_store(c, s->recv_peer, s->recv_id, &s->recv_n, &s->recv_head, p, d);
+        if (s->act_n == 1) {
+            uint32_t omit[2] = {me, p};
+            move_to_active(c, select_random(c, pas0, np0, omit, 2));
+        }
+        break;
+    }
+    case PSIM_MSG_NEIGHBOR_REQUEST: {             /* hyparview:975-1053 */
+        uint32_t p = m->src, d = m->a0;
+        uint32_t ack[PSIM_EXCHANGE_CAP];
+        uint32_t nack = build_exchange(c, ack);
+        if (addable_id(c, d, p)) {               /* priority is always high (:1706) */
+            if (connect_ok(c, p)) {
+                hv_send(c, p, PSIM_MSG_NEIGHBOR_ACCEPTED, 0, current_id(c, p), 0, ack, nack);
+                add_to_active(c, p);
+            }
+        } else {
+            hv_send(c, p, PSIM_MSG_NEIGHBOR_REJECTED, 0, 0, 0, ack, nack);
+        }
+        merge_exchange(c, m->ex, m->nex);
+        notify(c);
+        break;
+    }
+    case PSIM_MSG_NEIGHBOR_REJECTED:              /* hyparview:1056-1067 */
+        merge_exchange(c, m->ex, m->nex);
+        break;
+    case PSIM_MSG_NEIGHBOR_ACCEPTED:              /* hyparview:1070-1089 */
+        if (addable_id(c, m->a0, m->src)) add_to_active(c, m->src);
+        merge_exchange(c, m->ex, m->nex);
+        notify(c);
+        break;
+    case PSIM_MSG_SHUFFLE_REPLY:                  /* hyparview:1091-1093 */
+        merge_exchange(c, m->ex, m->nex);
+        break;
+    case PSIM_MSG_SHUFFLE: {                      /* hyparview:1095-1136 */
+        uint32_t ttl = m->ttl, sender = m->src;
+        if (ttl > 0 && s->act_n > 1) {
+            uint32_t omit[2] = {sender, me};
+            uint32_t r = select_random(c, s->act, s->act_n, omit, 2);
+            if (r != PSIM_NONE) hv_send(c, r, PSIM_MSG_SHUFFLE, ttl - 1, 0, 0, m->ex, m->nex);
+        } else {
+            uint32_t resp[PSIM_EXCHANGE_CAP];
+            uint32_t nr = select_random_sublist(c, s->pas, s->pas_n, m->nex, resp);
+            hv_send(c, sender, PSIM_MSG_SHUFFLE_REPLY, 0, 0, 0, resp, nr);
+            merge_exchange(c, m->ex, m->nex);
+        }
+        break;
+    }
+    default:
+        break;
+    }
+}
+
+static int timer_due(uint32_t period, uint64_t r, uint32_t start) {
+    return period > 0 && r > start && ((r - start) % period) == 0;
+}
+
+static void process_node(struct psim_handle *h, uint32_t n) {
+    node *s = &h->nodes[n];
+    ctx c = {h, s, n, 0};
+    uint64_t r = h->round;
+    size_t b = h->in_beg[n], e = h->in_beg[n + 1];
+    /* a fresh incarnation has no connections: traffic addressed to the
+     * previous one is lost */
+    if (s->start_round == r && e > b) { h->st->dropped += e - b; e = b; }
+    int promo = h->cfg.random_promotion && timer_due(h->cfg.promotion_period, r, s->start_round);
+    int shuf = timer_due(h->cfg.shuffle_period, r, s->start_round);
+    int origin = h->origin_now && h->origin_node == n && h->cfg.plumtree;
+    int lazy_due = h->cfg.plumtree && timer_due(h->cfg.lazy_tick_period, r, s->start_round);
+    int lazy = lazy_due && s->out_n > 0;
+    uint32_t exits[PSIM_ACTIVE_CAP], nexit = 0;
+    for (uint32_t i = 0; i < s->act_n; i++)
+        if (s->act[i] != n && h->crashed_now[s->act[i]]) exits[nexit++] = s->act[i];
+    int joining = (s->start_round == r && s->join_contact != PSIM_NONE);
+    if (!(e > b || joining || nexit || promo || shuf || origin || lazy)) return;
+    h->st->nodes_processed++;
+
+    /* handle_cast({join, Peer}), hyparview:500-515 */
+    if (joining) hv_send(&c, s->join_contact, PSIM_MSG_JOIN, 0, s->epoch, 0, NULL, 0);
+
+    /* handle_info({'EXIT', ..}), hyparview:609-654 */
+    for (uint32_t i = 0; i < nexit; i++) {
+        uint32_t d = exits[i];
+        h->st->exits++;
+        if (list_member(s->pas, s->pas_n, d)) set_del(s->pas, &s->pas_n, d);
+        if (list_member(s->act, s->act_n, d)) {
+            set_del(s->act, &s->act_n, d);
+            uint32_t omit[1] = {n};
+            move_to_active(&c, select_random(&c, s->pas, s->pas_n, omit, 1));
+        }
+    }
+
+    for (size_t i = b; i < e; i++)
+        if (h->inbox.v[i].type < PSIM_MSG_PT_BROADCAST) {
+            h->st->delivered[h->inbox.v[i].type]++;
+            hv_handle(&c, &h->inbox.v[i]);
+        }
+
+    if (promo && s->act_n < h->cfg.min_active_size) {   /* hyparview:542-561, :1718-1728 */
+        uint32_t omit[1] = {n};
+        move_to_active(&c, select_random(&c, s->pas, s->pas_n, omit, 1));
+    }
+
+    if (shuf) {                                          /* hyparview:572-607 */
+        uint32_t ex[PSIM_EXCHANGE_CAP];
+        uint32_t nex = build_exchange(&c, ex);
+        uint32_t omit[1] = {n};
+        uint32_t r2 = select_random(&c, s->act, s->act_n, omit, 1);
+        if (r2 != PSIM_NONE) hv_send(&c, r2, PSIM_MSG_SHUFFLE, h->cfg.arwl, 0, 0, ex, nex);
+    }
+
+    if (!h->cfg.plumtree) return;
+    for (size_t i = b; i < e; i++)
+        if (h->inbox.v[i].type >= PSIM_MSG_PT_BROADCAST && h->inbox.v[i].type <= PSIM_MSG_PT_GRAFT) {
+            h->st->delivered[h->inbox.v[i].type]++;
+            pt_handle(&c, &h->inbox.v[i]);
+        }
+
+    if (origin) {                                  /* plumtree:282-287, backend:179-200 */
+        uint32_t my = n | PSIM_MAP_BIT;
+        s->have |= 1u << (h->origin_msg & 31u);
+        s->trk_round = (uint32_t)r; s->trk_hop = 0;
+        pt_push(&c, h->origin_msg, 0, my, my);
+    }
+
+    if (lazy_due) {                               /* plumtree:341-345, :443-453 */
+        for (uint32_t i = 0; i < s->out_n; i++)
+            pt_send(&c, s->out_peer[i], PSIM_MSG_PT_IHAVE, s->out_msg[i], s->out_round[i],
+                    h->bcast_root);
+    }
+}
+
+/* ---------------------------------------------------------- rounds -- */
+static void node_init(struct psim_handle *h, uint32_t n, uint32_t contact) {
+    node *s = &h->nodes[n];
+    uint32_t ep = h->cfg.persist_epoch ? s->epoch + 1 : 1;
+    memset(s, 0, sizeof *s);
+    s->up = 1;
+    s->epoch = ep;
+    s->start_round = (uint32_t)h->round;
+    s->join_contact = contact;
+    s->act[0] = n; s->act_n = 1;                 /* sets:add_element(Myself, ..) :299 */
+    s->pt_all[0] = n; s->pt_all_n = 1;           /* plumtree start_link/0 :127-144 */
+    s->pt_common[0] = n; s->pt_common_n = 1;
+    s->pt_root = PSIM_NONE;
+    s->trk_round = PSIM_NONE;
+}
+
+static int cmp_dst(const void *a, const void *b) {
+    const omsg *x = (const omsg *)a, *y = (const omsg *)b;
+    if (x->dst != y->dst) return x->dst < y->dst ? -1 : 1;
+    if (x->src != y->src) return x->src < y->src ? -1 : 1;
+    return x->seq < y->seq ? -1 : x->seq > y->seq;
+}
+
+static void run_round(struct psim_handle *h, psim_round_stats *st) {
+    memset(st, 0, sizeof *st);
+    st->round = h->round;
+    h->st = st;
+    /* events */
+    for (size_t i = 0; i < h->pend_crash_n; i++) {
+        uint32_t n = h->pend_crash[i];
+        if (h->nodes[n].up) { h->nodes[n].up = 0; h->crashed_now[n] = 1; }
+    }
+    for (size_t i = 0; i < h->pend_join_n; i++) node_init(h, h->pend_join[i], h->pend_contact[i]);
+    if (h->pend_part_clear) memset(h->part, 0, h->N);
+    if (h->pend_part_set) memcpy(h->part, h->pend_part, h->N);
+    h->origin_now = 0;
+    if (h->pend_bcast) {
+        h->tracked_msg = h->pend_msg;
+        for (uint32_t n = 0; n < h->N; n++) {
+            h->nodes[n].have &= ~(1u << (h->pend_msg & 31u));
+            h->nodes[n].trk_round = PSIM_NONE;
+            h->nodes[n].trk_hop = 0;
+        }
+        if (h->nodes[h->pend_root].up) {
+            h->origin_now = 1; h->origin_node = h->pend_root; h->origin_msg = h->pend_msg;
+        }
+    }
+    h->pend_crash_n = h->pend_join_n = 0;
+    h->pend_part_set = h->pend_part_clear = 0;
+    h->pend_bcast = 0;
+
+    h->out.n = 0;
+    for (uint32_t n = 0; n < h->N; n++) {
+        if (h->nodes[n].up) {
+            st->nodes_up++;
+            process_node(h, n);
+        } else {
+            st->dropped += h->in_beg[n + 1] - h->in_beg[n];
+        }
+    }
+    memset(h->crashed_now, 0, h->N);
+    /* deliver: messages emitted in round r form the canonical inbox of r+1 */
+    qsort(h->out.v, h->out.n, sizeof(omsg), cmp_dst);
+    msgvec t = h->inbox; h->inbox = h->out; h->out = t;
+    size_t j = 0;
+    for (uint32_t n = 0; n <= h->N; n++) {
+        while (j < h->inbox.n && h->inbox.v[j].dst < n) j++;
+        h->in_beg[n] = j;
+    }
+    h->round++;
+}
+
+/* ------------------------------------------------------------- ABI -- */
+void orc_default_config(psim_config *cfg) {
+    memset(cfg, 0, sizeof *cfg);
+    cfg->abi_version = PSIM_ABI_VERSION;
+    cfg->n_nodes = 32;
+    cfg->seed = 1;
+    cfg->max_active_size = 6; cfg->min_active_size = 3; cfg->max_passive_size = 30;
+    cfg->arwl = 5; cfg->prwl = 30; cfg->k_active = 3; cfg->k_passive = 4;
+    cfg->shuffle_period = 10; cfg->promotion_period = 5; cfg->random_promotion = 1;
+    cfg->persist_epoch = 0; cfg->plumtree = 1; cfg->lazy_tick_period = 1;
+    cfg->device = -1; cfg->n_shards = 1; cfg->shard_world = 1;
+}
+
+int orc_create(const psim_config *cfg, struct psim_handle **out) {
+    if (!cfg || !out || cfg->abi_version != PSIM_ABI_VERSION || cfg->n_nodes == 0 ||
+        cfg->n_nodes >= PSIM_MAP_BIT || cfg->max_active_size < 2 ||
+        cfg->max_active_size > PSIM_ACTIVE_CAP || cfg->max_passive_size < 1 ||
+        cfg->max_passive_size > 30 || 1 + cfg->k_active + cfg->k_passive > PSIM_EXCHANGE_CAP ||
+        cfg->arwl > 255 || cfg->prwl > 255)
+        return PSIM_EINVAL;
+    struct psim_handle *h = (struct psim_handle *)calloc(1, sizeof *h);
+    if (!h) return PSIM_ENOMEM;
+    h->cfg = *cfg;
+    h->N = cfg->n_nodes;
+    h->nodes = (node *)calloc(h->N, sizeof(node));
+    h->part = (uint8_t *)calloc(h->N, 1);
+    h->crashed_now = (uint8_t *)calloc(h->N, 1);
+    h->in_beg = (size_t *)calloc((size_t)h->N + 1, sizeof(size_t));
+    h->pend_part = (uint8_t *)calloc(h->N, 1);
+    if (!h->nodes || !h->part || !h->crashed_now || !h->in_beg || !h->pend_part) return PSIM_ENOMEM;
+    h->bcast_root = PSIM_NONE;
+    h->tracked_msg = PSIM_NONE;
+    *out = h;
+    return PSIM_OK;
+}
+
+void orc_destroy(struct psim_handle *h) {
+    if (!h) return;
+    free(h->nodes); free(h->part); free(h->crashed_now); free(h->in_beg); free(h->pend_part);
+    free(h->inbox.v); free(h->out.v);
+    free(h->pend_crash); free(h->pend_join); free(h->pend_contact);
+    free(h);
+}
+
+int orc_join(struct psim_handle *h, const uint32_t *nodes, const uint32_t *contacts, size_t n) {
+    for (size_t i = 0; i < n; i++)
+        if (nodes[i] >= h->N || (contacts[i] != PSIM_NONE && contacts[i] >= h->N)) return PSIM_ERANGE;
+    if (h->pend_join_n + n > h->pend_join_cap) {
+        h->pend_join_cap = (h->pend_join_n + n) * 2;
+        h->pend_join = (uint32_t *)realloc(h->pend_join, h->pend_join_cap * 4);
+        h->pend_contact = (uint32_t *)realloc(h->pend_contact, h->pend_join_cap * 4);
+    }
+    for (size_t i = 0; i < n; i++) {
+        h->pend_join[h->pend_join_n] = nodes[i];
+        h->pend_contact[h->pend_join_n++] = contacts[i];
+    }
+    return PSIM_OK;
+}
+
+int orc_crash(struct psim_handle *h, const uint32_t *nodes, size_t n) {
+    for (size_t i = 0; i < n; i++)
+        if (nodes[i] >= h->N) return PSIM_ERANGE;
+    if (h->pend_crash_n + n > h->pend_crash_cap) {
+        h->pend_crash_cap = (h->pend_crash_n + n) * 2;
+        h->pend_crash = (uint32_t *)realloc(h->pend_crash, h->pend_crash_cap * 4);
+    }
+    for (size_t i = 0; i < n; i++) h->pend_crash[h->pend_crash_n++] = nodes[i];
+    return PSIM_OK;
+}
+
+int orc_set_partition(struct psim_handle *h, const uint8_t *group, size_t n) {
+    if (n != h->N) return PSIM_EINVAL;
+    memcpy(h->pend_part, group, n);
+    h->pend_part_set = 1; h->pend_part_clear = 0;
+    return PSIM_OK;
+}
+
+int orc_clear_partition(struct psim_handle *h) {
+    h->pend_part_clear = 1; h->pend_part_set = 0;
+    return PSIM_OK;
+}
+
+int orc_broadcast(struct psim_handle *h, uint32_t root, uint32_t msg_id) {
+    if (root >= h->N || msg_id > 0xFFFF) return PSIM_ERANGE;
+    uint32_t r = root | PSIM_MAP_BIT;
+    if (h->bcast_root != PSIM_NONE && h->bcast_root != r) return PSIM_EUNSUPPORTED;
+    h->bcast_root = r;
+    h->pend_bcast = 1; h->pend_root = root; h->pend_msg = msg_id;
+    return PSIM_OK;
+}
+
+int orc_step(struct psim_handle *h, uint32_t n_rounds, psim_round_stats *stats) {
+    psim_round_stats tmp;
+    for (uint32_t i = 0; i < n_rounds; i++) run_round(h, stats ? &stats[i] : &tmp);
+    return PSIM_OK;
+}
+
+int orc_get_round(struct psim_handle *h, uint64_t *round) { *round = h->round; return PSIM_OK; }
+
+int orc_get_nodes(struct psim_handle *h, uint32_t first, uint32_t count, psim_node_view *out) {
+    if ((uint64_t)first + count > h->N) return PSIM_ERANGE;
+    for (uint32_t k = 0; k < count; k++) {
+        const node *s = &h->nodes[first + k];
+        psim_node_view *v = &out[k];
+        memset(v, 0, sizeof *v);
+        v->up = s->up; v->epoch = s->epoch; v->start_round = s->start_round; v->pt_root = s->pt_root;
+        v->rng_ctr = s->rng;
+        v->act_n = s->act_n; v->pas_n = s->pas_n;
+        memcpy(v->act, s->act, sizeof v->act); memcpy(v->pas, s->pas, sizeof v->pas);
+        v->sent_n = s->sent_n; v->sent_head = s->sent_head; v->recv_n = s->recv_n; v->recv_head = s->recv_head;
+        memcpy(v->sent_peer, s->sent_peer, sizeof v->sent_peer); memcpy(v->sent_id, s->sent_id, sizeof v->sent_id);
+        memcpy(v->recv_peer, s->recv_peer, sizeof v->recv_peer); memcpy(v->recv_id, s->recv_id, sizeof v->recv_id);
+        v->pt_all_n = s->pt_all_n; v->pt_common_n = s->pt_common_n;
+        v->pt_eager_n = s->pt_eager_n; v->pt_lazy_n = s->pt_lazy_n; v->pt_out_n = s->out_n;
+        memcpy(v->pt_all, s->pt_all, sizeof v->pt_all); memcpy(v->pt_common, s->pt_common, sizeof v->pt_common);
+        memcpy(v->pt_eager, s->pt_eager, sizeof v->pt_eager); memcpy(v->pt_lazy, s->pt_lazy, sizeof v->pt_lazy);
+        memcpy(v->pt_out_peer, s->out_peer, sizeof v->pt_out_peer);
+        memcpy(v->pt_out_msg, s->out_msg, sizeof v->pt_out_msg);
+        memcpy(v->pt_out_round, s->out_round, sizeof v->pt_out_round);
+        v->have = s->have; v->trk_round = s->trk_round; v->trk_hop = s->trk_hop;
+    }
+    return PSIM_OK;
+}
+
+/* inbox of the next round, for message-level diffs in tests */
+int orc_get_inbox(struct psim_handle *h, uint32_t *out, size_t cap, size_t *n) {
+    *n = h->inbox.n;
+    if (!out) return PSIM_OK;
+    for (size_t i = 0; i < h->inbox.n && i < cap; i++) {
+        const omsg *m = &h->inbox.v[i];
+        uint32_t *o = out + i * 16;
+        o[0] = m->dst; o[1] = m->src; o[2] = m->seq; o[3] = m->type | (m->ttl << 8) | (m->nex << 16);
+        o[4] = m->a0; o[5] = m->a1; o[6] = m->a2; o[7] = 0;
+        for (int k = 0; k < 8; k++) o[8 + k] = k < (int)m->nex ? m->ex[k] : 0;
+    }
+    return PSIM_OK;
+}
+
+/* exposed for RNG known-answer tests */
+void orc_philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1,
+                uint32_t out[4]) {
+    philox(c0, c1, c2, c3, k0, k1, out);
+}
+uint32_t orc_bucket16(uint32_t id) { return bucket16(id); }

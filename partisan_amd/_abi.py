@@ -1,0 +1,120 @@
+"""ctypes mirror of include/partisan_gpu_sim.h (plain data types only).
+
+Shared by the product loader (partisan_amd/_lib.py) and the test drivers.
+Field order and widths must match the header exactly; tests/test_abi.py checks
+the struct sizes against the compiled library.
+"""
+import ctypes as C
+
+import numpy as np
+
+PSIM_ABI_VERSION = 1
+PSIM_MAP_BIT = 0x80000000
+PSIM_NONE = 0xFFFFFFFF
+ACTIVE_CAP, PASSIVE_CAP, IDMAP_CAP = 8, 32, 32
+PT_MEMBERS_CAP, PT_SET_CAP, PT_OUT_CAP, EXCHANGE_CAP = 8, 16, 32, 8
+NTYPES = 16
+
+MSG_TYPES = [
+    "JOIN", "FORWARD_JOIN", "NEIGHBOR", "DISCONNECT", "NEIGHBOR_REQUEST",
+    "NEIGHBOR_ACCEPTED", "NEIGHBOR_REJECTED", "SHUFFLE", "SHUFFLE_REPLY",
+    "PT_BROADCAST", "PT_PRUNE", "PT_IHAVE", "PT_IGNORED_IHAVE", "PT_GRAFT",
+]
+HV_TYPES = list(range(0, 9))
+PT_TYPES = list(range(9, 14))
+
+ERRORS = {
+    0: "PSIM_OK", -1: "PSIM_EINVAL", -2: "PSIM_ENOMEM", -3: "PSIM_EDEVICE",
+    -4: "PSIM_ESTATE", -5: "PSIM_ERANGE", -6: "PSIM_ECOMM", -7: "PSIM_EUNSUPPORTED",
+}
+
+
+class PsimConfig(C.Structure):
+    _fields_ = [
+        ("abi_version", C.c_uint32), ("n_nodes", C.c_uint32), ("seed", C.c_uint64),
+        ("max_active_size", C.c_uint32), ("min_active_size", C.c_uint32),
+        ("max_passive_size", C.c_uint32), ("arwl", C.c_uint32), ("prwl", C.c_uint32),
+        ("k_active", C.c_uint32), ("k_passive", C.c_uint32),
+        ("shuffle_period", C.c_uint32), ("promotion_period", C.c_uint32),
+        ("random_promotion", C.c_uint32), ("persist_epoch", C.c_uint32),
+        ("plumtree", C.c_uint32), ("lazy_tick_period", C.c_uint32),
+        ("device", C.c_int32), ("n_shards", C.c_uint32), ("shard_rank", C.c_uint32),
+        ("shard_world", C.c_uint32), ("comm_id", C.c_void_p),
+        ("max_msgs_per_round", C.c_uint64), ("reserved", C.c_uint32 * 8),
+    ]
+
+
+class PsimRoundStats(C.Structure):
+    _fields_ = [
+        ("round", C.c_uint64), ("emitted", C.c_uint64 * NTYPES),
+        ("delivered", C.c_uint64 * NTYPES), ("dropped", C.c_uint64),
+        ("nodes_up", C.c_uint64), ("nodes_processed", C.c_uint64), ("exits", C.c_uint64),
+        ("send_fail", C.c_uint64), ("first_deliveries", C.c_uint64), ("overflow", C.c_uint64),
+        ("digest", C.c_uint64), ("state_bytes", C.c_uint64), ("reserved", C.c_uint64 * 4),
+    ]
+
+
+class PsimNodeView(C.Structure):
+    _fields_ = [
+        ("up", C.c_uint32), ("epoch", C.c_uint32), ("start_round", C.c_uint32),
+        ("pt_root", C.c_uint32), ("rng_ctr", C.c_uint64),
+        ("act_n", C.c_uint32), ("pas_n", C.c_uint32),
+        ("act", C.c_uint32 * ACTIVE_CAP), ("pas", C.c_uint32 * PASSIVE_CAP),
+        ("sent_n", C.c_uint32), ("sent_head", C.c_uint32),
+        ("recv_n", C.c_uint32), ("recv_head", C.c_uint32),
+        ("sent_peer", C.c_uint32 * IDMAP_CAP), ("sent_id", C.c_uint32 * IDMAP_CAP),
+        ("recv_peer", C.c_uint32 * IDMAP_CAP), ("recv_id", C.c_uint32 * IDMAP_CAP),
+        ("pt_all_n", C.c_uint32), ("pt_common_n", C.c_uint32), ("pt_eager_n", C.c_uint32),
+        ("pt_lazy_n", C.c_uint32), ("pt_out_n", C.c_uint32), ("pt_pad", C.c_uint32),
+        ("pt_all", C.c_uint32 * PT_MEMBERS_CAP), ("pt_common", C.c_uint32 * PT_MEMBERS_CAP),
+        ("pt_eager", C.c_uint32 * PT_SET_CAP), ("pt_lazy", C.c_uint32 * PT_SET_CAP),
+        ("pt_out_peer", C.c_uint32 * PT_OUT_CAP), ("pt_out_msg", C.c_uint32 * PT_OUT_CAP),
+        ("pt_out_round", C.c_uint32 * PT_OUT_CAP),
+        ("have", C.c_uint32), ("trk_round", C.c_uint32), ("trk_hop", C.c_uint32),
+        ("pad1", C.c_uint32),
+    ]
+
+
+NODE_VIEW_DTYPE = np.dtype(PsimNodeView)
+STATS_DTYPE = np.dtype(PsimRoundStats)
+
+# entry points of the C ABI: name -> (restype, argtypes)
+_H = C.c_void_p
+_P32 = C.POINTER(C.c_uint32)
+SIGNATURES = {
+    "default_config": (None, [C.POINTER(PsimConfig)]),
+    "create": (C.c_int, [C.POINTER(PsimConfig), C.POINTER(C.c_void_p)]),
+    "destroy": (None, [_H]),
+    "join": (C.c_int, [_H, _P32, _P32, C.c_size_t]),
+    "crash": (C.c_int, [_H, _P32, C.c_size_t]),
+    "set_partition": (C.c_int, [_H, C.POINTER(C.c_uint8), C.c_size_t]),
+    "clear_partition": (C.c_int, [_H]),
+    "broadcast": (C.c_int, [_H, C.c_uint32, C.c_uint32]),
+    "step": (C.c_int, [_H, C.c_uint32, C.POINTER(PsimRoundStats)]),
+    "get_nodes": (C.c_int, [_H, C.c_uint32, C.c_uint32, C.POINTER(PsimNodeView)]),
+    "get_round": (C.c_int, [_H, C.POINTER(C.c_uint64)]),
+}
+# symbols only the GPU library exports
+GPU_ONLY = {
+    "strerror": (C.c_char_p, [C.c_int]),
+    "abi_version": (C.c_int, []),
+    "kernel_times": (C.c_int, [_H, C.POINTER(C.c_char_p), C.POINTER(C.c_double),
+                               C.POINTER(C.c_uint64), C.c_int]),
+    "comm_id_size": (C.c_int, []),
+    "get_comm_id": (C.c_int, [C.c_void_p, C.c_size_t]),
+}
+
+
+def bind(lib, prefix, names):
+    """Attach restype/argtypes for `prefix + name` and return {name: fn}."""
+    out = {}
+    for name, (res, args) in names.items():
+        fn = getattr(lib, prefix + name)
+        fn.restype = res
+        fn.argtypes = args
+        out[name] = fn
+    return out
+
+
+def u32p(a):
+    return a.ctypes.data_as(_P32)

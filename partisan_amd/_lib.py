@@ -1,0 +1,22 @@
+"""Loader for the in-tree HIP library.  No fallback: a missing or stale
+library is an error, so a GPU run can never silently use another path."""
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "csrc", "libpartisan_gpu_sim.so")
+
+_lib = None
+
+
+def load():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(
+                f"{LIB_PATH} is missing: build it with `make -C partisan_amd/csrc` "
+                "or __graft_entry__.build()")
+        _lib = ctypes.CDLL(LIB_PATH)
+        if _lib.psim_abi_version() != 1:
+            raise ImportError("libpartisan_gpu_sim.so ABI version mismatch")
+    return _lib

@@ -1,0 +1,108 @@
+// psim_device.h -- device-side data layout and primitives of the MI355X
+// overlay simulator (gfx950).  See DESIGN.md section 3 for the HBM layout.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/partisan_gpu_sim.h"
+
+namespace psim {
+
+// ---------------------------------------------------------------- layout --
+// Per-node header: one 64-B line holding every scalar of a node.
+struct __attribute__((aligned(16))) Hdr {
+    uint64_t rng;          // Philox draw counter of the node's manager process
+    uint32_t start_round;  // round the node (re)started
+    uint32_t join_contact; // contact to JOIN at start_round, PSIM_NONE for seeds
+    uint32_t epoch;
+    uint32_t pt_root;      // root of the single per-root eager/lazy slot, PSIM_NONE
+    uint32_t have;         // plumtree_backend ETS: bitmask of delivered msg ids (mod 32)
+    uint32_t trk_round;    // round of first delivery of the tracked broadcast
+    uint32_t trk_hop;      // plumtree Round + 1 at that delivery (0 at the root)
+    uint8_t act_n, pas_n, sent_n, sent_head;
+    uint8_t recv_n, recv_head, all_n, com_n;
+    uint8_t eag_n, laz_n, out_n, pad0;
+    uint32_t pad1[4];
+};
+static_assert(sizeof(Hdr) == 64, "Hdr must be one 64-B line");
+
+// Message record (64 B): written once by the sender, read once by the
+// receiver.  tt = type | ttl << 8 | nex << 16.
+struct __attribute__((aligned(16))) Msg {
+    uint32_t dst, src, tt, seq;
+    uint32_t a0, a1, a2, pad;
+    uint32_t ex[PSIM_EXCHANGE_CAP];
+};
+static_assert(sizeof(Msg) == 64, "Msg must be 64 B");
+
+// node flag byte
+enum : uint8_t { F_UP = 1, F_CRASHED = 2, F_LAZY = 4 };
+
+// route key: dst in the low 27 bits, the sender-side emission bound of the
+// message type in the top 5 (used to size the receiver's next outbox).
+constexpr uint32_t KEY_DST_BITS = 27;
+constexpr uint32_t KEY_DST_MASK = (1u << KEY_DST_BITS) - 1;
+
+// outbox bound: per inbox message (by type) and per node
+__host__ __device__ constexpr uint32_t max_emit(uint32_t type) {
+    // JOIN: DISCONNECT + NEIGHBOR + FORWARD_JOIN to up to ACTIVE_CAP-2 peers
+    return type == PSIM_MSG_JOIN ? 2 + (PSIM_ACTIVE_CAP - 2)
+         : type == PSIM_MSG_FORWARD_JOIN ? 2
+         : type == PSIM_MSG_NEIGHBOR ? 1
+         : type == PSIM_MSG_DISCONNECT ? 1
+         : type == PSIM_MSG_NEIGHBOR_REQUEST ? 2
+         : type == PSIM_MSG_NEIGHBOR_ACCEPTED ? 1
+         : type == PSIM_MSG_SHUFFLE ? 1
+         : type == PSIM_MSG_PT_BROADCAST ? PSIM_PT_SET_CAP
+         : type == PSIM_MSG_PT_IHAVE ? 1
+         : type == PSIM_MSG_PT_GRAFT ? 1
+         : 0;
+}
+constexpr uint32_t BOUND_BASE = 3;                        // JOIN send, promotion, shuffle
+constexpr uint32_t BOUND_EXITS = PSIM_ACTIVE_CAP - 1;     // EXIT-driven NEIGHBOR_REQUESTs
+constexpr uint32_t BOUND_LAZY = PSIM_PT_OUT_CAP;          // IHAVEs of one lazy tick
+constexpr uint32_t BOUND_ORIGIN = PSIM_PT_SET_CAP;        // eager push of the root
+
+// stats slots in the per-block partial arrays
+enum {
+    ST_EMIT = 0, ST_DELIV = 16, ST_DROPPED = 32, ST_UP, ST_PROC, ST_EXITS, ST_FAIL, ST_FIRST,
+    ST_OVF, ST_DIGEST, ST_BYTES, NST
+};
+
+// ------------------------------------------------------------------ RNG --
+// Philox4x32-10; key = seed, counter = (draw#, node id, stream).
+__device__ __forceinline__ void philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
+                                       uint32_t k0, uint32_t k1, uint32_t& o0, uint32_t& o1) {
+#pragma unroll
+    for (int i = 0; i < 10; i++) {
+        uint32_t lo0 = 0xD2511F53u * c0, hi0 = __umulhi(0xD2511F53u, c0);
+        uint32_t lo1 = 0xCD9E8D57u * c2, hi1 = __umulhi(0xCD9E8D57u, c2);
+        uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+        c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+        k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+    }
+    o0 = c0; o1 = c1;
+}
+
+__device__ __forceinline__ uint64_t draw58_at(uint64_t ctr, uint32_t node, uint64_t seed) {
+    uint32_t o0, o1;
+    philox((uint32_t)ctr, (uint32_t)(ctr >> 32), node, 0u, (uint32_t)seed, (uint32_t)(seed >> 32),
+           o0, o1);
+    return ((((uint64_t)o1) << 32) | o0) >> 6;
+}
+
+// sets v1 bucket of an element (stand-in for erlang:phash(NodeSpec, 16))
+__host__ __device__ __forceinline__ uint32_t bucket16(uint32_t id) {
+    uint32_t h = id;
+    h ^= h >> 16; h *= 0x85EBCA6Bu; h ^= h >> 13; h *= 0xC2B2AE35u; h ^= h >> 16;
+    return h & 15u;
+}
+
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+    z ^= z >> 30; z *= 0xBF58476D1CE4E5B9ull;
+    z ^= z >> 27; z *= 0x94D049BB133111EBull;
+    z ^= z >> 31;
+    return z;
+}
+
+}  // namespace psim

@@ -1,0 +1,36 @@
+// psim_kernels.h -- kernel argument blocks shared by the kernel TUs and the host.
+#pragma once
+#include "psim_device.h"
+
+namespace psim {
+
+struct RoundArgs {
+    // config
+    uint32_t n_nodes, round;
+    uint64_t seed;
+    uint32_t max_active, min_active, max_passive, arwl, prwl, k_active, k_passive;
+    uint32_t shuffle_period, promotion_period, random_promotion, plumtree, lazy_tick_period;
+    // per-round scalars
+    uint32_t crash_round, origin_now, origin_node, origin_msg, tracked_msg, bcast_root;
+    // node state (SoA rows)
+    uint8_t* flags;
+    const uint8_t* part;
+    Hdr* hdr;
+    uint32_t *act, *pas, *sentp, *senti, *recvp, *recvi;
+    uint32_t *pt_all, *pt_com, *pt_eag, *pt_laz;
+    uint64_t* pt_out;
+    // inbox (this round) and outbox (next round)
+    const uint32_t* in_beg;
+    const uint32_t* in_cnt;
+    const uint32_t* in_slot;
+    const Msg* rec_in;
+    const uint64_t* obase;
+    Msg* rec_out;
+    uint32_t* okey;
+    uint32_t* ocnt;
+    uint64_t* stat_part;   // [gridDim.x][NST]
+};
+
+__global__ void k_consume(RoundArgs args);
+
+}  // namespace psim

@@ -1,0 +1,170 @@
+"""Host-side driver over the C ABI (include/partisan_gpu_sim.h).
+
+`Simulator` is the product entry point: it loads only the HIP library
+(libpartisan_gpu_sim.so) and raises if it is missing.  `_Driver` holds the
+backend-independent logic so the tests can drive the CPU oracle through the
+same code (tests/_oracle.py).
+"""
+import ctypes as C
+
+import numpy as np
+
+from . import _abi
+from .workloads import NONE
+
+
+class SimError(RuntimeError):
+    pass
+
+
+def default_config(**kw):
+    cfg = _abi.PsimConfig()
+    cfg.abi_version = _abi.PSIM_ABI_VERSION
+    cfg.n_nodes = 32
+    cfg.seed = 1
+    # partisan_config.erl:102-145 defaults
+    cfg.max_active_size, cfg.min_active_size, cfg.max_passive_size = 6, 3, 30
+    cfg.arwl, cfg.prwl, cfg.k_active, cfg.k_passive = 5, 30, 3, 4
+    cfg.shuffle_period, cfg.promotion_period, cfg.random_promotion = 10, 5, 1
+    cfg.persist_epoch, cfg.plumtree, cfg.lazy_tick_period = 0, 1, 1
+    cfg.device, cfg.n_shards, cfg.shard_rank, cfg.shard_world = -1, 1, 0, 1
+    cfg.comm_id = None
+    cfg.max_msgs_per_round = 0
+    for k, v in kw.items():
+        if not hasattr(cfg, k):
+            raise KeyError(k)
+        setattr(cfg, k, v)
+    return cfg
+
+
+class _Driver:
+    """Backend-independent host logic: event batching, stats decoding."""
+
+    def __init__(self, api, cfg, errname=None):
+        self._api = api
+        self._errname = errname
+        self.cfg = cfg
+        self.n = cfg.n_nodes
+        h = C.c_void_p()
+        self._check(api["create"](C.byref(cfg), C.byref(h)), "create")
+        self._h = h
+
+    def _check(self, rc, what):
+        if rc != 0:
+            msg = _abi.ERRORS.get(rc, str(rc))
+            if self._errname is not None:
+                msg = self._errname(rc).decode()
+            raise SimError(f"{what}: {msg}")
+
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            self._api["destroy"](self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    # ---- events (applied at the start of the next round)
+    def join(self, nodes, contacts):
+        nodes = np.ascontiguousarray(nodes, np.uint32)
+        contacts = np.ascontiguousarray(contacts, np.uint32)
+        assert nodes.shape == contacts.shape
+        self._check(self._api["join"](self._h, _abi.u32p(nodes), _abi.u32p(contacts), nodes.size),
+                    "join")
+
+    def crash(self, nodes):
+        nodes = np.ascontiguousarray(nodes, np.uint32)
+        self._check(self._api["crash"](self._h, _abi.u32p(nodes), nodes.size), "crash")
+
+    def set_partition(self, group):
+        g = np.ascontiguousarray(group, np.uint8)
+        self._check(self._api["set_partition"](
+            self._h, g.ctypes.data_as(C.POINTER(C.c_uint8)), g.size), "set_partition")
+
+    def clear_partition(self):
+        self._check(self._api["clear_partition"](self._h), "clear_partition")
+
+    def broadcast(self, root, msg_id):
+        self._check(self._api["broadcast"](self._h, root, msg_id), "broadcast")
+
+    # ---- execution
+    def step(self, n_rounds=1):
+        st = np.zeros(n_rounds, _abi.STATS_DTYPE)
+        self._check(self._api["step"](self._h, n_rounds,
+                                      st.ctypes.data_as(C.POINTER(_abi.PsimRoundStats))), "step")
+        return st
+
+    @property
+    def round(self):
+        r = C.c_uint64()
+        self._check(self._api["get_round"](self._h, C.byref(r)), "get_round")
+        return r.value
+
+    def nodes(self, first=0, count=None):
+        if count is None:
+            count = self.n - first
+        out = np.zeros(count, _abi.NODE_VIEW_DTYPE)
+        self._check(self._api["get_nodes"](self._h, first, count,
+                                           out.ctypes.data_as(C.POINTER(_abi.PsimNodeView))),
+                    "get_nodes")
+        return out
+
+    def run_schedule(self, schedule, until_round, extra=None):
+        """Apply [(round, ids, contacts)] join events and step until `until_round`.
+        `extra(round)` may inject further events before each round."""
+        ev = {}
+        for r, ids, contacts in schedule:
+            ev.setdefault(r, []).append((ids, contacts))
+        stats = []
+        while self.round < until_round:
+            r = self.round
+            for ids, contacts in ev.get(r, []):
+                self.join(ids, contacts)
+            if extra is not None:
+                extra(r)
+            stats.append(self.step(1))
+        return np.concatenate(stats) if stats else np.zeros(0, _abi.STATS_DTYPE)
+
+    # ---- reference-style debug getters (hyparview:261-281)
+    def active(self, node):
+        v = self.nodes(node, 1)[0]
+        return [int(x) for x in v["act"][: v["act_n"]]]
+
+    def passive(self, node):
+        v = self.nodes(node, 1)[0]
+        return [int(x) for x in v["pas"][: v["pas_n"]]]
+
+
+class Simulator(_Driver):
+    """MI355X simulator handle (HIP library; fails loudly without it)."""
+
+    def __init__(self, cfg=None, **kw):
+        from . import _lib
+
+        lib = _lib.load()
+        api = _abi.bind(lib, "psim_", _abi.SIGNATURES)
+        extra = _abi.bind(lib, "psim_", _abi.GPU_ONLY)
+        self._extra = extra
+        if cfg is None:
+            cfg = default_config(**kw)
+        super().__init__(api, cfg, errname=extra["strerror"])
+
+    def kernel_times(self):
+        cap = 64
+        names = (C.c_char_p * cap)()
+        ms = (C.c_double * cap)()
+        launches = (C.c_uint64 * cap)()
+        k = self._extra["kernel_times"](self._h, names, ms, launches, cap)
+        return {names[i].decode(): (ms[i], launches[i]) for i in range(k)}
+
+
+__all__ = ["Simulator", "SimError", "default_config", "NONE"]

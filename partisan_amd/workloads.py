@@ -1,0 +1,69 @@
+"""Synthetic workloads for BASELINE.json configs A-E.
+
+Every schedule is a pure function of (N, seed) drawn from numpy's PCG64, so the
+GPU engine and the CPU oracle receive identical event streams.
+"""
+import numpy as np
+
+NONE = 0xFFFFFFFF
+
+
+def _rng(seed, salt):
+    return np.random.Generator(np.random.PCG64([int(seed) & 0xFFFFFFFFFFFFFFFF, salt]))
+
+
+def sequential_join(n_nodes):
+    """Config A topology (test/partisan_SUITE.erl:1591-1601, partisan_support
+    :377-388): node 0 is the server, node i joins node 0 at round i."""
+    sched = [(0, np.array([0], np.uint32), np.array([NONE], np.uint32))]
+    for i in range(1, n_nodes):
+        sched.append((i, np.array([i], np.uint32), np.array([0], np.uint32)))
+    return sched
+
+
+def doubling_join(n_nodes, seed):
+    """Bootstrap ramp for large overlays: round 0 starts node 0; round r >= 1
+    starts ids [2^(r-1), 2^r) and each joins a uniformly drawn node among the
+    ids started earlier (so every live node receives ~1 JOIN per round)."""
+    rng = _rng(seed, 1)
+    sched = [(0, np.array([0], np.uint32), np.array([NONE], np.uint32))]
+    lo, r = 1, 1
+    while lo < n_nodes:
+        hi = min(2 * lo, n_nodes)
+        ids = np.arange(lo, hi, dtype=np.uint32)
+        contacts = rng.integers(0, lo, size=hi - lo, dtype=np.uint64).astype(np.uint32)
+        sched.append((r, ids, contacts))
+        lo, r = hi, r + 1
+    return sched
+
+
+def star_join(n_nodes, at_round=1):
+    """Hot-spot case: every node joins node 0 in the same round."""
+    ids = np.arange(1, n_nodes, dtype=np.uint32)
+    return [(0, np.array([0], np.uint32), np.array([NONE], np.uint32)),
+            (at_round, ids, np.zeros(n_nodes - 1, np.uint32))]
+
+
+def churn_schedule(n_nodes, seed, frac, first_round, n_rounds, protect=(0,)):
+    """Config E churn: frac*N crashes spread uniformly over n_rounds starting
+    at first_round; each crashed node restarts the next round and rejoins a
+    uniformly drawn node that is not crashing."""
+    rng = _rng(seed, 2)
+    total = int(frac * n_nodes)
+    cand = np.setdiff1d(np.arange(n_nodes, dtype=np.uint32), np.array(protect, np.uint32))
+    victims = rng.choice(cand, size=min(total, cand.size), replace=False).astype(np.uint32)
+    per = np.array_split(victims, n_rounds)
+    out = []
+    for k, v in enumerate(per):
+        contacts = rng.integers(0, n_nodes, size=v.size, dtype=np.uint64).astype(np.uint32)
+        # never join yourself or someone crashing in the same round
+        bad = np.isin(contacts, v)
+        contacts[bad] = np.uint32(protect[0])
+        out.append((first_round + k, v, contacts))
+    return out
+
+
+def half_partition(n_nodes):
+    g = np.zeros(n_nodes, np.uint8)
+    g[n_nodes // 2:] = 1
+    return g

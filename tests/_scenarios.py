@@ -1,0 +1,120 @@
+"""Event scripts shared by the oracle tests and the GPU parity tests.  Each
+scenario drives any `_Driver` (GPU Simulator or CPU Oracle) through the same
+API calls, so two backends can be compared round by round."""
+import numpy as np
+
+from partisan_amd import workloads as W
+from partisan_amd.sim import default_config
+
+STAT_FIELDS = ["emitted", "delivered", "dropped", "nodes_up", "nodes_processed", "exits",
+               "send_fail", "first_deliveries", "overflow", "digest"]
+
+
+def _bcast_every(sim, period, first, root=0, count=None):
+    state = {"k": 0}
+
+    def hook(r):
+        if r >= first and (r - first) % period == 0 and (count is None or state["k"] < count):
+            sim.broadcast(root, state["k"] % 0x10000)
+            state["k"] += 1
+    return hook
+
+
+def config_a(make, seed=1, rounds=200, tail=40):
+    """Config A: 32 nodes join node 0 one per round, 200 rounds, then one
+    broadcast from node 0 (test/partisan_SUITE.erl:1591-1601, :2044-2108)."""
+    sim = make(default_config(n_nodes=32, seed=seed))
+    st = [sim.run_schedule(W.sequential_join(32), rounds)]
+    sim.broadcast(0, 7)
+    st.append(sim.step(tail))
+    return sim, np.concatenate(st)
+
+
+def doubling(make, n, seed, rounds, bcast_period=None, bcast_first=None, **cfg):
+    sim = make(default_config(n_nodes=n, seed=seed, **cfg))
+    hook = None
+    if bcast_period:
+        hook = _bcast_every(sim, bcast_period, bcast_first)
+    st = sim.run_schedule(W.doubling_join(n, seed), rounds, extra=hook)
+    return sim, st
+
+
+def churn_partition(make, n=2048, seed=5, rounds=140, **cfg):
+    """Config E in miniature: doubling bootstrap, 20% churn over rounds
+    40-79, a half/half partition for rounds 90-99, a broadcast every 10."""
+    sim = make(default_config(n_nodes=n, seed=seed, **cfg))
+    churn = {r: (v, c) for r, v, c in W.churn_schedule(n, seed, 0.2, 40, 40)}
+    part = W.half_partition(n)
+    bc = _bcast_every(sim, 10, 30)
+
+    def hook(r):
+        if r in churn:
+            v, c = churn[r]
+            sim.crash(v)
+            sim.join(v, c)
+        if r == 90:
+            sim.set_partition(part)
+        if r == 100:
+            sim.clear_partition()
+        bc(r)
+    st = sim.run_schedule(W.doubling_join(n, seed), rounds, extra=hook)
+    return sim, st
+
+
+def crash_only(make, n=1024, seed=9, rounds=80):
+    """Crashes without restarts: EXIT handling and the stopped-member check
+    (test/partisan_SUITE.erl:2024-2041)."""
+    sim = make(default_config(n_nodes=n, seed=seed))
+    victims = np.arange(3, n, 17, dtype=np.uint32)
+
+    def hook(r):
+        if r == 40:
+            sim.crash(victims)
+    st = sim.run_schedule(W.doubling_join(n, seed), rounds, extra=hook)
+    return sim, st, victims
+
+
+def star(make, n=512, seed=3, rounds=60):
+    sim = make(default_config(n_nodes=n, seed=seed))
+    st = sim.run_schedule(W.star_join(n), rounds)
+    sim.broadcast(0, 1)
+    st2 = sim.step(30)
+    return sim, np.concatenate([st, st2])
+
+
+def compare_stats(a, b):
+    assert a.shape == b.shape
+    for f in STAT_FIELDS:
+        if not np.array_equal(a[f], b[f]):
+            bad = np.nonzero((a[f] != b[f]).reshape(len(a), -1).any(1))[0]
+            raise AssertionError(f"stats field {f} differs first at round {int(a['round'][bad[0]])}")
+
+
+def compare_nodes(a, b):
+    for f in a.dtype.names:
+        if not np.array_equal(a[f], b[f]):
+            bad = np.nonzero((a[f] != b[f]).reshape(len(a), -1).any(1))[0]
+            raise AssertionError(f"node field {f} differs at nodes {bad[:8].tolist()}")
+
+
+def active_graph(views):
+    return {i: set(int(x) for x in v["act"][: v["act_n"]]) - {i}
+            for i, v in enumerate(views) if v["up"]}
+
+
+def connected(adj):
+    if not adj:
+        return True
+    start = next(iter(adj))
+    seen, stack = {start}, [start]
+    while stack:
+        x = stack.pop()
+        for y in adj[x]:
+            if y in adj and y not in seen:
+                seen.add(y)
+                stack.append(y)
+    return len(seen) == len(adj)
+
+
+def asymmetric(adj):
+    return [(i, j) for i in adj for j in adj[i] if j in adj and i not in adj[j]]
