@@ -145,12 +145,19 @@ __global__ void k_compact(const uint32_t* ocnt, const uint32_t* dpos, const uint
     }
 }
 
+// one block per stats slot; lanes stride over the per-block partials
 __global__ void k_stats_reduce(const uint64_t* part, uint32_t nblocks, uint64_t* out) {
-    uint32_t k = threadIdx.x;
-    if (k >= NST) return;
+    __shared__ uint64_t red[BLK];
+    uint32_t k = blockIdx.x;
     uint64_t s = 0;
-    for (uint32_t b = 0; b < nblocks; b++) s += part[(size_t)b * NST + k];
-    out[k] = s;
+    for (uint32_t b = threadIdx.x; b < nblocks; b += blockDim.x) s += part[(size_t)b * NST + k];
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (uint32_t w = blockDim.x / 2; w > 0; w >>= 1) {
+        if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) out[k] = red[0];
 }
 
 // ------------------------------------------------------------- buffers --
@@ -400,7 +407,7 @@ int run_round(psim_handle* h, uint64_t* stats_out) {
     }
     {
         KTimer t(h, KT_STATS);
-        k_stats_reduce<<<1, 64, 0, h->stream>>>(h->stat_part.p, cgrid, h->stat_out.p);
+        k_stats_reduce<<<NST, BLK, 0, h->stream>>>(h->stat_part.p, cgrid, h->stat_out.p);
         if (!crashed.empty()) {
             if ((rc = upload(h, h->ev_ids, crashed))) return rc;
             k_uncrash<<<grid_for(crashed.size()), BLK, 0, h->stream>>>(h->flags.p, h->ev_ids.p,
