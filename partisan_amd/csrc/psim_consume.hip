@@ -1,11 +1,18 @@
 // psim_consume.hip -- the node-round kernel (K-consume + K-timer + K-emit).
 //
-// One lane owns one node for the whole round: it runs the node's EXIT events,
-// its HyParView inbox, its timers, then its Plumtree inbox, origin broadcast
-// and lazy tick, in the fixed order of the round model R0 (DESIGN.md section
-// 2).  Everything the lane touches besides its own rows is read-only for the
-// round (the flag/partition bytes of peers and the previous round's message
-// records), so lanes never race.
+// One 64-lane wave owns one node at a time (grid-stride over nodes).  The
+// node's views are spread across lanes -- lane l holds active[l], passive[l],
+// the l-th disconnect-id slot, the l-th Plumtree set entries -- so every list
+// operation of the reference handlers (member, --, usort, select_random,
+// sublist(shuffle(..)), ordsets add/del) becomes a handful of ballots and
+// shuffles, and control flow is wave-uniform: no divergence between nodes
+// and no scratch.  Messages are read and written as one coalesced 64-B record
+// by lanes 0-15.
+//
+// The wave runs the node's EXIT events, HyParView inbox, timers, then its
+// Plumtree inbox, origin broadcast and lazy tick, in the fixed order of the
+// round model R0.  Besides its own rows a wave reads
+// only the flag/partition bytes of peers and the previous round's records.
 //
 // Reference handlers are cited as file:line under /root/reference:
 //   hv = src/partisan_hyparview_peer_service_manager.erl
@@ -18,456 +25,509 @@ namespace psim {
 #define ID_OF(e, n) (((uint32_t)(e) << 20) | (uint32_t)(n))
 #define ID_E(id) ((id) >> 20)
 #define ID_C(id) ((id)&0xFFFFFu)
+#define DEV __device__ __forceinline__
 
-struct Lane {
-    const RoundArgs* a;
-    uint32_t me;
-    uint8_t mypart;
-    Hdr h;
-    uint32_t *act, *pas, *sentp, *senti, *recvp, *recvi, *all, *com, *eag, *laz;
-    uint64_t* out;               // outstanding: peer << 32 | msg << 16 | round
-    Msg* ob;                     // this node's outbox region
-    uint32_t* okey;
-    uint32_t seq;
-    uint64_t* st;                // LDS stats of the block
-};
+constexpr int WAVES_PER_BLOCK = 4;
+constexpr uint32_t NONE = PSIM_NONE;
 
-__device__ __forceinline__ void st_add(Lane& L, int k, uint64_t v) {
-    atomicAdd((unsigned long long*)&L.st[k], (unsigned long long)v);
+// ------------------------------------------------------------ wave ops --
+DEV uint32_t lane_id() { return __lane_id(); }
+DEV uint64_t ballot(bool p) { return __ballot(p); }
+DEV uint32_t popc(uint64_t m) { return (uint32_t)__popcll(m); }
+DEV int ffs64(uint64_t m) { return m ? __ffsll((long long)m) - 1 : -1; }
+DEV uint64_t lt_mask() { return (1ull << lane_id()) - 1ull; }
+DEV uint32_t shfl(uint32_t v, int src) { return (uint32_t)__shfl((int)v, src); }
+DEV uint64_t shfl64(uint64_t v, int src) {
+    uint32_t lo = shfl((uint32_t)v, src), hi = shfl((uint32_t)(v >> 32), src);
+    return ((uint64_t)hi << 32) | lo;
+}
+DEV uint32_t rl(uint32_t v, int i) { return __builtin_amdgcn_readlane(v, i); }
+DEV uint64_t rl64(uint64_t v, int i) {
+    return ((uint64_t)rl((uint32_t)(v >> 32), i) << 32) | rl((uint32_t)v, i);
+}
+DEV uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+
+// lane-distributed list V of n entries (lanes >= n hold 0)
+DEV bool has(uint32_t V, uint32_t n, uint32_t e) { return ballot(lane_id() < n && V == e) != 0; }
+DEV int idx_of(uint32_t V, uint32_t n, uint32_t e) { return ffs64(ballot(lane_id() < n && V == e)); }
+
+// delete entry k (order preserving)
+DEV void vdel(uint32_t& V, uint32_t& n, uint32_t k) {
+    uint32_t l = lane_id();
+    uint32_t nx = shfl(V, (int)((l + 1) & 63));
+    V = l < k ? V : (l + 1 < n ? nx : 0u);
+    n--;
+}
+DEV void vdel64(uint64_t& V, uint32_t& n, uint32_t k) {
+    uint32_t l = lane_id();
+    uint64_t nx = shfl64(V, (int)((l + 1) & 63));
+    V = l < k ? V : (l + 1 < n ? nx : 0ull);
+    n--;
+}
+// insert e at position pos
+DEV void vins(uint32_t& V, uint32_t& n, uint32_t pos, uint32_t e) {
+    uint32_t l = lane_id();
+    uint32_t pv = shfl(V, (int)((l + 63) & 63));
+    V = l < pos ? V : (l == pos ? e : (l <= n ? pv : 0u));
+    n++;
+}
+DEV void vins64(uint64_t& V, uint32_t& n, uint32_t pos, uint64_t e) {
+    uint32_t l = lane_id();
+    uint64_t pv = shfl64(V, (int)((l + 63) & 63));
+    V = l < pos ? V : (l == pos ? e : (l <= n ? pv : 0ull));
+    n++;
+}
+DEV bool vdel_val(uint32_t& V, uint32_t& n, uint32_t e) {
+    int k = idx_of(V, n, e);
+    if (k < 0) return false;
+    vdel(V, n, (uint32_t)k);
+    return true;
+}
+// sets:add_element/2 in sets:to_list/1 order: after every element whose
+// bucket is <= the new element's bucket (new = youngest of its bucket)
+DEV void view_add(uint32_t& V, uint32_t& n, uint32_t e) {
+    uint32_t b = bucket16(e);
+    uint32_t pos = popc(ballot(lane_id() < n && bucket16(V) <= b));
+    vins(V, n, pos, e);
 }
 
-// ---------------------------------------------------------------- RNG --
-__device__ __forceinline__ uint64_t draw(Lane& L) { return draw58_at(L.h.rng++, L.me, L.a->seed); }
+// ascending bitonic sort of lanes 0..31 (lanes 32..63 sort their own half)
+DEV uint32_t sort32(uint32_t v) {
+    uint32_t l = lane_id();
+#pragma unroll
+    for (uint32_t k = 2; k <= 32; k <<= 1) {
+#pragma unroll
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            uint32_t p = (uint32_t)__shfl_xor((int)v, (int)j);
+            bool keep_min = ((l & j) == 0) == ((l & k) == 0);
+            v = keep_min ? min(v, p) : max(v, p);
+        }
+    }
+    return v;
+}
+
+// ------------------------------------------------------------ the wave --
+struct Wv {
+    const RoundArgs* a;
+    uint32_t* lds;       // 64 words of per-wave scratch
+    uint64_t* st;        // block stats (LDS)
+    uint32_t me, mypart, round;
+    Hdr h;
+    uint32_t act_n, pas_n, sent_n, sent_head, recv_n, recv_head;
+    uint32_t all_n, com_n, eag_n, laz_n, out_n;
+    uint32_t A, P, SP, SI, RP, RI, ALL, COM, EAG, LAZ;
+    uint64_t OUT;
+    bool maps, pt;
+    uint64_t obase;
+    uint32_t seq;
+    uint64_t digest;
+};
+
+DEV void st_add(Wv& w, int k, uint64_t v) {
+    if (lane_id() == 0) atomicAdd((unsigned long long*)&w.st[k], (unsigned long long)v);
+}
+
+// compact the lanes of V selected by `keep` (uniform mask) to the front
+DEV uint32_t compact(Wv& w, uint32_t V, uint64_t keep) {
+    uint32_t l = lane_id();
+    if ((keep >> l) & 1ull) w.lds[popc(keep & lt_mask())] = V;
+    __builtin_amdgcn_wave_barrier();
+    uint32_t m = popc(keep);
+    uint32_t r = l < m ? w.lds[l] : 0u;
+    __builtin_amdgcn_wave_barrier();
+    return r;
+}
+DEV uint64_t compact64(Wv& w, uint64_t V, uint64_t keep) {
+    uint32_t lo = compact(w, (uint32_t)V, keep);
+    uint32_t hi = compact(w, (uint32_t)(V >> 32), keep);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// lists:usort of the first m lanes of E; returns count, E sorted/unique, rest 0
+DEV uint32_t usort_lanes(Wv& w, uint32_t& E, uint32_t m) {
+    uint32_t l = lane_id();
+    uint32_t v = l < m ? E : 0xFFFFFFFFu;
+    v = sort32(v);
+    uint32_t prev = shfl(v, (int)((l + 63) & 63));
+    uint64_t keep = ballot(l < 32 && l < m && (l == 0 || v != prev));
+    E = compact(w, v, keep);
+    return popc(keep);
+}
+
+// ----------------------------------------------------------------- RNG --
+DEV uint64_t draw(Wv& w) { return draw58_at(w.h.rng++, w.me, w.a->seed); }
 
 // rand:uniform/1 with a 58-bit generator (OTP rand.erl ?uniform_range)
-__device__ uint32_t uniform_n(Lane& L, uint32_t n) {
+DEV uint32_t uniform_n(Wv& w, uint32_t n) {
     const uint64_t two58 = 1ull << 58;
     for (;;) {
-        uint64_t v = draw(L);
+        uint64_t v = draw(w);
         if (v < n) return (uint32_t)v + 1;
         uint64_t i = v % n;
         if (v - i <= two58 - n) return (uint32_t)i + 1;
     }
 }
 
-// ------------------------------------------------------- row primitives --
-__device__ __forceinline__ int find(const uint32_t* row, uint32_t n, uint32_t e) {
-    for (uint32_t i = 0; i < n; i++)
-        if (row[i] == e) return (int)i;
-    return -1;
+// select_random/2 (hv:1346-1356): rand:uniform(length(View -- Omit));
+// nothing drawn when nothing is eligible
+DEV uint32_t select_random(Wv& w, uint32_t V, uint32_t n, uint32_t o0, uint32_t o1, uint32_t o2) {
+    uint32_t l = lane_id();
+    uint64_t M = ballot(l < n && V != o0 && V != o1 && V != o2);
+    uint32_t cnt = popc(M);
+    if (cnt == 0) return NONE;
+    uint32_t k = uniform_n(w, cnt) - 1;
+    uint64_t sel = ballot(((M >> l) & 1ull) && popc(M & lt_mask()) == k);
+    return rl(V, ffs64(sel));
 }
 
-// sets:add_element/2 keeping sets:to_list/1 order: (bucket, insertion seq)
-__device__ void view_add(uint32_t* row, uint8_t& n, uint32_t e) {
-    uint32_t b = bucket16(e);
-    uint32_t i = n;
-    while (i > 0 && bucket16(row[i - 1]) > b) { row[i] = row[i - 1]; i--; }
-    row[i] = e;
-    n++;
-}
-
-// sets:del_element/2 (order preserving); vacated slot zeroed
-__device__ bool row_del(uint32_t* row, uint8_t& n, uint32_t e) {
-    int k = find(row, n, e);
-    if (k < 0) return false;
-    for (uint32_t i = k; i + 1 < n; i++) row[i] = row[i + 1];
-    n--;
-    row[n] = 0;
-    return true;
-}
-
-// ordsets:add_element/2 into a sorted row of capacity cap
-__device__ bool ord_add(Lane& L, uint32_t* row, uint8_t& n, uint32_t cap, uint32_t e) {
-    uint32_t i = n;
-    while (i > 0 && row[i - 1] > e) i--;
-    if (i > 0 && row[i - 1] == e) return true;
-    if (n >= cap) { st_add(L, ST_OVF, 1); return false; }
-    for (uint32_t j = n; j > i; j--) row[j] = row[j - 1];
-    row[i] = e;
-    n++;
-    return true;
-}
-
-// select_random/2 (hv:1346-1356): uniform index over View -- Omit, no draw
-// when nothing is eligible.  Up to three omitted elements.
-__device__ uint32_t select_random(Lane& L, const uint32_t* row, uint32_t n, uint32_t o0,
-                                  uint32_t o1, uint32_t o2) {
-    uint32_t cnt = 0;
-    for (uint32_t i = 0; i < n; i++) {
-        uint32_t e = row[i];
-        cnt += (e != o0 && e != o1 && e != o2);
-    }
-    if (cnt == 0) return PSIM_NONE;
-    uint32_t k = uniform_n(L, cnt) - 1;
-    for (uint32_t i = 0; i < n; i++) {
-        uint32_t e = row[i];
-        if (e != o0 && e != o1 && e != o2) {
-            if (k == 0) return e;
-            k--;
-        }
-    }
-    return PSIM_NONE;
-}
-
-// lists:sublist(shuffle(to_list(View)), K) (hv:1359-1361, :1586-1587).
-// Element i's sort key is the counter-based draw at rng+i, so the k smallest
-// (key, elem) pairs are found by k selection passes without storing keys.
-__device__ uint32_t sublist(Lane& L, const uint32_t* row, uint32_t n, uint32_t k, uint32_t* out,
-                            uint32_t on) {
-    uint64_t base = L.h.rng;
-    uint64_t pk = 0;
-    uint32_t pe = 0;
-    bool first = true;
+// lists:sublist(shuffle(to_list(View)), K) (hv:1359-1361, :1586-1587): one
+// rand:uniform() key per element (element l draws at rng + l), the K
+// smallest (key, element) pairs in order, appended to OUT at lanes on..
+DEV uint32_t sublist(Wv& w, uint32_t V, uint32_t n, uint32_t k, uint32_t& OUT, uint32_t on) {
+    uint32_t l = lane_id();
+    uint64_t base = w.h.rng;
+    uint64_t key = l < n ? (draw58_at(base + l, w.me, w.a->seed) >> 5) : ~0ull;
     uint32_t m = n < k ? n : k;
     for (uint32_t j = 0; j < m; j++) {
-        uint64_t bk = ~0ull;
-        uint32_t be = 0xFFFFFFFFu;
-        for (uint32_t i = 0; i < n; i++) {
-            uint64_t kk = draw58_at(base + i, L.me, L.a->seed) >> 5;
-            uint32_t e = row[i];
-            bool after = first || kk > pk || (kk == pk && e > pe);
-            bool better = kk < bk || (kk == bk && e < be);
-            if (after && better) { bk = kk; be = e; }
+        uint64_t bk = key;
+        uint32_t be = V;
+#pragma unroll
+        for (int off = 16; off > 0; off >>= 1) {
+            uint64_t ok = ((uint64_t)(uint32_t)__shfl_xor((int)(bk >> 32), off) << 32) |
+                          (uint32_t)__shfl_xor((int)(uint32_t)bk, off);
+            uint32_t oe = (uint32_t)__shfl_xor((int)be, off);
+            bool take = ok < bk || (ok == bk && oe < be);
+            bk = take ? ok : bk;
+            be = take ? oe : be;
         }
-        out[on + j] = be;
-        pk = bk; pe = be; first = false;
+        uint64_t wk = rl64(bk, 0);
+        uint32_t we = rl(be, 0);
+        OUT = l == on + j ? we : OUT;
+        key = (key == wk && V == we) ? ~0ull : key;
     }
-    L.h.rng = base + n;
+    w.h.rng = base + n;
     return on + m;
 }
 
-// insertion-sort + dedupe (lists:usort/1 over ids)
-__device__ uint32_t usort_small(uint32_t* v, uint32_t n) {
-    for (uint32_t i = 1; i < n; i++) {
-        uint32_t x = v[i];
-        int j = (int)i - 1;
-        while (j >= 0 && v[j] > x) { v[j + 1] = v[j]; j--; }
-        v[j + 1] = x;
-    }
-    uint32_t k = n ? 1 : 0;
-    for (uint32_t i = 1; i < n; i++)
-        if (v[i] != v[k - 1]) v[k++] = v[i];
-    return k;
-}
-
 // ------------------------------------------------------------- emission --
-__device__ void emit(Lane& L, uint32_t dst, uint32_t type, uint32_t ttl, uint32_t a0, uint32_t a1,
-                     uint32_t a2, const uint32_t* ex, uint32_t nex) {
-    uint32_t s = L.seq++;
-    Msg m;
-    m.dst = dst; m.src = L.me; m.tt = type | (ttl << 8) | (nex << 16); m.seq = s;
-    m.a0 = a0; m.a1 = a1; m.a2 = a2; m.pad = 0;
-#pragma unroll
-    for (int i = 0; i < PSIM_EXCHANGE_CAP; i++) m.ex[i] = (uint32_t)i < nex ? ex[i] : 0u;
-    uint4* d = reinterpret_cast<uint4*>(&L.ob[s]);
-    const uint4* q = reinterpret_cast<const uint4*>(&m);
-    d[0] = q[0]; d[1] = q[1]; d[2] = q[2]; d[3] = q[3];
-    L.okey[s] = dst | (max_emit(type) << KEY_DST_BITS);
-    // digest: identical fold in the oracle (msg_hash)
-    uint64_t hh = 0x9E3779B97F4A7C15ull ^ (((uint64_t)dst << 32) | L.me);
+DEV void emit(Wv& w, uint32_t dst, uint32_t type, uint32_t ttl, uint32_t a0, uint32_t a1,
+              uint32_t a2, uint32_t EX, uint32_t nex) {
+    uint32_t l = lane_id();
+    uint32_t s = w.seq++;
+    uint64_t slot = w.obase + s;
+    uint32_t tt = type | (ttl << 8) | (nex << 16);
+    uint32_t exv = shfl(EX, (int)((l - 8) & 63));
+    uint32_t word = l == 0 ? dst : l == 1 ? w.me : l == 2 ? tt : l == 3 ? s : l == 4 ? a0
+                  : l == 5 ? a1 : l == 6 ? a2 : l == 7 ? 0u : (l - 8 < nex ? exv : 0u);
+    if (l < 16) reinterpret_cast<uint32_t*>(w.a->rec_out + slot)[l] = word;
+    if (l == 0) w.a->okey[slot] = dst | (max_emit(type) << KEY_DST_BITS);
+    // digest (the oracle's msg_hash, folded identically)
+    uint64_t hh = 0x9E3779B97F4A7C15ull ^ (((uint64_t)dst << 32) | w.me);
     hh = mix64(hh ^ (((uint64_t)s << 32) | (type << 16) | (ttl << 8) | nex));
     hh = mix64(hh ^ (((uint64_t)a0 << 32) | a1));
     hh = mix64(hh ^ a2);
-    for (uint32_t i = 0; i < nex; i++) hh = mix64(hh ^ (((uint64_t)ex[i] << 32) | i));
-    st_add(L, ST_DIGEST, hh);
-    st_add(L, ST_EMIT + type, 1);
+    for (uint32_t i = 0; i < nex; i++) hh = mix64(hh ^ (((uint64_t)rl(EX, i) << 32) | i));
+    w.digest += hh;
+    st_add(w, ST_EMIT + type, 1);
 }
 
-// maybe_connect + find (partisan_util.erl:75-134)
-__device__ __forceinline__ bool connect_ok(const Lane& L, uint32_t dst) {
-    if (dst >= L.a->n_nodes || dst == L.me) return false;
-    return (L.a->flags[dst] & F_UP) && L.a->part[dst] == L.mypart;
+// maybe_connect + find (partisan_util.erl:75-134): the peer's manager runs
+// and no partition separates the two
+DEV bool connect_ok(const Wv& w, uint32_t dst) {
+    if (dst >= w.a->n_nodes || dst == w.me) return false;
+    return (w.a->flags[dst] & F_UP) && w.a->part[dst] == w.mypart;
 }
 
-// do_send_message/3 (hv:1274-1343); a successful send draws
-// rand:uniform(1) in partisan_util:dispatch_pid/1 (util:190-195), which
-// always consumes exactly one value.
-__device__ void hv_send(Lane& L, uint32_t dst, uint32_t type, uint32_t ttl, uint32_t a0,
-                        const uint32_t* ex, uint32_t nex) {
-    if (!connect_ok(L, dst)) { st_add(L, ST_FAIL, 1); return; }
-    L.h.rng++;
-    emit(L, dst, type, ttl, a0, 0, 0, ex, nex);
+// do_send_message/3 (hv:1274-1343); success draws rand:uniform(1) in
+// partisan_util:dispatch_pid/1 (util:190-195), always exactly one value
+DEV void hv_send(Wv& w, uint32_t dst, uint32_t type, uint32_t ttl, uint32_t a0, uint32_t a1,
+                 uint32_t EX, uint32_t nex) {
+    if (!connect_ok(w, dst)) { st_add(w, ST_FAIL, 1); return; }
+    w.h.rng++;
+    emit(w, dst, type, ttl, a0, a1, 0, EX, nex);
 }
 
-// ------------------------------------------------------- disconnect ids --
-__device__ __forceinline__ int map_find(const uint32_t* peer, uint32_t n, uint32_t p) {
-    return find(peer, n, p);
+// ----------------------------------------------------------- id maps --
+DEV void load_maps(Wv& w) {
+    if (w.maps) return;
+    uint32_t l = lane_id();
+    size_t b = (size_t)w.me * PSIM_IDMAP_CAP + l;
+    bool in = l < PSIM_IDMAP_CAP;
+    w.SP = in ? w.a->sentp[b] : 0u; w.SI = in ? w.a->senti[b] : 0u;
+    w.RP = in ? w.a->recvp[b] : 0u; w.RI = in ? w.a->recvi[b] : 0u;
+    w.maps = true;
 }
 
-__device__ void map_store(Lane& L, uint32_t* peer, uint32_t* id, uint8_t& n, uint8_t& head,
-                          uint32_t p, uint32_t v) {
-    int i = map_find(peer, n, p);
-    if (i >= 0) { id[i] = v; return; }
-    if (n < PSIM_IDMAP_CAP) { peer[n] = p; id[n] = v; n++; return; }
-    st_add(L, ST_OVF, 1);
-    peer[head] = p; id[head] = v;
-    head = (uint8_t)((head + 1) % PSIM_IDMAP_CAP);
+DEV void map_store(Wv& w, uint32_t& PV, uint32_t& IV, uint32_t& n, uint32_t& head, uint32_t p,
+                   uint32_t v) {
+    uint32_t l = lane_id();
+    int i = idx_of(PV, n, p);
+    if (i >= 0) { IV = l == (uint32_t)i ? v : IV; return; }
+    if (n < PSIM_IDMAP_CAP) {
+        PV = l == n ? p : PV; IV = l == n ? v : IV; n++;
+        return;
+    }
+    st_add(w, ST_OVF, 1);
+    PV = l == head ? p : PV; IV = l == head ? v : IV;
+    head = (head + 1) % PSIM_IDMAP_CAP;
 }
 
-__device__ uint32_t current_id(Lane& L, uint32_t p) {   // hv:1622-1630
-    int i = map_find(L.recvp, L.h.recv_n, p);
-    return i >= 0 ? L.recvi[i] : ID_OF(1, 0);
+DEV uint32_t current_id(Wv& w, uint32_t p) {             // hv:1622-1630
+    load_maps(w);
+    int i = idx_of(w.RP, w.recv_n, p);
+    return i >= 0 ? rl(w.RI, i) : ID_OF(1, 0);
 }
-
-__device__ uint32_t next_id(Lane& L, uint32_t p) {      // hv:1633-1639
-    int i = map_find(L.sentp, L.h.sent_n, p);
-    if (i >= 0 && ID_E(L.senti[i]) == L.h.epoch) return L.senti[i] + 1;
-    return ID_OF(L.h.epoch, 1);
+DEV uint32_t next_id(Wv& w, uint32_t p) {                // hv:1633-1639
+    load_maps(w);
+    int i = idx_of(w.SP, w.sent_n, p);
+    if (i >= 0) {
+        uint32_t s = rl(w.SI, i);
+        if (ID_E(s) == w.h.epoch) return s + 1;
+    }
+    return ID_OF(w.h.epoch, 1);
 }
-
-__device__ bool addable_epoch(Lane& L, uint32_t pe, uint32_t p) {   // hv:1670-1676
-    int i = map_find(L.sentp, L.h.sent_n, p);
-    return i < 0 || pe >= ID_E(L.senti[i]);
+DEV bool addable_epoch(Wv& w, uint32_t pe, uint32_t p) { // hv:1670-1676
+    load_maps(w);
+    int i = idx_of(w.SP, w.sent_n, p);
+    return i < 0 || pe >= ID_E(rl(w.SI, i));
 }
-
-__device__ bool addable_id(Lane& L, uint32_t d, uint32_t p) {       // hv:1656-1669
-    int i = map_find(L.sentp, L.h.sent_n, p);
+DEV bool addable_id(Wv& w, uint32_t d, uint32_t p) {     // hv:1656-1669
+    load_maps(w);
+    int i = idx_of(w.SP, w.sent_n, p);
     if (i < 0) return true;
-    uint32_t s = L.senti[i];
+    uint32_t s = rl(w.SI, i);
     if (ID_E(d) != ID_E(s)) return ID_E(d) > ID_E(s);
     return ID_C(d) >= ID_C(s);
 }
-
-__device__ bool valid_disconnect(Lane& L, uint32_t p, uint32_t d) { // hv:1642-1653
-    int i = map_find(L.recvp, L.h.recv_n, p);
+DEV bool valid_disconnect(Wv& w, uint32_t p, uint32_t d) { // hv:1642-1653
+    load_maps(w);
+    int i = idx_of(w.RP, w.recv_n, p);
     if (i < 0) return true;
-    uint32_t s = L.recvi[i];
+    uint32_t s = rl(w.RI, i);
     if (ID_E(d) > ID_E(s)) return true;
     return ID_C(d) > ID_C(s);
 }
 
-// ---------------------------------------------------------- view updates --
-__device__ void add_to_passive(Lane& L, uint32_t p) {   // hv:1423-1448
-    if (p == L.me || find(L.act, L.h.act_n, p) >= 0 || find(L.pas, L.h.pas_n, p) >= 0) return;
-    if (L.h.pas_n >= L.a->max_passive) {
-        uint32_t r = select_random(L, L.pas, L.h.pas_n, L.me, L.me, L.me);
-        if (r != PSIM_NONE) row_del(L.pas, L.h.pas_n, r);
+// ------------------------------------------------------- view updates --
+DEV void add_to_passive(Wv& w, uint32_t p) {             // hv:1423-1448
+    if (p == w.me || has(w.A, w.act_n, p) || has(w.P, w.pas_n, p)) return;
+    if (w.pas_n >= w.a->max_passive) {
+        uint32_t r = select_random(w, w.P, w.pas_n, w.me, w.me, w.me);
+        if (r != NONE) vdel_val(w.P, w.pas_n, r);
     }
-    view_add(L.pas, L.h.pas_n, p);
+    view_add(w.P, w.pas_n, p);
 }
 
-__device__ void drop_random_active(Lane& L) {           // hv:1467-1512
-    uint32_t p = select_random(L, L.act, L.h.act_n, L.me, L.me, L.me);
-    if (p == PSIM_NONE) return;
-    row_del(L.act, L.h.act_n, p);
-    add_to_passive(L, p);
-    uint32_t nid = next_id(L, p);
-    map_store(L, L.sentp, L.senti, L.h.sent_n, L.h.sent_head, p, nid);
-    hv_send(L, p, PSIM_MSG_DISCONNECT, 0, nid, nullptr, 0);
+DEV void drop_random_active(Wv& w) {                     // hv:1467-1512
+    uint32_t p = select_random(w, w.A, w.act_n, w.me, w.me, w.me);
+    if (p == NONE) return;
+    vdel_val(w.A, w.act_n, p);
+    add_to_passive(w, p);
+    uint32_t nid = next_id(w, p);
+    map_store(w, w.SP, w.SI, w.sent_n, w.sent_head, p, nid);
+    hv_send(w, p, PSIM_MSG_DISCONNECT, 0, nid, 0, 0, 0);
 }
 
-__device__ void add_to_active(Lane& L, uint32_t p) {    // hv:1371-1420
-    if (p == L.me || find(L.act, L.h.act_n, p) >= 0) return;
-    row_del(L.pas, L.h.pas_n, p);
-    if (L.h.act_n >= L.a->max_active) drop_random_active(L);
-    view_add(L.act, L.h.act_n, p);
+DEV void add_to_active(Wv& w, uint32_t p) {              // hv:1371-1420
+    if (p == w.me || has(w.A, w.act_n, p)) return;
+    vdel_val(w.P, w.pas_n, p);
+    if (w.act_n >= w.a->max_active) drop_random_active(w);
+    view_add(w.A, w.act_n, p);
 }
 
 // usort([Myself] ++ sublist(Active, k_active) ++ sublist(Passive, k_passive))
-__device__ uint32_t build_exchange(Lane& L, uint32_t* ex) {
-    ex[0] = L.me;
-    uint32_t n = 1;
-    n = sublist(L, L.act, L.h.act_n, L.a->k_active, ex, n);
-    n = sublist(L, L.pas, L.h.pas_n, L.a->k_passive, ex, n);
-    return usort_small(ex, n);
+DEV uint32_t build_exchange(Wv& w, uint32_t& EX) {
+    EX = lane_id() == 0 ? w.me : 0u;
+    uint32_t m = 1;
+    m = sublist(w, w.A, w.act_n, w.a->k_active, EX, m);
+    m = sublist(w, w.P, w.pas_n, w.a->k_passive, EX, m);
+    return usort_lanes(w, EX, m);
 }
 
-// merge_exchange/2 (hv:1590-1595): usort(Exchange -- [Me | Active]) folded
-// through add_to_passive_view in ascending id order.
-__device__ void merge_exchange(Lane& L, const uint32_t* ex, uint32_t nex) {
-    uint32_t prev = 0;
-    bool first = true;
-    for (;;) {
-        uint32_t best = 0xFFFFFFFFu;
-        bool found = false;
-        for (uint32_t i = 0; i < nex; i++) {
-            uint32_t e = ex[i];
-            if (e == L.me || (!first && e <= prev)) continue;
-            if (find(L.act, L.h.act_n, e) >= 0) continue;
-            if (!found || e < best) { best = e; found = true; }
-        }
-        if (!found) break;
-        add_to_passive(L, best);
-        prev = best;
-        first = false;
-    }
+// merge_exchange/2 (hv:1590-1595)
+DEV void merge_exchange(Wv& w, uint32_t EX, uint32_t nex) {
+    uint32_t l = lane_id();
+    bool in_act = false;
+    for (uint32_t j = 0; j < w.act_n; j++) in_act |= (EX == rl(w.A, j));
+    uint32_t cand = (l < nex && EX != w.me && !in_act) ? EX : 0xFFFFFFFFu;
+    uint32_t T = cand;
+    uint32_t mt = usort_lanes(w, T, 32);
+    // drop the 0xFFFFFFFF filler that sorts last
+    if (mt && rl(T, mt - 1) == 0xFFFFFFFFu) mt--;
+    for (uint32_t i = 0; i < mt; i++) add_to_passive(w, rl(T, i));
 }
 
-__device__ void move_to_active(Lane& L, uint32_t p) {   // hv:1679-1709
-    if (p == PSIM_NONE) return;
-    uint32_t ex[1 + 2 * PSIM_EXCHANGE_CAP];
-    uint32_t nex = build_exchange(L, ex);
-    hv_send(L, p, PSIM_MSG_NEIGHBOR_REQUEST, 0, current_id(L, p), ex, nex);
+DEV void move_to_active(Wv& w, uint32_t p) {             // hv:1679-1709
+    if (p == NONE) return;
+    uint32_t EX;
+    uint32_t nex = build_exchange(w, EX);
+    hv_send(w, p, PSIM_MSG_NEIGHBOR_REQUEST, 0, current_id(w, p), 0, EX, nex);
 }
 
 // ------------------------------------------------------------ plumtree --
-// notify/1 -> plumtree update/1: handle_cast({update, Members}) (pt:314-336)
-__device__ void notify(Lane& L) {
-    if (!L.a->plumtree) return;
-    uint32_t cur[PSIM_ACTIVE_CAP];
-    uint32_t nc = L.h.act_n;
-    for (uint32_t i = 0; i < nc; i++) cur[i] = L.act[i];
-    nc = usort_small(cur, nc);
-    bool any_new = false;
-    for (uint32_t i = 0; i < nc; i++)
-        if (find(L.all, L.h.all_n, cur[i]) < 0) any_new = true;
-    // Removed = all_members -- Current (computed before any reset)
-    uint32_t rem[PSIM_PT_MEMBERS_CAP];
-    uint32_t nr = 0;
-    for (uint32_t i = 0; i < L.h.all_n; i++) {
-        uint32_t e = L.all[i];
-        bool in = false;
-        for (uint32_t j = 0; j < nc; j++) in |= (cur[j] == e);
-        if (!in) rem[nr++] = e;
-    }
-    if (any_new) {
-        // common_eagers := (common_eagers U New); per-root sets wiped; all := Current
-        for (uint32_t i = 0; i < nc; i++)
-            if (find(L.all, L.h.all_n, cur[i]) < 0) {
-                // insert into the sorted common row (room: |common| <= |all| <= 8 before removals)
-                uint32_t e = cur[i];
-                if (find(L.com, L.h.com_n, e) >= 0) continue;
-                if (L.h.com_n >= PSIM_PT_MEMBERS_CAP) {
-                    // drop a member that is about to be removed to make room
-                    bool made = false;
-                    for (uint32_t r = 0; r < nr && !made; r++) made = row_del(L.com, L.h.com_n, rem[r]);
-                    if (!made) { st_add(L, ST_OVF, 1); continue; }
-                }
-                ord_add(L, L.com, L.h.com_n, PSIM_PT_MEMBERS_CAP, e);
+DEV void load_pt(Wv& w) {
+    if (w.pt) return;
+    uint32_t l = lane_id();
+    size_t n = w.me;
+    w.ALL = l < PSIM_PT_MEMBERS_CAP ? w.a->pt_all[n * PSIM_PT_MEMBERS_CAP + l] : 0u;
+    w.COM = l < PSIM_PT_MEMBERS_CAP ? w.a->pt_com[n * PSIM_PT_MEMBERS_CAP + l] : 0u;
+    w.EAG = l < PSIM_PT_SET_CAP ? w.a->pt_eag[n * PSIM_PT_SET_CAP + l] : 0u;
+    w.LAZ = l < PSIM_PT_SET_CAP ? w.a->pt_laz[n * PSIM_PT_SET_CAP + l] : 0u;
+    w.OUT = l < PSIM_PT_OUT_CAP ? w.a->pt_out[n * PSIM_PT_OUT_CAP + l] : 0ull;
+    w.pt = true;
+}
+
+DEV void ord_add(Wv& w, uint32_t& V, uint32_t& n, uint32_t cap, uint32_t e) {
+    uint32_t l = lane_id();
+    if (ballot(l < n && V == e)) return;
+    if (n >= cap) { st_add(w, ST_OVF, 1); return; }
+    vins(V, n, popc(ballot(l < n && V < e)), e);
+}
+
+// notify/1 (hv:1598-1599) -> plumtree update/1 -> handle_cast({update, ..})
+// (pt:314-336), reset_peers/4 (:652-659), neighbors_down/2 (:404-423)
+DEV void notify(Wv& w) {
+    if (!w.a->plumtree) return;
+    load_pt(w);
+    uint32_t l = lane_id();
+    uint32_t CUR = w.A;
+    uint32_t nc = usort_lanes(w, CUR, w.act_n);
+    bool in_all = false;
+    for (uint32_t j = 0; j < w.all_n; j++) in_all |= (CUR == rl(w.ALL, j));
+    uint64_t newm = ballot(l < nc && !in_all);
+    bool in_cur = false;
+    for (uint32_t j = 0; j < nc; j++) in_cur |= (w.ALL == rl(CUR, j));
+    uint64_t remm = ballot(l < w.all_n && !in_cur);
+    uint32_t REM = compact(w, w.ALL, remm);
+    uint32_t nr = popc(remm);
+    if (newm) {
+        for (uint64_t m = newm; m; m &= m - 1) {
+            uint32_t e = rl(CUR, ffs64(m));
+            if (has(w.COM, w.com_n, e)) continue;
+            if (w.com_n >= PSIM_PT_MEMBERS_CAP) {
+                bool made = false;
+                for (uint32_t r = 0; r < nr && !made; r++) made = vdel_val(w.COM, w.com_n, rl(REM, r));
+                if (!made) { st_add(w, ST_OVF, 1); continue; }
             }
-        L.h.pt_root = PSIM_NONE;
-        for (uint32_t i = 0; i < L.h.eag_n; i++) L.eag[i] = 0;
-        for (uint32_t i = 0; i < L.h.laz_n; i++) L.laz[i] = 0;
-        L.h.eag_n = L.h.laz_n = 0;
-        for (uint32_t i = 0; i < PSIM_PT_MEMBERS_CAP; i++) L.all[i] = i < nc ? cur[i] : 0u;
-        L.h.all_n = (uint8_t)nc;
+            ord_add(w, w.COM, w.com_n, PSIM_PT_MEMBERS_CAP, e);
+        }
+        w.h.pt_root = NONE;
+        w.EAG = 0; w.LAZ = 0; w.eag_n = w.laz_n = 0;
+        w.ALL = CUR; w.all_n = nc;
     }
-    // neighbors_down(Removed, ..) (pt:404-423)
     for (uint32_t r = 0; r < nr; r++) {
-        uint32_t e = rem[r];
-        row_del(L.com, L.h.com_n, e);
-        if (L.h.pt_root != PSIM_NONE) {
-            row_del(L.eag, L.h.eag_n, e);
-            row_del(L.laz, L.h.laz_n, e);
+        uint32_t e = rl(REM, r);
+        vdel_val(w.COM, w.com_n, e);
+        if (w.h.pt_root != NONE) {
+            vdel_val(w.EAG, w.eag_n, e);
+            vdel_val(w.LAZ, w.laz_n, e);
         }
-        uint32_t j = 0;
-        for (uint32_t k = 0; k < L.h.out_n; k++) {
-            uint64_t o = L.out[k];
-            if ((uint32_t)(o >> 32) != e) L.out[j++] = o;
+        uint64_t keep = ballot(l < w.out_n && (uint32_t)(w.OUT >> 32) != e);
+        if (popc(keep) != w.out_n) {
+            w.OUT = compact64(w, w.OUT, keep);
+            w.out_n = popc(keep);
         }
-        for (uint32_t k = j; k < L.h.out_n; k++) L.out[k] = 0;
-        L.h.out_n = (uint8_t)j;
     }
 }
 
-// the eager/lazy rows of Root: the per-root slot or the common default
-__device__ __forceinline__ bool root_slot(const Lane& L, uint32_t root) {
-    return L.h.pt_root != PSIM_NONE && L.h.pt_root == root;
-}
-
-// update_peers/5 (pt:599-609) for a single root slot
-__device__ void pt_update(Lane& L, uint32_t from, uint32_t root, bool to_eager) {
-    if (L.h.pt_root != PSIM_NONE && L.h.pt_root != root) { st_add(L, ST_OVF, 1); return; }
-    if (L.h.pt_root == PSIM_NONE) {
-        // first touch: the slot starts as (common_eagers, common_lazys = [])
-        for (uint32_t i = 0; i < L.h.com_n; i++) L.eag[i] = L.com[i];
-        L.h.eag_n = L.h.com_n;
-        L.h.laz_n = 0;
-        L.h.pt_root = root;
+// update_peers/5 + set_peers/4 (pt:593-609) for the single root slot
+DEV void pt_update(Wv& w, uint32_t from, uint32_t root, bool to_eager) {
+    if (w.h.pt_root != NONE && w.h.pt_root != root) { st_add(w, ST_OVF, 1); return; }
+    if (w.h.pt_root == NONE) {            // first touch: (common_eagers, [])
+        w.EAG = lane_id() < PSIM_PT_MEMBERS_CAP ? w.COM : 0u;
+        w.eag_n = w.com_n;
+        w.LAZ = 0; w.laz_n = 0;
+        w.h.pt_root = root;
     }
     if (to_eager) {
-        ord_add(L, L.eag, L.h.eag_n, PSIM_PT_SET_CAP, from);
-        row_del(L.laz, L.h.laz_n, from);
+        ord_add(w, w.EAG, w.eag_n, PSIM_PT_SET_CAP, from);
+        vdel_val(w.LAZ, w.laz_n, from);
     } else {
-        row_del(L.eag, L.h.eag_n, from);
-        ord_add(L, L.laz, L.h.laz_n, PSIM_PT_SET_CAP, from);
+        vdel_val(w.EAG, w.eag_n, from);
+        ord_add(w, w.LAZ, w.laz_n, PSIM_PT_SET_CAP, from);
     }
 }
 
 // send/3 (pt:633-638): only over an existing connection of the manager
-__device__ void pt_send(Lane& L, uint32_t ident, uint32_t type, uint32_t msg, uint32_t rnd,
-                        uint32_t root) {
+DEV void pt_send(Wv& w, uint32_t ident, uint32_t type, uint32_t msg, uint32_t rnd, uint32_t root) {
     uint32_t id = ident & ~PSIM_MAP_BIT;
-    if (id == L.me || find(L.act, L.h.act_n, id) < 0 || !(L.a->flags[id] & F_UP) ||
-        L.a->part[id] != L.mypart) {
-        st_add(L, ST_FAIL, 1);
+    if (id == w.me || !has(w.A, w.act_n, id) || !(w.a->flags[id] & F_UP) ||
+        w.a->part[id] != w.mypart) {
+        st_add(w, ST_FAIL, 1);
         return;
     }
-    emit(L, id, type, 0, msg, rnd, root, nullptr, 0);
+    emit(w, id, type, 0, msg, rnd, root, 0, 0);
 }
 
-__device__ void pt_add_out(Lane& L, uint32_t peer, uint32_t msg, uint32_t rnd) {  // pt:574-579
+DEV void pt_add_out(Wv& w, uint32_t peer, uint32_t msg, uint32_t rnd) {   // pt:574-579
+    uint32_t l = lane_id();
     uint64_t key = ((uint64_t)peer << 32) | (msg << 16) | (rnd & 0xFFFFu);
-    uint32_t i = L.h.out_n;
-    while (i > 0 && L.out[i - 1] > key) i--;
-    if (i > 0 && L.out[i - 1] == key) return;
-    if (L.h.out_n >= PSIM_PT_OUT_CAP) { st_add(L, ST_OVF, 1); return; }
-    for (uint32_t j = L.h.out_n; j > i; j--) L.out[j] = L.out[j - 1];
-    L.out[i] = key;
-    L.h.out_n++;
+    if (ballot(l < w.out_n && w.OUT == key)) return;
+    if (w.out_n >= PSIM_PT_OUT_CAP) { st_add(w, ST_OVF, 1); return; }
+    vins64(w.OUT, w.out_n, popc(ballot(l < w.out_n && w.OUT < key)), key);
 }
 
-__device__ void pt_ack_out(Lane& L, uint32_t peer, uint32_t msg, uint32_t rnd) {  // pt:562-567
+DEV void pt_ack_out(Wv& w, uint32_t peer, uint32_t msg, uint32_t rnd) {   // pt:562-567
     uint64_t key = ((uint64_t)peer << 32) | (msg << 16) | (rnd & 0xFFFFu);
-    for (uint32_t i = 0; i < L.h.out_n; i++)
-        if (L.out[i] == key) {
-            for (uint32_t j = i; j + 1 < L.h.out_n; j++) L.out[j] = L.out[j + 1];
-            L.h.out_n--;
-            L.out[L.h.out_n] = 0;
-            return;
-        }
+    int k = ffs64(ballot(lane_id() < w.out_n && w.OUT == key));
+    if (k >= 0) vdel64(w.OUT, w.out_n, (uint32_t)k);
 }
 
 // eager_push/7 + schedule_lazy_push/6 (pt:428-441)
-__device__ void pt_push(Lane& L, uint32_t msg, uint32_t rnd, uint32_t root, uint32_t from) {
-    if (root_slot(L, root)) {
-        for (uint32_t i = 0; i < L.h.eag_n; i++)
-            if (L.eag[i] != from) pt_send(L, L.eag[i], PSIM_MSG_PT_BROADCAST, msg, rnd, root);
-        for (uint32_t i = 0; i < L.h.laz_n; i++)
-            if (L.laz[i] != from) pt_add_out(L, L.laz[i], msg, rnd);
+DEV void pt_push(Wv& w, uint32_t msg, uint32_t rnd, uint32_t root, uint32_t from) {
+    if (w.h.pt_root != NONE && w.h.pt_root == root) {
+        for (uint32_t i = 0; i < w.eag_n; i++) {
+            uint32_t e = rl(w.EAG, i);
+            if (e != from) pt_send(w, e, PSIM_MSG_PT_BROADCAST, msg, rnd, root);
+        }
+        for (uint32_t i = 0; i < w.laz_n; i++) {
+            uint32_t e = rl(w.LAZ, i);
+            if (e != from) pt_add_out(w, e, msg, rnd);
+        }
     } else {
-        for (uint32_t i = 0; i < L.h.com_n; i++)
-            if (L.com[i] != from) pt_send(L, L.com[i], PSIM_MSG_PT_BROADCAST, msg, rnd, root);
+        for (uint32_t i = 0; i < w.com_n; i++) {
+            uint32_t e = rl(w.COM, i);
+            if (e != from) pt_send(w, e, PSIM_MSG_PT_BROADCAST, msg, rnd, root);
+        }
     }
 }
 
-__device__ __forceinline__ bool pt_have(const Lane& L, uint32_t msg) {
-    return (L.h.have >> (msg & 31u)) & 1u;
-}
+DEV bool pt_have(const Wv& w, uint32_t msg) { return (w.h.have >> (msg & 31u)) & 1u; }
 
-__device__ void pt_handle(Lane& L, const Msg& m, uint32_t type) {
-    uint32_t from = m.src | PSIM_MAP_BIT, msg = m.a0, rnd = m.a1, root = m.a2;
+DEV void pt_handle(Wv& w, uint32_t type, uint32_t src, uint32_t msg, uint32_t rnd, uint32_t root) {
+    uint32_t from = src | PSIM_MAP_BIT;
+    load_pt(w);
     switch (type) {
     case PSIM_MSG_PT_BROADCAST:                        // pt:288-293, :368-378
-        if (!pt_have(L, msg)) {                        // backend merge/2
-            L.h.have |= 1u << (msg & 31u);
-            st_add(L, ST_FIRST, 1);
-            if (msg == L.a->tracked_msg) { L.h.trk_round = L.a->round; L.h.trk_hop = rnd + 1; }
-            pt_update(L, from, root, true);
-            pt_push(L, msg, rnd + 1, root, from);
+        if (!pt_have(w, msg)) {                        // plumtree_backend merge/2
+            w.h.have |= 1u << (msg & 31u);
+            st_add(w, ST_FIRST, 1);
+            if (msg == w.a->tracked_msg) { w.h.trk_round = w.round; w.h.trk_hop = rnd + 1; }
+            pt_update(w, from, root, true);
+            pt_push(w, msg, rnd + 1, root, from);
         } else {
-            pt_update(L, from, root, false);
-            pt_send(L, from, PSIM_MSG_PT_PRUNE, 0, 0, root);
+            pt_update(w, from, root, false);
+            pt_send(w, from, PSIM_MSG_PT_PRUNE, 0, 0, root);
         }
         break;
     case PSIM_MSG_PT_PRUNE:                            // pt:294-298
-        pt_update(L, from, root, false);
+        pt_update(w, from, root, false);
         break;
     case PSIM_MSG_PT_IHAVE:                            // pt:299-303, :380-386
-        if (pt_have(L, msg)) {
-            pt_send(L, from, PSIM_MSG_PT_IGNORED_IHAVE, msg, rnd, root);
+        if (pt_have(w, msg)) {
+            pt_send(w, from, PSIM_MSG_PT_IGNORED_IHAVE, msg, rnd, root);
         } else {
-            pt_send(L, from, PSIM_MSG_PT_GRAFT, msg, rnd, root);
-            pt_update(L, from, root, true);
+            pt_send(w, from, PSIM_MSG_PT_GRAFT, msg, rnd, root);
+            pt_update(w, from, root, true);
         }
         break;
     case PSIM_MSG_PT_IGNORED_IHAVE:                    // pt:304-307
-        pt_ack_out(L, from, msg, rnd);
+        pt_ack_out(w, from, msg, rnd);
         break;
     case PSIM_MSG_PT_GRAFT:                            // pt:308-313, :388-402
-        if (pt_have(L, msg)) {
-            pt_update(L, from, root, true);
-            pt_send(L, from, PSIM_MSG_PT_BROADCAST, msg, rnd, root);
+        if (pt_have(w, msg)) {
+            pt_update(w, from, root, true);
+            pt_send(w, from, PSIM_MSG_PT_BROADCAST, msg, rnd, root);
         }
         break;
     default:
@@ -476,265 +536,281 @@ __device__ void pt_handle(Lane& L, const Msg& m, uint32_t type) {
 }
 
 // ----------------------------------------------------------- hyparview --
-__device__ void hv_handle(Lane& L, const Msg& m, uint32_t type) {
-    const RoundArgs& a = *L.a;
-    uint32_t me = L.me, p = m.src;
+DEV void hv_handle(Wv& w, uint32_t type, uint32_t p, uint32_t ttl, uint32_t a0, uint32_t a1,
+                   uint32_t EX, uint32_t nex) {
+    const RoundArgs& a = *w.a;
+    uint32_t me = w.me;
     switch (type) {
-    case PSIM_MSG_JOIN: {                              // hv:703-771
-        uint32_t pe = m.a0;
-        if (addable_epoch(L, pe, p) && find(L.act, L.h.act_n, p) < 0 && connect_ok(L, p)) {
-            add_to_active(L, p);
-            hv_send(L, p, PSIM_MSG_NEIGHBOR, 0, current_id(L, p), nullptr, 0);
-            // (members(Active) -- [Myself]) -- [Peer], in to_list order; the
-            // sends never change the active view, so iterate it in place
-            for (uint32_t i = 0; i < L.h.act_n; i++) {
-                uint32_t q = L.act[i];
-                if (q != me && q != p) {
-                    if (!connect_ok(L, q)) { st_add(L, ST_FAIL, 1); continue; }
-                    L.h.rng++;
-                    emit(L, q, PSIM_MSG_FORWARD_JOIN, a.arwl, p, pe, 0, nullptr, 0);
-                }
+    case PSIM_MSG_JOIN:                                // hv:703-771
+        if (addable_epoch(w, a0, p) && !has(w.A, w.act_n, p) && connect_ok(w, p)) {
+            add_to_active(w, p);
+            hv_send(w, p, PSIM_MSG_NEIGHBOR, 0, current_id(w, p), 0, 0, 0);
+            // (members(Active) -- [Myself]) -- [Peer], in to_list order
+            for (uint32_t i = 0; i < w.act_n; i++) {
+                uint32_t q = rl(w.A, i);
+                if (q != me && q != p) hv_send(w, q, PSIM_MSG_FORWARD_JOIN, a.arwl, p, a0, 0, 0);
             }
-            notify(L);
+            notify(w);
         }
         break;
-    }
     case PSIM_MSG_NEIGHBOR:                            // hv:774-805
-        if (addable_id(L, m.a0, p) && connect_ok(L, p)) add_to_active(L, p);
-        notify(L);
+        if (addable_id(w, a0, p) && connect_ok(w, p)) add_to_active(w, p);
+        notify(w);
         break;
     case PSIM_MSG_FORWARD_JOIN: {                      // hv:808-923
-        uint32_t q = m.a0, pe = m.a1, ttl = (m.tt >> 8) & 0xFF, sender = p;
-        if (ttl == 0 || L.h.act_n == 1) {
-            if (addable_epoch(L, pe, q) && find(L.act, L.h.act_n, q) < 0 && connect_ok(L, q)) {
-                add_to_active(L, q);
-                hv_send(L, q, PSIM_MSG_NEIGHBOR, 0, current_id(L, q), nullptr, 0);
+        uint32_t q = a0, pe = a1, sender = p;
+        if (ttl == 0 || w.act_n == 1) {
+            if (addable_epoch(w, pe, q) && !has(w.A, w.act_n, q) && connect_ok(w, q)) {
+                add_to_active(w, q);
+                hv_send(w, q, PSIM_MSG_NEIGHBOR, 0, current_id(w, q), 0, 0, 0);
             }
         } else {
             // the passive add at TTL == prwl never changes the active view,
-            // so Active0 is the live row for the select and the membership test
-            if (ttl == a.prwl) add_to_passive(L, q);
-            uint32_t r = select_random(L, L.act, L.h.act_n, sender, me, q);
-            if (r == PSIM_NONE) {
-                if (addable_epoch(L, pe, q) && find(L.act, L.h.act_n, q) < 0 && connect_ok(L, q)) {
-                    add_to_active(L, q);
-                    hv_send(L, q, PSIM_MSG_NEIGHBOR, 0, current_id(L, q), nullptr, 0);
+            // so the live active row is Active0 for the select and the test
+            if (ttl == a.prwl) add_to_passive(w, q);
+            uint32_t r = select_random(w, w.A, w.act_n, sender, me, q);
+            if (r == NONE) {
+                if (addable_epoch(w, pe, q) && !has(w.A, w.act_n, q) && connect_ok(w, q)) {
+                    add_to_active(w, q);
+                    hv_send(w, q, PSIM_MSG_NEIGHBOR, 0, current_id(w, q), 0, 0, 0);
                 }
-            } else if (connect_ok(L, r)) {
-                L.h.rng++;
-                emit(L, r, PSIM_MSG_FORWARD_JOIN, ttl - 1, q, pe, 0, nullptr, 0);
             } else {
-                st_add(L, ST_FAIL, 1);
+                hv_send(w, r, PSIM_MSG_FORWARD_JOIN, ttl - 1, q, pe, 0, 0);
             }
         }
-        notify(L);
+        notify(w);
         break;
     }
     case PSIM_MSG_DISCONNECT: {                        // hv:926-972
-        uint32_t d = m.a0;
-        if (!valid_disconnect(L, p, d)) break;
-        row_del(L.act, L.h.act_n, p);
-        // select_random(Passive0, [Myself, Peer]) uses the passive view from
-        // before the add below: draw over it first, in its own order, by
-        // remembering whether the add evicts (the only change the add makes
-        // besides inserting p, which is omitted from the draw anyway).
-        uint32_t pas0[PSIM_PASSIVE_CAP];
-        uint32_t np0 = L.h.pas_n;
-        bool isolated;
-        for (uint32_t i = 0; i < np0; i++) pas0[i] = L.pas[i];
-        add_to_passive(L, p);
-        map_store(L, L.recvp, L.recvi, L.h.recv_n, L.h.recv_head, p, d);
-        isolated = (L.h.act_n == 1);
-        if (isolated) move_to_active(L, select_random(L, pas0, np0, me, p, me));
+        if (!valid_disconnect(w, p, a0)) break;
+        vdel_val(w.A, w.act_n, p);
+        uint32_t P0 = w.P, np0 = w.pas_n;              // Passive before the add
+        add_to_passive(w, p);
+        map_store(w, w.RP, w.RI, w.recv_n, w.recv_head, p, a0);
+        if (w.act_n == 1) move_to_active(w, select_random(w, P0, np0, me, p, me));
         break;
     }
     case PSIM_MSG_NEIGHBOR_REQUEST: {                  // hv:975-1053
-        uint32_t ack[1 + 2 * PSIM_EXCHANGE_CAP];
-        uint32_t nack = build_exchange(L, ack);
-        if (addable_id(L, m.a0, p)) {
-            if (connect_ok(L, p)) {
-                hv_send(L, p, PSIM_MSG_NEIGHBOR_ACCEPTED, 0, current_id(L, p), ack, nack);
-                add_to_active(L, p);
+        uint32_t ACK;
+        uint32_t nack = build_exchange(w, ACK);
+        if (addable_id(w, a0, p)) {                    // priority is always high (:1706)
+            if (connect_ok(w, p)) {
+                hv_send(w, p, PSIM_MSG_NEIGHBOR_ACCEPTED, 0, current_id(w, p), 0, ACK, nack);
+                add_to_active(w, p);
             }
         } else {
-            hv_send(L, p, PSIM_MSG_NEIGHBOR_REJECTED, 0, 0, ack, nack);
+            hv_send(w, p, PSIM_MSG_NEIGHBOR_REJECTED, 0, 0, 0, ACK, nack);
         }
-        merge_exchange(L, m.ex, (m.tt >> 16) & 0xFF);
-        notify(L);
+        merge_exchange(w, EX, nex);
+        notify(w);
         break;
     }
     case PSIM_MSG_NEIGHBOR_REJECTED:                   // hv:1056-1067
-        merge_exchange(L, m.ex, (m.tt >> 16) & 0xFF);
+        merge_exchange(w, EX, nex);
         break;
     case PSIM_MSG_NEIGHBOR_ACCEPTED:                   // hv:1070-1089
-        if (addable_id(L, m.a0, p)) add_to_active(L, p);
-        merge_exchange(L, m.ex, (m.tt >> 16) & 0xFF);
-        notify(L);
+        if (addable_id(w, a0, p)) add_to_active(w, p);
+        merge_exchange(w, EX, nex);
+        notify(w);
         break;
     case PSIM_MSG_SHUFFLE_REPLY:                       // hv:1091-1093
-        merge_exchange(L, m.ex, (m.tt >> 16) & 0xFF);
+        merge_exchange(w, EX, nex);
         break;
-    case PSIM_MSG_SHUFFLE: {                           // hv:1095-1136
-        uint32_t ttl = (m.tt >> 8) & 0xFF, nex = (m.tt >> 16) & 0xFF;
-        if (ttl > 0 && L.h.act_n > 1) {
-            uint32_t r = select_random(L, L.act, L.h.act_n, p, me, me);
-            if (r != PSIM_NONE) hv_send(L, r, PSIM_MSG_SHUFFLE, ttl - 1, 0, m.ex, nex);
+    case PSIM_MSG_SHUFFLE:                             // hv:1095-1136
+        if (ttl > 0 && w.act_n > 1) {
+            uint32_t r = select_random(w, w.A, w.act_n, p, me, me);
+            if (r != NONE) hv_send(w, r, PSIM_MSG_SHUFFLE, ttl - 1, 0, 0, EX, nex);
         } else {
-            uint32_t resp[PSIM_EXCHANGE_CAP];
-            uint32_t nr = sublist(L, L.pas, L.h.pas_n, nex, resp, 0);
-            hv_send(L, p, PSIM_MSG_SHUFFLE_REPLY, 0, 0, resp, nr);
-            merge_exchange(L, m.ex, nex);
+            uint32_t RESP = 0;
+            uint32_t nr = sublist(w, w.P, w.pas_n, nex, RESP, 0);
+            hv_send(w, p, PSIM_MSG_SHUFFLE_REPLY, 0, 0, 0, RESP, nr);
+            merge_exchange(w, EX, nex);
         }
         break;
-    }
     default:
         break;
     }
 }
 
-__device__ __forceinline__ bool timer_due(uint32_t period, uint32_t r, uint32_t start) {
+DEV bool timer_due(uint32_t period, uint32_t r, uint32_t start) {
     return period > 0 && r > start && ((r - start) % period) == 0;
 }
 
-__device__ __forceinline__ void load_msg(const Msg* __restrict__ rec, uint32_t slot, Msg& m) {
-    const uint4* q = reinterpret_cast<const uint4*>(&rec[slot]);
-    uint4* d = reinterpret_cast<uint4*>(&m);
-    d[0] = q[0]; d[1] = q[1]; d[2] = q[2]; d[3] = q[3];
+// read inbox message i: lanes 0..15 load the 64-B record
+DEV uint32_t load_rec(const RoundArgs& a, uint32_t ib, uint32_t i) {
+    uint32_t slot = a.in_slot[ib + i];
+    uint32_t l = lane_id();
+    return l < 16 ? reinterpret_cast<const uint32_t*>(a.rec_in + slot)[l] : 0u;
+}
+
+DEV void process(Wv& w, uint32_t n, uint32_t fl, uint32_t ib, uint32_t ik) {
+    const RoundArgs& a = *w.a;
+    const uint32_t r = a.round;
+    uint32_t l = lane_id();
+    st_add(w, ST_UP, 1);
+    w.h = a.hdr[n];
+    if (w.h.start_round == r && ik) {           // fresh incarnation: no connections yet
+        st_add(w, ST_DROPPED, ik);
+        ik = 0;
+    }
+    bool promo = a.random_promotion && timer_due(a.promotion_period, r, w.h.start_round);
+    bool shuf = timer_due(a.shuffle_period, r, w.h.start_round);
+    bool origin = a.origin_now && a.origin_node == n && a.plumtree;
+    bool lazy_due = a.plumtree && timer_due(a.lazy_tick_period, r, w.h.start_round);
+    bool lazy = lazy_due && w.h.out_n > 0;
+    bool joining = w.h.start_round == r && w.h.join_contact != NONE;
+    w.act_n = w.h.act_n;
+    w.A = l < PSIM_ACTIVE_CAP ? a.act[(size_t)n * PSIM_ACTIVE_CAP + l] : 0u;
+    uint64_t exits = 0;
+    if (a.crash_round) {
+        bool dead = l < w.act_n && w.A != n && (a.flags[w.A] & F_CRASHED);
+        exits = ballot(dead);
+    }
+    if (!(ik || joining || exits || promo || shuf || origin || lazy)) return;
+    st_add(w, ST_PROC, 1);
+
+    w.me = n;
+    w.mypart = a.part[n];
+    w.pas_n = w.h.pas_n; w.sent_n = w.h.sent_n; w.sent_head = w.h.sent_head;
+    w.recv_n = w.h.recv_n; w.recv_head = w.h.recv_head;
+    w.all_n = w.h.all_n; w.com_n = w.h.com_n; w.eag_n = w.h.eag_n; w.laz_n = w.h.laz_n;
+    w.out_n = w.h.out_n;
+    w.P = l < PSIM_PASSIVE_CAP ? a.pas[(size_t)n * PSIM_PASSIVE_CAP + l] : 0u;
+    w.maps = false; w.pt = false;
+    w.SP = w.SI = w.RP = w.RI = 0;
+    w.ALL = w.COM = w.EAG = w.LAZ = 0; w.OUT = 0;
+    w.obase = a.obase[n];
+    w.seq = 0;
+    w.digest = 0;
+
+    if (joining)                                      // hv:500-515
+        hv_send(w, w.h.join_contact, PSIM_MSG_JOIN, 0, w.h.epoch, 0, 0, 0);
+
+    if (exits) {                                      // hv:609-654
+        uint32_t D = compact(w, w.A, exits);
+        uint32_t nd = popc(exits);
+        for (uint32_t i = 0; i < nd; i++) {
+            uint32_t d = rl(D, i);
+            st_add(w, ST_EXITS, 1);
+            vdel_val(w.P, w.pas_n, d);
+            if (vdel_val(w.A, w.act_n, d))
+                move_to_active(w, select_random(w, w.P, w.pas_n, n, n, n));
+        }
+    }
+
+    for (uint32_t i = 0; i < ik; i++) {               // HyParView inbox, canonical order
+        uint32_t R = load_rec(a, ib, i);
+        uint32_t tt = rl(R, 2), type = tt & 0xFF;
+        if (type >= PSIM_MSG_PT_BROADCAST) continue;
+        st_add(w, ST_DELIV + type, 1);
+        uint32_t nex = (tt >> 16) & 0xFF;
+        uint32_t ex = shfl(R, (int)((l + 8) & 63));
+        ex = l < nex ? ex : 0u;
+        hv_handle(w, type, rl(R, 1), (tt >> 8) & 0xFF, rl(R, 4), rl(R, 5), ex, nex);
+    }
+
+    if (promo && w.act_n < a.min_active)              // hv:542-561
+        move_to_active(w, select_random(w, w.P, w.pas_n, n, n, n));
+    if (shuf) {                                       // hv:572-607
+        uint32_t EX;
+        uint32_t nex = build_exchange(w, EX);
+        uint32_t t = select_random(w, w.A, w.act_n, n, n, n);
+        if (t != NONE) hv_send(w, t, PSIM_MSG_SHUFFLE, a.arwl, 0, 0, EX, nex);
+    }
+
+    if (a.plumtree) {
+        for (uint32_t i = 0; i < ik; i++) {           // Plumtree inbox
+            uint32_t R = load_rec(a, ib, i);
+            uint32_t type = rl(R, 2) & 0xFF;
+            if (type < PSIM_MSG_PT_BROADCAST || type > PSIM_MSG_PT_GRAFT) continue;
+            st_add(w, ST_DELIV + type, 1);
+            pt_handle(w, type, rl(R, 1), rl(R, 4), rl(R, 5), rl(R, 6));
+        }
+        if (origin) {                                 // pt:282-287, backend:179-200
+            load_pt(w);
+            uint32_t my = n | PSIM_MAP_BIT;
+            w.h.have |= 1u << (a.origin_msg & 31u);
+            w.h.trk_round = r;
+            w.h.trk_hop = 0;
+            pt_push(w, a.origin_msg, 0, my, my);
+        }
+        if (lazy_due && w.out_n > 0) {                // pt:341-345, :443-453
+            load_pt(w);
+            for (uint32_t i = 0; i < w.out_n; i++) {
+                uint64_t o = rl64(w.OUT, i);
+                pt_send(w, (uint32_t)(o >> 32), PSIM_MSG_PT_IHAVE, (uint32_t)(o >> 16) & 0xFFFFu,
+                        (uint32_t)o & 0xFFFFu, a.bcast_root);
+            }
+        }
+    }
+
+    // ---- write back
+    w.h.act_n = (uint8_t)w.act_n; w.h.pas_n = (uint8_t)w.pas_n;
+    w.h.sent_n = (uint8_t)w.sent_n; w.h.sent_head = (uint8_t)w.sent_head;
+    w.h.recv_n = (uint8_t)w.recv_n; w.h.recv_head = (uint8_t)w.recv_head;
+    w.h.all_n = (uint8_t)w.all_n; w.h.com_n = (uint8_t)w.com_n;
+    w.h.eag_n = (uint8_t)w.eag_n; w.h.laz_n = (uint8_t)w.laz_n; w.h.out_n = (uint8_t)w.out_n;
+    if (l < PSIM_ACTIVE_CAP) a.act[(size_t)n * PSIM_ACTIVE_CAP + l] = w.A;
+    if (l < PSIM_PASSIVE_CAP) a.pas[(size_t)n * PSIM_PASSIVE_CAP + l] = w.P;
+    if (w.maps && l < PSIM_IDMAP_CAP) {
+        size_t b = (size_t)n * PSIM_IDMAP_CAP + l;
+        a.sentp[b] = w.SP; a.senti[b] = w.SI; a.recvp[b] = w.RP; a.recvi[b] = w.RI;
+    }
+    if (w.pt) {
+        if (l < PSIM_PT_MEMBERS_CAP) {
+            a.pt_all[(size_t)n * PSIM_PT_MEMBERS_CAP + l] = w.ALL;
+            a.pt_com[(size_t)n * PSIM_PT_MEMBERS_CAP + l] = w.COM;
+        }
+        if (l < PSIM_PT_SET_CAP) {
+            a.pt_eag[(size_t)n * PSIM_PT_SET_CAP + l] = w.EAG;
+            a.pt_laz[(size_t)n * PSIM_PT_SET_CAP + l] = w.LAZ;
+        }
+        if (l < PSIM_PT_OUT_CAP) a.pt_out[(size_t)n * PSIM_PT_OUT_CAP + l] = w.OUT;
+    }
+    {
+        const uint32_t* hw = reinterpret_cast<const uint32_t*>(&w.h);
+        uint32_t v = 0;
+#pragma unroll
+        for (int k = 0; k < 16; k++) v = l == (uint32_t)k ? hw[k] : v;
+        if (l < 16) reinterpret_cast<uint32_t*>(a.hdr + n)[l] = v;
+    }
+    if (l == 0) {
+        a.ocnt[n] = w.seq;
+        // only this wave writes its node's flag byte; peers read F_UP/F_CRASHED
+        uint8_t nf = (uint8_t)((fl & ~F_LAZY) | (w.out_n ? F_LAZY : 0));
+        if (nf != fl) a.flags[n] = nf;
+    }
+    if (w.digest) st_add(w, ST_DIGEST, w.digest);
 }
 
 __global__ void __launch_bounds__(256) k_consume(RoundArgs args) {
     __shared__ uint64_t sst[NST];
+    __shared__ uint32_t scratch[WAVES_PER_BLOCK][64];
     for (int i = threadIdx.x; i < NST; i += blockDim.x) sst[i] = 0;
     __syncthreads();
 
-    const RoundArgs& a = args;
-    uint32_t n = blockIdx.x * blockDim.x + threadIdx.x;
-    if (n < a.n_nodes) do {
-        uint8_t fl = a.flags[n];
-        uint32_t ib = a.in_beg[n], ik = a.in_cnt[n];
+    const uint32_t wid = threadIdx.x >> 6;
+    const uint32_t gw = uni(blockIdx.x * WAVES_PER_BLOCK + wid);
+    const uint32_t nw = gridDim.x * WAVES_PER_BLOCK;
+    Wv w;
+    w.a = &args;
+    w.lds = scratch[wid];
+    w.st = sst;
+    w.round = args.round;
+    for (uint32_t n = gw; n < args.n_nodes; n += nw) {
+        uint32_t fl = args.flags[n];
+        uint32_t ik = args.in_cnt[n];
         if (!(fl & F_UP)) {
-            if (ik) atomicAdd((unsigned long long*)&sst[ST_DROPPED], (unsigned long long)ik);
-            break;
+            if (ik) st_add(w, ST_DROPPED, ik);
+            continue;
         }
-        atomicAdd((unsigned long long*)&sst[ST_UP], 1ull);
-        Lane L;
-        L.a = &args;
-        L.me = n;
-        L.mypart = a.part[n];
-        L.st = sst;
-        {
-            const uint4* q = reinterpret_cast<const uint4*>(&a.hdr[n]);
-            uint4* d = reinterpret_cast<uint4*>(&L.h);
-            d[0] = q[0]; d[1] = q[1]; d[2] = q[2]; d[3] = q[3];
-        }
-        const uint32_t r = a.round;
-        if (L.h.start_round == r && ik) {       // fresh incarnation: no connections yet
-            atomicAdd((unsigned long long*)&sst[ST_DROPPED], (unsigned long long)ik);
-            ik = 0;
-        }
-        L.act = a.act + (size_t)n * PSIM_ACTIVE_CAP;
-        bool promo = a.random_promotion && timer_due(a.promotion_period, r, L.h.start_round);
-        bool shuf = timer_due(a.shuffle_period, r, L.h.start_round);
-        bool origin = a.origin_now && a.origin_node == n && a.plumtree;
-        bool lazy_due = a.plumtree && timer_due(a.lazy_tick_period, r, L.h.start_round);
-        bool lazy = lazy_due && L.h.out_n > 0;
-        bool joining = L.h.start_round == r && L.h.join_contact != PSIM_NONE;
-        uint32_t exits[PSIM_ACTIVE_CAP];
-        uint32_t nexit = 0;
-        if (a.crash_round) {
-            for (uint32_t i = 0; i < L.h.act_n; i++) {
-                uint32_t d = L.act[i];
-                if (d != n && (a.flags[d] & F_CRASHED)) exits[nexit++] = d;
-            }
-        }
-        if (!(ik || joining || nexit || promo || shuf || origin || lazy)) break;
-        atomicAdd((unsigned long long*)&sst[ST_PROC], 1ull);
-
-        L.pas = a.pas + (size_t)n * PSIM_PASSIVE_CAP;
-        L.sentp = a.sentp + (size_t)n * PSIM_IDMAP_CAP;
-        L.senti = a.senti + (size_t)n * PSIM_IDMAP_CAP;
-        L.recvp = a.recvp + (size_t)n * PSIM_IDMAP_CAP;
-        L.recvi = a.recvi + (size_t)n * PSIM_IDMAP_CAP;
-        L.all = a.pt_all + (size_t)n * PSIM_PT_MEMBERS_CAP;
-        L.com = a.pt_com + (size_t)n * PSIM_PT_MEMBERS_CAP;
-        L.eag = a.pt_eag + (size_t)n * PSIM_PT_SET_CAP;
-        L.laz = a.pt_laz + (size_t)n * PSIM_PT_SET_CAP;
-        L.out = a.pt_out + (size_t)n * PSIM_PT_OUT_CAP;
-        L.ob = a.rec_out + a.obase[n];
-        L.okey = a.okey + a.obase[n];
-        L.seq = 0;
-
-        if (joining)                                    // hv:500-515
-            hv_send(L, L.h.join_contact, PSIM_MSG_JOIN, 0, L.h.epoch, nullptr, 0);
-
-        for (uint32_t i = 0; i < nexit; i++) {          // hv:609-654
-            uint32_t d = exits[i];
-            atomicAdd((unsigned long long*)&sst[ST_EXITS], 1ull);
-            row_del(L.pas, L.h.pas_n, d);
-            if (row_del(L.act, L.h.act_n, d))
-                move_to_active(L, select_random(L, L.pas, L.h.pas_n, n, n, n));
-        }
-
-        Msg m;
-        for (uint32_t i = 0; i < ik; i++) {             // HyParView inbox, canonical order
-            load_msg(a.rec_in, a.in_slot[ib + i], m);
-            uint32_t type = m.tt & 0xFF;
-            if (type < PSIM_MSG_PT_BROADCAST) {
-                atomicAdd((unsigned long long*)&sst[ST_DELIV + type], 1ull);
-                hv_handle(L, m, type);
-            }
-        }
-
-        if (promo && L.h.act_n < a.min_active) {        // hv:542-561
-            move_to_active(L, select_random(L, L.pas, L.h.pas_n, n, n, n));
-        }
-        if (shuf) {                                     // hv:572-607
-            uint32_t ex[1 + 2 * PSIM_EXCHANGE_CAP];
-            uint32_t nex = build_exchange(L, ex);
-            uint32_t t = select_random(L, L.act, L.h.act_n, n, n, n);
-            if (t != PSIM_NONE) hv_send(L, t, PSIM_MSG_SHUFFLE, a.arwl, 0, ex, nex);
-        }
-
-        if (a.plumtree) {
-            for (uint32_t i = 0; i < ik; i++) {         // Plumtree inbox
-                load_msg(a.rec_in, a.in_slot[ib + i], m);
-                uint32_t type = m.tt & 0xFF;
-                if (type >= PSIM_MSG_PT_BROADCAST && type <= PSIM_MSG_PT_GRAFT) {
-                    atomicAdd((unsigned long long*)&sst[ST_DELIV + type], 1ull);
-                    pt_handle(L, m, type);
-                }
-            }
-            if (origin) {                               // pt:282-287, backend:179-200
-                uint32_t my = n | PSIM_MAP_BIT;
-                L.h.have |= 1u << (a.origin_msg & 31u);
-                L.h.trk_round = r;
-                L.h.trk_hop = 0;
-                pt_push(L, a.origin_msg, 0, my, my);
-            }
-            if (lazy_due) {                             // pt:341-345, :443-453
-                for (uint32_t i = 0; i < L.h.out_n; i++) {
-                    uint64_t o = L.out[i];
-                    pt_send(L, (uint32_t)(o >> 32), PSIM_MSG_PT_IHAVE, (uint32_t)(o >> 16) & 0xFFFFu,
-                            (uint32_t)o & 0xFFFFu, a.bcast_root);
-                }
-            }
-        }
-
-        // write back the header and the outbox count
-        {
-            uint4* d = reinterpret_cast<uint4*>(&a.hdr[n]);
-            const uint4* q = reinterpret_cast<const uint4*>(&L.h);
-            d[0] = q[0]; d[1] = q[1]; d[2] = q[2]; d[3] = q[3];
-        }
-        a.ocnt[n] = L.seq;
-        // only this lane writes its own flag byte; peers read just F_UP/F_CRASHED
-        uint8_t nf = (fl & ~F_LAZY) | (L.h.out_n ? F_LAZY : 0);
-        if (nf != fl) a.flags[n] = nf;
-    } while (0);
+        w.me = n;
+        process(w, n, fl, args.in_beg[n], ik);
+    }
 
     __syncthreads();
     for (int i = threadIdx.x; i < NST; i += blockDim.x)
-        a.stat_part[(size_t)blockIdx.x * NST + i] = sst[i];
+        args.stat_part[(size_t)blockIdx.x * NST + i] = sst[i];
 }
 
 }  // namespace psim

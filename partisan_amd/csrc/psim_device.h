@@ -53,15 +53,18 @@ __host__ __device__ constexpr uint32_t max_emit(uint32_t type) {
          : type == PSIM_MSG_NEIGHBOR_REQUEST ? 2
          : type == PSIM_MSG_NEIGHBOR_ACCEPTED ? 1
          : type == PSIM_MSG_SHUFFLE ? 1
-         : type == PSIM_MSG_PT_BROADCAST ? PSIM_PT_SET_CAP
+         // eager push to eager-{From} (<= SET_CAP-1) plus IHAVEs, in this
+         // round's lazy tick, for outstanding entries added for lazy-{From}
+         : type == PSIM_MSG_PT_BROADCAST ? 2 * PSIM_PT_SET_CAP - 1
          : type == PSIM_MSG_PT_IHAVE ? 1
          : type == PSIM_MSG_PT_GRAFT ? 1
          : 0;
 }
 constexpr uint32_t BOUND_BASE = 3;                        // JOIN send, promotion, shuffle
 constexpr uint32_t BOUND_EXITS = PSIM_ACTIVE_CAP - 1;     // EXIT-driven NEIGHBOR_REQUESTs
-constexpr uint32_t BOUND_LAZY = PSIM_PT_OUT_CAP;          // IHAVEs of one lazy tick
-constexpr uint32_t BOUND_ORIGIN = PSIM_PT_SET_CAP;        // eager push of the root
+constexpr uint32_t BOUND_LAZY = PSIM_PT_OUT_CAP;          // IHAVEs of entries already outstanding
+static_assert(2 * PSIM_PT_SET_CAP - 1 < 32, "max_emit must fit the 5-bit key field");
+constexpr uint32_t BOUND_ORIGIN = 2 * PSIM_PT_SET_CAP;    // eager push + lazy adds of the root
 
 // stats slots in the per-block partial arrays
 enum {
