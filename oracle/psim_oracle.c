@@ -228,12 +228,16 @@ static uint64_t mix64(uint64_t z) {
     return z;
 }
 
+/* Digest of one message: the sum over the 16 words of its 64-B record
+ * image [dst, src, type|ttl<<8|nex<<16, seq, a0, a1, a2, 0, ex0..ex7] of
+ * mix64((word << 32 | index) ^ golden).  Position-sensitive, order-free
+ * across messages (the round digest is a sum), and lane-parallel on the GPU. */
 static uint64_t msg_hash(const omsg *m) {
-    uint64_t h = 0x9E3779B97F4A7C15ull ^ (((uint64_t)m->dst << 32) | m->src);
-    h = mix64(h ^ (((uint64_t)m->seq << 32) | (m->type << 16) | (m->ttl << 8) | m->nex));
-    h = mix64(h ^ (((uint64_t)m->a0 << 32) | m->a1));
-    h = mix64(h ^ m->a2);
-    for (uint32_t i = 0; i < m->nex; i++) h = mix64(h ^ (((uint64_t)m->ex[i] << 32) | i));
+    uint32_t w[16] = {m->dst, m->src, m->type | (m->ttl << 8) | (m->nex << 16), m->seq,
+                      m->a0, m->a1, m->a2, 0};
+    for (uint32_t i = 0; i < m->nex; i++) w[8 + i] = m->ex[i];
+    uint64_t h = 0;
+    for (uint64_t j = 0; j < 16; j++) h += mix64((((uint64_t)w[j]) << 32 | j) ^ 0x9E3779B97F4A7C15ull);
     return h;
 }
 
@@ -725,6 +729,8 @@ static void process_node(struct psim_handle *h, uint32_t n) {
      * previous one is lost */
     if (s->start_round == r && e > b) { h->st->dropped += e - b; e = b; }
     int promo = h->cfg.random_promotion && timer_due(h->cfg.promotion_period, r, s->start_round);
+    /* a due promotion timer is work only if it can act (hv:547-551) */
+    int promo_work = promo && s->act_n < h->cfg.min_active_size;
     int shuf = timer_due(h->cfg.shuffle_period, r, s->start_round);
     int origin = h->origin_now && h->origin_node == n && h->cfg.plumtree;
     int lazy_due = h->cfg.plumtree && timer_due(h->cfg.lazy_tick_period, r, s->start_round);
@@ -733,7 +739,7 @@ static void process_node(struct psim_handle *h, uint32_t n) {
     for (uint32_t i = 0; i < s->act_n; i++)
         if (s->act[i] != n && h->crashed_now[s->act[i]]) exits[nexit++] = s->act[i];
     int joining = (s->start_round == r && s->join_contact != PSIM_NONE);
-    if (!(e > b || joining || nexit || promo || shuf || origin || lazy)) return;
+    if (!(e > b || joining || nexit || promo_work || shuf || origin || lazy)) return;
     h->st->nodes_processed++;
 
     /* handle_cast({join, Peer}), hyparview:500-515 */

@@ -51,10 +51,19 @@ DEV uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 DEV bool has(uint32_t V, uint32_t n, uint32_t e) { return ballot(lane_id() < n && V == e) != 0; }
 DEV int idx_of(uint32_t V, uint32_t n, uint32_t e) { return ffs64(ballot(lane_id() < n && V == e)); }
 
+// whole-wave DPP shifts (gfx9 wave_shl:1 / wave_shr:1): lane l reads lane
+// l+1 / l-1 in one VALU op instead of an LDS permute
+DEV uint32_t from_next(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x130, 0xF, 0xF, true);
+}
+DEV uint32_t from_prev(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xF, 0xF, true);
+}
+
 // delete entry k (order preserving)
 DEV void vdel(uint32_t& V, uint32_t& n, uint32_t k) {
     uint32_t l = lane_id();
-    uint32_t nx = shfl(V, (int)((l + 1) & 63));
+    uint32_t nx = from_next(V);
     V = l < k ? V : (l + 1 < n ? nx : 0u);
     n--;
 }
@@ -67,7 +76,7 @@ DEV void vdel64(uint64_t& V, uint32_t& n, uint32_t k) {
 // insert e at position pos
 DEV void vins(uint32_t& V, uint32_t& n, uint32_t pos, uint32_t e) {
     uint32_t l = lane_id();
-    uint32_t pv = shfl(V, (int)((l + 63) & 63));
+    uint32_t pv = from_prev(V);
     V = l < pos ? V : (l == pos ? e : (l <= n ? pv : 0u));
     n++;
 }
@@ -117,15 +126,15 @@ struct Wv {
     uint32_t all_n, com_n, eag_n, laz_n, out_n;
     uint32_t A, P, SP, SI, RP, RI, ALL, COM, EAG, LAZ;
     uint64_t OUT;
-    bool maps, pt;
+    bool maps, pt, maps_dirty, pt_dirty;
     uint64_t obase;
     uint32_t seq;
-    uint64_t digest;
+    uint64_t digest;     // per-lane partial: lane j sums the hashes of record word j
+    uint32_t SC;         // per-lane stats counter: lane k counts stats slot k (< NST)
 };
 
-DEV void st_add(Wv& w, int k, uint64_t v) {
-    if (lane_id() == 0) atomicAdd((unsigned long long*)&w.st[k], (unsigned long long)v);
-}
+// stats: lane k of SC holds slot k's count for this wave; flushed once per wave
+DEV void st_add(Wv& w, int k, uint32_t v) { w.SC += lane_id() == (uint32_t)k ? v : 0u; }
 
 // compact the lanes of V selected by `keep` (uniform mask) to the front
 DEV uint32_t compact(Wv& w, uint32_t V, uint64_t keep) {
@@ -155,7 +164,22 @@ DEV uint32_t usort_lanes(Wv& w, uint32_t& E, uint32_t m) {
 }
 
 // ----------------------------------------------------------------- RNG --
-DEV uint64_t draw(Wv& w) { return draw58_at(w.h.rng++, w.me, w.a->seed); }
+// every single draw is wave-uniform: pin its inputs to scalar registers so
+// the Philox rounds run on the SALU
+DEV uint64_t draw(Wv& w) {
+    uint64_t c = w.h.rng++;
+    uint32_t o0, o1;
+    philox(uni((uint32_t)c), uni((uint32_t)(c >> 32)), uni(w.me), 0u, uni((uint32_t)w.a->seed),
+           uni((uint32_t)(w.a->seed >> 32)), o0, o1);
+    return ((((uint64_t)uni(o1)) << 32) | uni(o0)) >> 6;
+}
+
+// v mod n for n < 2^16 with 32-bit arithmetic: v = hi*2^32 + lo
+DEV uint32_t mod58(uint64_t v, uint32_t n) {
+    uint32_t hi = (uint32_t)(v >> 32), lo = (uint32_t)v;
+    uint32_t p32 = (uint32_t)(0x100000000ull % n);
+    return ((hi % n) * p32 + lo % n) % n;
+}
 
 // rand:uniform/1 with a 58-bit generator (OTP rand.erl ?uniform_range)
 DEV uint32_t uniform_n(Wv& w, uint32_t n) {
@@ -163,7 +187,7 @@ DEV uint32_t uniform_n(Wv& w, uint32_t n) {
     for (;;) {
         uint64_t v = draw(w);
         if (v < n) return (uint32_t)v + 1;
-        uint64_t i = v % n;
+        uint64_t i = mod58(v, n);
         if (v - i <= two58 - n) return (uint32_t)i + 1;
     }
 }
@@ -176,8 +200,8 @@ DEV uint32_t select_random(Wv& w, uint32_t V, uint32_t n, uint32_t o0, uint32_t 
     uint32_t cnt = popc(M);
     if (cnt == 0) return NONE;
     uint32_t k = uniform_n(w, cnt) - 1;
-    uint64_t sel = ballot(((M >> l) & 1ull) && popc(M & lt_mask()) == k);
-    return rl(V, ffs64(sel));
+    for (uint32_t j = 0; j < k; j++) M &= M - 1;   // k-th set bit, on the SALU
+    return rl(V, ffs64(M));
 }
 
 // lists:sublist(shuffle(to_list(View)), K) (hv:1359-1361, :1586-1587): one
@@ -219,15 +243,12 @@ DEV void emit(Wv& w, uint32_t dst, uint32_t type, uint32_t ttl, uint32_t a0, uin
     uint32_t exv = shfl(EX, (int)((l - 8) & 63));
     uint32_t word = l == 0 ? dst : l == 1 ? w.me : l == 2 ? tt : l == 3 ? s : l == 4 ? a0
                   : l == 5 ? a1 : l == 6 ? a2 : l == 7 ? 0u : (l - 8 < nex ? exv : 0u);
-    if (l < 16) reinterpret_cast<uint32_t*>(w.a->rec_out + slot)[l] = word;
+    if (l < 16) {
+        reinterpret_cast<uint32_t*>(w.a->rec_out + slot)[l] = word;
+        // digest: the oracle's msg_hash, one record word per lane
+        w.digest += mix64((((uint64_t)word) << 32 | l) ^ 0x9E3779B97F4A7C15ull);
+    }
     if (l == 0) w.a->okey[slot] = dst | (max_emit(type) << KEY_DST_BITS);
-    // digest (the oracle's msg_hash, folded identically)
-    uint64_t hh = 0x9E3779B97F4A7C15ull ^ (((uint64_t)dst << 32) | w.me);
-    hh = mix64(hh ^ (((uint64_t)s << 32) | (type << 16) | (ttl << 8) | nex));
-    hh = mix64(hh ^ (((uint64_t)a0 << 32) | a1));
-    hh = mix64(hh ^ a2);
-    for (uint32_t i = 0; i < nex; i++) hh = mix64(hh ^ (((uint64_t)rl(EX, i) << 32) | i));
-    w.digest += hh;
     st_add(w, ST_EMIT + type, 1);
 }
 
@@ -261,6 +282,7 @@ DEV void load_maps(Wv& w) {
 DEV void map_store(Wv& w, uint32_t& PV, uint32_t& IV, uint32_t& n, uint32_t& head, uint32_t p,
                    uint32_t v) {
     uint32_t l = lane_id();
+    w.maps_dirty = true;
     int i = idx_of(PV, n, p);
     if (i >= 0) { IV = l == (uint32_t)i ? v : IV; return; }
     if (n < PSIM_IDMAP_CAP) {
@@ -389,6 +411,7 @@ DEV void ord_add(Wv& w, uint32_t& V, uint32_t& n, uint32_t cap, uint32_t e) {
 DEV void notify(Wv& w) {
     if (!w.a->plumtree) return;
     load_pt(w);
+    w.pt_dirty = true;
     uint32_t l = lane_id();
     uint32_t CUR = w.A;
     uint32_t nc = usort_lanes(w, CUR, w.act_n);
@@ -432,6 +455,7 @@ DEV void notify(Wv& w) {
 
 // update_peers/5 + set_peers/4 (pt:593-609) for the single root slot
 DEV void pt_update(Wv& w, uint32_t from, uint32_t root, bool to_eager) {
+    w.pt_dirty = true;
     if (w.h.pt_root != NONE && w.h.pt_root != root) { st_add(w, ST_OVF, 1); return; }
     if (w.h.pt_root == NONE) {            // first touch: (common_eagers, [])
         w.EAG = lane_id() < PSIM_PT_MEMBERS_CAP ? w.COM : 0u;
@@ -462,6 +486,7 @@ DEV void pt_send(Wv& w, uint32_t ident, uint32_t type, uint32_t msg, uint32_t rn
 DEV void pt_add_out(Wv& w, uint32_t peer, uint32_t msg, uint32_t rnd) {   // pt:574-579
     uint32_t l = lane_id();
     uint64_t key = ((uint64_t)peer << 32) | (msg << 16) | (rnd & 0xFFFFu);
+    w.pt_dirty = true;
     if (ballot(l < w.out_n && w.OUT == key)) return;
     if (w.out_n >= PSIM_PT_OUT_CAP) { st_add(w, ST_OVF, 1); return; }
     vins64(w.OUT, w.out_n, popc(ballot(l < w.out_n && w.OUT < key)), key);
@@ -470,7 +495,7 @@ DEV void pt_add_out(Wv& w, uint32_t peer, uint32_t msg, uint32_t rnd) {   // pt:
 DEV void pt_ack_out(Wv& w, uint32_t peer, uint32_t msg, uint32_t rnd) {   // pt:562-567
     uint64_t key = ((uint64_t)peer << 32) | (msg << 16) | (rnd & 0xFFFFu);
     int k = ffs64(ballot(lane_id() < w.out_n && w.OUT == key));
-    if (k >= 0) vdel64(w.OUT, w.out_n, (uint32_t)k);
+    if (k >= 0) { vdel64(w.OUT, w.out_n, (uint32_t)k); w.pt_dirty = true; }
 }
 
 // eager_push/7 + schedule_lazy_push/6 (pt:428-441)
@@ -636,19 +661,31 @@ DEV bool timer_due(uint32_t period, uint32_t r, uint32_t start) {
     return period > 0 && r > start && ((r - start) % period) == 0;
 }
 
-// read inbox message i: lanes 0..15 load the 64-B record
-DEV uint32_t load_rec(const RoundArgs& a, uint32_t ib, uint32_t i) {
-    uint32_t slot = a.in_slot[ib + i];
+// Inbox chunk c (messages c..c+3): lane l loads word l&15 of message
+// c + (l>>4), so one load instruction brings four 64-B records.  SL holds
+// the slots of messages [c & ~63, +64) one per lane.
+DEV uint32_t load_chunk(const RoundArgs& a, uint32_t ib, uint32_t ik, uint32_t c, uint32_t& SL) {
     uint32_t l = lane_id();
-    return l < 16 ? reinterpret_cast<const uint32_t*>(a.rec_in + slot)[l] : 0u;
+    if ((c & 63) == 0) SL = (c + l < ik) ? a.in_slot[ib + c + l] : 0u;
+    uint32_t j = (c & 63) + (l >> 4);
+    uint32_t slot = shfl(SL, (int)j);
+    return (c + (l >> 4) < ik) ? reinterpret_cast<const uint32_t*>(a.rec_in + slot)[l & 15] : 0u;
 }
 
-DEV void process(Wv& w, uint32_t n, uint32_t fl, uint32_t ib, uint32_t ik) {
+DEV void process(Wv& w, uint32_t n) {
     const RoundArgs& a = *w.a;
     const uint32_t r = a.round;
     uint32_t l = lane_id();
-    st_add(w, ST_UP, 1);
+    // issue every load of the node up front
+    uint32_t fl = a.flags[n];
+    uint32_t ik = a.in_cnt[n], ib = a.in_beg[n];
     w.h = a.hdr[n];
+    w.A = l < PSIM_ACTIVE_CAP ? a.act[(size_t)n * PSIM_ACTIVE_CAP + l] : 0u;
+    w.P = l < PSIM_PASSIVE_CAP ? a.pas[(size_t)n * PSIM_PASSIVE_CAP + l] : 0u;
+    w.obase = a.obase[n];
+    w.mypart = a.part[n];
+    uint32_t SL = 0, R0 = 0;
+    if (ik) R0 = load_chunk(a, ib, ik, 0, SL);
     if (w.h.start_round == r && ik) {           // fresh incarnation: no connections yet
         st_add(w, ST_DROPPED, ik);
         ik = 0;
@@ -660,28 +697,25 @@ DEV void process(Wv& w, uint32_t n, uint32_t fl, uint32_t ib, uint32_t ik) {
     bool lazy = lazy_due && w.h.out_n > 0;
     bool joining = w.h.start_round == r && w.h.join_contact != NONE;
     w.act_n = w.h.act_n;
-    w.A = l < PSIM_ACTIVE_CAP ? a.act[(size_t)n * PSIM_ACTIVE_CAP + l] : 0u;
     uint64_t exits = 0;
     if (a.crash_round) {
         bool dead = l < w.act_n && w.A != n && (a.flags[w.A] & F_CRASHED);
         exits = ballot(dead);
     }
-    if (!(ik || joining || exits || promo || shuf || origin || lazy)) return;
+    bool promo_work = promo && w.act_n < a.min_active;
+    if (!(ik || joining || exits || promo_work || shuf || origin || lazy)) return;
     st_add(w, ST_PROC, 1);
 
     w.me = n;
-    w.mypart = a.part[n];
     w.pas_n = w.h.pas_n; w.sent_n = w.h.sent_n; w.sent_head = w.h.sent_head;
     w.recv_n = w.h.recv_n; w.recv_head = w.h.recv_head;
     w.all_n = w.h.all_n; w.com_n = w.h.com_n; w.eag_n = w.h.eag_n; w.laz_n = w.h.laz_n;
     w.out_n = w.h.out_n;
-    w.P = l < PSIM_PASSIVE_CAP ? a.pas[(size_t)n * PSIM_PASSIVE_CAP + l] : 0u;
-    w.maps = false; w.pt = false;
+    w.maps = false; w.pt = false; w.maps_dirty = false; w.pt_dirty = false;
+    const uint32_t A0 = w.A, P0 = w.P;
     w.SP = w.SI = w.RP = w.RI = 0;
     w.ALL = w.COM = w.EAG = w.LAZ = 0; w.OUT = 0;
-    w.obase = a.obase[n];
     w.seq = 0;
-    w.digest = 0;
 
     if (joining)                                      // hv:500-515
         hv_send(w, w.h.join_contact, PSIM_MSG_JOIN, 0, w.h.epoch, 0, 0, 0);
@@ -698,15 +732,19 @@ DEV void process(Wv& w, uint32_t n, uint32_t fl, uint32_t ib, uint32_t ik) {
         }
     }
 
-    for (uint32_t i = 0; i < ik; i++) {               // HyParView inbox, canonical order
-        uint32_t R = load_rec(a, ib, i);
-        uint32_t tt = rl(R, 2), type = tt & 0xFF;
-        if (type >= PSIM_MSG_PT_BROADCAST) continue;
-        st_add(w, ST_DELIV + type, 1);
-        uint32_t nex = (tt >> 16) & 0xFF;
-        uint32_t ex = shfl(R, (int)((l + 8) & 63));
-        ex = l < nex ? ex : 0u;
-        hv_handle(w, type, rl(R, 1), (tt >> 8) & 0xFF, rl(R, 4), rl(R, 5), ex, nex);
+    for (uint32_t c = 0; c < ik; c += 4) {            // HyParView inbox, canonical order
+        uint32_t R4 = c == 0 ? R0 : load_chunk(a, ib, ik, c, SL);
+        uint32_t cm = ik - c < 4 ? ik - c : 4;
+        for (uint32_t q = 0; q < cm; q++) {
+            uint32_t b = q * 16;
+            uint32_t tt = rl(R4, b + 2), type = tt & 0xFF;
+            if (type >= PSIM_MSG_PT_BROADCAST) continue;
+            st_add(w, ST_DELIV + type, 1);
+            uint32_t nex = (tt >> 16) & 0xFF;
+            uint32_t ex = shfl(R4, (int)((b + 8 + l) & 63));
+            ex = l < nex ? ex : 0u;
+            hv_handle(w, type, rl(R4, b + 1), (tt >> 8) & 0xFF, rl(R4, b + 4), rl(R4, b + 5), ex, nex);
+        }
     }
 
     if (promo && w.act_n < a.min_active)              // hv:542-561
@@ -719,12 +757,16 @@ DEV void process(Wv& w, uint32_t n, uint32_t fl, uint32_t ib, uint32_t ik) {
     }
 
     if (a.plumtree) {
-        for (uint32_t i = 0; i < ik; i++) {           // Plumtree inbox
-            uint32_t R = load_rec(a, ib, i);
-            uint32_t type = rl(R, 2) & 0xFF;
-            if (type < PSIM_MSG_PT_BROADCAST || type > PSIM_MSG_PT_GRAFT) continue;
-            st_add(w, ST_DELIV + type, 1);
-            pt_handle(w, type, rl(R, 1), rl(R, 4), rl(R, 5), rl(R, 6));
+        for (uint32_t c = 0; c < ik; c += 4) {        // Plumtree inbox
+            uint32_t R4 = c == 0 ? R0 : load_chunk(a, ib, ik, c, SL);
+            uint32_t cm = ik - c < 4 ? ik - c : 4;
+            for (uint32_t q = 0; q < cm; q++) {
+                uint32_t b = q * 16;
+                uint32_t type = rl(R4, b + 2) & 0xFF;
+                if (type < PSIM_MSG_PT_BROADCAST || type > PSIM_MSG_PT_GRAFT) continue;
+                st_add(w, ST_DELIV + type, 1);
+                pt_handle(w, type, rl(R4, b + 1), rl(R4, b + 4), rl(R4, b + 5), rl(R4, b + 6));
+            }
         }
         if (origin) {                                 // pt:282-287, backend:179-200
             load_pt(w);
@@ -750,13 +792,14 @@ DEV void process(Wv& w, uint32_t n, uint32_t fl, uint32_t ib, uint32_t ik) {
     w.h.recv_n = (uint8_t)w.recv_n; w.h.recv_head = (uint8_t)w.recv_head;
     w.h.all_n = (uint8_t)w.all_n; w.h.com_n = (uint8_t)w.com_n;
     w.h.eag_n = (uint8_t)w.eag_n; w.h.laz_n = (uint8_t)w.laz_n; w.h.out_n = (uint8_t)w.out_n;
-    if (l < PSIM_ACTIVE_CAP) a.act[(size_t)n * PSIM_ACTIVE_CAP + l] = w.A;
-    if (l < PSIM_PASSIVE_CAP) a.pas[(size_t)n * PSIM_PASSIVE_CAP + l] = w.P;
-    if (w.maps && l < PSIM_IDMAP_CAP) {
+    // write back only what changed
+    if (ballot(w.A != A0) && l < PSIM_ACTIVE_CAP) a.act[(size_t)n * PSIM_ACTIVE_CAP + l] = w.A;
+    if (ballot(w.P != P0) && l < PSIM_PASSIVE_CAP) a.pas[(size_t)n * PSIM_PASSIVE_CAP + l] = w.P;
+    if (w.maps_dirty && l < PSIM_IDMAP_CAP) {
         size_t b = (size_t)n * PSIM_IDMAP_CAP + l;
         a.sentp[b] = w.SP; a.senti[b] = w.SI; a.recvp[b] = w.RP; a.recvi[b] = w.RI;
     }
-    if (w.pt) {
+    if (w.pt_dirty) {
         if (l < PSIM_PT_MEMBERS_CAP) {
             a.pt_all[(size_t)n * PSIM_PT_MEMBERS_CAP + l] = w.ALL;
             a.pt_com[(size_t)n * PSIM_PT_MEMBERS_CAP + l] = w.COM;
@@ -777,10 +820,10 @@ DEV void process(Wv& w, uint32_t n, uint32_t fl, uint32_t ib, uint32_t ik) {
     if (l == 0) {
         a.ocnt[n] = w.seq;
         // only this wave writes its node's flag byte; peers read F_UP/F_CRASHED
-        uint8_t nf = (uint8_t)((fl & ~F_LAZY) | (w.out_n ? F_LAZY : 0));
+        uint8_t nf = (uint8_t)((fl & ~(F_LAZY | F_LOWACT)) | (w.out_n ? F_LAZY : 0) |
+                               (w.act_n < a.min_active ? F_LOWACT : 0));
         if (nf != fl) a.flags[n] = nf;
     }
-    if (w.digest) st_add(w, ST_DIGEST, w.digest);
 }
 
 __global__ void __launch_bounds__(256) k_consume(RoundArgs args) {
@@ -797,15 +840,18 @@ __global__ void __launch_bounds__(256) k_consume(RoundArgs args) {
     w.lds = scratch[wid];
     w.st = sst;
     w.round = args.round;
-    for (uint32_t n = gw; n < args.n_nodes; n += nw) {
-        uint32_t fl = args.flags[n];
-        uint32_t ik = args.in_cnt[n];
-        if (!(fl & F_UP)) {
-            if (ik) st_add(w, ST_DROPPED, ik);
-            continue;
-        }
-        w.me = n;
-        process(w, n, fl, args.in_beg[n], ik);
+    w.SC = 0;
+    w.digest = 0;
+    const uint32_t na = *args.n_alist;
+    for (uint32_t i = gw; i < na; i += nw) process(w, args.alist[i]);
+    // flush this wave's counters and digest partials into the block's LDS stats
+    {
+        uint32_t l = lane_id();
+        if (l < NST && w.SC) atomicAdd((unsigned long long*)&sst[l], (unsigned long long)w.SC);
+        uint64_t d = w.digest;
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) d += shfl64(d, (int)((l + off) & 63));
+        if (l == 0 && d) atomicAdd((unsigned long long*)&sst[ST_DIGEST], (unsigned long long)d);
     }
 
     __syncthreads();

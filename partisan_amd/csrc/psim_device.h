@@ -36,7 +36,9 @@ struct __attribute__((aligned(16))) Msg {
 static_assert(sizeof(Msg) == 64, "Msg must be 64 B");
 
 // node flag byte
-enum : uint8_t { F_UP = 1, F_CRASHED = 2, F_LAZY = 4 };
+// F_LAZY: outstanding lazy pushes; F_LOWACT: |active| < min_active_size (a due
+// promotion timer can act)
+enum : uint8_t { F_UP = 1, F_CRASHED = 2, F_LAZY = 4, F_LOWACT = 8 };
 
 // route key: dst in the low 27 bits, the sender-side emission bound of the
 // message type in the top 5 (used to size the receiver's next outbox).

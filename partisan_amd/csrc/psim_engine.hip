@@ -89,7 +89,8 @@ __global__ void k_join(RoundArgs a, const uint32_t* ids, const uint32_t* contact
         a.pt_laz[(size_t)id * PSIM_PT_SET_CAP + k] = 0;
     }
     for (int k = 0; k < PSIM_PT_OUT_CAP; k++) a.pt_out[(size_t)id * PSIM_PT_OUT_CAP + k] = 0;
-    a.flags[id] = (uint8_t)((a.flags[id] & F_CRASHED) | F_UP);
+    a.flags[id] = (uint8_t)((a.flags[id] & F_CRASHED) | F_UP | (1u < a.min_active ? F_LOWACT : 0));
+    const_cast<uint32_t*>(a.start)[id] = a.round;
 }
 
 __global__ void k_bcast_reset(Hdr* hdr, uint32_t n, uint32_t bit) {
@@ -115,19 +116,47 @@ __global__ void k_runs(const uint32_t* __restrict__ keys, const uint32_t* __rest
     }
 }
 
-// Upper bound of each node's emissions this round (sizes its outbox region).
-__global__ void k_bounds(const uint32_t* bsum, const uint8_t* flags, uint64_t* bound, uint32_t n,
-                         uint32_t crash_round, uint32_t origin_node) {
+__device__ __forceinline__ bool due(uint32_t period, uint32_t r, uint32_t start) {
+    return period > 0 && r > start && ((r - start) % period) == 0;
+}
+
+// Per node: the upper bound of its emissions this round (sizes its outbox
+// region) and whether it has any work (inbox, join, timers, EXIT scan,
+// origin, outstanding lazy pushes).  Also counts live nodes and messages
+// addressed to dead ones.
+__global__ void k_node_prep(RoundArgs a, const uint32_t* bsum, uint64_t* bound, uint32_t* work,
+                            uint64_t* part) {
+    __shared__ uint64_t s_up, s_drop;
+    if (threadIdx.x == 0) { s_up = 0; s_drop = 0; }
+    __syncthreads();
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    uint64_t b = 0;
-    if (flags[i] & F_UP) {
-        b = bsum[i] + BOUND_BASE;
-        if (flags[i] & F_LAZY) b += BOUND_LAZY;
-        if (crash_round) b += BOUND_EXITS;
-        if (i == origin_node) b += BOUND_ORIGIN;
+    if (i < a.n_nodes) {
+        uint8_t f = a.flags[i];
+        uint64_t b = 0;
+        uint32_t w = 0;
+        uint32_t c = a.in_cnt[i];
+        if (f & F_UP) {
+            uint32_t st = a.start[i], r = a.round;
+            b = bsum[i] + BOUND_BASE;
+            if (f & F_LAZY) b += BOUND_LAZY;
+            if (a.crash_round) b += BOUND_EXITS;
+            if (a.origin_now && i == a.origin_node) b += BOUND_ORIGIN;
+            w = c > 0 || st == r || a.crash_round || (f & F_LAZY) ||
+                (a.origin_now && i == a.origin_node) ||
+                (a.random_promotion && (f & F_LOWACT) && due(a.promotion_period, r, st)) ||
+                due(a.shuffle_period, r, st);
+            atomicAdd((unsigned long long*)&s_up, 1ull);
+        } else if (c) {
+            atomicAdd((unsigned long long*)&s_drop, (unsigned long long)c);
+        }
+        bound[i] = b;
+        work[i] = w;
     }
-    bound[i] = b;
+    __syncthreads();
+    if (threadIdx.x < NST) {
+        uint64_t v = threadIdx.x == ST_UP ? s_up : threadIdx.x == ST_DROPPED ? s_drop : 0ull;
+        part[(size_t)blockIdx.x * NST + threadIdx.x] = v;
+    }
 }
 
 // Dense (key, slot) pairs of this round's emissions, in node (= src, seq) order.
@@ -201,7 +230,7 @@ struct psim_handle {
     DBuf<uint64_t> pt_out;
     // route
     DBuf<Msg> rec[2];
-    DBuf<uint32_t> okey, ocnt, dpos, keys[2], vals[2], cnt, bsum, in_beg;
+    DBuf<uint32_t> okey, ocnt, dpos, keys[2], vals[2], cnt, bsum, in_beg, start, work, alist, d_nact;
     DBuf<uint64_t> bound, obase;
     DBuf<uint32_t> d_m;          // [0] = messages in the current inbox
     DBuf<uint64_t> stat_part, stat_out;
@@ -242,6 +271,7 @@ RoundArgs make_args(psim_handle* h) {
     a.recvp = h->recvp.p; a.recvi = h->recvi.p;
     a.pt_all = h->pt_all.p; a.pt_com = h->pt_com.p; a.pt_eag = h->pt_eag.p; a.pt_laz = h->pt_laz.p;
     a.pt_out = h->pt_out.p;
+    a.start = h->start.p;
     return a;
 }
 
@@ -336,8 +366,10 @@ int run_round(psim_handle* h, uint64_t* stats_out) {
     h->pend_part_set = h->pend_part_clear = false;
     h->pend_bcast = false;
 
-    // ---- prepare: inbox run lengths, outbox bounds, offsets
+    // ---- prepare: inbox run lengths, outbox bounds, offsets, active list
     uint64_t total_bound;
+    const uint32_t pgrid = grid_for(N);
+    const uint32_t cgrid = std::min<uint32_t>(grid_for(N), 2048);
     {
         KTimer t(h, KT_PREPARE);
         HIP_TRY(hipMemsetAsync(h->cnt.p, 0, (size_t)N * 4, h->stream));
@@ -346,8 +378,18 @@ int run_round(psim_handle* h, uint64_t* stats_out) {
             uint32_t g = std::min<uint32_t>(grid_for(h->m_in), 4096);
             k_runs<<<g, BLK, 0, h->stream>>>(h->keys[0].p, h->d_m.p, h->cnt.p, h->bsum.p);
         }
-        k_bounds<<<grid_for(N), BLK, 0, h->stream>>>(h->bsum.p, h->flags.p, h->bound.p, N, crashes,
-                                                      a.origin_now ? a.origin_node : PSIM_NONE);
+        a.in_cnt = h->cnt.p;
+        if (h->stat_part.ensure((size_t)(pgrid + cgrid) * NST)) return PSIM_ENOMEM;
+        k_node_prep<<<pgrid, BLK, 0, h->stream>>>(a, h->bsum.p, h->bound.p, h->work.p, h->stat_part.p);
+        {
+            size_t tb = 0;
+            hipcub::CountingInputIterator<uint32_t> ids(0);
+            HIP_TRY(hipcub::DeviceSelect::Flagged(nullptr, tb, ids, h->work.p, h->alist.p, h->d_nact.p,
+                                                  N, h->stream));
+            if (h->cub_tmp.ensure(tb)) return PSIM_ENOMEM;
+            HIP_TRY(hipcub::DeviceSelect::Flagged(h->cub_tmp.p, tb, ids, h->work.p, h->alist.p,
+                                                  h->d_nact.p, N, h->stream));
+        }
         if ((rc = scan_u32(h, h->cnt.p, h->in_beg.p, N))) return rc;
         if ((rc = scan_u64(h, h->bound.p, h->obase.p, N))) return rc;
         uint64_t last_b = read1(h, h->bound.p + (N - 1));
@@ -360,13 +402,12 @@ int run_round(psim_handle* h, uint64_t* stats_out) {
     if (h->okey.ensure(total_bound + 1)) return PSIM_ENOMEM;
 
     // ---- consume
-    uint32_t cgrid = grid_for(N);
-    if (h->stat_part.ensure((size_t)cgrid * NST)) return PSIM_ENOMEM;
     a.in_beg = h->in_beg.p; a.in_cnt = h->cnt.p; a.in_slot = h->vals[0].p;
+    a.alist = h->alist.p; a.n_alist = h->d_nact.p;
     a.rec_in = h->rec[h->cur].p;
     a.obase = h->obase.p;
     a.rec_out = h->rec[nxt].p; a.okey = h->okey.p; a.ocnt = h->ocnt.p;
-    a.stat_part = h->stat_part.p;
+    a.stat_part = h->stat_part.p + (size_t)pgrid * NST;
     {
         KTimer t(h, KT_CONSUME);
         HIP_TRY(hipMemsetAsync(h->ocnt.p, 0, (size_t)N * 4, h->stream));
@@ -407,7 +448,7 @@ int run_round(psim_handle* h, uint64_t* stats_out) {
     }
     {
         KTimer t(h, KT_STATS);
-        k_stats_reduce<<<NST, BLK, 0, h->stream>>>(h->stat_part.p, cgrid, h->stat_out.p);
+        k_stats_reduce<<<NST, BLK, 0, h->stream>>>(h->stat_part.p, pgrid + cgrid, h->stat_out.p);
         if (!crashed.empty()) {
             if ((rc = upload(h, h->ev_ids, crashed))) return rc;
             k_uncrash<<<grid_for(crashed.size()), BLK, 0, h->stream>>>(h->flags.p, h->ev_ids.p,
@@ -496,6 +537,7 @@ int psim_create(const psim_config* cfg, psim_handle** out) {
     rc |= h->pt_out.alloc(N * PSIM_PT_OUT_CAP);
     rc |= h->ocnt.alloc(N); rc |= h->dpos.alloc(N); rc |= h->cnt.alloc(N); rc |= h->bsum.alloc(N);
     rc |= h->in_beg.alloc(N); rc |= h->bound.alloc(N); rc |= h->obase.alloc(N);
+    rc |= h->start.alloc(N); rc |= h->work.alloc(N); rc |= h->alist.alloc(N); rc |= h->d_nact.alloc(1);
     rc |= h->d_m.alloc(1); rc |= h->stat_out.alloc(NST);
     rc |= h->keys[0].alloc(1024); rc |= h->vals[0].alloc(1024);
     rc |= h->rec[0].alloc(1024);
@@ -515,6 +557,7 @@ void psim_destroy(psim_handle* h) {
     for (int b = 0; b < 2; b++) { h->rec[b].release(); h->keys[b].release(); h->vals[b].release(); }
     h->okey.release(); h->ocnt.release(); h->dpos.release(); h->cnt.release(); h->bsum.release();
     h->in_beg.release(); h->bound.release(); h->obase.release(); h->d_m.release();
+    h->start.release(); h->work.release(); h->alist.release(); h->d_nact.release();
     h->stat_part.release(); h->stat_out.release(); h->cub_tmp.release();
     h->ev_ids.release(); h->ev_contacts.release();
     for (int k = 0; k < KT_N; k++) { hipEventDestroy(h->ev[k][0]); hipEventDestroy(h->ev[k][1]); }

@@ -22,6 +22,9 @@ struct RoundArgs {
     // inbox (this round) and outbox (next round)
     const uint32_t* in_beg;
     const uint32_t* in_cnt;
+    const uint32_t* start;      // start round per node (timer phases)
+    const uint32_t* alist;      // nodes with work this round
+    const uint32_t* n_alist;
     const uint32_t* in_slot;
     const Msg* rec_in;
     const uint64_t* obase;
