@@ -1,0 +1,155 @@
+/*
+ * partisan_gpu_sim_nif.c -- Erlang NIF shim over include/partisan_gpu_sim.h.
+ *
+ * Built only where erl_nif.h exists (not in this image):
+ *   cc -O2 -fPIC -shared -I$(ERTS_INCLUDE_DIR) -I../../include \
+ *      -o ../priv/partisan_gpu_sim_nif.so partisan_gpu_sim_nif.c \
+ *      -L../../partisan_amd/csrc -lpartisan_gpu_sim
+ *
+ * One resource per simulator handle; calls on a handle are serialised by a
+ * mutex (the ABI is thread-compatible, not thread-safe) and psim_step runs on
+ * a dirty CPU scheduler because it blocks for whole BSP rounds.
+ */
+#include <erl_nif.h>
+#include <string.h>
+
+#include "partisan_gpu_sim.h"
+
+typedef struct { psim_handle *h; ErlNifMutex *mu; } sim_res;
+static ErlNifResourceType *SIM_RT;
+
+static void sim_dtor(ErlNifEnv *env, void *obj) {
+    sim_res *r = (sim_res *)obj;
+    if (r->h) psim_destroy(r->h);
+    if (r->mu) enif_mutex_destroy(r->mu);
+}
+
+static int load(ErlNifEnv *env, void **priv, ERL_NIF_TERM info) {
+    SIM_RT = enif_open_resource_type(env, NULL, "psim", sim_dtor, ERL_NIF_RT_CREATE, NULL);
+    return SIM_RT ? 0 : -1;
+}
+
+static ERL_NIF_TERM err(ErlNifEnv *env, int rc) {
+    return enif_make_tuple2(env, enif_make_atom(env, "error"),
+                            enif_make_atom(env, psim_strerror(rc)));
+}
+
+static int get_u32(ErlNifEnv *env, ERL_NIF_TERM map, const char *k, uint32_t *out) {
+    ERL_NIF_TERM v;
+    unsigned int x;
+    if (!enif_get_map_value(env, map, enif_make_atom(env, k), &v)) return 1; /* keep default */
+    if (!enif_get_uint(env, v, &x)) return 0;
+    *out = x;
+    return 1;
+}
+
+/* create(#{n_nodes => N, seed => S, max_active_size => .., ...}) -> {ok, Ref} */
+static ERL_NIF_TERM nif_create(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[]) {
+    psim_config c;
+    ErlNifUInt64 seed;
+    ERL_NIF_TERM v;
+    psim_default_config(&c);
+    if (!get_u32(env, argv[0], "n_nodes", &c.n_nodes) ||
+        !get_u32(env, argv[0], "max_active_size", &c.max_active_size) ||
+        !get_u32(env, argv[0], "min_active_size", &c.min_active_size) ||
+        !get_u32(env, argv[0], "max_passive_size", &c.max_passive_size) ||
+        !get_u32(env, argv[0], "arwl", &c.arwl) || !get_u32(env, argv[0], "prwl", &c.prwl) ||
+        !get_u32(env, argv[0], "shuffle_period", &c.shuffle_period) ||
+        !get_u32(env, argv[0], "plumtree", &c.plumtree))
+        return enif_make_badarg(env);
+    if (enif_get_map_value(env, argv[0], enif_make_atom(env, "seed"), &v) &&
+        enif_get_uint64(env, v, &seed))
+        c.seed = seed;
+    sim_res *r = enif_alloc_resource(SIM_RT, sizeof *r);
+    r->mu = enif_mutex_create("psim");
+    int rc = psim_create(&c, &r->h);
+    if (rc) { r->h = NULL; enif_release_resource(r); return err(env, rc); }
+    ERL_NIF_TERM t = enif_make_resource(env, r);
+    enif_release_resource(r);
+    return enif_make_tuple2(env, enif_make_atom(env, "ok"), t);
+}
+
+/* join(Ref, NodesBin, ContactsBin): little-endian u32 arrays */
+static ERL_NIF_TERM nif_join(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[]) {
+    sim_res *r; ErlNifBinary a, b;
+    if (!enif_get_resource(env, argv[0], SIM_RT, (void **)&r) ||
+        !enif_inspect_binary(env, argv[1], &a) || !enif_inspect_binary(env, argv[2], &b) ||
+        a.size != b.size || a.size % 4)
+        return enif_make_badarg(env);
+    enif_mutex_lock(r->mu);
+    int rc = psim_join(r->h, (const uint32_t *)a.data, (const uint32_t *)b.data, a.size / 4);
+    enif_mutex_unlock(r->mu);
+    return rc ? err(env, rc) : enif_make_atom(env, "ok");
+}
+
+static ERL_NIF_TERM nif_crash(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[]) {
+    sim_res *r; ErlNifBinary a;
+    if (!enif_get_resource(env, argv[0], SIM_RT, (void **)&r) ||
+        !enif_inspect_binary(env, argv[1], &a) || a.size % 4)
+        return enif_make_badarg(env);
+    enif_mutex_lock(r->mu);
+    int rc = psim_crash(r->h, (const uint32_t *)a.data, a.size / 4);
+    enif_mutex_unlock(r->mu);
+    return rc ? err(env, rc) : enif_make_atom(env, "ok");
+}
+
+static ERL_NIF_TERM nif_broadcast(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[]) {
+    sim_res *r; unsigned root, id;
+    if (!enif_get_resource(env, argv[0], SIM_RT, (void **)&r) ||
+        !enif_get_uint(env, argv[1], &root) || !enif_get_uint(env, argv[2], &id))
+        return enif_make_badarg(env);
+    enif_mutex_lock(r->mu);
+    int rc = psim_broadcast(r->h, root, id);
+    enif_mutex_unlock(r->mu);
+    return rc ? err(env, rc) : enif_make_atom(env, "ok");
+}
+
+/* step(Ref, Rounds) -> {ok, [{Round, Emitted, Delivered, FirstDeliveries}]} (dirty CPU) */
+static ERL_NIF_TERM nif_step(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[]) {
+    sim_res *r; unsigned n;
+    if (!enif_get_resource(env, argv[0], SIM_RT, (void **)&r) || !enif_get_uint(env, argv[1], &n) ||
+        n == 0 || n > 100000)
+        return enif_make_badarg(env);
+    psim_round_stats *st = enif_alloc(n * sizeof *st);
+    enif_mutex_lock(r->mu);
+    int rc = psim_step(r->h, n, st);
+    enif_mutex_unlock(r->mu);
+    if (rc) { enif_free(st); return err(env, rc); }
+    ERL_NIF_TERM list = enif_make_list(env, 0);
+    for (unsigned i = n; i-- > 0;) {
+        uint64_t em = 0, de = 0;
+        for (int t = 0; t < PSIM_MSG_NTYPES; t++) { em += st[i].emitted[t]; de += st[i].delivered[t]; }
+        ERL_NIF_TERM e = enif_make_tuple4(env, enif_make_uint64(env, st[i].round),
+                                          enif_make_uint64(env, em), enif_make_uint64(env, de),
+                                          enif_make_uint64(env, st[i].first_deliveries));
+        list = enif_make_list_cell(env, e, list);
+    }
+    enif_free(st);
+    return enif_make_tuple2(env, enif_make_atom(env, "ok"), list);
+}
+
+/* active(Ref, Node) -> {ok, [Id]} : sets:to_list(Active) of one node */
+static ERL_NIF_TERM nif_active(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[]) {
+    sim_res *r; unsigned node;
+    psim_node_view v;
+    if (!enif_get_resource(env, argv[0], SIM_RT, (void **)&r) || !enif_get_uint(env, argv[1], &node))
+        return enif_make_badarg(env);
+    enif_mutex_lock(r->mu);
+    int rc = psim_get_nodes(r->h, node, 1, &v);
+    enif_mutex_unlock(r->mu);
+    if (rc) return err(env, rc);
+    ERL_NIF_TERM ids[PSIM_ACTIVE_CAP];
+    for (uint32_t i = 0; i < v.act_n; i++) ids[i] = enif_make_uint(env, v.act[i]);
+    return enif_make_tuple2(env, enif_make_atom(env, "ok"), enif_make_list_from_array(env, ids, v.act_n));
+}
+
+static ErlNifFunc funcs[] = {
+    {"create", 1, nif_create, 0},
+    {"join_nif", 3, nif_join, 0},
+    {"crash_nif", 2, nif_crash, 0},
+    {"broadcast", 3, nif_broadcast, 0},
+    {"step", 2, nif_step, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"active", 2, nif_active, 0},
+};
+
+ERL_NIF_INIT(partisan_gpu_sim, funcs, load, NULL, NULL, NULL)

@@ -1,0 +1,27 @@
+%% partisan_gpu_sim -- NIF bindings of the MI355X simulator
+%% (include/partisan_gpu_sim.h).  Node ids are the simulated nodes; an id maps
+%% to the harness node_spec #{name => 'n<id>@sim', ...} (DESIGN.md section 2).
+-module(partisan_gpu_sim).
+-export([create/1, join/3, crash/2, broadcast/3, step/2, active/2]).
+-on_load(init/0).
+
+init() ->
+    Priv = case code:priv_dir(partisan_gpu_sim) of
+               {error, _} -> "priv";
+               Dir -> Dir
+           end,
+    erlang:load_nif(filename:join(Priv, "partisan_gpu_sim_nif"), 0).
+
+-spec create(map()) -> {ok, reference()} | {error, atom()}.
+create(_Config) -> erlang:nif_error(nif_not_loaded).
+
+%% Nodes/Contacts: lists of ids, packed as little-endian u32 binaries.
+join(Sim, Nodes, Contacts) -> join_nif(Sim, pack(Nodes), pack(Contacts)).
+crash(Sim, Nodes) -> crash_nif(Sim, pack(Nodes)).
+broadcast(_Sim, _Root, _Id) -> erlang:nif_error(nif_not_loaded).
+step(_Sim, _Rounds) -> erlang:nif_error(nif_not_loaded).
+active(_Sim, _Node) -> erlang:nif_error(nif_not_loaded).
+
+pack(Ids) -> << <<I:32/little>> || I <- Ids >>.
+join_nif(_S, _N, _C) -> erlang:nif_error(nif_not_loaded).
+crash_nif(_S, _N) -> erlang:nif_error(nif_not_loaded).
