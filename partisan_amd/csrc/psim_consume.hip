@@ -120,7 +120,7 @@ struct Wv {
     const RoundArgs* a;
     uint32_t* lds;       // 64 words of per-wave scratch
     uint64_t* st;        // block stats (LDS)
-    uint32_t me, mypart, round;
+    uint32_t me, li, mypart, round;   // global id, local row index
     Hdr h;
     uint32_t act_n, pas_n, sent_n, sent_head, recv_n, recv_head;
     uint32_t all_n, com_n, eag_n, laz_n, out_n;
@@ -272,7 +272,7 @@ DEV void hv_send(Wv& w, uint32_t dst, uint32_t type, uint32_t ttl, uint32_t a0, 
 DEV void load_maps(Wv& w) {
     if (w.maps) return;
     uint32_t l = lane_id();
-    size_t b = (size_t)w.me * PSIM_IDMAP_CAP + l;
+    size_t b = (size_t)w.li * PSIM_IDMAP_CAP + l;
     bool in = l < PSIM_IDMAP_CAP;
     w.SP = in ? w.a->sentp[b] : 0u; w.SI = in ? w.a->senti[b] : 0u;
     w.RP = in ? w.a->recvp[b] : 0u; w.RI = in ? w.a->recvi[b] : 0u;
@@ -390,7 +390,7 @@ DEV void move_to_active(Wv& w, uint32_t p) {             // hv:1679-1709
 DEV void load_pt(Wv& w) {
     if (w.pt) return;
     uint32_t l = lane_id();
-    size_t n = w.me;
+    size_t n = w.li;
     w.ALL = l < PSIM_PT_MEMBERS_CAP ? w.a->pt_all[n * PSIM_PT_MEMBERS_CAP + l] : 0u;
     w.COM = l < PSIM_PT_MEMBERS_CAP ? w.a->pt_com[n * PSIM_PT_MEMBERS_CAP + l] : 0u;
     w.EAG = l < PSIM_PT_SET_CAP ? w.a->pt_eag[n * PSIM_PT_SET_CAP + l] : 0u;
@@ -677,12 +677,14 @@ DEV void process(Wv& w, uint32_t n) {
     const uint32_t r = a.round;
     uint32_t l = lane_id();
     // issue every load of the node up front
+    const uint32_t li = n - a.lo;
+    w.li = li;
     uint32_t fl = a.flags[n];
-    uint32_t ik = a.in_cnt[n], ib = a.in_beg[n];
-    w.h = a.hdr[n];
-    w.A = l < PSIM_ACTIVE_CAP ? a.act[(size_t)n * PSIM_ACTIVE_CAP + l] : 0u;
-    w.P = l < PSIM_PASSIVE_CAP ? a.pas[(size_t)n * PSIM_PASSIVE_CAP + l] : 0u;
-    w.obase = a.obase[n];
+    uint32_t ik = a.in_cnt[li], ib = a.in_beg[li];
+    w.h = a.hdr[li];
+    w.A = l < PSIM_ACTIVE_CAP ? a.act[(size_t)li * PSIM_ACTIVE_CAP + l] : 0u;
+    w.P = l < PSIM_PASSIVE_CAP ? a.pas[(size_t)li * PSIM_PASSIVE_CAP + l] : 0u;
+    w.obase = a.obase[li];
     w.mypart = a.part[n];
     uint32_t SL = 0, R0 = 0;
     if (ik) R0 = load_chunk(a, ib, ik, 0, SL);
@@ -793,32 +795,32 @@ DEV void process(Wv& w, uint32_t n) {
     w.h.all_n = (uint8_t)w.all_n; w.h.com_n = (uint8_t)w.com_n;
     w.h.eag_n = (uint8_t)w.eag_n; w.h.laz_n = (uint8_t)w.laz_n; w.h.out_n = (uint8_t)w.out_n;
     // write back only what changed
-    if (ballot(w.A != A0) && l < PSIM_ACTIVE_CAP) a.act[(size_t)n * PSIM_ACTIVE_CAP + l] = w.A;
-    if (ballot(w.P != P0) && l < PSIM_PASSIVE_CAP) a.pas[(size_t)n * PSIM_PASSIVE_CAP + l] = w.P;
+    if (ballot(w.A != A0) && l < PSIM_ACTIVE_CAP) a.act[(size_t)li * PSIM_ACTIVE_CAP + l] = w.A;
+    if (ballot(w.P != P0) && l < PSIM_PASSIVE_CAP) a.pas[(size_t)li * PSIM_PASSIVE_CAP + l] = w.P;
     if (w.maps_dirty && l < PSIM_IDMAP_CAP) {
-        size_t b = (size_t)n * PSIM_IDMAP_CAP + l;
+        size_t b = (size_t)li * PSIM_IDMAP_CAP + l;
         a.sentp[b] = w.SP; a.senti[b] = w.SI; a.recvp[b] = w.RP; a.recvi[b] = w.RI;
     }
     if (w.pt_dirty) {
         if (l < PSIM_PT_MEMBERS_CAP) {
-            a.pt_all[(size_t)n * PSIM_PT_MEMBERS_CAP + l] = w.ALL;
-            a.pt_com[(size_t)n * PSIM_PT_MEMBERS_CAP + l] = w.COM;
+            a.pt_all[(size_t)li * PSIM_PT_MEMBERS_CAP + l] = w.ALL;
+            a.pt_com[(size_t)li * PSIM_PT_MEMBERS_CAP + l] = w.COM;
         }
         if (l < PSIM_PT_SET_CAP) {
-            a.pt_eag[(size_t)n * PSIM_PT_SET_CAP + l] = w.EAG;
-            a.pt_laz[(size_t)n * PSIM_PT_SET_CAP + l] = w.LAZ;
+            a.pt_eag[(size_t)li * PSIM_PT_SET_CAP + l] = w.EAG;
+            a.pt_laz[(size_t)li * PSIM_PT_SET_CAP + l] = w.LAZ;
         }
-        if (l < PSIM_PT_OUT_CAP) a.pt_out[(size_t)n * PSIM_PT_OUT_CAP + l] = w.OUT;
+        if (l < PSIM_PT_OUT_CAP) a.pt_out[(size_t)li * PSIM_PT_OUT_CAP + l] = w.OUT;
     }
     {
         const uint32_t* hw = reinterpret_cast<const uint32_t*>(&w.h);
         uint32_t v = 0;
 #pragma unroll
         for (int k = 0; k < 16; k++) v = l == (uint32_t)k ? hw[k] : v;
-        if (l < 16) reinterpret_cast<uint32_t*>(a.hdr + n)[l] = v;
+        if (l < 16) reinterpret_cast<uint32_t*>(a.hdr + li)[l] = v;
     }
     if (l == 0) {
-        a.ocnt[n] = w.seq;
+        a.ocnt[li] = w.seq;
         // only this wave writes its node's flag byte; peers read F_UP/F_CRASHED
         uint8_t nf = (uint8_t)((fl & ~(F_LAZY | F_LOWACT)) | (w.out_n ? F_LAZY : 0) |
                                (w.act_n < a.min_active ? F_LOWACT : 0));
@@ -826,7 +828,7 @@ DEV void process(Wv& w, uint32_t n) {
     }
 }
 
-__global__ void __launch_bounds__(256) k_consume(RoundArgs args) {
+__global__ void __launch_bounds__(256, 4) k_consume(RoundArgs args) {
     __shared__ uint64_t sst[NST];
     __shared__ uint32_t scratch[WAVES_PER_BLOCK][64];
     for (int i = threadIdx.x; i < NST; i += blockDim.x) sst[i] = 0;

@@ -1,24 +1,32 @@
 // psim_engine.hip -- device memory, event kernels, the message route
-// (K-route) and the C ABI of include/partisan_gpu_sim.h.
+// (K-route), the cross-shard exchange and the C ABI of
+// include/partisan_gpu_sim.h.
 //
-// One round on one shard:
-//   events   -> k_crash / k_join / k_bcast_reset        (pending API calls)
-//   prepare  -> k_runs  : run lengths + outbox bounds of the sorted inbox
-//               k_bounds: per-node outbox bound; scans -> in_beg, obase
-//   consume  -> k_consume (psim_consume.hip)
-//   route    -> scan(ocnt) -> k_compact -> radix sort by dst (stable, so
-//               each inbox is in canonical (src, seq) order) -> next inbox
-//   stats    -> k_stats_reduce
+// The global id space [0, N) is cut into G contiguous shards.  A process owns
+// `n_shards` of them (virtual shards on its device, exchanged by device
+// copies) or exactly one when run as an RCCL rank (shard_world > 1).  Per
+// round and shard (DESIGN.md sections 3 and 7):
+//   events   k_crash / k_join / k_bcast_reset    (same event list on every shard)
+//   prepare  k_runs (inbox run lengths + emission bounds), k_node_prep
+//            (bounds, work flags), compaction -> active list, scans -> in_beg, obase
+//   consume  k_consume (psim_consume.hip)
+//   route    G == 1: scan(ocnt) -> k_compact -> stable radix sort by dst
+//            G  > 1: stable partition by owner shard -> gather records ->
+//                    all-to-all (counts, then records) -> stable sort of the
+//                    shard-ordered concatenation by dst
+//   stats    k_stats_reduce (+ sum over shards / ncclAllReduce)
+// A stable sort of a (src, seq)-ordered stream -- or of a concatenation
+// ordered by source shard -- yields each inbox in canonical (src, seq) order,
+// so any shard count gives bit-identical results.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
+#include <rccl/rccl.h>
 
 #include <algorithm>
-#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <new>
-#include <string>
 #include <vector>
 
 #include "psim_device.h"
@@ -40,6 +48,22 @@ constexpr int BLK = 256;
         }                                                                \
     } while (0)
 
+#define NCCL_TRY(x)                                                      \
+    do {                                                                 \
+        ncclResult_t r_ = (x);                                           \
+        if (r_ != ncclSuccess) {                                         \
+            std::fprintf(stderr, "psim: %s failed: %s (%s:%d)\n", #x,    \
+                         ncclGetErrorString(r_), __FILE__, __LINE__);    \
+            return PSIM_ECOMM;                                           \
+        }                                                                \
+    } while (0)
+
+#define TRY(x)                   \
+    do {                         \
+        int rc_ = (x);           \
+        if (rc_) return rc_;     \
+    } while (0)
+
 // ------------------------------------------------------------ kernels --
 __global__ void k_crash(uint8_t* flags, const uint32_t* ids, uint32_t n) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -56,14 +80,19 @@ __global__ void k_uncrash(uint8_t* flags, const uint32_t* ids, uint32_t n) {
 }
 
 // node start: init/1 of the manager (hv:289-354) and of the broadcast
-// server (pt:251-264, members = [own name]); one lane per joining node.
-__global__ void k_join(RoundArgs a, const uint32_t* ids, const uint32_t* contacts, uint32_t n,
-                       uint32_t persist_epoch) {
+// server (pt:251-264, members = [own name]).  Every shard marks every
+// joining node up in its replicated flag array; only the owner initialises
+// the node's rows.
+__global__ void k_join(RoundArgs a, uint32_t* start, const uint32_t* ids, const uint32_t* contacts,
+                       uint32_t n, uint32_t persist_epoch) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     uint32_t id = ids[i];
+    a.flags[id] = (uint8_t)((a.flags[id] & F_CRASHED) | F_UP | (1u < a.min_active ? F_LOWACT : 0));
+    if (id < a.lo || id >= a.lo + a.n_local) return;
+    uint32_t li = id - a.lo;
     Hdr h;
-    uint32_t old_epoch = a.hdr[id].epoch;
+    uint32_t old_epoch = a.hdr[li].epoch;
     memset(&h, 0, sizeof h);
     h.epoch = persist_epoch ? old_epoch + 1 : 1;
     h.start_round = a.round;
@@ -71,26 +100,25 @@ __global__ void k_join(RoundArgs a, const uint32_t* ids, const uint32_t* contact
     h.pt_root = PSIM_NONE;
     h.trk_round = PSIM_NONE;
     h.act_n = 1; h.all_n = 1; h.com_n = 1;
-    a.hdr[id] = h;
-    uint32_t* act = a.act + (size_t)id * PSIM_ACTIVE_CAP;
+    a.hdr[li] = h;
+    start[li] = a.round;
+    uint32_t* act = a.act + (size_t)li * PSIM_ACTIVE_CAP;
     for (int k = 0; k < PSIM_ACTIVE_CAP; k++) act[k] = k == 0 ? id : 0u;
-    uint32_t* pas = a.pas + (size_t)id * PSIM_PASSIVE_CAP;
+    uint32_t* pas = a.pas + (size_t)li * PSIM_PASSIVE_CAP;
     for (int k = 0; k < PSIM_PASSIVE_CAP; k++) pas[k] = 0;
     for (int k = 0; k < PSIM_IDMAP_CAP; k++) {
-        a.sentp[(size_t)id * PSIM_IDMAP_CAP + k] = 0; a.senti[(size_t)id * PSIM_IDMAP_CAP + k] = 0;
-        a.recvp[(size_t)id * PSIM_IDMAP_CAP + k] = 0; a.recvi[(size_t)id * PSIM_IDMAP_CAP + k] = 0;
+        size_t b = (size_t)li * PSIM_IDMAP_CAP + k;
+        a.sentp[b] = 0; a.senti[b] = 0; a.recvp[b] = 0; a.recvi[b] = 0;
     }
     for (int k = 0; k < PSIM_PT_MEMBERS_CAP; k++) {
-        a.pt_all[(size_t)id * PSIM_PT_MEMBERS_CAP + k] = k == 0 ? id : 0u;
-        a.pt_com[(size_t)id * PSIM_PT_MEMBERS_CAP + k] = k == 0 ? id : 0u;
+        a.pt_all[(size_t)li * PSIM_PT_MEMBERS_CAP + k] = k == 0 ? id : 0u;
+        a.pt_com[(size_t)li * PSIM_PT_MEMBERS_CAP + k] = k == 0 ? id : 0u;
     }
     for (int k = 0; k < PSIM_PT_SET_CAP; k++) {
-        a.pt_eag[(size_t)id * PSIM_PT_SET_CAP + k] = 0;
-        a.pt_laz[(size_t)id * PSIM_PT_SET_CAP + k] = 0;
+        a.pt_eag[(size_t)li * PSIM_PT_SET_CAP + k] = 0;
+        a.pt_laz[(size_t)li * PSIM_PT_SET_CAP + k] = 0;
     }
-    for (int k = 0; k < PSIM_PT_OUT_CAP; k++) a.pt_out[(size_t)id * PSIM_PT_OUT_CAP + k] = 0;
-    a.flags[id] = (uint8_t)((a.flags[id] & F_CRASHED) | F_UP | (1u < a.min_active ? F_LOWACT : 0));
-    const_cast<uint32_t*>(a.start)[id] = a.round;
+    for (int k = 0; k < PSIM_PT_OUT_CAP; k++) a.pt_out[(size_t)li * PSIM_PT_OUT_CAP + k] = 0;
 }
 
 __global__ void k_bcast_reset(Hdr* hdr, uint32_t n, uint32_t bit) {
@@ -101,13 +129,11 @@ __global__ void k_bcast_reset(Hdr* hdr, uint32_t n, uint32_t bit) {
     hdr[i].trk_hop = 0;
 }
 
-// Run lengths of the sorted inbox: the lane at the start of each dst run
-// writes the run's length and the sum of its messages' emission bounds.
-__global__ void k_runs(const uint32_t* __restrict__ keys, const uint32_t* __restrict__ m_ptr,
-                       uint32_t* cnt, uint32_t* bsum) {
-    uint32_t m = *m_ptr;
+// Run lengths of the sorted inbox (local dst): the lane at the start of each
+// run writes the run's length and the sum of its messages' emission bounds.
+__global__ void k_runs(const uint32_t* __restrict__ keys, uint32_t m, uint32_t* cnt, uint32_t* bsum) {
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < m; i += gridDim.x * blockDim.x) {
-        uint32_t k = keys[i], d = k & KEY_DST_MASK;
+        uint32_t d = keys[i] & KEY_DST_MASK;
         if (i > 0 && (keys[i - 1] & KEY_DST_MASK) == d) continue;
         uint32_t j = i, s = 0;
         while (j < m && (keys[j] & KEY_DST_MASK) == d) { s += keys[j] >> KEY_DST_BITS; j++; }
@@ -120,29 +146,30 @@ __device__ __forceinline__ bool due(uint32_t period, uint32_t r, uint32_t start)
     return period > 0 && r > start && ((r - start) % period) == 0;
 }
 
-// Per node: the upper bound of its emissions this round (sizes its outbox
-// region) and whether it has any work (inbox, join, timers, EXIT scan,
-// origin, outstanding lazy pushes).  Also counts live nodes and messages
-// addressed to dead ones.
+// Per local node: the upper bound of its emissions this round (sizes its
+// outbox region) and whether it has any work (inbox, join, timers, EXIT
+// scan, origin, outstanding lazy pushes).  Also counts live nodes and
+// messages addressed to dead ones.
 __global__ void k_node_prep(RoundArgs a, const uint32_t* bsum, uint64_t* bound, uint32_t* work,
                             uint64_t* part) {
     __shared__ uint64_t s_up, s_drop;
     if (threadIdx.x == 0) { s_up = 0; s_drop = 0; }
     __syncthreads();
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < a.n_nodes) {
-        uint8_t f = a.flags[i];
+    if (i < a.n_local) {
+        uint32_t id = a.lo + i;
+        uint8_t f = a.flags[id];
         uint64_t b = 0;
         uint32_t w = 0;
         uint32_t c = a.in_cnt[i];
         if (f & F_UP) {
             uint32_t st = a.start[i], r = a.round;
+            bool origin = a.origin_now && id == a.origin_node;
             b = bsum[i] + BOUND_BASE;
             if (f & F_LAZY) b += BOUND_LAZY;
             if (a.crash_round) b += BOUND_EXITS;
-            if (a.origin_now && i == a.origin_node) b += BOUND_ORIGIN;
-            w = c > 0 || st == r || a.crash_round || (f & F_LAZY) ||
-                (a.origin_now && i == a.origin_node) ||
+            if (origin) b += BOUND_ORIGIN;
+            w = c > 0 || st == r || a.crash_round || (f & F_LAZY) || origin ||
                 (a.random_promotion && (f & F_LOWACT) && due(a.promotion_period, r, st)) ||
                 due(a.shuffle_period, r, st);
             atomicAdd((unsigned long long*)&s_up, 1ull);
@@ -174,6 +201,44 @@ __global__ void k_compact(const uint32_t* ocnt, const uint32_t* dpos, const uint
     }
 }
 
+// owner shard of each emitted message (G > 1)
+__global__ void k_owner(const uint32_t* keys, uint32_t* owner, uint32_t m, uint32_t per) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < m) owner[i] = (keys[i] & KEY_DST_MASK) / per;
+}
+
+// first index of each owner in the owner-sorted array (G + 1 entries)
+__global__ void k_owner_bounds(const uint32_t* owner, uint32_t m, uint32_t g, uint64_t* off) {
+    uint32_t t = threadIdx.x;
+    if (t > g) return;
+    uint32_t lo = 0, hi = m;
+    while (lo < hi) {
+        uint32_t mid = (lo + hi) >> 1;
+        if (owner[mid] < t) lo = mid + 1; else hi = mid;
+    }
+    off[t] = lo;
+}
+
+// send buffer in owner order: 64-B records, 4 lanes x 16 B per record
+__global__ void k_gather(const Msg* __restrict__ rec, const uint32_t* __restrict__ slots, uint32_t m,
+                         Msg* __restrict__ out) {
+    uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    uint64_t i = t >> 2;
+    if (i >= m) return;
+    const uint4* s = reinterpret_cast<const uint4*>(&rec[slots[i]]);
+    reinterpret_cast<uint4*>(&out[i])[t & 3] = s[t & 3];
+}
+
+// receive side: route keys of the received records (local dst | bound)
+__global__ void k_rkeys(const Msg* __restrict__ rec, uint32_t m, uint32_t lo, uint32_t* keys,
+                        uint32_t* vals) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    uint32_t type = rec[i].tt & 0xFF;
+    keys[i] = (rec[i].dst - lo) | (max_emit(type) << KEY_DST_BITS);
+    vals[i] = i;
+}
+
 // one block per stats slot; lanes stride over the per-block partials
 __global__ void k_stats_reduce(const uint64_t* part, uint32_t nblocks, uint64_t* out) {
     __shared__ uint64_t red[BLK];
@@ -194,50 +259,76 @@ template <typename T>
 struct DBuf {
     T* p = nullptr;
     size_t n = 0;
-    int ensure(size_t want) {
+    int ensure(size_t want) {   // grow, contents not kept
         if (want <= n) return PSIM_OK;
-        if (p) hipFree(p);
+        if (p) (void)hipFree(p);
         p = nullptr; n = 0;
         size_t cap = std::max<size_t>(want + want / 4, 1024);
         if (hipMalloc(&p, cap * sizeof(T)) != hipSuccess) return PSIM_ENOMEM;
         n = cap;
         return PSIM_OK;
     }
-    int alloc(size_t want) {   // exact, zeroed
+    int alloc(size_t want) {    // exact, zeroed
         if (hipMalloc(&p, std::max<size_t>(want, 1) * sizeof(T)) != hipSuccess) return PSIM_ENOMEM;
         n = want;
         if (hipMemset(p, 0, std::max<size_t>(want, 1) * sizeof(T)) != hipSuccess) return PSIM_EDEVICE;
         return PSIM_OK;
     }
-    void release() { if (p) hipFree(p); p = nullptr; n = 0; }
+    void release() { if (p) (void)hipFree(p); p = nullptr; n = 0; }
 };
 
-enum Kern { KT_EVENTS, KT_PREPARE, KT_CONSUME, KT_SCAN, KT_COMPACT, KT_SORT, KT_STATS, KT_N };
-const char* kKernName[KT_N] = {"events", "prepare", "consume", "scan", "compact", "sort", "stats"};
+enum Kern { KT_EVENTS, KT_PREPARE, KT_CONSUME, KT_SCAN, KT_COMPACT, KT_SORT, KT_EXCHANGE, KT_STATS, KT_N };
+const char* kKernName[KT_N] = {"events", "prepare", "consume", "scan", "compact", "sort",
+                               "exchange", "stats"};
+
+inline uint32_t grid_for(uint64_t n) { return (uint32_t)std::max<uint64_t>(1, (n + BLK - 1) / BLK); }
+
+int bits_for(uint64_t n) {
+    int b = 1;
+    while (b < 32 && (1ull << b) < n) b++;
+    return b;
+}
+
+struct Shard {
+    uint32_t idx = 0, lo = 0, n = 0;    // global shard index, owned [lo, lo + n)
+    hipStream_t stream = nullptr;
+    // replicated (global id)
+    DBuf<uint8_t> flags, part;
+    // local rows
+    DBuf<Hdr> hdr;
+    DBuf<uint32_t> act, pas, sentp, senti, recvp, recvi, pt_all, pt_com, pt_eag, pt_laz, start;
+    DBuf<uint64_t> pt_out;
+    // inbox of the next round: sorted (local dst | bound, record index) pairs
+    DBuf<uint32_t> ikeys, ivals;
+    uint32_t m_in = 0;
+    DBuf<Msg> rec[2];                   // records the inbox indexes (rec[cur])
+    uint32_t cur = 0;
+    DBuf<Msg> outbox;                   // G > 1 outbox (G == 1 writes rec[cur ^ 1])
+    // per-round scratch
+    DBuf<uint32_t> okey, ocnt, dpos, keys, vals, owner, owner_s, vals_s, cnt, bsum, in_beg, work,
+        alist, d_nact;
+    DBuf<uint64_t> bound, obase, stat_part, stat_out, d_off;
+    DBuf<uint8_t> cub_tmp;
+    DBuf<uint32_t> ev_ids, ev_contacts;
+    DBuf<Msg> sendbuf;
+    std::vector<uint64_t> soff, scnt;   // per destination shard (G + 1 offsets)
+    uint32_t m_out = 0, pgrid = 0, cgrid = 0;
+    uint64_t st_host[NST];
+    hipEvent_t ev[KT_N][2];
+    bool ev_live = false;
+};
 
 }  // namespace
 
 struct psim_handle {
     psim_config cfg;
-    uint32_t N;
-    int device;
-    hipStream_t stream;
+    uint32_t N = 0, G = 1, per = 0;
+    int device = 0;
     uint64_t round = 0;
-    // node state
-    DBuf<uint8_t> flags, part;
-    DBuf<Hdr> hdr;
-    DBuf<uint32_t> act, pas, sentp, senti, recvp, recvi, pt_all, pt_com, pt_eag, pt_laz;
-    DBuf<uint64_t> pt_out;
-    // route
-    DBuf<Msg> rec[2];
-    DBuf<uint32_t> okey, ocnt, dpos, keys[2], vals[2], cnt, bsum, in_beg, start, work, alist, d_nact;
-    DBuf<uint64_t> bound, obase;
-    DBuf<uint32_t> d_m;          // [0] = messages in the current inbox
-    DBuf<uint64_t> stat_part, stat_out;
-    DBuf<uint8_t> cub_tmp;
-    DBuf<uint32_t> ev_ids, ev_contacts;
-    uint32_t cur = 0;            // rec[cur] holds the inbox records
-    uint32_t m_in = 0;           // messages in the inbox
+    std::vector<Shard*> shards;         // shards owned by this process
+    int rank = 0, world = 1;
+    ncclComm_t comm = nullptr;
+    DBuf<uint64_t> comm_cnt;            // RCCL: [send counts | recv counts]
     // pending events
     std::vector<uint32_t> pend_crash, pend_join, pend_contact;
     std::vector<uint8_t> pend_part;
@@ -245,19 +336,18 @@ struct psim_handle {
     bool pend_bcast = false;
     uint32_t pend_root = 0, pend_msg = 0;
     uint32_t bcast_root = PSIM_NONE, tracked_msg = PSIM_NONE;
-    // profiling
-    hipEvent_t ev[KT_N][2];
     double kt_ms[KT_N] = {0};
     uint64_t kt_n[KT_N] = {0};
 };
 
 namespace {
 
-RoundArgs make_args(psim_handle* h) {
+RoundArgs make_args(psim_handle* h, Shard* s) {
     RoundArgs a;
     memset(&a, 0, sizeof a);
     const psim_config& c = h->cfg;
     a.n_nodes = h->N; a.round = (uint32_t)h->round; a.seed = c.seed;
+    a.lo = s->lo; a.n_local = s->n;
     a.max_active = c.max_active_size; a.min_active = c.min_active_size;
     a.max_passive = c.max_passive_size; a.arwl = c.arwl; a.prwl = c.prwl;
     a.k_active = c.k_active; a.k_passive = c.k_passive;
@@ -266,199 +356,328 @@ RoundArgs make_args(psim_handle* h) {
     a.lazy_tick_period = c.lazy_tick_period;
     a.tracked_msg = h->tracked_msg; a.bcast_root = h->bcast_root;
     a.origin_node = PSIM_NONE;
-    a.flags = h->flags.p; a.part = h->part.p; a.hdr = h->hdr.p;
-    a.act = h->act.p; a.pas = h->pas.p; a.sentp = h->sentp.p; a.senti = h->senti.p;
-    a.recvp = h->recvp.p; a.recvi = h->recvi.p;
-    a.pt_all = h->pt_all.p; a.pt_com = h->pt_com.p; a.pt_eag = h->pt_eag.p; a.pt_laz = h->pt_laz.p;
-    a.pt_out = h->pt_out.p;
-    a.start = h->start.p;
+    a.flags = s->flags.p; a.part = s->part.p; a.hdr = s->hdr.p;
+    a.act = s->act.p; a.pas = s->pas.p; a.sentp = s->sentp.p; a.senti = s->senti.p;
+    a.recvp = s->recvp.p; a.recvi = s->recvi.p;
+    a.pt_all = s->pt_all.p; a.pt_com = s->pt_com.p; a.pt_eag = s->pt_eag.p; a.pt_laz = s->pt_laz.p;
+    a.pt_out = s->pt_out.p;
+    a.start = s->start.p;
     return a;
 }
 
+// per-kernel-class device time, HIP events on the shard's stream
 struct KTimer {
     psim_handle* h;
+    Shard* s;
     int k;
-    KTimer(psim_handle* h_, int k_) : h(h_), k(k_) { hipEventRecord(h->ev[k][0], h->stream); }
+    KTimer(psim_handle* h_, Shard* s_, int k_) : h(h_), s(s_), k(k_) {
+        (void)hipEventRecord(s->ev[k][0], s->stream);
+    }
     ~KTimer() {
-        hipEventRecord(h->ev[k][1], h->stream);
-        hipEventSynchronize(h->ev[k][1]);
+        (void)hipEventRecord(s->ev[k][1], s->stream);
+        (void)hipEventSynchronize(s->ev[k][1]);
         float ms = 0;
-        hipEventElapsedTime(&ms, h->ev[k][0], h->ev[k][1]);
+        (void)hipEventElapsedTime(&ms, s->ev[k][0], s->ev[k][1]);
         h->kt_ms[k] += ms;
         h->kt_n[k]++;
     }
 };
 
-inline uint32_t grid_for(uint64_t n) { return (uint32_t)std::max<uint64_t>(1, (n + BLK - 1) / BLK); }
-
-int scan_u32(psim_handle* h, const uint32_t* in, uint32_t* out, uint32_t n) {
+template <typename T>
+int scan_excl(Shard* s, const T* in, T* out, uint32_t n) {
     size_t tb = 0;
-    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, in, out, n, h->stream));
-    if (h->cub_tmp.ensure(tb)) return PSIM_ENOMEM;
-    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(h->cub_tmp.p, tb, in, out, n, h->stream));
+    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, in, out, n, s->stream));
+    TRY(s->cub_tmp.ensure(tb));
+    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(s->cub_tmp.p, tb, in, out, n, s->stream));
     return PSIM_OK;
 }
 
-int scan_u64(psim_handle* h, const uint64_t* in, uint64_t* out, uint32_t n) {
+int sort_pairs(Shard* s, const uint32_t* kin, uint32_t* kout, const uint32_t* vin, uint32_t* vout,
+               uint32_t m, int bits) {
+    if (!m) return PSIM_OK;
     size_t tb = 0;
-    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, in, out, n, h->stream));
-    if (h->cub_tmp.ensure(tb)) return PSIM_ENOMEM;
-    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(h->cub_tmp.p, tb, in, out, n, h->stream));
+    HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, kin, kout, vin, vout, m, 0, bits, s->stream));
+    TRY(s->cub_tmp.ensure(tb));
+    HIP_TRY(hipcub::DeviceRadixSort::SortPairs(s->cub_tmp.p, tb, kin, kout, vin, vout, m, 0, bits,
+                                               s->stream));
     return PSIM_OK;
 }
 
 template <typename T>
-T read1(psim_handle* h, const T* p) {
+T read1(Shard* s, const T* p) {
     T v{};
-    hipMemcpyAsync(&v, p, sizeof(T), hipMemcpyDeviceToHost, h->stream);
-    hipStreamSynchronize(h->stream);
+    (void)hipMemcpyAsync(&v, p, sizeof(T), hipMemcpyDeviceToHost, s->stream);
+    (void)hipStreamSynchronize(s->stream);
     return v;
 }
 
-int upload(psim_handle* h, DBuf<uint32_t>& b, const std::vector<uint32_t>& v) {
-    if (b.ensure(v.size())) return PSIM_ENOMEM;
-    HIP_TRY(hipMemcpyAsync(b.p, v.data(), v.size() * 4, hipMemcpyHostToDevice, h->stream));
+int upload(Shard* s, DBuf<uint32_t>& b, const std::vector<uint32_t>& v) {
+    TRY(b.ensure(v.size()));
+    HIP_TRY(hipMemcpyAsync(b.p, v.data(), v.size() * 4, hipMemcpyHostToDevice, s->stream));
     return PSIM_OK;
 }
 
-int dst_bits(uint32_t n) {
-    int b = 1;
-    while (b < (int)KEY_DST_BITS && (1ull << b) < n) b++;
-    return b;
-}
+struct RoundCtl {
+    bool crashes = false, origin = false;
+    uint32_t origin_node = PSIM_NONE, origin_msg = 0;
+};
 
-int run_round(psim_handle* h, uint64_t* stats_out) {
-    const uint32_t N = h->N;
-    RoundArgs a = make_args(h);
-    int rc;
-    bool crashes = !h->pend_crash.empty();
-    // ---- events
+// events + prepare for one shard; leaves `a` ready for k_consume
+int phase_events_prepare(psim_handle* h, Shard* s, const RoundCtl& ctl, RoundArgs& a) {
+    const uint32_t n = s->n;
+    a = make_args(h, s);
+    a.crash_round = ctl.crashes;
+    if (ctl.origin) { a.origin_now = 1; a.origin_node = ctl.origin_node; a.origin_msg = ctl.origin_msg; }
     {
-        KTimer t(h, KT_EVENTS);
-        if (crashes) {
-            if ((rc = upload(h, h->ev_ids, h->pend_crash))) return rc;
-            k_crash<<<grid_for(h->pend_crash.size()), BLK, 0, h->stream>>>(
-                h->flags.p, h->ev_ids.p, (uint32_t)h->pend_crash.size());
+        KTimer t(h, s, KT_EVENTS);
+        if (ctl.crashes) {
+            TRY(upload(s, s->ev_ids, h->pend_crash));
+            k_crash<<<grid_for(h->pend_crash.size()), BLK, 0, s->stream>>>(
+                s->flags.p, s->ev_ids.p, (uint32_t)h->pend_crash.size());
         }
         if (!h->pend_join.empty()) {
-            if ((rc = upload(h, h->ev_ids, h->pend_join))) return rc;
-            if ((rc = upload(h, h->ev_contacts, h->pend_contact))) return rc;
-            k_join<<<grid_for(h->pend_join.size()), BLK, 0, h->stream>>>(
-                a, h->ev_ids.p, h->ev_contacts.p, (uint32_t)h->pend_join.size(), h->cfg.persist_epoch);
+            TRY(upload(s, s->ev_ids, h->pend_join));
+            TRY(upload(s, s->ev_contacts, h->pend_contact));
+            k_join<<<grid_for(h->pend_join.size()), BLK, 0, s->stream>>>(
+                a, s->start.p, s->ev_ids.p, s->ev_contacts.p, (uint32_t)h->pend_join.size(),
+                h->cfg.persist_epoch);
         }
-        if (h->pend_part_clear) HIP_TRY(hipMemsetAsync(h->part.p, 0, N, h->stream));
+        if (h->pend_part_clear) HIP_TRY(hipMemsetAsync(s->part.p, 0, h->N, s->stream));
         if (h->pend_part_set)
-            HIP_TRY(hipMemcpyAsync(h->part.p, h->pend_part.data(), N, hipMemcpyHostToDevice, h->stream));
-        if (h->pend_bcast) {
-            h->tracked_msg = h->pend_msg;
-            k_bcast_reset<<<grid_for(N), BLK, 0, h->stream>>>(h->hdr.p, N, 1u << (h->pend_msg & 31u));
-            // origin only if the root's manager is running after the events
-            uint8_t f = 0;
-            HIP_TRY(hipMemcpyAsync(&f, h->flags.p + h->pend_root, 1, hipMemcpyDeviceToHost, h->stream));
-            HIP_TRY(hipStreamSynchronize(h->stream));
-            if (f & F_UP) { a.origin_now = 1; a.origin_node = h->pend_root; a.origin_msg = h->pend_msg; }
-        }
-        a.tracked_msg = h->tracked_msg;
-        a.crash_round = crashes;
+            HIP_TRY(hipMemcpyAsync(s->part.p, h->pend_part.data(), h->N, hipMemcpyHostToDevice, s->stream));
+        if (h->pend_bcast)
+            k_bcast_reset<<<grid_for(n), BLK, 0, s->stream>>>(s->hdr.p, n, 1u << (h->pend_msg & 31u));
     }
-    std::vector<uint32_t> crashed = h->pend_crash;
+    {
+        KTimer t(h, s, KT_PREPARE);
+        HIP_TRY(hipMemsetAsync(s->cnt.p, 0, (size_t)n * 4, s->stream));
+        HIP_TRY(hipMemsetAsync(s->bsum.p, 0, (size_t)n * 4, s->stream));
+        if (s->m_in) {
+            uint32_t g = std::min<uint32_t>(grid_for(s->m_in), 4096);
+            k_runs<<<g, BLK, 0, s->stream>>>(s->ikeys.p, s->m_in, s->cnt.p, s->bsum.p);
+        }
+        a.in_cnt = s->cnt.p;
+        s->pgrid = grid_for(n);
+        s->cgrid = std::min<uint32_t>(grid_for(n), 2048);
+        TRY(s->stat_part.ensure((size_t)(s->pgrid + s->cgrid) * NST));
+        k_node_prep<<<s->pgrid, BLK, 0, s->stream>>>(a, s->bsum.p, s->bound.p, s->work.p, s->stat_part.p);
+        {
+            size_t tb = 0;
+            hipcub::CountingInputIterator<uint32_t> ids(s->lo);
+            HIP_TRY(hipcub::DeviceSelect::Flagged(nullptr, tb, ids, s->work.p, s->alist.p, s->d_nact.p,
+                                                  n, s->stream));
+            TRY(s->cub_tmp.ensure(tb));
+            HIP_TRY(hipcub::DeviceSelect::Flagged(s->cub_tmp.p, tb, ids, s->work.p, s->alist.p,
+                                                  s->d_nact.p, n, s->stream));
+        }
+        TRY(scan_excl(s, s->cnt.p, s->in_beg.p, n));
+        TRY(scan_excl(s, s->bound.p, s->obase.p, n));
+        uint64_t total = read1(s, s->bound.p + (n - 1)) + read1(s, s->obase.p + (n - 1));
+        if (total >= 0xFFFFFFFFull) return PSIM_ENOMEM;
+        if (h->G == 1) TRY(s->rec[s->cur ^ 1].ensure(total + 1));
+        else TRY(s->outbox.ensure(total + 1));
+        TRY(s->okey.ensure(total + 1));
+    }
+    a.in_beg = s->in_beg.p; a.in_slot = s->ivals.p;
+    a.alist = s->alist.p; a.n_alist = s->d_nact.p;
+    a.rec_in = s->rec[s->cur].p;
+    a.obase = s->obase.p;
+    a.rec_out = h->G == 1 ? s->rec[s->cur ^ 1].p : s->outbox.p;
+    a.okey = s->okey.p; a.ocnt = s->ocnt.p;
+    a.stat_part = s->stat_part.p + (size_t)s->pgrid * NST;
+    return PSIM_OK;
+}
+
+int phase_consume(psim_handle* h, Shard* s, const RoundArgs& a) {
+    KTimer t(h, s, KT_CONSUME);
+    HIP_TRY(hipMemsetAsync(s->ocnt.p, 0, (size_t)s->n * 4, s->stream));
+    k_consume<<<s->cgrid, BLK, 0, s->stream>>>(a);
+    HIP_TRY(hipGetLastError());
+    return PSIM_OK;
+}
+
+// dense emission list in (src, seq) order: keys = dst | bound, vals = slot
+int phase_compact(psim_handle* h, Shard* s) {
+    {
+        KTimer t(h, s, KT_SCAN);
+        TRY(scan_excl(s, s->ocnt.p, s->dpos.p, s->n));
+        s->m_out = read1(s, s->ocnt.p + (s->n - 1)) + read1(s, s->dpos.p + (s->n - 1));
+    }
+    TRY(s->keys.ensure(s->m_out + 1));
+    TRY(s->vals.ensure(s->m_out + 1));
+    KTimer t(h, s, KT_COMPACT);
+    k_compact<<<grid_for(s->n), BLK, 0, s->stream>>>(s->ocnt.p, s->dpos.p, s->obase.p, s->okey.p,
+                                                     s->keys.p, s->vals.p, s->n);
+    return PSIM_OK;
+}
+
+// G == 1: the stable sort by dst is the whole route
+int phase_route_local(psim_handle* h, Shard* s) {
+    TRY(phase_compact(h, s));
+    TRY(s->ikeys.ensure(s->m_out + 1));
+    TRY(s->ivals.ensure(s->m_out + 1));
+    KTimer t(h, s, KT_SORT);
+    TRY(sort_pairs(s, s->keys.p, s->ikeys.p, s->vals.p, s->ivals.p, s->m_out, bits_for(s->n)));
+    s->m_in = s->m_out;
+    s->cur ^= 1;
+    return PSIM_OK;
+}
+
+// G > 1, sender side: stable partition by owner shard, records gathered
+// into the send buffer in that order; per-owner counts/offsets on the host
+int phase_partition(psim_handle* h, Shard* s) {
+    TRY(phase_compact(h, s));
+    const uint32_t m = s->m_out;
+    TRY(s->owner.ensure(m + 1)); TRY(s->owner_s.ensure(m + 1)); TRY(s->vals_s.ensure(m + 1));
+    TRY(s->sendbuf.ensure(m + 1));
+    TRY(s->d_off.ensure(h->G + 1));
+    KTimer t(h, s, KT_SORT);
+    s->soff.assign(h->G + 1, 0);
+    if (m) {
+        k_owner<<<grid_for(m), BLK, 0, s->stream>>>(s->keys.p, s->owner.p, m, h->per);
+        TRY(sort_pairs(s, s->owner.p, s->owner_s.p, s->vals.p, s->vals_s.p, m, bits_for(h->G)));
+        k_gather<<<grid_for((uint64_t)m * 4), BLK, 0, s->stream>>>(s->outbox.p, s->vals_s.p, m,
+                                                                    s->sendbuf.p);
+        k_owner_bounds<<<1, 128, 0, s->stream>>>(s->owner_s.p, m, h->G, s->d_off.p);
+        HIP_TRY(hipMemcpyAsync(s->soff.data(), s->d_off.p, (h->G + 1) * 8, hipMemcpyDeviceToHost,
+                               s->stream));
+        HIP_TRY(hipStreamSynchronize(s->stream));
+    }
+    s->soff[h->G] = m;
+    s->scnt.resize(h->G);
+    for (uint32_t g = 0; g < h->G; g++) s->scnt[g] = s->soff[g + 1] - s->soff[g];
+    return PSIM_OK;
+}
+
+// G > 1, receiver side: route keys of the shard-ordered concatenation, stable sort by dst
+int phase_receive(psim_handle* h, Shard* s, uint32_t m) {
+    uint32_t nxt = s->cur ^ 1;
+    TRY(s->keys.ensure(m + 1)); TRY(s->vals.ensure(m + 1));
+    TRY(s->ikeys.ensure(m + 1)); TRY(s->ivals.ensure(m + 1));
+    KTimer t(h, s, KT_SORT);
+    if (m) {
+        k_rkeys<<<grid_for(m), BLK, 0, s->stream>>>(s->rec[nxt].p, m, s->lo, s->keys.p, s->vals.p);
+        TRY(sort_pairs(s, s->keys.p, s->ikeys.p, s->vals.p, s->ivals.p, m, bits_for(s->n)));
+    }
+    s->m_in = m;
+    s->cur = nxt;
+    return PSIM_OK;
+}
+
+// virtual shards of this process: device copies between shard buffers
+int exchange_local(psim_handle* h) {
+    const uint32_t G = h->G;
+    std::vector<uint64_t> m(G, 0);
+    for (Shard* d : h->shards) {
+        for (Shard* s : h->shards) m[d->idx] += s->scnt[d->idx];
+        TRY(d->rec[d->cur ^ 1].ensure(m[d->idx] + 1));
+    }
+    for (Shard* d : h->shards) {
+        {
+            KTimer t(h, d, KT_EXCHANGE);
+            uint64_t off = 0;
+            for (uint32_t g = 0; g < G; g++) {  // concatenation in source-shard order
+                Shard* s = h->shards[g];
+                uint64_t c = s->scnt[d->idx];
+                if (c)
+                    HIP_TRY(hipMemcpyAsync(d->rec[d->cur ^ 1].p + off, s->sendbuf.p + s->soff[d->idx],
+                                           c * sizeof(Msg), hipMemcpyDeviceToDevice, d->stream));
+                off += c;
+            }
+        }
+        TRY(phase_receive(h, d, (uint32_t)m[d->idx]));
+    }
+    return PSIM_OK;
+}
+
+// one shard per RCCL rank: counts by all-to-all, records by grouped send/recv
+int exchange_rccl(psim_handle* h) {
+    Shard* s = h->shards[0];
+    const uint32_t G = h->G;
+    uint64_t m = 0;
+    {
+        KTimer t(h, s, KT_EXCHANGE);
+        TRY(h->comm_cnt.ensure(2 * G));
+        HIP_TRY(hipMemcpyAsync(h->comm_cnt.p, s->scnt.data(), G * 8, hipMemcpyHostToDevice, s->stream));
+        NCCL_TRY(ncclAllToAll(h->comm_cnt.p, h->comm_cnt.p + G, 1, ncclUint64, h->comm, s->stream));
+        std::vector<uint64_t> rcnt(G);
+        HIP_TRY(hipMemcpyAsync(rcnt.data(), h->comm_cnt.p + G, G * 8, hipMemcpyDeviceToHost, s->stream));
+        HIP_TRY(hipStreamSynchronize(s->stream));
+        std::vector<uint64_t> roff(G);
+        for (uint32_t g = 0; g < G; g++) { roff[g] = m; m += rcnt[g]; }
+        TRY(s->rec[s->cur ^ 1].ensure(m + 1));
+        Msg* rb = s->rec[s->cur ^ 1].p;
+        NCCL_TRY(ncclGroupStart());
+        for (uint32_t g = 0; g < G; g++) {
+            if (g == s->idx) continue;
+            if (s->scnt[g])
+                NCCL_TRY(ncclSend(s->sendbuf.p + s->soff[g], s->scnt[g] * sizeof(Msg), ncclUint8, (int)g,
+                                  h->comm, s->stream));
+            if (rcnt[g])
+                NCCL_TRY(ncclRecv(rb + roff[g], rcnt[g] * sizeof(Msg), ncclUint8, (int)g, h->comm,
+                                  s->stream));
+        }
+        NCCL_TRY(ncclGroupEnd());
+        if (rcnt[s->idx])
+            HIP_TRY(hipMemcpyAsync(rb + roff[s->idx], s->sendbuf.p + s->soff[s->idx],
+                                   rcnt[s->idx] * sizeof(Msg), hipMemcpyDeviceToDevice, s->stream));
+    }
+    return phase_receive(h, s, (uint32_t)m);
+}
+
+int phase_stats(psim_handle* h, Shard* s, const std::vector<uint32_t>& crashed) {
+    KTimer t(h, s, KT_STATS);
+    k_stats_reduce<<<NST, BLK, 0, s->stream>>>(s->stat_part.p, s->pgrid + s->cgrid, s->stat_out.p);
+    if (!crashed.empty()) {
+        TRY(upload(s, s->ev_ids, crashed));
+        k_uncrash<<<grid_for(crashed.size()), BLK, 0, s->stream>>>(s->flags.p, s->ev_ids.p,
+                                                                  (uint32_t)crashed.size());
+    }
+    return PSIM_OK;
+}
+
+int run_round(psim_handle* h, uint64_t* st) {
+    RoundCtl ctl;
+    ctl.crashes = !h->pend_crash.empty();
+    if (h->pend_bcast) {
+        h->tracked_msg = h->pend_msg;
+        // the root must be running after this round's events (flags are
+        // replicated, so any shard answers for any node)
+        Shard* s0 = h->shards[0];
+        uint8_t f = read1(s0, s0->flags.p + h->pend_root);
+        bool up_after = (f & F_UP) != 0;
+        for (uint32_t c : h->pend_crash) if (c == h->pend_root) up_after = false;
+        for (uint32_t j : h->pend_join) if (j == h->pend_root) up_after = true;
+        if (up_after) { ctl.origin = true; ctl.origin_node = h->pend_root; ctl.origin_msg = h->pend_msg; }
+    }
+    std::vector<RoundArgs> args(h->shards.size());
+    for (size_t i = 0; i < h->shards.size(); i++) TRY(phase_events_prepare(h, h->shards[i], ctl, args[i]));
+    for (size_t i = 0; i < h->shards.size(); i++) TRY(phase_consume(h, h->shards[i], args[i]));
+    if (h->G == 1) {
+        TRY(phase_route_local(h, h->shards[0]));
+    } else {
+        for (Shard* s : h->shards) TRY(phase_partition(h, s));
+        if (h->world > 1) TRY(exchange_rccl(h));
+        else TRY(exchange_local(h));
+    }
+    for (Shard* s : h->shards) TRY(phase_stats(h, s, h->pend_crash));
+    memset(st, 0, NST * 8);
+    for (Shard* s : h->shards) {
+        HIP_TRY(hipMemcpyAsync(s->st_host, s->stat_out.p, NST * 8, hipMemcpyDeviceToHost, s->stream));
+        HIP_TRY(hipStreamSynchronize(s->stream));
+        for (int k = 0; k < NST; k++) st[k] += s->st_host[k];
+    }
+    if (h->world > 1) {
+        Shard* s = h->shards[0];
+        TRY(h->comm_cnt.ensure(NST));
+        HIP_TRY(hipMemcpyAsync(h->comm_cnt.p, st, NST * 8, hipMemcpyHostToDevice, s->stream));
+        NCCL_TRY(ncclAllReduce(h->comm_cnt.p, h->comm_cnt.p, NST, ncclUint64, ncclSum, h->comm, s->stream));
+        HIP_TRY(hipMemcpyAsync(st, h->comm_cnt.p, NST * 8, hipMemcpyDeviceToHost, s->stream));
+        HIP_TRY(hipStreamSynchronize(s->stream));
+    }
     h->pend_crash.clear(); h->pend_join.clear(); h->pend_contact.clear();
     h->pend_part_set = h->pend_part_clear = false;
     h->pend_bcast = false;
-
-    // ---- prepare: inbox run lengths, outbox bounds, offsets, active list
-    uint64_t total_bound;
-    const uint32_t pgrid = grid_for(N);
-    const uint32_t cgrid = std::min<uint32_t>(grid_for(N), 2048);
-    {
-        KTimer t(h, KT_PREPARE);
-        HIP_TRY(hipMemsetAsync(h->cnt.p, 0, (size_t)N * 4, h->stream));
-        HIP_TRY(hipMemsetAsync(h->bsum.p, 0, (size_t)N * 4, h->stream));
-        if (h->m_in) {
-            uint32_t g = std::min<uint32_t>(grid_for(h->m_in), 4096);
-            k_runs<<<g, BLK, 0, h->stream>>>(h->keys[0].p, h->d_m.p, h->cnt.p, h->bsum.p);
-        }
-        a.in_cnt = h->cnt.p;
-        if (h->stat_part.ensure((size_t)(pgrid + cgrid) * NST)) return PSIM_ENOMEM;
-        k_node_prep<<<pgrid, BLK, 0, h->stream>>>(a, h->bsum.p, h->bound.p, h->work.p, h->stat_part.p);
-        {
-            size_t tb = 0;
-            hipcub::CountingInputIterator<uint32_t> ids(0);
-            HIP_TRY(hipcub::DeviceSelect::Flagged(nullptr, tb, ids, h->work.p, h->alist.p, h->d_nact.p,
-                                                  N, h->stream));
-            if (h->cub_tmp.ensure(tb)) return PSIM_ENOMEM;
-            HIP_TRY(hipcub::DeviceSelect::Flagged(h->cub_tmp.p, tb, ids, h->work.p, h->alist.p,
-                                                  h->d_nact.p, N, h->stream));
-        }
-        if ((rc = scan_u32(h, h->cnt.p, h->in_beg.p, N))) return rc;
-        if ((rc = scan_u64(h, h->bound.p, h->obase.p, N))) return rc;
-        uint64_t last_b = read1(h, h->bound.p + (N - 1));
-        uint64_t last_o = read1(h, h->obase.p + (N - 1));
-        total_bound = last_b + last_o;
-    }
-    if (total_bound >= 0xFFFFFFFFull) return PSIM_ENOMEM;
-    uint32_t nxt = h->cur ^ 1;
-    if (h->rec[nxt].ensure(total_bound + 1)) return PSIM_ENOMEM;
-    if (h->okey.ensure(total_bound + 1)) return PSIM_ENOMEM;
-
-    // ---- consume
-    a.in_beg = h->in_beg.p; a.in_cnt = h->cnt.p; a.in_slot = h->vals[0].p;
-    a.alist = h->alist.p; a.n_alist = h->d_nact.p;
-    a.rec_in = h->rec[h->cur].p;
-    a.obase = h->obase.p;
-    a.rec_out = h->rec[nxt].p; a.okey = h->okey.p; a.ocnt = h->ocnt.p;
-    a.stat_part = h->stat_part.p + (size_t)pgrid * NST;
-    {
-        KTimer t(h, KT_CONSUME);
-        HIP_TRY(hipMemsetAsync(h->ocnt.p, 0, (size_t)N * 4, h->stream));
-        k_consume<<<cgrid, BLK, 0, h->stream>>>(a);
-        HIP_TRY(hipGetLastError());
-    }
-    // ---- route: dense (dst, slot) pairs, stable sort by dst
-    uint32_t m_out;
-    {
-        KTimer t(h, KT_SCAN);
-        if ((rc = scan_u32(h, h->ocnt.p, h->dpos.p, N))) return rc;
-        uint32_t last_c = read1(h, h->ocnt.p + (N - 1));
-        uint32_t last_p = read1(h, h->dpos.p + (N - 1));
-        m_out = last_c + last_p;
-    }
-    for (int b = 0; b < 2; b++) {
-        if (h->keys[b].ensure(m_out + 1) || h->vals[b].ensure(m_out + 1)) return PSIM_ENOMEM;
-    }
-    {
-        KTimer t(h, KT_COMPACT);
-        k_compact<<<grid_for(N), BLK, 0, h->stream>>>(h->ocnt.p, h->dpos.p, h->obase.p, h->okey.p,
-                                                     h->keys[1].p, h->vals[1].p, N);
-    }
-    {
-        KTimer t(h, KT_SORT);
-        if (m_out) {
-            size_t tb = 0;
-            int bits = dst_bits(N);
-            HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, h->keys[1].p, h->keys[0].p,
-                                                       h->vals[1].p, h->vals[0].p, m_out, 0, bits,
-                                                       h->stream));
-            if (h->cub_tmp.ensure(tb)) return PSIM_ENOMEM;
-            HIP_TRY(hipcub::DeviceRadixSort::SortPairs(h->cub_tmp.p, tb, h->keys[1].p, h->keys[0].p,
-                                                       h->vals[1].p, h->vals[0].p, m_out, 0, bits,
-                                                       h->stream));
-        }
-        HIP_TRY(hipMemcpyAsync(h->d_m.p, &m_out, 4, hipMemcpyHostToDevice, h->stream));
-    }
-    {
-        KTimer t(h, KT_STATS);
-        k_stats_reduce<<<NST, BLK, 0, h->stream>>>(h->stat_part.p, pgrid + cgrid, h->stat_out.p);
-        if (!crashed.empty()) {
-            if ((rc = upload(h, h->ev_ids, crashed))) return rc;
-            k_uncrash<<<grid_for(crashed.size()), BLK, 0, h->stream>>>(h->flags.p, h->ev_ids.p,
-                                                                      (uint32_t)crashed.size());
-        }
-        HIP_TRY(hipMemcpyAsync(stats_out, h->stat_out.p, NST * 8, hipMemcpyDeviceToHost, h->stream));
-        HIP_TRY(hipStreamSynchronize(h->stream));
-    }
-    h->m_in = m_out;
-    h->cur = nxt;
     h->round++;
     return PSIM_OK;
 }
@@ -473,6 +692,53 @@ void fill_stats(const uint64_t* s, uint64_t round, psim_round_stats* o) {
     o->dropped = s[ST_DROPPED]; o->nodes_up = s[ST_UP]; o->nodes_processed = s[ST_PROC];
     o->exits = s[ST_EXITS]; o->send_fail = s[ST_FAIL]; o->first_deliveries = s[ST_FIRST];
     o->overflow = s[ST_OVF]; o->digest = s[ST_DIGEST]; o->state_bytes = s[ST_BYTES];
+}
+
+int shard_alloc(psim_handle* h, Shard* s) {
+    HIP_TRY(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
+    for (int k = 0; k < KT_N; k++) {
+        HIP_TRY(hipEventCreate(&s->ev[k][0]));
+        HIP_TRY(hipEventCreate(&s->ev[k][1]));
+    }
+    s->ev_live = true;
+    const size_t N = h->N, n = std::max<uint32_t>(s->n, 1);
+    int rc = 0;
+    rc |= s->flags.alloc(N); rc |= s->part.alloc(N); rc |= s->hdr.alloc(n);
+    rc |= s->act.alloc(n * PSIM_ACTIVE_CAP); rc |= s->pas.alloc(n * PSIM_PASSIVE_CAP);
+    rc |= s->sentp.alloc(n * PSIM_IDMAP_CAP); rc |= s->senti.alloc(n * PSIM_IDMAP_CAP);
+    rc |= s->recvp.alloc(n * PSIM_IDMAP_CAP); rc |= s->recvi.alloc(n * PSIM_IDMAP_CAP);
+    rc |= s->pt_all.alloc(n * PSIM_PT_MEMBERS_CAP); rc |= s->pt_com.alloc(n * PSIM_PT_MEMBERS_CAP);
+    rc |= s->pt_eag.alloc(n * PSIM_PT_SET_CAP); rc |= s->pt_laz.alloc(n * PSIM_PT_SET_CAP);
+    rc |= s->pt_out.alloc(n * PSIM_PT_OUT_CAP); rc |= s->start.alloc(n);
+    rc |= s->ocnt.alloc(n); rc |= s->dpos.alloc(n); rc |= s->cnt.alloc(n); rc |= s->bsum.alloc(n);
+    rc |= s->in_beg.alloc(n); rc |= s->bound.alloc(n); rc |= s->obase.alloc(n);
+    rc |= s->work.alloc(n); rc |= s->alist.alloc(n); rc |= s->d_nact.alloc(1);
+    rc |= s->stat_out.alloc(NST);
+    rc |= s->ikeys.alloc(1024); rc |= s->ivals.alloc(1024);
+    rc |= s->rec[0].alloc(1024); rc |= s->rec[1].alloc(1024);
+    return rc ? PSIM_ENOMEM : PSIM_OK;
+}
+
+void shard_free(Shard* s) {
+    if (s->stream) (void)hipStreamSynchronize(s->stream);
+    s->flags.release(); s->part.release(); s->hdr.release();
+    s->act.release(); s->pas.release(); s->sentp.release(); s->senti.release();
+    s->recvp.release(); s->recvi.release(); s->pt_all.release(); s->pt_com.release();
+    s->pt_eag.release(); s->pt_laz.release(); s->pt_out.release(); s->start.release();
+    s->ikeys.release(); s->ivals.release(); s->rec[0].release(); s->rec[1].release();
+    s->outbox.release(); s->okey.release(); s->ocnt.release(); s->dpos.release();
+    s->keys.release(); s->vals.release(); s->owner.release(); s->owner_s.release();
+    s->vals_s.release(); s->cnt.release(); s->bsum.release(); s->in_beg.release();
+    s->work.release(); s->alist.release(); s->d_nact.release(); s->bound.release();
+    s->obase.release(); s->stat_part.release(); s->stat_out.release(); s->d_off.release();
+    s->cub_tmp.release(); s->ev_ids.release(); s->ev_contacts.release(); s->sendbuf.release();
+    if (s->ev_live)
+        for (int k = 0; k < KT_N; k++) {
+            (void)hipEventDestroy(s->ev[k][0]);
+            (void)hipEventDestroy(s->ev[k][1]);
+        }
+    if (s->stream) (void)hipStreamDestroy(s->stream);
+    delete s;
 }
 
 }  // namespace
@@ -508,6 +774,8 @@ void psim_default_config(psim_config* cfg) {
     cfg->device = -1; cfg->n_shards = 1; cfg->shard_world = 1;
 }
 
+void psim_destroy(psim_handle* h);
+
 int psim_create(const psim_config* cfg, psim_handle** out) {
     if (!cfg || !out || cfg->abi_version != PSIM_ABI_VERSION || cfg->n_nodes == 0 ||
         cfg->n_nodes > KEY_DST_MASK || cfg->max_active_size < 2 ||
@@ -515,53 +783,54 @@ int psim_create(const psim_config* cfg, psim_handle** out) {
         cfg->max_passive_size > 30 || 1 + cfg->k_active + cfg->k_passive > PSIM_EXCHANGE_CAP ||
         cfg->arwl > 255 || cfg->prwl > 255)
         return PSIM_EINVAL;
-    if (cfg->n_shards > 1 || cfg->shard_world > 1) return PSIM_EUNSUPPORTED;
+    uint32_t world = std::max<uint32_t>(cfg->shard_world, 1);
+    uint32_t local = std::max<uint32_t>(cfg->n_shards, 1);
+    if (world > 1 && (local != 1 || !cfg->comm_id || cfg->shard_rank >= world)) return PSIM_EINVAL;
+    uint32_t G = world > 1 ? world : local;
+    if (G > 64 || G > cfg->n_nodes) return PSIM_EINVAL;
     psim_handle* h = new (std::nothrow) psim_handle();
     if (!h) return PSIM_ENOMEM;
     h->cfg = *cfg;
     h->N = cfg->n_nodes;
+    h->G = G;
+    h->per = (h->N + G - 1) / G;
+    h->world = (int)world;
+    h->rank = (int)cfg->shard_rank;
     int dev = cfg->device;
-    if (dev < 0) { if (hipGetDevice(&dev) != hipSuccess) { delete h; return PSIM_EDEVICE; } }
+    if (dev < 0 && hipGetDevice(&dev) != hipSuccess) { delete h; return PSIM_EDEVICE; }
     if (hipSetDevice(dev) != hipSuccess) { delete h; return PSIM_EDEVICE; }
     h->device = dev;
-    if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) { delete h; return PSIM_EDEVICE; }
-    for (int k = 0; k < KT_N; k++) { hipEventCreate(&h->ev[k][0]); hipEventCreate(&h->ev[k][1]); }
-    const size_t N = h->N;
-    int rc = 0;
-    rc |= h->flags.alloc(N); rc |= h->part.alloc(N); rc |= h->hdr.alloc(N);
-    rc |= h->act.alloc(N * PSIM_ACTIVE_CAP); rc |= h->pas.alloc(N * PSIM_PASSIVE_CAP);
-    rc |= h->sentp.alloc(N * PSIM_IDMAP_CAP); rc |= h->senti.alloc(N * PSIM_IDMAP_CAP);
-    rc |= h->recvp.alloc(N * PSIM_IDMAP_CAP); rc |= h->recvi.alloc(N * PSIM_IDMAP_CAP);
-    rc |= h->pt_all.alloc(N * PSIM_PT_MEMBERS_CAP); rc |= h->pt_com.alloc(N * PSIM_PT_MEMBERS_CAP);
-    rc |= h->pt_eag.alloc(N * PSIM_PT_SET_CAP); rc |= h->pt_laz.alloc(N * PSIM_PT_SET_CAP);
-    rc |= h->pt_out.alloc(N * PSIM_PT_OUT_CAP);
-    rc |= h->ocnt.alloc(N); rc |= h->dpos.alloc(N); rc |= h->cnt.alloc(N); rc |= h->bsum.alloc(N);
-    rc |= h->in_beg.alloc(N); rc |= h->bound.alloc(N); rc |= h->obase.alloc(N);
-    rc |= h->start.alloc(N); rc |= h->work.alloc(N); rc |= h->alist.alloc(N); rc |= h->d_nact.alloc(1);
-    rc |= h->d_m.alloc(1); rc |= h->stat_out.alloc(NST);
-    rc |= h->keys[0].alloc(1024); rc |= h->vals[0].alloc(1024);
-    rc |= h->rec[0].alloc(1024);
-    if (rc) { psim_destroy(h); return PSIM_ENOMEM; }
+    for (uint32_t g = 0; g < G; g++) {
+        if (world > 1 && g != cfg->shard_rank) continue;
+        Shard* s = new (std::nothrow) Shard();
+        if (!s) { psim_destroy(h); return PSIM_ENOMEM; }
+        s->idx = g;
+        s->lo = std::min<uint32_t>(g * h->per, h->N);
+        s->n = std::min<uint32_t>(h->N, s->lo + h->per) - s->lo;
+        h->shards.push_back(s);
+        int rc = shard_alloc(h, s);
+        if (rc) { psim_destroy(h); return rc; }
+    }
+    if (world > 1) {
+        ncclUniqueId id;
+        memcpy(&id, cfg->comm_id, sizeof id);
+        if (ncclCommInitRank(&h->comm, (int)world, id, (int)cfg->shard_rank) != ncclSuccess) {
+            h->comm = nullptr;
+            psim_destroy(h);
+            return PSIM_ECOMM;
+        }
+    }
     *out = h;
     return PSIM_OK;
 }
 
 void psim_destroy(psim_handle* h) {
     if (!h) return;
-    hipSetDevice(h->device);
-    hipStreamSynchronize(h->stream);
-    h->flags.release(); h->part.release(); h->hdr.release();
-    h->act.release(); h->pas.release(); h->sentp.release(); h->senti.release();
-    h->recvp.release(); h->recvi.release(); h->pt_all.release(); h->pt_com.release();
-    h->pt_eag.release(); h->pt_laz.release(); h->pt_out.release();
-    for (int b = 0; b < 2; b++) { h->rec[b].release(); h->keys[b].release(); h->vals[b].release(); }
-    h->okey.release(); h->ocnt.release(); h->dpos.release(); h->cnt.release(); h->bsum.release();
-    h->in_beg.release(); h->bound.release(); h->obase.release(); h->d_m.release();
-    h->start.release(); h->work.release(); h->alist.release(); h->d_nact.release();
-    h->stat_part.release(); h->stat_out.release(); h->cub_tmp.release();
-    h->ev_ids.release(); h->ev_contacts.release();
-    for (int k = 0; k < KT_N; k++) { hipEventDestroy(h->ev[k][0]); hipEventDestroy(h->ev[k][1]); }
-    hipStreamDestroy(h->stream);
+    (void)hipSetDevice(h->device);
+    for (Shard* s : h->shards) shard_free(s);
+    h->shards.clear();
+    h->comm_cnt.release();
+    if (h->comm) ncclCommDestroy(h->comm);
     delete h;
 }
 
@@ -625,11 +894,7 @@ int psim_get_round(psim_handle* h, uint64_t* round) {
     return PSIM_OK;
 }
 
-int psim_get_nodes(psim_handle* h, uint32_t first, uint32_t count, psim_node_view* out) {
-    if (!h || (count && !out)) return PSIM_EINVAL;
-    if ((uint64_t)first + count > h->N) return PSIM_ERANGE;
-    if (!count) return PSIM_OK;
-    if (hipSetDevice(h->device) != hipSuccess) return PSIM_EDEVICE;
+static int get_shard_nodes(Shard* s, uint32_t first, uint32_t count, psim_node_view* out) {
     std::vector<Hdr> hd(count);
     std::vector<uint8_t> fl(count);
     std::vector<uint32_t> act((size_t)count * PSIM_ACTIVE_CAP), pas((size_t)count * PSIM_PASSIVE_CAP);
@@ -637,23 +902,24 @@ int psim_get_nodes(psim_handle* h, uint32_t first, uint32_t count, psim_node_vie
     std::vector<uint32_t> all((size_t)count * PSIM_PT_MEMBERS_CAP), com(all.size());
     std::vector<uint32_t> eag((size_t)count * PSIM_PT_SET_CAP), laz(eag.size());
     std::vector<uint64_t> po((size_t)count * PSIM_PT_OUT_CAP);
+    const size_t li = first - s->lo;
     auto cp = [&](void* dst, const void* src, size_t bytes) {
-        return hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, h->stream);
+        return hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, s->stream);
     };
-    HIP_TRY(cp(hd.data(), h->hdr.p + first, count * sizeof(Hdr)));
-    HIP_TRY(cp(fl.data(), h->flags.p + first, count));
-    HIP_TRY(cp(act.data(), h->act.p + (size_t)first * PSIM_ACTIVE_CAP, act.size() * 4));
-    HIP_TRY(cp(pas.data(), h->pas.p + (size_t)first * PSIM_PASSIVE_CAP, pas.size() * 4));
-    HIP_TRY(cp(sp.data(), h->sentp.p + (size_t)first * PSIM_IDMAP_CAP, sp.size() * 4));
-    HIP_TRY(cp(si.data(), h->senti.p + (size_t)first * PSIM_IDMAP_CAP, si.size() * 4));
-    HIP_TRY(cp(rp.data(), h->recvp.p + (size_t)first * PSIM_IDMAP_CAP, rp.size() * 4));
-    HIP_TRY(cp(ri.data(), h->recvi.p + (size_t)first * PSIM_IDMAP_CAP, ri.size() * 4));
-    HIP_TRY(cp(all.data(), h->pt_all.p + (size_t)first * PSIM_PT_MEMBERS_CAP, all.size() * 4));
-    HIP_TRY(cp(com.data(), h->pt_com.p + (size_t)first * PSIM_PT_MEMBERS_CAP, com.size() * 4));
-    HIP_TRY(cp(eag.data(), h->pt_eag.p + (size_t)first * PSIM_PT_SET_CAP, eag.size() * 4));
-    HIP_TRY(cp(laz.data(), h->pt_laz.p + (size_t)first * PSIM_PT_SET_CAP, laz.size() * 4));
-    HIP_TRY(cp(po.data(), h->pt_out.p + (size_t)first * PSIM_PT_OUT_CAP, po.size() * 8));
-    HIP_TRY(hipStreamSynchronize(h->stream));
+    HIP_TRY(cp(hd.data(), s->hdr.p + li, count * sizeof(Hdr)));
+    HIP_TRY(cp(fl.data(), s->flags.p + first, count));
+    HIP_TRY(cp(act.data(), s->act.p + li * PSIM_ACTIVE_CAP, act.size() * 4));
+    HIP_TRY(cp(pas.data(), s->pas.p + li * PSIM_PASSIVE_CAP, pas.size() * 4));
+    HIP_TRY(cp(sp.data(), s->sentp.p + li * PSIM_IDMAP_CAP, sp.size() * 4));
+    HIP_TRY(cp(si.data(), s->senti.p + li * PSIM_IDMAP_CAP, si.size() * 4));
+    HIP_TRY(cp(rp.data(), s->recvp.p + li * PSIM_IDMAP_CAP, rp.size() * 4));
+    HIP_TRY(cp(ri.data(), s->recvi.p + li * PSIM_IDMAP_CAP, ri.size() * 4));
+    HIP_TRY(cp(all.data(), s->pt_all.p + li * PSIM_PT_MEMBERS_CAP, all.size() * 4));
+    HIP_TRY(cp(com.data(), s->pt_com.p + li * PSIM_PT_MEMBERS_CAP, com.size() * 4));
+    HIP_TRY(cp(eag.data(), s->pt_eag.p + li * PSIM_PT_SET_CAP, eag.size() * 4));
+    HIP_TRY(cp(laz.data(), s->pt_laz.p + li * PSIM_PT_SET_CAP, laz.size() * 4));
+    HIP_TRY(cp(po.data(), s->pt_out.p + li * PSIM_PT_OUT_CAP, po.size() * 8));
+    HIP_TRY(hipStreamSynchronize(s->stream));
     for (uint32_t k = 0; k < count; k++) {
         psim_node_view* v = &out[k];
         const Hdr& x = hd[k];
@@ -685,6 +951,26 @@ int psim_get_nodes(psim_handle* h, uint32_t first, uint32_t count, psim_node_vie
     return PSIM_OK;
 }
 
+// nodes [first, first+count): every node must be owned by a shard of this process
+int psim_get_nodes(psim_handle* h, uint32_t first, uint32_t count, psim_node_view* out) {
+    if (!h || (count && !out)) return PSIM_EINVAL;
+    if ((uint64_t)first + count > h->N) return PSIM_ERANGE;
+    if (hipSetDevice(h->device) != hipSuccess) return PSIM_EDEVICE;
+    uint32_t done = 0;
+    while (done < count) {
+        uint32_t id = first + done;
+        Shard* s = nullptr;
+        for (Shard* c : h->shards)
+            if (id >= c->lo && id < c->lo + c->n) s = c;
+        if (!s) return PSIM_ERANGE;
+        uint32_t k = std::min<uint32_t>(count - done, s->lo + s->n - id);
+        int rc = get_shard_nodes(s, id, k, out + done);
+        if (rc) return rc;
+        done += k;
+    }
+    return PSIM_OK;
+}
+
 int psim_kernel_times(psim_handle* h, const char** names, double* ms, uint64_t* launches, int cap) {
     if (!h) return PSIM_EINVAL;
     int k = 0;
@@ -696,11 +982,14 @@ int psim_kernel_times(psim_handle* h, const char** names, double* ms, uint64_t* 
     return k;
 }
 
-int psim_comm_id_size(void) { return 128; }
+int psim_comm_id_size(void) { return (int)sizeof(ncclUniqueId); }
 
 int psim_get_comm_id(void* buf, size_t cap) {
-    (void)buf; (void)cap;
-    return PSIM_EUNSUPPORTED;
+    if (!buf || cap < sizeof(ncclUniqueId)) return PSIM_EINVAL;
+    ncclUniqueId id;
+    if (ncclGetUniqueId(&id) != ncclSuccess) return PSIM_ECOMM;
+    memcpy(buf, &id, sizeof id);
+    return PSIM_OK;
 }
 
 }  // extern "C"

@@ -7,12 +7,14 @@ namespace psim {
 struct RoundArgs {
     // config
     uint32_t n_nodes, round;
+    uint32_t lo, n_local;       // this shard owns global ids [lo, lo + n_local)
     uint64_t seed;
     uint32_t max_active, min_active, max_passive, arwl, prwl, k_active, k_passive;
     uint32_t shuffle_period, promotion_period, random_promotion, plumtree, lazy_tick_period;
     // per-round scalars
     uint32_t crash_round, origin_now, origin_node, origin_msg, tracked_msg, bcast_root;
-    // node state (SoA rows)
+    // node state: flags/part are replicated and indexed by global id;
+    // every other row is local (index = id - lo)
     uint8_t* flags;
     const uint8_t* part;
     Hdr* hdr;

@@ -144,10 +144,28 @@ class _Driver:
         return [int(x) for x in v["pas"][: v["pas_n"]]]
 
 
-class Simulator(_Driver):
-    """MI355X simulator handle (HIP library; fails loudly without it)."""
+def comm_id():
+    """A fresh RCCL unique id (rank 0 creates it and shares the bytes)."""
+    from . import _lib
 
-    def __init__(self, cfg=None, **kw):
+    lib = _lib.load()
+    extra = _abi.bind(lib, "psim_", _abi.GPU_ONLY)
+    n = extra["comm_id_size"]()
+    buf = C.create_string_buffer(n)
+    rc = extra["get_comm_id"](buf, n)
+    if rc != 0:
+        raise SimError(f"get_comm_id: {extra['strerror'](rc).decode()}")
+    return buf.raw
+
+
+class Simulator(_Driver):
+    """MI355X simulator handle (HIP library; fails loudly without it).
+
+    Multi-GPU: one process per GPU, all with the same global n_nodes and
+    `shard_world`, each with its `shard_rank` and the same `comm` bytes from
+    comm_id() on rank 0; every rank then issues the same event calls."""
+
+    def __init__(self, cfg=None, comm=None, **kw):
         from . import _lib
 
         lib = _lib.load()
@@ -156,6 +174,9 @@ class Simulator(_Driver):
         self._extra = extra
         if cfg is None:
             cfg = default_config(**kw)
+        if comm is not None:
+            self._comm_buf = C.create_string_buffer(bytes(comm), len(comm))
+            cfg.comm_id = C.cast(self._comm_buf, C.c_void_p)
         super().__init__(api, cfg, errname=extra["strerror"])
 
     def kernel_times(self):
@@ -167,4 +188,4 @@ class Simulator(_Driver):
         return {names[i].decode(): (ms[i], launches[i]) for i in range(k)}
 
 
-__all__ = ["Simulator", "SimError", "default_config", "NONE"]
+__all__ = ["Simulator", "SimError", "default_config", "comm_id", "NONE"]

@@ -93,3 +93,34 @@ def test_large_properties():
     assert np.array_equal(em, dl)
     assert allst["overflow"].sum() == 0
     assert int(allst["first_deliveries"].sum()) == int(((v["have"] >> 5) & 1).sum()) - 1
+
+
+@pytest.mark.parametrize("shards", [2, 3, 8])
+def test_shard_count_invariance(shards):
+    """Node-range sharding (virtual shards on one GPU, exchanged by device
+    copies through the same partition/exchange/merge path the RCCL ranks
+    use) is bit-identical to the unsharded run and to the oracle."""
+    def gpu_sharded(cfg):
+        cfg.n_shards = shards
+        return _gpu(cfg)
+    gs, gst = S.churn_partition(gpu_sharded, n=2048)
+    os_, ost = S.churn_partition(Oracle, n=2048)
+    S.compare_stats(gst, ost)
+    S.compare_nodes(gs.nodes(), os_.nodes())
+
+
+def test_shard_invariance_64k():
+    def run(make):
+        sim, st = S.doubling(make, 1 << 16, 21, 60)
+        sim.broadcast(0, 5)
+        return sim, np.concatenate([st, sim.step(30)])
+
+    def g1(cfg):
+        return _gpu(cfg)
+
+    def g4(cfg):
+        cfg.n_shards = 4
+        return _gpu(cfg)
+    (a, ast), (b, bst) = run(g1), run(g4)
+    S.compare_stats(ast, bst)
+    S.compare_nodes(a.nodes(), b.nodes())
