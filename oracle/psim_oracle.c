@@ -83,6 +83,7 @@ typedef struct msgvec { omsg *v; size_t n, cap; } msgvec;
 struct psim_handle {
     psim_config cfg;
     uint32_t N;
+    uint32_t lo, hi;                /* owned id range (sharded protocol) */
     node *nodes;
     uint8_t *part, *crashed_now;
     uint64_t round;
@@ -820,11 +821,13 @@ static int cmp_dst(const void *a, const void *b) {
     return x->seq < y->seq ? -1 : x->seq > y->seq;
 }
 
-static void run_round(struct psim_handle *h, psim_round_stats *st) {
+/* Round, first half: events (applied to every node: up/partition state is
+ * replicated on every shard) and the handlers of the owned nodes; the
+ * round's emissions are left in h->out in (src, seq) order. */
+static void round_begin(struct psim_handle *h, psim_round_stats *st) {
     memset(st, 0, sizeof *st);
     st->round = h->round;
     h->st = st;
-    /* events */
     for (size_t i = 0; i < h->pend_crash_n; i++) {
         uint32_t n = h->pend_crash[i];
         if (h->nodes[n].up) { h->nodes[n].up = 0; h->crashed_now[n] = 1; }
@@ -849,7 +852,7 @@ static void run_round(struct psim_handle *h, psim_round_stats *st) {
     h->pend_bcast = 0;
 
     h->out.n = 0;
-    for (uint32_t n = 0; n < h->N; n++) {
+    for (uint32_t n = h->lo; n < h->hi; n++) {
         if (h->nodes[n].up) {
             st->nodes_up++;
             process_node(h, n);
@@ -858,15 +861,26 @@ static void run_round(struct psim_handle *h, psim_round_stats *st) {
         }
     }
     memset(h->crashed_now, 0, h->N);
-    /* deliver: messages emitted in round r form the canonical inbox of r+1 */
-    qsort(h->out.v, h->out.n, sizeof(omsg), cmp_dst);
-    msgvec t = h->inbox; h->inbox = h->out; h->out = t;
+}
+
+/* Round, second half: the messages addressed to the owned nodes (from every
+ * shard) become the canonical inbox of round r+1, sorted by (dst, src, seq). */
+static void round_end(struct psim_handle *h, msgvec *in) {
+    qsort(in->v, in->n, sizeof(omsg), cmp_dst);
+    if (in != &h->inbox) {
+        msgvec t = h->inbox; h->inbox = *in; *in = t;
+    }
     size_t j = 0;
     for (uint32_t n = 0; n <= h->N; n++) {
         while (j < h->inbox.n && h->inbox.v[j].dst < n) j++;
         h->in_beg[n] = j;
     }
     h->round++;
+}
+
+static void run_round(struct psim_handle *h, psim_round_stats *st) {
+    round_begin(h, st);
+    round_end(h, &h->out);
 }
 
 /* ------------------------------------------------------------- ABI -- */
@@ -893,6 +907,13 @@ int orc_create(const psim_config *cfg, struct psim_handle **out) {
     if (!h) return PSIM_ENOMEM;
     h->cfg = *cfg;
     h->N = cfg->n_nodes;
+    h->lo = 0; h->hi = h->N;
+    if (cfg->shard_world > 1) {
+        if (cfg->shard_rank >= cfg->shard_world || cfg->shard_world > h->N) { free(h); return PSIM_EINVAL; }
+        uint32_t per = (h->N + cfg->shard_world - 1) / cfg->shard_world;
+        h->lo = cfg->shard_rank * per < h->N ? cfg->shard_rank * per : h->N;
+        h->hi = h->lo + per < h->N ? h->lo + per : h->N;
+    }
     h->nodes = (node *)calloc(h->N, sizeof(node));
     h->part = (uint8_t *)calloc(h->N, 1);
     h->crashed_now = (uint8_t *)calloc(h->N, 1);
@@ -1013,3 +1034,44 @@ void orc_philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0,
     philox(c0, c1, c2, c3, k0, k1, out);
 }
 uint32_t orc_bucket16(uint32_t id) { return bucket16(id); }
+
+/* ---------------------------------------------- sharded protocol (tests) --
+ * One oracle per rank owns [lo, hi); a round is orc_round_emit (events +
+ * owned handlers; the emissions are read with orc_get_outbox in (src, seq)
+ * order, packed like orc_get_inbox), the host exchanges messages by owner,
+ * then orc_round_absorb with every message addressed to the owned range. */
+static void pack(const omsg *m, uint32_t *o) {
+    o[0] = m->dst; o[1] = m->src; o[2] = m->seq; o[3] = m->type | (m->ttl << 8) | (m->nex << 16);
+    o[4] = m->a0; o[5] = m->a1; o[6] = m->a2; o[7] = 0;
+    for (int k = 0; k < 8; k++) o[8 + k] = k < (int)m->nex ? m->ex[k] : 0;
+}
+
+int orc_round_emit(struct psim_handle *h, psim_round_stats *st) {
+    round_begin(h, st);
+    return PSIM_OK;
+}
+
+int orc_get_outbox(struct psim_handle *h, uint32_t *out, size_t cap, size_t *n) {
+    *n = h->out.n;
+    if (!out) return PSIM_OK;
+    for (size_t i = 0; i < h->out.n && i < cap; i++) pack(&h->out.v[i], out + i * 16);
+    return PSIM_OK;
+}
+
+int orc_round_absorb(struct psim_handle *h, const uint32_t *recs, size_t n) {
+    msgvec in = {0, 0, 0};
+    for (size_t i = 0; i < n; i++) {
+        const uint32_t *o = recs + i * 16;
+        omsg m;
+        memset(&m, 0, sizeof m);
+        m.dst = o[0]; m.src = o[1]; m.seq = o[2];
+        m.type = o[3] & 0xFF; m.ttl = (o[3] >> 8) & 0xFF; m.nex = (o[3] >> 16) & 0xFF;
+        m.a0 = o[4]; m.a1 = o[5]; m.a2 = o[6];
+        for (int k = 0; k < 8; k++) m.ex[k] = o[8 + k];
+        if (m.dst < h->lo || m.dst >= h->hi) { free(in.v); return PSIM_ERANGE; }
+        vec_push(&in, &m);
+    }
+    round_end(h, &in);
+    free(in.v);
+    return PSIM_OK;
+}

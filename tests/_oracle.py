@@ -29,6 +29,12 @@ def load():
         _lib.orc_philox.argtypes = [C.c_uint32] * 6 + [C.POINTER(C.c_uint32)]
         _lib.orc_bucket16.restype = C.c_uint32
         _lib.orc_bucket16.argtypes = [C.c_uint32]
+        _lib.orc_round_emit.restype = C.c_int
+        _lib.orc_round_emit.argtypes = [C.c_void_p, C.c_void_p]
+        _lib.orc_get_outbox.restype = C.c_int
+        _lib.orc_get_outbox.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.POINTER(C.c_size_t)]
+        _lib.orc_round_absorb.restype = C.c_int
+        _lib.orc_round_absorb.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t]
     return _lib
 
 
@@ -45,4 +51,56 @@ class Oracle(_Driver):
         self._lib.orc_get_inbox(self._h, None, 0, C.byref(n))
         out = np.zeros((n.value, 16), np.uint32)
         self._lib.orc_get_inbox(self._h, out.ctypes.data, n.value, C.byref(n))
+        return out
+
+
+class ShardedOracle(Oracle):
+    """One rank of the sharded round protocol over a
+    torch.distributed process group: emit -> exchange by owner shard ->
+    absorb.  Stats of step() are summed over ranks; nodes() covers only the
+    owned range."""
+
+    def __init__(self, cfg, group=None):
+        import torch.distributed as dist
+
+        self._dist = dist
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self._group = group
+        cfg.shard_world, cfg.shard_rank = self.world, self.rank
+        super().__init__(cfg)
+        per = (cfg.n_nodes + self.world - 1) // self.world
+        self.lo, self.hi = self.rank * per, min(cfg.n_nodes, (self.rank + 1) * per)
+        self.per = per
+
+    def step(self, n_rounds=1):
+        import numpy as np
+        import torch
+
+        from partisan_amd import _abi
+
+        out = np.zeros(n_rounds, _abi.STATS_DTYPE)
+        for i in range(n_rounds):
+            st = np.zeros(1, _abi.STATS_DTYPE)
+            rc = self._lib.orc_round_emit(self._h, st.ctypes.data)
+            assert rc == 0
+            n = C.c_size_t()
+            self._lib.orc_get_outbox(self._h, None, 0, C.byref(n))
+            box = np.zeros((n.value, 16), np.uint32)
+            self._lib.orc_get_outbox(self._h, box.ctypes.data, n.value, C.byref(n))
+            owner = box[:, 0] // self.per
+            parts = [box[owner == g] for g in range(self.world)]   # keeps (src, seq) order
+            gathered = [None] * self.world
+            self._dist.all_gather_object(gathered, parts, group=self._group)
+            mine = np.concatenate([gathered[g][self.rank] for g in range(self.world)]
+                                  ).astype(np.uint32).reshape(-1, 16)
+            mine = np.ascontiguousarray(mine)
+            rc = self._lib.orc_round_absorb(self._h, mine.ctypes.data, mine.shape[0])
+            assert rc == 0
+            flat = st.view(np.uint64).astype(np.int64)
+            t = torch.from_numpy(flat.copy())
+            self._dist.all_reduce(t, group=self._group)
+            summed = t.numpy().astype(np.uint64)
+            summed[0] = st.view(np.uint64)[0]           # the round number is not summed
+            out[i] = summed.view(_abi.STATS_DTYPE)[0]
         return out
