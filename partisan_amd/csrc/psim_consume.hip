@@ -28,6 +28,20 @@ namespace psim {
 #define DEV __device__ __forceinline__
 
 constexpr int WAVES_PER_BLOCK = 4;
+
+// Diagnostic build only (-DPSIM_STAMPS): s_memtime between phase
+// boundaries, summed per phase over all waves (psim::debug_stamps).
+#ifdef PSIM_STAMPS
+__device__ unsigned long long g_stamps[32];
+#define STAMP(w, k)                                                                  \
+    do {                                                                             \
+        uint64_t t_ = __builtin_amdgcn_s_memtime();                                  \
+        if (lane_id() == 0) (w).stl[(k)] += t_ - (w).t_last;                         \
+        (w).t_last = t_;                                                             \
+    } while (0)
+#else
+#define STAMP(w, k) do { } while (0)
+#endif
 constexpr uint32_t NONE = PSIM_NONE;
 
 // ------------------------------------------------------------ wave ops --
@@ -100,25 +114,16 @@ DEV void view_add(uint32_t& V, uint32_t& n, uint32_t e) {
     vins(V, n, pos, e);
 }
 
-// ascending bitonic sort of lanes 0..31 (lanes 32..63 sort their own half)
-DEV uint32_t sort32(uint32_t v) {
-    uint32_t l = lane_id();
-#pragma unroll
-    for (uint32_t k = 2; k <= 32; k <<= 1) {
-#pragma unroll
-        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-            uint32_t p = (uint32_t)__shfl_xor((int)v, (int)j);
-            bool keep_min = ((l & j) == 0) == ((l & k) == 0);
-            v = keep_min ? min(v, p) : max(v, p);
-        }
-    }
-    return v;
-}
-
 // ------------------------------------------------------------ the wave --
 struct Wv {
     const RoundArgs* a;
     uint32_t* lds;       // 64 words of per-wave scratch
+    uint32_t* nlog;      // notify log: NLOG snapshots x 8 ids + NLOG counts
+    uint32_t nlog_n;
+#ifdef PSIM_STAMPS
+    uint64_t* stl;
+    uint64_t t_last;
+#endif
     uint64_t* st;        // block stats (LDS)
     uint32_t me, li, mypart, round;   // global id, local row index
     Hdr h;
@@ -129,6 +134,8 @@ struct Wv {
     bool maps, pt, maps_dirty, pt_dirty;
     uint64_t obase;
     uint32_t seq;
+    uint32_t CV, CF;     // connection cache: ids of Passive (lanes 0-31) and Active
+                         // (32-39) at node start; CF = flags | part << 8 of each
     uint64_t digest;     // per-lane partial: lane j sums the hashes of record word j
     uint32_t SC;         // per-lane stats counter: lane k counts stats slot k (< NST)
 };
@@ -152,15 +159,29 @@ DEV uint64_t compact64(Wv& w, uint64_t V, uint64_t keep) {
     return ((uint64_t)hi << 32) | lo;
 }
 
-// lists:usort of the first m lanes of E; returns count, E sorted/unique, rest 0
-DEV uint32_t usort_lanes(Wv& w, uint32_t& E, uint32_t m) {
+// lists:usort of the lanes of E selected by `valid` (uniform mask, lists
+// of at most a few dozen entries): the first occurrence of each value is
+// kept and lands at its rank among the kept values.  Returns the count; E
+// holds the sorted unique values in lanes 0.., zeros above.
+DEV uint32_t usort_mask(Wv& w, uint32_t& E, uint64_t valid) {
     uint32_t l = lane_id();
-    uint32_t v = l < m ? E : 0xFFFFFFFFu;
-    v = sort32(v);
-    uint32_t prev = shfl(v, (int)((l + 63) & 63));
-    uint64_t keep = ballot(l < 32 && l < m && (l == 0 || v != prev));
-    E = compact(w, v, keep);
-    return popc(keep);
+    bool dup = false;
+    for (uint64_t m = valid; m; m &= m - 1) {             // drop later duplicates
+        int j = ffs64(m);
+        dup |= ((uint32_t)j < l) && rl(E, j) == E;
+    }
+    uint64_t keep = valid & ballot(!dup);
+    uint32_t rank = 0;
+    for (uint64_t m = keep; m; m &= m - 1) rank += rl(E, ffs64(m)) < E ? 1u : 0u;
+    if ((keep >> l) & 1ull) w.lds[rank] = E;
+    __builtin_amdgcn_wave_barrier();
+    uint32_t c = popc(keep);
+    E = l < c ? w.lds[l] : 0u;
+    __builtin_amdgcn_wave_barrier();
+    return c;
+}
+DEV uint32_t usort_lanes(Wv& w, uint32_t& E, uint32_t m) {
+    return usort_mask(w, E, m >= 64 ? ~0ull : ((1ull << m) - 1ull));
 }
 
 // ----------------------------------------------------------------- RNG --
@@ -181,13 +202,31 @@ DEV uint32_t mod58(uint64_t v, uint32_t n) {
     return ((hi % n) * p32 + lo % n) % n;
 }
 
+// v mod n for n in [1, 64]: Horner over 15-bit digits; each digit step
+// x = r * 2^15 + d < 2^21 divides by a v_rcp_f32 reciprocal, whose error
+// moves the truncated quotient by at most one, fixed by one correction.
+DEV uint32_t mod_small(uint64_t v, uint32_t n) {
+    const float rn = __builtin_amdgcn_rcpf((float)n);
+    uint32_t r = 0;
+#pragma unroll
+    for (int sh = 45; sh >= 0; sh -= 15) {
+        uint32_t x = (r << 15) | (uint32_t)((v >> sh) & 0x7FFFu);
+        uint32_t q = (uint32_t)((float)x * rn);
+        int32_t rr = (int32_t)(x - q * n);
+        rr = rr < 0 ? rr + (int32_t)n : rr;
+        rr = rr >= (int32_t)n ? rr - (int32_t)n : rr;
+        r = (uint32_t)rr;
+    }
+    return r;
+}
+
 // rand:uniform/1 with a 58-bit generator (OTP rand.erl ?uniform_range)
 DEV uint32_t uniform_n(Wv& w, uint32_t n) {
     const uint64_t two58 = 1ull << 58;
     for (;;) {
         uint64_t v = draw(w);
         if (v < n) return (uint32_t)v + 1;
-        uint64_t i = mod58(v, n);
+        uint64_t i = n <= 64 ? mod_small(v, n) : mod58(v, n);
         if (v - i <= two58 - n) return (uint32_t)i + 1;
     }
 }
@@ -200,8 +239,8 @@ DEV uint32_t select_random(Wv& w, uint32_t V, uint32_t n, uint32_t o0, uint32_t 
     uint32_t cnt = popc(M);
     if (cnt == 0) return NONE;
     uint32_t k = uniform_n(w, cnt) - 1;
-    for (uint32_t j = 0; j < k; j++) M &= M - 1;   // k-th set bit, on the SALU
-    return rl(V, ffs64(M));
+    // the k-th set bit of M: the lane in M with k members of M below it
+    return rl(V, ffs64(ballot(((M >> l) & 1ull) && popc(M & lt_mask()) == k)));
 }
 
 // lists:sublist(shuffle(to_list(View)), K) (hv:1359-1361, :1586-1587): one
@@ -254,9 +293,14 @@ DEV void emit(Wv& w, uint32_t dst, uint32_t type, uint32_t ttl, uint32_t a0, uin
 
 // maybe_connect + find (partisan_util.erl:75-134): the peer's manager runs
 // and no partition separates the two
+// F_UP and the partition of another node cannot change during k_consume,
+// so the cache filled at node start answers exactly for its members
 DEV bool connect_ok(const Wv& w, uint32_t dst) {
     if (dst >= w.a->n_nodes || dst == w.me) return false;
-    return (w.a->flags[dst] & F_UP) && w.a->part[dst] == w.mypart;
+    uint64_t m = ballot(w.CV == dst);
+    uint32_t v = m ? rl(w.CF, ffs64(m))
+                   : ((uint32_t)w.a->flags[dst] | ((uint32_t)w.a->part[dst] << 8));
+    return (v & F_UP) && (v >> 8) == w.mypart;
 }
 
 // do_send_message/3 (hv:1274-1343); success draws rand:uniform(1) in
@@ -371,11 +415,8 @@ DEV void merge_exchange(Wv& w, uint32_t EX, uint32_t nex) {
     uint32_t l = lane_id();
     bool in_act = false;
     for (uint32_t j = 0; j < w.act_n; j++) in_act |= (EX == rl(w.A, j));
-    uint32_t cand = (l < nex && EX != w.me && !in_act) ? EX : 0xFFFFFFFFu;
-    uint32_t T = cand;
-    uint32_t mt = usort_lanes(w, T, 32);
-    // drop the 0xFFFFFFFF filler that sorts last
-    if (mt && rl(T, mt - 1) == 0xFFFFFFFFu) mt--;
+    uint32_t T = EX;
+    uint32_t mt = usort_mask(w, T, ballot(l < nex && EX != w.me && !in_act));
     for (uint32_t i = 0; i < mt; i++) add_to_passive(w, rl(T, i));
 }
 
@@ -408,13 +449,12 @@ DEV void ord_add(Wv& w, uint32_t& V, uint32_t& n, uint32_t cap, uint32_t e) {
 
 // notify/1 (hv:1598-1599) -> plumtree update/1 -> handle_cast({update, ..})
 // (pt:314-336), reset_peers/4 (:652-659), neighbors_down/2 (:404-423)
-DEV void notify(Wv& w) {
-    if (!w.a->plumtree) return;
+DEV void apply_notify(Wv& w, uint32_t SNAP, uint32_t sn) {
     load_pt(w);
     w.pt_dirty = true;
     uint32_t l = lane_id();
-    uint32_t CUR = w.A;
-    uint32_t nc = usort_lanes(w, CUR, w.act_n);
+    uint32_t CUR = SNAP;
+    uint32_t nc = usort_lanes(w, CUR, sn);
     bool in_all = false;
     for (uint32_t j = 0; j < w.all_n; j++) in_all |= (CUR == rl(w.ALL, j));
     uint64_t newm = ballot(l < nc && !in_all);
@@ -453,6 +493,39 @@ DEV void notify(Wv& w) {
     }
 }
 
+// notify/1 only ever feeds Plumtree state, which nothing reads during the
+// HyParView phase, so each call logs the active view it would publish and the
+// log is replayed, in order, before the Plumtree phase (one inlined copy of
+// the update logic instead of one per call site).  A notify identical to the
+// previous one is a no-op (New and Removed are both empty) and is not logged.
+constexpr uint32_t NLOG = 16;
+DEV void replay_notifies(Wv& w) {
+    uint32_t l = lane_id();
+    for (uint32_t i = 0; i < w.nlog_n; i++) {
+        uint32_t V = l < PSIM_ACTIVE_CAP ? w.nlog[i * PSIM_ACTIVE_CAP + l] : 0u;
+        uint32_t n = w.nlog[NLOG * PSIM_ACTIVE_CAP + i];
+        __builtin_amdgcn_wave_barrier();
+        apply_notify(w, V, n);
+    }
+    w.nlog_n = 0;
+}
+DEV void notify(Wv& w) {
+    if (!w.a->plumtree) return;
+    uint32_t l = lane_id();
+    if (w.nlog_n) {
+        uint32_t k = w.nlog_n - 1;
+        uint32_t V = l < PSIM_ACTIVE_CAP ? w.nlog[k * PSIM_ACTIVE_CAP + l] : 0u;
+        uint32_t n = w.nlog[NLOG * PSIM_ACTIVE_CAP + k];
+        __builtin_amdgcn_wave_barrier();
+        if (n == w.act_n && !ballot(l < PSIM_ACTIVE_CAP && V != w.A)) return;
+    }
+    if (w.nlog_n == NLOG) replay_notifies(w);
+    if (l < PSIM_ACTIVE_CAP) w.nlog[w.nlog_n * PSIM_ACTIVE_CAP + l] = w.A;
+    if (l == 0) w.nlog[NLOG * PSIM_ACTIVE_CAP + w.nlog_n] = w.act_n;
+    __builtin_amdgcn_wave_barrier();
+    w.nlog_n++;
+}
+
 // update_peers/5 + set_peers/4 (pt:593-609) for the single root slot
 DEV void pt_update(Wv& w, uint32_t from, uint32_t root, bool to_eager) {
     w.pt_dirty = true;
@@ -475,8 +548,7 @@ DEV void pt_update(Wv& w, uint32_t from, uint32_t root, bool to_eager) {
 // send/3 (pt:633-638): only over an existing connection of the manager
 DEV void pt_send(Wv& w, uint32_t ident, uint32_t type, uint32_t msg, uint32_t rnd, uint32_t root) {
     uint32_t id = ident & ~PSIM_MAP_BIT;
-    if (id == w.me || !has(w.A, w.act_n, id) || !(w.a->flags[id] & F_UP) ||
-        w.a->part[id] != w.mypart) {
+    if (id == w.me || !has(w.A, w.act_n, id) || !connect_ok(w, id)) {
         st_add(w, ST_FAIL, 1);
         return;
     }
@@ -661,33 +733,66 @@ DEV bool timer_due(uint32_t period, uint32_t r, uint32_t start) {
     return period > 0 && r > start && ((r - start) % period) == 0;
 }
 
-// Inbox chunk c (messages c..c+3): lane l loads word l&15 of message
-// c + (l>>4), so one load instruction brings four 64-B records.  SL holds
-// the slots of messages [c & ~63, +64) one per lane.
-DEV uint32_t load_chunk(const RoundArgs& a, uint32_t ib, uint32_t ik, uint32_t c, uint32_t& SL) {
+// Inbox chunk c (messages c..c+3 of the node's dense run): lane l loads
+// word l&15 of message c + (l>>4), one 256-B load instruction per chunk.
+DEV uint32_t load_chunk(const RoundArgs& a, uint32_t ib, uint32_t ik, uint32_t c) {
     uint32_t l = lane_id();
-    if ((c & 63) == 0) SL = (c + l < ik) ? a.in_slot[ib + c + l] : 0u;
-    uint32_t j = (c & 63) + (l >> 4);
-    uint32_t slot = shfl(SL, (int)j);
-    return (c + (l >> 4) < ik) ? reinterpret_cast<const uint32_t*>(a.rec_in + slot)[l & 15] : 0u;
+    return (c + (l >> 4) < ik) ? reinterpret_cast<const uint32_t*>(a.rec_in + ib + c + (l >> 4))[l & 15]
+                               : 0u;
 }
 
-DEV void process(Wv& w, uint32_t n) {
+// Everything a node's processing reads first, loaded one node ahead: the
+// work descriptor (node, inbox begin, inbox count, outbox base) gives every
+// address, so the header, the views, the flag bytes and the first inbox
+// chunk are one round trip, issued while the previous node is processed.
+// Only vector loads (vmcnt, in order): a scalar load in flight would hold
+// up every LDS operation of the node being processed (lgkmcnt).
+struct NodeIn {
+    uint32_t n, ib, ik, ob;
+    uint32_t H;                 // header word l in lane l < 16
+    uint32_t A, P, R0;
+    uint32_t fl, part;
+};
+
+DEV uint32_t load_desc(const RoundArgs& a, uint32_t k) {
+    uint32_t l = lane_id();
+    return l < 4 ? reinterpret_cast<const uint32_t*>(a.desc + k)[l] : 0u;
+}
+
+DEV NodeIn load_node(const RoundArgs& a, uint32_t D) {
+    uint32_t l = lane_id();
+    NodeIn x;
+    x.n = rl(D, 0); x.ib = rl(D, 1); x.ik = rl(D, 2); x.ob = rl(D, 3);
+    const uint32_t li = x.n - a.lo;
+    x.H = l < 16 ? reinterpret_cast<const uint32_t*>(a.hdr + li)[l] : 0u;
+    x.A = l < PSIM_ACTIVE_CAP ? a.act[(size_t)li * PSIM_ACTIVE_CAP + l] : 0u;
+    x.P = l < PSIM_PASSIVE_CAP ? a.pas[(size_t)li * PSIM_PASSIVE_CAP + l] : 0u;
+    x.R0 = load_chunk(a, x.ib, x.ik, 0);
+    x.fl = a.flags[x.n];
+    x.part = a.part[x.n];
+    return x;
+}
+
+DEV void process(Wv& w, const NodeIn& x) {
     const RoundArgs& a = *w.a;
     const uint32_t r = a.round;
     uint32_t l = lane_id();
-    // issue every load of the node up front
+    const uint32_t n = x.n;
     const uint32_t li = n - a.lo;
     w.li = li;
-    uint32_t fl = a.flags[n];
-    uint32_t ik = a.in_cnt[li], ib = a.in_beg[li];
-    w.h = a.hdr[li];
-    w.A = l < PSIM_ACTIVE_CAP ? a.act[(size_t)li * PSIM_ACTIVE_CAP + l] : 0u;
-    w.P = l < PSIM_PASSIVE_CAP ? a.pas[(size_t)li * PSIM_PASSIVE_CAP + l] : 0u;
-    w.obase = a.obase[li];
-    w.mypart = a.part[n];
-    uint32_t SL = 0, R0 = 0;
-    if (ik) R0 = load_chunk(a, ib, ik, 0, SL);
+    uint32_t fl = x.fl;
+    uint32_t ik = x.ik;
+    const uint32_t ib = x.ib;
+    {
+        uint32_t* hw = reinterpret_cast<uint32_t*>(&w.h);
+#pragma unroll
+        for (int k = 0; k < 16; k++) hw[k] = rl(x.H, k);
+    }
+    w.A = x.A;
+    w.P = x.P;
+    w.obase = x.ob;
+    w.mypart = x.part;
+    const uint32_t R0 = x.R0;
     if (w.h.start_round == r && ik) {           // fresh incarnation: no connections yet
         st_add(w, ST_DROPPED, ik);
         ik = 0;
@@ -705,10 +810,17 @@ DEV void process(Wv& w, uint32_t n) {
         exits = ballot(dead);
     }
     bool promo_work = promo && w.act_n < a.min_active;
-    if (!(ik || joining || exits || promo_work || shuf || origin || lazy)) return;
+    if (!(ik || joining || exits || promo_work || shuf || origin || lazy)) { STAMP(w, 0); return; }
     st_add(w, ST_PROC, 1);
+    STAMP(w, 1);
 
     w.me = n;
+    {
+        uint32_t av = shfl(w.A, (int)((l - 32) & 63));
+        uint32_t cv = l < 32 ? (l < w.h.pas_n ? w.P : NONE) : (l - 32 < w.act_n ? av : NONE);
+        w.CV = cv;
+        w.CF = cv < a.n_nodes ? ((uint32_t)a.flags[cv] | ((uint32_t)a.part[cv] << 8)) : 0u;
+    }
     w.pas_n = w.h.pas_n; w.sent_n = w.h.sent_n; w.sent_head = w.h.sent_head;
     w.recv_n = w.h.recv_n; w.recv_head = w.h.recv_head;
     w.all_n = w.h.all_n; w.com_n = w.h.com_n; w.eag_n = w.h.eag_n; w.laz_n = w.h.laz_n;
@@ -718,6 +830,7 @@ DEV void process(Wv& w, uint32_t n) {
     w.SP = w.SI = w.RP = w.RI = 0;
     w.ALL = w.COM = w.EAG = w.LAZ = 0; w.OUT = 0;
     w.seq = 0;
+    w.nlog_n = 0;
 
     if (joining)                                      // hv:500-515
         hv_send(w, w.h.join_contact, PSIM_MSG_JOIN, 0, w.h.epoch, 0, 0, 0);
@@ -734,8 +847,9 @@ DEV void process(Wv& w, uint32_t n) {
         }
     }
 
+    STAMP(w, 2);
     for (uint32_t c = 0; c < ik; c += 4) {            // HyParView inbox, canonical order
-        uint32_t R4 = c == 0 ? R0 : load_chunk(a, ib, ik, c, SL);
+        uint32_t R4 = c == 0 ? R0 : load_chunk(a, ib, ik, c);
         uint32_t cm = ik - c < 4 ? ik - c : 4;
         for (uint32_t q = 0; q < cm; q++) {
             uint32_t b = q * 16;
@@ -745,12 +859,16 @@ DEV void process(Wv& w, uint32_t n) {
             uint32_t nex = (tt >> 16) & 0xFF;
             uint32_t ex = shfl(R4, (int)((b + 8 + l) & 63));
             ex = l < nex ? ex : 0u;
+            STAMP(w, 3);
             hv_handle(w, type, rl(R4, b + 1), (tt >> 8) & 0xFF, rl(R4, b + 4), rl(R4, b + 5), ex, nex);
+            STAMP(w, 4 + type);
         }
     }
 
+    STAMP(w, 3);
     if (promo && w.act_n < a.min_active)              // hv:542-561
         move_to_active(w, select_random(w, w.P, w.pas_n, n, n, n));
+    STAMP(w, 13);
     if (shuf) {                                       // hv:572-607
         uint32_t EX;
         uint32_t nex = build_exchange(w, EX);
@@ -758,18 +876,24 @@ DEV void process(Wv& w, uint32_t n) {
         if (t != NONE) hv_send(w, t, PSIM_MSG_SHUFFLE, a.arwl, 0, 0, EX, nex);
     }
 
+    STAMP(w, 14);
     if (a.plumtree) {
+        replay_notifies(w);
+        STAMP(w, 15);
         for (uint32_t c = 0; c < ik; c += 4) {        // Plumtree inbox
-            uint32_t R4 = c == 0 ? R0 : load_chunk(a, ib, ik, c, SL);
+            uint32_t R4 = c == 0 ? R0 : load_chunk(a, ib, ik, c);
             uint32_t cm = ik - c < 4 ? ik - c : 4;
             for (uint32_t q = 0; q < cm; q++) {
                 uint32_t b = q * 16;
                 uint32_t type = rl(R4, b + 2) & 0xFF;
                 if (type < PSIM_MSG_PT_BROADCAST || type > PSIM_MSG_PT_GRAFT) continue;
                 st_add(w, ST_DELIV + type, 1);
+                STAMP(w, 3);
                 pt_handle(w, type, rl(R4, b + 1), rl(R4, b + 4), rl(R4, b + 5), rl(R4, b + 6));
+                STAMP(w, 16 + type - PSIM_MSG_PT_BROADCAST);
             }
         }
+        STAMP(w, 3);
         if (origin) {                                 // pt:282-287, backend:179-200
             load_pt(w);
             uint32_t my = n | PSIM_MAP_BIT;
@@ -778,6 +902,7 @@ DEV void process(Wv& w, uint32_t n) {
             w.h.trk_hop = 0;
             pt_push(w, a.origin_msg, 0, my, my);
         }
+        STAMP(w, 21);
         if (lazy_due && w.out_n > 0) {                // pt:341-345, :443-453
             load_pt(w);
             for (uint32_t i = 0; i < w.out_n; i++) {
@@ -788,6 +913,7 @@ DEV void process(Wv& w, uint32_t n) {
         }
     }
 
+    STAMP(w, 22);
     // ---- write back
     w.h.act_n = (uint8_t)w.act_n; w.h.pas_n = (uint8_t)w.pas_n;
     w.h.sent_n = (uint8_t)w.sent_n; w.h.sent_head = (uint8_t)w.sent_head;
@@ -826,11 +952,13 @@ DEV void process(Wv& w, uint32_t n) {
                                (w.act_n < a.min_active ? F_LOWACT : 0));
         if (nf != fl) a.flags[n] = nf;
     }
+    STAMP(w, 23);
 }
 
-__global__ void __launch_bounds__(256, 4) k_consume(RoundArgs args) {
+__global__ void __launch_bounds__(256, 3) k_consume(RoundArgs args) {
     __shared__ uint64_t sst[NST];
     __shared__ uint32_t scratch[WAVES_PER_BLOCK][64];
+    __shared__ uint32_t nlogs[WAVES_PER_BLOCK][NLOG * (PSIM_ACTIVE_CAP + 1)];
     for (int i = threadIdx.x; i < NST; i += blockDim.x) sst[i] = 0;
     __syncthreads();
 
@@ -840,12 +968,35 @@ __global__ void __launch_bounds__(256, 4) k_consume(RoundArgs args) {
     Wv w;
     w.a = &args;
     w.lds = scratch[wid];
+    w.nlog = nlogs[wid];
+#ifdef PSIM_STAMPS
+    __shared__ uint64_t stamps[WAVES_PER_BLOCK][32];
+    if ((threadIdx.x & 63) < 32) stamps[wid][threadIdx.x & 63] = 0;
+    w.stl = stamps[wid];
+    w.t_last = __builtin_amdgcn_s_memtime();
+#endif
     w.st = sst;
     w.round = args.round;
     w.SC = 0;
     w.digest = 0;
     const uint32_t na = *args.n_alist;
-    for (uint32_t i = gw; i < na; i += nw) process(w, args.alist[i]);
+    if (gw < na) {
+        // software pipeline: node i is processed while node i + nw's loads
+        // are in flight and node i + 2nw's descriptor is being fetched
+        const uint32_t last = na - 1;
+        NodeIn x0 = load_node(args, load_desc(args, gw));
+        uint32_t d1 = load_desc(args, min(gw + nw, last));
+        for (uint32_t i = gw; i < na; i += nw) {
+            NodeIn x1 = load_node(args, d1);
+            d1 = load_desc(args, min(i + 2 * nw, last));
+            STAMP(w, 24);
+            process(w, x0);
+            x0 = x1;
+        }
+    }
+#ifdef PSIM_STAMPS
+    if (lane_id() < 32) atomicAdd(&g_stamps[lane_id()], (unsigned long long)w.stl[lane_id()]);
+#endif
     // flush this wave's counters and digest partials into the block's LDS stats
     {
         uint32_t l = lane_id();
@@ -860,5 +1011,28 @@ __global__ void __launch_bounds__(256, 4) k_consume(RoundArgs args) {
     for (int i = threadIdx.x; i < NST; i += blockDim.x)
         args.stat_part[(size_t)blockIdx.x * NST + i] = sst[i];
 }
+
+// one wave-slot per resident wave: the grid strides over the active list
+// with no second generation of waves (a partial generation is a tail)
+uint32_t consume_grid() {
+    int dev = 0, nb = 0;
+    hipDeviceProp_t p;
+    if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&p, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_consume, WAVES_PER_BLOCK * 64, 0) != hipSuccess ||
+        nb <= 0)
+        return 1024;
+    return (uint32_t)nb * (uint32_t)p.multiProcessorCount;
+}
+
+#ifdef PSIM_STAMPS
+int debug_stamps(unsigned long long* out) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 32) != hipSuccess) return -1;
+    unsigned long long z[32] = {0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), z, sizeof z) != hipSuccess) return -1;
+    return 32;
+}
+#else
+int debug_stamps(unsigned long long*) { return 0; }
+#endif
 
 }  // namespace psim

@@ -186,6 +186,17 @@ __global__ void k_node_prep(RoundArgs a, const uint32_t* bsum, uint64_t* bound, 
     }
 }
 
+// work descriptors of the active list: every address k_consume needs first
+__global__ void k_desc(const uint32_t* __restrict__ alist, const uint32_t* __restrict__ nact,
+                       const uint32_t* __restrict__ in_beg, const uint32_t* __restrict__ cnt,
+                       const uint64_t* __restrict__ obase, uint32_t lo, uint4* __restrict__ desc) {
+    const uint32_t na = *nact;
+    for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < na; k += gridDim.x * blockDim.x) {
+        uint32_t n = alist[k], li = n - lo;
+        desc[k] = make_uint4(n, in_beg[li], cnt[li], (uint32_t)obase[li]);
+    }
+}
+
 // Dense (key, slot) pairs of this round's emissions, in node (= src, seq) order.
 __global__ void k_compact(const uint32_t* ocnt, const uint32_t* dpos, const uint64_t* obase,
                           const uint32_t* okey, uint32_t* keys, uint32_t* vals, uint32_t n) {
@@ -277,9 +288,10 @@ struct DBuf {
     void release() { if (p) (void)hipFree(p); p = nullptr; n = 0; }
 };
 
-enum Kern { KT_EVENTS, KT_PREPARE, KT_CONSUME, KT_SCAN, KT_COMPACT, KT_SORT, KT_EXCHANGE, KT_STATS, KT_N };
+enum Kern { KT_EVENTS, KT_PREPARE, KT_CONSUME, KT_SCAN, KT_COMPACT, KT_SORT, KT_EXCHANGE, KT_GATHER,
+            KT_STATS, KT_N };
 const char* kKernName[KT_N] = {"events", "prepare", "consume", "scan", "compact", "sort",
-                               "exchange", "stats"};
+                               "exchange", "gather", "stats"};
 
 inline uint32_t grid_for(uint64_t n) { return (uint32_t)std::max<uint64_t>(1, (n + BLK - 1) / BLK); }
 
@@ -301,12 +313,13 @@ struct Shard {
     // inbox of the next round: sorted (local dst | bound, record index) pairs
     DBuf<uint32_t> ikeys, ivals;
     uint32_t m_in = 0;
-    DBuf<Msg> rec[2];                   // records the inbox indexes (rec[cur])
-    uint32_t cur = 0;
-    DBuf<Msg> outbox;                   // G > 1 outbox (G == 1 writes rec[cur ^ 1])
+    DBuf<Msg> outbox;                   // this round's emissions (holes between node regions)
+    DBuf<Msg> recvbuf;                  // G > 1: received records, in source-shard order
+    DBuf<Msg> inbox;                    // next round's records, dense, in inbox order
     // per-round scratch
     DBuf<uint32_t> okey, ocnt, dpos, keys, vals, owner, owner_s, vals_s, cnt, bsum, in_beg, work,
         alist, d_nact;
+    DBuf<uint4> desc;
     DBuf<uint64_t> bound, obase, stat_part, stat_out, d_off;
     DBuf<uint8_t> cub_tmp;
     DBuf<uint32_t> ev_ids, ev_contacts;
@@ -324,6 +337,7 @@ struct psim_handle {
     psim_config cfg;
     uint32_t N = 0, G = 1, per = 0;
     int device = 0;
+    uint32_t consume_blocks = 1024;     // resident k_consume blocks on the device
     uint64_t round = 0;
     std::vector<Shard*> shards;         // shards owned by this process
     int rank = 0, world = 1;
@@ -458,7 +472,7 @@ int phase_events_prepare(psim_handle* h, Shard* s, const RoundCtl& ctl, RoundArg
         }
         a.in_cnt = s->cnt.p;
         s->pgrid = grid_for(n);
-        s->cgrid = std::min<uint32_t>(grid_for(n), 2048);
+        s->cgrid = std::min<uint32_t>(grid_for(n), h->consume_blocks);
         TRY(s->stat_part.ensure((size_t)(s->pgrid + s->cgrid) * NST));
         k_node_prep<<<s->pgrid, BLK, 0, s->stream>>>(a, s->bsum.p, s->bound.p, s->work.p, s->stat_part.p);
         {
@@ -474,15 +488,16 @@ int phase_events_prepare(psim_handle* h, Shard* s, const RoundCtl& ctl, RoundArg
         TRY(scan_excl(s, s->bound.p, s->obase.p, n));
         uint64_t total = read1(s, s->bound.p + (n - 1)) + read1(s, s->obase.p + (n - 1));
         if (total >= 0xFFFFFFFFull) return PSIM_ENOMEM;
-        if (h->G == 1) TRY(s->rec[s->cur ^ 1].ensure(total + 1));
-        else TRY(s->outbox.ensure(total + 1));
+        TRY(s->outbox.ensure(total + 1));
         TRY(s->okey.ensure(total + 1));
+        k_desc<<<std::min<uint32_t>(grid_for(n), 4096), BLK, 0, s->stream>>>(
+            s->alist.p, s->d_nact.p, s->in_beg.p, s->cnt.p, s->obase.p, s->lo, s->desc.p);
     }
-    a.in_beg = s->in_beg.p; a.in_slot = s->ivals.p;
-    a.alist = s->alist.p; a.n_alist = s->d_nact.p;
-    a.rec_in = s->rec[s->cur].p;
+    a.in_beg = s->in_beg.p;
+    a.desc = s->desc.p; a.n_alist = s->d_nact.p;
+    a.rec_in = s->inbox.p;
     a.obase = s->obase.p;
-    a.rec_out = h->G == 1 ? s->rec[s->cur ^ 1].p : s->outbox.p;
+    a.rec_out = s->outbox.p;
     a.okey = s->okey.p; a.ocnt = s->ocnt.p;
     a.stat_part = s->stat_part.p + (size_t)s->pgrid * NST;
     return PSIM_OK;
@@ -493,6 +508,17 @@ int phase_consume(psim_handle* h, Shard* s, const RoundArgs& a) {
     HIP_TRY(hipMemsetAsync(s->ocnt.p, 0, (size_t)s->n * 4, s->stream));
     k_consume<<<s->cgrid, BLK, 0, s->stream>>>(a);
     HIP_TRY(hipGetLastError());
+    return PSIM_OK;
+}
+
+// records of the sorted inbox, gathered dense in inbox order: k_consume
+// then reads each node's messages as one contiguous run
+int gather_inbox(psim_handle* h, Shard* s, const Msg* src) {
+    TRY(s->inbox.ensure((size_t)s->m_in + 1));
+    KTimer t(h, s, KT_GATHER);
+    if (s->m_in)
+        k_gather<<<grid_for((uint64_t)s->m_in * 4), BLK, 0, s->stream>>>(src, s->ivals.p, s->m_in,
+                                                                          s->inbox.p);
     return PSIM_OK;
 }
 
@@ -519,8 +545,7 @@ int phase_route_local(psim_handle* h, Shard* s) {
     KTimer t(h, s, KT_SORT);
     TRY(sort_pairs(s, s->keys.p, s->ikeys.p, s->vals.p, s->ivals.p, s->m_out, bits_for(s->n)));
     s->m_in = s->m_out;
-    s->cur ^= 1;
-    return PSIM_OK;
+    return gather_inbox(h, s, s->outbox.p);
 }
 
 // G > 1, sender side: stable partition by owner shard, records gathered
@@ -551,17 +576,15 @@ int phase_partition(psim_handle* h, Shard* s) {
 
 // G > 1, receiver side: route keys of the shard-ordered concatenation, stable sort by dst
 int phase_receive(psim_handle* h, Shard* s, uint32_t m) {
-    uint32_t nxt = s->cur ^ 1;
     TRY(s->keys.ensure(m + 1)); TRY(s->vals.ensure(m + 1));
     TRY(s->ikeys.ensure(m + 1)); TRY(s->ivals.ensure(m + 1));
     KTimer t(h, s, KT_SORT);
     if (m) {
-        k_rkeys<<<grid_for(m), BLK, 0, s->stream>>>(s->rec[nxt].p, m, s->lo, s->keys.p, s->vals.p);
+        k_rkeys<<<grid_for(m), BLK, 0, s->stream>>>(s->recvbuf.p, m, s->lo, s->keys.p, s->vals.p);
         TRY(sort_pairs(s, s->keys.p, s->ikeys.p, s->vals.p, s->ivals.p, m, bits_for(s->n)));
     }
     s->m_in = m;
-    s->cur = nxt;
-    return PSIM_OK;
+    return gather_inbox(h, s, s->recvbuf.p);
 }
 
 // virtual shards of this process: device copies between shard buffers
@@ -570,7 +593,7 @@ int exchange_local(psim_handle* h) {
     std::vector<uint64_t> m(G, 0);
     for (Shard* d : h->shards) {
         for (Shard* s : h->shards) m[d->idx] += s->scnt[d->idx];
-        TRY(d->rec[d->cur ^ 1].ensure(m[d->idx] + 1));
+        TRY(d->recvbuf.ensure(m[d->idx] + 1));
     }
     for (Shard* d : h->shards) {
         {
@@ -580,7 +603,7 @@ int exchange_local(psim_handle* h) {
                 Shard* s = h->shards[g];
                 uint64_t c = s->scnt[d->idx];
                 if (c)
-                    HIP_TRY(hipMemcpyAsync(d->rec[d->cur ^ 1].p + off, s->sendbuf.p + s->soff[d->idx],
+                    HIP_TRY(hipMemcpyAsync(d->recvbuf.p + off, s->sendbuf.p + s->soff[d->idx],
                                            c * sizeof(Msg), hipMemcpyDeviceToDevice, d->stream));
                 off += c;
             }
@@ -605,8 +628,8 @@ int exchange_rccl(psim_handle* h) {
         HIP_TRY(hipStreamSynchronize(s->stream));
         std::vector<uint64_t> roff(G);
         for (uint32_t g = 0; g < G; g++) { roff[g] = m; m += rcnt[g]; }
-        TRY(s->rec[s->cur ^ 1].ensure(m + 1));
-        Msg* rb = s->rec[s->cur ^ 1].p;
+        TRY(s->recvbuf.ensure(m + 1));
+        Msg* rb = s->recvbuf.p;
         NCCL_TRY(ncclGroupStart());
         for (uint32_t g = 0; g < G; g++) {
             if (g == s->idx) continue;
@@ -712,10 +735,10 @@ int shard_alloc(psim_handle* h, Shard* s) {
     rc |= s->pt_out.alloc(n * PSIM_PT_OUT_CAP); rc |= s->start.alloc(n);
     rc |= s->ocnt.alloc(n); rc |= s->dpos.alloc(n); rc |= s->cnt.alloc(n); rc |= s->bsum.alloc(n);
     rc |= s->in_beg.alloc(n); rc |= s->bound.alloc(n); rc |= s->obase.alloc(n);
-    rc |= s->work.alloc(n); rc |= s->alist.alloc(n); rc |= s->d_nact.alloc(1);
+    rc |= s->work.alloc(n); rc |= s->alist.alloc(n); rc |= s->desc.alloc(n); rc |= s->d_nact.alloc(1);
     rc |= s->stat_out.alloc(NST);
     rc |= s->ikeys.alloc(1024); rc |= s->ivals.alloc(1024);
-    rc |= s->rec[0].alloc(1024); rc |= s->rec[1].alloc(1024);
+    rc |= s->recvbuf.alloc(1024); rc |= s->inbox.alloc(1024); rc |= s->outbox.alloc(1024);
     return rc ? PSIM_ENOMEM : PSIM_OK;
 }
 
@@ -725,11 +748,11 @@ void shard_free(Shard* s) {
     s->act.release(); s->pas.release(); s->sentp.release(); s->senti.release();
     s->recvp.release(); s->recvi.release(); s->pt_all.release(); s->pt_com.release();
     s->pt_eag.release(); s->pt_laz.release(); s->pt_out.release(); s->start.release();
-    s->ikeys.release(); s->ivals.release(); s->rec[0].release(); s->rec[1].release();
+    s->ikeys.release(); s->ivals.release(); s->recvbuf.release(); s->inbox.release();
     s->outbox.release(); s->okey.release(); s->ocnt.release(); s->dpos.release();
     s->keys.release(); s->vals.release(); s->owner.release(); s->owner_s.release();
     s->vals_s.release(); s->cnt.release(); s->bsum.release(); s->in_beg.release();
-    s->work.release(); s->alist.release(); s->d_nact.release(); s->bound.release();
+    s->work.release(); s->alist.release(); s->desc.release(); s->d_nact.release(); s->bound.release();
     s->obase.release(); s->stat_part.release(); s->stat_out.release(); s->d_off.release();
     s->cub_tmp.release(); s->ev_ids.release(); s->ev_contacts.release(); s->sendbuf.release();
     if (s->ev_live)
@@ -799,6 +822,7 @@ int psim_create(const psim_config* cfg, psim_handle** out) {
     int dev = cfg->device;
     if (dev < 0 && hipGetDevice(&dev) != hipSuccess) { delete h; return PSIM_EDEVICE; }
     if (hipSetDevice(dev) != hipSuccess) { delete h; return PSIM_EDEVICE; }
+    h->consume_blocks = psim::consume_grid();
     h->device = dev;
     for (uint32_t g = 0; g < G; g++) {
         if (world > 1 && g != cfg->shard_rank) continue;
@@ -980,6 +1004,12 @@ int psim_kernel_times(psim_handle* h, const char** names, double* ms, uint64_t* 
         if (launches) launches[k] = h->kt_n[k];
     }
     return k;
+}
+
+// diagnostic: per-phase s_memtime sums of k_consume (zeros unless built with -DPSIM_STAMPS)
+int psim_debug_stamps(unsigned long long* out, int cap) {
+    if (!out || cap < 32) return PSIM_EINVAL;
+    return psim::debug_stamps(out);
 }
 
 int psim_comm_id_size(void) { return (int)sizeof(ncclUniqueId); }

@@ -25,10 +25,9 @@ struct RoundArgs {
     const uint32_t* in_beg;
     const uint32_t* in_cnt;
     const uint32_t* start;      // start round per node (timer phases)
-    const uint32_t* alist;      // nodes with work this round
+    const uint4* desc;          // per node with work: (id, inbox begin, inbox count, outbox base)
     const uint32_t* n_alist;
-    const uint32_t* in_slot;
-    const Msg* rec_in;
+    const Msg* rec_in;          // dense, in inbox order (node runs at in_beg)
     const uint64_t* obase;
     Msg* rec_out;
     uint32_t* okey;
@@ -37,5 +36,9 @@ struct RoundArgs {
 };
 
 __global__ void k_consume(RoundArgs args);
+// diagnostic builds (-DPSIM_STAMPS): per-phase cycle sums of k_consume, reset on read
+int debug_stamps(unsigned long long* out);
+// resident-block count of k_consume on the current device
+uint32_t consume_grid();
 
 }  // namespace psim
