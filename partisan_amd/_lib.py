@@ -4,7 +4,10 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "csrc", "libpartisan_gpu_sim.so")
+# PSIM_LIB=stamps selects the diagnostic build (profiles/stamps.py); it is the
+# same engine with per-phase s_memtime stamps compiled into k_consume
+_VARIANT = os.environ.get("PSIM_LIB", "")
+LIB_PATH = os.path.join(HERE, "csrc", "libpartisan_gpu_sim%s.so" % ("_" + _VARIANT if _VARIANT else ""))
 
 _lib = None
 

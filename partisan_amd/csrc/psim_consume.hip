@@ -28,6 +28,9 @@ namespace psim {
 #define DEV __device__ __forceinline__
 
 constexpr int WAVES_PER_BLOCK = 4;
+#ifndef PSIM_WAVES_PER_SIMD
+#define PSIM_WAVES_PER_SIMD 3
+#endif
 
 // Diagnostic build only (-DPSIM_STAMPS): s_memtime between phase
 // boundaries, summed per phase over all waves (psim::debug_stamps).
@@ -83,7 +86,7 @@ DEV void vdel(uint32_t& V, uint32_t& n, uint32_t k) {
 }
 DEV void vdel64(uint64_t& V, uint32_t& n, uint32_t k) {
     uint32_t l = lane_id();
-    uint64_t nx = shfl64(V, (int)((l + 1) & 63));
+    uint64_t nx = ((uint64_t)from_next((uint32_t)(V >> 32)) << 32) | from_next((uint32_t)V);
     V = l < k ? V : (l + 1 < n ? nx : 0ull);
     n--;
 }
@@ -96,7 +99,7 @@ DEV void vins(uint32_t& V, uint32_t& n, uint32_t pos, uint32_t e) {
 }
 DEV void vins64(uint64_t& V, uint32_t& n, uint32_t pos, uint64_t e) {
     uint32_t l = lane_id();
-    uint64_t pv = shfl64(V, (int)((l + 63) & 63));
+    uint64_t pv = ((uint64_t)from_prev((uint32_t)(V >> 32)) << 32) | from_prev((uint32_t)V);
     V = l < pos ? V : (l == pos ? e : (l <= n ? pv : 0ull));
     n++;
 }
@@ -138,7 +141,12 @@ struct Wv {
                          // (32-39) at node start; CF = flags | part << 8 of each
     uint64_t digest;     // per-lane partial: lane j sums the hashes of record word j
     uint32_t SC;         // per-lane stats counter: lane k counts stats slot k (< NST)
+    // draw cache: lane l holds the 58-bit draw of counter dc_base + l, filled
+    // by one VALU Philox for 64 counters at once (dc_base = NONE64: empty)
+    uint32_t DCL, DCH;
+    uint64_t dc_base;
 };
+constexpr uint64_t NONE64 = ~0ull;
 
 // stats: lane k of SC holds slot k's count for this wave; flushed once per wave
 DEV void st_add(Wv& w, int k, uint32_t v) { w.SC += lane_id() == (uint32_t)k ? v : 0u; }
@@ -185,14 +193,19 @@ DEV uint32_t usort_lanes(Wv& w, uint32_t& E, uint32_t m) {
 }
 
 // ----------------------------------------------------------------- RNG --
-// every single draw is wave-uniform: pin its inputs to scalar registers so
-// the Philox rounds run on the SALU
+// The node's draws are consecutive Philox counters, so a cache line of 64
+// of them costs one VALU Philox (every lane a counter) instead of 64 scalar
+// ones; select_random and sublist both read it.
+DEV void dc_fill(Wv& w, uint64_t base) {
+    uint64_t v = draw58_at(base + lane_id(), w.me, w.a->seed);
+    w.DCL = (uint32_t)v; w.DCH = (uint32_t)(v >> 32);
+    w.dc_base = base;
+}
 DEV uint64_t draw(Wv& w) {
     uint64_t c = w.h.rng++;
-    uint32_t o0, o1;
-    philox(uni((uint32_t)c), uni((uint32_t)(c >> 32)), uni(w.me), 0u, uni((uint32_t)w.a->seed),
-           uni((uint32_t)(w.a->seed >> 32)), o0, o1);
-    return ((((uint64_t)uni(o1)) << 32) | uni(o0)) >> 6;
+    if (c < w.dc_base || c - w.dc_base >= 64) dc_fill(w, c);   // miss (or empty: NONE64)
+    uint32_t i = (uint32_t)(c - w.dc_base);
+    return ((uint64_t)rl(w.DCH, i) << 32) | rl(w.DCL, i);
 }
 
 // v mod n for n < 2^16 with 32-bit arithmetic: v = hi*2^32 + lo
@@ -244,30 +257,29 @@ DEV uint32_t select_random(Wv& w, uint32_t V, uint32_t n, uint32_t o0, uint32_t 
 }
 
 // lists:sublist(shuffle(to_list(View)), K) (hv:1359-1361, :1586-1587): one
-// rand:uniform() key per element (element l draws at rng + l), the K
-// smallest (key, element) pairs in order, appended to OUT at lanes on..
+// rand:uniform() key per element (element l draws counter rng + l); each lane
+// counts the (key, element) pairs below its own -- its position in the sorted
+// list -- and the first K positions are appended to OUT at lanes on..
 DEV uint32_t sublist(Wv& w, uint32_t V, uint32_t n, uint32_t k, uint32_t& OUT, uint32_t on) {
     uint32_t l = lane_id();
     uint64_t base = w.h.rng;
-    uint64_t key = l < n ? (draw58_at(base + l, w.me, w.a->seed) >> 5) : ~0ull;
+    if (base < w.dc_base || base + n - w.dc_base > 64) dc_fill(w, base);   // must cover [base, base + n)
+    uint32_t off = (uint32_t)(base - w.dc_base);
+    uint32_t src = (l + off) & 63;
+    uint32_t kl = shfl(w.DCL, (int)src), kh = shfl(w.DCH, (int)src);
+    uint64_t key = l < n ? ((((uint64_t)kh) << 32) | kl) >> 5 : ~0ull;
     uint32_t m = n < k ? n : k;
-    for (uint32_t j = 0; j < m; j++) {
-        uint64_t bk = key;
-        uint32_t be = V;
-#pragma unroll
-        for (int off = 16; off > 0; off >>= 1) {
-            uint64_t ok = ((uint64_t)(uint32_t)__shfl_xor((int)(bk >> 32), off) << 32) |
-                          (uint32_t)__shfl_xor((int)(uint32_t)bk, off);
-            uint32_t oe = (uint32_t)__shfl_xor((int)be, off);
-            bool take = ok < bk || (ok == bk && oe < be);
-            bk = take ? ok : bk;
-            be = take ? oe : be;
-        }
-        uint64_t wk = rl64(bk, 0);
-        uint32_t we = rl(be, 0);
-        OUT = l == on + j ? we : OUT;
-        key = (key == wk && V == we) ? ~0ull : key;
+    uint32_t rank = 0;
+    for (uint32_t j = 0; j < n; j++) {
+        uint64_t kj = rl64(key, j);
+        uint32_t ej = rl(V, j);
+        rank += (kj < key || (kj == key && ej < V)) ? 1u : 0u;
     }
+    if (l < n && rank < m) w.lds[rank] = V;
+    __builtin_amdgcn_wave_barrier();
+    uint32_t got = (l >= on && l < on + m) ? w.lds[(l - on) & 63] : 0u;
+    __builtin_amdgcn_wave_barrier();
+    OUT = (l >= on && l < on + m) ? got : OUT;
     w.h.rng = base + n;
     return on + m;
 }
@@ -279,7 +291,7 @@ DEV void emit(Wv& w, uint32_t dst, uint32_t type, uint32_t ttl, uint32_t a0, uin
     uint32_t s = w.seq++;
     uint64_t slot = w.obase + s;
     uint32_t tt = type | (ttl << 8) | (nex << 16);
-    uint32_t exv = shfl(EX, (int)((l - 8) & 63));
+    uint32_t exv = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)EX, 0x118, 0xF, 0xF, true);
     uint32_t word = l == 0 ? dst : l == 1 ? w.me : l == 2 ? tt : l == 3 ? s : l == 4 ? a0
                   : l == 5 ? a1 : l == 6 ? a2 : l == 7 ? 0u : (l - 8 < nex ? exv : 0u);
     if (l < 16) {
@@ -831,6 +843,7 @@ DEV void process(Wv& w, const NodeIn& x) {
     w.ALL = w.COM = w.EAG = w.LAZ = 0; w.OUT = 0;
     w.seq = 0;
     w.nlog_n = 0;
+    w.dc_base = NONE64;                                // the cache holds another node's stream
 
     if (joining)                                      // hv:500-515
         hv_send(w, w.h.join_contact, PSIM_MSG_JOIN, 0, w.h.epoch, 0, 0, 0);
@@ -955,7 +968,7 @@ DEV void process(Wv& w, const NodeIn& x) {
     STAMP(w, 23);
 }
 
-__global__ void __launch_bounds__(256, 3) k_consume(RoundArgs args) {
+__global__ void __launch_bounds__(256, PSIM_WAVES_PER_SIMD) k_consume(RoundArgs args) {
     __shared__ uint64_t sst[NST];
     __shared__ uint32_t scratch[WAVES_PER_BLOCK][64];
     __shared__ uint32_t nlogs[WAVES_PER_BLOCK][NLOG * (PSIM_ACTIVE_CAP + 1)];
