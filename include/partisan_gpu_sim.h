@@ -34,6 +34,16 @@
  *       debug getters active/0, passive/0 (hyparview:261-281),
  *       plumtree debug_get_peers/2,3 (:222-231), broadcast_members/0 (:188-195)
  *
+ * With cfg.manager = PSIM_MANAGER_PLUGGABLE a handle simulates
+ * partisan_pluggable_peer_service_manager driving one membership strategy
+ * (partisan_membership_strategy.erl:32-36) instead:
+ *   psim_join    internal_join/3 + the hello/state handshake + Strategy:join/3
+ *                (pluggable:1423-1458, :986-1044; server:125-148)
+ *   psim_step    Strategy:handle_message/2 per inbox message (pluggable:1153-1195)
+ *                and Strategy:periodic/1 (pluggable:881-903)
+ *   psim_get_strategy_nodes / psim_get_member_bits
+ *                get_local_state/0 (pluggable:625-626), members/0 (:618-620)
+ *
  * Conventions: every function returns 0 on success or a negative PSIM_E*
  * code; psim_strerror() names it.  No exceptions or aborts cross the ABI.
  * A handle is thread-compatible (not thread-safe): the NIF shim serialises
@@ -50,7 +60,7 @@
 extern "C" {
 #endif
 
-#define PSIM_ABI_VERSION 1
+#define PSIM_ABI_VERSION 2
 
 /* error codes */
 #define PSIM_OK 0
@@ -80,6 +90,25 @@ enum psim_msg_type {
     PSIM_MSG_PT_GRAFT = 13,         /* {graft, Id, Mod, Round, Root, From}       plumtree:308  */
     PSIM_MSG_NTYPES = 16
 };
+
+/* message types of a PLUGGABLE handle (same record and stats slots) */
+enum psim_pl_msg_type {
+    PSIM_PL_HELLO = 0,     /* client hello on connect             peer_service_client:246-260 */
+    PSIM_PL_STATE = 1,     /* server reply {state, Tag, LocalState}  peer_service_server:125-148 */
+    PSIM_PL_GOSSIP = 2,    /* full: {membership_strategy, {Myself, State}}   full:127-144 */
+    PSIM_PL_FWD_SUB = 3,   /* scamp: {forward_subscription, Node}  scamp_v1:212-252, v2:284-327 */
+    PSIM_PL_PING = 4,      /* scamp: {ping, SourceNode}           scamp_v1:177-188, v2:181-191 */
+    PSIM_PL_KEEP_SUB = 5   /* scamp v2: {keep_subscription, Node}  scamp_v2:328-338 */
+};
+
+/* cfg.manager */
+#define PSIM_MANAGER_HYPARVIEW 0   /* partisan_hyparview_peer_service_manager (+ Plumtree) */
+#define PSIM_MANAGER_PLUGGABLE 1   /* partisan_pluggable_peer_service_manager + cfg.strategy */
+/* cfg.strategy (PLUGGABLE) */
+#define PSIM_STRATEGY_FULL 0       /* partisan_full_membership_strategy */
+#define PSIM_STRATEGY_SCAMP_V1 1   /* partisan_scamp_v1_membership_strategy */
+#define PSIM_STRATEGY_SCAMP_V2 2   /* partisan_scamp_v2_membership_strategy */
+#define PSIM_SVIEW_CAP 64          /* SCAMP membership / partial_view / in_view slots */
 
 /* Plumtree peer identities: an atom name is the bare node id; a node_spec
  * map (myself(), From, Root) has this bit set.  Erlang term order puts every
@@ -123,7 +152,14 @@ typedef struct psim_config {
     uint32_t shard_world;        /* RCCL world size, 1 */
     const void *comm_id;         /* ncclUniqueId bytes when shard_world > 1, else NULL */
     uint64_t max_msgs_per_round; /* 0 = auto */
-    uint32_t reserved[8];
+    /* pluggable manager */
+    uint32_t manager;            /* PSIM_MANAGER_*, 0 = HyParView */
+    uint32_t strategy;           /* PSIM_STRATEGY_* when manager = PLUGGABLE */
+    uint32_t periodic_interval;  /* rounds; periodic_interval 10000 ms (partisan_config.erl:130) */
+    uint32_t scamp_c;            /* scamp_c, ?SCAMP_C_VALUE = 5 (partisan.hrl:31) */
+    uint32_t fanout;             /* full: 0 = gossip to every member (reference);
+                                    k > 0 = k uniformly drawn members (config B extension) */
+    uint32_t reserved[3];
 } psim_config;
 
 typedef struct psim_round_stats {
@@ -159,6 +195,20 @@ typedef struct psim_node_view {
     uint32_t have, trk_round, trk_hop, pad1;
 } psim_node_view;
 
+/* Per-node state of a PLUGGABLE handle (inspection; unused slots zero). */
+typedef struct psim_strategy_view {
+    uint32_t up, start_round;
+    uint32_t pending;                        /* contact of an unfinished join, PSIM_NONE */
+    uint32_t last_ping;                      /* scamp: round of the last ping, PSIM_NONE = undefined */
+    uint64_t rng_ctr;
+    uint32_t view_n, in_n;
+    uint32_t view[PSIM_SVIEW_CAP];           /* scamp v1 membership (sets:to_list order) /
+                                                scamp v2 partial_view (list order) */
+    uint32_t in_view[PSIM_SVIEW_CAP];        /* scamp v2 in_view (list order) */
+    uint32_t members, pad;                   /* full: size of query(ORSet) */
+    uint64_t members_hash;                   /* full: sum of mix64(id + 1) over members */
+} psim_strategy_view;
+
 typedef struct psim_handle psim_handle;
 
 void psim_default_config(psim_config *cfg);
@@ -180,6 +230,10 @@ int psim_step(psim_handle *h, uint32_t n_rounds, psim_round_stats *stats);
 /* Inspection: views of nodes [first, first+count) into caller buffers. */
 int psim_get_nodes(psim_handle *h, uint32_t first, uint32_t count, psim_node_view *out);
 int psim_get_round(psim_handle *h, uint64_t *round);
+/* PLUGGABLE handles: strategy state of nodes [first, first+count) */
+int psim_get_strategy_nodes(psim_handle *h, uint32_t first, uint32_t count, psim_strategy_view *out);
+/* full strategy: the member bitset of one node (bit j of word j/32 = node j) */
+int psim_get_member_bits(psim_handle *h, uint32_t node, uint32_t *words, size_t n_words);
 /* Per-kernel device time (ms) accumulated over the last psim_step call:
  * names[i] is a static string; returns the number of entries. */
 int psim_kernel_times(psim_handle *h, const char **names, double *ms, uint64_t *launches, int cap);

@@ -76,7 +76,17 @@ typedef struct omsg {
     uint32_t type, ttl, nex;
     uint32_t a0, a1, a2;
     uint32_t ex[PSIM_EXCHANGE_CAP];
+    uint32_t slot;                  /* full strategy: payload snapshot (not part of the record digest) */
 } omsg;
+
+/* pluggable manager + membership strategy state of a node */
+typedef struct snode {
+    uint32_t started;               /* has ever been started (full: no restarts) */
+    uint32_t pending, hello_sent;   /* internal_join/3: Pending = [Contact] until the handshake */
+    uint32_t last_ping;             /* scamp last_message_time as a round, PSIM_NONE = undefined */
+    uint32_t view[PSIM_SVIEW_CAP], view_n;   /* scamp v1 membership / v2 partial_view */
+    uint32_t inv[PSIM_SVIEW_CAP], inv_n;     /* scamp v2 in_view */
+} snode;
 
 typedef struct msgvec { omsg *v; size_t n, cap; } msgvec;
 
@@ -98,6 +108,12 @@ struct psim_handle {
     uint32_t origin_node, origin_msg; int origin_now;
     uint32_t tracked_msg;
     psim_round_stats *st;           /* stats of the round being executed */
+    /* PLUGGABLE handles */
+    snode *sn;
+    uint32_t W;                     /* full: words per member bitset */
+    uint32_t *fbits;                /* full: N rows of W words (the ORSet's members) */
+    uint32_t *pay_in, *pay_out;     /* full: gossip payload snapshots of rounds r-1 and r */
+    size_t pay_out_n, pay_out_cap, pay_in_cap;
 };
 
 /* per-node execution context */
@@ -106,6 +122,9 @@ typedef struct ctx {
     node *s;
     uint32_t me;
     uint32_t seq;
+    uint32_t snap;                  /* full: payload slot of the current state, PSIM_NONE */
+    int dirty;                      /* full: state changed since that snapshot */
+    int gossip_due;                 /* full, fanout > 0: a coalesced gossip is owed this round */
 } ctx;
 
 static uint64_t draw58(ctx *c) {
@@ -723,7 +742,7 @@ static int timer_due(uint32_t period, uint64_t r, uint32_t start) {
 
 static void process_node(struct psim_handle *h, uint32_t n) {
     node *s = &h->nodes[n];
-    ctx c = {h, s, n, 0};
+    ctx c = {h, s, n, 0, PSIM_NONE, 0, 0};
     uint64_t r = h->round;
     size_t b = h->in_beg[n], e = h->in_beg[n + 1];
     /* a fresh incarnation has no connections: traffic addressed to the
@@ -798,6 +817,291 @@ static void process_node(struct psim_handle *h, uint32_t n) {
     }
 }
 
+/* ================================================== pluggable manager ==
+ * partisan_pluggable_peer_service_manager driving one membership strategy
+ * (round model R0-P):
+ *   full      partisan_full_membership_strategy.erl   (ORSet of node_specs as
+ *             a member bitset: adds only -- leave/rmv is not simulated)
+ *   scamp v1  partisan_scamp_v1_membership_strategy.erl
+ *   scamp v2  partisan_scamp_v2_membership_strategy.erl
+ * A join is internal_join/3 (pluggable:1423-1458): the joiner's client
+ * connects and says hello, the contact's server answers with its
+ * get_local_state/0 (peer_service_server:125-148), and the joiner's manager
+ * runs Strategy:join/3 on {connected, ..} (pluggable:986-1044).  Strategy
+ * messages go out through do_send_message/7 (pluggable:1309-1363). */
+
+static int is_pl(const struct psim_handle *h) { return h->cfg.manager == PSIM_MANAGER_PLUGGABLE; }
+static uint32_t *fb_row(struct psim_handle *h, uint32_t n) { return h->fbits + (size_t)n * h->W; }
+
+static uint32_t pl_member(ctx *c, uint32_t p) {
+    struct psim_handle *h = c->h;
+    if (h->cfg.strategy == PSIM_STRATEGY_FULL) return (fb_row(h, c->me)[p >> 5] >> (p & 31u)) & 1u;
+    snode *q = &h->sn[c->me];
+    return (uint32_t)list_member(q->view, q->view_n, p);
+}
+
+static void pl_emit(ctx *c, uint32_t dst, uint32_t type, uint32_t a0, uint32_t slot) {
+    emit(c, dst, type, 0, a0, 0, 0, NULL, 0);
+    c->h->out.v[c->h->out.n - 1].slot = slot;
+}
+
+/* A strategy message to Peer: establish_connections/3 (pluggable:1096-1108)
+ * keeps a connection to every member and pending node, so the send succeeds
+ * iff Peer is one of them, runs and is not partitioned away; a successful
+ * dispatch draws rand:uniform(1) (partisan_util:dispatch_pid/3 util:190-195). */
+static int pl_send(ctx *c, uint32_t dst, uint32_t type, uint32_t a0, uint32_t slot) {
+    if (!connect_ok(c, dst) || !(pl_member(c, dst) || dst == c->h->sn[c->me].pending)) {
+        c->h->st->send_fail++;
+        return 0;
+    }
+    (void)uniform_n(c, 1);
+    pl_emit(c, dst, type, a0, slot);
+    return 1;
+}
+
+/* --------------------------------------------------------------- full -- */
+static uint32_t popcount32(uint32_t x) { return (uint32_t)__builtin_popcount(x); }
+
+static uint32_t full_count(struct psim_handle *h, const uint32_t *b) {
+    uint32_t k = 0;
+    for (uint32_t w = 0; w < h->W; w++) k += popcount32(b[w]);
+    return k;
+}
+
+/* the k-th (0-based) member in id order */
+static uint32_t full_nth(struct psim_handle *h, const uint32_t *b, uint32_t k) {
+    for (uint32_t w = 0; w < h->W; w++) {
+        uint32_t x = b[w], pc = popcount32(x);
+        if (k < pc) {
+            for (; k; k--) x &= x - 1;
+            return w * 32 + (uint32_t)__builtin_ctz(x);
+        }
+        k -= pc;
+    }
+    return PSIM_NONE;
+}
+
+/* The Erlang message carries the state term of its moment: one snapshot per
+ * distinct state a node gossips during the round. */
+static uint32_t full_snapshot(ctx *c) {
+    struct psim_handle *h = c->h;
+    if (c->snap != PSIM_NONE && !c->dirty) return c->snap;
+    if (h->pay_out_n == h->pay_out_cap) {
+        h->pay_out_cap = h->pay_out_cap ? h->pay_out_cap * 2 : 64;
+        h->pay_out = (uint32_t *)realloc(h->pay_out, h->pay_out_cap * h->W * sizeof(uint32_t));
+    }
+    memcpy(h->pay_out + h->pay_out_n * h->W, fb_row(h, c->me), h->W * sizeof(uint32_t));
+    c->snap = (uint32_t)h->pay_out_n++;
+    c->dirty = 0;
+    return c->snap;
+}
+
+/* gossip_messages/1 (full:127-144): {membership_strategy, {Myself, State}} to
+ * every member of membership_list/1 (fanout 0: the reference), or -- config
+ * B's extension of the `fanout` key no strategy reads --
+ * to `fanout` members, each drawn as rand:uniform(length(Members)).  The
+ * whole list is built before the manager sends any of it.
+ * With fanout > 0 the gossips a round owes (join, every non-equal merge,
+ * periodic) are coalesced into one, sent after the node's inbox: the
+ * reference's gossip-on-every-change multiplies the message count by the
+ * fanout each round until the states agree. */
+static void full_gossip(ctx *c) {
+    struct psim_handle *h = c->h;
+    const uint32_t *b = fb_row(h, c->me);
+    uint32_t slot = full_snapshot(c), cnt = full_count(h, b);
+    if (h->cfg.fanout == 0) {
+        for (uint32_t w = 0; w < h->W; w++)
+            for (uint32_t x = b[w]; x; x &= x - 1)
+                pl_send(c, w * 32 + (uint32_t)__builtin_ctz(x), PSIM_PL_GOSSIP, cnt, slot);
+        return;
+    }
+    uint32_t tgt[PSIM_SVIEW_CAP];
+    for (uint32_t i = 0; i < h->cfg.fanout; i++) tgt[i] = full_nth(h, b, uniform_n(c, cnt) - 1);
+    for (uint32_t i = 0; i < h->cfg.fanout; i++) pl_send(c, tgt[i], PSIM_PL_GOSSIP, cnt, slot);
+}
+
+/* ?SET:merge/2 into the node's state; returns whether it was ?SET:equal/2 */
+static int full_merge(ctx *c, const uint32_t *p) {
+    struct psim_handle *h = c->h;
+    uint32_t *b = fb_row(h, c->me);
+    int equal = 1;
+    for (uint32_t w = 0; w < h->W; w++) {
+        if (b[w] != p[w]) equal = 0;
+        uint32_t m = b[w] | p[w];
+        if (m != b[w]) { b[w] = m; c->dirty = 1; }
+    }
+    return equal;
+}
+
+/* -------------------------------------------------------------- scamp -- */
+/* select_random_sublist/2 + shuffle/1 (scamp_v1:263-269, scamp_v2:345-350) */
+static uint32_t sublist_view(ctx *c, const uint32_t *view, uint32_t n, uint32_t k, uint32_t *out) {
+    uint64_t key[PSIM_SVIEW_CAP];
+    uint32_t el[PSIM_SVIEW_CAP];
+    for (uint32_t i = 0; i < n; i++) { key[i] = uniform_key(c); el[i] = view[i]; }
+    for (uint32_t i = 1; i < n; i++) {
+        uint64_t kk = key[i]; uint32_t ee = el[i]; int j = (int)i - 1;
+        while (j >= 0 && (key[j] > kk || (key[j] == kk && el[j] > ee))) {
+            key[j + 1] = key[j]; el[j + 1] = el[j]; j--;
+        }
+        key[j + 1] = kk; el[j + 1] = ee;
+    }
+    uint32_t m = n < k ? n : k;
+    for (uint32_t i = 0; i < m; i++) out[i] = el[i];
+    return m;
+}
+
+/* random_0_or_1/0 (scamp_v1:272-279): rand:uniform(10) >= 5 */
+static uint32_t random_0_or_1(ctx *c) { return uniform_n(c, 10) >= 5 ? 1u : 0u; }
+
+/* sets:add_element/2 (v1) or [Node | List] (v2) into a fixed table */
+static void scamp_add(ctx *c, uint32_t *l, uint32_t *n, uint32_t e, int as_set) {
+    if (as_set && list_member(l, *n, e)) return;
+    if (*n >= PSIM_SVIEW_CAP) { c->h->st->overflow++; return; }
+    if (as_set) { set_add(l, n, e); return; }
+    for (uint32_t i = *n; i > 0; i--) l[i] = l[i - 1];
+    l[0] = e;
+    (*n)++;
+}
+
+/* Strategy:join/3 at the joiner (scamp_v1:52-99, scamp_v2:64-113): add the
+ * contact; forward_subscription(Myself) to it, forward_subscription(Contact)
+ * to every member known before (v1: sets:fold/3, the reverse of to_list;
+ * v2: lists:foldl/3) and to C (v1) / C - 1 (v2) random ones of them. */
+static void scamp_join(ctx *c, uint32_t contact) {
+    snode *q = &c->h->sn[c->me];
+    int v1 = c->h->cfg.strategy == PSIM_STRATEGY_SCAMP_V1;
+    uint32_t m0[PSIM_SVIEW_CAP], n0 = q->view_n;
+    memcpy(m0, q->view, sizeof m0);
+    scamp_add(c, q->view, &q->view_n, contact, v1);
+    uint32_t dst[1 + 2 * PSIM_SVIEW_CAP], arg[1 + 2 * PSIM_SVIEW_CAP], k = 0;
+    dst[k] = contact; arg[k++] = c->me;
+    for (uint32_t i = 0; i < n0; i++) { dst[k] = m0[v1 ? n0 - 1 - i : i]; arg[k++] = contact; }
+    uint32_t sel[PSIM_SVIEW_CAP];
+    uint32_t ns = sublist_view(c, m0, n0, v1 ? c->h->cfg.scamp_c : c->h->cfg.scamp_c - 1, sel);
+    for (uint32_t i = 0; i < ns; i++) { dst[k] = sel[i]; arg[k++] = contact; }
+    for (uint32_t i = 0; i < k; i++) pl_send(c, dst[i], PSIM_PL_FWD_SUB, arg[i], PSIM_NONE);
+}
+
+/* periodic/1 (scamp_v1:125-174, scamp_v2:130-178): "isolated" when a ping
+ * was ever received and the last one is older than
+ * ?PERIODIC_INTERVAL * ?SCAMP_MESSAGE_WINDOW = 100000 us (App. A Q12: in
+ * rounds of 1 s, any earlier round) -> forward_subscription(Myself) to one
+ * random member; then a ping to every member. */
+static void scamp_periodic(ctx *c) {
+    snode *q = &c->h->sn[c->me];
+    uint32_t m[PSIM_SVIEW_CAP], n = q->view_n;
+    memcpy(m, q->view, sizeof m);
+    int isolated = q->last_ping != PSIM_NONE && (uint32_t)c->h->round > q->last_ping;
+    uint32_t sel[1], ns = 0;
+    if (isolated) ns = sublist_view(c, m, n, 1, sel);
+    for (uint32_t i = 0; i < ns; i++) pl_send(c, sel[i], PSIM_PL_FWD_SUB, c->me, PSIM_NONE);
+    for (uint32_t i = 0; i < n; i++) pl_send(c, m[i], PSIM_PL_PING, c->me, PSIM_NONE);
+}
+
+/* handle_message(.., {forward_subscription, Node}) (scamp_v1:212-252,
+ * scamp_v2:284-327): Keep = trunc((size + 1) * random_0_or_1()), so the
+ * subscription is kept iff the draw is 0 and Node is not a member yet (v2
+ * then asks Node to keep us); otherwise it is forwarded to one random member */
+static void scamp_fwd(ctx *c, uint32_t node) {
+    snode *q = &c->h->sn[c->me];
+    int v1 = c->h->cfg.strategy == PSIM_STRATEGY_SCAMP_V1;
+    uint32_t rnd = random_0_or_1(c);
+    if (rnd == 0 && !list_member(q->view, q->view_n, node)) {
+        scamp_add(c, q->view, &q->view_n, node, v1);
+        if (!v1) pl_send(c, node, PSIM_PL_KEEP_SUB, c->me, PSIM_NONE);
+        return;
+    }
+    uint32_t sel[1];
+    uint32_t m0[PSIM_SVIEW_CAP];
+    memcpy(m0, q->view, sizeof m0);
+    if (sublist_view(c, m0, q->view_n, 1, sel)) pl_send(c, sel[0], PSIM_PL_FWD_SUB, node, PSIM_NONE);
+}
+
+/* ------------------------------------------------------------- driver -- */
+static void pl_handle(ctx *c, const omsg *m) {
+    struct psim_handle *h = c->h;
+    snode *q = &h->sn[c->me];
+    int full = h->cfg.strategy == PSIM_STRATEGY_FULL;
+    switch (m->type) {
+    case PSIM_PL_HELLO:       /* the server's answer: {state, Tag, get_local_state()} */
+        if (!connect_ok(c, m->src)) { h->st->send_fail++; break; }
+        if (full) pl_emit(c, m->src, PSIM_PL_STATE, full_count(h, fb_row(h, c->me)), full_snapshot(c));
+        else pl_emit(c, m->src, PSIM_PL_STATE, 0, PSIM_NONE);
+        break;
+    case PSIM_PL_STATE:       /* handle_info({connected, Node, _, RemoteState}) pluggable:986-1044 */
+        if (q->pending != m->src) break;
+        q->pending = PSIM_NONE;
+        if (full) {           /* join/3 full:49-55: merge, then gossip */
+            full_merge(c, h->pay_in + (size_t)m->slot * h->W);
+            if (h->cfg.fanout) c->gossip_due = 1;
+            else full_gossip(c);
+        } else {
+            scamp_join(c, m->src);
+        }
+        break;
+    case PSIM_PL_GOSSIP:      /* handle_message/2 full:99-116 */
+        if (!full) break;
+        if (!full_merge(c, h->pay_in + (size_t)m->slot * h->W)) {
+            if (h->cfg.fanout) c->gossip_due = 1;
+            else full_gossip(c);
+        }
+        break;
+    case PSIM_PL_FWD_SUB:
+        if (!full) scamp_fwd(c, m->a0);
+        break;
+    case PSIM_PL_PING:        /* scamp_v1:177-188, scamp_v2:181-191 */
+        if (!full) q->last_ping = (uint32_t)h->round;
+        break;
+    case PSIM_PL_KEEP_SUB:    /* scamp_v2:328-338: InView = [Node | InView0] */
+        if (h->cfg.strategy == PSIM_STRATEGY_SCAMP_V2) scamp_add(c, q->inv, &q->inv_n, m->a0, 0);
+        break;
+    default:
+        break;
+    }
+}
+
+static void pl_process_node(struct psim_handle *h, uint32_t n) {
+    node *s = &h->nodes[n];
+    snode *q = &h->sn[n];
+    ctx c = {h, s, n, 0, PSIM_NONE, 0, 0};
+    uint64_t r = h->round;
+    size_t b = h->in_beg[n], e = h->in_beg[n + 1];
+    if (s->start_round == r && e > b) { h->st->dropped += e - b; e = b; }
+    int hello = q->pending != PSIM_NONE && !q->hello_sent;
+    int periodic = timer_due(h->cfg.periodic_interval, r, s->start_round);
+    if (!(e > b || hello || periodic)) return;
+    h->st->nodes_processed++;
+    if (hello) {              /* establish_connections -> client connect + hello */
+        if (connect_ok(&c, q->pending)) { pl_emit(&c, q->pending, PSIM_PL_HELLO, 0, PSIM_NONE); q->hello_sent = 1; }
+        else h->st->send_fail++;
+    }
+    for (size_t i = b; i < e; i++) {
+        h->st->delivered[h->inbox.v[i].type]++;
+        pl_handle(&c, &h->inbox.v[i]);
+    }
+    if (periodic) {           /* handle_info(periodic) pluggable:881-903 */
+        if (h->cfg.strategy == PSIM_STRATEGY_FULL) c.gossip_due = 1;
+        else scamp_periodic(&c);
+    }
+    if (c.gossip_due) full_gossip(&c);
+}
+
+static void pl_node_init(struct psim_handle *h, uint32_t n, uint32_t contact) {
+    snode *q = &h->sn[n];
+    memset(q, 0, sizeof *q);
+    q->started = 1;
+    q->pending = contact;
+    q->last_ping = PSIM_NONE;
+    q->view[0] = n; q->view_n = 1;               /* init/1: Myself only */
+    if (h->cfg.strategy == PSIM_STRATEGY_FULL) {
+        q->view_n = 0; q->view[0] = 0;
+        uint32_t *b = fb_row(h, n);
+        memset(b, 0, h->W * sizeof(uint32_t));
+        b[n >> 5] |= 1u << (n & 31u);            /* new_state/1 full:171-175 */
+    }
+}
+
 /* ---------------------------------------------------------- rounds -- */
 static void node_init(struct psim_handle *h, uint32_t n, uint32_t contact) {
     node *s = &h->nodes[n];
@@ -812,6 +1116,7 @@ static void node_init(struct psim_handle *h, uint32_t n, uint32_t contact) {
     s->pt_common[0] = n; s->pt_common_n = 1;
     s->pt_root = PSIM_NONE;
     s->trk_round = PSIM_NONE;
+    if (is_pl(h)) pl_node_init(h, n, contact);
 }
 
 static int cmp_dst(const void *a, const void *b) {
@@ -855,7 +1160,8 @@ static void round_begin(struct psim_handle *h, psim_round_stats *st) {
     for (uint32_t n = h->lo; n < h->hi; n++) {
         if (h->nodes[n].up) {
             st->nodes_up++;
-            process_node(h, n);
+            if (is_pl(h)) pl_process_node(h, n);
+            else process_node(h, n);
         } else {
             st->dropped += h->in_beg[n + 1] - h->in_beg[n];
         }
@@ -867,6 +1173,11 @@ static void round_begin(struct psim_handle *h, psim_round_stats *st) {
  * shard) become the canonical inbox of round r+1, sorted by (dst, src, seq). */
 static void round_end(struct psim_handle *h, msgvec *in) {
     qsort(in->v, in->n, sizeof(omsg), cmp_dst);
+    if (h->fbits) {                 /* this round's snapshots are read next round */
+        uint32_t *t = h->pay_in; h->pay_in = h->pay_out; h->pay_out = t;
+        size_t tc = h->pay_in_cap; h->pay_in_cap = h->pay_out_cap; h->pay_out_cap = tc;
+        h->pay_out_n = 0;
+    }
     if (in != &h->inbox) {
         msgvec t = h->inbox; h->inbox = *in; *in = t;
     }
@@ -894,6 +1205,8 @@ void orc_default_config(psim_config *cfg) {
     cfg->shuffle_period = 10; cfg->promotion_period = 5; cfg->random_promotion = 1;
     cfg->persist_epoch = 0; cfg->plumtree = 1; cfg->lazy_tick_period = 1;
     cfg->device = -1; cfg->n_shards = 1; cfg->shard_world = 1;
+    cfg->manager = PSIM_MANAGER_HYPARVIEW; cfg->strategy = PSIM_STRATEGY_FULL;
+    cfg->periodic_interval = 10; cfg->scamp_c = 5; cfg->fanout = 0;
 }
 
 int orc_create(const psim_config *cfg, struct psim_handle **out) {
@@ -901,8 +1214,12 @@ int orc_create(const psim_config *cfg, struct psim_handle **out) {
         cfg->n_nodes >= PSIM_MAP_BIT || cfg->max_active_size < 2 ||
         cfg->max_active_size > PSIM_ACTIVE_CAP || cfg->max_passive_size < 1 ||
         cfg->max_passive_size > 30 || 1 + cfg->k_active + cfg->k_passive > PSIM_EXCHANGE_CAP ||
-        cfg->arwl > 255 || cfg->prwl > 255)
+        cfg->arwl > 255 || cfg->prwl > 255 || cfg->manager > PSIM_MANAGER_PLUGGABLE ||
+        cfg->strategy > PSIM_STRATEGY_SCAMP_V2 || cfg->scamp_c < 1 || cfg->scamp_c > PSIM_SVIEW_CAP ||
+        cfg->fanout > PSIM_SVIEW_CAP)
         return PSIM_EINVAL;
+    int full = cfg->manager == PSIM_MANAGER_PLUGGABLE && cfg->strategy == PSIM_STRATEGY_FULL;
+    if (full && cfg->shard_world > 1) return PSIM_EUNSUPPORTED;   /* payloads are shard-local */
     struct psim_handle *h = (struct psim_handle *)calloc(1, sizeof *h);
     if (!h) return PSIM_ENOMEM;
     h->cfg = *cfg;
@@ -920,6 +1237,15 @@ int orc_create(const psim_config *cfg, struct psim_handle **out) {
     h->in_beg = (size_t *)calloc((size_t)h->N + 1, sizeof(size_t));
     h->pend_part = (uint8_t *)calloc(h->N, 1);
     if (!h->nodes || !h->part || !h->crashed_now || !h->in_beg || !h->pend_part) return PSIM_ENOMEM;
+    if (cfg->manager == PSIM_MANAGER_PLUGGABLE) {
+        h->sn = (snode *)calloc(h->N, sizeof(snode));
+        if (!h->sn) return PSIM_ENOMEM;
+        if (full) {
+            h->W = (h->N + 31) / 32;
+            h->fbits = (uint32_t *)calloc((size_t)h->N * h->W, sizeof(uint32_t));
+            if (!h->fbits) return PSIM_ENOMEM;
+        }
+    }
     h->bcast_root = PSIM_NONE;
     h->tracked_msg = PSIM_NONE;
     *out = h;
@@ -931,12 +1257,18 @@ void orc_destroy(struct psim_handle *h) {
     free(h->nodes); free(h->part); free(h->crashed_now); free(h->in_beg); free(h->pend_part);
     free(h->inbox.v); free(h->out.v);
     free(h->pend_crash); free(h->pend_join); free(h->pend_contact);
+    free(h->sn); free(h->fbits); free(h->pay_in); free(h->pay_out);
     free(h);
 }
 
 int orc_join(struct psim_handle *h, const uint32_t *nodes, const uint32_t *contacts, size_t n) {
     for (size_t i = 0; i < n; i++)
         if (nodes[i] >= h->N || (contacts[i] != PSIM_NONE && contacts[i] >= h->N)) return PSIM_ERANGE;
+    if (h->fbits) {                 /* an ORSet re-add would need per-incarnation tokens */
+        for (size_t i = 0; i < n; i++)
+            if (h->sn[nodes[i]].started) return PSIM_EUNSUPPORTED;
+        for (size_t i = 0; i < n; i++) h->sn[nodes[i]].started = 1;
+    }
     if (h->pend_join_n + n > h->pend_join_cap) {
         h->pend_join_cap = (h->pend_join_n + n) * 2;
         h->pend_join = (uint32_t *)realloc(h->pend_join, h->pend_join_cap * 4);
@@ -973,6 +1305,7 @@ int orc_clear_partition(struct psim_handle *h) {
 }
 
 int orc_broadcast(struct psim_handle *h, uint32_t root, uint32_t msg_id) {
+    if (is_pl(h)) return PSIM_EUNSUPPORTED;      /* Plumtree runs over the HyParView manager */
     if (root >= h->N || msg_id > 0xFFFF) return PSIM_ERANGE;
     uint32_t r = root | PSIM_MAP_BIT;
     if (h->bcast_root != PSIM_NONE && h->bcast_root != r) return PSIM_EUNSUPPORTED;
@@ -1011,6 +1344,44 @@ int orc_get_nodes(struct psim_handle *h, uint32_t first, uint32_t count, psim_no
         memcpy(v->pt_out_round, s->out_round, sizeof v->pt_out_round);
         v->have = s->have; v->trk_round = s->trk_round; v->trk_hop = s->trk_hop;
     }
+    return PSIM_OK;
+}
+
+static uint64_t members_hash(struct psim_handle *h, const uint32_t *b) {
+    uint64_t x = 0;
+    for (uint32_t w = 0; w < h->W; w++)
+        for (uint32_t v = b[w]; v; v &= v - 1) x += mix64((uint64_t)(w * 32 + (uint32_t)__builtin_ctz(v)) + 1);
+    return x;
+}
+
+int orc_get_strategy_nodes(struct psim_handle *h, uint32_t first, uint32_t count, psim_strategy_view *out) {
+    if (!is_pl(h)) return PSIM_ESTATE;
+    if ((uint64_t)first + count > h->N) return PSIM_ERANGE;
+    for (uint32_t k = 0; k < count; k++) {
+        uint32_t n = first + k;
+        const node *s = &h->nodes[n];
+        const snode *q = &h->sn[n];
+        psim_strategy_view *v = &out[k];
+        memset(v, 0, sizeof *v);
+        v->up = s->up; v->start_round = s->start_round; v->rng_ctr = s->rng;
+        v->pending = q->started ? q->pending : PSIM_NONE;
+        v->last_ping = q->started ? q->last_ping : PSIM_NONE;
+        v->view_n = q->view_n; v->in_n = q->inv_n;
+        memcpy(v->view, q->view, sizeof v->view);
+        memcpy(v->in_view, q->inv, sizeof v->in_view);
+        if (h->fbits) {
+            v->members = full_count(h, fb_row(h, n));
+            v->members_hash = members_hash(h, fb_row(h, n));
+        }
+    }
+    return PSIM_OK;
+}
+
+int orc_get_member_bits(struct psim_handle *h, uint32_t node, uint32_t *words, size_t n_words) {
+    if (!h->fbits) return PSIM_ESTATE;
+    if (node >= h->N) return PSIM_ERANGE;
+    if (n_words < h->W) return PSIM_EINVAL;
+    memcpy(words, fb_row(h, node), h->W * sizeof(uint32_t));
     return PSIM_OK;
 }
 

@@ -8,18 +8,22 @@ import ctypes as C
 
 import numpy as np
 
-PSIM_ABI_VERSION = 1
+PSIM_ABI_VERSION = 2
 PSIM_MAP_BIT = 0x80000000
 PSIM_NONE = 0xFFFFFFFF
 ACTIVE_CAP, PASSIVE_CAP, IDMAP_CAP = 8, 32, 32
 PT_MEMBERS_CAP, PT_SET_CAP, PT_OUT_CAP, EXCHANGE_CAP = 8, 16, 32, 8
 NTYPES = 16
+SVIEW_CAP = 64
+MANAGER_HYPARVIEW, MANAGER_PLUGGABLE = 0, 1
+STRATEGY_FULL, STRATEGY_SCAMP_V1, STRATEGY_SCAMP_V2 = 0, 1, 2
 
 MSG_TYPES = [
     "JOIN", "FORWARD_JOIN", "NEIGHBOR", "DISCONNECT", "NEIGHBOR_REQUEST",
     "NEIGHBOR_ACCEPTED", "NEIGHBOR_REJECTED", "SHUFFLE", "SHUFFLE_REPLY",
     "PT_BROADCAST", "PT_PRUNE", "PT_IHAVE", "PT_IGNORED_IHAVE", "PT_GRAFT",
 ]
+PL_MSG_TYPES = ["HELLO", "STATE", "GOSSIP", "FWD_SUB", "PING", "KEEP_SUB"]
 HV_TYPES = list(range(0, 9))
 PT_TYPES = list(range(9, 14))
 
@@ -40,7 +44,9 @@ class PsimConfig(C.Structure):
         ("plumtree", C.c_uint32), ("lazy_tick_period", C.c_uint32),
         ("device", C.c_int32), ("n_shards", C.c_uint32), ("shard_rank", C.c_uint32),
         ("shard_world", C.c_uint32), ("comm_id", C.c_void_p),
-        ("max_msgs_per_round", C.c_uint64), ("reserved", C.c_uint32 * 8),
+        ("max_msgs_per_round", C.c_uint64),
+        ("manager", C.c_uint32), ("strategy", C.c_uint32), ("periodic_interval", C.c_uint32),
+        ("scamp_c", C.c_uint32), ("fanout", C.c_uint32), ("reserved", C.c_uint32 * 3),
     ]
 
 
@@ -75,7 +81,18 @@ class PsimNodeView(C.Structure):
     ]
 
 
+class PsimStrategyView(C.Structure):
+    _fields_ = [
+        ("up", C.c_uint32), ("start_round", C.c_uint32), ("pending", C.c_uint32),
+        ("last_ping", C.c_uint32), ("rng_ctr", C.c_uint64),
+        ("view_n", C.c_uint32), ("in_n", C.c_uint32),
+        ("view", C.c_uint32 * SVIEW_CAP), ("in_view", C.c_uint32 * SVIEW_CAP),
+        ("members", C.c_uint32), ("pad", C.c_uint32), ("members_hash", C.c_uint64),
+    ]
+
+
 NODE_VIEW_DTYPE = np.dtype(PsimNodeView)
+STRATEGY_VIEW_DTYPE = np.dtype(PsimStrategyView)
 STATS_DTYPE = np.dtype(PsimRoundStats)
 
 # entry points of the C ABI: name -> (restype, argtypes)
@@ -93,6 +110,8 @@ SIGNATURES = {
     "step": (C.c_int, [_H, C.c_uint32, C.POINTER(PsimRoundStats)]),
     "get_nodes": (C.c_int, [_H, C.c_uint32, C.c_uint32, C.POINTER(PsimNodeView)]),
     "get_round": (C.c_int, [_H, C.POINTER(C.c_uint64)]),
+    "get_strategy_nodes": (C.c_int, [_H, C.c_uint32, C.c_uint32, C.POINTER(PsimStrategyView)]),
+    "get_member_bits": (C.c_int, [_H, C.c_uint32, _P32, C.c_size_t]),
 }
 # symbols only the GPU library exports
 GPU_ONLY = {

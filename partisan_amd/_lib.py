@@ -20,6 +20,7 @@ def load():
                 f"{LIB_PATH} is missing: build it with `make -C partisan_amd/csrc` "
                 "or __graft_entry__.build()")
         _lib = ctypes.CDLL(LIB_PATH)
-        if _lib.psim_abi_version() != 1:
-            raise ImportError("libpartisan_gpu_sim.so ABI version mismatch")
+        from ._abi import PSIM_ABI_VERSION
+        if _lib.psim_abi_version() != PSIM_ABI_VERSION:
+            raise ImportError("libpartisan_gpu_sim.so ABI version mismatch: rebuild it")
     return _lib

@@ -119,6 +119,21 @@ __global__ void k_join(RoundArgs a, uint32_t* start, const uint32_t* ids, const 
         a.pt_laz[(size_t)li * PSIM_PT_SET_CAP + k] = 0;
     }
     for (int k = 0; k < PSIM_PT_OUT_CAP; k++) a.pt_out[(size_t)li * PSIM_PT_OUT_CAP + k] = 0;
+    if (a.pl) {                    // the pluggable manager's init/1 (pl:346-402) + Strategy:init/1
+        Hdr& x = a.hdr[li];
+        x.pt_root = PSIM_NONE;     // last ping: undefined
+        x.have = 0;                // hello not sent
+        x.act_n = a.strategy == PSIM_STRATEGY_FULL ? 0 : 1;
+        x.pas_n = 0; x.all_n = 0; x.com_n = 0;
+        if (a.strategy == PSIM_STRATEGY_FULL) {
+            a.fbits[(size_t)li * a.fw + (id >> 5)] |= 1u << (id & 31u);   // new_state/1 full:171-175
+        } else {
+            for (int k = 0; k < PSIM_SVIEW_CAP; k++) {
+                a.sview[(size_t)li * PSIM_SVIEW_CAP + k] = k == 0 ? id : 0u;   // [Myself]
+                if (a.sinv) a.sinv[(size_t)li * PSIM_SVIEW_CAP + k] = 0u;
+            }
+        }
+    }
 }
 
 __global__ void k_bcast_reset(Hdr* hdr, uint32_t n, uint32_t bit) {
@@ -164,6 +179,17 @@ __global__ void k_node_prep(RoundArgs a, const uint32_t* bsum, uint64_t* bound, 
         uint32_t c = a.in_cnt[i];
         if (f & F_UP) {
             uint32_t st = a.start[i], r = a.round;
+            if (a.pl) {            // emission bounds of the pluggable round (R0-P)
+                const Hdr& x = a.hdr[i];
+                bool pending = x.join_contact != PSIM_NONE;
+                bool per = due(a.periodic, r, st);
+                if (a.strategy == PSIM_STRATEGY_FULL)
+                    b = a.fanout ? (uint64_t)c + a.fanout + 1 : ((uint64_t)c + 2) * (a.n_nodes + 1);
+                else
+                    b = (uint64_t)c + (pending ? 2 + PSIM_SVIEW_CAP + a.scamp_c : 0) +
+                        (per ? 1 + PSIM_SVIEW_CAP : 0) + 1;
+                w = c > 0 || (pending && !x.have) || per;
+            } else {
             bool origin = a.origin_now && id == a.origin_node;
             b = bsum[i] + BOUND_BASE;
             if (f & F_LAZY) b += BOUND_LAZY;
@@ -172,6 +198,7 @@ __global__ void k_node_prep(RoundArgs a, const uint32_t* bsum, uint64_t* bound, 
             w = c > 0 || st == r || a.crash_round || (f & F_LAZY) || origin ||
                 (a.random_promotion && (f & F_LOWACT) && due(a.promotion_period, r, st)) ||
                 due(a.shuffle_period, r, st);
+            }
             atomicAdd((unsigned long long*)&s_up, 1ull);
         } else if (c) {
             atomicAdd((unsigned long long*)&s_drop, (unsigned long long)c);
@@ -242,11 +269,11 @@ __global__ void k_gather(const Msg* __restrict__ rec, const uint32_t* __restrict
 
 // receive side: route keys of the received records (local dst | bound)
 __global__ void k_rkeys(const Msg* __restrict__ rec, uint32_t m, uint32_t lo, uint32_t* keys,
-                        uint32_t* vals) {
+                        uint32_t* vals, uint32_t pl) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= m) return;
     uint32_t type = rec[i].tt & 0xFF;
-    keys[i] = (rec[i].dst - lo) | (max_emit(type) << KEY_DST_BITS);
+    keys[i] = (rec[i].dst - lo) | ((pl ? 0u : max_emit(type)) << KEY_DST_BITS);
     vals[i] = i;
 }
 
@@ -324,6 +351,9 @@ struct Shard {
     DBuf<uint8_t> cub_tmp;
     DBuf<uint32_t> ev_ids, ev_contacts;
     DBuf<Msg> sendbuf;
+    // pluggable manager
+    DBuf<uint32_t> sview, sinv, fbits, pay[2], pay_top;
+    int pay_cur = 0;
     std::vector<uint64_t> soff, scnt;   // per destination shard (G + 1 offsets)
     uint32_t m_out = 0, pgrid = 0, cgrid = 0;
     uint64_t st_host[NST];
@@ -350,6 +380,8 @@ struct psim_handle {
     bool pend_bcast = false;
     uint32_t pend_root = 0, pend_msg = 0;
     uint32_t bcast_root = PSIM_NONE, tracked_msg = PSIM_NONE;
+    uint32_t fw = 0;                    // full strategy: words per member row
+    std::vector<uint8_t> started;       // full strategy: ids ever started (no restarts)
     double kt_ms[KT_N] = {0};
     uint64_t kt_n[KT_N] = {0};
 };
@@ -376,6 +408,10 @@ RoundArgs make_args(psim_handle* h, Shard* s) {
     a.pt_all = s->pt_all.p; a.pt_com = s->pt_com.p; a.pt_eag = s->pt_eag.p; a.pt_laz = s->pt_laz.p;
     a.pt_out = s->pt_out.p;
     a.start = s->start.p;
+    a.pl = c.manager == PSIM_MANAGER_PLUGGABLE;
+    a.strategy = c.strategy; a.periodic = c.periodic_interval; a.scamp_c = c.scamp_c;
+    a.fanout = c.fanout; a.fw = h->fw;
+    a.fbits = s->fbits.p; a.sview = s->sview.p; a.sinv = s->sinv.p;
     return a;
 }
 
@@ -503,11 +539,24 @@ int phase_events_prepare(psim_handle* h, Shard* s, const RoundCtl& ctl, RoundArg
     return PSIM_OK;
 }
 
-int phase_consume(psim_handle* h, Shard* s, const RoundArgs& a) {
+int phase_consume(psim_handle* h, Shard* s, RoundArgs& a) {
+    if (a.pl && a.strategy == PSIM_STRATEGY_FULL) {
+        // snapshots: at most one per node plus one per inbox message
+        uint64_t slots = (uint64_t)s->m_in + s->n + 1;
+        if (slots > 0xFFFFFFFFull) return PSIM_ENOMEM;
+        TRY(s->pay[s->pay_cur].ensure(slots * h->fw));
+        a.pay_out = s->pay[s->pay_cur].p;
+        a.pay_in = s->pay[s->pay_cur ^ 1].p;
+        a.pay_top = s->pay_top.p;
+        a.pay_cap = (uint32_t)(s->pay[s->pay_cur].n / h->fw);
+        HIP_TRY(hipMemsetAsync(s->pay_top.p, 0, 4, s->stream));
+    }
     KTimer t(h, s, KT_CONSUME);
     HIP_TRY(hipMemsetAsync(s->ocnt.p, 0, (size_t)s->n * 4, s->stream));
-    k_consume<<<s->cgrid, BLK, 0, s->stream>>>(a);
+    if (a.pl) k_consume_pl<<<s->cgrid, BLK, 0, s->stream>>>(a);
+    else k_consume<<<s->cgrid, BLK, 0, s->stream>>>(a);
     HIP_TRY(hipGetLastError());
+    s->pay_cur ^= 1;
     return PSIM_OK;
 }
 
@@ -580,7 +629,8 @@ int phase_receive(psim_handle* h, Shard* s, uint32_t m) {
     TRY(s->ikeys.ensure(m + 1)); TRY(s->ivals.ensure(m + 1));
     KTimer t(h, s, KT_SORT);
     if (m) {
-        k_rkeys<<<grid_for(m), BLK, 0, s->stream>>>(s->recvbuf.p, m, s->lo, s->keys.p, s->vals.p);
+        k_rkeys<<<grid_for(m), BLK, 0, s->stream>>>(s->recvbuf.p, m, s->lo, s->keys.p, s->vals.p,
+                                                    h->cfg.manager == PSIM_MANAGER_PLUGGABLE);
         TRY(sort_pairs(s, s->keys.p, s->ikeys.p, s->vals.p, s->ivals.p, m, bits_for(s->n)));
     }
     s->m_in = m;
@@ -673,7 +723,7 @@ int run_round(psim_handle* h, uint64_t* st) {
         for (uint32_t j : h->pend_join) if (j == h->pend_root) up_after = true;
         if (up_after) { ctl.origin = true; ctl.origin_node = h->pend_root; ctl.origin_msg = h->pend_msg; }
     }
-    std::vector<RoundArgs> args(h->shards.size());
+    std::vector<RoundArgs> args(h->shards.size());   // (consume fills the payload arena fields)
     for (size_t i = 0; i < h->shards.size(); i++) TRY(phase_events_prepare(h, h->shards[i], ctl, args[i]));
     for (size_t i = 0; i < h->shards.size(); i++) TRY(phase_consume(h, h->shards[i], args[i]));
     if (h->G == 1) {
@@ -739,6 +789,16 @@ int shard_alloc(psim_handle* h, Shard* s) {
     rc |= s->stat_out.alloc(NST);
     rc |= s->ikeys.alloc(1024); rc |= s->ivals.alloc(1024);
     rc |= s->recvbuf.alloc(1024); rc |= s->inbox.alloc(1024); rc |= s->outbox.alloc(1024);
+    if (h->cfg.manager == PSIM_MANAGER_PLUGGABLE) {
+        if (h->cfg.strategy == PSIM_STRATEGY_FULL) {
+            rc |= s->fbits.alloc(n * h->fw);
+            rc |= s->pay_top.alloc(1);
+            rc |= s->pay[0].alloc(h->fw); rc |= s->pay[1].alloc(h->fw);
+        } else {
+            rc |= s->sview.alloc(n * PSIM_SVIEW_CAP);
+            if (h->cfg.strategy == PSIM_STRATEGY_SCAMP_V2) rc |= s->sinv.alloc(n * PSIM_SVIEW_CAP);
+        }
+    }
     return rc ? PSIM_ENOMEM : PSIM_OK;
 }
 
@@ -755,6 +815,8 @@ void shard_free(Shard* s) {
     s->work.release(); s->alist.release(); s->desc.release(); s->d_nact.release(); s->bound.release();
     s->obase.release(); s->stat_part.release(); s->stat_out.release(); s->d_off.release();
     s->cub_tmp.release(); s->ev_ids.release(); s->ev_contacts.release(); s->sendbuf.release();
+    s->sview.release(); s->sinv.release(); s->fbits.release(); s->pay[0].release(); s->pay[1].release();
+    s->pay_top.release();
     if (s->ev_live)
         for (int k = 0; k < KT_N; k++) {
             (void)hipEventDestroy(s->ev[k][0]);
@@ -795,6 +857,8 @@ void psim_default_config(psim_config* cfg) {
     cfg->shuffle_period = 10; cfg->promotion_period = 5; cfg->random_promotion = 1;
     cfg->persist_epoch = 0; cfg->plumtree = 1; cfg->lazy_tick_period = 1;
     cfg->device = -1; cfg->n_shards = 1; cfg->shard_world = 1;
+    cfg->manager = PSIM_MANAGER_HYPARVIEW; cfg->strategy = PSIM_STRATEGY_FULL;
+    cfg->periodic_interval = 10; cfg->scamp_c = 5; cfg->fanout = 0;
 }
 
 void psim_destroy(psim_handle* h);
@@ -804,16 +868,24 @@ int psim_create(const psim_config* cfg, psim_handle** out) {
         cfg->n_nodes > KEY_DST_MASK || cfg->max_active_size < 2 ||
         cfg->max_active_size > PSIM_ACTIVE_CAP || cfg->max_passive_size < 1 ||
         cfg->max_passive_size > 30 || 1 + cfg->k_active + cfg->k_passive > PSIM_EXCHANGE_CAP ||
-        cfg->arwl > 255 || cfg->prwl > 255)
+        cfg->arwl > 255 || cfg->prwl > 255 || cfg->manager > PSIM_MANAGER_PLUGGABLE ||
+        cfg->strategy > PSIM_STRATEGY_SCAMP_V2 || cfg->scamp_c < 1 || cfg->scamp_c > PSIM_SVIEW_CAP ||
+        cfg->fanout > PSIM_SVIEW_CAP)
         return PSIM_EINVAL;
+    const bool full = cfg->manager == PSIM_MANAGER_PLUGGABLE && cfg->strategy == PSIM_STRATEGY_FULL;
     uint32_t world = std::max<uint32_t>(cfg->shard_world, 1);
     uint32_t local = std::max<uint32_t>(cfg->n_shards, 1);
     if (world > 1 && (local != 1 || !cfg->comm_id || cfg->shard_rank >= world)) return PSIM_EINVAL;
     uint32_t G = world > 1 ? world : local;
     if (G > 64 || G > cfg->n_nodes) return PSIM_EINVAL;
+    if (full && G > 1) return PSIM_EUNSUPPORTED;      // gossip payloads are shard-local
     psim_handle* h = new (std::nothrow) psim_handle();
     if (!h) return PSIM_ENOMEM;
     h->cfg = *cfg;
+    if (full) {
+        h->fw = ((cfg->n_nodes + 31) / 32 + 3) & ~3u;
+        h->started.assign(cfg->n_nodes, 0);
+    }
     h->N = cfg->n_nodes;
     h->G = G;
     h->per = (h->N + G - 1) / G;
@@ -862,6 +934,11 @@ int psim_join(psim_handle* h, const uint32_t* nodes, const uint32_t* contacts, s
     if (!h || (n && (!nodes || !contacts))) return PSIM_EINVAL;
     for (size_t i = 0; i < n; i++)
         if (nodes[i] >= h->N || (contacts[i] != PSIM_NONE && contacts[i] >= h->N)) return PSIM_ERANGE;
+    if (!h->started.empty()) {          // an ORSet re-add would need per-incarnation tokens
+        for (size_t i = 0; i < n; i++)
+            if (h->started[nodes[i]]) return PSIM_EUNSUPPORTED;
+        for (size_t i = 0; i < n; i++) h->started[nodes[i]] = 1;
+    }
     h->pend_join.insert(h->pend_join.end(), nodes, nodes + n);
     h->pend_contact.insert(h->pend_contact.end(), contacts, contacts + n);
     return PSIM_OK;
@@ -890,6 +967,7 @@ int psim_clear_partition(psim_handle* h) {
 
 int psim_broadcast(psim_handle* h, uint32_t root, uint32_t msg_id) {
     if (!h) return PSIM_EINVAL;
+    if (h->cfg.manager == PSIM_MANAGER_PLUGGABLE) return PSIM_EUNSUPPORTED;   // Plumtree runs over HyParView
     if (root >= h->N || msg_id > 0xFFFF) return PSIM_ERANGE;
     uint32_t r = root | PSIM_MAP_BIT;
     if (h->bcast_root != PSIM_NONE && h->bcast_root != r) return PSIM_EUNSUPPORTED;
@@ -992,6 +1070,99 @@ int psim_get_nodes(psim_handle* h, uint32_t first, uint32_t count, psim_node_vie
         if (rc) return rc;
         done += k;
     }
+    return PSIM_OK;
+}
+
+static uint64_t mix64_host(uint64_t z) {
+    z ^= z >> 30; z *= 0xBF58476D1CE4E5B9ull;
+    z ^= z >> 27; z *= 0x94D049BB133111EBull;
+    z ^= z >> 31;
+    return z;
+}
+
+static uint64_t members_hash(const uint32_t* row, uint32_t words) {
+    uint64_t x = 0;
+    for (uint32_t w = 0; w < words; w++)
+        for (uint32_t v = row[w]; v; v &= v - 1) x += mix64_host((uint64_t)(w * 32 + (uint32_t)__builtin_ctz(v)) + 1);
+    return x;
+}
+
+static Shard* owner_of(psim_handle* h, uint32_t id) {
+    for (Shard* c : h->shards)
+        if (id >= c->lo && id < c->lo + c->n) return c;
+    return nullptr;
+}
+
+int psim_get_strategy_nodes(psim_handle* h, uint32_t first, uint32_t count, psim_strategy_view* out) {
+    if (!h || (count && !out)) return PSIM_EINVAL;
+    if (h->cfg.manager != PSIM_MANAGER_PLUGGABLE) return PSIM_ESTATE;
+    if ((uint64_t)first + count > h->N) return PSIM_ERANGE;
+    if (hipSetDevice(h->device) != hipSuccess) return PSIM_EDEVICE;
+    const bool full = h->cfg.strategy == PSIM_STRATEGY_FULL;
+    uint32_t done = 0;
+    while (done < count) {
+        uint32_t id = first + done;
+        Shard* s = owner_of(h, id);
+        if (!s) return PSIM_ERANGE;
+        uint32_t k = std::min<uint32_t>(count - done, s->lo + s->n - id);
+        const size_t li = id - s->lo;
+        std::vector<Hdr> hd(k);
+        std::vector<uint8_t> fl(k);
+        std::vector<uint32_t> view, inv, rows;
+        HIP_TRY(hipMemcpyAsync(hd.data(), s->hdr.p + li, k * sizeof(Hdr), hipMemcpyDeviceToHost, s->stream));
+        HIP_TRY(hipMemcpyAsync(fl.data(), s->flags.p + id, k, hipMemcpyDeviceToHost, s->stream));
+        if (full) {
+            rows.resize((size_t)k * h->fw);
+            HIP_TRY(hipMemcpyAsync(rows.data(), s->fbits.p + li * h->fw, rows.size() * 4,
+                                   hipMemcpyDeviceToHost, s->stream));
+        } else {
+            view.resize((size_t)k * PSIM_SVIEW_CAP);
+            HIP_TRY(hipMemcpyAsync(view.data(), s->sview.p + li * PSIM_SVIEW_CAP, view.size() * 4,
+                                   hipMemcpyDeviceToHost, s->stream));
+            if (s->sinv.p) {
+                inv.resize(view.size());
+                HIP_TRY(hipMemcpyAsync(inv.data(), s->sinv.p + li * PSIM_SVIEW_CAP, inv.size() * 4,
+                                       hipMemcpyDeviceToHost, s->stream));
+            }
+        }
+        HIP_TRY(hipStreamSynchronize(s->stream));
+        for (uint32_t j = 0; j < k; j++) {
+            psim_strategy_view* v = &out[done + j];
+            const Hdr& x = hd[j];
+            memset(v, 0, sizeof *v);
+            bool started = x.epoch != 0;       // k_join sets epoch >= 1
+            v->up = fl[j] & F_UP; v->start_round = x.start_round; v->rng_ctr = x.rng;
+            v->pending = started ? x.join_contact : PSIM_NONE;
+            v->last_ping = started ? x.pt_root : PSIM_NONE;
+            v->view_n = x.act_n; v->in_n = x.pas_n;
+            if (full) {
+                const uint32_t* row = &rows[(size_t)j * h->fw];
+                uint32_t c = 0;
+                for (uint32_t w = 0; w < h->fw; w++) c += (uint32_t)__builtin_popcount(row[w]);
+                v->members = c;
+                v->members_hash = members_hash(row, h->fw);
+            } else {
+                memcpy(v->view, &view[(size_t)j * PSIM_SVIEW_CAP], sizeof v->view);
+                if (!inv.empty()) memcpy(v->in_view, &inv[(size_t)j * PSIM_SVIEW_CAP], sizeof v->in_view);
+            }
+        }
+        done += k;
+    }
+    return PSIM_OK;
+}
+
+int psim_get_member_bits(psim_handle* h, uint32_t node, uint32_t* words, size_t n_words) {
+    if (!h || !words) return PSIM_EINVAL;
+    if (h->cfg.manager != PSIM_MANAGER_PLUGGABLE || h->cfg.strategy != PSIM_STRATEGY_FULL) return PSIM_ESTATE;
+    if (node >= h->N) return PSIM_ERANGE;
+    const uint32_t W = (h->N + 31) / 32;
+    if (n_words < W) return PSIM_EINVAL;
+    if (hipSetDevice(h->device) != hipSuccess) return PSIM_EDEVICE;
+    Shard* s = owner_of(h, node);
+    if (!s) return PSIM_ERANGE;
+    HIP_TRY(hipMemcpyAsync(words, s->fbits.p + (size_t)(node - s->lo) * h->fw, W * 4, hipMemcpyDeviceToHost,
+                           s->stream));
+    HIP_TRY(hipStreamSynchronize(s->stream));
     return PSIM_OK;
 }
 

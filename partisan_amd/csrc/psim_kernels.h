@@ -33,9 +33,22 @@ struct RoundArgs {
     uint32_t* okey;
     uint32_t* ocnt;
     uint64_t* stat_part;   // [gridDim.x][NST]
+    // pluggable manager (k_consume_pl); Hdr fields are reused as
+    // join_contact = pending contact, pt_root = last ping round,
+    // have = hello sent, act_n = view length, pas_n = in_view length
+    uint32_t pl, strategy, periodic, scamp_c, fanout;
+    uint32_t fw;                 // full: words per member bitset row (multiple of 4)
+    uint32_t* fbits;             // full: n_local rows of fw words
+    const uint32_t* pay_in;      // full: snapshots read this round (slot * fw)
+    uint32_t* pay_out;           // full: snapshots written this round
+    uint32_t* pay_top;           // full: next free slot of pay_out
+    uint32_t pay_cap;
+    uint32_t* sview;             // scamp: n_local rows of PSIM_SVIEW_CAP ids
+    uint32_t* sinv;              // scamp v2: in_view rows
 };
 
 __global__ void k_consume(RoundArgs args);
+__global__ void k_consume_pl(RoundArgs args);
 // diagnostic builds (-DPSIM_STAMPS): per-phase cycle sums of k_consume, reset on read
 int debug_stamps(unsigned long long* out);
 // resident-block count of k_consume on the current device

@@ -1,0 +1,476 @@
+// psim_strategy.hip -- the node-round kernel of a PLUGGABLE handle:
+// partisan's pluggable peer-service manager driving one membership strategy
+// (round model R0-P).
+//
+// One 64-lane wave per node with work, as in psim_consume.hip.  A SCAMP
+// membership / partial view / in-view lives one id per lane, so the
+// strategies' list operations (lists:member, [N | L], sets:add_element,
+// sublist(shuffle(L), K)) are ballots, DPP lane shifts and one rank count.
+// The full strategy's ORSet is the node's member bitset row, walked 1 KiB
+// (64 lanes x 16 B) per step for merge / equal / count / k-th member; a
+// gossip carries a snapshot of the row (the Erlang message carries the state
+// term of its moment), written once into this round's payload arena and
+// read by the receivers next round.
+//
+// Reference handlers are cited as file:line under /root/reference:
+//   full = src/partisan_full_membership_strategy.erl
+//   sv1  = src/partisan_scamp_v1_membership_strategy.erl
+//   sv2  = src/partisan_scamp_v2_membership_strategy.erl
+//   pl   = src/partisan_pluggable_peer_service_manager.erl
+#include "psim_device.h"
+#include "psim_kernels.h"
+#include "psim_wave.h"
+
+namespace psim {
+
+namespace {
+
+constexpr int PL_WAVES = 4;        // waves per block
+constexpr uint32_t NONE = PSIM_NONE;
+constexpr uint64_t NONE64 = ~0ull;
+
+// Hdr fields of a pluggable node (see RoundArgs): join_contact = pending
+// contact, pt_root = round of the last ping, have = hello sent,
+// act_n = view length, pas_n = in_view length.
+struct Pw {
+    const RoundArgs* a;
+    uint32_t* lds;                 // 64 words of per-wave scratch
+    uint32_t me, li, mypart, round;
+    Hdr h;
+    uint32_t V, I;                 // scamp: view / in_view, one id per lane
+    uint32_t vn, in_n;
+    uint32_t CV, CF;               // connection cache: view ids at node start and
+                                   // flags | part << 8 of each
+    uint32_t seq;
+    uint64_t obase;
+    uint64_t digest;               // lane j sums the hashes of record word j
+    uint32_t SC;                   // lane k counts stats slot k
+    uint32_t DCL, DCH;             // draw cache: counters dc_base + lane
+    uint64_t dc_base;
+    uint32_t* row;                 // full: the node's member bitset
+    uint32_t snap;                 // full: payload slot of the current state
+    bool dirty, gossip_due;
+};
+
+DEV void st_add(Pw& w, int k, uint32_t v) { w.SC += lane_id() == (uint32_t)k ? v : 0u; }
+
+DEV uint32_t wave_sum(uint32_t v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += (uint32_t)__shfl_xor((int)v, off);
+    return v;
+}
+
+// ----------------------------------------------------------------- RNG --
+DEV void dc_fill(Pw& w, uint64_t base) {
+    uint64_t v = draw58_at(base + lane_id(), w.me, w.a->seed);
+    w.DCL = (uint32_t)v; w.DCH = (uint32_t)(v >> 32);
+    w.dc_base = base;
+}
+DEV uint64_t draw(Pw& w) {
+    uint64_t c = w.h.rng++;
+    if (c < w.dc_base || c - w.dc_base >= 64) dc_fill(w, c);
+    uint32_t i = (uint32_t)(c - w.dc_base);
+    return ((uint64_t)rl(w.DCH, i) << 32) | rl(w.DCL, i);
+}
+// rand:uniform/1 with a 58-bit generator (OTP rand.erl ?uniform_range)
+DEV uint32_t uniform_n(Pw& w, uint32_t n) {
+    const uint64_t two58 = 1ull << 58;
+    for (;;) {
+        uint64_t v = draw(w);
+        if (v < n) return (uint32_t)v + 1;
+        uint64_t i = n <= 64 ? mod_small(v, n) : mod58(v, n);
+        if (v - i <= two58 - n) return (uint32_t)i + 1;
+    }
+}
+
+// lists:sublist(shuffle(L), K) (sv1:263-269, sv2:345-350) over a list of up
+// to 64 ids: element l keys on counter rng + l; its rank among the (key, id)
+// pairs is its position after lists:sort; the first K land in OUT lanes 0..
+DEV uint32_t sublist(Pw& w, uint32_t V, uint32_t n, uint32_t k, uint32_t& OUT) {
+    uint32_t l = lane_id();
+    uint64_t base = w.h.rng;
+    if (base < w.dc_base || base + n - w.dc_base > 64) dc_fill(w, base);
+    uint32_t off = (uint32_t)(base - w.dc_base);
+    uint32_t src = (l + off) & 63;
+    uint32_t kl = shfl(w.DCL, (int)src), kh = shfl(w.DCH, (int)src);
+    uint64_t key = l < n ? ((((uint64_t)kh) << 32) | kl) >> 5 : ~0ull;
+    uint32_t m = n < k ? n : k;
+    uint32_t rank = 0;
+    for (uint32_t j = 0; j < n; j++) {
+        uint64_t kj = rl64(key, j);
+        uint32_t ej = rl(V, j);
+        rank += (kj < key || (kj == key && ej < V)) ? 1u : 0u;
+    }
+    if (l < n && rank < m) w.lds[rank] = V;
+    __builtin_amdgcn_wave_barrier();
+    uint32_t got = l < m ? w.lds[l] : 0u;
+    __builtin_amdgcn_wave_barrier();
+    OUT = got;
+    w.h.rng = base + n;
+    return m;
+}
+
+// ------------------------------------------------------------ emission --
+// record {dst, src, type, seq, a0, 0, 0, payload slot, 0 x 8}; the slot is
+// an arena index, not part of the message, so it is hashed as 0
+DEV void emit(Pw& w, uint32_t dst, uint32_t type, uint32_t a0, uint32_t slot) {
+    uint32_t l = lane_id();
+    uint32_t s = w.seq++;
+    uint64_t at = w.obase + s;
+    uint32_t word = l == 0 ? dst : l == 1 ? w.me : l == 2 ? type : l == 3 ? s : l == 4 ? a0
+                  : l == 7 ? slot : 0u;
+    if (l < 16) {
+        reinterpret_cast<uint32_t*>(w.a->rec_out + at)[l] = word;
+        uint32_t hw = l == 7 ? 0u : word;
+        w.digest += mix64((((uint64_t)hw) << 32 | l) ^ 0x9E3779B97F4A7C15ull);
+    }
+    if (l == 0) w.a->okey[at] = dst;     // pluggable bounds come from k_node_prep
+    st_add(w, ST_EMIT + type, 1);
+}
+
+// maybe_connect + find (partisan_util.erl:75-134): the peer runs and no
+// partition separates the two; view members answer from the cache
+DEV bool connect_ok(const Pw& w, uint32_t dst) {
+    if (dst >= w.a->n_nodes || dst == w.me) return false;
+    uint64_t m = ballot(w.CV == dst);
+    uint32_t v = m ? rl(w.CF, ffs64(m))
+                   : ((uint32_t)w.a->flags[dst] | ((uint32_t)w.a->part[dst] << 8));
+    return (v & F_UP) && (v >> 8) == w.mypart;
+}
+
+// establish_connections/3 (pl:1096-1108) connects to members and the pending
+// contact only.  The full strategy sends to members only (every target is
+// read from its own member row), so only SCAMP needs the check.
+DEV bool connected(const Pw& w, uint32_t p) {
+    if (w.a->strategy == PSIM_STRATEGY_FULL) return true;
+    return ballot(lane_id() < w.vn && w.V == p) != 0 || p == w.h.join_contact;
+}
+
+// do_send_message/7 (pl:1309-1363); success draws rand:uniform(1) in
+// partisan_util:dispatch_pid/3 (util:190-195)
+DEV void pl_send(Pw& w, uint32_t dst, uint32_t type, uint32_t a0, uint32_t slot) {
+    if (!connect_ok(w, dst) || !connected(w, dst)) { st_add(w, ST_FAIL, 1); return; }
+    w.h.rng++;
+    emit(w, dst, type, a0, slot);
+}
+
+// ---------------------------------------------------------------- full --
+// ?SET:merge/2 into the row (full:49-55, :99-116); returns ?SET:equal/2 of
+// the two states before it
+DEV bool full_merge(Pw& w, const uint32_t* p) {
+    const uint32_t fw = w.a->fw;
+    bool neq = false, chg = false;
+    for (uint32_t base = 0; base < fw; base += 256) {
+        uint32_t i = base + 4 * lane_id();
+        if (i < fw) {
+            uint4 o = *reinterpret_cast<const uint4*>(w.row + i);
+            uint4 q = *reinterpret_cast<const uint4*>(p + i);
+            neq |= (o.x != q.x) | (o.y != q.y) | (o.z != q.z) | (o.w != q.w);
+            uint4 m = make_uint4(o.x | q.x, o.y | q.y, o.z | q.z, o.w | q.w);
+            if (m.x != o.x || m.y != o.y || m.z != o.z || m.w != o.w) {
+                *reinterpret_cast<uint4*>(w.row + i) = m;
+                chg = true;
+            }
+        }
+    }
+    if (ballot(chg)) w.dirty = true;
+    return ballot(neq) == 0;
+}
+
+DEV uint32_t full_count(const Pw& w) {
+    const uint32_t fw = w.a->fw;
+    uint32_t c = 0;
+    for (uint32_t base = 0; base < fw; base += 256) {
+        uint32_t i = base + 4 * lane_id();
+        if (i < fw) {
+            uint4 o = *reinterpret_cast<const uint4*>(w.row + i);
+            c += __popc(o.x) + __popc(o.y) + __popc(o.z) + __popc(o.w);
+        }
+    }
+    return uni(wave_sum(c));
+}
+
+// the k-th (0-based) member in id order
+DEV uint32_t full_nth(const Pw& w, uint32_t k) {
+    const uint32_t fw = w.a->fw;
+    const uint32_t l = lane_id();
+    for (uint32_t base = 0; base < fw; base += 256) {
+        uint32_t i = base + 4 * l;
+        uint4 o = i < fw ? *reinterpret_cast<const uint4*>(w.row + i) : make_uint4(0, 0, 0, 0);
+        uint32_t inc = __popc(o.x) + __popc(o.y) + __popc(o.z) + __popc(o.w);
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            uint32_t t = (uint32_t)__shfl_up((int)inc, off);
+            if (l >= (uint32_t)off) inc += t;
+        }
+        uint32_t tot = rl(inc, 63);
+        if (k < tot) {
+            int L = ffs64(ballot(inc > k));
+            uint32_t kk = k - (L ? rl(inc, L - 1) : 0u);
+            uint32_t ws[4] = {rl(o.x, L), rl(o.y, L), rl(o.z, L), rl(o.w, L)};
+            for (int j = 0; j < 4; j++) {
+                uint32_t pc = __popc(ws[j]);
+                if (kk < pc) {
+                    uint32_t x = ws[j];
+                    for (; kk; kk--) x &= x - 1;
+                    return (base + 4 * (uint32_t)L + (uint32_t)j) * 32 + (uint32_t)(__ffs(x) - 1);
+                }
+                kk -= pc;
+            }
+        }
+        k -= tot;
+    }
+    return NONE;
+}
+
+// a snapshot of the state for the messages of one gossip: one arena slot per
+// distinct state the node sends this round
+DEV uint32_t full_snapshot(Pw& w) {
+    if (w.snap != NONE && !w.dirty) return w.snap;
+    uint32_t s = 0;
+    if (lane_id() == 0) s = atomicAdd(w.a->pay_top, 1u);
+    s = rl(s, 0);
+    if (s >= w.a->pay_cap) { st_add(w, ST_OVF, 1); s = w.a->pay_cap - 1; }
+    const uint32_t fw = w.a->fw;
+    uint32_t* dst = w.a->pay_out + (size_t)s * fw;
+    for (uint32_t base = 0; base < fw; base += 256) {
+        uint32_t i = base + 4 * lane_id();
+        if (i < fw) *reinterpret_cast<uint4*>(dst + i) = *reinterpret_cast<const uint4*>(w.row + i);
+    }
+    w.snap = s;
+    w.dirty = false;
+    return s;
+}
+
+// gossip_messages/1 (full:127-144) to every member (fanout 0), or to
+// `fanout` members each drawn as rand:uniform(length(Members)) -- config B's
+// extension, coalesced to one gossip per round.  The
+// whole list is built before the manager sends any of it.
+DEV void full_gossip(Pw& w) {
+    uint32_t slot = full_snapshot(w), cnt = full_count(w);
+    const uint32_t fw = w.a->fw;
+    if (w.a->fanout == 0) {
+        for (uint32_t base = 0; base < fw; base += 256) {
+            uint32_t i = base + 4 * lane_id();
+            uint4 o = i < fw ? *reinterpret_cast<const uint4*>(w.row + i) : make_uint4(0, 0, 0, 0);
+            for (uint64_t nz = ballot((o.x | o.y | o.z | o.w) != 0); nz; nz &= nz - 1) {
+                int L = ffs64(nz);
+                uint32_t ws[4] = {rl(o.x, L), rl(o.y, L), rl(o.z, L), rl(o.w, L)};
+                for (int j = 0; j < 4; j++)
+                    for (uint32_t x = ws[j]; x; x &= x - 1)
+                        pl_send(w, (base + 4 * (uint32_t)L + (uint32_t)j) * 32 + (uint32_t)(__ffs(x) - 1),
+                                PSIM_PL_GOSSIP, cnt, slot);
+            }
+        }
+        return;
+    }
+    uint32_t TG = 0;
+    for (uint32_t i = 0; i < w.a->fanout; i++) {
+        uint32_t t = full_nth(w, uniform_n(w, cnt) - 1);
+        TG = lane_id() == i ? t : TG;
+    }
+    for (uint32_t i = 0; i < w.a->fanout; i++) pl_send(w, rl(TG, i), PSIM_PL_GOSSIP, cnt, slot);
+}
+
+// --------------------------------------------------------------- scamp --
+// sets:add_element/2 (v1, sets:to_list order) or [E | L] (v2) into a fixed table
+DEV void scamp_add(Pw& w, uint32_t& L, uint32_t& n, uint32_t e, bool as_set) {
+    if (as_set && has(L, n, e)) return;
+    if (n >= PSIM_SVIEW_CAP) { st_add(w, ST_OVF, 1); return; }
+    if (as_set) view_add(L, n, e);
+    else vins(L, n, 0, e);
+}
+
+// Strategy:join/3 at the joiner (sv1:52-99, sv2:64-113)
+DEV void scamp_join(Pw& w, uint32_t contact) {
+    const bool v1 = w.a->strategy == PSIM_STRATEGY_SCAMP_V1;
+    const uint32_t M0 = w.V, n0 = w.vn;
+    scamp_add(w, w.V, w.vn, contact, v1);
+    uint32_t SEL = 0;
+    uint32_t ns = sublist(w, M0, n0, v1 ? w.a->scamp_c : w.a->scamp_c - 1, SEL);
+    pl_send(w, contact, PSIM_PL_FWD_SUB, w.me, NONE);
+    for (uint32_t i = 0; i < n0; i++)            // v1: sets:fold/3 = reverse of to_list
+        pl_send(w, rl(M0, v1 ? n0 - 1 - i : i), PSIM_PL_FWD_SUB, contact, NONE);
+    for (uint32_t i = 0; i < ns; i++) pl_send(w, rl(SEL, i), PSIM_PL_FWD_SUB, contact, NONE);
+}
+
+// periodic/1 (sv1:125-174, sv2:130-178); "isolated" = a ping was received
+// and not this round (App. A Q12: 100000 us against 1-s rounds)
+DEV void scamp_periodic(Pw& w) {
+    const uint32_t M = w.V, n = w.vn;
+    const bool isolated = w.h.pt_root != NONE && w.round > w.h.pt_root;
+    if (isolated) {
+        uint32_t SEL = 0;
+        if (sublist(w, M, n, 1, SEL)) pl_send(w, rl(SEL, 0), PSIM_PL_FWD_SUB, w.me, NONE);
+    }
+    for (uint32_t i = 0; i < n; i++) pl_send(w, rl(M, i), PSIM_PL_PING, w.me, NONE);
+}
+
+// handle_message(.., {forward_subscription, Node}) (sv1:212-252, sv2:284-327)
+DEV void scamp_fwd(Pw& w, uint32_t node) {
+    const bool v1 = w.a->strategy == PSIM_STRATEGY_SCAMP_V1;
+    const uint32_t rnd = uniform_n(w, 10) >= 5 ? 1u : 0u;    // random_0_or_1/0 sv1:272-279
+    if (rnd == 0 && !has(w.V, w.vn, node)) {
+        scamp_add(w, w.V, w.vn, node, v1);
+        if (!v1) pl_send(w, node, PSIM_PL_KEEP_SUB, w.me, NONE);
+        return;
+    }
+    uint32_t SEL = 0;
+    if (sublist(w, w.V, w.vn, 1, SEL)) pl_send(w, rl(SEL, 0), PSIM_PL_FWD_SUB, node, NONE);
+}
+
+// -------------------------------------------------------------- driver --
+DEV void pl_handle(Pw& w, uint32_t type, uint32_t src, uint32_t a0, uint32_t slot) {
+    const bool full = w.a->strategy == PSIM_STRATEGY_FULL;
+    switch (type) {
+    case PSIM_PL_HELLO:            // server: {state, Tag, get_local_state()} server:125-148
+        if (!connect_ok(w, src)) { st_add(w, ST_FAIL, 1); break; }
+        if (full) {
+            uint32_t cnt = full_count(w);
+            emit(w, src, PSIM_PL_STATE, cnt, full_snapshot(w));
+        } else {
+            emit(w, src, PSIM_PL_STATE, 0, NONE);
+        }
+        break;
+    case PSIM_PL_STATE:            // handle_info({connected, ..}) pl:986-1044
+        if (w.h.join_contact != src) break;
+        w.h.join_contact = NONE;
+        if (full) {                // join/3 full:49-55
+            full_merge(w, w.a->pay_in + (size_t)slot * w.a->fw);
+            if (w.a->fanout) w.gossip_due = true;
+            else full_gossip(w);
+        } else {
+            scamp_join(w, src);
+        }
+        break;
+    case PSIM_PL_GOSSIP:           // handle_message/2 full:99-116
+        if (!full) break;
+        if (!full_merge(w, w.a->pay_in + (size_t)slot * w.a->fw)) {
+            if (w.a->fanout) w.gossip_due = true;
+            else full_gossip(w);
+        }
+        break;
+    case PSIM_PL_FWD_SUB:
+        if (!full) scamp_fwd(w, a0);
+        break;
+    case PSIM_PL_PING:             // sv1:177-188, sv2:181-191
+        if (!full) w.h.pt_root = w.round;
+        break;
+    case PSIM_PL_KEEP_SUB:         // sv2:328-338: InView = [Node | InView0]
+        if (w.a->strategy == PSIM_STRATEGY_SCAMP_V2) scamp_add(w, w.I, w.in_n, a0, false);
+        break;
+    default:
+        break;
+    }
+}
+
+DEV uint32_t load_chunk(const RoundArgs& a, uint32_t ib, uint32_t ik, uint32_t c) {
+    uint32_t l = lane_id();
+    return (c + (l >> 4) < ik) ? reinterpret_cast<const uint32_t*>(a.rec_in + ib + c + (l >> 4))[l & 15]
+                               : 0u;
+}
+
+DEV void process_pl(Pw& w, uint32_t n, uint32_t ib, uint32_t ik, uint32_t ob) {
+    const RoundArgs& a = *w.a;
+    const uint32_t l = lane_id();
+    const uint32_t li = n - a.lo;
+    const uint32_t r = a.round;
+    {
+        uint32_t H = l < 16 ? reinterpret_cast<const uint32_t*>(a.hdr + li)[l] : 0u;
+        uint32_t* hw = reinterpret_cast<uint32_t*>(&w.h);
+#pragma unroll
+        for (int k = 0; k < 16; k++) hw[k] = rl(H, k);
+    }
+    w.me = n; w.li = li;
+    w.mypart = a.part[n];
+    if (w.h.start_round == r && ik) { st_add(w, ST_DROPPED, ik); ik = 0; }
+    const bool hello = w.h.join_contact != NONE && !w.h.have;
+    const bool periodic = a.periodic > 0 && r > w.h.start_round && ((r - w.h.start_round) % a.periodic) == 0;
+    if (!(ik || hello || periodic)) return;
+    st_add(w, ST_PROC, 1);
+    const bool full = a.strategy == PSIM_STRATEGY_FULL;
+    w.vn = w.h.act_n; w.in_n = w.h.pas_n;
+    w.V = full ? 0u : a.sview[(size_t)li * PSIM_SVIEW_CAP + l];
+    w.I = a.strategy == PSIM_STRATEGY_SCAMP_V2 ? a.sinv[(size_t)li * PSIM_SVIEW_CAP + l] : 0u;
+    const uint32_t V0 = w.V, I0 = w.I;
+    w.CV = l < w.vn ? w.V : NONE;
+    w.CF = w.CV < a.n_nodes ? ((uint32_t)a.flags[w.CV] | ((uint32_t)a.part[w.CV] << 8)) : 0u;
+    w.row = full ? a.fbits + (size_t)li * a.fw : nullptr;
+    w.seq = 0; w.obase = ob;
+    w.snap = NONE; w.dirty = false; w.gossip_due = false;
+    w.dc_base = NONE64;
+
+    if (hello) {                   // internal_join/3 -> connect + hello (pl:1423-1458)
+        if (connect_ok(w, w.h.join_contact)) {
+            emit(w, w.h.join_contact, PSIM_PL_HELLO, 0, NONE);
+            w.h.have = 1;
+        } else {
+            st_add(w, ST_FAIL, 1);
+        }
+    }
+    for (uint32_t c = 0; c < ik; c += 4) {
+        uint32_t R4 = load_chunk(a, ib, ik, c);
+        uint32_t cm = ik - c < 4 ? ik - c : 4;
+        for (uint32_t q = 0; q < cm; q++) {
+            uint32_t b = q * 16;
+            uint32_t type = rl(R4, b + 2) & 0xFF;
+            st_add(w, ST_DELIV + type, 1);
+            pl_handle(w, type, rl(R4, b + 1), rl(R4, b + 4), rl(R4, b + 7));
+        }
+    }
+    if (periodic) {                // handle_info(periodic) pl:881-903
+        if (full) w.gossip_due = true;
+        else scamp_periodic(w);
+    }
+    if (w.gossip_due) full_gossip(w);
+
+    // ---- write back
+    w.h.act_n = (uint8_t)w.vn; w.h.pas_n = (uint8_t)w.in_n;
+    if (!full && ballot(w.V != V0)) a.sview[(size_t)li * PSIM_SVIEW_CAP + l] = w.V;
+    if (a.strategy == PSIM_STRATEGY_SCAMP_V2 && ballot(w.I != I0))
+        a.sinv[(size_t)li * PSIM_SVIEW_CAP + l] = w.I;
+    {
+        const uint32_t* hw = reinterpret_cast<const uint32_t*>(&w.h);
+        uint32_t v = 0;
+#pragma unroll
+        for (int k = 0; k < 16; k++) v = l == (uint32_t)k ? hw[k] : v;
+        if (l < 16) reinterpret_cast<uint32_t*>(a.hdr + li)[l] = v;
+    }
+    if (l == 0) a.ocnt[li] = w.seq;
+}
+
+}  // namespace
+
+__global__ void __launch_bounds__(256) k_consume_pl(RoundArgs args) {
+    __shared__ uint64_t sst[NST];
+    __shared__ uint32_t scratch[PL_WAVES][64];
+    for (int i = threadIdx.x; i < NST; i += blockDim.x) sst[i] = 0;
+    __syncthreads();
+    const uint32_t wid = threadIdx.x >> 6;
+    const uint32_t gw = uni(blockIdx.x * PL_WAVES + wid);
+    const uint32_t nw = gridDim.x * PL_WAVES;
+    Pw w;
+    w.a = &args;
+    w.lds = scratch[wid];
+    w.round = args.round;
+    w.SC = 0;
+    w.digest = 0;
+    const uint32_t na = *args.n_alist;
+    for (uint32_t k = gw; k < na; k += nw) {
+        const uint4 d = args.desc[k];
+        process_pl(w, uni(d.x), uni(d.y), uni(d.z), uni(d.w));
+    }
+    {
+        uint32_t l = lane_id();
+        if (l < NST && w.SC) atomicAdd((unsigned long long*)&sst[l], (unsigned long long)w.SC);
+        uint64_t d = w.digest;
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) d += shfl64(d, (int)((l + off) & 63));
+        if (l == 0 && d) atomicAdd((unsigned long long*)&sst[ST_DIGEST], (unsigned long long)d);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < NST; i += blockDim.x)
+        args.stat_part[(size_t)blockIdx.x * NST + i] = sst[i];
+}
+
+}  // namespace psim

@@ -30,6 +30,9 @@ def default_config(**kw):
     cfg.device, cfg.n_shards, cfg.shard_rank, cfg.shard_world = -1, 1, 0, 1
     cfg.comm_id = None
     cfg.max_msgs_per_round = 0
+    # pluggable manager (partisan_config.erl:129-130, partisan.hrl:31)
+    cfg.manager, cfg.strategy = _abi.MANAGER_HYPARVIEW, _abi.STRATEGY_FULL
+    cfg.periodic_interval, cfg.scamp_c, cfg.fanout = 10, 5, 0
     for k, v in kw.items():
         if not hasattr(cfg, k):
             raise KeyError(k)
@@ -133,6 +136,31 @@ class _Driver:
                 extra(r)
             stats.append(self.step(1))
         return np.concatenate(stats) if stats else np.zeros(0, _abi.STATS_DTYPE)
+
+    # ---- pluggable manager state (get_local_state/0, members/0)
+    def strategy_nodes(self, first=0, count=None):
+        if count is None:
+            count = self.n - first
+        out = np.zeros(count, _abi.STRATEGY_VIEW_DTYPE)
+        self._check(self._api["get_strategy_nodes"](
+            self._h, first, count, out.ctypes.data_as(C.POINTER(_abi.PsimStrategyView))),
+            "get_strategy_nodes")
+        return out
+
+    def member_bits(self, node):
+        w = np.zeros((self.n + 31) // 32, np.uint32)
+        self._check(self._api["get_member_bits"](self._h, node, _abi.u32p(w), w.size),
+                    "get_member_bits")
+        return w
+
+    def members(self, node):
+        """membership_list/1 of a node: full -> ids of query(ORSet) in id order;
+        scamp -> the view in its list order"""
+        if self.cfg.strategy == _abi.STRATEGY_FULL:
+            w = self.member_bits(node)
+            return [int(i) for i in np.nonzero(np.unpackbits(w.view(np.uint8), bitorder="little"))[0]]
+        v = self.strategy_nodes(node, 1)[0]
+        return [int(x) for x in v["view"][: v["view_n"]]]
 
     # ---- reference-style debug getters (hyparview:261-281)
     def active(self, node):

@@ -82,6 +82,37 @@ def star(make, n=512, seed=3, rounds=60):
     return sim, np.concatenate([st, st2])
 
 
+def pl_doubling(make, n, seed, rounds, strategy, fanout=0, crash_at=None, part_at=None, **cfg):
+    """The pluggable manager with one membership strategy (SURVEY 8(a)
+    s1-s4): doubling bootstrap, then optional crashes (scamp: 10% of the
+    nodes, restarted and rejoined 5 rounds later; full: not restarted) and a
+    half/half partition for 10 rounds."""
+    sim = make(default_config(n_nodes=n, seed=seed, manager=1, strategy=strategy, fanout=fanout, **cfg))
+    rng = np.random.Generator(np.random.PCG64([seed, 7]))
+    victims = np.sort(rng.choice(np.arange(1, n, dtype=np.uint32), size=max(1, n // 10),
+                                 replace=False)).astype(np.uint32)
+
+    def hook(r):
+        if crash_at is not None and r == crash_at:
+            sim.crash(victims)
+        if crash_at is not None and r == crash_at + 5 and strategy != 0:
+            sim.join(victims, np.zeros(victims.size, np.uint32))
+        if part_at is not None and r == part_at:
+            sim.set_partition(W.half_partition(n))
+        if part_at is not None and r == part_at + 10:
+            sim.clear_partition()
+    st = sim.run_schedule(W.doubling_join(n, seed), rounds, extra=hook)
+    return sim, st
+
+
+def compare_strategy(a, b, full_bits=None):
+    """strategy_nodes() of two backends; for the full strategy also the
+    member bitsets of the nodes in full_bits"""
+    compare_nodes(a.strategy_nodes(), b.strategy_nodes())
+    for node in (full_bits or []):
+        assert np.array_equal(a.member_bits(node), b.member_bits(node)), node
+
+
 def compare_stats(a, b):
     assert a.shape == b.shape
     for f in STAT_FIELDS:

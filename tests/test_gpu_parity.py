@@ -124,3 +124,29 @@ def test_shard_invariance_64k():
     (a, ast), (b, bst) = run(g1), run(g4)
     S.compare_stats(ast, bst)
     S.compare_nodes(a.nodes(), b.nodes())
+
+
+# ---- pluggable manager + membership strategies
+@pytest.mark.parametrize("strategy,n,fanout", [(0, 16, 0), (0, 2048, 5), (1, 2048, 0), (2, 2048, 0)])
+def test_strategy_parity(strategy, n, fanout):
+    (gs, gst), (os_, ost) = _both(S.pl_doubling, n, 11, 100, strategy=strategy, fanout=fanout,
+                                  crash_at=40, part_at=60)
+    S.compare_stats(gst, ost)
+    S.compare_strategy(gs, os_, full_bits=[0, 1, n // 2, n - 1] if strategy == 0 else None)
+
+
+@pytest.mark.parametrize("strategy", [1, 2])
+def test_strategy_shard_invariance(strategy):
+    def sharded(cfg):
+        cfg.n_shards = 4
+        return _gpu(cfg)
+    gs, gst = S.pl_doubling(sharded, 4096, 12, 80, strategy=strategy, crash_at=40)
+    os_, ost = S.pl_doubling(Oracle, 4096, 12, 80, strategy=strategy, crash_at=40)
+    S.compare_stats(gst, ost)
+    S.compare_strategy(gs, os_)
+
+
+def test_strategy_64k_parity():
+    (gs, gst), (os_, ost) = _both(S.pl_doubling, 1 << 16, 13, 60, strategy=2)
+    S.compare_stats(gst, ost)
+    S.compare_strategy(gs, os_)

@@ -1,0 +1,130 @@
+"""CPU tests of the pluggable-manager strategies in the oracle (SURVEY 8(a)
+s1-s4): the reference's own assertions for them, restated over the round
+model R0-P.
+
+- membership agreement (test/prop_partisan.erl:944-967): with the full
+  strategy every live node ends with the same member set, all started nodes;
+- connectivity_test / check_forward_message (test/partisan_SUITE.erl
+  :1214-1259, :1955-1994): every node's members are reachable -- the overlay
+  the SCAMP views span is connected and holds only started nodes;
+- scamp v2 keep_subscription (scamp_v2:284-338): X in in_view(Y) => Y in
+  partial_view(X).
+Parity against the Erlang modules is unpinned (no VM here)."""
+import numpy as np
+import pytest
+
+import _scenarios as S
+from _oracle import Oracle
+from partisan_amd.sim import default_config
+
+NONE = 0xFFFFFFFF
+
+
+def _views(sim):
+    v = sim.strategy_nodes()
+    return {i: [int(x) for x in v["view"][i][: v["view_n"][i]]] for i in range(len(v)) if v["up"][i]}
+
+
+def _weakly_connected(adj):
+    if not adj:
+        return True
+    und = {i: set() for i in adj}
+    for i, vs in adj.items():
+        for j in vs:
+            if j in und and j != i:
+                und[i].add(j)
+                und[j].add(i)
+    start = next(iter(und))
+    seen, stack = {start}, [start]
+    while stack:
+        x = stack.pop()
+        for y in und[x] - seen:
+            seen.add(y)
+            stack.append(y)
+    return len(seen) == len(und)
+
+
+@pytest.mark.parametrize("fanout", [0, 5])
+def test_full_membership_agreement(fanout):
+    n = 16 if fanout == 0 else 2048
+    sim, st = S.pl_doubling(Oracle, n, 3, 60, strategy=0, fanout=fanout)
+    v = sim.strategy_nodes()
+    assert (v["members"] == n).all()
+    assert len(set(v["members_hash"].tolist())) == 1
+    assert sim.members(5) == list(range(n))
+    assert st["overflow"].sum() == 0
+    # the handshake: one HELLO and one STATE per joiner
+    assert st["emitted"][:, 0].sum() == n - 1 and st["delivered"][:, 1].sum() == n - 1
+
+
+def test_full_fanout_bounds_messages():
+    n = 4096
+    sim, st = S.pl_doubling(Oracle, n, 5, 60, strategy=0, fanout=5)
+    # coalesced gossip: at most one gossip of `fanout` messages per node and round
+    assert (st["emitted"][:, 2] <= 5 * n).all()
+    assert (sim.strategy_nodes()["members"] == n).all()
+
+
+def test_full_crashed_members_stay_members():
+    """no leave: a crashed node stays in every ORSet, sends to it fail"""
+    n = 1024
+    sim, st = S.pl_doubling(Oracle, n, 4, 80, strategy=0, fanout=5, crash_at=40)
+    v = sim.strategy_nodes()
+    assert (v["members"] == n).all()
+    assert st["send_fail"][41:].sum() > 0
+
+
+def test_full_restart_rejected():
+    sim = Oracle(default_config(n_nodes=8, manager=1, strategy=0))
+    sim.join(np.array([0], np.uint32), np.array([NONE], np.uint32))
+    with pytest.raises(Exception):
+        sim.join(np.array([0], np.uint32), np.array([NONE], np.uint32))
+
+
+@pytest.mark.parametrize("strategy", [1, 2])
+def test_scamp_views_connected(strategy):
+    n = 2048
+    sim, st = S.pl_doubling(Oracle, n, 6, 120, strategy=strategy)
+    views = _views(sim)
+    assert len(views) == n
+    assert _weakly_connected(views)
+    assert all(0 <= j < n for vs in views.values() for j in vs)
+    assert all(i in vs for i, vs in views.items())      # myself() stays a member
+    assert st["overflow"].sum() == 0
+    assert (sim.strategy_nodes()["pending"] == NONE).all()
+
+
+def test_scamp_v2_in_view_consistent():
+    n = 1024
+    sim, st = S.pl_doubling(Oracle, n, 8, 100, strategy=2)
+    v = sim.strategy_nodes()
+    for y in range(n):
+        for x in v["in_view"][y][: v["in_n"][y]]:
+            assert y in v["view"][x][: v["view_n"][x]], (x, y)
+
+
+def test_scamp_v1_set_order_and_no_duplicates():
+    n = 1024
+    sim, _ = S.pl_doubling(Oracle, n, 2, 80, strategy=1)
+    from _oracle import load
+    lib = load()
+    for i, vs in _views(sim).items():
+        assert len(set(vs)) == len(vs)
+        b = [lib.orc_bucket16(x) for x in vs]
+        assert b == sorted(b), i                        # sets:to_list/1 bucket order
+
+
+@pytest.mark.parametrize("strategy", [1, 2])
+def test_scamp_churn_partition(strategy):
+    n = 1024
+    sim, st = S.pl_doubling(Oracle, n, 9, 120, strategy=strategy, crash_at=50, part_at=70)
+    assert st["send_fail"].sum() > 0
+    v = sim.strategy_nodes()
+    assert v["up"].all()
+    assert _weakly_connected(_views(sim))
+
+
+def test_pluggable_rejects_broadcast():
+    sim = Oracle(default_config(n_nodes=8, manager=1, strategy=1))
+    with pytest.raises(Exception):
+        sim.broadcast(0, 1)
