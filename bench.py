@@ -32,6 +32,9 @@ def parse():
     p.add_argument("--cpu-sample-nodes", type=int, default=1 << 16)
     p.add_argument("--cpu-sample-rounds", type=int, default=40)
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--workload", default="C", choices=["C", "B", "D"],
+                   help="C (default, the headline line): HyParView+Plumtree; "
+                        "B: full-membership strategy, fanout 5; D: SCAMP v2 (c=5)")
     return p.parse_args()
 
 
@@ -64,8 +67,65 @@ def cpu_baseline(args):
                       f"rounds after a doubling bootstrap, broadcast every 10 rounds, 1 thread"}
 
 
+def main_strategy(args):
+    """Configs B and D of BASELINE.json on the pluggable manager (extra
+    lines, not the driver's headline): a step is one round over every node.
+    B: partisan_full_membership_strategy, 100k nodes, fanout 5 (the
+       extension of SURVEY App. A Q10), periodic gossip every round.
+    D: partisan_scamp_v2_membership_strategy, c = 5, 2^21 nodes per GPU."""
+    from partisan_amd import Simulator
+    from partisan_amd import workloads as W
+    from partisan_amd.sim import default_config
+    if args.workload == "B":
+        n = 100000 if args.nodes == 1 << 20 else args.nodes
+        cfg = default_config(n_nodes=n, seed=args.seed, manager=1, strategy=0, fanout=5,
+                             periodic_interval=1)
+        name = "B: full-membership strategy (ORSet bitsets), fanout 5, gossip every round"
+    else:
+        n = (1 << 21) if args.nodes == 1 << 20 else args.nodes
+        cfg = default_config(n_nodes=n, seed=args.seed, manager=1, strategy=2, scamp_c=5)
+        name = "D: SCAMP v2 (c=5), doubling bootstrap, steady state"
+    cfg.device = int(os.environ.get("PSIM_DEVICE", "0"))
+    sim = Simulator(cfg)
+    boot = W.doubling_join(n, args.seed)
+    sim.run_schedule(boot, boot[-1][0] + 1 + args.settle)
+    sim.step(args.warmup)
+    t0 = time.perf_counter()
+    st = sim.step(args.steps)
+    dt = time.perf_counter() - t0
+    kt = sim.kernel_times()
+    msgs = int(st["emitted"].sum())
+    c_ms, c_n = kt.get("consume", (0.0, 1))
+    # algorithmic bytes of the consume kernel: member-row bytes it touches
+    # (state_bytes, full) or the 64-B view row + header per processed node
+    # (scamp), plus every message record read once and written once
+    if args.workload == "B":
+        state = int(st["state_bytes"].sum())
+    else:
+        state = int(st["nodes_processed"].sum()) * 2 * (64 + 4 * 64 * 2)
+    alg = state + int(st["delivered"].sum()) * S_MSG + msgs * (S_MSG + 4)
+    achieved = alg / (c_ms / 1e3) / 1e9 if c_ms > 0 else 0.0
+    out = {
+        "metric": "simulated node-rounds/sec (+ msgs/sec), pluggable manager " + args.workload,
+        "value": n * args.steps / dt, "unit": "node-rounds/s", "msgs_per_sec": msgs / dt,
+        "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "u32", "data": "synthetic",
+        "config": {"workload": name, "nodes": n, "seed": args.seed, "parallelism": "1 GPU"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": "k_consume_pl",
+                     "alg_bytes_per_launch": alg / max(1, c_n), "avg_launch_ms": c_ms / max(1, c_n)},
+        "kernel_ms_per_step": {k: v[0] / args.steps for k, v in kt.items()},
+        "overflow": int(st["overflow"].sum()),
+        "members_min": int(sim.strategy_nodes(0, min(n, 4096))["members"].min()) if args.workload == "B" else None,
+    }
+    print(json.dumps(out), flush=True)
+
+
 def main():
     args = parse()
+    if args.workload != "C":
+        return main_strategy(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     from partisan_amd import Simulator

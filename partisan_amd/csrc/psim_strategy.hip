@@ -174,6 +174,7 @@ DEV bool full_merge(Pw& w, const uint32_t* p) {
         }
     }
     if (ballot(chg)) w.dirty = true;
+    st_add(w, ST_BYTES, 8 * fw);
     return ballot(neq) == 0;
 }
 
@@ -187,6 +188,7 @@ DEV uint32_t full_count(const Pw& w) {
             c += __popc(o.x) + __popc(o.y) + __popc(o.z) + __popc(o.w);
         }
     }
+    st_add(const_cast<Pw&>(w), ST_BYTES, 4 * fw);
     return uni(wave_sum(c));
 }
 
@@ -204,6 +206,7 @@ DEV uint32_t full_nth(const Pw& w, uint32_t k) {
             if (l >= (uint32_t)off) inc += t;
         }
         uint32_t tot = rl(inc, 63);
+        st_add(const_cast<Pw&>(w), ST_BYTES, 1024);
         if (k < tot) {
             int L = ffs64(ballot(inc > k));
             uint32_t kk = k - (L ? rl(inc, L - 1) : 0u);
@@ -239,6 +242,7 @@ DEV uint32_t full_snapshot(Pw& w) {
     }
     w.snap = s;
     w.dirty = false;
+    st_add(w, ST_BYTES, 8 * fw);
     return s;
 }
 
