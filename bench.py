@@ -32,9 +32,10 @@ def parse():
     p.add_argument("--cpu-sample-nodes", type=int, default=1 << 16)
     p.add_argument("--cpu-sample-rounds", type=int, default=40)
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--workload", default="C", choices=["C", "B", "D"],
+    p.add_argument("--workload", default="C", choices=["C", "B", "D", "E"],
                    help="C (default, the headline line): HyParView+Plumtree; "
-                        "B: full-membership strategy, fanout 5; D: SCAMP v2 (c=5)")
+                        "B: full-membership strategy, fanout 5; D: SCAMP v2 (c=5); "
+                        "E: C with 20%% churn over 100 rounds + a half/half partition")
     return p.parse_args()
 
 
@@ -124,7 +125,7 @@ def main_strategy(args):
 
 def main():
     args = parse()
-    if args.workload != "C":
+    if args.workload in ("B", "D"):
         return main_strategy(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -150,11 +151,28 @@ def main():
     sim.run_schedule(boot, boot[-1][0] + 1 + args.settle)
 
     state = {"k": 0}
+    churn = {}
+    if args.workload == "E":
+        # config E: 0.2*N crashes spread over 100 rounds, each
+        # victim restarts the next round and rejoins; ids [0, N/2) | [N/2, N)
+        # partitioned for 20 rounds from round 20 of the measured window
+        for r, v, c in W.churn_schedule(n, args.seed, 0.2, 0, 100):
+            churn[r] = (v, c)
+        part = W.half_partition(n)
 
     def round_events(i):
         if i % 10 == 0:
             sim.broadcast(0, state["k"] % 0x10000)
             state["k"] += 1
+        if args.workload == "E":
+            if i in churn:
+                sim.crash(churn[i][0])
+            if i - 1 in churn:
+                sim.join(churn[i - 1][0], churn[i - 1][1])
+            if i == 20:
+                sim.set_partition(part)
+            if i == 40:
+                sim.clear_partition()
 
     for i in range(args.warmup):
         round_events(i)
@@ -192,7 +210,8 @@ def main():
     per_launch_s = (c_ms / 1e3) / max(1, c_n)
     achieved = per_launch_bytes / per_launch_s / 1e9 if per_launch_s > 0 else 0.0
     out = {
-        "metric": "simulated node-rounds/sec (+ msgs/sec), 1M-node HyParView+Plumtree",
+        "metric": "simulated node-rounds/sec (+ msgs/sec), 1M-node HyParView+Plumtree"
+                  + ("" if args.workload == "C" else " (config E: churn + partition)"),
         "value": node_rounds / dt,
         "unit": "node-rounds/s",
         "msgs_per_sec": msgs / dt,
@@ -200,8 +219,10 @@ def main():
         "ms_per_step": dt / args.steps * 1e3,
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": "u32", "data": "synthetic",
-        "config": {"workload": "C: HyParView+Plumtree, doubling bootstrap, steady state, "
-                               "broadcast from node 0 every 10 rounds",
+        "config": {"workload": ("C: HyParView+Plumtree, doubling bootstrap, steady state, "
+                                "broadcast from node 0 every 10 rounds") if args.workload == "C" else
+                               ("E: HyParView+Plumtree, 20% churn over 100 rounds (crash, restart, rejoin), "
+                                "half/half partition for rounds 20-39, broadcast every 10 rounds"),
                    "nodes": n, "nodes_per_gpu": args.nodes, "seed": args.seed,
                    "parallelism": f"node-range sharded x{world}, RCCL all-to-all" if world > 1 else "1 GPU"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -211,7 +232,14 @@ def main():
         "kernel_ms_per_step": {k: v[0] / args.steps for k, v in kt.items()},
         "overflow": int(st["overflow"].sum()),
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if args.workload == "E":
+        lo = sim.cfg.shard_rank * args.nodes if world > 1 else 0
+        v = sim.nodes(lo, min(args.nodes, 1 << 18))       # a sample of this rank's range
+        # the second-to-last broadcast has had >= 10 rounds to spread
+        got = (v["have"] >> ((state["k"] - 2) % 32)) & 1
+        out["reliability_broadcast"] = {"msg": state["k"] - 2, "rounds": args.warmup + args.steps - 10 * (state["k"] - 2),
+                                        "delivered_fraction": float(got[v["up"] == 1].mean())}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.workload == "C":
         out["cpu_baseline"] = cpu_baseline(args)
     if rank == 0:
         print(json.dumps(out), flush=True)

@@ -11,15 +11,23 @@ def main():
     if "--kernel" in sys.argv:
         ksub = sys.argv[sys.argv.index("--kernel") + 1]
         args.remove(ksub)
+    last = None                      # only the last K dispatches (the timed rounds)
+    if "--last" in sys.argv:
+        v = sys.argv[sys.argv.index("--last") + 1]
+        last = int(v)
+        args.remove(v)
     tot = defaultdict(float)
     disp = defaultdict(set)
     for d in args:
         with open(f"{d}/run_counter_collection.csv") as f:
-            for row in csv.DictReader(f):
-                if ksub not in row["Kernel_Name"]:
-                    continue
-                tot[row["Counter_Name"]] += float(row["Counter_Value"])
-                disp[row["Counter_Name"]].add(row["Dispatch_Id"])
+            rows = [r for r in csv.DictReader(f) if ksub in r["Kernel_Name"]]
+        if last:
+            ids = sorted({int(r["Dispatch_Id"]) for r in rows})[-last:]
+            keep = set(ids)
+            rows = [r for r in rows if int(r["Dispatch_Id"]) in keep]
+        for row in rows:
+            tot[row["Counter_Name"]] += float(row["Counter_Value"])
+            disp[row["Counter_Name"]].add(row["Dispatch_Id"])
     for k in sorted(tot):
         n = len(disp[k])
         print(f"{k:24s} total {tot[k]:.4g}  per-dispatch {tot[k] / n:.4g}  ({n} dispatches)")

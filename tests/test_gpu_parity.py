@@ -150,3 +150,27 @@ def test_strategy_64k_parity():
     (gs, gst), (os_, ost) = _both(S.pl_doubling, 1 << 16, 13, 60, strategy=2)
     S.compare_stats(gst, ost)
     S.compare_strategy(gs, os_)
+
+
+def test_gpu_matches_committed_oracle_traces():
+    """The GPU engine against tests/golden/oracle_traces.json directly (the
+    committed per-round digests of the oracle scenarios)."""
+    import json
+    import os
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, os.path.join(here, "golden"))
+    import gen_oracle_traces as G
+    golden = json.load(open(os.path.join(here, "golden", "oracle_traces.json")))["traces"]
+    scen = {
+        "config_a": lambda: S.config_a(_gpu),
+        "churn_partition_1024": lambda: S.churn_partition(_gpu, n=1024),
+        "full_16_fanout0": lambda: S.pl_doubling(_gpu, 16, 11, 80, strategy=0, fanout=0, crash_at=40),
+        "full_1024_fanout5": lambda: S.pl_doubling(_gpu, 1024, 11, 80, strategy=0, fanout=5, part_at=50),
+        "scamp_v1_1024": lambda: S.pl_doubling(_gpu, 1024, 11, 100, strategy=1, crash_at=40, part_at=60),
+        "scamp_v2_1024": lambda: S.pl_doubling(_gpu, 1024, 11, 100, strategy=2, crash_at=40, part_at=60),
+    }
+    assert set(scen) == set(G.SCENARIOS)
+    for name, run in scen.items():
+        _, st = run()
+        assert [int(x) for x in st["digest"]] == golden[name]["digest"], name
