@@ -293,10 +293,13 @@ DEV bool valid_disconnect(Wv& w, uint32_t p, uint32_t d) { // hv:1642-1653
 
 // ------------------------------------------------------- view updates --
 DEV void add_to_passive(Wv& w, uint32_t p) {             // hv:1423-1448
-    if (p == w.me || has(w.A, w.act_n, p) || has(w.P, w.pas_n, p)) return;
+    uint32_t l = lane_id();
+    if (p == w.me || ballot((l < w.act_n && w.A == p) || (l < w.pas_n && w.P == p))) return;
     if (w.pas_n >= w.a->max_passive) {
-        uint32_t r = select_random(w, w.P, w.pas_n, w.me, w.me, w.me);
-        if (r != NONE) vdel_val(w.P, w.pas_n, r);
+        // select_random(Passive, [Myself]): Myself is never in Passive (no
+        // path inserts it), so the index draw addresses Passive directly
+        uint32_t k = uniform_n(w, w.pas_n) - 1;
+        vdel(w.P, w.pas_n, k);
     }
     view_add(w.P, w.pas_n, p);
 }
@@ -665,7 +668,7 @@ DEV uint32_t load_chunk(const RoundArgs& a, uint32_t ib, uint32_t ik, uint32_t c
 // Only vector loads (vmcnt, in order): a scalar load in flight would hold
 // up every LDS operation of the node being processed (lgkmcnt).
 struct NodeIn {
-    uint32_t n, ib, ik, ob;
+    uint32_t n, ib, ik, ob, tf;    // tf: due timers (DESC_* bits, k_desc)
     uint32_t H;                 // header word l in lane l < 16
     uint32_t A, P, R0;
     uint32_t fl, part;
@@ -679,7 +682,7 @@ DEV uint32_t load_desc(const RoundArgs& a, uint32_t k) {
 DEV NodeIn load_node(const RoundArgs& a, uint32_t D) {
     uint32_t l = lane_id();
     NodeIn x;
-    x.n = rl(D, 0); x.ib = rl(D, 1); x.ik = rl(D, 2); x.ob = rl(D, 3);
+    x.n = rl(D, 0); x.ib = rl(D, 1); x.ik = rl(D, 2) & DESC_CNT_MASK; x.tf = rl(D, 2) >> 28; x.ob = rl(D, 3);
     const uint32_t li = x.n - a.lo;
     x.H = l < 16 ? reinterpret_cast<const uint32_t*>(a.hdr + li)[l] : 0u;
     x.A = l < PSIM_ACTIVE_CAP ? a.act[(size_t)li * PSIM_ACTIVE_CAP + l] : 0u;
@@ -714,10 +717,10 @@ DEV void process(Wv& w, const NodeIn& x) {
         st_add(w, ST_DROPPED, ik);
         ik = 0;
     }
-    bool promo = a.random_promotion && timer_due(a.promotion_period, r, w.h.start_round);
-    bool shuf = timer_due(a.shuffle_period, r, w.h.start_round);
+    bool promo = (x.tf & DESC_PROMO) != 0;
+    bool shuf = (x.tf & DESC_SHUFFLE) != 0;
     bool origin = a.origin_now && a.origin_node == n && a.plumtree;
-    bool lazy_due = a.plumtree && timer_due(a.lazy_tick_period, r, w.h.start_round);
+    bool lazy_due = (x.tf & DESC_LAZY) != 0;
     bool lazy = lazy_due && w.h.out_n > 0;
     bool joining = w.h.start_round == r && w.h.join_contact != NONE;
     w.act_n = w.h.act_n;

@@ -68,6 +68,11 @@ constexpr uint32_t BOUND_LAZY = PSIM_PT_OUT_CAP;          // IHAVEs of entries a
 static_assert(2 * PSIM_PT_SET_CAP - 1 < 32, "max_emit must fit the 5-bit key field");
 constexpr uint32_t BOUND_ORIGIN = 2 * PSIM_PT_SET_CAP;    // eager push + lazy adds of the root
 
+// work descriptor (id, inbox begin, inbox count | due timers << 28, outbox
+// base): the timers k_desc found due this round for the node
+constexpr uint32_t DESC_CNT_MASK = (1u << 28) - 1;
+enum : uint32_t { DESC_PROMO = 1, DESC_SHUFFLE = 2, DESC_LAZY = 4 };
+
 // stats slots in the per-block partial arrays
 enum {
     ST_EMIT = 0, ST_DELIV = 16, ST_DROPPED = 32, ST_UP, ST_PROC, ST_EXITS, ST_FAIL, ST_FIRST,

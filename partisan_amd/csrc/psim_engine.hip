@@ -213,14 +213,20 @@ __global__ void k_node_prep(RoundArgs a, const uint32_t* bsum, uint64_t* bound, 
     }
 }
 
-// work descriptors of the active list: every address k_consume needs first
+// work descriptors of the active list: every address k_consume needs first,
+// and which of the node's timers are due (hv:542-607, pt:341-345)
 __global__ void k_desc(const uint32_t* __restrict__ alist, const uint32_t* __restrict__ nact,
                        const uint32_t* __restrict__ in_beg, const uint32_t* __restrict__ cnt,
-                       const uint64_t* __restrict__ obase, uint32_t lo, uint4* __restrict__ desc) {
+                       const uint64_t* __restrict__ obase, const uint32_t* __restrict__ start,
+                       RoundArgs a, uint4* __restrict__ desc) {
     const uint32_t na = *nact;
     for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < na; k += gridDim.x * blockDim.x) {
-        uint32_t n = alist[k], li = n - lo;
-        desc[k] = make_uint4(n, in_beg[li], cnt[li], (uint32_t)obase[li]);
+        uint32_t n = alist[k], li = n - a.lo;
+        uint32_t st = start[li], r = a.round;
+        uint32_t tf = (a.random_promotion && due(a.promotion_period, r, st) ? DESC_PROMO : 0u) |
+                      (due(a.shuffle_period, r, st) ? DESC_SHUFFLE : 0u) |
+                      (a.plumtree && due(a.lazy_tick_period, r, st) ? DESC_LAZY : 0u);
+        desc[k] = make_uint4(n, in_beg[li], cnt[li] | (tf << 28), (uint32_t)obase[li]);
     }
 }
 
@@ -522,12 +528,13 @@ int phase_events_prepare(psim_handle* h, Shard* s, const RoundCtl& ctl, RoundArg
         }
         TRY(scan_excl(s, s->cnt.p, s->in_beg.p, n));
         TRY(scan_excl(s, s->bound.p, s->obase.p, n));
+        if (s->m_in > DESC_CNT_MASK) return PSIM_ENOMEM;   // per-node inbox counts must fit 28 bits
         uint64_t total = read1(s, s->bound.p + (n - 1)) + read1(s, s->obase.p + (n - 1));
         if (total >= 0xFFFFFFFFull) return PSIM_ENOMEM;
         TRY(s->outbox.ensure(total + 1));
         TRY(s->okey.ensure(total + 1));
         k_desc<<<std::min<uint32_t>(grid_for(n), 4096), BLK, 0, s->stream>>>(
-            s->alist.p, s->d_nact.p, s->in_beg.p, s->cnt.p, s->obase.p, s->lo, s->desc.p);
+            s->alist.p, s->d_nact.p, s->in_beg.p, s->cnt.p, s->obase.p, s->start.p, a, s->desc.p);
     }
     a.in_beg = s->in_beg.p;
     a.desc = s->desc.p; a.n_alist = s->d_nact.p;
@@ -799,7 +806,11 @@ int shard_alloc(psim_handle* h, Shard* s) {
             if (h->cfg.strategy == PSIM_STRATEGY_SCAMP_V2) rc |= s->sinv.alloc(n * PSIM_SVIEW_CAP);
         }
     }
-    return rc ? PSIM_ENOMEM : PSIM_OK;
+    if (rc) return PSIM_ENOMEM;
+    // the zero fills above run on the null stream, which a non-blocking
+    // stream does not wait for: finish them before any kernel of the shard
+    HIP_TRY(hipDeviceSynchronize());
+    return PSIM_OK;
 }
 
 void shard_free(Shard* s) {

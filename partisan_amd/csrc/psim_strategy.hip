@@ -462,7 +462,7 @@ __global__ void __launch_bounds__(256) k_consume_pl(RoundArgs args) {
     const uint32_t na = *args.n_alist;
     for (uint32_t k = gw; k < na; k += nw) {
         const uint4 d = args.desc[k];
-        process_pl(w, uni(d.x), uni(d.y), uni(d.z), uni(d.w));
+        process_pl(w, uni(d.x), uni(d.y), uni(d.z) & DESC_CNT_MASK, uni(d.w));
     }
     {
         uint32_t l = lane_id();

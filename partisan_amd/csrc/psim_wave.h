@@ -90,19 +90,32 @@ DEV uint32_t mod58(uint64_t v, uint32_t n) {
 // v mod n for n in [1, 64]: Horner over 15-bit digits; each digit step
 // x = r * 2^15 + d < 2^21 divides by a v_rcp_f32 reciprocal, whose error
 // moves the truncated quotient by at most one, fixed by one correction.
+// ceil(2^32 / n) for 2 <= n <= 64: for x < 2^26, x / n = mul_hi(x, M) exactly
+// (the error x * (M - 2^32/n) / 2^32 < 1/64 never crosses an integer)
+__constant__ const uint32_t kMagic[65] = {
+    0x00000000u, 0x00000000u, 0x80000000u, 0x55555556u, 0x40000000u, 0x33333334u, 0x2AAAAAABu, 0x24924925u,
+    0x20000000u, 0x1C71C71Du, 0x1999999Au, 0x1745D175u, 0x15555556u, 0x13B13B14u, 0x12492493u, 0x11111112u,
+    0x10000000u, 0x0F0F0F10u, 0x0E38E38Fu, 0x0D79435Fu, 0x0CCCCCCDu, 0x0C30C30Du, 0x0BA2E8BBu, 0x0B21642Du,
+    0x0AAAAAABu, 0x0A3D70A4u, 0x09D89D8Au, 0x097B425Fu, 0x0924924Au, 0x08D3DCB1u, 0x08888889u, 0x08421085u,
+    0x08000000u, 0x07C1F07Du, 0x07878788u, 0x07507508u, 0x071C71C8u, 0x06EB3E46u, 0x06BCA1B0u, 0x06906907u,
+    0x06666667u, 0x063E7064u, 0x06186187u, 0x05F417D1u, 0x05D1745Eu, 0x05B05B06u, 0x0590B217u, 0x0572620Bu,
+    0x05555556u, 0x0539782Au, 0x051EB852u, 0x05050506u, 0x04EC4EC5u, 0x04D4873Fu, 0x04BDA130u, 0x04A7904Bu,
+    0x04924925u, 0x047DC120u, 0x0469EE59u, 0x0456C798u, 0x04444445u, 0x04325C54u, 0x04210843u, 0x04104105u,
+    0x04000000u,
+};
+
+// v mod n for a 58-bit v and 1 <= n <= 64: Horner over an 18-bit and two
+// 20-bit digits, each step x = r * 2^20 + d < 2^26 divided by one mul_hi;
+// all operands are wave-uniform, so this runs on the SALU
 DEV uint32_t mod_small(uint64_t v, uint32_t n) {
-    const float rn = __builtin_amdgcn_rcpf((float)n);
-    uint32_t r = 0;
-#pragma unroll
-    for (int sh = 45; sh >= 0; sh -= 15) {
-        uint32_t x = (r << 15) | (uint32_t)((v >> sh) & 0x7FFFu);
-        uint32_t q = (uint32_t)((float)x * rn);
-        int32_t rr = (int32_t)(x - q * n);
-        rr = rr < 0 ? rr + (int32_t)n : rr;
-        rr = rr >= (int32_t)n ? rr - (int32_t)n : rr;
-        r = (uint32_t)rr;
-    }
-    return r;
+    if (n == 1) return 0;
+    const uint32_t M = kMagic[n];
+    uint32_t x = (uint32_t)(v >> 40);
+    uint32_t r = x - __umulhi(x, M) * n;
+    x = (r << 20) | (uint32_t)((v >> 20) & 0xFFFFFu);
+    r = x - __umulhi(x, M) * n;
+    x = (r << 20) | (uint32_t)(v & 0xFFFFFu);
+    return x - __umulhi(x, M) * n;
 }
 
 }  // namespace psim

@@ -23,9 +23,9 @@ def _both(fn, *a, **kw):
 
 
 def test_gpu_loads_native_library():
-    from partisan_amd import _lib
+    from partisan_amd import _abi, _lib
     lib = _lib.load()
-    assert lib.psim_abi_version() == 1
+    assert lib.psim_abi_version() == _abi.PSIM_ABI_VERSION
 
 
 def test_config_a_parity():
@@ -173,4 +173,6 @@ def test_gpu_matches_committed_oracle_traces():
     assert set(scen) == set(G.SCENARIOS)
     for name, run in scen.items():
         _, st = run()
-        assert [int(x) for x in st["digest"]] == golden[name]["digest"], name
+        got = [int(x) for x in st["digest"]]
+        assert got == golden[name]["digest"], (name, st["emitted"].sum(1)[:8].tolist(),
+                                               st["nodes_processed"][:8].tolist(), got[:4])
