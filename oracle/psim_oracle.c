@@ -250,14 +250,17 @@ static uint64_t mix64(uint64_t z) {
 
 /* Digest of one message: the sum over the 16 words of its 64-B record
  * image [dst, src, type|ttl<<8|nex<<16, seq, a0, a1, a2, 0, ex0..ex7] of
- * mix64((word << 32 | index) ^ golden).  Position-sensitive, order-free
- * across messages (the round digest is a sum), and lane-parallel on the GPU. */
+ * word_j * (0x9E3779B1 + 2j * 0x632BE5AB) mod 2^64 (odd multipliers).
+ * Position-sensitive, order-free across messages (the round digest is a sum),
+ * and one multiply-add per lane on the GPU. */
+static uint64_t digest_mul(uint32_t j) { return (uint64_t)(uint32_t)(0x9E3779B1u + 2u * j * 0x632BE5ABu); }
+
 static uint64_t msg_hash(const omsg *m) {
     uint32_t w[16] = {m->dst, m->src, m->type | (m->ttl << 8) | (m->nex << 16), m->seq,
                       m->a0, m->a1, m->a2, 0};
     for (uint32_t i = 0; i < m->nex; i++) w[8 + i] = m->ex[i];
     uint64_t h = 0;
-    for (uint64_t j = 0; j < 16; j++) h += mix64((((uint64_t)w[j]) << 32 | j) ^ 0x9E3779B97F4A7C15ull);
+    for (uint32_t j = 0; j < 16; j++) h += (uint64_t)w[j] * digest_mul(j);
     return h;
 }
 

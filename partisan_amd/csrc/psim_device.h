@@ -108,6 +108,11 @@ __host__ __device__ __forceinline__ uint32_t bucket16(uint32_t id) {
     return h & 15u;
 }
 
+// digest multiplier of record word j (oracle msg_hash): odd, position-distinct
+__device__ __forceinline__ uint64_t digest_mul(uint32_t j) {
+    return (uint64_t)(uint32_t)(0x9E3779B1u + 2u * j * 0x632BE5ABu);
+}
+
 __device__ __forceinline__ uint64_t mix64(uint64_t z) {
     z ^= z >> 30; z *= 0xBF58476D1CE4E5B9ull;
     z ^= z >> 27; z *= 0x94D049BB133111EBull;

@@ -122,7 +122,7 @@ DEV void emit(Pw& w, uint32_t dst, uint32_t type, uint32_t a0, uint32_t slot) {
     if (l < 16) {
         reinterpret_cast<uint32_t*>(w.a->rec_out + at)[l] = word;
         uint32_t hw = l == 7 ? 0u : word;
-        w.digest += mix64((((uint64_t)hw) << 32 | l) ^ 0x9E3779B97F4A7C15ull);
+        w.digest += (uint64_t)hw * digest_mul(l);
     }
     if (l == 0) w.a->okey[at] = dst;     // pluggable bounds come from k_node_prep
     st_add(w, ST_EMIT + type, 1);
