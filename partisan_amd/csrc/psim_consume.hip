@@ -75,8 +75,16 @@ struct Wv {
     // by one VALU Philox for 64 counters at once (dc_base = NONE64: empty)
     uint32_t DCL, DCH;
     uint64_t dc_base;
+    // emissions are staged in LDS and written once per node (flush_recs), so
+    // the body issues no global store: a later vmcnt wait never drains one
+    uint32_t* srec;      // STAGE records x 16 words
+    uint32_t* skey;      // their route keys
+    uint32_t flushed;    // records already written for this node
+    uint32_t fl, A0, P0; // flag byte and views at node start (writeback)
+    bool work;           // the node had work this round
 };
 constexpr uint64_t NONE64 = ~0ull;
+constexpr uint32_t STAGE = 16;
 
 // stats: lane k of SC holds slot k's count for this wave; flushed once per wave
 DEV void st_add(Wv& w, int k, uint32_t v) { w.SC += lane_id() == (uint32_t)k ? v : 0u; }
@@ -191,22 +199,52 @@ DEV uint32_t sublist(Wv& w, uint32_t V, uint32_t n, uint32_t k, uint32_t& OUT, u
 }
 
 // ------------------------------------------------------------- emission --
+DEV void flush_recs(Wv& w);
+
 DEV void emit(Wv& w, uint32_t dst, uint32_t type, uint32_t ttl, uint32_t a0, uint32_t a1,
               uint32_t a2, uint32_t EX, uint32_t nex) {
     uint32_t l = lane_id();
     uint32_t s = w.seq++;
-    uint64_t slot = w.obase + s;
+    uint32_t k = s - w.flushed;                      // staging slot
     uint32_t tt = type | (ttl << 8) | (nex << 16);
+    // lanes 8..15 take the exchange ids of lanes 0..7 (DPP row_shr:8)
     uint32_t exv = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)EX, 0x118, 0xF, 0xF, true);
     uint32_t word = l == 0 ? dst : l == 1 ? w.me : l == 2 ? tt : l == 3 ? s : l == 4 ? a0
                   : l == 5 ? a1 : l == 6 ? a2 : l == 7 ? 0u : (l - 8 < nex ? exv : 0u);
     if (l < 16) {
-        reinterpret_cast<uint32_t*>(w.a->rec_out + slot)[l] = word;
-        // digest: the oracle's msg_hash, one record word per lane
+        w.srec[k * 16 + l] = word;
         w.digest += (uint64_t)word * digest_mul(l);   // the oracle's msg_hash, word l
     }
-    if (l == 0) w.a->okey[slot] = dst | (max_emit(type) << KEY_DST_BITS);
+    if (l == 0) w.skey[k] = dst | (max_emit(type) << KEY_DST_BITS);
     st_add(w, ST_EMIT + type, 1);
+    if (k + 1 == STAGE) flush_recs(w);               // a node with > STAGE emissions
+}
+
+// The staged records [flushed, seq) to outbox slots obase + flushed..: one
+// 1-KiB store (lane l: 16-B piece l & 3 of record l >> 2) and one route-key
+// store.  Both always run with every lane active -- lanes past the last
+// record repeat it, and with nothing staged they rewrite the node's own
+// first slot (reserved, and unused when ocnt says so) -- so every node issues
+// the same number of vector memory operations and the compiler's vmcnt
+// waits for later loads are exact instead of draining these stores.
+DEV void flush_recs(Wv& w) {
+    const uint32_t l = lane_id();
+    const uint32_t cnt = w.seq - w.flushed;
+    uint32_t j, g, jk, gk;                           // staging / outbox index (records, keys)
+    if (cnt) {
+        j = min(l >> 2, cnt - 1); g = w.flushed + j;
+        jk = min(l, cnt - 1); gk = w.flushed + jk;
+    } else {
+        j = w.flushed ? STAGE - 1 : 0; g = w.flushed ? w.flushed - 1 : 0;
+        jk = j; gk = g;
+    }
+    __builtin_amdgcn_wave_barrier();
+    const uint4 piece = reinterpret_cast<const uint4*>(w.srec + j * 16)[l & 3];
+    const uint32_t key = w.skey[jk];
+    reinterpret_cast<uint4*>(w.a->rec_out + w.obase + g)[l & 3] = piece;
+    w.a->okey[w.obase + gk] = key;
+    __builtin_amdgcn_wave_barrier();
+    w.flushed = w.seq;
 }
 
 // maybe_connect + find (partisan_util.erl:75-134): the peer's manager runs
@@ -231,15 +269,7 @@ DEV void hv_send(Wv& w, uint32_t dst, uint32_t type, uint32_t ttl, uint32_t a0, 
 }
 
 // ----------------------------------------------------------- id maps --
-DEV void load_maps(Wv& w) {
-    if (w.maps) return;
-    uint32_t l = lane_id();
-    size_t b = (size_t)w.li * PSIM_IDMAP_CAP + l;
-    bool in = l < PSIM_IDMAP_CAP;
-    w.SP = in ? w.a->sentp[b] : 0u; w.SI = in ? w.a->senti[b] : 0u;
-    w.RP = in ? w.a->recvp[b] : 0u; w.RI = in ? w.a->recvi[b] : 0u;
-    w.maps = true;
-}
+DEV void load_maps(Wv& w) {}      // loaded with the node (NodeX)
 
 DEV void map_store(Wv& w, uint32_t& PV, uint32_t& IV, uint32_t& n, uint32_t& head, uint32_t p,
                    uint32_t v) {
@@ -349,17 +379,7 @@ DEV void move_to_active(Wv& w, uint32_t p) {             // hv:1679-1709
 }
 
 // ------------------------------------------------------------ plumtree --
-DEV void load_pt(Wv& w) {
-    if (w.pt) return;
-    uint32_t l = lane_id();
-    size_t n = w.li;
-    w.ALL = l < PSIM_PT_MEMBERS_CAP ? w.a->pt_all[n * PSIM_PT_MEMBERS_CAP + l] : 0u;
-    w.COM = l < PSIM_PT_MEMBERS_CAP ? w.a->pt_com[n * PSIM_PT_MEMBERS_CAP + l] : 0u;
-    w.EAG = l < PSIM_PT_SET_CAP ? w.a->pt_eag[n * PSIM_PT_SET_CAP + l] : 0u;
-    w.LAZ = l < PSIM_PT_SET_CAP ? w.a->pt_laz[n * PSIM_PT_SET_CAP + l] : 0u;
-    w.OUT = l < PSIM_PT_OUT_CAP ? w.a->pt_out[n * PSIM_PT_OUT_CAP + l] : 0ull;
-    w.pt = true;
-}
+DEV void load_pt(Wv& w) {}        // loaded with the node (NodeX)
 
 DEV void ord_add(Wv& w, uint32_t& V, uint32_t& n, uint32_t cap, uint32_t e) {
     uint32_t l = lane_id();
@@ -662,57 +682,110 @@ DEV uint32_t load_chunk(const RoundArgs& a, uint32_t ib, uint32_t ik, uint32_t c
                                : 0u;
 }
 
-// Everything a node's processing reads first, loaded one node ahead: the
-// work descriptor (node, inbox begin, inbox count, outbox base) gives every
-// address, so the header, the views, the flag bytes and the first inbox
-// chunk are one round trip, issued while the previous node is processed.
-// Only vector loads (vmcnt, in order): a scalar load in flight would hold
-// up every LDS operation of the node being processed (lgkmcnt).
+// A node's inputs arrive in two stages, each issued one step ahead with every
+// lane loading (lanes beyond a row re-read an element of it), so every node
+// issues the same vector memory operations:
+//   NodeIn (rows, from the work descriptor): header, active and passive
+//          views, the first inbox chunk, the node's flag and partition bytes;
+//   NodeX  (needs the rows): flag/partition bytes of every view member (the
+//          connection cache), the disconnect-id maps and the Plumtree rows.
 struct NodeIn {
     uint32_t n, ib, ik, ob, tf;    // tf: due timers (DESC_* bits, k_desc)
-    uint32_t H;                 // header word l in lane l < 16
+    uint32_t H;                    // header word l & 15
     uint32_t A, P, R0;
     uint32_t fl, part;
+};
+struct NodeX {
+    uint32_t CV, CF;               // view ids (passive 0-31, active 32-39), their flags | part << 8
+    uint32_t MS, MR;               // sent / recv maps: peers in lanes 0-31, ids in 32-63
+    uint32_t PA, PE, PO;           // pt_all | pt_com, pt_eag | pt_laz, pt_out (lo, hi words)
 };
 
 DEV uint32_t load_desc(const RoundArgs& a, uint32_t k) {
     uint32_t l = lane_id();
-    return l < 4 ? reinterpret_cast<const uint32_t*>(a.desc + k)[l] : 0u;
+    return reinterpret_cast<const uint32_t*>(a.desc + k)[l & 3];
 }
 
 DEV NodeIn load_node(const RoundArgs& a, uint32_t D) {
     uint32_t l = lane_id();
     NodeIn x;
     x.n = rl(D, 0); x.ib = rl(D, 1); x.ik = rl(D, 2) & DESC_CNT_MASK; x.tf = rl(D, 2) >> 28; x.ob = rl(D, 3);
-    const uint32_t li = x.n - a.lo;
-    x.H = l < 16 ? reinterpret_cast<const uint32_t*>(a.hdr + li)[l] : 0u;
-    x.A = l < PSIM_ACTIVE_CAP ? a.act[(size_t)li * PSIM_ACTIVE_CAP + l] : 0u;
-    x.P = l < PSIM_PASSIVE_CAP ? a.pas[(size_t)li * PSIM_PASSIVE_CAP + l] : 0u;
-    x.R0 = load_chunk(a, x.ib, x.ik, 0);
+    const size_t li = x.n - a.lo;
+    x.H = reinterpret_cast<const uint32_t*>(a.hdr + li)[l & 15];
+    x.A = a.act[li * PSIM_ACTIVE_CAP + (l & 7)];
+    x.P = a.pas[li * PSIM_PASSIVE_CAP + (l & 31)];
+    uint32_t m = x.ik ? min(l >> 4, x.ik - 1) : 0u;  // record ib exists (the inbox has one spare)
+    x.R0 = reinterpret_cast<const uint32_t*>(a.rec_in + x.ib + m)[l & 15];
     x.fl = a.flags[x.n];
     x.part = a.part[x.n];
     return x;
 }
 
-DEV void process(Wv& w, const NodeIn& x) {
-    const RoundArgs& a = *w.a;
-    const uint32_t r = a.round;
+DEV NodeX load_x(const RoundArgs& a, const NodeIn& x) {
     uint32_t l = lane_id();
-    const uint32_t n = x.n;
-    const uint32_t li = n - a.lo;
-    w.li = li;
-    uint32_t fl = x.fl;
-    uint32_t ik = x.ik;
-    const uint32_t ib = x.ib;
+    NodeX y;
+    const size_t li = x.n - a.lo;
+    const uint32_t hw9 = rl(x.H, 9);                 // act_n, pas_n, .. (Hdr word 9)
+    const uint32_t act_n = hw9 & 0xFF, pas_n = (hw9 >> 8) & 0xFF;
+    uint32_t av = shfl(x.A, (int)(l & 7));
+    uint32_t cv = l < 32 ? (l < pas_n ? x.P : NONE) : (l < 40 && l - 32 < act_n ? av : NONE);
+    uint32_t ca = cv < a.n_nodes ? cv : x.n;
+    uint32_t f = a.flags[ca], pt = a.part[ca];
+    y.CV = cv;
+    y.CF = cv < a.n_nodes ? (f | (pt << 8)) : 0u;
+    const uint32_t l31 = l & 31;
+    y.MS = (l < 32 ? a.sentp : a.senti)[li * PSIM_IDMAP_CAP + l31];
+    y.MR = (l < 32 ? a.recvp : a.recvi)[li * PSIM_IDMAP_CAP + l31];
+    y.PA = ((l & 15) < 8 ? a.pt_all : a.pt_com)[li * PSIM_PT_MEMBERS_CAP + (l & 7)];
+    y.PE = (l31 < 16 ? a.pt_eag : a.pt_laz)[li * PSIM_PT_SET_CAP + (l & 15)];
+    y.PO = reinterpret_cast<const uint32_t*>(a.pt_out + li * PSIM_PT_OUT_CAP)[l];
+    return y;
+}
+
+// node state and the per-node scratch of the wave, from the staged inputs
+DEV void begin_node(Wv& w, const NodeIn& x, const NodeX& y) {
+    const uint32_t l = lane_id();
+    w.li = x.n - w.a->lo;
+    w.me = x.n;
     {
         uint32_t* hw = reinterpret_cast<uint32_t*>(&w.h);
 #pragma unroll
         for (int k = 0; k < 16; k++) hw[k] = rl(x.H, k);
     }
-    w.A = x.A;
-    w.P = x.P;
+    w.A = l < PSIM_ACTIVE_CAP ? x.A : 0u;
+    w.P = l < PSIM_PASSIVE_CAP ? x.P : 0u;
+    w.A0 = w.A; w.P0 = w.P;
+    w.fl = x.fl;
     w.obase = x.ob;
     w.mypart = x.part;
+    w.CV = y.CV; w.CF = y.CF;
+    uint32_t msi = shfl(y.MS, (int)((l + 32) & 63)), mri = shfl(y.MR, (int)((l + 32) & 63));
+    w.SP = l < 32 ? y.MS : 0u; w.SI = l < 32 ? msi : 0u;
+    w.RP = l < 32 ? y.MR : 0u; w.RI = l < 32 ? mri : 0u;
+    uint32_t com = shfl(y.PA, (int)((l + 8) & 63)), laz = shfl(y.PE, (int)((l + 16) & 63));
+    w.ALL = l < PSIM_PT_MEMBERS_CAP ? y.PA : 0u; w.COM = l < PSIM_PT_MEMBERS_CAP ? com : 0u;
+    w.EAG = l < PSIM_PT_SET_CAP ? y.PE : 0u; w.LAZ = l < PSIM_PT_SET_CAP ? laz : 0u;
+    uint32_t olo = shfl(y.PO, (int)((2 * l) & 63)), ohi = shfl(y.PO, (int)((2 * l + 1) & 63));
+    w.OUT = l < PSIM_PT_OUT_CAP ? (((uint64_t)ohi << 32) | olo) : 0ull;
+    w.act_n = w.h.act_n; w.pas_n = w.h.pas_n; w.sent_n = w.h.sent_n; w.sent_head = w.h.sent_head;
+    w.recv_n = w.h.recv_n; w.recv_head = w.h.recv_head;
+    w.all_n = w.h.all_n; w.com_n = w.h.com_n; w.eag_n = w.h.eag_n; w.laz_n = w.h.laz_n;
+    w.out_n = w.h.out_n;
+    w.maps = true; w.pt = true; w.maps_dirty = false; w.pt_dirty = false;
+    w.seq = 0; w.flushed = 0;
+    w.nlog_n = 0;
+    w.dc_base = NONE64;                                // the cache holds another node's stream
+    w.work = false;
+}
+
+// The node's handlers in the order of round model R0.  No global store.
+DEV void body(Wv& w, const NodeIn& x) {
+    const RoundArgs& a = *w.a;
+    const uint32_t r = a.round;
+    const uint32_t l = lane_id();
+    const uint32_t n = x.n;
+    uint32_t ik = x.ik;
+    const uint32_t ib = x.ib;
     const uint32_t R0 = x.R0;
     if (w.h.start_round == r && ik) {           // fresh incarnation: no connections yet
         st_add(w, ST_DROPPED, ik);
@@ -724,35 +797,16 @@ DEV void process(Wv& w, const NodeIn& x) {
     bool lazy_due = (x.tf & DESC_LAZY) != 0;
     bool lazy = lazy_due && w.h.out_n > 0;
     bool joining = w.h.start_round == r && w.h.join_contact != NONE;
-    w.act_n = w.h.act_n;
     uint64_t exits = 0;
-    if (a.crash_round) {
-        bool dead = l < w.act_n && w.A != n && (a.flags[w.A] & F_CRASHED);
-        exits = ballot(dead);
+    if (a.crash_round) {                        // F_CRASHED of the active members (cache lanes 32-39)
+        bool dead = l >= 32 && l - 32 < w.act_n && w.CV != n && (w.CF & F_CRASHED);
+        exits = ballot(dead) >> 32;
     }
     bool promo_work = promo && w.act_n < a.min_active;
     if (!(ik || joining || exits || promo_work || shuf || origin || lazy)) { STAMP(w, 0); return; }
+    w.work = true;
     st_add(w, ST_PROC, 1);
     STAMP(w, 1);
-
-    w.me = n;
-    {
-        uint32_t av = shfl(w.A, (int)((l - 32) & 63));
-        uint32_t cv = l < 32 ? (l < w.h.pas_n ? w.P : NONE) : (l - 32 < w.act_n ? av : NONE);
-        w.CV = cv;
-        w.CF = cv < a.n_nodes ? ((uint32_t)a.flags[cv] | ((uint32_t)a.part[cv] << 8)) : 0u;
-    }
-    w.pas_n = w.h.pas_n; w.sent_n = w.h.sent_n; w.sent_head = w.h.sent_head;
-    w.recv_n = w.h.recv_n; w.recv_head = w.h.recv_head;
-    w.all_n = w.h.all_n; w.com_n = w.h.com_n; w.eag_n = w.h.eag_n; w.laz_n = w.h.laz_n;
-    w.out_n = w.h.out_n;
-    w.maps = false; w.pt = false; w.maps_dirty = false; w.pt_dirty = false;
-    const uint32_t A0 = w.A, P0 = w.P;
-    w.SP = w.SI = w.RP = w.RI = 0;
-    w.ALL = w.COM = w.EAG = w.LAZ = 0; w.OUT = 0;
-    w.seq = 0;
-    w.nlog_n = 0;
-    w.dc_base = NONE64;                                // the cache holds another node's stream
 
     if (joining)                                      // hv:500-515
         hv_send(w, w.h.join_contact, PSIM_MSG_JOIN, 0, w.h.epoch, 0, 0, 0);
@@ -817,7 +871,6 @@ DEV void process(Wv& w, const NodeIn& x) {
         }
         STAMP(w, 3);
         if (origin) {                                 // pt:282-287, backend:179-200
-            load_pt(w);
             uint32_t my = n | PSIM_MAP_BIT;
             w.h.have |= 1u << (a.origin_msg & 31u);
             w.h.trk_round = r;
@@ -826,7 +879,6 @@ DEV void process(Wv& w, const NodeIn& x) {
         }
         STAMP(w, 21);
         if (lazy_due && w.out_n > 0) {                // pt:341-345, :443-453
-            load_pt(w);
             for (uint32_t i = 0; i < w.out_n; i++) {
                 uint64_t o = rl64(w.OUT, i);
                 pt_send(w, (uint32_t)(o >> 32), PSIM_MSG_PT_IHAVE, (uint32_t)(o >> 16) & 0xFFFFu,
@@ -834,46 +886,66 @@ DEV void process(Wv& w, const NodeIn& x) {
             }
         }
     }
-
     STAMP(w, 22);
-    // ---- write back
+}
+
+// Write back the node: a fixed set of full-wave stores (each lane past a
+// row's end repeats one of its elements; a row that did not change is
+// "stored" as a rewrite of header word 0 with its own value), then the
+// staged records.  12 vector memory operations for every node.
+DEV void writeback(Wv& w) {
+    const RoundArgs& a = *w.a;
+    const uint32_t l = lane_id();
+    const size_t li = w.li;
     w.h.act_n = (uint8_t)w.act_n; w.h.pas_n = (uint8_t)w.pas_n;
     w.h.sent_n = (uint8_t)w.sent_n; w.h.sent_head = (uint8_t)w.sent_head;
     w.h.recv_n = (uint8_t)w.recv_n; w.h.recv_head = (uint8_t)w.recv_head;
     w.h.all_n = (uint8_t)w.all_n; w.h.com_n = (uint8_t)w.com_n;
     w.h.eag_n = (uint8_t)w.eag_n; w.h.laz_n = (uint8_t)w.laz_n; w.h.out_n = (uint8_t)w.out_n;
-    // write back only what changed
-    if (ballot(w.A != A0) && l < PSIM_ACTIVE_CAP) a.act[(size_t)li * PSIM_ACTIVE_CAP + l] = w.A;
-    if (ballot(w.P != P0) && l < PSIM_PASSIVE_CAP) a.pas[(size_t)li * PSIM_PASSIVE_CAP + l] = w.P;
-    if (w.maps_dirty && l < PSIM_IDMAP_CAP) {
-        size_t b = (size_t)li * PSIM_IDMAP_CAP + l;
-        a.sentp[b] = w.SP; a.senti[b] = w.SI; a.recvp[b] = w.RP; a.recvi[b] = w.RI;
-    }
-    if (w.pt_dirty) {
-        if (l < PSIM_PT_MEMBERS_CAP) {
-            a.pt_all[(size_t)li * PSIM_PT_MEMBERS_CAP + l] = w.ALL;
-            a.pt_com[(size_t)li * PSIM_PT_MEMBERS_CAP + l] = w.COM;
-        }
-        if (l < PSIM_PT_SET_CAP) {
-            a.pt_eag[(size_t)li * PSIM_PT_SET_CAP + l] = w.EAG;
-            a.pt_laz[(size_t)li * PSIM_PT_SET_CAP + l] = w.LAZ;
-        }
-        if (l < PSIM_PT_OUT_CAP) a.pt_out[(size_t)li * PSIM_PT_OUT_CAP + l] = w.OUT;
+    const uint32_t* hw = reinterpret_cast<const uint32_t*>(&w.h);
+    uint32_t v = 0;
+#pragma unroll
+    for (int k = 0; k < 16; k++) v = (l & 15) == (uint32_t)k ? hw[k] : v;
+    uint32_t* hrow = reinterpret_cast<uint32_t*>(a.hdr + li);
+    const uint32_t h0 = hw[0];
+    hrow[l & 15] = v;
+    {
+        bool dirty = ballot(w.A != w.A0) != 0;
+        uint32_t x = shfl(w.A, (int)(l & 7));
+        *(dirty ? a.act + li * PSIM_ACTIVE_CAP + (l & 7) : hrow) = dirty ? x : h0;
     }
     {
-        const uint32_t* hw = reinterpret_cast<const uint32_t*>(&w.h);
-        uint32_t v = 0;
-#pragma unroll
-        for (int k = 0; k < 16; k++) v = l == (uint32_t)k ? hw[k] : v;
-        if (l < 16) reinterpret_cast<uint32_t*>(a.hdr + li)[l] = v;
+        bool dirty = ballot(w.P != w.P0) != 0;
+        uint32_t x = shfl(w.P, (int)(l & 31));
+        *(dirty ? a.pas + li * PSIM_PASSIVE_CAP + (l & 31) : hrow) = dirty ? x : h0;
     }
-    if (l == 0) {
-        a.ocnt[li] = w.seq;
-        // only this wave writes its node's flag byte; peers read F_UP/F_CRASHED
-        uint8_t nf = (uint8_t)((fl & ~(F_LAZY | F_LOWACT)) | (w.out_n ? F_LAZY : 0) |
-                               (w.act_n < a.min_active ? F_LOWACT : 0));
-        if (nf != fl) a.flags[n] = nf;
+    {
+        const bool d = w.maps_dirty;
+        const uint32_t l31 = l & 31;
+        uint32_t si = shfl(w.SI, (int)l31), ri = shfl(w.RI, (int)l31);
+        uint32_t* p1 = (l < 32 ? a.sentp : a.senti) + li * PSIM_IDMAP_CAP + l31;
+        uint32_t* p2 = (l < 32 ? a.recvp : a.recvi) + li * PSIM_IDMAP_CAP + l31;
+        *(d ? p1 : hrow) = d ? (l < 32 ? w.SP : si) : h0;
+        *(d ? p2 : hrow) = d ? (l < 32 ? w.RP : ri) : h0;
     }
+    {
+        const bool d = w.pt_dirty;
+        uint32_t all = shfl(w.ALL, (int)(l & 7)), com = shfl(w.COM, (int)(l & 7));
+        uint32_t eag = shfl(w.EAG, (int)(l & 15)), laz = shfl(w.LAZ, (int)(l & 15));
+        uint64_t o = shfl64(w.OUT, (int)(l >> 1));
+        const bool lo8 = (l & 15) < 8, lo16 = (l & 31) < 16;
+        uint32_t* p1 = (lo8 ? a.pt_all : a.pt_com) + li * PSIM_PT_MEMBERS_CAP + (l & 7);
+        uint32_t* p2 = (lo16 ? a.pt_eag : a.pt_laz) + li * PSIM_PT_SET_CAP + (l & 15);
+        uint32_t* p3 = reinterpret_cast<uint32_t*>(a.pt_out + li * PSIM_PT_OUT_CAP) + l;
+        *(d ? p1 : hrow) = d ? (lo8 ? all : com) : h0;
+        *(d ? p2 : hrow) = d ? (lo16 ? eag : laz) : h0;
+        *(d ? p3 : hrow) = d ? ((l & 1) ? (uint32_t)(o >> 32) : (uint32_t)o) : h0;
+    }
+    a.ocnt[li] = w.seq;
+    // only this wave writes its node's flag byte; peers read F_UP/F_CRASHED
+    a.flags[w.me] = (uint8_t)((w.fl & ~(F_LAZY | F_LOWACT)) | (w.out_n ? F_LAZY : 0) |
+                              (w.act_n < a.min_active ? F_LOWACT : 0));
+    flush_recs(w);
     STAMP(w, 23);
 }
 
@@ -881,6 +953,8 @@ __global__ void __launch_bounds__(256, PSIM_WAVES_PER_SIMD) k_consume(RoundArgs 
     __shared__ uint64_t sst[NST];
     __shared__ uint32_t scratch[WAVES_PER_BLOCK][64];
     __shared__ uint32_t nlogs[WAVES_PER_BLOCK][NLOG * (PSIM_ACTIVE_CAP + 1)];
+    __shared__ __attribute__((aligned(16))) uint32_t srecs[WAVES_PER_BLOCK][STAGE * 16];
+    __shared__ uint32_t skeys[WAVES_PER_BLOCK][STAGE];
     for (int i = threadIdx.x; i < NST; i += blockDim.x) sst[i] = 0;
     __syncthreads();
 
@@ -891,6 +965,8 @@ __global__ void __launch_bounds__(256, PSIM_WAVES_PER_SIMD) k_consume(RoundArgs 
     w.a = &args;
     w.lds = scratch[wid];
     w.nlog = nlogs[wid];
+    w.srec = srecs[wid];
+    w.skey = skeys[wid];
 #ifdef PSIM_STAMPS
     __shared__ uint64_t stamps[WAVES_PER_BLOCK][32];
     if ((threadIdx.x & 63) < 32) stamps[wid][threadIdx.x & 63] = 0;
@@ -903,17 +979,25 @@ __global__ void __launch_bounds__(256, PSIM_WAVES_PER_SIMD) k_consume(RoundArgs 
     w.digest = 0;
     const uint32_t na = *args.n_alist;
     if (gw < na) {
-        // software pipeline: node i is processed while node i + nw's loads
-        // are in flight and node i + 2nw's descriptor is being fetched
+        // Pipeline over this wave's nodes i, i + nw, ...: while node i is
+        // processed, the rows of node i + nw are in flight; after its body the
+        // second-stage loads of node i + nw go out, then node i's stores, then
+        // the rows of node i + 2nw.  Every node issues the same loads and
+        // stores, so each wait is for exactly the stage it needs.
         const uint32_t last = na - 1;
-        NodeIn x0 = load_node(args, load_desc(args, gw));
-        uint32_t d1 = load_desc(args, min(gw + nw, last));
+        NodeIn x = load_node(args, load_desc(args, gw));
+        NodeX y = load_x(args, x);
+        NodeIn xn = load_node(args, load_desc(args, min(gw + nw, last)));
+        uint32_t d = load_desc(args, min(gw + 2 * nw, last));
         for (uint32_t i = gw; i < na; i += nw) {
-            NodeIn x1 = load_node(args, d1);
-            d1 = load_desc(args, min(i + 2 * nw, last));
             STAMP(w, 24);
-            process(w, x0);
-            x0 = x1;
+            begin_node(w, x, y);
+            body(w, x);
+            NodeX yn = load_x(args, xn);
+            writeback(w);
+            NodeIn xnn = load_node(args, d);
+            d = load_desc(args, min(i + 3 * nw, last));
+            x = xn; y = yn; xn = xnn;
         }
     }
 #ifdef PSIM_STAMPS
@@ -923,10 +1007,10 @@ __global__ void __launch_bounds__(256, PSIM_WAVES_PER_SIMD) k_consume(RoundArgs 
     {
         uint32_t l = lane_id();
         if (l < NST && w.SC) atomicAdd((unsigned long long*)&sst[l], (unsigned long long)w.SC);
-        uint64_t d = w.digest;
+        uint64_t dg = w.digest;
 #pragma unroll
-        for (int off = 32; off > 0; off >>= 1) d += shfl64(d, (int)((l + off) & 63));
-        if (l == 0 && d) atomicAdd((unsigned long long*)&sst[ST_DIGEST], (unsigned long long)d);
+        for (int off = 32; off > 0; off >>= 1) dg += shfl64(dg, (int)((l + off) & 63));
+        if (l == 0 && dg) atomicAdd((unsigned long long*)&sst[ST_DIGEST], (unsigned long long)dg);
     }
 
     __syncthreads();
