@@ -921,7 +921,10 @@ int psim_create(const psim_config* cfg, psim_handle** out) {
     if (world > 1) {
         ncclUniqueId id;
         memcpy(&id, cfg->comm_id, sizeof id);
-        if (ncclCommInitRank(&h->comm, (int)world, id, (int)cfg->shard_rank) != ncclSuccess) {
+        ncclResult_t r = ncclCommInitRank(&h->comm, (int)world, id, (int)cfg->shard_rank);
+        if (r != ncclSuccess) {
+            std::fprintf(stderr, "psim: ncclCommInitRank(world %u, rank %u) failed: %s\n", world,
+                         cfg->shard_rank, ncclGetErrorString(r));
             h->comm = nullptr;
             psim_destroy(h);
             return PSIM_ECOMM;
