@@ -43,7 +43,10 @@ static int get_u32(ErlNifEnv *env, ERL_NIF_TERM map, const char *k, uint32_t *ou
     return 1;
 }
 
-/* create(#{n_nodes => N, seed => S, max_active_size => .., ...}) -> {ok, Ref} */
+/* create(#{n_nodes => N, seed => S, max_active_size => .., ...,
+ *         manager => 0 | 1, strategy => 0 | 1 | 2, fanout => K, scamp_c => C,
+ *         periodic_interval => Rounds}) -> {ok, Ref}
+ * manager 1 = the pluggable manager with strategy 0 full, 1 scamp v1, 2 scamp v2 */
 static ERL_NIF_TERM nif_create(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[]) {
     psim_config c;
     ErlNifUInt64 seed;
@@ -55,7 +58,12 @@ static ERL_NIF_TERM nif_create(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv
         !get_u32(env, argv[0], "max_passive_size", &c.max_passive_size) ||
         !get_u32(env, argv[0], "arwl", &c.arwl) || !get_u32(env, argv[0], "prwl", &c.prwl) ||
         !get_u32(env, argv[0], "shuffle_period", &c.shuffle_period) ||
-        !get_u32(env, argv[0], "plumtree", &c.plumtree))
+        !get_u32(env, argv[0], "plumtree", &c.plumtree) ||
+        !get_u32(env, argv[0], "manager", &c.manager) ||
+        !get_u32(env, argv[0], "strategy", &c.strategy) ||
+        !get_u32(env, argv[0], "fanout", &c.fanout) ||
+        !get_u32(env, argv[0], "scamp_c", &c.scamp_c) ||
+        !get_u32(env, argv[0], "periodic_interval", &c.periodic_interval))
         return enif_make_badarg(env);
     if (enif_get_map_value(env, argv[0], enif_make_atom(env, "seed"), &v) &&
         enif_get_uint64(env, v, &seed))
@@ -143,6 +151,38 @@ static ERL_NIF_TERM nif_active(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv
     return enif_make_tuple2(env, enif_make_atom(env, "ok"), enif_make_list_from_array(env, ids, v.act_n));
 }
 
+/* members(Ref, Node) -> {ok, [Id]} : the pluggable manager's membership of one
+ * node -- full: query(ORSet) in id order; scamp: the view in list order */
+static ERL_NIF_TERM nif_members(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[]) {
+    sim_res *r; unsigned node, n_nodes;
+    psim_strategy_view v;
+    if (!enif_get_resource(env, argv[0], SIM_RT, (void **)&r) || !enif_get_uint(env, argv[1], &node) ||
+        !enif_get_uint(env, argv[2], &n_nodes))
+        return enif_make_badarg(env);
+    enif_mutex_lock(r->mu);
+    int rc = psim_get_strategy_nodes(r->h, node, 1, &v);
+    uint32_t *bits = NULL;
+    size_t words = (n_nodes + 31) / 32;
+    if (!rc && v.members) {           /* full strategy */
+        bits = enif_alloc(words * 4);
+        rc = psim_get_member_bits(r->h, node, bits, words);
+    }
+    enif_mutex_unlock(r->mu);
+    if (rc) { if (bits) enif_free(bits); return err(env, rc); }
+    ERL_NIF_TERM list = enif_make_list(env, 0);
+    if (bits) {
+        for (size_t i = words; i-- > 0;)
+            for (int b = 31; b >= 0; b--)
+                if ((bits[i] >> b) & 1u)
+                    list = enif_make_list_cell(env, enif_make_uint(env, (unsigned)(i * 32 + b)), list);
+        enif_free(bits);
+    } else {
+        for (uint32_t i = v.view_n; i-- > 0;)
+            list = enif_make_list_cell(env, enif_make_uint(env, v.view[i]), list);
+    }
+    return enif_make_tuple2(env, enif_make_atom(env, "ok"), list);
+}
+
 static ErlNifFunc funcs[] = {
     {"create", 1, nif_create, 0},
     {"join_nif", 3, nif_join, 0},
@@ -150,6 +190,7 @@ static ErlNifFunc funcs[] = {
     {"broadcast", 3, nif_broadcast, 0},
     {"step", 2, nif_step, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"active", 2, nif_active, 0},
+    {"members", 3, nif_members, 0},
 };
 
 ERL_NIF_INIT(partisan_gpu_sim, funcs, load, NULL, NULL, NULL)

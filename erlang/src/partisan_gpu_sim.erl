@@ -2,7 +2,7 @@
 %% (include/partisan_gpu_sim.h).  Node ids are the simulated nodes; an id maps
 %% to the harness node_spec #{name => 'n<id>@sim', ...} (DESIGN.md section 2).
 -module(partisan_gpu_sim).
--export([create/1, join/3, crash/2, broadcast/3, step/2, active/2]).
+-export([create/1, join/3, crash/2, broadcast/3, step/2, active/2, members/3]).
 -on_load(init/0).
 
 init() ->
@@ -21,6 +21,8 @@ crash(Sim, Nodes) -> crash_nif(Sim, pack(Nodes)).
 broadcast(_Sim, _Root, _Id) -> erlang:nif_error(nif_not_loaded).
 step(_Sim, _Rounds) -> erlang:nif_error(nif_not_loaded).
 active(_Sim, _Node) -> erlang:nif_error(nif_not_loaded).
+%% pluggable manager handles: the strategy membership of Node (N = n_nodes)
+members(_Sim, _Node, _N) -> erlang:nif_error(nif_not_loaded).
 
 pack(Ids) -> << <<I:32/little>> || I <- Ids >>.
 join_nif(_S, _N, _C) -> erlang:nif_error(nif_not_loaded).

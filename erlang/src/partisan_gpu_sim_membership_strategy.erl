@@ -1,0 +1,69 @@
+%% partisan_gpu_sim_membership_strategy -- the partisan_membership_strategy
+%% behaviour (src/partisan_membership_strategy.erl:32-36) backed by the MI355X
+%% simulator.  One simulator handle (manager = pluggable, strategy = full /
+%% scamp v1 / scamp v2 from partisan_config) holds every simulated node; this
+%% module answers the callbacks of one of them (`sim_node`), so the pluggable
+%% manager (pluggable:384, :886, :1001, :1162, :1398) can be pointed at it
+%% with partisan_config:set(membership_strategy, ?MODULE).
+%%
+%% The simulator runs the strategy's own message exchange on the GPU, so the
+%% outgoing-message lists returned here are empty: the manager has nothing to
+%% forward.  periodic/1 advances the whole overlay by one round (R0-P,
+%% DESIGN.md section 2b) -- call it from one node only (the `sim_driver`).
+-module(partisan_gpu_sim_membership_strategy).
+-behaviour(partisan_membership_strategy).
+
+-export([init/1, join/3, leave/2, periodic/1, handle_message/2]).
+
+-record(sim_strategy, {sim, me :: non_neg_integer(), n :: pos_integer(), driver :: boolean()}).
+
+init(_Identity) ->
+    N = partisan_config:get(sim_nodes, 32),
+    Me = partisan_config:get(sim_node, 0),
+    Strategy = case partisan_config:get(membership_strategy_sim, full) of
+                   full -> 0; scamp_v1 -> 1; scamp_v2 -> 2
+               end,
+    {ok, Sim} = case partisan_config:get(sim_handle, undefined) of
+                    undefined ->
+                        partisan_gpu_sim:create(#{n_nodes => N, seed => partisan_config:get(sim_seed, 1),
+                                                  manager => 1, strategy => Strategy,
+                                                  fanout => partisan_config:get(sim_fanout, 0),
+                                                  scamp_c => partisan_config:get(scamp_c, 5),
+                                                  periodic_interval => 10});
+                    H -> {ok, H}
+                end,
+    ok = partisan_gpu_sim:join(Sim, [Me], [16#FFFFFFFF]),
+    State = #sim_strategy{sim = Sim, me = Me, n = N,
+                          driver = partisan_config:get(sim_driver, false)},
+    {ok, membership(State), State}.
+
+%% Strategy:join/3 at the joiner: the simulated hello/state handshake and the
+%% strategy's join happen in the next rounds of the simulator.
+join(State = #sim_strategy{sim = Sim, me = Me}, #{name := Name}, _RemoteState) ->
+    ok = partisan_gpu_sim:join(Sim, [Me], [id(Name)]),
+    {ok, membership(State), [], State}.
+
+%% leave/2 is not simulated (DESIGN.md section 2b).
+leave(State, _Node) ->
+    {ok, membership(State), [], State}.
+
+periodic(State = #sim_strategy{sim = Sim, driver = true}) ->
+    {ok, _Stats} = partisan_gpu_sim:step(Sim, 1),
+    {ok, membership(State), [], State};
+periodic(State) ->
+    {ok, membership(State), [], State}.
+
+%% messages between simulated nodes never leave the GPU
+handle_message(State, _Message) ->
+    {ok, membership(State), [], State}.
+
+membership(#sim_strategy{sim = Sim, me = Me, n = N}) ->
+    {ok, Ids} = partisan_gpu_sim:members(Sim, Me, N),
+    [#{name => name(I), listen_addrs => [#{ip => {10, (I bsr 16) band 255, (I bsr 8) band 255, I band 255},
+                                           port => 9090}],
+       channels => [undefined], parallelism => 1} || I <- Ids].
+
+name(Id) -> list_to_atom(lists:flatten(io_lib:format("n~10..0B@sim", [Id]))).
+id(Name) ->
+    [$n | Rest] = atom_to_list(Name),
+    list_to_integer(lists:takewhile(fun(C) -> C >= $0 andalso C =< $9 end, Rest)).
