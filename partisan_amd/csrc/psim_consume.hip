@@ -183,11 +183,22 @@ DEV uint32_t sublist(Wv& w, uint32_t V, uint32_t n, uint32_t k, uint32_t& OUT, u
     uint32_t kl = shfl(w.DCL, (int)src), kh = shfl(w.DCH, (int)src);
     uint64_t key = l < n ? ((((uint64_t)kh) << 32) | kl) >> 5 : ~0ull;
     uint32_t m = n < k ? n : k;
-    uint32_t rank = 0;
+    // rank on the top 32 of the 53 key bits; only when two of them tie (about
+    // once in 10^7 sublists) is the full (key, element) order recounted
+    const uint32_t hi = (uint32_t)(key >> 21);
+    uint32_t rank = 0, eq = 0;
     for (uint32_t j = 0; j < n; j++) {
-        uint64_t kj = rl64(key, j);
-        uint32_t ej = rl(V, j);
-        rank += (kj < key || (kj == key && ej < V)) ? 1u : 0u;
+        uint32_t hj = rl(hi, j);
+        rank += hj < hi ? 1u : 0u;
+        eq += hj == hi ? 1u : 0u;
+    }
+    if (ballot(l < n && eq > 1)) {
+        rank = 0;
+        for (uint32_t j = 0; j < n; j++) {
+            uint64_t kj = rl64(key, j);
+            uint32_t ej = rl(V, j);
+            rank += (kj < key || (kj == key && ej < V)) ? 1u : 0u;
+        }
     }
     if (l < n && rank < m) w.lds[rank] = V;
     __builtin_amdgcn_wave_barrier();
