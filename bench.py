@@ -116,7 +116,7 @@ def main_strategy(args):
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": "k_consume_pl",
                      "alg_bytes_per_launch": alg / max(1, c_n), "avg_launch_ms": c_ms / max(1, c_n)},
-        "kernel_ms_per_step": {k: v[0] / args.steps for k, v in kt.items()},
+        "kernel_ms_per_step": {k: v[0] / args.steps for k, v in kt.items() if v[1]},
         "overflow": int(st["overflow"].sum()),
         "members_min": int(sim.strategy_nodes(0, min(n, 4096))["members"].min()) if args.workload == "B" else None,
     }
@@ -174,6 +174,9 @@ def main():
             if i == 40:
                 sim.clear_partition()
 
+    def has_events(i):
+        return i % 10 == 0 or (args.workload == "E" and (i in churn or i - 1 in churn or i in (20, 40)))
+
     for i in range(args.warmup):
         round_events(i)
         sim.step(1)
@@ -182,9 +185,15 @@ def main():
     t0 = time.perf_counter()
     stats = []
     kt = {}
-    for i in range(args.steps):
+    i = 0
+    while i < args.steps:
+        # rounds up to the next one with host events run in one step call
         round_events(args.warmup + i)
-        stats.append(sim.step(1))
+        k = 1
+        while i + k < args.steps and not has_events(args.warmup + i + k):
+            k += 1
+        stats.append(sim.step(k))
+        i += k
         for name, (ms, cnt) in sim.kernel_times().items():
             a, b = kt.get(name, (0.0, 0))
             kt[name] = (a + ms, b + cnt)
@@ -229,7 +238,7 @@ def main():
                      "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                      "kernel": "k_consume", "alg_bytes_per_launch": per_launch_bytes,
                      "avg_launch_ms": per_launch_s * 1e3},
-        "kernel_ms_per_step": {k: v[0] / args.steps for k, v in kt.items()},
+        "kernel_ms_per_step": {k: v[0] / args.steps for k, v in kt.items() if v[1]},
         "overflow": int(st["overflow"].sum()),
     }
     if args.workload == "E":

@@ -967,6 +967,7 @@ __global__ void __launch_bounds__(256, PSIM_WAVES_PER_SIMD) k_consume(RoundArgs 
     __shared__ __attribute__((aligned(16))) uint32_t srecs[WAVES_PER_BLOCK][STAGE * 16];
     __shared__ uint32_t skeys[WAVES_PER_BLOCK][STAGE];
     for (int i = threadIdx.x; i < NST; i += blockDim.x) sst[i] = 0;
+    if (threadIdx.x == 0) atomicMin(&args.ktime[0], (unsigned long long)__builtin_amdgcn_s_memrealtime());
     __syncthreads();
 
     const uint32_t wid = threadIdx.x >> 6;
@@ -1027,6 +1028,7 @@ __global__ void __launch_bounds__(256, PSIM_WAVES_PER_SIMD) k_consume(RoundArgs 
     __syncthreads();
     for (int i = threadIdx.x; i < NST; i += blockDim.x)
         args.stat_part[(size_t)blockIdx.x * NST + i] = sst[i];
+    if (threadIdx.x == 0) atomicMax(&args.ktime[1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
 }
 
 // one wave-slot per resident wave: the grid strides over the active list

@@ -7,16 +7,19 @@
 // copies) or exactly one when run as an RCCL rank (shard_world > 1).  Per
 // round and shard (DESIGN.md sections 3 and 7):
 //   events   k_crash / k_join / k_bcast_reset    (same event list on every shard)
-//   prepare  k_runs (inbox run lengths + emission bounds), k_node_prep
-//            (bounds, work flags), compaction -> active list, scans -> in_beg, obase
+//   prepare  k_node_prep (bounds, work flags), compaction -> active list,
+//            scan -> obase
 //   consume  k_consume (psim_consume.hip)
-//   route    G == 1: scan(ocnt) -> k_compact -> stable radix sort by dst
+//   route    G == 1: count (atomics) -> scan -> scatter -> per-run sort of
+//                    source indices -> gather (stable radix sort when one run
+//                    is too long)
 //            G  > 1: stable partition by owner shard -> gather records ->
-//                    all-to-all (counts, then records) -> stable sort of the
-//                    shard-ordered concatenation by dst
+//                    all-to-all (counts, then records) -> the same grouping
+//                    of the shard-ordered concatenation by dst
 //   stats    k_stats_reduce (+ sum over shards / ncclAllReduce)
-// A stable sort of a (src, seq)-ordered stream -- or of a concatenation
-// ordered by source shard -- yields each inbox in canonical (src, seq) order,
+// Grouping a (src, seq)-ordered stream -- or a concatenation ordered by
+// source shard -- by dst, each group in stream order, yields each inbox in
+// canonical (src, seq) order,
 // so any shard count gives bit-identical results.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
@@ -144,17 +147,170 @@ __global__ void k_bcast_reset(Hdr* hdr, uint32_t n, uint32_t bit) {
     hdr[i].trk_hop = 0;
 }
 
-// Run lengths of the sorted inbox (local dst): the lane at the start of each
-// run writes the run's length and the sum of its messages' emission bounds.
-__global__ void k_runs(const uint32_t* __restrict__ keys, uint32_t m, uint32_t* cnt, uint32_t* bsum) {
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < m; i += gridDim.x * blockDim.x) {
-        uint32_t d = keys[i] & KEY_DST_MASK;
-        if (i > 0 && (keys[i - 1] & KEY_DST_MASK) == d) continue;
-        uint32_t j = i, s = 0;
-        while (j < m && (keys[j] & KEY_DST_MASK) == d) { s += keys[j] >> KEY_DST_BITS; j++; }
-        cnt[d] = j - i;
-        bsum[d] = s;
+// ------------------------------------------------------------- route --
+// The route groups a round's records by local destination, each group in
+// emission order: ascending source index (an outbox slot, or a position in
+// the source-shard-ordered receive buffer), which is (src, seq) order.
+//   count    one atomic per record: run length and emission-bound sum of its
+//            destination (cnt has n + 1 entries, cnt[n] = 0)
+//   scan     run starts in_beg[0..n]; in_beg[n] is the record count m
+//   scatter  each record's source index into its run, at an atomic cursor
+//   sort     every run ascending: <= RUN_SHORT by its own thread in
+//            registers, longer ones by one block (bitonic in LDS up to
+//            RUN_LDS, LDS-sorted chunks merged through `tmp` beyond)
+// The order inside a run before the sort depends on atomic timing; the sort
+// by source index makes the inbox deterministic.
+constexpr uint32_t RUN_SHORT = 16;
+constexpr uint32_t RUN_LDS = 2048;
+
+// A wave takes 64 consecutive source nodes and expands their outbox runs
+// (ocnt[i] records at obase[i]) into consecutive record numbers t: lane l
+// handles records l, l + 64, ..., so okey is read in slot order.
+template <bool SCATTER>
+__global__ void __launch_bounds__(256) k_route_runs(const uint32_t* __restrict__ okey,
+                                                    const uint64_t* __restrict__ obase,
+                                                    const uint32_t* __restrict__ ocnt, uint32_t n,
+                                                    uint32_t lo, uint32_t* cnt, uint32_t* bsum,
+                                                    const uint32_t* __restrict__ in_beg, uint32_t* fill,
+                                                    uint32_t* idx) {
+    __shared__ uint32_t spre[4][65];
+    __shared__ uint64_t sbase[4][64];
+    const uint32_t w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t c = i < n ? ocnt[i] : 0u;
+    uint32_t inc = c;                                 // inclusive prefix over the wave
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(inc, o);
+        if (l >= (uint32_t)o) inc += y;
     }
+    spre[w][l + 1] = inc;
+    if (l == 0) spre[w][0] = 0;
+    sbase[w][l] = i < n ? obase[i] : 0ull;
+    const uint32_t T = __shfl(inc, 63);
+    __syncthreads();
+    const uint32_t* pre = spre[w];
+    for (uint32_t t = l; t < T; t += 64) {
+        uint32_t a = 0, b = 64;                       // the node j with pre[j] <= t < pre[j + 1]
+        while (b - a > 1) {
+            const uint32_t mid = (a + b) >> 1;
+            if (pre[mid] <= t) a = mid; else b = mid;
+        }
+        const uint64_t g = sbase[w][a] + (t - pre[a]);
+        const uint32_t key = okey[g], d = (key & KEY_DST_MASK) - lo;
+        if (SCATTER) {
+            idx[in_beg[d] + atomicAdd(&fill[d], 1u)] = (uint32_t)g;
+        } else {
+            atomicAdd(&cnt[d], 1u);
+            if (key >> KEY_DST_BITS) atomicAdd(&bsum[d], key >> KEY_DST_BITS);
+        }
+    }
+}
+
+// G > 1, receive side: thread per record of the receive buffer
+__global__ void k_count_dense(const Msg* __restrict__ rec, uint32_t m, uint32_t lo, uint32_t pl,
+                              uint32_t* cnt, uint32_t* bsum) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    const uint32_t d = rec[i].dst - lo, cls = pl ? 0u : max_emit(rec[i].tt & 0xFF);
+    atomicAdd(&cnt[d], 1u);
+    if (cls) atomicAdd(&bsum[d], cls);
+}
+
+__global__ void k_scatter_dense(const Msg* __restrict__ rec, uint32_t m, uint32_t lo,
+                                const uint32_t* __restrict__ in_beg, uint32_t* fill, uint32_t* idx) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    const uint32_t d = rec[i].dst - lo;
+    idx[in_beg[d] + atomicAdd(&fill[d], 1u)] = i;
+}
+
+// short runs in registers (odd-even transposition network); longer ones are
+// listed for k_run_sort_long (n_long: its device-side count)
+__global__ void k_run_sort(const uint32_t* __restrict__ in_beg, const uint32_t* __restrict__ cnt,
+                           uint32_t n, uint32_t* idx, uint32_t* long_list, uint32_t* n_long) {
+    uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
+    if (d >= n) return;
+    const uint32_t k = cnt[d];
+    if (k < 2) return;
+    if (k > RUN_SHORT) { long_list[atomicAdd(n_long, 1u)] = d; return; }
+    uint32_t* p = idx + in_beg[d];
+    uint32_t v[RUN_SHORT];
+#pragma unroll
+    for (uint32_t t = 0; t < RUN_SHORT; t++) v[t] = t < k ? p[t] : 0xFFFFFFFFu;
+#pragma unroll
+    for (uint32_t r = 0; r < RUN_SHORT; r++) {
+#pragma unroll
+        for (uint32_t t = r & 1; t + 1 < RUN_SHORT; t += 2) {
+            const uint32_t a = v[t], b = v[t + 1];
+            v[t] = min(a, b);
+            v[t + 1] = max(a, b);
+        }
+    }
+#pragma unroll
+    for (uint32_t t = 0; t < RUN_SHORT; t++)
+        if (t < k) p[t] = v[t];
+}
+
+// bitonic sort of p[0..k) (k <= RUN_LDS) through LDS, whole block
+__device__ void block_sort_lds(uint32_t* sv, uint32_t* p, uint32_t k) {
+    uint32_t P = 1;
+    while (P < k) P <<= 1;
+    for (uint32_t t = threadIdx.x; t < P; t += blockDim.x) sv[t] = t < k ? p[t] : 0xFFFFFFFFu;
+    __syncthreads();
+    for (uint32_t kk = 2; kk <= P; kk <<= 1) {
+        for (uint32_t jj = kk >> 1; jj > 0; jj >>= 1) {
+            for (uint32_t t = threadIdx.x; t < P; t += blockDim.x) {
+                const uint32_t u = t ^ jj;
+                if (u > t) {
+                    const uint32_t a = sv[t], b = sv[u];
+                    if ((a > b) == ((t & kk) == 0)) { sv[t] = b; sv[u] = a; }
+                }
+            }
+            __syncthreads();
+        }
+    }
+    for (uint32_t t = threadIdx.x; t < k; t += blockDim.x) p[t] = sv[t];
+    __syncthreads();
+}
+
+// one block per listed run; a run longer than RUN_LDS (a join storm on one
+// contact) is sorted in RUN_LDS chunks, then merged pairwise through tmp
+// (the run's own range of it) -- slow, and only for such rounds
+__global__ void __launch_bounds__(256) k_run_sort_long(const uint32_t* __restrict__ in_beg,
+                                                       const uint32_t* __restrict__ cnt, uint32_t* idx,
+                                                       uint32_t* tmp, const uint32_t* __restrict__ long_list,
+                                                       const uint32_t* n_long) {
+    __shared__ uint32_t sv[RUN_LDS];
+    const uint32_t nl = *n_long;
+    for (uint32_t q = blockIdx.x; q < nl; q += gridDim.x) {
+        const uint32_t d = long_list[q], k = cnt[d];
+        uint32_t* p = idx + in_beg[d];
+        for (uint32_t c0 = 0; c0 < k; c0 += RUN_LDS) block_sort_lds(sv, p + c0, min(RUN_LDS, k - c0));
+        uint32_t* x = p;
+        uint32_t* y = tmp + in_beg[d];
+        for (uint32_t wd = RUN_LDS; wd < k; wd *= 2) {
+            for (uint32_t a0 = threadIdx.x * 2 * wd; a0 < k; a0 += blockDim.x * 2 * wd) {
+                const uint32_t m0 = min(a0 + wd, k), e0 = min(a0 + 2 * wd, k);
+                uint32_t u = a0, v = m0, o = a0;
+                while (u < m0 && v < e0) y[o++] = x[u] <= x[v] ? x[u++] : x[v++];
+                while (u < m0) y[o++] = x[u++];
+                while (v < e0) y[o++] = x[v++];
+            }
+            __syncthreads();
+            uint32_t* z = x; x = y; y = z;
+        }
+        if (x != p)
+            for (uint32_t t = threadIdx.x; t < k; t += blockDim.x) p[t] = x[t];
+        __syncthreads();
+    }
+}
+
+// cnt[0..n], bsum, fill, and the long-run count
+__global__ void k_route_clear(uint32_t* cnt, uint32_t* bsum, uint32_t* fill, uint32_t n, uint32_t* n_long) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i <= n) cnt[i] = 0;
+    if (i < n) { bsum[i] = 0; fill[i] = 0; }
+    if (i == 0) *n_long = 0;
 }
 
 __device__ __forceinline__ bool due(uint32_t period, uint32_t r, uint32_t start) {
@@ -166,9 +322,10 @@ __device__ __forceinline__ bool due(uint32_t period, uint32_t r, uint32_t start)
 // scan, origin, outstanding lazy pushes).  Also counts live nodes and
 // messages addressed to dead ones.
 __global__ void k_node_prep(RoundArgs a, const uint32_t* bsum, uint64_t* bound, uint32_t* work,
-                            uint64_t* part) {
+                            uint64_t* part, uint32_t* ocnt) {
     __shared__ uint64_t s_up, s_drop;
     if (threadIdx.x == 0) { s_up = 0; s_drop = 0; }
+    if (blockIdx.x == 0 && threadIdx.x == 0) { a.ktime[0] = ~0ull; a.ktime[1] = 0; }
     __syncthreads();
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < a.n_local) {
@@ -205,6 +362,7 @@ __global__ void k_node_prep(RoundArgs a, const uint32_t* bsum, uint64_t* bound, 
         }
         bound[i] = b;
         work[i] = w;
+        ocnt[i] = 0;               // consume writes the count of every node it runs
     }
     __syncthreads();
     if (threadIdx.x < NST) {
@@ -263,6 +421,18 @@ __global__ void k_owner_bounds(const uint32_t* owner, uint32_t m, uint32_t g, ui
     off[t] = lo;
 }
 
+// records src[slots[i]] -> out[i] for i < *pm, grid-stride, 4 lanes x 16 B
+__global__ void k_gather_dev(const Msg* __restrict__ rec, const uint32_t* __restrict__ slots,
+                             const uint32_t* __restrict__ pm, Msg* __restrict__ out) {
+    const uint64_t m4 = (uint64_t)*pm * 4;
+    for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < m4;
+         t += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t i = t >> 2;
+        const uint4* sp = reinterpret_cast<const uint4*>(&rec[slots[i]]);
+        reinterpret_cast<uint4*>(&out[i])[t & 3] = sp[t & 3];
+    }
+}
+
 // send buffer in owner order: 64-B records, 4 lanes x 16 B per record
 __global__ void k_gather(const Msg* __restrict__ rec, const uint32_t* __restrict__ slots, uint32_t m,
                          Msg* __restrict__ out) {
@@ -271,16 +441,6 @@ __global__ void k_gather(const Msg* __restrict__ rec, const uint32_t* __restrict
     if (i >= m) return;
     const uint4* s = reinterpret_cast<const uint4*>(&rec[slots[i]]);
     reinterpret_cast<uint4*>(&out[i])[t & 3] = s[t & 3];
-}
-
-// receive side: route keys of the received records (local dst | bound)
-__global__ void k_rkeys(const Msg* __restrict__ rec, uint32_t m, uint32_t lo, uint32_t* keys,
-                        uint32_t* vals, uint32_t pl) {
-    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= m) return;
-    uint32_t type = rec[i].tt & 0xFF;
-    keys[i] = (rec[i].dst - lo) | ((pl ? 0u : max_emit(type)) << KEY_DST_BITS);
-    vals[i] = i;
 }
 
 // one block per stats slot; lanes stride over the per-block partials
@@ -303,11 +463,15 @@ template <typename T>
 struct DBuf {
     T* p = nullptr;
     size_t n = 0;
-    int ensure(size_t want) {   // grow, contents not kept
+    // grow to the next power of two (per-round sizes peak on broadcast
+    // rounds; a 25 % step re-allocated -- 1 ms each -- for many rounds),
+    // contents not kept
+    int ensure(size_t want) {
         if (want <= n) return PSIM_OK;
         if (p) (void)hipFree(p);
         p = nullptr; n = 0;
-        size_t cap = std::max<size_t>(want + want / 4, 1024);
+        size_t cap = 1024;
+        while (cap < want) cap <<= 1;
         if (hipMalloc(&p, cap * sizeof(T)) != hipSuccess) return PSIM_ENOMEM;
         n = cap;
         return PSIM_OK;
@@ -334,6 +498,8 @@ int bits_for(uint64_t n) {
     return b;
 }
 
+enum { PIN_TOTAL = NST + 2, PIN_M = NST + 3 };
+
 struct Shard {
     uint32_t idx = 0, lo = 0, n = 0;    // global shard index, owned [lo, lo + n)
     hipStream_t stream = nullptr;
@@ -348,10 +514,11 @@ struct Shard {
     uint32_t m_in = 0;
     DBuf<Msg> outbox;                   // this round's emissions (holes between node regions)
     DBuf<Msg> recvbuf;                  // G > 1: received records, in source-shard order
-    DBuf<Msg> inbox;                    // next round's records, dense, in inbox order
+    DBuf<Msg> inbox[2];                 // records by node run, in inbox order: inbox[in_cur] is
+    int in_cur = 0;                     // read by this round's consume, the other one is routed into
     // per-round scratch
     DBuf<uint32_t> okey, ocnt, dpos, keys, vals, owner, owner_s, vals_s, cnt, bsum, in_beg, work,
-        alist, d_nact;
+        alist, d_nact, fill, long_list, n_long, tmp;
     DBuf<uint4> desc;
     DBuf<uint64_t> bound, obase, stat_part, stat_out, d_off;
     DBuf<uint8_t> cub_tmp;
@@ -362,8 +529,16 @@ struct Shard {
     int pay_cur = 0;
     std::vector<uint64_t> soff, scnt;   // per destination shard (G + 1 offsets)
     uint32_t m_out = 0, pgrid = 0, cgrid = 0;
-    uint64_t st_host[NST];
-    hipEvent_t ev[KT_N][2];
+    // pinned host words: NST stats and the consume span (stat_out), then the
+    // outbox total and the routed record count: the round's two read-backs
+    uint64_t* pin = nullptr;
+    // phase timers: event pairs recorded on the stream and read back once per
+    // round, after the round's final synchronisation (no sync per phase)
+    static constexpr int MAXT = 32;
+    hipEvent_t ev[MAXT][2];
+    int tk[MAXT];
+    int tn = 0;
+    hipEvent_t wait_ev = nullptr;
     bool ev_live = false;
 };
 
@@ -390,6 +565,10 @@ struct psim_handle {
     std::vector<uint8_t> started;       // full strategy: ids ever started (no restarts)
     double kt_ms[KT_N] = {0};
     uint64_t kt_n[KT_N] = {0};
+    // per-phase event timers (PSIM_PHASE_TIMERS=1): each event pair puts a
+    // ~10 us bubble between kernels, so by default only k_consume is timed,
+    // from its in-kernel span (RoundArgs::ktime)
+    bool phase_timers = false;
 };
 
 namespace {
@@ -418,26 +597,35 @@ RoundArgs make_args(psim_handle* h, Shard* s) {
     a.strategy = c.strategy; a.periodic = c.periodic_interval; a.scamp_c = c.scamp_c;
     a.fanout = c.fanout; a.fw = h->fw;
     a.fbits = s->fbits.p; a.sview = s->sview.p; a.sinv = s->sinv.p;
+    a.ktime = reinterpret_cast<unsigned long long*>(s->stat_out.p + NST);
     return a;
 }
 
-// per-kernel-class device time, HIP events on the shard's stream
+// per-kernel-class device time, HIP events on the shard's stream; the
+// elapsed times are collected by flush_timers once the round has synchronised
 struct KTimer {
-    psim_handle* h;
     Shard* s;
-    int k;
-    KTimer(psim_handle* h_, Shard* s_, int k_) : h(h_), s(s_), k(k_) {
-        (void)hipEventRecord(s->ev[k][0], s->stream);
+    int slot;
+    KTimer(psim_handle* h, Shard* s_, int k) : s(s_), slot(-1) {
+        if (!h->phase_timers || s->tn >= Shard::MAXT) return;
+        slot = s->tn++;
+        s->tk[slot] = k;
+        (void)hipEventRecord(s->ev[slot][0], s->stream);
     }
     ~KTimer() {
-        (void)hipEventRecord(s->ev[k][1], s->stream);
-        (void)hipEventSynchronize(s->ev[k][1]);
-        float ms = 0;
-        (void)hipEventElapsedTime(&ms, s->ev[k][0], s->ev[k][1]);
-        h->kt_ms[k] += ms;
-        h->kt_n[k]++;
+        if (slot >= 0) (void)hipEventRecord(s->ev[slot][1], s->stream);
     }
 };
+
+void flush_timers(psim_handle* h, Shard* s) {
+    for (int i = 0; i < s->tn; i++) {
+        float ms = 0;
+        if (hipEventElapsedTime(&ms, s->ev[i][0], s->ev[i][1]) != hipSuccess) continue;
+        h->kt_ms[s->tk[i]] += ms;
+        h->kt_n[s->tk[i]]++;
+    }
+    s->tn = 0;
+}
 
 template <typename T>
 int scan_excl(Shard* s, const T* in, T* out, uint32_t n) {
@@ -459,11 +647,29 @@ int sort_pairs(Shard* s, const uint32_t* kin, uint32_t* kout, const uint32_t* vi
     return PSIM_OK;
 }
 
+// Wait for the shard's stream by polling an event: a blocking synchronise
+// sleeps the host thread, and waking it cost ~100 us of idle GPU per round
+int stream_wait(Shard* s) {
+    HIP_TRY(hipEventRecord(s->wait_ev, s->stream));
+    hipError_t e;
+    while ((e = hipEventQuery(s->wait_ev)) == hipErrorNotReady) {
+    }
+    if (e != hipSuccess) {
+        // an event query error is reported once and settled by a blocking
+        // synchronise, which fails too if the stream itself has faulted
+        static bool said = false;
+        if (!said) std::fprintf(stderr, "psim: event query: %s; synchronising\n", hipGetErrorString(e));
+        said = true;
+        HIP_TRY(hipStreamSynchronize(s->stream));
+    }
+    return PSIM_OK;
+}
+
 template <typename T>
 T read1(Shard* s, const T* p) {
     T v{};
     (void)hipMemcpyAsync(&v, p, sizeof(T), hipMemcpyDeviceToHost, s->stream);
-    (void)hipStreamSynchronize(s->stream);
+    (void)stream_wait(s);
     return v;
 }
 
@@ -506,17 +712,12 @@ int phase_events_prepare(psim_handle* h, Shard* s, const RoundCtl& ctl, RoundArg
     }
     {
         KTimer t(h, s, KT_PREPARE);
-        HIP_TRY(hipMemsetAsync(s->cnt.p, 0, (size_t)n * 4, s->stream));
-        HIP_TRY(hipMemsetAsync(s->bsum.p, 0, (size_t)n * 4, s->stream));
-        if (s->m_in) {
-            uint32_t g = std::min<uint32_t>(grid_for(s->m_in), 4096);
-            k_runs<<<g, BLK, 0, s->stream>>>(s->ikeys.p, s->m_in, s->cnt.p, s->bsum.p);
-        }
         a.in_cnt = s->cnt.p;
         s->pgrid = grid_for(n);
         s->cgrid = std::min<uint32_t>(grid_for(n), h->consume_blocks);
         TRY(s->stat_part.ensure((size_t)(s->pgrid + s->cgrid) * NST));
-        k_node_prep<<<s->pgrid, BLK, 0, s->stream>>>(a, s->bsum.p, s->bound.p, s->work.p, s->stat_part.p);
+        k_node_prep<<<s->pgrid, BLK, 0, s->stream>>>(a, s->bsum.p, s->bound.p, s->work.p, s->stat_part.p,
+                                                     s->ocnt.p);
         {
             size_t tb = 0;
             hipcub::CountingInputIterator<uint32_t> ids(s->lo);
@@ -526,19 +727,26 @@ int phase_events_prepare(psim_handle* h, Shard* s, const RoundCtl& ctl, RoundArg
             HIP_TRY(hipcub::DeviceSelect::Flagged(s->cub_tmp.p, tb, ids, s->work.p, s->alist.p,
                                                   s->d_nact.p, n, s->stream));
         }
-        TRY(scan_excl(s, s->cnt.p, s->in_beg.p, n));
-        TRY(scan_excl(s, s->bound.p, s->obase.p, n));
+        // bound[n] = 0, so obase[n] is the outbox total (in_beg: the last route's scan)
+        TRY(scan_excl(s, s->bound.p, s->obase.p, n + 1));
         if (s->m_in > DESC_CNT_MASK) return PSIM_ENOMEM;   // per-node inbox counts must fit 28 bits
-        uint64_t total = read1(s, s->bound.p + (n - 1)) + read1(s, s->obase.p + (n - 1));
+        HIP_TRY(hipMemcpyAsync(s->pin + PIN_TOTAL, s->obase.p + n, 8, hipMemcpyDeviceToHost, s->stream));
+        TRY(stream_wait(s));
+        const uint64_t total = s->pin[PIN_TOTAL];
         if (total >= 0xFFFFFFFFull) return PSIM_ENOMEM;
         TRY(s->outbox.ensure(total + 1));
         TRY(s->okey.ensure(total + 1));
+        if (h->G == 1) {            // the route runs without a host sync: sized by the bound
+            TRY(s->ivals.ensure(total + 1));
+            TRY(s->tmp.ensure(total + 1));
+            TRY(s->inbox[s->in_cur ^ 1].ensure(total + 1));
+        }
         k_desc<<<std::min<uint32_t>(grid_for(n), 4096), BLK, 0, s->stream>>>(
             s->alist.p, s->d_nact.p, s->in_beg.p, s->cnt.p, s->obase.p, s->start.p, a, s->desc.p);
     }
     a.in_beg = s->in_beg.p;
     a.desc = s->desc.p; a.n_alist = s->d_nact.p;
-    a.rec_in = s->inbox.p;
+    a.rec_in = s->inbox[s->in_cur].p;
     a.obase = s->obase.p;
     a.rec_out = s->outbox.p;
     a.okey = s->okey.p; a.ocnt = s->ocnt.p;
@@ -558,8 +766,6 @@ int phase_consume(psim_handle* h, Shard* s, RoundArgs& a) {
         a.pay_cap = (uint32_t)(s->pay[s->pay_cur].n / h->fw);
         HIP_TRY(hipMemsetAsync(s->pay_top.p, 0, 4, s->stream));
     }
-    KTimer t(h, s, KT_CONSUME);
-    HIP_TRY(hipMemsetAsync(s->ocnt.p, 0, (size_t)s->n * 4, s->stream));
     if (a.pl) k_consume_pl<<<s->cgrid, BLK, 0, s->stream>>>(a);
     else k_consume<<<s->cgrid, BLK, 0, s->stream>>>(a);
     HIP_TRY(hipGetLastError());
@@ -567,14 +773,15 @@ int phase_consume(psim_handle* h, Shard* s, RoundArgs& a) {
     return PSIM_OK;
 }
 
-// records of the sorted inbox, gathered dense in inbox order: k_consume
-// then reads each node's messages as one contiguous run
-int gather_inbox(psim_handle* h, Shard* s, const Msg* src) {
-    TRY(s->inbox.ensure((size_t)s->m_in + 1));
+// records of the grouped source indices, gathered into the other inbox:
+// k_consume then reads each node's messages as one contiguous run.  The
+// record count is read on the device (in_beg[n] for G == 1).
+int gather_inbox(psim_handle* h, Shard* s, const Msg* src, const uint32_t* dev_m, uint32_t max_m) {
     KTimer t(h, s, KT_GATHER);
-    if (s->m_in)
-        k_gather<<<grid_for((uint64_t)s->m_in * 4), BLK, 0, s->stream>>>(src, s->ivals.p, s->m_in,
-                                                                          s->inbox.p);
+    if (max_m)
+        k_gather_dev<<<std::min<uint32_t>(grid_for((uint64_t)max_m * 4), 8192), BLK, 0, s->stream>>>(
+            src, s->ivals.p, dev_m, s->inbox[s->in_cur ^ 1].p);
+    s->in_cur ^= 1;
     return PSIM_OK;
 }
 
@@ -593,15 +800,47 @@ int phase_compact(psim_handle* h, Shard* s) {
     return PSIM_OK;
 }
 
-// G == 1: the stable sort by dst is the whole route
+// Route counting pass over the outbox runs (dense == nullptr) or the `m`
+// records of `dense`: per-destination counts and bounds, run starts
+// (in_beg[n] = the record count, on the device)
+int route_count(psim_handle* h, Shard* s, const Msg* dense, uint32_t m) {
+    const uint32_t n = s->n;
+    KTimer t(h, s, KT_SCAN);
+    k_route_clear<<<grid_for(n + 1), BLK, 0, s->stream>>>(s->cnt.p, s->bsum.p, s->fill.p, n, s->n_long.p);
+    if (!dense)
+        k_route_runs<false><<<grid_for(n), BLK, 0, s->stream>>>(s->okey.p, s->obase.p, s->ocnt.p, n, s->lo,
+                                                                s->cnt.p, s->bsum.p, nullptr, nullptr,
+                                                                nullptr);
+    else if (m)
+        k_count_dense<<<grid_for(m), BLK, 0, s->stream>>>(dense, m, s->lo,
+                                                          h->cfg.manager == PSIM_MANAGER_PLUGGABLE,
+                                                          s->cnt.p, s->bsum.p);
+    TRY(scan_excl(s, s->cnt.p, s->in_beg.p, n + 1));
+    return PSIM_OK;
+}
+
+// sort every run of ivals (after a scatter)
+int route_sort_runs(Shard* s) {
+    k_run_sort<<<grid_for(s->n), BLK, 0, s->stream>>>(s->in_beg.p, s->cnt.p, s->n, s->ivals.p,
+                                                      s->long_list.p, s->n_long.p);
+    k_run_sort_long<<<std::min<uint32_t>(s->n, 512), 256, 0, s->stream>>>(
+        s->in_beg.p, s->cnt.p, s->ivals.p, s->tmp.p, s->long_list.p, s->n_long.p);
+    return PSIM_OK;
+}
+
+// G == 1: the outbox runs grouped by destination are the whole route
 int phase_route_local(psim_handle* h, Shard* s) {
-    TRY(phase_compact(h, s));
-    TRY(s->ikeys.ensure(s->m_out + 1));
-    TRY(s->ivals.ensure(s->m_out + 1));
-    KTimer t(h, s, KT_SORT);
-    TRY(sort_pairs(s, s->keys.p, s->ikeys.p, s->vals.p, s->ivals.p, s->m_out, bits_for(s->n)));
-    s->m_in = s->m_out;
-    return gather_inbox(h, s, s->outbox.p);
+    TRY(route_count(h, s, nullptr, 0));
+    {
+        KTimer t(h, s, KT_SORT);
+        k_route_runs<true><<<grid_for(s->n), BLK, 0, s->stream>>>(s->okey.p, s->obase.p, s->ocnt.p, s->n,
+                                                                  s->lo, nullptr, nullptr, s->in_beg.p,
+                                                                  s->fill.p, s->ivals.p);
+        TRY(route_sort_runs(s));
+    }
+    // (m_in: read back with the round's stats; ivals, tmp and the inbox were
+    // sized in prepare by the outbox total, which bounds it)
+    return gather_inbox(h, s, s->outbox.p, s->in_beg.p + s->n, (uint32_t)std::min<uint64_t>(s->pin[PIN_TOTAL], 0xFFFFFFFFu));
 }
 
 // G > 1, sender side: stable partition by owner shard, records gathered
@@ -622,7 +861,7 @@ int phase_partition(psim_handle* h, Shard* s) {
         k_owner_bounds<<<1, 128, 0, s->stream>>>(s->owner_s.p, m, h->G, s->d_off.p);
         HIP_TRY(hipMemcpyAsync(s->soff.data(), s->d_off.p, (h->G + 1) * 8, hipMemcpyDeviceToHost,
                                s->stream));
-        HIP_TRY(hipStreamSynchronize(s->stream));
+        TRY(stream_wait(s));
     }
     s->soff[h->G] = m;
     s->scnt.resize(h->G);
@@ -630,18 +869,21 @@ int phase_partition(psim_handle* h, Shard* s) {
     return PSIM_OK;
 }
 
-// G > 1, receiver side: route keys of the shard-ordered concatenation, stable sort by dst
+// G > 1, receiver side: the shard-ordered concatenation grouped by dst
 int phase_receive(psim_handle* h, Shard* s, uint32_t m) {
-    TRY(s->keys.ensure(m + 1)); TRY(s->vals.ensure(m + 1));
-    TRY(s->ikeys.ensure(m + 1)); TRY(s->ivals.ensure(m + 1));
-    KTimer t(h, s, KT_SORT);
-    if (m) {
-        k_rkeys<<<grid_for(m), BLK, 0, s->stream>>>(s->recvbuf.p, m, s->lo, s->keys.p, s->vals.p,
-                                                    h->cfg.manager == PSIM_MANAGER_PLUGGABLE);
-        TRY(sort_pairs(s, s->keys.p, s->ikeys.p, s->vals.p, s->ivals.p, m, bits_for(s->n)));
+    TRY(s->ivals.ensure(m + 1));
+    TRY(s->tmp.ensure(m + 1));
+    TRY(s->inbox[s->in_cur ^ 1].ensure(m + 1));
+    TRY(route_count(h, s, s->recvbuf.p, m));
+    {
+        KTimer t(h, s, KT_SORT);
+        if (m)
+            k_scatter_dense<<<grid_for(m), BLK, 0, s->stream>>>(s->recvbuf.p, m, s->lo, s->in_beg.p,
+                                                               s->fill.p, s->ivals.p);
+        TRY(route_sort_runs(s));
     }
     s->m_in = m;
-    return gather_inbox(h, s, s->recvbuf.p);
+    return gather_inbox(h, s, s->recvbuf.p, s->in_beg.p + s->n, m);
 }
 
 // virtual shards of this process: device copies between shard buffers
@@ -682,7 +924,7 @@ int exchange_rccl(psim_handle* h) {
         NCCL_TRY(ncclAllToAll(h->comm_cnt.p, h->comm_cnt.p + G, 1, ncclUint64, h->comm, s->stream));
         std::vector<uint64_t> rcnt(G);
         HIP_TRY(hipMemcpyAsync(rcnt.data(), h->comm_cnt.p + G, G * 8, hipMemcpyDeviceToHost, s->stream));
-        HIP_TRY(hipStreamSynchronize(s->stream));
+        TRY(stream_wait(s));
         std::vector<uint64_t> roff(G);
         for (uint32_t g = 0; g < G; g++) { roff[g] = m; m += rcnt[g]; }
         TRY(s->recvbuf.ensure(m + 1));
@@ -730,6 +972,7 @@ int run_round(psim_handle* h, uint64_t* st) {
         for (uint32_t j : h->pend_join) if (j == h->pend_root) up_after = true;
         if (up_after) { ctl.origin = true; ctl.origin_node = h->pend_root; ctl.origin_msg = h->pend_msg; }
     }
+    for (Shard* s : h->shards) s->tn = 0;        // (timers of a round that failed)
     std::vector<RoundArgs> args(h->shards.size());   // (consume fills the payload arena fields)
     for (size_t i = 0; i < h->shards.size(); i++) TRY(phase_events_prepare(h, h->shards[i], ctl, args[i]));
     for (size_t i = 0; i < h->shards.size(); i++) TRY(phase_consume(h, h->shards[i], args[i]));
@@ -743,9 +986,17 @@ int run_round(psim_handle* h, uint64_t* st) {
     for (Shard* s : h->shards) TRY(phase_stats(h, s, h->pend_crash));
     memset(st, 0, NST * 8);
     for (Shard* s : h->shards) {
-        HIP_TRY(hipMemcpyAsync(s->st_host, s->stat_out.p, NST * 8, hipMemcpyDeviceToHost, s->stream));
-        HIP_TRY(hipStreamSynchronize(s->stream));
-        for (int k = 0; k < NST; k++) st[k] += s->st_host[k];
+        HIP_TRY(hipMemcpyAsync(s->pin, s->stat_out.p, (NST + 2) * 8, hipMemcpyDeviceToHost, s->stream));
+        if (h->G == 1)
+            HIP_TRY(hipMemcpyAsync(s->pin + PIN_M, s->in_beg.p + s->n, 4, hipMemcpyDeviceToHost, s->stream));
+        TRY(stream_wait(s));
+        flush_timers(h, s);
+        for (int k = 0; k < NST; k++) st[k] += s->pin[k];
+        if (h->G == 1) s->m_in = (uint32_t)s->pin[PIN_M];   // routed this round
+        if (s->pin[NST] != ~0ull && s->pin[NST + 1] > s->pin[NST]) {   // 100 MHz ticks
+            h->kt_ms[KT_CONSUME] += (double)(s->pin[NST + 1] - s->pin[NST]) * 1e-5;
+            h->kt_n[KT_CONSUME]++;
+        }
     }
     if (h->world > 1) {
         Shard* s = h->shards[0];
@@ -753,7 +1004,7 @@ int run_round(psim_handle* h, uint64_t* st) {
         HIP_TRY(hipMemcpyAsync(h->comm_cnt.p, st, NST * 8, hipMemcpyHostToDevice, s->stream));
         NCCL_TRY(ncclAllReduce(h->comm_cnt.p, h->comm_cnt.p, NST, ncclUint64, ncclSum, h->comm, s->stream));
         HIP_TRY(hipMemcpyAsync(st, h->comm_cnt.p, NST * 8, hipMemcpyDeviceToHost, s->stream));
-        HIP_TRY(hipStreamSynchronize(s->stream));
+        TRY(stream_wait(s));
     }
     h->pend_crash.clear(); h->pend_join.clear(); h->pend_contact.clear();
     h->pend_part_set = h->pend_part_clear = false;
@@ -776,7 +1027,10 @@ void fill_stats(const uint64_t* s, uint64_t round, psim_round_stats* o) {
 
 int shard_alloc(psim_handle* h, Shard* s) {
     HIP_TRY(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
-    for (int k = 0; k < KT_N; k++) {
+    HIP_TRY(hipEventCreateWithFlags(&s->wait_ev, hipEventDisableTiming));
+    HIP_TRY(hipHostMalloc((void**)&s->pin, (NST + 8) * sizeof(uint64_t), hipHostMallocDefault));
+    memset(s->pin, 0, (NST + 8) * sizeof(uint64_t));
+    for (int k = 0; k < Shard::MAXT; k++) {
         HIP_TRY(hipEventCreate(&s->ev[k][0]));
         HIP_TRY(hipEventCreate(&s->ev[k][1]));
     }
@@ -790,12 +1044,13 @@ int shard_alloc(psim_handle* h, Shard* s) {
     rc |= s->pt_all.alloc(n * PSIM_PT_MEMBERS_CAP); rc |= s->pt_com.alloc(n * PSIM_PT_MEMBERS_CAP);
     rc |= s->pt_eag.alloc(n * PSIM_PT_SET_CAP); rc |= s->pt_laz.alloc(n * PSIM_PT_SET_CAP);
     rc |= s->pt_out.alloc(n * PSIM_PT_OUT_CAP); rc |= s->start.alloc(n);
-    rc |= s->ocnt.alloc(n); rc |= s->dpos.alloc(n); rc |= s->cnt.alloc(n); rc |= s->bsum.alloc(n);
-    rc |= s->in_beg.alloc(n); rc |= s->bound.alloc(n); rc |= s->obase.alloc(n);
+    rc |= s->ocnt.alloc(n); rc |= s->dpos.alloc(n); rc |= s->cnt.alloc(n + 1); rc |= s->bsum.alloc(n);
+    rc |= s->in_beg.alloc(n + 1); rc |= s->bound.alloc(n + 1); rc |= s->obase.alloc(n + 1);
+    rc |= s->fill.alloc(n); rc |= s->long_list.alloc(n); rc |= s->n_long.alloc(1);
     rc |= s->work.alloc(n); rc |= s->alist.alloc(n); rc |= s->desc.alloc(n); rc |= s->d_nact.alloc(1);
-    rc |= s->stat_out.alloc(NST);
+    rc |= s->stat_out.alloc(NST + 2);   // + the consume span
     rc |= s->ikeys.alloc(1024); rc |= s->ivals.alloc(1024);
-    rc |= s->recvbuf.alloc(1024); rc |= s->inbox.alloc(1024); rc |= s->outbox.alloc(1024);
+    rc |= s->recvbuf.alloc(1024); rc |= s->inbox[0].alloc(1024); rc |= s->inbox[1].alloc(1024); rc |= s->outbox.alloc(1024);
     if (h->cfg.manager == PSIM_MANAGER_PLUGGABLE) {
         if (h->cfg.strategy == PSIM_STRATEGY_FULL) {
             rc |= s->fbits.alloc(n * h->fw);
@@ -819,17 +1074,22 @@ void shard_free(Shard* s) {
     s->act.release(); s->pas.release(); s->sentp.release(); s->senti.release();
     s->recvp.release(); s->recvi.release(); s->pt_all.release(); s->pt_com.release();
     s->pt_eag.release(); s->pt_laz.release(); s->pt_out.release(); s->start.release();
-    s->ikeys.release(); s->ivals.release(); s->recvbuf.release(); s->inbox.release();
+    s->ikeys.release(); s->ivals.release(); s->recvbuf.release(); s->inbox[0].release(); s->inbox[1].release();
+    if (s->pin) (void)hipHostFree(s->pin);
+    if (s->wait_ev) (void)hipEventDestroy(s->wait_ev);
+    s->wait_ev = nullptr;
+    s->pin = nullptr;
     s->outbox.release(); s->okey.release(); s->ocnt.release(); s->dpos.release();
     s->keys.release(); s->vals.release(); s->owner.release(); s->owner_s.release();
     s->vals_s.release(); s->cnt.release(); s->bsum.release(); s->in_beg.release();
+    s->fill.release(); s->long_list.release(); s->n_long.release(); s->tmp.release();
     s->work.release(); s->alist.release(); s->desc.release(); s->d_nact.release(); s->bound.release();
     s->obase.release(); s->stat_part.release(); s->stat_out.release(); s->d_off.release();
     s->cub_tmp.release(); s->ev_ids.release(); s->ev_contacts.release(); s->sendbuf.release();
     s->sview.release(); s->sinv.release(); s->fbits.release(); s->pay[0].release(); s->pay[1].release();
     s->pay_top.release();
     if (s->ev_live)
-        for (int k = 0; k < KT_N; k++) {
+        for (int k = 0; k < Shard::MAXT; k++) {
             (void)hipEventDestroy(s->ev[k][0]);
             (void)hipEventDestroy(s->ev[k][1]);
         }
@@ -906,6 +1166,10 @@ int psim_create(const psim_config* cfg, psim_handle** out) {
     if (dev < 0 && hipGetDevice(&dev) != hipSuccess) { delete h; return PSIM_EDEVICE; }
     if (hipSetDevice(dev) != hipSuccess) { delete h; return PSIM_EDEVICE; }
     h->consume_blocks = psim::consume_grid();
+    {
+        const char* e = getenv("PSIM_PHASE_TIMERS");
+        h->phase_timers = e && *e && *e != '0';
+    }
     h->device = dev;
     for (uint32_t g = 0; g < G; g++) {
         if (world > 1 && g != cfg->shard_rank) continue;

@@ -33,6 +33,9 @@ struct RoundArgs {
     uint32_t* okey;
     uint32_t* ocnt;
     uint64_t* stat_part;   // [gridDim.x][NST]
+    // consume kernel span: min block-start and max block-end s_memrealtime
+    // (100 MHz), reset by k_node_prep
+    unsigned long long* ktime;
     // pluggable manager (k_consume_pl); Hdr fields are reused as
     // join_contact = pending contact, pt_root = last ping round,
     // have = hello sent, act_n = view length, pas_n = in_view length

@@ -449,6 +449,7 @@ __global__ void __launch_bounds__(256) k_consume_pl(RoundArgs args) {
     __shared__ uint64_t sst[NST];
     __shared__ uint32_t scratch[PL_WAVES][64];
     for (int i = threadIdx.x; i < NST; i += blockDim.x) sst[i] = 0;
+    if (threadIdx.x == 0) atomicMin(&args.ktime[0], (unsigned long long)__builtin_amdgcn_s_memrealtime());
     __syncthreads();
     const uint32_t wid = threadIdx.x >> 6;
     const uint32_t gw = uni(blockIdx.x * PL_WAVES + wid);
@@ -475,6 +476,7 @@ __global__ void __launch_bounds__(256) k_consume_pl(RoundArgs args) {
     __syncthreads();
     for (int i = threadIdx.x; i < NST; i += blockDim.x)
         args.stat_part[(size_t)blockIdx.x * NST + i] = sst[i];
+    if (threadIdx.x == 0) atomicMax(&args.ktime[1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
 }
 
 }  // namespace psim
