@@ -152,9 +152,10 @@ __global__ void k_bcast_reset(Hdr* hdr, uint32_t n, uint32_t bit) {
 // emission order: ascending source index (an outbox slot, or a position in
 // the source-shard-ordered receive buffer), which is (src, seq) order.
 //   count    one atomic per record: run length and emission-bound sum of its
-//            destination (cnt has n + 1 entries, cnt[n] = 0)
+//            destination (cb: n + 1 entries, cb[n] = 0), and the record's
+//            arrival rank in its run
 //   scan     run starts in_beg[0..n]; in_beg[n] is the record count m
-//   scatter  each record's source index into its run, at an atomic cursor
+//   scatter  each record's source index to in_beg[dst] + rank
 //   sort     every run ascending: <= RUN_SHORT by its own thread in
 //            registers, longer ones by one block (bitonic in LDS up to
 //            RUN_LDS, LDS-sorted chunks merged through `tmp` beyond)
@@ -166,13 +167,16 @@ constexpr uint32_t RUN_LDS = 2048;
 // A wave takes 64 consecutive source nodes and expands their outbox runs
 // (ocnt[i] records at obase[i]) into consecutive record numbers t: lane l
 // handles records l, l + 64, ..., so okey is read in slot order.
+//   count:   one 64-bit atomic per record adds 1 to its destination's count
+//            (low word) and its emission bound to the bound sum (high word);
+//            the old count is the record's arrival rank in its run
+//   scatter: the record's slot to in_beg[dst] + rank, no atomics
 template <bool SCATTER>
 __global__ void __launch_bounds__(256) k_route_runs(const uint32_t* __restrict__ okey,
                                                     const uint64_t* __restrict__ obase,
                                                     const uint32_t* __restrict__ ocnt, uint32_t n,
-                                                    uint32_t lo, uint32_t* cnt, uint32_t* bsum,
-                                                    const uint32_t* __restrict__ in_beg, uint32_t* fill,
-                                                    uint32_t* idx) {
+                                                    uint32_t lo, unsigned long long* cb, uint32_t* rank,
+                                                    const uint32_t* __restrict__ in_beg, uint32_t* idx) {
     __shared__ uint32_t spre[4][65];
     __shared__ uint64_t sbase[4][64];
     const uint32_t w = threadIdx.x >> 6, l = threadIdx.x & 63;
@@ -197,40 +201,37 @@ __global__ void __launch_bounds__(256) k_route_runs(const uint32_t* __restrict__
         }
         const uint64_t g = sbase[w][a] + (t - pre[a]);
         const uint32_t key = okey[g], d = (key & KEY_DST_MASK) - lo;
-        if (SCATTER) {
-            idx[in_beg[d] + atomicAdd(&fill[d], 1u)] = (uint32_t)g;
-        } else {
-            atomicAdd(&cnt[d], 1u);
-            if (key >> KEY_DST_BITS) atomicAdd(&bsum[d], key >> KEY_DST_BITS);
-        }
+        if (SCATTER)
+            idx[in_beg[d] + rank[g]] = (uint32_t)g;
+        else
+            rank[g] = (uint32_t)atomicAdd(&cb[d], 1ull | ((unsigned long long)(key >> KEY_DST_BITS) << 32));
     }
 }
 
 // G > 1, receive side: thread per record of the receive buffer
 __global__ void k_count_dense(const Msg* __restrict__ rec, uint32_t m, uint32_t lo, uint32_t pl,
-                              uint32_t* cnt, uint32_t* bsum) {
+                              unsigned long long* cb, uint32_t* rank) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= m) return;
     const uint32_t d = rec[i].dst - lo, cls = pl ? 0u : max_emit(rec[i].tt & 0xFF);
-    atomicAdd(&cnt[d], 1u);
-    if (cls) atomicAdd(&bsum[d], cls);
+    rank[i] = (uint32_t)atomicAdd(&cb[d], 1ull | ((unsigned long long)cls << 32));
 }
 
 __global__ void k_scatter_dense(const Msg* __restrict__ rec, uint32_t m, uint32_t lo,
-                                const uint32_t* __restrict__ in_beg, uint32_t* fill, uint32_t* idx) {
+                                const uint32_t* __restrict__ in_beg, const uint32_t* __restrict__ rank,
+                                uint32_t* idx) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= m) return;
-    const uint32_t d = rec[i].dst - lo;
-    idx[in_beg[d] + atomicAdd(&fill[d], 1u)] = i;
+    idx[in_beg[rec[i].dst - lo] + rank[i]] = i;
 }
 
 // short runs in registers (odd-even transposition network); longer ones are
 // listed for k_run_sort_long (n_long: its device-side count)
-__global__ void k_run_sort(const uint32_t* __restrict__ in_beg, const uint32_t* __restrict__ cnt,
+__global__ void k_run_sort(const uint32_t* __restrict__ in_beg, const unsigned long long* __restrict__ cb,
                            uint32_t n, uint32_t* idx, uint32_t* long_list, uint32_t* n_long) {
     uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
     if (d >= n) return;
-    const uint32_t k = cnt[d];
+    const uint32_t k = (uint32_t)cb[d];
     if (k < 2) return;
     if (k > RUN_SHORT) { long_list[atomicAdd(n_long, 1u)] = d; return; }
     uint32_t* p = idx + in_beg[d];
@@ -277,13 +278,13 @@ __device__ void block_sort_lds(uint32_t* sv, uint32_t* p, uint32_t k) {
 // contact) is sorted in RUN_LDS chunks, then merged pairwise through tmp
 // (the run's own range of it) -- slow, and only for such rounds
 __global__ void __launch_bounds__(256) k_run_sort_long(const uint32_t* __restrict__ in_beg,
-                                                       const uint32_t* __restrict__ cnt, uint32_t* idx,
+                                                       const unsigned long long* __restrict__ cb, uint32_t* idx,
                                                        uint32_t* tmp, const uint32_t* __restrict__ long_list,
                                                        const uint32_t* n_long) {
     __shared__ uint32_t sv[RUN_LDS];
     const uint32_t nl = *n_long;
     for (uint32_t q = blockIdx.x; q < nl; q += gridDim.x) {
-        const uint32_t d = long_list[q], k = cnt[d];
+        const uint32_t d = long_list[q], k = (uint32_t)cb[d];
         uint32_t* p = idx + in_beg[d];
         for (uint32_t c0 = 0; c0 < k; c0 += RUN_LDS) block_sort_lds(sv, p + c0, min(RUN_LDS, k - c0));
         uint32_t* x = p;
@@ -305,13 +306,16 @@ __global__ void __launch_bounds__(256) k_run_sort_long(const uint32_t* __restric
     }
 }
 
-// cnt[0..n], bsum, fill, and the long-run count
-__global__ void k_route_clear(uint32_t* cnt, uint32_t* bsum, uint32_t* fill, uint32_t n, uint32_t* n_long) {
+// cb[0..n] and the long-run count
+__global__ void k_route_clear(unsigned long long* cb, uint32_t n, uint32_t* n_long) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i <= n) cnt[i] = 0;
-    if (i < n) { bsum[i] = 0; fill[i] = 0; }
+    if (i <= n) cb[i] = 0;
     if (i == 0) *n_long = 0;
 }
+
+struct Lo32 {
+    __host__ __device__ uint32_t operator()(unsigned long long v) const { return (uint32_t)v; }
+};
 
 __device__ __forceinline__ bool due(uint32_t period, uint32_t r, uint32_t start) {
     return period > 0 && r > start && ((r - start) % period) == 0;
@@ -321,8 +325,7 @@ __device__ __forceinline__ bool due(uint32_t period, uint32_t r, uint32_t start)
 // outbox region) and whether it has any work (inbox, join, timers, EXIT
 // scan, origin, outstanding lazy pushes).  Also counts live nodes and
 // messages addressed to dead ones.
-__global__ void k_node_prep(RoundArgs a, const uint32_t* bsum, uint64_t* bound, uint32_t* work,
-                            uint64_t* part, uint32_t* ocnt) {
+__global__ void k_node_prep(RoundArgs a, uint64_t* bound, uint32_t* work, uint64_t* part, uint32_t* ocnt) {
     __shared__ uint64_t s_up, s_drop;
     if (threadIdx.x == 0) { s_up = 0; s_drop = 0; }
     if (blockIdx.x == 0 && threadIdx.x == 0) { a.ktime[0] = ~0ull; a.ktime[1] = 0; }
@@ -333,7 +336,8 @@ __global__ void k_node_prep(RoundArgs a, const uint32_t* bsum, uint64_t* bound, 
         uint8_t f = a.flags[id];
         uint64_t b = 0;
         uint32_t w = 0;
-        uint32_t c = a.in_cnt[i];
+        const unsigned long long cbi = a.in_cb[i];       // inbox count | bound sum << 32
+        uint32_t c = (uint32_t)cbi;
         if (f & F_UP) {
             uint32_t st = a.start[i], r = a.round;
             if (a.pl) {            // emission bounds of the pluggable round (R0-P)
@@ -348,7 +352,7 @@ __global__ void k_node_prep(RoundArgs a, const uint32_t* bsum, uint64_t* bound, 
                 w = c > 0 || (pending && !x.have) || per;
             } else {
             bool origin = a.origin_now && id == a.origin_node;
-            b = bsum[i] + BOUND_BASE;
+            b = (cbi >> 32) + BOUND_BASE;
             if (f & F_LAZY) b += BOUND_LAZY;
             if (a.crash_round) b += BOUND_EXITS;
             if (origin) b += BOUND_ORIGIN;
@@ -374,7 +378,7 @@ __global__ void k_node_prep(RoundArgs a, const uint32_t* bsum, uint64_t* bound, 
 // work descriptors of the active list: every address k_consume needs first,
 // and which of the node's timers are due (hv:542-607, pt:341-345)
 __global__ void k_desc(const uint32_t* __restrict__ alist, const uint32_t* __restrict__ nact,
-                       const uint32_t* __restrict__ in_beg, const uint32_t* __restrict__ cnt,
+                       const uint32_t* __restrict__ in_beg, const unsigned long long* __restrict__ cb,
                        const uint64_t* __restrict__ obase, const uint32_t* __restrict__ start,
                        RoundArgs a, uint4* __restrict__ desc) {
     const uint32_t na = *nact;
@@ -384,7 +388,7 @@ __global__ void k_desc(const uint32_t* __restrict__ alist, const uint32_t* __res
         uint32_t tf = (a.random_promotion && due(a.promotion_period, r, st) ? DESC_PROMO : 0u) |
                       (due(a.shuffle_period, r, st) ? DESC_SHUFFLE : 0u) |
                       (a.plumtree && due(a.lazy_tick_period, r, st) ? DESC_LAZY : 0u);
-        desc[k] = make_uint4(n, in_beg[li], cnt[li] | (tf << 28), (uint32_t)obase[li]);
+        desc[k] = make_uint4(n, in_beg[li], (uint32_t)cb[li] | (tf << 28), (uint32_t)obase[li]);
     }
 }
 
@@ -517,8 +521,9 @@ struct Shard {
     DBuf<Msg> inbox[2];                 // records by node run, in inbox order: inbox[in_cur] is
     int in_cur = 0;                     // read by this round's consume, the other one is routed into
     // per-round scratch
-    DBuf<uint32_t> okey, ocnt, dpos, keys, vals, owner, owner_s, vals_s, cnt, bsum, in_beg, work,
-        alist, d_nact, fill, long_list, n_long, tmp;
+    DBuf<uint32_t> okey, ocnt, dpos, keys, vals, owner, owner_s, vals_s, in_beg, work,
+        alist, d_nact, rank, long_list, n_long, tmp;
+    DBuf<unsigned long long> cb;        // per local node: inbox count | bound sum << 32 (n + 1)
     DBuf<uint4> desc;
     DBuf<uint64_t> bound, obase, stat_part, stat_out, d_off;
     DBuf<uint8_t> cub_tmp;
@@ -712,12 +717,11 @@ int phase_events_prepare(psim_handle* h, Shard* s, const RoundCtl& ctl, RoundArg
     }
     {
         KTimer t(h, s, KT_PREPARE);
-        a.in_cnt = s->cnt.p;
+        a.in_cb = s->cb.p;
         s->pgrid = grid_for(n);
         s->cgrid = std::min<uint32_t>(grid_for(n), h->consume_blocks);
         TRY(s->stat_part.ensure((size_t)(s->pgrid + s->cgrid) * NST));
-        k_node_prep<<<s->pgrid, BLK, 0, s->stream>>>(a, s->bsum.p, s->bound.p, s->work.p, s->stat_part.p,
-                                                     s->ocnt.p);
+        k_node_prep<<<s->pgrid, BLK, 0, s->stream>>>(a, s->bound.p, s->work.p, s->stat_part.p, s->ocnt.p);
         {
             size_t tb = 0;
             hipcub::CountingInputIterator<uint32_t> ids(s->lo);
@@ -739,10 +743,11 @@ int phase_events_prepare(psim_handle* h, Shard* s, const RoundCtl& ctl, RoundArg
         if (h->G == 1) {            // the route runs without a host sync: sized by the bound
             TRY(s->ivals.ensure(total + 1));
             TRY(s->tmp.ensure(total + 1));
+            TRY(s->rank.ensure(total + 1));
             TRY(s->inbox[s->in_cur ^ 1].ensure(total + 1));
         }
         k_desc<<<std::min<uint32_t>(grid_for(n), 4096), BLK, 0, s->stream>>>(
-            s->alist.p, s->d_nact.p, s->in_beg.p, s->cnt.p, s->obase.p, s->start.p, a, s->desc.p);
+            s->alist.p, s->d_nact.p, s->in_beg.p, s->cb.p, s->obase.p, s->start.p, a, s->desc.p);
     }
     a.in_beg = s->in_beg.p;
     a.desc = s->desc.p; a.n_alist = s->d_nact.p;
@@ -806,25 +811,30 @@ int phase_compact(psim_handle* h, Shard* s) {
 int route_count(psim_handle* h, Shard* s, const Msg* dense, uint32_t m) {
     const uint32_t n = s->n;
     KTimer t(h, s, KT_SCAN);
-    k_route_clear<<<grid_for(n + 1), BLK, 0, s->stream>>>(s->cnt.p, s->bsum.p, s->fill.p, n, s->n_long.p);
+    k_route_clear<<<grid_for(n + 1), BLK, 0, s->stream>>>(s->cb.p, n, s->n_long.p);
     if (!dense)
         k_route_runs<false><<<grid_for(n), BLK, 0, s->stream>>>(s->okey.p, s->obase.p, s->ocnt.p, n, s->lo,
-                                                                s->cnt.p, s->bsum.p, nullptr, nullptr,
-                                                                nullptr);
+                                                                s->cb.p, s->rank.p, nullptr, nullptr);
     else if (m)
         k_count_dense<<<grid_for(m), BLK, 0, s->stream>>>(dense, m, s->lo,
                                                           h->cfg.manager == PSIM_MANAGER_PLUGGABLE,
-                                                          s->cnt.p, s->bsum.p);
-    TRY(scan_excl(s, s->cnt.p, s->in_beg.p, n + 1));
+                                                          s->cb.p, s->rank.p);
+    {
+        hipcub::TransformInputIterator<uint32_t, Lo32, const unsigned long long*> cnt(s->cb.p, Lo32());
+        size_t tb = 0;
+        HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, cnt, s->in_beg.p, n + 1, s->stream));
+        TRY(s->cub_tmp.ensure(tb));
+        HIP_TRY(hipcub::DeviceScan::ExclusiveSum(s->cub_tmp.p, tb, cnt, s->in_beg.p, n + 1, s->stream));
+    }
     return PSIM_OK;
 }
 
 // sort every run of ivals (after a scatter)
 int route_sort_runs(Shard* s) {
-    k_run_sort<<<grid_for(s->n), BLK, 0, s->stream>>>(s->in_beg.p, s->cnt.p, s->n, s->ivals.p,
+    k_run_sort<<<grid_for(s->n), BLK, 0, s->stream>>>(s->in_beg.p, s->cb.p, s->n, s->ivals.p,
                                                       s->long_list.p, s->n_long.p);
     k_run_sort_long<<<std::min<uint32_t>(s->n, 512), 256, 0, s->stream>>>(
-        s->in_beg.p, s->cnt.p, s->ivals.p, s->tmp.p, s->long_list.p, s->n_long.p);
+        s->in_beg.p, s->cb.p, s->ivals.p, s->tmp.p, s->long_list.p, s->n_long.p);
     return PSIM_OK;
 }
 
@@ -834,8 +844,8 @@ int phase_route_local(psim_handle* h, Shard* s) {
     {
         KTimer t(h, s, KT_SORT);
         k_route_runs<true><<<grid_for(s->n), BLK, 0, s->stream>>>(s->okey.p, s->obase.p, s->ocnt.p, s->n,
-                                                                  s->lo, nullptr, nullptr, s->in_beg.p,
-                                                                  s->fill.p, s->ivals.p);
+                                                                  s->lo, nullptr, s->rank.p, s->in_beg.p,
+                                                                  s->ivals.p);
         TRY(route_sort_runs(s));
     }
     // (m_in: read back with the round's stats; ivals, tmp and the inbox were
@@ -873,13 +883,14 @@ int phase_partition(psim_handle* h, Shard* s) {
 int phase_receive(psim_handle* h, Shard* s, uint32_t m) {
     TRY(s->ivals.ensure(m + 1));
     TRY(s->tmp.ensure(m + 1));
+    TRY(s->rank.ensure(m + 1));
     TRY(s->inbox[s->in_cur ^ 1].ensure(m + 1));
     TRY(route_count(h, s, s->recvbuf.p, m));
     {
         KTimer t(h, s, KT_SORT);
         if (m)
             k_scatter_dense<<<grid_for(m), BLK, 0, s->stream>>>(s->recvbuf.p, m, s->lo, s->in_beg.p,
-                                                               s->fill.p, s->ivals.p);
+                                                               s->rank.p, s->ivals.p);
         TRY(route_sort_runs(s));
     }
     s->m_in = m;
@@ -1044,9 +1055,9 @@ int shard_alloc(psim_handle* h, Shard* s) {
     rc |= s->pt_all.alloc(n * PSIM_PT_MEMBERS_CAP); rc |= s->pt_com.alloc(n * PSIM_PT_MEMBERS_CAP);
     rc |= s->pt_eag.alloc(n * PSIM_PT_SET_CAP); rc |= s->pt_laz.alloc(n * PSIM_PT_SET_CAP);
     rc |= s->pt_out.alloc(n * PSIM_PT_OUT_CAP); rc |= s->start.alloc(n);
-    rc |= s->ocnt.alloc(n); rc |= s->dpos.alloc(n); rc |= s->cnt.alloc(n + 1); rc |= s->bsum.alloc(n);
+    rc |= s->ocnt.alloc(n); rc |= s->dpos.alloc(n); rc |= s->cb.alloc(n + 1);
     rc |= s->in_beg.alloc(n + 1); rc |= s->bound.alloc(n + 1); rc |= s->obase.alloc(n + 1);
-    rc |= s->fill.alloc(n); rc |= s->long_list.alloc(n); rc |= s->n_long.alloc(1);
+    rc |= s->long_list.alloc(n); rc |= s->n_long.alloc(1);
     rc |= s->work.alloc(n); rc |= s->alist.alloc(n); rc |= s->desc.alloc(n); rc |= s->d_nact.alloc(1);
     rc |= s->stat_out.alloc(NST + 2);   // + the consume span
     rc |= s->ikeys.alloc(1024); rc |= s->ivals.alloc(1024);
@@ -1081,8 +1092,8 @@ void shard_free(Shard* s) {
     s->pin = nullptr;
     s->outbox.release(); s->okey.release(); s->ocnt.release(); s->dpos.release();
     s->keys.release(); s->vals.release(); s->owner.release(); s->owner_s.release();
-    s->vals_s.release(); s->cnt.release(); s->bsum.release(); s->in_beg.release();
-    s->fill.release(); s->long_list.release(); s->n_long.release(); s->tmp.release();
+    s->vals_s.release(); s->cb.release(); s->in_beg.release();
+    s->rank.release(); s->long_list.release(); s->n_long.release(); s->tmp.release();
     s->work.release(); s->alist.release(); s->desc.release(); s->d_nact.release(); s->bound.release();
     s->obase.release(); s->stat_part.release(); s->stat_out.release(); s->d_off.release();
     s->cub_tmp.release(); s->ev_ids.release(); s->ev_contacts.release(); s->sendbuf.release();

@@ -23,7 +23,7 @@ struct RoundArgs {
     uint64_t* pt_out;
     // inbox (this round) and outbox (next round)
     const uint32_t* in_beg;
-    const uint32_t* in_cnt;
+    const unsigned long long* in_cb;   // inbox count | emission-bound sum << 32
     const uint32_t* start;      // start round per node (timer phases)
     const uint4* desc;          // per node with work: (id, inbox begin, inbox count, outbox base)
     const uint32_t* n_alist;
