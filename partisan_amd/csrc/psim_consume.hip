@@ -147,13 +147,15 @@ DEV uint64_t draw(Wv& w) {
     return ((uint64_t)rl(w.DCH, i) << 32) | rl(w.DCL, i);
 }
 
-// rand:uniform/1 with a 58-bit generator (OTP rand.erl ?uniform_range)
+// rand:uniform/1 with a 58-bit generator (OTP rand.erl ?uniform_range);
+// here n <= 64 always (a count of lanes), so only the exact small modulo
+// is compiled in
 DEV uint32_t uniform_n(Wv& w, uint32_t n) {
     const uint64_t two58 = 1ull << 58;
     for (;;) {
         uint64_t v = draw(w);
         if (v < n) return (uint32_t)v + 1;
-        uint64_t i = n <= 64 ? mod_small(v, n) : mod58(v, n);
+        uint64_t i = mod_small(v, n);
         if (v - i <= two58 - n) return (uint32_t)i + 1;
     }
 }
@@ -669,11 +671,15 @@ DEV void hv_handle(Wv& w, uint32_t type, uint32_t p, uint32_t ttl, uint32_t a0, 
         if (ttl > 0 && w.act_n > 1) {
             uint32_t r = select_random(w, w.A, w.act_n, p, me, me);
             if (r != NONE) hv_send(w, r, PSIM_MSG_SHUFFLE, ttl - 1, 0, 0, EX, nex);
+            STAMP(w, 25);
         } else {
             uint32_t RESP = 0;
             uint32_t nr = sublist(w, w.P, w.pas_n, nex, RESP, 0);
+            STAMP(w, 26);
             hv_send(w, p, PSIM_MSG_SHUFFLE_REPLY, 0, 0, 0, RESP, nr);
+            STAMP(w, 27);
             merge_exchange(w, EX, nex);
+            STAMP(w, 28);
         }
         break;
     default:

@@ -15,7 +15,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 NAMES = {0: "idle-node", 1: "setup+loads", 2: "join+exits", 3: "inbox-chunk/misc",
          13: "promotion", 14: "shuffle", 15: "notify-replay", 21: "origin",
-         22: "lazy-tick", 23: "writeback", 24: "loop"}
+         22: "lazy-tick", 23: "writeback", 24: "loop", 25: "shuffle:forward",
+         26: "shuffle:accept-sublist", 27: "shuffle:accept-reply", 28: "shuffle:accept-merge"}
 HV = ["JOIN", "FWD_JOIN", "NEIGHBOR", "DISCONNECT", "NEIGHBOR_REQ", "NEIGHBOR_ACC",
       "NEIGHBOR_REJ", "SHUFFLE", "SHUFFLE_REPLY"]
 PT = ["BROADCAST", "PRUNE", "IHAVE", "IGNORED_IHAVE", "GRAFT"]
@@ -55,7 +56,9 @@ def main():
     tot = v.sum()
     print(f"rounds {a.steps}  processed {int(st['nodes_processed'].sum())}  "
           f"delivered {int(st['delivered'].sum())}  emitted {int(st['emitted'].sum())}")
-    print(f"total wave-ticks {tot:.4g} (s_memtime, 100 MHz)")
+    print(f"total wave-ticks {tot:.4g} (s_memtime: shader clock)")
+    dl = st["delivered"].sum(axis=0) / a.steps
+    print("delivered/round: " + ", ".join(f"{n}={int(dl[i])}" for i, n in enumerate(HV + PT) if dl[i]))
     for k in np.argsort(-v):
         if v[k] == 0:
             continue
