@@ -213,6 +213,7 @@ DEV uint32_t sublist(Wv& w, uint32_t V, uint32_t n, uint32_t k, uint32_t& OUT, u
 
 // ------------------------------------------------------------- emission --
 DEV void flush_recs(Wv& w);
+DEV void flush_full(Wv& w);
 
 DEV void emit(Wv& w, uint32_t dst, uint32_t type, uint32_t ttl, uint32_t a0, uint32_t a1,
               uint32_t a2, uint32_t EX, uint32_t nex) {
@@ -230,7 +231,7 @@ DEV void emit(Wv& w, uint32_t dst, uint32_t type, uint32_t ttl, uint32_t a0, uin
     }
     if (l == 0) w.skey[k] = dst | (max_emit(type) << KEY_DST_BITS);
     st_add(w, ST_EMIT + type, 1);
-    if (k + 1 == STAGE) flush_recs(w);               // a node with > STAGE emissions
+    if (k + 1 == STAGE) flush_full(w);               // a node with > STAGE emissions
 }
 
 // The staged records [flushed, seq) to outbox slots obase + flushed..: one
@@ -256,6 +257,22 @@ DEV void flush_recs(Wv& w) {
     const uint32_t key = w.skey[jk];
     reinterpret_cast<uint4*>(w.a->rec_out + w.obase + g)[l & 3] = piece;
     w.a->okey[w.obase + gk] = key;
+    __builtin_amdgcn_wave_barrier();
+    w.flushed = w.seq;
+}
+
+// A full staging buffer from inside emit: lane l stores piece l of the 16
+// records (record l >> 2, 16-B piece l & 3 -- i.e. uint4 l of the run) and
+// lanes 0-15 their route keys.  Kept apart from flush_recs so the emit
+// sites carry only these few temporaries (uniform bases, one index).
+DEV void flush_full(Wv& w) {
+    const uint32_t l = lane_id();
+    __builtin_amdgcn_wave_barrier();
+    const uint64_t r0 = w.obase + w.flushed;
+    uint4* rb = reinterpret_cast<uint4*>(w.a->rec_out + r0);
+    uint32_t* kb = w.a->okey + r0;
+    rb[l] = reinterpret_cast<const uint4*>(w.srec)[l];
+    kb[l & (STAGE - 1)] = w.skey[l & (STAGE - 1)];
     __builtin_amdgcn_wave_barrier();
     w.flushed = w.seq;
 }
