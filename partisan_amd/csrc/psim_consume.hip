@@ -81,6 +81,7 @@ struct Wv {
     uint32_t* skey;      // their route keys
     uint32_t flushed;    // records already written for this node
     uint32_t fl, A0, P0; // flag byte and views at node start (writeback)
+    uint32_t KM;         // magic_lanes(): the exact-modulo multipliers
     bool work;           // the node had work this round
 };
 constexpr uint64_t NONE64 = ~0ull;
@@ -155,7 +156,7 @@ DEV uint32_t uniform_n(Wv& w, uint32_t n) {
     for (;;) {
         uint64_t v = draw(w);
         if (v < n) return (uint32_t)v + 1;
-        uint64_t i = mod_small(v, n);
+        uint64_t i = mod_small_m(v, n, rl(w.KM, n & 63));
         if (v - i <= two58 - n) return (uint32_t)i + 1;
     }
 }
@@ -1012,6 +1013,7 @@ __global__ void __launch_bounds__(256, PSIM_WAVES_PER_SIMD) k_consume(RoundArgs 
     w.round = args.round;
     w.SC = 0;
     w.digest = 0;
+    w.KM = magic_lanes();
     const uint32_t na = *args.n_alist;
     if (gw < na) {
         // Pipeline over this wave's nodes i, i + nw, ...: while node i is

@@ -107,15 +107,21 @@ __constant__ const uint32_t kMagic[65] = {
 // v mod n for a 58-bit v and 1 <= n <= 64: Horner over an 18-bit and two
 // 20-bit digits, each step x = r * 2^20 + d < 2^26 divided by one mul_hi;
 // all operands are wave-uniform, so this runs on the SALU
-DEV uint32_t mod_small(uint64_t v, uint32_t n) {
+DEV uint32_t mod_small_m(uint64_t v, uint32_t n, uint32_t M) {
     if (n == 1) return 0;
-    const uint32_t M = kMagic[n];
     uint32_t x = (uint32_t)(v >> 40);
     uint32_t r = x - __umulhi(x, M) * n;
     x = (r << 20) | (uint32_t)((v >> 20) & 0xFFFFFu);
     r = x - __umulhi(x, M) * n;
     x = (r << 20) | (uint32_t)(v & 0xFFFFFu);
     return x - __umulhi(x, M) * n;
+}
+DEV uint32_t mod_small(uint64_t v, uint32_t n) { return mod_small_m(v, n, kMagic[n]); }
+// the table in a register: lane l holds kMagic[l] (lane 0: kMagic[64]), so
+// a lookup is one v_readlane instead of a scalar load and its wait
+DEV uint32_t magic_lanes() {
+    const uint32_t l = lane_id();
+    return kMagic[l == 0 ? 64 : l];
 }
 
 }  // namespace psim
