@@ -21,6 +21,26 @@ S_NODE = 416                    # algorithmic state bytes per processed node (SU
 S_MSG = 64                      # message record bytes
 
 
+def pmc_traffic(workload):
+    """HBM bytes per k_consume launch from the committed PMC passes of this
+    same bench command (profiles/run_pmc.sh -> profiles/pmc_latest.txt):
+    FETCH_SIZE doubled (gfx950 tallies 128-B read requests at 64 B,
+    MI355X_MICROARCH.md HBM section) plus WRITE_SIZE, both in KiB per
+    dispatch.  Config C only; None when the file is absent."""
+    if workload != "C":
+        return None
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "pmc_latest.txt")
+    try:
+        vals = {}
+        for line in open(path):
+            f = line.split()
+            if len(f) >= 5 and f[0] in ("FETCH_SIZE", "WRITE_SIZE") and f[3] == "per-dispatch":
+                vals[f[0]] = float(f[4])
+        return (2 * vals["FETCH_SIZE"] + vals["WRITE_SIZE"]) * 1024.0
+    except (OSError, KeyError, ValueError):
+        return None
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -114,7 +134,7 @@ def main_strategy(args):
         "vs_baseline": None, "dtype": "u32", "data": "synthetic",
         "config": {"workload": name, "nodes": n, "seed": args.seed, "parallelism": "1 GPU"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": "k_consume_pl",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(args.workload), "kernel": "k_consume_pl",
                      "alg_bytes_per_launch": alg / max(1, c_n), "avg_launch_ms": c_ms / max(1, c_n)},
         "kernel_ms_per_step": {k: v[0] / args.steps for k, v in kt.items() if v[1]},
         "overflow": int(st["overflow"].sum()),
@@ -182,6 +202,8 @@ def main():
         sim.step(1)
     if world > 1:
         dist.barrier()
+    if os.environ.get("PSIM_TRACE_GROW"):
+        print("bench: timed rounds start", file=sys.stderr, flush=True)
     t0 = time.perf_counter()
     stats = []
     kt = {}
@@ -235,7 +257,7 @@ def main():
                    "nodes": n, "nodes_per_gpu": args.nodes, "seed": args.seed,
                    "parallelism": f"node-range sharded x{world}, RCCL all-to-all" if world > 1 else "1 GPU"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(args.workload),
                      "kernel": "k_consume", "alg_bytes_per_launch": per_launch_bytes,
                      "avg_launch_ms": per_launch_s * 1e3},
         "kernel_ms_per_step": {k: v[0] / args.steps for k, v in kt.items() if v[1]},

@@ -46,6 +46,8 @@ constexpr uint32_t KEY_DST_BITS = 27;
 constexpr uint32_t KEY_DST_MASK = (1u << KEY_DST_BITS) - 1;
 
 // outbox bound: per inbox message (by type) and per node
+constexpr uint32_t KEY_BCAST = 31;
+constexpr uint32_t BCAST_FIRST = PSIM_PT_SET_CAP;         // eager push of a first delivery
 __host__ __device__ constexpr uint32_t max_emit(uint32_t type) {
     // JOIN: DISCONNECT + NEIGHBOR + FORWARD_JOIN to up to ACTIVE_CAP-2 peers
     return type == PSIM_MSG_JOIN ? 2 + (PSIM_ACTIVE_CAP - 2)
@@ -55,9 +57,10 @@ __host__ __device__ constexpr uint32_t max_emit(uint32_t type) {
          : type == PSIM_MSG_NEIGHBOR_REQUEST ? 2
          : type == PSIM_MSG_NEIGHBOR_ACCEPTED ? 1
          : type == PSIM_MSG_SHUFFLE ? 1
-         // eager push to eager-{From} (<= SET_CAP-1) plus IHAVEs, in this
-         // round's lazy tick, for outstanding entries added for lazy-{From}
-         : type == PSIM_MSG_PT_BROADCAST ? 2 * PSIM_PT_SET_CAP - 1
+         // a marker, not a count: the route counts a BROADCAST as 1 (the
+         // PRUNE of a duplicate) and adds BCAST_FIRST once per distinct
+         // message id (msg & 31, the `have` bit) the destination receives
+         : type == PSIM_MSG_PT_BROADCAST ? KEY_BCAST
          : type == PSIM_MSG_PT_IHAVE ? 1
          : type == PSIM_MSG_PT_GRAFT ? 1
          : 0;
@@ -65,7 +68,7 @@ __host__ __device__ constexpr uint32_t max_emit(uint32_t type) {
 constexpr uint32_t BOUND_BASE = 3;                        // JOIN send, promotion, shuffle
 constexpr uint32_t BOUND_EXITS = PSIM_ACTIVE_CAP - 1;     // EXIT-driven NEIGHBOR_REQUESTs
 constexpr uint32_t BOUND_LAZY = PSIM_PT_OUT_CAP;          // IHAVEs of entries already outstanding
-static_assert(2 * PSIM_PT_SET_CAP - 1 < 32, "max_emit must fit the 5-bit key field");
+static_assert(PSIM_ACTIVE_CAP < KEY_BCAST, "max_emit must fit the 5-bit key field below the marker");
 constexpr uint32_t BOUND_ORIGIN = 2 * PSIM_PT_SET_CAP;    // eager push + lazy adds of the root
 
 // work descriptor (id, inbox begin, inbox count | due timers << 28, outbox

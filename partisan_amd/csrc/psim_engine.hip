@@ -171,12 +171,24 @@ constexpr uint32_t RUN_LDS = 2048;
 //            (low word) and its emission bound to the bound sum (high word);
 //            the old count is the record's arrival rank in its run
 //   scatter: the record's slot to in_beg[dst] + rank, no atomics
+// a record's contribution to its destination's bound word; BROADCASTs also
+// set their message id bit in bmask (distinct first deliveries)
+__device__ __forceinline__ unsigned long long route_add(uint32_t cls, const Msg* rec, uint32_t d,
+                                                         uint32_t* bmask) {
+    if (cls == KEY_BCAST) {
+        atomicOr(&bmask[d], 1u << (rec->a0 & 31u));
+        cls = 1;
+    }
+    return 1ull | ((unsigned long long)cls << 32);
+}
+
 template <bool SCATTER>
-__global__ void __launch_bounds__(256) k_route_runs(const uint32_t* __restrict__ okey,
+__global__ void __launch_bounds__(256) k_route_runs(const Msg* __restrict__ rec, const uint32_t* __restrict__ okey,
                                                     const uint64_t* __restrict__ obase,
                                                     const uint32_t* __restrict__ ocnt, uint32_t n,
-                                                    uint32_t lo, unsigned long long* cb, uint32_t* rank,
-                                                    const uint32_t* __restrict__ in_beg, uint32_t* idx) {
+                                                    uint32_t lo, unsigned long long* cb, uint32_t* bmask,
+                                                    uint32_t* rank, const uint32_t* __restrict__ in_beg,
+                                                    uint32_t* idx) {
     __shared__ uint32_t spre[4][65];
     __shared__ uint64_t sbase[4][64];
     const uint32_t w = threadIdx.x >> 6, l = threadIdx.x & 63;
@@ -204,17 +216,17 @@ __global__ void __launch_bounds__(256) k_route_runs(const uint32_t* __restrict__
         if (SCATTER)
             idx[in_beg[d] + rank[g]] = (uint32_t)g;
         else
-            rank[g] = (uint32_t)atomicAdd(&cb[d], 1ull | ((unsigned long long)(key >> KEY_DST_BITS) << 32));
+            rank[g] = (uint32_t)atomicAdd(&cb[d], route_add(key >> KEY_DST_BITS, rec + g, d, bmask));
     }
 }
 
 // G > 1, receive side: thread per record of the receive buffer
 __global__ void k_count_dense(const Msg* __restrict__ rec, uint32_t m, uint32_t lo, uint32_t pl,
-                              unsigned long long* cb, uint32_t* rank) {
+                              unsigned long long* cb, uint32_t* bmask, uint32_t* rank) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= m) return;
     const uint32_t d = rec[i].dst - lo, cls = pl ? 0u : max_emit(rec[i].tt & 0xFF);
-    rank[i] = (uint32_t)atomicAdd(&cb[d], 1ull | ((unsigned long long)cls << 32));
+    rank[i] = (uint32_t)atomicAdd(&cb[d], route_add(cls, rec + i, d, bmask));
 }
 
 __global__ void k_scatter_dense(const Msg* __restrict__ rec, uint32_t m, uint32_t lo,
@@ -306,10 +318,11 @@ __global__ void __launch_bounds__(256) k_run_sort_long(const uint32_t* __restric
     }
 }
 
-// cb[0..n] and the long-run count
-__global__ void k_route_clear(unsigned long long* cb, uint32_t n, uint32_t* n_long) {
+// cb[0..n], bmask and the long-run count
+__global__ void k_route_clear(unsigned long long* cb, uint32_t* bmask, uint32_t n, uint32_t* n_long) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i <= n) cb[i] = 0;
+    if (i < n) bmask[i] = 0;
     if (i == 0) *n_long = 0;
 }
 
@@ -325,7 +338,8 @@ __device__ __forceinline__ bool due(uint32_t period, uint32_t r, uint32_t start)
 // outbox region) and whether it has any work (inbox, join, timers, EXIT
 // scan, origin, outstanding lazy pushes).  Also counts live nodes and
 // messages addressed to dead ones.
-__global__ void k_node_prep(RoundArgs a, uint64_t* bound, uint32_t* work, uint64_t* part, uint32_t* ocnt) {
+__global__ void k_node_prep(RoundArgs a, const uint32_t* bmask, uint64_t* bound, uint32_t* work, uint64_t* part,
+                            uint32_t* ocnt) {
     __shared__ uint64_t s_up, s_drop;
     if (threadIdx.x == 0) { s_up = 0; s_drop = 0; }
     if (blockIdx.x == 0 && threadIdx.x == 0) { a.ktime[0] = ~0ull; a.ktime[1] = 0; }
@@ -352,8 +366,12 @@ __global__ void k_node_prep(RoundArgs a, uint64_t* bound, uint32_t* work, uint64
                 w = c > 0 || (pending && !x.have) || per;
             } else {
             bool origin = a.origin_now && id == a.origin_node;
-            b = (cbi >> 32) + BOUND_BASE;
-            if (f & F_LAZY) b += BOUND_LAZY;
+            // per message its class bound (a BROADCAST: 1), per distinct
+            // BROADCAST id an eager push, and the lazy tick's IHAVEs if
+            // entries are outstanding or may be added this round
+            const uint32_t bm = c ? bmask[i] : 0u;
+            b = (cbi >> 32) + BOUND_BASE + (uint64_t)__popc(bm) * BCAST_FIRST;
+            if ((f & F_LAZY) || bm) b += BOUND_LAZY;
             if (a.crash_round) b += BOUND_EXITS;
             if (origin) b += BOUND_ORIGIN;
             w = c > 0 || st == r || a.crash_round || (f & F_LAZY) || origin ||
@@ -470,12 +488,16 @@ struct DBuf {
     // grow to the next power of two (per-round sizes peak on broadcast
     // rounds; a 25 % step re-allocated -- 1 ms each -- for many rounds),
     // contents not kept
-    int ensure(size_t want) {
+    // headroom: grow to the power of two at or above want * (1 + headroom / 4)
+    int ensure(size_t want, int headroom = 0) {
         if (want <= n) return PSIM_OK;
+        static const bool trace = getenv("PSIM_TRACE_GROW") != nullptr;
+        if (trace && p) std::fprintf(stderr, "psim: grow %zu -> %zu x %zu B\n", n, want, sizeof(T));
         if (p) (void)hipFree(p);
         p = nullptr; n = 0;
+        const size_t goal = want + want / 4 * (size_t)headroom;
         size_t cap = 1024;
-        while (cap < want) cap <<= 1;
+        while (cap < goal) cap <<= 1;
         if (hipMalloc(&p, cap * sizeof(T)) != hipSuccess) return PSIM_ENOMEM;
         n = cap;
         return PSIM_OK;
@@ -503,6 +525,7 @@ int bits_for(uint64_t n) {
 }
 
 enum { PIN_TOTAL = NST + 2, PIN_M = NST + 3 };
+constexpr uint64_t RESERVE_PER_NODE = 24;   // outbox slots per node reserved up front
 
 struct Shard {
     uint32_t idx = 0, lo = 0, n = 0;    // global shard index, owned [lo, lo + n)
@@ -522,7 +545,7 @@ struct Shard {
     int in_cur = 0;                     // read by this round's consume, the other one is routed into
     // per-round scratch
     DBuf<uint32_t> okey, ocnt, dpos, keys, vals, owner, owner_s, vals_s, in_beg, work,
-        alist, d_nact, rank, long_list, n_long, tmp;
+        alist, d_nact, rank, long_list, n_long, tmp, bmask;
     DBuf<unsigned long long> cb;        // per local node: inbox count | bound sum << 32 (n + 1)
     DBuf<uint4> desc;
     DBuf<uint64_t> bound, obase, stat_part, stat_out, d_off;
@@ -545,6 +568,7 @@ struct Shard {
     int tn = 0;
     hipEvent_t wait_ev = nullptr;
     bool ev_live = false;
+    bool reserved = false;              // first-round capacity reservation done
 };
 
 }  // namespace
@@ -721,7 +745,8 @@ int phase_events_prepare(psim_handle* h, Shard* s, const RoundCtl& ctl, RoundArg
         s->pgrid = grid_for(n);
         s->cgrid = std::min<uint32_t>(grid_for(n), h->consume_blocks);
         TRY(s->stat_part.ensure((size_t)(s->pgrid + s->cgrid) * NST));
-        k_node_prep<<<s->pgrid, BLK, 0, s->stream>>>(a, s->bound.p, s->work.p, s->stat_part.p, s->ocnt.p);
+        k_node_prep<<<s->pgrid, BLK, 0, s->stream>>>(a, s->bmask.p, s->bound.p, s->work.p, s->stat_part.p,
+                                                     s->ocnt.p);
         {
             size_t tb = 0;
             hipcub::CountingInputIterator<uint32_t> ids(s->lo);
@@ -738,13 +763,31 @@ int phase_events_prepare(psim_handle* h, Shard* s, const RoundCtl& ctl, RoundArg
         TRY(stream_wait(s));
         const uint64_t total = s->pin[PIN_TOTAL];
         if (total >= 0xFFFFFFFFull) return PSIM_ENOMEM;
-        TRY(s->outbox.ensure(total + 1));
-        TRY(s->okey.ensure(total + 1));
+        // the bound peaks on broadcast rounds and creeps up for many rounds:
+        // each growth (a free + malloc, ~2 ms at GB sizes) reserves 1.5x;
+        // the first round reserves RESERVE_PER_NODE slots per node instead,
+        // where that takes at most a quarter of the free device memory
+        uint64_t want = total + 1;
+        int headroom = 2;
+        if (!s->reserved) {
+            s->reserved = true;
+            size_t fr = 0, tot = 0;
+            const uint64_t r = (uint64_t)n * RESERVE_PER_NODE;
+            const uint64_t per_slot = 3 * sizeof(Msg) + 4 * sizeof(uint32_t);
+            if (hipMemGetInfo(&fr, &tot) == hipSuccess && r * per_slot <= fr / 4 && r > want) {
+                want = r;
+                headroom = 0;
+            }
+        }
+        TRY(s->outbox.ensure(want, headroom));
+        TRY(s->okey.ensure(want, headroom));
         if (h->G == 1) {            // the route runs without a host sync: sized by the bound
-            TRY(s->ivals.ensure(total + 1));
-            TRY(s->tmp.ensure(total + 1));
-            TRY(s->rank.ensure(total + 1));
-            TRY(s->inbox[s->in_cur ^ 1].ensure(total + 1));
+            TRY(s->ivals.ensure(want, headroom));
+            TRY(s->tmp.ensure(want, headroom));
+            TRY(s->rank.ensure(want, headroom));
+            TRY(s->inbox[s->in_cur ^ 1].ensure(want, headroom));
+            if (s->m_in == 0)       // nothing to read in the current one: grow both
+                TRY(s->inbox[s->in_cur].ensure(want, headroom));
         }
         k_desc<<<std::min<uint32_t>(grid_for(n), 4096), BLK, 0, s->stream>>>(
             s->alist.p, s->d_nact.p, s->in_beg.p, s->cb.p, s->obase.p, s->start.p, a, s->desc.p);
@@ -811,14 +854,15 @@ int phase_compact(psim_handle* h, Shard* s) {
 int route_count(psim_handle* h, Shard* s, const Msg* dense, uint32_t m) {
     const uint32_t n = s->n;
     KTimer t(h, s, KT_SCAN);
-    k_route_clear<<<grid_for(n + 1), BLK, 0, s->stream>>>(s->cb.p, n, s->n_long.p);
+    k_route_clear<<<grid_for(n + 1), BLK, 0, s->stream>>>(s->cb.p, s->bmask.p, n, s->n_long.p);
     if (!dense)
-        k_route_runs<false><<<grid_for(n), BLK, 0, s->stream>>>(s->okey.p, s->obase.p, s->ocnt.p, n, s->lo,
-                                                                s->cb.p, s->rank.p, nullptr, nullptr);
+        k_route_runs<false><<<grid_for(n), BLK, 0, s->stream>>>(s->outbox.p, s->okey.p, s->obase.p, s->ocnt.p,
+                                                                n, s->lo, s->cb.p, s->bmask.p, s->rank.p,
+                                                                nullptr, nullptr);
     else if (m)
         k_count_dense<<<grid_for(m), BLK, 0, s->stream>>>(dense, m, s->lo,
                                                           h->cfg.manager == PSIM_MANAGER_PLUGGABLE,
-                                                          s->cb.p, s->rank.p);
+                                                          s->cb.p, s->bmask.p, s->rank.p);
     {
         hipcub::TransformInputIterator<uint32_t, Lo32, const unsigned long long*> cnt(s->cb.p, Lo32());
         size_t tb = 0;
@@ -843,9 +887,9 @@ int phase_route_local(psim_handle* h, Shard* s) {
     TRY(route_count(h, s, nullptr, 0));
     {
         KTimer t(h, s, KT_SORT);
-        k_route_runs<true><<<grid_for(s->n), BLK, 0, s->stream>>>(s->okey.p, s->obase.p, s->ocnt.p, s->n,
-                                                                  s->lo, nullptr, s->rank.p, s->in_beg.p,
-                                                                  s->ivals.p);
+        k_route_runs<true><<<grid_for(s->n), BLK, 0, s->stream>>>(s->outbox.p, s->okey.p, s->obase.p,
+                                                                  s->ocnt.p, s->n, s->lo, nullptr, nullptr,
+                                                                  s->rank.p, s->in_beg.p, s->ivals.p);
         TRY(route_sort_runs(s));
     }
     // (m_in: read back with the round's stats; ivals, tmp and the inbox were
@@ -1057,7 +1101,7 @@ int shard_alloc(psim_handle* h, Shard* s) {
     rc |= s->pt_out.alloc(n * PSIM_PT_OUT_CAP); rc |= s->start.alloc(n);
     rc |= s->ocnt.alloc(n); rc |= s->dpos.alloc(n); rc |= s->cb.alloc(n + 1);
     rc |= s->in_beg.alloc(n + 1); rc |= s->bound.alloc(n + 1); rc |= s->obase.alloc(n + 1);
-    rc |= s->long_list.alloc(n); rc |= s->n_long.alloc(1);
+    rc |= s->long_list.alloc(n); rc |= s->bmask.alloc(n); rc |= s->n_long.alloc(1);
     rc |= s->work.alloc(n); rc |= s->alist.alloc(n); rc |= s->desc.alloc(n); rc |= s->d_nact.alloc(1);
     rc |= s->stat_out.alloc(NST + 2);   // + the consume span
     rc |= s->ikeys.alloc(1024); rc |= s->ivals.alloc(1024);
@@ -1093,7 +1137,7 @@ void shard_free(Shard* s) {
     s->outbox.release(); s->okey.release(); s->ocnt.release(); s->dpos.release();
     s->keys.release(); s->vals.release(); s->owner.release(); s->owner_s.release();
     s->vals_s.release(); s->cb.release(); s->in_beg.release();
-    s->rank.release(); s->long_list.release(); s->n_long.release(); s->tmp.release();
+    s->rank.release(); s->long_list.release(); s->bmask.release(); s->n_long.release(); s->tmp.release();
     s->work.release(); s->alist.release(); s->desc.release(); s->d_nact.release(); s->bound.release();
     s->obase.release(); s->stat_part.release(); s->stat_out.release(); s->d_off.release();
     s->cub_tmp.release(); s->ev_ids.release(); s->ev_contacts.release(); s->sendbuf.release();
