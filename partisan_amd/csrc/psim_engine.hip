@@ -148,60 +148,72 @@ __global__ void k_bcast_reset(Hdr* hdr, uint32_t n, uint32_t bit) {
 }
 
 // ------------------------------------------------------------- route --
-// The route groups a round's records by local destination, each group in
-// emission order: ascending source index (an outbox slot, or a position in
-// the source-shard-ordered receive buffer), which is (src, seq) order.
-//   count    one atomic per record: run length and emission-bound sum of its
-//            destination (cb: n + 1 entries, cb[n] = 0), and the record's
-//            arrival rank in its run
-//   scan     run starts in_beg[0..n]; in_beg[n] is the record count m
-//   scatter  each record's source index to in_beg[dst] + rank
-//   sort     every run ascending: <= RUN_SHORT by its own thread in
-//            registers, longer ones by one block (bitonic in LDS up to
-//            RUN_LDS, LDS-sorted chunks merged through `tmp` beyond)
-// The order inside a run before the sort depends on atomic timing; the sort
-// by source index makes the inbox deterministic.
+// The route groups a round's records by local destination; each group ends
+// up in emission order -- ascending source index (an outbox slot, or a
+// position in the source-shard-ordered receive buffer), i.e. (src, seq)
+// order.  Destinations are cut into buckets of W = 2^wshift consecutive
+// nodes, and everything per destination happens in one block's LDS:
+//   k_bucket_hist<>    a block takes fixed steps of source records and
+//                      histograms their buckets in LDS -> hist[b * nblk + blk]
+//   scan               over hist: where block blk's records of bucket b go;
+//                      the extra last entry becomes the record count
+//   k_bucket_scatter<> the same steps again: each record's (destination in
+//                      bucket | bound class, source index) pair to its place
+//   k_bucket_route     one block per bucket: per destination the count, the
+//                      bound sum and the BROADCAST id mask (LDS atomics; the
+//                      returned count is the record's rank in its run), the
+//                      run starts (block scan), each source index into its
+//                      run, and every run of <= RUN_SHORT sorted in registers
+//   k_run_sort_long    runs longer than RUN_SHORT, one block each: bitonic
+//                      in LDS up to RUN_LDS, LDS-sorted chunks merged through
+//                      `tmp` beyond
+// Run order before the sort depends on atomic timing; sorting each run by
+// source index makes the inbox deterministic.
 constexpr uint32_t RUN_SHORT = 16;
 constexpr uint32_t RUN_LDS = 2048;
+constexpr uint32_t RB_STEP = 256;          // source nodes (or dense records) per block step
+constexpr uint32_t RB_MAX_BLOCKS = 1024;   // blocks of the two passes over the sources
+constexpr uint32_t RR_THREADS = 512;       // k_bucket_route block
 
-// A wave takes 64 consecutive source nodes and expands their outbox runs
-// (ocnt[i] records at obase[i]) into consecutive record numbers t: lane l
-// handles records l, l + 64, ..., so okey is read in slot order.
-//   count:   one 64-bit atomic per record adds 1 to its destination's count
-//            (low word) and its emission bound to the bound sum (high word);
-//            the old count is the record's arrival rank in its run
-//   scatter: the record's slot to in_beg[dst] + rank, no atomics
-// a record's contribution to its destination's bound word; BROADCASTs also
-// set their message id bit in bmask (distinct first deliveries)
-__device__ __forceinline__ unsigned long long route_add(uint32_t cls, const Msg* rec, uint32_t d,
-                                                         uint32_t* bmask) {
-    if (cls == KEY_BCAST) {
-        atomicOr(&bmask[d], 1u << (rec->a0 & 31u));
-        cls = 1;
-    }
-    return 1ull | ((unsigned long long)cls << 32);
-}
+// the sources of one route: the outbox runs of this shard's nodes (G == 1),
+// or a dense receive buffer (G > 1)
+struct RouteIn {
+    const Msg* rec;
+    const uint32_t* okey;      // runs: route key of every outbox slot
+    const uint64_t* obase;     // runs: each source node's first slot
+    const uint32_t* ocnt;      // runs: and its record count
+    uint32_t n_src;            // runs: source nodes; dense: records
+    uint32_t lo;               // first local node id
+    uint32_t pl;               // dense: pluggable manager (bound class 0)
+};
 
-template <bool SCATTER>
-__global__ void __launch_bounds__(256) k_route_runs(const Msg* __restrict__ rec, const uint32_t* __restrict__ okey,
-                                                    const uint64_t* __restrict__ obase,
-                                                    const uint32_t* __restrict__ ocnt, uint32_t n,
-                                                    uint32_t lo, unsigned long long* cb, uint32_t* bmask,
-                                                    uint32_t* rank, const uint32_t* __restrict__ in_beg,
-                                                    uint32_t* idx) {
-    __shared__ uint32_t spre[4][65];
-    __shared__ uint64_t sbase[4][64];
+// Calls f(g, d, cls) for every record of block step `step`: source index g,
+// local destination d, bound class cls.  The runs form has a wave expand 64
+// consecutive source nodes' runs into consecutive record numbers (lane l
+// takes records l, l + 64, ..., so okey is read in slot order); every thread
+// of the block must call it.
+template <bool DENSE, typename F>
+__device__ __forceinline__ void route_step(const RouteIn& in, uint32_t step, uint32_t (*spre)[65],
+                                           uint64_t (*sbase)[64], F f) {
     const uint32_t w = threadIdx.x >> 6, l = threadIdx.x & 63;
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t c = i < n ? ocnt[i] : 0u;
+    const uint32_t i = step * RB_STEP + threadIdx.x;
+    if (DENSE) {
+        if (i < in.n_src) {
+            const Msg& r = in.rec[i];
+            f(i, r.dst - in.lo, in.pl ? 0u : max_emit(r.tt & 0xFF));
+        }
+        return;
+    }
+    const uint32_t c = i < in.n_src ? in.ocnt[i] : 0u;
     uint32_t inc = c;                                 // inclusive prefix over the wave
     for (int o = 1; o < 64; o <<= 1) {
         const uint32_t y = __shfl_up(inc, o);
         if (l >= (uint32_t)o) inc += y;
     }
+    __syncthreads();                                  // the previous step's readers are done
     spre[w][l + 1] = inc;
     if (l == 0) spre[w][0] = 0;
-    sbase[w][l] = i < n ? obase[i] : 0ull;
+    sbase[w][l] = i < in.n_src ? in.obase[i] : 0ull;
     const uint32_t T = __shfl(inc, 63);
     __syncthreads();
     const uint32_t* pre = spre[w];
@@ -212,56 +224,129 @@ __global__ void __launch_bounds__(256) k_route_runs(const Msg* __restrict__ rec,
             if (pre[mid] <= t) a = mid; else b = mid;
         }
         const uint64_t g = sbase[w][a] + (t - pre[a]);
-        const uint32_t key = okey[g], d = (key & KEY_DST_MASK) - lo;
-        if (SCATTER)
-            idx[in_beg[d] + rank[g]] = (uint32_t)g;
-        else
-            rank[g] = (uint32_t)atomicAdd(&cb[d], route_add(key >> KEY_DST_BITS, rec + g, d, bmask));
+        const uint32_t key = in.okey[g];
+        f((uint32_t)g, (key & KEY_DST_MASK) - in.lo, key >> KEY_DST_BITS);
     }
 }
 
-// G > 1, receive side: thread per record of the receive buffer
-__global__ void k_count_dense(const Msg* __restrict__ rec, uint32_t m, uint32_t lo, uint32_t pl,
-                              unsigned long long* cb, uint32_t* bmask, uint32_t* rank) {
-    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= m) return;
-    const uint32_t d = rec[i].dst - lo, cls = pl ? 0u : max_emit(rec[i].tt & 0xFF);
-    rank[i] = (uint32_t)atomicAdd(&cb[d], route_add(cls, rec + i, d, bmask));
+template <bool DENSE>
+__global__ void __launch_bounds__(RB_STEP) k_bucket_hist(RouteIn in, uint32_t nsteps, uint32_t nb,
+                                                         uint32_t wshift, uint32_t* hist, uint32_t* n_long) {
+    extern __shared__ uint32_t hcnt[];                // nb bucket counters
+    __shared__ uint32_t spre[4][65];
+    __shared__ uint64_t sbase[4][64];
+    for (uint32_t j = threadIdx.x; j < nb; j += blockDim.x) hcnt[j] = 0;
+    if (blockIdx.x == 0 && threadIdx.x == 0) *n_long = 0;
+    __syncthreads();
+    for (uint32_t step = blockIdx.x; step < nsteps; step += gridDim.x)
+        route_step<DENSE>(in, step, spre, sbase,
+                          [&](uint32_t, uint32_t d, uint32_t) { atomicAdd(&hcnt[d >> wshift], 1u); });
+    __syncthreads();
+    for (uint32_t j = threadIdx.x; j < nb; j += blockDim.x) hist[(size_t)j * gridDim.x + blockIdx.x] = hcnt[j];
 }
 
-__global__ void k_scatter_dense(const Msg* __restrict__ rec, uint32_t m, uint32_t lo,
-                                const uint32_t* __restrict__ in_beg, const uint32_t* __restrict__ rank,
-                                uint32_t* idx) {
-    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= m) return;
-    idx[in_beg[rec[i].dst - lo] + rank[i]] = i;
+template <bool DENSE>
+__global__ void __launch_bounds__(RB_STEP) k_bucket_scatter(RouteIn in, uint32_t nsteps, uint32_t nb,
+                                                            uint32_t wshift, const uint32_t* __restrict__ off,
+                                                            uint2* pairs) {
+    extern __shared__ uint32_t hcnt[];                // nb rank counters
+    __shared__ uint32_t spre[4][65];
+    __shared__ uint64_t sbase[4][64];
+    for (uint32_t j = threadIdx.x; j < nb; j += blockDim.x) hcnt[j] = 0;
+    __syncthreads();
+    const uint32_t wmask = (1u << wshift) - 1;
+    for (uint32_t step = blockIdx.x; step < nsteps; step += gridDim.x)
+        route_step<DENSE>(in, step, spre, sbase, [&](uint32_t g, uint32_t d, uint32_t cls) {
+            const uint32_t b = d >> wshift;
+            const uint32_t r = atomicAdd(&hcnt[b], 1u);
+            pairs[off[(size_t)b * gridDim.x + blockIdx.x] + r] = make_uint2((d & wmask) | (cls << 16), g);
+        });
 }
 
-// short runs in registers (odd-even transposition network); longer ones are
-// listed for k_run_sort_long (n_long: its device-side count)
-__global__ void k_run_sort(const uint32_t* __restrict__ in_beg, const unsigned long long* __restrict__ cb,
-                           uint32_t n, uint32_t* idx, uint32_t* long_list, uint32_t* n_long) {
-    uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
-    if (d >= n) return;
-    const uint32_t k = (uint32_t)cb[d];
-    if (k < 2) return;
-    if (k > RUN_SHORT) { long_list[atomicAdd(n_long, 1u)] = d; return; }
-    uint32_t* p = idx + in_beg[d];
-    uint32_t v[RUN_SHORT];
-#pragma unroll
-    for (uint32_t t = 0; t < RUN_SHORT; t++) v[t] = t < k ? p[t] : 0xFFFFFFFFu;
-#pragma unroll
-    for (uint32_t r = 0; r < RUN_SHORT; r++) {
-#pragma unroll
-        for (uint32_t t = r & 1; t + 1 < RUN_SHORT; t += 2) {
-            const uint32_t a = v[t], b = v[t + 1];
-            v[t] = min(a, b);
-            v[t + 1] = max(a, b);
+// One block per bucket of W destinations; LDS holds per destination the
+// count, bound sum, id mask and run start (4 x W words).
+__global__ void __launch_bounds__(RR_THREADS) k_bucket_route(
+    uint32_t n, uint32_t wshift, uint32_t nblk, const uint32_t* __restrict__ off,
+    const uint2* __restrict__ pairs, const Msg* __restrict__ rec, uint32_t* rank, unsigned long long* cb,
+    uint32_t* bmask, uint32_t* in_beg, uint32_t* idx, uint32_t* long_list, uint32_t* n_long) {
+    extern __shared__ uint32_t sm[];
+    __shared__ uint32_t spart[RR_THREADS];
+    const uint32_t W = 1u << wshift, wmask = W - 1, b = blockIdx.x;
+    uint32_t* cnt = sm;
+    uint32_t* bs = sm + W;
+    uint32_t* mk = sm + 2 * W;
+    uint32_t* pre = sm + 3 * W;
+    const uint32_t s0 = off[(size_t)b * nblk], s1 = off[(size_t)(b + 1) * nblk];
+    for (uint32_t j = threadIdx.x; j < 3 * W; j += blockDim.x) sm[j] = 0;
+    __syncthreads();
+    for (uint32_t p = s0 + threadIdx.x; p < s1; p += blockDim.x) {
+        const uint2 x = pairs[p];
+        const uint32_t dl = x.x & wmask, cls = x.x >> 16;
+        rank[p] = atomicAdd(&cnt[dl], 1u);
+        if (cls == KEY_BCAST) {                       // 1 (a duplicate's PRUNE) + the id bit
+            atomicAdd(&bs[dl], 1u);
+            atomicOr(&mk[dl], 1u << (rec[x.y].a0 & 31u));
+        } else if (cls) {
+            atomicAdd(&bs[dl], cls);
         }
     }
+    __syncthreads();
+    // run starts: each thread scans W / RR_THREADS consecutive counts, then
+    // the block scans the thread totals
+    const uint32_t per = W / RR_THREADS, j0 = threadIdx.x * per;
+    uint32_t sum = 0;
+    for (uint32_t j = 0; j < per; j++) sum += cnt[j0 + j];
+    spart[threadIdx.x] = sum;
+    __syncthreads();
+    for (uint32_t o = 1; o < RR_THREADS; o <<= 1) {   // Hillis-Steele inclusive scan
+        const uint32_t v = threadIdx.x >= o ? spart[threadIdx.x - o] : 0u;
+        __syncthreads();
+        spart[threadIdx.x] += v;
+        __syncthreads();
+    }
+    uint32_t run = spart[threadIdx.x] - sum;
+    for (uint32_t j = 0; j < per; j++) {
+        pre[j0 + j] = run;
+        run += cnt[j0 + j];
+    }
+    __syncthreads();
+    for (uint32_t dl = threadIdx.x; dl < W; dl += blockDim.x) {
+        const uint32_t d = (b << wshift) + dl;
+        if (d >= n) break;
+        cb[d] = cnt[dl] | ((unsigned long long)bs[dl] << 32);
+        bmask[d] = mk[dl];
+        in_beg[d] = s0 + pre[dl];
+    }
+    if (b == gridDim.x - 1 && threadIdx.x == 0) in_beg[n] = s1;   // the record count
+    for (uint32_t p = s0 + threadIdx.x; p < s1; p += blockDim.x) {
+        const uint2 x = pairs[p];
+        idx[s0 + pre[x.x & wmask] + rank[p]] = x.y;
+    }
+    __syncthreads();                                  // the runs are in place (same block)
+    for (uint32_t dl = threadIdx.x; dl < W; dl += blockDim.x) {
+        const uint32_t k = cnt[dl];
+        if (k < 2) continue;
+        if (k > RUN_SHORT) {
+            long_list[atomicAdd(n_long, 1u)] = (b << wshift) + dl;
+            continue;
+        }
+        uint32_t* q = idx + s0 + pre[dl];
+        uint32_t v[RUN_SHORT];
 #pragma unroll
-    for (uint32_t t = 0; t < RUN_SHORT; t++)
-        if (t < k) p[t] = v[t];
+        for (uint32_t t = 0; t < RUN_SHORT; t++) v[t] = t < k ? q[t] : 0xFFFFFFFFu;
+#pragma unroll
+        for (uint32_t r = 0; r < RUN_SHORT; r++) {
+#pragma unroll
+            for (uint32_t t = r & 1; t + 1 < RUN_SHORT; t += 2) {
+                const uint32_t lo_ = v[t], hi_ = v[t + 1];
+                v[t] = min(lo_, hi_);
+                v[t + 1] = max(lo_, hi_);
+            }
+        }
+#pragma unroll
+        for (uint32_t t = 0; t < RUN_SHORT; t++)
+            if (t < k) q[t] = v[t];
+    }
 }
 
 // bitonic sort of p[0..k) (k <= RUN_LDS) through LDS, whole block
@@ -317,18 +402,6 @@ __global__ void __launch_bounds__(256) k_run_sort_long(const uint32_t* __restric
         __syncthreads();
     }
 }
-
-// cb[0..n], bmask and the long-run count
-__global__ void k_route_clear(unsigned long long* cb, uint32_t* bmask, uint32_t n, uint32_t* n_long) {
-    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i <= n) cb[i] = 0;
-    if (i < n) bmask[i] = 0;
-    if (i == 0) *n_long = 0;
-}
-
-struct Lo32 {
-    __host__ __device__ uint32_t operator()(unsigned long long v) const { return (uint32_t)v; }
-};
 
 __device__ __forceinline__ bool due(uint32_t period, uint32_t r, uint32_t start) {
     return period > 0 && r > start && ((r - start) % period) == 0;
@@ -545,7 +618,8 @@ struct Shard {
     int in_cur = 0;                     // read by this round's consume, the other one is routed into
     // per-round scratch
     DBuf<uint32_t> okey, ocnt, dpos, keys, vals, owner, owner_s, vals_s, in_beg, work,
-        alist, d_nact, rank, long_list, n_long, tmp, bmask;
+        alist, d_nact, rank, long_list, n_long, tmp, bmask, hist, hoff;
+    DBuf<uint2> pairs;                  // route: (destination in bucket | class, source index)
     DBuf<unsigned long long> cb;        // per local node: inbox count | bound sum << 32 (n + 1)
     DBuf<uint4> desc;
     DBuf<uint64_t> bound, obase, stat_part, stat_out, d_off;
@@ -773,7 +847,7 @@ int phase_events_prepare(psim_handle* h, Shard* s, const RoundCtl& ctl, RoundArg
             s->reserved = true;
             size_t fr = 0, tot = 0;
             const uint64_t r = (uint64_t)n * RESERVE_PER_NODE;
-            const uint64_t per_slot = 3 * sizeof(Msg) + 4 * sizeof(uint32_t);
+            const uint64_t per_slot = 3 * sizeof(Msg) + 6 * sizeof(uint32_t);
             if (hipMemGetInfo(&fr, &tot) == hipSuccess && r * per_slot <= fr / 4 && r > want) {
                 want = r;
                 headroom = 0;
@@ -785,6 +859,7 @@ int phase_events_prepare(psim_handle* h, Shard* s, const RoundCtl& ctl, RoundArg
             TRY(s->ivals.ensure(want, headroom));
             TRY(s->tmp.ensure(want, headroom));
             TRY(s->rank.ensure(want, headroom));
+            TRY(s->pairs.ensure(want, headroom));
             TRY(s->inbox[s->in_cur ^ 1].ensure(want, headroom));
             if (s->m_in == 0)       // nothing to read in the current one: grow both
                 TRY(s->inbox[s->in_cur].ensure(want, headroom));
@@ -848,53 +923,50 @@ int phase_compact(psim_handle* h, Shard* s) {
     return PSIM_OK;
 }
 
-// Route counting pass over the outbox runs (dense == nullptr) or the `m`
-// records of `dense`: per-destination counts and bounds, run starts
-// (in_beg[n] = the record count, on the device)
-int route_count(psim_handle* h, Shard* s, const Msg* dense, uint32_t m) {
+// The route (section comment above the kernels) over this shard's outbox
+// runs (dense == nullptr) or the m records of `dense`; leaves cb, bmask,
+// in_beg[0..n] (in_beg[n] = the record count) and the sorted runs of
+// source indices in ivals.  No host synchronisation.
+int route_group(psim_handle* h, Shard* s, const Msg* dense, uint32_t m) {
     const uint32_t n = s->n;
-    KTimer t(h, s, KT_SCAN);
-    k_route_clear<<<grid_for(n + 1), BLK, 0, s->stream>>>(s->cb.p, s->bmask.p, n, s->n_long.p);
-    if (!dense)
-        k_route_runs<false><<<grid_for(n), BLK, 0, s->stream>>>(s->outbox.p, s->okey.p, s->obase.p, s->ocnt.p,
-                                                                n, s->lo, s->cb.p, s->bmask.p, s->rank.p,
-                                                                nullptr, nullptr);
-    else if (m)
-        k_count_dense<<<grid_for(m), BLK, 0, s->stream>>>(dense, m, s->lo,
-                                                          h->cfg.manager == PSIM_MANAGER_PLUGGABLE,
-                                                          s->cb.p, s->bmask.p, s->rank.p);
-    {
-        hipcub::TransformInputIterator<uint32_t, Lo32, const unsigned long long*> cnt(s->cb.p, Lo32());
-        size_t tb = 0;
-        HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, cnt, s->in_beg.p, n + 1, s->stream));
-        TRY(s->cub_tmp.ensure(tb));
-        HIP_TRY(hipcub::DeviceScan::ExclusiveSum(s->cub_tmp.p, tb, cnt, s->in_beg.p, n + 1, s->stream));
-    }
-    return PSIM_OK;
-}
-
-// sort every run of ivals (after a scatter)
-int route_sort_runs(Shard* s) {
-    k_run_sort<<<grid_for(s->n), BLK, 0, s->stream>>>(s->in_beg.p, s->cb.p, s->n, s->ivals.p,
-                                                      s->long_list.p, s->n_long.p);
-    k_run_sort_long<<<std::min<uint32_t>(s->n, 512), 256, 0, s->stream>>>(
-        s->in_beg.p, s->cb.p, s->ivals.p, s->tmp.p, s->long_list.p, s->n_long.p);
+    const uint32_t wshift = n > (1u << 26) ? 13 : 12;
+    const uint32_t W = 1u << wshift, nb = (n + W - 1) >> wshift;
+    const RouteIn in{dense ? dense : s->outbox.p, s->okey.p, s->obase.p, s->ocnt.p, dense ? m : n, s->lo,
+                     h->cfg.manager == PSIM_MANAGER_PLUGGABLE};
+    const uint32_t nsteps = std::max<uint32_t>(1, (in.n_src + RB_STEP - 1) / RB_STEP);
+    const uint32_t nblk = std::min<uint32_t>(nsteps, RB_MAX_BLOCKS);
+    const size_t nh = (size_t)nb * nblk + 1;
+    TRY(s->hist.ensure(nh));
+    TRY(s->hoff.ensure(nh));
+    const size_t lds_h = (size_t)nb * 4, lds_r = (size_t)W * 16;
+    KTimer t(h, s, KT_SORT);
+    HIP_TRY(hipMemsetAsync(s->hist.p + nh - 1, 0, 4, s->stream));
+    if (dense)
+        k_bucket_hist<true><<<nblk, RB_STEP, lds_h, s->stream>>>(in, nsteps, nb, wshift, s->hist.p, s->n_long.p);
+    else
+        k_bucket_hist<false><<<nblk, RB_STEP, lds_h, s->stream>>>(in, nsteps, nb, wshift, s->hist.p, s->n_long.p);
+    TRY(scan_excl(s, s->hist.p, s->hoff.p, (uint32_t)nh));
+    if (dense)
+        k_bucket_scatter<true><<<nblk, RB_STEP, lds_h, s->stream>>>(in, nsteps, nb, wshift, s->hoff.p, s->pairs.p);
+    else
+        k_bucket_scatter<false><<<nblk, RB_STEP, lds_h, s->stream>>>(in, nsteps, nb, wshift, s->hoff.p,
+                                                                     s->pairs.p);
+    k_bucket_route<<<nb, RR_THREADS, lds_r, s->stream>>>(n, wshift, nblk, s->hoff.p, s->pairs.p, in.rec, s->rank.p,
+                                                          s->cb.p, s->bmask.p, s->in_beg.p, s->ivals.p,
+                                                          s->long_list.p, s->n_long.p);
+    k_run_sort_long<<<std::min<uint32_t>(n, 512), 256, 0, s->stream>>>(s->in_beg.p, s->cb.p, s->ivals.p, s->tmp.p,
+                                                                       s->long_list.p, s->n_long.p);
+    HIP_TRY(hipGetLastError());
     return PSIM_OK;
 }
 
 // G == 1: the outbox runs grouped by destination are the whole route
 int phase_route_local(psim_handle* h, Shard* s) {
-    TRY(route_count(h, s, nullptr, 0));
-    {
-        KTimer t(h, s, KT_SORT);
-        k_route_runs<true><<<grid_for(s->n), BLK, 0, s->stream>>>(s->outbox.p, s->okey.p, s->obase.p,
-                                                                  s->ocnt.p, s->n, s->lo, nullptr, nullptr,
-                                                                  s->rank.p, s->in_beg.p, s->ivals.p);
-        TRY(route_sort_runs(s));
-    }
-    // (m_in: read back with the round's stats; ivals, tmp and the inbox were
-    // sized in prepare by the outbox total, which bounds it)
-    return gather_inbox(h, s, s->outbox.p, s->in_beg.p + s->n, (uint32_t)std::min<uint64_t>(s->pin[PIN_TOTAL], 0xFFFFFFFFu));
+    TRY(route_group(h, s, nullptr, 0));
+    // (m_in: read back with the round's stats; ivals, pairs, rank, tmp and the
+    // inbox were sized in prepare by the outbox total, which bounds it)
+    return gather_inbox(h, s, s->outbox.p, s->in_beg.p + s->n,
+                        (uint32_t)std::min<uint64_t>(s->pin[PIN_TOTAL], 0xFFFFFFFFu));
 }
 
 // G > 1, sender side: stable partition by owner shard, records gathered
@@ -928,15 +1000,9 @@ int phase_receive(psim_handle* h, Shard* s, uint32_t m) {
     TRY(s->ivals.ensure(m + 1));
     TRY(s->tmp.ensure(m + 1));
     TRY(s->rank.ensure(m + 1));
+    TRY(s->pairs.ensure(m + 1));
     TRY(s->inbox[s->in_cur ^ 1].ensure(m + 1));
-    TRY(route_count(h, s, s->recvbuf.p, m));
-    {
-        KTimer t(h, s, KT_SORT);
-        if (m)
-            k_scatter_dense<<<grid_for(m), BLK, 0, s->stream>>>(s->recvbuf.p, m, s->lo, s->in_beg.p,
-                                                               s->rank.p, s->ivals.p);
-        TRY(route_sort_runs(s));
-    }
+    TRY(route_group(h, s, s->recvbuf.p, m));
     s->m_in = m;
     return gather_inbox(h, s, s->recvbuf.p, s->in_beg.p + s->n, m);
 }
@@ -1083,6 +1149,9 @@ void fill_stats(const uint64_t* s, uint64_t round, psim_round_stats* o) {
 int shard_alloc(psim_handle* h, Shard* s) {
     HIP_TRY(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
     HIP_TRY(hipEventCreateWithFlags(&s->wait_ev, hipEventDisableTiming));
+    if (s->n > (1u << 26))      // route buckets of 8192 destinations: 128 KiB of LDS per block
+        HIP_TRY(hipFuncSetAttribute((const void*)k_bucket_route, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    8192 * 16));
     HIP_TRY(hipHostMalloc((void**)&s->pin, (NST + 8) * sizeof(uint64_t), hipHostMallocDefault));
     memset(s->pin, 0, (NST + 8) * sizeof(uint64_t));
     for (int k = 0; k < Shard::MAXT; k++) {
@@ -1137,7 +1206,8 @@ void shard_free(Shard* s) {
     s->outbox.release(); s->okey.release(); s->ocnt.release(); s->dpos.release();
     s->keys.release(); s->vals.release(); s->owner.release(); s->owner_s.release();
     s->vals_s.release(); s->cb.release(); s->in_beg.release();
-    s->rank.release(); s->long_list.release(); s->bmask.release(); s->n_long.release(); s->tmp.release();
+    s->rank.release(); s->long_list.release(); s->bmask.release();
+    s->hist.release(); s->hoff.release(); s->pairs.release(); s->n_long.release(); s->tmp.release();
     s->work.release(); s->alist.release(); s->desc.release(); s->d_nact.release(); s->bound.release();
     s->obase.release(); s->stat_part.release(); s->stat_out.release(); s->d_off.release();
     s->cub_tmp.release(); s->ev_ids.release(); s->ev_contacts.release(); s->sendbuf.release();
