@@ -7,8 +7,8 @@
 // copies) or exactly one when run as an RCCL rank (shard_world > 1).  Per
 // round and shard (DESIGN.md sections 3 and 7):
 //   events   k_crash / k_join / k_bcast_reset    (same event list on every shard)
-//   prepare  k_node_prep (bounds, work flags), compaction -> active list,
-//            scan -> obase
+//   prepare  k_node_prep (packed bound | work flag per node), one scan of them,
+//            k_desc (outbox bases + descriptors of the nodes with work)
 //   consume  k_consume (psim_consume.hip)
 //   route    G == 1: count (atomics) -> scan -> scatter -> per-run sort of
 //                    source indices -> gather (stable radix sort when one run
@@ -231,12 +231,17 @@ __device__ __forceinline__ void route_step(const RouteIn& in, uint32_t step, uin
 
 template <bool DENSE>
 __global__ void __launch_bounds__(RB_STEP) k_bucket_hist(RouteIn in, uint32_t nsteps, uint32_t nb,
-                                                         uint32_t wshift, uint32_t* hist, uint32_t* n_long) {
+                                                         uint32_t wshift, uint32_t* hist, uint32_t* n_long,
+                                                         unsigned long long* btot) {
     extern __shared__ uint32_t hcnt[];                // nb bucket counters
     __shared__ uint32_t spre[4][65];
     __shared__ uint64_t sbase[4][64];
     for (uint32_t j = threadIdx.x; j < nb; j += blockDim.x) hcnt[j] = 0;
-    if (blockIdx.x == 0 && threadIdx.x == 0) *n_long = 0;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        *n_long = 0;
+        *btot = 0;                                    // summed again by the next k_node_prep
+        hist[(size_t)nb * gridDim.x] = 0;             // the scan's extra entry
+    }
     __syncthreads();
     for (uint32_t step = blockIdx.x; step < nsteps; step += gridDim.x)
         route_step<DENSE>(in, step, spre, sbase,
@@ -411,14 +416,14 @@ __device__ __forceinline__ bool due(uint32_t period, uint32_t r, uint32_t start)
 // outbox region) and whether it has any work (inbox, join, timers, EXIT
 // scan, origin, outstanding lazy pushes).  Also counts live nodes and
 // messages addressed to dead ones.
-__global__ void k_node_prep(RoundArgs a, const uint32_t* bmask, uint64_t* bound, uint32_t* work, uint64_t* part,
-                            uint32_t* ocnt) {
-    __shared__ uint64_t s_up, s_drop;
-    if (threadIdx.x == 0) { s_up = 0; s_drop = 0; }
+__global__ void __launch_bounds__(256) k_node_prep(RoundArgs a, const uint32_t* bmask, uint64_t* packed,
+                                                   uint64_t* part, uint32_t* ocnt, unsigned long long* btot) {
+    __shared__ unsigned long long s_up, s_drop, s_b;
+    if (threadIdx.x == 0) { s_up = 0; s_drop = 0; s_b = 0; }
     if (blockIdx.x == 0 && threadIdx.x == 0) { a.ktime[0] = ~0ull; a.ktime[1] = 0; }
     __syncthreads();
-    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < a.n_local) {
+    unsigned long long up = 0, drop = 0, bs = 0;        // this thread's sums (wave-summed below)
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < a.n_local; i += gridDim.x * blockDim.x) {
         uint32_t id = a.lo + i;
         uint8_t f = a.flags[id];
         uint64_t b = 0;
@@ -438,49 +443,68 @@ __global__ void k_node_prep(RoundArgs a, const uint32_t* bmask, uint64_t* bound,
                         (per ? 1 + PSIM_SVIEW_CAP : 0) + 1;
                 w = c > 0 || (pending && !x.have) || per;
             } else {
-            bool origin = a.origin_now && id == a.origin_node;
-            // per message its class bound (a BROADCAST: 1), per distinct
-            // BROADCAST id an eager push, and the lazy tick's IHAVEs if
-            // entries are outstanding or may be added this round
-            const uint32_t bm = c ? bmask[i] : 0u;
-            b = (cbi >> 32) + BOUND_BASE + (uint64_t)__popc(bm) * BCAST_FIRST;
-            if ((f & F_LAZY) || bm) b += BOUND_LAZY;
-            if (a.crash_round) b += BOUND_EXITS;
-            if (origin) b += BOUND_ORIGIN;
-            w = c > 0 || st == r || a.crash_round || (f & F_LAZY) || origin ||
-                (a.random_promotion && (f & F_LOWACT) && due(a.promotion_period, r, st)) ||
-                due(a.shuffle_period, r, st);
+                bool origin = a.origin_now && id == a.origin_node;
+                // per message its class bound (a BROADCAST: 1), per distinct
+                // BROADCAST id an eager push, and the lazy tick's IHAVEs if
+                // entries are outstanding or may be added this round
+                const uint32_t bm = c ? bmask[i] : 0u;
+                b = (cbi >> 32) + BOUND_BASE + (uint64_t)__popc(bm) * BCAST_FIRST;
+                if ((f & F_LAZY) || bm) b += BOUND_LAZY;
+                if (a.crash_round) b += BOUND_EXITS;
+                if (origin) b += BOUND_ORIGIN;
+                w = c > 0 || st == r || a.crash_round || (f & F_LAZY) || origin ||
+                    (a.random_promotion && (f & F_LOWACT) && due(a.promotion_period, r, st)) ||
+                    due(a.shuffle_period, r, st);
             }
-            atomicAdd((unsigned long long*)&s_up, 1ull);
-        } else if (c) {
-            atomicAdd((unsigned long long*)&s_drop, (unsigned long long)c);
+            up++;
+        } else {
+            drop += c;
         }
-        bound[i] = b;
-        work[i] = w;
+        // one scan gives both the outbox base (high word: the bounds) and
+        // the position in the active list (low word: the work flags)
+        packed[i] = (b << 32) | w;
         ocnt[i] = 0;               // consume writes the count of every node it runs
+        bs += b;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        up += __shfl_xor(up, o);
+        drop += __shfl_xor(drop, o);
+        bs += __shfl_xor(bs, o);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        if (up) atomicAdd(&s_up, up);
+        if (drop) atomicAdd(&s_drop, drop);
+        if (bs) atomicAdd(&s_b, bs);
     }
     __syncthreads();
+    // the exact total (the packed scan's high word wraps past 2^32 slots):
+    // one global add per block, few blocks
+    if (threadIdx.x == 0 && s_b) atomicAdd(btot, s_b);
     if (threadIdx.x < NST) {
         uint64_t v = threadIdx.x == ST_UP ? s_up : threadIdx.x == ST_DROPPED ? s_drop : 0ull;
         part[(size_t)blockIdx.x * NST + threadIdx.x] = v;
     }
 }
 
-// work descriptors of the active list: every address k_consume needs first,
-// and which of the node's timers are due (hv:542-607, pt:341-345)
-__global__ void k_desc(const uint32_t* __restrict__ alist, const uint32_t* __restrict__ nact,
+// Per node, from the scan of the packed (bound, work) words: the outbox
+// base, and for a node with work its descriptor at its active-list position
+// -- every address k_consume needs first and which of the node's timers are
+// due (hv:542-607, pt:341-345).  Entry n: the outbox total and the count.
+__global__ void k_desc(const uint64_t* __restrict__ packed, const uint64_t* __restrict__ pscan,
                        const uint32_t* __restrict__ in_beg, const unsigned long long* __restrict__ cb,
-                       const uint64_t* __restrict__ obase, const uint32_t* __restrict__ start,
-                       RoundArgs a, uint4* __restrict__ desc) {
-    const uint32_t na = *nact;
-    for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < na; k += gridDim.x * blockDim.x) {
-        uint32_t n = alist[k], li = n - a.lo;
-        uint32_t st = start[li], r = a.round;
-        uint32_t tf = (a.random_promotion && due(a.promotion_period, r, st) ? DESC_PROMO : 0u) |
-                      (due(a.shuffle_period, r, st) ? DESC_SHUFFLE : 0u) |
-                      (a.plumtree && due(a.lazy_tick_period, r, st) ? DESC_LAZY : 0u);
-        desc[k] = make_uint4(n, in_beg[li], (uint32_t)cb[li] | (tf << 28), (uint32_t)obase[li]);
-    }
+                       const uint32_t* __restrict__ start, RoundArgs a, uint4* __restrict__ desc,
+                       uint64_t* __restrict__ obase, uint32_t* nact, const unsigned long long* btot) {
+    const uint32_t li = blockIdx.x * blockDim.x + threadIdx.x;
+    if (li > a.n_local) return;
+    const uint64_t P = pscan[li];
+    obase[li] = P >> 32;
+    if (li == a.n_local) { *nact = (uint32_t)P; obase[li] = *btot; return; }
+    if (!(packed[li] & 1u)) return;
+    const uint32_t st = start[li], r = a.round;
+    const uint32_t tf = (a.random_promotion && due(a.promotion_period, r, st) ? DESC_PROMO : 0u) |
+                        (due(a.shuffle_period, r, st) ? DESC_SHUFFLE : 0u) |
+                        (a.plumtree && due(a.lazy_tick_period, r, st) ? DESC_LAZY : 0u);
+    desc[(uint32_t)P] = make_uint4(a.lo + li, in_beg[li], (uint32_t)cb[li] | (tf << 28), (uint32_t)(P >> 32));
 }
 
 // Dense (key, slot) pairs of this round's emissions, in node (= src, seq) order.
@@ -617,12 +641,13 @@ struct Shard {
     DBuf<Msg> inbox[2];                 // records by node run, in inbox order: inbox[in_cur] is
     int in_cur = 0;                     // read by this round's consume, the other one is routed into
     // per-round scratch
-    DBuf<uint32_t> okey, ocnt, dpos, keys, vals, owner, owner_s, vals_s, in_beg, work,
-        alist, d_nact, rank, long_list, n_long, tmp, bmask, hist, hoff;
+    DBuf<uint32_t> okey, ocnt, dpos, keys, vals, owner, owner_s, vals_s, in_beg,
+        d_nact, rank, long_list, n_long, tmp, bmask, hist, hoff;
     DBuf<uint2> pairs;                  // route: (destination in bucket | class, source index)
     DBuf<unsigned long long> cb;        // per local node: inbox count | bound sum << 32 (n + 1)
+    DBuf<unsigned long long> btot;      // this round's outbox total (k_node_prep)
     DBuf<uint4> desc;
-    DBuf<uint64_t> bound, obase, stat_part, stat_out, d_off;
+    DBuf<uint64_t> bound, pscan, obase, stat_part, stat_out, d_off;   // bound: packed (bound << 32 | work)
     DBuf<uint8_t> cub_tmp;
     DBuf<uint32_t> ev_ids, ev_contacts;
     DBuf<Msg> sendbuf;
@@ -816,22 +841,16 @@ int phase_events_prepare(psim_handle* h, Shard* s, const RoundCtl& ctl, RoundArg
     {
         KTimer t(h, s, KT_PREPARE);
         a.in_cb = s->cb.p;
-        s->pgrid = grid_for(n);
+        s->pgrid = std::min<uint32_t>(grid_for(n), 512);   // grid-stride: few partials
         s->cgrid = std::min<uint32_t>(grid_for(n), h->consume_blocks);
         TRY(s->stat_part.ensure((size_t)(s->pgrid + s->cgrid) * NST));
-        k_node_prep<<<s->pgrid, BLK, 0, s->stream>>>(a, s->bmask.p, s->bound.p, s->work.p, s->stat_part.p,
-                                                     s->ocnt.p);
-        {
-            size_t tb = 0;
-            hipcub::CountingInputIterator<uint32_t> ids(s->lo);
-            HIP_TRY(hipcub::DeviceSelect::Flagged(nullptr, tb, ids, s->work.p, s->alist.p, s->d_nact.p,
-                                                  n, s->stream));
-            TRY(s->cub_tmp.ensure(tb));
-            HIP_TRY(hipcub::DeviceSelect::Flagged(s->cub_tmp.p, tb, ids, s->work.p, s->alist.p,
-                                                  s->d_nact.p, n, s->stream));
-        }
-        // bound[n] = 0, so obase[n] is the outbox total (in_beg: the last route's scan)
-        TRY(scan_excl(s, s->bound.p, s->obase.p, n + 1));
+        k_node_prep<<<s->pgrid, BLK, 0, s->stream>>>(a, s->bmask.p, s->bound.p, s->stat_part.p, s->ocnt.p,
+                                                     s->btot.p);
+        // bound[n] = 0: pscan[n] = (outbox total << 32) | active count;
+        // obase[n] = the exact total (btot, summed by k_node_prep)
+        TRY(scan_excl(s, s->bound.p, s->pscan.p, n + 1));
+        k_desc<<<grid_for(n + 1), BLK, 0, s->stream>>>(s->bound.p, s->pscan.p, s->in_beg.p, s->cb.p, s->start.p, a,
+                                                        s->desc.p, s->obase.p, s->d_nact.p, s->btot.p);
         if (s->m_in > DESC_CNT_MASK) return PSIM_ENOMEM;   // per-node inbox counts must fit 28 bits
         HIP_TRY(hipMemcpyAsync(s->pin + PIN_TOTAL, s->obase.p + n, 8, hipMemcpyDeviceToHost, s->stream));
         TRY(stream_wait(s));
@@ -864,8 +883,6 @@ int phase_events_prepare(psim_handle* h, Shard* s, const RoundCtl& ctl, RoundArg
             if (s->m_in == 0)       // nothing to read in the current one: grow both
                 TRY(s->inbox[s->in_cur].ensure(want, headroom));
         }
-        k_desc<<<std::min<uint32_t>(grid_for(n), 4096), BLK, 0, s->stream>>>(
-            s->alist.p, s->d_nact.p, s->in_beg.p, s->cb.p, s->obase.p, s->start.p, a, s->desc.p);
     }
     a.in_beg = s->in_beg.p;
     a.desc = s->desc.p; a.n_alist = s->d_nact.p;
@@ -940,11 +957,12 @@ int route_group(psim_handle* h, Shard* s, const Msg* dense, uint32_t m) {
     TRY(s->hoff.ensure(nh));
     const size_t lds_h = (size_t)nb * 4, lds_r = (size_t)W * 16;
     KTimer t(h, s, KT_SORT);
-    HIP_TRY(hipMemsetAsync(s->hist.p + nh - 1, 0, 4, s->stream));
     if (dense)
-        k_bucket_hist<true><<<nblk, RB_STEP, lds_h, s->stream>>>(in, nsteps, nb, wshift, s->hist.p, s->n_long.p);
+        k_bucket_hist<true><<<nblk, RB_STEP, lds_h, s->stream>>>(in, nsteps, nb, wshift, s->hist.p, s->n_long.p,
+                                                                 s->btot.p);
     else
-        k_bucket_hist<false><<<nblk, RB_STEP, lds_h, s->stream>>>(in, nsteps, nb, wshift, s->hist.p, s->n_long.p);
+        k_bucket_hist<false><<<nblk, RB_STEP, lds_h, s->stream>>>(in, nsteps, nb, wshift, s->hist.p, s->n_long.p,
+                                                                  s->btot.p);
     TRY(scan_excl(s, s->hist.p, s->hoff.p, (uint32_t)nh));
     if (dense)
         k_bucket_scatter<true><<<nblk, RB_STEP, lds_h, s->stream>>>(in, nsteps, nb, wshift, s->hoff.p, s->pairs.p);
@@ -1169,9 +1187,9 @@ int shard_alloc(psim_handle* h, Shard* s) {
     rc |= s->pt_eag.alloc(n * PSIM_PT_SET_CAP); rc |= s->pt_laz.alloc(n * PSIM_PT_SET_CAP);
     rc |= s->pt_out.alloc(n * PSIM_PT_OUT_CAP); rc |= s->start.alloc(n);
     rc |= s->ocnt.alloc(n); rc |= s->dpos.alloc(n); rc |= s->cb.alloc(n + 1);
-    rc |= s->in_beg.alloc(n + 1); rc |= s->bound.alloc(n + 1); rc |= s->obase.alloc(n + 1);
-    rc |= s->long_list.alloc(n); rc |= s->bmask.alloc(n); rc |= s->n_long.alloc(1);
-    rc |= s->work.alloc(n); rc |= s->alist.alloc(n); rc |= s->desc.alloc(n); rc |= s->d_nact.alloc(1);
+    rc |= s->in_beg.alloc(n + 1); rc |= s->bound.alloc(n + 1); rc |= s->pscan.alloc(n + 1); rc |= s->obase.alloc(n + 1);
+    rc |= s->long_list.alloc(n); rc |= s->bmask.alloc(n); rc |= s->btot.alloc(1); rc |= s->n_long.alloc(1);
+    rc |= s->desc.alloc(n); rc |= s->d_nact.alloc(1);
     rc |= s->stat_out.alloc(NST + 2);   // + the consume span
     rc |= s->ikeys.alloc(1024); rc |= s->ivals.alloc(1024);
     rc |= s->recvbuf.alloc(1024); rc |= s->inbox[0].alloc(1024); rc |= s->inbox[1].alloc(1024); rc |= s->outbox.alloc(1024);
@@ -1206,9 +1224,9 @@ void shard_free(Shard* s) {
     s->outbox.release(); s->okey.release(); s->ocnt.release(); s->dpos.release();
     s->keys.release(); s->vals.release(); s->owner.release(); s->owner_s.release();
     s->vals_s.release(); s->cb.release(); s->in_beg.release();
-    s->rank.release(); s->long_list.release(); s->bmask.release();
+    s->rank.release(); s->long_list.release(); s->bmask.release(); s->btot.release();
     s->hist.release(); s->hoff.release(); s->pairs.release(); s->n_long.release(); s->tmp.release();
-    s->work.release(); s->alist.release(); s->desc.release(); s->d_nact.release(); s->bound.release();
+    s->desc.release(); s->d_nact.release(); s->bound.release(); s->pscan.release();
     s->obase.release(); s->stat_part.release(); s->stat_out.release(); s->d_off.release();
     s->cub_tmp.release(); s->ev_ids.release(); s->ev_contacts.release(); s->sendbuf.release();
     s->sview.release(); s->sinv.release(); s->fbits.release(); s->pay[0].release(); s->pay[1].release();
