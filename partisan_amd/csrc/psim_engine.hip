@@ -40,6 +40,9 @@ using namespace psim;
 namespace {
 
 constexpr int BLK = 256;
+// pinned host words per shard (Shard::pin): NST stats, the consume span, the
+// outbox total, the routed record count -- stored by kernels, read by the host
+enum { PIN_TOTAL = NST + 2, PIN_M = NST + 3 };
 
 #define HIP_TRY(x)                                                       \
     do {                                                                 \
@@ -273,7 +276,7 @@ __global__ void __launch_bounds__(RB_STEP) k_bucket_scatter(RouteIn in, uint32_t
 __global__ void __launch_bounds__(RR_THREADS) k_bucket_route(
     uint32_t n, uint32_t wshift, uint32_t nblk, const uint32_t* __restrict__ off,
     const uint2* __restrict__ pairs, const Msg* __restrict__ rec, uint32_t* rank, unsigned long long* cb,
-    uint32_t* bmask, uint32_t* in_beg, uint32_t* idx, uint32_t* long_list, uint32_t* n_long) {
+    uint32_t* bmask, uint32_t* in_beg, uint32_t* idx, uint32_t* long_list, uint32_t* n_long, uint64_t* hm) {
     extern __shared__ uint32_t sm[];
     __shared__ uint32_t spart[RR_THREADS];
     const uint32_t W = 1u << wshift, wmask = W - 1, b = blockIdx.x;
@@ -322,7 +325,10 @@ __global__ void __launch_bounds__(RR_THREADS) k_bucket_route(
         bmask[d] = mk[dl];
         in_beg[d] = s0 + pre[dl];
     }
-    if (b == gridDim.x - 1 && threadIdx.x == 0) in_beg[n] = s1;   // the record count
+    if (b == gridDim.x - 1 && threadIdx.x == 0) {   // the record count
+        in_beg[n] = s1;
+        *hm = s1;
+    }
     for (uint32_t p = s0 + threadIdx.x; p < s1; p += blockDim.x) {
         const uint2 x = pairs[p];
         idx[s0 + pre[x.x & wmask] + rank[p]] = x.y;
@@ -493,12 +499,18 @@ __global__ void __launch_bounds__(256) k_node_prep(RoundArgs a, const uint32_t* 
 __global__ void k_desc(const uint64_t* __restrict__ packed, const uint64_t* __restrict__ pscan,
                        const uint32_t* __restrict__ in_beg, const unsigned long long* __restrict__ cb,
                        const uint32_t* __restrict__ start, RoundArgs a, uint4* __restrict__ desc,
-                       uint64_t* __restrict__ obase, uint32_t* nact, const unsigned long long* btot) {
+                       uint64_t* __restrict__ obase, uint32_t* nact, const unsigned long long* btot,
+                       uint64_t* hout) {
     const uint32_t li = blockIdx.x * blockDim.x + threadIdx.x;
     if (li > a.n_local) return;
     const uint64_t P = pscan[li];
     obase[li] = P >> 32;
-    if (li == a.n_local) { *nact = (uint32_t)P; obase[li] = *btot; return; }
+    if (li == a.n_local) {
+        *nact = (uint32_t)P;
+        obase[li] = *btot;
+        hout[PIN_TOTAL] = *btot;                      // the host's one mid-round read
+        return;
+    }
     if (!(packed[li] & 1u)) return;
     const uint32_t st = start[li], r = a.round;
     const uint32_t tf = (a.random_promotion && due(a.promotion_period, r, st) ? DESC_PROMO : 0u) |
@@ -562,8 +574,11 @@ __global__ void k_gather(const Msg* __restrict__ rec, const uint32_t* __restrict
     reinterpret_cast<uint4*>(&out[i])[t & 3] = s[t & 3];
 }
 
-// one block per stats slot; lanes stride over the per-block partials
-__global__ void k_stats_reduce(const uint64_t* part, uint32_t nblocks, uint64_t* out) {
+// one block per stats slot; lanes stride over the per-block partials.  The
+// sums (and the consume span, out[NST..NST+1]) are also stored straight
+// into the shard's pinned host words, so the host reads them after its
+// end-of-round wait without a copy.
+__global__ void k_stats_reduce(const uint64_t* part, uint32_t nblocks, uint64_t* out, uint64_t* hout) {
     __shared__ uint64_t red[BLK];
     uint32_t k = blockIdx.x;
     uint64_t s = 0;
@@ -574,7 +589,11 @@ __global__ void k_stats_reduce(const uint64_t* part, uint32_t nblocks, uint64_t*
         if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
         __syncthreads();
     }
-    if (threadIdx.x == 0) out[k] = red[0];
+    if (threadIdx.x == 0) {
+        out[k] = red[0];
+        hout[k] = red[0];
+        if (k == 0) { hout[NST] = out[NST]; hout[NST + 1] = out[NST + 1]; }
+    }
 }
 
 // ------------------------------------------------------------- buffers --
@@ -621,7 +640,6 @@ int bits_for(uint64_t n) {
     return b;
 }
 
-enum { PIN_TOTAL = NST + 2, PIN_M = NST + 3 };
 constexpr uint64_t RESERVE_PER_NODE = 24;   // outbox slots per node reserved up front
 
 struct Shard {
@@ -659,6 +677,7 @@ struct Shard {
     // pinned host words: NST stats and the consume span (stat_out), then the
     // outbox total and the routed record count: the round's two read-backs
     uint64_t* pin = nullptr;
+    uint64_t* pin_dev = nullptr;        // the same words, as the kernels store them
     // phase timers: event pairs recorded on the stream and read back once per
     // round, after the round's final synchronisation (no sync per phase)
     static constexpr int MAXT = 32;
@@ -850,10 +869,9 @@ int phase_events_prepare(psim_handle* h, Shard* s, const RoundCtl& ctl, RoundArg
         // obase[n] = the exact total (btot, summed by k_node_prep)
         TRY(scan_excl(s, s->bound.p, s->pscan.p, n + 1));
         k_desc<<<grid_for(n + 1), BLK, 0, s->stream>>>(s->bound.p, s->pscan.p, s->in_beg.p, s->cb.p, s->start.p, a,
-                                                        s->desc.p, s->obase.p, s->d_nact.p, s->btot.p);
+                                                        s->desc.p, s->obase.p, s->d_nact.p, s->btot.p, s->pin_dev);
         if (s->m_in > DESC_CNT_MASK) return PSIM_ENOMEM;   // per-node inbox counts must fit 28 bits
-        HIP_TRY(hipMemcpyAsync(s->pin + PIN_TOTAL, s->obase.p + n, 8, hipMemcpyDeviceToHost, s->stream));
-        TRY(stream_wait(s));
+        TRY(stream_wait(s));                          // (k_desc stored the total in pin)
         const uint64_t total = s->pin[PIN_TOTAL];
         if (total >= 0xFFFFFFFFull) return PSIM_ENOMEM;
         // the bound peaks on broadcast rounds and creeps up for many rounds:
@@ -971,7 +989,7 @@ int route_group(psim_handle* h, Shard* s, const Msg* dense, uint32_t m) {
                                                                      s->pairs.p);
     k_bucket_route<<<nb, RR_THREADS, lds_r, s->stream>>>(n, wshift, nblk, s->hoff.p, s->pairs.p, in.rec, s->rank.p,
                                                           s->cb.p, s->bmask.p, s->in_beg.p, s->ivals.p,
-                                                          s->long_list.p, s->n_long.p);
+                                                          s->long_list.p, s->n_long.p, s->pin_dev + PIN_M);
     k_run_sort_long<<<std::min<uint32_t>(n, 512), 256, 0, s->stream>>>(s->in_beg.p, s->cb.p, s->ivals.p, s->tmp.p,
                                                                        s->long_list.p, s->n_long.p);
     HIP_TRY(hipGetLastError());
@@ -1088,7 +1106,7 @@ int exchange_rccl(psim_handle* h) {
 
 int phase_stats(psim_handle* h, Shard* s, const std::vector<uint32_t>& crashed) {
     KTimer t(h, s, KT_STATS);
-    k_stats_reduce<<<NST, BLK, 0, s->stream>>>(s->stat_part.p, s->pgrid + s->cgrid, s->stat_out.p);
+    k_stats_reduce<<<NST, BLK, 0, s->stream>>>(s->stat_part.p, s->pgrid + s->cgrid, s->stat_out.p, s->pin_dev);
     if (!crashed.empty()) {
         TRY(upload(s, s->ev_ids, crashed));
         k_uncrash<<<grid_for(crashed.size()), BLK, 0, s->stream>>>(s->flags.p, s->ev_ids.p,
@@ -1125,9 +1143,6 @@ int run_round(psim_handle* h, uint64_t* st) {
     for (Shard* s : h->shards) TRY(phase_stats(h, s, h->pend_crash));
     memset(st, 0, NST * 8);
     for (Shard* s : h->shards) {
-        HIP_TRY(hipMemcpyAsync(s->pin, s->stat_out.p, (NST + 2) * 8, hipMemcpyDeviceToHost, s->stream));
-        if (h->G == 1)
-            HIP_TRY(hipMemcpyAsync(s->pin + PIN_M, s->in_beg.p + s->n, 4, hipMemcpyDeviceToHost, s->stream));
         TRY(stream_wait(s));
         flush_timers(h, s);
         for (int k = 0; k < NST; k++) st[k] += s->pin[k];
@@ -1170,7 +1185,8 @@ int shard_alloc(psim_handle* h, Shard* s) {
     if (s->n > (1u << 26))      // route buckets of 8192 destinations: 128 KiB of LDS per block
         HIP_TRY(hipFuncSetAttribute((const void*)k_bucket_route, hipFuncAttributeMaxDynamicSharedMemorySize,
                                     8192 * 16));
-    HIP_TRY(hipHostMalloc((void**)&s->pin, (NST + 8) * sizeof(uint64_t), hipHostMallocDefault));
+    HIP_TRY(hipHostMalloc((void**)&s->pin, (NST + 8) * sizeof(uint64_t), hipHostMallocMapped));
+    HIP_TRY(hipHostGetDevicePointer((void**)&s->pin_dev, s->pin, 0));
     memset(s->pin, 0, (NST + 8) * sizeof(uint64_t));
     for (int k = 0; k < Shard::MAXT; k++) {
         HIP_TRY(hipEventCreate(&s->ev[k][0]));
