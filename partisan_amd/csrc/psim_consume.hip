@@ -978,7 +978,8 @@ DEV void writeback(Wv& w) {
     }
     a.ocnt[li] = w.seq;
     // only this wave writes its node's flag byte; peers read F_UP/F_CRASHED
-    a.flags[w.me] = (uint8_t)((w.fl & ~(F_LAZY | F_LOWACT)) | (w.out_n ? F_LAZY : 0) |
+    a.flags[w.me] = (uint8_t)((w.fl & (F_UP | F_CRASHED)) | (w.out_n ? F_LAZY : 0) |
+                              (min(w.out_n, 15u) << F_OUTN_SHIFT) |
                               (w.act_n < a.min_active ? F_LOWACT : 0));
     flush_recs(w);
     STAMP(w, 23);

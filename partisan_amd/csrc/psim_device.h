@@ -38,7 +38,10 @@ static_assert(sizeof(Msg) == 64, "Msg must be 64 B");
 // node flag byte
 // F_LAZY: outstanding lazy pushes; F_LOWACT: |active| < min_active_size (a due
 // promotion timer can act)
+// high nibble: the node's outstanding lazy pushes after its last round,
+// saturating at 15 (the next round's lazy-tick bound, k_node_prep)
 enum : uint8_t { F_UP = 1, F_CRASHED = 2, F_LAZY = 4, F_LOWACT = 8 };
+constexpr uint32_t F_OUTN_SHIFT = 4;
 
 // route key: dst in the low 27 bits, the sender-side emission bound of the
 // message type in the top 5 (used to size the receiver's next outbox).

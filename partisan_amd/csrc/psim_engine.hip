@@ -42,7 +42,7 @@ namespace {
 constexpr int BLK = 256;
 // pinned host words per shard (Shard::pin): NST stats, the consume span, the
 // outbox total, the routed record count -- stored by kernels, read by the host
-enum { PIN_TOTAL = NST + 2, PIN_M = NST + 3 };
+enum { PIN_TOTAL = NST + 2, PIN_M = NST + 3, PIN_OVF = NST + 4 };
 
 #define HIP_TRY(x)                                                       \
     do {                                                                 \
@@ -256,8 +256,13 @@ __global__ void __launch_bounds__(RB_STEP) k_bucket_hist(RouteIn in, uint32_t ns
 template <bool DENSE>
 __global__ void __launch_bounds__(RB_STEP) k_bucket_scatter(RouteIn in, uint32_t nsteps, uint32_t nb,
                                                             uint32_t wshift, const uint32_t* __restrict__ off,
-                                                            uint2* pairs) {
+                                                            uint2* pairs, uint64_t cap, uint64_t* hovf) {
     extern __shared__ uint32_t hcnt[];                // nb rank counters
+    const uint32_t m = off[(size_t)nb * gridDim.x];   // the record count
+    if (m > cap) {                                    // the route buffers are too small:
+        if (blockIdx.x == 0 && threadIdx.x == 0) *hovf = m;   // the host grows them and reruns
+        return;
+    }
     __shared__ uint32_t spre[4][65];
     __shared__ uint64_t sbase[4][64];
     for (uint32_t j = threadIdx.x; j < nb; j += blockDim.x) hcnt[j] = 0;
@@ -276,7 +281,8 @@ __global__ void __launch_bounds__(RB_STEP) k_bucket_scatter(RouteIn in, uint32_t
 __global__ void __launch_bounds__(RR_THREADS) k_bucket_route(
     uint32_t n, uint32_t wshift, uint32_t nblk, const uint32_t* __restrict__ off,
     const uint2* __restrict__ pairs, const Msg* __restrict__ rec, uint32_t* rank, unsigned long long* cb,
-    uint32_t* bmask, uint32_t* in_beg, uint32_t* idx, uint32_t* long_list, uint32_t* n_long, uint64_t* hm) {
+    uint32_t* bmask, uint32_t* in_beg, uint32_t* idx, uint32_t* long_list, uint32_t* n_long, uint64_t* hm,
+    uint64_t cap) {
     extern __shared__ uint32_t sm[];
     __shared__ uint32_t spart[RR_THREADS];
     const uint32_t W = 1u << wshift, wmask = W - 1, b = blockIdx.x;
@@ -285,6 +291,7 @@ __global__ void __launch_bounds__(RR_THREADS) k_bucket_route(
     uint32_t* mk = sm + 2 * W;
     uint32_t* pre = sm + 3 * W;
     const uint32_t s0 = off[(size_t)b * nblk], s1 = off[(size_t)(b + 1) * nblk];
+    if (off[(size_t)gridDim.x * nblk] > cap) return;  // overflow (k_bucket_scatter flagged it)
     for (uint32_t j = threadIdx.x; j < 3 * W; j += blockDim.x) sm[j] = 0;
     __syncthreads();
     for (uint32_t p = s0 + threadIdx.x; p < s1; p += blockDim.x) {
@@ -455,7 +462,14 @@ __global__ void __launch_bounds__(256) k_node_prep(RoundArgs a, const uint32_t* 
                 // entries are outstanding or may be added this round
                 const uint32_t bm = c ? bmask[i] : 0u;
                 b = (cbi >> 32) + BOUND_BASE + (uint64_t)__popc(bm) * BCAST_FIRST;
-                if ((f & F_LAZY) || bm) b += BOUND_LAZY;
+                // a due lazy tick sends every outstanding entry: those left
+                // from last round (flag nibble) and those this round's first
+                // deliveries and origin add, at most PT_OUT_CAP
+                if (a.plumtree && due(a.lazy_tick_period, r, st)) {
+                    const uint32_t prev = (f >> F_OUTN_SHIFT) >= 15 ? PSIM_PT_OUT_CAP : (f >> F_OUTN_SHIFT);
+                    b += min((uint32_t)PSIM_PT_OUT_CAP,
+                             prev + (__popc(bm) + (origin ? 1u : 0u)) * PSIM_PT_SET_CAP);
+                }
                 if (a.crash_round) b += BOUND_EXITS;
                 if (origin) b += BOUND_ORIGIN;
                 w = c > 0 || st == r || a.crash_round || (f & F_LAZY) || origin ||
@@ -554,7 +568,8 @@ __global__ void k_owner_bounds(const uint32_t* owner, uint32_t m, uint32_t g, ui
 
 // records src[slots[i]] -> out[i] for i < *pm, grid-stride, 4 lanes x 16 B
 __global__ void k_gather_dev(const Msg* __restrict__ rec, const uint32_t* __restrict__ slots,
-                             const uint32_t* __restrict__ pm, Msg* __restrict__ out) {
+                             const uint32_t* __restrict__ pm, Msg* __restrict__ out, uint64_t cap) {
+    if (*pm > cap) return;                            // the route overflowed: redone by the host
     const uint64_t m4 = (uint64_t)*pm * 4;
     for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < m4;
          t += (uint64_t)gridDim.x * blockDim.x) {
@@ -641,6 +656,7 @@ int bits_for(uint64_t n) {
 }
 
 constexpr uint64_t RESERVE_PER_NODE = 24;   // outbox slots per node reserved up front
+constexpr uint64_t RCAP_PER_NODE = 4;       // initial route capacity (records) per node
 
 struct Shard {
     uint32_t idx = 0, lo = 0, n = 0;    // global shard index, owned [lo, lo + n)
@@ -687,6 +703,7 @@ struct Shard {
     hipEvent_t wait_ev = nullptr;
     bool ev_live = false;
     bool reserved = false;              // first-round capacity reservation done
+    uint64_t rcap = 0;                  // records the route's buffers hold (G == 1: checked on the device)
 };
 
 }  // namespace
@@ -750,6 +767,8 @@ RoundArgs make_args(psim_handle* h, Shard* s) {
 
 // per-kernel-class device time, HIP events on the shard's stream; the
 // elapsed times are collected by flush_timers once the round has synchronised
+int route_buffers(Shard* s, bool both_inboxes);
+
 struct KTimer {
     Shard* s;
     int slot;
@@ -884,7 +903,7 @@ int phase_events_prepare(psim_handle* h, Shard* s, const RoundCtl& ctl, RoundArg
             s->reserved = true;
             size_t fr = 0, tot = 0;
             const uint64_t r = (uint64_t)n * RESERVE_PER_NODE;
-            const uint64_t per_slot = 3 * sizeof(Msg) + 6 * sizeof(uint32_t);
+            const uint64_t per_slot = sizeof(Msg) + sizeof(uint32_t);
             if (hipMemGetInfo(&fr, &tot) == hipSuccess && r * per_slot <= fr / 4 && r > want) {
                 want = r;
                 headroom = 0;
@@ -892,14 +911,12 @@ int phase_events_prepare(psim_handle* h, Shard* s, const RoundCtl& ctl, RoundArg
         }
         TRY(s->outbox.ensure(want, headroom));
         TRY(s->okey.ensure(want, headroom));
-        if (h->G == 1) {            // the route runs without a host sync: sized by the bound
-            TRY(s->ivals.ensure(want, headroom));
-            TRY(s->tmp.ensure(want, headroom));
-            TRY(s->rank.ensure(want, headroom));
-            TRY(s->pairs.ensure(want, headroom));
-            TRY(s->inbox[s->in_cur ^ 1].ensure(want, headroom));
-            if (s->m_in == 0)       // nothing to read in the current one: grow both
-                TRY(s->inbox[s->in_cur].ensure(want, headroom));
+        if (h->G == 1) {            // the route runs without a host sync, checking its capacity
+            if (!s->rcap) {
+                s->rcap = 4096;
+                while (s->rcap < (uint64_t)n * RCAP_PER_NODE) s->rcap <<= 1;
+            }
+            TRY(route_buffers(s, s->m_in == 0));
         }
     }
     a.in_beg = s->in_beg.p;
@@ -938,7 +955,7 @@ int gather_inbox(psim_handle* h, Shard* s, const Msg* src, const uint32_t* dev_m
     KTimer t(h, s, KT_GATHER);
     if (max_m)
         k_gather_dev<<<std::min<uint32_t>(grid_for((uint64_t)max_m * 4), 8192), BLK, 0, s->stream>>>(
-            src, s->ivals.p, dev_m, s->inbox[s->in_cur ^ 1].p);
+            src, s->ivals.p, dev_m, s->inbox[s->in_cur ^ 1].p, s->rcap);
     s->in_cur ^= 1;
     return PSIM_OK;
 }
@@ -983,16 +1000,27 @@ int route_group(psim_handle* h, Shard* s, const Msg* dense, uint32_t m) {
                                                                   s->btot.p);
     TRY(scan_excl(s, s->hist.p, s->hoff.p, (uint32_t)nh));
     if (dense)
-        k_bucket_scatter<true><<<nblk, RB_STEP, lds_h, s->stream>>>(in, nsteps, nb, wshift, s->hoff.p, s->pairs.p);
+        k_bucket_scatter<true><<<nblk, RB_STEP, lds_h, s->stream>>>(in, nsteps, nb, wshift, s->hoff.p, s->pairs.p,
+                                                                    s->rcap, s->pin_dev + PIN_OVF);
     else
         k_bucket_scatter<false><<<nblk, RB_STEP, lds_h, s->stream>>>(in, nsteps, nb, wshift, s->hoff.p,
-                                                                     s->pairs.p);
+                                                                     s->pairs.p, s->rcap, s->pin_dev + PIN_OVF);
     k_bucket_route<<<nb, RR_THREADS, lds_r, s->stream>>>(n, wshift, nblk, s->hoff.p, s->pairs.p, in.rec, s->rank.p,
                                                           s->cb.p, s->bmask.p, s->in_beg.p, s->ivals.p,
-                                                          s->long_list.p, s->n_long.p, s->pin_dev + PIN_M);
+                                                          s->long_list.p, s->n_long.p, s->pin_dev + PIN_M, s->rcap);
     k_run_sort_long<<<std::min<uint32_t>(n, 512), 256, 0, s->stream>>>(s->in_beg.p, s->cb.p, s->ivals.p, s->tmp.p,
                                                                        s->long_list.p, s->n_long.p);
     HIP_TRY(hipGetLastError());
+    return PSIM_OK;
+}
+
+// the route's buffers for rcap records (and the current inbox too when it
+// holds nothing yet)
+int route_buffers(Shard* s, bool both_inboxes) {
+    const size_t c = s->rcap + 1;
+    TRY(s->ivals.ensure(c)); TRY(s->tmp.ensure(c)); TRY(s->rank.ensure(c)); TRY(s->pairs.ensure(c));
+    TRY(s->inbox[s->in_cur ^ 1].ensure(c));
+    if (both_inboxes) TRY(s->inbox[s->in_cur].ensure(c));
     return PSIM_OK;
 }
 
@@ -1002,7 +1030,7 @@ int phase_route_local(psim_handle* h, Shard* s) {
     // (m_in: read back with the round's stats; ivals, pairs, rank, tmp and the
     // inbox were sized in prepare by the outbox total, which bounds it)
     return gather_inbox(h, s, s->outbox.p, s->in_beg.p + s->n,
-                        (uint32_t)std::min<uint64_t>(s->pin[PIN_TOTAL], 0xFFFFFFFFu));
+                        (uint32_t)std::min<uint64_t>(s->pin[PIN_TOTAL], s->rcap));
 }
 
 // G > 1, sender side: stable partition by owner shard, records gathered
@@ -1033,11 +1061,8 @@ int phase_partition(psim_handle* h, Shard* s) {
 
 // G > 1, receiver side: the shard-ordered concatenation grouped by dst
 int phase_receive(psim_handle* h, Shard* s, uint32_t m) {
-    TRY(s->ivals.ensure(m + 1));
-    TRY(s->tmp.ensure(m + 1));
-    TRY(s->rank.ensure(m + 1));
-    TRY(s->pairs.ensure(m + 1));
-    TRY(s->inbox[s->in_cur ^ 1].ensure(m + 1));
+    s->rcap = std::max<uint64_t>(s->rcap, m);   // exact: the count is on the host here
+    TRY(route_buffers(s, false));
     TRY(route_group(h, s, s->recvbuf.p, m));
     s->m_in = m;
     return gather_inbox(h, s, s->recvbuf.p, s->in_beg.p + s->n, m);
@@ -1146,6 +1171,17 @@ int run_round(psim_handle* h, uint64_t* st) {
         TRY(stream_wait(s));
         flush_timers(h, s);
         for (int k = 0; k < NST; k++) st[k] += s->pin[k];
+        if (h->G == 1 && s->pin[PIN_OVF]) {
+            // the route found more records than its buffers hold: grow them
+            // (1.5x, power of two) and route this round's outbox again
+            const uint64_t m = s->pin[PIN_OVF];
+            s->pin[PIN_OVF] = 0;
+            while (s->rcap < m + m / 2) s->rcap <<= 1;
+            s->in_cur ^= 1;                           // the skipped gather's flip
+            TRY(route_buffers(s, false));
+            TRY(phase_route_local(h, s));
+            TRY(stream_wait(s));
+        }
         if (h->G == 1) s->m_in = (uint32_t)s->pin[PIN_M];   // routed this round
         if (s->pin[NST] != ~0ull && s->pin[NST + 1] > s->pin[NST]) {   // 100 MHz ticks
             h->kt_ms[KT_CONSUME] += (double)(s->pin[NST + 1] - s->pin[NST]) * 1e-5;
