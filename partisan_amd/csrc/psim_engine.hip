@@ -915,6 +915,8 @@ int phase_events_prepare(psim_handle* h, Shard* s, const RoundCtl& ctl, RoundArg
             if (!s->rcap) {
                 s->rcap = 4096;
                 while (s->rcap < (uint64_t)n * RCAP_PER_NODE) s->rcap <<= 1;
+                // (test hook: a small start capacity exercises the regrow + reroute)
+                if (const char* e = getenv("PSIM_RCAP_INIT")) s->rcap = std::max<uint64_t>(16, strtoull(e, nullptr, 10));
             }
             TRY(route_buffers(s, s->m_in == 0));
         }

@@ -176,3 +176,13 @@ def test_gpu_matches_committed_oracle_traces():
         got = [int(x) for x in st["digest"]]
         assert got == golden[name]["digest"], (name, st["emitted"].sum(1)[:8].tolist(),
                                                st["nodes_processed"][:8].tolist(), got[:4])
+
+
+def test_route_regrow_parity(monkeypatch):
+    """A route capacity of 16 records forces the device-side overflow check,
+    the host's regrow and the reroute of the same outbox in most early
+    rounds (PSIM_RCAP_INIT, psim_engine.hip); results stay bit-identical."""
+    monkeypatch.setenv("PSIM_RCAP_INIT", "16")
+    (gs, gst), (os_, ost) = _both(S.doubling, 1024, 4, 40, bcast_period=10, bcast_first=15)
+    S.compare_stats(gst, ost)
+    S.compare_nodes(gs.nodes(), os_.nodes())
