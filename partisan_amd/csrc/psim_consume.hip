@@ -392,14 +392,50 @@ DEV uint32_t build_exchange(Wv& w, uint32_t& EX) {
     return usort_lanes(w, EX, m);
 }
 
-// merge_exchange/2 (hv:1590-1595)
+// merge_exchange/2 (hv:1590-1595): add_to_passive for each of
+// usort(Exchange) -- Active -- [Myself], in order.  Every eviction draws
+// rand:uniform(|Passive|) with |Passive| = max_passive_size, so the draws of
+// up to mt evictions are taken in parallel (lane j: the j-th eviction's
+// index); if any of them would be rejected by ?uniform_range (p ~ 2^-53)
+// the sequential add_to_passive chain runs instead.  The passive entries'
+// bucket tags are kept beside them for the to_list-order inserts.
 DEV void merge_exchange(Wv& w, uint32_t EX, uint32_t nex) {
-    uint32_t l = lane_id();
+    const uint32_t l = lane_id();
     bool in_act = false;
     for (uint32_t j = 0; j < w.act_n; j++) in_act |= (EX == rl(w.A, j));
     uint32_t T = EX;
-    uint32_t mt = usort_mask(w, T, ballot(l < nex && EX != w.me && !in_act));
-    for (uint32_t i = 0; i < mt; i++) add_to_passive(w, rl(T, i));
+    const uint32_t mt = usort_mask(w, T, ballot(l < nex && EX != w.me && !in_act));
+    if (!mt) return;
+    const uint32_t maxp = w.a->max_passive;
+    const uint64_t c0 = w.h.rng;
+    if (c0 < w.dc_base || c0 + mt - w.dc_base > 64) dc_fill(w, c0);   // cover [c0, c0 + mt)
+    const uint32_t off = (uint32_t)(c0 - w.dc_base);
+    const uint32_t src = (off + l) & 63;
+    const uint64_t v = ((uint64_t)shfl(w.DCH, (int)src) << 32) | shfl(w.DCL, (int)src);
+    const uint32_t KI = mod_small_m(v, maxp, rl(w.KM, maxp & 63));
+    const bool rej = v >= maxp && v - KI > (1ull << 58) - maxp;
+    if (maxp > 64 || ballot(l < mt && rej)) {
+        for (uint32_t i = 0; i < mt; i++) add_to_passive(w, rl(T, i));
+        return;
+    }
+    uint32_t PB = l < w.pas_n ? bucket16(w.P) : 0u;
+    uint32_t used = 0;
+    for (uint32_t i = 0; i < mt; i++) {
+        const uint32_t t = rl(T, i);
+        if (ballot(l < w.pas_n && w.P == t)) continue;
+        if (w.pas_n >= maxp) {                       // select_random(Passive, [Myself]) + remove
+            const uint32_t k = rl(KI, used++);
+            uint32_t n2 = w.pas_n;
+            vdel(PB, n2, k);
+            vdel(w.P, w.pas_n, k);
+        }
+        const uint32_t b = bucket16(t);
+        const uint32_t pos = popc(ballot(l < w.pas_n && PB <= b));
+        uint32_t n2 = w.pas_n;
+        vins(PB, n2, pos, b);
+        vins(w.P, w.pas_n, pos, t);
+    }
+    w.h.rng = c0 + used;
 }
 
 DEV void move_to_active(Wv& w, uint32_t p) {             // hv:1679-1709
