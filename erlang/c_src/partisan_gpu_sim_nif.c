@@ -183,6 +183,75 @@ static ERL_NIF_TERM nif_members(ErlNifEnv *env, int argc, const ERL_NIF_TERM arg
     return enif_make_tuple2(env, enif_make_atom(env, "ok"), list);
 }
 
+/* delivery(Ref, Node) -> {ok, {Have, Round, Hop}} : the tracked broadcast at
+ * one node (plumtree_backend merge/2 and the Round field, pt:288-293) */
+static ERL_NIF_TERM nif_delivery(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[]) {
+    sim_res *r; unsigned node;
+    uint8_t have; uint32_t rnd, hop;
+    if (!enif_get_resource(env, argv[0], SIM_RT, (void **)&r) || !enif_get_uint(env, argv[1], &node))
+        return enif_make_badarg(env);
+    enif_mutex_lock(r->mu);
+    int rc = psim_get_delivery(r->h, node, 1, &have, &rnd, &hop);
+    enif_mutex_unlock(r->mu);
+    if (rc) return err(env, rc);
+    return enif_make_tuple2(env, enif_make_atom(env, "ok"),
+                            enif_make_tuple3(env, enif_make_atom(env, have ? "true" : "false"),
+                                             enif_make_uint(env, rnd), enif_make_uint(env, hop)));
+}
+
+/* histograms(Ref) -> {ok, #{...}} : overlay statistics (psim_histograms) */
+static ERL_NIF_TERM nif_histograms(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[]) {
+    sim_res *r;
+    psim_histograms hs;
+    if (!enif_get_resource(env, argv[0], SIM_RT, (void **)&r)) return enif_make_badarg(env);
+    enif_mutex_lock(r->mu);
+    int rc = psim_get_histograms(r->h, &hs);
+    enif_mutex_unlock(r->mu);
+    if (rc) return err(env, rc);
+    const uint64_t *bins[5] = {hs.active_in, hs.passive_in, hs.active_out, hs.passive_fill, hs.hop};
+    const char *bnames[5] = {"active_in", "passive_in", "active_out", "passive_fill", "hop"};
+    ERL_NIF_TERM m = enif_make_new_map(env);
+    for (int k = 0; k < 5; k++) {
+        ERL_NIF_TERM v[PSIM_HIST_BINS];
+        for (int b = 0; b < PSIM_HIST_BINS; b++) v[b] = enif_make_uint64(env, bins[k][b]);
+        enif_make_map_put(env, m, enif_make_atom(env, bnames[k]),
+                          enif_make_list_from_array(env, v, PSIM_HIST_BINS), &m);
+    }
+    const char *snames[7] = {"n_up", "delivered", "last_round", "active_links", "symmetric_links",
+                             "components", "largest_component"};
+    const uint64_t svals[7] = {hs.n_up, hs.delivered, hs.last_round, hs.active_links, hs.symmetric_links,
+                               hs.components, hs.largest_component};
+    for (int k = 0; k < 7; k++)
+        enif_make_map_put(env, m, enif_make_atom(env, snames[k]), enif_make_uint64(env, svals[k]), &m);
+    return enif_make_tuple2(env, enif_make_atom(env, "ok"), m);
+}
+
+/* snapshot(Ref) -> {ok, Binary} ; restore(Ref, Binary) -> ok */
+static ERL_NIF_TERM nif_snapshot(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[]) {
+    sim_res *r;
+    size_t need = 0;
+    ErlNifBinary bin;
+    if (!enif_get_resource(env, argv[0], SIM_RT, (void **)&r)) return enif_make_badarg(env);
+    enif_mutex_lock(r->mu);
+    int rc = psim_snapshot(r->h, NULL, 0, &need);
+    if (!rc && !enif_alloc_binary(need, &bin)) rc = PSIM_ENOMEM;
+    if (!rc) rc = psim_snapshot(r->h, bin.data, bin.size, &need);
+    enif_mutex_unlock(r->mu);
+    if (rc) return err(env, rc);
+    return enif_make_tuple2(env, enif_make_atom(env, "ok"), enif_make_binary(env, &bin));
+}
+
+static ERL_NIF_TERM nif_restore(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[]) {
+    sim_res *r;
+    ErlNifBinary bin;
+    if (!enif_get_resource(env, argv[0], SIM_RT, (void **)&r) || !enif_inspect_binary(env, argv[1], &bin))
+        return enif_make_badarg(env);
+    enif_mutex_lock(r->mu);
+    int rc = psim_restore(r->h, bin.data, bin.size);
+    enif_mutex_unlock(r->mu);
+    return rc ? err(env, rc) : enif_make_atom(env, "ok");
+}
+
 static ErlNifFunc funcs[] = {
     {"create", 1, nif_create, 0},
     {"join_nif", 3, nif_join, 0},
@@ -191,6 +260,10 @@ static ErlNifFunc funcs[] = {
     {"step", 2, nif_step, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"active", 2, nif_active, 0},
     {"members", 3, nif_members, 0},
+    {"delivery", 2, nif_delivery, 0},
+    {"histograms", 1, nif_histograms, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"snapshot", 1, nif_snapshot, ERL_NIF_DIRTY_JOB_IO_BOUND},
+    {"restore", 2, nif_restore, ERL_NIF_DIRTY_JOB_IO_BOUND},
 };
 
 ERL_NIF_INIT(partisan_gpu_sim, funcs, load, NULL, NULL, NULL)

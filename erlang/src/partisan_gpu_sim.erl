@@ -2,7 +2,8 @@
 %% (include/partisan_gpu_sim.h).  Node ids are the simulated nodes; an id maps
 %% to the harness node_spec #{name => 'n<id>@sim', ...} (DESIGN.md section 2).
 -module(partisan_gpu_sim).
--export([create/1, join/3, crash/2, broadcast/3, step/2, active/2, members/3]).
+-export([create/1, join/3, crash/2, broadcast/3, step/2, active/2, members/3,
+         delivery/2, histograms/1, snapshot/1, restore/2]).
 -on_load(init/0).
 
 init() ->
@@ -23,6 +24,13 @@ step(_Sim, _Rounds) -> erlang:nif_error(nif_not_loaded).
 active(_Sim, _Node) -> erlang:nif_error(nif_not_loaded).
 %% pluggable manager handles: the strategy membership of Node (N = n_nodes)
 members(_Sim, _Node, _N) -> erlang:nif_error(nif_not_loaded).
+%% the tracked broadcast at Node: {ok, {Have, FirstRound, Hop}}
+delivery(_Sim, _Node) -> erlang:nif_error(nif_not_loaded).
+%% overlay statistics (psim_histograms) as a map
+histograms(_Sim) -> erlang:nif_error(nif_not_loaded).
+%% whole-simulation state as a binary, and back into a handle of the same config
+snapshot(_Sim) -> erlang:nif_error(nif_not_loaded).
+restore(_Sim, _Bin) -> erlang:nif_error(nif_not_loaded).
 
 pack(Ids) -> << <<I:32/little>> || I <- Ids >>.
 join_nif(_S, _N, _C) -> erlang:nif_error(nif_not_loaded).

@@ -60,7 +60,7 @@
 extern "C" {
 #endif
 
-#define PSIM_ABI_VERSION 2
+#define PSIM_ABI_VERSION 3
 
 /* error codes */
 #define PSIM_OK 0
@@ -209,6 +209,30 @@ typedef struct psim_strategy_view {
     uint64_t members_hash;                   /* full: sum of mix64(id + 1) over members */
 } psim_strategy_view;
 
+/* Overlay statistics of a HyParView handle (SURVEY 8(b) psim_get_histograms,
+ * 8(d) configs C/D): histograms over live nodes, bin k = value k, the last
+ * bin = PSIM_HIST_BINS - 1 or more.  Links count live -> live only.
+ * Replaces the reference's overlay checks: orchestration graph BFS
+ * (partisan_orchestration_backend.erl:333-413, 467-489) and the SUITE's
+ * connected + symmetric active views (test/partisan_SUITE.erl:2044-2108). */
+#define PSIM_HIST_BINS 64
+typedef struct psim_histograms {
+    uint64_t n_up;                           /* live nodes */
+    uint64_t active_in[PSIM_HIST_BINS];      /* by active in-degree */
+    uint64_t passive_in[PSIM_HIST_BINS];     /* by passive in-degree */
+    uint64_t active_out[PSIM_HIST_BINS];     /* by active view size (self excluded) */
+    uint64_t passive_fill[PSIM_HIST_BINS];   /* by passive view size */
+    uint64_t hop[PSIM_HIST_BINS];            /* tracked broadcast: delivered nodes by hop count */
+    uint64_t delivered;                      /* live nodes holding the tracked broadcast */
+    uint64_t last_round;                     /* latest first-delivery round of it (0: none) */
+    uint64_t active_links;                   /* directed active links between live nodes */
+    uint64_t symmetric_links;                /* ... whose reverse link exists (UINT64_MAX: not computed) */
+    uint64_t components;                     /* weakly connected components of live nodes over
+                                                active links (UINT64_MAX: not computed) */
+    uint64_t largest_component;
+    uint64_t reserved[6];
+} psim_histograms;
+
 typedef struct psim_handle psim_handle;
 
 void psim_default_config(psim_config *cfg);
@@ -234,6 +258,23 @@ int psim_get_round(psim_handle *h, uint64_t *round);
 int psim_get_strategy_nodes(psim_handle *h, uint32_t first, uint32_t count, psim_strategy_view *out);
 /* full strategy: the member bitset of one node (bit j of word j/32 = node j) */
 int psim_get_member_bits(psim_handle *h, uint32_t node, uint32_t *words, size_t n_words);
+/* Delivery state of the tracked broadcast (the last psim_broadcast) at nodes
+ * [first, first+count): have (0/1), first-delivery round and hop count
+ * (plumtree_backend merge/2 + the broadcast's Round field, pt:288-293). */
+int psim_get_delivery(psim_handle *h, uint32_t first, uint32_t count, uint8_t *have, uint32_t *round,
+                      uint32_t *hop);
+/* Overlay statistics (psim_histograms above); HyParView handles only.
+ * Symmetry and connectivity are computed when the whole overlay is in this
+ * process (one shard), otherwise reported as UINT64_MAX. */
+int psim_get_histograms(psim_handle *h, psim_histograms *out);
+/* Snapshot of the whole simulation state of this process (node rows,
+ * in-flight messages, round, events not yet applied are not included):
+ * with buf == NULL (or cap too small) only *need is set.  psim_restore
+ * loads it into a handle created with the same config; the rounds that
+ * follow are identical to the original's (HyParView handles). */
+int psim_snapshot(psim_handle *h, void *buf, size_t cap, size_t *need);
+int psim_restore(psim_handle *h, const void *buf, size_t size);
+
 /* Per-kernel device time (ms) accumulated over the last psim_step call:
  * names[i] is a static string; returns the number of entries. */
 int psim_kernel_times(psim_handle *h, const char **names, double *ms, uint64_t *launches, int cap);

@@ -1350,6 +1350,79 @@ int orc_get_nodes(struct psim_handle *h, uint32_t first, uint32_t count, psim_no
     return PSIM_OK;
 }
 
+/* Delivery of the tracked broadcast (psim_get_delivery). */
+int orc_get_delivery(struct psim_handle *h, uint32_t first, uint32_t count, uint8_t *have, uint32_t *round,
+                     uint32_t *hop) {
+    if ((uint64_t)first + count > h->N) return PSIM_ERANGE;
+    uint32_t bit = h->tracked_msg == PSIM_NONE ? 0u : 1u << (h->tracked_msg & 31u);
+    for (uint32_t k = 0; k < count; k++) {
+        const node *s = &h->nodes[first + k];
+        have[k] = (s->have & bit) ? 1 : 0;
+        round[k] = s->trk_round;
+        hop[k] = s->trk_hop;
+    }
+    return PSIM_OK;
+}
+
+static uint32_t hbin(uint32_t v) { return v < PSIM_HIST_BINS ? v : PSIM_HIST_BINS - 1; }
+static uint32_t uf_find(uint32_t *p, uint32_t x) {
+    while (p[x] != x) { p[x] = p[p[x]]; x = p[x]; }
+    return x;
+}
+
+/* Overlay statistics (psim_get_histograms), list-style over all nodes:
+ * in-degrees counted link by link, symmetry by scanning the peer's view,
+ * components by union-find over live active links. */
+int orc_get_histograms(struct psim_handle *h, psim_histograms *out) {
+    if (is_pl(h)) return PSIM_EUNSUPPORTED;
+    memset(out, 0, sizeof *out);
+    uint32_t N = h->N;
+    uint32_t *ina = calloc(N, 4), *inp = calloc(N, 4), *par = malloc((size_t)N * 4), *sz = calloc(N, 4);
+    if (!ina || !inp || !par || !sz) { free(ina); free(inp); free(par); free(sz); return PSIM_ENOMEM; }
+    uint32_t bit = h->tracked_msg == PSIM_NONE ? 0u : 1u << (h->tracked_msg & 31u);
+    for (uint32_t i = 0; i < N; i++) par[i] = i;
+    for (uint32_t i = 0; i < N; i++) {
+        const node *s = &h->nodes[i];
+        if (!s->up) continue;
+        out->n_up++;
+        uint32_t deg = 0;
+        for (uint32_t k = 0; k < s->act_n; k++) {
+            uint32_t p = s->act[k];
+            if (p == i) continue;
+            deg++;
+            if (!h->nodes[p].up) continue;
+            ina[p]++;
+            out->active_links++;
+            const node *q = &h->nodes[p];
+            for (uint32_t j = 0; j < q->act_n; j++)
+                if (q->act[j] == i) { out->symmetric_links++; break; }
+            uint32_t a = uf_find(par, i), b = uf_find(par, p);
+            if (a != b) par[a > b ? a : b] = a < b ? a : b;
+        }
+        for (uint32_t k = 0; k < s->pas_n; k++) {
+            uint32_t p = s->pas[k];
+            if (p != i && h->nodes[p].up) inp[p]++;
+        }
+        out->active_out[hbin(deg)]++;
+        out->passive_fill[hbin(s->pas_n)]++;
+        if (bit && (s->have & bit)) {
+            out->delivered++;
+            out->hop[hbin(s->trk_hop)]++;
+            if (s->trk_round != PSIM_NONE && s->trk_round > out->last_round) out->last_round = s->trk_round;
+        }
+    }
+    for (uint32_t i = 0; i < N; i++) {
+        if (!h->nodes[i].up) continue;
+        out->active_in[hbin(ina[i])]++;
+        out->passive_in[hbin(inp[i])]++;
+        uint32_t r = uf_find(par, i);
+        if (r == i) out->components++;
+        if (++sz[r] > out->largest_component) out->largest_component = sz[r];
+    }
+    free(ina); free(inp); free(par); free(sz);
+    return PSIM_OK;
+}
+
 static uint64_t members_hash(struct psim_handle *h, const uint32_t *b) {
     uint64_t x = 0;
     for (uint32_t w = 0; w < h->W; w++)

@@ -8,7 +8,7 @@ import ctypes as C
 
 import numpy as np
 
-PSIM_ABI_VERSION = 2
+PSIM_ABI_VERSION = 3
 PSIM_MAP_BIT = 0x80000000
 PSIM_NONE = 0xFFFFFFFF
 ACTIVE_CAP, PASSIVE_CAP, IDMAP_CAP = 8, 32, 32
@@ -91,6 +91,22 @@ class PsimStrategyView(C.Structure):
     ]
 
 
+HIST_BINS = 64
+
+
+class PsimHistograms(C.Structure):
+    _fields_ = [
+        ("n_up", C.c_uint64),
+        ("active_in", C.c_uint64 * HIST_BINS), ("passive_in", C.c_uint64 * HIST_BINS),
+        ("active_out", C.c_uint64 * HIST_BINS), ("passive_fill", C.c_uint64 * HIST_BINS),
+        ("hop", C.c_uint64 * HIST_BINS),
+        ("delivered", C.c_uint64), ("last_round", C.c_uint64),
+        ("active_links", C.c_uint64), ("symmetric_links", C.c_uint64),
+        ("components", C.c_uint64), ("largest_component", C.c_uint64),
+        ("reserved", C.c_uint64 * 6),
+    ]
+
+
 NODE_VIEW_DTYPE = np.dtype(PsimNodeView)
 STRATEGY_VIEW_DTYPE = np.dtype(PsimStrategyView)
 STATS_DTYPE = np.dtype(PsimRoundStats)
@@ -112,6 +128,8 @@ SIGNATURES = {
     "get_round": (C.c_int, [_H, C.POINTER(C.c_uint64)]),
     "get_strategy_nodes": (C.c_int, [_H, C.c_uint32, C.c_uint32, C.POINTER(PsimStrategyView)]),
     "get_member_bits": (C.c_int, [_H, C.c_uint32, _P32, C.c_size_t]),
+    "get_delivery": (C.c_int, [_H, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint8), _P32, _P32]),
+    "get_histograms": (C.c_int, [_H, C.POINTER(PsimHistograms)]),
 }
 # symbols only the GPU library exports
 GPU_ONLY = {
@@ -121,6 +139,8 @@ GPU_ONLY = {
                                C.POINTER(C.c_uint64), C.c_int]),
     "comm_id_size": (C.c_int, []),
     "get_comm_id": (C.c_int, [C.c_void_p, C.c_size_t]),
+    "snapshot": (C.c_int, [_H, C.c_void_p, C.c_size_t, C.POINTER(C.c_size_t)]),
+    "restore": (C.c_int, [_H, C.c_void_p, C.c_size_t]),
 }
 
 

@@ -611,6 +611,124 @@ __global__ void k_stats_reduce(const uint64_t* part, uint32_t nblocks, uint64_t*
     }
 }
 
+// --------------------------------------------------------- overlay stats --
+// psim_get_histograms: per live node its view sizes, the in-degree links it
+// contributes (global id arrays, summed over shards / RCCL ranks) and the
+// tracked broadcast's delivery.  hist layout: 5 histograms of
+// PSIM_HIST_BINS, then n_up, delivered, last_round, active_links.
+enum { H_AIN = 0, H_PIN = 1, H_AOUT = 2, H_PFILL = 3, H_HOP = 4, H_NUP = 5 * PSIM_HIST_BINS,
+       H_DELIV, H_LAST, H_LINKS, H_N };
+
+__device__ __forceinline__ uint32_t hbin(uint32_t v) { return v < PSIM_HIST_BINS ? v : PSIM_HIST_BINS - 1; }
+
+__global__ void k_hist_out(const Hdr* __restrict__ hdr, const uint32_t* __restrict__ act,
+                           const uint32_t* __restrict__ pas, const uint8_t* __restrict__ flags, uint32_t lo,
+                           uint32_t n, uint32_t tbit, uint32_t* indeg_a, uint32_t* indeg_p,
+                           unsigned long long* hist) {
+    __shared__ unsigned long long sh[H_N];
+    for (uint32_t j = threadIdx.x; j < H_N; j += blockDim.x) sh[j] = 0;
+    __syncthreads();
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n && (flags[lo + i] & F_UP)) {
+        const Hdr& x = hdr[i];
+        const uint32_t me = lo + i;
+        uint32_t out = 0;
+        for (uint32_t k = 0; k < x.act_n; k++) {
+            const uint32_t p = act[(size_t)i * PSIM_ACTIVE_CAP + k];
+            if (p == me) continue;
+            out++;
+            if (flags[p] & F_UP) { atomicAdd(&indeg_a[p], 1u); atomicAdd(&sh[H_LINKS], 1ull); }
+        }
+        for (uint32_t k = 0; k < x.pas_n; k++) {
+            const uint32_t p = pas[(size_t)i * PSIM_PASSIVE_CAP + k];
+            if (p != me && (flags[p] & F_UP)) atomicAdd(&indeg_p[p], 1u);
+        }
+        atomicAdd(&sh[H_AOUT * PSIM_HIST_BINS + hbin(out)], 1ull);
+        atomicAdd(&sh[H_PFILL * PSIM_HIST_BINS + hbin(x.pas_n)], 1ull);
+        atomicAdd(&sh[H_NUP], 1ull);
+        if (tbit && (x.have & tbit)) {
+            atomicAdd(&sh[H_DELIV], 1ull);
+            atomicAdd(&sh[H_HOP * PSIM_HIST_BINS + hbin(x.trk_hop)], 1ull);
+            if (x.trk_round != PSIM_NONE) atomicMax(&sh[H_LAST], (unsigned long long)x.trk_round);
+        }
+    }
+    __syncthreads();
+    for (uint32_t j = threadIdx.x; j < H_N; j += blockDim.x) {
+        if (!sh[j]) continue;
+        if (j == H_LAST) atomicMax(&hist[j], sh[j]);
+        else atomicAdd(&hist[j], sh[j]);
+    }
+}
+
+__global__ void k_hist_in(const uint32_t* __restrict__ indeg_a, const uint32_t* __restrict__ indeg_p,
+                          const uint8_t* __restrict__ flags, uint32_t lo, uint32_t n, unsigned long long* hist) {
+    __shared__ unsigned long long sh[2 * PSIM_HIST_BINS];
+    for (uint32_t j = threadIdx.x; j < 2 * PSIM_HIST_BINS; j += blockDim.x) sh[j] = 0;
+    __syncthreads();
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n && (flags[lo + i] & F_UP)) {
+        atomicAdd(&sh[hbin(indeg_a[lo + i])], 1ull);
+        atomicAdd(&sh[PSIM_HIST_BINS + hbin(indeg_p[lo + i])], 1ull);
+    }
+    __syncthreads();
+    for (uint32_t j = threadIdx.x; j < 2 * PSIM_HIST_BINS; j += blockDim.x)
+        if (sh[j]) atomicAdd(&hist[H_AIN * PSIM_HIST_BINS + j], sh[j]);
+}
+
+// one shard holds the whole overlay: reverse-link test and label
+// propagation over live active links (min label, then pointer jumping)
+__global__ void k_hist_sym(const Hdr* __restrict__ hdr, const uint32_t* __restrict__ act,
+                           const uint8_t* __restrict__ flags, uint32_t n, unsigned long long* sym) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n || !(flags[i] & F_UP)) return;
+    uint32_t c = 0;
+    for (uint32_t k = 0; k < hdr[i].act_n; k++) {
+        const uint32_t p = act[(size_t)i * PSIM_ACTIVE_CAP + k];
+        if (p == i || !(flags[p] & F_UP)) continue;
+        for (uint32_t q = 0; q < hdr[p].act_n; q++)
+            if (act[(size_t)p * PSIM_ACTIVE_CAP + q] == i) { c++; break; }
+    }
+    if (c) atomicAdd(sym, (unsigned long long)c);
+}
+
+__global__ void k_cc_init(const uint8_t* __restrict__ flags, uint32_t n, uint32_t* L) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) L[i] = (flags[i] & F_UP) ? i : PSIM_NONE;
+}
+
+__global__ void k_cc_hook(const Hdr* __restrict__ hdr, const uint32_t* __restrict__ act,
+                          const uint8_t* __restrict__ flags, uint32_t n, uint32_t* L, uint32_t* changed) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n || !(flags[i] & F_UP)) return;
+    for (uint32_t k = 0; k < hdr[i].act_n; k++) {
+        const uint32_t p = act[(size_t)i * PSIM_ACTIVE_CAP + k];
+        if (p == i || !(flags[p] & F_UP)) continue;
+        const uint32_t a = L[i], b = L[p];
+        if (a < b) { if (atomicMin(&L[p], a) > a) *changed = 1; }
+        else if (b < a) { if (atomicMin(&L[i], b) > b) *changed = 1; }
+    }
+}
+
+__global__ void k_cc_jump(uint32_t n, uint32_t* L) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n || L[i] == PSIM_NONE) return;
+    uint32_t r = L[i];
+    while (L[r] != r) r = L[r];
+    L[i] = r;
+}
+
+__global__ void k_cc_count(const uint32_t* __restrict__ L, uint32_t n, uint32_t* size, unsigned long long* comps) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n || L[i] == PSIM_NONE) return;
+    atomicAdd(&size[L[i]], 1u);
+    if (L[i] == i) atomicAdd(comps, 1ull);
+}
+
+__global__ void k_cc_max(const uint32_t* __restrict__ size, uint32_t n, unsigned long long* largest) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n && size[i]) atomicMax(largest, (unsigned long long)size[i]);
+}
+
 // ------------------------------------------------------------- buffers --
 template <typename T>
 struct DBuf {
@@ -1638,6 +1756,219 @@ int psim_get_member_bits(psim_handle* h, uint32_t node, uint32_t* words, size_t 
     HIP_TRY(hipMemcpyAsync(words, s->fbits.p + (size_t)(node - s->lo) * h->fw, W * 4, hipMemcpyDeviceToHost,
                            s->stream));
     HIP_TRY(hipStreamSynchronize(s->stream));
+    return PSIM_OK;
+}
+
+
+int psim_get_delivery(psim_handle* h, uint32_t first, uint32_t count, uint8_t* have, uint32_t* round,
+                      uint32_t* hop) {
+    if (!h || (count && (!have || !round || !hop))) return PSIM_EINVAL;
+    if ((uint64_t)first + count > h->N) return PSIM_ERANGE;
+    if (hipSetDevice(h->device) != hipSuccess) return PSIM_EDEVICE;
+    const uint32_t bit = h->tracked_msg == PSIM_NONE ? 0u : 1u << (h->tracked_msg & 31u);
+    uint32_t done = 0;
+    while (done < count) {
+        const uint32_t id = first + done;
+        Shard* s = owner_of(h, id);
+        if (!s) return PSIM_ERANGE;
+        const uint32_t k = std::min<uint32_t>(count - done, s->lo + s->n - id);
+        std::vector<Hdr> hd(k);
+        HIP_TRY(hipMemcpyAsync(hd.data(), s->hdr.p + (id - s->lo), k * sizeof(Hdr), hipMemcpyDeviceToHost,
+                               s->stream));
+        HIP_TRY(hipStreamSynchronize(s->stream));
+        for (uint32_t j = 0; j < k; j++) {
+            have[done + j] = (hd[j].have & bit) ? 1 : 0;
+            round[done + j] = hd[j].trk_round;
+            hop[done + j] = hd[j].trk_hop;
+        }
+        done += k;
+    }
+    return PSIM_OK;
+}
+
+int psim_get_histograms(psim_handle* h, psim_histograms* out) {
+    if (!h || !out) return PSIM_EINVAL;
+    if (h->cfg.manager == PSIM_MANAGER_PLUGGABLE) return PSIM_EUNSUPPORTED;
+    if (hipSetDevice(h->device) != hipSuccess) return PSIM_EDEVICE;
+    memset(out, 0, sizeof *out);
+    Shard* s0 = h->shards[0];
+    hipStream_t st = s0->stream;
+    for (Shard* s : h->shards) HIP_TRY(hipStreamSynchronize(s->stream));
+    const size_t N = h->N;
+    DBuf<uint32_t> ind;                          // in-degrees, active then passive, by global id
+    DBuf<unsigned long long> hist;
+    TRY(ind.alloc(2 * N));
+    TRY(hist.alloc(H_N + 4));
+    const uint32_t tbit = h->tracked_msg == PSIM_NONE ? 0u : 1u << (h->tracked_msg & 31u);
+    for (Shard* s : h->shards)
+        k_hist_out<<<grid_for(s->n), BLK, 0, st>>>(s->hdr.p, s->act.p, s->pas.p, s->flags.p, s->lo, s->n, tbit,
+                                                   ind.p, ind.p + N, hist.p);
+    if (h->world > 1) {
+        NCCL_TRY(ncclAllReduce(ind.p, ind.p, 2 * N, ncclUint32, ncclSum, h->comm, st));
+    }
+    for (Shard* s : h->shards)
+        k_hist_in<<<grid_for(s->n), BLK, 0, st>>>(ind.p, ind.p + N, s->flags.p, s->lo, s->n, hist.p);
+    std::vector<unsigned long long> hv(H_N + 4, 0);
+    HIP_TRY(hipMemcpyAsync(hv.data(), hist.p, (H_N + 4) * 8, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    if (h->world > 1) {                          // sums over ranks (the latest round: max)
+        uint64_t last = hv[H_LAST];
+        TRY(h->comm_cnt.ensure(H_N + 4));
+        HIP_TRY(hipMemcpyAsync(h->comm_cnt.p, hv.data(), (H_N + 4) * 8, hipMemcpyHostToDevice, st));
+        NCCL_TRY(ncclAllReduce(h->comm_cnt.p, h->comm_cnt.p, H_N, ncclUint64, ncclSum, h->comm, st));
+        NCCL_TRY(ncclAllReduce(h->comm_cnt.p + H_LAST, h->comm_cnt.p + H_LAST, 1, ncclUint64, ncclMax, h->comm, st));
+        HIP_TRY(hipMemcpyAsync(hv.data(), h->comm_cnt.p, (H_N + 4) * 8, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        (void)last;
+    }
+    for (int k = 0; k < PSIM_HIST_BINS; k++) {
+        out->active_in[k] = hv[H_AIN * PSIM_HIST_BINS + k];
+        out->passive_in[k] = hv[H_PIN * PSIM_HIST_BINS + k];
+        out->active_out[k] = hv[H_AOUT * PSIM_HIST_BINS + k];
+        out->passive_fill[k] = hv[H_PFILL * PSIM_HIST_BINS + k];
+        out->hop[k] = hv[H_HOP * PSIM_HIST_BINS + k];
+    }
+    out->n_up = hv[H_NUP]; out->delivered = hv[H_DELIV]; out->last_round = hv[H_LAST];
+    out->active_links = hv[H_LINKS];
+    out->symmetric_links = out->components = out->largest_component = ~0ull;
+    if (h->G == 1) {                             // the whole overlay is this shard
+        const uint32_t n = s0->n;
+        DBuf<uint32_t> L, sz, flag;
+        DBuf<unsigned long long> r;
+        TRY(L.alloc(n)); TRY(sz.alloc(n)); TRY(flag.alloc(1)); TRY(r.alloc(3));
+        k_hist_sym<<<grid_for(n), BLK, 0, st>>>(s0->hdr.p, s0->act.p, s0->flags.p, n, r.p);
+        k_cc_init<<<grid_for(n), BLK, 0, st>>>(s0->flags.p, n, L.p);
+        for (int it = 0; it < 4096; it++) {
+            uint32_t changed = 0;
+            HIP_TRY(hipMemsetAsync(flag.p, 0, 4, st));
+            k_cc_hook<<<grid_for(n), BLK, 0, st>>>(s0->hdr.p, s0->act.p, s0->flags.p, n, L.p, flag.p);
+            k_cc_jump<<<grid_for(n), BLK, 0, st>>>(n, L.p);
+            HIP_TRY(hipMemcpyAsync(&changed, flag.p, 4, hipMemcpyDeviceToHost, st));
+            HIP_TRY(hipStreamSynchronize(st));
+            if (!changed) break;
+        }
+        k_cc_count<<<grid_for(n), BLK, 0, st>>>(L.p, n, sz.p, r.p + 1);
+        k_cc_max<<<grid_for(n), BLK, 0, st>>>(sz.p, n, r.p + 2);
+        unsigned long long rv[3];
+        HIP_TRY(hipMemcpyAsync(rv, r.p, sizeof rv, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        out->symmetric_links = rv[0]; out->components = rv[1]; out->largest_component = rv[2];
+        L.release(); sz.release(); flag.release(); r.release();
+    }
+    ind.release(); hist.release();
+    return PSIM_OK;
+}
+
+
+// ----------------------------------------------------------- snapshot --
+// Layout: SnapHead, then per local shard a ShardHead and its arrays in
+// snap_sections() order.  Pending (not yet applied) events are not state:
+// a snapshot with events pending is refused.
+struct SnapHead {
+    uint32_t magic, abi, n_nodes, n_local_shards, manager, strategy, fw, started_n;
+    uint64_t round;
+    uint32_t tracked_msg, bcast_root, G, world;
+};
+struct ShardHead {
+    uint32_t lo, n, m_in, in_cur, pay_cur, pay_rows, pad[2];
+};
+constexpr uint32_t SNAP_MAGIC = 0x4D495350u;   // "PSIM"
+
+struct Section { void* p; size_t bytes; };
+
+// the arrays that make up a shard's state between rounds
+static std::vector<Section> snap_sections(psim_handle* h, Shard* s, const ShardHead& sh) {
+    const size_t N = h->N, n = s->n;
+    std::vector<Section> v = {
+        {s->flags.p, N}, {s->part.p, N}, {s->hdr.p, n * sizeof(Hdr)},
+        {s->act.p, n * PSIM_ACTIVE_CAP * 4}, {s->pas.p, n * PSIM_PASSIVE_CAP * 4},
+        {s->sentp.p, n * PSIM_IDMAP_CAP * 4}, {s->senti.p, n * PSIM_IDMAP_CAP * 4},
+        {s->recvp.p, n * PSIM_IDMAP_CAP * 4}, {s->recvi.p, n * PSIM_IDMAP_CAP * 4},
+        {s->pt_all.p, n * PSIM_PT_MEMBERS_CAP * 4}, {s->pt_com.p, n * PSIM_PT_MEMBERS_CAP * 4},
+        {s->pt_eag.p, n * PSIM_PT_SET_CAP * 4}, {s->pt_laz.p, n * PSIM_PT_SET_CAP * 4},
+        {s->pt_out.p, n * PSIM_PT_OUT_CAP * 8}, {s->start.p, n * 4},
+        {s->cb.p, (n + 1) * 8}, {s->bmask.p, n * 4}, {s->in_beg.p, (n + 1) * 4},
+        {s->inbox[sh.in_cur].p, (size_t)sh.m_in * sizeof(Msg)},
+    };
+    if (h->cfg.manager == PSIM_MANAGER_PLUGGABLE) {
+        if (s->sview.p) v.push_back({s->sview.p, n * PSIM_SVIEW_CAP * 4});
+        if (s->sinv.p) v.push_back({s->sinv.p, n * PSIM_SVIEW_CAP * 4});
+        if (s->fbits.p) v.push_back({s->fbits.p, n * h->fw * 4});
+        if (sh.pay_rows) v.push_back({s->pay[sh.pay_cur ^ 1].p, (size_t)sh.pay_rows * h->fw * 4});
+    }
+    return v;
+}
+
+int psim_snapshot(psim_handle* h, void* buf, size_t cap, size_t* need) {
+    if (!h || !need) return PSIM_EINVAL;
+    if (!h->pend_crash.empty() || !h->pend_join.empty() || h->pend_part_set || h->pend_part_clear ||
+        h->pend_bcast)
+        return PSIM_ESTATE;
+    if (hipSetDevice(h->device) != hipSuccess) return PSIM_EDEVICE;
+    std::vector<ShardHead> heads;
+    size_t total = sizeof(SnapHead) + h->started.size();
+    for (Shard* s : h->shards) {
+        HIP_TRY(hipStreamSynchronize(s->stream));
+        ShardHead sh{s->lo, s->n, s->m_in, (uint32_t)s->in_cur, (uint32_t)s->pay_cur, 0, {0, 0}};
+        if (h->cfg.manager == PSIM_MANAGER_PLUGGABLE && s->pay_top.p)
+            sh.pay_rows = read1(s, s->pay_top.p);
+        heads.push_back(sh);
+        total += sizeof(ShardHead);
+        for (const Section& x : snap_sections(h, s, sh)) total += x.bytes;
+    }
+    *need = total;
+    if (!buf || cap < total) return PSIM_OK;
+    char* o = static_cast<char*>(buf);
+    SnapHead hd{SNAP_MAGIC, PSIM_ABI_VERSION, h->N, (uint32_t)h->shards.size(), h->cfg.manager, h->cfg.strategy,
+                h->fw, (uint32_t)h->started.size(), h->round, h->tracked_msg, h->bcast_root, h->G, (uint32_t)h->world};
+    memcpy(o, &hd, sizeof hd); o += sizeof hd;
+    if (!h->started.empty()) { memcpy(o, h->started.data(), h->started.size()); o += h->started.size(); }
+    for (size_t k = 0; k < h->shards.size(); k++) {
+        Shard* s = h->shards[k];
+        memcpy(o, &heads[k], sizeof(ShardHead)); o += sizeof(ShardHead);
+        for (const Section& x : snap_sections(h, s, heads[k])) {
+            if (x.bytes) HIP_TRY(hipMemcpy(o, x.p, x.bytes, hipMemcpyDeviceToHost));
+            o += x.bytes;
+        }
+    }
+    return PSIM_OK;
+}
+
+int psim_restore(psim_handle* h, const void* buf, size_t size) {
+    if (!h || !buf || size < sizeof(SnapHead)) return PSIM_EINVAL;
+    if (hipSetDevice(h->device) != hipSuccess) return PSIM_EDEVICE;
+    const char* o = static_cast<const char*>(buf);
+    const char* end = o + size;
+    SnapHead hd;
+    memcpy(&hd, o, sizeof hd); o += sizeof hd;
+    if (hd.magic != SNAP_MAGIC || hd.abi != PSIM_ABI_VERSION || hd.n_nodes != h->N ||
+        hd.n_local_shards != h->shards.size() || hd.manager != h->cfg.manager || hd.strategy != h->cfg.strategy ||
+        hd.fw != h->fw || hd.G != h->G || hd.world != (uint32_t)h->world)
+        return PSIM_EINVAL;
+    if (hd.started_n) {
+        if ((size_t)(end - o) < hd.started_n) return PSIM_EINVAL;
+        h->started.assign(o, o + hd.started_n); o += hd.started_n;
+    }
+    for (Shard* s : h->shards) {
+        HIP_TRY(hipStreamSynchronize(s->stream));
+        if ((size_t)(end - o) < sizeof(ShardHead)) return PSIM_EINVAL;
+        ShardHead sh;
+        memcpy(&sh, o, sizeof sh); o += sizeof sh;
+        if (sh.lo != s->lo || sh.n != s->n) return PSIM_EINVAL;
+        s->m_in = sh.m_in; s->in_cur = (int)sh.in_cur; s->pay_cur = (int)sh.pay_cur;
+        TRY(s->inbox[s->in_cur].ensure((size_t)sh.m_in + 1));
+        if (sh.pay_rows) TRY(s->pay[s->pay_cur ^ 1].ensure((size_t)sh.pay_rows * h->fw));
+        if (h->cfg.manager == PSIM_MANAGER_PLUGGABLE && s->pay_top.p)
+            HIP_TRY(hipMemcpy(s->pay_top.p, &sh.pay_rows, 4, hipMemcpyHostToDevice));
+        for (const Section& x : snap_sections(h, s, sh)) {
+            if ((size_t)(end - o) < x.bytes) return PSIM_EINVAL;
+            if (x.bytes) HIP_TRY(hipMemcpy(x.p, o, x.bytes, hipMemcpyHostToDevice));
+            o += x.bytes;
+        }
+        s->reserved = false;
+    }
+    h->round = hd.round; h->tracked_msg = hd.tracked_msg; h->bcast_root = hd.bcast_root;
+    HIP_TRY(hipDeviceSynchronize());
     return PSIM_OK;
 }
 

@@ -121,6 +121,30 @@ class _Driver:
                     "get_nodes")
         return out
 
+    def delivery(self, first=0, count=None):
+        """Tracked broadcast per node: (have, first-delivery round, hop)."""
+        if count is None:
+            count = self.n - first
+        have = np.zeros(count, np.uint8)
+        rnd = np.zeros(count, np.uint32)
+        hop = np.zeros(count, np.uint32)
+        self._check(self._api["get_delivery"](self._h, first, count,
+                                              have.ctypes.data_as(C.POINTER(C.c_uint8)),
+                                              _abi.u32p(rnd), _abi.u32p(hop)), "get_delivery")
+        return have, rnd, hop
+
+    def histograms(self):
+        """Overlay statistics (psim_histograms) as a dict of ints / arrays."""
+        h = _abi.PsimHistograms()
+        self._check(self._api["get_histograms"](self._h, C.byref(h)), "get_histograms")
+        out = {}
+        for name, _ in _abi.PsimHistograms._fields_:
+            if name == "reserved":
+                continue
+            v = getattr(h, name)
+            out[name] = np.array(v[:], np.uint64) if hasattr(v, "__len__") else int(v)
+        return out
+
     def run_schedule(self, schedule, until_round, extra=None):
         """Apply [(round, ids, contacts)] join events and step until `until_round`.
         `extra(round)` may inject further events before each round."""
@@ -206,6 +230,19 @@ class Simulator(_Driver):
             self._comm_buf = C.create_string_buffer(bytes(comm), len(comm))
             cfg.comm_id = C.cast(self._comm_buf, C.c_void_p)
         super().__init__(api, cfg, errname=extra["strerror"])
+
+    def snapshot(self):
+        """The whole simulation state as bytes (psim_snapshot)."""
+        need = C.c_size_t()
+        self._check(self._extra["snapshot"](self._h, None, 0, C.byref(need)), "snapshot")
+        buf = C.create_string_buffer(need.value)
+        self._check(self._extra["snapshot"](self._h, buf, need.value, C.byref(need)), "snapshot")
+        return buf.raw[:need.value]
+
+    def restore(self, data):
+        """Load a snapshot into this handle (same config)."""
+        buf = C.create_string_buffer(bytes(data), len(data))
+        self._check(self._extra["restore"](self._h, buf, len(data)), "restore")
 
     def kernel_times(self):
         cap = 64

@@ -52,18 +52,20 @@ def test_struct_layout_matches_header(tmp_path):
     prog = tmp_path / "sz.c"
     prog.write_text(
         '#include <stdio.h>\n#include <stddef.h>\n#include "%s"\n'
-        'int main(){printf("%%zu %%zu %%zu %%zu %%zu %%zu %%zu %%zu %%zu\\n", sizeof(psim_config),'
+        'int main(){printf("%%zu %%zu %%zu %%zu %%zu %%zu %%zu %%zu %%zu %%zu %%zu\\n", sizeof(psim_config),'
         'sizeof(psim_round_stats), sizeof(psim_node_view), offsetof(psim_config, comm_id),'
         'offsetof(psim_node_view, have), offsetof(psim_round_stats, digest),'
         'sizeof(psim_strategy_view), offsetof(psim_config, fanout),'
-        'offsetof(psim_strategy_view, members_hash));return 0;}\n' % HDR)
+        'offsetof(psim_strategy_view, members_hash), sizeof(psim_histograms),'
+        'offsetof(psim_histograms, components));return 0;}\n' % HDR)
     exe = tmp_path / "sz"
     subprocess.check_call(["gcc", "-o", str(exe), str(prog)])
     got = [int(x) for x in subprocess.check_output([str(exe)]).split()]
     want = [C.sizeof(_abi.PsimConfig), C.sizeof(_abi.PsimRoundStats), C.sizeof(_abi.PsimNodeView),
             _abi.PsimConfig.comm_id.offset, _abi.PsimNodeView.have.offset,
             _abi.PsimRoundStats.digest.offset, C.sizeof(_abi.PsimStrategyView),
-            _abi.PsimConfig.fanout.offset, _abi.PsimStrategyView.members_hash.offset]
+            _abi.PsimConfig.fanout.offset, _abi.PsimStrategyView.members_hash.offset,
+            C.sizeof(_abi.PsimHistograms), _abi.PsimHistograms.components.offset]
     assert got == want
 
 

@@ -186,3 +186,39 @@ def test_route_regrow_parity(monkeypatch):
     (gs, gst), (os_, ost) = _both(S.doubling, 1024, 4, 40, bcast_period=10, bcast_first=15)
     S.compare_stats(gst, ost)
     S.compare_nodes(gs.nodes(), os_.nodes())
+
+
+def test_histograms_delivery_parity():
+    """psim_get_histograms / psim_get_delivery: the GPU's device kernels
+    (in-degree atomics, reverse-link test, label propagation) against the
+    oracle's list-style statistics on the same run."""
+    def run(make):
+        sim, _ = S.doubling(make, 2048, 3, 70, bcast_period=25, bcast_first=30)
+        sim.crash(np.arange(5, 2048, 61, dtype=np.uint32))
+        sim.step(2)
+        return sim
+    g, o = run(_gpu), run(Oracle)
+    hg, ho = g.histograms(), o.histograms()
+    for k in ho:
+        assert np.array_equal(np.asarray(hg[k]), np.asarray(ho[k])), k
+    for a, b in zip(g.delivery(), o.delivery()):
+        assert np.array_equal(a, b)
+    assert hg["components"] == 1
+
+
+def test_snapshot_restore_continues_identically():
+    """psim_snapshot after 60 rounds, restored into a fresh handle: the next
+    40 rounds (a broadcast included) are identical to the original's."""
+    from partisan_amd import Simulator
+    from partisan_amd.sim import default_config
+    sim, _ = S.doubling(_gpu, 4096, 2, 60)
+    snap = sim.snapshot()
+    sim.broadcast(0, 7)
+    a = sim.step(40)
+    other = Simulator(default_config(n_nodes=4096, seed=2))
+    other.restore(snap)
+    assert other.round == 60
+    other.broadcast(0, 7)
+    b = other.step(40)
+    S.compare_stats(a, b)
+    S.compare_nodes(sim.nodes(), other.nodes())
