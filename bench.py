@@ -16,6 +16,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+OVERLAY_DRAIN = 40               # untimed rounds before the overlay statistics
 HBM_PEAK_GBS = 8000.0           # MI355X HBM3E spec (MI355X_MICROARCH.md)
 S_NODE = 416                    # algorithmic state bytes per processed node
 S_MSG = 64                      # message record bytes
@@ -270,6 +271,26 @@ def main():
         got = (v["have"] >> ((state["k"] - 2) % 32)) & 1
         out["reliability_broadcast"] = {"msg": state["k"] - 2, "rounds": args.warmup + args.steps - 10 * (state["k"] - 2),
                                         "delivered_fraction": float(got[v["up"] == 1].mean())}
+    # overlay statistics (psim_get_histograms; outside the measurement, after
+    # OVERLAY_DRAIN more rounds without new broadcasts so the last one has
+    # settled): the tracked broadcast's reach and hop depth, active view
+    # symmetry and connectivity, mean in-degrees -- SURVEY 8(d)'s report
+    sim.step(OVERLAY_DRAIN)
+    ov = sim.histograms()
+    bins = np.arange(len(ov["hop"]))
+    nup = max(1, ov["n_up"])
+    out["overlay"] = {
+        "nodes_up": ov["n_up"],
+        "tracked_broadcast_reliability": ov["delivered"] / nup,
+        "tracked_broadcast_last_hop": int(bins[ov["hop"] > 0].max()) if ov["delivered"] else None,
+        "active_in_mean": float((ov["active_in"] * bins).sum() / nup),
+        "passive_in_mean": float((ov["passive_in"] * bins).sum() / nup),
+        "symmetric_active_links": (ov["symmetric_links"] / max(1, ov["active_links"])
+                                   if ov["symmetric_links"] != 2**64 - 1 else None),
+        "components": ov["components"] if ov["components"] != 2**64 - 1 else None,
+        "largest_component": ov["largest_component"] if ov["components"] != 2**64 - 1 else None,
+        "rounds_since_tracked_broadcast": OVERLAY_DRAIN + (args.warmup + args.steps - 1) % 10 + 1,
+    }
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.workload == "C":
         out["cpu_baseline"] = cpu_baseline(args)
     if rank == 0:
