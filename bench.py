@@ -53,6 +53,9 @@ def parse():
     p.add_argument("--cpu-sample-nodes", type=int, default=1 << 16)
     p.add_argument("--cpu-sample-rounds", type=int, default=40)
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--vshards", type=int, default=1,
+                   help="diagnostic: G virtual shards of --nodes each on this one GPU (the sharded "
+                        "partition / exchange / receive path with device copies instead of RCCL)")
     p.add_argument("--workload", default="C", choices=["C", "B", "D", "E"],
                    help="C (default, the headline line): HyParView+Plumtree; "
                         "B: full-membership strategy, fanout 5; D: SCAMP v2 (c=5); "
@@ -156,8 +159,9 @@ def main():
 
     # weak scaling: --nodes per GPU; the overlay spans all GPUs, node-range
     # sharded, one RCCL rank per GPU
-    n = args.nodes * world
+    n = args.nodes * world * args.vshards
     cfg = default_config(n_nodes=n, seed=args.seed)
+    cfg.n_shards = args.vshards
     cfg.device = int(os.environ.get("PSIM_DEVICE", os.environ.get("LOCAL_RANK", "0")))
     comm = None
     if world > 1:
@@ -234,9 +238,10 @@ def main():
     node_rounds = n * args.steps
     # roofline of the dominant kernel (consume): algorithmic bytes per launch
     # of this rank (global counters / world: the shards are equal ranges)
-    proc = int(st["nodes_processed"].sum()) / world
-    deliv = int(st["delivered"].sum()) / world
-    alg_bytes = proc * 2 * S_NODE + deliv * S_MSG + msgs / world * (S_MSG + 4)
+    per = world                                # this process's share (its launches: c_n)
+    proc = int(st["nodes_processed"].sum()) / per
+    deliv = int(st["delivered"].sum()) / per
+    alg_bytes = proc * 2 * S_NODE + deliv * S_MSG + msgs / per * (S_MSG + 4)
     c_ms, c_n = kt.get("consume", (0.0, 0))
     per_launch_bytes = alg_bytes / max(1, c_n)
     per_launch_s = (c_ms / 1e3) / max(1, c_n)
@@ -256,7 +261,8 @@ def main():
                                ("E: HyParView+Plumtree, 20% churn over 100 rounds (crash, restart, rejoin), "
                                 "half/half partition for rounds 20-39, broadcast every 10 rounds"),
                    "nodes": n, "nodes_per_gpu": args.nodes, "seed": args.seed,
-                   "parallelism": f"node-range sharded x{world}, RCCL all-to-all" if world > 1 else "1 GPU"},
+                   "parallelism": (f"node-range sharded x{world}, RCCL all-to-all" if world > 1 else
+                                   f"1 GPU, {args.vshards} virtual shards" if args.vshards > 1 else "1 GPU")},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(args.workload),
                      "kernel": "k_consume", "alg_bytes_per_launch": per_launch_bytes,

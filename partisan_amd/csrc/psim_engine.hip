@@ -276,6 +276,109 @@ __global__ void __launch_bounds__(RB_STEP) k_bucket_scatter(RouteIn in, uint32_t
         });
 }
 
+// G > 1, sender side: this shard's outbox runs stably partitioned by owner
+// shard (owner = dst / per) straight into the send buffer, so each owner's
+// records stay in (src, seq) order -- the receiver's route relies on it.
+// Two passes with the same block steps as the route:
+//   WRITE = false  per block and owner the record count -> hist[q * nblk + blk]
+//                  (hist[G * nblk] = 0: the scan's extra entry, the total)
+//   WRITE = true   after the scan, each record's 64 B to off[q * nblk + blk]
+//                  + its rank among the block's records of owner q
+// A wave walks its 64 nodes' records in slot order, 64 at a time; the rank
+// within a batch is a ballot over the lanes of the same owner, one ballot
+// per distinct owner in the batch (<= G).
+template <bool WRITE>
+__global__ void __launch_bounds__(RB_STEP) k_owner_part(RouteIn in, uint32_t nsteps, uint32_t G, uint32_t per,
+                                                        uint32_t* hist, const uint32_t* __restrict__ off,
+                                                        Msg* __restrict__ out) {
+    __shared__ uint32_t spre[4][65];
+    __shared__ uint64_t sbase[4][64];
+    __shared__ uint32_t wc[4][64];                    // per wave and owner: records in this step
+    __shared__ uint32_t run[64];                      // per owner: the block's next position
+    const uint32_t w = threadIdx.x >> 6, l = threadIdx.x & 63, nblk = gridDim.x;
+    if (threadIdx.x < 64) run[threadIdx.x] = (WRITE && threadIdx.x < G) ? off[threadIdx.x * nblk + blockIdx.x] : 0u;
+    if (!WRITE && blockIdx.x == 0 && threadIdx.x == 0) hist[G * nblk] = 0;
+    for (uint32_t step = blockIdx.x; step < nsteps; step += nblk) {
+        const uint32_t i = step * RB_STEP + threadIdx.x;
+        const uint32_t c = i < in.n_src ? in.ocnt[i] : 0u;
+        uint32_t inc = c;                             // inclusive prefix over the wave
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(inc, o);
+            if (l >= (uint32_t)o) inc += y;
+        }
+        __syncthreads();                              // the previous step's readers are done
+        spre[w][l + 1] = inc;
+        if (l == 0) spre[w][0] = 0;
+        sbase[w][l] = i < in.n_src ? in.obase[i] : 0ull;
+        const uint32_t T = __shfl(inc, 63);
+        __syncthreads();
+        const uint32_t* pre = spre[w];
+        // record t of the wave: its outbox slot and owner (none past T)
+        auto rec_at = [&](uint32_t t, uint64_t& g) -> uint32_t {
+            if (t >= T) return 0xFFFFFFFFu;
+            uint32_t a = 0, b = 64;
+            while (b - a > 1) {
+                const uint32_t mid = (a + b) >> 1;
+                if (pre[mid] <= t) a = mid; else b = mid;
+            }
+            g = sbase[w][a] + (t - pre[a]);
+            return (in.okey[g] & KEY_DST_MASK) / per;
+        };
+        uint32_t cnt = 0;                             // lane q: this wave's records of owner q
+        for (uint32_t t0 = 0; t0 < T; t0 += 64) {
+            uint64_t g = 0;
+            const uint32_t o = rec_at(t0 + l, g);
+            for (uint64_t todo = __ballot(o != 0xFFFFFFFFu); todo;) {
+                const uint32_t q = __builtin_amdgcn_readlane(o, __ffsll((long long)todo) - 1);
+                const uint64_t m = __ballot(o == q);
+                cnt += l == q ? (uint32_t)__popcll(m) : 0u;
+                todo &= ~m;
+            }
+        }
+        wc[w][l] = cnt;
+        __syncthreads();
+        if (WRITE) {
+            uint32_t B = 0;                           // lane q: where this wave's next owner-q record goes
+            if (l < G) {
+                B = run[l];
+                for (uint32_t v = 0; v < w; v++) B += wc[v][l];
+            }
+            for (uint32_t t0 = 0; t0 < T; t0 += 64) {
+                uint64_t g = 0;
+                const uint32_t o = rec_at(t0 + l, g);
+                uint32_t pos = 0;
+                for (uint64_t todo = __ballot(o != 0xFFFFFFFFu); todo;) {
+                    const uint32_t q = __builtin_amdgcn_readlane(o, __ffsll((long long)todo) - 1);
+                    const uint64_t m = __ballot(o == q);
+                    if (o == q) pos = __builtin_amdgcn_readlane(B, q) + (uint32_t)__popcll(m & ((1ull << l) - 1ull));
+                    B += l == q ? (uint32_t)__popcll(m) : 0u;
+                    todo &= ~m;
+                }
+                if (o != 0xFFFFFFFFu) {
+                    const uint4* sp = reinterpret_cast<const uint4*>(&in.rec[g]);
+                    uint4* dp = reinterpret_cast<uint4*>(&out[pos]);
+                    const uint4 x0 = sp[0], x1 = sp[1], x2 = sp[2], x3 = sp[3];
+                    dp[0] = x0; dp[1] = x1; dp[2] = x2; dp[3] = x3;
+                }
+            }
+        }
+        __syncthreads();
+        if (threadIdx.x < G) run[threadIdx.x] += wc[0][threadIdx.x] + wc[1][threadIdx.x] + wc[2][threadIdx.x] +
+                                                 wc[3][threadIdx.x];
+    }
+    if (!WRITE) {
+        __syncthreads();
+        if (threadIdx.x < G) hist[threadIdx.x * nblk + blockIdx.x] = run[threadIdx.x];
+    }
+}
+
+// each owner's first send-buffer position (G + 1 entries: the last is the total)
+__global__ void k_owner_offsets(const uint32_t* hoff, uint32_t nblk, uint32_t G, uint64_t* d_off) {
+    const uint32_t q = threadIdx.x;
+    if (q <= G) d_off[q] = hoff[q * nblk];
+}
+
+
 // One block per bucket of W destinations; LDS holds per destination the
 // count, bound sum, id mask and run start (4 x W words).
 __global__ void __launch_bounds__(RR_THREADS) k_bucket_route(
@@ -533,39 +636,6 @@ __global__ void k_desc(const uint64_t* __restrict__ packed, const uint64_t* __re
     desc[(uint32_t)P] = make_uint4(a.lo + li, in_beg[li], (uint32_t)cb[li] | (tf << 28), (uint32_t)(P >> 32));
 }
 
-// Dense (key, slot) pairs of this round's emissions, in node (= src, seq) order.
-__global__ void k_compact(const uint32_t* ocnt, const uint32_t* dpos, const uint64_t* obase,
-                          const uint32_t* okey, uint32_t* keys, uint32_t* vals, uint32_t n) {
-    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    uint32_t c = ocnt[i];
-    if (!c) return;
-    uint32_t p = dpos[i];
-    uint64_t b = obase[i];
-    for (uint32_t j = 0; j < c; j++) {
-        keys[p + j] = okey[b + j];
-        vals[p + j] = (uint32_t)(b + j);
-    }
-}
-
-// owner shard of each emitted message (G > 1)
-__global__ void k_owner(const uint32_t* keys, uint32_t* owner, uint32_t m, uint32_t per) {
-    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < m) owner[i] = (keys[i] & KEY_DST_MASK) / per;
-}
-
-// first index of each owner in the owner-sorted array (G + 1 entries)
-__global__ void k_owner_bounds(const uint32_t* owner, uint32_t m, uint32_t g, uint64_t* off) {
-    uint32_t t = threadIdx.x;
-    if (t > g) return;
-    uint32_t lo = 0, hi = m;
-    while (lo < hi) {
-        uint32_t mid = (lo + hi) >> 1;
-        if (owner[mid] < t) lo = mid + 1; else hi = mid;
-    }
-    off[t] = lo;
-}
-
 // records src[slots[i]] -> out[i] for i < *pm, grid-stride, 4 lanes x 16 B
 __global__ void k_gather_dev(const Msg* __restrict__ rec, const uint32_t* __restrict__ slots,
                              const uint32_t* __restrict__ pm, Msg* __restrict__ out, uint64_t cap) {
@@ -577,16 +647,6 @@ __global__ void k_gather_dev(const Msg* __restrict__ rec, const uint32_t* __rest
         const uint4* sp = reinterpret_cast<const uint4*>(&rec[slots[i]]);
         reinterpret_cast<uint4*>(&out[i])[t & 3] = sp[t & 3];
     }
-}
-
-// send buffer in owner order: 64-B records, 4 lanes x 16 B per record
-__global__ void k_gather(const Msg* __restrict__ rec, const uint32_t* __restrict__ slots, uint32_t m,
-                         Msg* __restrict__ out) {
-    uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    uint64_t i = t >> 2;
-    if (i >= m) return;
-    const uint4* s = reinterpret_cast<const uint4*>(&rec[slots[i]]);
-    reinterpret_cast<uint4*>(&out[i])[t & 3] = s[t & 3];
 }
 
 // one block per stats slot; lanes stride over the per-block partials.  The
@@ -793,7 +853,7 @@ struct Shard {
     DBuf<Msg> inbox[2];                 // records by node run, in inbox order: inbox[in_cur] is
     int in_cur = 0;                     // read by this round's consume, the other one is routed into
     // per-round scratch
-    DBuf<uint32_t> okey, ocnt, dpos, keys, vals, owner, owner_s, vals_s, in_beg,
+    DBuf<uint32_t> okey, ocnt, in_beg,
         d_nact, rank, long_list, n_long, tmp, bmask, hist, hoff;
     DBuf<uint2> pairs;                  // route: (destination in bucket | class, source index)
     DBuf<unsigned long long> cb;        // per local node: inbox count | bound sum << 32 (n + 1)
@@ -807,7 +867,7 @@ struct Shard {
     DBuf<uint32_t> sview, sinv, fbits, pay[2], pay_top;
     int pay_cur = 0;
     std::vector<uint64_t> soff, scnt;   // per destination shard (G + 1 offsets)
-    uint32_t m_out = 0, pgrid = 0, cgrid = 0;
+    uint32_t pgrid = 0, cgrid = 0;
     // pinned host words: NST stats and the consume span (stat_out), then the
     // outbox total and the routed record count: the round's two read-backs
     uint64_t* pin = nullptr;
@@ -917,17 +977,6 @@ int scan_excl(Shard* s, const T* in, T* out, uint32_t n) {
     HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, in, out, n, s->stream));
     TRY(s->cub_tmp.ensure(tb));
     HIP_TRY(hipcub::DeviceScan::ExclusiveSum(s->cub_tmp.p, tb, in, out, n, s->stream));
-    return PSIM_OK;
-}
-
-int sort_pairs(Shard* s, const uint32_t* kin, uint32_t* kout, const uint32_t* vin, uint32_t* vout,
-               uint32_t m, int bits) {
-    if (!m) return PSIM_OK;
-    size_t tb = 0;
-    HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, kin, kout, vin, vout, m, 0, bits, s->stream));
-    TRY(s->cub_tmp.ensure(tb));
-    HIP_TRY(hipcub::DeviceRadixSort::SortPairs(s->cub_tmp.p, tb, kin, kout, vin, vout, m, 0, bits,
-                                               s->stream));
     return PSIM_OK;
 }
 
@@ -1081,20 +1130,6 @@ int gather_inbox(psim_handle* h, Shard* s, const Msg* src, const uint32_t* dev_m
 }
 
 // dense emission list in (src, seq) order: keys = dst | bound, vals = slot
-int phase_compact(psim_handle* h, Shard* s) {
-    {
-        KTimer t(h, s, KT_SCAN);
-        TRY(scan_excl(s, s->ocnt.p, s->dpos.p, s->n));
-        s->m_out = read1(s, s->ocnt.p + (s->n - 1)) + read1(s, s->dpos.p + (s->n - 1));
-    }
-    TRY(s->keys.ensure(s->m_out + 1));
-    TRY(s->vals.ensure(s->m_out + 1));
-    KTimer t(h, s, KT_COMPACT);
-    k_compact<<<grid_for(s->n), BLK, 0, s->stream>>>(s->ocnt.p, s->dpos.p, s->obase.p, s->okey.p,
-                                                     s->keys.p, s->vals.p, s->n);
-    return PSIM_OK;
-}
-
 // The route (section comment above the kernels) over this shard's outbox
 // runs (dense == nullptr) or the m records of `dense`; leaves cb, bmask,
 // in_beg[0..n] (in_beg[n] = the record count) and the sorted runs of
@@ -1153,29 +1188,32 @@ int phase_route_local(psim_handle* h, Shard* s) {
                         (uint32_t)std::min<uint64_t>(s->pin[PIN_TOTAL], s->rcap));
 }
 
-// G > 1, sender side: stable partition by owner shard, records gathered
-// into the send buffer in that order; per-owner counts/offsets on the host
+// G > 1, sender side: the outbox partitioned by owner shard into the send
+// buffer (k_owner_part); per-owner counts/offsets on the host
 int phase_partition(psim_handle* h, Shard* s) {
-    TRY(phase_compact(h, s));
-    const uint32_t m = s->m_out;
-    TRY(s->owner.ensure(m + 1)); TRY(s->owner_s.ensure(m + 1)); TRY(s->vals_s.ensure(m + 1));
-    TRY(s->sendbuf.ensure(m + 1));
-    TRY(s->d_off.ensure(h->G + 1));
-    KTimer t(h, s, KT_SORT);
-    s->soff.assign(h->G + 1, 0);
-    if (m) {
-        k_owner<<<grid_for(m), BLK, 0, s->stream>>>(s->keys.p, s->owner.p, m, h->per);
-        TRY(sort_pairs(s, s->owner.p, s->owner_s.p, s->vals.p, s->vals_s.p, m, bits_for(h->G)));
-        k_gather<<<grid_for((uint64_t)m * 4), BLK, 0, s->stream>>>(s->outbox.p, s->vals_s.p, m,
-                                                                    s->sendbuf.p);
-        k_owner_bounds<<<1, 128, 0, s->stream>>>(s->owner_s.p, m, h->G, s->d_off.p);
-        HIP_TRY(hipMemcpyAsync(s->soff.data(), s->d_off.p, (h->G + 1) * 8, hipMemcpyDeviceToHost,
-                               s->stream));
+    const uint32_t G = h->G;
+    const RouteIn in{s->outbox.p, s->okey.p, s->obase.p, s->ocnt.p, s->n, 0, 0};
+    const uint32_t nsteps = std::max<uint32_t>(1, (s->n + RB_STEP - 1) / RB_STEP);
+    const uint32_t nblk = std::min<uint32_t>(nsteps, RB_MAX_BLOCKS);
+    const size_t nh = (size_t)G * nblk + 1;
+    TRY(s->hist.ensure(nh));
+    TRY(s->hoff.ensure(nh));
+    TRY(s->sendbuf.ensure(s->pin[PIN_TOTAL] + 1, 2));   // the outbox bound bounds the records
+    TRY(s->d_off.ensure(G + 1));
+    s->soff.assign(G + 1, 0);
+    {
+        KTimer t(h, s, KT_SORT);
+        k_owner_part<false><<<nblk, RB_STEP, 0, s->stream>>>(in, nsteps, G, h->per, s->hist.p, nullptr, nullptr);
+        TRY(scan_excl(s, s->hist.p, s->hoff.p, (uint32_t)nh));
+        k_owner_part<true><<<nblk, RB_STEP, 0, s->stream>>>(in, nsteps, G, h->per, nullptr, s->hoff.p,
+                                                             s->sendbuf.p);
+        k_owner_offsets<<<1, 128, 0, s->stream>>>(s->hoff.p, nblk, G, s->d_off.p);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipMemcpyAsync(s->soff.data(), s->d_off.p, (G + 1) * 8, hipMemcpyDeviceToHost, s->stream));
         TRY(stream_wait(s));
     }
-    s->soff[h->G] = m;
-    s->scnt.resize(h->G);
-    for (uint32_t g = 0; g < h->G; g++) s->scnt[g] = s->soff[g + 1] - s->soff[g];
+    s->scnt.resize(G);
+    for (uint32_t g = 0; g < G; g++) s->scnt[g] = s->soff[g + 1] - s->soff[g];
     return PSIM_OK;
 }
 
@@ -1358,7 +1396,7 @@ int shard_alloc(psim_handle* h, Shard* s) {
     rc |= s->pt_all.alloc(n * PSIM_PT_MEMBERS_CAP); rc |= s->pt_com.alloc(n * PSIM_PT_MEMBERS_CAP);
     rc |= s->pt_eag.alloc(n * PSIM_PT_SET_CAP); rc |= s->pt_laz.alloc(n * PSIM_PT_SET_CAP);
     rc |= s->pt_out.alloc(n * PSIM_PT_OUT_CAP); rc |= s->start.alloc(n);
-    rc |= s->ocnt.alloc(n); rc |= s->dpos.alloc(n); rc |= s->cb.alloc(n + 1);
+    rc |= s->ocnt.alloc(n); rc |= s->cb.alloc(n + 1);
     rc |= s->in_beg.alloc(n + 1); rc |= s->bound.alloc(n + 1); rc |= s->pscan.alloc(n + 1); rc |= s->obase.alloc(n + 1);
     rc |= s->long_list.alloc(n); rc |= s->bmask.alloc(n); rc |= s->btot.alloc(1); rc |= s->n_long.alloc(1);
     rc |= s->desc.alloc(n); rc |= s->d_nact.alloc(1);
@@ -1393,9 +1431,8 @@ void shard_free(Shard* s) {
     if (s->wait_ev) (void)hipEventDestroy(s->wait_ev);
     s->wait_ev = nullptr;
     s->pin = nullptr;
-    s->outbox.release(); s->okey.release(); s->ocnt.release(); s->dpos.release();
-    s->keys.release(); s->vals.release(); s->owner.release(); s->owner_s.release();
-    s->vals_s.release(); s->cb.release(); s->in_beg.release();
+    s->outbox.release(); s->okey.release(); s->ocnt.release();
+    s->cb.release(); s->in_beg.release();
     s->rank.release(); s->long_list.release(); s->bmask.release(); s->btot.release();
     s->hist.release(); s->hoff.release(); s->pairs.release(); s->n_long.release(); s->tmp.release();
     s->desc.release(); s->d_nact.release(); s->bound.release(); s->pscan.release();
