@@ -77,6 +77,21 @@ def test_64k_parity():
     S.compare_nodes(gs.nodes(), os_.nodes())
 
 
+def test_config_c_1m_parity():
+    """Config C at its full size (BASELINE.json configs[2]): 2^20 nodes, the
+    bench's doubling bootstrap, 20 settle rounds, then a broadcast from node 0
+    and 20 rounds more -- every round's statistics and digest and every
+    node's final state bit-identical to the oracle (~40 s of oracle time)."""
+    def run(make):
+        sim, st = S.doubling(make, 1 << 20, 1, 41)
+        sim.broadcast(0, 0)
+        return sim, np.concatenate([st, sim.step(20)])
+    (gs, gst), (os_, ost) = _both(run)
+    S.compare_stats(gst, ost)
+    S.compare_nodes(gs.nodes(), os_.nodes())
+    assert int(gst["first_deliveries"].sum()) > 0
+
+
 def test_large_properties():
     """2^18 nodes: size-independent properties (the oracle is not run):
     view bounds, broadcast reliability, message conservation (every message
