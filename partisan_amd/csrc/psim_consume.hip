@@ -1093,6 +1093,169 @@ __global__ void __launch_bounds__(256, PSIM_WAVES_PER_SIMD) k_consume(RoundArgs 
     if (threadIdx.x == 0) atomicMax(&args.ktime[1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
 }
 
+// ------------------------------------------------ relays and lazy ticks --
+// Most nodes with work in a steady-state round do little: relay the one
+// SHUFFLE of their inbox (hv:1095-1136 with TTL > 0 and |active| > 1: a
+// select_random over active -- [Sender, Myself], then do_send_message)
+// and/or run the lazy tick over outstanding entries (pt:341-345, :443-453:
+// an IHAVE per entry, sent only over a live active connection).  Such a
+// node needs no wave: k_relay gives it one lane, reading its header, active
+// row, outstanding row and the record, and writing the emitted records, its
+// draw counter, outbox count and flag byte exactly as k_consume's body and
+// writeback would (no other inbox message, no timer of HyParView due, no
+// join, no crash round, not the origin).  Every other node with work is
+// appended to desc_slow for k_consume; the order of that list does not
+// matter (each node writes its own rows and outbox region; the stats and the
+// digest are sums).
+DEV uint64_t relay_emit(const RoundArgs& a, uint64_t slot, uint32_t dst, uint32_t me, uint32_t tt, uint32_t seq,
+                        uint32_t a0, uint32_t a1, uint32_t a2, const uint32_t (&X)[8]) {
+    const uint32_t W[16] = {dst, me, tt, seq, a0, a1, a2, 0u, X[0], X[1], X[2], X[3], X[4], X[5], X[6], X[7]};
+    uint64_t dg = 0;
+#pragma unroll
+    for (int j = 0; j < 16; j++) dg += (uint64_t)W[j] * digest_mul(j);
+    uint4* o = reinterpret_cast<uint4*>(a.rec_out + slot);
+    o[0] = make_uint4(dst, me, tt, seq);
+    o[1] = make_uint4(a0, a1, a2, 0u);
+    o[2] = make_uint4(X[0], X[1], X[2], X[3]);
+    o[3] = make_uint4(X[4], X[5], X[6], X[7]);
+    a.okey[slot] = dst | (max_emit(tt & 0xFF) << KEY_DST_BITS);
+    return dg;
+}
+
+__global__ void __launch_bounds__(256) k_relay(RoundArgs a) {
+    enum { R_PROC, R_DELIV, R_SHUF, R_IHAVE, R_FAIL, R_DIGEST, R_N };
+    __shared__ unsigned long long sst[R_N];
+    if (threadIdx.x < R_N) sst[threadIdx.x] = 0;
+    if (threadIdx.x == 0) atomicMin(&a.ktime[0], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+    __syncthreads();
+    const uint32_t l = lane_id();
+    const uint32_t na = *a.n_alist;
+    const uint64_t two58 = 1ull << 58;
+    unsigned long long v[R_N] = {0, 0, 0, 0, 0, 0};
+    for (uint32_t base = blockIdx.x * blockDim.x; base < na; base += gridDim.x * blockDim.x) {
+        const uint32_t P = base + threadIdx.x;
+        uint4 D = make_uint4(0, 0, 0, 0);
+        bool fast = false;
+        Hdr h;
+        uint32_t ik = 0, ttl = 0, nex = 0, src = 0;
+        bool lazy = false;
+        const Msg* rp = nullptr;
+        if (P < na) {
+            D = a.desc[P];
+            const uint32_t id = D.x, tf = D.z >> 28;
+            ik = D.z & DESC_CNT_MASK;
+            fast = ik <= 1 && !(tf & DESC_SHUFFLE) && !a.crash_round &&
+                   !(a.origin_now && a.plumtree && a.origin_node == id);
+            if (fast) {
+                h = a.hdr[id - a.lo];
+                lazy = (tf & DESC_LAZY) && h.out_n > 0;
+                fast = h.start_round != a.round && (!(tf & DESC_PROMO) || h.act_n >= a.min_active);
+                if (ik) {
+                    rp = a.rec_in + D.y;
+                    const uint32_t tt = rp->tt;
+                    ttl = (tt >> 8) & 0xFF;
+                    nex = (tt >> 16) & 0xFF;
+                    src = rp->src;
+                    fast = fast && h.act_n > 1 && (tt & 0xFF) == PSIM_MSG_SHUFFLE && ttl > 0;
+                }
+            }
+        }
+        const bool slow = P < na && !fast;
+        const uint64_t m = ballot(slow);
+        if (m) {
+            const int lead = ffs64(m);
+            uint32_t b0 = 0;
+            if (l == (uint32_t)lead) b0 = atomicAdd(a.n_slow, popc(m));
+            b0 = shfl(b0, lead);
+            if (slow) a.desc_slow[b0 + popc(m & lt_mask())] = D;
+        }
+        if (!fast) continue;
+        const uint32_t id = D.x;
+        const size_t li = id - a.lo;
+        const uint4* ar = reinterpret_cast<const uint4*>(a.act + li * PSIM_ACTIVE_CAP);
+        const uint4 a0 = ar[0], a1 = ar[1];
+        const uint32_t A[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+        const uint32_t me_part = a.part[id];
+        uint64_t rng = h.rng;
+        uint32_t seq = 0;
+        v[R_PROC]++;
+        if (ik) {
+            v[R_DELIV]++;
+            // select_random(Active, [Sender, Myself]) (hv:1346-1356)
+            uint32_t elig = 0;
+#pragma unroll
+            for (int j = 0; j < 8; j++) elig |= (j < h.act_n && A[j] != src && A[j] != id) ? (1u << j) : 0u;
+            const uint32_t cnt = __popc(elig);
+            if (cnt) {
+                uint32_t k;
+                for (;;) {                                // rand:uniform(cnt) - 1 (?uniform_range)
+                    const uint64_t x = draw58_at(rng++, id, a.seed);
+                    if (x < cnt) { k = (uint32_t)x; break; }
+                    const uint32_t i = mod_small(x, cnt);
+                    if (x - i <= two58 - cnt) { k = i; break; }
+                }
+                uint32_t e = elig;
+                for (uint32_t j = 0; j < k; j++) e &= e - 1;
+                const uint32_t r = A[__ffs(e) - 1];
+                // do_send_message: maybe_connect + find, then the dispatch draw
+                if (r < a.n_nodes && (a.flags[r] & F_UP) && a.part[r] == me_part) {
+                    rng++;
+                    const uint4* ex = reinterpret_cast<const uint4*>(rp->ex);
+                    const uint4 e0 = ex[0], e1 = ex[1];
+                    uint32_t X[8] = {e0.x, e0.y, e0.z, e0.w, e1.x, e1.y, e1.z, e1.w};
+#pragma unroll
+                    for (int j = 0; j < 8; j++) X[j] = (uint32_t)j < nex ? X[j] : 0u;
+                    v[R_DIGEST] += relay_emit(a, D.w, r, id, PSIM_MSG_SHUFFLE | ((ttl - 1) << 8) | (nex << 16), seq,
+                                              0u, 0u, 0u, X);
+                    seq++;
+                    v[R_SHUF]++;
+                } else {
+                    v[R_FAIL]++;
+                }
+            }
+        }
+        if (lazy) {                                   // send_lazy: every outstanding entry, in order
+            const uint32_t X[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+            const uint64_t* orow = a.pt_out + li * PSIM_PT_OUT_CAP;
+            for (uint32_t i = 0; i < h.out_n; i++) {
+                const uint64_t o = orow[i];
+                const uint32_t p = (uint32_t)(o >> 32) & ~PSIM_MAP_BIT;
+                bool ok = p != id && p < a.n_nodes;   // send/3: an existing connection
+                if (ok) {
+                    bool in = false;
+#pragma unroll
+                    for (int j = 0; j < 8; j++) in |= j < h.act_n && A[j] == p;
+                    ok = in && (a.flags[p] & F_UP) && a.part[p] == me_part;
+                }
+                if (!ok) { v[R_FAIL]++; continue; }
+                v[R_DIGEST] += relay_emit(a, D.w + seq, p, id, PSIM_MSG_PT_IHAVE, seq, (uint32_t)(o >> 16) & 0xFFFFu,
+                                          (uint32_t)o & 0xFFFFu, a.bcast_root, X);
+                seq++;
+                v[R_IHAVE]++;
+            }
+        }
+        if (rng != h.rng) a.hdr[li].rng = rng;
+        a.ocnt[li] = seq;
+        const uint8_t fl = a.flags[id];
+        a.flags[id] = (uint8_t)((fl & (F_UP | F_CRASHED)) | (h.out_n ? F_LAZY : 0) |
+                                (min((uint32_t)h.out_n, 15u) << F_OUTN_SHIFT) |
+                                (h.act_n < a.min_active ? F_LOWACT : 0));
+    }
+    // wave sums, then one LDS atomic per wave and counter
+#pragma unroll
+    for (int k = 0; k < R_N; k++)
+        for (int o = 32; o > 0; o >>= 1) v[k] += __shfl_xor(v[k], o);
+    if (l == 0)
+        for (int k = 0; k < R_N; k++)
+            if (v[k]) atomicAdd(&sst[k], v[k]);
+    __syncthreads();
+    uint64_t* row = a.stat_relay + (size_t)blockIdx.x * NST;
+    for (uint32_t k = threadIdx.x; k < NST; k += blockDim.x)
+        row[k] = k == ST_PROC ? sst[R_PROC] : k == ST_DELIV + PSIM_MSG_SHUFFLE ? sst[R_DELIV]
+               : k == ST_EMIT + PSIM_MSG_SHUFFLE ? sst[R_SHUF] : k == ST_EMIT + PSIM_MSG_PT_IHAVE ? sst[R_IHAVE]
+               : k == ST_FAIL ? sst[R_FAIL] : k == ST_DIGEST ? sst[R_DIGEST] : 0ull;
+}
+
 // one wave-slot per resident wave: the grid strides over the active list
 // with no second generation of waves (a partial generation is a tail)
 uint32_t consume_grid() {

@@ -536,7 +536,7 @@ __global__ void __launch_bounds__(256) k_node_prep(RoundArgs a, const uint32_t* 
                                                    uint64_t* part, uint32_t* ocnt, unsigned long long* btot) {
     __shared__ unsigned long long s_up, s_drop, s_b;
     if (threadIdx.x == 0) { s_up = 0; s_drop = 0; s_b = 0; }
-    if (blockIdx.x == 0 && threadIdx.x == 0) { a.ktime[0] = ~0ull; a.ktime[1] = 0; }
+    if (blockIdx.x == 0 && threadIdx.x == 0) { a.ktime[0] = ~0ull; a.ktime[1] = 0; *a.n_slow = 0; }
     __syncthreads();
     unsigned long long up = 0, drop = 0, bs = 0;        // this thread's sums (wave-summed below)
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < a.n_local; i += gridDim.x * blockDim.x) {
@@ -854,11 +854,11 @@ struct Shard {
     int in_cur = 0;                     // read by this round's consume, the other one is routed into
     // per-round scratch
     DBuf<uint32_t> okey, ocnt, in_beg,
-        d_nact, rank, long_list, n_long, tmp, bmask, hist, hoff;
+        d_nact, n_slow, rank, long_list, n_long, tmp, bmask, hist, hoff;
     DBuf<uint2> pairs;                  // route: (destination in bucket | class, source index)
     DBuf<unsigned long long> cb;        // per local node: inbox count | bound sum << 32 (n + 1)
     DBuf<unsigned long long> btot;      // this round's outbox total (k_node_prep)
-    DBuf<uint4> desc;
+    DBuf<uint4> desc, desc_slow;            // work descriptors; those k_relay leaves to k_consume
     DBuf<uint64_t> bound, pscan, obase, stat_part, stat_out, d_off;   // bound: packed (bound << 32 | work)
     DBuf<uint8_t> cub_tmp;
     DBuf<uint32_t> ev_ids, ev_contacts;
@@ -867,7 +867,7 @@ struct Shard {
     DBuf<uint32_t> sview, sinv, fbits, pay[2], pay_top;
     int pay_cur = 0;
     std::vector<uint64_t> soff, scnt;   // per destination shard (G + 1 offsets)
-    uint32_t pgrid = 0, cgrid = 0;
+    uint32_t pgrid = 0, cgrid = 0, rgrid = 0;   // stats rows: prepare, consume, relay blocks
     // pinned host words: NST stats and the consume span (stat_out), then the
     // outbox total and the routed record count: the round's two read-backs
     uint64_t* pin = nullptr;
@@ -911,6 +911,7 @@ struct psim_handle {
     // ~10 us bubble between kernels, so by default only k_consume is timed,
     // from its in-kernel span (RoundArgs::ktime)
     bool phase_timers = false;
+    bool relay = true;                  // k_relay ahead of k_consume (PSIM_NO_RELAY=1: off)
 };
 
 namespace {
@@ -940,6 +941,7 @@ RoundArgs make_args(psim_handle* h, Shard* s) {
     a.fanout = c.fanout; a.fw = h->fw;
     a.fbits = s->fbits.p; a.sview = s->sview.p; a.sinv = s->sinv.p;
     a.ktime = reinterpret_cast<unsigned long long*>(s->stat_out.p + NST);
+    a.desc_slow = s->desc_slow.p; a.n_slow = s->n_slow.p;
     return a;
 }
 
@@ -1048,7 +1050,8 @@ int phase_events_prepare(psim_handle* h, Shard* s, const RoundCtl& ctl, RoundArg
         a.in_cb = s->cb.p;
         s->pgrid = std::min<uint32_t>(grid_for(n), 512);   // grid-stride: few partials
         s->cgrid = std::min<uint32_t>(grid_for(n), h->consume_blocks);
-        TRY(s->stat_part.ensure((size_t)(s->pgrid + s->cgrid) * NST));
+        s->rgrid = h->relay && h->cfg.manager != PSIM_MANAGER_PLUGGABLE ? RELAY_BLOCKS : 0;
+        TRY(s->stat_part.ensure((size_t)(s->pgrid + s->cgrid + s->rgrid) * NST));
         k_node_prep<<<s->pgrid, BLK, 0, s->stream>>>(a, s->bmask.p, s->bound.p, s->stat_part.p, s->ocnt.p,
                                                      s->btot.p);
         // bound[n] = 0: pscan[n] = (outbox total << 32) | active count;
@@ -1095,6 +1098,7 @@ int phase_events_prepare(psim_handle* h, Shard* s, const RoundCtl& ctl, RoundArg
     a.rec_out = s->outbox.p;
     a.okey = s->okey.p; a.ocnt = s->ocnt.p;
     a.stat_part = s->stat_part.p + (size_t)s->pgrid * NST;
+    a.stat_relay = s->stat_part.p + (size_t)(s->pgrid + s->cgrid) * NST;
     return PSIM_OK;
 }
 
@@ -1110,8 +1114,18 @@ int phase_consume(psim_handle* h, Shard* s, RoundArgs& a) {
         a.pay_cap = (uint32_t)(s->pay[s->pay_cur].n / h->fw);
         HIP_TRY(hipMemsetAsync(s->pay_top.p, 0, 4, s->stream));
     }
-    if (a.pl) k_consume_pl<<<s->cgrid, BLK, 0, s->stream>>>(a);
-    else k_consume<<<s->cgrid, BLK, 0, s->stream>>>(a);
+    if (a.pl) {
+        k_consume_pl<<<s->cgrid, BLK, 0, s->stream>>>(a);
+    } else if (s->rgrid) {
+        // SHUFFLE relays one lane each, every other node one wave
+        k_relay<<<s->rgrid, BLK, 0, s->stream>>>(a);
+        RoundArgs b = a;
+        b.desc = s->desc_slow.p;
+        b.n_alist = s->n_slow.p;
+        k_consume<<<s->cgrid, BLK, 0, s->stream>>>(b);
+    } else {
+        k_consume<<<s->cgrid, BLK, 0, s->stream>>>(a);
+    }
     HIP_TRY(hipGetLastError());
     s->pay_cur ^= 1;
     return PSIM_OK;
@@ -1289,7 +1303,8 @@ int exchange_rccl(psim_handle* h) {
 
 int phase_stats(psim_handle* h, Shard* s, const std::vector<uint32_t>& crashed) {
     KTimer t(h, s, KT_STATS);
-    k_stats_reduce<<<NST, BLK, 0, s->stream>>>(s->stat_part.p, s->pgrid + s->cgrid, s->stat_out.p, s->pin_dev);
+    k_stats_reduce<<<NST, BLK, 0, s->stream>>>(s->stat_part.p, s->pgrid + s->cgrid + s->rgrid, s->stat_out.p,
+                                                s->pin_dev);
     if (!crashed.empty()) {
         TRY(upload(s, s->ev_ids, crashed));
         k_uncrash<<<grid_for(crashed.size()), BLK, 0, s->stream>>>(s->flags.p, s->ev_ids.p,
@@ -1341,6 +1356,10 @@ int run_round(psim_handle* h, uint64_t* st) {
             TRY(stream_wait(s));
         }
         if (h->G == 1) s->m_in = (uint32_t)s->pin[PIN_M];   // routed this round
+        static const bool trace_relay = getenv("PSIM_TRACE_RELAY") != nullptr;
+        if (trace_relay && s->rgrid)
+            std::fprintf(stderr, "psim: round %llu shard %u: %u nodes with work, %u to k_consume\n",
+                         (unsigned long long)h->round, s->idx, read1(s, s->d_nact.p), read1(s, s->n_slow.p));
         if (s->pin[NST] != ~0ull && s->pin[NST + 1] > s->pin[NST]) {   // 100 MHz ticks
             h->kt_ms[KT_CONSUME] += (double)(s->pin[NST + 1] - s->pin[NST]) * 1e-5;
             h->kt_n[KT_CONSUME]++;
@@ -1400,6 +1419,7 @@ int shard_alloc(psim_handle* h, Shard* s) {
     rc |= s->in_beg.alloc(n + 1); rc |= s->bound.alloc(n + 1); rc |= s->pscan.alloc(n + 1); rc |= s->obase.alloc(n + 1);
     rc |= s->long_list.alloc(n); rc |= s->bmask.alloc(n); rc |= s->btot.alloc(1); rc |= s->n_long.alloc(1);
     rc |= s->desc.alloc(n); rc |= s->d_nact.alloc(1);
+    rc |= s->desc_slow.alloc(n); rc |= s->n_slow.alloc(1);
     rc |= s->stat_out.alloc(NST + 2);   // + the consume span
     rc |= s->ikeys.alloc(1024); rc |= s->ivals.alloc(1024);
     rc |= s->recvbuf.alloc(1024); rc |= s->inbox[0].alloc(1024); rc |= s->inbox[1].alloc(1024); rc |= s->outbox.alloc(1024);
@@ -1435,7 +1455,7 @@ void shard_free(Shard* s) {
     s->cb.release(); s->in_beg.release();
     s->rank.release(); s->long_list.release(); s->bmask.release(); s->btot.release();
     s->hist.release(); s->hoff.release(); s->pairs.release(); s->n_long.release(); s->tmp.release();
-    s->desc.release(); s->d_nact.release(); s->bound.release(); s->pscan.release();
+    s->desc.release(); s->d_nact.release(); s->desc_slow.release(); s->n_slow.release(); s->bound.release(); s->pscan.release();
     s->obase.release(); s->stat_part.release(); s->stat_out.release(); s->d_off.release();
     s->cub_tmp.release(); s->ev_ids.release(); s->ev_contacts.release(); s->sendbuf.release();
     s->sview.release(); s->sinv.release(); s->fbits.release(); s->pay[0].release(); s->pay[1].release();
@@ -1521,6 +1541,8 @@ int psim_create(const psim_config* cfg, psim_handle** out) {
     {
         const char* e = getenv("PSIM_PHASE_TIMERS");
         h->phase_timers = e && *e && *e != '0';
+        const char* r = getenv("PSIM_NO_RELAY");
+        h->relay = !(r && *r && *r != '0');
     }
     h->device = dev;
     for (uint32_t g = 0; g < G; g++) {

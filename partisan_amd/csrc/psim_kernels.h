@@ -27,6 +27,11 @@ struct RoundArgs {
     const uint32_t* start;      // start round per node (timer phases)
     const uint4* desc;          // per node with work: (id, inbox begin, inbox count, outbox base)
     const uint32_t* n_alist;
+    // k_relay: the nodes it leaves to k_consume (desc_slow[0..*n_slow)), its
+    // per-block stats rows
+    uint4* desc_slow;
+    uint32_t* n_slow;
+    uint64_t* stat_relay;
     const Msg* rec_in;          // dense, in inbox order (node runs at in_beg)
     const uint64_t* obase;
     Msg* rec_out;
@@ -51,6 +56,9 @@ struct RoundArgs {
 };
 
 __global__ void k_consume(RoundArgs args);
+// lane-per-node SHUFFLE relays ahead of k_consume (psim_consume.hip)
+constexpr uint32_t RELAY_BLOCKS = 512;
+__global__ void k_relay(RoundArgs args);
 __global__ void k_consume_pl(RoundArgs args);
 // diagnostic builds (-DPSIM_STAMPS): per-phase cycle sums of k_consume, reset on read
 int debug_stamps(unsigned long long* out);
