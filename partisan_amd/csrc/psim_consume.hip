@@ -1125,6 +1125,7 @@ DEV uint64_t relay_emit(const RoundArgs& a, uint64_t slot, uint32_t dst, uint32_
 __global__ void __launch_bounds__(256) k_relay(RoundArgs a) {
     enum { R_PROC, R_DELIV, R_SHUF, R_IHAVE, R_FAIL, R_DIGEST, R_N };
     __shared__ unsigned long long sst[R_N];
+    __shared__ uint32_t wcnt[5];                      // per wave slow counts, then the block's base
     if (threadIdx.x < R_N) sst[threadIdx.x] = 0;
     if (threadIdx.x == 0) atomicMin(&a.ktime[0], (unsigned long long)__builtin_amdgcn_s_memrealtime());
     __syncthreads();
@@ -1160,14 +1161,24 @@ __global__ void __launch_bounds__(256) k_relay(RoundArgs a) {
                 }
             }
         }
+        // the slow entries of this block step: wave counts, a block scan in
+        // LDS, one global atomic per block step (a same-address atomic per
+        // wave serialised at L2 and cost ~100 us per round)
         const bool slow = P < na && !fast;
         const uint64_t m = ballot(slow);
-        if (m) {
-            const int lead = ffs64(m);
-            uint32_t b0 = 0;
-            if (l == (uint32_t)lead) b0 = atomicAdd(a.n_slow, popc(m));
-            b0 = shfl(b0, lead);
-            if (slow) a.desc_slow[b0 + popc(m & lt_mask())] = D;
+        const uint32_t wv = threadIdx.x >> 6;
+        __syncthreads();                              // the previous step's readers of wcnt are done
+        if (l == 0) wcnt[wv] = popc(m);
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const uint32_t t = wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
+            wcnt[4] = t ? atomicAdd(a.n_slow, t) : 0u;
+        }
+        __syncthreads();
+        if (slow) {
+            uint32_t b0 = wcnt[4];
+            for (uint32_t k = 0; k < wv; k++) b0 += wcnt[k];
+            a.desc_slow[b0 + popc(m & lt_mask())] = D;
         }
         if (!fast) continue;
         const uint32_t id = D.x;
@@ -1216,22 +1227,33 @@ __global__ void __launch_bounds__(256) k_relay(RoundArgs a) {
         }
         if (lazy) {                                   // send_lazy: every outstanding entry, in order
             const uint32_t X[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-            const uint64_t* orow = a.pt_out + li * PSIM_PT_OUT_CAP;
-            for (uint32_t i = 0; i < h.out_n; i++) {
-                const uint64_t o = orow[i];
-                const uint32_t p = (uint32_t)(o >> 32) & ~PSIM_MAP_BIT;
-                bool ok = p != id && p < a.n_nodes;   // send/3: an existing connection
-                if (ok) {
-                    bool in = false;
+            // the row in chunks of 4 entries (two 16-B loads in flight at once)
+            const uint4* orow = reinterpret_cast<const uint4*>(a.pt_out + li * PSIM_PT_OUT_CAP);
+            for (uint32_t i0 = 0; i0 < h.out_n; i0 += 4) {
+                const uint4 q0 = orow[i0 >> 1], q1 = orow[(i0 >> 1) + 1];
+                const uint64_t O[4] = {((uint64_t)q0.y << 32) | q0.x, ((uint64_t)q0.w << 32) | q0.z,
+                                       ((uint64_t)q1.y << 32) | q1.x, ((uint64_t)q1.w << 32) | q1.z};
+                bool in[4];
 #pragma unroll
-                    for (int j = 0; j < 8; j++) in |= j < h.act_n && A[j] == p;
-                    ok = in && (a.flags[p] & F_UP) && a.part[p] == me_part;
+                for (int c = 0; c < 4; c++) {         // send/3: an existing connection (member of Active)
+                    const uint32_t p = (uint32_t)(O[c] >> 32) & ~PSIM_MAP_BIT;
+                    bool x = false;
+#pragma unroll
+                    for (int j = 0; j < 8; j++) x |= j < h.act_n && A[j] == p;
+                    in[c] = x && p != id && i0 + c < h.out_n;
                 }
-                if (!ok) { v[R_FAIL]++; continue; }
-                v[R_DIGEST] += relay_emit(a, D.w + seq, p, id, PSIM_MSG_PT_IHAVE, seq, (uint32_t)(o >> 16) & 0xFFFFu,
-                                          (uint32_t)o & 0xFFFFu, a.bcast_root, X);
-                seq++;
-                v[R_IHAVE]++;
+                for (int c = 0; c < 4 && i0 + c < h.out_n; c++) {
+                    const uint64_t o = O[c];
+                    const uint32_t p = (uint32_t)(o >> 32) & ~PSIM_MAP_BIT;
+                    if (!(in[c] && p < a.n_nodes && (a.flags[p] & F_UP) && a.part[p] == me_part)) {
+                        v[R_FAIL]++;
+                        continue;
+                    }
+                    v[R_DIGEST] += relay_emit(a, D.w + seq, p, id, PSIM_MSG_PT_IHAVE, seq,
+                                              (uint32_t)(o >> 16) & 0xFFFFu, (uint32_t)o & 0xFFFFu, a.bcast_root, X);
+                    seq++;
+                    v[R_IHAVE]++;
+                }
             }
         }
         if (rng != h.rng) a.hdr[li].rng = rng;

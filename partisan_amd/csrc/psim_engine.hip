@@ -1050,7 +1050,9 @@ int phase_events_prepare(psim_handle* h, Shard* s, const RoundCtl& ctl, RoundArg
         a.in_cb = s->cb.p;
         s->pgrid = std::min<uint32_t>(grid_for(n), 512);   // grid-stride: few partials
         s->cgrid = std::min<uint32_t>(grid_for(n), h->consume_blocks);
-        s->rgrid = h->relay && h->cfg.manager != PSIM_MANAGER_PLUGGABLE ? RELAY_BLOCKS : 0;
+        // one lane per possible working node (up to RELAY_MAX_BLOCKS, then grid-stride):
+        // the relays are chains of dependent random loads, so latency wants lanes
+        s->rgrid = h->relay && h->cfg.manager != PSIM_MANAGER_PLUGGABLE ? std::min<uint32_t>(grid_for(n), RELAY_MAX_BLOCKS) : 0;
         TRY(s->stat_part.ensure((size_t)(s->pgrid + s->cgrid + s->rgrid) * NST));
         k_node_prep<<<s->pgrid, BLK, 0, s->stream>>>(a, s->bmask.p, s->bound.p, s->stat_part.p, s->ocnt.p,
                                                      s->btot.p);

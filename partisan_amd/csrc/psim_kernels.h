@@ -57,7 +57,7 @@ struct RoundArgs {
 
 __global__ void k_consume(RoundArgs args);
 // lane-per-node SHUFFLE relays ahead of k_consume (psim_consume.hip)
-constexpr uint32_t RELAY_BLOCKS = 512;
+constexpr uint32_t RELAY_MAX_BLOCKS = 8192;
 __global__ void k_relay(RoundArgs args);
 __global__ void k_consume_pl(RoundArgs args);
 // diagnostic builds (-DPSIM_STAMPS): per-phase cycle sums of k_consume, reset on read
