@@ -23,11 +23,12 @@ S_MSG = 64                      # message record bytes
 
 
 def pmc_traffic(workload):
-    """HBM bytes per k_consume launch from the committed PMC passes of this
-    same bench command (profiles/run_pmc.sh -> profiles/pmc_latest.txt):
-    FETCH_SIZE doubled (gfx950 tallies 128-B read requests at 64 B,
-    MI355X_MICROARCH.md HBM section) plus WRITE_SIZE, both in KiB per
-    dispatch.  Config C only; None when the file is absent."""
+    """HBM bytes per round of the node-round kernels (k_relay + k_consume)
+    from the committed PMC passes of this same bench command
+    (profiles/run_pmc.sh -> profiles/pmc_latest.txt): FETCH_SIZE doubled
+    (gfx950 tallies 128-B read requests at 64 B, MI355X_MICROARCH.md HBM
+    section) plus WRITE_SIZE, both in KiB per timed round.  Config C only;
+    None when the file is absent."""
     if workload != "C":
         return None
     path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "pmc_latest.txt")
@@ -35,7 +36,7 @@ def pmc_traffic(workload):
         vals = {}
         for line in open(path):
             f = line.split()
-            if len(f) >= 5 and f[0] in ("FETCH_SIZE", "WRITE_SIZE") and f[3] == "per-dispatch":
+            if len(f) >= 5 and f[0] in ("FETCH_SIZE", "WRITE_SIZE") and f[3] == "per-round":
                 vals[f[0]] = float(f[4])
         return (2 * vals["FETCH_SIZE"] + vals["WRITE_SIZE"]) * 1024.0
     except (OSError, KeyError, ValueError):
@@ -265,7 +266,9 @@ def main():
                                    f"1 GPU, {args.vshards} virtual shards" if args.vshards > 1 else "1 GPU")},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(args.workload),
-                     "kernel": "k_consume", "alg_bytes_per_launch": per_launch_bytes,
+                     "kernel": "k_relay + k_consume (the node-round phase: one launch of each per round, "
+                               "timed from k_relay's first block to k_consume's last)",
+                     "alg_bytes_per_launch": per_launch_bytes,
                      "avg_launch_ms": per_launch_s * 1e3},
         "kernel_ms_per_step": {k: v[0] / args.steps for k, v in kt.items() if v[1]},
         "overflow": int(st["overflow"].sum()),

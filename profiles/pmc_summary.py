@@ -1,36 +1,49 @@
-"""Sum rocprofv3 --pmc counters per kernel from run_counter_collection.csv files.
-Usage: python profiles/pmc_summary.py DIR [DIR...] [--kernel SUBSTR]"""
+"""Sum rocprofv3 --pmc counters of the node-round kernels per timed round,
+from run_counter_collection.csv files.
+Usage: python profiles/pmc_summary.py DIR [DIR...] [--kernels k_relay(,k_consume(]
+                                       [--rounds 10] [--tail 40]
+The timed rounds are the ROUNDS dispatches of each kernel before the TAIL
+overlay-drain dispatches at the end of bench.py (OVERLAY_DRAIN = 40)."""
 import csv
 import sys
 from collections import defaultdict
 
 
+def opt(name, default):
+    if name in sys.argv:
+        v = sys.argv[sys.argv.index(name) + 1]
+        return v
+    return default
+
+
 def main():
-    args = [a for a in sys.argv[1:] if not a.startswith("--")]
-    ksub = "k_consume"
-    if "--kernel" in sys.argv:
-        ksub = sys.argv[sys.argv.index("--kernel") + 1]
-        args.remove(ksub)
-    last = None                      # only the last K dispatches (the timed rounds)
-    if "--last" in sys.argv:
-        v = sys.argv[sys.argv.index("--last") + 1]
-        last = int(v)
-        args.remove(v)
+    flags = {"--kernels", "--rounds", "--tail"}
+    args, skip = [], False
+    for a in sys.argv[1:]:
+        if skip:
+            skip = False
+            continue
+        if a in flags:
+            skip = True
+            continue
+        args.append(a)
+    kernels = opt("--kernels", "k_relay(,k_consume(").split(",")
+    rounds = int(opt("--rounds", "10"))
+    tail = int(opt("--tail", "40"))
     tot = defaultdict(float)
-    disp = defaultdict(set)
     for d in args:
         with open(f"{d}/run_counter_collection.csv") as f:
-            rows = [r for r in csv.DictReader(f) if ksub in r["Kernel_Name"]]
-        if last:
-            ids = sorted({int(r["Dispatch_Id"]) for r in rows})[-last:]
-            keep = set(ids)
-            rows = [r for r in rows if int(r["Dispatch_Id"]) in keep]
-        for row in rows:
-            tot[row["Counter_Name"]] += float(row["Counter_Value"])
-            disp[row["Counter_Name"]].add(row["Dispatch_Id"])
+            rows = list(csv.DictReader(f))
+        for k in kernels:
+            kr = [r for r in rows if k in r["Kernel_Name"]]
+            ids = sorted({int(r["Dispatch_Id"]) for r in kr})
+            keep = set(ids[len(ids) - tail - rounds:len(ids) - tail])
+            for r in kr:
+                if int(r["Dispatch_Id"]) in keep:
+                    tot[r["Counter_Name"]] += float(r["Counter_Value"])
+    print(f"# kernels {','.join(kernels)}; {rounds} timed rounds before the last {tail} dispatches")
     for k in sorted(tot):
-        n = len(disp[k])
-        print(f"{k:24s} total {tot[k]:.4g}  per-dispatch {tot[k] / n:.4g}  ({n} dispatches)")
+        print(f"{k:24s} total {tot[k]:.4g}  per-round {tot[k] / rounds:.4g}  ({rounds} rounds)")
     if "SQ_WAVE_CYCLES" in tot:
         wc = tot["SQ_WAVE_CYCLES"]
         for k in ("SQ_WAIT_ANY", "SQ_ACTIVE_INST_ANY", "SQ_WAIT_INST_ANY"):

@@ -15,7 +15,7 @@ pass p1 SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_LDS SQ_WAVE_
 pass p2 SQ_WAIT_INST_ANY SQ_BUSY_CYCLES SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_MISC
 pass p3 FETCH_SIZE
 pass p4 WRITE_SIZE
-python3 $R/profiles/pmc_summary.py $OUT/p1 $OUT/p2 $OUT/p3 $OUT/p4 --last 10 > $OUT/summary.txt
+python3 $R/profiles/pmc_summary.py $OUT/p1 $OUT/p2 $OUT/p3 $OUT/p4 --rounds 10 > $OUT/summary.txt
 cat $OUT/summary.txt
 rm -rf $OUT/p1 $OUT/p2 $OUT/p3 $OUT/p4      # keep gpurun_out small (<64 MiB merges back)
 echo pmc done
