@@ -20,6 +20,8 @@
  *       handle_cast({join, Peer})                               (hyparview:225-226, :500-515)
  *   psim_crash
  *       connection death -> handle_info({'EXIT', ...})          (hyparview:609-654)
+ *   psim_revive
+ *       a restarted manager: init/1 without a join              (hyparview:289-354)
  *   psim_set_partition / psim_clear_partition
  *       inject_partition/2, resolve_partition/1                 (hyparview:244-250, :1731-1797)
  *       (modelled as a network partition)
@@ -244,6 +246,12 @@ int psim_abi_version(void);
 /* Events take effect at the start of the next round. */
 int psim_join(psim_handle *h, const uint32_t *nodes, const uint32_t *contacts, size_t n);
 int psim_crash(psim_handle *h, const uint32_t *nodes, size_t n);
+/* Restart nodes (crashed, or never started) without a join: each comes back
+ * with init/1 state -- empty views, a fresh incarnation (epoch + 1 when
+ * persist_epoch), its draw counter back at 0 -- and waits to be reached
+ * (hyparview:289-354; a node restarted by its supervisor, not told to
+ * join).  Same as psim_join with every contact PSIM_NONE. */
+int psim_revive(psim_handle *h, const uint32_t *nodes, size_t n);
 int psim_set_partition(psim_handle *h, const uint8_t *group, size_t n);
 int psim_clear_partition(psim_handle *h);
 int psim_broadcast(psim_handle *h, uint32_t root, uint32_t msg_id);

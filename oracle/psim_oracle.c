@@ -1284,6 +1284,16 @@ int orc_join(struct psim_handle *h, const uint32_t *nodes, const uint32_t *conta
     return PSIM_OK;
 }
 
+/* psim_revive: a restart without a join (psim_join with no contact) */
+int orc_revive(struct psim_handle *h, const uint32_t *nodes, size_t n) {
+    uint32_t *none = (uint32_t *)malloc((n ? n : 1) * sizeof(uint32_t));
+    if (!none) return PSIM_ENOMEM;
+    for (size_t i = 0; i < n; i++) none[i] = PSIM_NONE;
+    int rc = orc_join(h, nodes, none, n);
+    free(none);
+    return rc;
+}
+
 int orc_crash(struct psim_handle *h, const uint32_t *nodes, size_t n) {
     for (size_t i = 0; i < n; i++)
         if (nodes[i] >= h->N) return PSIM_ERANGE;

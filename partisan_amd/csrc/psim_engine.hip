@@ -1598,6 +1598,12 @@ int psim_join(psim_handle* h, const uint32_t* nodes, const uint32_t* contacts, s
     return PSIM_OK;
 }
 
+int psim_revive(psim_handle* h, const uint32_t* nodes, size_t n) {
+    if (!h || (n && !nodes)) return PSIM_EINVAL;
+    std::vector<uint32_t> none(n, PSIM_NONE);
+    return psim_join(h, nodes, none.data(), n);
+}
+
 int psim_crash(psim_handle* h, const uint32_t* nodes, size_t n) {
     if (!h || (n && !nodes)) return PSIM_EINVAL;
     for (size_t i = 0; i < n; i++)

@@ -88,6 +88,11 @@ class _Driver:
         nodes = np.ascontiguousarray(nodes, np.uint32)
         self._check(self._api["crash"](self._h, _abi.u32p(nodes), nodes.size), "crash")
 
+    def revive(self, nodes):
+        """Restart nodes without a join (init/1 state, reached by others)."""
+        nodes = np.ascontiguousarray(nodes, np.uint32)
+        self._check(self._api["revive"](self._h, _abi.u32p(nodes), nodes.size), "revive")
+
     def set_partition(self, group):
         g = np.ascontiguousarray(group, np.uint8)
         self._check(self._api["set_partition"](

@@ -74,6 +74,24 @@ def crash_only(make, n=1024, seed=9, rounds=80):
     return sim, st, victims
 
 
+def crash_revive(make, n=1024, seed=11, rounds=100):
+    """Crashes at round 40, the same nodes restarted without a join at round
+    50 (psim_revive: init/1 state, reached through other nodes' passive
+    views), a broadcast at round 70."""
+    sim = make(default_config(n_nodes=n, seed=seed))
+    victims = np.arange(5, n, 13, dtype=np.uint32)
+    bc = _bcast_every(sim, 1000, 70)
+
+    def hook(r):
+        if r == 40:
+            sim.crash(victims)
+        if r == 50:
+            sim.revive(victims)
+        bc(r)
+    st = sim.run_schedule(W.doubling_join(n, seed), rounds, extra=hook)
+    return sim, st, victims
+
+
 def star(make, n=512, seed=3, rounds=60):
     sim = make(default_config(n_nodes=n, seed=seed))
     st = sim.run_schedule(W.star_join(n), rounds)

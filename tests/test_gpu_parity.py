@@ -53,6 +53,12 @@ def test_crash_parity():
     S.compare_nodes(gs.nodes(), os_.nodes())
 
 
+def test_crash_revive_parity():
+    (gs, gst, _), (os_, ost, _) = _both(S.crash_revive)
+    S.compare_stats(gst, ost)
+    S.compare_nodes(gs.nodes(), os_.nodes())
+
+
 def test_star_hotspot_parity():
     (gs, gst), (os_, ost) = _both(S.star, n=512)
     S.compare_stats(gst, ost)

@@ -76,6 +76,31 @@ def test_stopped_members_leave_active_views():
     assert st["exits"].sum() > 0
 
 
+def test_revived_nodes_restart_without_join():
+    """psim_revive: restarted without a join, a node comes back with init/1
+    state (only itself active, empty passive view, start round = the restart)
+    and is reached only by a node that still holds it in its passive view and
+    promotes it (NEIGHBOR_REQUEST, hv:975-1053).  EXIT removed it from every
+    holder's views and a full active view never promotes, so in this run all
+    of them stay isolated -- the reference's behaviour for a restarted
+    manager that is not told to join.  The rest of the overlay stays
+    connected and symmetric, and the broadcast after the restart reaches
+    every linked node and no isolated one."""
+    sim, st, victims = S.crash_revive(Oracle)
+    v = sim.nodes()
+    assert v["up"][victims].all()
+    assert (v["start_round"][victims] == 50).all()
+    assert (v["act_n"][victims] == 1).all() and (v["act"][victims, 0] == victims).all()
+    adj = S.active_graph(v)
+    linked = {i: p for i, p in adj.items() if p}
+    assert len(linked) == len(v) - len(victims)
+    assert S.connected(linked)
+    assert not S.asymmetric(linked)
+    got = (v["have"] & 1).astype(bool)
+    assert all(got[i] for i in linked), "broadcast missed a linked node"
+    assert not got[victims].any()
+
+
 def test_churn_partition_invariants():
     sim, st = S.churn_partition(Oracle, n=1024)
     v = sim.nodes()
