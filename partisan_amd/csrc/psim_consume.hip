@@ -1141,6 +1141,8 @@ __global__ void __launch_bounds__(256) k_relay(RoundArgs a) {
         uint32_t ik = 0, ttl = 0, nex = 0, src = 0;
         bool lazy = false;
         const Msg* rp = nullptr;
+        uint4 act0 = make_uint4(0, 0, 0, 0), act1 = act0;
+        uint32_t me_part = 0;
         if (P < na) {
             D = a.desc[P];
             const uint32_t id = D.x, tf = D.z >> 28;
@@ -1148,15 +1150,23 @@ __global__ void __launch_bounds__(256) k_relay(RoundArgs a) {
             fast = ik <= 1 && !(tf & DESC_SHUFFLE) && !a.crash_round &&
                    !(a.origin_now && a.plumtree && a.origin_node == id);
             if (fast) {
-                h = a.hdr[id - a.lo];
+                // the header, the record's first 16 B, the active row and the
+                // partition byte are independent: issued together, waited once
+                const size_t li = id - a.lo;
+                rp = a.rec_in + D.y;
+                const uint4 r0 = ik ? *reinterpret_cast<const uint4*>(rp) : make_uint4(0, 0, 0, 0);
+                h = a.hdr[li];
+                const uint4* ar = reinterpret_cast<const uint4*>(a.act + li * PSIM_ACTIVE_CAP);
+                act0 = ar[0];
+                act1 = ar[1];
+                me_part = a.part[id];
                 lazy = (tf & DESC_LAZY) && h.out_n > 0;
                 fast = h.start_round != a.round && (!(tf & DESC_PROMO) || h.act_n >= a.min_active);
                 if (ik) {
-                    rp = a.rec_in + D.y;
-                    const uint32_t tt = rp->tt;
+                    const uint32_t tt = r0.z;
                     ttl = (tt >> 8) & 0xFF;
                     nex = (tt >> 16) & 0xFF;
-                    src = rp->src;
+                    src = r0.y;
                     fast = fast && h.act_n > 1 && (tt & 0xFF) == PSIM_MSG_SHUFFLE && ttl > 0;
                 }
             }
@@ -1183,10 +1193,7 @@ __global__ void __launch_bounds__(256) k_relay(RoundArgs a) {
         if (!fast) continue;
         const uint32_t id = D.x;
         const size_t li = id - a.lo;
-        const uint4* ar = reinterpret_cast<const uint4*>(a.act + li * PSIM_ACTIVE_CAP);
-        const uint4 a0 = ar[0], a1 = ar[1];
-        const uint32_t A[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
-        const uint32_t me_part = a.part[id];
+        const uint32_t A[8] = {act0.x, act0.y, act0.z, act0.w, act1.x, act1.y, act1.z, act1.w};
         uint64_t rng = h.rng;
         uint32_t seq = 0;
         v[R_PROC]++;
