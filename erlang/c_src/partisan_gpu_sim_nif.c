@@ -113,6 +113,18 @@ static ERL_NIF_TERM nif_revive(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv
     return rc ? err(env, rc) : enif_make_atom(env, "ok");
 }
 
+/* psim_leave: leave/0 at each node under the pluggable manager */
+static ERL_NIF_TERM nif_leave(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[]) {
+    sim_res *r; ErlNifBinary a;
+    if (!enif_get_resource(env, argv[0], SIM_RT, (void **)&r) ||
+        !enif_inspect_binary(env, argv[1], &a) || a.size % 4)
+        return enif_make_badarg(env);
+    enif_mutex_lock(r->mu);
+    int rc = psim_leave(r->h, (const uint32_t *)a.data, a.size / 4);
+    enif_mutex_unlock(r->mu);
+    return rc ? err(env, rc) : enif_make_atom(env, "ok");
+}
+
 static ERL_NIF_TERM nif_broadcast(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[]) {
     sim_res *r; unsigned root, id;
     if (!enif_get_resource(env, argv[0], SIM_RT, (void **)&r) ||
@@ -269,6 +281,7 @@ static ErlNifFunc funcs[] = {
     {"join_nif", 3, nif_join, 0},
     {"crash_nif", 2, nif_crash, 0},
     {"revive_nif", 2, nif_revive, 0},
+    {"leave_nif", 2, nif_leave, 0},
     {"broadcast", 3, nif_broadcast, 0},
     {"step", 2, nif_step, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"active", 2, nif_active, 0},

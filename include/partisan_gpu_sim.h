@@ -22,6 +22,8 @@
  *       connection death -> handle_info({'EXIT', ...})          (hyparview:609-654)
  *   psim_revive
  *       a restarted manager: init/1 without a join              (hyparview:289-354)
+ *   psim_leave
+ *       leave/0 under the pluggable manager                     (pluggable:283-284, :502-515)
  *   psim_set_partition / psim_clear_partition
  *       inject_partition/2, resolve_partition/1                 (hyparview:244-250, :1731-1797)
  *       (modelled as a network partition)
@@ -252,6 +254,13 @@ int psim_crash(psim_handle *h, const uint32_t *nodes, size_t n);
  * (hyparview:289-354; a node restarted by its supervisor, not told to
  * join).  Same as psim_join with every contact PSIM_NONE. */
 int psim_revive(psim_handle *h, const uint32_t *nodes, size_t n);
+/* leave/0 at each node (pluggable manager only; the HyParView manager's
+ * leave answers `error`, hv:363-364, so PSIM_EUNSUPPORTED there).  The
+ * manager stops inside handle_call({leave, Myself}) (pluggable:502-515)
+ * before the Strategy:leave/2 messages it cast to itself are sent
+ * (pluggable:1390-1420, :1585-1609), so the node goes down without a word,
+ * exactly as psim_crash.  Revive with psim_revive. */
+int psim_leave(psim_handle *h, const uint32_t *nodes, size_t n);
 int psim_set_partition(psim_handle *h, const uint8_t *group, size_t n);
 int psim_clear_partition(psim_handle *h);
 int psim_broadcast(psim_handle *h, uint32_t root, uint32_t msg_id);

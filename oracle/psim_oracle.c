@@ -1305,6 +1305,15 @@ int orc_crash(struct psim_handle *h, const uint32_t *nodes, size_t n) {
     return PSIM_OK;
 }
 
+/* psim_leave: leave/0 under the pluggable manager stops the manager before
+ * the Strategy:leave/2 messages it cast to itself go out
+ * (pluggable:502-515, :1390-1420, :1585-1609) -- a crash; the HyParView
+ * manager answers `error` (hyparview:363-364). */
+int orc_leave(struct psim_handle *h, const uint32_t *nodes, size_t n) {
+    if (!is_pl(h)) return PSIM_EUNSUPPORTED;
+    return orc_crash(h, nodes, n);
+}
+
 int orc_set_partition(struct psim_handle *h, const uint8_t *group, size_t n) {
     if (n != h->N) return PSIM_EINVAL;
     memcpy(h->pend_part, group, n);

@@ -1612,6 +1612,18 @@ int psim_crash(psim_handle* h, const uint32_t* nodes, size_t n) {
     return PSIM_OK;
 }
 
+// leave/0 under the pluggable manager: handle_call({leave, Myself})
+// (pl:502-515) runs internal_leave/2 (pl:1390-1420), whose Strategy:leave/2
+// messages are casts to the manager itself (schedule_self_message_delivery/6
+// pl:1585-1609), then returns {stop, normal}: the casts die in its mailbox and
+// the node stops as if crashed.  HyParView's leave answers `error`
+// (hv:363-364).
+int psim_leave(psim_handle* h, const uint32_t* nodes, size_t n) {
+    if (!h || (n && !nodes)) return PSIM_EINVAL;
+    if (h->cfg.manager != PSIM_MANAGER_PLUGGABLE) return PSIM_EUNSUPPORTED;
+    return psim_crash(h, nodes, n);
+}
+
 int psim_set_partition(psim_handle* h, const uint8_t* group, size_t n) {
     if (!h || !group || n != h->N) return PSIM_EINVAL;
     h->pend_part.assign(group, group + n);

@@ -93,6 +93,13 @@ class _Driver:
         nodes = np.ascontiguousarray(nodes, np.uint32)
         self._check(self._api["revive"](self._h, _abi.u32p(nodes), nodes.size), "revive")
 
+    def leave(self, nodes):
+        """leave/0 at each node (pluggable manager; raises on HyParView, whose
+        leave answers `error`): the manager stops before its leave messages
+        go out, so the node goes down as in crash()."""
+        nodes = np.ascontiguousarray(nodes, np.uint32)
+        self._check(self._api["leave"](self._h, _abi.u32p(nodes), nodes.size), "leave")
+
     def set_partition(self, group):
         g = np.ascontiguousarray(group, np.uint8)
         self._check(self._api["set_partition"](

@@ -100,11 +100,13 @@ def star(make, n=512, seed=3, rounds=60):
     return sim, np.concatenate([st, st2])
 
 
-def pl_doubling(make, n, seed, rounds, strategy, fanout=0, crash_at=None, part_at=None, **cfg):
+def pl_doubling(make, n, seed, rounds, strategy, fanout=0, crash_at=None, part_at=None, leave=False,
+                **cfg):
     """The pluggable manager with one membership strategy (SURVEY 8(a)
     s1-s4): doubling bootstrap, then optional crashes (scamp: 10% of the
     nodes, restarted and rejoined 5 rounds later; full: not restarted) and a
-    half/half partition for 10 rounds."""
+    half/half partition for 10 rounds.  leave=True: the victims call leave/0
+    (psim_leave) at crash_at instead of crashing."""
     sim = make(default_config(n_nodes=n, seed=seed, manager=1, strategy=strategy, fanout=fanout, **cfg))
     rng = np.random.Generator(np.random.PCG64([seed, 7]))
     victims = np.sort(rng.choice(np.arange(1, n, dtype=np.uint32), size=max(1, n // 10),
@@ -112,7 +114,7 @@ def pl_doubling(make, n, seed, rounds, strategy, fanout=0, crash_at=None, part_a
 
     def hook(r):
         if crash_at is not None and r == crash_at:
-            sim.crash(victims)
+            (sim.leave if leave else sim.crash)(victims)
         if crash_at is not None and r == crash_at + 5 and strategy != 0:
             sim.join(victims, np.zeros(victims.size, np.uint32))
         if part_at is not None and r == part_at:

@@ -156,6 +156,17 @@ def test_strategy_parity(strategy, n, fanout):
     S.compare_strategy(gs, os_, full_bits=[0, 1, n // 2, n - 1] if strategy == 0 else None)
 
 
+@pytest.mark.parametrize("strategy", [0, 1, 2])
+def test_strategy_leave_parity(strategy):
+    """psim_leave (leave/0: the manager stops before its leave messages go
+    out) at round 40 for 10% of the nodes, then a partition: bit-identical
+    to the oracle."""
+    kw = dict(strategy=strategy, fanout=5 if strategy == 0 else 0, crash_at=40, part_at=60, leave=True)
+    (gs, gst), (os_, ost) = _both(S.pl_doubling, 1024, 11, 90, **kw)
+    S.compare_stats(gst, ost)
+    S.compare_strategy(gs, os_, full_bits=[0, 1, 512, 1023] if strategy == 0 else None)
+
+
 @pytest.mark.parametrize("strategy", [1, 2])
 def test_strategy_shard_invariance(strategy):
     def sharded(cfg):

@@ -124,6 +124,26 @@ def test_scamp_churn_partition(strategy):
     assert _weakly_connected(_views(sim))
 
 
+@pytest.mark.parametrize("strategy", [0, 1, 2])
+def test_leave_stops_like_a_crash(strategy):
+    """leave/0 under the pluggable manager (pluggable:502-515, :1390-1420):
+    the Strategy:leave/2 messages are casts to the manager itself, lost when
+    it stops, so the run is identical to crashing the same nodes."""
+    n = 1024
+    kw = dict(strategy=strategy, fanout=5 if strategy == 0 else 0, crash_at=40, part_at=60)
+    _, a = S.pl_doubling(Oracle, n, 11, 90, leave=True, **kw)
+    _, b = S.pl_doubling(Oracle, n, 11, 90, **kw)
+    S.compare_stats(a, b)
+    assert a["send_fail"][41:].sum() > 0
+
+
+def test_hyparview_leave_is_an_error():
+    """hyparview:363-364: handle_call({leave, _}) replies `error`"""
+    sim = Oracle(default_config(n_nodes=8))
+    with pytest.raises(Exception):
+        sim.leave(np.array([1], np.uint32))
+
+
 def test_pluggable_rejects_broadcast():
     sim = Oracle(default_config(n_nodes=8, manager=1, strategy=1))
     with pytest.raises(Exception):
