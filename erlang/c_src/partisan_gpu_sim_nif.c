@@ -125,6 +125,19 @@ static ERL_NIF_TERM nif_leave(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[
     return rc ? err(env, rc) : enif_make_atom(env, "ok");
 }
 
+/* psim_leave_node: leave/1, Actors[i] removes Targets[i] */
+static ERL_NIF_TERM nif_leave_node(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[]) {
+    sim_res *r; ErlNifBinary a, t;
+    if (!enif_get_resource(env, argv[0], SIM_RT, (void **)&r) ||
+        !enif_inspect_binary(env, argv[1], &a) || !enif_inspect_binary(env, argv[2], &t) ||
+        a.size % 4 || a.size != t.size)
+        return enif_make_badarg(env);
+    enif_mutex_lock(r->mu);
+    int rc = psim_leave_node(r->h, (const uint32_t *)a.data, (const uint32_t *)t.data, a.size / 4);
+    enif_mutex_unlock(r->mu);
+    return rc ? err(env, rc) : enif_make_atom(env, "ok");
+}
+
 static ERL_NIF_TERM nif_broadcast(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[]) {
     sim_res *r; unsigned root, id;
     if (!enif_get_resource(env, argv[0], SIM_RT, (void **)&r) ||
@@ -282,6 +295,7 @@ static ErlNifFunc funcs[] = {
     {"crash_nif", 2, nif_crash, 0},
     {"revive_nif", 2, nif_revive, 0},
     {"leave_nif", 2, nif_leave, 0},
+    {"leave_node_nif", 3, nif_leave_node, 0},
     {"broadcast", 3, nif_broadcast, 0},
     {"step", 2, nif_step, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"active", 2, nif_active, 0},

@@ -2,7 +2,7 @@
 %% (include/partisan_gpu_sim.h).  Node ids are the simulated nodes; an id maps
 %% to the harness node_spec #{name => 'n<id>@sim', ...} (DESIGN.md section 2).
 -module(partisan_gpu_sim).
--export([create/1, join/3, crash/2, revive/2, leave/2, broadcast/3, step/2, active/2, members/3,
+-export([create/1, join/3, crash/2, revive/2, leave/2, leave_node/3, broadcast/3, step/2, active/2, members/3,
          delivery/2, histograms/1, snapshot/1, restore/2]).
 -on_load(init/0).
 
@@ -23,6 +23,8 @@ crash(Sim, Nodes) -> crash_nif(Sim, pack(Nodes)).
 revive(Sim, Nodes) -> revive_nif(Sim, pack(Nodes)).
 %% leave/0 at each node (pluggable manager handles; {error, unsupported} on HyParView)
 leave(Sim, Nodes) -> leave_nif(Sim, pack(Nodes)).
+%% leave/1 at each actor: Actors[i] removes Targets[i] (SCAMP v1 / v2 handles)
+leave_node(Sim, Actors, Targets) -> leave_node_nif(Sim, pack(Actors), pack(Targets)).
 broadcast(_Sim, _Root, _Id) -> erlang:nif_error(nif_not_loaded).
 step(_Sim, _Rounds) -> erlang:nif_error(nif_not_loaded).
 active(_Sim, _Node) -> erlang:nif_error(nif_not_loaded).
@@ -41,3 +43,4 @@ join_nif(_S, _N, _C) -> erlang:nif_error(nif_not_loaded).
 crash_nif(_S, _N) -> erlang:nif_error(nif_not_loaded).
 revive_nif(_S, _N) -> erlang:nif_error(nif_not_loaded).
 leave_nif(_S, _N) -> erlang:nif_error(nif_not_loaded).
+leave_node_nif(_S, _A, _T) -> erlang:nif_error(nif_not_loaded).

@@ -102,7 +102,9 @@ enum psim_pl_msg_type {
     PSIM_PL_GOSSIP = 2,    /* full: {membership_strategy, {Myself, State}}   full:127-144 */
     PSIM_PL_FWD_SUB = 3,   /* scamp: {forward_subscription, Node}  scamp_v1:212-252, v2:284-327 */
     PSIM_PL_PING = 4,      /* scamp: {ping, SourceNode}           scamp_v1:177-188, v2:181-191 */
-    PSIM_PL_KEEP_SUB = 5   /* scamp v2: {keep_subscription, Node}  scamp_v2:328-338 */
+    PSIM_PL_KEEP_SUB = 5,  /* scamp v2: {keep_subscription, Node}  scamp_v2:328-338 */
+    PSIM_PL_REMOVE_SUB = 6,  /* scamp v1: {remove_subscription, Node}  scamp_v1:102-122, :190-211 */
+    PSIM_PL_BOOT_REMOVE = 7  /* scamp v2: {bootstrap_remove_subscription, Node}  scamp_v2:116-127, :192-238 */
 };
 
 /* cfg.manager */
@@ -261,6 +263,22 @@ int psim_revive(psim_handle *h, const uint32_t *nodes, size_t n);
  * (pluggable:1390-1420, :1585-1609), so the node goes down without a word,
  * exactly as psim_crash.  Revive with psim_revive. */
 int psim_leave(psim_handle *h, const uint32_t *nodes, size_t n);
+/* leave/1: actors[i] removes targets[i] from the cluster
+ * (handle_call({leave, Node}) pluggable:502-515 -> internal_leave/2
+ * :1390-1420); actor == target is leave/0 above.  SCAMP v1 / v2 handles:
+ *   v1: the actor drops the target and sends {remove_subscription, T} to its
+ *       old membership (scamp_v1:102-122); a receiver holding T crashes on
+ *       the swapped sets:del_element/2 arguments (scamp_v1:197, SURVEY App. A
+ *       Q12) -- T itself included;
+ *   v2: the actor sends {bootstrap_remove_subscription, T} to its partial
+ *       view (scamp_v2:116-127); T, on receipt, stops before its replacement
+ *       casts go out (lists:nth(0, ..) or the self-less reset, :192-238).
+ * A stopping manager sends nothing in that round (its sends are casts to
+ * itself) and is down from the next round on.  One call per actor per
+ * round.  PSIM_EUNSUPPORTED for the full strategy (an ORSet removal needs
+ * tombstones the member bitsets do not hold), HyParView handles and
+ * multi-rank handles. */
+int psim_leave_node(psim_handle *h, const uint32_t *actors, const uint32_t *targets, size_t n);
 int psim_set_partition(psim_handle *h, const uint8_t *group, size_t n);
 int psim_clear_partition(psim_handle *h);
 int psim_broadcast(psim_handle *h, uint32_t root, uint32_t msg_id);

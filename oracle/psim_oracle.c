@@ -86,6 +86,7 @@ typedef struct snode {
     uint32_t last_ping;             /* scamp last_message_time as a round, PSIM_NONE = undefined */
     uint32_t view[PSIM_SVIEW_CAP], view_n;   /* scamp v1 membership / v2 partial_view */
     uint32_t inv[PSIM_SVIEW_CAP], inv_n;     /* scamp v2 in_view */
+    uint32_t leave_tgt;             /* leave/1 call of this round: target + 1, 0 = none */
 } snode;
 
 typedef struct msgvec { omsg *v; size_t n, cap; } msgvec;
@@ -102,6 +103,7 @@ struct psim_handle {
     /* pending events */
     uint32_t *pend_crash; size_t pend_crash_n, pend_crash_cap;
     uint32_t *pend_join, *pend_contact; size_t pend_join_n, pend_join_cap;
+    uint32_t *pend_lv_a, *pend_lv_t; size_t pend_lv_n, pend_lv_cap;
     uint8_t *pend_part; int pend_part_set, pend_part_clear;
     int pend_bcast; uint32_t pend_root, pend_msg;
     uint32_t bcast_root;            /* single-root restriction */
@@ -125,6 +127,7 @@ typedef struct ctx {
     uint32_t snap;                  /* full: payload slot of the current state, PSIM_NONE */
     int dirty;                      /* full: state changed since that snapshot */
     int gossip_due;                 /* full, fanout > 0: a coalesced gossip is owed this round */
+    int stop;                       /* the manager stopped in this round (leave, App. A Q12) */
 } ctx;
 
 static uint64_t draw58(ctx *c) {
@@ -745,7 +748,7 @@ static int timer_due(uint32_t period, uint64_t r, uint32_t start) {
 
 static void process_node(struct psim_handle *h, uint32_t n) {
     node *s = &h->nodes[n];
-    ctx c = {h, s, n, 0, PSIM_NONE, 0, 0};
+    ctx c = {h, s, n, 0, PSIM_NONE, 0, 0, 0};
     uint64_t r = h->round;
     size_t b = h->in_beg[n], e = h->in_beg[n + 1];
     /* a fresh incarnation has no connections: traffic addressed to the
@@ -1021,6 +1024,29 @@ static void scamp_fwd(ctx *c, uint32_t node) {
     if (sublist_view(c, m0, q->view_n, 1, sel)) pl_send(c, sel[0], PSIM_PL_FWD_SUB, node, PSIM_NONE);
 }
 
+/* leave/1 at the actor, Node = t (handle_call({leave, Node}) pluggable:502-515
+ * -> internal_leave/2 :1390-1420, not the actor itself):
+ *   v1 leave/2 (scamp_v1:102-122): delete t from the membership, then
+ *      {remove_subscription, t} to every member of the old list (to_list order);
+ *   v2 leave/2 (scamp_v2:116-127): {bootstrap_remove_subscription, t} to every
+ *      member of the partial view, no state change. */
+static void scamp_leave(ctx *c, uint32_t t) {
+    snode *q = &c->h->sn[c->me];
+    uint32_t m0[PSIM_SVIEW_CAP], n0 = q->view_n;
+    memcpy(m0, q->view, sizeof m0);
+    int v1 = c->h->cfg.strategy == PSIM_STRATEGY_SCAMP_V1;
+    /* the connections to the old members stay open (they close only on
+     * 'EXIT', pluggable:971-984), so the sends are judged on the old view */
+    for (uint32_t i = 0; i < n0; i++)
+        pl_send(c, m0[i], v1 ? PSIM_PL_REMOVE_SUB : PSIM_PL_BOOT_REMOVE, t, PSIM_NONE);
+    if (v1) {
+        uint32_t k = 0;
+        for (uint32_t i = 0; i < q->view_n; i++) if (q->view[i] != t) q->view[k++] = q->view[i];
+        for (uint32_t i = k; i < q->view_n; i++) q->view[i] = 0;
+        q->view_n = k;
+    }
+}
+
 /* ------------------------------------------------------------- driver -- */
 static void pl_handle(ctx *c, const omsg *m) {
     struct psim_handle *h = c->h;
@@ -1059,29 +1085,61 @@ static void pl_handle(ctx *c, const omsg *m) {
     case PSIM_PL_KEEP_SUB:    /* scamp_v2:328-338: InView = [Node | InView0] */
         if (h->cfg.strategy == PSIM_STRATEGY_SCAMP_V2) scamp_add(c, q->inv, &q->inv_n, m->a0, 0);
         break;
+    case PSIM_PL_REMOVE_SUB:  /* scamp_v1:190-211: a member Node reaches
+                                 sets:del_element(Membership0, Node) with its
+                                 arguments swapped (App. A Q12): the manager crashes */
+        if (h->cfg.strategy == PSIM_STRATEGY_SCAMP_V1 && list_member(q->view, q->view_n, m->a0)) c->stop = 1;
+        break;
+    case PSIM_PL_BOOT_REMOVE: /* scamp_v2:192-238: at Node itself every branch
+                                 stops the manager before its casts go out --
+                                 lists:nth(0, ..) (App. A Q12), or the reset
+                                 partial view leaves it out of its own membership
+                                 (pluggable:1182-1188) */
+        if (h->cfg.strategy == PSIM_STRATEGY_SCAMP_V2 && m->a0 == c->me) c->stop = 1;
+        break;
     default:
         break;
     }
 }
 
+int orc_crash(struct psim_handle *h, const uint32_t *nodes, size_t n);
+
 static void pl_process_node(struct psim_handle *h, uint32_t n) {
     node *s = &h->nodes[n];
     snode *q = &h->sn[n];
-    ctx c = {h, s, n, 0, PSIM_NONE, 0, 0};
+    ctx c = {h, s, n, 0, PSIM_NONE, 0, 0, 0};
     uint64_t r = h->round;
     size_t b = h->in_beg[n], e = h->in_beg[n + 1];
     if (s->start_round == r && e > b) { h->st->dropped += e - b; e = b; }
     int hello = q->pending != PSIM_NONE && !q->hello_sent;
     int periodic = timer_due(h->cfg.periodic_interval, r, s->start_round);
-    if (!(e > b || hello || periodic)) return;
+    uint32_t leave = q->leave_tgt;
+    if (!(e > b || hello || periodic || leave)) return;
     h->st->nodes_processed++;
+    /* a manager that stops this round sends nothing: its sends are casts to
+     * itself (schedule_self_message_delivery/6 pluggable:1585-1609) */
+    size_t out0 = h->out.n;
+    uint64_t em0[PSIM_MSG_NTYPES], dig0 = h->st->digest, fail0 = h->st->send_fail;
+    memcpy(em0, h->st->emitted, sizeof em0);
+    if (leave) {              /* leave/1 (pluggable:502-515, :1390-1420) */
+        q->leave_tgt = 0;
+        scamp_leave(&c, leave - 1);
+    }
     if (hello) {              /* establish_connections -> client connect + hello */
         if (connect_ok(&c, q->pending)) { pl_emit(&c, q->pending, PSIM_PL_HELLO, 0, PSIM_NONE); q->hello_sent = 1; }
         else h->st->send_fail++;
     }
-    for (size_t i = b; i < e; i++) {
+    for (size_t i = b; i < e && !c.stop; i++) {
         h->st->delivered[h->inbox.v[i].type]++;
         pl_handle(&c, &h->inbox.v[i]);
+        if (c.stop) h->st->dropped += e - i - 1;
+    }
+    if (c.stop) {             /* down from the next round, as a crash */
+        h->out.n = out0;
+        memcpy(h->st->emitted, em0, sizeof em0);
+        h->st->digest = dig0; h->st->send_fail = fail0;
+        orc_crash(h, &n, 1);
+        return;
     }
     if (periodic) {           /* handle_info(periodic) pluggable:881-903 */
         if (h->cfg.strategy == PSIM_STRATEGY_FULL) c.gossip_due = 1;
@@ -1141,6 +1199,8 @@ static void round_begin(struct psim_handle *h, psim_round_stats *st) {
         if (h->nodes[n].up) { h->nodes[n].up = 0; h->crashed_now[n] = 1; }
     }
     for (size_t i = 0; i < h->pend_join_n; i++) node_init(h, h->pend_join[i], h->pend_contact[i]);
+    for (size_t i = 0; i < h->pend_lv_n; i++) h->sn[h->pend_lv_a[i]].leave_tgt = h->pend_lv_t[i] + 1;
+    h->pend_lv_n = 0;
     if (h->pend_part_clear) memset(h->part, 0, h->N);
     if (h->pend_part_set) memcpy(h->part, h->pend_part, h->N);
     h->origin_now = 0;
@@ -1260,6 +1320,7 @@ void orc_destroy(struct psim_handle *h) {
     free(h->nodes); free(h->part); free(h->crashed_now); free(h->in_beg); free(h->pend_part);
     free(h->inbox.v); free(h->out.v);
     free(h->pend_crash); free(h->pend_join); free(h->pend_contact);
+    free(h->pend_lv_a); free(h->pend_lv_t);
     free(h->sn); free(h->fbits); free(h->pay_in); free(h->pay_out);
     free(h);
 }
@@ -1312,6 +1373,36 @@ int orc_crash(struct psim_handle *h, const uint32_t *nodes, size_t n) {
 int orc_leave(struct psim_handle *h, const uint32_t *nodes, size_t n) {
     if (!is_pl(h)) return PSIM_EUNSUPPORTED;
     return orc_crash(h, nodes, n);
+}
+
+/* psim_leave_node: leave/1 -- actors[i] removes targets[i]
+ * (handle_call({leave, Node}) pluggable:502-515).  actor == target is
+ * leave/0.  SCAMP v1 / v2 only: the full strategy's ORSet removal needs
+ * remove tombstones the member bitsets do not hold; one call per actor and
+ * round; unsharded handles only (a stop is known on its own shard). */
+int orc_leave_node(struct psim_handle *h, const uint32_t *actors, const uint32_t *targets, size_t n) {
+    if (!is_pl(h) || h->cfg.strategy == PSIM_STRATEGY_FULL || h->lo != 0 || h->hi != h->N)
+        return PSIM_EUNSUPPORTED;
+    for (size_t i = 0; i < n; i++) {
+        if (actors[i] >= h->N || targets[i] >= h->N) return PSIM_ERANGE;
+        for (size_t j = 0; j < h->pend_lv_n; j++) if (h->pend_lv_a[j] == actors[i]) return PSIM_EINVAL;
+        for (size_t j = 0; j < i; j++) if (actors[j] == actors[i]) return PSIM_EINVAL;
+    }
+    for (size_t i = 0; i < n; i++) {
+        if (actors[i] == targets[i]) {
+            int rc = orc_crash(h, &actors[i], 1);
+            if (rc) return rc;
+            continue;
+        }
+        if (h->pend_lv_n == h->pend_lv_cap) {
+            h->pend_lv_cap = h->pend_lv_cap ? 2 * h->pend_lv_cap : 64;
+            h->pend_lv_a = (uint32_t *)realloc(h->pend_lv_a, h->pend_lv_cap * 4);
+            h->pend_lv_t = (uint32_t *)realloc(h->pend_lv_t, h->pend_lv_cap * 4);
+        }
+        h->pend_lv_a[h->pend_lv_n] = actors[i];
+        h->pend_lv_t[h->pend_lv_n++] = targets[i];
+    }
+    return PSIM_OK;
 }
 
 int orc_set_partition(struct psim_handle *h, const uint8_t *group, size_t n) {

@@ -122,6 +122,7 @@ SIGNATURES = {
     "crash": (C.c_int, [_H, _P32, C.c_size_t]),
     "revive": (C.c_int, [_H, _P32, C.c_size_t]),
     "leave": (C.c_int, [_H, _P32, C.c_size_t]),
+    "leave_node": (C.c_int, [_H, _P32, _P32, C.c_size_t]),
     "set_partition": (C.c_int, [_H, C.POINTER(C.c_uint8), C.c_size_t]),
     "clear_partition": (C.c_int, [_H]),
     "broadcast": (C.c_int, [_H, C.c_uint32, C.c_uint32]),

@@ -22,7 +22,7 @@ struct __attribute__((aligned(16))) Hdr {
     uint8_t act_n, pas_n, sent_n, sent_head;
     uint8_t recv_n, recv_head, all_n, com_n;
     uint8_t eag_n, laz_n, out_n, pad0;
-    uint32_t pad1[4];
+    uint32_t pad1[4];      // pluggable: pad1[0] = leave/1 target of this round + 1, 0 = none
 };
 static_assert(sizeof(Hdr) == 64, "Hdr must be one 64-B line");
 
@@ -82,7 +82,7 @@ enum : uint32_t { DESC_PROMO = 1, DESC_SHUFFLE = 2, DESC_LAZY = 4 };
 // stats slots in the per-block partial arrays
 enum {
     ST_EMIT = 0, ST_DELIV = 16, ST_DROPPED = 32, ST_UP, ST_PROC, ST_EXITS, ST_FAIL, ST_FIRST,
-    ST_OVF, ST_DIGEST, ST_BYTES, NST
+    ST_OVF, ST_DIGEST, ST_BYTES, ST_STOP, NST
 };
 
 // ------------------------------------------------------------------ RNG --

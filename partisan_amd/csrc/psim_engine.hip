@@ -79,6 +79,16 @@ __global__ void k_crash(uint8_t* flags, const uint32_t* ids, uint32_t n) {
     if (f & F_UP) flags[id] = (uint8_t)((f & ~F_UP) | F_CRASHED);
 }
 
+// leave/1 calls of this round (pluggable): Hdr pad1[0] = target + 1 at
+// each actor this shard owns
+__global__ void k_leave_set(Hdr* hdr, uint32_t lo, uint32_t n_local, const uint32_t* actors,
+                            const uint32_t* targets, uint32_t n) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint32_t id = actors[i];
+    if (id >= lo && id < lo + n_local) hdr[id - lo].pad1[0] = targets[i] + 1;
+}
+
 __global__ void k_uncrash(uint8_t* flags, const uint32_t* ids, uint32_t n) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
@@ -536,7 +546,10 @@ __global__ void __launch_bounds__(256) k_node_prep(RoundArgs a, const uint32_t* 
                                                    uint64_t* part, uint32_t* ocnt, unsigned long long* btot) {
     __shared__ unsigned long long s_up, s_drop, s_b;
     if (threadIdx.x == 0) { s_up = 0; s_drop = 0; s_b = 0; }
-    if (blockIdx.x == 0 && threadIdx.x == 0) { a.ktime[0] = ~0ull; a.ktime[1] = 0; *a.n_slow = 0; }
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        a.ktime[0] = ~0ull; a.ktime[1] = 0; *a.n_slow = 0;
+        if (a.n_stop) *a.n_stop = 0;
+    }
     __syncthreads();
     unsigned long long up = 0, drop = 0, bs = 0;        // this thread's sums (wave-summed below)
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < a.n_local; i += gridDim.x * blockDim.x) {
@@ -552,12 +565,13 @@ __global__ void __launch_bounds__(256) k_node_prep(RoundArgs a, const uint32_t* 
                 const Hdr& x = a.hdr[i];
                 bool pending = x.join_contact != PSIM_NONE;
                 bool per = due(a.periodic, r, st);
+                bool leave = x.pad1[0] != 0;
                 if (a.strategy == PSIM_STRATEGY_FULL)
                     b = a.fanout ? (uint64_t)c + a.fanout + 1 : ((uint64_t)c + 2) * (a.n_nodes + 1);
                 else
                     b = (uint64_t)c + (pending ? 2 + PSIM_SVIEW_CAP + a.scamp_c : 0) +
-                        (per ? 1 + PSIM_SVIEW_CAP : 0) + 1;
-                w = c > 0 || (pending && !x.have) || per;
+                        (per ? 1 + PSIM_SVIEW_CAP : 0) + (leave ? PSIM_SVIEW_CAP : 0) + 1;
+                w = c > 0 || (pending && !x.have) || per || leave;
             } else {
                 bool origin = a.origin_now && id == a.origin_node;
                 // per message its class bound (a BROADCAST: 1), per distinct
@@ -861,7 +875,7 @@ struct Shard {
     DBuf<uint4> desc, desc_slow;            // work descriptors; those k_relay leaves to k_consume
     DBuf<uint64_t> bound, pscan, obase, stat_part, stat_out, d_off;   // bound: packed (bound << 32 | work)
     DBuf<uint8_t> cub_tmp;
-    DBuf<uint32_t> ev_ids, ev_contacts;
+    DBuf<uint32_t> ev_ids, ev_contacts, stop_ids, n_stop;
     DBuf<Msg> sendbuf;
     // pluggable manager
     DBuf<uint32_t> sview, sinv, fbits, pay[2], pay_top;
@@ -898,6 +912,7 @@ struct psim_handle {
     DBuf<uint64_t> comm_cnt;            // RCCL: [send counts | recv counts]
     // pending events
     std::vector<uint32_t> pend_crash, pend_join, pend_contact;
+    std::vector<uint32_t> pend_lv_a, pend_lv_t;     // leave/1 calls: actor, target
     std::vector<uint8_t> pend_part;
     bool pend_part_set = false, pend_part_clear = false;
     bool pend_bcast = false;
@@ -942,6 +957,7 @@ RoundArgs make_args(psim_handle* h, Shard* s) {
     a.fbits = s->fbits.p; a.sview = s->sview.p; a.sinv = s->sinv.p;
     a.ktime = reinterpret_cast<unsigned long long*>(s->stat_out.p + NST);
     a.desc_slow = s->desc_slow.p; a.n_slow = s->n_slow.p;
+    a.stop_ids = s->stop_ids.p; a.n_stop = s->n_stop.p;
     return a;
 }
 
@@ -1038,6 +1054,12 @@ int phase_events_prepare(psim_handle* h, Shard* s, const RoundCtl& ctl, RoundArg
             k_join<<<grid_for(h->pend_join.size()), BLK, 0, s->stream>>>(
                 a, s->start.p, s->ev_ids.p, s->ev_contacts.p, (uint32_t)h->pend_join.size(),
                 h->cfg.persist_epoch);
+        }
+        if (!h->pend_lv_a.empty()) {
+            TRY(upload(s, s->ev_ids, h->pend_lv_a));
+            TRY(upload(s, s->ev_contacts, h->pend_lv_t));
+            k_leave_set<<<grid_for(h->pend_lv_a.size()), BLK, 0, s->stream>>>(
+                s->hdr.p, s->lo, s->n, s->ev_ids.p, s->ev_contacts.p, (uint32_t)h->pend_lv_a.size());
         }
         if (h->pend_part_clear) HIP_TRY(hipMemsetAsync(s->part.p, 0, h->N, s->stream));
         if (h->pend_part_set)
@@ -1376,6 +1398,22 @@ int run_round(psim_handle* h, uint64_t* st) {
         TRY(stream_wait(s));
     }
     h->pend_crash.clear(); h->pend_join.clear(); h->pend_contact.clear();
+    h->pend_lv_a.clear(); h->pend_lv_t.clear();
+    if (st[ST_STOP]) {
+        // managers that stopped this round (psim_leave_node) are down from the
+        // next round on: the next round's crash events (single-rank handles)
+        std::vector<uint32_t> ids;
+        for (Shard* s : h->shards) {
+            const size_t k = s->pin[ST_STOP];
+            if (!k) continue;
+            const size_t at = ids.size();
+            ids.resize(at + k);
+            HIP_TRY(hipMemcpyAsync(ids.data() + at, s->stop_ids.p, k * 4, hipMemcpyDeviceToHost, s->stream));
+            TRY(stream_wait(s));
+        }
+        std::sort(ids.begin(), ids.end());
+        h->pend_crash.insert(h->pend_crash.end(), ids.begin(), ids.end());
+    }
     h->pend_part_set = h->pend_part_clear = false;
     h->pend_bcast = false;
     h->round++;
@@ -1422,6 +1460,7 @@ int shard_alloc(psim_handle* h, Shard* s) {
     rc |= s->long_list.alloc(n); rc |= s->bmask.alloc(n); rc |= s->btot.alloc(1); rc |= s->n_long.alloc(1);
     rc |= s->desc.alloc(n); rc |= s->d_nact.alloc(1);
     rc |= s->desc_slow.alloc(n); rc |= s->n_slow.alloc(1);
+    if (h->cfg.manager == PSIM_MANAGER_PLUGGABLE) { rc |= s->stop_ids.alloc(n); rc |= s->n_stop.alloc(1); }
     rc |= s->stat_out.alloc(NST + 2);   // + the consume span
     rc |= s->ikeys.alloc(1024); rc |= s->ivals.alloc(1024);
     rc |= s->recvbuf.alloc(1024); rc |= s->inbox[0].alloc(1024); rc |= s->inbox[1].alloc(1024); rc |= s->outbox.alloc(1024);
@@ -1457,6 +1496,7 @@ void shard_free(Shard* s) {
     s->cb.release(); s->in_beg.release();
     s->rank.release(); s->long_list.release(); s->bmask.release(); s->btot.release();
     s->hist.release(); s->hoff.release(); s->pairs.release(); s->n_long.release(); s->tmp.release();
+    s->stop_ids.release(); s->n_stop.release();
     s->desc.release(); s->d_nact.release(); s->desc_slow.release(); s->n_slow.release(); s->bound.release(); s->pscan.release();
     s->obase.release(); s->stat_part.release(); s->stat_out.release(); s->d_off.release();
     s->cub_tmp.release(); s->ev_ids.release(); s->ev_contacts.release(); s->sendbuf.release();
@@ -1622,6 +1662,26 @@ int psim_leave(psim_handle* h, const uint32_t* nodes, size_t n) {
     if (!h || (n && !nodes)) return PSIM_EINVAL;
     if (h->cfg.manager != PSIM_MANAGER_PLUGGABLE) return PSIM_EUNSUPPORTED;
     return psim_crash(h, nodes, n);
+}
+
+// leave/1: actors[i] removes targets[i] (pl:502-515 -> internal_leave/2
+// :1390-1420); actor == target is leave/0.  SCAMP v1 / v2 single-rank
+// handles (a stop is learned from the owner shard's list after the round).
+int psim_leave_node(psim_handle* h, const uint32_t* actors, const uint32_t* targets, size_t n) {
+    if (!h || (n && (!actors || !targets))) return PSIM_EINVAL;
+    if (h->cfg.manager != PSIM_MANAGER_PLUGGABLE || h->cfg.strategy == PSIM_STRATEGY_FULL || h->world > 1)
+        return PSIM_EUNSUPPORTED;
+    for (size_t i = 0; i < n; i++) {
+        if (actors[i] >= h->N || targets[i] >= h->N) return PSIM_ERANGE;
+        for (uint32_t a : h->pend_lv_a) if (a == actors[i]) return PSIM_EINVAL;
+        for (size_t j = 0; j < i; j++) if (actors[j] == actors[i]) return PSIM_EINVAL;
+    }
+    for (size_t i = 0; i < n; i++) {
+        if (actors[i] == targets[i]) { TRY(psim_crash(h, &actors[i], 1)); continue; }
+        h->pend_lv_a.push_back(actors[i]);
+        h->pend_lv_t.push_back(targets[i]);
+    }
+    return PSIM_OK;
 }
 
 int psim_set_partition(psim_handle* h, const uint8_t* group, size_t n) {
@@ -1980,7 +2040,7 @@ static std::vector<Section> snap_sections(psim_handle* h, Shard* s, const ShardH
 
 int psim_snapshot(psim_handle* h, void* buf, size_t cap, size_t* need) {
     if (!h || !need) return PSIM_EINVAL;
-    if (!h->pend_crash.empty() || !h->pend_join.empty() || h->pend_part_set || h->pend_part_clear ||
+    if (!h->pend_crash.empty() || !h->pend_join.empty() || !h->pend_lv_a.empty() || h->pend_part_set || h->pend_part_clear ||
         h->pend_bcast)
         return PSIM_ESTATE;
     if (hipSetDevice(h->device) != hipSuccess) return PSIM_EDEVICE;

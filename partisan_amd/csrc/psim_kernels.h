@@ -53,6 +53,8 @@ struct RoundArgs {
     uint32_t pay_cap;
     uint32_t* sview;             // scamp: n_local rows of PSIM_SVIEW_CAP ids
     uint32_t* sinv;              // scamp v2: in_view rows
+    uint32_t* stop_ids;          // pluggable: managers that stopped this round
+    uint32_t* n_stop;            //   (their count, reset by k_node_prep)
 };
 
 __global__ void k_consume(RoundArgs args);

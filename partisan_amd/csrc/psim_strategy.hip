@@ -50,6 +50,7 @@ struct Pw {
     uint32_t* row;                 // full: the node's member bitset
     uint32_t snap;                 // full: payload slot of the current state
     bool dirty, gossip_due;
+    bool stop;                     // the manager stopped this round (leave, App. A Q12)
 };
 
 DEV void st_add(Pw& w, int k, uint32_t v) { w.SC += lane_id() == (uint32_t)k ? v : 0u; }
@@ -323,6 +324,31 @@ DEV void scamp_fwd(Pw& w, uint32_t node) {
     if (sublist(w, w.V, w.vn, 1, SEL)) pl_send(w, rl(SEL, 0), PSIM_PL_FWD_SUB, node, NONE);
 }
 
+// leave/1 at the actor, Node = t (pl:502-515 -> internal_leave/2 :1390-1420):
+// v1 leave/2 (sv1:102-122) deletes t and sends {remove_subscription, t} to
+// the old membership; v2 leave/2 (sv2:116-127) sends
+// {bootstrap_remove_subscription, t} to the partial view, state unchanged
+DEV void scamp_leave(Pw& w, uint32_t t) {
+    const bool v1 = w.a->strategy == PSIM_STRATEGY_SCAMP_V1;
+    const uint32_t M0 = w.V, n0 = w.vn;
+    // the connections to the old members stay open (closed only on 'EXIT',
+    // pl:971-984): the sends are judged on the old view
+    for (uint32_t i = 0; i < n0; i++)
+        pl_send(w, rl(M0, i), v1 ? PSIM_PL_REMOVE_SUB : PSIM_PL_BOOT_REMOVE, t, NONE);
+    if (v1) {
+        const uint32_t l = lane_id();
+        const bool keep = l < w.vn && w.V != t;
+        const uint64_t km = ballot(keep);
+        const uint32_t pos = __popcll(km & ((1ull << l) - 1));
+        if (keep) w.lds[pos] = w.V;
+        __builtin_amdgcn_wave_barrier();
+        const uint32_t k = (uint32_t)__popcll(km);
+        w.V = l < k ? w.lds[l] : 0u;
+        __builtin_amdgcn_wave_barrier();
+        w.vn = k;
+    }
+}
+
 // -------------------------------------------------------------- driver --
 DEV void pl_handle(Pw& w, uint32_t type, uint32_t src, uint32_t a0, uint32_t slot) {
     const bool full = w.a->strategy == PSIM_STRATEGY_FULL;
@@ -363,6 +389,14 @@ DEV void pl_handle(Pw& w, uint32_t type, uint32_t src, uint32_t a0, uint32_t slo
     case PSIM_PL_KEEP_SUB:         // sv2:328-338: InView = [Node | InView0]
         if (w.a->strategy == PSIM_STRATEGY_SCAMP_V2) scamp_add(w, w.I, w.in_n, a0, false);
         break;
+    case PSIM_PL_REMOVE_SUB:       // sv1:190-211: a member Node hits the swapped
+                                   // sets:del_element/2 arguments (App. A Q12): crash
+        if (w.a->strategy == PSIM_STRATEGY_SCAMP_V1 && has(w.V, w.vn, a0)) w.stop = true;
+        break;
+    case PSIM_PL_BOOT_REMOVE:      // sv2:192-238: Node itself stops before its casts
+                                   // go out (lists:nth(0, ..), or the self-less reset, pl:1182-1188)
+        if (w.a->strategy == PSIM_STRATEGY_SCAMP_V2 && a0 == w.me) w.stop = true;
+        break;
     default:
         break;
     }
@@ -390,7 +424,8 @@ DEV void process_pl(Pw& w, uint32_t n, uint32_t ib, uint32_t ik, uint32_t ob) {
     if (w.h.start_round == r && ik) { st_add(w, ST_DROPPED, ik); ik = 0; }
     const bool hello = w.h.join_contact != NONE && !w.h.have;
     const bool periodic = a.periodic > 0 && r > w.h.start_round && ((r - w.h.start_round) % a.periodic) == 0;
-    if (!(ik || hello || periodic)) return;
+    const uint32_t leave = w.h.pad1[0];
+    if (!(ik || hello || periodic || leave)) return;
     st_add(w, ST_PROC, 1);
     const bool full = a.strategy == PSIM_STRATEGY_FULL;
     w.vn = w.h.act_n; w.in_n = w.h.pas_n;
@@ -403,6 +438,16 @@ DEV void process_pl(Pw& w, uint32_t n, uint32_t ib, uint32_t ik, uint32_t ob) {
     w.seq = 0; w.obase = ob;
     w.snap = NONE; w.dirty = false; w.gossip_due = false;
     w.dc_base = NONE64;
+    w.stop = false;
+    // a manager that stops this round sends nothing: its sends are casts to
+    // itself (schedule_self_message_delivery/6 pl:1585-1609)
+    const uint32_t SC0 = w.SC;
+    const uint64_t dig0 = w.digest;
+
+    if (leave) {                   // leave/1 (pl:502-515, :1390-1420)
+        w.h.pad1[0] = 0;
+        scamp_leave(w, leave - 1);
+    }
 
     if (hello) {                   // internal_join/3 -> connect + hello (pl:1423-1458)
         if (connect_ok(w, w.h.join_contact)) {
@@ -420,13 +465,24 @@ DEV void process_pl(Pw& w, uint32_t n, uint32_t ib, uint32_t ik, uint32_t ob) {
             uint32_t type = rl(R4, b + 2) & 0xFF;
             st_add(w, ST_DELIV + type, 1);
             pl_handle(w, type, rl(R4, b + 1), rl(R4, b + 4), rl(R4, b + 7));
+            if (w.stop) { st_add(w, ST_DROPPED, ik - (c + q) - 1); break; }
         }
+        if (w.stop) break;
     }
-    if (periodic) {                // handle_info(periodic) pl:881-903
+    if (w.stop) {                  // down from the next round, as a crash
+        const uint32_t l2 = lane_id();
+        if ((l2 >= ST_EMIT && l2 < ST_EMIT + PSIM_MSG_NTYPES) || l2 == ST_FAIL)
+            w.SC = SC0;                         // this node's sends and failures undone
+        w.digest = dig0;
+        st_add(w, ST_STOP, 1);
+        if (l2 == 0) a.stop_ids[atomicAdd(a.n_stop, 1u)] = n;
+        w.seq = 0;
+    }
+    if (periodic && !w.stop) {                // handle_info(periodic) pl:881-903
         if (full) w.gossip_due = true;
         else scamp_periodic(w);
     }
-    if (w.gossip_due) full_gossip(w);
+    if (w.gossip_due && !w.stop) full_gossip(w);
 
     // ---- write back
     w.h.act_n = (uint8_t)w.vn; w.h.pas_n = (uint8_t)w.in_n;

@@ -100,6 +100,14 @@ class _Driver:
         nodes = np.ascontiguousarray(nodes, np.uint32)
         self._check(self._api["leave"](self._h, _abi.u32p(nodes), nodes.size), "leave")
 
+    def leave_node(self, actors, targets):
+        """leave/1: actors[i] removes targets[i] (SCAMP v1 / v2 handles)."""
+        a = np.ascontiguousarray(actors, np.uint32)
+        t = np.ascontiguousarray(targets, np.uint32)
+        if a.size != t.size:
+            raise ValueError("actors and targets differ in length")
+        self._check(self._api["leave_node"](self._h, _abi.u32p(a), _abi.u32p(t), a.size), "leave_node")
+
     def set_partition(self, group):
         g = np.ascontiguousarray(group, np.uint8)
         self._check(self._api["set_partition"](

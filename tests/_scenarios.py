@@ -125,6 +125,34 @@ def pl_doubling(make, n, seed, rounds, strategy, fanout=0, crash_at=None, part_a
     return sim, st
 
 
+def pl_leave_remote(make, n, seed, rounds, strategy, leave_at=40, k=16, part_at=None):
+    """SCAMP with leave/1 (psim_leave_node): a doubling bootstrap, then at
+    leave_at k nodes each remove the second entry of their view (the first
+    is themselves); targets distinct.  Returns (sim, stats, actors, targets)."""
+    sim = make(default_config(n_nodes=n, seed=seed, manager=1, strategy=strategy))
+    rng = np.random.Generator(np.random.PCG64([seed, 9]))
+    picked = {}
+
+    def hook(r):
+        if r == leave_at:
+            v = sim.strategy_nodes()
+            actors, targets, used = [], [], set()
+            for x in rng.permutation(n):
+                row = [int(y) for y in v["view"][x][: v["view_n"][x]] if int(y) != x]
+                if row and row[0] not in used and row[0] not in picked.get("a", []) and x not in used:
+                    actors.append(int(x)); targets.append(row[0]); used.update((int(x), row[0]))
+                if len(actors) == k:
+                    break
+            picked["a"], picked["t"] = actors, targets
+            sim.leave_node(np.array(actors, np.uint32), np.array(targets, np.uint32))
+        if part_at is not None and r == part_at:
+            sim.set_partition(W.half_partition(n))
+        if part_at is not None and r == part_at + 10:
+            sim.clear_partition()
+    st = sim.run_schedule(W.doubling_join(n, seed), rounds, extra=hook)
+    return sim, st, np.array(picked["a"], np.uint32), np.array(picked["t"], np.uint32)
+
+
 def compare_strategy(a, b, full_bits=None):
     """strategy_nodes() of two backends; for the full strategy also the
     member bitsets of the nodes in full_bits"""

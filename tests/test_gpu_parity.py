@@ -168,6 +168,21 @@ def test_strategy_leave_parity(strategy):
 
 
 @pytest.mark.parametrize("strategy", [1, 2])
+def test_strategy_remote_leave_parity(strategy):
+    """psim_leave_node (leave/1, stops mid-round dropping the manager's sends,
+    down from the next round) and a partition: bit-identical to the oracle,
+    unsharded and over 4 virtual shards."""
+    def sharded(cfg):
+        cfg.n_shards = 4
+        return _gpu(cfg)
+    os_, ost, _, _ = S.pl_leave_remote(Oracle, 2048, 7, 90, strategy=strategy, part_at=60)
+    for make in (_gpu, sharded):
+        gs, gst, _, _ = S.pl_leave_remote(make, 2048, 7, 90, strategy=strategy, part_at=60)
+        S.compare_stats(gst, ost)
+        S.compare_strategy(gs, os_)
+
+
+@pytest.mark.parametrize("strategy", [1, 2])
 def test_strategy_shard_invariance(strategy):
     def sharded(cfg):
         cfg.n_shards = 4

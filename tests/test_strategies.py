@@ -137,6 +137,51 @@ def test_leave_stops_like_a_crash(strategy):
     assert a["send_fail"][41:].sum() > 0
 
 
+def test_scamp_v2_remote_leave_stops_exactly_the_targets():
+    """leave/1 under SCAMP v2: {bootstrap_remove_subscription, T} reaches T
+    (it is in the actor's partial view), which stops (scamp_v2:192-238);
+    nobody else changes state because of it."""
+    n = 1024
+    sim, st, actors, targets = S.pl_leave_remote(Oracle, n, 5, 60, strategy=2)
+    up = sim.strategy_nodes()["up"].astype(bool)
+    down = set(np.nonzero(~up)[0].tolist())
+    assert down == set(targets.tolist())
+    assert st["emitted"][40, 7] > 0 and st["delivered"][41, 7] == st["emitted"][40, 7]
+
+
+def test_scamp_v1_remote_leave_crashes_every_holder():
+    """leave/1 under SCAMP v1: {remove_subscription, T} to the actor's old
+    membership; every receiver holding T crashes on the swapped
+    sets:del_element/2 arguments (App. A Q12), T itself included, and the
+    actor's view no longer holds T."""
+    n = 1024
+    sim, st, actors, targets = S.pl_leave_remote(Oracle, n, 6, 60, strategy=1)
+    v = sim.strategy_nodes()
+    up = v["up"].astype(bool)
+    assert not up[targets].any()
+    assert (~up).sum() >= len(targets)
+    for x, t in zip(actors, targets):
+        if up[x]:
+            assert t not in v["view"][x][: v["view_n"][x]]
+    # a stopped manager's round sends nothing: emitted == delivered + dropped next round
+    em = st["emitted"].sum(1)
+    assert (em[40:-1] == st["delivered"].sum(1)[41:] + st["dropped"][41:]).all()
+
+
+def test_leave_node_rejections():
+    full = Oracle(default_config(n_nodes=8, manager=1, strategy=0))
+    with pytest.raises(Exception):
+        full.leave_node(np.array([1], np.uint32), np.array([2], np.uint32))
+    hv = Oracle(default_config(n_nodes=8))
+    with pytest.raises(Exception):
+        hv.leave_node(np.array([1], np.uint32), np.array([2], np.uint32))
+    sv = Oracle(default_config(n_nodes=8, manager=1, strategy=1))
+    with pytest.raises(Exception):     # one leave/1 call per actor and round
+        sv.leave_node(np.array([1, 1], np.uint32), np.array([2, 3], np.uint32))
+    with pytest.raises(Exception):
+        sv.leave_node(np.array([1], np.uint32), np.array([9], np.uint32))
+
+
 def test_hyparview_leave_is_an_error():
     """hyparview:363-364: handle_call({leave, _}) replies `error`"""
     sim = Oracle(default_config(n_nodes=8))
