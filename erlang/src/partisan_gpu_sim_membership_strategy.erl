@@ -43,8 +43,15 @@ join(State = #sim_strategy{sim = Sim, me = Me}, #{name := Name}, _RemoteState) -
     ok = partisan_gpu_sim:join(Sim, [Me], [id(Name)]),
     {ok, membership(State), [], State}.
 
-%% leave/2 is not simulated (DESIGN.md section 2b).
-leave(State, _Node) ->
+%% leave/2: the pluggable manager calls it from handle_call({leave, Node})
+%% (pluggable:502-515).  Node = myself is leave/0 (the node stops in the next
+%% round, psim_leave); another node is leave/1 at this node (psim_leave_node:
+%% SCAMP v1 / v2; the full strategy answers {error, unsupported}).
+leave(State = #sim_strategy{sim = Sim, me = Me}, #{name := Name}) ->
+    ok = case id(Name) of
+             Me -> partisan_gpu_sim:leave(Sim, [Me]);
+             T -> partisan_gpu_sim:leave_node(Sim, [Me], [T])
+         end,
     {ok, membership(State), [], State}.
 
 periodic(State = #sim_strategy{sim = Sim, driver = true}) ->
