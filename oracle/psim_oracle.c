@@ -113,7 +113,8 @@ struct psim_handle {
     /* PLUGGABLE handles */
     snode *sn;
     uint32_t W;                     /* full: words per member bitset */
-    uint32_t *fbits;                /* full: N rows of W words (the ORSet's members) */
+    uint32_t *fbits;                /* full: N rows of 2W words: the ORSet's adds, then its
+                                       removes (tombstones); member = add & ~rmv */
     uint32_t *pay_in, *pay_out;     /* full: gossip payload snapshots of rounds r-1 and r */
     size_t pay_out_n, pay_out_cap, pay_in_cap;
 };
@@ -837,11 +838,13 @@ static void process_node(struct psim_handle *h, uint32_t n) {
  * messages go out through do_send_message/7 (pluggable:1309-1363). */
 
 static int is_pl(const struct psim_handle *h) { return h->cfg.manager == PSIM_MANAGER_PLUGGABLE; }
-static uint32_t *fb_row(struct psim_handle *h, uint32_t n) { return h->fbits + (size_t)n * h->W; }
+static uint32_t *fb_row(struct psim_handle *h, uint32_t n) { return h->fbits + (size_t)n * 2 * h->W; }
+/* word w of the member set of a [adds | removes] row */
+static uint32_t fb_mem(const struct psim_handle *h, const uint32_t *b, uint32_t w) { return b[w] & ~b[h->W + w]; }
 
 static uint32_t pl_member(ctx *c, uint32_t p) {
     struct psim_handle *h = c->h;
-    if (h->cfg.strategy == PSIM_STRATEGY_FULL) return (fb_row(h, c->me)[p >> 5] >> (p & 31u)) & 1u;
+    if (h->cfg.strategy == PSIM_STRATEGY_FULL) return (fb_mem(h, fb_row(h, c->me), p >> 5) >> (p & 31u)) & 1u;
     snode *q = &h->sn[c->me];
     return (uint32_t)list_member(q->view, q->view_n, p);
 }
@@ -856,7 +859,10 @@ static void pl_emit(ctx *c, uint32_t dst, uint32_t type, uint32_t a0, uint32_t s
  * iff Peer is one of them, runs and is not partitioned away; a successful
  * dispatch draws rand:uniform(1) (partisan_util:dispatch_pid/3 util:190-195). */
 static int pl_send(ctx *c, uint32_t dst, uint32_t type, uint32_t a0, uint32_t slot) {
-    if (!connect_ok(c, dst) || !(pl_member(c, dst) || dst == c->h->sn[c->me].pending)) {
+    /* full: every target comes from the node's own member row, or is an old
+     * member whose connection is still open (leave/1) */
+    int full = c->h->cfg.strategy == PSIM_STRATEGY_FULL;
+    if (!connect_ok(c, dst) || !(full || pl_member(c, dst) || dst == c->h->sn[c->me].pending)) {
         c->h->st->send_fail++;
         return 0;
     }
@@ -870,14 +876,14 @@ static uint32_t popcount32(uint32_t x) { return (uint32_t)__builtin_popcount(x);
 
 static uint32_t full_count(struct psim_handle *h, const uint32_t *b) {
     uint32_t k = 0;
-    for (uint32_t w = 0; w < h->W; w++) k += popcount32(b[w]);
+    for (uint32_t w = 0; w < h->W; w++) k += popcount32(fb_mem(h, b, w));
     return k;
 }
 
 /* the k-th (0-based) member in id order */
 static uint32_t full_nth(struct psim_handle *h, const uint32_t *b, uint32_t k) {
     for (uint32_t w = 0; w < h->W; w++) {
-        uint32_t x = b[w], pc = popcount32(x);
+        uint32_t x = fb_mem(h, b, w), pc = popcount32(x);
         if (k < pc) {
             for (; k; k--) x &= x - 1;
             return w * 32 + (uint32_t)__builtin_ctz(x);
@@ -894,9 +900,9 @@ static uint32_t full_snapshot(ctx *c) {
     if (c->snap != PSIM_NONE && !c->dirty) return c->snap;
     if (h->pay_out_n == h->pay_out_cap) {
         h->pay_out_cap = h->pay_out_cap ? h->pay_out_cap * 2 : 64;
-        h->pay_out = (uint32_t *)realloc(h->pay_out, h->pay_out_cap * h->W * sizeof(uint32_t));
+        h->pay_out = (uint32_t *)realloc(h->pay_out, h->pay_out_cap * 2 * h->W * sizeof(uint32_t));
     }
-    memcpy(h->pay_out + h->pay_out_n * h->W, fb_row(h, c->me), h->W * sizeof(uint32_t));
+    memcpy(h->pay_out + h->pay_out_n * 2 * h->W, fb_row(h, c->me), 2 * h->W * sizeof(uint32_t));
     c->snap = (uint32_t)h->pay_out_n++;
     c->dirty = 0;
     return c->snap;
@@ -917,7 +923,7 @@ static void full_gossip(ctx *c) {
     uint32_t slot = full_snapshot(c), cnt = full_count(h, b);
     if (h->cfg.fanout == 0) {
         for (uint32_t w = 0; w < h->W; w++)
-            for (uint32_t x = b[w]; x; x &= x - 1)
+            for (uint32_t x = fb_mem(h, b, w); x; x &= x - 1)
                 pl_send(c, w * 32 + (uint32_t)__builtin_ctz(x), PSIM_PL_GOSSIP, cnt, slot);
         return;
     }
@@ -931,7 +937,7 @@ static int full_merge(ctx *c, const uint32_t *p) {
     struct psim_handle *h = c->h;
     uint32_t *b = fb_row(h, c->me);
     int equal = 1;
-    for (uint32_t w = 0; w < h->W; w++) {
+    for (uint32_t w = 0; w < 2 * h->W; w++) {     /* adds and removes */
         if (b[w] != p[w]) equal = 0;
         uint32_t m = b[w] | p[w];
         if (m != b[w]) { b[w] = m; c->dirty = 1; }
@@ -1047,6 +1053,25 @@ static void scamp_leave(ctx *c, uint32_t t) {
     }
 }
 
+/* leave/1 of the full strategy at the actor, NameToRemove = t (full:58-89):
+ * ?SET:mutate({rmv, N}) of t's spec if it is a member (its add is
+ * tombstoned), then gossip_messages(State0, StateToGossip): the new state to
+ * every member of the OLD list (t included).  fanout > 0 (config B's
+ * extension): the coalesced gossip of the round instead. */
+static void full_leave(ctx *c, uint32_t t) {
+    struct psim_handle *h = c->h;
+    uint32_t *b = fb_row(h, c->me);
+    uint32_t was = (fb_mem(h, b, t >> 5) >> (t & 31u)) & 1u;
+    if (was) { b[h->W + (t >> 5)] |= 1u << (t & 31u); c->dirty = 1; }
+    if (h->cfg.fanout) { c->gossip_due = 1; return; }
+    uint32_t slot = full_snapshot(c), cnt = full_count(h, b);
+    for (uint32_t w = 0; w < h->W; w++) {
+        uint32_t x = fb_mem(h, b, w);
+        if (was && w == (t >> 5)) x |= 1u << (t & 31u);
+        for (; x; x &= x - 1) pl_send(c, w * 32 + (uint32_t)__builtin_ctz(x), PSIM_PL_GOSSIP, cnt, slot);
+    }
+}
+
 /* ------------------------------------------------------------- driver -- */
 static void pl_handle(ctx *c, const omsg *m) {
     struct psim_handle *h = c->h;
@@ -1062,7 +1087,7 @@ static void pl_handle(ctx *c, const omsg *m) {
         if (q->pending != m->src) break;
         q->pending = PSIM_NONE;
         if (full) {           /* join/3 full:49-55: merge, then gossip */
-            full_merge(c, h->pay_in + (size_t)m->slot * h->W);
+            full_merge(c, h->pay_in + (size_t)m->slot * 2 * h->W);
             if (h->cfg.fanout) c->gossip_due = 1;
             else full_gossip(c);
         } else {
@@ -1071,7 +1096,10 @@ static void pl_handle(ctx *c, const omsg *m) {
         break;
     case PSIM_PL_GOSSIP:      /* handle_message/2 full:99-116 */
         if (!full) break;
-        if (!full_merge(c, h->pay_in + (size_t)m->slot * h->W)) {
+        if (!full_merge(c, h->pay_in + (size_t)m->slot * 2 * h->W)) {
+            /* a merged removal of ourselves: the manager stops
+               (pluggable:1182-1188) before the gossip it cast goes out */
+            if (!pl_member(c, c->me)) { c->stop = 1; break; }
             if (h->cfg.fanout) c->gossip_due = 1;
             else full_gossip(c);
         }
@@ -1123,7 +1151,8 @@ static void pl_process_node(struct psim_handle *h, uint32_t n) {
     memcpy(em0, h->st->emitted, sizeof em0);
     if (leave) {              /* leave/1 (pluggable:502-515, :1390-1420) */
         q->leave_tgt = 0;
-        scamp_leave(&c, leave - 1);
+        if (h->cfg.strategy == PSIM_STRATEGY_FULL) full_leave(&c, leave - 1);
+        else scamp_leave(&c, leave - 1);
     }
     if (hello) {              /* establish_connections -> client connect + hello */
         if (connect_ok(&c, q->pending)) { pl_emit(&c, q->pending, PSIM_PL_HELLO, 0, PSIM_NONE); q->hello_sent = 1; }
@@ -1158,7 +1187,7 @@ static void pl_node_init(struct psim_handle *h, uint32_t n, uint32_t contact) {
     if (h->cfg.strategy == PSIM_STRATEGY_FULL) {
         q->view_n = 0; q->view[0] = 0;
         uint32_t *b = fb_row(h, n);
-        memset(b, 0, h->W * sizeof(uint32_t));
+        memset(b, 0, 2 * h->W * sizeof(uint32_t));
         b[n >> 5] |= 1u << (n & 31u);            /* new_state/1 full:171-175 */
     }
 }
@@ -1305,7 +1334,7 @@ int orc_create(const psim_config *cfg, struct psim_handle **out) {
         if (!h->sn) return PSIM_ENOMEM;
         if (full) {
             h->W = (h->N + 31) / 32;
-            h->fbits = (uint32_t *)calloc((size_t)h->N * h->W, sizeof(uint32_t));
+            h->fbits = (uint32_t *)calloc((size_t)h->N * 2 * h->W, sizeof(uint32_t));
             if (!h->fbits) return PSIM_ENOMEM;
         }
     }
@@ -1381,8 +1410,7 @@ int orc_leave(struct psim_handle *h, const uint32_t *nodes, size_t n) {
  * remove tombstones the member bitsets do not hold; one call per actor and
  * round; unsharded handles only (a stop is known on its own shard). */
 int orc_leave_node(struct psim_handle *h, const uint32_t *actors, const uint32_t *targets, size_t n) {
-    if (!is_pl(h) || h->cfg.strategy == PSIM_STRATEGY_FULL || h->lo != 0 || h->hi != h->N)
-        return PSIM_EUNSUPPORTED;
+    if (!is_pl(h) || h->lo != 0 || h->hi != h->N) return PSIM_EUNSUPPORTED;
     for (size_t i = 0; i < n; i++) {
         if (actors[i] >= h->N || targets[i] >= h->N) return PSIM_ERANGE;
         for (size_t j = 0; j < h->pend_lv_n; j++) if (h->pend_lv_a[j] == actors[i]) return PSIM_EINVAL;
@@ -1536,7 +1564,7 @@ int orc_get_histograms(struct psim_handle *h, psim_histograms *out) {
 static uint64_t members_hash(struct psim_handle *h, const uint32_t *b) {
     uint64_t x = 0;
     for (uint32_t w = 0; w < h->W; w++)
-        for (uint32_t v = b[w]; v; v &= v - 1) x += mix64((uint64_t)(w * 32 + (uint32_t)__builtin_ctz(v)) + 1);
+        for (uint32_t v = fb_mem(h, b, w); v; v &= v - 1) x += mix64((uint64_t)(w * 32 + (uint32_t)__builtin_ctz(v)) + 1);
     return x;
 }
 
@@ -1567,7 +1595,8 @@ int orc_get_member_bits(struct psim_handle *h, uint32_t node, uint32_t *words, s
     if (!h->fbits) return PSIM_ESTATE;
     if (node >= h->N) return PSIM_ERANGE;
     if (n_words < h->W) return PSIM_EINVAL;
-    memcpy(words, fb_row(h, node), h->W * sizeof(uint32_t));
+    const uint32_t *b = fb_row(h, node);
+    for (uint32_t w = 0; w < h->W; w++) words[w] = fb_mem(h, b, w);
     return PSIM_OK;
 }
 

@@ -142,7 +142,7 @@ __global__ void k_join(RoundArgs a, uint32_t* start, const uint32_t* ids, const 
         x.act_n = a.strategy == PSIM_STRATEGY_FULL ? 0 : 1;
         x.pas_n = 0; x.all_n = 0; x.com_n = 0;
         if (a.strategy == PSIM_STRATEGY_FULL) {
-            a.fbits[(size_t)li * a.fw + (id >> 5)] |= 1u << (id & 31u);   // new_state/1 full:171-175
+            a.fbits[(size_t)li * 2 * a.fw + (id >> 5)] |= 1u << (id & 31u);   // new_state/1 full:171-175
         } else {
             for (int k = 0; k < PSIM_SVIEW_CAP; k++) {
                 a.sview[(size_t)li * PSIM_SVIEW_CAP + k] = k == 0 ? id : 0u;   // [Myself]
@@ -567,7 +567,8 @@ __global__ void __launch_bounds__(256) k_node_prep(RoundArgs a, const uint32_t* 
                 bool per = due(a.periodic, r, st);
                 bool leave = x.pad1[0] != 0;
                 if (a.strategy == PSIM_STRATEGY_FULL)
-                    b = a.fanout ? (uint64_t)c + a.fanout + 1 : ((uint64_t)c + 2) * (a.n_nodes + 1);
+                    b = a.fanout ? (uint64_t)c + a.fanout + 1
+                                 : ((uint64_t)c + 2 + (leave ? 1 : 0)) * (a.n_nodes + 1);
                 else
                     b = (uint64_t)c + (pending ? 2 + PSIM_SVIEW_CAP + a.scamp_c : 0) +
                         (per ? 1 + PSIM_SVIEW_CAP : 0) + (leave ? PSIM_SVIEW_CAP : 0) + 1;
@@ -876,6 +877,7 @@ struct Shard {
     DBuf<uint64_t> bound, pscan, obase, stat_part, stat_out, d_off;   // bound: packed (bound << 32 | work)
     DBuf<uint8_t> cub_tmp;
     DBuf<uint32_t> ev_ids, ev_contacts, stop_ids, n_stop;
+    bool tomb_live = false;             // full: snapshots carry their remove rows
     DBuf<Msg> sendbuf;
     // pluggable manager
     DBuf<uint32_t> sview, sinv, fbits, pay[2], pay_top;
@@ -918,7 +920,8 @@ struct psim_handle {
     bool pend_bcast = false;
     uint32_t pend_root = 0, pend_msg = 0;
     uint32_t bcast_root = PSIM_NONE, tracked_msg = PSIM_NONE;
-    uint32_t fw = 0;                    // full strategy: words per member row
+    uint32_t fw = 0;                    // full strategy: words per member row (adds; removes beside)
+    bool tomb = false;                  // full: an ORSet remove exists (leave/1): kernels read remove rows
     std::vector<uint8_t> started;       // full strategy: ids ever started (no restarts)
     double kt_ms[KT_N] = {0};
     uint64_t kt_n[KT_N] = {0};
@@ -953,7 +956,7 @@ RoundArgs make_args(psim_handle* h, Shard* s) {
     a.start = s->start.p;
     a.pl = c.manager == PSIM_MANAGER_PLUGGABLE;
     a.strategy = c.strategy; a.periodic = c.periodic_interval; a.scamp_c = c.scamp_c;
-    a.fanout = c.fanout; a.fw = h->fw;
+    a.fanout = c.fanout; a.fw = h->fw; a.tomb = h->tomb;
     a.fbits = s->fbits.p; a.sview = s->sview.p; a.sinv = s->sinv.p;
     a.ktime = reinterpret_cast<unsigned long long*>(s->stat_out.p + NST);
     a.desc_slow = s->desc_slow.p; a.n_slow = s->n_slow.p;
@@ -1131,11 +1134,20 @@ int phase_consume(psim_handle* h, Shard* s, RoundArgs& a) {
         // snapshots: at most one per node plus one per inbox message
         uint64_t slots = (uint64_t)s->m_in + s->n + 1;
         if (slots > 0xFFFFFFFFull) return PSIM_ENOMEM;
-        TRY(s->pay[s->pay_cur].ensure(slots * h->fw));
+        TRY(s->pay[s->pay_cur].ensure(slots * 2 * h->fw));
+        if (h->tomb && !s->tomb_live) {
+            // the first round with removes: last round's snapshots were
+            // written without their remove rows
+            DBuf<uint32_t>& in = s->pay[s->pay_cur ^ 1];
+            const size_t rows = in.n / (2 * h->fw);
+            if (rows)
+                HIP_TRY(hipMemset2DAsync(in.p + h->fw, 2 * h->fw * 4, 0, h->fw * 4, rows, s->stream));
+            s->tomb_live = true;
+        }
         a.pay_out = s->pay[s->pay_cur].p;
         a.pay_in = s->pay[s->pay_cur ^ 1].p;
         a.pay_top = s->pay_top.p;
-        a.pay_cap = (uint32_t)(s->pay[s->pay_cur].n / h->fw);
+        a.pay_cap = (uint32_t)(s->pay[s->pay_cur].n / (2 * h->fw));
         HIP_TRY(hipMemsetAsync(s->pay_top.p, 0, 4, s->stream));
     }
     if (a.pl) {
@@ -1466,9 +1478,9 @@ int shard_alloc(psim_handle* h, Shard* s) {
     rc |= s->recvbuf.alloc(1024); rc |= s->inbox[0].alloc(1024); rc |= s->inbox[1].alloc(1024); rc |= s->outbox.alloc(1024);
     if (h->cfg.manager == PSIM_MANAGER_PLUGGABLE) {
         if (h->cfg.strategy == PSIM_STRATEGY_FULL) {
-            rc |= s->fbits.alloc(n * h->fw);
+            rc |= s->fbits.alloc(n * 2 * h->fw);     // [adds | removes] per node
             rc |= s->pay_top.alloc(1);
-            rc |= s->pay[0].alloc(h->fw); rc |= s->pay[1].alloc(h->fw);
+            rc |= s->pay[0].alloc(2 * h->fw); rc |= s->pay[1].alloc(2 * h->fw);
         } else {
             rc |= s->sview.alloc(n * PSIM_SVIEW_CAP);
             if (h->cfg.strategy == PSIM_STRATEGY_SCAMP_V2) rc |= s->sinv.alloc(n * PSIM_SVIEW_CAP);
@@ -1669,8 +1681,7 @@ int psim_leave(psim_handle* h, const uint32_t* nodes, size_t n) {
 // handles (a stop is learned from the owner shard's list after the round).
 int psim_leave_node(psim_handle* h, const uint32_t* actors, const uint32_t* targets, size_t n) {
     if (!h || (n && (!actors || !targets))) return PSIM_EINVAL;
-    if (h->cfg.manager != PSIM_MANAGER_PLUGGABLE || h->cfg.strategy == PSIM_STRATEGY_FULL || h->world > 1)
-        return PSIM_EUNSUPPORTED;
+    if (h->cfg.manager != PSIM_MANAGER_PLUGGABLE || h->world > 1) return PSIM_EUNSUPPORTED;
     for (size_t i = 0; i < n; i++) {
         if (actors[i] >= h->N || targets[i] >= h->N) return PSIM_ERANGE;
         for (uint32_t a : h->pend_lv_a) if (a == actors[i]) return PSIM_EINVAL;
@@ -1678,6 +1689,7 @@ int psim_leave_node(psim_handle* h, const uint32_t* actors, const uint32_t* targ
     }
     for (size_t i = 0; i < n; i++) {
         if (actors[i] == targets[i]) { TRY(psim_crash(h, &actors[i], 1)); continue; }
+        if (h->cfg.strategy == PSIM_STRATEGY_FULL) h->tomb = true;
         h->pend_lv_a.push_back(actors[i]);
         h->pend_lv_t.push_back(targets[i]);
     }
@@ -1844,8 +1856,8 @@ int psim_get_strategy_nodes(psim_handle* h, uint32_t first, uint32_t count, psim
         HIP_TRY(hipMemcpyAsync(hd.data(), s->hdr.p + li, k * sizeof(Hdr), hipMemcpyDeviceToHost, s->stream));
         HIP_TRY(hipMemcpyAsync(fl.data(), s->flags.p + id, k, hipMemcpyDeviceToHost, s->stream));
         if (full) {
-            rows.resize((size_t)k * h->fw);
-            HIP_TRY(hipMemcpyAsync(rows.data(), s->fbits.p + li * h->fw, rows.size() * 4,
+            rows.resize((size_t)k * 2 * h->fw);
+            HIP_TRY(hipMemcpyAsync(rows.data(), s->fbits.p + li * 2 * h->fw, rows.size() * 4,
                                    hipMemcpyDeviceToHost, s->stream));
         } else {
             view.resize((size_t)k * PSIM_SVIEW_CAP);
@@ -1868,11 +1880,15 @@ int psim_get_strategy_nodes(psim_handle* h, uint32_t first, uint32_t count, psim
             v->last_ping = started ? x.pt_root : PSIM_NONE;
             v->view_n = x.act_n; v->in_n = x.pas_n;
             if (full) {
-                const uint32_t* row = &rows[(size_t)j * h->fw];
+                const uint32_t* row = &rows[(size_t)j * 2 * h->fw];
+                std::vector<uint32_t> mem(h->fw);
                 uint32_t c = 0;
-                for (uint32_t w = 0; w < h->fw; w++) c += (uint32_t)__builtin_popcount(row[w]);
+                for (uint32_t w = 0; w < h->fw; w++) {
+                    mem[w] = row[w] & ~row[h->fw + w];       // add & ~remove
+                    c += (uint32_t)__builtin_popcount(mem[w]);
+                }
                 v->members = c;
-                v->members_hash = members_hash(row, h->fw);
+                v->members_hash = members_hash(mem.data(), h->fw);
             } else {
                 memcpy(v->view, &view[(size_t)j * PSIM_SVIEW_CAP], sizeof v->view);
                 if (!inv.empty()) memcpy(v->in_view, &inv[(size_t)j * PSIM_SVIEW_CAP], sizeof v->in_view);
@@ -1892,9 +1908,11 @@ int psim_get_member_bits(psim_handle* h, uint32_t node, uint32_t* words, size_t 
     if (hipSetDevice(h->device) != hipSuccess) return PSIM_EDEVICE;
     Shard* s = owner_of(h, node);
     if (!s) return PSIM_ERANGE;
-    HIP_TRY(hipMemcpyAsync(words, s->fbits.p + (size_t)(node - s->lo) * h->fw, W * 4, hipMemcpyDeviceToHost,
-                           s->stream));
+    std::vector<uint32_t> row(2 * h->fw);
+    HIP_TRY(hipMemcpyAsync(row.data(), s->fbits.p + (size_t)(node - s->lo) * 2 * h->fw, row.size() * 4,
+                           hipMemcpyDeviceToHost, s->stream));
     HIP_TRY(hipStreamSynchronize(s->stream));
+    for (uint32_t w = 0; w < W; w++) words[w] = row[w] & ~row[h->fw + w];
     return PSIM_OK;
 }
 
@@ -2032,8 +2050,8 @@ static std::vector<Section> snap_sections(psim_handle* h, Shard* s, const ShardH
     if (h->cfg.manager == PSIM_MANAGER_PLUGGABLE) {
         if (s->sview.p) v.push_back({s->sview.p, n * PSIM_SVIEW_CAP * 4});
         if (s->sinv.p) v.push_back({s->sinv.p, n * PSIM_SVIEW_CAP * 4});
-        if (s->fbits.p) v.push_back({s->fbits.p, n * h->fw * 4});
-        if (sh.pay_rows) v.push_back({s->pay[sh.pay_cur ^ 1].p, (size_t)sh.pay_rows * h->fw * 4});
+        if (s->fbits.p) v.push_back({s->fbits.p, n * 2 * h->fw * 4});
+        if (sh.pay_rows) v.push_back({s->pay[sh.pay_cur ^ 1].p, (size_t)sh.pay_rows * 2 * h->fw * 4});
     }
     return v;
 }
@@ -2051,6 +2069,7 @@ int psim_snapshot(psim_handle* h, void* buf, size_t cap, size_t* need) {
         ShardHead sh{s->lo, s->n, s->m_in, (uint32_t)s->in_cur, (uint32_t)s->pay_cur, 0, {0, 0}};
         if (h->cfg.manager == PSIM_MANAGER_PLUGGABLE && s->pay_top.p)
             sh.pay_rows = read1(s, s->pay_top.p);
+        sh.pad[0] = s->tomb_live ? 1u : 0u;            // full: snapshots carry remove rows
         heads.push_back(sh);
         total += sizeof(ShardHead);
         for (const Section& x : snap_sections(h, s, sh)) total += x.bytes;
@@ -2095,8 +2114,10 @@ int psim_restore(psim_handle* h, const void* buf, size_t size) {
         memcpy(&sh, o, sizeof sh); o += sizeof sh;
         if (sh.lo != s->lo || sh.n != s->n) return PSIM_EINVAL;
         s->m_in = sh.m_in; s->in_cur = (int)sh.in_cur; s->pay_cur = (int)sh.pay_cur;
+        s->tomb_live = sh.pad[0] != 0;
+        if (s->tomb_live) h->tomb = true;
         TRY(s->inbox[s->in_cur].ensure((size_t)sh.m_in + 1));
-        if (sh.pay_rows) TRY(s->pay[s->pay_cur ^ 1].ensure((size_t)sh.pay_rows * h->fw));
+        if (sh.pay_rows) TRY(s->pay[s->pay_cur ^ 1].ensure((size_t)sh.pay_rows * 2 * h->fw));
         if (h->cfg.manager == PSIM_MANAGER_PLUGGABLE && s->pay_top.p)
             HIP_TRY(hipMemcpy(s->pay_top.p, &sh.pay_rows, 4, hipMemcpyHostToDevice));
         for (const Section& x : snap_sections(h, s, sh)) {

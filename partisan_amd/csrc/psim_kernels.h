@@ -45,7 +45,9 @@ struct RoundArgs {
     // join_contact = pending contact, pt_root = last ping round,
     // have = hello sent, act_n = view length, pas_n = in_view length
     uint32_t pl, strategy, periodic, scamp_c, fanout;
-    uint32_t fw;                 // full: words per member bitset row (multiple of 4)
+    uint32_t fw;                 // full: words per member bitset (multiple of 4); a node's row
+                                 // is 2 fw words: adds, then removes (ORSet tombstones)
+    uint32_t tomb;               // full: removes exist -- read and carry the remove rows
     uint32_t* fbits;             // full: n_local rows of fw words
     const uint32_t* pay_in;      // full: snapshots read this round (slot * fw)
     uint32_t* pay_out;           // full: snapshots written this round

@@ -159,7 +159,7 @@ DEV void pl_send(Pw& w, uint32_t dst, uint32_t type, uint32_t a0, uint32_t slot)
 // ?SET:merge/2 into the row (full:49-55, :99-116); returns ?SET:equal/2 of
 // the two states before it
 DEV bool full_merge(Pw& w, const uint32_t* p) {
-    const uint32_t fw = w.a->fw;
+    const uint32_t fw = w.a->tomb ? 2 * w.a->fw : w.a->fw;   // adds (+ removes)
     bool neq = false, chg = false;
     for (uint32_t base = 0; base < fw; base += 256) {
         uint32_t i = base + 4 * lane_id();
@@ -179,13 +179,23 @@ DEV bool full_merge(Pw& w, const uint32_t* p) {
     return ballot(neq) == 0;
 }
 
+// four member words (add & ~remove) of the node's row at word i
+DEV uint4 mem4(const Pw& w, uint32_t i) {
+    uint4 o = *reinterpret_cast<const uint4*>(w.row + i);
+    if (w.a->tomb) {
+        const uint4 t = *reinterpret_cast<const uint4*>(w.row + w.a->fw + i);
+        o = make_uint4(o.x & ~t.x, o.y & ~t.y, o.z & ~t.z, o.w & ~t.w);
+    }
+    return o;
+}
+
 DEV uint32_t full_count(const Pw& w) {
     const uint32_t fw = w.a->fw;
     uint32_t c = 0;
     for (uint32_t base = 0; base < fw; base += 256) {
         uint32_t i = base + 4 * lane_id();
         if (i < fw) {
-            uint4 o = *reinterpret_cast<const uint4*>(w.row + i);
+            uint4 o = mem4(w, i);
             c += __popc(o.x) + __popc(o.y) + __popc(o.z) + __popc(o.w);
         }
     }
@@ -199,7 +209,7 @@ DEV uint32_t full_nth(const Pw& w, uint32_t k) {
     const uint32_t l = lane_id();
     for (uint32_t base = 0; base < fw; base += 256) {
         uint32_t i = base + 4 * l;
-        uint4 o = i < fw ? *reinterpret_cast<const uint4*>(w.row + i) : make_uint4(0, 0, 0, 0);
+        uint4 o = i < fw ? mem4(w, i) : make_uint4(0, 0, 0, 0);
         uint32_t inc = __popc(o.x) + __popc(o.y) + __popc(o.z) + __popc(o.w);
 #pragma unroll
         for (int off = 1; off < 64; off <<= 1) {
@@ -235,8 +245,8 @@ DEV uint32_t full_snapshot(Pw& w) {
     if (lane_id() == 0) s = atomicAdd(w.a->pay_top, 1u);
     s = rl(s, 0);
     if (s >= w.a->pay_cap) { st_add(w, ST_OVF, 1); s = w.a->pay_cap - 1; }
-    const uint32_t fw = w.a->fw;
-    uint32_t* dst = w.a->pay_out + (size_t)s * fw;
+    const uint32_t fw = w.a->tomb ? 2 * w.a->fw : w.a->fw;   // adds (+ removes)
+    uint32_t* dst = w.a->pay_out + (size_t)s * 2 * w.a->fw;
     for (uint32_t base = 0; base < fw; base += 256) {
         uint32_t i = base + 4 * lane_id();
         if (i < fw) *reinterpret_cast<uint4*>(dst + i) = *reinterpret_cast<const uint4*>(w.row + i);
@@ -251,13 +261,18 @@ DEV uint32_t full_snapshot(Pw& w) {
 // `fanout` members each drawn as rand:uniform(length(Members)) -- config B's
 // extension, coalesced to one gossip per round.  The
 // whole list is built before the manager sends any of it.
-DEV void full_gossip(Pw& w) {
+DEV void full_gossip(Pw& w, uint32_t extra = NONE) {
     uint32_t slot = full_snapshot(w), cnt = full_count(w);
     const uint32_t fw = w.a->fw;
     if (w.a->fanout == 0) {
         for (uint32_t base = 0; base < fw; base += 256) {
             uint32_t i = base + 4 * lane_id();
-            uint4 o = i < fw ? *reinterpret_cast<const uint4*>(w.row + i) : make_uint4(0, 0, 0, 0);
+            uint4 o = i < fw ? mem4(w, i) : make_uint4(0, 0, 0, 0);
+            if (extra != NONE && i == ((extra >> 5) & ~3u)) {    // an old member (leave/1)
+                const uint32_t b = 1u << (extra & 31u), q = (extra >> 5) & 3u;
+                o.x |= q == 0 ? b : 0u; o.y |= q == 1 ? b : 0u;
+                o.z |= q == 2 ? b : 0u; o.w |= q == 3 ? b : 0u;
+            }
             for (uint64_t nz = ballot((o.x | o.y | o.z | o.w) != 0); nz; nz &= nz - 1) {
                 int L = ffs64(nz);
                 uint32_t ws[4] = {rl(o.x, L), rl(o.y, L), rl(o.z, L), rl(o.w, L)};
@@ -349,6 +364,23 @@ DEV void scamp_leave(Pw& w, uint32_t t) {
     }
 }
 
+// leave/1 of the full strategy at the actor (full:58-89): the target's add is
+// tombstoned if it is a member, then the new state goes to every member of
+// the OLD list (the target included); fanout > 0: the round's coalesced gossip
+DEV void full_leave(Pw& w, uint32_t t) {
+    const uint32_t wi = t >> 5, bit = 1u << (t & 31u);
+    const bool was = (w.row[wi] & ~w.row[w.a->fw + wi] & bit) != 0;   // (tomb is on)
+    __builtin_amdgcn_wave_barrier();
+    if (was) {
+        if (lane_id() == 0) w.row[w.a->fw + wi] |= bit;
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        w.dirty = true;
+    }
+    if (w.a->fanout) { w.gossip_due = true; return; }
+    full_gossip(w, was ? t : NONE);
+}
+
 // -------------------------------------------------------------- driver --
 DEV void pl_handle(Pw& w, uint32_t type, uint32_t src, uint32_t a0, uint32_t slot) {
     const bool full = w.a->strategy == PSIM_STRATEGY_FULL;
@@ -366,7 +398,7 @@ DEV void pl_handle(Pw& w, uint32_t type, uint32_t src, uint32_t a0, uint32_t slo
         if (w.h.join_contact != src) break;
         w.h.join_contact = NONE;
         if (full) {                // join/3 full:49-55
-            full_merge(w, w.a->pay_in + (size_t)slot * w.a->fw);
+            full_merge(w, w.a->pay_in + (size_t)slot * 2 * w.a->fw);
             if (w.a->fanout) w.gossip_due = true;
             else full_gossip(w);
         } else {
@@ -375,7 +407,10 @@ DEV void pl_handle(Pw& w, uint32_t type, uint32_t src, uint32_t a0, uint32_t slo
         break;
     case PSIM_PL_GOSSIP:           // handle_message/2 full:99-116
         if (!full) break;
-        if (!full_merge(w, w.a->pay_in + (size_t)slot * w.a->fw)) {
+        if (!full_merge(w, w.a->pay_in + (size_t)slot * 2 * w.a->fw)) {
+            // a merged removal of ourselves: the manager stops (pl:1182-1188)
+            // before the gossip it cast goes out
+            if (w.a->tomb && ((w.row[w.a->fw + (w.me >> 5)] >> (w.me & 31u)) & 1u)) { w.stop = true; break; }
             if (w.a->fanout) w.gossip_due = true;
             else full_gossip(w);
         }
@@ -434,7 +469,7 @@ DEV void process_pl(Pw& w, uint32_t n, uint32_t ib, uint32_t ik, uint32_t ob) {
     const uint32_t V0 = w.V, I0 = w.I;
     w.CV = l < w.vn ? w.V : NONE;
     w.CF = w.CV < a.n_nodes ? ((uint32_t)a.flags[w.CV] | ((uint32_t)a.part[w.CV] << 8)) : 0u;
-    w.row = full ? a.fbits + (size_t)li * a.fw : nullptr;
+    w.row = full ? a.fbits + (size_t)li * 2 * a.fw : nullptr;
     w.seq = 0; w.obase = ob;
     w.snap = NONE; w.dirty = false; w.gossip_due = false;
     w.dc_base = NONE64;
@@ -446,7 +481,8 @@ DEV void process_pl(Pw& w, uint32_t n, uint32_t ib, uint32_t ik, uint32_t ob) {
 
     if (leave) {                   // leave/1 (pl:502-515, :1390-1420)
         w.h.pad1[0] = 0;
-        scamp_leave(w, leave - 1);
+        if (full) full_leave(w, leave - 1);
+        else scamp_leave(w, leave - 1);
     }
 
     if (hello) {                   // internal_join/3 -> connect + hello (pl:1423-1458)

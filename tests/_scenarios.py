@@ -125,11 +125,12 @@ def pl_doubling(make, n, seed, rounds, strategy, fanout=0, crash_at=None, part_a
     return sim, st
 
 
-def pl_leave_remote(make, n, seed, rounds, strategy, leave_at=40, k=16, part_at=None):
+def pl_leave_remote(make, n, seed, rounds, strategy, leave_at=40, k=16, part_at=None, fanout=0):
     """SCAMP with leave/1 (psim_leave_node): a doubling bootstrap, then at
     leave_at k nodes each remove the second entry of their view (the first
-    is themselves); targets distinct.  Returns (sim, stats, actors, targets)."""
-    sim = make(default_config(n_nodes=n, seed=seed, manager=1, strategy=strategy))
+    is themselves; full strategy: a random other node); targets distinct.
+    Returns (sim, stats, actors, targets)."""
+    sim = make(default_config(n_nodes=n, seed=seed, manager=1, strategy=strategy, fanout=fanout))
     rng = np.random.Generator(np.random.PCG64([seed, 9]))
     picked = {}
 
@@ -138,7 +139,10 @@ def pl_leave_remote(make, n, seed, rounds, strategy, leave_at=40, k=16, part_at=
             v = sim.strategy_nodes()
             actors, targets, used = [], [], set()
             for x in rng.permutation(n):
-                row = [int(y) for y in v["view"][x][: v["view_n"][x]] if int(y) != x]
+                if strategy == 0:
+                    row = [int(y) for y in rng.permutation(n)[:4] if int(y) != x]
+                else:
+                    row = [int(y) for y in v["view"][x][: v["view_n"][x]] if int(y) != x]
                 if row and row[0] not in used and row[0] not in picked.get("a", []) and x not in used:
                     actors.append(int(x)); targets.append(row[0]); used.update((int(x), row[0]))
                 if len(actors) == k:

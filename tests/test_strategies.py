@@ -168,10 +168,29 @@ def test_scamp_v1_remote_leave_crashes_every_holder():
     assert (em[40:-1] == st["delivered"].sum(1)[41:] + st["dropped"][41:]).all()
 
 
+@pytest.mark.parametrize("fanout", [0, 5])
+def test_full_remote_leave_tombstones(fanout):
+    """leave/1 under the full strategy (full:58-89): the actor tombstones the
+    target's add and gossips; the removal spreads by merge (adds and removes
+    OR-ed) until every running member agrees on n - k members; with the
+    reference's gossip-to-all (fanout 0) every target gets the actor's
+    gossip, finds itself removed and stops (pluggable:1182-1188)."""
+    n = 32 if fanout == 0 else 1024          # fanout 0: |members| messages per gossip
+    sim, st, actors, targets = S.pl_leave_remote(Oracle, n, 3, 90, strategy=0, fanout=fanout, k=4)
+    v = sim.strategy_nodes()
+    up = v["up"].astype(bool)
+    if fanout == 0:
+        assert not up[targets].any()
+        assert up.sum() == n - len(targets)
+    others = up.copy()
+    others[targets] = False                 # (fanout 5: a target nobody gossiped to yet runs on)
+    assert (v["members"][others] == n - len(targets)).all()
+    bits = sim.member_bits(int(np.nonzero(others)[0][0]))
+    ids = {i for i in range(n) if (int(bits[i >> 5]) >> (i & 31)) & 1}
+    assert not ids & set(targets.tolist())
+
+
 def test_leave_node_rejections():
-    full = Oracle(default_config(n_nodes=8, manager=1, strategy=0))
-    with pytest.raises(Exception):
-        full.leave_node(np.array([1], np.uint32), np.array([2], np.uint32))
     hv = Oracle(default_config(n_nodes=8))
     with pytest.raises(Exception):
         hv.leave_node(np.array([1], np.uint32), np.array([2], np.uint32))
