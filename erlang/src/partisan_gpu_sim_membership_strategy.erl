@@ -45,8 +45,7 @@ join(State = #sim_strategy{sim = Sim, me = Me}, #{name := Name}, _RemoteState) -
 
 %% leave/2: the pluggable manager calls it from handle_call({leave, Node})
 %% (pluggable:502-515).  Node = myself is leave/0 (the node stops in the next
-%% round, psim_leave); another node is leave/1 at this node (psim_leave_node:
-%% SCAMP v1 / v2; the full strategy answers {error, unsupported}).
+%% round, psim_leave); another node is leave/1 at this node (psim_leave_node).
 leave(State = #sim_strategy{sim = Sim, me = Me}, #{name := Name}) ->
     ok = case id(Name) of
              Me -> partisan_gpu_sim:leave(Sim, [Me]);

@@ -272,12 +272,13 @@ int psim_leave(psim_handle *h, const uint32_t *nodes, size_t n);
  *       Q12) -- T itself included;
  *   v2: the actor sends {bootstrap_remove_subscription, T} to its partial
  *       view (scamp_v2:116-127); T, on receipt, stops before its replacement
- *       casts go out (lists:nth(0, ..) or the self-less reset, :192-238).
+ *       casts go out (lists:nth(0, ..) or the self-less reset, :192-238);
+ *   full: the actor tombstones T's add in its ORSet and gossips the new state
+ *       to its old members (full:58-89); merges carry the removal on, and a
+ *       node that merges a removal of itself stops (pluggable:1182-1188).
  * A stopping manager sends nothing in that round (its sends are casts to
  * itself) and is down from the next round on.  One call per actor per
- * round.  PSIM_EUNSUPPORTED for the full strategy (an ORSet removal needs
- * tombstones the member bitsets do not hold), HyParView handles and
- * multi-rank handles. */
+ * round.  PSIM_EUNSUPPORTED for HyParView handles and multi-rank handles. */
 int psim_leave_node(psim_handle *h, const uint32_t *actors, const uint32_t *targets, size_t n);
 int psim_set_partition(psim_handle *h, const uint8_t *group, size_t n);
 int psim_clear_partition(psim_handle *h);

@@ -828,7 +828,7 @@ static void process_node(struct psim_handle *h, uint32_t n) {
  * partisan_pluggable_peer_service_manager driving one membership strategy
  * (round model R0-P):
  *   full      partisan_full_membership_strategy.erl   (ORSet of node_specs as
- *             a member bitset: adds only -- leave/rmv is not simulated)
+ *             an add bitset and a remove bitset: member = add & ~remove)
  *   scamp v1  partisan_scamp_v1_membership_strategy.erl
  *   scamp v2  partisan_scamp_v2_membership_strategy.erl
  * A join is internal_join/3 (pluggable:1423-1458): the joiner's client
@@ -1406,9 +1406,8 @@ int orc_leave(struct psim_handle *h, const uint32_t *nodes, size_t n) {
 
 /* psim_leave_node: leave/1 -- actors[i] removes targets[i]
  * (handle_call({leave, Node}) pluggable:502-515).  actor == target is
- * leave/0.  SCAMP v1 / v2 only: the full strategy's ORSet removal needs
- * remove tombstones the member bitsets do not hold; one call per actor and
- * round; unsharded handles only (a stop is known on its own shard). */
+ * leave/0.  One call per actor and round; unsharded handles only (a stop is
+ * known on its own shard). */
 int orc_leave_node(struct psim_handle *h, const uint32_t *actors, const uint32_t *targets, size_t n) {
     if (!is_pl(h) || h->lo != 0 || h->hi != h->N) return PSIM_EUNSUPPORTED;
     for (size_t i = 0; i < n; i++) {

@@ -1677,8 +1677,8 @@ int psim_leave(psim_handle* h, const uint32_t* nodes, size_t n) {
 }
 
 // leave/1: actors[i] removes targets[i] (pl:502-515 -> internal_leave/2
-// :1390-1420); actor == target is leave/0.  SCAMP v1 / v2 single-rank
-// handles (a stop is learned from the owner shard's list after the round).
+// :1390-1420); actor == target is leave/0.  Single-rank handles (a stop is
+// learned from the owner shard's list after the round).
 int psim_leave_node(psim_handle* h, const uint32_t* actors, const uint32_t* targets, size_t n) {
     if (!h || (n && (!actors || !targets))) return PSIM_EINVAL;
     if (h->cfg.manager != PSIM_MANAGER_PLUGGABLE || h->world > 1) return PSIM_EUNSUPPORTED;

@@ -186,17 +186,13 @@ def test_strategy_remote_leave_parity(strategy):
 def test_full_remote_leave_parity(n, fanout):
     """psim_leave_node under the full strategy: ORSet remove rows (tombstones)
     merged with the adds, the two-row gossip payload, a target stopping on a
-    merged removal of itself -- bit-identical to the oracle, unsharded and
-    over 4 virtual shards."""
-    def sharded(cfg):
-        cfg.n_shards = 4
-        return _gpu(cfg)
+    merged removal of itself -- bit-identical to the oracle (full-strategy
+    handles are single-shard: gossip payloads are shard-local)."""
     kw = dict(strategy=0, fanout=fanout, k=4, part_at=60)
     os_, ost, _, _ = S.pl_leave_remote(Oracle, n, 8, 90, **kw)
-    for make in (_gpu, sharded):
-        gs, gst, _, _ = S.pl_leave_remote(make, n, 8, 90, **kw)
-        S.compare_stats(gst, ost)
-        S.compare_strategy(gs, os_, full_bits=[0, 1, n // 2, n - 1])
+    gs, gst, _, _ = S.pl_leave_remote(_gpu, n, 8, 90, **kw)
+    S.compare_stats(gst, ost)
+    S.compare_strategy(gs, os_, full_bits=[0, 1, n // 2, n - 1])
 
 
 @pytest.mark.parametrize("strategy", [1, 2])
