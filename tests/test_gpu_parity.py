@@ -229,6 +229,9 @@ def test_gpu_matches_committed_oracle_traces():
         "full_1024_fanout5": lambda: S.pl_doubling(_gpu, 1024, 11, 80, strategy=0, fanout=5, part_at=50),
         "scamp_v1_1024": lambda: S.pl_doubling(_gpu, 1024, 11, 100, strategy=1, crash_at=40, part_at=60),
         "scamp_v2_1024": lambda: S.pl_doubling(_gpu, 1024, 11, 100, strategy=2, crash_at=40, part_at=60),
+        "scamp_v1_leave_1024": lambda: S.pl_leave_remote(_gpu, 1024, 7, 90, strategy=1, part_at=60)[:2],
+        "scamp_v2_leave_1024": lambda: S.pl_leave_remote(_gpu, 1024, 7, 90, strategy=2, part_at=60)[:2],
+        "full_leave_1024_fanout5": lambda: S.pl_leave_remote(_gpu, 1024, 8, 90, strategy=0, fanout=5, k=4)[:2],
     }
     assert set(scen) == set(G.SCENARIOS)
     for name, run in scen.items():
