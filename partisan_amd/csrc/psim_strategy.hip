@@ -374,7 +374,6 @@ DEV void full_leave(Pw& w, uint32_t t) {
     if (was) {
         if (lane_id() == 0) w.row[w.a->fw + wi] |= bit;
         __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         w.dirty = true;
     }
     if (w.a->fanout) { w.gossip_due = true; return; }
