@@ -51,6 +51,7 @@ struct Pw {
     uint32_t snap;                 // full: payload slot of the current state
     bool dirty, gossip_due;
     bool stop;                     // the manager stopped this round (leave, App. A Q12)
+    uint32_t nfail;                // this node's failed sends this round (uniform)
 };
 
 DEV void st_add(Pw& w, int k, uint32_t v) { w.SC += lane_id() == (uint32_t)k ? v : 0u; }
@@ -150,7 +151,7 @@ DEV bool connected(const Pw& w, uint32_t p) {
 // do_send_message/7 (pl:1309-1363); success draws rand:uniform(1) in
 // partisan_util:dispatch_pid/3 (util:190-195)
 DEV void pl_send(Pw& w, uint32_t dst, uint32_t type, uint32_t a0, uint32_t slot) {
-    if (!connect_ok(w, dst) || !connected(w, dst)) { st_add(w, ST_FAIL, 1); return; }
+    if (!connect_ok(w, dst) || !connected(w, dst)) { st_add(w, ST_FAIL, 1); w.nfail++; return; }
     w.h.rng++;
     emit(w, dst, type, a0, slot);
 }
@@ -385,7 +386,7 @@ DEV void pl_handle(Pw& w, uint32_t type, uint32_t src, uint32_t a0, uint32_t slo
     const bool full = w.a->strategy == PSIM_STRATEGY_FULL;
     switch (type) {
     case PSIM_PL_HELLO:            // server: {state, Tag, get_local_state()} server:125-148
-        if (!connect_ok(w, src)) { st_add(w, ST_FAIL, 1); break; }
+        if (!connect_ok(w, src)) { st_add(w, ST_FAIL, 1); w.nfail++; break; }
         if (full) {
             uint32_t cnt = full_count(w);
             emit(w, src, PSIM_PL_STATE, cnt, full_snapshot(w));
@@ -475,8 +476,7 @@ DEV void process_pl(Pw& w, uint32_t n, uint32_t ib, uint32_t ik, uint32_t ob) {
     w.stop = false;
     // a manager that stops this round sends nothing: its sends are casts to
     // itself (schedule_self_message_delivery/6 pl:1585-1609)
-    const uint32_t SC0 = w.SC;
-    const uint64_t dig0 = w.digest;
+    w.nfail = 0;
 
     if (leave) {                   // leave/1 (pl:502-515, :1390-1420)
         w.h.pad1[0] = 0;
@@ -489,7 +489,7 @@ DEV void process_pl(Pw& w, uint32_t n, uint32_t ib, uint32_t ik, uint32_t ob) {
             emit(w, w.h.join_contact, PSIM_PL_HELLO, 0, NONE);
             w.h.have = 1;
         } else {
-            st_add(w, ST_FAIL, 1);
+            st_add(w, ST_FAIL, 1); w.nfail++;
         }
     }
     for (uint32_t c = 0; c < ik; c += 4) {
@@ -505,10 +505,15 @@ DEV void process_pl(Pw& w, uint32_t n, uint32_t ib, uint32_t ik, uint32_t ob) {
         if (w.stop) break;
     }
     if (w.stop) {                  // down from the next round, as a crash
+        // this node's sends and failures undone: the records it wrote are
+        // read back (no per-node snapshot of the counters held in registers)
         const uint32_t l2 = lane_id();
-        if ((l2 >= ST_EMIT && l2 < ST_EMIT + PSIM_MSG_NTYPES) || l2 == ST_FAIL)
-            w.SC = SC0;                         // this node's sends and failures undone
-        w.digest = dig0;
+        for (uint32_t k = 0; k < w.seq; k++) {
+            const uint32_t word = l2 < 16 ? reinterpret_cast<const uint32_t*>(a.rec_out + w.obase + k)[l2] : 0u;
+            w.digest -= (uint64_t)(l2 == 7 ? 0u : word) * digest_mul(l2);
+            st_add(w, ST_EMIT + rl(word, 2), (uint32_t)-1);
+        }
+        st_add(w, ST_FAIL, (uint32_t)-w.nfail);
         st_add(w, ST_STOP, 1);
         if (l2 == 0) a.stop_ids[atomicAdd(a.n_stop, 1u)] = n;
         w.seq = 0;
