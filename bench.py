@@ -2,12 +2,25 @@
 
 A step is one BSP round of the hot path (HyParView handlers + timers,
 Plumtree broadcast, message route) over every node of a 2^20-node overlay
-(steady state after a doubling bootstrap; a broadcast from node 0 every 10
-rounds).  Prints ONE JSON line (rank 0).  See DESIGN.md section 5.
+per GPU (steady state after a doubling bootstrap; a broadcast from node 0
+every 10 rounds).  Prints ONE JSON line (rank 0).  See DESIGN.md section 5.
+
+  python bench.py                      1 GPU (config C)
+  python bench.py --gpus N             N GPUs: N ranks are started here, one
+                                       per GPU, node-range sharded over RCCL
+  torchrun --nproc-per-node N bench.py --gpus N   the same, ranks by torchrun
+
+Every run first checks the sharded round against the one-shard engine on a
+small churn + partition scenario (digest of every emitted record, every
+round; node rows; overlay statistics): N RCCL ranks against one GPU, or, on
+one GPU, two virtual shards against one.  A mismatch fails the run.
 """
 import argparse
+import hashlib
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -16,31 +29,20 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-OVERLAY_DRAIN = 40               # untimed rounds before the overlay statistics
+BCAST_PERIOD = 10               # broadcast_heartbeat_interval cadence (rounds)
+STEADY_ROUNDS = 40              # untimed broadcast rounds before the warmup (any --warmup)
+OVERLAY_DRAIN = 40              # untimed rounds before the overlay statistics (at least)
 HBM_PEAK_GBS = 8000.0           # MI355X HBM3E spec (MI355X_MICROARCH.md)
 S_NODE = 416                    # algorithmic state bytes per processed node
 S_MSG = 64                      # message record bytes
-
-
-def pmc_traffic(workload):
-    """HBM bytes per round of the node-round kernels (k_relay + k_consume)
-    from the committed PMC passes of this same bench command
-    (profiles/run_pmc.sh -> profiles/pmc_latest.txt): FETCH_SIZE doubled
-    (gfx950 tallies 128-B read requests at 64 B, MI355X_MICROARCH.md HBM
-    section) plus WRITE_SIZE, both in KiB per timed round.  Config C only;
-    None when the file is absent."""
-    if workload != "C":
-        return None
-    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "pmc_latest.txt")
-    try:
-        vals = {}
-        for line in open(path):
-            f = line.split()
-            if len(f) >= 5 and f[0] in ("FETCH_SIZE", "WRITE_SIZE") and f[3] == "per-round":
-                vals[f[0]] = float(f[4])
-        return (2 * vals["FETCH_SIZE"] + vals["WRITE_SIZE"]) * 1024.0
-    except (OSError, KeyError, ValueError):
-        return None
+CHECK_NODES = 1 << 14           # the built-in sharding check
+CHECK_ROUNDS = 90
+SCHEDULE_VERSION = 2            # bumps when the event schedule of a run changes (PMC keys)
+ALG_FORMULA = ("B = N_proc * 2 * 416 + M_in * 64 + M_out * 68 per round, N_proc = nodes with work "
+               "(stats nodes_processed), M_in / M_out = delivered / emitted records.  Departs from "
+               "SURVEY 8(d) (every node's 416 B read, touched nodes' written, 32-B Plumtree records): "
+               "idle nodes are not read by the kernels and are not counted; every record is the "
+               "64-B record the engine moves, plus its 4-B route key")
 
 
 def parse():
@@ -48,12 +50,18 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=50)
     p.add_argument("--warmup", type=int, default=10)
-    p.add_argument("--nodes", type=int, default=1 << 20)
+    p.add_argument("--nodes", type=int, default=1 << 20, help="nodes per GPU (weak scaling)")
     p.add_argument("--seed", type=int, default=1)
     p.add_argument("--settle", type=int, default=60, help="untimed rounds after bootstrap")
     p.add_argument("--cpu-sample-nodes", type=int, default=1 << 16)
     p.add_argument("--cpu-sample-rounds", type=int, default=40)
+    p.add_argument("--cpu-workers", type=int, default=16,
+                   help="processes of the all-cores CPU baseline (the GPU box's CPU share is 16)")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-check", action="store_true", help="skip the built-in sharding check")
+    p.add_argument("--dry-run", action="store_true",
+                   help="launcher test on CPU: the ranks rendezvous (gloo), time a host loop with the "
+                        "same barriers and max-over-ranks, and rank 0 prints the line; no GPU")
     p.add_argument("--vshards", type=int, default=1,
                    help="diagnostic: G virtual shards of --nodes each on this one GPU (the sharded "
                         "partition / exchange / receive path with device copies instead of RCCL)")
@@ -64,35 +72,246 @@ def parse():
     return p.parse_args()
 
 
-def cpu_baseline(args):
-    """The CPU oracle (port of the reference handlers, 1 thread) on a bounded
-    sample of the same workload: 2^16 nodes, same bootstrap, timed rounds
-    with the same broadcast cadence."""
+# ------------------------------------------------------------ launcher --
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(args):
+    """--gpus N without a launcher: start N ranks of this script (one per
+    GPU) before anything here touches a GPU, and exit with their status."""
+    import torch                # device_count() does not initialise the GPU on this image
+
+    have = torch.cuda.device_count()
+    if have < args.gpus and not args.dry_run:
+        print(f"bench: --gpus {args.gpus} needs {args.gpus} GPUs, this machine shows {have}",
+              file=sys.stderr, flush=True)
+        return 2
+    port = _free_port()
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    alive = list(procs)
+    while alive:
+        for p in list(alive):
+            code = p.poll()
+            if code is None:
+                continue
+            alive.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                for q in alive:          # one rank failed: the others would wait in a collective
+                    q.terminate()
+        time.sleep(0.05)
+    return rc
+
+
+# -------------------------------------------------------- CPU baseline --
+def _cpu_sample(n, seed, rounds, barrier=None):
+    """The CPU oracle (a port of the reference handlers, 1 thread) on a
+    bounded sample of the workload: same bootstrap, same broadcast cadence.
+    Returns (node-rounds, msgs, seconds)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from _oracle import Oracle
     from partisan_amd import workloads as W
     from partisan_amd.sim import default_config
 
-    n = args.cpu_sample_nodes
-    o = Oracle(default_config(n_nodes=n, seed=args.seed))
-    o.run_schedule(W.doubling_join(n, args.seed), 40)
-    k = 0
+    o = Oracle(default_config(n_nodes=n, seed=seed))
+    o.run_schedule(W.doubling_join(n, seed), 40)
+    k, msgs = 0, 0
+    if barrier is not None:                   # all workers time their rounds together
+        barrier.wait()
     t0 = time.perf_counter()
-    msgs = 0
-    for r in range(args.cpu_sample_rounds):
-        if r % 10 == 0:
+    for r in range(rounds):
+        if r % BCAST_PERIOD == 0:
             o.broadcast(0, k)
             k += 1
-        st = o.step(1)
-        msgs += int(st["emitted"].sum())
-    dt = time.perf_counter() - t0
-    return {"value": n * args.cpu_sample_rounds / dt, "unit": "node-rounds/s", "cores": 1,
-            "kind": "port",
+        msgs += int(o.step(1)["emitted"].sum())
+    return n * rounds, msgs, time.perf_counter() - t0
+
+
+def _cpu_worker(a, barrier, q):
+    q.put(_cpu_sample(*a, barrier=barrier))
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
+def cpu_baseline(args):
+    """Run before the GPU is touched (worker processes are forked).  One
+    thread, then `workers` independent oracle processes on the same sample
+    with different seeds (the oracle is sequential: all-cores throughput is
+    the aggregate of independent replicas)."""
+    import multiprocessing as mp
+
+    n, rounds = args.cpu_sample_nodes, args.cpu_sample_rounds
+    nr, msgs, dt = _cpu_sample(n, args.seed, rounds)
+    workers = max(1, min(args.cpu_workers, len(os.sched_getaffinity(0))))
+    ctx = mp.get_context("fork")
+    barrier, q = ctx.Barrier(workers), ctx.Queue()
+    procs = [ctx.Process(target=_cpu_worker, args=((n, args.seed + i, rounds), barrier, q))
+             for i in range(workers)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=600) for _ in procs]
+    for p in procs:
+        p.join()
+    wall = max(r[2] for r in res)
+    tot = sum(r[0] for r in res)
+    return {"value": nr / dt, "unit": "node-rounds/s", "cores": 1, "kind": "port",
             "msgs_per_sec": msgs / dt,
-            "sample": f"oracle/psim_oracle.c, {n} nodes, {args.cpu_sample_rounds} steady-state "
-                      f"rounds after a doubling bootstrap, broadcast every 10 rounds, 1 thread"}
+            "sample": f"oracle/psim_oracle.c, {n} nodes, {rounds} steady-state rounds after a doubling "
+                      f"bootstrap, broadcast every {BCAST_PERIOD} rounds, 1 thread",
+            "all_cores": {"value": tot / wall, "unit": "node-rounds/s", "cores": workers,
+                          "msgs_per_sec": sum(r[1] for r in res) / wall,
+                          "sample": f"{workers} oracle processes at once, each the 1-thread sample "
+                                    f"with its own seed, timed rounds started together (barrier); "
+                                    f"node-rounds of all / the slowest one's time"},
+            "cpu_model": cpu_model(), "nproc": os.cpu_count(),
+            "affinity_cpus": len(os.sched_getaffinity(0))}
 
 
+# --------------------------------------------------------- shard check --
+STAT_FIELDS = ["emitted", "delivered", "dropped", "nodes_up", "nodes_processed", "exits",
+               "send_fail", "first_deliveries", "overflow", "digest"]
+
+
+def _check_schedule(sim, n, ch, r):
+    """Config E in miniature (rounds of the check): churn 20% over rounds
+    30-49 (crash, restart + rejoin), a half/half partition for 55-64, a
+    broadcast from node 0 every 10 rounds from round 20."""
+    from partisan_amd import workloads as W
+    if r in ch:
+        sim.crash(ch[r][0])
+        sim.join(ch[r][0], ch[r][1])
+    if r == 55:
+        sim.set_partition(W.half_partition(n))
+    if r == 65:
+        sim.clear_partition()
+    if r >= 20 and r % BCAST_PERIOD == 0:
+        sim.broadcast(0, (r // BCAST_PERIOD) % 0x10000)
+
+
+def shard_check(args, world, rank, dist, comm):
+    """The sharded engine (world RCCL ranks, or 2 virtual shards on one GPU)
+    against the one-shard engine on this GPU: stats + digest every round,
+    this rank's node rows, the overlay statistics.  Raises on a mismatch."""
+    from partisan_amd import Simulator
+    from partisan_amd import workloads as W
+    from partisan_amd.sim import default_config
+
+    n, seed = CHECK_NODES, args.seed + 100
+    dev = int(os.environ.get("PSIM_DEVICE", os.environ.get("LOCAL_RANK", "0")))
+
+    ch = {r: (v, c) for r, v, c in W.churn_schedule(n, seed, 0.2, 30, 20)}
+
+    def run(sim):
+        return sim.run_schedule(W.doubling_join(n, seed), CHECK_ROUNDS,
+                                extra=lambda r: _check_schedule(sim, n, ch, r))
+
+    cfg = default_config(n_nodes=n, seed=seed, device=dev)
+    # the sharded handle's route and owner partition run with 3 blocks, so
+    # every block takes several consecutive source steps, as they do at full
+    # size (>= 2^19 nodes per shard) -- the small check covers that path too
+    os.environ["PSIM_ROUTE_BLOCKS"] = "3"
+    try:
+        if world > 1:
+            cfg.shard_world, cfg.shard_rank = world, rank
+            sh = Simulator(cfg, comm=comm)
+            shards = world
+        else:
+            cfg.n_shards = 2
+            sh = Simulator(cfg)
+            shards = 2
+    finally:
+        del os.environ["PSIM_ROUTE_BLOCKS"]
+    st_sh = run(sh)
+    hist_sh = sh.histograms()             # a collective across ranks
+    per = (n + shards - 1) // shards
+    lo, cnt = (rank * per, min(n, (rank + 1) * per) - rank * per) if world > 1 else (0, n)
+    nodes_sh = sh.nodes(lo, cnt)
+    sh.close()
+    one = Simulator(default_config(n_nodes=n, seed=seed, device=dev))
+    st_one = run(one)
+    hist_one = one.histograms()
+    nodes_one = one.nodes(lo, cnt)
+    one.close()
+    bad = []
+    for f in STAT_FIELDS:
+        if not np.array_equal(st_sh[f], st_one[f]):
+            i = np.nonzero((st_sh[f] != st_one[f]).reshape(len(st_sh), -1).any(1))[0][0]
+            bad.append(f"stats.{f} differs first at round {int(st_one['round'][i])}")
+    for f in nodes_one.dtype.names:
+        if not np.array_equal(nodes_sh[f], nodes_one[f]):
+            bad.append(f"node rows field {f} differ")
+    for k, v in hist_one.items():
+        if not np.array_equal(np.asarray(hist_sh[k]), np.asarray(v)):
+            bad.append(f"histograms.{k} differ")
+    if world > 1:                             # every rank learns whether any rank failed
+        import torch
+        t = torch.tensor([len(bad)], dtype=torch.int64)
+        dist.all_reduce(t)
+        if int(t.item()) and not bad:
+            bad.append("another rank's check failed")
+    if bad:
+        raise SystemExit(f"bench: sharding check failed on rank {rank}: {bad[:4]}")
+    return {"nodes": n, "rounds": CHECK_ROUNDS, "shards": shards,
+            "against": "the one-shard engine on this GPU",
+            "scenario": "doubling bootstrap, 20% churn rounds 30-49, half/half partition 55-64, "
+                        "broadcast every 10 rounds",
+            "equal": ["per-round stats and record digest", "node rows", "overlay statistics"],
+            "route_blocks": 3,
+            "msgs": int(st_one["emitted"].sum()),
+            "symmetric_links": int(hist_one["symmetric_links"]), "components": int(hist_one["components"])}
+
+
+# --------------------------------------------------------- PMC traffic --
+def src_hash():
+    h = hashlib.sha256()
+    d = os.path.join(ROOT, "partisan_amd", "csrc")
+    for f in sorted(os.listdir(d)):
+        if f.endswith((".hip", ".h")):
+            h.update(f.encode())
+            h.update(open(os.path.join(d, f), "rb").read())
+    h.update(open(os.path.join(ROOT, "include", "partisan_gpu_sim.h"), "rb").read())
+    return h.hexdigest()[:16]
+
+
+def pmc_key(args, world, n):
+    return {"workload": args.workload, "nodes": n, "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "seed": args.seed, "schedule": SCHEDULE_VERSION, "src": src_hash()}
+
+
+def pmc_traffic(key):
+    """HBM bytes per launch of the node-round kernels from a committed PMC
+    record (profiles/pmc_records.json, written by profiles/run_pmc.sh) of
+    this same command -- workload, size, GPUs, steps, warmup, seed, event
+    schedule and kernel sources.  None when no record matches."""
+    try:
+        recs = json.load(open(os.path.join(ROOT, "profiles", "pmc_records.json")))
+    except (OSError, ValueError):
+        return None, None
+    for r in recs:
+        if r.get("key") == key:
+            return r["traffic_per_launch"], r.get("source")
+    return None, None
+
+
+# ---------------------------------------------------- pluggable (B, D) --
 def main_strategy(args):
     """Configs B and D of BASELINE.json on the pluggable manager (extra
     lines, not the driver's headline): a step is one round over every node.
@@ -131,6 +350,7 @@ def main_strategy(args):
         state = int(st["nodes_processed"].sum()) * 2 * (64 + 4 * 64 * 2)
     alg = state + int(st["delivered"].sum()) * S_MSG + msgs * (S_MSG + 4)
     achieved = alg / (c_ms / 1e3) / 1e9 if c_ms > 0 else 0.0
+    traffic, tsrc = pmc_traffic(pmc_key(args, 1, n))
     out = {
         "metric": "simulated node-rounds/sec (+ msgs/sec), pluggable manager " + args.workload,
         "value": n * args.steps / dt, "unit": "node-rounds/s", "msgs_per_sec": msgs / dt,
@@ -139,7 +359,8 @@ def main_strategy(args):
         "vs_baseline": None, "dtype": "u32", "data": "synthetic",
         "config": {"workload": name, "nodes": n, "seed": args.seed, "parallelism": "1 GPU"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(args.workload), "kernel": "k_consume_pl",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": tsrc,
+                     "kernel": "k_consume_pl",
                      "alg_bytes_per_launch": alg / max(1, c_n), "avg_launch_ms": c_ms / max(1, c_n)},
         "kernel_ms_per_step": {k: v[0] / args.steps for k, v in kt.items() if v[1]},
         "overflow": int(st["overflow"].sum()),
@@ -148,15 +369,81 @@ def main_strategy(args):
     print(json.dumps(out), flush=True)
 
 
+def dry_run(args, world, rank, dist):
+    """The rank protocol of main() without a GPU: rendezvous, barrier,
+    EXACTLY --steps timed steps of host work, barrier, max over ranks."""
+    if os.environ.get("PSIM_BENCH_FAIL_RANK") == str(rank):
+        raise SystemExit(3)                   # (test hook: a failing rank)
+    x = np.arange(1 << 16, dtype=np.uint64)
+    for _ in range(args.warmup):
+        x = (x * 6364136223846793005 + 1442695040888963407) & 0xFFFFFFFFFFFF
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        x = (x * 6364136223846793005 + 1442695040888963407) & 0xFFFFFFFFFFFF
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        import torch
+        t = torch.tensor([dt], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    if rank == 0:
+        print(json.dumps({"metric": "dry run (launcher test)", "value": world * args.steps / dt,
+                          "unit": "steps/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                          "ms_per_step": dt / args.steps * 1e3, "dry_run": True,
+                          "ranks": world, "checksum": int(x.sum() & 0xFFFF)}), flush=True)
+    dist.destroy_process_group() if world > 1 else None
+
+
+# ----------------------------------------------------- HyParView (C, E) --
 def main():
     args = parse()
-    if args.workload in ("B", "D"):
-        return main_strategy(args)
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        sys.exit(launch_ranks(args))
+    world = int(env_world or "1")
     rank = int(os.environ.get("RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench: WORLD_SIZE={world} but --gpus {args.gpus}: one rank per GPU")
+    if args.workload in ("B", "D"):
+        if world > 1:
+            raise SystemExit("bench: --workload B/D are single-GPU lines")
+        return main_strategy(args)
+    if world > 1 and args.vshards > 1:
+        raise SystemExit("bench: --vshards is a single-GPU diagnostic")
+
+    # the CPU baseline first, while no GPU has been touched (it forks)
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.workload == "C":
+        cpu = cpu_baseline(args)
+
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        if torch.cuda.device_count() < world and not args.dry_run:
+            raise SystemExit(f"bench: {world} ranks but {torch.cuda.device_count()} GPUs: one rank per GPU")
+        dist.init_process_group("gloo")
+    if args.dry_run:
+        return dry_run(args, world, rank, dist)
+
     from partisan_amd import Simulator
     from partisan_amd import workloads as W
     from partisan_amd.sim import comm_id, default_config
+
+    def shared_comm():
+        if world == 1:
+            return None
+        obj = [comm_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        return obj[0]
+
+    check = None
+    if not args.no_check:
+        check = shard_check(args, world, rank, dist, shared_comm())
 
     # weak scaling: --nodes per GPU; the overlay spans all GPUs, node-range
     # sharded, one RCCL rank per GPU (DESIGN.md section 7)
@@ -164,61 +451,60 @@ def main():
     cfg = default_config(n_nodes=n, seed=args.seed)
     cfg.n_shards = args.vshards
     cfg.device = int(os.environ.get("PSIM_DEVICE", os.environ.get("LOCAL_RANK", "0")))
-    comm = None
+    comm = shared_comm()
     if world > 1:
-        import torch.distributed as dist
-        dist.init_process_group("gloo")
-        obj = [comm_id() if rank == 0 else None]
-        dist.broadcast_object_list(obj, src=0)
-        comm = obj[0]
         cfg.shard_world, cfg.shard_rank = world, rank
     sim = Simulator(cfg, comm=comm)
     boot = W.doubling_join(n, args.seed)
     sim.run_schedule(boot, boot[-1][0] + 1 + args.settle)
 
-    state = {"k": 0}
+    # event index i counts rounds from the start of the broadcast phase:
+    # STEADY_ROUNDS untimed broadcast rounds (whatever --warmup is), the
+    # warmup rounds, then the timed window
+    state = {"k": 0, "last_bcast": None}
     churn = {}
+    t_start = STEADY_ROUNDS + args.warmup
     if args.workload == "E":
         # config E: 0.2*N crashes spread over 100 rounds, each
         # victim restarts the next round and rejoins; ids [0, N/2) | [N/2, N)
         # partitioned for 20 rounds from round 20 of the measured window
-        for r, v, c in W.churn_schedule(n, args.seed, 0.2, 0, 100):
+        for r, v, c in W.churn_schedule(n, args.seed, 0.2, STEADY_ROUNDS, 100):
             churn[r] = (v, c)
         part = W.half_partition(n)
+        p_on, p_off = t_start + 20, t_start + 40
 
     def round_events(i):
-        if i % 10 == 0:
+        if i % BCAST_PERIOD == 0:
             sim.broadcast(0, state["k"] % 0x10000)
             state["k"] += 1
+            state["last_bcast"] = i
         if args.workload == "E":
             if i in churn:
                 sim.crash(churn[i][0])
             if i - 1 in churn:
                 sim.join(churn[i - 1][0], churn[i - 1][1])
-            if i == 20:
+            if i == p_on:
                 sim.set_partition(part)
-            if i == 40:
+            if i == p_off:
                 sim.clear_partition()
 
     def has_events(i):
-        return i % 10 == 0 or (args.workload == "E" and (i in churn or i - 1 in churn or i in (20, 40)))
+        return i % BCAST_PERIOD == 0 or (args.workload == "E" and (i in churn or i - 1 in churn or i in (p_on, p_off)))
 
-    for i in range(args.warmup):
+    for i in range(t_start):
         round_events(i)
         sim.step(1)
     if world > 1:
         dist.barrier()
-    if os.environ.get("PSIM_TRACE_GROW"):
-        print("bench: timed rounds start", file=sys.stderr, flush=True)
     t0 = time.perf_counter()
     stats = []
     kt = {}
     i = 0
     while i < args.steps:
         # rounds up to the next one with host events run in one step call
-        round_events(args.warmup + i)
+        round_events(t_start + i)
         k = 1
-        while i + k < args.steps and not has_events(args.warmup + i + k):
+        while i + k < args.steps and not has_events(t_start + i + k):
             k += 1
         stats.append(sim.step(k))
         i += k
@@ -237,9 +523,9 @@ def main():
         dt = float(t.item())
     msgs = int(st["emitted"].sum())            # stats are global (all ranks)
     node_rounds = n * args.steps
-    # roofline of the dominant kernel (consume): algorithmic bytes per launch
-    # of this rank (global counters / world: the shards are equal ranges)
-    per = world                                # this process's share (its launches: c_n)
+    # roofline of the dominant kernel (the node-round phase): algorithmic
+    # bytes per launch of this rank (global counters / world: equal ranges)
+    per = world
     proc = int(st["nodes_processed"].sum()) / per
     deliv = int(st["delivered"].sum()) / per
     alg_bytes = proc * 2 * S_NODE + deliv * S_MSG + msgs / per * (S_MSG + 4)
@@ -247,6 +533,9 @@ def main():
     per_launch_bytes = alg_bytes / max(1, c_n)
     per_launch_s = (c_ms / 1e3) / max(1, c_n)
     achieved = per_launch_bytes / per_launch_s / 1e9 if per_launch_s > 0 else 0.0
+    key = pmc_key(args, world, n)
+    traffic, tsrc = pmc_traffic(key)
+    n_bc = sum(1 for j in range(t_start, t_start + args.steps) if j % BCAST_PERIOD == 0)
     out = {
         "metric": "simulated node-rounds/sec (+ msgs/sec), 1M-node HyParView+Plumtree"
                   + ("" if args.workload == "C" else " (config E: churn + partition)"),
@@ -262,48 +551,57 @@ def main():
                                ("E: HyParView+Plumtree, 20% churn over 100 rounds (crash, restart, rejoin), "
                                 "half/half partition for rounds 20-39, broadcast every 10 rounds"),
                    "nodes": n, "nodes_per_gpu": args.nodes, "seed": args.seed,
+                   "untimed_broadcast_rounds": STEADY_ROUNDS + args.warmup,
+                   "broadcasts_before_window": (t_start + BCAST_PERIOD - 1) // BCAST_PERIOD,
+                   "broadcasts_in_window": n_bc,
                    "parallelism": (f"node-range sharded x{world}, RCCL all-to-all" if world > 1 else
                                    f"1 GPU, {args.vshards} virtual shards" if args.vshards > 1 else "1 GPU")},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(args.workload),
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": tsrc,
                      "kernel": "k_relay + k_consume (the node-round phase: one launch of each per round, "
                                "timed from k_relay's first block to k_consume's last)",
                      "alg_bytes_per_launch": per_launch_bytes,
+                     "alg_bytes_formula": ALG_FORMULA,
                      "avg_launch_ms": per_launch_s * 1e3},
         "kernel_ms_per_step": {k: v[0] / args.steps for k, v in kt.items() if v[1]},
         "overflow": int(st["overflow"].sum()),
+        "pmc_key": key,
     }
-    if args.workload == "E":
-        lo = sim.cfg.shard_rank * args.nodes if world > 1 else 0
-        v = sim.nodes(lo, min(args.nodes, 1 << 18))       # a sample of this rank's range
-        # the second-to-last broadcast has had >= 10 rounds to spread
-        got = (v["have"] >> ((state["k"] - 2) % 32)) & 1
-        out["reliability_broadcast"] = {"msg": state["k"] - 2, "rounds": args.warmup + args.steps - 10 * (state["k"] - 2),
-                                        "delivered_fraction": float(got[v["up"] == 1].mean())}
-    # overlay statistics (psim_get_histograms; outside the measurement, after
-    # OVERLAY_DRAIN more rounds without new broadcasts so the last one has
-    # settled): the tracked broadcast's reach and hop depth, active view
-    # symmetry and connectivity, mean in-degrees -- SURVEY 8(d)'s report
+    if check is not None:
+        out["check"] = check
+    # overlay statistics (psim_get_histograms; outside the measurement):
+    # drain rounds without new broadcasts until the tracked (last) broadcast
+    # has had at least its last hop + 5 rounds and OVERLAY_DRAIN rounds
+    since = t_start + args.steps - state["last_bcast"]
     sim.step(OVERLAY_DRAIN)
-    ov = sim.histograms()
-    bins = np.arange(len(ov["hop"]))
+    drained = OVERLAY_DRAIN
+    while True:
+        ov = sim.histograms()
+        bins = np.arange(len(ov["hop"]))
+        last_hop = int(bins[ov["hop"] > 0].max()) if ov["delivered"] else 0
+        if since + drained >= last_hop + 5 or drained >= 400:
+            break
+        sim.step(10)
+        drained += 10
     nup = max(1, ov["n_up"])
     out["overlay"] = {
         "nodes_up": ov["n_up"],
         "tracked_broadcast_reliability": ov["delivered"] / nup,
-        "tracked_broadcast_last_hop": int(bins[ov["hop"] > 0].max()) if ov["delivered"] else None,
+        "tracked_broadcast_last_hop": last_hop if ov["delivered"] else None,
         "active_in_mean": float((ov["active_in"] * bins).sum() / nup),
         "passive_in_mean": float((ov["passive_in"] * bins).sum() / nup),
-        "symmetric_active_links": (ov["symmetric_links"] / max(1, ov["active_links"])
-                                   if ov["symmetric_links"] != 2**64 - 1 else None),
-        "components": ov["components"] if ov["components"] != 2**64 - 1 else None,
-        "largest_component": ov["largest_component"] if ov["components"] != 2**64 - 1 else None,
-        "rounds_since_tracked_broadcast": OVERLAY_DRAIN + (args.warmup + args.steps - 1) % 10 + 1,
+        "symmetric_active_links": ov["symmetric_links"] / max(1, ov["active_links"]),
+        "active_links": ov["active_links"],
+        "components": ov["components"],
+        "largest_component": ov["largest_component"],
+        "rounds_since_tracked_broadcast": since + drained,
+        "rounds_drained": drained,
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.workload == "C":
-        out["cpu_baseline"] = cpu_baseline(args)
+    if cpu is not None:
+        out["cpu_baseline"] = cpu
     if rank == 0:
         print(json.dumps(out), flush=True)
+    sim.close()
     if world > 1:
         dist.destroy_process_group()
 

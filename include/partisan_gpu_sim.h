@@ -232,9 +232,9 @@ typedef struct psim_histograms {
     uint64_t delivered;                      /* live nodes holding the tracked broadcast */
     uint64_t last_round;                     /* latest first-delivery round of it (0: none) */
     uint64_t active_links;                   /* directed active links between live nodes */
-    uint64_t symmetric_links;                /* ... whose reverse link exists (UINT64_MAX: not computed) */
+    uint64_t symmetric_links;                /* ... whose reverse link exists */
     uint64_t components;                     /* weakly connected components of live nodes over
-                                                active links (UINT64_MAX: not computed) */
+                                                active links */
     uint64_t largest_component;
     uint64_t reserved[6];
 } psim_histograms;
@@ -300,8 +300,9 @@ int psim_get_member_bits(psim_handle *h, uint32_t node, uint32_t *words, size_t 
 int psim_get_delivery(psim_handle *h, uint32_t first, uint32_t count, uint8_t *have, uint32_t *round,
                       uint32_t *hop);
 /* Overlay statistics (psim_histograms above); HyParView handles only.
- * Symmetry and connectivity are computed when the whole overlay is in this
- * process (one shard), otherwise reported as UINT64_MAX. */
+ * Symmetry and connectivity cover the whole overlay for any shard count:
+ * sharded handles gather every node's active row first (device copies, or an
+ * ncclAllGather across RCCL ranks -- a collective: every rank must call). */
 int psim_get_histograms(psim_handle *h, psim_histograms *out);
 /* Snapshot of the whole simulation state of this process (node rows,
  * in-flight messages, round, events not yet applied are not included):

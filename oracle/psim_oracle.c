@@ -103,6 +103,7 @@ struct psim_handle {
     /* pending events */
     uint32_t *pend_crash; size_t pend_crash_n, pend_crash_cap;
     uint32_t *pend_join, *pend_contact; size_t pend_join_n, pend_join_cap;
+    uint8_t *pend_join_mark;   /* ids in pend_join: a node starts at most once per round */
     uint32_t *pend_lv_a, *pend_lv_t; size_t pend_lv_n, pend_lv_cap;
     uint8_t *pend_part; int pend_part_set, pend_part_clear;
     int pend_bcast; uint32_t pend_root, pend_msg;
@@ -668,13 +669,23 @@ static void hv_handle(ctx *c, const omsg *m) {
         } else {
             uint32_t act0[PSIM_ACTIVE_CAP], n0 = s->act_n;
             memcpy(act0, s->act, sizeof act0);
-            if (ttl == h->cfg.prwl) add_to_passive(c, p);
+            uint32_t pas0[PSIM_PASSIVE_CAP], np0 = s->pas_n;   /* State0's passive view */
+            memcpy(pas0, s->pas, sizeof pas0);
+            if (ttl == h->cfg.prwl) add_to_passive(c, p);   /* State2 (:859-866) */
             uint32_t omit[3] = {sender, me, p};
             uint32_t r = select_random(c, act0, n0, omit, 3);
             if (r == PSIM_NONE) {
-                if (addable_epoch(c, pe, p) && !list_member(act0, n0, p) && connect_ok(c, p)) {
-                    add_to_active(c, p);
-                    hv_send(c, p, PSIM_MSG_NEIGHBOR, 0, current_id(c, p), 0, NULL, 0);
+                if (addable_epoch(c, pe, p) && !list_member(act0, n0, p)) {
+                    if (connect_ok(c, p)) {
+                        add_to_active(c, p);
+                        hv_send(c, p, PSIM_MSG_NEIGHBOR, 0, current_id(c, p), 0, NULL, 0);
+                    } else {
+                        /* {error, not_found} -> State0 (:896-897): the passive
+                         * insert is discarded; its eviction draw stays consumed
+                         * (the rand state lives in the process dictionary) */
+                        memcpy(s->pas, pas0, sizeof pas0);
+                        s->pas_n = np0;
+                    }
                 }
             } else {
                 hv_send(c, r, PSIM_MSG_FORWARD_JOIN, ttl - 1, p, pe, NULL, 0);
@@ -1227,7 +1238,10 @@ static void round_begin(struct psim_handle *h, psim_round_stats *st) {
         uint32_t n = h->pend_crash[i];
         if (h->nodes[n].up) { h->nodes[n].up = 0; h->crashed_now[n] = 1; }
     }
-    for (size_t i = 0; i < h->pend_join_n; i++) node_init(h, h->pend_join[i], h->pend_contact[i]);
+    for (size_t i = 0; i < h->pend_join_n; i++) {
+        node_init(h, h->pend_join[i], h->pend_contact[i]);
+        h->pend_join_mark[h->pend_join[i]] = 0;
+    }
     for (size_t i = 0; i < h->pend_lv_n; i++) h->sn[h->pend_lv_a[i]].leave_tgt = h->pend_lv_t[i] + 1;
     h->pend_lv_n = 0;
     if (h->pend_part_clear) memset(h->part, 0, h->N);
@@ -1348,7 +1362,7 @@ void orc_destroy(struct psim_handle *h) {
     if (!h) return;
     free(h->nodes); free(h->part); free(h->crashed_now); free(h->in_beg); free(h->pend_part);
     free(h->inbox.v); free(h->out.v);
-    free(h->pend_crash); free(h->pend_join); free(h->pend_contact);
+    free(h->pend_crash); free(h->pend_join); free(h->pend_contact); free(h->pend_join_mark);
     free(h->pend_lv_a); free(h->pend_lv_t);
     free(h->sn); free(h->fbits); free(h->pay_in); free(h->pay_out);
     free(h);
@@ -1357,9 +1371,20 @@ void orc_destroy(struct psim_handle *h) {
 int orc_join(struct psim_handle *h, const uint32_t *nodes, const uint32_t *contacts, size_t n) {
     for (size_t i = 0; i < n; i++)
         if (nodes[i] >= h->N || (contacts[i] != PSIM_NONE && contacts[i] >= h->N)) return PSIM_ERANGE;
+    if (!h->pend_join_mark && !(h->pend_join_mark = (uint8_t *)calloc(h->N, 1))) return PSIM_ENOMEM;
+    for (size_t i = 0; i < n; i++) {
+        if (h->pend_join_mark[nodes[i]]) {          /* a second start of the node this round */
+            for (size_t j = 0; j < i; j++) h->pend_join_mark[nodes[j]] = 0;
+            return PSIM_EINVAL;
+        }
+        h->pend_join_mark[nodes[i]] = 1;
+    }
     if (h->fbits) {                 /* an ORSet re-add would need per-incarnation tokens */
         for (size_t i = 0; i < n; i++)
-            if (h->sn[nodes[i]].started) return PSIM_EUNSUPPORTED;
+            if (h->sn[nodes[i]].started) {
+                for (size_t j = 0; j < n; j++) h->pend_join_mark[nodes[j]] = 0;
+                return PSIM_EUNSUPPORTED;
+            }
         for (size_t i = 0; i < n; i++) h->sn[nodes[i]].started = 1;
     }
     if (h->pend_join_n + n > h->pend_join_cap) {

@@ -672,12 +672,19 @@ DEV void hv_handle(Wv& w, uint32_t type, uint32_t p, uint32_t ttl, uint32_t a0, 
         } else {
             // the passive add at TTL == prwl never changes the active view,
             // so the live active row is Active0 for the select and the test
-            if (ttl == a.prwl) add_to_passive(w, q);
+            const uint32_t P_s = w.P, np_s = w.pas_n;  // State0's passive view
+            if (ttl == a.prwl) add_to_passive(w, q);    // State2 (hv:859-866)
             uint32_t r = select_random(w, w.A, w.act_n, sender, me, q);
             if (r == NONE) {
-                if (addable_epoch(w, pe, q) && !has(w.A, w.act_n, q) && connect_ok(w, q)) {
-                    add_to_active(w, q);
-                    hv_send(w, q, PSIM_MSG_NEIGHBOR, 0, current_id(w, q), 0, 0, 0);
+                if (addable_epoch(w, pe, q) && !has(w.A, w.act_n, q)) {
+                    if (connect_ok(w, q)) {
+                        add_to_active(w, q);
+                        hv_send(w, q, PSIM_MSG_NEIGHBOR, 0, current_id(w, q), 0, 0, 0);
+                    } else {
+                        // {error, not_found} -> State0 (hv:896-897): the insert
+                        // is discarded, its eviction draw stays consumed
+                        w.P = P_s; w.pas_n = np_s;
+                    }
                 }
             } else {
                 hv_send(w, r, PSIM_MSG_FORWARD_JOIN, ttl - 1, q, pe, 0, 0);

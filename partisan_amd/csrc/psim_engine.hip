@@ -289,7 +289,10 @@ __global__ void __launch_bounds__(RB_STEP) k_bucket_scatter(RouteIn in, uint32_t
 // G > 1, sender side: this shard's outbox runs stably partitioned by owner
 // shard (owner = dst / per) straight into the send buffer, so each owner's
 // records stay in (src, seq) order -- the receiver's route relies on it.
-// Two passes with the same block steps as the route:
+// Two passes; block blk takes the consecutive block steps [blk * spb,
+// (blk + 1) * spb), so block order is source order (a grid-stride step
+// assignment would put a block's later steps before the next block's
+// earlier ones and break the (src, seq) order once a block runs two steps):
 //   WRITE = false  per block and owner the record count -> hist[q * nblk + blk]
 //                  (hist[G * nblk] = 0: the scan's extra entry, the total)
 //   WRITE = true   after the scan, each record's 64 B to off[q * nblk + blk]
@@ -298,9 +301,9 @@ __global__ void __launch_bounds__(RB_STEP) k_bucket_scatter(RouteIn in, uint32_t
 // within a batch is a ballot over the lanes of the same owner, one ballot
 // per distinct owner in the batch (<= G).
 template <bool WRITE>
-__global__ void __launch_bounds__(RB_STEP) k_owner_part(RouteIn in, uint32_t nsteps, uint32_t G, uint32_t per,
-                                                        uint32_t* hist, const uint32_t* __restrict__ off,
-                                                        Msg* __restrict__ out) {
+__global__ void __launch_bounds__(RB_STEP) k_owner_part(RouteIn in, uint32_t nsteps, uint32_t spb, uint32_t G,
+                                                        uint32_t per, uint32_t* hist,
+                                                        const uint32_t* __restrict__ off, Msg* __restrict__ out) {
     __shared__ uint32_t spre[4][65];
     __shared__ uint64_t sbase[4][64];
     __shared__ uint32_t wc[4][64];                    // per wave and owner: records in this step
@@ -308,7 +311,8 @@ __global__ void __launch_bounds__(RB_STEP) k_owner_part(RouteIn in, uint32_t nst
     const uint32_t w = threadIdx.x >> 6, l = threadIdx.x & 63, nblk = gridDim.x;
     if (threadIdx.x < 64) run[threadIdx.x] = (WRITE && threadIdx.x < G) ? off[threadIdx.x * nblk + blockIdx.x] : 0u;
     if (!WRITE && blockIdx.x == 0 && threadIdx.x == 0) hist[G * nblk] = 0;
-    for (uint32_t step = blockIdx.x; step < nsteps; step += nblk) {
+    const uint32_t s_end = min(nsteps, (blockIdx.x + 1) * spb);
+    for (uint32_t step = blockIdx.x * spb; step < s_end; step++) {
         const uint32_t i = step * RB_STEP + threadIdx.x;
         const uint32_t c = i < in.n_src ? in.ocnt[i] : 0u;
         uint32_t inc = c;                             // inclusive prefix over the wave
@@ -750,17 +754,27 @@ __global__ void k_hist_in(const uint32_t* __restrict__ indeg_a, const uint32_t* 
         if (sh[j]) atomicAdd(&hist[H_AIN * PSIM_HIST_BINS + j], sh[j]);
 }
 
-// one shard holds the whole overlay: reverse-link test and label
-// propagation over live active links (min label, then pointer jumping)
-__global__ void k_hist_sym(const Hdr* __restrict__ hdr, const uint32_t* __restrict__ act,
+// the whole overlay's active rows (gathered from every shard / RCCL rank into
+// gact / gan by global id): reverse-link test and label propagation over live
+// active links (min label, then pointer jumping)
+__global__ void k_pack_act(const Hdr* __restrict__ hdr, const uint32_t* __restrict__ act, uint32_t n,
+                           uint32_t* gact, uint8_t* gan) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t k = hdr[i].act_n;
+    gan[i] = (uint8_t)k;
+    for (uint32_t j = 0; j < PSIM_ACTIVE_CAP; j++) gact[(size_t)i * PSIM_ACTIVE_CAP + j] = act[(size_t)i * PSIM_ACTIVE_CAP + j];
+}
+
+__global__ void k_hist_sym(const uint8_t* __restrict__ gan, const uint32_t* __restrict__ act,
                            const uint8_t* __restrict__ flags, uint32_t n, unsigned long long* sym) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n || !(flags[i] & F_UP)) return;
     uint32_t c = 0;
-    for (uint32_t k = 0; k < hdr[i].act_n; k++) {
+    for (uint32_t k = 0; k < gan[i]; k++) {
         const uint32_t p = act[(size_t)i * PSIM_ACTIVE_CAP + k];
-        if (p == i || !(flags[p] & F_UP)) continue;
-        for (uint32_t q = 0; q < hdr[p].act_n; q++)
+        if (p == i || p >= n || !(flags[p] & F_UP)) continue;
+        for (uint32_t q = 0; q < gan[p]; q++)
             if (act[(size_t)p * PSIM_ACTIVE_CAP + q] == i) { c++; break; }
     }
     if (c) atomicAdd(sym, (unsigned long long)c);
@@ -771,13 +785,13 @@ __global__ void k_cc_init(const uint8_t* __restrict__ flags, uint32_t n, uint32_
     if (i < n) L[i] = (flags[i] & F_UP) ? i : PSIM_NONE;
 }
 
-__global__ void k_cc_hook(const Hdr* __restrict__ hdr, const uint32_t* __restrict__ act,
+__global__ void k_cc_hook(const uint8_t* __restrict__ gan, const uint32_t* __restrict__ act,
                           const uint8_t* __restrict__ flags, uint32_t n, uint32_t* L, uint32_t* changed) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n || !(flags[i] & F_UP)) return;
-    for (uint32_t k = 0; k < hdr[i].act_n; k++) {
+    for (uint32_t k = 0; k < gan[i]; k++) {
         const uint32_t p = act[(size_t)i * PSIM_ACTIVE_CAP + k];
-        if (p == i || !(flags[p] & F_UP)) continue;
+        if (p == i || p >= n || !(flags[p] & F_UP)) continue;
         const uint32_t a = L[i], b = L[p];
         if (a < b) { if (atomicMin(&L[p], a) > a) *changed = 1; }
         else if (b < a) { if (atomicMin(&L[i], b) > b) *changed = 1; }
@@ -832,7 +846,24 @@ struct DBuf {
         if (hipMemset(p, 0, std::max<size_t>(want, 1) * sizeof(T)) != hipSuccess) return PSIM_EDEVICE;
         return PSIM_OK;
     }
+    // exact, zeroed on `st` (ordered before the stream's later kernels; the
+    // null-stream fill of alloc() is not ordered with a non-blocking stream)
+    int alloc_on(size_t want, hipStream_t st) {
+        if (hipMalloc(&p, std::max<size_t>(want, 1) * sizeof(T)) != hipSuccess) return PSIM_ENOMEM;
+        n = want;
+        if (hipMemsetAsync(p, 0, std::max<size_t>(want, 1) * sizeof(T), st) != hipSuccess) return PSIM_EDEVICE;
+        return PSIM_OK;
+    }
     void release() { if (p) (void)hipFree(p); p = nullptr; n = 0; }
+};
+
+// a temporary device buffer, released on every return path
+template <typename T>
+struct TmpBuf : DBuf<T> {
+    TmpBuf() = default;
+    TmpBuf(const TmpBuf&) = delete;
+    TmpBuf& operator=(const TmpBuf&) = delete;
+    ~TmpBuf() { this->release(); }
 };
 
 enum Kern { KT_EVENTS, KT_PREPARE, KT_CONSUME, KT_SCAN, KT_COMPACT, KT_SORT, KT_EXCHANGE, KT_GATHER,
@@ -914,6 +945,7 @@ struct psim_handle {
     DBuf<uint64_t> comm_cnt;            // RCCL: [send counts | recv counts]
     // pending events
     std::vector<uint32_t> pend_crash, pend_join, pend_contact;
+    std::vector<uint8_t> pend_join_mark;   // ids in pend_join (a node starts at most once per round)
     std::vector<uint32_t> pend_lv_a, pend_lv_t;     // leave/1 calls: actor, target
     std::vector<uint8_t> pend_part;
     bool pend_part_set = false, pend_part_clear = false;
@@ -930,6 +962,9 @@ struct psim_handle {
     // from its in-kernel span (RoundArgs::ktime)
     bool phase_timers = false;
     bool relay = true;                  // k_relay ahead of k_consume (PSIM_NO_RELAY=1: off)
+    // blocks of the route / owner-partition passes (RB_MAX_BLOCKS; a test
+    // hook, PSIM_ROUTE_BLOCKS, lowers it so small runs take several steps per block)
+    uint32_t rb_blocks = RB_MAX_BLOCKS;
 };
 
 namespace {
@@ -1191,7 +1226,7 @@ int route_group(psim_handle* h, Shard* s, const Msg* dense, uint32_t m) {
     const RouteIn in{dense ? dense : s->outbox.p, s->okey.p, s->obase.p, s->ocnt.p, dense ? m : n, s->lo,
                      h->cfg.manager == PSIM_MANAGER_PLUGGABLE};
     const uint32_t nsteps = std::max<uint32_t>(1, (in.n_src + RB_STEP - 1) / RB_STEP);
-    const uint32_t nblk = std::min<uint32_t>(nsteps, RB_MAX_BLOCKS);
+    const uint32_t nblk = std::min<uint32_t>(nsteps, h->rb_blocks);
     const size_t nh = (size_t)nb * nblk + 1;
     TRY(s->hist.ensure(nh));
     TRY(s->hoff.ensure(nh));
@@ -1244,7 +1279,8 @@ int phase_partition(psim_handle* h, Shard* s) {
     const uint32_t G = h->G;
     const RouteIn in{s->outbox.p, s->okey.p, s->obase.p, s->ocnt.p, s->n, 0, 0};
     const uint32_t nsteps = std::max<uint32_t>(1, (s->n + RB_STEP - 1) / RB_STEP);
-    const uint32_t nblk = std::min<uint32_t>(nsteps, RB_MAX_BLOCKS);
+    const uint32_t spb = (nsteps + h->rb_blocks - 1) / h->rb_blocks;    // consecutive steps per block
+    const uint32_t nblk = (nsteps + spb - 1) / spb;
     const size_t nh = (size_t)G * nblk + 1;
     TRY(s->hist.ensure(nh));
     TRY(s->hoff.ensure(nh));
@@ -1253,9 +1289,10 @@ int phase_partition(psim_handle* h, Shard* s) {
     s->soff.assign(G + 1, 0);
     {
         KTimer t(h, s, KT_SORT);
-        k_owner_part<false><<<nblk, RB_STEP, 0, s->stream>>>(in, nsteps, G, h->per, s->hist.p, nullptr, nullptr);
+        k_owner_part<false><<<nblk, RB_STEP, 0, s->stream>>>(in, nsteps, spb, G, h->per, s->hist.p, nullptr,
+                                                              nullptr);
         TRY(scan_excl(s, s->hist.p, s->hoff.p, (uint32_t)nh));
-        k_owner_part<true><<<nblk, RB_STEP, 0, s->stream>>>(in, nsteps, G, h->per, nullptr, s->hoff.p,
+        k_owner_part<true><<<nblk, RB_STEP, 0, s->stream>>>(in, nsteps, spb, G, h->per, nullptr, s->hoff.p,
                                                              s->sendbuf.p);
         k_owner_offsets<<<1, 128, 0, s->stream>>>(s->hoff.p, nblk, G, s->d_off.p);
         HIP_TRY(hipGetLastError());
@@ -1409,6 +1446,7 @@ int run_round(psim_handle* h, uint64_t* st) {
         HIP_TRY(hipMemcpyAsync(st, h->comm_cnt.p, NST * 8, hipMemcpyDeviceToHost, s->stream));
         TRY(stream_wait(s));
     }
+    for (uint32_t j : h->pend_join) h->pend_join_mark[j] = 0;
     h->pend_crash.clear(); h->pend_join.clear(); h->pend_contact.clear();
     h->pend_lv_a.clear(); h->pend_lv_t.clear();
     if (st[ST_STOP]) {
@@ -1597,6 +1635,8 @@ int psim_create(const psim_config* cfg, psim_handle** out) {
         h->phase_timers = e && *e && *e != '0';
         const char* r = getenv("PSIM_NO_RELAY");
         h->relay = !(r && *r && *r != '0');
+        const char* b = getenv("PSIM_ROUTE_BLOCKS");
+        if (b && *b) h->rb_blocks = std::max<uint32_t>(1, std::min<uint32_t>(RB_MAX_BLOCKS, (uint32_t)atoi(b)));
     }
     h->device = dev;
     for (uint32_t g = 0; g < G; g++) {
@@ -1640,9 +1680,26 @@ int psim_join(psim_handle* h, const uint32_t* nodes, const uint32_t* contacts, s
     if (!h || (n && (!nodes || !contacts))) return PSIM_EINVAL;
     for (size_t i = 0; i < n; i++)
         if (nodes[i] >= h->N || (contacts[i] != PSIM_NONE && contacts[i] >= h->N)) return PSIM_ERANGE;
+    // a node starts at most once per round: k_join runs one thread per entry,
+    // so two entries of one id would race on its rows
+    if (h->pend_join_mark.size() != h->N) h->pend_join_mark.assign(h->N, 0);
+    {
+        size_t i = 0;
+        for (; i < n; i++) {
+            if (h->pend_join_mark[nodes[i]]) break;
+            h->pend_join_mark[nodes[i]] = 1;
+        }
+        if (i < n) {                    // undo this call's marks
+            for (size_t j = 0; j < i; j++) h->pend_join_mark[nodes[j]] = 0;
+            return PSIM_EINVAL;
+        }
+    }
     if (!h->started.empty()) {          // an ORSet re-add would need per-incarnation tokens
         for (size_t i = 0; i < n; i++)
-            if (h->started[nodes[i]]) return PSIM_EUNSUPPORTED;
+            if (h->started[nodes[i]]) {
+                for (size_t j = 0; j < n; j++) h->pend_join_mark[nodes[j]] = 0;
+                return PSIM_EUNSUPPORTED;
+            }
         for (size_t i = 0; i < n; i++) h->started[nodes[i]] = 1;
     }
     h->pend_join.insert(h->pend_join.end(), nodes, nodes + n);
@@ -1952,10 +2009,10 @@ int psim_get_histograms(psim_handle* h, psim_histograms* out) {
     hipStream_t st = s0->stream;
     for (Shard* s : h->shards) HIP_TRY(hipStreamSynchronize(s->stream));
     const size_t N = h->N;
-    DBuf<uint32_t> ind;                          // in-degrees, active then passive, by global id
-    DBuf<unsigned long long> hist;
-    TRY(ind.alloc(2 * N));
-    TRY(hist.alloc(H_N + 4));
+    TmpBuf<uint32_t> ind;                        // in-degrees, active then passive, by global id
+    TmpBuf<unsigned long long> hist;
+    TRY(ind.alloc_on(2 * N, st));
+    TRY(hist.alloc_on(H_N + 4, st));
     const uint32_t tbit = h->tracked_msg == PSIM_NONE ? 0u : 1u << (h->tracked_msg & 31u);
     for (Shard* s : h->shards)
         k_hist_out<<<grid_for(s->n), BLK, 0, st>>>(s->hdr.p, s->act.p, s->pas.p, s->flags.p, s->lo, s->n, tbit,
@@ -1968,15 +2025,15 @@ int psim_get_histograms(psim_handle* h, psim_histograms* out) {
     std::vector<unsigned long long> hv(H_N + 4, 0);
     HIP_TRY(hipMemcpyAsync(hv.data(), hist.p, (H_N + 4) * 8, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
-    if (h->world > 1) {                          // sums over ranks (the latest round: max)
-        uint64_t last = hv[H_LAST];
+    if (h->world > 1) {                          // sums over ranks; the latest round: max
+        hv[H_N] = hv[H_LAST];
         TRY(h->comm_cnt.ensure(H_N + 4));
         HIP_TRY(hipMemcpyAsync(h->comm_cnt.p, hv.data(), (H_N + 4) * 8, hipMemcpyHostToDevice, st));
         NCCL_TRY(ncclAllReduce(h->comm_cnt.p, h->comm_cnt.p, H_N, ncclUint64, ncclSum, h->comm, st));
-        NCCL_TRY(ncclAllReduce(h->comm_cnt.p + H_LAST, h->comm_cnt.p + H_LAST, 1, ncclUint64, ncclMax, h->comm, st));
+        NCCL_TRY(ncclAllReduce(h->comm_cnt.p + H_N, h->comm_cnt.p + H_N, 1, ncclUint64, ncclMax, h->comm, st));
         HIP_TRY(hipMemcpyAsync(hv.data(), h->comm_cnt.p, (H_N + 4) * 8, hipMemcpyDeviceToHost, st));
         HIP_TRY(hipStreamSynchronize(st));
-        (void)last;
+        hv[H_LAST] = hv[H_N];
     }
     for (int k = 0; k < PSIM_HIST_BINS; k++) {
         out->active_in[k] = hv[H_AIN * PSIM_HIST_BINS + k];
@@ -1987,18 +2044,36 @@ int psim_get_histograms(psim_handle* h, psim_histograms* out) {
     }
     out->n_up = hv[H_NUP]; out->delivered = hv[H_DELIV]; out->last_round = hv[H_LAST];
     out->active_links = hv[H_LINKS];
-    out->symmetric_links = out->components = out->largest_component = ~0ull;
-    if (h->G == 1) {                             // the whole overlay is this shard
-        const uint32_t n = s0->n;
-        DBuf<uint32_t> L, sz, flag;
-        DBuf<unsigned long long> r;
-        TRY(L.alloc(n)); TRY(sz.alloc(n)); TRY(flag.alloc(1)); TRY(r.alloc(3));
-        k_hist_sym<<<grid_for(n), BLK, 0, st>>>(s0->hdr.p, s0->act.p, s0->flags.p, n, r.p);
-        k_cc_init<<<grid_for(n), BLK, 0, st>>>(s0->flags.p, n, L.p);
+    {
+        // symmetry and components need every node's active row: the shards'
+        // rows are gathered by global id (device copies for virtual shards,
+        // an in-place ncclAllGather of equal per-rank slots for RCCL ranks;
+        // 33 B per node), and every process then runs the same kernels over
+        // the whole overlay
+        const uint32_t per = h->per, n = h->N;
+        const size_t npad = (size_t)per * h->G;
+        TmpBuf<uint32_t> gact, L, sz, flag;
+        TmpBuf<uint8_t> gan;
+        TmpBuf<unsigned long long> r;
+        TRY(gact.alloc_on(npad * PSIM_ACTIVE_CAP, st)); TRY(gan.alloc_on(npad, st));
+        for (Shard* s : h->shards)
+            if (s->n)
+                k_pack_act<<<grid_for(s->n), BLK, 0, st>>>(s->hdr.p, s->act.p, s->n,
+                                                           gact.p + (size_t)s->lo * PSIM_ACTIVE_CAP, gan.p + s->lo);
+        if (h->world > 1) {
+            const size_t off = (size_t)h->rank * per;
+            NCCL_TRY(ncclAllGather(gact.p + off * PSIM_ACTIVE_CAP, gact.p, (size_t)per * PSIM_ACTIVE_CAP, ncclUint32,
+                                   h->comm, st));
+            NCCL_TRY(ncclAllGather(gan.p + off, gan.p, per, ncclUint8, h->comm, st));
+        }
+        const uint8_t* fl = s0->flags.p;         // replicated: every shard holds all N
+        TRY(L.alloc_on(n, st)); TRY(sz.alloc_on(n, st)); TRY(flag.alloc_on(1, st)); TRY(r.alloc_on(3, st));
+        k_hist_sym<<<grid_for(n), BLK, 0, st>>>(gan.p, gact.p, fl, n, r.p);
+        k_cc_init<<<grid_for(n), BLK, 0, st>>>(fl, n, L.p);
         for (int it = 0; it < 4096; it++) {
             uint32_t changed = 0;
             HIP_TRY(hipMemsetAsync(flag.p, 0, 4, st));
-            k_cc_hook<<<grid_for(n), BLK, 0, st>>>(s0->hdr.p, s0->act.p, s0->flags.p, n, L.p, flag.p);
+            k_cc_hook<<<grid_for(n), BLK, 0, st>>>(gan.p, gact.p, fl, n, L.p, flag.p);
             k_cc_jump<<<grid_for(n), BLK, 0, st>>>(n, L.p);
             HIP_TRY(hipMemcpyAsync(&changed, flag.p, 4, hipMemcpyDeviceToHost, st));
             HIP_TRY(hipStreamSynchronize(st));
@@ -2010,9 +2085,7 @@ int psim_get_histograms(psim_handle* h, psim_histograms* out) {
         HIP_TRY(hipMemcpyAsync(rv, r.p, sizeof rv, hipMemcpyDeviceToHost, st));
         HIP_TRY(hipStreamSynchronize(st));
         out->symmetric_links = rv[0]; out->components = rv[1]; out->largest_component = rv[2];
-        L.release(); sz.release(); flag.release(); r.release();
     }
-    ind.release(); hist.release();
     return PSIM_OK;
 }
 

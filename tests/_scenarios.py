@@ -61,6 +61,26 @@ def churn_partition(make, n=2048, seed=5, rounds=140, **cfg):
     return sim, st
 
 
+def joiner_crash(make, n=2048, seed=3, rounds=40, **cfg):
+    """A doubling bootstrap where a third of each round's joiners crash two
+    rounds after they start, while their FORWARD_JOINs are still walking.
+    With arwl = prwl (the variant config) the first hop inserts the joiner
+    into the passive view (hv:859-863) and, when no forward target exists and
+    the joiner is unreachable, the reference discards that insert
+    (hv:896-897, {error, not_found} -> State0): ~600 such reverts per run."""
+    sim = make(default_config(n_nodes=n, seed=seed, **cfg))
+
+    def hook(r):
+        if r >= 3 and (1 << (r - 3)) < n:
+            ids = np.arange(1 << (r - 3), min(n, 1 << (r - 2)), dtype=np.uint32)
+            sim.crash(ids[::3])
+    st = sim.run_schedule(W.doubling_join(n, seed), rounds, extra=hook)
+    return sim, st
+
+
+VARIANT = dict(max_active_size=8, max_passive_size=20, arwl=6, prwl=6, persist_epoch=1)
+
+
 def crash_only(make, n=1024, seed=9, rounds=80):
     """Crashes without restarts: EXIT handling and the stopped-member check
     (test/partisan_SUITE.erl:2024-2041)."""

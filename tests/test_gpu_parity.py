@@ -72,6 +72,17 @@ def test_variants_parity():
     S.compare_nodes(gs.nodes(), os_.nodes())
 
 
+@pytest.mark.parametrize("seed", [3, 4])
+def test_forward_join_revert_parity(seed):
+    """hv:896-897: a FORWARD_JOIN whose TTL == prwl inserted the joiner into
+    the passive view, found no forward target and could not reach the
+    joiner returns State0 -- the insert is undone, its draw stays consumed.
+    Variant config (arwl = prwl = 6) with joiners crashing mid-walk."""
+    (gs, gst), (os_, ost) = _both(S.joiner_crash, seed=seed, **S.VARIANT)
+    S.compare_stats(gst, ost)
+    S.compare_nodes(gs.nodes(), os_.nodes())
+
+
 def test_64k_parity():
     """2^16 nodes, 60 rounds + a broadcast: still cheap for the oracle (~5 s)."""
     def run(make):
@@ -126,6 +137,23 @@ def test_shard_count_invariance(shards):
         return _gpu(cfg)
     gs, gst = S.churn_partition(gpu_sharded, n=2048)
     os_, ost = S.churn_partition(Oracle, n=2048)
+    S.compare_stats(gst, ost)
+    S.compare_nodes(gs.nodes(), os_.nodes())
+
+
+@pytest.mark.parametrize("shards", [2, 4])
+def test_shard_invariance_multistep_blocks(shards, monkeypatch):
+    """The route and the owner partition with few blocks (PSIM_ROUTE_BLOCKS=3),
+    so every block runs several consecutive source steps, as at >= 2^19
+    nodes per shard: still bit-identical to the oracle (a grid-stride step
+    order broke the partition's (src, seq) order there)."""
+    monkeypatch.setenv("PSIM_ROUTE_BLOCKS", "3")
+
+    def gpu_sharded(cfg):
+        cfg.n_shards = shards
+        return _gpu(cfg)
+    gs, gst = S.churn_partition(gpu_sharded, n=4096)
+    os_, ost = S.churn_partition(Oracle, n=4096)
     S.compare_stats(gst, ost)
     S.compare_nodes(gs.nodes(), os_.nodes())
 
@@ -267,6 +295,73 @@ def test_histograms_delivery_parity():
     for a, b in zip(g.delivery(), o.delivery()):
         assert np.array_equal(a, b)
     assert hg["components"] == 1
+
+
+def test_duplicate_join_rejected_gpu():
+    """The engine refuses a second start of a pending id (EINVAL), as the
+    oracle does; the run then matches the oracle."""
+    from partisan_amd.sim import default_config
+
+    def run(make):
+        sim = make(default_config(n_nodes=64, seed=4))
+        with pytest.raises(Exception):
+            sim.join(np.array([0, 0], np.uint32), np.array([0xFFFFFFFF, 0xFFFFFFFF], np.uint32))
+        sim.join(np.array([0], np.uint32), np.array([0xFFFFFFFF], np.uint32))
+        sim.step(1)
+        ids = np.arange(1, 64, dtype=np.uint32)
+        sim.join(ids, np.zeros(63, np.uint32))
+        with pytest.raises(Exception):
+            sim.join(ids[5:6], np.zeros(1, np.uint32))
+        return sim, sim.step(30)
+    (g, gst), (o, ost) = run(_gpu), run(Oracle)
+    S.compare_stats(gst, ost)
+    S.compare_nodes(g.nodes(), o.nodes())
+
+
+@pytest.mark.parametrize("shards", [1, 4])
+def test_histograms_large_properties(shards):
+    """Overlay statistics at 2^22 nodes (the oracle is not run): symmetric
+    links <= active links, every histogram sums to the live nodes, the link
+    and in-degree totals agree, and a host recount over the node rows
+    (active in-degrees, symmetric links, out-degrees) matches.  With 4
+    virtual shards the statistics must equal the unsharded ones (the
+    gathered-row symmetry / components path of sharded handles)."""
+    def make(cfg):
+        cfg.n_shards = shards
+        return _gpu(cfg)
+    n = 1 << 22
+    sim, _ = S.doubling(make, n, 7, 40)
+    sim.broadcast(0, 3)
+    sim.step(30)
+    h = sim.histograms()
+    up = h["n_up"]
+    assert up == n
+    for k in ("active_in", "passive_in", "active_out", "passive_fill"):
+        assert int(h[k].sum()) == up, k
+    assert h["symmetric_links"] <= h["active_links"]
+    bins = np.arange(len(h["active_in"]), dtype=np.uint64)
+    assert int((h["active_in"] * bins).sum()) == h["active_links"]
+    assert int((h["active_out"] * bins).sum()) == h["active_links"]
+    assert h["delivered"] == int(h["hop"].sum())
+    v = sim.nodes()
+    act = v["act"].astype(np.int64)
+    k = np.arange(8)[None, :] < v["act_n"][:, None].astype(np.int64)
+    me = np.arange(n)[:, None]
+    link = k & (act != me)
+    src = np.broadcast_to(me, act.shape)[link]
+    dst = act[link]
+    assert link.sum() == h["active_links"]
+    assert np.array_equal(np.bincount(np.minimum(np.bincount(dst, minlength=n), 63), minlength=64),
+                          h["active_in"].astype(np.int64))
+    fwd = np.unique(src * n + dst)
+    rev = np.unique(dst * n + src)
+    assert np.intersect1d(fwd, rev, assume_unique=True).size == h["symmetric_links"]
+    global _HIST_1
+    if shards == 1:
+        _HIST_1 = h
+    elif "_HIST_1" in globals():
+        for kk in _HIST_1:
+            assert np.array_equal(np.asarray(h[kk]), np.asarray(_HIST_1[kk])), kk
 
 
 def test_snapshot_restore_continues_identically():

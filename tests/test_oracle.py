@@ -12,6 +12,8 @@ from _oracle import Oracle, load
 from partisan_amd import workloads as W
 from partisan_amd.sim import default_config
 
+NONE = 0xFFFFFFFF
+
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 
@@ -139,6 +141,22 @@ def test_event_validation():
     sim.broadcast(0, 1)
     with pytest.raises(Exception):
         sim.broadcast(1, 2)          # single-root restriction
+
+
+def test_duplicate_join_rejected():
+    """A node starts at most once per round: a second psim_join of an id
+    pending for the same round (in one batch or another call) is EINVAL and
+    leaves the earlier joins in place (duplicates raced in k_join)."""
+    sim = Oracle(default_config(n_nodes=16))
+    with pytest.raises(Exception):
+        sim.join(np.array([0, 3, 3], np.uint32), np.array([NONE, 0, 0], np.uint32))
+    sim.join(np.array([0, 3], np.uint32), np.array([NONE, 0], np.uint32))
+    with pytest.raises(Exception):
+        sim.join(np.array([3], np.uint32), np.array([0], np.uint32))
+    sim.step(1)
+    sim.join(np.array([3], np.uint32), np.array([0], np.uint32))   # a later round: a restart
+    sim.step(3)
+    assert sim.nodes(3, 1)["up"][0] == 1
 
 
 def test_plumtree_off():
