@@ -7,15 +7,17 @@
  *      -L../../partisan_amd/csrc -lpartisan_gpu_sim
  *
  * One resource per simulator handle; calls on a handle are serialised by a
- * mutex (the ABI is thread-compatible, not thread-safe) and psim_step runs on
- * a dirty CPU scheduler because it blocks for whole BSP rounds.
+ * mutex (the ABI is thread-compatible, not thread-safe).  psim_step and the
+ * other long calls run on dirty schedulers and wait for the mutex; the short
+ * NIFs run on normal schedulers and never block one: when the handle is busy
+ * (a step in progress) they return {error, busy} and the caller retries.
  */
 #include <erl_nif.h>
 #include <string.h>
 
 #include "partisan_gpu_sim.h"
 
-typedef struct { psim_handle *h; ErlNifMutex *mu; } sim_res;
+typedef struct { psim_handle *h; ErlNifMutex *mu; uint32_t n_nodes; } sim_res;
 static ErlNifResourceType *SIM_RT;
 
 static void sim_dtor(ErlNifEnv *env, void *obj) {
@@ -33,6 +35,13 @@ static ERL_NIF_TERM err(ErlNifEnv *env, int rc) {
     return enif_make_tuple2(env, enif_make_atom(env, "error"),
                             enif_make_atom(env, psim_strerror(rc)));
 }
+
+static ERL_NIF_TERM busy(ErlNifEnv *env) {
+    return enif_make_tuple2(env, enif_make_atom(env, "error"), enif_make_atom(env, "busy"));
+}
+
+/* normal-scheduler NIFs: take the handle's mutex only if it is free */
+#define LOCK_OR_BUSY(r) do { if (enif_mutex_trylock((r)->mu) != 0) return busy(env); } while (0)
 
 static int get_u32(ErlNifEnv *env, ERL_NIF_TERM map, const char *k, uint32_t *out) {
     ERL_NIF_TERM v;
@@ -70,6 +79,7 @@ static ERL_NIF_TERM nif_create(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv
         c.seed = seed;
     sim_res *r = enif_alloc_resource(SIM_RT, sizeof *r);
     r->mu = enif_mutex_create("psim");
+    r->n_nodes = c.n_nodes;
     int rc = psim_create(&c, &r->h);
     if (rc) { r->h = NULL; enif_release_resource(r); return err(env, rc); }
     ERL_NIF_TERM t = enif_make_resource(env, r);
@@ -84,7 +94,7 @@ static ERL_NIF_TERM nif_join(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[]
         !enif_inspect_binary(env, argv[1], &a) || !enif_inspect_binary(env, argv[2], &b) ||
         a.size != b.size || a.size % 4)
         return enif_make_badarg(env);
-    enif_mutex_lock(r->mu);
+    LOCK_OR_BUSY(r);
     int rc = psim_join(r->h, (const uint32_t *)a.data, (const uint32_t *)b.data, a.size / 4);
     enif_mutex_unlock(r->mu);
     return rc ? err(env, rc) : enif_make_atom(env, "ok");
@@ -95,7 +105,7 @@ static ERL_NIF_TERM nif_crash(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[
     if (!enif_get_resource(env, argv[0], SIM_RT, (void **)&r) ||
         !enif_inspect_binary(env, argv[1], &a) || a.size % 4)
         return enif_make_badarg(env);
-    enif_mutex_lock(r->mu);
+    LOCK_OR_BUSY(r);
     int rc = psim_crash(r->h, (const uint32_t *)a.data, a.size / 4);
     enif_mutex_unlock(r->mu);
     return rc ? err(env, rc) : enif_make_atom(env, "ok");
@@ -107,7 +117,7 @@ static ERL_NIF_TERM nif_revive(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv
     if (!enif_get_resource(env, argv[0], SIM_RT, (void **)&r) ||
         !enif_inspect_binary(env, argv[1], &a) || a.size % 4)
         return enif_make_badarg(env);
-    enif_mutex_lock(r->mu);
+    LOCK_OR_BUSY(r);
     int rc = psim_revive(r->h, (const uint32_t *)a.data, a.size / 4);
     enif_mutex_unlock(r->mu);
     return rc ? err(env, rc) : enif_make_atom(env, "ok");
@@ -119,7 +129,7 @@ static ERL_NIF_TERM nif_leave(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[
     if (!enif_get_resource(env, argv[0], SIM_RT, (void **)&r) ||
         !enif_inspect_binary(env, argv[1], &a) || a.size % 4)
         return enif_make_badarg(env);
-    enif_mutex_lock(r->mu);
+    LOCK_OR_BUSY(r);
     int rc = psim_leave(r->h, (const uint32_t *)a.data, a.size / 4);
     enif_mutex_unlock(r->mu);
     return rc ? err(env, rc) : enif_make_atom(env, "ok");
@@ -132,7 +142,7 @@ static ERL_NIF_TERM nif_leave_node(ErlNifEnv *env, int argc, const ERL_NIF_TERM 
         !enif_inspect_binary(env, argv[1], &a) || !enif_inspect_binary(env, argv[2], &t) ||
         a.size % 4 || a.size != t.size)
         return enif_make_badarg(env);
-    enif_mutex_lock(r->mu);
+    LOCK_OR_BUSY(r);
     int rc = psim_leave_node(r->h, (const uint32_t *)a.data, (const uint32_t *)t.data, a.size / 4);
     enif_mutex_unlock(r->mu);
     return rc ? err(env, rc) : enif_make_atom(env, "ok");
@@ -143,7 +153,7 @@ static ERL_NIF_TERM nif_broadcast(ErlNifEnv *env, int argc, const ERL_NIF_TERM a
     if (!enif_get_resource(env, argv[0], SIM_RT, (void **)&r) ||
         !enif_get_uint(env, argv[1], &root) || !enif_get_uint(env, argv[2], &id))
         return enif_make_badarg(env);
-    enif_mutex_lock(r->mu);
+    LOCK_OR_BUSY(r);
     int rc = psim_broadcast(r->h, root, id);
     enif_mutex_unlock(r->mu);
     return rc ? err(env, rc) : enif_make_atom(env, "ok");
@@ -179,7 +189,7 @@ static ERL_NIF_TERM nif_active(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv
     psim_node_view v;
     if (!enif_get_resource(env, argv[0], SIM_RT, (void **)&r) || !enif_get_uint(env, argv[1], &node))
         return enif_make_badarg(env);
-    enif_mutex_lock(r->mu);
+    LOCK_OR_BUSY(r);
     int rc = psim_get_nodes(r->h, node, 1, &v);
     enif_mutex_unlock(r->mu);
     if (rc) return err(env, rc);
@@ -196,13 +206,18 @@ static ERL_NIF_TERM nif_members(ErlNifEnv *env, int argc, const ERL_NIF_TERM arg
     if (!enif_get_resource(env, argv[0], SIM_RT, (void **)&r) || !enif_get_uint(env, argv[1], &node) ||
         !enif_get_uint(env, argv[2], &n_nodes))
         return enif_make_badarg(env);
-    enif_mutex_lock(r->mu);
+    if (n_nodes != r->n_nodes) return enif_make_badarg(env);
+    LOCK_OR_BUSY(r);
     int rc = psim_get_strategy_nodes(r->h, node, 1, &v);
     uint32_t *bits = NULL;
-    size_t words = (n_nodes + 31) / 32;
+    size_t words = (r->n_nodes + 31) / 32;     /* psim_get_member_bits fills exactly these */
     if (!rc && v.members) {           /* full strategy */
         bits = enif_alloc(words * 4);
-        rc = psim_get_member_bits(r->h, node, bits, words);
+        if (!bits) rc = PSIM_ENOMEM;
+        else {
+            memset(bits, 0, words * 4);
+            rc = psim_get_member_bits(r->h, node, bits, words);
+        }
     }
     enif_mutex_unlock(r->mu);
     if (rc) { if (bits) enif_free(bits); return err(env, rc); }
@@ -227,7 +242,7 @@ static ERL_NIF_TERM nif_delivery(ErlNifEnv *env, int argc, const ERL_NIF_TERM ar
     uint8_t have; uint32_t rnd, hop;
     if (!enif_get_resource(env, argv[0], SIM_RT, (void **)&r) || !enif_get_uint(env, argv[1], &node))
         return enif_make_badarg(env);
-    enif_mutex_lock(r->mu);
+    LOCK_OR_BUSY(r);
     int rc = psim_get_delivery(r->h, node, 1, &have, &rnd, &hop);
     enif_mutex_unlock(r->mu);
     if (rc) return err(env, rc);
@@ -269,12 +284,19 @@ static ERL_NIF_TERM nif_snapshot(ErlNifEnv *env, int argc, const ERL_NIF_TERM ar
     size_t need = 0;
     ErlNifBinary bin;
     if (!enif_get_resource(env, argv[0], SIM_RT, (void **)&r)) return enif_make_badarg(env);
+    int have_bin = 0;
     enif_mutex_lock(r->mu);
     int rc = psim_snapshot(r->h, NULL, 0, &need);
-    if (!rc && !enif_alloc_binary(need, &bin)) rc = PSIM_ENOMEM;
+    if (!rc) {
+        if (enif_alloc_binary(need, &bin)) have_bin = 1;
+        else rc = PSIM_ENOMEM;
+    }
     if (!rc) rc = psim_snapshot(r->h, bin.data, bin.size, &need);
     enif_mutex_unlock(r->mu);
-    if (rc) return err(env, rc);
+    if (rc) {
+        if (have_bin) enif_release_binary(&bin);
+        return err(env, rc);
+    }
     return enif_make_tuple2(env, enif_make_atom(env, "ok"), enif_make_binary(env, &bin));
 }
 
@@ -287,6 +309,59 @@ static ERL_NIF_TERM nif_restore(ErlNifEnv *env, int argc, const ERL_NIF_TERM arg
     int rc = psim_restore(r->h, bin.data, bin.size);
     enif_mutex_unlock(r->mu);
     return rc ? err(env, rc) : enif_make_atom(env, "ok");
+}
+
+/* set_partition(Ref, GroupsBin): one byte per node, the partition group of
+ * each (inject_partition/2 as a network partition);
+ * clear_partition(Ref): resolve_partition/1 */
+static ERL_NIF_TERM nif_set_partition(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[]) {
+    sim_res *r; ErlNifBinary g;
+    if (!enif_get_resource(env, argv[0], SIM_RT, (void **)&r) || !enif_inspect_binary(env, argv[1], &g) ||
+        g.size != r->n_nodes)
+        return enif_make_badarg(env);
+    LOCK_OR_BUSY(r);
+    int rc = psim_set_partition(r->h, (const uint8_t *)g.data, g.size);
+    enif_mutex_unlock(r->mu);
+    return rc ? err(env, rc) : enif_make_atom(env, "ok");
+}
+
+static ERL_NIF_TERM nif_clear_partition(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[]) {
+    sim_res *r;
+    if (!enif_get_resource(env, argv[0], SIM_RT, (void **)&r)) return enif_make_badarg(env);
+    LOCK_OR_BUSY(r);
+    int rc = psim_clear_partition(r->h);
+    enif_mutex_unlock(r->mu);
+    return rc ? err(env, rc) : enif_make_atom(env, "ok");
+}
+
+static ERL_NIF_TERM id_list(ErlNifEnv *env, const uint32_t *v, uint32_t n) {
+    ERL_NIF_TERM l = enif_make_list(env, 0);
+    for (uint32_t i = n; i-- > 0;) l = enif_make_list_cell(env, enif_make_uint(env, v[i]), l);
+    return l;
+}
+
+/* node(Ref, Node) -> {ok, #{up, epoch, active, passive, have, round}} :
+ * one node's HyParView views (sets:to_list order) and its Plumtree
+ * delivery mask (bit m: message id m mod 32 merged, plumtree_backend ETS) */
+static ERL_NIF_TERM nif_node(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[]) {
+    sim_res *r; unsigned node;
+    psim_node_view v;
+    uint64_t round = 0;
+    if (!enif_get_resource(env, argv[0], SIM_RT, (void **)&r) || !enif_get_uint(env, argv[1], &node))
+        return enif_make_badarg(env);
+    LOCK_OR_BUSY(r);
+    int rc = psim_get_nodes(r->h, node, 1, &v);
+    if (!rc) rc = psim_get_round(r->h, &round);
+    enif_mutex_unlock(r->mu);
+    if (rc) return err(env, rc);
+    ERL_NIF_TERM m = enif_make_new_map(env);
+    enif_make_map_put(env, m, enif_make_atom(env, "up"), enif_make_atom(env, v.up ? "true" : "false"), &m);
+    enif_make_map_put(env, m, enif_make_atom(env, "epoch"), enif_make_uint(env, v.epoch), &m);
+    enif_make_map_put(env, m, enif_make_atom(env, "active"), id_list(env, v.act, v.act_n), &m);
+    enif_make_map_put(env, m, enif_make_atom(env, "passive"), id_list(env, v.pas, v.pas_n), &m);
+    enif_make_map_put(env, m, enif_make_atom(env, "have"), enif_make_uint(env, v.have), &m);
+    enif_make_map_put(env, m, enif_make_atom(env, "round"), enif_make_uint64(env, round), &m);
+    return enif_make_tuple2(env, enif_make_atom(env, "ok"), m);
 }
 
 static ErlNifFunc funcs[] = {
@@ -302,6 +377,9 @@ static ErlNifFunc funcs[] = {
     {"members", 3, nif_members, 0},
     {"delivery", 2, nif_delivery, 0},
     {"histograms", 1, nif_histograms, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"set_partition_nif", 2, nif_set_partition, 0},
+    {"clear_partition", 1, nif_clear_partition, 0},
+    {"node", 2, nif_node, 0},
     {"snapshot", 1, nif_snapshot, ERL_NIF_DIRTY_JOB_IO_BOUND},
     {"restore", 2, nif_restore, ERL_NIF_DIRTY_JOB_IO_BOUND},
 };

@@ -1,0 +1,116 @@
+"""Reference parity through the in-BEAM harness (erlang/harness/README.md).
+
+  python erlang/harness/compare_trace.py scenario config_a DIR
+      writes DIR/config_a.terms (the event script psim_harness:run/2 reads)
+      and DIR/config_a.oracle (the CPU oracle's record stream of the same
+      scenario: one line per emitted message, in the harness's format)
+  python erlang/harness/compare_trace.py compare DIR/config_a.harness DIR/config_a.oracle
+      diffs the two streams round by round; exit status 1 at the first
+      differing record.  Bucket lines (B id phash16) of the harness output
+      are also written to DIR/bucket16.txt: the sets v1 order the engine's
+      bucket16() stands in for (psim_device.h).
+
+The oracle is the checker (test infrastructure); the GPU engine is pinned to
+it bit for bit by tests/test_gpu_parity.py, so harness == oracle extends to
+harness == engine."""
+import ctypes as C
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "tests")]
+
+from partisan_amd import _abi  # noqa: E402
+from partisan_amd import workloads as W  # noqa: E402
+from partisan_amd.sim import default_config  # noqa: E402
+
+NONE = 0xFFFFFFFF
+
+SCENARIOS = {
+    # config A (test/partisan_SUITE.erl:1591-1601): node i joins node 0 at
+    # round i, 200 rounds, a broadcast from node 0 at round 200, 40 more
+    "config_a": dict(n=32, seed=1, rounds=240, joins=lambda n, s: W.sequential_join(n),
+                     bcast=[(200, 0, 7)], crash={}),
+    # a doubling bootstrap with crashes (EXIT handling) and broadcasts
+    "doubling_crash_256": dict(n=256, seed=3, rounds=80, joins=lambda n, s: W.doubling_join(n, s),
+                               bcast=[(30, 0, 1), (60, 0, 2)], crash={40: list(range(5, 256, 17))}),
+}
+
+
+def scenario(name, out_dir):
+    sc = SCENARIOS[name]
+    n, seed, rounds = sc["n"], sc["seed"], sc["rounds"]
+    joins = sc["joins"](n, seed)
+    os.makedirs(out_dir, exist_ok=True)
+    with open(os.path.join(out_dir, name + ".terms"), "w") as f:
+        f.write(f"{{config, #{{n_nodes => {n}, seed => {seed}, rounds => {rounds}}}}}.\n")
+        for r, ids, contacts in joins:
+            pairs = ", ".join(f"{{{int(i)}, {'none' if int(c) == NONE else int(c)}}}" for i, c in zip(ids, contacts))
+            f.write(f"{{join, {r}, [{pairs}]}}.\n")
+        for r, ids in sc["crash"].items():
+            f.write(f"{{crash, {r}, [{', '.join(str(i) for i in ids)}]}}.\n")
+        for r, root, msg in sc["bcast"]:
+            f.write(f"{{broadcast, {r}, {root}, {msg}}}.\n")
+    lines = oracle_stream(n, seed, rounds, joins, sc["bcast"], sc["crash"])
+    with open(os.path.join(out_dir, name + ".oracle"), "w") as f:
+        f.write("\n".join(lines) + "\n")
+    print(f"wrote {name}.terms and {name}.oracle ({len(lines)} records)")
+
+
+def oracle_stream(n, seed, rounds, joins, bcast, crash):
+    from _oracle import Oracle
+    o = Oracle(default_config(n_nodes=n, seed=seed))
+    lib = o._lib
+    ev = {}
+    for r, ids, contacts in joins:
+        ev.setdefault(r, []).append((ids, contacts))
+    bc = {r: (root, msg) for r, root, msg in bcast}
+    lines = []
+    for r in range(rounds):
+        for ids, contacts in ev.get(r, []):
+            o.join(ids, contacts)
+        if r in crash:
+            o.crash(np.array(crash[r], np.uint32))
+        if r in bc:
+            o.broadcast(*bc[r])
+        st = np.zeros(1, _abi.STATS_DTYPE)
+        assert lib.orc_round_emit(o._h, st.ctypes.data) == 0
+        k = C.c_size_t()
+        lib.orc_get_outbox(o._h, None, 0, C.byref(k))
+        box = np.zeros((k.value, 16), np.uint32)
+        lib.orc_get_outbox(o._h, box.ctypes.data, k.value, C.byref(k))
+        for rec in box:
+            dst, src, seq, tt = (int(x) for x in rec[:4])
+            t, ttl, nex = tt & 0xFF, (tt >> 8) & 0xFF, (tt >> 16) & 0xFF
+            ex = "".join(f" {int(x)}" for x in rec[8:8 + nex])
+            lines.append(f"R {r} {src} {seq} {dst} {t} {ttl} {int(rec[4])} {int(rec[5])} {int(rec[6])} {nex}{ex}")
+        box = np.ascontiguousarray(box)
+        assert lib.orc_round_absorb(o._h, box.ctypes.data, box.shape[0]) == 0
+    return lines
+
+
+def compare(harness, oracle):
+    h = [l.rstrip("\n") for l in open(harness) if l.startswith("R ")]
+    o = [l.rstrip("\n") for l in open(oracle) if l.startswith("R ")]
+    buckets = [l for l in open(harness) if l.startswith("B ")]
+    if buckets:
+        with open(os.path.join(os.path.dirname(os.path.abspath(harness)), "bucket16.txt"), "w") as f:
+            f.writelines(buckets)
+    for i, (a, b) in enumerate(zip(h, o)):
+        if a != b:
+            print(f"record {i} differs:\n  harness {a}\n  oracle  {b}")
+            return 1
+    if len(h) != len(o):
+        print(f"record counts differ: harness {len(h)}, oracle {len(o)}")
+        return 1
+    print(f"{len(h)} records identical")
+    return 0
+
+
+if __name__ == "__main__":
+    if sys.argv[1] == "scenario":
+        scenario(sys.argv[2], sys.argv[3])
+    else:
+        sys.exit(compare(sys.argv[2], sys.argv[3]))

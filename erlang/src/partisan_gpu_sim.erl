@@ -3,7 +3,7 @@
 %% to the harness node_spec #{name => 'n<id>@sim', ...} (DESIGN.md section 2).
 -module(partisan_gpu_sim).
 -export([create/1, join/3, crash/2, revive/2, leave/2, leave_node/3, broadcast/3, step/2, active/2, members/3,
-         delivery/2, histograms/1, snapshot/1, restore/2]).
+         delivery/2, histograms/1, snapshot/1, restore/2, set_partition/2, clear_partition/1, node/2]).
 -on_load(init/0).
 
 init() ->
@@ -38,7 +38,16 @@ histograms(_Sim) -> erlang:nif_error(nif_not_loaded).
 snapshot(_Sim) -> erlang:nif_error(nif_not_loaded).
 restore(_Sim, _Bin) -> erlang:nif_error(nif_not_loaded).
 
+%% the partition group of every node (a list of N small integers): an
+%% injected partition as a network partition (DESIGN.md section 2);
+%% clear_partition/1 resolves it
+set_partition(Sim, Groups) -> set_partition_nif(Sim, << <<G:8>> || G <- Groups >>).
+clear_partition(_Sim) -> erlang:nif_error(nif_not_loaded).
+%% one node: {ok, #{up, epoch, active, passive, have, round}}
+node(_Sim, _Node) -> erlang:nif_error(nif_not_loaded).
+
 pack(Ids) -> << <<I:32/little>> || I <- Ids >>.
+set_partition_nif(_S, _G) -> erlang:nif_error(nif_not_loaded).
 join_nif(_S, _N, _C) -> erlang:nif_error(nif_not_loaded).
 crash_nif(_S, _N) -> erlang:nif_error(nif_not_loaded).
 revive_nif(_S, _N) -> erlang:nif_error(nif_not_loaded).

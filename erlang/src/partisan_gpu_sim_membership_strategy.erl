@@ -15,8 +15,15 @@
 
 -export([init/1, join/3, leave/2, periodic/1, handle_message/2]).
 
--record(sim_strategy, {sim, me :: non_neg_integer(), n :: pos_integer(), driver :: boolean()}).
+-record(sim_strategy, {sim, me :: non_neg_integer(), n :: pos_integer(), driver :: boolean(),
+                       started = false :: boolean()}).
 
+-define(NONE, 16#FFFFFFFF).
+
+%% The node starts in the simulator exactly once: at join/3 with its contact,
+%% or -- a seed that never joins -- at its first periodic/1 without one.
+%% (psim_join refuses a second start of a node in one round, and a full-
+%% strategy node cannot restart at all.)
 init(_Identity) ->
     N = partisan_config:get(sim_nodes, 32),
     Me = partisan_config:get(sim_node, 0),
@@ -32,16 +39,19 @@ init(_Identity) ->
                                                   periodic_interval => 10});
                     H -> {ok, H}
                 end,
-    ok = partisan_gpu_sim:join(Sim, [Me], [16#FFFFFFFF]),
     State = #sim_strategy{sim = Sim, me = Me, n = N,
                           driver = partisan_config:get(sim_driver, false)},
     {ok, membership(State), State}.
 
 %% Strategy:join/3 at the joiner: the simulated hello/state handshake and the
-%% strategy's join happen in the next rounds of the simulator.
+%% strategy's join happen in the next rounds of the simulator.  A second
+%% join of a running node is not forwarded (the node keeps its state).
+join(State = #sim_strategy{started = true}, _Node, _RemoteState) ->
+    {ok, membership(State), [], State};
 join(State = #sim_strategy{sim = Sim, me = Me}, #{name := Name}, _RemoteState) ->
     ok = partisan_gpu_sim:join(Sim, [Me], [id(Name)]),
-    {ok, membership(State), [], State}.
+    State1 = State#sim_strategy{started = true},
+    {ok, membership(State1), [], State1}.
 
 %% leave/2: the pluggable manager calls it from handle_call({leave, Node})
 %% (pluggable:502-515).  Node = myself is leave/0 (the node stops in the next
@@ -53,6 +63,9 @@ leave(State = #sim_strategy{sim = Sim, me = Me}, #{name := Name}) ->
          end,
     {ok, membership(State), [], State}.
 
+periodic(State = #sim_strategy{started = false, sim = Sim, me = Me}) ->
+    ok = partisan_gpu_sim:join(Sim, [Me], [?NONE]),          % a seed: starts alone
+    periodic(State#sim_strategy{started = true});
 periodic(State = #sim_strategy{sim = Sim, driver = true}) ->
     {ok, _Stats} = partisan_gpu_sim:step(Sim, 1),
     {ok, membership(State), [], State};
@@ -63,11 +76,16 @@ periodic(State) ->
 handle_message(State, _Message) ->
     {ok, membership(State), [], State}.
 
+membership(#sim_strategy{started = false, me = Me}) ->
+    [spec(Me)];                                              % init/1: [Myself]
 membership(#sim_strategy{sim = Sim, me = Me, n = N}) ->
     {ok, Ids} = partisan_gpu_sim:members(Sim, Me, N),
-    [#{name => name(I), listen_addrs => [#{ip => {10, (I bsr 16) band 255, (I bsr 8) band 255, I band 255},
+    [spec(I) || I <- Ids].
+
+spec(I) ->
+    #{name => name(I), listen_addrs => [#{ip => {10, (I bsr 16) band 255, (I bsr 8) band 255, I band 255},
                                            port => 9090}],
-       channels => [undefined], parallelism => 1} || I <- Ids].
+       channels => [undefined], parallelism => 1}.
 
 name(Id) -> list_to_atom(lists:flatten(io_lib:format("n~10..0B@sim", [Id]))).
 id(Name) ->

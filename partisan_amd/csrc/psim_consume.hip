@@ -77,6 +77,8 @@ struct Wv {
     uint64_t dc_base;
     // emissions are staged in LDS and written once per node (flush_recs), so
     // the body issues no global store: a later vmcnt wait never drains one
+    uint32_t* inb;       // inbox messages 4..15 of the node (3 chunks x 64 words),
+                         // prefetched with the node's second input stage
     uint32_t* srec;      // STAGE records x 16 words
     uint32_t* skey;      // their route keys
     uint32_t flushed;    // records already written for this node
@@ -86,6 +88,7 @@ struct Wv {
 };
 constexpr uint64_t NONE64 = ~0ull;
 constexpr uint32_t STAGE = 16;
+constexpr uint32_t INB_CHUNKS = 3;   // inbox chunks after the first held in LDS (messages 4..15)
 
 // stats: lane k of SC holds slot k's count for this wave; flushed once per wave
 DEV void st_add(Wv& w, int k, uint32_t v) { w.SC += lane_id() == (uint32_t)k ? v : 0u; }
@@ -760,6 +763,14 @@ DEV uint32_t load_chunk(const RoundArgs& a, uint32_t ib, uint32_t ik, uint32_t c
                                : 0u;
 }
 
+// chunk c (a multiple of 4) of the node's inbox: the first from the first
+// input stage, the next three from LDS (second stage), any later one loaded
+DEV uint32_t inbox_chunk(const Wv& w, const RoundArgs& a, uint32_t ib, uint32_t ik, uint32_t c, uint32_t R0) {
+    if (c == 0) return R0;
+    if (c < 4 * (INB_CHUNKS + 1)) return w.inb[((c >> 2) - 1) * 64 + lane_id()];
+    return load_chunk(a, ib, ik, c);
+}
+
 // A node's inputs arrive in two stages, each issued one step ahead with every
 // lane loading (lanes beyond a row re-read an element of it), so every node
 // issues the same vector memory operations:
@@ -774,6 +785,7 @@ struct NodeIn {
     uint32_t fl, part;
 };
 struct NodeX {
+    uint32_t R[INB_CHUNKS];        // inbox chunks 1..3 (lane l: word l & 15 of message 4c + (l >> 4))
     uint32_t CV, CF;               // view ids (passive 0-31, active 32-39), their flags | part << 8
     uint32_t MS, MR;               // sent / recv maps: peers in lanes 0-31, ids in 32-63
     uint32_t PA, PE, PO;           // pt_all | pt_com, pt_eag | pt_laz, pt_out (lo, hi words)
@@ -803,6 +815,16 @@ DEV NodeX load_x(const RoundArgs& a, const NodeIn& x) {
     uint32_t l = lane_id();
     NodeX y;
     const size_t li = x.n - a.lo;
+    {
+        // the rest of the inbox up to message 15, a record index clamped into
+        // the node's run (or the spare record after an empty one)
+        const uint32_t last = x.ik ? x.ik - 1 : 0u;
+#pragma unroll
+        for (uint32_t c = 0; c < INB_CHUNKS; c++) {
+            const uint32_t m = min(4 * (c + 1) + (l >> 4), last);
+            y.R[c] = reinterpret_cast<const uint32_t*>(a.rec_in + x.ib + m)[l & 15];
+        }
+    }
     const uint32_t hw9 = rl(x.H, 9);                 // act_n, pas_n, .. (Hdr word 9)
     const uint32_t act_n = hw9 & 0xFF, pas_n = (hw9 >> 8) & 0xFF;
     uint32_t av = shfl(x.A, (int)(l & 7));
@@ -837,6 +859,8 @@ DEV void begin_node(Wv& w, const NodeIn& x, const NodeX& y) {
     w.obase = x.ob;
     w.mypart = x.part;
     w.CV = y.CV; w.CF = y.CF;
+#pragma unroll
+    for (uint32_t c = 0; c < INB_CHUNKS; c++) w.inb[c * 64 + l] = y.R[c];
     uint32_t msi = shfl(y.MS, (int)((l + 32) & 63)), mri = shfl(y.MR, (int)((l + 32) & 63));
     w.SP = l < 32 ? y.MS : 0u; w.SI = l < 32 ? msi : 0u;
     w.RP = l < 32 ? y.MR : 0u; w.RI = l < 32 ? mri : 0u;
@@ -903,7 +927,7 @@ DEV void body(Wv& w, const NodeIn& x) {
 
     STAMP(w, 2);
     for (uint32_t c = 0; c < ik; c += 4) {            // HyParView inbox, canonical order
-        uint32_t R4 = c == 0 ? R0 : load_chunk(a, ib, ik, c);
+        uint32_t R4 = inbox_chunk(w, a, ib, ik, c, R0);
         uint32_t cm = ik - c < 4 ? ik - c : 4;
         for (uint32_t q = 0; q < cm; q++) {
             uint32_t b = q * 16;
@@ -935,7 +959,7 @@ DEV void body(Wv& w, const NodeIn& x) {
         replay_notifies(w);
         STAMP(w, 15);
         for (uint32_t c = 0; c < ik; c += 4) {        // Plumtree inbox
-            uint32_t R4 = c == 0 ? R0 : load_chunk(a, ib, ik, c);
+            uint32_t R4 = inbox_chunk(w, a, ib, ik, c, R0);
             uint32_t cm = ik - c < 4 ? ik - c : 4;
             for (uint32_t q = 0; q < cm; q++) {
                 uint32_t b = q * 16;
@@ -1034,6 +1058,7 @@ __global__ void __launch_bounds__(256, PSIM_WAVES_PER_SIMD) k_consume(RoundArgs 
     __shared__ uint32_t nlogs[WAVES_PER_BLOCK][NLOG * (PSIM_ACTIVE_CAP + 1)];
     __shared__ __attribute__((aligned(16))) uint32_t srecs[WAVES_PER_BLOCK][STAGE * 16];
     __shared__ uint32_t skeys[WAVES_PER_BLOCK][STAGE];
+    __shared__ uint32_t inbs[WAVES_PER_BLOCK][INB_CHUNKS * 64];
     for (int i = threadIdx.x; i < NST; i += blockDim.x) sst[i] = 0;
     if (threadIdx.x == 0) atomicMin(&args.ktime[0], (unsigned long long)__builtin_amdgcn_s_memrealtime());
     __syncthreads();
@@ -1047,6 +1072,7 @@ __global__ void __launch_bounds__(256, PSIM_WAVES_PER_SIMD) k_consume(RoundArgs 
     w.nlog = nlogs[wid];
     w.srec = srecs[wid];
     w.skey = skeys[wid];
+    w.inb = inbs[wid];
 #ifdef PSIM_STAMPS
     __shared__ uint64_t stamps[WAVES_PER_BLOCK][32];
     if ((threadIdx.x & 63) < 32) stamps[wid][threadIdx.x & 63] = 0;

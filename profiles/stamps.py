@@ -42,13 +42,22 @@ def main():
     sim = Simulator(default_config(n_nodes=a.nodes, seed=1))
     boot = W.doubling_join(a.nodes, 1)
     sim.run_schedule(boot, boot[-1][0] + 61)
+    # bench.py's schedule: 45 untimed broadcast rounds (steady state), then
+    # the measured rounds, a broadcast from node 0 every 10 rounds
+    k = 0
+    for i in range(45):
+        if i % 10 == 0:
+            sim.broadcast(0, k)
+            k += 1
+        sim.step(1)
     if lib.psim_debug_stamps(buf, 32) != 32:
         print("library built without -DPSIM_STAMPS")
         return
     st = []
-    for i in range(a.steps):
+    for i in range(45, 45 + a.steps):
         if i % 10 == 0:
-            sim.broadcast(0, i)
+            sim.broadcast(0, k)
+            k += 1
         st.append(sim.step(1))
     lib.psim_debug_stamps(buf, 32)
     st = np.concatenate(st)

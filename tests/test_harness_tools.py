@@ -1,0 +1,39 @@
+"""The harness comparison tool (erlang/harness/compare_trace.py) on CPU:
+its scenario files and the oracle's record stream are well formed, the
+stream is deterministic, and compare() flags the first differing record.
+The Erlang side itself cannot run here (no Erlang VM)."""
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+TOOL = os.path.join(ROOT, "erlang", "harness", "compare_trace.py")
+
+
+def _run(*a):
+    return subprocess.run([sys.executable, TOOL] + list(a), capture_output=True, text=True, timeout=300)
+
+
+def test_scenario_and_compare(tmp_path):
+    d = str(tmp_path)
+    r = _run("scenario", "doubling_crash_256", d)
+    assert r.returncode == 0, r.stderr
+    terms = open(os.path.join(d, "doubling_crash_256.terms")).read()
+    assert terms.startswith("{config, #{n_nodes => 256") and "{crash, 40, [5, 22" in terms
+    stream = os.path.join(d, "doubling_crash_256.oracle")
+    lines = open(stream).read().splitlines()
+    assert len(lines) > 1000 and all(l.startswith("R ") for l in lines)
+    # (src, seq) numbering: per round and source, seq runs 0, 1, 2, ...
+    seen = {}
+    for l in lines:
+        f = l.split()
+        key = (f[1], f[2])
+        assert int(f[3]) == seen.get(key, -1) + 1
+        seen[key] = int(f[3])
+    assert _run("compare", stream, stream).returncode == 0
+    bad = os.path.join(d, "bad")
+    mod = lines[:]
+    mod[500] = mod[500].rsplit(" ", 1)[0] + " 999"
+    open(bad, "w").write("\n".join(mod) + "\n")
+    r = _run("compare", bad, stream)
+    assert r.returncode == 1 and "record 500 differs" in r.stdout
