@@ -342,7 +342,7 @@ static ERL_NIF_TERM id_list(ErlNifEnv *env, const uint32_t *v, uint32_t n) {
 
 /* node(Ref, Node) -> {ok, #{up, epoch, active, passive, have, round}} :
  * one node's HyParView views (sets:to_list order) and its Plumtree
- * delivery mask (bit m: message id m mod 32 merged, plumtree_backend ETS) */
+ * delivery mask (bit m: message id m mod 64 merged, plumtree_backend ETS) */
 static ERL_NIF_TERM nif_node(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[]) {
     sim_res *r; unsigned node;
     psim_node_view v;
@@ -359,7 +359,7 @@ static ERL_NIF_TERM nif_node(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[]
     enif_make_map_put(env, m, enif_make_atom(env, "epoch"), enif_make_uint(env, v.epoch), &m);
     enif_make_map_put(env, m, enif_make_atom(env, "active"), id_list(env, v.act, v.act_n), &m);
     enif_make_map_put(env, m, enif_make_atom(env, "passive"), id_list(env, v.pas, v.pas_n), &m);
-    enif_make_map_put(env, m, enif_make_atom(env, "have"), enif_make_uint(env, v.have), &m);
+    enif_make_map_put(env, m, enif_make_atom(env, "have"), enif_make_uint64(env, v.have), &m);
     enif_make_map_put(env, m, enif_make_atom(env, "round"), enif_make_uint64(env, round), &m);
     return enif_make_tuple2(env, enif_make_atom(env, "ok"), m);
 }

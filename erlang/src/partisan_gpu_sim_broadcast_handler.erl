@@ -9,7 +9,7 @@
 %% Messages follow the backend's heartbeat shape: the id is
 %% {RootName, Counter} (plumtree_backend:179-200) and the payload is the id.
 %% Counter is the simulator's 16-bit message id; the delivery state of a node
-%% is a mask over Counter mod 32 (DESIGN.md section 2).
+%% is a mask over Counter mod 64 (PSIM_MSG_SLOTS, DESIGN.md section 2).
 %%
 %%   broadcast_data/1  {Id, Payload} of a #sim_broadcast{}        (handler :23-24)
 %%   merge/2           true iff the simulated node had not yet
@@ -41,7 +41,7 @@ merge(Id, _Payload) ->
 is_stale({_Root, Counter}) ->
     {Sim, Me} = handle(),
     {ok, #{have := Have}} = partisan_gpu_sim:node(Sim, Me),
-    (Have bsr (Counter band 31)) band 1 =:= 1.
+    (Have bsr (Counter rem 64)) band 1 =:= 1.
 
 graft(Id) ->
     case is_stale(Id) of

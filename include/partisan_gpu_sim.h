@@ -29,7 +29,7 @@
  *       (modelled as a network partition)
  *   psim_broadcast
  *       partisan_plumtree_broadcast:broadcast/2 with the default
- *       partisan_plumtree_backend handler                       (plumtree:176-178, backend:179-200)
+ *       partisan_plumtree_backend handler, any number of roots  (plumtree:176-178, backend:179-200)
  *   psim_step
  *       one BSP round of every node's timers and inbox:
  *       hyparview handle_message/2 (:693-1166), handle_info timers (:542-607),
@@ -64,7 +64,7 @@
 extern "C" {
 #endif
 
-#define PSIM_ABI_VERSION 3
+#define PSIM_ABI_VERSION 4
 
 /* error codes */
 #define PSIM_OK 0
@@ -131,6 +131,16 @@ enum psim_pl_msg_type {
 #define PSIM_PT_SET_CAP 16
 #define PSIM_PT_OUT_CAP 32
 #define PSIM_EXCHANGE_CAP 8
+/* Plumtree roots a node keeps per-root eager/lazy sets for at once
+ * (eager_sets / lazy_sets orddicts, plumtree:76-84, :599-631): a root
+ * touched with every slot taken counts an overflow and is served from the
+ * common sets. */
+#define PSIM_PT_ROOTS 4
+/* Live broadcast messages: message id m owns slot m mod PSIM_MSG_SLOTS of
+ * every node's delivery mask (plumtree_backend's ETS set, :140-167); a new
+ * broadcast retires the previous id of its slot, and a message of a retired
+ * id still in flight counts an overflow and is treated as stale. */
+#define PSIM_MSG_SLOTS 64
 
 typedef struct psim_config {
     uint32_t abi_version;        /* must be PSIM_ABI_VERSION */
@@ -186,7 +196,7 @@ typedef struct psim_round_stats {
 
 /* Canonical per-node view (inspection; unused slots zero). */
 typedef struct psim_node_view {
-    uint32_t up, epoch, start_round, pt_root;
+    uint32_t up, epoch, start_round, pad0;
     uint64_t rng_ctr;
     uint32_t act_n, pas_n;
     uint32_t act[PSIM_ACTIVE_CAP];           /* sets:to_list order, self included */
@@ -194,11 +204,14 @@ typedef struct psim_node_view {
     uint32_t sent_n, sent_head, recv_n, recv_head;
     uint32_t sent_peer[PSIM_IDMAP_CAP], sent_id[PSIM_IDMAP_CAP];
     uint32_t recv_peer[PSIM_IDMAP_CAP], recv_id[PSIM_IDMAP_CAP];
-    uint32_t pt_all_n, pt_common_n, pt_eager_n, pt_lazy_n, pt_out_n, pt_pad;
+    uint32_t pt_all_n, pt_common_n, pt_out_n, pt_pad;
     uint32_t pt_all[PSIM_PT_MEMBERS_CAP], pt_common[PSIM_PT_MEMBERS_CAP];
-    uint32_t pt_eager[PSIM_PT_SET_CAP], pt_lazy[PSIM_PT_SET_CAP];
+    /* per-root sets, slot k: root pt_root[k] (PSIM_NONE = free) */
+    uint32_t pt_root[PSIM_PT_ROOTS], pt_eager_n[PSIM_PT_ROOTS], pt_lazy_n[PSIM_PT_ROOTS];
+    uint32_t pt_eager[PSIM_PT_ROOTS][PSIM_PT_SET_CAP], pt_lazy[PSIM_PT_ROOTS][PSIM_PT_SET_CAP];
     uint32_t pt_out_peer[PSIM_PT_OUT_CAP], pt_out_msg[PSIM_PT_OUT_CAP], pt_out_round[PSIM_PT_OUT_CAP];
-    uint32_t have, trk_round, trk_hop, pad1;
+    uint64_t have;                           /* delivered: bit (msg id mod PSIM_MSG_SLOTS) */
+    uint32_t trk_round, trk_hop;
 } psim_node_view;
 
 /* Per-node state of a PLUGGABLE handle (inspection; unused slots zero). */
@@ -282,6 +295,11 @@ int psim_leave(psim_handle *h, const uint32_t *nodes, size_t n);
 int psim_leave_node(psim_handle *h, const uint32_t *actors, const uint32_t *targets, size_t n);
 int psim_set_partition(psim_handle *h, const uint8_t *group, size_t n);
 int psim_clear_partition(psim_handle *h);
+/* broadcast/2 at `root` (plumtree:176-178) with the partisan_plumtree_backend
+ * heartbeat semantics (backend:179-200), originated in the next round.  Any
+ * node can be a root; per round at most one broadcast per root and per
+ * message slot (msg_id mod PSIM_MSG_SLOTS), else PSIM_EINVAL.  The last call
+ * names the tracked broadcast of psim_get_delivery / psim_get_histograms. */
 int psim_broadcast(psim_handle *h, uint32_t root, uint32_t msg_id);
 
 /* Run n_rounds BSP rounds; stats (may be NULL) receives one entry per round. */

@@ -64,11 +64,13 @@ typedef struct node {
     uint32_t recv_peer[PSIM_IDMAP_CAP], recv_id[PSIM_IDMAP_CAP], recv_n, recv_head;
     uint32_t pt_all[PSIM_PT_MEMBERS_CAP], pt_all_n;
     uint32_t pt_common[PSIM_PT_MEMBERS_CAP], pt_common_n;
-    uint32_t pt_root;
-    uint32_t pt_eager[PSIM_PT_SET_CAP], pt_eager_n;
-    uint32_t pt_lazy[PSIM_PT_SET_CAP], pt_lazy_n;
+    /* eager_sets / lazy_sets (plumtree:76-84): one slot per root, PSIM_NONE = free */
+    uint32_t rt_root[PSIM_PT_ROOTS];
+    uint32_t rt_eag[PSIM_PT_ROOTS][PSIM_PT_SET_CAP], rt_eag_n[PSIM_PT_ROOTS];
+    uint32_t rt_laz[PSIM_PT_ROOTS][PSIM_PT_SET_CAP], rt_laz_n[PSIM_PT_ROOTS];
     uint32_t out_peer[PSIM_PT_OUT_CAP], out_msg[PSIM_PT_OUT_CAP], out_round[PSIM_PT_OUT_CAP], out_n;
-    uint32_t have, trk_round, trk_hop;
+    uint64_t have;                  /* plumtree_backend ETS: bit (msg id mod PSIM_MSG_SLOTS) */
+    uint32_t trk_round, trk_hop;
 } node;
 
 typedef struct omsg {
@@ -106,9 +108,11 @@ struct psim_handle {
     uint8_t *pend_join_mark;   /* ids in pend_join: a node starts at most once per round */
     uint32_t *pend_lv_a, *pend_lv_t; size_t pend_lv_n, pend_lv_cap;
     uint8_t *pend_part; int pend_part_set, pend_part_clear;
-    int pend_bcast; uint32_t pend_root, pend_msg;
-    uint32_t bcast_root;            /* single-root restriction */
-    uint32_t origin_node, origin_msg; int origin_now;
+    /* broadcasts of the next round (psim_broadcast, in call order) */
+    uint32_t pend_b_root[PSIM_MSG_SLOTS], pend_b_msg[PSIM_MSG_SLOTS]; uint32_t pend_b_n;
+    /* message slots: the id owning slot k and its root (node_spec map identity) */
+    uint32_t slot_msg[PSIM_MSG_SLOTS], slot_root[PSIM_MSG_SLOTS];
+    uint32_t *origin;               /* per node: message id + 1 it originates this round, 0 = none */
     uint32_t tracked_msg;
     psim_round_stats *st;           /* stats of the round being executed */
     /* PLUGGABLE handles */
@@ -453,6 +457,19 @@ static void pt_set_add(uint32_t *l, uint32_t *n, uint32_t cap, uint32_t e, ctx *
 
 static void pt_set_del(uint32_t *l, uint32_t *n, uint32_t e) { set_del(l, n, e); }
 
+static void rt_clear(node *s, int k) {
+    s->rt_root[k] = PSIM_NONE;
+    memset(s->rt_eag[k], 0, sizeof s->rt_eag[k]); s->rt_eag_n[k] = 0;
+    memset(s->rt_laz[k], 0, sizeof s->rt_laz[k]); s->rt_laz_n[k] = 0;
+}
+
+/* the root slot of `root`, -1 if it has no per-root sets */
+static int rt_find(const node *s, uint32_t root) {
+    for (int k = 0; k < PSIM_PT_ROOTS; k++)
+        if (s->rt_root[k] == root) return k;
+    return -1;
+}
+
 /* notify/1 (hyparview:1598-1599) -> partisan_peer_service:decode/1
  * (peer_service.erl:117-119) -> plumtree update/1 -> handle_cast({update,..})
  * (plumtree:314-336), reset_peers/4 (:652-659), neighbors_down/2 (:404-423). */
@@ -475,10 +492,9 @@ static void notify(ctx *c) {
         memset(s->pt_common, 0, sizeof s->pt_common);
         for (uint32_t i = 0; i < nu; i++) s->pt_common[i] = u[i];
         s->pt_common_n = nu;
-        /* del_element(myself(), ..) removes nothing: myself() is a map (Q6) */
-        s->pt_root = PSIM_NONE;
-        memset(s->pt_eager, 0, sizeof s->pt_eager); s->pt_eager_n = 0;
-        memset(s->pt_lazy, 0, sizeof s->pt_lazy); s->pt_lazy_n = 0;
+        /* del_element(myself(), ..) removes nothing: myself() is a map (Q6);
+         * eager_sets = lazy_sets = orddict:new() (:656-657) */
+        for (int k = 0; k < PSIM_PT_ROOTS; k++) rt_clear(s, k);
         memset(s->pt_all, 0, sizeof s->pt_all);
         for (uint32_t i = 0; i < ncur; i++) s->pt_all[i] = cur[i];
         s->pt_all_n = ncur;
@@ -486,10 +502,11 @@ static void notify(ctx *c) {
     /* neighbors_down(Removed, ..) */
     for (uint32_t i = 0; i < nrem; i++) {
         pt_set_del(s->pt_common, &s->pt_common_n, rem[i]);
-        if (s->pt_root != PSIM_NONE) {
-            pt_set_del(s->pt_eager, &s->pt_eager_n, rem[i]);
-            pt_set_del(s->pt_lazy, &s->pt_lazy_n, rem[i]);
-        }
+        for (int k = 0; k < PSIM_PT_ROOTS; k++)        /* every root's sets (:410-413) */
+            if (s->rt_root[k] != PSIM_NONE) {
+                pt_set_del(s->rt_eag[k], &s->rt_eag_n[k], rem[i]);
+                pt_set_del(s->rt_laz[k], &s->rt_laz_n[k], rem[i]);
+            }
         uint32_t j = 0;
         for (uint32_t k = 0; k < s->out_n; k++)
             if (s->out_peer[k] != rem[i]) {
@@ -504,42 +521,51 @@ static void notify(ctx *c) {
 /* all_peers/3 (plumtree:627-631): the per-root set or the common default */
 static void pt_get(ctx *c, uint32_t root, uint32_t *eg, uint32_t *ne, uint32_t *lz, uint32_t *nl) {
     node *s = c->s;
-    if (s->pt_root != PSIM_NONE && s->pt_root == root) {
-        *ne = s->pt_eager_n; memcpy(eg, s->pt_eager, sizeof s->pt_eager);
-        *nl = s->pt_lazy_n; memcpy(lz, s->pt_lazy, sizeof s->pt_lazy);
+    int k = rt_find(s, root);
+    if (k >= 0) {
+        *ne = s->rt_eag_n[k]; memcpy(eg, s->rt_eag[k], sizeof s->rt_eag[k]);
+        *nl = s->rt_laz_n[k]; memcpy(lz, s->rt_laz[k], sizeof s->rt_laz[k]);
     } else {
-        memset(eg, 0, sizeof s->pt_eager); memset(lz, 0, sizeof s->pt_lazy);
+        memset(eg, 0, PSIM_PT_SET_CAP * 4); memset(lz, 0, PSIM_PT_SET_CAP * 4);
         *ne = s->pt_common_n;
         for (uint32_t i = 0; i < s->pt_common_n; i++) eg[i] = s->pt_common[i];
         *nl = 0;                                   /* common_lazys is always [] */
     }
 }
 
-/* update_peers/5 + set_peers/4 (plumtree:593-609) */
+/* update_peers/5 + set_peers/4 (plumtree:593-609): orddict:store(Root, ..)
+ * into the root's slot, a new root into the lowest free slot; with every
+ * slot taken the store is an overflow (the sets stay as they were) */
 static void pt_update(ctx *c, uint32_t from, uint32_t root, int to_eager) {
     node *s = c->s;
     uint32_t eg[PSIM_PT_SET_CAP], lz[PSIM_PT_SET_CAP], ne, nl;
     pt_get(c, root, eg, &ne, lz, &nl);
     if (to_eager) { pt_set_add(eg, &ne, PSIM_PT_SET_CAP, from, c); pt_set_del(lz, &nl, from); }
     else { pt_set_del(eg, &ne, from); pt_set_add(lz, &nl, PSIM_PT_SET_CAP, from, c); }
-    if (s->pt_root != PSIM_NONE && s->pt_root != root) { c->h->st->overflow++; return; }
-    s->pt_root = root;
-    memcpy(s->pt_eager, eg, sizeof eg); s->pt_eager_n = ne;
-    memcpy(s->pt_lazy, lz, sizeof lz); s->pt_lazy_n = nl;
+    int k = rt_find(s, root);
+    if (k < 0) k = rt_find(s, PSIM_NONE);
+    if (k < 0) { c->h->st->overflow++; return; }
+    s->rt_root[k] = root;
+    memcpy(s->rt_eag[k], eg, sizeof eg); s->rt_eag_n[k] = ne;
+    memcpy(s->rt_laz[k], lz, sizeof lz); s->rt_laz_n[k] = nl;
 }
 
 /* send/3 (plumtree:633-638) -> cast_message -> forward_message: succeeds only
  * over an existing connection of this node's manager. */
-static void pt_send(ctx *c, uint32_t ident, uint32_t type, uint32_t msg, uint32_t rnd,
-                    uint32_t root) {
+static int pt_conn(ctx *c, uint32_t ident) {
     uint32_t id = ident & ~PSIM_MAP_BIT;
     node *s = c->s;
-    if (id == c->me || !list_member(s->act, s->act_n, id) || !c->h->nodes[id].up ||
-        c->h->part[id] != c->h->part[c->me]) {
+    return !(id == c->me || !list_member(s->act, s->act_n, id) || !c->h->nodes[id].up ||
+             c->h->part[id] != c->h->part[c->me]);
+}
+
+static void pt_send(ctx *c, uint32_t ident, uint32_t type, uint32_t msg, uint32_t rnd,
+                    uint32_t root) {
+    if (!pt_conn(c, ident)) {
         c->h->st->send_fail++;
         return;
     }
-    emit(c, id, type, 0, msg, rnd, root, NULL, 0);
+    emit(c, ident & ~PSIM_MAP_BIT, type, 0, msg, rnd, root, NULL, 0);
 }
 
 /* add_outstanding/6 (plumtree:574-579): ordset keyed by peer, then {Id,..,Round,Root} */
@@ -576,7 +602,22 @@ static void pt_ack_out(ctx *c, uint32_t peer, uint32_t msg, uint32_t rnd) {
         }
 }
 
-static int pt_have(ctx *c, uint32_t msg) { return (c->s->have >> (msg & 31u)) & 1u; }
+/* plumtree_backend is_stale/1 (:101-104, :148-152) over the node's message
+ * slots; a retired id (its slot taken by a newer broadcast) is an overflow
+ * and answers stale */
+static int pt_have(ctx *c, uint32_t msg) {
+    uint32_t k = msg % PSIM_MSG_SLOTS;
+    if (c->h->slot_msg[k] != msg) { c->h->st->overflow++; return 1; }
+    return (int)((c->s->have >> k) & 1u);
+}
+
+/* the root of a live message id (IHAVE of an outstanding entry); a retired
+ * id is an overflow and PSIM_NONE */
+static uint32_t msg_root(ctx *c, uint32_t msg) {
+    uint32_t k = msg % PSIM_MSG_SLOTS;
+    if (c->h->slot_msg[k] != msg) { c->h->st->overflow++; return PSIM_NONE; }
+    return c->h->slot_root[k];
+}
 
 /* eager_push/7 + schedule_lazy_push/6 (plumtree:428-441) */
 static void pt_push(ctx *c, uint32_t msg, uint32_t rnd, uint32_t root, uint32_t from) {
@@ -596,7 +637,7 @@ static void pt_handle(ctx *c, const omsg *m) {
     case PSIM_MSG_PT_BROADCAST: {                 /* plumtree:288-293, :368-378 */
         int valid = !pt_have(c, msg);             /* plumtree_backend merge/2 :87-96 */
         if (valid) {
-            s->have |= 1u << (msg & 31u);
+            s->have |= 1ull << (msg % PSIM_MSG_SLOTS);
             c->h->st->first_deliveries++;
             if (msg == c->h->tracked_msg) { s->trk_round = (uint32_t)c->h->round; s->trk_hop = rnd + 1; }
             pt_update(c, from, root, 1);
@@ -770,7 +811,7 @@ static void process_node(struct psim_handle *h, uint32_t n) {
     /* a due promotion timer is work only if it can act (hv:547-551) */
     int promo_work = promo && s->act_n < h->cfg.min_active_size;
     int shuf = timer_due(h->cfg.shuffle_period, r, s->start_round);
-    int origin = h->origin_now && h->origin_node == n && h->cfg.plumtree;
+    int origin = h->origin[n] != 0 && h->cfg.plumtree;
     int lazy_due = h->cfg.plumtree && timer_due(h->cfg.lazy_tick_period, r, s->start_round);
     int lazy = lazy_due && s->out_n > 0;
     uint32_t exits[PSIM_ACTIVE_CAP], nexit = 0;
@@ -822,16 +863,18 @@ static void process_node(struct psim_handle *h, uint32_t n) {
         }
 
     if (origin) {                                  /* plumtree:282-287, backend:179-200 */
-        uint32_t my = n | PSIM_MAP_BIT;
-        s->have |= 1u << (h->origin_msg & 31u);
-        s->trk_round = (uint32_t)r; s->trk_hop = 0;
-        pt_push(&c, h->origin_msg, 0, my, my);
+        uint32_t my = n | PSIM_MAP_BIT, msg = h->origin[n] - 1;
+        s->have |= 1ull << (msg % PSIM_MSG_SLOTS);
+        if (msg == h->tracked_msg) { s->trk_round = (uint32_t)r; s->trk_hop = 0; }
+        pt_push(&c, msg, 0, my, my);
     }
 
     if (lazy_due) {                               /* plumtree:341-345, :443-453 */
-        for (uint32_t i = 0; i < s->out_n; i++)
-            pt_send(&c, s->out_peer[i], PSIM_MSG_PT_IHAVE, s->out_msg[i], s->out_round[i],
-                    h->bcast_root);
+        for (uint32_t i = 0; i < s->out_n; i++) {
+            if (!pt_conn(&c, s->out_peer[i])) { h->st->send_fail++; continue; }
+            emit(&c, s->out_peer[i] & ~PSIM_MAP_BIT, PSIM_MSG_PT_IHAVE, 0, s->out_msg[i], s->out_round[i],
+                 msg_root(&c, s->out_msg[i]), NULL, 0);
+        }
     }
 }
 
@@ -1215,7 +1258,7 @@ static void node_init(struct psim_handle *h, uint32_t n, uint32_t contact) {
     s->act[0] = n; s->act_n = 1;                 /* sets:add_element(Myself, ..) :299 */
     s->pt_all[0] = n; s->pt_all_n = 1;           /* plumtree start_link/0 :127-144 */
     s->pt_common[0] = n; s->pt_common_n = 1;
-    s->pt_root = PSIM_NONE;
+    for (int k = 0; k < PSIM_PT_ROOTS; k++) s->rt_root[k] = PSIM_NONE;
     s->trk_round = PSIM_NONE;
     if (is_pl(h)) pl_node_init(h, n, contact);
 }
@@ -1246,21 +1289,29 @@ static void round_begin(struct psim_handle *h, psim_round_stats *st) {
     h->pend_lv_n = 0;
     if (h->pend_part_clear) memset(h->part, 0, h->N);
     if (h->pend_part_set) memcpy(h->part, h->pend_part, h->N);
-    h->origin_now = 0;
-    if (h->pend_bcast) {
-        h->tracked_msg = h->pend_msg;
+    /* broadcasts: each takes its message slot (the slot's previous id is
+     * retired: its delivery bit cleared everywhere) and is originated this
+     * round at its root if the root runs; the last one is the tracked one */
+    for (uint32_t n = 0; n < h->N; n++) h->origin[n] = 0;
+    if (h->pend_b_n) {
+        uint64_t clear = 0;
+        for (uint32_t i = 0; i < h->pend_b_n; i++) {
+            uint32_t k = h->pend_b_msg[i] % PSIM_MSG_SLOTS;
+            clear |= 1ull << k;
+            h->slot_msg[k] = h->pend_b_msg[i];
+            h->slot_root[k] = h->pend_b_root[i] | PSIM_MAP_BIT;
+            if (h->nodes[h->pend_b_root[i]].up) h->origin[h->pend_b_root[i]] = h->pend_b_msg[i] + 1;
+        }
+        h->tracked_msg = h->pend_b_msg[h->pend_b_n - 1];
         for (uint32_t n = 0; n < h->N; n++) {
-            h->nodes[n].have &= ~(1u << (h->pend_msg & 31u));
+            h->nodes[n].have &= ~clear;
             h->nodes[n].trk_round = PSIM_NONE;
             h->nodes[n].trk_hop = 0;
-        }
-        if (h->nodes[h->pend_root].up) {
-            h->origin_now = 1; h->origin_node = h->pend_root; h->origin_msg = h->pend_msg;
         }
     }
     h->pend_crash_n = h->pend_join_n = 0;
     h->pend_part_set = h->pend_part_clear = 0;
-    h->pend_bcast = 0;
+    h->pend_b_n = 0;
 
     h->out.n = 0;
     for (uint32_t n = h->lo; n < h->hi; n++) {
@@ -1352,7 +1403,9 @@ int orc_create(const psim_config *cfg, struct psim_handle **out) {
             if (!h->fbits) return PSIM_ENOMEM;
         }
     }
-    h->bcast_root = PSIM_NONE;
+    h->origin = (uint32_t *)calloc(h->N, sizeof(uint32_t));
+    if (!h->origin) return PSIM_ENOMEM;
+    for (int k = 0; k < PSIM_MSG_SLOTS; k++) h->slot_msg[k] = h->slot_root[k] = PSIM_NONE;
     h->tracked_msg = PSIM_NONE;
     *out = h;
     return PSIM_OK;
@@ -1362,7 +1415,7 @@ void orc_destroy(struct psim_handle *h) {
     if (!h) return;
     free(h->nodes); free(h->part); free(h->crashed_now); free(h->in_beg); free(h->pend_part);
     free(h->inbox.v); free(h->out.v);
-    free(h->pend_crash); free(h->pend_join); free(h->pend_contact); free(h->pend_join_mark);
+    free(h->pend_crash); free(h->pend_join); free(h->pend_contact); free(h->pend_join_mark); free(h->origin);
     free(h->pend_lv_a); free(h->pend_lv_t);
     free(h->sn); free(h->fbits); free(h->pay_in); free(h->pay_out);
     free(h);
@@ -1472,10 +1525,11 @@ int orc_clear_partition(struct psim_handle *h) {
 int orc_broadcast(struct psim_handle *h, uint32_t root, uint32_t msg_id) {
     if (is_pl(h)) return PSIM_EUNSUPPORTED;      /* Plumtree runs over the HyParView manager */
     if (root >= h->N || msg_id > 0xFFFF) return PSIM_ERANGE;
-    uint32_t r = root | PSIM_MAP_BIT;
-    if (h->bcast_root != PSIM_NONE && h->bcast_root != r) return PSIM_EUNSUPPORTED;
-    h->bcast_root = r;
-    h->pend_bcast = 1; h->pend_root = root; h->pend_msg = msg_id;
+    for (uint32_t i = 0; i < h->pend_b_n; i++)    /* one per root and per slot per round */
+        if (h->pend_b_root[i] == root || h->pend_b_msg[i] % PSIM_MSG_SLOTS == msg_id % PSIM_MSG_SLOTS)
+            return PSIM_EINVAL;
+    h->pend_b_root[h->pend_b_n] = root;
+    h->pend_b_msg[h->pend_b_n++] = msg_id;
     return PSIM_OK;
 }
 
@@ -1493,7 +1547,7 @@ int orc_get_nodes(struct psim_handle *h, uint32_t first, uint32_t count, psim_no
         const node *s = &h->nodes[first + k];
         psim_node_view *v = &out[k];
         memset(v, 0, sizeof *v);
-        v->up = s->up; v->epoch = s->epoch; v->start_round = s->start_round; v->pt_root = s->pt_root;
+        v->up = s->up; v->epoch = s->epoch; v->start_round = s->start_round;
         v->rng_ctr = s->rng;
         v->act_n = s->act_n; v->pas_n = s->pas_n;
         memcpy(v->act, s->act, sizeof v->act); memcpy(v->pas, s->pas, sizeof v->pas);
@@ -1501,9 +1555,12 @@ int orc_get_nodes(struct psim_handle *h, uint32_t first, uint32_t count, psim_no
         memcpy(v->sent_peer, s->sent_peer, sizeof v->sent_peer); memcpy(v->sent_id, s->sent_id, sizeof v->sent_id);
         memcpy(v->recv_peer, s->recv_peer, sizeof v->recv_peer); memcpy(v->recv_id, s->recv_id, sizeof v->recv_id);
         v->pt_all_n = s->pt_all_n; v->pt_common_n = s->pt_common_n;
-        v->pt_eager_n = s->pt_eager_n; v->pt_lazy_n = s->pt_lazy_n; v->pt_out_n = s->out_n;
+        v->pt_out_n = s->out_n;
         memcpy(v->pt_all, s->pt_all, sizeof v->pt_all); memcpy(v->pt_common, s->pt_common, sizeof v->pt_common);
-        memcpy(v->pt_eager, s->pt_eager, sizeof v->pt_eager); memcpy(v->pt_lazy, s->pt_lazy, sizeof v->pt_lazy);
+        for (int q = 0; q < PSIM_PT_ROOTS; q++) {
+            v->pt_root[q] = s->rt_root[q]; v->pt_eager_n[q] = s->rt_eag_n[q]; v->pt_lazy_n[q] = s->rt_laz_n[q];
+        }
+        memcpy(v->pt_eager, s->rt_eag, sizeof v->pt_eager); memcpy(v->pt_lazy, s->rt_laz, sizeof v->pt_lazy);
         memcpy(v->pt_out_peer, s->out_peer, sizeof v->pt_out_peer);
         memcpy(v->pt_out_msg, s->out_msg, sizeof v->pt_out_msg);
         memcpy(v->pt_out_round, s->out_round, sizeof v->pt_out_round);
@@ -1516,7 +1573,7 @@ int orc_get_nodes(struct psim_handle *h, uint32_t first, uint32_t count, psim_no
 int orc_get_delivery(struct psim_handle *h, uint32_t first, uint32_t count, uint8_t *have, uint32_t *round,
                      uint32_t *hop) {
     if ((uint64_t)first + count > h->N) return PSIM_ERANGE;
-    uint32_t bit = h->tracked_msg == PSIM_NONE ? 0u : 1u << (h->tracked_msg & 31u);
+    uint64_t bit = h->tracked_msg == PSIM_NONE ? 0ull : 1ull << (h->tracked_msg % PSIM_MSG_SLOTS);
     for (uint32_t k = 0; k < count; k++) {
         const node *s = &h->nodes[first + k];
         have[k] = (s->have & bit) ? 1 : 0;
@@ -1541,7 +1598,7 @@ int orc_get_histograms(struct psim_handle *h, psim_histograms *out) {
     uint32_t N = h->N;
     uint32_t *ina = calloc(N, 4), *inp = calloc(N, 4), *par = malloc((size_t)N * 4), *sz = calloc(N, 4);
     if (!ina || !inp || !par || !sz) { free(ina); free(inp); free(par); free(sz); return PSIM_ENOMEM; }
-    uint32_t bit = h->tracked_msg == PSIM_NONE ? 0u : 1u << (h->tracked_msg & 31u);
+    uint64_t bit = h->tracked_msg == PSIM_NONE ? 0ull : 1ull << (h->tracked_msg % PSIM_MSG_SLOTS);
     for (uint32_t i = 0; i < N; i++) par[i] = i;
     for (uint32_t i = 0; i < N; i++) {
         const node *s = &h->nodes[i];

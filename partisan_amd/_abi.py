@@ -8,11 +8,12 @@ import ctypes as C
 
 import numpy as np
 
-PSIM_ABI_VERSION = 3
+PSIM_ABI_VERSION = 4
 PSIM_MAP_BIT = 0x80000000
 PSIM_NONE = 0xFFFFFFFF
 ACTIVE_CAP, PASSIVE_CAP, IDMAP_CAP = 8, 32, 32
 PT_MEMBERS_CAP, PT_SET_CAP, PT_OUT_CAP, EXCHANGE_CAP = 8, 16, 32, 8
+PT_ROOTS, MSG_SLOTS = 4, 64
 NTYPES = 16
 SVIEW_CAP = 64
 MANAGER_HYPARVIEW, MANAGER_PLUGGABLE = 0, 1
@@ -63,21 +64,22 @@ class PsimRoundStats(C.Structure):
 class PsimNodeView(C.Structure):
     _fields_ = [
         ("up", C.c_uint32), ("epoch", C.c_uint32), ("start_round", C.c_uint32),
-        ("pt_root", C.c_uint32), ("rng_ctr", C.c_uint64),
+        ("pad0", C.c_uint32), ("rng_ctr", C.c_uint64),
         ("act_n", C.c_uint32), ("pas_n", C.c_uint32),
         ("act", C.c_uint32 * ACTIVE_CAP), ("pas", C.c_uint32 * PASSIVE_CAP),
         ("sent_n", C.c_uint32), ("sent_head", C.c_uint32),
         ("recv_n", C.c_uint32), ("recv_head", C.c_uint32),
         ("sent_peer", C.c_uint32 * IDMAP_CAP), ("sent_id", C.c_uint32 * IDMAP_CAP),
         ("recv_peer", C.c_uint32 * IDMAP_CAP), ("recv_id", C.c_uint32 * IDMAP_CAP),
-        ("pt_all_n", C.c_uint32), ("pt_common_n", C.c_uint32), ("pt_eager_n", C.c_uint32),
-        ("pt_lazy_n", C.c_uint32), ("pt_out_n", C.c_uint32), ("pt_pad", C.c_uint32),
+        ("pt_all_n", C.c_uint32), ("pt_common_n", C.c_uint32),
+        ("pt_out_n", C.c_uint32), ("pt_pad", C.c_uint32),
         ("pt_all", C.c_uint32 * PT_MEMBERS_CAP), ("pt_common", C.c_uint32 * PT_MEMBERS_CAP),
-        ("pt_eager", C.c_uint32 * PT_SET_CAP), ("pt_lazy", C.c_uint32 * PT_SET_CAP),
+        ("pt_root", C.c_uint32 * PT_ROOTS), ("pt_eager_n", C.c_uint32 * PT_ROOTS),
+        ("pt_lazy_n", C.c_uint32 * PT_ROOTS),
+        ("pt_eager", (C.c_uint32 * PT_SET_CAP) * PT_ROOTS), ("pt_lazy", (C.c_uint32 * PT_SET_CAP) * PT_ROOTS),
         ("pt_out_peer", C.c_uint32 * PT_OUT_CAP), ("pt_out_msg", C.c_uint32 * PT_OUT_CAP),
         ("pt_out_round", C.c_uint32 * PT_OUT_CAP),
-        ("have", C.c_uint32), ("trk_round", C.c_uint32), ("trk_hop", C.c_uint32),
-        ("pad1", C.c_uint32),
+        ("have", C.c_uint64), ("trk_round", C.c_uint32), ("trk_hop", C.c_uint32),
     ]
 
 

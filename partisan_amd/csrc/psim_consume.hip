@@ -59,10 +59,18 @@ struct Wv {
 #endif
     uint64_t* st;        // block stats (LDS)
     uint32_t me, li, mypart, round;   // global id, local row index
-    Hdr h;
+    // the node's header fields (Hdr, psim_device.h)
+    uint64_t rng;                     // the Philox draw counter
+    uint32_t start_round, contact, epoch;
+    uint32_t have, aux, trk_round, trk_hop;
+    uint32_t vd;                      // views changed this round: 1 active, 2 passive
     uint32_t act_n, pas_n, sent_n, sent_head, recv_n, recv_head;
-    uint32_t all_n, com_n, eag_n, laz_n, out_n;
-    uint32_t A, P, SP, SI, RP, RI, ALL, COM, EAG, LAZ;
+    uint32_t all_n, com_n, out_n;
+    uint32_t A, P, SP, SI, RP, RI, COM, EAG, LAZ;
+    uint32_t AR;         // lanes 0-7: all_members; lanes RTB..: the root row -- lane RTB + k
+                         // (k < PSIM_PT_ROOTS) root k (NONE = free), RTB + RT_EN / RT_LN the
+                         // eager / lazy counts (byte k: slot k)
+    const uint32_t* slots;   // the message slots in LDS (ids, then roots)
     uint64_t OUT;
     bool maps, pt, maps_dirty, pt_dirty;
     uint64_t obase;
@@ -77,18 +85,16 @@ struct Wv {
     uint64_t dc_base;
     // emissions are staged in LDS and written once per node (flush_recs), so
     // the body issues no global store: a later vmcnt wait never drains one
-    uint32_t* inb;       // inbox messages 4..15 of the node (3 chunks x 64 words),
-                         // prefetched with the node's second input stage
     uint32_t* srec;      // STAGE records x 16 words
     uint32_t* skey;      // their route keys
     uint32_t flushed;    // records already written for this node
-    uint32_t fl, A0, P0; // flag byte and views at node start (writeback)
+    uint32_t fl;         // flag byte at node start (writeback)
     uint32_t KM;         // magic_lanes(): the exact-modulo multipliers
     bool work;           // the node had work this round
 };
 constexpr uint64_t NONE64 = ~0ull;
 constexpr uint32_t STAGE = 16;
-constexpr uint32_t INB_CHUNKS = 3;   // inbox chunks after the first held in LDS (messages 4..15)
+constexpr uint32_t RTB = PSIM_PT_MEMBERS_CAP;   // first lane of the root row in Wv::AR
 
 // stats: lane k of SC holds slot k's count for this wave; flushed once per wave
 DEV void st_add(Wv& w, int k, uint32_t v) { w.SC += lane_id() == (uint32_t)k ? v : 0u; }
@@ -134,6 +140,10 @@ DEV uint32_t usort_lanes(Wv& w, uint32_t& E, uint32_t m) {
     return usort_mask(w, E, m >= 64 ? ~0ull : ((1ull << m) - 1ull));
 }
 
+DEV uint32_t hw_start(const Wv& w) { return w.start_round; }
+DEV uint32_t hw_contact(const Wv& w) { return w.contact; }
+DEV uint32_t hw_epoch(const Wv& w) { return w.epoch; }
+
 // ----------------------------------------------------------------- RNG --
 // The node's draws are consecutive Philox counters, so a cache line of 64
 // of them costs one VALU Philox (every lane a counter) instead of 64 scalar
@@ -144,7 +154,7 @@ DEV void dc_fill(Wv& w, uint64_t base) {
     w.dc_base = base;
 }
 DEV uint64_t draw(Wv& w) {
-    uint64_t c = w.h.rng++;
+    uint64_t c = w.rng++;
     // (a single SALU Philox for a node's first draw measured 3 % slower)
     if (c < w.dc_base || c - w.dc_base >= 64) dc_fill(w, c);
     uint32_t i = (uint32_t)(c - w.dc_base);
@@ -182,7 +192,7 @@ DEV uint32_t select_random(Wv& w, uint32_t V, uint32_t n, uint32_t o0, uint32_t 
 // list -- and the first K positions are appended to OUT at lanes on..
 DEV uint32_t sublist(Wv& w, uint32_t V, uint32_t n, uint32_t k, uint32_t& OUT, uint32_t on) {
     uint32_t l = lane_id();
-    uint64_t base = w.h.rng;
+    uint64_t base = w.rng;
     if (base < w.dc_base || base + n - w.dc_base > 64) dc_fill(w, base);   // must cover [base, base + n)
     uint32_t off = (uint32_t)(base - w.dc_base);
     uint32_t src = (l + off) & 63;
@@ -211,7 +221,7 @@ DEV uint32_t sublist(Wv& w, uint32_t V, uint32_t n, uint32_t k, uint32_t& OUT, u
     uint32_t got = (l >= on && l < on + m) ? w.lds[(l - on) & 63] : 0u;
     __builtin_amdgcn_wave_barrier();
     OUT = (l >= on && l < on + m) ? got : OUT;
-    w.h.rng = base + n;
+    w.rng = base + n;
     return on + m;
 }
 
@@ -298,7 +308,7 @@ DEV bool connect_ok(const Wv& w, uint32_t dst) {
 DEV void hv_send(Wv& w, uint32_t dst, uint32_t type, uint32_t ttl, uint32_t a0, uint32_t a1,
                  uint32_t EX, uint32_t nex) {
     if (!connect_ok(w, dst)) { st_add(w, ST_FAIL, 1); return; }
-    w.h.rng++;
+    w.rng++;
     emit(w, dst, type, ttl, a0, a1, 0, EX, nex);
 }
 
@@ -330,9 +340,9 @@ DEV uint32_t next_id(Wv& w, uint32_t p) {                // hv:1633-1639
     int i = idx_of(w.SP, w.sent_n, p);
     if (i >= 0) {
         uint32_t s = rl(w.SI, i);
-        if (ID_E(s) == w.h.epoch) return s + 1;
+        if (ID_E(s) == hw_epoch(w)) return s + 1;
     }
-    return ID_OF(w.h.epoch, 1);
+    return ID_OF(hw_epoch(w), 1);
 }
 DEV bool addable_epoch(Wv& w, uint32_t pe, uint32_t p) { // hv:1670-1676
     load_maps(w);
@@ -367,12 +377,14 @@ DEV void add_to_passive(Wv& w, uint32_t p) {             // hv:1423-1448
         vdel(w.P, w.pas_n, k);
     }
     view_add(w.P, w.pas_n, p);
+    w.vd |= 2u;
 }
 
 DEV void drop_random_active(Wv& w) {                     // hv:1467-1512
     uint32_t p = select_random(w, w.A, w.act_n, w.me, w.me, w.me);
     if (p == NONE) return;
     vdel_val(w.A, w.act_n, p);
+    w.vd |= 1u;
     add_to_passive(w, p);
     uint32_t nid = next_id(w, p);
     map_store(w, w.SP, w.SI, w.sent_n, w.sent_head, p, nid);
@@ -381,9 +393,10 @@ DEV void drop_random_active(Wv& w) {                     // hv:1467-1512
 
 DEV void add_to_active(Wv& w, uint32_t p) {              // hv:1371-1420
     if (p == w.me || has(w.A, w.act_n, p)) return;
-    vdel_val(w.P, w.pas_n, p);
+    if (vdel_val(w.P, w.pas_n, p)) w.vd |= 2u;
     if (w.act_n >= w.a->max_active) drop_random_active(w);
     view_add(w.A, w.act_n, p);
+    w.vd |= 1u;
 }
 
 // usort([Myself] ++ sublist(Active, k_active) ++ sublist(Passive, k_passive))
@@ -410,7 +423,7 @@ DEV void merge_exchange(Wv& w, uint32_t EX, uint32_t nex) {
     const uint32_t mt = usort_mask(w, T, ballot(l < nex && EX != w.me && !in_act));
     if (!mt) return;
     const uint32_t maxp = w.a->max_passive;
-    const uint64_t c0 = w.h.rng;
+    const uint64_t c0 = w.rng;
     if (c0 < w.dc_base || c0 + mt - w.dc_base > 64) dc_fill(w, c0);   // cover [c0, c0 + mt)
     const uint32_t off = (uint32_t)(c0 - w.dc_base);
     const uint32_t src = (off + l) & 63;
@@ -437,8 +450,9 @@ DEV void merge_exchange(Wv& w, uint32_t EX, uint32_t nex) {
         uint32_t n2 = w.pas_n;
         vins(PB, n2, pos, b);
         vins(w.P, w.pas_n, pos, t);
+        w.vd |= 2u;
     }
-    w.h.rng = c0 + used;
+    w.rng = c0 + used;
 }
 
 DEV void move_to_active(Wv& w, uint32_t p) {             // hv:1679-1709
@@ -458,6 +472,43 @@ DEV void ord_add(Wv& w, uint32_t& V, uint32_t& n, uint32_t cap, uint32_t e) {
     vins(V, n, popc(ballot(l < n && V < e)), e);
 }
 
+// per-root slot k of the 64-entry eager / lazy registers: entries in lanes
+// 16k .. 16k + 15, the count in byte k of RT lane RT_EN / RT_LN
+DEV uint32_t rt_count(const Wv& w, uint32_t which, uint32_t k) { return (rl(w.AR, RTB + which) >> (8 * k)) & 0xFFu; }
+DEV void rt_set_count(Wv& w, uint32_t which, uint32_t k, uint32_t n) {
+    const uint32_t l = lane_id();
+    w.AR = l == RTB + which ? ((w.AR & ~(0xFFu << (8 * k))) | (n << (8 * k))) : w.AR;
+}
+DEV uint32_t rt_root(const Wv& w, uint32_t k) { return rl(w.AR, RTB + k); }
+// the slot of `root`, -1 without per-root sets
+DEV int rt_find(const Wv& w, uint32_t root) {
+    const uint32_t l = lane_id();
+    const int at = ffs64(ballot(l >= RTB && l < RTB + PSIM_PT_ROOTS && w.AR == root));
+    return at < 0 ? -1 : at - (int)RTB;
+}
+
+// ordsets add_element / del_element within slot k (n = its count)
+DEV void slot_add(Wv& w, uint32_t& V, uint32_t k, uint32_t& n, uint32_t e) {
+    const uint32_t l = lane_id(), b = k * PSIM_PT_SET_CAP;
+    const bool in = l >= b && l < b + PSIM_PT_SET_CAP;
+    const uint32_t j = l - b;
+    if (ballot(in && j < n && V == e)) return;
+    if (n >= PSIM_PT_SET_CAP) { st_add(w, ST_OVF, 1); return; }
+    const uint32_t pos = popc(ballot(in && j < n && V < e));
+    const uint32_t pv = from_prev(V);
+    V = (!in || j < pos) ? V : (j == pos ? e : (j <= n ? pv : 0u));
+    n++;
+}
+DEV void slot_del(uint32_t& V, uint32_t k, uint32_t& n, uint32_t e) {
+    const uint32_t l = lane_id(), b = k * PSIM_PT_SET_CAP;
+    const bool in = l >= b && l < b + PSIM_PT_SET_CAP;
+    const int at = ffs64(ballot(in && l - b < n && V == e));
+    if (at < 0) return;
+    const uint32_t nx = from_next(V);
+    V = (!in || l < (uint32_t)at) ? V : (l - b + 1 < n ? nx : 0u);
+    n--;
+}
+
 // notify/1 (hv:1598-1599) -> plumtree update/1 -> handle_cast({update, ..})
 // (pt:314-336), reset_peers/4 (:652-659), neighbors_down/2 (:404-423)
 DEV void apply_notify(Wv& w, uint32_t SNAP, uint32_t sn) {
@@ -467,12 +518,12 @@ DEV void apply_notify(Wv& w, uint32_t SNAP, uint32_t sn) {
     uint32_t CUR = SNAP;
     uint32_t nc = usort_lanes(w, CUR, sn);
     bool in_all = false;
-    for (uint32_t j = 0; j < w.all_n; j++) in_all |= (CUR == rl(w.ALL, j));
+    for (uint32_t j = 0; j < w.all_n; j++) in_all |= (CUR == rl(w.AR, j));
     uint64_t newm = ballot(l < nc && !in_all);
     bool in_cur = false;
-    for (uint32_t j = 0; j < nc; j++) in_cur |= (w.ALL == rl(CUR, j));
+    for (uint32_t j = 0; j < nc; j++) in_cur |= (w.AR == rl(CUR, j));
     uint64_t remm = ballot(l < w.all_n && !in_cur);
-    uint32_t REM = compact(w, w.ALL, remm);
+    uint32_t REM = compact(w, w.AR, remm);
     uint32_t nr = popc(remm);
     if (newm) {
         for (uint64_t m = newm; m; m &= m - 1) {
@@ -485,16 +536,21 @@ DEV void apply_notify(Wv& w, uint32_t SNAP, uint32_t sn) {
             }
             ord_add(w, w.COM, w.com_n, PSIM_PT_MEMBERS_CAP, e);
         }
-        w.h.pt_root = NONE;
-        w.EAG = 0; w.LAZ = 0; w.eag_n = w.laz_n = 0;
-        w.ALL = CUR; w.all_n = nc;
+        // eager_sets = lazy_sets = orddict:new() (pt:656-657)
+        w.AR = l < RTB ? CUR : (l < RTB + PSIM_PT_ROOTS ? NONE : 0u);
+        w.EAG = 0; w.LAZ = 0;
+        w.all_n = nc;
     }
     for (uint32_t r = 0; r < nr; r++) {
         uint32_t e = rl(REM, r);
         vdel_val(w.COM, w.com_n, e);
-        if (w.h.pt_root != NONE) {
-            vdel_val(w.EAG, w.eag_n, e);
-            vdel_val(w.LAZ, w.laz_n, e);
+        for (uint32_t k = 0; k < PSIM_PT_ROOTS; k++) {   // every root's sets (pt:410-413)
+            if (rt_root(w, k) == NONE) continue;
+            uint32_t ne = rt_count(w, RT_EN, k), nl = rt_count(w, RT_LN, k);
+            slot_del(w.EAG, k, ne, e);
+            slot_del(w.LAZ, k, nl, e);
+            rt_set_count(w, RT_EN, k, ne);
+            rt_set_count(w, RT_LN, k, nl);
         }
         uint64_t keep = ballot(l < w.out_n && (uint32_t)(w.OUT >> 32) != e);
         if (popc(keep) != w.out_n) {
@@ -537,33 +593,47 @@ DEV void notify(Wv& w) {
     w.nlog_n++;
 }
 
-// update_peers/5 + set_peers/4 (pt:593-609) for the single root slot
+// update_peers/5 + set_peers/4 (pt:593-609): the root's slot; a new root
+// takes the lowest free slot, its sets starting as (common_eagers, []); with
+// every slot taken the store is an overflow
 DEV void pt_update(Wv& w, uint32_t from, uint32_t root, bool to_eager) {
     w.pt_dirty = true;
-    if (w.h.pt_root != NONE && w.h.pt_root != root) { st_add(w, ST_OVF, 1); return; }
-    if (w.h.pt_root == NONE) {            // first touch: (common_eagers, [])
-        w.EAG = lane_id() < PSIM_PT_MEMBERS_CAP ? w.COM : 0u;
-        w.eag_n = w.com_n;
-        w.LAZ = 0; w.laz_n = 0;
-        w.h.pt_root = root;
+    int k = rt_find(w, root);
+    if (k < 0) {
+        k = rt_find(w, NONE);
+        if (k < 0) { st_add(w, ST_OVF, 1); return; }
+        const uint32_t l = lane_id(), b = (uint32_t)k * PSIM_PT_SET_CAP;
+        const uint32_t c = shfl(w.COM, (int)((l - b) & 63));   // first touch: (common_eagers, [])
+        const bool in = l >= b && l < b + PSIM_PT_SET_CAP;
+        w.EAG = in ? (l - b < w.com_n ? c : 0u) : w.EAG;
+        w.LAZ = in ? 0u : w.LAZ;
+        w.AR = l == RTB + (uint32_t)k ? root : w.AR;
+        rt_set_count(w, RT_EN, k, w.com_n);
+        rt_set_count(w, RT_LN, k, 0);
     }
+    uint32_t ne = rt_count(w, RT_EN, k), nl = rt_count(w, RT_LN, k);
     if (to_eager) {
-        ord_add(w, w.EAG, w.eag_n, PSIM_PT_SET_CAP, from);
-        vdel_val(w.LAZ, w.laz_n, from);
+        slot_add(w, w.EAG, k, ne, from);
+        slot_del(w.LAZ, k, nl, from);
     } else {
-        vdel_val(w.EAG, w.eag_n, from);
-        ord_add(w, w.LAZ, w.laz_n, PSIM_PT_SET_CAP, from);
+        slot_del(w.EAG, k, ne, from);
+        slot_add(w, w.LAZ, k, nl, from);
     }
+    rt_set_count(w, RT_EN, k, ne);
+    rt_set_count(w, RT_LN, k, nl);
 }
 
 // send/3 (pt:633-638): only over an existing connection of the manager
-DEV void pt_send(Wv& w, uint32_t ident, uint32_t type, uint32_t msg, uint32_t rnd, uint32_t root) {
+DEV bool pt_conn(const Wv& w, uint32_t ident) {
     uint32_t id = ident & ~PSIM_MAP_BIT;
-    if (id == w.me || !has(w.A, w.act_n, id) || !connect_ok(w, id)) {
+    return id != w.me && has(w.A, w.act_n, id) && connect_ok(w, id);
+}
+DEV void pt_send(Wv& w, uint32_t ident, uint32_t type, uint32_t msg, uint32_t rnd, uint32_t root) {
+    if (!pt_conn(w, ident)) {
         st_add(w, ST_FAIL, 1);
         return;
     }
-    emit(w, id, type, 0, msg, rnd, root, 0, 0);
+    emit(w, ident & ~PSIM_MAP_BIT, type, 0, msg, rnd, root, 0, 0);
 }
 
 DEV void pt_add_out(Wv& w, uint32_t peer, uint32_t msg, uint32_t rnd) {   // pt:574-579
@@ -581,15 +651,19 @@ DEV void pt_ack_out(Wv& w, uint32_t peer, uint32_t msg, uint32_t rnd) {   // pt:
     if (k >= 0) { vdel64(w.OUT, w.out_n, (uint32_t)k); w.pt_dirty = true; }
 }
 
-// eager_push/7 + schedule_lazy_push/6 (pt:428-441)
+// eager_push/7 + schedule_lazy_push/6 (pt:428-441) over all_peers/3: the
+// root's slot, or the common eagers (and no lazys)
 DEV void pt_push(Wv& w, uint32_t msg, uint32_t rnd, uint32_t root, uint32_t from) {
-    if (w.h.pt_root != NONE && w.h.pt_root == root) {
-        for (uint32_t i = 0; i < w.eag_n; i++) {
-            uint32_t e = rl(w.EAG, i);
+    const int k = rt_find(w, root);
+    if (k >= 0) {
+        const uint32_t b = (uint32_t)k * PSIM_PT_SET_CAP;
+        const uint32_t ne = rt_count(w, RT_EN, k), nl = rt_count(w, RT_LN, k);
+        for (uint32_t i = 0; i < ne; i++) {
+            uint32_t e = rl(w.EAG, b + i);
             if (e != from) pt_send(w, e, PSIM_MSG_PT_BROADCAST, msg, rnd, root);
         }
-        for (uint32_t i = 0; i < w.laz_n; i++) {
-            uint32_t e = rl(w.LAZ, i);
+        for (uint32_t i = 0; i < nl; i++) {
+            uint32_t e = rl(w.LAZ, b + i);
             if (e != from) pt_add_out(w, e, msg, rnd);
         }
     } else {
@@ -600,7 +674,25 @@ DEV void pt_push(Wv& w, uint32_t msg, uint32_t rnd, uint32_t root, uint32_t from
     }
 }
 
-DEV bool pt_have(const Wv& w, uint32_t msg) { return (w.h.have >> (msg & 31u)) & 1u; }
+// plumtree_backend is_stale/1 (:101-104, :148-152) over the message slots; a
+// retired id (its slot taken by a newer broadcast) counts an overflow and
+// answers stale
+DEV bool pt_have(Wv& w, uint32_t msg) {
+    const uint32_t k = msg % PSIM_MSG_SLOTS;
+    if (w.slots[k] != msg) { st_add(w, ST_OVF, 1); return true; }
+    return ((k < 32 ? w.have >> k : w.aux >> (k - 32)) & 1u) != 0;
+}
+DEV void pt_mark(Wv& w, uint32_t msg) {
+    const uint32_t k = msg % PSIM_MSG_SLOTS;
+    if (k < 32) w.have |= 1u << k; else w.aux |= 1u << (k - 32);
+}
+// the root of a live message id (an IHAVE of an outstanding entry); a
+// retired id counts an overflow and is PSIM_NONE
+DEV uint32_t msg_root(Wv& w, uint32_t msg) {
+    const uint32_t k = msg % PSIM_MSG_SLOTS;
+    if (w.slots[k] != msg) { st_add(w, ST_OVF, 1); return NONE; }
+    return w.slots[PSIM_MSG_SLOTS + k];
+}
 
 DEV void pt_handle(Wv& w, uint32_t type, uint32_t src, uint32_t msg, uint32_t rnd, uint32_t root) {
     uint32_t from = src | PSIM_MAP_BIT;
@@ -608,9 +700,9 @@ DEV void pt_handle(Wv& w, uint32_t type, uint32_t src, uint32_t msg, uint32_t rn
     switch (type) {
     case PSIM_MSG_PT_BROADCAST:                        // pt:288-293, :368-378
         if (!pt_have(w, msg)) {                        // plumtree_backend merge/2
-            w.h.have |= 1u << (msg & 31u);
+            pt_mark(w, msg);
             st_add(w, ST_FIRST, 1);
-            if (msg == w.a->tracked_msg) { w.h.trk_round = w.round; w.h.trk_hop = rnd + 1; }
+            if (msg == w.a->tracked_msg) { w.trk_round = w.round; w.trk_hop = rnd + 1; }
             pt_update(w, from, root, true);
             pt_push(w, msg, rnd + 1, root, from);
         } else {
@@ -699,6 +791,7 @@ DEV void hv_handle(Wv& w, uint32_t type, uint32_t p, uint32_t ttl, uint32_t a0, 
     case PSIM_MSG_DISCONNECT: {                        // hv:926-972
         if (!valid_disconnect(w, p, a0)) break;
         vdel_val(w.A, w.act_n, p);
+        w.vd |= 1u;
         uint32_t P0 = w.P, np0 = w.pas_n;              // Passive before the add
         add_to_passive(w, p);
         map_store(w, w.RP, w.RI, w.recv_n, w.recv_head, p, a0);
@@ -764,11 +857,9 @@ DEV uint32_t load_chunk(const RoundArgs& a, uint32_t ib, uint32_t ik, uint32_t c
 }
 
 // chunk c (a multiple of 4) of the node's inbox: the first from the first
-// input stage, the next three from LDS (second stage), any later one loaded
+// input stage, any later one loaded
 DEV uint32_t inbox_chunk(const Wv& w, const RoundArgs& a, uint32_t ib, uint32_t ik, uint32_t c, uint32_t R0) {
-    if (c == 0) return R0;
-    if (c < 4 * (INB_CHUNKS + 1)) return w.inb[((c >> 2) - 1) * 64 + lane_id()];
-    return load_chunk(a, ib, ik, c);
+    return c == 0 ? R0 : load_chunk(a, ib, ik, c);
 }
 
 // A node's inputs arrive in two stages, each issued one step ahead with every
@@ -785,10 +876,9 @@ struct NodeIn {
     uint32_t fl, part;
 };
 struct NodeX {
-    uint32_t R[INB_CHUNKS];        // inbox chunks 1..3 (lane l: word l & 15 of message 4c + (l >> 4))
     uint32_t CV, CF;               // view ids (passive 0-31, active 32-39), their flags | part << 8
     uint32_t MS, MR;               // sent / recv maps: peers in lanes 0-31, ids in 32-63
-    uint32_t PA, PE, PO;           // pt_all | pt_com, pt_eag | pt_laz, pt_out (lo, hi words)
+    uint32_t PA, PG, PL, PO;       // pt_all | pt_com | pt_rt, pt_eag, pt_laz, pt_out (lo, hi words)
 };
 
 DEV uint32_t load_desc(const RoundArgs& a, uint32_t k) {
@@ -815,16 +905,7 @@ DEV NodeX load_x(const RoundArgs& a, const NodeIn& x) {
     uint32_t l = lane_id();
     NodeX y;
     const size_t li = x.n - a.lo;
-    {
-        // the rest of the inbox up to message 15, a record index clamped into
-        // the node's run (or the spare record after an empty one)
-        const uint32_t last = x.ik ? x.ik - 1 : 0u;
-#pragma unroll
-        for (uint32_t c = 0; c < INB_CHUNKS; c++) {
-            const uint32_t m = min(4 * (c + 1) + (l >> 4), last);
-            y.R[c] = reinterpret_cast<const uint32_t*>(a.rec_in + x.ib + m)[l & 15];
-        }
-    }
+
     const uint32_t hw9 = rl(x.H, 9);                 // act_n, pas_n, .. (Hdr word 9)
     const uint32_t act_n = hw9 & 0xFF, pas_n = (hw9 >> 8) & 0xFF;
     uint32_t av = shfl(x.A, (int)(l & 7));
@@ -836,8 +917,11 @@ DEV NodeX load_x(const RoundArgs& a, const NodeIn& x) {
     const uint32_t l31 = l & 31;
     y.MS = (l < 32 ? a.sentp : a.senti)[li * PSIM_IDMAP_CAP + l31];
     y.MR = (l < 32 ? a.recvp : a.recvi)[li * PSIM_IDMAP_CAP + l31];
-    y.PA = ((l & 15) < 8 ? a.pt_all : a.pt_com)[li * PSIM_PT_MEMBERS_CAP + (l & 7)];
-    y.PE = (l31 < 16 ? a.pt_eag : a.pt_laz)[li * PSIM_PT_SET_CAP + (l & 15)];
+    // lanes 0-7 pt_all, 8-15 pt_com, 16-23 the root row (and again above 24)
+    y.PA = ((l & 31) < 8 ? a.pt_all + li * PSIM_PT_MEMBERS_CAP
+                         : (l & 31) < 16 ? a.pt_com + li * PSIM_PT_MEMBERS_CAP : a.pt_rt + li * RT_WORDS)[l & 7];
+    y.PG = a.pt_eag[li * RT_SET + l];
+    y.PL = a.pt_laz[li * RT_SET + l];
     y.PO = reinterpret_cast<const uint32_t*>(a.pt_out + li * PSIM_PT_OUT_CAP)[l];
     return y;
 }
@@ -847,32 +931,31 @@ DEV void begin_node(Wv& w, const NodeIn& x, const NodeX& y) {
     const uint32_t l = lane_id();
     w.li = x.n - w.a->lo;
     w.me = x.n;
-    {
-        uint32_t* hw = reinterpret_cast<uint32_t*>(&w.h);
-#pragma unroll
-        for (int k = 0; k < 16; k++) hw[k] = rl(x.H, k);
-    }
+    w.start_round = rl(x.H, 2); w.contact = rl(x.H, 3); w.epoch = rl(x.H, 4);
+    w.vd = 0;
+    w.rng = ((uint64_t)rl(x.H, 1) << 32) | rl(x.H, 0);
+    w.aux = rl(x.H, 5); w.have = rl(x.H, 6); w.trk_round = rl(x.H, 7); w.trk_hop = rl(x.H, 8);
     w.A = l < PSIM_ACTIVE_CAP ? x.A : 0u;
     w.P = l < PSIM_PASSIVE_CAP ? x.P : 0u;
-    w.A0 = w.A; w.P0 = w.P;
     w.fl = x.fl;
     w.obase = x.ob;
     w.mypart = x.part;
     w.CV = y.CV; w.CF = y.CF;
-#pragma unroll
-    for (uint32_t c = 0; c < INB_CHUNKS; c++) w.inb[c * 64 + l] = y.R[c];
+
     uint32_t msi = shfl(y.MS, (int)((l + 32) & 63)), mri = shfl(y.MR, (int)((l + 32) & 63));
     w.SP = l < 32 ? y.MS : 0u; w.SI = l < 32 ? msi : 0u;
     w.RP = l < 32 ? y.MR : 0u; w.RI = l < 32 ? mri : 0u;
-    uint32_t com = shfl(y.PA, (int)((l + 8) & 63)), laz = shfl(y.PE, (int)((l + 16) & 63));
-    w.ALL = l < PSIM_PT_MEMBERS_CAP ? y.PA : 0u; w.COM = l < PSIM_PT_MEMBERS_CAP ? com : 0u;
-    w.EAG = l < PSIM_PT_SET_CAP ? y.PE : 0u; w.LAZ = l < PSIM_PT_SET_CAP ? laz : 0u;
+    uint32_t com = shfl(y.PA, (int)((l + 8) & 63)), rt = shfl(y.PA, (int)((l + 8) & 63));   // (lanes 8-15: 16-23)
+    w.AR = l < RTB ? y.PA : (l < RTB + RT_WORDS ? rt : 0u); w.COM = l < PSIM_PT_MEMBERS_CAP ? com : 0u;
+    w.EAG = y.PG; w.LAZ = y.PL;
     uint32_t olo = shfl(y.PO, (int)((2 * l) & 63)), ohi = shfl(y.PO, (int)((2 * l + 1) & 63));
     w.OUT = l < PSIM_PT_OUT_CAP ? (((uint64_t)ohi << 32) | olo) : 0ull;
-    w.act_n = w.h.act_n; w.pas_n = w.h.pas_n; w.sent_n = w.h.sent_n; w.sent_head = w.h.sent_head;
-    w.recv_n = w.h.recv_n; w.recv_head = w.h.recv_head;
-    w.all_n = w.h.all_n; w.com_n = w.h.com_n; w.eag_n = w.h.eag_n; w.laz_n = w.h.laz_n;
-    w.out_n = w.h.out_n;
+    {
+        const uint32_t w9 = rl(x.H, 9), w10 = rl(x.H, 10), w11 = rl(x.H, 11);
+        w.act_n = w9 & 0xFF; w.pas_n = (w9 >> 8) & 0xFF; w.sent_n = (w9 >> 16) & 0xFF; w.sent_head = w9 >> 24;
+        w.recv_n = w10 & 0xFF; w.recv_head = (w10 >> 8) & 0xFF; w.all_n = (w10 >> 16) & 0xFF; w.com_n = w10 >> 24;
+        w.out_n = (w11 >> 16) & 0xFF;
+    }
     w.maps = true; w.pt = true; w.maps_dirty = false; w.pt_dirty = false;
     w.seq = 0; w.flushed = 0;
     w.nlog_n = 0;
@@ -889,16 +972,16 @@ DEV void body(Wv& w, const NodeIn& x) {
     uint32_t ik = x.ik;
     const uint32_t ib = x.ib;
     const uint32_t R0 = x.R0;
-    if (w.h.start_round == r && ik) {           // fresh incarnation: no connections yet
+    if (hw_start(w) == r && ik) {           // fresh incarnation: no connections yet
         st_add(w, ST_DROPPED, ik);
         ik = 0;
     }
     bool promo = (x.tf & DESC_PROMO) != 0;
     bool shuf = (x.tf & DESC_SHUFFLE) != 0;
-    bool origin = a.origin_now && a.origin_node == n && a.plumtree;
+    bool origin = (x.tf & DESC_ORIGIN) != 0;
     bool lazy_due = (x.tf & DESC_LAZY) != 0;
-    bool lazy = lazy_due && w.h.out_n > 0;
-    bool joining = w.h.start_round == r && w.h.join_contact != NONE;
+    bool lazy = lazy_due && w.out_n > 0;
+    bool joining = hw_start(w) == r && hw_contact(w) != NONE;
     uint64_t exits = 0;
     if (a.crash_round) {                        // F_CRASHED of the active members (cache lanes 32-39)
         bool dead = l >= 32 && l - 32 < w.act_n && w.CV != n && (w.CF & F_CRASHED);
@@ -911,7 +994,7 @@ DEV void body(Wv& w, const NodeIn& x) {
     STAMP(w, 1);
 
     if (joining)                                      // hv:500-515
-        hv_send(w, w.h.join_contact, PSIM_MSG_JOIN, 0, w.h.epoch, 0, 0, 0);
+        hv_send(w, hw_contact(w), PSIM_MSG_JOIN, 0, hw_epoch(w), 0, 0, 0);
 
     if (exits) {                                      // hv:609-654
         uint32_t D = compact(w, w.A, exits);
@@ -919,9 +1002,11 @@ DEV void body(Wv& w, const NodeIn& x) {
         for (uint32_t i = 0; i < nd; i++) {
             uint32_t d = rl(D, i);
             st_add(w, ST_EXITS, 1);
-            vdel_val(w.P, w.pas_n, d);
-            if (vdel_val(w.A, w.act_n, d))
+            if (vdel_val(w.P, w.pas_n, d)) w.vd |= 2u;
+            if (vdel_val(w.A, w.act_n, d)) {
+                w.vd |= 1u;
                 move_to_active(w, select_random(w, w.P, w.pas_n, n, n, n));
+            }
         }
     }
 
@@ -973,18 +1058,18 @@ DEV void body(Wv& w, const NodeIn& x) {
         }
         STAMP(w, 3);
         if (origin) {                                 // pt:282-287, backend:179-200
-            uint32_t my = n | PSIM_MAP_BIT;
-            w.h.have |= 1u << (a.origin_msg & 31u);
-            w.h.trk_round = r;
-            w.h.trk_hop = 0;
-            pt_push(w, a.origin_msg, 0, my, my);
+            const uint32_t my = n | PSIM_MAP_BIT, msg = uni(a.origin[n - a.lo]) - 1;
+            pt_mark(w, msg);
+            if (msg == a.tracked_msg) { w.trk_round = r; w.trk_hop = 0; }
+            pt_push(w, msg, 0, my, my);
         }
         STAMP(w, 21);
         if (lazy_due && w.out_n > 0) {                // pt:341-345, :443-453
             for (uint32_t i = 0; i < w.out_n; i++) {
                 uint64_t o = rl64(w.OUT, i);
-                pt_send(w, (uint32_t)(o >> 32), PSIM_MSG_PT_IHAVE, (uint32_t)(o >> 16) & 0xFFFFu,
-                        (uint32_t)o & 0xFFFFu, a.bcast_root);
+                const uint32_t peer = (uint32_t)(o >> 32), msg = (uint32_t)(o >> 16) & 0xFFFFu;
+                if (!pt_conn(w, peer)) { st_add(w, ST_FAIL, 1); continue; }
+                emit(w, peer & ~PSIM_MAP_BIT, PSIM_MSG_PT_IHAVE, 0, msg, (uint32_t)o & 0xFFFFu, msg_root(w, msg), 0, 0);
             }
         }
     }
@@ -999,25 +1084,31 @@ DEV void writeback(Wv& w) {
     const RoundArgs& a = *w.a;
     const uint32_t l = lane_id();
     const size_t li = w.li;
-    w.h.act_n = (uint8_t)w.act_n; w.h.pas_n = (uint8_t)w.pas_n;
-    w.h.sent_n = (uint8_t)w.sent_n; w.h.sent_head = (uint8_t)w.sent_head;
-    w.h.recv_n = (uint8_t)w.recv_n; w.h.recv_head = (uint8_t)w.recv_head;
-    w.h.all_n = (uint8_t)w.all_n; w.h.com_n = (uint8_t)w.com_n;
-    w.h.eag_n = (uint8_t)w.eag_n; w.h.laz_n = (uint8_t)w.laz_n; w.h.out_n = (uint8_t)w.out_n;
-    const uint32_t* hw = reinterpret_cast<const uint32_t*>(&w.h);
-    uint32_t v = 0;
-#pragma unroll
-    for (int k = 0; k < 16; k++) v = (l & 15) == (uint32_t)k ? hw[k] : v;
+    // header word l & 15: the loaded word, or the round's value of it
+    const uint32_t k = l & 15;
+    const uint32_t h0 = (uint32_t)w.rng;
+    uint32_t v = 0;                                  // pad words: 0 on a HyParView handle
+    v = k == 0 ? h0 : v;
+    v = k == 1 ? (uint32_t)(w.rng >> 32) : v;
+    v = k == 2 ? w.start_round : v;
+    v = k == 3 ? w.contact : v;
+    v = k == 4 ? w.epoch : v;
+    v = k == 5 ? w.aux : v;
+    v = k == 6 ? w.have : v;
+    v = k == 7 ? w.trk_round : v;
+    v = k == 8 ? w.trk_hop : v;
+    v = k == 9 ? (w.act_n | (w.pas_n << 8) | (w.sent_n << 16) | (w.sent_head << 24)) : v;
+    v = k == 10 ? (w.recv_n | (w.recv_head << 8) | (w.all_n << 16) | (w.com_n << 24)) : v;
+    v = k == 11 ? (w.out_n << 16) : v;
     uint32_t* hrow = reinterpret_cast<uint32_t*>(a.hdr + li);
-    const uint32_t h0 = hw[0];
-    hrow[l & 15] = v;
+    hrow[k] = v;
     {
-        bool dirty = ballot(w.A != w.A0) != 0;
+        bool dirty = (w.vd & 1u) != 0;
         uint32_t x = shfl(w.A, (int)(l & 7));
         *(dirty ? a.act + li * PSIM_ACTIVE_CAP + (l & 7) : hrow) = dirty ? x : h0;
     }
     {
-        bool dirty = ballot(w.P != w.P0) != 0;
+        bool dirty = (w.vd & 2u) != 0;
         uint32_t x = shfl(w.P, (int)(l & 31));
         *(dirty ? a.pas + li * PSIM_PASSIVE_CAP + (l & 31) : hrow) = dirty ? x : h0;
     }
@@ -1032,15 +1123,15 @@ DEV void writeback(Wv& w) {
     }
     {
         const bool d = w.pt_dirty;
-        uint32_t all = shfl(w.ALL, (int)(l & 7)), com = shfl(w.COM, (int)(l & 7));
-        uint32_t eag = shfl(w.EAG, (int)(l & 15)), laz = shfl(w.LAZ, (int)(l & 15));
+        uint32_t all = shfl(w.AR, (int)(l & 7)), com = shfl(w.COM, (int)(l & 7)), rt = shfl(w.AR, (int)(RTB + (l & 7)));
         uint64_t o = shfl64(w.OUT, (int)(l >> 1));
-        const bool lo8 = (l & 15) < 8, lo16 = (l & 31) < 16;
-        uint32_t* p1 = (lo8 ? a.pt_all : a.pt_com) + li * PSIM_PT_MEMBERS_CAP + (l & 7);
-        uint32_t* p2 = (lo16 ? a.pt_eag : a.pt_laz) + li * PSIM_PT_SET_CAP + (l & 15);
+        const uint32_t l31 = l & 31;
+        uint32_t* p1 = (l31 < 8 ? a.pt_all + li * PSIM_PT_MEMBERS_CAP
+                                : l31 < 16 ? a.pt_com + li * PSIM_PT_MEMBERS_CAP : a.pt_rt + li * RT_WORDS) + (l & 7);
         uint32_t* p3 = reinterpret_cast<uint32_t*>(a.pt_out + li * PSIM_PT_OUT_CAP) + l;
-        *(d ? p1 : hrow) = d ? (lo8 ? all : com) : h0;
-        *(d ? p2 : hrow) = d ? (lo16 ? eag : laz) : h0;
+        *(d ? p1 : hrow) = d ? (l31 < 8 ? all : l31 < 16 ? com : rt) : h0;
+        *(d ? a.pt_eag + li * RT_SET + l : hrow) = d ? w.EAG : h0;
+        *(d ? a.pt_laz + li * RT_SET + l : hrow) = d ? w.LAZ : h0;
         *(d ? p3 : hrow) = d ? ((l & 1) ? (uint32_t)(o >> 32) : (uint32_t)o) : h0;
     }
     a.ocnt[li] = w.seq;
@@ -1058,7 +1149,8 @@ __global__ void __launch_bounds__(256, PSIM_WAVES_PER_SIMD) k_consume(RoundArgs 
     __shared__ uint32_t nlogs[WAVES_PER_BLOCK][NLOG * (PSIM_ACTIVE_CAP + 1)];
     __shared__ __attribute__((aligned(16))) uint32_t srecs[WAVES_PER_BLOCK][STAGE * 16];
     __shared__ uint32_t skeys[WAVES_PER_BLOCK][STAGE];
-    __shared__ uint32_t inbs[WAVES_PER_BLOCK][INB_CHUNKS * 64];
+    __shared__ uint32_t sslots[2 * PSIM_MSG_SLOTS];
+    for (int i = threadIdx.x; i < 2 * PSIM_MSG_SLOTS; i += blockDim.x) sslots[i] = args.slots[i];
     for (int i = threadIdx.x; i < NST; i += blockDim.x) sst[i] = 0;
     if (threadIdx.x == 0) atomicMin(&args.ktime[0], (unsigned long long)__builtin_amdgcn_s_memrealtime());
     __syncthreads();
@@ -1072,7 +1164,7 @@ __global__ void __launch_bounds__(256, PSIM_WAVES_PER_SIMD) k_consume(RoundArgs 
     w.nlog = nlogs[wid];
     w.srec = srecs[wid];
     w.skey = skeys[wid];
-    w.inb = inbs[wid];
+    w.slots = sslots;
 #ifdef PSIM_STAMPS
     __shared__ uint64_t stamps[WAVES_PER_BLOCK][32];
     if ((threadIdx.x & 63) < 32) stamps[wid][threadIdx.x & 63] = 0;
@@ -1156,8 +1248,10 @@ DEV uint64_t relay_emit(const RoundArgs& a, uint64_t slot, uint32_t dst, uint32_
 }
 
 __global__ void __launch_bounds__(256) k_relay(RoundArgs a) {
-    enum { R_PROC, R_DELIV, R_SHUF, R_IHAVE, R_FAIL, R_DIGEST, R_N };
+    enum { R_PROC, R_DELIV, R_SHUF, R_IHAVE, R_FAIL, R_DIGEST, R_OVF, R_N };
     __shared__ unsigned long long sst[R_N];
+    __shared__ uint32_t sslots[2 * PSIM_MSG_SLOTS];
+    for (int i = threadIdx.x; i < 2 * PSIM_MSG_SLOTS; i += blockDim.x) sslots[i] = a.slots[i];
     __shared__ uint32_t wcnt[5];                      // per wave slow counts, then the block's base
     if (threadIdx.x < R_N) sst[threadIdx.x] = 0;
     if (threadIdx.x == 0) atomicMin(&a.ktime[0], (unsigned long long)__builtin_amdgcn_s_memrealtime());
@@ -1165,7 +1259,7 @@ __global__ void __launch_bounds__(256) k_relay(RoundArgs a) {
     const uint32_t l = lane_id();
     const uint32_t na = *a.n_alist;
     const uint64_t two58 = 1ull << 58;
-    unsigned long long v[R_N] = {0, 0, 0, 0, 0, 0};
+    unsigned long long v[R_N] = {0, 0, 0, 0, 0, 0, 0};
     for (uint32_t base = blockIdx.x * blockDim.x; base < na; base += gridDim.x * blockDim.x) {
         const uint32_t P = base + threadIdx.x;
         uint4 D = make_uint4(0, 0, 0, 0);
@@ -1180,8 +1274,7 @@ __global__ void __launch_bounds__(256) k_relay(RoundArgs a) {
             D = a.desc[P];
             const uint32_t id = D.x, tf = D.z >> 28;
             ik = D.z & DESC_CNT_MASK;
-            fast = ik <= 1 && !(tf & DESC_SHUFFLE) && !a.crash_round &&
-                   !(a.origin_now && a.plumtree && a.origin_node == id);
+            fast = ik <= 1 && !(tf & (DESC_SHUFFLE | DESC_ORIGIN)) && !a.crash_round;
             if (fast) {
                 // the header, the record's first 16 B, the active row and the
                 // partition byte are independent: issued together, waited once
@@ -1289,8 +1382,12 @@ __global__ void __launch_bounds__(256) k_relay(RoundArgs a) {
                         v[R_FAIL]++;
                         continue;
                     }
-                    v[R_DIGEST] += relay_emit(a, D.w + seq, p, id, PSIM_MSG_PT_IHAVE, seq,
-                                              (uint32_t)(o >> 16) & 0xFFFFu, (uint32_t)o & 0xFFFFu, a.bcast_root, X);
+                    // the message's root from its slot (a retired id: overflow, PSIM_NONE)
+                    const uint32_t msg = (uint32_t)(o >> 16) & 0xFFFFu, sk = msg % PSIM_MSG_SLOTS;
+                    const bool live = sslots[sk] == msg;
+                    v[R_OVF] += live ? 0u : 1u;
+                    v[R_DIGEST] += relay_emit(a, D.w + seq, p, id, PSIM_MSG_PT_IHAVE, seq, msg, (uint32_t)o & 0xFFFFu,
+                                              live ? sslots[PSIM_MSG_SLOTS + sk] : PSIM_NONE, X);
                     seq++;
                     v[R_IHAVE]++;
                 }
@@ -1315,7 +1412,7 @@ __global__ void __launch_bounds__(256) k_relay(RoundArgs a) {
     for (uint32_t k = threadIdx.x; k < NST; k += blockDim.x)
         row[k] = k == ST_PROC ? sst[R_PROC] : k == ST_DELIV + PSIM_MSG_SHUFFLE ? sst[R_DELIV]
                : k == ST_EMIT + PSIM_MSG_SHUFFLE ? sst[R_SHUF] : k == ST_EMIT + PSIM_MSG_PT_IHAVE ? sst[R_IHAVE]
-               : k == ST_FAIL ? sst[R_FAIL] : k == ST_DIGEST ? sst[R_DIGEST] : 0ull;
+               : k == ST_FAIL ? sst[R_FAIL] : k == ST_DIGEST ? sst[R_DIGEST] : k == ST_OVF ? sst[R_OVF] : 0ull;
 }
 
 // one wave-slot per resident wave: the grid strides over the active list

@@ -15,13 +15,14 @@ struct __attribute__((aligned(16))) Hdr {
     uint32_t start_round;  // round the node (re)started
     uint32_t join_contact; // contact to JOIN at start_round, PSIM_NONE for seeds
     uint32_t epoch;
-    uint32_t pt_root;      // root of the single per-root eager/lazy slot, PSIM_NONE
-    uint32_t have;         // plumtree_backend ETS: bitmask of delivered msg ids (mod 32)
+    uint32_t aux;          // HyParView: delivery mask bits 32-63; pluggable: round of the last ping
+    uint32_t have;         // HyParView: delivery mask bits 0-31 (plumtree_backend ETS, bit =
+                           // msg id mod PSIM_MSG_SLOTS); pluggable: hello sent
     uint32_t trk_round;    // round of first delivery of the tracked broadcast
     uint32_t trk_hop;      // plumtree Round + 1 at that delivery (0 at the root)
     uint8_t act_n, pas_n, sent_n, sent_head;
     uint8_t recv_n, recv_head, all_n, com_n;
-    uint8_t eag_n, laz_n, out_n, pad0;
+    uint8_t pad2, pad3, out_n, pad0;
     uint32_t pad1[4];      // pluggable: pad1[0] = leave/1 target of this round + 1, 0 = none
 };
 static_assert(sizeof(Hdr) == 64, "Hdr must be one 64-B line");
@@ -42,6 +43,15 @@ static_assert(sizeof(Msg) == 64, "Msg must be 64 B");
 // saturating at 15 (the next round's lazy-tick bound, k_node_prep)
 enum : uint8_t { F_UP = 1, F_CRASHED = 2, F_LAZY = 4, F_LOWACT = 8 };
 constexpr uint32_t F_OUTN_SHIFT = 4;
+
+// per-root Plumtree sets: PSIM_PT_ROOTS slots of PSIM_PT_SET_CAP entries in a
+// 64-entry eager row and a 64-entry lazy row (slot k = entries 16k..16k+15);
+// the root row (RT_WORDS per node): root of slot k in word k (PSIM_NONE =
+// free), then the eager counts and the lazy counts, one byte per slot
+constexpr uint32_t RT_SET = PSIM_PT_ROOTS * PSIM_PT_SET_CAP;
+constexpr uint32_t RT_WORDS = 8;
+constexpr uint32_t RT_EN = PSIM_PT_ROOTS, RT_LN = PSIM_PT_ROOTS + 1;
+static_assert(RT_SET == 64, "the eager / lazy rows are one 64-lane register");
 
 // route key: dst in the low 27 bits, the sender-side emission bound of the
 // message type in the top 5 (used to size the receiver's next outbox).
@@ -77,7 +87,7 @@ constexpr uint32_t BOUND_ORIGIN = 2 * PSIM_PT_SET_CAP;    // eager push + lazy a
 // work descriptor (id, inbox begin, inbox count | due timers << 28, outbox
 // base): the timers k_desc found due this round for the node
 constexpr uint32_t DESC_CNT_MASK = (1u << 28) - 1;
-enum : uint32_t { DESC_PROMO = 1, DESC_SHUFFLE = 2, DESC_LAZY = 4 };
+enum : uint32_t { DESC_PROMO = 1, DESC_SHUFFLE = 2, DESC_LAZY = 4, DESC_ORIGIN = 8 };
 
 // stats slots in the per-block partial arrays
 enum {

@@ -113,7 +113,7 @@ __global__ void k_join(RoundArgs a, uint32_t* start, const uint32_t* ids, const 
     h.epoch = persist_epoch ? old_epoch + 1 : 1;
     h.start_round = a.round;
     h.join_contact = contacts[i];
-    h.pt_root = PSIM_NONE;
+    h.aux = 0;
     h.trk_round = PSIM_NONE;
     h.act_n = 1; h.all_n = 1; h.com_n = 1;
     a.hdr[li] = h;
@@ -130,14 +130,15 @@ __global__ void k_join(RoundArgs a, uint32_t* start, const uint32_t* ids, const 
         a.pt_all[(size_t)li * PSIM_PT_MEMBERS_CAP + k] = k == 0 ? id : 0u;
         a.pt_com[(size_t)li * PSIM_PT_MEMBERS_CAP + k] = k == 0 ? id : 0u;
     }
-    for (int k = 0; k < PSIM_PT_SET_CAP; k++) {
-        a.pt_eag[(size_t)li * PSIM_PT_SET_CAP + k] = 0;
-        a.pt_laz[(size_t)li * PSIM_PT_SET_CAP + k] = 0;
+    for (uint32_t k = 0; k < RT_SET; k++) {
+        a.pt_eag[(size_t)li * RT_SET + k] = 0;
+        a.pt_laz[(size_t)li * RT_SET + k] = 0;
     }
+    for (uint32_t k = 0; k < RT_WORDS; k++) a.pt_rt[(size_t)li * RT_WORDS + k] = k < PSIM_PT_ROOTS ? PSIM_NONE : 0u;
     for (int k = 0; k < PSIM_PT_OUT_CAP; k++) a.pt_out[(size_t)li * PSIM_PT_OUT_CAP + k] = 0;
     if (a.pl) {                    // the pluggable manager's init/1 (pl:346-402) + Strategy:init/1
         Hdr& x = a.hdr[li];
-        x.pt_root = PSIM_NONE;     // last ping: undefined
+        x.aux = PSIM_NONE;         // last ping: undefined
         x.have = 0;                // hello not sent
         x.act_n = a.strategy == PSIM_STRATEGY_FULL ? 0 : 1;
         x.pas_n = 0; x.all_n = 0; x.com_n = 0;
@@ -152,12 +153,28 @@ __global__ void k_join(RoundArgs a, uint32_t* start, const uint32_t* ids, const 
     }
 }
 
-__global__ void k_bcast_reset(Hdr* hdr, uint32_t n, uint32_t bit) {
+// this round's broadcasts retire the previous ids of their message slots:
+// the slots' delivery bits are cleared at every node (mask lo | hi << 32)
+__global__ void k_bcast_reset(Hdr* hdr, uint32_t n, uint32_t lo, uint32_t hi) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    hdr[i].have &= ~bit;
+    hdr[i].have &= ~lo;
+    hdr[i].aux &= ~hi;
     hdr[i].trk_round = PSIM_NONE;
     hdr[i].trk_hop = 0;
+}
+
+// the roots of this round's broadcasts that run (after the round's crash and
+// start events, which precede this on the stream) originate them:
+// origin[root - lo] = msg + 1; clear = true resets the same entries
+__global__ void k_origin(uint32_t* origin, uint32_t lo, uint32_t n_local, const uint32_t* roots,
+                         const uint32_t* msgs, uint32_t k, const uint8_t* flags, bool clear) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= k) return;
+    const uint32_t r = roots[i];
+    if (r < lo || r >= lo + n_local) return;
+    if (clear) origin[r - lo] = 0;
+    else if (flags[r] & F_UP) origin[r - lo] = msgs[i] + 1;
 }
 
 // ------------------------------------------------------------- route --
@@ -578,7 +595,7 @@ __global__ void __launch_bounds__(256) k_node_prep(RoundArgs a, const uint32_t* 
                         (per ? 1 + PSIM_SVIEW_CAP : 0) + (leave ? PSIM_SVIEW_CAP : 0) + 1;
                 w = c > 0 || (pending && !x.have) || per || leave;
             } else {
-                bool origin = a.origin_now && id == a.origin_node;
+                bool origin = a.origin[i] != 0;
                 // per message its class bound (a BROADCAST: 1), per distinct
                 // BROADCAST id an eager push, and the lazy tick's IHAVEs if
                 // entries are outstanding or may be added this round
@@ -651,7 +668,8 @@ __global__ void k_desc(const uint64_t* __restrict__ packed, const uint64_t* __re
     const uint32_t st = start[li], r = a.round;
     const uint32_t tf = (a.random_promotion && due(a.promotion_period, r, st) ? DESC_PROMO : 0u) |
                         (due(a.shuffle_period, r, st) ? DESC_SHUFFLE : 0u) |
-                        (a.plumtree && due(a.lazy_tick_period, r, st) ? DESC_LAZY : 0u);
+                        (a.plumtree && due(a.lazy_tick_period, r, st) ? DESC_LAZY : 0u) |
+                        (a.plumtree && !a.pl && a.origin[li] ? DESC_ORIGIN : 0u);
     desc[(uint32_t)P] = make_uint4(a.lo + li, in_beg[li], (uint32_t)cb[li] | (tf << 28), (uint32_t)(P >> 32));
 }
 
@@ -702,7 +720,7 @@ __device__ __forceinline__ uint32_t hbin(uint32_t v) { return v < PSIM_HIST_BINS
 
 __global__ void k_hist_out(const Hdr* __restrict__ hdr, const uint32_t* __restrict__ act,
                            const uint32_t* __restrict__ pas, const uint8_t* __restrict__ flags, uint32_t lo,
-                           uint32_t n, uint32_t tbit, uint32_t* indeg_a, uint32_t* indeg_p,
+                           uint32_t n, uint64_t tbit, uint32_t* indeg_a, uint32_t* indeg_p,
                            unsigned long long* hist) {
     __shared__ unsigned long long sh[H_N];
     for (uint32_t j = threadIdx.x; j < H_N; j += blockDim.x) sh[j] = 0;
@@ -725,7 +743,7 @@ __global__ void k_hist_out(const Hdr* __restrict__ hdr, const uint32_t* __restri
         atomicAdd(&sh[H_AOUT * PSIM_HIST_BINS + hbin(out)], 1ull);
         atomicAdd(&sh[H_PFILL * PSIM_HIST_BINS + hbin(x.pas_n)], 1ull);
         atomicAdd(&sh[H_NUP], 1ull);
-        if (tbit && (x.have & tbit)) {
+        if (tbit && ((((uint64_t)x.aux << 32) | x.have) & tbit)) {
             atomicAdd(&sh[H_DELIV], 1ull);
             atomicAdd(&sh[H_HOP * PSIM_HIST_BINS + hbin(x.trk_hop)], 1ull);
             if (x.trk_round != PSIM_NONE) atomicMax(&sh[H_LAST], (unsigned long long)x.trk_round);
@@ -889,7 +907,10 @@ struct Shard {
     DBuf<uint8_t> flags, part;
     // local rows
     DBuf<Hdr> hdr;
-    DBuf<uint32_t> act, pas, sentp, senti, recvp, recvi, pt_all, pt_com, pt_eag, pt_laz, start;
+    DBuf<uint32_t> act, pas, sentp, senti, recvp, recvi, pt_all, pt_com, pt_eag, pt_laz, pt_rt, start;
+    DBuf<uint32_t> origin;              // per local node: msg id + 1 it originates this round
+    DBuf<uint32_t> slots;               // the message slots (msg ids, then roots), a copy of the host's
+    DBuf<uint32_t> bc_roots, bc_msgs;   // this round's broadcasts
     DBuf<uint64_t> pt_out;
     // inbox of the next round: sorted (local dst | bound, record index) pairs
     DBuf<uint32_t> ikeys, ivals;
@@ -949,9 +970,9 @@ struct psim_handle {
     std::vector<uint32_t> pend_lv_a, pend_lv_t;     // leave/1 calls: actor, target
     std::vector<uint8_t> pend_part;
     bool pend_part_set = false, pend_part_clear = false;
-    bool pend_bcast = false;
-    uint32_t pend_root = 0, pend_msg = 0;
-    uint32_t bcast_root = PSIM_NONE, tracked_msg = PSIM_NONE;
+    std::vector<uint32_t> pend_b_root, pend_b_msg;    // broadcasts of the next round, in call order
+    uint32_t slot_tab[2 * PSIM_MSG_SLOTS];            // slot k: msg id [k], root [PSIM_MSG_SLOTS + k]
+    uint32_t tracked_msg = PSIM_NONE;
     uint32_t fw = 0;                    // full strategy: words per member row (adds; removes beside)
     bool tomb = false;                  // full: an ORSet remove exists (leave/1): kernels read remove rows
     std::vector<uint8_t> started;       // full strategy: ids ever started (no restarts)
@@ -981,12 +1002,14 @@ RoundArgs make_args(psim_handle* h, Shard* s) {
     a.shuffle_period = c.shuffle_period; a.promotion_period = c.promotion_period;
     a.random_promotion = c.random_promotion; a.plumtree = c.plumtree;
     a.lazy_tick_period = c.lazy_tick_period;
-    a.tracked_msg = h->tracked_msg; a.bcast_root = h->bcast_root;
-    a.origin_node = PSIM_NONE;
+    a.tracked_msg = h->tracked_msg;
+    a.origin = s->origin.p;
+    a.slots = s->slots.p;
     a.flags = s->flags.p; a.part = s->part.p; a.hdr = s->hdr.p;
     a.act = s->act.p; a.pas = s->pas.p; a.sentp = s->sentp.p; a.senti = s->senti.p;
     a.recvp = s->recvp.p; a.recvi = s->recvi.p;
     a.pt_all = s->pt_all.p; a.pt_com = s->pt_com.p; a.pt_eag = s->pt_eag.p; a.pt_laz = s->pt_laz.p;
+    a.pt_rt = s->pt_rt.p;
     a.pt_out = s->pt_out.p;
     a.start = s->start.p;
     a.pl = c.manager == PSIM_MANAGER_PLUGGABLE;
@@ -1069,8 +1092,8 @@ int upload(Shard* s, DBuf<uint32_t>& b, const std::vector<uint32_t>& v) {
 }
 
 struct RoundCtl {
-    bool crashes = false, origin = false;
-    uint32_t origin_node = PSIM_NONE, origin_msg = 0;
+    bool crashes = false;
+    uint64_t bcast_clear = 0;           // message slots this round's broadcasts retire
 };
 
 // events + prepare for one shard; leaves `a` ready for k_consume
@@ -1078,7 +1101,6 @@ int phase_events_prepare(psim_handle* h, Shard* s, const RoundCtl& ctl, RoundArg
     const uint32_t n = s->n;
     a = make_args(h, s);
     a.crash_round = ctl.crashes;
-    if (ctl.origin) { a.origin_now = 1; a.origin_node = ctl.origin_node; a.origin_msg = ctl.origin_msg; }
     {
         KTimer t(h, s, KT_EVENTS);
         if (ctl.crashes) {
@@ -1102,8 +1124,16 @@ int phase_events_prepare(psim_handle* h, Shard* s, const RoundCtl& ctl, RoundArg
         if (h->pend_part_clear) HIP_TRY(hipMemsetAsync(s->part.p, 0, h->N, s->stream));
         if (h->pend_part_set)
             HIP_TRY(hipMemcpyAsync(s->part.p, h->pend_part.data(), h->N, hipMemcpyHostToDevice, s->stream));
-        if (h->pend_bcast)
-            k_bcast_reset<<<grid_for(n), BLK, 0, s->stream>>>(s->hdr.p, n, 1u << (h->pend_msg & 31u));
+        if (!h->pend_b_root.empty()) {
+            const uint32_t k = (uint32_t)h->pend_b_root.size();
+            k_bcast_reset<<<grid_for(n), BLK, 0, s->stream>>>(s->hdr.p, n, (uint32_t)ctl.bcast_clear,
+                                                               (uint32_t)(ctl.bcast_clear >> 32));
+            TRY(upload(s, s->bc_roots, h->pend_b_root));
+            TRY(upload(s, s->bc_msgs, h->pend_b_msg));
+            HIP_TRY(hipMemcpyAsync(s->slots.p, h->slot_tab, sizeof h->slot_tab, hipMemcpyHostToDevice, s->stream));
+            k_origin<<<grid_for(k), BLK, 0, s->stream>>>(s->origin.p, s->lo, n, s->bc_roots.p, s->bc_msgs.p, k,
+                                                          s->flags.p, false);
+        }
     }
     {
         KTimer t(h, s, KT_PREPARE);
@@ -1389,16 +1419,17 @@ int phase_stats(psim_handle* h, Shard* s, const std::vector<uint32_t>& crashed) 
 int run_round(psim_handle* h, uint64_t* st) {
     RoundCtl ctl;
     ctl.crashes = !h->pend_crash.empty();
-    if (h->pend_bcast) {
-        h->tracked_msg = h->pend_msg;
-        // the root must be running after this round's events (flags are
-        // replicated, so any shard answers for any node)
-        Shard* s0 = h->shards[0];
-        uint8_t f = read1(s0, s0->flags.p + h->pend_root);
-        bool up_after = (f & F_UP) != 0;
-        for (uint32_t c : h->pend_crash) if (c == h->pend_root) up_after = false;
-        for (uint32_t j : h->pend_join) if (j == h->pend_root) up_after = true;
-        if (up_after) { ctl.origin = true; ctl.origin_node = h->pend_root; ctl.origin_msg = h->pend_msg; }
+    if (!h->pend_b_root.empty()) {
+        // each broadcast takes its message slot (the previous id of the slot
+        // retires); the roots' origin entries are set on the device after the
+        // round's crash and start events (k_origin); the last is tracked
+        for (size_t i = 0; i < h->pend_b_root.size(); i++) {
+            const uint32_t k = h->pend_b_msg[i] % PSIM_MSG_SLOTS;
+            ctl.bcast_clear |= 1ull << k;
+            h->slot_tab[k] = h->pend_b_msg[i];
+            h->slot_tab[PSIM_MSG_SLOTS + k] = h->pend_b_root[i] | PSIM_MAP_BIT;
+        }
+        h->tracked_msg = h->pend_b_msg.back();
     }
     for (Shard* s : h->shards) s->tn = 0;        // (timers of a round that failed)
     std::vector<RoundArgs> args(h->shards.size());   // (consume fills the payload arena fields)
@@ -1411,7 +1442,13 @@ int run_round(psim_handle* h, uint64_t* st) {
         if (h->world > 1) TRY(exchange_rccl(h));
         else TRY(exchange_local(h));
     }
-    for (Shard* s : h->shards) TRY(phase_stats(h, s, h->pend_crash));
+    for (Shard* s : h->shards) {
+        TRY(phase_stats(h, s, h->pend_crash));
+        if (!h->pend_b_root.empty())        // this round's origins are spent
+            k_origin<<<grid_for(h->pend_b_root.size()), BLK, 0, s->stream>>>(
+                s->origin.p, s->lo, s->n, s->bc_roots.p, s->bc_msgs.p, (uint32_t)h->pend_b_root.size(), s->flags.p,
+                true);
+    }
     memset(st, 0, NST * 8);
     for (Shard* s : h->shards) {
         TRY(stream_wait(s));
@@ -1465,7 +1502,7 @@ int run_round(psim_handle* h, uint64_t* st) {
         h->pend_crash.insert(h->pend_crash.end(), ids.begin(), ids.end());
     }
     h->pend_part_set = h->pend_part_clear = false;
-    h->pend_bcast = false;
+    h->pend_b_root.clear(); h->pend_b_msg.clear();
     h->round++;
     return PSIM_OK;
 }
@@ -1503,7 +1540,8 @@ int shard_alloc(psim_handle* h, Shard* s) {
     rc |= s->sentp.alloc(n * PSIM_IDMAP_CAP); rc |= s->senti.alloc(n * PSIM_IDMAP_CAP);
     rc |= s->recvp.alloc(n * PSIM_IDMAP_CAP); rc |= s->recvi.alloc(n * PSIM_IDMAP_CAP);
     rc |= s->pt_all.alloc(n * PSIM_PT_MEMBERS_CAP); rc |= s->pt_com.alloc(n * PSIM_PT_MEMBERS_CAP);
-    rc |= s->pt_eag.alloc(n * PSIM_PT_SET_CAP); rc |= s->pt_laz.alloc(n * PSIM_PT_SET_CAP);
+    rc |= s->pt_eag.alloc(n * RT_SET); rc |= s->pt_laz.alloc(n * RT_SET); rc |= s->pt_rt.alloc(n * RT_WORDS);
+    rc |= s->origin.alloc(n); rc |= s->slots.alloc(2 * PSIM_MSG_SLOTS);
     rc |= s->pt_out.alloc(n * PSIM_PT_OUT_CAP); rc |= s->start.alloc(n);
     rc |= s->ocnt.alloc(n); rc |= s->cb.alloc(n + 1);
     rc |= s->in_beg.alloc(n + 1); rc |= s->bound.alloc(n + 1); rc |= s->pscan.alloc(n + 1); rc |= s->obase.alloc(n + 1);
@@ -1537,6 +1575,7 @@ void shard_free(Shard* s) {
     s->act.release(); s->pas.release(); s->sentp.release(); s->senti.release();
     s->recvp.release(); s->recvi.release(); s->pt_all.release(); s->pt_com.release();
     s->pt_eag.release(); s->pt_laz.release(); s->pt_out.release(); s->start.release();
+    s->pt_rt.release(); s->origin.release(); s->slots.release(); s->bc_roots.release(); s->bc_msgs.release();
     s->ikeys.release(); s->ivals.release(); s->recvbuf.release(); s->inbox[0].release(); s->inbox[1].release();
     if (s->pin) (void)hipHostFree(s->pin);
     if (s->wait_ev) (void)hipEventDestroy(s->wait_ev);
@@ -1623,6 +1662,7 @@ int psim_create(const psim_config* cfg, psim_handle** out) {
     }
     h->N = cfg->n_nodes;
     h->G = G;
+    for (uint32_t k = 0; k < 2 * PSIM_MSG_SLOTS; k++) h->slot_tab[k] = PSIM_NONE;
     h->per = (h->N + G - 1) / G;
     h->world = (int)world;
     h->rank = (int)cfg->shard_rank;
@@ -1648,6 +1688,8 @@ int psim_create(const psim_config* cfg, psim_handle** out) {
         s->n = std::min<uint32_t>(h->N, s->lo + h->per) - s->lo;
         h->shards.push_back(s);
         int rc = shard_alloc(h, s);
+        if (!rc && hipMemcpy(s->slots.p, h->slot_tab, sizeof h->slot_tab, hipMemcpyHostToDevice) != hipSuccess)
+            rc = PSIM_EDEVICE;
         if (rc) { psim_destroy(h); return rc; }
     }
     if (world > 1) {
@@ -1770,10 +1812,11 @@ int psim_broadcast(psim_handle* h, uint32_t root, uint32_t msg_id) {
     if (!h) return PSIM_EINVAL;
     if (h->cfg.manager == PSIM_MANAGER_PLUGGABLE) return PSIM_EUNSUPPORTED;   // Plumtree runs over HyParView
     if (root >= h->N || msg_id > 0xFFFF) return PSIM_ERANGE;
-    uint32_t r = root | PSIM_MAP_BIT;
-    if (h->bcast_root != PSIM_NONE && h->bcast_root != r) return PSIM_EUNSUPPORTED;
-    h->bcast_root = r;
-    h->pend_bcast = true; h->pend_root = root; h->pend_msg = msg_id;
+    for (size_t i = 0; i < h->pend_b_root.size(); i++)   // one per root and per slot per round
+        if (h->pend_b_root[i] == root || h->pend_b_msg[i] % PSIM_MSG_SLOTS == msg_id % PSIM_MSG_SLOTS)
+            return PSIM_EINVAL;
+    h->pend_b_root.push_back(root);
+    h->pend_b_msg.push_back(msg_id);
     return PSIM_OK;
 }
 
@@ -1803,7 +1846,7 @@ static int get_shard_nodes(Shard* s, uint32_t first, uint32_t count, psim_node_v
     std::vector<uint32_t> act((size_t)count * PSIM_ACTIVE_CAP), pas((size_t)count * PSIM_PASSIVE_CAP);
     std::vector<uint32_t> sp((size_t)count * PSIM_IDMAP_CAP), si(sp.size()), rp(sp.size()), ri(sp.size());
     std::vector<uint32_t> all((size_t)count * PSIM_PT_MEMBERS_CAP), com(all.size());
-    std::vector<uint32_t> eag((size_t)count * PSIM_PT_SET_CAP), laz(eag.size());
+    std::vector<uint32_t> eag((size_t)count * RT_SET), laz(eag.size()), rt((size_t)count * RT_WORDS);
     std::vector<uint64_t> po((size_t)count * PSIM_PT_OUT_CAP);
     const size_t li = first - s->lo;
     auto cp = [&](void* dst, const void* src, size_t bytes) {
@@ -1819,15 +1862,16 @@ static int get_shard_nodes(Shard* s, uint32_t first, uint32_t count, psim_node_v
     HIP_TRY(cp(ri.data(), s->recvi.p + li * PSIM_IDMAP_CAP, ri.size() * 4));
     HIP_TRY(cp(all.data(), s->pt_all.p + li * PSIM_PT_MEMBERS_CAP, all.size() * 4));
     HIP_TRY(cp(com.data(), s->pt_com.p + li * PSIM_PT_MEMBERS_CAP, com.size() * 4));
-    HIP_TRY(cp(eag.data(), s->pt_eag.p + li * PSIM_PT_SET_CAP, eag.size() * 4));
-    HIP_TRY(cp(laz.data(), s->pt_laz.p + li * PSIM_PT_SET_CAP, laz.size() * 4));
+    HIP_TRY(cp(eag.data(), s->pt_eag.p + li * RT_SET, eag.size() * 4));
+    HIP_TRY(cp(laz.data(), s->pt_laz.p + li * RT_SET, laz.size() * 4));
+    HIP_TRY(cp(rt.data(), s->pt_rt.p + li * RT_WORDS, rt.size() * 4));
     HIP_TRY(cp(po.data(), s->pt_out.p + li * PSIM_PT_OUT_CAP, po.size() * 8));
     HIP_TRY(hipStreamSynchronize(s->stream));
     for (uint32_t k = 0; k < count; k++) {
         psim_node_view* v = &out[k];
         const Hdr& x = hd[k];
         memset(v, 0, sizeof *v);
-        v->up = fl[k] & F_UP; v->epoch = x.epoch; v->start_round = x.start_round; v->pt_root = x.pt_root;
+        v->up = fl[k] & F_UP; v->epoch = x.epoch; v->start_round = x.start_round;
         v->rng_ctr = x.rng;
         v->act_n = x.act_n; v->pas_n = x.pas_n;
         memcpy(v->act, &act[(size_t)k * PSIM_ACTIVE_CAP], sizeof v->act);
@@ -1837,19 +1881,24 @@ static int get_shard_nodes(Shard* s, uint32_t first, uint32_t count, psim_node_v
         memcpy(v->sent_id, &si[(size_t)k * PSIM_IDMAP_CAP], sizeof v->sent_id);
         memcpy(v->recv_peer, &rp[(size_t)k * PSIM_IDMAP_CAP], sizeof v->recv_peer);
         memcpy(v->recv_id, &ri[(size_t)k * PSIM_IDMAP_CAP], sizeof v->recv_id);
-        v->pt_all_n = x.all_n; v->pt_common_n = x.com_n; v->pt_eager_n = x.eag_n;
-        v->pt_lazy_n = x.laz_n; v->pt_out_n = x.out_n;
+        v->pt_all_n = x.all_n; v->pt_common_n = x.com_n; v->pt_out_n = x.out_n;
+        const uint32_t* r8 = &rt[(size_t)k * RT_WORDS];
+        for (int q = 0; q < PSIM_PT_ROOTS; q++) {
+            v->pt_root[q] = r8[q];
+            v->pt_eager_n[q] = (r8[RT_EN] >> (8 * q)) & 0xFFu;
+            v->pt_lazy_n[q] = (r8[RT_LN] >> (8 * q)) & 0xFFu;
+        }
         memcpy(v->pt_all, &all[(size_t)k * PSIM_PT_MEMBERS_CAP], sizeof v->pt_all);
         memcpy(v->pt_common, &com[(size_t)k * PSIM_PT_MEMBERS_CAP], sizeof v->pt_common);
-        memcpy(v->pt_eager, &eag[(size_t)k * PSIM_PT_SET_CAP], sizeof v->pt_eager);
-        memcpy(v->pt_lazy, &laz[(size_t)k * PSIM_PT_SET_CAP], sizeof v->pt_lazy);
+        memcpy(v->pt_eager, &eag[(size_t)k * RT_SET], sizeof v->pt_eager);
+        memcpy(v->pt_lazy, &laz[(size_t)k * RT_SET], sizeof v->pt_lazy);
         for (int j = 0; j < PSIM_PT_OUT_CAP; j++) {
             uint64_t o = po[(size_t)k * PSIM_PT_OUT_CAP + j];
             v->pt_out_peer[j] = (uint32_t)(o >> 32);
             v->pt_out_msg[j] = (uint32_t)(o >> 16) & 0xFFFFu;
             v->pt_out_round[j] = (uint32_t)o & 0xFFFFu;
         }
-        v->have = x.have; v->trk_round = x.trk_round; v->trk_hop = x.trk_hop;
+        v->have = ((uint64_t)x.aux << 32) | x.have; v->trk_round = x.trk_round; v->trk_hop = x.trk_hop;
     }
     return PSIM_OK;
 }
@@ -1934,7 +1983,7 @@ int psim_get_strategy_nodes(psim_handle* h, uint32_t first, uint32_t count, psim
             bool started = x.epoch != 0;       // k_join sets epoch >= 1
             v->up = fl[j] & F_UP; v->start_round = x.start_round; v->rng_ctr = x.rng;
             v->pending = started ? x.join_contact : PSIM_NONE;
-            v->last_ping = started ? x.pt_root : PSIM_NONE;
+            v->last_ping = started ? x.aux : PSIM_NONE;
             v->view_n = x.act_n; v->in_n = x.pas_n;
             if (full) {
                 const uint32_t* row = &rows[(size_t)j * 2 * h->fw];
@@ -1979,7 +2028,7 @@ int psim_get_delivery(psim_handle* h, uint32_t first, uint32_t count, uint8_t* h
     if (!h || (count && (!have || !round || !hop))) return PSIM_EINVAL;
     if ((uint64_t)first + count > h->N) return PSIM_ERANGE;
     if (hipSetDevice(h->device) != hipSuccess) return PSIM_EDEVICE;
-    const uint32_t bit = h->tracked_msg == PSIM_NONE ? 0u : 1u << (h->tracked_msg & 31u);
+    const uint64_t bit = h->tracked_msg == PSIM_NONE ? 0ull : 1ull << (h->tracked_msg % PSIM_MSG_SLOTS);
     uint32_t done = 0;
     while (done < count) {
         const uint32_t id = first + done;
@@ -1991,7 +2040,7 @@ int psim_get_delivery(psim_handle* h, uint32_t first, uint32_t count, uint8_t* h
                                s->stream));
         HIP_TRY(hipStreamSynchronize(s->stream));
         for (uint32_t j = 0; j < k; j++) {
-            have[done + j] = (hd[j].have & bit) ? 1 : 0;
+            have[done + j] = ((((uint64_t)hd[j].aux << 32) | hd[j].have) & bit) ? 1 : 0;
             round[done + j] = hd[j].trk_round;
             hop[done + j] = hd[j].trk_hop;
         }
@@ -2013,7 +2062,7 @@ int psim_get_histograms(psim_handle* h, psim_histograms* out) {
     TmpBuf<unsigned long long> hist;
     TRY(ind.alloc_on(2 * N, st));
     TRY(hist.alloc_on(H_N + 4, st));
-    const uint32_t tbit = h->tracked_msg == PSIM_NONE ? 0u : 1u << (h->tracked_msg & 31u);
+    const uint64_t tbit = h->tracked_msg == PSIM_NONE ? 0ull : 1ull << (h->tracked_msg % PSIM_MSG_SLOTS);
     for (Shard* s : h->shards)
         k_hist_out<<<grid_for(s->n), BLK, 0, st>>>(s->hdr.p, s->act.p, s->pas.p, s->flags.p, s->lo, s->n, tbit,
                                                    ind.p, ind.p + N, hist.p);
@@ -2097,7 +2146,8 @@ int psim_get_histograms(psim_handle* h, psim_histograms* out) {
 struct SnapHead {
     uint32_t magic, abi, n_nodes, n_local_shards, manager, strategy, fw, started_n;
     uint64_t round;
-    uint32_t tracked_msg, bcast_root, G, world;
+    uint32_t tracked_msg, pad, G, world;
+    uint32_t slot_tab[2 * PSIM_MSG_SLOTS];
 };
 struct ShardHead {
     uint32_t lo, n, m_in, in_cur, pay_cur, pay_rows, pad[2];
@@ -2115,7 +2165,7 @@ static std::vector<Section> snap_sections(psim_handle* h, Shard* s, const ShardH
         {s->sentp.p, n * PSIM_IDMAP_CAP * 4}, {s->senti.p, n * PSIM_IDMAP_CAP * 4},
         {s->recvp.p, n * PSIM_IDMAP_CAP * 4}, {s->recvi.p, n * PSIM_IDMAP_CAP * 4},
         {s->pt_all.p, n * PSIM_PT_MEMBERS_CAP * 4}, {s->pt_com.p, n * PSIM_PT_MEMBERS_CAP * 4},
-        {s->pt_eag.p, n * PSIM_PT_SET_CAP * 4}, {s->pt_laz.p, n * PSIM_PT_SET_CAP * 4},
+        {s->pt_eag.p, n * RT_SET * 4}, {s->pt_laz.p, n * RT_SET * 4}, {s->pt_rt.p, n * RT_WORDS * 4},
         {s->pt_out.p, n * PSIM_PT_OUT_CAP * 8}, {s->start.p, n * 4},
         {s->cb.p, (n + 1) * 8}, {s->bmask.p, n * 4}, {s->in_beg.p, (n + 1) * 4},
         {s->inbox[sh.in_cur].p, (size_t)sh.m_in * sizeof(Msg)},
@@ -2132,7 +2182,7 @@ static std::vector<Section> snap_sections(psim_handle* h, Shard* s, const ShardH
 int psim_snapshot(psim_handle* h, void* buf, size_t cap, size_t* need) {
     if (!h || !need) return PSIM_EINVAL;
     if (!h->pend_crash.empty() || !h->pend_join.empty() || !h->pend_lv_a.empty() || h->pend_part_set || h->pend_part_clear ||
-        h->pend_bcast)
+        !h->pend_b_root.empty())
         return PSIM_ESTATE;
     if (hipSetDevice(h->device) != hipSuccess) return PSIM_EDEVICE;
     std::vector<ShardHead> heads;
@@ -2151,7 +2201,8 @@ int psim_snapshot(psim_handle* h, void* buf, size_t cap, size_t* need) {
     if (!buf || cap < total) return PSIM_OK;
     char* o = static_cast<char*>(buf);
     SnapHead hd{SNAP_MAGIC, PSIM_ABI_VERSION, h->N, (uint32_t)h->shards.size(), h->cfg.manager, h->cfg.strategy,
-                h->fw, (uint32_t)h->started.size(), h->round, h->tracked_msg, h->bcast_root, h->G, (uint32_t)h->world};
+                h->fw, (uint32_t)h->started.size(), h->round, h->tracked_msg, 0, h->G, (uint32_t)h->world, {}};
+    memcpy(hd.slot_tab, h->slot_tab, sizeof h->slot_tab);
     memcpy(o, &hd, sizeof hd); o += sizeof hd;
     if (!h->started.empty()) { memcpy(o, h->started.data(), h->started.size()); o += h->started.size(); }
     for (size_t k = 0; k < h->shards.size(); k++) {
@@ -2200,7 +2251,10 @@ int psim_restore(psim_handle* h, const void* buf, size_t size) {
         }
         s->reserved = false;
     }
-    h->round = hd.round; h->tracked_msg = hd.tracked_msg; h->bcast_root = hd.bcast_root;
+    h->round = hd.round; h->tracked_msg = hd.tracked_msg;
+    memcpy(h->slot_tab, hd.slot_tab, sizeof h->slot_tab);
+    for (Shard* s : h->shards)
+        HIP_TRY(hipMemcpy(s->slots.p, h->slot_tab, sizeof h->slot_tab, hipMemcpyHostToDevice));
     HIP_TRY(hipDeviceSynchronize());
     return PSIM_OK;
 }

@@ -12,15 +12,20 @@ struct RoundArgs {
     uint32_t max_active, min_active, max_passive, arwl, prwl, k_active, k_passive;
     uint32_t shuffle_period, promotion_period, random_promotion, plumtree, lazy_tick_period;
     // per-round scalars
-    uint32_t crash_round, origin_now, origin_node, origin_msg, tracked_msg, bcast_root;
+    uint32_t crash_round, tracked_msg;
     // node state: flags/part are replicated and indexed by global id;
     // every other row is local (index = id - lo)
     uint8_t* flags;
     const uint8_t* part;
     Hdr* hdr;
     uint32_t *act, *pas, *sentp, *senti, *recvp, *recvi;
-    uint32_t *pt_all, *pt_com, *pt_eag, *pt_laz;
+    uint32_t *pt_all, *pt_com, *pt_eag, *pt_laz, *pt_rt;
     uint64_t* pt_out;
+    // broadcasts: per local node the message id + 1 it originates this
+    // round (0 = none); the message slots (id of slot k in word k, its root
+    // in word PSIM_MSG_SLOTS + k, PSIM_NONE = free)
+    const uint32_t* origin;
+    const uint32_t* slots;
     // inbox (this round) and outbox (next round)
     const uint32_t* in_beg;
     const unsigned long long* in_cb;   // inbox count | emission-bound sum << 32
@@ -42,7 +47,7 @@ struct RoundArgs {
     // (100 MHz), reset by k_node_prep
     unsigned long long* ktime;
     // pluggable manager (k_consume_pl); Hdr fields are reused as
-    // join_contact = pending contact, pt_root = last ping round,
+    // join_contact = pending contact, aux = last ping round,
     // have = hello sent, act_n = view length, pas_n = in_view length
     uint32_t pl, strategy, periodic, scamp_c, fanout;
     uint32_t fw;                 // full: words per member bitset (multiple of 4); a node's row

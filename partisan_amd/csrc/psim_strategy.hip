@@ -30,7 +30,7 @@ constexpr uint32_t NONE = PSIM_NONE;
 constexpr uint64_t NONE64 = ~0ull;
 
 // Hdr fields of a pluggable node (see RoundArgs): join_contact = pending
-// contact, pt_root = round of the last ping, have = hello sent,
+// contact, aux = round of the last ping, have = hello sent,
 // act_n = view length, pas_n = in_view length.
 struct Pw {
     const RoundArgs* a;
@@ -319,7 +319,7 @@ DEV void scamp_join(Pw& w, uint32_t contact) {
 // and not this round (App. A Q12: 100000 us against 1-s rounds)
 DEV void scamp_periodic(Pw& w) {
     const uint32_t M = w.V, n = w.vn;
-    const bool isolated = w.h.pt_root != NONE && w.round > w.h.pt_root;
+    const bool isolated = w.h.aux != NONE && w.round > w.h.aux;
     if (isolated) {
         uint32_t SEL = 0;
         if (sublist(w, M, n, 1, SEL)) pl_send(w, rl(SEL, 0), PSIM_PL_FWD_SUB, w.me, NONE);
@@ -419,7 +419,7 @@ DEV void pl_handle(Pw& w, uint32_t type, uint32_t src, uint32_t a0, uint32_t slo
         if (!full) scamp_fwd(w, a0);
         break;
     case PSIM_PL_PING:             // sv1:177-188, sv2:181-191
-        if (!full) w.h.pt_root = w.round;
+        if (!full) w.h.aux = w.round;
         break;
     case PSIM_PL_KEEP_SUB:         // sv2:328-338: InView = [Node | InView0]
         if (w.a->strategy == PSIM_STRATEGY_SCAMP_V2) scamp_add(w, w.I, w.in_n, a0, false);

@@ -81,6 +81,32 @@ def joiner_crash(make, n=2048, seed=3, rounds=40, **cfg):
 VARIANT = dict(max_active_size=8, max_passive_size=20, arwl=6, prwl=6, persist_epoch=1)
 
 
+def multi_root(make, n=2048, seed=17, rounds=160, roots=4, period=10, first=30, churn=False, **cfg):
+    """Plumtree with several roots (pt:76-84 per-root eager/lazy sets,
+    backend:179-200 heartbeat broadcasts): `roots` distinct nodes, drawn
+    once, each originate a broadcast every `period` rounds from `first`, in
+    the same round; message ids count up, past PSIM_MSG_SLOTS on long runs
+    (old ids retire).  churn=True adds 10% crash + rejoin churn over rounds
+    60-79.  With roots <= PSIM_PT_ROOTS every node keeps every root's sets
+    (overflow 0); more roots exercise the full-slots path."""
+    sim = make(default_config(n_nodes=n, seed=seed, **cfg))
+    rng = np.random.Generator(np.random.PCG64([seed, 31]))
+    rs = [int(x) for x in rng.choice(n, size=roots, replace=False)]
+    ch = {r: (v, c) for r, v, c in W.churn_schedule(n, seed, 0.1, 60, 20, protect=tuple(rs))} if churn else {}
+    state = {"k": 0}
+
+    def hook(r):
+        if r in ch:
+            sim.crash(ch[r][0])
+            sim.join(ch[r][0], ch[r][1])
+        if r >= first and (r - first) % period == 0:
+            for root in rs:
+                sim.broadcast(root, state["k"] % 0x10000)
+                state["k"] += 1
+    st = sim.run_schedule(W.doubling_join(n, seed), rounds, extra=hook)
+    return sim, st, rs
+
+
 def crash_only(make, n=1024, seed=9, rounds=80):
     """Crashes without restarts: EXIT handling and the stopped-member check
     (test/partisan_SUITE.erl:2024-2041)."""

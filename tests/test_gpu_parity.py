@@ -364,6 +364,29 @@ def test_histograms_large_properties(shards):
             assert np.array_equal(np.asarray(h[kk]), np.asarray(_HIST_1[kk])), kk
 
 
+@pytest.mark.parametrize("roots,rounds,churn", [(4, 200, False), (4, 160, True), (6, 120, False)])
+def test_multi_root_parity(roots, rounds, churn):
+    """Several Plumtree roots at once (per-root eager / lazy sets in 4 root
+    slots, pt:76-84, :599-631; message ids past the 64 message slots): the
+    engine equals the oracle, with 4 roots (no overflow), under churn, and
+    with 6 roots (full root slots, counted as overflow identically)."""
+    (gs, gst, _), (os_, ost, _) = _both(S.multi_root, roots=roots, rounds=rounds, churn=churn)
+    S.compare_stats(gst, ost)
+    S.compare_nodes(gs.nodes(), os_.nodes())
+    if roots <= 4 and not churn:
+        assert int(gst["overflow"].sum()) == 0
+
+
+def test_multi_root_shard_invariance():
+    """Four roots over 3 virtual shards: bit-identical to the oracle."""
+    def g3(cfg):
+        cfg.n_shards = 3
+        return _gpu(cfg)
+    (gs, gst, _), (os_, ost, _) = S.multi_root(g3, roots=4, rounds=120), S.multi_root(Oracle, roots=4, rounds=120)
+    S.compare_stats(gst, ost)
+    S.compare_nodes(gs.nodes(), os_.nodes())
+
+
 def test_snapshot_restore_continues_identically():
     """psim_snapshot after 60 rounds, restored into a fresh handle: the next
     40 rounds (a broadcast included) are identical to the original's."""

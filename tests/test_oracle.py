@@ -140,7 +140,10 @@ def test_event_validation():
         sim.join(np.array([99], np.uint32), np.array([0], np.uint32))
     sim.broadcast(0, 1)
     with pytest.raises(Exception):
-        sim.broadcast(1, 2)          # single-root restriction
+        sim.broadcast(0, 2)          # a second broadcast at the same root in one round
+    with pytest.raises(Exception):
+        sim.broadcast(1, 65)         # the message slot of id 1 (65 mod 64) is taken this round
+    sim.broadcast(1, 2)              # another root: any node can broadcast
 
 
 def test_duplicate_join_rejected():
@@ -157,6 +160,28 @@ def test_duplicate_join_rejected():
     sim.join(np.array([3], np.uint32), np.array([0], np.uint32))   # a later round: a restart
     sim.step(3)
     assert sim.nodes(3, 1)["up"][0] == 1
+
+
+def test_multi_root_plumtree():
+    """Four roots broadcasting together every 10 rounds for 200 rounds (68
+    message ids, past the 64 message slots): every node keeps a per-root
+    eager / lazy set for each root (pt:76-84, :599-631) with no overflow,
+    each broadcast reaches (nearly) every node, and the per-root sets are
+    ordsets of at most PSIM_PT_SET_CAP peers."""
+    sim, st, roots = S.multi_root(Oracle, n=2048, roots=4, rounds=200)
+    assert int(st["overflow"].sum()) == 0
+    v = sim.nodes()
+    used = v["pt_root"] != 0xFFFFFFFF
+    assert used.sum(1).max() == 4
+    got = {int(r) for r in np.unique(v["pt_root"][used])}
+    assert got <= {r | 0x80000000 for r in roots}
+    for i in range(0, 2048, 97):
+        for k in range(4):
+            ne = int(v["pt_eager_n"][i][k])
+            e = [int(x) for x in v["pt_eager"][i][k][:ne]]
+            assert e == sorted(set(e)) and ne <= 16
+    # 68 broadcasts, each delivered to nearly all 2048 nodes
+    assert int(st["first_deliveries"].sum()) > 0.98 * 68 * 2047
 
 
 def test_plumtree_off():
