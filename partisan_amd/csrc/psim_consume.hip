@@ -9,10 +9,13 @@
 // and no scratch.  Messages are read and written as one coalesced 64-B record
 // by lanes 0-15.
 //
-// The wave runs the node's EXIT events, HyParView inbox, timers, then its
-// Plumtree inbox, origin broadcast and lazy tick, in the fixed order of the
-// round model R0.  Besides its own rows a wave reads
-// only the flag/partition bytes of peers and the previous round's records.
+// k_consume runs the node's EXIT events, HyParView inbox and timers (and
+// replays its notifies into the Plumtree state); k_pt then runs its Plumtree
+// inbox, origin broadcast and lazy tick -- the fixed order of the round model
+// R0.  k_relay, ahead of both, does the lone SHUFFLE
+// relays and lazy ticks of a steady round in one lane per node and lists the
+// rest for the two wave kernels.  Besides its own rows a wave reads only the
+// flag/partition bytes of peers and the previous round's records.
 //
 // Reference handlers are cited as file:line under /root/reference:
 //   hv = src/partisan_hyparview_peer_service_manager.erl
@@ -98,6 +101,15 @@ constexpr uint32_t RTB = PSIM_PT_MEMBERS_CAP;   // first lane of the root row in
 
 // stats: lane k of SC holds slot k's count for this wave; flushed once per wave
 DEV void st_add(Wv& w, int k, uint32_t v) { w.SC += lane_id() == (uint32_t)k ? v : 0u; }
+// this wave's counters and digest partials into the block's LDS stats
+DEV void flush_wave_stats(const Wv& w, uint64_t* sst) {
+    const uint32_t l = lane_id();
+    if (l < NST && w.SC) atomicAdd((unsigned long long*)&sst[l], (unsigned long long)w.SC);
+    uint64_t dg = w.digest;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) dg += shfl64(dg, (int)((l + off) & 63));
+    if (l == 0 && dg) atomicAdd((unsigned long long*)&sst[ST_DIGEST], (unsigned long long)dg);
+}
 
 // compact the lanes of V selected by `keep` (uniform mask) to the front
 DEV uint32_t compact(Wv& w, uint32_t V, uint64_t keep) {
@@ -463,8 +475,6 @@ DEV void move_to_active(Wv& w, uint32_t p) {             // hv:1679-1709
 }
 
 // ------------------------------------------------------------ plumtree --
-DEV void load_pt(Wv& w) {}        // loaded with the node (NodeX)
-
 DEV void ord_add(Wv& w, uint32_t& V, uint32_t& n, uint32_t cap, uint32_t e) {
     uint32_t l = lane_id();
     if (ballot(l < n && V == e)) return;
@@ -512,7 +522,6 @@ DEV void slot_del(uint32_t& V, uint32_t k, uint32_t& n, uint32_t e) {
 // notify/1 (hv:1598-1599) -> plumtree update/1 -> handle_cast({update, ..})
 // (pt:314-336), reset_peers/4 (:652-659), neighbors_down/2 (:404-423)
 DEV void apply_notify(Wv& w, uint32_t SNAP, uint32_t sn) {
-    load_pt(w);
     w.pt_dirty = true;
     uint32_t l = lane_id();
     uint32_t CUR = SNAP;
@@ -566,7 +575,10 @@ DEV void apply_notify(Wv& w, uint32_t SNAP, uint32_t sn) {
 // the update logic instead of one per call site).  A notify identical to the
 // previous one is a no-op (New and Removed are both empty) and is not logged.
 constexpr uint32_t NLOG = 16;
+DEV void load_pt_rows(Wv& w);
 DEV void replay_notifies(Wv& w) {
+    if (!w.nlog_n) return;
+    if (!w.pt) load_pt_rows(w);                  // the Plumtree rows, on the first replay only
     uint32_t l = lane_id();
     for (uint32_t i = 0; i < w.nlog_n; i++) {
         uint32_t V = l < PSIM_ACTIVE_CAP ? w.nlog[i * PSIM_ACTIVE_CAP + l] : 0u;
@@ -696,7 +708,6 @@ DEV uint32_t msg_root(Wv& w, uint32_t msg) {
 
 DEV void pt_handle(Wv& w, uint32_t type, uint32_t src, uint32_t msg, uint32_t rnd, uint32_t root) {
     uint32_t from = src | PSIM_MAP_BIT;
-    load_pt(w);
     switch (type) {
     case PSIM_MSG_PT_BROADCAST:                        // pt:288-293, :368-378
         if (!pt_have(w, msg)) {                        // plumtree_backend merge/2
@@ -862,13 +873,15 @@ DEV uint32_t inbox_chunk(const Wv& w, const RoundArgs& a, uint32_t ib, uint32_t 
     return c == 0 ? R0 : load_chunk(a, ib, ik, c);
 }
 
-// A node's inputs arrive in two stages, each issued one step ahead with every
-// lane loading (lanes beyond a row re-read an element of it), so every node
-// issues the same vector memory operations:
+// The HyParView kernel's inputs arrive in two stages, each issued one step
+// ahead with every lane loading (lanes beyond a row re-read an element of
+// it), so every node issues the same vector memory operations:
 //   NodeIn (rows, from the work descriptor): header, active and passive
 //          views, the first inbox chunk, the node's flag and partition bytes;
 //   NodeX  (needs the rows): flag/partition bytes of every view member (the
-//          connection cache), the disconnect-id maps and the Plumtree rows.
+//          connection cache) and the disconnect-id maps.
+// The Plumtree rows are not staged: the Plumtree phase runs in k_pt; this
+// kernel reads them only to replay notifies (load_pt_rows).
 struct NodeIn {
     uint32_t n, ib, ik, ob, tf;    // tf: due timers (DESC_* bits, k_desc)
     uint32_t H;                    // header word l & 15
@@ -878,7 +891,6 @@ struct NodeIn {
 struct NodeX {
     uint32_t CV, CF;               // view ids (passive 0-31, active 32-39), their flags | part << 8
     uint32_t MS, MR;               // sent / recv maps: peers in lanes 0-31, ids in 32-63
-    uint32_t PA, PG, PL, PO;       // pt_all | pt_com | pt_rt, pt_eag, pt_laz, pt_out (lo, hi words)
 };
 
 DEV uint32_t load_desc(const RoundArgs& a, uint32_t k) {
@@ -901,29 +913,64 @@ DEV NodeIn load_node(const RoundArgs& a, uint32_t D) {
     return x;
 }
 
+// flag | partition << 8 of the view members in CV (the connection cache)
+DEV uint32_t cache_flags(const RoundArgs& a, uint32_t cv, uint32_t me) {
+    const uint32_t ca = cv < a.n_nodes ? cv : me;
+    const uint32_t f = a.flags[ca], pt = a.part[ca];
+    return cv < a.n_nodes ? (f | (pt << 8)) : 0u;
+}
+
 DEV NodeX load_x(const RoundArgs& a, const NodeIn& x) {
     uint32_t l = lane_id();
     NodeX y;
     const size_t li = x.n - a.lo;
-
     const uint32_t hw9 = rl(x.H, 9);                 // act_n, pas_n, .. (Hdr word 9)
     const uint32_t act_n = hw9 & 0xFF, pas_n = (hw9 >> 8) & 0xFF;
     uint32_t av = shfl(x.A, (int)(l & 7));
     uint32_t cv = l < 32 ? (l < pas_n ? x.P : NONE) : (l < 40 && l - 32 < act_n ? av : NONE);
-    uint32_t ca = cv < a.n_nodes ? cv : x.n;
-    uint32_t f = a.flags[ca], pt = a.part[ca];
     y.CV = cv;
-    y.CF = cv < a.n_nodes ? (f | (pt << 8)) : 0u;
+    y.CF = cache_flags(a, cv, x.n);
     const uint32_t l31 = l & 31;
     y.MS = (l < 32 ? a.sentp : a.senti)[li * PSIM_IDMAP_CAP + l31];
     y.MR = (l < 32 ? a.recvp : a.recvi)[li * PSIM_IDMAP_CAP + l31];
-    // lanes 0-7 pt_all, 8-15 pt_com, 16-23 the root row (and again above 24)
-    y.PA = ((l & 31) < 8 ? a.pt_all + li * PSIM_PT_MEMBERS_CAP
-                         : (l & 31) < 16 ? a.pt_com + li * PSIM_PT_MEMBERS_CAP : a.pt_rt + li * RT_WORDS)[l & 7];
-    y.PG = a.pt_eag[li * RT_SET + l];
-    y.PL = a.pt_laz[li * RT_SET + l];
-    y.PO = reinterpret_cast<const uint32_t*>(a.pt_out + li * PSIM_PT_OUT_CAP)[l];
     return y;
+}
+
+// the Plumtree rows of the running node (all_members | common_eagers | root
+// row, per-root eager and lazy sets, outstanding) into the wave's registers
+DEV void load_pt_regs(Wv& w, uint32_t PA, uint32_t PG, uint32_t PL, uint32_t PO) {
+    const uint32_t l = lane_id();
+    const uint32_t c8 = shfl(PA, (int)((l + 8) & 63));   // lanes 0-7: com (8-15); lanes 8-15: the root row (16-23)
+    w.AR = l < RTB ? PA : (l < RTB + RT_WORDS ? c8 : 0u);
+    w.COM = l < PSIM_PT_MEMBERS_CAP ? c8 : 0u;
+    w.EAG = PG; w.LAZ = PL;
+    uint32_t olo = shfl(PO, (int)((2 * l) & 63)), ohi = shfl(PO, (int)((2 * l + 1) & 63));
+    w.OUT = l < PSIM_PT_OUT_CAP ? (((uint64_t)ohi << 32) | olo) : 0ull;
+    w.pt = true;
+}
+// lanes 0-7 pt_all, 8-15 pt_com, 16-23 the root row (and again above 24)
+DEV uint32_t load_pa(const RoundArgs& a, size_t li) {
+    const uint32_t l = lane_id();
+    return ((l & 31) < 8 ? a.pt_all + li * PSIM_PT_MEMBERS_CAP
+                         : (l & 31) < 16 ? a.pt_com + li * PSIM_PT_MEMBERS_CAP : a.pt_rt + li * RT_WORDS)[l & 7];
+}
+DEV void load_pt_rows(Wv& w) {
+    const RoundArgs& a = *w.a;
+    const uint32_t l = lane_id();
+    const size_t li = w.li;
+    load_pt_regs(w, load_pa(a, li), a.pt_eag[li * RT_SET + l], a.pt_laz[li * RT_SET + l],
+                 reinterpret_cast<const uint32_t*>(a.pt_out + li * PSIM_PT_OUT_CAP)[l]);
+}
+
+// the header words of the node into the wave's scalars
+DEV void begin_header(Wv& w, uint32_t H) {
+    w.start_round = rl(H, 2); w.contact = rl(H, 3); w.epoch = rl(H, 4);
+    w.rng = ((uint64_t)rl(H, 1) << 32) | rl(H, 0);
+    w.aux = rl(H, 5); w.have = rl(H, 6); w.trk_round = rl(H, 7); w.trk_hop = rl(H, 8);
+    const uint32_t w9 = rl(H, 9), w10 = rl(H, 10), w11 = rl(H, 11);
+    w.act_n = w9 & 0xFF; w.pas_n = (w9 >> 8) & 0xFF; w.sent_n = (w9 >> 16) & 0xFF; w.sent_head = w9 >> 24;
+    w.recv_n = w10 & 0xFF; w.recv_head = (w10 >> 8) & 0xFF; w.all_n = (w10 >> 16) & 0xFF; w.com_n = w10 >> 24;
+    w.out_n = (w11 >> 16) & 0xFF;
 }
 
 // node state and the per-node scratch of the wave, from the staged inputs
@@ -931,40 +978,28 @@ DEV void begin_node(Wv& w, const NodeIn& x, const NodeX& y) {
     const uint32_t l = lane_id();
     w.li = x.n - w.a->lo;
     w.me = x.n;
-    w.start_round = rl(x.H, 2); w.contact = rl(x.H, 3); w.epoch = rl(x.H, 4);
+    begin_header(w, x.H);
     w.vd = 0;
-    w.rng = ((uint64_t)rl(x.H, 1) << 32) | rl(x.H, 0);
-    w.aux = rl(x.H, 5); w.have = rl(x.H, 6); w.trk_round = rl(x.H, 7); w.trk_hop = rl(x.H, 8);
     w.A = l < PSIM_ACTIVE_CAP ? x.A : 0u;
     w.P = l < PSIM_PASSIVE_CAP ? x.P : 0u;
     w.fl = x.fl;
     w.obase = x.ob;
     w.mypart = x.part;
     w.CV = y.CV; w.CF = y.CF;
-
     uint32_t msi = shfl(y.MS, (int)((l + 32) & 63)), mri = shfl(y.MR, (int)((l + 32) & 63));
     w.SP = l < 32 ? y.MS : 0u; w.SI = l < 32 ? msi : 0u;
     w.RP = l < 32 ? y.MR : 0u; w.RI = l < 32 ? mri : 0u;
-    uint32_t com = shfl(y.PA, (int)((l + 8) & 63)), rt = shfl(y.PA, (int)((l + 8) & 63));   // (lanes 8-15: 16-23)
-    w.AR = l < RTB ? y.PA : (l < RTB + RT_WORDS ? rt : 0u); w.COM = l < PSIM_PT_MEMBERS_CAP ? com : 0u;
-    w.EAG = y.PG; w.LAZ = y.PL;
-    uint32_t olo = shfl(y.PO, (int)((2 * l) & 63)), ohi = shfl(y.PO, (int)((2 * l + 1) & 63));
-    w.OUT = l < PSIM_PT_OUT_CAP ? (((uint64_t)ohi << 32) | olo) : 0ull;
-    {
-        const uint32_t w9 = rl(x.H, 9), w10 = rl(x.H, 10), w11 = rl(x.H, 11);
-        w.act_n = w9 & 0xFF; w.pas_n = (w9 >> 8) & 0xFF; w.sent_n = (w9 >> 16) & 0xFF; w.sent_head = w9 >> 24;
-        w.recv_n = w10 & 0xFF; w.recv_head = (w10 >> 8) & 0xFF; w.all_n = (w10 >> 16) & 0xFF; w.com_n = w10 >> 24;
-        w.out_n = (w11 >> 16) & 0xFF;
-    }
-    w.maps = true; w.pt = true; w.maps_dirty = false; w.pt_dirty = false;
+    w.maps = true; w.pt = false; w.maps_dirty = false; w.pt_dirty = false;
     w.seq = 0; w.flushed = 0;
     w.nlog_n = 0;
     w.dc_base = NONE64;                                // the cache holds another node's stream
     w.work = false;
 }
 
-// The node's handlers in the order of round model R0.  No global store.
-DEV void body(Wv& w, const NodeIn& x) {
+// The node's HyParView handlers in the order of round model R0, then the
+// replay of its notifies into the Plumtree state.  No global store.  The
+// Plumtree inbox, origin and lazy tick follow in k_pt.
+DEV void body_hv(Wv& w, const NodeIn& x) {
     const RoundArgs& a = *w.a;
     const uint32_t r = a.round;
     const uint32_t l = lane_id();
@@ -979,8 +1014,7 @@ DEV void body(Wv& w, const NodeIn& x) {
     bool promo = (x.tf & DESC_PROMO) != 0;
     bool shuf = (x.tf & DESC_SHUFFLE) != 0;
     bool origin = (x.tf & DESC_ORIGIN) != 0;
-    bool lazy_due = (x.tf & DESC_LAZY) != 0;
-    bool lazy = lazy_due && w.out_n > 0;
+    bool lazy = (x.tf & DESC_LAZY) != 0 && w.out_n > 0;
     bool joining = hw_start(w) == r && hw_contact(w) != NONE;
     uint64_t exits = 0;
     if (a.crash_round) {                        // F_CRASHED of the active members (cache lanes 32-39)
@@ -1038,57 +1072,15 @@ DEV void body(Wv& w, const NodeIn& x) {
         uint32_t t = select_random(w, w.A, w.act_n, n, n, n);
         if (t != NONE) hv_send(w, t, PSIM_MSG_SHUFFLE, a.arwl, 0, 0, EX, nex);
     }
-
     STAMP(w, 14);
-    if (a.plumtree) {
-        replay_notifies(w);
-        STAMP(w, 15);
-        for (uint32_t c = 0; c < ik; c += 4) {        // Plumtree inbox
-            uint32_t R4 = inbox_chunk(w, a, ib, ik, c, R0);
-            uint32_t cm = ik - c < 4 ? ik - c : 4;
-            for (uint32_t q = 0; q < cm; q++) {
-                uint32_t b = q * 16;
-                uint32_t type = rl(R4, b + 2) & 0xFF;
-                if (type < PSIM_MSG_PT_BROADCAST || type > PSIM_MSG_PT_GRAFT) continue;
-                st_add(w, ST_DELIV + type, 1);
-                STAMP(w, 3);
-                pt_handle(w, type, rl(R4, b + 1), rl(R4, b + 4), rl(R4, b + 5), rl(R4, b + 6));
-                STAMP(w, 16 + type - PSIM_MSG_PT_BROADCAST);
-            }
-        }
-        STAMP(w, 3);
-        if (origin) {                                 // pt:282-287, backend:179-200
-            const uint32_t my = n | PSIM_MAP_BIT, msg = uni(a.origin[n - a.lo]) - 1;
-            pt_mark(w, msg);
-            if (msg == a.tracked_msg) { w.trk_round = r; w.trk_hop = 0; }
-            pt_push(w, msg, 0, my, my);
-        }
-        STAMP(w, 21);
-        if (lazy_due && w.out_n > 0) {                // pt:341-345, :443-453
-            for (uint32_t i = 0; i < w.out_n; i++) {
-                uint64_t o = rl64(w.OUT, i);
-                const uint32_t peer = (uint32_t)(o >> 32), msg = (uint32_t)(o >> 16) & 0xFFFFu;
-                if (!pt_conn(w, peer)) { st_add(w, ST_FAIL, 1); continue; }
-                emit(w, peer & ~PSIM_MAP_BIT, PSIM_MSG_PT_IHAVE, 0, msg, (uint32_t)o & 0xFFFFu, msg_root(w, msg), 0, 0);
-            }
-        }
-    }
-    STAMP(w, 22);
+    if (a.plumtree) replay_notifies(w);
+    STAMP(w, 15);
 }
 
-// Write back the node: a fixed set of full-wave stores (each lane past a
-// row's end repeats one of its elements; a row that did not change is
-// "stored" as a rewrite of header word 0 with its own value), then the
-// staged records.  12 vector memory operations for every node.
-DEV void writeback(Wv& w) {
-    const RoundArgs& a = *w.a;
-    const uint32_t l = lane_id();
-    const size_t li = w.li;
-    // header word l & 15: the loaded word, or the round's value of it
-    const uint32_t k = l & 15;
-    const uint32_t h0 = (uint32_t)w.rng;
+// the header word l & 15 from the wave's scalars
+DEV uint32_t header_word(const Wv& w, uint32_t k) {
     uint32_t v = 0;                                  // pad words: 0 on a HyParView handle
-    v = k == 0 ? h0 : v;
+    v = k == 0 ? (uint32_t)w.rng : v;
     v = k == 1 ? (uint32_t)(w.rng >> 32) : v;
     v = k == 2 ? w.start_round : v;
     v = k == 3 ? w.contact : v;
@@ -1100,8 +1092,43 @@ DEV void writeback(Wv& w) {
     v = k == 9 ? (w.act_n | (w.pas_n << 8) | (w.sent_n << 16) | (w.sent_head << 24)) : v;
     v = k == 10 ? (w.recv_n | (w.recv_head << 8) | (w.all_n << 16) | (w.com_n << 24)) : v;
     v = k == 11 ? (w.out_n << 16) : v;
+    return v;
+}
+
+// the Plumtree rows of the wave back (a rare branch in the HyParView
+// kernel: only after a notify replay)
+DEV void store_pt_rows(Wv& w) {
+    const RoundArgs& a = *w.a;
+    const uint32_t l = lane_id();
+    const size_t li = w.li;
+    uint32_t all = shfl(w.AR, (int)(l & 7)), com = shfl(w.COM, (int)(l & 7)), rt = shfl(w.AR, (int)(RTB + (l & 7)));
+    uint64_t o = shfl64(w.OUT, (int)(l >> 1));
+    const uint32_t l31 = l & 31;
+    uint32_t* p1 = (l31 < 8 ? a.pt_all + li * PSIM_PT_MEMBERS_CAP
+                            : l31 < 16 ? a.pt_com + li * PSIM_PT_MEMBERS_CAP : a.pt_rt + li * RT_WORDS) + (l & 7);
+    *p1 = l31 < 8 ? all : l31 < 16 ? com : rt;
+    a.pt_eag[li * RT_SET + l] = w.EAG;
+    a.pt_laz[li * RT_SET + l] = w.LAZ;
+    reinterpret_cast<uint32_t*>(a.pt_out + li * PSIM_PT_OUT_CAP)[l] = (l & 1) ? (uint32_t)(o >> 32) : (uint32_t)o;
+}
+
+DEV uint8_t flag_byte(const Wv& w) {
+    return (uint8_t)((w.fl & (F_UP | F_CRASHED)) | (w.out_n ? F_LAZY : 0) | (min(w.out_n, 15u) << F_OUTN_SHIFT) |
+                     (w.act_n < w.a->min_active ? F_LOWACT : 0));
+}
+
+// Write back the node: a fixed set of full-wave stores (each lane past a
+// row's end repeats one of its elements; a row that did not change is
+// "stored" as a rewrite of header word 0 with its own value), then the
+// staged records.  8 vector memory operations for every node, the Plumtree
+// rows too after a notify replay.
+DEV void writeback(Wv& w) {
+    const RoundArgs& a = *w.a;
+    const uint32_t l = lane_id();
+    const size_t li = w.li;
+    const uint32_t h0 = (uint32_t)w.rng;
     uint32_t* hrow = reinterpret_cast<uint32_t*>(a.hdr + li);
-    hrow[k] = v;
+    hrow[l & 15] = header_word(w, l & 15);
     {
         bool dirty = (w.vd & 1u) != 0;
         uint32_t x = shfl(w.A, (int)(l & 7));
@@ -1121,36 +1148,22 @@ DEV void writeback(Wv& w) {
         *(d ? p1 : hrow) = d ? (l < 32 ? w.SP : si) : h0;
         *(d ? p2 : hrow) = d ? (l < 32 ? w.RP : ri) : h0;
     }
-    {
-        const bool d = w.pt_dirty;
-        uint32_t all = shfl(w.AR, (int)(l & 7)), com = shfl(w.COM, (int)(l & 7)), rt = shfl(w.AR, (int)(RTB + (l & 7)));
-        uint64_t o = shfl64(w.OUT, (int)(l >> 1));
-        const uint32_t l31 = l & 31;
-        uint32_t* p1 = (l31 < 8 ? a.pt_all + li * PSIM_PT_MEMBERS_CAP
-                                : l31 < 16 ? a.pt_com + li * PSIM_PT_MEMBERS_CAP : a.pt_rt + li * RT_WORDS) + (l & 7);
-        uint32_t* p3 = reinterpret_cast<uint32_t*>(a.pt_out + li * PSIM_PT_OUT_CAP) + l;
-        *(d ? p1 : hrow) = d ? (l31 < 8 ? all : l31 < 16 ? com : rt) : h0;
-        *(d ? a.pt_eag + li * RT_SET + l : hrow) = d ? w.EAG : h0;
-        *(d ? a.pt_laz + li * RT_SET + l : hrow) = d ? w.LAZ : h0;
-        *(d ? p3 : hrow) = d ? ((l & 1) ? (uint32_t)(o >> 32) : (uint32_t)o) : h0;
-    }
+    if (w.pt_dirty) store_pt_rows(w);
     a.ocnt[li] = w.seq;
     // only this wave writes its node's flag byte; peers read F_UP/F_CRASHED
-    a.flags[w.me] = (uint8_t)((w.fl & (F_UP | F_CRASHED)) | (w.out_n ? F_LAZY : 0) |
-                              (min(w.out_n, 15u) << F_OUTN_SHIFT) |
-                              (w.act_n < a.min_active ? F_LOWACT : 0));
+    a.flags[w.me] = flag_byte(w);
     flush_recs(w);
     STAMP(w, 23);
 }
 
+// one HyParView-phase wave per node of the list (k_relay leaves here every
+// node whose HyParView work is more than one SHUFFLE relay)
 __global__ void __launch_bounds__(256, PSIM_WAVES_PER_SIMD) k_consume(RoundArgs args) {
     __shared__ uint64_t sst[NST];
     __shared__ uint32_t scratch[WAVES_PER_BLOCK][64];
     __shared__ uint32_t nlogs[WAVES_PER_BLOCK][NLOG * (PSIM_ACTIVE_CAP + 1)];
     __shared__ __attribute__((aligned(16))) uint32_t srecs[WAVES_PER_BLOCK][STAGE * 16];
     __shared__ uint32_t skeys[WAVES_PER_BLOCK][STAGE];
-    __shared__ uint32_t sslots[2 * PSIM_MSG_SLOTS];
-    for (int i = threadIdx.x; i < 2 * PSIM_MSG_SLOTS; i += blockDim.x) sslots[i] = args.slots[i];
     for (int i = threadIdx.x; i < NST; i += blockDim.x) sst[i] = 0;
     if (threadIdx.x == 0) atomicMin(&args.ktime[0], (unsigned long long)__builtin_amdgcn_s_memrealtime());
     __syncthreads();
@@ -1164,7 +1177,7 @@ __global__ void __launch_bounds__(256, PSIM_WAVES_PER_SIMD) k_consume(RoundArgs 
     w.nlog = nlogs[wid];
     w.srec = srecs[wid];
     w.skey = skeys[wid];
-    w.slots = sslots;
+    w.slots = nullptr;
 #ifdef PSIM_STAMPS
     __shared__ uint64_t stamps[WAVES_PER_BLOCK][32];
     if ((threadIdx.x & 63) < 32) stamps[wid][threadIdx.x & 63] = 0;
@@ -1191,7 +1204,7 @@ __global__ void __launch_bounds__(256, PSIM_WAVES_PER_SIMD) k_consume(RoundArgs 
         for (uint32_t i = gw; i < na; i += nw) {
             STAMP(w, 24);
             begin_node(w, x, y);
-            body(w, x);
+            body_hv(w, x);
             NodeX yn = load_x(args, xn);
             writeback(w);
             NodeIn xnn = load_node(args, d);
@@ -1202,16 +1215,171 @@ __global__ void __launch_bounds__(256, PSIM_WAVES_PER_SIMD) k_consume(RoundArgs 
 #ifdef PSIM_STAMPS
     if (lane_id() < 32) atomicAdd(&g_stamps[lane_id()], (unsigned long long)w.stl[lane_id()]);
 #endif
-    // flush this wave's counters and digest partials into the block's LDS stats
-    {
-        uint32_t l = lane_id();
-        if (l < NST && w.SC) atomicAdd((unsigned long long*)&sst[l], (unsigned long long)w.SC);
-        uint64_t dg = w.digest;
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) dg += shfl64(dg, (int)((l + off) & 63));
-        if (l == 0 && dg) atomicAdd((unsigned long long*)&sst[ST_DIGEST], (unsigned long long)dg);
-    }
+    flush_wave_stats(w, sst);
+    __syncthreads();
+    for (int i = threadIdx.x; i < NST; i += blockDim.x)
+        args.stat_part[(size_t)blockIdx.x * NST + i] = sst[i];
+    if (threadIdx.x == 0) atomicMax(&args.ktime[1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+}
 
+// ------------------------------------------------------- Plumtree phase --
+// k_pt: one wave per node with Plumtree work (k_relay's second list), after
+// the node's HyParView phase (k_relay's lane or k_consume): its Plumtree
+// inbox in canonical order, its origin broadcast and its lazy tick
+// (pt:282-313, :341-345, :443-453; round model R0 steps 2f-2h).  It reads
+// the header, active view and outbox count the HyParView phase left and
+// continues the node's emissions after them.  The same two-stage pipeline:
+//   PtIn   header, active view, first inbox chunk, flag / partition bytes,
+//          the outbox count so far
+//   PtX    flag / partition bytes of the active members, the Plumtree rows
+struct PtIn {
+    uint32_t n, ib, ik, ob, tf;
+    uint32_t H, A, R0;
+    uint32_t fl, part, oc;
+};
+struct PtX {
+    uint32_t CF, PA, PG, PL, PO;
+};
+
+DEV PtIn load_pt_node(const RoundArgs& a, uint32_t D) {
+    const uint32_t l = lane_id();
+    PtIn x;
+    x.n = rl(D, 0); x.ib = rl(D, 1); x.ik = rl(D, 2) & DESC_CNT_MASK; x.tf = rl(D, 2) >> 28; x.ob = rl(D, 3);
+    const size_t li = x.n - a.lo;
+    x.H = reinterpret_cast<const uint32_t*>(a.hdr + li)[l & 15];
+    x.A = a.act[li * PSIM_ACTIVE_CAP + (l & 7)];
+    const uint32_t m = x.ik ? min(l >> 4, x.ik - 1) : 0u;
+    x.R0 = reinterpret_cast<const uint32_t*>(a.rec_in + x.ib + m)[l & 15];
+    x.fl = a.flags[x.n];
+    x.part = a.part[x.n];
+    x.oc = a.ocnt[li];
+    return x;
+}
+
+// the active members' ids in cache lanes 32-39 (connect_ok)
+DEV uint32_t act_cache(const PtIn& x) {
+    const uint32_t l = lane_id(), act_n = rl(x.H, 9) & 0xFF;
+    const uint32_t av = shfl(x.A, (int)(l & 7));
+    return l >= 32 && l < 40 && l - 32 < act_n ? av : NONE;
+}
+
+DEV PtX load_pt_x(const RoundArgs& a, const PtIn& x) {
+    const uint32_t l = lane_id();
+    PtX y;
+    const size_t li = x.n - a.lo;
+    y.CF = cache_flags(a, act_cache(x), x.n);
+    y.PA = load_pa(a, li);
+    y.PG = a.pt_eag[li * RT_SET + l];
+    y.PL = a.pt_laz[li * RT_SET + l];
+    y.PO = reinterpret_cast<const uint32_t*>(a.pt_out + li * PSIM_PT_OUT_CAP)[l];
+    return y;
+}
+
+DEV void begin_pt(Wv& w, const PtIn& x, const PtX& y) {
+    const uint32_t l = lane_id();
+    w.li = x.n - w.a->lo;
+    w.me = x.n;
+    begin_header(w, x.H);
+    w.A = l < PSIM_ACTIVE_CAP ? x.A : 0u;
+    w.fl = x.fl;
+    w.obase = x.ob;
+    w.mypart = x.part;
+    w.CV = act_cache(x); w.CF = y.CF;
+    load_pt_regs(w, y.PA, y.PG, y.PL, y.PO);
+    w.pt_dirty = false;
+    w.seq = x.oc; w.flushed = x.oc;                  // after the HyParView phase's records
+}
+
+DEV void body_pt(Wv& w, const PtIn& x) {
+    const RoundArgs& a = *w.a;
+    const uint32_t r = a.round, n = x.n;
+    // a fresh incarnation drops its inbox (counted by the HyParView phase)
+    const uint32_t ik = hw_start(w) == r ? 0u : x.ik;
+    for (uint32_t c = 0; c < ik; c += 4) {            // Plumtree inbox, canonical order
+        uint32_t R4 = c == 0 ? x.R0 : load_chunk(a, x.ib, ik, c);
+        uint32_t cm = ik - c < 4 ? ik - c : 4;
+        for (uint32_t q = 0; q < cm; q++) {
+            uint32_t b = q * 16;
+            uint32_t type = rl(R4, b + 2) & 0xFF;
+            if (type < PSIM_MSG_PT_BROADCAST || type > PSIM_MSG_PT_GRAFT) continue;
+            st_add(w, ST_DELIV + type, 1);
+            pt_handle(w, type, rl(R4, b + 1), rl(R4, b + 4), rl(R4, b + 5), rl(R4, b + 6));
+        }
+    }
+    if (x.tf & DESC_ORIGIN) {                         // pt:282-287, backend:179-200
+        const uint32_t my = n | PSIM_MAP_BIT, msg = uni(a.origin[n - a.lo]) - 1;
+        pt_mark(w, msg);
+        if (msg == a.tracked_msg) { w.trk_round = r; w.trk_hop = 0; }
+        pt_push(w, msg, 0, my, my);
+    }
+    if ((x.tf & DESC_LAZY) && w.out_n > 0) {          // pt:341-345, :443-453
+        for (uint32_t i = 0; i < w.out_n; i++) {
+            uint64_t o = rl64(w.OUT, i);
+            const uint32_t peer = (uint32_t)(o >> 32), msg = (uint32_t)(o >> 16) & 0xFFFFu;
+            if (!pt_conn(w, peer)) { st_add(w, ST_FAIL, 1); continue; }
+            emit(w, peer & ~PSIM_MAP_BIT, PSIM_MSG_PT_IHAVE, 0, msg, (uint32_t)o & 0xFFFFu, msg_root(w, msg), 0, 0);
+        }
+    }
+}
+
+DEV void writeback_pt(Wv& w) {
+    const RoundArgs& a = *w.a;
+    const uint32_t l = lane_id();
+    const size_t li = w.li;
+    reinterpret_cast<uint32_t*>(a.hdr + li)[l & 15] = header_word(w, l & 15);
+    if (w.pt_dirty) store_pt_rows(w);
+    a.ocnt[li] = w.seq;
+    a.flags[w.me] = flag_byte(w);
+    if (w.seq != w.flushed) flush_recs(w);
+}
+
+__global__ void __launch_bounds__(256) k_pt(RoundArgs args) {
+    __shared__ uint64_t sst[NST];
+    __shared__ uint32_t scratch[WAVES_PER_BLOCK][64];
+    __shared__ __attribute__((aligned(16))) uint32_t srecs[WAVES_PER_BLOCK][STAGE * 16];
+    __shared__ uint32_t skeys[WAVES_PER_BLOCK][STAGE];
+    __shared__ uint32_t sslots[2 * PSIM_MSG_SLOTS];
+    for (int i = threadIdx.x; i < 2 * PSIM_MSG_SLOTS; i += blockDim.x) sslots[i] = args.slots[i];
+    for (int i = threadIdx.x; i < NST; i += blockDim.x) sst[i] = 0;
+    __syncthreads();
+    const uint32_t wid = threadIdx.x >> 6;
+    const uint32_t gw = uni(blockIdx.x * WAVES_PER_BLOCK + wid);
+    const uint32_t nw = gridDim.x * WAVES_PER_BLOCK;
+    Wv w;
+    w.a = &args;
+    w.lds = scratch[wid];
+    w.nlog = nullptr;
+    w.srec = srecs[wid];
+    w.skey = skeys[wid];
+    w.slots = sslots;
+#ifdef PSIM_STAMPS
+    __shared__ uint64_t stamps[WAVES_PER_BLOCK][32];
+    if ((threadIdx.x & 63) < 32) stamps[wid][threadIdx.x & 63] = 0;
+    w.stl = stamps[wid];
+    w.t_last = __builtin_amdgcn_s_memtime();
+#endif
+    w.st = sst;
+    w.round = args.round;
+    w.SC = 0;
+    w.digest = 0;
+    const uint32_t na = *args.n_alist;
+    if (gw < na) {
+        const uint32_t last = na - 1;
+        PtIn x = load_pt_node(args, load_desc(args, gw));
+        PtX y = load_pt_x(args, x);
+        PtIn xn = load_pt_node(args, load_desc(args, min(gw + nw, last)));
+        uint32_t d = load_desc(args, min(gw + 2 * nw, last));
+        for (uint32_t i = gw; i < na; i += nw) {
+            begin_pt(w, x, y);
+            body_pt(w, x);
+            PtX yn = load_pt_x(args, xn);
+            writeback_pt(w);
+            PtIn xnn = load_pt_node(args, d);
+            d = load_desc(args, min(i + 3 * nw, last));
+            x = xn; y = yn; xn = xnn;
+        }
+    }
+    flush_wave_stats(w, sst);
     __syncthreads();
     for (int i = threadIdx.x; i < NST; i += blockDim.x)
         args.stat_part[(size_t)blockIdx.x * NST + i] = sst[i];
@@ -1219,19 +1387,20 @@ __global__ void __launch_bounds__(256, PSIM_WAVES_PER_SIMD) k_consume(RoundArgs 
 }
 
 // ------------------------------------------------ relays and lazy ticks --
-// Most nodes with work in a steady-state round do little: relay the one
-// SHUFFLE of their inbox (hv:1095-1136 with TTL > 0 and |active| > 1: a
-// select_random over active -- [Sender, Myself], then do_send_message)
-// and/or run the lazy tick over outstanding entries (pt:341-345, :443-453:
-// an IHAVE per entry, sent only over a live active connection).  Such a
-// node needs no wave: k_relay gives it one lane, reading its header, active
-// row, outstanding row and the record, and writing the emitted records, its
-// draw counter, outbox count and flag byte exactly as k_consume's body and
-// writeback would (no other inbox message, no timer of HyParView due, no
-// join, no crash round, not the origin).  Every other node with work is
-// appended to desc_slow for k_consume; the order of that list does not
-// matter (each node writes its own rows and outbox region; the stats and the
-// digest are sums).
+// k_relay gives every node with work one lane and sorts it: most nodes with
+// work in a steady-state round do little for HyParView -- at most relay the
+// one SHUFFLE of their inbox (hv:1095-1136 with TTL > 0 and |active| > 1: a
+// select_random over active -- [Sender, Myself], then do_send_message) --
+// and such a lane does it here, exactly as k_consume's body and writeback
+// would (the same draws, records, sequence numbers, digest and stats).  A
+// node with more HyParView work (other messages, a due timer that can act,
+// a join, a crash round) goes to k_consume's list.  A node with Plumtree
+// work (Plumtree messages, an origin, a due lazy tick with entries
+// outstanding) goes to k_pt's list -- unless its only Plumtree work is the
+// lazy tick and its HyParView work is done here: then the lane runs the
+// tick too (an IHAVE per outstanding entry over live active connections).
+// The order of the lists does not matter (each node writes its own rows and
+// outbox region; the stats and the digest are sums).
 DEV uint64_t relay_emit(const RoundArgs& a, uint64_t slot, uint32_t dst, uint32_t me, uint32_t tt, uint32_t seq,
                         uint32_t a0, uint32_t a1, uint32_t a2, const uint32_t (&X)[8]) {
     const uint32_t W[16] = {dst, me, tt, seq, a0, a1, a2, 0u, X[0], X[1], X[2], X[3], X[4], X[5], X[6], X[7]};
@@ -1247,12 +1416,33 @@ DEV uint64_t relay_emit(const RoundArgs& a, uint64_t slot, uint32_t dst, uint32_
     return dg;
 }
 
+// appends the lanes with `go` of this block step to list `desc` (counter
+// `cnt`): wave counts, a block scan in LDS, one global atomic per block step
+// (a same-address atomic per wave serialised at L2 and cost ~100 us per round)
+DEV void block_append(bool go, const uint4& D, uint4* desc, uint32_t* cnt, uint32_t* wcnt) {
+    const uint64_t m = ballot(go);
+    const uint32_t wv = threadIdx.x >> 6;
+    __syncthreads();                                  // the previous use's readers of wcnt are done
+    if (lane_id() == 0) wcnt[wv] = popc(m);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t t = wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
+        wcnt[4] = t ? atomicAdd(cnt, t) : 0u;
+    }
+    __syncthreads();
+    if (go) {
+        uint32_t b0 = wcnt[4];
+        for (uint32_t k = 0; k < wv; k++) b0 += wcnt[k];
+        desc[b0 + popc(m & lt_mask())] = D;
+    }
+}
+
 __global__ void __launch_bounds__(256) k_relay(RoundArgs a) {
     enum { R_PROC, R_DELIV, R_SHUF, R_IHAVE, R_FAIL, R_DIGEST, R_OVF, R_N };
     __shared__ unsigned long long sst[R_N];
     __shared__ uint32_t sslots[2 * PSIM_MSG_SLOTS];
     for (int i = threadIdx.x; i < 2 * PSIM_MSG_SLOTS; i += blockDim.x) sslots[i] = a.slots[i];
-    __shared__ uint32_t wcnt[5];                      // per wave slow counts, then the block's base
+    __shared__ uint32_t wcnt[5];                      // per wave list counts, then the block's base
     if (threadIdx.x < R_N) sst[threadIdx.x] = 0;
     if (threadIdx.x == 0) atomicMin(&a.ktime[0], (unsigned long long)__builtin_amdgcn_s_memrealtime());
     __syncthreads();
@@ -1263,10 +1453,9 @@ __global__ void __launch_bounds__(256) k_relay(RoundArgs a) {
     for (uint32_t base = blockIdx.x * blockDim.x; base < na; base += gridDim.x * blockDim.x) {
         const uint32_t P = base + threadIdx.x;
         uint4 D = make_uint4(0, 0, 0, 0);
-        bool fast = false;
+        bool heavy = false, to_pt = false, relay = false, lazy_here = false;
         Hdr h;
-        uint32_t ik = 0, ttl = 0, nex = 0, src = 0;
-        bool lazy = false;
+        uint32_t ik = 0, ttl = 0, nex = 0, src = 0, hv_at = 0;
         const Msg* rp = nullptr;
         uint4 act0 = make_uint4(0, 0, 0, 0), act1 = act0;
         uint32_t me_part = 0;
@@ -1274,56 +1463,50 @@ __global__ void __launch_bounds__(256) k_relay(RoundArgs a) {
             D = a.desc[P];
             const uint32_t id = D.x, tf = D.z >> 28;
             ik = D.z & DESC_CNT_MASK;
-            fast = ik <= 1 && !(tf & (DESC_SHUFFLE | DESC_ORIGIN)) && !a.crash_round;
-            if (fast) {
-                // the header, the record's first 16 B, the active row and the
-                // partition byte are independent: issued together, waited once
-                const size_t li = id - a.lo;
-                rp = a.rec_in + D.y;
-                const uint4 r0 = ik ? *reinterpret_cast<const uint4*>(rp) : make_uint4(0, 0, 0, 0);
-                h = a.hdr[li];
-                const uint4* ar = reinterpret_cast<const uint4*>(a.act + li * PSIM_ACTIVE_CAP);
-                act0 = ar[0];
-                act1 = ar[1];
-                me_part = a.part[id];
-                lazy = (tf & DESC_LAZY) && h.out_n > 0;
-                fast = h.start_round != a.round && (!(tf & DESC_PROMO) || h.act_n >= a.min_active);
-                if (ik) {
-                    const uint32_t tt = r0.z;
-                    ttl = (tt >> 8) & 0xFF;
-                    nex = (tt >> 16) & 0xFF;
-                    src = r0.y;
-                    fast = fast && h.act_n > 1 && (tt & 0xFF) == PSIM_MSG_SHUFFLE && ttl > 0;
+            // the header, the active row and the partition byte are
+            // independent: issued together, waited once
+            const size_t li = id - a.lo;
+            h = a.hdr[li];
+            const uint4* ar = reinterpret_cast<const uint4*>(a.act + li * PSIM_ACTIVE_CAP);
+            act0 = ar[0];
+            act1 = ar[1];
+            me_part = a.part[id];
+            // the inbox: how many HyParView messages, and the first of them
+            uint32_t hvn = 0, hv_tt = 0;
+            for (uint32_t j = 0; j < ik; j++) {
+                const uint32_t tt = a.rec_in[D.y + j].tt;
+                if ((tt & 0xFF) < PSIM_MSG_PT_BROADCAST) {
+                    if (!hvn) { hv_at = j; hv_tt = tt; }
+                    hvn++;
                 }
             }
+            const bool fresh = h.start_round == a.round;
+            heavy = a.crash_round || fresh || (tf & DESC_SHUFFLE) || ((tf & DESC_PROMO) && h.act_n < a.min_active) ||
+                    hvn > 1;
+            if (!heavy && hvn == 1) {
+                ttl = (hv_tt >> 8) & 0xFF;
+                nex = (hv_tt >> 16) & 0xFF;
+                relay = h.act_n > 1 && (hv_tt & 0xFF) == PSIM_MSG_SHUFFLE && ttl > 0;
+                heavy = !relay;
+            }
+            const bool pt_msgs = !fresh && ik > hvn, origin = (tf & DESC_ORIGIN) != 0;
+            const bool lazy = (tf & DESC_LAZY) && h.out_n > 0;
+            to_pt = a.plumtree && (pt_msgs || origin || (heavy && lazy));
+            lazy_here = !heavy && !to_pt && lazy;
+            relay = relay && !heavy;
+            if (!heavy && (relay || to_pt || lazy_here)) v[R_PROC]++;   // (k_consume counts its own)
         }
-        // the slow entries of this block step: wave counts, a block scan in
-        // LDS, one global atomic per block step (a same-address atomic per
-        // wave serialised at L2 and cost ~100 us per round)
-        const bool slow = P < na && !fast;
-        const uint64_t m = ballot(slow);
-        const uint32_t wv = threadIdx.x >> 6;
-        __syncthreads();                              // the previous step's readers of wcnt are done
-        if (l == 0) wcnt[wv] = popc(m);
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            const uint32_t t = wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
-            wcnt[4] = t ? atomicAdd(a.n_slow, t) : 0u;
-        }
-        __syncthreads();
-        if (slow) {
-            uint32_t b0 = wcnt[4];
-            for (uint32_t k = 0; k < wv; k++) b0 += wcnt[k];
-            a.desc_slow[b0 + popc(m & lt_mask())] = D;
-        }
-        if (!fast) continue;
+        block_append(P < na && heavy, D, a.desc_slow, a.n_slow, wcnt);
+        block_append(P < na && to_pt, D, a.desc_pt, a.n_pt, wcnt);
+        if (P >= na || heavy) continue;
         const uint32_t id = D.x;
         const size_t li = id - a.lo;
         const uint32_t A[8] = {act0.x, act0.y, act0.z, act0.w, act1.x, act1.y, act1.z, act1.w};
         uint64_t rng = h.rng;
         uint32_t seq = 0;
-        v[R_PROC]++;
-        if (ik) {
+        if (relay) {
+            rp = a.rec_in + D.y + hv_at;
+            src = rp->src;
             v[R_DELIV]++;
             // select_random(Active, [Sender, Myself]) (hv:1346-1356)
             uint32_t elig = 0;
@@ -1358,7 +1541,7 @@ __global__ void __launch_bounds__(256) k_relay(RoundArgs a) {
                 }
             }
         }
-        if (lazy) {                                   // send_lazy: every outstanding entry, in order
+        if (lazy_here) {                              // send_lazy: every outstanding entry, in order
             const uint32_t X[8] = {0, 0, 0, 0, 0, 0, 0, 0};
             // the row in chunks of 4 entries (two 16-B loads in flight at once)
             const uint4* orow = reinterpret_cast<const uint4*>(a.pt_out + li * PSIM_PT_OUT_CAP);
@@ -1395,10 +1578,12 @@ __global__ void __launch_bounds__(256) k_relay(RoundArgs a) {
         }
         if (rng != h.rng) a.hdr[li].rng = rng;
         a.ocnt[li] = seq;
-        const uint8_t fl = a.flags[id];
-        a.flags[id] = (uint8_t)((fl & (F_UP | F_CRASHED)) | (h.out_n ? F_LAZY : 0) |
-                                (min((uint32_t)h.out_n, 15u) << F_OUTN_SHIFT) |
-                                (h.act_n < a.min_active ? F_LOWACT : 0));
+        if (!to_pt) {                                 // (k_pt writes the byte of its nodes)
+            const uint8_t fl = a.flags[id];
+            a.flags[id] = (uint8_t)((fl & (F_UP | F_CRASHED)) | (h.out_n ? F_LAZY : 0) |
+                                    (min((uint32_t)h.out_n, 15u) << F_OUTN_SHIFT) |
+                                    (h.act_n < a.min_active ? F_LOWACT : 0));
+        }
     }
     // wave sums, then one LDS atomic per wave and counter
 #pragma unroll
@@ -1417,15 +1602,16 @@ __global__ void __launch_bounds__(256) k_relay(RoundArgs a) {
 
 // one wave-slot per resident wave: the grid strides over the active list
 // with no second generation of waves (a partial generation is a tail)
-uint32_t consume_grid() {
+static uint32_t resident_grid(const void* k) {
     int dev = 0, nb = 0;
     hipDeviceProp_t p;
     if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&p, dev) != hipSuccess ||
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_consume, WAVES_PER_BLOCK * 64, 0) != hipSuccess ||
-        nb <= 0)
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, WAVES_PER_BLOCK * 64, 0) != hipSuccess || nb <= 0)
         return 1024;
     return (uint32_t)nb * (uint32_t)p.multiProcessorCount;
 }
+uint32_t consume_grid() { return resident_grid((const void*)k_consume); }
+uint32_t pt_grid() { return resident_grid((const void*)k_pt); }
 
 #ifdef PSIM_STAMPS
 int debug_stamps(unsigned long long* out) {

@@ -411,30 +411,31 @@ __global__ void k_owner_offsets(const uint32_t* hoff, uint32_t nblk, uint32_t G,
 
 
 // One block per bucket of W destinations; LDS holds per destination the
-// count, bound sum, id mask and run start (4 x W words).
+// count, the bound sum (later the run start, in the same words) and the
+// BROADCAST message-slot mask (64 bits): 4 x W words.
 __global__ void __launch_bounds__(RR_THREADS) k_bucket_route(
     uint32_t n, uint32_t wshift, uint32_t nblk, const uint32_t* __restrict__ off,
     const uint2* __restrict__ pairs, const Msg* __restrict__ rec, uint32_t* rank, unsigned long long* cb,
-    uint32_t* bmask, uint32_t* in_beg, uint32_t* idx, uint32_t* long_list, uint32_t* n_long, uint64_t* hm,
+    unsigned long long* bmask, uint32_t* in_beg, uint32_t* idx, uint32_t* long_list, uint32_t* n_long, uint64_t* hm,
     uint64_t cap) {
     extern __shared__ uint32_t sm[];
     __shared__ uint32_t spart[RR_THREADS];
     const uint32_t W = 1u << wshift, wmask = W - 1, b = blockIdx.x;
     uint32_t* cnt = sm;
     uint32_t* bs = sm + W;
-    uint32_t* mk = sm + 2 * W;
-    uint32_t* pre = sm + 3 * W;
+    unsigned long long* mk = reinterpret_cast<unsigned long long*>(sm + 2 * W);
+    uint32_t* pre = bs;                               // (after the bound sums are written out)
     const uint32_t s0 = off[(size_t)b * nblk], s1 = off[(size_t)(b + 1) * nblk];
     if (off[(size_t)gridDim.x * nblk] > cap) return;  // overflow (k_bucket_scatter flagged it)
-    for (uint32_t j = threadIdx.x; j < 3 * W; j += blockDim.x) sm[j] = 0;
+    for (uint32_t j = threadIdx.x; j < 4 * W; j += blockDim.x) sm[j] = 0;
     __syncthreads();
     for (uint32_t p = s0 + threadIdx.x; p < s1; p += blockDim.x) {
         const uint2 x = pairs[p];
         const uint32_t dl = x.x & wmask, cls = x.x >> 16;
         rank[p] = atomicAdd(&cnt[dl], 1u);
-        if (cls == KEY_BCAST) {                       // 1 (a duplicate's PRUNE) + the id bit
+        if (cls == KEY_BCAST) {                       // 1 (a duplicate's PRUNE) + the slot bit
             atomicAdd(&bs[dl], 1u);
-            atomicOr(&mk[dl], 1u << (rec[x.y].a0 & 31u));
+            atomicOr(&mk[dl], 1ull << (rec[x.y].a0 % PSIM_MSG_SLOTS));
         } else if (cls) {
             atomicAdd(&bs[dl], cls);
         }
@@ -453,6 +454,13 @@ __global__ void __launch_bounds__(RR_THREADS) k_bucket_route(
         spart[threadIdx.x] += v;
         __syncthreads();
     }
+    for (uint32_t dl = threadIdx.x; dl < W; dl += blockDim.x) {
+        const uint32_t d = (b << wshift) + dl;
+        if (d >= n) break;
+        cb[d] = cnt[dl] | ((unsigned long long)bs[dl] << 32);
+        bmask[d] = mk[dl];
+    }
+    __syncthreads();                                  // the bound sums are out: pre reuses them
     uint32_t run = spart[threadIdx.x] - sum;
     for (uint32_t j = 0; j < per; j++) {
         pre[j0 + j] = run;
@@ -462,8 +470,6 @@ __global__ void __launch_bounds__(RR_THREADS) k_bucket_route(
     for (uint32_t dl = threadIdx.x; dl < W; dl += blockDim.x) {
         const uint32_t d = (b << wshift) + dl;
         if (d >= n) break;
-        cb[d] = cnt[dl] | ((unsigned long long)bs[dl] << 32);
-        bmask[d] = mk[dl];
         in_beg[d] = s0 + pre[dl];
     }
     if (b == gridDim.x - 1 && threadIdx.x == 0) {   // the record count
@@ -563,12 +569,12 @@ __device__ __forceinline__ bool due(uint32_t period, uint32_t r, uint32_t start)
 // outbox region) and whether it has any work (inbox, join, timers, EXIT
 // scan, origin, outstanding lazy pushes).  Also counts live nodes and
 // messages addressed to dead ones.
-__global__ void __launch_bounds__(256) k_node_prep(RoundArgs a, const uint32_t* bmask, uint64_t* packed,
+__global__ void __launch_bounds__(256) k_node_prep(RoundArgs a, const unsigned long long* bmask, uint64_t* packed,
                                                    uint64_t* part, uint32_t* ocnt, unsigned long long* btot) {
     __shared__ unsigned long long s_up, s_drop, s_b;
     if (threadIdx.x == 0) { s_up = 0; s_drop = 0; s_b = 0; }
     if (blockIdx.x == 0 && threadIdx.x == 0) {
-        a.ktime[0] = ~0ull; a.ktime[1] = 0; *a.n_slow = 0;
+        a.ktime[0] = ~0ull; a.ktime[1] = 0; *a.n_slow = 0; *a.n_pt = 0;
         if (a.n_stop) *a.n_stop = 0;
     }
     __syncthreads();
@@ -599,15 +605,15 @@ __global__ void __launch_bounds__(256) k_node_prep(RoundArgs a, const uint32_t* 
                 // per message its class bound (a BROADCAST: 1), per distinct
                 // BROADCAST id an eager push, and the lazy tick's IHAVEs if
                 // entries are outstanding or may be added this round
-                const uint32_t bm = c ? bmask[i] : 0u;
-                b = (cbi >> 32) + BOUND_BASE + (uint64_t)__popc(bm) * BCAST_FIRST;
+                const unsigned long long bm = c ? bmask[i] : 0ull;
+                b = (cbi >> 32) + BOUND_BASE + (uint64_t)__popcll(bm) * BCAST_FIRST;
                 // a due lazy tick sends every outstanding entry: those left
                 // from last round (flag nibble) and those this round's first
                 // deliveries and origin add, at most PT_OUT_CAP
                 if (a.plumtree && due(a.lazy_tick_period, r, st)) {
                     const uint32_t prev = (f >> F_OUTN_SHIFT) >= 15 ? PSIM_PT_OUT_CAP : (f >> F_OUTN_SHIFT);
                     b += min((uint32_t)PSIM_PT_OUT_CAP,
-                             prev + (__popc(bm) + (origin ? 1u : 0u)) * PSIM_PT_SET_CAP);
+                             prev + ((uint32_t)__popcll(bm) + (origin ? 1u : 0u)) * PSIM_PT_SET_CAP);
                 }
                 if (a.crash_round) b += BOUND_EXITS;
                 if (origin) b += BOUND_ORIGIN;
@@ -921,11 +927,12 @@ struct Shard {
     int in_cur = 0;                     // read by this round's consume, the other one is routed into
     // per-round scratch
     DBuf<uint32_t> okey, ocnt, in_beg,
-        d_nact, n_slow, rank, long_list, n_long, tmp, bmask, hist, hoff;
+        d_nact, n_slow, n_pt, rank, long_list, n_long, tmp, hist, hoff;
+    DBuf<unsigned long long> bmask;     // per local node: message slots of its BROADCAST records
     DBuf<uint2> pairs;                  // route: (destination in bucket | class, source index)
     DBuf<unsigned long long> cb;        // per local node: inbox count | bound sum << 32 (n + 1)
     DBuf<unsigned long long> btot;      // this round's outbox total (k_node_prep)
-    DBuf<uint4> desc, desc_slow;            // work descriptors; those k_relay leaves to k_consume
+    DBuf<uint4> desc, desc_slow, desc_pt;   // work descriptors; those k_relay leaves to k_consume / k_pt
     DBuf<uint64_t> bound, pscan, obase, stat_part, stat_out, d_off;   // bound: packed (bound << 32 | work)
     DBuf<uint8_t> cub_tmp;
     DBuf<uint32_t> ev_ids, ev_contacts, stop_ids, n_stop;
@@ -935,7 +942,7 @@ struct Shard {
     DBuf<uint32_t> sview, sinv, fbits, pay[2], pay_top;
     int pay_cur = 0;
     std::vector<uint64_t> soff, scnt;   // per destination shard (G + 1 offsets)
-    uint32_t pgrid = 0, cgrid = 0, rgrid = 0;   // stats rows: prepare, consume, relay blocks
+    uint32_t pgrid = 0, cgrid = 0, rgrid = 0, tgrid = 0;   // stats rows: prepare, consume, relay, plumtree blocks
     // pinned host words: NST stats and the consume span (stat_out), then the
     // outbox total and the routed record count: the round's two read-backs
     uint64_t* pin = nullptr;
@@ -959,6 +966,7 @@ struct psim_handle {
     uint32_t N = 0, G = 1, per = 0;
     int device = 0;
     uint32_t consume_blocks = 1024;     // resident k_consume blocks on the device
+    uint32_t pt_blocks = 1024;          // ... and k_pt blocks
     uint64_t round = 0;
     std::vector<Shard*> shards;         // shards owned by this process
     int rank = 0, world = 1;
@@ -982,7 +990,6 @@ struct psim_handle {
     // ~10 us bubble between kernels, so by default only k_consume is timed,
     // from its in-kernel span (RoundArgs::ktime)
     bool phase_timers = false;
-    bool relay = true;                  // k_relay ahead of k_consume (PSIM_NO_RELAY=1: off)
     // blocks of the route / owner-partition passes (RB_MAX_BLOCKS; a test
     // hook, PSIM_ROUTE_BLOCKS, lowers it so small runs take several steps per block)
     uint32_t rb_blocks = RB_MAX_BLOCKS;
@@ -1018,6 +1025,7 @@ RoundArgs make_args(psim_handle* h, Shard* s) {
     a.fbits = s->fbits.p; a.sview = s->sview.p; a.sinv = s->sinv.p;
     a.ktime = reinterpret_cast<unsigned long long*>(s->stat_out.p + NST);
     a.desc_slow = s->desc_slow.p; a.n_slow = s->n_slow.p;
+    a.desc_pt = s->desc_pt.p; a.n_pt = s->n_pt.p;
     a.stop_ids = s->stop_ids.p; a.n_stop = s->n_stop.p;
     return a;
 }
@@ -1142,8 +1150,10 @@ int phase_events_prepare(psim_handle* h, Shard* s, const RoundCtl& ctl, RoundArg
         s->cgrid = std::min<uint32_t>(grid_for(n), h->consume_blocks);
         // one lane per possible working node (up to RELAY_MAX_BLOCKS, then grid-stride):
         // the relays are chains of dependent random loads, so latency wants lanes
-        s->rgrid = h->relay && h->cfg.manager != PSIM_MANAGER_PLUGGABLE ? std::min<uint32_t>(grid_for(n), RELAY_MAX_BLOCKS) : 0;
-        TRY(s->stat_part.ensure((size_t)(s->pgrid + s->cgrid + s->rgrid) * NST));
+        const bool hv = h->cfg.manager != PSIM_MANAGER_PLUGGABLE;
+        s->rgrid = hv ? std::min<uint32_t>(grid_for(n), RELAY_MAX_BLOCKS) : 0;
+        s->tgrid = hv && h->cfg.plumtree ? std::min<uint32_t>(grid_for(n), h->pt_blocks) : 0;
+        TRY(s->stat_part.ensure((size_t)(s->pgrid + s->cgrid + s->rgrid + s->tgrid) * NST));
         k_node_prep<<<s->pgrid, BLK, 0, s->stream>>>(a, s->bmask.p, s->bound.p, s->stat_part.p, s->ocnt.p,
                                                      s->btot.p);
         // bound[n] = 0: pscan[n] = (outbox total << 32) | active count;
@@ -1191,6 +1201,7 @@ int phase_events_prepare(psim_handle* h, Shard* s, const RoundCtl& ctl, RoundArg
     a.okey = s->okey.p; a.ocnt = s->ocnt.p;
     a.stat_part = s->stat_part.p + (size_t)s->pgrid * NST;
     a.stat_relay = s->stat_part.p + (size_t)(s->pgrid + s->cgrid) * NST;
+    a.stat_pt = s->stat_part.p + (size_t)(s->pgrid + s->cgrid + s->rgrid) * NST;
     return PSIM_OK;
 }
 
@@ -1217,15 +1228,22 @@ int phase_consume(psim_handle* h, Shard* s, RoundArgs& a) {
     }
     if (a.pl) {
         k_consume_pl<<<s->cgrid, BLK, 0, s->stream>>>(a);
-    } else if (s->rgrid) {
-        // SHUFFLE relays one lane each, every other node one wave
+    } else {
+        // k_relay sorts the nodes with work: a lone SHUFFLE relay (and a
+        // lazy tick) one lane each, more HyParView work one k_consume wave,
+        // Plumtree work one k_pt wave after the node's HyParView phase
         k_relay<<<s->rgrid, BLK, 0, s->stream>>>(a);
         RoundArgs b = a;
         b.desc = s->desc_slow.p;
         b.n_alist = s->n_slow.p;
         k_consume<<<s->cgrid, BLK, 0, s->stream>>>(b);
-    } else {
-        k_consume<<<s->cgrid, BLK, 0, s->stream>>>(a);
+        if (s->tgrid) {
+            RoundArgs c = a;
+            c.desc = s->desc_pt.p;
+            c.n_alist = s->n_pt.p;
+            c.stat_part = a.stat_pt;
+            k_pt<<<s->tgrid, BLK, 0, s->stream>>>(c);
+        }
     }
     HIP_TRY(hipGetLastError());
     s->pay_cur ^= 1;
@@ -1406,7 +1424,7 @@ int exchange_rccl(psim_handle* h) {
 
 int phase_stats(psim_handle* h, Shard* s, const std::vector<uint32_t>& crashed) {
     KTimer t(h, s, KT_STATS);
-    k_stats_reduce<<<NST, BLK, 0, s->stream>>>(s->stat_part.p, s->pgrid + s->cgrid + s->rgrid, s->stat_out.p,
+    k_stats_reduce<<<NST, BLK, 0, s->stream>>>(s->stat_part.p, s->pgrid + s->cgrid + s->rgrid + s->tgrid, s->stat_out.p,
                                                 s->pin_dev);
     if (!crashed.empty()) {
         TRY(upload(s, s->ev_ids, crashed));
@@ -1548,6 +1566,7 @@ int shard_alloc(psim_handle* h, Shard* s) {
     rc |= s->long_list.alloc(n); rc |= s->bmask.alloc(n); rc |= s->btot.alloc(1); rc |= s->n_long.alloc(1);
     rc |= s->desc.alloc(n); rc |= s->d_nact.alloc(1);
     rc |= s->desc_slow.alloc(n); rc |= s->n_slow.alloc(1);
+    rc |= s->desc_pt.alloc(n); rc |= s->n_pt.alloc(1);
     if (h->cfg.manager == PSIM_MANAGER_PLUGGABLE) { rc |= s->stop_ids.alloc(n); rc |= s->n_stop.alloc(1); }
     rc |= s->stat_out.alloc(NST + 2);   // + the consume span
     rc |= s->ikeys.alloc(1024); rc |= s->ivals.alloc(1024);
@@ -1586,7 +1605,7 @@ void shard_free(Shard* s) {
     s->rank.release(); s->long_list.release(); s->bmask.release(); s->btot.release();
     s->hist.release(); s->hoff.release(); s->pairs.release(); s->n_long.release(); s->tmp.release();
     s->stop_ids.release(); s->n_stop.release();
-    s->desc.release(); s->d_nact.release(); s->desc_slow.release(); s->n_slow.release(); s->bound.release(); s->pscan.release();
+    s->desc.release(); s->d_nact.release(); s->desc_slow.release(); s->n_slow.release(); s->desc_pt.release(); s->n_pt.release(); s->bound.release(); s->pscan.release();
     s->obase.release(); s->stat_part.release(); s->stat_out.release(); s->d_off.release();
     s->cub_tmp.release(); s->ev_ids.release(); s->ev_contacts.release(); s->sendbuf.release();
     s->sview.release(); s->sinv.release(); s->fbits.release(); s->pay[0].release(); s->pay[1].release();
@@ -1670,11 +1689,10 @@ int psim_create(const psim_config* cfg, psim_handle** out) {
     if (dev < 0 && hipGetDevice(&dev) != hipSuccess) { delete h; return PSIM_EDEVICE; }
     if (hipSetDevice(dev) != hipSuccess) { delete h; return PSIM_EDEVICE; }
     h->consume_blocks = psim::consume_grid();
+    h->pt_blocks = psim::pt_grid();
     {
         const char* e = getenv("PSIM_PHASE_TIMERS");
         h->phase_timers = e && *e && *e != '0';
-        const char* r = getenv("PSIM_NO_RELAY");
-        h->relay = !(r && *r && *r != '0');
         const char* b = getenv("PSIM_ROUTE_BLOCKS");
         if (b && *b) h->rb_blocks = std::max<uint32_t>(1, std::min<uint32_t>(RB_MAX_BLOCKS, (uint32_t)atoi(b)));
     }
@@ -2167,7 +2185,7 @@ static std::vector<Section> snap_sections(psim_handle* h, Shard* s, const ShardH
         {s->pt_all.p, n * PSIM_PT_MEMBERS_CAP * 4}, {s->pt_com.p, n * PSIM_PT_MEMBERS_CAP * 4},
         {s->pt_eag.p, n * RT_SET * 4}, {s->pt_laz.p, n * RT_SET * 4}, {s->pt_rt.p, n * RT_WORDS * 4},
         {s->pt_out.p, n * PSIM_PT_OUT_CAP * 8}, {s->start.p, n * 4},
-        {s->cb.p, (n + 1) * 8}, {s->bmask.p, n * 4}, {s->in_beg.p, (n + 1) * 4},
+        {s->cb.p, (n + 1) * 8}, {s->bmask.p, n * 8}, {s->in_beg.p, (n + 1) * 4},
         {s->inbox[sh.in_cur].p, (size_t)sh.m_in * sizeof(Msg)},
     };
     if (h->cfg.manager == PSIM_MANAGER_PLUGGABLE) {

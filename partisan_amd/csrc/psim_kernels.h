@@ -36,7 +36,10 @@ struct RoundArgs {
     // per-block stats rows
     uint4* desc_slow;
     uint32_t* n_slow;
+    uint4* desc_pt;             // ... and the nodes with Plumtree work, for k_pt
+    uint32_t* n_pt;
     uint64_t* stat_relay;
+    uint64_t* stat_pt;          // k_pt's per-block stats rows
     const Msg* rec_in;          // dense, in inbox order (node runs at in_beg)
     const uint64_t* obase;
     Msg* rec_out;
@@ -69,9 +72,12 @@ __global__ void k_consume(RoundArgs args);
 constexpr uint32_t RELAY_MAX_BLOCKS = 8192;
 __global__ void k_relay(RoundArgs args);
 __global__ void k_consume_pl(RoundArgs args);
+// the Plumtree phase of the nodes k_relay listed (psim_consume.hip)
+__global__ void k_pt(RoundArgs args);
 // diagnostic builds (-DPSIM_STAMPS): per-phase cycle sums of k_consume, reset on read
 int debug_stamps(unsigned long long* out);
 // resident-block count of k_consume on the current device
 uint32_t consume_grid();
+uint32_t pt_grid();
 
 }  // namespace psim

@@ -5,7 +5,7 @@ TAG=${1:-q}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 200 --timeout-method thread \
-  -k "config_a or doubling or churn or star or variants or revert or crash or shard_count or multistep or histograms_delivery or 1m" > $OUT/tests.txt 2>&1
+  -k "config_a or doubling or churn or star or variants or revert or crash or shard_count or multistep or histograms_delivery or 1m or multi_root" > $OUT/tests.txt 2>&1
 rc=$?
 tail -2 $OUT/tests.txt
 [ $rc -eq 0 ] || exit $rc
