@@ -38,6 +38,7 @@ S_MSG = 64                      # message record bytes
 CHECK_NODES = 1 << 14           # the built-in sharding check
 CHECK_ROUNDS = 90
 SCHEDULE_VERSION = 2            # bumps when the event schedule of a run changes (PMC keys)
+OVF_KINDS = ("idmap", "pt_outstanding", "pt_sets_roots_msgs", "strategy")   # PSIM_OVF_*
 ALG_FORMULA = ("B = N_proc * 2 * 416 + M_in * 64 + M_out * 68 per round, N_proc = nodes with work "
                "(stats nodes_processed), M_in / M_out = delivered / emitted records.  Departs from "
                "SURVEY 8(d) (every node's 416 B read, touched nodes' written, 32-B Plumtree records): "
@@ -70,6 +71,19 @@ def parse():
                         "B: full-membership strategy, fanout 5; D: SCAMP v2 (c=5); "
                         "E: C with 20%% churn over 100 rounds + a half/half partition")
     return p.parse_args()
+
+
+def device_mem_used_gb():
+    """hipMemGetInfo of this process's device: used = total - free (GB)."""
+    import ctypes as C
+    try:
+        hip = C.CDLL("libamdhip64.so")
+        free, tot = C.c_size_t(), C.c_size_t()
+        if hip.hipMemGetInfo(C.byref(free), C.byref(tot)) != 0:
+            return None
+        return (tot.value - free.value) / 1e9
+    except OSError:
+        return None
 
 
 # ------------------------------------------------------------ launcher --
@@ -455,8 +469,15 @@ def main():
     if world > 1:
         cfg.shard_world, cfg.shard_rank = world, rank
     sim = Simulator(cfg, comm=comm)
+    ovf_run = np.zeros(4, np.uint64)          # overflows by table over every round of the run
+
+    def step(k):
+        s_ = sim.step(k)
+        ovf_run[:] += s_["overflow_by"].sum(axis=0).astype(np.uint64)
+        return s_
+
     boot = W.doubling_join(n, args.seed)
-    sim.run_schedule(boot, boot[-1][0] + 1 + args.settle)
+    ovf_run[:] += sim.run_schedule(boot, boot[-1][0] + 1 + args.settle)["overflow_by"].sum(axis=0).astype(np.uint64)
 
     # event index i counts rounds from the start of the broadcast phase:
     # STEADY_ROUNDS untimed broadcast rounds (whatever --warmup is), the
@@ -493,7 +514,7 @@ def main():
 
     for i in range(t_start):
         round_events(i)
-        sim.step(1)
+        step(1)
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
@@ -506,7 +527,7 @@ def main():
         k = 1
         while i + k < args.steps and not has_events(t_start + i + k):
             k += 1
-        stats.append(sim.step(k))
+        stats.append(step(k))
         i += k
         for name, (ms, cnt) in sim.kernel_times().items():
             a, b = kt.get(name, (0.0, 0))
@@ -558,8 +579,8 @@ def main():
                                    f"1 GPU, {args.vshards} virtual shards" if args.vshards > 1 else "1 GPU")},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": tsrc,
-                     "kernel": "k_relay + k_consume (the node-round phase: one launch of each per round, "
-                               "timed from k_relay's first block to k_consume's last)",
+                     "kernel": "k_relay + k_consume + k_pt (the node-round phase: one launch of each per round, "
+                               "timed from k_relay's first block to the last block of k_consume or k_pt)",
                      "alg_bytes_per_launch": per_launch_bytes,
                      "alg_bytes_formula": ALG_FORMULA,
                      "avg_launch_ms": per_launch_s * 1e3},
@@ -573,7 +594,7 @@ def main():
     # drain rounds without new broadcasts until the tracked (last) broadcast
     # has had at least its last hop + 5 rounds and OVERLAY_DRAIN rounds
     since = t_start + args.steps - state["last_bcast"]
-    sim.step(OVERLAY_DRAIN)
+    step(OVERLAY_DRAIN)
     drained = OVERLAY_DRAIN
     while True:
         ov = sim.histograms()
@@ -581,7 +602,7 @@ def main():
         last_hop = int(bins[ov["hop"] > 0].max()) if ov["delivered"] else 0
         if since + drained >= last_hop + 5 or drained >= 400:
             break
-        sim.step(10)
+        step(10)
         drained += 10
     nup = max(1, ov["n_up"])
     out["overlay"] = {
@@ -597,6 +618,15 @@ def main():
         "rounds_since_tracked_broadcast": since + drained,
         "rounds_drained": drained,
     }
+    # message conservation over the window: every record emitted in round
+    # r is delivered or dropped in round r + 1
+    em = st["emitted"].sum(axis=1)
+    got = st["delivered"].sum(axis=1) + st["dropped"]
+    out["conservation"] = {"rounds_checked": int(len(st) - 1),
+                           "ok": bool(np.array_equal(em[:-1], got[1:]))}
+    out["device_mem_used_gb"] = device_mem_used_gb()
+    out["overflow_run"] = {"rounds": sim.round, **{k: int(v) for k, v in zip(OVF_KINDS, ovf_run)},
+                           "total": int(ovf_run.sum())}
     if cpu is not None:
         out["cpu_baseline"] = cpu
     if rank == 0:

@@ -64,7 +64,7 @@
 extern "C" {
 #endif
 
-#define PSIM_ABI_VERSION 4
+#define PSIM_ABI_VERSION 5
 
 /* error codes */
 #define PSIM_OK 0
@@ -126,21 +126,29 @@ enum psim_pl_msg_type {
 /* capacities of the fixed-size per-node tables */
 #define PSIM_ACTIVE_CAP 8
 #define PSIM_PASSIVE_CAP 32
-#define PSIM_IDMAP_CAP 32   /* sent_message_map / recv_message_map slots */
+#define PSIM_IDMAP_CAP 64   /* sent_message_map / recv_message_map slots */
 #define PSIM_PT_MEMBERS_CAP 8
-#define PSIM_PT_SET_CAP 16
-#define PSIM_PT_OUT_CAP 32
+#define PSIM_PT_OUT_CAP 64
 #define PSIM_EXCHANGE_CAP 8
 /* Plumtree roots a node keeps per-root eager/lazy sets for at once
  * (eager_sets / lazy_sets orddicts, plumtree:76-84, :599-631): a root
  * touched with every slot taken counts an overflow and is served from the
- * common sets. */
+ * common sets.  The sets of all slots share one pool of PSIM_PT_SET_POOL
+ * eager and one of PSIM_PT_SET_POOL lazy entries (slot k's entries follow
+ * those of slots 0..k-1); an add to a full pool counts an overflow. */
 #define PSIM_PT_ROOTS 4
+#define PSIM_PT_SET_POOL 64
 /* Live broadcast messages: message id m owns slot m mod PSIM_MSG_SLOTS of
  * every node's delivery mask (plumtree_backend's ETS set, :140-167); a new
  * broadcast retires the previous id of its slot, and a message of a retired
  * id still in flight counts an overflow and is treated as stale. */
 #define PSIM_MSG_SLOTS 64
+/* psim_round_stats.overflow_by: which fixed table overflowed */
+#define PSIM_OVF_IDMAP 0     /* sent / recv disconnect-id maps (oldest entry replaced) */
+#define PSIM_OVF_PT_OUT 1    /* Plumtree outstanding IHAVE entries (the new entry dropped) */
+#define PSIM_OVF_PT 2        /* Plumtree members, per-root sets, root slots, retired message ids */
+#define PSIM_OVF_STRATEGY 3  /* pluggable: SCAMP views, full-membership snapshot payload */
+#define PSIM_OVF_NKINDS 4
 
 typedef struct psim_config {
     uint32_t abi_version;        /* must be PSIM_ABI_VERSION */
@@ -191,7 +199,7 @@ typedef struct psim_round_stats {
     uint64_t overflow;                       /* fixed-table overflows (must be 0 in parity runs) */
     uint64_t digest;                         /* sum of per-message hashes of emitted messages */
     uint64_t state_bytes;                    /* algorithmic state bytes read+written */
-    uint64_t reserved[4];
+    uint64_t overflow_by[PSIM_OVF_NKINDS];   /* overflow by table (PSIM_OVF_*), summing to overflow */
 } psim_round_stats;
 
 /* Canonical per-node view (inspection; unused slots zero). */
@@ -206,9 +214,11 @@ typedef struct psim_node_view {
     uint32_t recv_peer[PSIM_IDMAP_CAP], recv_id[PSIM_IDMAP_CAP];
     uint32_t pt_all_n, pt_common_n, pt_out_n, pt_pad;
     uint32_t pt_all[PSIM_PT_MEMBERS_CAP], pt_common[PSIM_PT_MEMBERS_CAP];
-    /* per-root sets, slot k: root pt_root[k] (PSIM_NONE = free) */
+    /* per-root sets, slot k: root pt_root[k] (PSIM_NONE = free); its eager
+     * entries are pt_eager[o .. o + pt_eager_n[k]) with o the sum of
+     * pt_eager_n[0..k) (ordsets order), the lazy ones likewise */
     uint32_t pt_root[PSIM_PT_ROOTS], pt_eager_n[PSIM_PT_ROOTS], pt_lazy_n[PSIM_PT_ROOTS];
-    uint32_t pt_eager[PSIM_PT_ROOTS][PSIM_PT_SET_CAP], pt_lazy[PSIM_PT_ROOTS][PSIM_PT_SET_CAP];
+    uint32_t pt_eager[PSIM_PT_SET_POOL], pt_lazy[PSIM_PT_SET_POOL];
     uint32_t pt_out_peer[PSIM_PT_OUT_CAP], pt_out_msg[PSIM_PT_OUT_CAP], pt_out_round[PSIM_PT_OUT_CAP];
     uint64_t have;                           /* delivered: bit (msg id mod PSIM_MSG_SLOTS) */
     uint32_t trk_round, trk_hop;

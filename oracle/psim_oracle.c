@@ -66,8 +66,9 @@ typedef struct node {
     uint32_t pt_common[PSIM_PT_MEMBERS_CAP], pt_common_n;
     /* eager_sets / lazy_sets (plumtree:76-84): one slot per root, PSIM_NONE = free */
     uint32_t rt_root[PSIM_PT_ROOTS];
-    uint32_t rt_eag[PSIM_PT_ROOTS][PSIM_PT_SET_CAP], rt_eag_n[PSIM_PT_ROOTS];
-    uint32_t rt_laz[PSIM_PT_ROOTS][PSIM_PT_SET_CAP], rt_laz_n[PSIM_PT_ROOTS];
+    /* the sets of all slots share a pool of PSIM_PT_SET_POOL entries each */
+    uint32_t rt_eag[PSIM_PT_ROOTS][PSIM_PT_SET_POOL], rt_eag_n[PSIM_PT_ROOTS];
+    uint32_t rt_laz[PSIM_PT_ROOTS][PSIM_PT_SET_POOL], rt_laz_n[PSIM_PT_ROOTS];
     uint32_t out_peer[PSIM_PT_OUT_CAP], out_msg[PSIM_PT_OUT_CAP], out_round[PSIM_PT_OUT_CAP], out_n;
     uint64_t have;                  /* plumtree_backend ETS: bit (msg id mod PSIM_MSG_SLOTS) */
     uint32_t trk_round, trk_hop;
@@ -135,6 +136,12 @@ typedef struct ctx {
     int gossip_due;                 /* full, fanout > 0: a coalesced gossip is owed this round */
     int stop;                       /* the manager stopped in this round (leave, App. A Q12) */
 } ctx;
+
+/* a fixed-table overflow of kind PSIM_OVF_* */
+static void ovf(ctx *c, int kind) {
+    c->h->st->overflow++;
+    c->h->st->overflow_by[kind]++;
+}
 
 static uint64_t draw58(ctx *c) {
     uint32_t o[4];
@@ -331,7 +338,7 @@ static void map_store(ctx *c, uint32_t *peer, uint32_t *id, uint32_t *n, uint32_
     int i = map_find(peer, *n, p);
     if (i >= 0) { id[i] = v; return; }
     if (*n < PSIM_IDMAP_CAP) { peer[*n] = p; id[*n] = v; (*n)++; return; }
-    c->h->st->overflow++;
+    ovf(c, PSIM_OVF_IDMAP);
     peer[*head] = p; id[*head] = v;
     *head = (*head + 1) % PSIM_IDMAP_CAP;
 }
@@ -449,7 +456,7 @@ static void pt_set_add(uint32_t *l, uint32_t *n, uint32_t cap, uint32_t e, ctx *
     uint32_t i = 0;
     while (i < *n && l[i] < e) i++;
     if (i < *n && l[i] == e) return;
-    if (*n >= cap) { c->h->st->overflow++; return; }
+    if (*n >= cap) { ovf(c, PSIM_OVF_PT); return; }
     for (uint32_t j = *n; j > i; j--) l[j] = l[j - 1];
     l[i] = e;
     (*n)++;
@@ -526,28 +533,51 @@ static void pt_get(ctx *c, uint32_t root, uint32_t *eg, uint32_t *ne, uint32_t *
         *ne = s->rt_eag_n[k]; memcpy(eg, s->rt_eag[k], sizeof s->rt_eag[k]);
         *nl = s->rt_laz_n[k]; memcpy(lz, s->rt_laz[k], sizeof s->rt_laz[k]);
     } else {
-        memset(eg, 0, PSIM_PT_SET_CAP * 4); memset(lz, 0, PSIM_PT_SET_CAP * 4);
+        memset(eg, 0, PSIM_PT_SET_POOL * 4); memset(lz, 0, PSIM_PT_SET_POOL * 4);
         *ne = s->pt_common_n;
         for (uint32_t i = 0; i < s->pt_common_n; i++) eg[i] = s->pt_common[i];
         *nl = 0;                                   /* common_lazys is always [] */
     }
 }
 
+/* entries of all slots of a pool */
+static uint32_t pool_n(const uint32_t *n) {
+    uint32_t t = 0;
+    for (int k = 0; k < PSIM_PT_ROOTS; k++) t += n[k];
+    return t;
+}
+
+/* ordsets:add_element into slot k of a pool: an add to a full pool is an
+ * overflow */
+static void pool_add(ctx *c, uint32_t (*set)[PSIM_PT_SET_POOL], uint32_t *n, int k, uint32_t e) {
+    for (uint32_t i = 0; i < n[k]; i++)
+        if (set[k][i] == e) return;
+    if (pool_n(n) >= PSIM_PT_SET_POOL) { ovf(c, PSIM_OVF_PT); return; }
+    pt_set_add(set[k], &n[k], PSIM_PT_SET_POOL, e, c);
+}
+
 /* update_peers/5 + set_peers/4 (plumtree:593-609): orddict:store(Root, ..)
- * into the root's slot, a new root into the lowest free slot; with every
- * slot taken the store is an overflow (the sets stay as they were) */
+ * into the root's slot; a new root takes the lowest free slot, its sets
+ * starting as (common_eagers, []) -- with every slot taken, or the eager pool
+ * too full for the common eagers, the store is an overflow (the sets stay
+ * as they were) */
 static void pt_update(ctx *c, uint32_t from, uint32_t root, int to_eager) {
     node *s = c->s;
-    uint32_t eg[PSIM_PT_SET_CAP], lz[PSIM_PT_SET_CAP], ne, nl;
-    pt_get(c, root, eg, &ne, lz, &nl);
-    if (to_eager) { pt_set_add(eg, &ne, PSIM_PT_SET_CAP, from, c); pt_set_del(lz, &nl, from); }
-    else { pt_set_del(eg, &ne, from); pt_set_add(lz, &nl, PSIM_PT_SET_CAP, from, c); }
     int k = rt_find(s, root);
-    if (k < 0) k = rt_find(s, PSIM_NONE);
-    if (k < 0) { c->h->st->overflow++; return; }
-    s->rt_root[k] = root;
-    memcpy(s->rt_eag[k], eg, sizeof eg); s->rt_eag_n[k] = ne;
-    memcpy(s->rt_laz[k], lz, sizeof lz); s->rt_laz_n[k] = nl;
+    if (k < 0) {
+        k = rt_find(s, PSIM_NONE);
+        if (k < 0 || pool_n(s->rt_eag_n) + s->pt_common_n > PSIM_PT_SET_POOL) { ovf(c, PSIM_OVF_PT); return; }
+        s->rt_root[k] = root;
+        memcpy(s->rt_eag[k], s->pt_common, s->pt_common_n * 4); s->rt_eag_n[k] = s->pt_common_n;
+        s->rt_laz_n[k] = 0;
+    }
+    if (to_eager) {
+        pool_add(c, s->rt_eag, s->rt_eag_n, k, from);
+        pt_set_del(s->rt_laz[k], &s->rt_laz_n[k], from);
+    } else {
+        pt_set_del(s->rt_eag[k], &s->rt_eag_n[k], from);
+        pool_add(c, s->rt_laz, s->rt_laz_n, k, from);
+    }
 }
 
 /* send/3 (plumtree:633-638) -> cast_message -> forward_message: succeeds only
@@ -578,7 +608,7 @@ static void pt_add_out(ctx *c, uint32_t peer, uint32_t msg, uint32_t rnd) {
         i++;
     if (i < s->out_n && s->out_peer[i] == peer && s->out_msg[i] == msg && s->out_round[i] == rnd)
         return;
-    if (s->out_n >= PSIM_PT_OUT_CAP) { c->h->st->overflow++; return; }
+    if (s->out_n >= PSIM_PT_OUT_CAP) { ovf(c, PSIM_OVF_PT_OUT); return; }
     for (uint32_t j = s->out_n; j > i; j--) {
         s->out_peer[j] = s->out_peer[j - 1]; s->out_msg[j] = s->out_msg[j - 1];
         s->out_round[j] = s->out_round[j - 1];
@@ -607,7 +637,7 @@ static void pt_ack_out(ctx *c, uint32_t peer, uint32_t msg, uint32_t rnd) {
  * and answers stale */
 static int pt_have(ctx *c, uint32_t msg) {
     uint32_t k = msg % PSIM_MSG_SLOTS;
-    if (c->h->slot_msg[k] != msg) { c->h->st->overflow++; return 1; }
+    if (c->h->slot_msg[k] != msg) { ovf(c, PSIM_OVF_PT); return 1; }
     return (int)((c->s->have >> k) & 1u);
 }
 
@@ -615,13 +645,13 @@ static int pt_have(ctx *c, uint32_t msg) {
  * id is an overflow and PSIM_NONE */
 static uint32_t msg_root(ctx *c, uint32_t msg) {
     uint32_t k = msg % PSIM_MSG_SLOTS;
-    if (c->h->slot_msg[k] != msg) { c->h->st->overflow++; return PSIM_NONE; }
+    if (c->h->slot_msg[k] != msg) { ovf(c, PSIM_OVF_PT); return PSIM_NONE; }
     return c->h->slot_root[k];
 }
 
 /* eager_push/7 + schedule_lazy_push/6 (plumtree:428-441) */
 static void pt_push(ctx *c, uint32_t msg, uint32_t rnd, uint32_t root, uint32_t from) {
-    uint32_t eg[PSIM_PT_SET_CAP], lz[PSIM_PT_SET_CAP], ne, nl;
+    uint32_t eg[PSIM_PT_SET_POOL], lz[PSIM_PT_SET_POOL], ne, nl;
     pt_get(c, root, eg, &ne, lz, &nl);
     pt_set_del(eg, &ne, from);                    /* all_filtered_peers/4 */
     for (uint32_t i = 0; i < ne; i++) pt_send(c, eg[i], PSIM_MSG_PT_BROADCAST, msg, rnd, root);
@@ -1023,7 +1053,7 @@ static uint32_t random_0_or_1(ctx *c) { return uniform_n(c, 10) >= 5 ? 1u : 0u; 
 /* sets:add_element/2 (v1) or [Node | List] (v2) into a fixed table */
 static void scamp_add(ctx *c, uint32_t *l, uint32_t *n, uint32_t e, int as_set) {
     if (as_set && list_member(l, *n, e)) return;
-    if (*n >= PSIM_SVIEW_CAP) { c->h->st->overflow++; return; }
+    if (*n >= PSIM_SVIEW_CAP) { ovf(c, PSIM_OVF_STRATEGY); return; }
     if (as_set) { set_add(l, n, e); return; }
     for (uint32_t i = *n; i > 0; i--) l[i] = l[i - 1];
     l[0] = e;
@@ -1560,7 +1590,10 @@ int orc_get_nodes(struct psim_handle *h, uint32_t first, uint32_t count, psim_no
         for (int q = 0; q < PSIM_PT_ROOTS; q++) {
             v->pt_root[q] = s->rt_root[q]; v->pt_eager_n[q] = s->rt_eag_n[q]; v->pt_lazy_n[q] = s->rt_laz_n[q];
         }
-        memcpy(v->pt_eager, s->rt_eag, sizeof v->pt_eager); memcpy(v->pt_lazy, s->rt_laz, sizeof v->pt_lazy);
+        for (int q = 0, oe = 0, ol = 0; q < PSIM_PT_ROOTS; q++) {      /* pooled: slot by slot */
+            memcpy(v->pt_eager + oe, s->rt_eag[q], s->rt_eag_n[q] * 4); oe += (int)s->rt_eag_n[q];
+            memcpy(v->pt_lazy + ol, s->rt_laz[q], s->rt_laz_n[q] * 4); ol += (int)s->rt_laz_n[q];
+        }
         memcpy(v->pt_out_peer, s->out_peer, sizeof v->pt_out_peer);
         memcpy(v->pt_out_msg, s->out_msg, sizeof v->pt_out_msg);
         memcpy(v->pt_out_round, s->out_round, sizeof v->pt_out_round);

@@ -8,11 +8,11 @@ import ctypes as C
 
 import numpy as np
 
-PSIM_ABI_VERSION = 4
+PSIM_ABI_VERSION = 5
 PSIM_MAP_BIT = 0x80000000
 PSIM_NONE = 0xFFFFFFFF
-ACTIVE_CAP, PASSIVE_CAP, IDMAP_CAP = 8, 32, 32
-PT_MEMBERS_CAP, PT_SET_CAP, PT_OUT_CAP, EXCHANGE_CAP = 8, 16, 32, 8
+ACTIVE_CAP, PASSIVE_CAP, IDMAP_CAP = 8, 32, 64
+PT_MEMBERS_CAP, PT_SET_POOL, PT_OUT_CAP, EXCHANGE_CAP = 8, 64, 64, 8
 PT_ROOTS, MSG_SLOTS = 4, 64
 NTYPES = 16
 SVIEW_CAP = 64
@@ -57,7 +57,7 @@ class PsimRoundStats(C.Structure):
         ("delivered", C.c_uint64 * NTYPES), ("dropped", C.c_uint64),
         ("nodes_up", C.c_uint64), ("nodes_processed", C.c_uint64), ("exits", C.c_uint64),
         ("send_fail", C.c_uint64), ("first_deliveries", C.c_uint64), ("overflow", C.c_uint64),
-        ("digest", C.c_uint64), ("state_bytes", C.c_uint64), ("reserved", C.c_uint64 * 4),
+        ("digest", C.c_uint64), ("state_bytes", C.c_uint64), ("overflow_by", C.c_uint64 * 4),
     ]
 
 
@@ -76,7 +76,7 @@ class PsimNodeView(C.Structure):
         ("pt_all", C.c_uint32 * PT_MEMBERS_CAP), ("pt_common", C.c_uint32 * PT_MEMBERS_CAP),
         ("pt_root", C.c_uint32 * PT_ROOTS), ("pt_eager_n", C.c_uint32 * PT_ROOTS),
         ("pt_lazy_n", C.c_uint32 * PT_ROOTS),
-        ("pt_eager", (C.c_uint32 * PT_SET_CAP) * PT_ROOTS), ("pt_lazy", (C.c_uint32 * PT_SET_CAP) * PT_ROOTS),
+        ("pt_eager", C.c_uint32 * PT_SET_POOL), ("pt_lazy", C.c_uint32 * PT_SET_POOL),
         ("pt_out_peer", C.c_uint32 * PT_OUT_CAP), ("pt_out_msg", C.c_uint32 * PT_OUT_CAP),
         ("pt_out_round", C.c_uint32 * PT_OUT_CAP),
         ("have", C.c_uint64), ("trk_round", C.c_uint32), ("trk_hop", C.c_uint32),

@@ -67,6 +67,7 @@ struct Wv {
     uint32_t start_round, contact, epoch;
     uint32_t have, aux, trk_round, trk_hop;
     uint32_t vd;                      // views changed this round: 1 active, 2 passive
+    uint32_t sx, rx, ox;              // id-map / outstanding extension rows + 1 (0: none)
     uint32_t act_n, pas_n, sent_n, sent_head, recv_n, recv_head;
     uint32_t all_n, com_n, out_n;
     uint32_t A, P, SP, SI, RP, RI, COM, EAG, LAZ;
@@ -101,6 +102,11 @@ constexpr uint32_t RTB = PSIM_PT_MEMBERS_CAP;   // first lane of the root row in
 
 // stats: lane k of SC holds slot k's count for this wave; flushed once per wave
 DEV void st_add(Wv& w, int k, uint32_t v) { w.SC += lane_id() == (uint32_t)k ? v : 0u; }
+// a fixed-table overflow of kind PSIM_OVF_*
+DEV void ovf(Wv& w, int kind) {
+    const uint32_t l = lane_id();
+    w.SC += (l == (uint32_t)ST_OVF || l == (uint32_t)(ST_OVF_BY + kind)) ? 1u : 0u;
+}
 // this wave's counters and digest partials into the block's LDS stats
 DEV void flush_wave_stats(const Wv& w, uint64_t* sst) {
     const uint32_t l = lane_id();
@@ -325,7 +331,25 @@ DEV void hv_send(Wv& w, uint32_t dst, uint32_t type, uint32_t ttl, uint32_t a0, 
 }
 
 // ----------------------------------------------------------- id maps --
-DEV void load_maps(Wv& w) {}      // loaded with the node (NodeX)
+// The id maps, loaded on first use (most nodes of a round never touch
+// them): lanes below IDMAP_IN hold the node's own entries, lanes above its
+// extension row's -- one load per array either way.
+DEV void load_maps(Wv& w) {
+    if (w.maps) return;
+    static_assert(PSIM_IDMAP_CAP == 64, "an id map is one entry per lane");
+    const RoundArgs& a = *w.a;
+    const uint32_t l = lane_id(), sx = w.sx, rx = w.rx;
+    const bool own = l < IDMAP_IN;
+    const size_t io = w.li * IDMAP_IN + (l & (IDMAP_IN - 1));
+    const size_t so = sx ? (size_t)(sx - 1) * IDMAP_EXT + ((l - IDMAP_IN) & 63) : 0;
+    const size_t ro = rx ? (size_t)(rx - 1) * IDMAP_EXT + ((l - IDMAP_IN) & 63) : 0;
+    const uint64_t sv = *(own || !sx ? a.sentm + io : a.mapx + so);
+    const uint64_t rv = *(own || !rx ? a.recvm + io : a.mapx + ro);
+    const uint64_t s2 = own || sx ? sv : 0ull, r2 = own || rx ? rv : 0ull;
+    w.SP = (uint32_t)s2; w.SI = (uint32_t)(s2 >> 32);
+    w.RP = (uint32_t)r2; w.RI = (uint32_t)(r2 >> 32);
+    w.maps = true;
+}
 
 DEV void map_store(Wv& w, uint32_t& PV, uint32_t& IV, uint32_t& n, uint32_t& head, uint32_t p,
                    uint32_t v) {
@@ -337,18 +361,16 @@ DEV void map_store(Wv& w, uint32_t& PV, uint32_t& IV, uint32_t& n, uint32_t& hea
         PV = l == n ? p : PV; IV = l == n ? v : IV; n++;
         return;
     }
-    st_add(w, ST_OVF, 1);
+    ovf(w, PSIM_OVF_IDMAP);
     PV = l == head ? p : PV; IV = l == head ? v : IV;
     head = (head + 1) % PSIM_IDMAP_CAP;
 }
 
 DEV uint32_t current_id(Wv& w, uint32_t p) {             // hv:1622-1630
-    load_maps(w);
     int i = idx_of(w.RP, w.recv_n, p);
     return i >= 0 ? rl(w.RI, i) : ID_OF(1, 0);
 }
 DEV uint32_t next_id(Wv& w, uint32_t p) {                // hv:1633-1639
-    load_maps(w);
     int i = idx_of(w.SP, w.sent_n, p);
     if (i >= 0) {
         uint32_t s = rl(w.SI, i);
@@ -357,12 +379,10 @@ DEV uint32_t next_id(Wv& w, uint32_t p) {                // hv:1633-1639
     return ID_OF(hw_epoch(w), 1);
 }
 DEV bool addable_epoch(Wv& w, uint32_t pe, uint32_t p) { // hv:1670-1676
-    load_maps(w);
     int i = idx_of(w.SP, w.sent_n, p);
     return i < 0 || pe >= ID_E(rl(w.SI, i));
 }
 DEV bool addable_id(Wv& w, uint32_t d, uint32_t p) {     // hv:1656-1669
-    load_maps(w);
     int i = idx_of(w.SP, w.sent_n, p);
     if (i < 0) return true;
     uint32_t s = rl(w.SI, i);
@@ -370,7 +390,6 @@ DEV bool addable_id(Wv& w, uint32_t d, uint32_t p) {     // hv:1656-1669
     return ID_C(d) >= ID_C(s);
 }
 DEV bool valid_disconnect(Wv& w, uint32_t p, uint32_t d) { // hv:1642-1653
-    load_maps(w);
     int i = idx_of(w.RP, w.recv_n, p);
     if (i < 0) return true;
     uint32_t s = rl(w.RI, i);
@@ -478,13 +497,18 @@ DEV void move_to_active(Wv& w, uint32_t p) {             // hv:1679-1709
 DEV void ord_add(Wv& w, uint32_t& V, uint32_t& n, uint32_t cap, uint32_t e) {
     uint32_t l = lane_id();
     if (ballot(l < n && V == e)) return;
-    if (n >= cap) { st_add(w, ST_OVF, 1); return; }
+    if (n >= cap) { ovf(w, PSIM_OVF_PT); return; }
     vins(V, n, popc(ballot(l < n && V < e)), e);
 }
 
-// per-root slot k of the 64-entry eager / lazy registers: entries in lanes
-// 16k .. 16k + 15, the count in byte k of RT lane RT_EN / RT_LN
-DEV uint32_t rt_count(const Wv& w, uint32_t which, uint32_t k) { return (rl(w.AR, RTB + which) >> (8 * k)) & 0xFFu; }
+// Per-root sets, pooled: the eager (lazy) entries of every slot in one
+// 64-lane register -- slot 0's entries first, then slot 1's, ... -- with slot
+// k's count in byte k of RT lane RT_EN (RT_LN), so its entries start at the
+// sum of the counts below k.  Only the total over the slots is bounded.
+DEV uint32_t rt_word(const Wv& w, uint32_t which) { return rl(w.AR, RTB + which); }
+DEV uint32_t byte_sum(uint32_t c) { return (c * 0x01010101u) >> 24; }   // counts <= 64: no carry
+DEV uint32_t rt_off(uint32_t cw, uint32_t k) { return k ? byte_sum(cw & (0xFFFFFFFFu >> (32 - 8 * k))) : 0u; }
+DEV uint32_t rt_count(const Wv& w, uint32_t which, uint32_t k) { return (rt_word(w, which) >> (8 * k)) & 0xFFu; }
 DEV void rt_set_count(Wv& w, uint32_t which, uint32_t k, uint32_t n) {
     const uint32_t l = lane_id();
     w.AR = l == RTB + which ? ((w.AR & ~(0xFFu << (8 * k))) | (n << (8 * k))) : w.AR;
@@ -497,26 +521,26 @@ DEV int rt_find(const Wv& w, uint32_t root) {
     return at < 0 ? -1 : at - (int)RTB;
 }
 
-// ordsets add_element / del_element within slot k (n = its count)
-DEV void slot_add(Wv& w, uint32_t& V, uint32_t k, uint32_t& n, uint32_t e) {
-    const uint32_t l = lane_id(), b = k * PSIM_PT_SET_CAP;
-    const bool in = l >= b && l < b + PSIM_PT_SET_CAP;
-    const uint32_t j = l - b;
-    if (ballot(in && j < n && V == e)) return;
-    if (n >= PSIM_PT_SET_CAP) { st_add(w, ST_OVF, 1); return; }
-    const uint32_t pos = popc(ballot(in && j < n && V < e));
-    const uint32_t pv = from_prev(V);
-    V = (!in || j < pos) ? V : (j == pos ? e : (j <= n ? pv : 0u));
-    n++;
+// ordsets add_element / del_element within slot k of the pool V (which =
+// RT_EN for the eager pool, RT_LN for the lazy one)
+DEV void slot_add(Wv& w, uint32_t& V, uint32_t which, uint32_t k, uint32_t e) {
+    const uint32_t l = lane_id(), cw = rt_word(w, which);
+    const uint32_t n = (cw >> (8 * k)) & 0xFFu, b = rt_off(cw, k);
+    const bool in = l >= b && l < b + n;
+    if (ballot(in && V == e)) return;
+    uint32_t T = byte_sum(cw);
+    if (T >= PSIM_PT_SET_POOL) { ovf(w, PSIM_OVF_PT); return; }
+    vins(V, T, b + popc(ballot(in && V < e)), e);
+    rt_set_count(w, which, k, n + 1);
 }
-DEV void slot_del(uint32_t& V, uint32_t k, uint32_t& n, uint32_t e) {
-    const uint32_t l = lane_id(), b = k * PSIM_PT_SET_CAP;
-    const bool in = l >= b && l < b + PSIM_PT_SET_CAP;
-    const int at = ffs64(ballot(in && l - b < n && V == e));
+DEV void slot_del(Wv& w, uint32_t& V, uint32_t which, uint32_t k, uint32_t e) {
+    const uint32_t l = lane_id(), cw = rt_word(w, which);
+    const uint32_t n = (cw >> (8 * k)) & 0xFFu, b = rt_off(cw, k);
+    const int at = ffs64(ballot(l >= b && l < b + n && V == e));
     if (at < 0) return;
-    const uint32_t nx = from_next(V);
-    V = (!in || l < (uint32_t)at) ? V : (l - b + 1 < n ? nx : 0u);
-    n--;
+    uint32_t T = byte_sum(cw);
+    vdel(V, T, (uint32_t)at);
+    rt_set_count(w, which, k, n - 1);
 }
 
 // notify/1 (hv:1598-1599) -> plumtree update/1 -> handle_cast({update, ..})
@@ -541,7 +565,7 @@ DEV void apply_notify(Wv& w, uint32_t SNAP, uint32_t sn) {
             if (w.com_n >= PSIM_PT_MEMBERS_CAP) {
                 bool made = false;
                 for (uint32_t r = 0; r < nr && !made; r++) made = vdel_val(w.COM, w.com_n, rl(REM, r));
-                if (!made) { st_add(w, ST_OVF, 1); continue; }
+                if (!made) { ovf(w, PSIM_OVF_PT); continue; }
             }
             ord_add(w, w.COM, w.com_n, PSIM_PT_MEMBERS_CAP, e);
         }
@@ -555,11 +579,8 @@ DEV void apply_notify(Wv& w, uint32_t SNAP, uint32_t sn) {
         vdel_val(w.COM, w.com_n, e);
         for (uint32_t k = 0; k < PSIM_PT_ROOTS; k++) {   // every root's sets (pt:410-413)
             if (rt_root(w, k) == NONE) continue;
-            uint32_t ne = rt_count(w, RT_EN, k), nl = rt_count(w, RT_LN, k);
-            slot_del(w.EAG, k, ne, e);
-            slot_del(w.LAZ, k, nl, e);
-            rt_set_count(w, RT_EN, k, ne);
-            rt_set_count(w, RT_LN, k, nl);
+            slot_del(w, w.EAG, RT_EN, k, e);
+            slot_del(w, w.LAZ, RT_LN, k, e);
         }
         uint64_t keep = ballot(l < w.out_n && (uint32_t)(w.OUT >> 32) != e);
         if (popc(keep) != w.out_n) {
@@ -606,33 +627,30 @@ DEV void notify(Wv& w) {
 }
 
 // update_peers/5 + set_peers/4 (pt:593-609): the root's slot; a new root
-// takes the lowest free slot, its sets starting as (common_eagers, []); with
-// every slot taken the store is an overflow
+// takes the lowest free slot, its sets starting as (common_eagers, []) at its
+// place in the pools; with every slot taken, or no room in the eager pool
+// for the common eagers, the store is an overflow
 DEV void pt_update(Wv& w, uint32_t from, uint32_t root, bool to_eager) {
     w.pt_dirty = true;
     int k = rt_find(w, root);
     if (k < 0) {
         k = rt_find(w, NONE);
-        if (k < 0) { st_add(w, ST_OVF, 1); return; }
-        const uint32_t l = lane_id(), b = (uint32_t)k * PSIM_PT_SET_CAP;
-        const uint32_t c = shfl(w.COM, (int)((l - b) & 63));   // first touch: (common_eagers, [])
-        const bool in = l >= b && l < b + PSIM_PT_SET_CAP;
-        w.EAG = in ? (l - b < w.com_n ? c : 0u) : w.EAG;
-        w.LAZ = in ? 0u : w.LAZ;
+        const uint32_t cw = rt_word(w, RT_EN), m = w.com_n;
+        if (k < 0 || byte_sum(cw) + m > PSIM_PT_SET_POOL) { ovf(w, PSIM_OVF_PT); return; }
+        const uint32_t l = lane_id(), b = rt_off(cw, (uint32_t)k);
+        const uint32_t c = shfl(w.COM, (int)((l - b) & 63)), up = shfl(w.EAG, (int)((l - m) & 63));
+        w.EAG = l < b ? w.EAG : (l < b + m ? c : up);
         w.AR = l == RTB + (uint32_t)k ? root : w.AR;
-        rt_set_count(w, RT_EN, k, w.com_n);
+        rt_set_count(w, RT_EN, k, m);
         rt_set_count(w, RT_LN, k, 0);
     }
-    uint32_t ne = rt_count(w, RT_EN, k), nl = rt_count(w, RT_LN, k);
     if (to_eager) {
-        slot_add(w, w.EAG, k, ne, from);
-        slot_del(w.LAZ, k, nl, from);
+        slot_add(w, w.EAG, RT_EN, k, from);
+        slot_del(w, w.LAZ, RT_LN, k, from);
     } else {
-        slot_del(w.EAG, k, ne, from);
-        slot_add(w, w.LAZ, k, nl, from);
+        slot_del(w, w.EAG, RT_EN, k, from);
+        slot_add(w, w.LAZ, RT_LN, k, from);
     }
-    rt_set_count(w, RT_EN, k, ne);
-    rt_set_count(w, RT_LN, k, nl);
 }
 
 // send/3 (pt:633-638): only over an existing connection of the manager
@@ -653,7 +671,7 @@ DEV void pt_add_out(Wv& w, uint32_t peer, uint32_t msg, uint32_t rnd) {   // pt:
     uint64_t key = ((uint64_t)peer << 32) | (msg << 16) | (rnd & 0xFFFFu);
     w.pt_dirty = true;
     if (ballot(l < w.out_n && w.OUT == key)) return;
-    if (w.out_n >= PSIM_PT_OUT_CAP) { st_add(w, ST_OVF, 1); return; }
+    if (w.out_n >= PSIM_PT_OUT_CAP) { ovf(w, PSIM_OVF_PT_OUT); return; }
     vins64(w.OUT, w.out_n, popc(ballot(l < w.out_n && w.OUT < key)), key);
 }
 
@@ -668,14 +686,15 @@ DEV void pt_ack_out(Wv& w, uint32_t peer, uint32_t msg, uint32_t rnd) {   // pt:
 DEV void pt_push(Wv& w, uint32_t msg, uint32_t rnd, uint32_t root, uint32_t from) {
     const int k = rt_find(w, root);
     if (k >= 0) {
-        const uint32_t b = (uint32_t)k * PSIM_PT_SET_CAP;
-        const uint32_t ne = rt_count(w, RT_EN, k), nl = rt_count(w, RT_LN, k);
+        const uint32_t ce = rt_word(w, RT_EN), cl = rt_word(w, RT_LN);
+        const uint32_t be = rt_off(ce, (uint32_t)k), bl = rt_off(cl, (uint32_t)k);
+        const uint32_t ne = (ce >> (8 * k)) & 0xFFu, nl = (cl >> (8 * k)) & 0xFFu;
         for (uint32_t i = 0; i < ne; i++) {
-            uint32_t e = rl(w.EAG, b + i);
+            uint32_t e = rl(w.EAG, be + i);
             if (e != from) pt_send(w, e, PSIM_MSG_PT_BROADCAST, msg, rnd, root);
         }
         for (uint32_t i = 0; i < nl; i++) {
-            uint32_t e = rl(w.LAZ, b + i);
+            uint32_t e = rl(w.LAZ, bl + i);
             if (e != from) pt_add_out(w, e, msg, rnd);
         }
     } else {
@@ -691,7 +710,7 @@ DEV void pt_push(Wv& w, uint32_t msg, uint32_t rnd, uint32_t root, uint32_t from
 // answers stale
 DEV bool pt_have(Wv& w, uint32_t msg) {
     const uint32_t k = msg % PSIM_MSG_SLOTS;
-    if (w.slots[k] != msg) { st_add(w, ST_OVF, 1); return true; }
+    if (w.slots[k] != msg) { ovf(w, PSIM_OVF_PT); return true; }
     return ((k < 32 ? w.have >> k : w.aux >> (k - 32)) & 1u) != 0;
 }
 DEV void pt_mark(Wv& w, uint32_t msg) {
@@ -702,7 +721,7 @@ DEV void pt_mark(Wv& w, uint32_t msg) {
 // retired id counts an overflow and is PSIM_NONE
 DEV uint32_t msg_root(Wv& w, uint32_t msg) {
     const uint32_t k = msg % PSIM_MSG_SLOTS;
-    if (w.slots[k] != msg) { st_add(w, ST_OVF, 1); return NONE; }
+    if (w.slots[k] != msg) { ovf(w, PSIM_OVF_PT); return NONE; }
     return w.slots[PSIM_MSG_SLOTS + k];
 }
 
@@ -879,18 +898,19 @@ DEV uint32_t inbox_chunk(const Wv& w, const RoundArgs& a, uint32_t ib, uint32_t 
 //   NodeIn (rows, from the work descriptor): header, active and passive
 //          views, the first inbox chunk, the node's flag and partition bytes;
 //   NodeX  (needs the rows): flag/partition bytes of every view member (the
-//          connection cache) and the disconnect-id maps.
+//          connection cache).
+// The disconnect-id maps are loaded on first use (load_maps).
 // The Plumtree rows are not staged: the Plumtree phase runs in k_pt; this
 // kernel reads them only to replay notifies (load_pt_rows).
 struct NodeIn {
     uint32_t n, ib, ik, ob, tf;    // tf: due timers (DESC_* bits, k_desc)
+    bool maps;                     // DESC_MAPS_BIT (k_relay)
     uint32_t H;                    // header word l & 15
     uint32_t A, P, R0;
     uint32_t fl, part;
 };
 struct NodeX {
     uint32_t CV, CF;               // view ids (passive 0-31, active 32-39), their flags | part << 8
-    uint32_t MS, MR;               // sent / recv maps: peers in lanes 0-31, ids in 32-63
 };
 
 DEV uint32_t load_desc(const RoundArgs& a, uint32_t k) {
@@ -902,6 +922,7 @@ DEV NodeIn load_node(const RoundArgs& a, uint32_t D) {
     uint32_t l = lane_id();
     NodeIn x;
     x.n = rl(D, 0); x.ib = rl(D, 1); x.ik = rl(D, 2) & DESC_CNT_MASK; x.tf = rl(D, 2) >> 28; x.ob = rl(D, 3);
+    x.maps = (rl(D, 2) & DESC_MAPS_BIT) != 0;
     const size_t li = x.n - a.lo;
     x.H = reinterpret_cast<const uint32_t*>(a.hdr + li)[l & 15];
     x.A = a.act[li * PSIM_ACTIVE_CAP + (l & 7)];
@@ -923,30 +944,35 @@ DEV uint32_t cache_flags(const RoundArgs& a, uint32_t cv, uint32_t me) {
 DEV NodeX load_x(const RoundArgs& a, const NodeIn& x) {
     uint32_t l = lane_id();
     NodeX y;
-    const size_t li = x.n - a.lo;
     const uint32_t hw9 = rl(x.H, 9);                 // act_n, pas_n, .. (Hdr word 9)
     const uint32_t act_n = hw9 & 0xFF, pas_n = (hw9 >> 8) & 0xFF;
     uint32_t av = shfl(x.A, (int)(l & 7));
     uint32_t cv = l < 32 ? (l < pas_n ? x.P : NONE) : (l < 40 && l - 32 < act_n ? av : NONE);
     y.CV = cv;
     y.CF = cache_flags(a, cv, x.n);
-    const uint32_t l31 = l & 31;
-    y.MS = (l < 32 ? a.sentp : a.senti)[li * PSIM_IDMAP_CAP + l31];
-    y.MR = (l < 32 ? a.recvp : a.recvi)[li * PSIM_IDMAP_CAP + l31];
     return y;
 }
 
 // the Plumtree rows of the running node (all_members | common_eagers | root
 // row, per-root eager and lazy sets, outstanding) into the wave's registers
-DEV void load_pt_regs(Wv& w, uint32_t PA, uint32_t PG, uint32_t PL, uint32_t PO) {
+DEV void load_pt_regs(Wv& w, uint32_t PA, uint32_t PG, uint32_t PL, uint64_t PO) {
     const uint32_t l = lane_id();
     const uint32_t c8 = shfl(PA, (int)((l + 8) & 63));   // lanes 0-7: com (8-15); lanes 8-15: the root row (16-23)
     w.AR = l < RTB ? PA : (l < RTB + RT_WORDS ? c8 : 0u);
     w.COM = l < PSIM_PT_MEMBERS_CAP ? c8 : 0u;
     w.EAG = PG; w.LAZ = PL;
-    uint32_t olo = shfl(PO, (int)((2 * l) & 63)), ohi = shfl(PO, (int)((2 * l + 1) & 63));
-    w.OUT = l < PSIM_PT_OUT_CAP ? (((uint64_t)ohi << 32) | olo) : 0ull;
+    w.OUT = PO;
     w.pt = true;
+}
+// outstanding entry l of the node (its row, then its extension row: one
+// 8-B load per lane either way)
+DEV uint64_t load_po(const RoundArgs& a, size_t li, uint32_t ox) {
+    const uint32_t l = lane_id();
+    const bool own = l < OUT_IN;
+    const uint64_t* p = own || !ox ? a.pt_out + li * OUT_IN + (l & (OUT_IN - 1))
+                                   : a.outx + (size_t)(ox - 1) * OUT_EXT + (l - OUT_IN);
+    const uint64_t v = *p;
+    return own || ox ? v : 0ull;
 }
 // lanes 0-7 pt_all, 8-15 pt_com, 16-23 the root row (and again above 24)
 DEV uint32_t load_pa(const RoundArgs& a, size_t li) {
@@ -958,8 +984,7 @@ DEV void load_pt_rows(Wv& w) {
     const RoundArgs& a = *w.a;
     const uint32_t l = lane_id();
     const size_t li = w.li;
-    load_pt_regs(w, load_pa(a, li), a.pt_eag[li * RT_SET + l], a.pt_laz[li * RT_SET + l],
-                 reinterpret_cast<const uint32_t*>(a.pt_out + li * PSIM_PT_OUT_CAP)[l]);
+    load_pt_regs(w, load_pa(a, li), a.pt_eag[li * RT_SET + l], a.pt_laz[li * RT_SET + l], load_po(a, li, w.ox));
 }
 
 // the header words of the node into the wave's scalars
@@ -971,6 +996,7 @@ DEV void begin_header(Wv& w, uint32_t H) {
     w.act_n = w9 & 0xFF; w.pas_n = (w9 >> 8) & 0xFF; w.sent_n = (w9 >> 16) & 0xFF; w.sent_head = w9 >> 24;
     w.recv_n = w10 & 0xFF; w.recv_head = (w10 >> 8) & 0xFF; w.all_n = (w10 >> 16) & 0xFF; w.com_n = w10 >> 24;
     w.out_n = (w11 >> 16) & 0xFF;
+    w.sx = rl(H, HW_SENT_EXT); w.rx = rl(H, HW_RECV_EXT); w.ox = rl(H, HW_OUT_EXT);
 }
 
 // node state and the per-node scratch of the wave, from the staged inputs
@@ -986,10 +1012,7 @@ DEV void begin_node(Wv& w, const NodeIn& x, const NodeX& y) {
     w.obase = x.ob;
     w.mypart = x.part;
     w.CV = y.CV; w.CF = y.CF;
-    uint32_t msi = shfl(y.MS, (int)((l + 32) & 63)), mri = shfl(y.MR, (int)((l + 32) & 63));
-    w.SP = l < 32 ? y.MS : 0u; w.SI = l < 32 ? msi : 0u;
-    w.RP = l < 32 ? y.MR : 0u; w.RI = l < 32 ? mri : 0u;
-    w.maps = true; w.pt = false; w.maps_dirty = false; w.pt_dirty = false;
+    w.maps = false; w.pt = false; w.maps_dirty = false; w.pt_dirty = false;
     w.seq = 0; w.flushed = 0;
     w.nlog_n = 0;
     w.dc_base = NONE64;                                // the cache holds another node's stream
@@ -1025,6 +1048,7 @@ DEV void body_hv(Wv& w, const NodeIn& x) {
     if (!(ik || joining || exits || promo_work || shuf || origin || lazy)) { STAMP(w, 0); return; }
     w.work = true;
     st_add(w, ST_PROC, 1);
+    if (x.maps) load_maps(w);                         // (k_relay: a handler here may use them)
     STAMP(w, 1);
 
     if (joining)                                      // hv:500-515
@@ -1092,6 +1116,9 @@ DEV uint32_t header_word(const Wv& w, uint32_t k) {
     v = k == 9 ? (w.act_n | (w.pas_n << 8) | (w.sent_n << 16) | (w.sent_head << 24)) : v;
     v = k == 10 ? (w.recv_n | (w.recv_head << 8) | (w.all_n << 16) | (w.com_n << 24)) : v;
     v = k == 11 ? (w.out_n << 16) : v;
+    v = k == HW_SENT_EXT ? w.sx : v;
+    v = k == HW_RECV_EXT ? w.rx : v;
+    v = k == HW_OUT_EXT ? w.ox : v;
     return v;
 }
 
@@ -1102,14 +1129,33 @@ DEV void store_pt_rows(Wv& w) {
     const uint32_t l = lane_id();
     const size_t li = w.li;
     uint32_t all = shfl(w.AR, (int)(l & 7)), com = shfl(w.COM, (int)(l & 7)), rt = shfl(w.AR, (int)(RTB + (l & 7)));
-    uint64_t o = shfl64(w.OUT, (int)(l >> 1));
     const uint32_t l31 = l & 31;
     uint32_t* p1 = (l31 < 8 ? a.pt_all + li * PSIM_PT_MEMBERS_CAP
                             : l31 < 16 ? a.pt_com + li * PSIM_PT_MEMBERS_CAP : a.pt_rt + li * RT_WORDS) + (l & 7);
     *p1 = l31 < 8 ? all : l31 < 16 ? com : rt;
     a.pt_eag[li * RT_SET + l] = w.EAG;
     a.pt_laz[li * RT_SET + l] = w.LAZ;
-    reinterpret_cast<uint32_t*>(a.pt_out + li * PSIM_PT_OUT_CAP)[l] = (l & 1) ? (uint32_t)(o >> 32) : (uint32_t)o;
+    // outstanding: own entries, the extension row (lanes without one
+    // rewrite the header's draw counter)
+    const bool own = l < OUT_IN;
+    uint64_t* po = own ? a.pt_out + li * OUT_IN + l
+                       : w.ox ? a.outx + (size_t)(w.ox - 1) * OUT_EXT + (l - OUT_IN)
+                              : reinterpret_cast<uint64_t*>(a.hdr + li);
+    *po = own || w.ox ? w.OUT : w.rng;
+}
+
+// an extension row (+ 1) of a pool; 0 with the pool exhausted (an overflow
+// of `kind`: the table keeps its own entries)
+DEV uint32_t take_ext_row(Wv& w, uint32_t* top, uint32_t rows, int kind) {
+    uint32_t r = 0;
+    if (lane_id() == 0) r = atomicAdd(top, 1u);
+    r = uni(r);
+    if (r >= rows) { ovf(w, kind); return 0; }
+    return r + 1;
+}
+// the outstanding table outgrew its own row
+DEV void out_ext(Wv& w) {
+    if (w.pt_dirty && w.out_n > OUT_IN && !w.ox) w.ox = take_ext_row(w, w.a->outx_top, w.a->outx_rows, PSIM_OVF_PT_OUT);
 }
 
 DEV uint8_t flag_byte(const Wv& w) {
@@ -1120,13 +1166,18 @@ DEV uint8_t flag_byte(const Wv& w) {
 // Write back the node: a fixed set of full-wave stores (each lane past a
 // row's end repeats one of its elements; a row that did not change is
 // "stored" as a rewrite of header word 0 with its own value), then the
-// staged records.  8 vector memory operations for every node, the Plumtree
+// staged records.  10 vector memory operations for every node, the Plumtree
 // rows too after a notify replay.
 DEV void writeback(Wv& w) {
     const RoundArgs& a = *w.a;
     const uint32_t l = lane_id();
     const size_t li = w.li;
     const uint32_t h0 = (uint32_t)w.rng;
+    if (w.maps_dirty) {                               // a map outgrew its own rows
+        if (w.sent_n > IDMAP_IN && !w.sx) w.sx = take_ext_row(w, a.mapx_top, a.mapx_rows, PSIM_OVF_IDMAP);
+        if (w.recv_n > IDMAP_IN && !w.rx) w.rx = take_ext_row(w, a.mapx_top, a.mapx_rows, PSIM_OVF_IDMAP);
+    }
+    out_ext(w);
     uint32_t* hrow = reinterpret_cast<uint32_t*>(a.hdr + li);
     hrow[l & 15] = header_word(w, l & 15);
     {
@@ -1140,16 +1191,20 @@ DEV void writeback(Wv& w) {
         *(dirty ? a.pas + li * PSIM_PASSIVE_CAP + (l & 31) : hrow) = dirty ? x : h0;
     }
     {
-        const bool d = w.maps_dirty;
-        const uint32_t l31 = l & 31;
-        uint32_t si = shfl(w.SI, (int)l31), ri = shfl(w.RI, (int)l31);
-        uint32_t* p1 = (l < 32 ? a.sentp : a.senti) + li * PSIM_IDMAP_CAP + l31;
-        uint32_t* p2 = (l < 32 ? a.recvp : a.recvi) + li * PSIM_IDMAP_CAP + l31;
-        *(d ? p1 : hrow) = d ? (l < 32 ? w.SP : si) : h0;
-        *(d ? p2 : hrow) = d ? (l < 32 ? w.RP : ri) : h0;
+        // own entries, then the extension rows (lanes without a row: the
+        // header's draw counter rewritten)
+        const bool own = l < IDMAP_IN;
+        const bool ds = w.maps_dirty && (own || w.sx), dr = w.maps_dirty && (own || w.rx);
+        const size_t io = li * IDMAP_IN + (l & (IDMAP_IN - 1));
+        const size_t so = w.sx ? (size_t)(w.sx - 1) * IDMAP_EXT + ((l - IDMAP_IN) & 63) : 0;
+        const size_t ro = w.rx ? (size_t)(w.rx - 1) * IDMAP_EXT + ((l - IDMAP_IN) & 63) : 0;
+        uint64_t* h64 = reinterpret_cast<uint64_t*>(hrow);   // (the draw counter, rewritten)
+        *(ds ? (own ? a.sentm + io : a.mapx + so) : h64) = ds ? (((uint64_t)w.SI << 32) | w.SP) : w.rng;
+        *(dr ? (own ? a.recvm + io : a.mapx + ro) : h64) = dr ? (((uint64_t)w.RI << 32) | w.RP) : w.rng;
     }
     if (w.pt_dirty) store_pt_rows(w);
     a.ocnt[li] = w.seq;
+    st_add(w, ST_BOUND, w.seq > a.obase[li + 1] - w.obase ? 1u : 0u);   // (checked by the engine)
     // only this wave writes its node's flag byte; peers read F_UP/F_CRASHED
     a.flags[w.me] = flag_byte(w);
     flush_recs(w);
@@ -1238,7 +1293,8 @@ struct PtIn {
     uint32_t fl, part, oc;
 };
 struct PtX {
-    uint32_t CF, PA, PG, PL, PO;
+    uint32_t CF, PA, PG, PL;
+    uint64_t PO;
 };
 
 DEV PtIn load_pt_node(const RoundArgs& a, uint32_t D) {
@@ -1271,7 +1327,7 @@ DEV PtX load_pt_x(const RoundArgs& a, const PtIn& x) {
     y.PA = load_pa(a, li);
     y.PG = a.pt_eag[li * RT_SET + l];
     y.PL = a.pt_laz[li * RT_SET + l];
-    y.PO = reinterpret_cast<const uint32_t*>(a.pt_out + li * PSIM_PT_OUT_CAP)[l];
+    y.PO = load_po(a, li, rl(x.H, HW_OUT_EXT));
     return y;
 }
 
@@ -1326,9 +1382,11 @@ DEV void writeback_pt(Wv& w) {
     const RoundArgs& a = *w.a;
     const uint32_t l = lane_id();
     const size_t li = w.li;
+    out_ext(w);
     reinterpret_cast<uint32_t*>(a.hdr + li)[l & 15] = header_word(w, l & 15);
     if (w.pt_dirty) store_pt_rows(w);
     a.ocnt[li] = w.seq;
+    st_add(w, ST_BOUND, w.seq > a.obase[li + 1] - w.obase ? 1u : 0u);
     a.flags[w.me] = flag_byte(w);
     if (w.seq != w.flushed) flush_recs(w);
 }
@@ -1438,7 +1496,7 @@ DEV void block_append(bool go, const uint4& D, uint4* desc, uint32_t* cnt, uint3
 }
 
 __global__ void __launch_bounds__(256) k_relay(RoundArgs a) {
-    enum { R_PROC, R_DELIV, R_SHUF, R_IHAVE, R_FAIL, R_DIGEST, R_OVF, R_N };
+    enum { R_PROC, R_DELIV, R_SHUF, R_IHAVE, R_FAIL, R_DIGEST, R_OVF, R_BOUND, R_N };
     __shared__ unsigned long long sst[R_N];
     __shared__ uint32_t sslots[2 * PSIM_MSG_SLOTS];
     for (int i = threadIdx.x; i < 2 * PSIM_MSG_SLOTS; i += blockDim.x) sslots[i] = a.slots[i];
@@ -1449,11 +1507,11 @@ __global__ void __launch_bounds__(256) k_relay(RoundArgs a) {
     const uint32_t l = lane_id();
     const uint32_t na = *a.n_alist;
     const uint64_t two58 = 1ull << 58;
-    unsigned long long v[R_N] = {0, 0, 0, 0, 0, 0, 0};
+    unsigned long long v[R_N] = {0, 0, 0, 0, 0, 0, 0, 0};
     for (uint32_t base = blockIdx.x * blockDim.x; base < na; base += gridDim.x * blockDim.x) {
         const uint32_t P = base + threadIdx.x;
         uint4 D = make_uint4(0, 0, 0, 0);
-        bool heavy = false, to_pt = false, relay = false, lazy_here = false;
+        bool heavy = false, to_pt = false, relay = false, lazy_here = false, maps = false;
         Hdr h;
         uint32_t ik = 0, ttl = 0, nex = 0, src = 0, hv_at = 0;
         const Msg* rp = nullptr;
@@ -1478,11 +1536,19 @@ __global__ void __launch_bounds__(256) k_relay(RoundArgs a) {
                 if ((tt & 0xFF) < PSIM_MSG_PT_BROADCAST) {
                     if (!hvn) { hv_at = j; hv_tt = tt; }
                     hvn++;
+                    maps |= (tt & 0xFF) <= PSIM_MSG_NEIGHBOR_ACCEPTED;   // id maps (hv:703-1089)
                 }
             }
             const bool fresh = h.start_round == a.round;
-            heavy = a.crash_round || fresh || (tf & DESC_SHUFFLE) || ((tf & DESC_PROMO) && h.act_n < a.min_active) ||
-                    hvn > 1;
+            bool exits = false;                       // a crashed active member: EXIT events
+            if (a.crash_round) {
+                const uint32_t av[8] = {act0.x, act0.y, act0.z, act0.w, act1.x, act1.y, act1.z, act1.w};
+#pragma unroll
+                for (int j = 0; j < 8; j++)
+                    exits |= (uint32_t)j < h.act_n && av[j] != id && av[j] < a.n_nodes && (a.flags[av[j]] & F_CRASHED);
+            }
+            heavy = exits || fresh || (tf & DESC_SHUFFLE) || ((tf & DESC_PROMO) && h.act_n < a.min_active) || hvn > 1;
+            maps = maps || exits || (tf & DESC_PROMO);        // move_to_active: current_id
             if (!heavy && hvn == 1) {
                 ttl = (hv_tt >> 8) & 0xFF;
                 nex = (hv_tt >> 16) & 0xFF;
@@ -1496,7 +1562,8 @@ __global__ void __launch_bounds__(256) k_relay(RoundArgs a) {
             relay = relay && !heavy;
             if (!heavy && (relay || to_pt || lazy_here)) v[R_PROC]++;   // (k_consume counts its own)
         }
-        block_append(P < na && heavy, D, a.desc_slow, a.n_slow, wcnt);
+        block_append(P < na && heavy, maps ? make_uint4(D.x, D.y, D.z | DESC_MAPS_BIT, D.w) : D, a.desc_slow, a.n_slow,
+                     wcnt);
         block_append(P < na && to_pt, D, a.desc_pt, a.n_pt, wcnt);
         if (P >= na || heavy) continue;
         const uint32_t id = D.x;
@@ -1543,10 +1610,13 @@ __global__ void __launch_bounds__(256) k_relay(RoundArgs a) {
         }
         if (lazy_here) {                              // send_lazy: every outstanding entry, in order
             const uint32_t X[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-            // the row in chunks of 4 entries (two 16-B loads in flight at once)
-            const uint4* orow = reinterpret_cast<const uint4*>(a.pt_out + li * PSIM_PT_OUT_CAP);
+            // the rows in chunks of 4 entries (two 16-B loads in flight at
+            // once): the node's own, then its extension row
+            const uint64_t* own = a.pt_out + li * OUT_IN;
+            const uint64_t* ext = a.outx + (size_t)(h.pad1[3] ? h.pad1[3] - 1 : 0) * OUT_EXT;
             for (uint32_t i0 = 0; i0 < h.out_n; i0 += 4) {
-                const uint4 q0 = orow[i0 >> 1], q1 = orow[(i0 >> 1) + 1];
+                const uint4* orow = reinterpret_cast<const uint4*>(i0 < OUT_IN ? own + i0 : ext + (i0 - OUT_IN));
+                const uint4 q0 = orow[0], q1 = orow[1];
                 const uint64_t O[4] = {((uint64_t)q0.y << 32) | q0.x, ((uint64_t)q0.w << 32) | q0.z,
                                        ((uint64_t)q1.y << 32) | q1.x, ((uint64_t)q1.w << 32) | q1.z};
                 bool in[4];
@@ -1578,6 +1648,7 @@ __global__ void __launch_bounds__(256) k_relay(RoundArgs a) {
         }
         if (rng != h.rng) a.hdr[li].rng = rng;
         a.ocnt[li] = seq;
+        v[R_BOUND] += seq > a.obase[li + 1] - D.w ? 1u : 0u;
         if (!to_pt) {                                 // (k_pt writes the byte of its nodes)
             const uint8_t fl = a.flags[id];
             a.flags[id] = (uint8_t)((fl & (F_UP | F_CRASHED)) | (h.out_n ? F_LAZY : 0) |
@@ -1597,7 +1668,8 @@ __global__ void __launch_bounds__(256) k_relay(RoundArgs a) {
     for (uint32_t k = threadIdx.x; k < NST; k += blockDim.x)
         row[k] = k == ST_PROC ? sst[R_PROC] : k == ST_DELIV + PSIM_MSG_SHUFFLE ? sst[R_DELIV]
                : k == ST_EMIT + PSIM_MSG_SHUFFLE ? sst[R_SHUF] : k == ST_EMIT + PSIM_MSG_PT_IHAVE ? sst[R_IHAVE]
-               : k == ST_FAIL ? sst[R_FAIL] : k == ST_DIGEST ? sst[R_DIGEST] : k == ST_OVF ? sst[R_OVF] : 0ull;
+               : k == ST_FAIL ? sst[R_FAIL] : k == ST_DIGEST ? sst[R_DIGEST] : k == ST_OVF ? sst[R_OVF]
+               : k == ST_OVF_BY + PSIM_OVF_PT ? sst[R_OVF] : k == ST_BOUND ? sst[R_BOUND] : 0ull;
 }
 
 // one wave-slot per resident wave: the grid strides over the active list

@@ -23,7 +23,10 @@ struct __attribute__((aligned(16))) Hdr {
     uint8_t act_n, pas_n, sent_n, sent_head;
     uint8_t recv_n, recv_head, all_n, com_n;
     uint8_t pad2, pad3, out_n, pad0;
-    uint32_t pad1[4];      // pluggable: pad1[0] = leave/1 target of this round + 1, 0 = none
+    uint32_t pad1[4];      // pluggable: pad1[0] = leave/1 target of this round + 1, 0 = none;
+                           // HyParView: pad1[1] / pad1[2] = the sent / recv id map's
+                           // extension row + 1 (0 = none), words HW_SENT_EXT / HW_RECV_EXT;
+                           // pad1[3] = the outstanding table's, word HW_OUT_EXT
 };
 static_assert(sizeof(Hdr) == 64, "Hdr must be one 64-B line");
 
@@ -44,14 +47,29 @@ static_assert(sizeof(Msg) == 64, "Msg must be 64 B");
 enum : uint8_t { F_UP = 1, F_CRASHED = 2, F_LAZY = 4, F_LOWACT = 8 };
 constexpr uint32_t F_OUTN_SHIFT = 4;
 
-// per-root Plumtree sets: PSIM_PT_ROOTS slots of PSIM_PT_SET_CAP entries in a
-// 64-entry eager row and a 64-entry lazy row (slot k = entries 16k..16k+15);
-// the root row (RT_WORDS per node): root of slot k in word k (PSIM_NONE =
-// free), then the eager counts and the lazy counts, one byte per slot
-constexpr uint32_t RT_SET = PSIM_PT_ROOTS * PSIM_PT_SET_CAP;
+// per-root Plumtree sets: the eager entries of all PSIM_PT_ROOTS slots pooled
+// in one 64-entry row (slot 0's first, then slot 1's, ...), the lazy ones in
+// another; the root row (RT_WORDS per node): root of slot k in word k
+// (PSIM_NONE = free), then the eager counts and the lazy counts, one byte per
+// slot (slot k's entries start at the sum of the counts below it)
+constexpr uint32_t RT_SET = PSIM_PT_SET_POOL;
 constexpr uint32_t RT_WORDS = 8;
 constexpr uint32_t RT_EN = PSIM_PT_ROOTS, RT_LN = PSIM_PT_ROOTS + 1;
 static_assert(RT_SET == 64, "the eager / lazy rows are one 64-lane register");
+
+// Disconnect-id maps (sent_message_map / recv_message_map, PSIM_IDMAP_CAP
+// entries each): the first IDMAP_IN entries in the node's own rows, the rest
+// in an extension row of a shared pool, taken once per node and map the first
+// time the map outgrows its own rows (few nodes ever do: at 2^23 nodes under
+// config E the largest map holds ~30 entries, most hold 0-4)
+constexpr uint32_t IDMAP_IN = 16;
+constexpr uint32_t IDMAP_EXT = PSIM_IDMAP_CAP - IDMAP_IN;
+constexpr uint32_t HW_SENT_EXT = 13, HW_RECV_EXT = 14;   // header words (Hdr pad1[1], pad1[2])
+// Plumtree outstanding table (PSIM_PT_OUT_CAP entries): likewise OUT_IN in
+// the node's row, the rest in an extension row of another pool
+constexpr uint32_t OUT_IN = 16;
+constexpr uint32_t OUT_EXT = PSIM_PT_OUT_CAP - OUT_IN;
+constexpr uint32_t HW_OUT_EXT = 15;
 
 // route key: dst in the low 27 bits, the sender-side emission bound of the
 // message type in the top 5 (used to size the receiver's next outbox).
@@ -60,7 +78,6 @@ constexpr uint32_t KEY_DST_MASK = (1u << KEY_DST_BITS) - 1;
 
 // outbox bound: per inbox message (by type) and per node
 constexpr uint32_t KEY_BCAST = 31;
-constexpr uint32_t BCAST_FIRST = PSIM_PT_SET_CAP;         // eager push of a first delivery
 __host__ __device__ constexpr uint32_t max_emit(uint32_t type) {
     // JOIN: DISCONNECT + NEIGHBOR + FORWARD_JOIN to up to ACTIVE_CAP-2 peers
     return type == PSIM_MSG_JOIN ? 2 + (PSIM_ACTIVE_CAP - 2)
@@ -71,28 +88,33 @@ __host__ __device__ constexpr uint32_t max_emit(uint32_t type) {
          : type == PSIM_MSG_NEIGHBOR_ACCEPTED ? 1
          : type == PSIM_MSG_SHUFFLE ? 1
          // a marker, not a count: the route counts a BROADCAST as 1 (the
-         // PRUNE of a duplicate) and adds BCAST_FIRST once per distinct
-         // message id (msg & 31, the `have` bit) the destination receives
+         // PRUNE of a duplicate) and k_node_prep adds an eager push
+         // and lazy adds once per distinct message slot the destination
+         // receives
          : type == PSIM_MSG_PT_BROADCAST ? KEY_BCAST
          : type == PSIM_MSG_PT_IHAVE ? 1
          : type == PSIM_MSG_PT_GRAFT ? 1
          : 0;
 }
-constexpr uint32_t BOUND_BASE = 3;                        // JOIN send, promotion, shuffle
-constexpr uint32_t BOUND_EXITS = PSIM_ACTIVE_CAP - 1;     // EXIT-driven NEIGHBOR_REQUESTs
-constexpr uint32_t BOUND_LAZY = PSIM_PT_OUT_CAP;          // IHAVEs of entries already outstanding
 static_assert(PSIM_ACTIVE_CAP < KEY_BCAST, "max_emit must fit the 5-bit key field below the marker");
-constexpr uint32_t BOUND_ORIGIN = 2 * PSIM_PT_SET_CAP;    // eager push + lazy adds of the root
+// (the per-node terms of the outbox bound -- due timers, pushes, the lazy
+// tick, crash-round exits -- are k_node_prep's, psim_engine.hip)
 
 // work descriptor (id, inbox begin, inbox count | due timers << 28, outbox
 // base): the timers k_desc found due this round for the node
-constexpr uint32_t DESC_CNT_MASK = (1u << 28) - 1;
+constexpr uint32_t DESC_CNT_MASK = (1u << 27) - 1;
 enum : uint32_t { DESC_PROMO = 1, DESC_SHUFFLE = 2, DESC_LAZY = 4, DESC_ORIGIN = 8 };
+// bit 27 of k_consume's descriptors (k_relay): the node's HyParView phase may
+// read or write its disconnect-id maps (a JOIN .. NEIGHBOR_ACCEPTED message,
+// an EXIT, a promotion)
+constexpr uint32_t DESC_MAPS_BIT = 1u << 27;
 
 // stats slots in the per-block partial arrays
 enum {
     ST_EMIT = 0, ST_DELIV = 16, ST_DROPPED = 32, ST_UP, ST_PROC, ST_EXITS, ST_FAIL, ST_FIRST,
-    ST_OVF, ST_DIGEST, ST_BYTES, ST_STOP, NST
+    ST_OVF, ST_DIGEST, ST_BYTES, ST_STOP,
+    ST_BOUND,       // nodes that emitted more records than their outbox bound (an engine bug: fails the round)
+    ST_OVF_BY, NST = ST_OVF_BY + PSIM_OVF_NKINDS
 };
 
 // ------------------------------------------------------------------ RNG --

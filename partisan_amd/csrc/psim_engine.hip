@@ -42,7 +42,7 @@ namespace {
 constexpr int BLK = 256;
 // pinned host words per shard (Shard::pin): NST stats, the consume span, the
 // outbox total, the routed record count -- stored by kernels, read by the host
-enum { PIN_TOTAL = NST + 2, PIN_M = NST + 3, PIN_OVF = NST + 4 };
+enum { PIN_TOTAL = NST + 2, PIN_M = NST + 3, PIN_OVF = NST + 4, PIN_BIGIN = NST + 5 };
 
 #define HIP_TRY(x)                                                       \
     do {                                                                 \
@@ -108,8 +108,11 @@ __global__ void k_join(RoundArgs a, uint32_t* start, const uint32_t* ids, const 
     if (id < a.lo || id >= a.lo + a.n_local) return;
     uint32_t li = id - a.lo;
     Hdr h;
-    uint32_t old_epoch = a.hdr[li].epoch;
+    const uint32_t old_epoch = a.hdr[li].epoch;
+    const uint32_t sx = a.pl ? 0u : a.hdr[li].pad1[1], rx = a.pl ? 0u : a.hdr[li].pad1[2];
+    const uint32_t ox = a.pl ? 0u : a.hdr[li].pad1[3];
     memset(&h, 0, sizeof h);
+    h.pad1[1] = sx; h.pad1[2] = rx; h.pad1[3] = ox;   // a restart keeps its extension rows (zeroed)
     h.epoch = persist_epoch ? old_epoch + 1 : 1;
     h.start_round = a.round;
     h.join_contact = contacts[i];
@@ -122,9 +125,13 @@ __global__ void k_join(RoundArgs a, uint32_t* start, const uint32_t* ids, const 
     for (int k = 0; k < PSIM_ACTIVE_CAP; k++) act[k] = k == 0 ? id : 0u;
     uint32_t* pas = a.pas + (size_t)li * PSIM_PASSIVE_CAP;
     for (int k = 0; k < PSIM_PASSIVE_CAP; k++) pas[k] = 0;
-    for (int k = 0; k < PSIM_IDMAP_CAP; k++) {
-        size_t b = (size_t)li * PSIM_IDMAP_CAP + k;
-        a.sentp[b] = 0; a.senti[b] = 0; a.recvp[b] = 0; a.recvi[b] = 0;
+    for (uint32_t k = 0; k < IDMAP_IN; k++) {
+        a.sentm[(size_t)li * IDMAP_IN + k] = 0;
+        a.recvm[(size_t)li * IDMAP_IN + k] = 0;
+    }
+    for (uint32_t k = 0; k < IDMAP_EXT; k++) {
+        if (sx) a.mapx[(size_t)(sx - 1) * IDMAP_EXT + k] = 0;
+        if (rx) a.mapx[(size_t)(rx - 1) * IDMAP_EXT + k] = 0;
     }
     for (int k = 0; k < PSIM_PT_MEMBERS_CAP; k++) {
         a.pt_all[(size_t)li * PSIM_PT_MEMBERS_CAP + k] = k == 0 ? id : 0u;
@@ -135,7 +142,9 @@ __global__ void k_join(RoundArgs a, uint32_t* start, const uint32_t* ids, const 
         a.pt_laz[(size_t)li * RT_SET + k] = 0;
     }
     for (uint32_t k = 0; k < RT_WORDS; k++) a.pt_rt[(size_t)li * RT_WORDS + k] = k < PSIM_PT_ROOTS ? PSIM_NONE : 0u;
-    for (int k = 0; k < PSIM_PT_OUT_CAP; k++) a.pt_out[(size_t)li * PSIM_PT_OUT_CAP + k] = 0;
+    for (uint32_t k = 0; k < OUT_IN; k++) a.pt_out[(size_t)li * OUT_IN + k] = 0;
+    if (ox)
+        for (uint32_t k = 0; k < OUT_EXT; k++) a.outx[(size_t)(ox - 1) * OUT_EXT + k] = 0;
     if (a.pl) {                    // the pluggable manager's init/1 (pl:346-402) + Strategy:init/1
         Hdr& x = a.hdr[li];
         x.aux = PSIM_NONE;         // last ping: undefined
@@ -602,24 +611,60 @@ __global__ void __launch_bounds__(256) k_node_prep(RoundArgs a, const unsigned l
                 w = c > 0 || (pending && !x.have) || per || leave;
             } else {
                 bool origin = a.origin[i] != 0;
-                // per message its class bound (a BROADCAST: 1), per distinct
-                // BROADCAST id an eager push, and the lazy tick's IHAVEs if
-                // entries are outstanding or may be added this round
+                const Hdr& x = a.hdr[i];
+                // the due timers' sends: the JOIN of a fresh start, a
+                // promotion's NEIGHBOR_REQUEST (the active view may shrink
+                // during the round: any due promotion), a shuffle
+                const bool promo = a.random_promotion && due(a.promotion_period, r, st);
+                b = (cbi >> 32) + (st == r && x.join_contact != PSIM_NONE ? 1u : 0u) + (promo ? 1u : 0u) +
+                    (due(a.shuffle_period, r, st) ? 1u : 0u);
+                // per BROADCAST message slot a first delivery's eager push
+                // and lazy adds (plus the origin's): at most the root's sets
+                // at round start -- or the common eagers of a new root or of a
+                // reset -- plus one per message handled before; the push's
+                // sends need an active connection: at most two per active
+                // member (its atom and its node_spec identity, App. A Q6)
                 const unsigned long long bm = c ? bmask[i] : 0ull;
-                b = (cbi >> 32) + BOUND_BASE + (uint64_t)__popcll(bm) * BCAST_FIRST;
-                // a due lazy tick sends every outstanding entry: those left
-                // from last round (flag nibble) and those this round's first
-                // deliveries and origin add, at most PT_OUT_CAP
-                if (a.plumtree && due(a.lazy_tick_period, r, st)) {
-                    const uint32_t prev = (f >> F_OUTN_SHIFT) >= 15 ? PSIM_PT_OUT_CAP : (f >> F_OUTN_SHIFT);
-                    b += min((uint32_t)PSIM_PT_OUT_CAP,
-                             prev + ((uint32_t)__popcll(bm) + (origin ? 1u : 0u)) * PSIM_PT_SET_CAP);
+                const uint32_t pushes = (uint32_t)__popcll(bm) + (origin ? 1u : 0u);
+                const bool lazy = a.plumtree && due(a.lazy_tick_period, r, st);
+                uint32_t lazy_add = 0;
+                if (pushes) {
+                    const uint4 r0 = *reinterpret_cast<const uint4*>(a.pt_rt + (size_t)i * RT_WORDS);
+                    const uint2 cn = *reinterpret_cast<const uint2*>(a.pt_rt + (size_t)i * RT_WORDS + RT_EN);
+                    const uint32_t rts[4] = {r0.x, r0.y, r0.z, r0.w};
+                    auto push = [&](uint32_t root) {
+                        uint32_t ne = PSIM_PT_MEMBERS_CAP, nl = 0;
+#pragma unroll
+                        for (int k = 0; k < PSIM_PT_ROOTS; k++)
+                            if (rts[k] == root) {
+                                ne = max(ne, (cn.x >> (8 * k)) & 0xFFu);
+                                nl = (cn.y >> (8 * k)) & 0xFFu;
+                            }
+                        b += min(2u * PSIM_ACTIVE_CAP, ne + c);
+                        lazy_add += nl + c;
+                    };
+                    for (unsigned long long m = bm; m; m &= m - 1) push(a.slots[PSIM_MSG_SLOTS + __ffsll(m) - 1]);
+                    if (origin) push((a.lo + i) | PSIM_MAP_BIT);
                 }
-                if (a.crash_round) b += BOUND_EXITS;
-                if (origin) b += BOUND_ORIGIN;
+                // a due lazy tick sends every outstanding entry: those left
+                // from last round and those this round's pushes add, at most
+                // PT_OUT_CAP
+                if (lazy) b += min((uint32_t)PSIM_PT_OUT_CAP, (uint32_t)x.out_n + lazy_add);
+                // a crash round: a NEIGHBOR_REQUEST per crashed active member
+                if (a.crash_round) {
+                    const uint4* ar = reinterpret_cast<const uint4*>(a.act + (size_t)i * PSIM_ACTIVE_CAP);
+                    const uint4 a0 = ar[0], a1 = ar[1];
+                    const uint32_t av[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+#pragma unroll
+                    for (int k = 0; k < PSIM_ACTIVE_CAP; k++)
+                        if ((uint32_t)k < x.act_n && av[k] < a.n_nodes && (a.flags[av[k]] & F_CRASHED)) b++;
+                }
                 w = c > 0 || st == r || a.crash_round || (f & F_LAZY) || origin ||
                     (a.random_promotion && (f & F_LOWACT) && due(a.promotion_period, r, st)) ||
                     due(a.shuffle_period, r, st);
+                // a working node's first slot is reserved: a wave that emits
+                // nothing rewrites it (flush_recs' fixed store)
+                if (w && b == 0) b = 1;
             }
             up++;
         } else {
@@ -671,6 +716,7 @@ __global__ void k_desc(const uint64_t* __restrict__ packed, const uint64_t* __re
         return;
     }
     if (!(packed[li] & 1u)) return;
+    if ((uint32_t)cb[li] > DESC_CNT_MASK) hout[PIN_BIGIN] = 1;   // (the descriptor packs it in 27 bits)
     const uint32_t st = start[li], r = a.round;
     const uint32_t tf = (a.random_promotion && due(a.promotion_period, r, st) ? DESC_PROMO : 0u) |
                         (due(a.shuffle_period, r, st) ? DESC_SHUFFLE : 0u) |
@@ -854,17 +900,50 @@ struct DBuf {
     int ensure(size_t want, int headroom = 0) {
         if (want <= n) return PSIM_OK;
         static const bool trace = getenv("PSIM_TRACE_GROW") != nullptr;
-        if (trace && p) std::fprintf(stderr, "psim: grow %zu -> %zu x %zu B\n", n, want, sizeof(T));
+        if (trace && want >= (1u << 20))
+            std::fprintf(stderr, "psim: grow %zu -> %zu (want) x %zu B\n", n, want, sizeof(T));
         if (p) (void)hipFree(p);
         p = nullptr; n = 0;
         const size_t goal = want + want / 4 * (size_t)headroom;
         size_t cap = 1024;
         while (cap < goal) cap <<= 1;
-        if (hipMalloc(&p, cap * sizeof(T)) != hipSuccess) return PSIM_ENOMEM;
+        // past 1 GiB a power of two (or the caller's headroom) may waste up
+        // to half: 1/8 headroom in 64 MiB steps instead (at 2^26 nodes the
+        // message buffers are tens of GB)
+        if (cap * sizeof(T) > (1ull << 30)) {
+            const size_t step = (64ull << 20) / sizeof(T);
+            cap = (want + want / 8 + step - 1) / step * step;
+        }
+        if (hipMalloc(&p, cap * sizeof(T)) != hipSuccess) {
+            size_t fr = 0, tot = 0;
+            (void)hipGetLastError();
+            if (hipMemGetInfo(&fr, &tot) == hipSuccess)
+                std::fprintf(stderr, "psim: device allocation of %.2f GB failed (%.2f of %.2f GB free)\n",
+                             cap * sizeof(T) / 1e9, fr / 1e9, tot / 1e9);
+            p = nullptr;
+            return PSIM_ENOMEM;
+        }
         n = cap;
         return PSIM_OK;
     }
+    // grow like ensure(), keeping the first `keep` elements (copied on `st`)
+    int ensure_keep(size_t want, size_t keep, hipStream_t st) {
+        if (want <= n) return PSIM_OK;
+        if (!p || !keep) return ensure(want);
+        DBuf<T> nb;
+        TRY(nb.ensure(want));
+        if (hipMemcpyAsync(nb.p, p, std::min(keep, n) * sizeof(T), hipMemcpyDeviceToDevice, st) != hipSuccess ||
+            hipStreamSynchronize(st) != hipSuccess) {
+            nb.release();
+            return PSIM_EDEVICE;
+        }
+        release();
+        p = nb.p; n = nb.n;
+        return PSIM_OK;
+    }
     int alloc(size_t want) {    // exact, zeroed
+        static const bool trace = getenv("PSIM_TRACE_GROW") != nullptr;
+        if (trace && want >= (1u << 20)) std::fprintf(stderr, "psim: alloc %zu x %zu B\n", want, sizeof(T));
         if (hipMalloc(&p, std::max<size_t>(want, 1) * sizeof(T)) != hipSuccess) return PSIM_ENOMEM;
         n = want;
         if (hipMemset(p, 0, std::max<size_t>(want, 1) * sizeof(T)) != hipSuccess) return PSIM_EDEVICE;
@@ -913,18 +992,23 @@ struct Shard {
     DBuf<uint8_t> flags, part;
     // local rows
     DBuf<Hdr> hdr;
-    DBuf<uint32_t> act, pas, sentp, senti, recvp, recvi, pt_all, pt_com, pt_eag, pt_laz, pt_rt, start;
+    DBuf<uint32_t> act, pas, pt_all, pt_com, pt_eag, pt_laz, pt_rt, start;
+    DBuf<uint64_t> sentm, recvm, mapx;  // id maps (id << 32 | peer): own rows, extension rows (pool)
+    DBuf<uint32_t> mapx_top;
     DBuf<uint32_t> origin;              // per local node: msg id + 1 it originates this round
     DBuf<uint32_t> slots;               // the message slots (msg ids, then roots), a copy of the host's
     DBuf<uint32_t> bc_roots, bc_msgs;   // this round's broadcasts
-    DBuf<uint64_t> pt_out;
+    DBuf<uint64_t> pt_out, outx;        // outstanding: own rows, extension rows (pool)
+    DBuf<uint32_t> outx_top;
     // inbox of the next round: sorted (local dst | bound, record index) pairs
     DBuf<uint32_t> ikeys, ivals;
     uint32_t m_in = 0;
     DBuf<Msg> outbox;                   // this round's emissions (holes between node regions)
     DBuf<Msg> recvbuf;                  // G > 1: received records, in source-shard order
-    DBuf<Msg> inbox[2];                 // records by node run, in inbox order: inbox[in_cur] is
-    int in_cur = 0;                     // read by this round's consume, the other one is routed into
+    // records by node run, in inbox order: read by this round's node-round
+    // kernels, then (same stream) overwritten by the route with the next
+    // round's -- one buffer, nothing reads a round's inbox after its consume
+    DBuf<Msg> inbox;
     // per-round scratch
     DBuf<uint32_t> okey, ocnt, in_beg,
         d_nact, n_slow, n_pt, rank, long_list, n_long, tmp, hist, hoff;
@@ -1013,11 +1097,13 @@ RoundArgs make_args(psim_handle* h, Shard* s) {
     a.origin = s->origin.p;
     a.slots = s->slots.p;
     a.flags = s->flags.p; a.part = s->part.p; a.hdr = s->hdr.p;
-    a.act = s->act.p; a.pas = s->pas.p; a.sentp = s->sentp.p; a.senti = s->senti.p;
-    a.recvp = s->recvp.p; a.recvi = s->recvi.p;
+    a.act = s->act.p; a.pas = s->pas.p; a.sentm = s->sentm.p; a.recvm = s->recvm.p;
+    a.mapx = s->mapx.p; a.mapx_top = s->mapx_top.p;
+    a.mapx_rows = (uint32_t)(s->mapx.n / IDMAP_EXT);
     a.pt_all = s->pt_all.p; a.pt_com = s->pt_com.p; a.pt_eag = s->pt_eag.p; a.pt_laz = s->pt_laz.p;
     a.pt_rt = s->pt_rt.p;
-    a.pt_out = s->pt_out.p;
+    a.pt_out = s->pt_out.p; a.outx = s->outx.p; a.outx_top = s->outx_top.p;
+    a.outx_rows = (uint32_t)(s->outx.n / OUT_EXT);
     a.start = s->start.p;
     a.pl = c.manager == PSIM_MANAGER_PLUGGABLE;
     a.strategy = c.strategy; a.periodic = c.periodic_interval; a.scamp_c = c.scamp_c;
@@ -1161,7 +1247,7 @@ int phase_events_prepare(psim_handle* h, Shard* s, const RoundCtl& ctl, RoundArg
         TRY(scan_excl(s, s->bound.p, s->pscan.p, n + 1));
         k_desc<<<grid_for(n + 1), BLK, 0, s->stream>>>(s->bound.p, s->pscan.p, s->in_beg.p, s->cb.p, s->start.p, a,
                                                         s->desc.p, s->obase.p, s->d_nact.p, s->btot.p, s->pin_dev);
-        if (s->m_in > DESC_CNT_MASK) return PSIM_ENOMEM;   // per-node inbox counts must fit 28 bits
+        if (s->pin[PIN_BIGIN]) return PSIM_ENOMEM;    // a node's inbox count must fit 27 bits
         TRY(stream_wait(s));                          // (k_desc stored the total in pin)
         const uint64_t total = s->pin[PIN_TOTAL];
         if (total >= 0xFFFFFFFFull) return PSIM_ENOMEM;
@@ -1195,7 +1281,7 @@ int phase_events_prepare(psim_handle* h, Shard* s, const RoundCtl& ctl, RoundArg
     }
     a.in_beg = s->in_beg.p;
     a.desc = s->desc.p; a.n_alist = s->d_nact.p;
-    a.rec_in = s->inbox[s->in_cur].p;
+    a.rec_in = s->inbox.p;
     a.obase = s->obase.p;
     a.rec_out = s->outbox.p;
     a.okey = s->okey.p; a.ocnt = s->ocnt.p;
@@ -1257,8 +1343,7 @@ int gather_inbox(psim_handle* h, Shard* s, const Msg* src, const uint32_t* dev_m
     KTimer t(h, s, KT_GATHER);
     if (max_m)
         k_gather_dev<<<std::min<uint32_t>(grid_for((uint64_t)max_m * 4), 8192), BLK, 0, s->stream>>>(
-            src, s->ivals.p, dev_m, s->inbox[s->in_cur ^ 1].p, s->rcap);
-    s->in_cur ^= 1;
+            src, s->ivals.p, dev_m, s->inbox.p, s->rcap);
     return PSIM_OK;
 }
 
@@ -1307,8 +1392,10 @@ int route_group(psim_handle* h, Shard* s, const Msg* dense, uint32_t m) {
 int route_buffers(Shard* s, bool both_inboxes) {
     const size_t c = s->rcap + 1;
     TRY(s->ivals.ensure(c)); TRY(s->tmp.ensure(c)); TRY(s->rank.ensure(c)); TRY(s->pairs.ensure(c));
-    TRY(s->inbox[s->in_cur ^ 1].ensure(c));
-    if (both_inboxes) TRY(s->inbox[s->in_cur].ensure(c));
+    // the inbox may hold this round's records (the first round after a
+    // restore): a growth keeps them
+    (void)both_inboxes;
+    TRY(s->inbox.ensure_keep(c, s->m_in, s->stream));
     return PSIM_OK;
 }
 
@@ -1477,8 +1564,12 @@ int run_round(psim_handle* h, uint64_t* st) {
             // (1.5x, power of two) and route this round's outbox again
             const uint64_t m = s->pin[PIN_OVF];
             s->pin[PIN_OVF] = 0;
-            while (s->rcap < m + m / 2) s->rcap <<= 1;
-            s->in_cur ^= 1;                           // the skipped gather's flip
+            if (s->rcap < m + m / 2) {
+                // 1.5x, a power of two up to 2^26 records, then in 2^20 steps
+                const uint64_t want = m + m / 2;
+                if (want <= (1ull << 26)) while (s->rcap < want) s->rcap <<= 1;
+                else s->rcap = (want + (1ull << 20) - 1) >> 20 << 20;
+            }
             TRY(route_buffers(s, false));
             TRY(phase_route_local(h, s));
             TRY(stream_wait(s));
@@ -1486,8 +1577,14 @@ int run_round(psim_handle* h, uint64_t* st) {
         if (h->G == 1) s->m_in = (uint32_t)s->pin[PIN_M];   // routed this round
         static const bool trace_relay = getenv("PSIM_TRACE_RELAY") != nullptr;
         if (trace_relay && s->rgrid)
-            std::fprintf(stderr, "psim: round %llu shard %u: %u nodes with work, %u to k_consume\n",
-                         (unsigned long long)h->round, s->idx, read1(s, s->d_nact.p), read1(s, s->n_slow.p));
+        {
+            uint64_t em = 0;
+            for (int k = 0; k < PSIM_MSG_NTYPES; k++) em += s->pin[ST_EMIT + k];
+            std::fprintf(stderr, "psim: round %llu shard %u: %u nodes with work, %u to k_consume, %u to k_pt, "
+                         "outbox bound %llu, emitted %llu\n",
+                         (unsigned long long)h->round, s->idx, read1(s, s->d_nact.p), read1(s, s->n_slow.p),
+                         read1(s, s->n_pt.p), (unsigned long long)s->pin[PIN_TOTAL], (unsigned long long)em);
+        }
         if (s->pin[NST] != ~0ull && s->pin[NST + 1] > s->pin[NST]) {   // 100 MHz ticks
             h->kt_ms[KT_CONSUME] += (double)(s->pin[NST + 1] - s->pin[NST]) * 1e-5;
             h->kt_n[KT_CONSUME]++;
@@ -1500,6 +1597,11 @@ int run_round(psim_handle* h, uint64_t* st) {
         NCCL_TRY(ncclAllReduce(h->comm_cnt.p, h->comm_cnt.p, NST, ncclUint64, ncclSum, h->comm, s->stream));
         HIP_TRY(hipMemcpyAsync(st, h->comm_cnt.p, NST * 8, hipMemcpyDeviceToHost, s->stream));
         TRY(stream_wait(s));
+    }
+    if (st[ST_BOUND]) {
+        std::fprintf(stderr, "psim: round %llu: %llu nodes emitted past their outbox bound (engine bug)\n",
+                     (unsigned long long)h->round, (unsigned long long)st[ST_BOUND]);
+        return PSIM_EDEVICE;
     }
     for (uint32_t j : h->pend_join) h->pend_join_mark[j] = 0;
     h->pend_crash.clear(); h->pend_join.clear(); h->pend_contact.clear();
@@ -1535,6 +1637,7 @@ void fill_stats(const uint64_t* s, uint64_t round, psim_round_stats* o) {
     o->dropped = s[ST_DROPPED]; o->nodes_up = s[ST_UP]; o->nodes_processed = s[ST_PROC];
     o->exits = s[ST_EXITS]; o->send_fail = s[ST_FAIL]; o->first_deliveries = s[ST_FIRST];
     o->overflow = s[ST_OVF]; o->digest = s[ST_DIGEST]; o->state_bytes = s[ST_BYTES];
+    for (int k = 0; k < PSIM_OVF_NKINDS; k++) o->overflow_by[k] = s[ST_OVF_BY + k];
 }
 
 int shard_alloc(psim_handle* h, Shard* s) {
@@ -1555,12 +1658,19 @@ int shard_alloc(psim_handle* h, Shard* s) {
     int rc = 0;
     rc |= s->flags.alloc(N); rc |= s->part.alloc(N); rc |= s->hdr.alloc(n);
     rc |= s->act.alloc(n * PSIM_ACTIVE_CAP); rc |= s->pas.alloc(n * PSIM_PASSIVE_CAP);
-    rc |= s->sentp.alloc(n * PSIM_IDMAP_CAP); rc |= s->senti.alloc(n * PSIM_IDMAP_CAP);
-    rc |= s->recvp.alloc(n * PSIM_IDMAP_CAP); rc |= s->recvi.alloc(n * PSIM_IDMAP_CAP);
+    rc |= s->sentm.alloc(n * IDMAP_IN); rc |= s->recvm.alloc(n * IDMAP_IN);
+    if (h->cfg.manager != PSIM_MANAGER_PLUGGABLE) {
+        // extension rows for 1/32 of the nodes (~1/1700 used at 2^23 under config E)
+        const size_t rows = std::max<size_t>(1024, n / 32);
+        rc |= s->mapx.alloc(rows * IDMAP_EXT);
+    }
+    rc |= s->mapx_top.alloc(1);
     rc |= s->pt_all.alloc(n * PSIM_PT_MEMBERS_CAP); rc |= s->pt_com.alloc(n * PSIM_PT_MEMBERS_CAP);
     rc |= s->pt_eag.alloc(n * RT_SET); rc |= s->pt_laz.alloc(n * RT_SET); rc |= s->pt_rt.alloc(n * RT_WORDS);
     rc |= s->origin.alloc(n); rc |= s->slots.alloc(2 * PSIM_MSG_SLOTS);
-    rc |= s->pt_out.alloc(n * PSIM_PT_OUT_CAP); rc |= s->start.alloc(n);
+    rc |= s->pt_out.alloc(n * OUT_IN); rc |= s->start.alloc(n);
+    if (h->cfg.manager != PSIM_MANAGER_PLUGGABLE) rc |= s->outx.alloc(std::max<size_t>(1024, n / 32) * OUT_EXT);
+    rc |= s->outx_top.alloc(1);
     rc |= s->ocnt.alloc(n); rc |= s->cb.alloc(n + 1);
     rc |= s->in_beg.alloc(n + 1); rc |= s->bound.alloc(n + 1); rc |= s->pscan.alloc(n + 1); rc |= s->obase.alloc(n + 1);
     rc |= s->long_list.alloc(n); rc |= s->bmask.alloc(n); rc |= s->btot.alloc(1); rc |= s->n_long.alloc(1);
@@ -1570,7 +1680,7 @@ int shard_alloc(psim_handle* h, Shard* s) {
     if (h->cfg.manager == PSIM_MANAGER_PLUGGABLE) { rc |= s->stop_ids.alloc(n); rc |= s->n_stop.alloc(1); }
     rc |= s->stat_out.alloc(NST + 2);   // + the consume span
     rc |= s->ikeys.alloc(1024); rc |= s->ivals.alloc(1024);
-    rc |= s->recvbuf.alloc(1024); rc |= s->inbox[0].alloc(1024); rc |= s->inbox[1].alloc(1024); rc |= s->outbox.alloc(1024);
+    rc |= s->recvbuf.alloc(1024); rc |= s->inbox.alloc(1024); rc |= s->outbox.alloc(1024);
     if (h->cfg.manager == PSIM_MANAGER_PLUGGABLE) {
         if (h->cfg.strategy == PSIM_STRATEGY_FULL) {
             rc |= s->fbits.alloc(n * 2 * h->fw);     // [adds | removes] per node
@@ -1591,11 +1701,13 @@ int shard_alloc(psim_handle* h, Shard* s) {
 void shard_free(Shard* s) {
     if (s->stream) (void)hipStreamSynchronize(s->stream);
     s->flags.release(); s->part.release(); s->hdr.release();
-    s->act.release(); s->pas.release(); s->sentp.release(); s->senti.release();
-    s->recvp.release(); s->recvi.release(); s->pt_all.release(); s->pt_com.release();
+    s->act.release(); s->pas.release(); s->sentm.release(); s->recvm.release();
+    s->pt_all.release(); s->pt_com.release();
+    s->mapx.release(); s->mapx_top.release();
     s->pt_eag.release(); s->pt_laz.release(); s->pt_out.release(); s->start.release();
+    s->outx.release(); s->outx_top.release();
     s->pt_rt.release(); s->origin.release(); s->slots.release(); s->bc_roots.release(); s->bc_msgs.release();
-    s->ikeys.release(); s->ivals.release(); s->recvbuf.release(); s->inbox[0].release(); s->inbox[1].release();
+    s->ikeys.release(); s->ivals.release(); s->recvbuf.release(); s->inbox.release();
     if (s->pin) (void)hipHostFree(s->pin);
     if (s->wait_ev) (void)hipEventDestroy(s->wait_ev);
     s->wait_ev = nullptr;
@@ -1862,10 +1974,10 @@ static int get_shard_nodes(Shard* s, uint32_t first, uint32_t count, psim_node_v
     std::vector<Hdr> hd(count);
     std::vector<uint8_t> fl(count);
     std::vector<uint32_t> act((size_t)count * PSIM_ACTIVE_CAP), pas((size_t)count * PSIM_PASSIVE_CAP);
-    std::vector<uint32_t> sp((size_t)count * PSIM_IDMAP_CAP), si(sp.size()), rp(sp.size()), ri(sp.size());
+    std::vector<uint64_t> sm((size_t)count * IDMAP_IN), rm(sm.size());
     std::vector<uint32_t> all((size_t)count * PSIM_PT_MEMBERS_CAP), com(all.size());
     std::vector<uint32_t> eag((size_t)count * RT_SET), laz(eag.size()), rt((size_t)count * RT_WORDS);
-    std::vector<uint64_t> po((size_t)count * PSIM_PT_OUT_CAP);
+    std::vector<uint64_t> po((size_t)count * OUT_IN);
     const size_t li = first - s->lo;
     auto cp = [&](void* dst, const void* src, size_t bytes) {
         return hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, s->stream);
@@ -1874,16 +1986,21 @@ static int get_shard_nodes(Shard* s, uint32_t first, uint32_t count, psim_node_v
     HIP_TRY(cp(fl.data(), s->flags.p + first, count));
     HIP_TRY(cp(act.data(), s->act.p + li * PSIM_ACTIVE_CAP, act.size() * 4));
     HIP_TRY(cp(pas.data(), s->pas.p + li * PSIM_PASSIVE_CAP, pas.size() * 4));
-    HIP_TRY(cp(sp.data(), s->sentp.p + li * PSIM_IDMAP_CAP, sp.size() * 4));
-    HIP_TRY(cp(si.data(), s->senti.p + li * PSIM_IDMAP_CAP, si.size() * 4));
-    HIP_TRY(cp(rp.data(), s->recvp.p + li * PSIM_IDMAP_CAP, rp.size() * 4));
-    HIP_TRY(cp(ri.data(), s->recvi.p + li * PSIM_IDMAP_CAP, ri.size() * 4));
+    HIP_TRY(cp(sm.data(), s->sentm.p + li * IDMAP_IN, sm.size() * 8));
+    HIP_TRY(cp(rm.data(), s->recvm.p + li * IDMAP_IN, rm.size() * 8));
+    // the extension rows taken so far (few)
+    const uint32_t top = s->mapx.p ? std::min<uint32_t>(read1(s, s->mapx_top.p), (uint32_t)(s->mapx.n / IDMAP_EXT)) : 0u;
+    std::vector<uint64_t> xm((size_t)top * IDMAP_EXT);
+    if (top) HIP_TRY(cp(xm.data(), s->mapx.p, xm.size() * 8));
     HIP_TRY(cp(all.data(), s->pt_all.p + li * PSIM_PT_MEMBERS_CAP, all.size() * 4));
     HIP_TRY(cp(com.data(), s->pt_com.p + li * PSIM_PT_MEMBERS_CAP, com.size() * 4));
     HIP_TRY(cp(eag.data(), s->pt_eag.p + li * RT_SET, eag.size() * 4));
     HIP_TRY(cp(laz.data(), s->pt_laz.p + li * RT_SET, laz.size() * 4));
     HIP_TRY(cp(rt.data(), s->pt_rt.p + li * RT_WORDS, rt.size() * 4));
-    HIP_TRY(cp(po.data(), s->pt_out.p + li * PSIM_PT_OUT_CAP, po.size() * 8));
+    HIP_TRY(cp(po.data(), s->pt_out.p + li * OUT_IN, po.size() * 8));
+    const uint32_t otop = s->outx.p ? std::min<uint32_t>(read1(s, s->outx_top.p), (uint32_t)(s->outx.n / OUT_EXT)) : 0u;
+    std::vector<uint64_t> xo((size_t)otop * OUT_EXT);
+    if (otop) HIP_TRY(cp(xo.data(), s->outx.p, xo.size() * 8));
     HIP_TRY(hipStreamSynchronize(s->stream));
     for (uint32_t k = 0; k < count; k++) {
         psim_node_view* v = &out[k];
@@ -1895,10 +2012,15 @@ static int get_shard_nodes(Shard* s, uint32_t first, uint32_t count, psim_node_v
         memcpy(v->act, &act[(size_t)k * PSIM_ACTIVE_CAP], sizeof v->act);
         memcpy(v->pas, &pas[(size_t)k * PSIM_PASSIVE_CAP], sizeof v->pas);
         v->sent_n = x.sent_n; v->sent_head = x.sent_head; v->recv_n = x.recv_n; v->recv_head = x.recv_head;
-        memcpy(v->sent_peer, &sp[(size_t)k * PSIM_IDMAP_CAP], sizeof v->sent_peer);
-        memcpy(v->sent_id, &si[(size_t)k * PSIM_IDMAP_CAP], sizeof v->sent_id);
-        memcpy(v->recv_peer, &rp[(size_t)k * PSIM_IDMAP_CAP], sizeof v->recv_peer);
-        memcpy(v->recv_id, &ri[(size_t)k * PSIM_IDMAP_CAP], sizeof v->recv_id);
+        const uint32_t sx = x.pad1[1], rx = x.pad1[2];
+        for (uint32_t j = 0; j < PSIM_IDMAP_CAP; j++) {
+            const uint64_t e = j < IDMAP_IN ? sm[(size_t)k * IDMAP_IN + j]
+                             : sx && sx <= top ? xm[(size_t)(sx - 1) * IDMAP_EXT + j - IDMAP_IN] : 0ull;
+            const uint64_t f = j < IDMAP_IN ? rm[(size_t)k * IDMAP_IN + j]
+                             : rx && rx <= top ? xm[(size_t)(rx - 1) * IDMAP_EXT + j - IDMAP_IN] : 0ull;
+            v->sent_peer[j] = (uint32_t)e; v->sent_id[j] = (uint32_t)(e >> 32);
+            v->recv_peer[j] = (uint32_t)f; v->recv_id[j] = (uint32_t)(f >> 32);
+        }
         v->pt_all_n = x.all_n; v->pt_common_n = x.com_n; v->pt_out_n = x.out_n;
         const uint32_t* r8 = &rt[(size_t)k * RT_WORDS];
         for (int q = 0; q < PSIM_PT_ROOTS; q++) {
@@ -1910,8 +2032,10 @@ static int get_shard_nodes(Shard* s, uint32_t first, uint32_t count, psim_node_v
         memcpy(v->pt_common, &com[(size_t)k * PSIM_PT_MEMBERS_CAP], sizeof v->pt_common);
         memcpy(v->pt_eager, &eag[(size_t)k * RT_SET], sizeof v->pt_eager);
         memcpy(v->pt_lazy, &laz[(size_t)k * RT_SET], sizeof v->pt_lazy);
-        for (int j = 0; j < PSIM_PT_OUT_CAP; j++) {
-            uint64_t o = po[(size_t)k * PSIM_PT_OUT_CAP + j];
+        const uint32_t ox = x.pad1[3];
+        for (uint32_t j = 0; j < PSIM_PT_OUT_CAP; j++) {
+            const uint64_t o = j < OUT_IN ? po[(size_t)k * OUT_IN + j]
+                             : ox && ox <= otop ? xo[(size_t)(ox - 1) * OUT_EXT + j - OUT_IN] : 0ull;
             v->pt_out_peer[j] = (uint32_t)(o >> 32);
             v->pt_out_msg[j] = (uint32_t)(o >> 16) & 0xFFFFu;
             v->pt_out_round[j] = (uint32_t)o & 0xFFFFu;
@@ -2169,6 +2293,7 @@ struct SnapHead {
 };
 struct ShardHead {
     uint32_t lo, n, m_in, in_cur, pay_cur, pay_rows, pad[2];
+    uint32_t out_rows, pad2[3];     // outstanding extension rows taken
 };
 constexpr uint32_t SNAP_MAGIC = 0x4D495350u;   // "PSIM"
 
@@ -2180,13 +2305,13 @@ static std::vector<Section> snap_sections(psim_handle* h, Shard* s, const ShardH
     std::vector<Section> v = {
         {s->flags.p, N}, {s->part.p, N}, {s->hdr.p, n * sizeof(Hdr)},
         {s->act.p, n * PSIM_ACTIVE_CAP * 4}, {s->pas.p, n * PSIM_PASSIVE_CAP * 4},
-        {s->sentp.p, n * PSIM_IDMAP_CAP * 4}, {s->senti.p, n * PSIM_IDMAP_CAP * 4},
-        {s->recvp.p, n * PSIM_IDMAP_CAP * 4}, {s->recvi.p, n * PSIM_IDMAP_CAP * 4},
+        {s->sentm.p, n * IDMAP_IN * 8}, {s->recvm.p, n * IDMAP_IN * 8},
+        {s->mapx.p, (size_t)sh.pad[1] * IDMAP_EXT * 8},
         {s->pt_all.p, n * PSIM_PT_MEMBERS_CAP * 4}, {s->pt_com.p, n * PSIM_PT_MEMBERS_CAP * 4},
         {s->pt_eag.p, n * RT_SET * 4}, {s->pt_laz.p, n * RT_SET * 4}, {s->pt_rt.p, n * RT_WORDS * 4},
-        {s->pt_out.p, n * PSIM_PT_OUT_CAP * 8}, {s->start.p, n * 4},
+        {s->pt_out.p, n * OUT_IN * 8}, {s->outx.p, (size_t)sh.out_rows * OUT_EXT * 8}, {s->start.p, n * 4},
         {s->cb.p, (n + 1) * 8}, {s->bmask.p, n * 8}, {s->in_beg.p, (n + 1) * 4},
-        {s->inbox[sh.in_cur].p, (size_t)sh.m_in * sizeof(Msg)},
+        {s->inbox.p, (size_t)sh.m_in * sizeof(Msg)},
     };
     if (h->cfg.manager == PSIM_MANAGER_PLUGGABLE) {
         if (s->sview.p) v.push_back({s->sview.p, n * PSIM_SVIEW_CAP * 4});
@@ -2207,10 +2332,12 @@ int psim_snapshot(psim_handle* h, void* buf, size_t cap, size_t* need) {
     size_t total = sizeof(SnapHead) + h->started.size();
     for (Shard* s : h->shards) {
         HIP_TRY(hipStreamSynchronize(s->stream));
-        ShardHead sh{s->lo, s->n, s->m_in, (uint32_t)s->in_cur, (uint32_t)s->pay_cur, 0, {0, 0}};
+        ShardHead sh{s->lo, s->n, s->m_in, 0u, (uint32_t)s->pay_cur, 0, {0, 0}, 0, {0, 0, 0}};
         if (h->cfg.manager == PSIM_MANAGER_PLUGGABLE && s->pay_top.p)
             sh.pay_rows = read1(s, s->pay_top.p);
         sh.pad[0] = s->tomb_live ? 1u : 0u;            // full: snapshots carry remove rows
+        sh.pad[1] = s->mapx.p ? std::min<uint32_t>(read1(s, s->mapx_top.p), (uint32_t)(s->mapx.n / IDMAP_EXT)) : 0u;
+        sh.out_rows = s->outx.p ? std::min<uint32_t>(read1(s, s->outx_top.p), (uint32_t)(s->outx.n / OUT_EXT)) : 0u;
         heads.push_back(sh);
         total += sizeof(ShardHead);
         for (const Section& x : snap_sections(h, s, sh)) total += x.bytes;
@@ -2255,13 +2382,17 @@ int psim_restore(psim_handle* h, const void* buf, size_t size) {
         ShardHead sh;
         memcpy(&sh, o, sizeof sh); o += sizeof sh;
         if (sh.lo != s->lo || sh.n != s->n) return PSIM_EINVAL;
-        s->m_in = sh.m_in; s->in_cur = (int)sh.in_cur; s->pay_cur = (int)sh.pay_cur;
+        s->m_in = sh.m_in; s->pay_cur = (int)sh.pay_cur;
         s->tomb_live = sh.pad[0] != 0;
         if (s->tomb_live) h->tomb = true;
-        TRY(s->inbox[s->in_cur].ensure((size_t)sh.m_in + 1));
+        TRY(s->inbox.ensure((size_t)sh.m_in + 1));
         if (sh.pay_rows) TRY(s->pay[s->pay_cur ^ 1].ensure((size_t)sh.pay_rows * 2 * h->fw));
         if (h->cfg.manager == PSIM_MANAGER_PLUGGABLE && s->pay_top.p)
             HIP_TRY(hipMemcpy(s->pay_top.p, &sh.pay_rows, 4, hipMemcpyHostToDevice));
+        if ((size_t)sh.pad[1] * IDMAP_EXT > s->mapx.n) return PSIM_EINVAL;
+        HIP_TRY(hipMemcpy(s->mapx_top.p, &sh.pad[1], 4, hipMemcpyHostToDevice));
+        if ((size_t)sh.out_rows * OUT_EXT > s->outx.n) return PSIM_EINVAL;
+        HIP_TRY(hipMemcpy(s->outx_top.p, &sh.out_rows, 4, hipMemcpyHostToDevice));
         for (const Section& x : snap_sections(h, s, sh)) {
             if ((size_t)(end - o) < x.bytes) return PSIM_EINVAL;
             if (x.bytes) HIP_TRY(hipMemcpy(x.p, o, x.bytes, hipMemcpyHostToDevice));

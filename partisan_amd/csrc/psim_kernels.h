@@ -18,9 +18,16 @@ struct RoundArgs {
     uint8_t* flags;
     const uint8_t* part;
     Hdr* hdr;
-    uint32_t *act, *pas, *sentp, *senti, *recvp, *recvi;
+    uint32_t *act, *pas;
+    uint64_t *sentm, *recvm;    // id maps: the IDMAP_IN own entries, id << 32 | peer
+    uint64_t* mapx;             // id-map extension rows (IDMAP_EXT entries), a shared pool
+    uint32_t* mapx_top;         // pool rows taken
+    uint32_t mapx_rows;         // pool rows
     uint32_t *pt_all, *pt_com, *pt_eag, *pt_laz, *pt_rt;
-    uint64_t* pt_out;
+    uint64_t* pt_out;           // outstanding: the OUT_IN own entries
+    uint64_t* outx;             // outstanding extension rows (OUT_EXT entries), a shared pool
+    uint32_t* outx_top;
+    uint32_t outx_rows;
     // broadcasts: per local node the message id + 1 it originates this
     // round (0 = none); the message slots (id of slot k in word k, its root
     // in word PSIM_MSG_SLOTS + k, PSIM_NONE = free)

@@ -55,6 +55,10 @@ struct Pw {
 };
 
 DEV void st_add(Pw& w, int k, uint32_t v) { w.SC += lane_id() == (uint32_t)k ? v : 0u; }
+DEV void ovf(Pw& w, int kind) {                       // a fixed-table overflow of kind PSIM_OVF_*
+    const uint32_t l = lane_id();
+    w.SC += (l == (uint32_t)ST_OVF || l == (uint32_t)(ST_OVF_BY + kind)) ? 1u : 0u;
+}
 
 DEV uint32_t wave_sum(uint32_t v) {
 #pragma unroll
@@ -245,7 +249,7 @@ DEV uint32_t full_snapshot(Pw& w) {
     uint32_t s = 0;
     if (lane_id() == 0) s = atomicAdd(w.a->pay_top, 1u);
     s = rl(s, 0);
-    if (s >= w.a->pay_cap) { st_add(w, ST_OVF, 1); s = w.a->pay_cap - 1; }
+    if (s >= w.a->pay_cap) { ovf(w, PSIM_OVF_STRATEGY); s = w.a->pay_cap - 1; }
     const uint32_t fw = w.a->tomb ? 2 * w.a->fw : w.a->fw;   // adds (+ removes)
     uint32_t* dst = w.a->pay_out + (size_t)s * 2 * w.a->fw;
     for (uint32_t base = 0; base < fw; base += 256) {
@@ -297,7 +301,7 @@ DEV void full_gossip(Pw& w, uint32_t extra = NONE) {
 // sets:add_element/2 (v1, sets:to_list order) or [E | L] (v2) into a fixed table
 DEV void scamp_add(Pw& w, uint32_t& L, uint32_t& n, uint32_t e, bool as_set) {
     if (as_set && has(L, n, e)) return;
-    if (n >= PSIM_SVIEW_CAP) { st_add(w, ST_OVF, 1); return; }
+    if (n >= PSIM_SVIEW_CAP) { ovf(w, PSIM_OVF_STRATEGY); return; }
     if (as_set) view_add(L, n, e);
     else vins(L, n, 0, e);
 }

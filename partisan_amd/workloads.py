@@ -21,15 +21,21 @@ def sequential_join(n_nodes):
     return sched
 
 
-def doubling_join(n_nodes, seed):
+MAX_JOINS_PER_ROUND = 1 << 23
+
+
+def doubling_join(n_nodes, seed, max_per_round=MAX_JOINS_PER_ROUND):
     """Bootstrap ramp for large overlays: round 0 starts node 0; round r >= 1
     starts ids [2^(r-1), 2^r) and each joins a uniformly drawn node among the
-    ids started earlier (so every live node receives ~1 JOIN per round)."""
+    ids started earlier (so every live node receives ~1 JOIN per round).
+    Past max_per_round joiners a round the ramp goes on linearly (overlays
+    above 2^24 nodes: the JOIN flood of one doubling round -- ~9 records per
+    joiner -- would not fit one GPU's route buffers next to 2^26 nodes)."""
     rng = _rng(seed, 1)
     sched = [(0, np.array([0], np.uint32), np.array([NONE], np.uint32))]
     lo, r = 1, 1
     while lo < n_nodes:
-        hi = min(2 * lo, n_nodes)
+        hi = min(2 * lo, lo + max_per_round, n_nodes)
         ids = np.arange(lo, hi, dtype=np.uint32)
         contacts = rng.integers(0, lo, size=hi - lo, dtype=np.uint64).astype(np.uint32)
         sched.append((r, ids, contacts))
@@ -47,7 +53,9 @@ def star_join(n_nodes, at_round=1):
 def churn_schedule(n_nodes, seed, frac, first_round, n_rounds, protect=(0,)):
     """Config E churn: frac*N crashes spread uniformly over n_rounds starting
     at first_round; each crashed node restarts the next round and rejoins a
-    uniformly drawn node that is not crashing."""
+    uniformly drawn node that is up when the JOIN is sent (SURVEY.md section
+    8(d) E): not one of the restarting nodes, nor one crashing in that round.
+    The contacts of round k's victims are used at round k + 1."""
     rng = _rng(seed, 2)
     total = int(frac * n_nodes)
     cand = np.setdiff1d(np.arange(n_nodes, dtype=np.uint32), np.array(protect, np.uint32))
@@ -55,10 +63,12 @@ def churn_schedule(n_nodes, seed, frac, first_round, n_rounds, protect=(0,)):
     per = np.array_split(victims, n_rounds)
     out = []
     for k, v in enumerate(per):
+        down = np.concatenate([v, per[k + 1]]) if k + 1 < len(per) else v
         contacts = rng.integers(0, n_nodes, size=v.size, dtype=np.uint64).astype(np.uint32)
-        # never join yourself or someone crashing in the same round
-        bad = np.isin(contacts, v)
-        contacts[bad] = np.uint32(protect[0])
+        bad = np.isin(contacts, down)
+        while bad.any():                      # redraw (uniform over the nodes up)
+            contacts[bad] = rng.integers(0, n_nodes, size=int(bad.sum()), dtype=np.uint64).astype(np.uint32)
+            bad = np.isin(contacts, down)
         out.append((first_round + k, v, contacts))
     return out
 

@@ -2,7 +2,9 @@
 rocprofv3 kernel trace: the window opens at the STEPS-th last k_consume
 dispatch (the timed rounds come last) and each kernel's summed duration is
 divided by STEPS.  Also the window's wall span per round (gaps included).
-Usage: python profiles/steady_kernels.py run_kernel_trace.csv [--steps 50]"""
+Rounds after the window (bench's overlay drain, `--tail`, from the bench
+line's overlay.rounds_drained) are excluded.
+Usage: python profiles/steady_kernels.py run_kernel_trace.csv [--steps 50] [--tail 40]"""
 import collections
 import csv
 import sys
@@ -24,11 +26,15 @@ def main():
     steps = int(sys.argv[sys.argv.index("--steps") + 1]) if "--steps" in sys.argv else 50
     rows = list(csv.DictReader(open(path)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    tail = int(sys.argv[sys.argv.index("--tail") + 1]) if "--tail" in sys.argv else 0
     cons = [i for i, r in enumerate(rows) if "k_consume(" in r["Kernel_Name"]]
+    if tail:
+        cons = cons[:-tail]
     first = cons[-steps]
     # the window: from the end of the round before the first timed consume
+    # to the end of the last timed one
     prev = cons[-steps - 1] if len(cons) > steps else 0
-    win = rows[prev + 1:]
+    win = rows[prev + 1:cons[-1] + 1]
     tot = collections.Counter()
     calls = collections.Counter()
     for r in win:

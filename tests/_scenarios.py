@@ -7,7 +7,7 @@ from partisan_amd import workloads as W
 from partisan_amd.sim import default_config
 
 STAT_FIELDS = ["emitted", "delivered", "dropped", "nodes_up", "nodes_processed", "exits",
-               "send_fail", "first_deliveries", "overflow", "digest"]
+               "send_fail", "first_deliveries", "overflow", "overflow_by", "digest"]
 
 
 def _bcast_every(sim, period, first, root=0, count=None):
