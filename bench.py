@@ -321,7 +321,7 @@ def pmc_traffic(key):
         return None, None
     for r in recs:
         if r.get("key") == key:
-            return r["traffic_per_launch"], r.get("source")
+            return r["traffic_per_launch"], r
     return None, None
 
 
@@ -364,7 +364,8 @@ def main_strategy(args):
         state = int(st["nodes_processed"].sum()) * 2 * (64 + 4 * 64 * 2)
     alg = state + int(st["delivered"].sum()) * S_MSG + msgs * (S_MSG + 4)
     achieved = alg / (c_ms / 1e3) / 1e9 if c_ms > 0 else 0.0
-    traffic, tsrc = pmc_traffic(pmc_key(args, 1, n))
+    traffic, trec = pmc_traffic(pmc_key(args, 1, n))
+    tsrc = trec.get("source") if trec else None
     out = {
         "metric": "simulated node-rounds/sec (+ msgs/sec), pluggable manager " + args.workload,
         "value": n * args.steps / dt, "unit": "node-rounds/s", "msgs_per_sec": msgs / dt,
@@ -555,7 +556,8 @@ def main():
     per_launch_s = (c_ms / 1e3) / max(1, c_n)
     achieved = per_launch_bytes / per_launch_s / 1e9 if per_launch_s > 0 else 0.0
     key = pmc_key(args, world, n)
-    traffic, tsrc = pmc_traffic(key)
+    traffic, trec = pmc_traffic(key)
+    tsrc = trec.get("source") if trec else None
     n_bc = sum(1 for j in range(t_start, t_start + args.steps) if j % BCAST_PERIOD == 0)
     out = {
         "metric": "simulated node-rounds/sec (+ msgs/sec), 1M-node HyParView+Plumtree"
@@ -579,6 +581,7 @@ def main():
                                    f"1 GPU, {args.vshards} virtual shards" if args.vshards > 1 else "1 GPU")},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": tsrc,
+                     "traffic_upper": trec.get("traffic_upper_per_launch") if trec else None,
                      "kernel": "k_relay + k_consume + k_pt (the node-round phase: one launch of each per round, "
                                "timed from k_relay's first block to the last block of k_consume or k_pt)",
                      "alg_bytes_per_launch": per_launch_bytes,

@@ -1359,14 +1359,18 @@ DEV void body_pt(Wv& w, const PtIn& x) {
             uint32_t type = rl(R4, b + 2) & 0xFF;
             if (type < PSIM_MSG_PT_BROADCAST || type > PSIM_MSG_PT_GRAFT) continue;
             st_add(w, ST_DELIV + type, 1);
+            STAMP(w, 29);
             pt_handle(w, type, rl(R4, b + 1), rl(R4, b + 4), rl(R4, b + 5), rl(R4, b + 6));
+            STAMP(w, 16 + type - PSIM_MSG_PT_BROADCAST);
         }
     }
+    STAMP(w, 29);
     if (x.tf & DESC_ORIGIN) {                         // pt:282-287, backend:179-200
         const uint32_t my = n | PSIM_MAP_BIT, msg = uni(a.origin[n - a.lo]) - 1;
         pt_mark(w, msg);
         if (msg == a.tracked_msg) { w.trk_round = r; w.trk_hop = 0; }
         pt_push(w, msg, 0, my, my);
+        STAMP(w, 21);
     }
     if ((x.tf & DESC_LAZY) && w.out_n > 0) {          // pt:341-345, :443-453
         for (uint32_t i = 0; i < w.out_n; i++) {
@@ -1375,6 +1379,7 @@ DEV void body_pt(Wv& w, const PtIn& x) {
             if (!pt_conn(w, peer)) { st_add(w, ST_FAIL, 1); continue; }
             emit(w, peer & ~PSIM_MAP_BIT, PSIM_MSG_PT_IHAVE, 0, msg, (uint32_t)o & 0xFFFFu, msg_root(w, msg), 0, 0);
         }
+        STAMP(w, 22);
     }
 }
 
@@ -1391,7 +1396,10 @@ DEV void writeback_pt(Wv& w) {
     if (w.seq != w.flushed) flush_recs(w);
 }
 
-__global__ void __launch_bounds__(256) k_pt(RoundArgs args) {
+#ifndef PSIM_PT_WAVES
+#define PSIM_PT_WAVES 4
+#endif
+__global__ void __launch_bounds__(256, PSIM_PT_WAVES) k_pt(RoundArgs args) {
     __shared__ uint64_t sst[NST];
     __shared__ uint32_t scratch[WAVES_PER_BLOCK][64];
     __shared__ __attribute__((aligned(16))) uint32_t srecs[WAVES_PER_BLOCK][STAGE * 16];
@@ -1428,15 +1436,21 @@ __global__ void __launch_bounds__(256) k_pt(RoundArgs args) {
         PtIn xn = load_pt_node(args, load_desc(args, min(gw + nw, last)));
         uint32_t d = load_desc(args, min(gw + 2 * nw, last));
         for (uint32_t i = gw; i < na; i += nw) {
+            STAMP(w, 31);
             begin_pt(w, x, y);
+            STAMP(w, 29);
             body_pt(w, x);
             PtX yn = load_pt_x(args, xn);
             writeback_pt(w);
+            STAMP(w, 30);
             PtIn xnn = load_pt_node(args, d);
             d = load_desc(args, min(i + 3 * nw, last));
             x = xn; y = yn; xn = xnn;
         }
     }
+#ifdef PSIM_STAMPS
+    if (lane_id() < 32) atomicAdd(&g_stamps[lane_id()], (unsigned long long)w.stl[lane_id()]);
+#endif
     flush_wave_stats(w, sst);
     __syncthreads();
     for (int i = threadIdx.x; i < NST; i += blockDim.x)
@@ -1447,12 +1461,12 @@ __global__ void __launch_bounds__(256) k_pt(RoundArgs args) {
 // ------------------------------------------------ relays and lazy ticks --
 // k_relay gives every node with work one lane and sorts it: most nodes with
 // work in a steady-state round do little for HyParView -- at most relay the
-// one SHUFFLE of their inbox (hv:1095-1136 with TTL > 0 and |active| > 1: a
+// SHUFFLEs of their inbox (hv:1095-1136 with TTL > 0 and |active| > 1: a
 // select_random over active -- [Sender, Myself], then do_send_message) --
 // and such a lane does it here, exactly as k_consume's body and writeback
 // would (the same draws, records, sequence numbers, digest and stats).  A
-// node with more HyParView work (other messages, a due timer that can act,
-// a join, a crash round) goes to k_consume's list.  A node with Plumtree
+// node with more HyParView work (another message type, a due timer that can
+// act, a join, a crashed active member) goes to k_consume's list.  A node with Plumtree
 // work (Plumtree messages, an origin, a due lazy tick with entries
 // outstanding) goes to k_pt's list -- unless its only Plumtree work is the
 // lazy tick and its HyParView work is done here: then the lane runs the
@@ -1496,7 +1510,7 @@ DEV void block_append(bool go, const uint4& D, uint4* desc, uint32_t* cnt, uint3
 }
 
 __global__ void __launch_bounds__(256) k_relay(RoundArgs a) {
-    enum { R_PROC, R_DELIV, R_SHUF, R_IHAVE, R_FAIL, R_DIGEST, R_OVF, R_BOUND, R_N };
+    enum { R_PROC, R_DELIV, R_SHUF, R_IHAVE, R_FAIL, R_DIGEST, R_OVF, R_BOUND, R_DIH, R_DIGN, R_EIGN, R_N };
     __shared__ unsigned long long sst[R_N];
     __shared__ uint32_t sslots[2 * PSIM_MSG_SLOTS];
     for (int i = threadIdx.x; i < 2 * PSIM_MSG_SLOTS; i += blockDim.x) sslots[i] = a.slots[i];
@@ -1507,14 +1521,13 @@ __global__ void __launch_bounds__(256) k_relay(RoundArgs a) {
     const uint32_t l = lane_id();
     const uint32_t na = *a.n_alist;
     const uint64_t two58 = 1ull << 58;
-    unsigned long long v[R_N] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long v[R_N] = {};
     for (uint32_t base = blockIdx.x * blockDim.x; base < na; base += gridDim.x * blockDim.x) {
         const uint32_t P = base + threadIdx.x;
         uint4 D = make_uint4(0, 0, 0, 0);
-        bool heavy = false, to_pt = false, relay = false, lazy_here = false, maps = false;
+        bool heavy = false, to_pt = false, relay = false, pt_lane = false, maps = false;
         Hdr h;
-        uint32_t ik = 0, ttl = 0, nex = 0, src = 0, hv_at = 0;
-        const Msg* rp = nullptr;
+        uint32_t ik = 0;
         uint4 act0 = make_uint4(0, 0, 0, 0), act1 = act0;
         uint32_t me_part = 0;
         if (P < na) {
@@ -1529,14 +1542,24 @@ __global__ void __launch_bounds__(256) k_relay(RoundArgs a) {
             act0 = ar[0];
             act1 = ar[1];
             me_part = a.part[id];
-            // the inbox: how many HyParView messages, and the first of them
-            uint32_t hvn = 0, hv_tt = 0;
+            // the inbox: how many HyParView messages, and whether each is a
+            // SHUFFLE with TTL left (a relay while |active| > 1)
+            uint32_t hvn = 0;
+            bool all_relay = true, pt_light = true;
             for (uint32_t j = 0; j < ik; j++) {
-                const uint32_t tt = a.rec_in[D.y + j].tt;
-                if ((tt & 0xFF) < PSIM_MSG_PT_BROADCAST) {
-                    if (!hvn) { hv_at = j; hv_tt = tt; }
+                const Msg& m = a.rec_in[D.y + j];
+                const uint32_t tt = m.tt, type = tt & 0xFF;
+                if (type < PSIM_MSG_PT_BROADCAST) {
                     hvn++;
-                    maps |= (tt & 0xFF) <= PSIM_MSG_NEIGHBOR_ACCEPTED;   // id maps (hv:703-1089)
+                    maps |= type <= PSIM_MSG_NEIGHBOR_ACCEPTED;   // id maps (hv:703-1089)
+                    all_relay &= type == PSIM_MSG_SHUFFLE && ((tt >> 8) & 0xFF) > 0;
+                } else if (type == PSIM_MSG_PT_IHAVE) {
+                    // an IHAVE of a delivered (or retired: stale) id only
+                    // answers IGNORED_IHAVE (pt:380-386)
+                    const uint32_t k = m.a0 % PSIM_MSG_SLOTS;
+                    pt_light &= sslots[k] != m.a0 || (((k < 32 ? h.have : h.aux) >> (k & 31)) & 1u);
+                } else {
+                    pt_light &= type == PSIM_MSG_PT_IGNORED_IHAVE;   // an ack (pt:304-307)
                 }
             }
             const bool fresh = h.start_round == a.round;
@@ -1547,20 +1570,18 @@ __global__ void __launch_bounds__(256) k_relay(RoundArgs a) {
                 for (int j = 0; j < 8; j++)
                     exits |= (uint32_t)j < h.act_n && av[j] != id && av[j] < a.n_nodes && (a.flags[av[j]] & F_CRASHED);
             }
-            heavy = exits || fresh || (tf & DESC_SHUFFLE) || ((tf & DESC_PROMO) && h.act_n < a.min_active) || hvn > 1;
+            heavy = exits || fresh || (tf & DESC_SHUFFLE) || ((tf & DESC_PROMO) && h.act_n < a.min_active) ||
+                    (hvn && !(all_relay && h.act_n > 1));
             maps = maps || exits || (tf & DESC_PROMO);        // move_to_active: current_id
-            if (!heavy && hvn == 1) {
-                ttl = (hv_tt >> 8) & 0xFF;
-                nex = (hv_tt >> 16) & 0xFF;
-                relay = h.act_n > 1 && (hv_tt & 0xFF) == PSIM_MSG_SHUFFLE && ttl > 0;
-                heavy = !relay;
-            }
+            relay = !heavy && hvn > 0;
             const bool pt_msgs = !fresh && ik > hvn, origin = (tf & DESC_ORIGIN) != 0;
             const bool lazy = (tf & DESC_LAZY) && h.out_n > 0;
-            to_pt = a.plumtree && (pt_msgs || origin || (heavy && lazy));
-            lazy_here = !heavy && !to_pt && lazy;
-            relay = relay && !heavy;
-            if (!heavy && (relay || to_pt || lazy_here)) v[R_PROC]++;   // (k_consume counts its own)
+            // the Plumtree phase runs in the lane when the node's HyParView
+            // phase does and its Plumtree work is IHAVE answers, acks and the
+            // lazy tick; else in k_pt (after k_consume for a heavy node)
+            pt_lane = a.plumtree && !heavy && !origin && (pt_msgs ? pt_light : lazy);
+            to_pt = a.plumtree && (pt_msgs || origin || (heavy && lazy)) && !pt_lane;
+            if (!heavy && (relay || to_pt || pt_lane)) v[R_PROC]++;   // (k_consume counts its own)
         }
         block_append(P < na && heavy, maps ? make_uint4(D.x, D.y, D.z | DESC_MAPS_BIT, D.w) : D, a.desc_slow, a.n_slow,
                      wcnt);
@@ -1571,9 +1592,11 @@ __global__ void __launch_bounds__(256) k_relay(RoundArgs a) {
         const uint32_t A[8] = {act0.x, act0.y, act0.z, act0.w, act1.x, act1.y, act1.z, act1.w};
         uint64_t rng = h.rng;
         uint32_t seq = 0;
-        if (relay) {
-            rp = a.rec_in + D.y + hv_at;
-            src = rp->src;
+        for (uint32_t jr = 0; relay && jr < ik; jr++) {  // the SHUFFLE relays, in inbox order
+            const Msg* rp = a.rec_in + D.y + jr;
+            const uint32_t tt = rp->tt;
+            if ((tt & 0xFF) >= PSIM_MSG_PT_BROADCAST) continue;
+            const uint32_t ttl = (tt >> 8) & 0xFF, nex = (tt >> 16) & 0xFF, src = rp->src;
             v[R_DELIV]++;
             // select_random(Active, [Sender, Myself]) (hv:1346-1356)
             uint32_t elig = 0;
@@ -1599,8 +1622,8 @@ __global__ void __launch_bounds__(256) k_relay(RoundArgs a) {
                     uint32_t X[8] = {e0.x, e0.y, e0.z, e0.w, e1.x, e1.y, e1.z, e1.w};
 #pragma unroll
                     for (int j = 0; j < 8; j++) X[j] = (uint32_t)j < nex ? X[j] : 0u;
-                    v[R_DIGEST] += relay_emit(a, D.w, r, id, PSIM_MSG_SHUFFLE | ((ttl - 1) << 8) | (nex << 16), seq,
-                                              0u, 0u, 0u, X);
+                    v[R_DIGEST] += relay_emit(a, D.w + seq, r, id, PSIM_MSG_SHUFFLE | ((ttl - 1) << 8) | (nex << 16),
+                                              seq, 0u, 0u, 0u, X);
                     seq++;
                     v[R_SHUF]++;
                 } else {
@@ -1608,13 +1631,60 @@ __global__ void __launch_bounds__(256) k_relay(RoundArgs a) {
                 }
             }
         }
-        if (lazy_here) {                              // send_lazy: every outstanding entry, in order
+        uint32_t out_n = h.out_n;
+        if (pt_lane) {
             const uint32_t X[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-            // the rows in chunks of 4 entries (two 16-B loads in flight at
-            // once): the node's own, then its extension row
-            const uint64_t* own = a.pt_out + li * OUT_IN;
-            const uint64_t* ext = a.outx + (size_t)(h.pad1[3] ? h.pad1[3] - 1 : 0) * OUT_EXT;
-            for (uint32_t i0 = 0; i0 < h.out_n; i0 += 4) {
+            uint64_t* own = a.pt_out + li * OUT_IN;   // outstanding: own row, then the extension row
+            uint64_t* ext = a.outx + (size_t)(h.pad1[3] ? h.pad1[3] - 1 : 0) * OUT_EXT;
+            // the Plumtree inbox in canonical order: IHAVE -> IGNORED_IHAVE
+            // over an active connection (pt:380-386, send/3 pt:633-638),
+            // IGNORED_IHAVE -> the outstanding entry acked (pt:562-567)
+            uint64_t gone = 0;
+            for (uint32_t j = 0; j < ik; j++) {
+                const Msg* rp = a.rec_in + D.y + j;
+                const uint32_t tt = rp->tt, type = tt & 0xFF;
+                if (type < PSIM_MSG_PT_BROADCAST) continue;
+                const uint32_t p = rp->src, msg = rp->a0, rnd = rp->a1;
+                if (type == PSIM_MSG_PT_IHAVE) {
+                    v[R_DIH]++;
+                    v[R_OVF] += sslots[msg % PSIM_MSG_SLOTS] != msg ? 1u : 0u;   // a retired id (pt_have)
+                    bool in = false;
+#pragma unroll
+                    for (int q = 0; q < 8; q++) in |= q < h.act_n && A[q] == p;
+                    if (in && p != id && p < a.n_nodes && (a.flags[p] & F_UP) && a.part[p] == me_part) {
+                        v[R_DIGEST] += relay_emit(a, D.w + seq, p, id, PSIM_MSG_PT_IGNORED_IHAVE, seq, msg, rnd, rp->a2, X);
+                        seq++;
+                        v[R_EIGN]++;
+                    } else {
+                        v[R_FAIL]++;
+                    }
+                } else {
+                    v[R_DIGN]++;
+                    const uint64_t key = ((uint64_t)(p | PSIM_MAP_BIT) << 32) | (msg << 16) | (rnd & 0xFFFFu);
+                    for (uint32_t e = 0; e < out_n; e++)
+                        if (!((gone >> e) & 1u) && (e < OUT_IN ? own[e] : ext[e - OUT_IN]) == key) {
+                            gone |= 1ull << e;
+                            break;
+                        }
+                }
+            }
+            if (gone) {                               // the acked entries out, order kept
+                uint32_t k = 0;
+                for (uint32_t e = 0; e < out_n; e++) {
+                    if ((gone >> e) & 1u) continue;
+                    if (k != e) {
+                        const uint64_t o = e < OUT_IN ? own[e] : ext[e - OUT_IN];
+                        (k < OUT_IN ? own[k] : ext[k - OUT_IN]) = o;
+                    }
+                    k++;
+                }
+                for (uint32_t e = k; e < out_n; e++) (e < OUT_IN ? own[e] : ext[e - OUT_IN]) = 0ull;
+                out_n = k;
+                reinterpret_cast<uint32_t*>(a.hdr + li)[11] = out_n << 16;   // Hdr word 11: out_n
+            }
+            // the lazy tick: an IHAVE per outstanding entry, in order (send_lazy
+            // pt:443-453) -- rows in chunks of 4 entries, two 16-B loads in flight
+            for (uint32_t i0 = 0; ((D.z >> 28) & DESC_LAZY) && i0 < out_n; i0 += 4) {
                 const uint4* orow = reinterpret_cast<const uint4*>(i0 < OUT_IN ? own + i0 : ext + (i0 - OUT_IN));
                 const uint4 q0 = orow[0], q1 = orow[1];
                 const uint64_t O[4] = {((uint64_t)q0.y << 32) | q0.x, ((uint64_t)q0.w << 32) | q0.z,
@@ -1626,9 +1696,9 @@ __global__ void __launch_bounds__(256) k_relay(RoundArgs a) {
                     bool x = false;
 #pragma unroll
                     for (int j = 0; j < 8; j++) x |= j < h.act_n && A[j] == p;
-                    in[c] = x && p != id && i0 + c < h.out_n;
+                    in[c] = x && p != id && i0 + c < out_n;
                 }
-                for (int c = 0; c < 4 && i0 + c < h.out_n; c++) {
+                for (int c = 0; c < 4 && i0 + c < out_n; c++) {
                     const uint64_t o = O[c];
                     const uint32_t p = (uint32_t)(o >> 32) & ~PSIM_MAP_BIT;
                     if (!(in[c] && p < a.n_nodes && (a.flags[p] & F_UP) && a.part[p] == me_part)) {
@@ -1651,8 +1721,8 @@ __global__ void __launch_bounds__(256) k_relay(RoundArgs a) {
         v[R_BOUND] += seq > a.obase[li + 1] - D.w ? 1u : 0u;
         if (!to_pt) {                                 // (k_pt writes the byte of its nodes)
             const uint8_t fl = a.flags[id];
-            a.flags[id] = (uint8_t)((fl & (F_UP | F_CRASHED)) | (h.out_n ? F_LAZY : 0) |
-                                    (min((uint32_t)h.out_n, 15u) << F_OUTN_SHIFT) |
+            a.flags[id] = (uint8_t)((fl & (F_UP | F_CRASHED)) | (out_n ? F_LAZY : 0) |
+                                    (min(out_n, 15u) << F_OUTN_SHIFT) |
                                     (h.act_n < a.min_active ? F_LOWACT : 0));
         }
     }
@@ -1669,7 +1739,9 @@ __global__ void __launch_bounds__(256) k_relay(RoundArgs a) {
         row[k] = k == ST_PROC ? sst[R_PROC] : k == ST_DELIV + PSIM_MSG_SHUFFLE ? sst[R_DELIV]
                : k == ST_EMIT + PSIM_MSG_SHUFFLE ? sst[R_SHUF] : k == ST_EMIT + PSIM_MSG_PT_IHAVE ? sst[R_IHAVE]
                : k == ST_FAIL ? sst[R_FAIL] : k == ST_DIGEST ? sst[R_DIGEST] : k == ST_OVF ? sst[R_OVF]
-               : k == ST_OVF_BY + PSIM_OVF_PT ? sst[R_OVF] : k == ST_BOUND ? sst[R_BOUND] : 0ull;
+               : k == ST_OVF_BY + PSIM_OVF_PT ? sst[R_OVF] : k == ST_BOUND ? sst[R_BOUND]
+               : k == ST_DELIV + PSIM_MSG_PT_IHAVE ? sst[R_DIH] : k == ST_DELIV + PSIM_MSG_PT_IGNORED_IHAVE ? sst[R_DIGN]
+               : k == ST_EMIT + PSIM_MSG_PT_IGNORED_IHAVE ? sst[R_EIGN] : 0ull;
 }
 
 // one wave-slot per resident wave: the grid strides over the active list

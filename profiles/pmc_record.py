@@ -1,0 +1,61 @@
+"""HBM traffic record of the node-round kernels for one bench.py command,
+from a FETCH_SIZE pass and a WRITE_SIZE pass of that same command
+(profiles/run_pmc.sh).  Appends / replaces the record in
+profiles/pmc_records.json, which bench.py reads back by its pmc_key.
+
+Window: the `steps` timed rounds are the dispatches of each kernel before the
+overlay-drain rounds bench.py runs after its window (overlay.rounds_drained).
+Per round: the sum over k_relay, k_consume and k_pt.
+
+Units and corrections (profiles/calib/, measured on this MI355X): FETCH_SIZE
+counts 64-B memory requests -- a random dword or a random 64-B record reads as
+exactly 64 B, a fully coalesced 16-B-per-lane stream as half its bytes (128-B
+requests tallied at 64 B, the guide's x2).  The node-round kernels read
+random rows and records, so `traffic` = FETCH_SIZE + WRITE_SIZE (the
+random-access calibration) and `traffic_upper` = 2 x FETCH_SIZE + WRITE_SIZE
+(every read a 128-B request).
+Usage: python profiles/pmc_record.py BENCH_JSON FETCH_CSV WRITE_CSV"""
+import csv
+import json
+import os
+import sys
+
+KERNELS = ("k_relay(", "k_consume(", "k_pt(")
+
+
+def per_round(path, steps, tail):
+    rows = list(csv.DictReader(open(path)))
+    tot = 0.0
+    for k in KERNELS:
+        kr = [r for r in rows if k in r["Kernel_Name"]]
+        ids = sorted({int(r["Dispatch_Id"]) for r in kr})
+        keep = set(ids[len(ids) - tail - steps:len(ids) - tail])
+        tot += sum(float(r["Counter_Value"]) for r in kr if int(r["Dispatch_Id"]) in keep)
+    return tot * 1024 / steps          # KiB -> bytes, per round
+
+
+def main():
+    bench = json.load(open(sys.argv[1]))
+    steps, tail = bench["steps"], bench["overlay"]["rounds_drained"]
+    fetch = per_round(sys.argv[2], steps, tail)
+    write = per_round(sys.argv[3], steps, tail)
+    rec = {"key": bench["pmc_key"],
+           "traffic_per_launch": fetch + write,
+           "traffic_upper_per_launch": 2 * fetch + write,
+           "fetch_size_bytes": fetch, "write_size_bytes": write,
+           "alg_bytes_per_launch": bench["roofline"]["alg_bytes_per_launch"],
+           "source": "FETCH_SIZE + WRITE_SIZE per timed round of k_relay + k_consume + k_pt, separate "
+                     "rocprofv3 --pmc passes of this command (profiles/run_pmc.sh); FETCH_SIZE uncorrected: "
+                     "random 64-B requests count exactly (profiles/calib/)"}
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "pmc_records.json")
+    try:
+        recs = json.load(open(path))
+    except (OSError, ValueError):
+        recs = []
+    recs = [r for r in recs if r.get("key") != rec["key"]] + [rec]
+    json.dump(recs, open(path, "w"), indent=1)
+    print(json.dumps(rec))
+
+
+if __name__ == "__main__":
+    main()

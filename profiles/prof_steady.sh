@@ -11,5 +11,5 @@ cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace -d $O/trace -o run --output-format csv -- python3 $R/bench.py --no-cpu-baseline --steps 20 --warmup 5 "$@" > $O/bench.json 2> $O/prof.err || { echo PROF FAILED; tail -20 $O/prof.err; exit 1; }
 cd $R
 TAIL=$(python -c "import json,sys; print(json.load(open(sys.argv[1]))['overlay']['rounds_drained'])" $O/bench.json)
-python profiles/steady_kernels.py $(find $O/trace -name "*kernel_trace.csv" | head -1) --steps 20 --tail $TAIL > $O/steady.txt && cat $O/steady.txt
+python profiles/steady_kernels.py $(find $O/trace -name "*kernel_trace.csv" | head -1) --steps 20 --tail $TAIL --per-round > $O/steady.txt && cat $O/steady.txt
 gzip -f $(find $O/trace -name "*kernel_trace.csv")

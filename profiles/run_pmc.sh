@@ -1,21 +1,23 @@
 #!/bin/bash
-# SQ/TCC counter passes over bench.py (one pass per counter group; each pass
-# its own run, as rocprofv3 does not split counters over passes).
-# Usage (GPU box, repo root): bash profiles/run_pmc.sh TAG [bench args]
+# HBM traffic of the node-round kernels for ONE bench.py command: a
+# FETCH_SIZE pass and a WRITE_SIZE pass (each its own run: rocprofv3 does not
+# split counters over passes), then profiles/pmc_record.py files the record
+# under the command's pmc_key in profiles/pmc_records.json (copied back via
+# gpurun_out/).  Usage (GPU box, repo root):
+#   bash profiles/run_pmc.sh TAG [bench args, e.g. --steps 20 --warmup 5]
 TAG=$1; shift
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/pmc_$TAG
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
-pass() {
-  name=$1; shift
-  timeout -s KILL 120 rocprofv3 --pmc "$@" -d $OUT/$name -o run --output-format csv -- python3 $R/bench.py --no-cpu-baseline --steps 10 --warmup 3 > $OUT/$name.json 2> $OUT/$name.err || { echo "$name failed"; tail -3 $OUT/$name.err; exit 1; }
-}
-pass p1 SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY
-pass p2 SQ_WAIT_INST_ANY SQ_BUSY_CYCLES SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_MISC
-pass p3 FETCH_SIZE
-pass p4 WRITE_SIZE
-python3 $R/profiles/pmc_summary.py $OUT/p1 $OUT/p2 $OUT/p3 $OUT/p4 --rounds 10 > $OUT/summary.txt
-cat $OUT/summary.txt
-rm -rf $OUT/p1 $OUT/p2 $OUT/p3 $OUT/p4      # keep gpurun_out small (<64 MiB merges back)
-echo pmc done
+for c in FETCH_SIZE WRITE_SIZE; do
+  timeout -s KILL 300 rocprofv3 --pmc $c --kernel-include-regex "k_relay|k_consume|k_pt" -d $OUT/$c -o run \
+    --output-format csv -- python3 $R/bench.py --no-cpu-baseline "$@" > $OUT/$c.json 2> $OUT/$c.err \
+    || { echo "$c pass failed"; tail -3 $OUT/$c.err; exit 1; }
+done
+cd $R
+python3 profiles/pmc_record.py $OUT/FETCH_SIZE.json $(find $OUT/FETCH_SIZE -name "*counter_collection.csv" | head -1) \
+  $(find $OUT/WRITE_SIZE -name "*counter_collection.csv" | head -1) > $OUT/record.json || exit 1
+cp profiles/pmc_records.json $OUT/pmc_records.json
+cat $OUT/record.json
+rm -rf $OUT/FETCH_SIZE $OUT/WRITE_SIZE

@@ -16,7 +16,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 NAMES = {0: "idle-node", 1: "setup+loads", 2: "join+exits", 3: "inbox-chunk/misc",
          13: "promotion", 14: "shuffle", 15: "notify-replay", 21: "origin",
          22: "lazy-tick", 23: "writeback", 24: "loop", 25: "shuffle:forward",
-         26: "shuffle:accept-sublist", 27: "shuffle:accept-reply", 28: "shuffle:accept-merge"}
+         26: "shuffle:accept-sublist", 27: "shuffle:accept-reply", 28: "shuffle:accept-merge",
+         29: "k_pt setup/inbox-misc", 30: "k_pt writeback", 31: "k_pt loop"}
 HV = ["JOIN", "FWD_JOIN", "NEIGHBOR", "DISCONNECT", "NEIGHBOR_REQ", "NEIGHBOR_ACC",
       "NEIGHBOR_REJ", "SHUFFLE", "SHUFFLE_REPLY"]
 PT = ["BROADCAST", "PRUNE", "IHAVE", "IGNORED_IHAVE", "GRAFT"]

@@ -46,6 +46,16 @@ def main():
     print(f"timed rounds {steps}: wall {span / steps / 1e6:.4f} ms/round, kernels {busy / steps / 1e6:.4f} ms/round")
     for k, t in tot.most_common():
         print(f"  {k:40s} {calls[k] / steps:5.1f}/round {t / steps / 1e3:9.1f} us/round")
+    if "--per-round" in sys.argv:                 # the node-round kernels of each timed round
+        print("per round (us): k_relay k_consume k_pt")
+        cur = {}
+        for r in win:
+            k = short(r["Kernel_Name"]).replace("psim::", "")
+            if k in ("k_relay", "k_consume", "k_pt"):
+                cur[k] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+                if k == "k_pt" or (k == "k_consume" and "k_pt" not in cur and False):
+                    print(f"  {cur.get('k_relay', 0):7.1f} {cur.get('k_consume', 0):7.1f} {cur.get('k_pt', 0):7.1f}")
+                    cur = {}
     _ = first
 
 
