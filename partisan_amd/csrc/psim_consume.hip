@@ -666,6 +666,66 @@ DEV void pt_send(Wv& w, uint32_t ident, uint32_t type, uint32_t msg, uint32_t rn
     emit(w, ident & ~PSIM_MAP_BIT, type, 0, msg, rnd, root, 0, 0);
 }
 
+// Batched sends of one handler: the lanes of `cand` (ascending = the
+// reference's list order) each hold a peer identity; returns the lanes whose
+// send/3 finds a connection -- the peer in the active view, running, same
+// partition (k_pt's cache lanes 32-39 are its active view) -- and counts a
+// send failure for each of the others.
+DEV uint64_t pt_conn_mask(Wv& w, uint64_t cand, uint32_t IDENT) {
+    const uint32_t l = lane_id(), id = IDENT & ~PSIM_MAP_BIT;
+    uint32_t fl = 0;
+    bool in = false;
+    for (uint32_t j = 0; j < w.act_n; j++) {          // (has/3 + the cache lookup of connect_ok)
+        const uint32_t aj = rl(w.A, j), cj = rl(w.CF, 32 + j);
+        const bool hit = aj == id;
+        in |= hit;
+        fl = hit ? cj : fl;
+    }
+    const bool ok = ((cand >> l) & 1ull) && in && id != w.me && id < w.a->n_nodes && (fl & F_UP) &&
+                    (fl >> 8) == w.mypart;
+    const uint64_t m = ballot(ok);
+    st_add(w, ST_FAIL, popc(cand) - popc(m));
+    return m;
+}
+
+// emit() for the lanes of `m` at once, in ascending lane order: record k
+// takes dst (and, PER_LANE, a0 / a1 / a2) from the k-th lane of m; four
+// records per wave step through the staging buffer (same words, digest, keys
+// and stats as k emit() calls)
+template <bool PER_LANE>
+DEV void emit_batch(Wv& w, uint64_t m, uint32_t type, uint32_t DST, uint32_t A0, uint32_t A1, uint32_t A2) {
+    const uint32_t n = popc(m);
+    if (!n) return;
+    const uint32_t l = lane_id(), j = l & 15, r = l >> 4;
+    for (uint64_t rem = m; rem;) {
+        // the next (up to) four records: lanes s0..s3 of m
+        int s[4];
+        uint32_t c = 0;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            s[q] = rem ? ffs64(rem) : s[q > 0 ? q - 1 : 0];
+            c += rem ? 1u : 0u;
+            rem &= rem - 1;
+        }
+        uint32_t staged = w.seq - w.flushed;
+        if (staged + c > STAGE) { flush_recs(w); staged = 0; }
+        const int src = r == 0 ? s[0] : r == 1 ? s[1] : r == 2 ? s[2] : s[3];
+        const uint32_t dk = shfl(DST, src);
+        const uint32_t b0 = PER_LANE ? shfl(A0, src) : A0, b1 = PER_LANE ? shfl(A1, src) : A1;
+        const uint32_t b2 = PER_LANE ? shfl(A2, src) : A2;
+        const uint32_t word = j == 0 ? dk : j == 1 ? w.me : j == 2 ? type : j == 3 ? w.seq + r
+                            : j == 4 ? b0 : j == 5 ? b1 : j == 6 ? b2 : 0u;
+        if (r < c) {
+            w.srec[(staged + r) * 16 + j] = word;
+            w.digest += (uint64_t)word * digest_mul(j);
+            if (j == 0) w.skey[staged + r] = dk | (max_emit(type) << KEY_DST_BITS);
+        }
+        w.seq += c;
+        if (staged + c == STAGE) flush_full(w);
+    }
+    st_add(w, ST_EMIT + type, n);
+}
+
 DEV void pt_add_out(Wv& w, uint32_t peer, uint32_t msg, uint32_t rnd) {   // pt:574-579
     uint32_t l = lane_id();
     uint64_t key = ((uint64_t)peer << 32) | (msg << 16) | (rnd & 0xFFFFu);
@@ -689,19 +749,17 @@ DEV void pt_push(Wv& w, uint32_t msg, uint32_t rnd, uint32_t root, uint32_t from
         const uint32_t ce = rt_word(w, RT_EN), cl = rt_word(w, RT_LN);
         const uint32_t be = rt_off(ce, (uint32_t)k), bl = rt_off(cl, (uint32_t)k);
         const uint32_t ne = (ce >> (8 * k)) & 0xFFu, nl = (cl >> (8 * k)) & 0xFFu;
-        for (uint32_t i = 0; i < ne; i++) {
-            uint32_t e = rl(w.EAG, be + i);
-            if (e != from) pt_send(w, e, PSIM_MSG_PT_BROADCAST, msg, rnd, root);
-        }
+        // the eager sends, batched (entries of the slot: lanes be .. be + ne)
+        const uint32_t l = lane_id();
+        const uint64_t cand = ballot(l >= be && l < be + ne && w.EAG != from);
+        emit_batch<false>(w, pt_conn_mask(w, cand, w.EAG), PSIM_MSG_PT_BROADCAST, w.EAG & ~PSIM_MAP_BIT, msg, rnd, root);
         for (uint32_t i = 0; i < nl; i++) {
             uint32_t e = rl(w.LAZ, bl + i);
             if (e != from) pt_add_out(w, e, msg, rnd);
         }
     } else {
-        for (uint32_t i = 0; i < w.com_n; i++) {
-            uint32_t e = rl(w.COM, i);
-            if (e != from) pt_send(w, e, PSIM_MSG_PT_BROADCAST, msg, rnd, root);
-        }
+        const uint64_t cand = ballot(lane_id() < w.com_n && w.COM != from);
+        emit_batch<false>(w, pt_conn_mask(w, cand, w.COM), PSIM_MSG_PT_BROADCAST, w.COM & ~PSIM_MAP_BIT, msg, rnd, root);
     }
 }
 
@@ -1373,12 +1431,19 @@ DEV void body_pt(Wv& w, const PtIn& x) {
         STAMP(w, 21);
     }
     if ((x.tf & DESC_LAZY) && w.out_n > 0) {          // pt:341-345, :443-453
-        for (uint32_t i = 0; i < w.out_n; i++) {
-            uint64_t o = rl64(w.OUT, i);
-            const uint32_t peer = (uint32_t)(o >> 32), msg = (uint32_t)(o >> 16) & 0xFFFFu;
-            if (!pt_conn(w, peer)) { st_add(w, ST_FAIL, 1); continue; }
-            emit(w, peer & ~PSIM_MAP_BIT, PSIM_MSG_PT_IHAVE, 0, msg, (uint32_t)o & 0xFFFFu, msg_root(w, msg), 0, 0);
-        }
+        // an IHAVE per outstanding entry (lane e: entry e), batched; the
+        // root of a sent entry's id from its slot (a retired id: overflow,
+        // PSIM_NONE)
+        const uint32_t l = lane_id();
+        const uint32_t peer = (uint32_t)(w.OUT >> 32), msg = ((uint32_t)w.OUT >> 16) & 0xFFFFu;
+        const uint64_t ok = pt_conn_mask(w, ballot(l < w.out_n), peer);
+        const uint32_t sk = msg % PSIM_MSG_SLOTS;
+        const bool live = w.slots[sk] == msg;
+        const uint32_t root = live ? w.slots[PSIM_MSG_SLOTS + sk] : NONE;
+        const uint32_t dead = popc(ok & ballot(!live));
+        st_add(w, ST_OVF, dead);
+        st_add(w, ST_OVF_BY + PSIM_OVF_PT, dead);
+        emit_batch<true>(w, ok, PSIM_MSG_PT_IHAVE, peer & ~PSIM_MAP_BIT, msg, (uint32_t)w.OUT & 0xFFFFu, root);
         STAMP(w, 22);
     }
 }
@@ -1397,7 +1462,7 @@ DEV void writeback_pt(Wv& w) {
 }
 
 #ifndef PSIM_PT_WAVES
-#define PSIM_PT_WAVES 4
+#define PSIM_PT_WAVES 5
 #endif
 __global__ void __launch_bounds__(256, PSIM_PT_WAVES) k_pt(RoundArgs args) {
     __shared__ uint64_t sst[NST];
