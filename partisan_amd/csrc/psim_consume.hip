@@ -217,9 +217,29 @@ DEV uint32_t sublist(Wv& w, uint32_t V, uint32_t n, uint32_t k, uint32_t& OUT, u
     uint32_t kl = shfl(w.DCL, (int)src), kh = shfl(w.DCH, (int)src);
     uint64_t key = l < n ? ((((uint64_t)kh) << 32) | kl) >> 5 : ~0ull;
     uint32_t m = n < k ? n : k;
+    const uint32_t hi = (uint32_t)(key >> 21);
+    // few of many (a passive view): the m smallest of the top 32 key bits,
+    // one wave minimum each; a tie at a pick (about once in 10^7) falls
+    // through to the exact path below
+    if (n >= 3 * m) {
+        uint32_t H = hi, O = OUT;
+        bool tie = false;
+        for (uint32_t i = 0; i < m && !tie; i++) {
+            const uint32_t mn = wave_min(H);
+            const uint64_t at = ballot(H == mn);
+            tie = popc(at) > 1;
+            const int j = ffs64(at);
+            O = l == on + i ? rl(V, j) : O;
+            H = l == (uint32_t)j ? 0xFFFFFFFFu : H;
+        }
+        if (!tie) {
+            OUT = O;
+            w.rng = base + n;
+            return on + m;
+        }
+    }
     // rank on the top 32 of the 53 key bits; only when two of them tie (about
     // once in 10^7 sublists) is the full (key, element) order recounted
-    const uint32_t hi = (uint32_t)(key >> 21);
     uint32_t rank = 0, eq = 0;
     for (uint32_t j = 0; j < n; j++) {
         uint32_t hj = rl(hi, j);
@@ -1262,6 +1282,8 @@ DEV void writeback(Wv& w) {
     }
     if (w.pt_dirty) store_pt_rows(w);
     a.ocnt[li] = w.seq;
+    // (the next node's base, loaded here: in the input stages its register
+    // cost more than the wait, measured)
     st_add(w, ST_BOUND, w.seq > a.obase[li + 1] - w.obase ? 1u : 0u);   // (checked by the engine)
     // only this wave writes its node's flag byte; peers read F_UP/F_CRASHED
     a.flags[w.me] = flag_byte(w);
@@ -1592,7 +1614,7 @@ __global__ void __launch_bounds__(256) k_relay(RoundArgs a) {
         uint4 D = make_uint4(0, 0, 0, 0);
         bool heavy = false, to_pt = false, relay = false, pt_lane = false, maps = false;
         Hdr h;
-        uint32_t ik = 0;
+        uint32_t ik = 0, oend = 0;
         uint4 act0 = make_uint4(0, 0, 0, 0), act1 = act0;
         uint32_t me_part = 0;
         if (P < na) {
@@ -1603,6 +1625,7 @@ __global__ void __launch_bounds__(256) k_relay(RoundArgs a) {
             // independent: issued together, waited once
             const size_t li = id - a.lo;
             h = a.hdr[li];
+            oend = (uint32_t)a.obase[li + 1];
             const uint4* ar = reinterpret_cast<const uint4*>(a.act + li * PSIM_ACTIVE_CAP);
             act0 = ar[0];
             act1 = ar[1];
@@ -1783,7 +1806,7 @@ __global__ void __launch_bounds__(256) k_relay(RoundArgs a) {
         }
         if (rng != h.rng) a.hdr[li].rng = rng;
         a.ocnt[li] = seq;
-        v[R_BOUND] += seq > a.obase[li + 1] - D.w ? 1u : 0u;
+        v[R_BOUND] += seq > oend - D.w ? 1u : 0u;
         if (!to_pt) {                                 // (k_pt writes the byte of its nodes)
             const uint8_t fl = a.flags[id];
             a.flags[id] = (uint8_t)((fl & (F_UP | F_CRASHED)) | (out_n ? F_LAZY : 0) |

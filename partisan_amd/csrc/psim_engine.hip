@@ -22,7 +22,6 @@
 // canonical (src, seq) order,
 // so any shard count gives bit-identical results.
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
 #include <rccl/rccl.h>
 
 #include <algorithm>
@@ -1018,7 +1017,7 @@ struct Shard {
     DBuf<unsigned long long> btot;      // this round's outbox total (k_node_prep)
     DBuf<uint4> desc, desc_slow, desc_pt;   // work descriptors; those k_relay leaves to k_consume / k_pt
     DBuf<uint64_t> bound, pscan, obase, stat_part, stat_out, d_off;   // bound: packed (bound << 32 | work)
-    DBuf<uint8_t> cub_tmp;
+    DBuf<uint8_t> cub_tmp;              // the scan's tile totals
     DBuf<uint32_t> ev_ids, ev_contacts, stop_ids, n_stop;
     bool tomb_live = false;             // full: snapshots carry their remove rows
     DBuf<Msg> sendbuf;
@@ -1144,12 +1143,96 @@ void flush_timers(psim_handle* h, Shard* s) {
     s->tn = 0;
 }
 
+// ------------------------------------------------ exclusive prefix sum --
+// Reduce-then-scan over tiles of SCAN_TILE elements (256 threads x 8
+// consecutive elements each): tile totals, one block scans the totals, each
+// tile scans itself from its total's prefix.  Three launches, the input read
+// twice (at 2^20 nodes: 8 MB per read, a few microseconds); a count that
+// fits one tile is one launch.
+constexpr uint32_t SCAN_ITEMS = 8, SCAN_TILE = BLK * SCAN_ITEMS;
+
+// exclusive scan of one value per thread across the block; returns the
+// block total in *total (every thread)
+template <typename T>
+__device__ T block_excl(T v, T* total) {
+    __shared__ T wsum[BLK / 64];
+    const uint32_t l = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    T x = v;                                          // inclusive scan within the wave
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const T y = __shfl_up(x, d);
+        if (l >= (uint32_t)d) x += y;
+    }
+    if (l == 63) wsum[wv] = x;
+    __syncthreads();
+    T base = 0, tot = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < BLK / 64; k++) {
+        base += k < wv ? wsum[k] : T(0);
+        tot += wsum[k];
+    }
+    __syncthreads();
+    *total = tot;
+    return base + x - v;
+}
+
+template <typename T>
+__global__ void __launch_bounds__(BLK) k_scan_tiles(const T* __restrict__ in, uint32_t n, T* __restrict__ sums) {
+    const size_t b0 = (size_t)blockIdx.x * SCAN_TILE + (size_t)threadIdx.x * SCAN_ITEMS;
+    T v = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < SCAN_ITEMS; k++) v += b0 + k < n ? in[b0 + k] : T(0);
+    T tot;
+    (void)block_excl(v, &tot);
+    if (threadIdx.x == 0) sums[blockIdx.x] = tot;
+}
+
+// one block: exclusive scan of the nt tile totals in place, in chunks of BLK
+template <typename T>
+__global__ void __launch_bounds__(BLK) k_scan_sums(T* sums, uint32_t nt) {
+    T carry = 0;
+    for (uint32_t c = 0; c < nt; c += BLK) {
+        const uint32_t i = c + threadIdx.x;
+        const T v = i < nt ? sums[i] : T(0);
+        T tot;
+        const T e = block_excl(v, &tot);
+        if (i < nt) sums[i] = carry + e;
+        carry += tot;
+    }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(BLK) k_scan_apply(const T* __restrict__ in, T* __restrict__ out, uint32_t n,
+                                                   const T* __restrict__ sums) {
+    const size_t b0 = (size_t)blockIdx.x * SCAN_TILE + (size_t)threadIdx.x * SCAN_ITEMS;
+    T x[SCAN_ITEMS], v = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < SCAN_ITEMS; k++) {
+        x[k] = b0 + k < n ? in[b0 + k] : T(0);
+        v += x[k];
+    }
+    T tot;
+    T run = block_excl(v, &tot) + (sums ? sums[blockIdx.x] : T(0));
+#pragma unroll
+    for (uint32_t k = 0; k < SCAN_ITEMS; k++) {
+        if (b0 + k < n) out[b0 + k] = run;
+        run += x[k];
+    }
+}
+
 template <typename T>
 int scan_excl(Shard* s, const T* in, T* out, uint32_t n) {
-    size_t tb = 0;
-    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, in, out, n, s->stream));
-    TRY(s->cub_tmp.ensure(tb));
-    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(s->cub_tmp.p, tb, in, out, n, s->stream));
+    const uint32_t nt = (uint32_t)(((uint64_t)n + SCAN_TILE - 1) / SCAN_TILE);
+    if (nt <= 1) {
+        k_scan_apply<T><<<1, BLK, 0, s->stream>>>(in, out, n, nullptr);
+    } else {
+        TRY(s->cub_tmp.ensure((size_t)nt * sizeof(T)));
+        T* sums = reinterpret_cast<T*>(s->cub_tmp.p);
+        k_scan_tiles<T><<<nt, BLK, 0, s->stream>>>(in, n, sums);
+        k_scan_sums<T><<<1, BLK, 0, s->stream>>>(sums, nt);
+        k_scan_apply<T><<<nt, BLK, 0, s->stream>>>(in, out, n, sums);
+    }
+    HIP_TRY(hipGetLastError());
     return PSIM_OK;
 }
 

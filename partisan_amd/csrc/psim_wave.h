@@ -40,6 +40,24 @@ DEV uint32_t from_prev(uint32_t v) {
     return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xF, 0xF, true);
 }
 
+// minimum over the wave's 64 lanes (DPP: row shifts, then the row
+// broadcasts; lanes without a source keep their own value), in an SGPR
+template <int CTRL, int ROW_MASK, int BANK_MASK>
+DEV uint32_t dpp_min(uint32_t x) {
+    const uint32_t y = (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, CTRL, ROW_MASK, BANK_MASK, false);
+    return x < y ? x : y;
+}
+DEV uint32_t wave_min(uint32_t x) {
+    x = dpp_min<0x111, 0xF, 0xF>(x);     // row_shr:1
+    x = dpp_min<0x112, 0xF, 0xF>(x);     // row_shr:2
+    x = dpp_min<0x113, 0xF, 0xF>(x);     // row_shr:3
+    x = dpp_min<0x114, 0xF, 0xE>(x);     // row_shr:4, banks 1-3
+    x = dpp_min<0x118, 0xF, 0xC>(x);     // row_shr:8, banks 2-3
+    x = dpp_min<0x142, 0xA, 0xF>(x);     // row_bcast:15, rows 1 and 3
+    x = dpp_min<0x143, 0xC, 0xF>(x);     // row_bcast:31, rows 2 and 3
+    return __builtin_amdgcn_readlane(x, 63);
+}
+
 // delete entry k (order preserving)
 DEV void vdel(uint32_t& V, uint32_t& n, uint32_t k) {
     uint32_t l = lane_id();
