@@ -1415,7 +1415,15 @@ DEV void begin_pt(Wv& w, const PtIn& x, const PtX& y) {
     const uint32_t l = lane_id();
     w.li = x.n - w.a->lo;
     w.me = x.n;
-    begin_header(w, x.H);
+    // only the header fields the Plumtree phase reads or writes live in
+    // scalars (the rest go back from the loaded word)
+    w.rng = ((uint64_t)rl(x.H, 1) << 32) | rl(x.H, 0);   // (store_pt_rows' fixed store rewrites it)
+    w.start_round = rl(x.H, 2);
+    w.aux = rl(x.H, 5); w.have = rl(x.H, 6); w.trk_round = rl(x.H, 7); w.trk_hop = rl(x.H, 8);
+    const uint32_t w10 = rl(x.H, 10);
+    w.act_n = rl(x.H, 9) & 0xFF; w.all_n = (w10 >> 16) & 0xFF; w.com_n = w10 >> 24;
+    w.out_n = (rl(x.H, 11) >> 16) & 0xFF;
+    w.ox = rl(x.H, HW_OUT_EXT);
     w.A = l < PSIM_ACTIVE_CAP ? x.A : 0u;
     w.fl = x.fl;
     w.obase = x.ob;
@@ -1470,12 +1478,25 @@ DEV void body_pt(Wv& w, const PtIn& x) {
     }
 }
 
-DEV void writeback_pt(Wv& w) {
+// H: the header word l & 15 as loaded (the words the Plumtree phase leaves
+// alone are stored back from it)
+DEV void writeback_pt(Wv& w, uint32_t H) {
     const RoundArgs& a = *w.a;
     const uint32_t l = lane_id();
     const size_t li = w.li;
     out_ext(w);
-    reinterpret_cast<uint32_t*>(a.hdr + li)[l & 15] = header_word(w, l & 15);
+    {
+        const uint32_t k = l & 15;
+        uint32_t v = H;
+        v = k == 5 ? w.aux : v;
+        v = k == 6 ? w.have : v;
+        v = k == 7 ? w.trk_round : v;
+        v = k == 8 ? w.trk_hop : v;
+        v = k == 10 ? ((v & 0xFFFFu) | (w.all_n << 16) | (w.com_n << 24)) : v;
+        v = k == 11 ? ((v & ~0xFF0000u) | (w.out_n << 16)) : v;
+        v = k == HW_OUT_EXT ? w.ox : v;
+        reinterpret_cast<uint32_t*>(a.hdr + li)[k] = v;
+    }
     if (w.pt_dirty) store_pt_rows(w);
     a.ocnt[li] = w.seq;
     st_add(w, ST_BOUND, w.seq > a.obase[li + 1] - w.obase ? 1u : 0u);
@@ -1528,7 +1549,7 @@ __global__ void __launch_bounds__(256, PSIM_PT_WAVES) k_pt(RoundArgs args) {
             STAMP(w, 29);
             body_pt(w, x);
             PtX yn = load_pt_x(args, xn);
-            writeback_pt(w);
+            writeback_pt(w, x.H);
             STAMP(w, 30);
             PtIn xnn = load_pt_node(args, d);
             d = load_desc(args, min(i + 3 * nw, last));
