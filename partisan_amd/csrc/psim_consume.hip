@@ -26,6 +26,17 @@
 
 namespace psim {
 
+// The launch's RoundArgs, read through an opaque constant-address pointer:
+// each helper re-reads the fields it needs with scalar loads, instead of the
+// kernel holding all 188 dwords of arguments in SGPRs (which spilled to VGPR
+// lanes: a v_readlane per reuse on the hot path).
+typedef const __attribute__((address_space(4))) RoundArgs KArgs;
+DEV KArgs& kargs() {
+    KArgs* p = (KArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(p));
+    return *p;
+}
+
 #define ID_OF(e, n) (((uint32_t)(e) << 20) | (uint32_t)(n))
 #define ID_E(id) ((id) >> 20)
 #define ID_C(id) ((id)&0xFFFFFu)
@@ -167,7 +178,7 @@ DEV uint32_t hw_epoch(const Wv& w) { return w.epoch; }
 // of them costs one VALU Philox (every lane a counter) instead of 64 scalar
 // ones; select_random and sublist both read it.
 DEV void dc_fill(Wv& w, uint64_t base) {
-    uint64_t v = draw58_at(base + lane_id(), w.me, w.a->seed);
+    uint64_t v = draw58_at(base + lane_id(), w.me, kargs().seed);
     w.DCL = (uint32_t)v; w.DCH = (uint32_t)(v >> 32);
     w.dc_base = base;
 }
@@ -307,8 +318,8 @@ DEV void flush_recs(Wv& w) {
     __builtin_amdgcn_wave_barrier();
     const uint4 piece = reinterpret_cast<const uint4*>(w.srec + j * 16)[l & 3];
     const uint32_t key = w.skey[jk];
-    reinterpret_cast<uint4*>(w.a->rec_out + w.obase + g)[l & 3] = piece;
-    w.a->okey[w.obase + gk] = key;
+    reinterpret_cast<uint4*>(kargs().rec_out + w.obase + g)[l & 3] = piece;
+    kargs().okey[w.obase + gk] = key;
     __builtin_amdgcn_wave_barrier();
     w.flushed = w.seq;
 }
@@ -321,8 +332,8 @@ DEV void flush_full(Wv& w) {
     const uint32_t l = lane_id();
     __builtin_amdgcn_wave_barrier();
     const uint64_t r0 = w.obase + w.flushed;
-    uint4* rb = reinterpret_cast<uint4*>(w.a->rec_out + r0);
-    uint32_t* kb = w.a->okey + r0;
+    uint4* rb = reinterpret_cast<uint4*>(kargs().rec_out + r0);
+    uint32_t* kb = kargs().okey + r0;
     rb[l] = reinterpret_cast<const uint4*>(w.srec)[l];
     kb[l & (STAGE - 1)] = w.skey[l & (STAGE - 1)];
     __builtin_amdgcn_wave_barrier();
@@ -334,10 +345,10 @@ DEV void flush_full(Wv& w) {
 // F_UP and the partition of another node cannot change during k_consume,
 // so the cache filled at node start answers exactly for its members
 DEV bool connect_ok(const Wv& w, uint32_t dst) {
-    if (dst >= w.a->n_nodes || dst == w.me) return false;
+    if (dst >= kargs().n_nodes || dst == w.me) return false;
     uint64_t m = ballot(w.CV == dst);
     uint32_t v = m ? rl(w.CF, ffs64(m))
-                   : ((uint32_t)w.a->flags[dst] | ((uint32_t)w.a->part[dst] << 8));
+                   : ((uint32_t)kargs().flags[dst] | ((uint32_t)kargs().part[dst] << 8));
     return (v & F_UP) && (v >> 8) == w.mypart;
 }
 
@@ -357,7 +368,7 @@ DEV void hv_send(Wv& w, uint32_t dst, uint32_t type, uint32_t ttl, uint32_t a0, 
 DEV void load_maps(Wv& w) {
     if (w.maps) return;
     static_assert(PSIM_IDMAP_CAP == 64, "an id map is one entry per lane");
-    const RoundArgs& a = *w.a;
+    KArgs& a = kargs();
     const uint32_t l = lane_id(), sx = w.sx, rx = w.rx;
     const bool own = l < IDMAP_IN;
     const size_t io = w.li * IDMAP_IN + (l & (IDMAP_IN - 1));
@@ -421,7 +432,7 @@ DEV bool valid_disconnect(Wv& w, uint32_t p, uint32_t d) { // hv:1642-1653
 DEV void add_to_passive(Wv& w, uint32_t p) {             // hv:1423-1448
     uint32_t l = lane_id();
     if (p == w.me || ballot((l < w.act_n && w.A == p) || (l < w.pas_n && w.P == p))) return;
-    if (w.pas_n >= w.a->max_passive) {
+    if (w.pas_n >= kargs().max_passive) {
         // select_random(Passive, [Myself]): Myself is never in Passive (no
         // path inserts it), so the index draw addresses Passive directly
         uint32_t k = uniform_n(w, w.pas_n) - 1;
@@ -445,7 +456,7 @@ DEV void drop_random_active(Wv& w) {                     // hv:1467-1512
 DEV void add_to_active(Wv& w, uint32_t p) {              // hv:1371-1420
     if (p == w.me || has(w.A, w.act_n, p)) return;
     if (vdel_val(w.P, w.pas_n, p)) w.vd |= 2u;
-    if (w.act_n >= w.a->max_active) drop_random_active(w);
+    if (w.act_n >= kargs().max_active) drop_random_active(w);
     view_add(w.A, w.act_n, p);
     w.vd |= 1u;
 }
@@ -454,8 +465,8 @@ DEV void add_to_active(Wv& w, uint32_t p) {              // hv:1371-1420
 DEV uint32_t build_exchange(Wv& w, uint32_t& EX) {
     EX = lane_id() == 0 ? w.me : 0u;
     uint32_t m = 1;
-    m = sublist(w, w.A, w.act_n, w.a->k_active, EX, m);
-    m = sublist(w, w.P, w.pas_n, w.a->k_passive, EX, m);
+    m = sublist(w, w.A, w.act_n, kargs().k_active, EX, m);
+    m = sublist(w, w.P, w.pas_n, kargs().k_passive, EX, m);
     return usort_lanes(w, EX, m);
 }
 
@@ -473,7 +484,7 @@ DEV void merge_exchange(Wv& w, uint32_t EX, uint32_t nex) {
     uint32_t T = EX;
     const uint32_t mt = usort_mask(w, T, ballot(l < nex && EX != w.me && !in_act));
     if (!mt) return;
-    const uint32_t maxp = w.a->max_passive;
+    const uint32_t maxp = kargs().max_passive;
     const uint64_t c0 = w.rng;
     if (c0 < w.dc_base || c0 + mt - w.dc_base > 64) dc_fill(w, c0);   // cover [c0, c0 + mt)
     const uint32_t off = (uint32_t)(c0 - w.dc_base);
@@ -630,7 +641,7 @@ DEV void replay_notifies(Wv& w) {
     w.nlog_n = 0;
 }
 DEV void notify(Wv& w) {
-    if (!w.a->plumtree) return;
+    if (!kargs().plumtree) return;
     uint32_t l = lane_id();
     if (w.nlog_n) {
         uint32_t k = w.nlog_n - 1;
@@ -701,7 +712,7 @@ DEV uint64_t pt_conn_mask(Wv& w, uint64_t cand, uint32_t IDENT) {
         in |= hit;
         fl = hit ? cj : fl;
     }
-    const bool ok = ((cand >> l) & 1ull) && in && id != w.me && id < w.a->n_nodes && (fl & F_UP) &&
+    const bool ok = ((cand >> l) & 1ull) && in && id != w.me && id < kargs().n_nodes && (fl & F_UP) &&
                     (fl >> 8) == w.mypart;
     const uint64_t m = ballot(ok);
     st_add(w, ST_FAIL, popc(cand) - popc(m));
@@ -810,7 +821,7 @@ DEV void pt_handle(Wv& w, uint32_t type, uint32_t src, uint32_t msg, uint32_t rn
         if (!pt_have(w, msg)) {                        // plumtree_backend merge/2
             pt_mark(w, msg);
             st_add(w, ST_FIRST, 1);
-            if (msg == w.a->tracked_msg) { w.trk_round = w.round; w.trk_hop = rnd + 1; }
+            if (msg == kargs().tracked_msg) { w.trk_round = w.round; w.trk_hop = rnd + 1; }
             pt_update(w, from, root, true);
             pt_push(w, msg, rnd + 1, root, from);
         } else {
@@ -846,7 +857,7 @@ DEV void pt_handle(Wv& w, uint32_t type, uint32_t src, uint32_t msg, uint32_t rn
 // ----------------------------------------------------------- hyparview --
 DEV void hv_handle(Wv& w, uint32_t type, uint32_t p, uint32_t ttl, uint32_t a0, uint32_t a1,
                    uint32_t EX, uint32_t nex) {
-    const RoundArgs& a = *w.a;
+    KArgs& a = kargs();
     uint32_t me = w.me;
     switch (type) {
     case PSIM_MSG_JOIN:                                // hv:703-771
@@ -958,7 +969,7 @@ DEV bool timer_due(uint32_t period, uint32_t r, uint32_t start) {
 
 // Inbox chunk c (messages c..c+3 of the node's dense run): lane l loads
 // word l&15 of message c + (l>>4), one 256-B load instruction per chunk.
-DEV uint32_t load_chunk(const RoundArgs& a, uint32_t ib, uint32_t ik, uint32_t c) {
+DEV uint32_t load_chunk(KArgs& a, uint32_t ib, uint32_t ik, uint32_t c) {
     uint32_t l = lane_id();
     return (c + (l >> 4) < ik) ? reinterpret_cast<const uint32_t*>(a.rec_in + ib + c + (l >> 4))[l & 15]
                                : 0u;
@@ -966,7 +977,7 @@ DEV uint32_t load_chunk(const RoundArgs& a, uint32_t ib, uint32_t ik, uint32_t c
 
 // chunk c (a multiple of 4) of the node's inbox: the first from the first
 // input stage, any later one loaded
-DEV uint32_t inbox_chunk(const Wv& w, const RoundArgs& a, uint32_t ib, uint32_t ik, uint32_t c, uint32_t R0) {
+DEV uint32_t inbox_chunk(const Wv& w, KArgs& a, uint32_t ib, uint32_t ik, uint32_t c, uint32_t R0) {
     return c == 0 ? R0 : load_chunk(a, ib, ik, c);
 }
 
@@ -991,12 +1002,12 @@ struct NodeX {
     uint32_t CV, CF;               // view ids (passive 0-31, active 32-39), their flags | part << 8
 };
 
-DEV uint32_t load_desc(const RoundArgs& a, uint32_t k) {
+DEV uint32_t load_desc(KArgs& a, uint32_t k) {
     uint32_t l = lane_id();
     return reinterpret_cast<const uint32_t*>(a.desc + k)[l & 3];
 }
 
-DEV NodeIn load_node(const RoundArgs& a, uint32_t D) {
+DEV NodeIn load_node(KArgs& a, uint32_t D) {
     uint32_t l = lane_id();
     NodeIn x;
     x.n = rl(D, 0); x.ib = rl(D, 1); x.ik = rl(D, 2) & DESC_CNT_MASK; x.tf = rl(D, 2) >> 28; x.ob = rl(D, 3);
@@ -1013,13 +1024,13 @@ DEV NodeIn load_node(const RoundArgs& a, uint32_t D) {
 }
 
 // flag | partition << 8 of the view members in CV (the connection cache)
-DEV uint32_t cache_flags(const RoundArgs& a, uint32_t cv, uint32_t me) {
+DEV uint32_t cache_flags(KArgs& a, uint32_t cv, uint32_t me) {
     const uint32_t ca = cv < a.n_nodes ? cv : me;
     const uint32_t f = a.flags[ca], pt = a.part[ca];
     return cv < a.n_nodes ? (f | (pt << 8)) : 0u;
 }
 
-DEV NodeX load_x(const RoundArgs& a, const NodeIn& x) {
+DEV NodeX load_x(KArgs& a, const NodeIn& x) {
     uint32_t l = lane_id();
     NodeX y;
     const uint32_t hw9 = rl(x.H, 9);                 // act_n, pas_n, .. (Hdr word 9)
@@ -1044,7 +1055,7 @@ DEV void load_pt_regs(Wv& w, uint32_t PA, uint32_t PG, uint32_t PL, uint64_t PO)
 }
 // outstanding entry l of the node (its row, then its extension row: one
 // 8-B load per lane either way)
-DEV uint64_t load_po(const RoundArgs& a, size_t li, uint32_t ox) {
+DEV uint64_t load_po(KArgs& a, size_t li, uint32_t ox) {
     const uint32_t l = lane_id();
     const bool own = l < OUT_IN;
     const uint64_t* p = own || !ox ? a.pt_out + li * OUT_IN + (l & (OUT_IN - 1))
@@ -1053,13 +1064,13 @@ DEV uint64_t load_po(const RoundArgs& a, size_t li, uint32_t ox) {
     return own || ox ? v : 0ull;
 }
 // lanes 0-7 pt_all, 8-15 pt_com, 16-23 the root row (and again above 24)
-DEV uint32_t load_pa(const RoundArgs& a, size_t li) {
+DEV uint32_t load_pa(KArgs& a, size_t li) {
     const uint32_t l = lane_id();
     return ((l & 31) < 8 ? a.pt_all + li * PSIM_PT_MEMBERS_CAP
                          : (l & 31) < 16 ? a.pt_com + li * PSIM_PT_MEMBERS_CAP : a.pt_rt + li * RT_WORDS)[l & 7];
 }
 DEV void load_pt_rows(Wv& w) {
-    const RoundArgs& a = *w.a;
+    KArgs& a = kargs();
     const uint32_t l = lane_id();
     const size_t li = w.li;
     load_pt_regs(w, load_pa(a, li), a.pt_eag[li * RT_SET + l], a.pt_laz[li * RT_SET + l], load_po(a, li, w.ox));
@@ -1080,7 +1091,7 @@ DEV void begin_header(Wv& w, uint32_t H) {
 // node state and the per-node scratch of the wave, from the staged inputs
 DEV void begin_node(Wv& w, const NodeIn& x, const NodeX& y) {
     const uint32_t l = lane_id();
-    w.li = x.n - w.a->lo;
+    w.li = x.n - kargs().lo;
     w.me = x.n;
     begin_header(w, x.H);
     w.vd = 0;
@@ -1101,7 +1112,7 @@ DEV void begin_node(Wv& w, const NodeIn& x, const NodeX& y) {
 // replay of its notifies into the Plumtree state.  No global store.  The
 // Plumtree inbox, origin and lazy tick follow in k_pt.
 DEV void body_hv(Wv& w, const NodeIn& x) {
-    const RoundArgs& a = *w.a;
+    KArgs& a = kargs();
     const uint32_t r = a.round;
     const uint32_t l = lane_id();
     const uint32_t n = x.n;
@@ -1203,7 +1214,7 @@ DEV uint32_t header_word(const Wv& w, uint32_t k) {
 // the Plumtree rows of the wave back (a rare branch in the HyParView
 // kernel: only after a notify replay)
 DEV void store_pt_rows(Wv& w) {
-    const RoundArgs& a = *w.a;
+    KArgs& a = kargs();
     const uint32_t l = lane_id();
     const size_t li = w.li;
     uint32_t all = shfl(w.AR, (int)(l & 7)), com = shfl(w.COM, (int)(l & 7)), rt = shfl(w.AR, (int)(RTB + (l & 7)));
@@ -1233,12 +1244,12 @@ DEV uint32_t take_ext_row(Wv& w, uint32_t* top, uint32_t rows, int kind) {
 }
 // the outstanding table outgrew its own row
 DEV void out_ext(Wv& w) {
-    if (w.pt_dirty && w.out_n > OUT_IN && !w.ox) w.ox = take_ext_row(w, w.a->outx_top, w.a->outx_rows, PSIM_OVF_PT_OUT);
+    if (w.pt_dirty && w.out_n > OUT_IN && !w.ox) w.ox = take_ext_row(w, kargs().outx_top, kargs().outx_rows, PSIM_OVF_PT_OUT);
 }
 
 DEV uint8_t flag_byte(const Wv& w) {
     return (uint8_t)((w.fl & (F_UP | F_CRASHED)) | (w.out_n ? F_LAZY : 0) | (min(w.out_n, 15u) << F_OUTN_SHIFT) |
-                     (w.act_n < w.a->min_active ? F_LOWACT : 0));
+                     (w.act_n < kargs().min_active ? F_LOWACT : 0));
 }
 
 // Write back the node: a fixed set of full-wave stores (each lane past a
@@ -1247,7 +1258,7 @@ DEV uint8_t flag_byte(const Wv& w) {
 // staged records.  10 vector memory operations for every node, the Plumtree
 // rows too after a notify replay.
 DEV void writeback(Wv& w) {
-    const RoundArgs& a = *w.a;
+    KArgs& a = kargs();
     const uint32_t l = lane_id();
     const size_t li = w.li;
     const uint32_t h0 = (uint32_t)w.rng;
@@ -1300,7 +1311,7 @@ __global__ void __launch_bounds__(256, PSIM_WAVES_PER_SIMD) k_consume(RoundArgs 
     __shared__ __attribute__((aligned(16))) uint32_t srecs[WAVES_PER_BLOCK][STAGE * 16];
     __shared__ uint32_t skeys[WAVES_PER_BLOCK][STAGE];
     for (int i = threadIdx.x; i < NST; i += blockDim.x) sst[i] = 0;
-    if (threadIdx.x == 0) atomicMin(&args.ktime[0], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+    if (threadIdx.x == 0) atomicMin(&kargs().ktime[0], (unsigned long long)__builtin_amdgcn_s_memrealtime());
     __syncthreads();
 
     const uint32_t wid = threadIdx.x >> 6;
@@ -1320,11 +1331,11 @@ __global__ void __launch_bounds__(256, PSIM_WAVES_PER_SIMD) k_consume(RoundArgs 
     w.t_last = __builtin_amdgcn_s_memtime();
 #endif
     w.st = sst;
-    w.round = args.round;
+    w.round = kargs().round;
     w.SC = 0;
     w.digest = 0;
     w.KM = magic_lanes();
-    const uint32_t na = *args.n_alist;
+    const uint32_t na = *kargs().n_alist;
     if (gw < na) {
         // Pipeline over this wave's nodes i, i + nw, ...: while node i is
         // processed, the rows of node i + nw are in flight; after its body the
@@ -1332,18 +1343,18 @@ __global__ void __launch_bounds__(256, PSIM_WAVES_PER_SIMD) k_consume(RoundArgs 
         // the rows of node i + 2nw.  Every node issues the same loads and
         // stores, so each wait is for exactly the stage it needs.
         const uint32_t last = na - 1;
-        NodeIn x = load_node(args, load_desc(args, gw));
-        NodeX y = load_x(args, x);
-        NodeIn xn = load_node(args, load_desc(args, min(gw + nw, last)));
-        uint32_t d = load_desc(args, min(gw + 2 * nw, last));
+        NodeIn x = load_node(kargs(), load_desc(kargs(), gw));
+        NodeX y = load_x(kargs(), x);
+        NodeIn xn = load_node(kargs(), load_desc(kargs(), min(gw + nw, last)));
+        uint32_t d = load_desc(kargs(), min(gw + 2 * nw, last));
         for (uint32_t i = gw; i < na; i += nw) {
             STAMP(w, 24);
             begin_node(w, x, y);
             body_hv(w, x);
-            NodeX yn = load_x(args, xn);
+            NodeX yn = load_x(kargs(), xn);
             writeback(w);
-            NodeIn xnn = load_node(args, d);
-            d = load_desc(args, min(i + 3 * nw, last));
+            NodeIn xnn = load_node(kargs(), d);
+            d = load_desc(kargs(), min(i + 3 * nw, last));
             x = xn; y = yn; xn = xnn;
         }
     }
@@ -1353,8 +1364,8 @@ __global__ void __launch_bounds__(256, PSIM_WAVES_PER_SIMD) k_consume(RoundArgs 
     flush_wave_stats(w, sst);
     __syncthreads();
     for (int i = threadIdx.x; i < NST; i += blockDim.x)
-        args.stat_part[(size_t)blockIdx.x * NST + i] = sst[i];
-    if (threadIdx.x == 0) atomicMax(&args.ktime[1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+        kargs().stat_part[(size_t)blockIdx.x * NST + i] = sst[i];
+    if (threadIdx.x == 0) atomicMax(&kargs().ktime[1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
 }
 
 // ------------------------------------------------------- Plumtree phase --
@@ -1377,7 +1388,7 @@ struct PtX {
     uint64_t PO;
 };
 
-DEV PtIn load_pt_node(const RoundArgs& a, uint32_t D) {
+DEV PtIn load_pt_node(KArgs& a, uint32_t D) {
     const uint32_t l = lane_id();
     PtIn x;
     x.n = rl(D, 0); x.ib = rl(D, 1); x.ik = rl(D, 2) & DESC_CNT_MASK; x.tf = rl(D, 2) >> 28; x.ob = rl(D, 3);
@@ -1399,7 +1410,7 @@ DEV uint32_t act_cache(const PtIn& x) {
     return l >= 32 && l < 40 && l - 32 < act_n ? av : NONE;
 }
 
-DEV PtX load_pt_x(const RoundArgs& a, const PtIn& x) {
+DEV PtX load_pt_x(KArgs& a, const PtIn& x) {
     const uint32_t l = lane_id();
     PtX y;
     const size_t li = x.n - a.lo;
@@ -1413,7 +1424,7 @@ DEV PtX load_pt_x(const RoundArgs& a, const PtIn& x) {
 
 DEV void begin_pt(Wv& w, const PtIn& x, const PtX& y) {
     const uint32_t l = lane_id();
-    w.li = x.n - w.a->lo;
+    w.li = x.n - kargs().lo;
     w.me = x.n;
     // only the header fields the Plumtree phase reads or writes live in
     // scalars (the rest go back from the loaded word)
@@ -1435,7 +1446,7 @@ DEV void begin_pt(Wv& w, const PtIn& x, const PtX& y) {
 }
 
 DEV void body_pt(Wv& w, const PtIn& x) {
-    const RoundArgs& a = *w.a;
+    KArgs& a = kargs();
     const uint32_t r = a.round, n = x.n;
     // a fresh incarnation drops its inbox (counted by the HyParView phase)
     const uint32_t ik = hw_start(w) == r ? 0u : x.ik;
@@ -1481,7 +1492,7 @@ DEV void body_pt(Wv& w, const PtIn& x) {
 // H: the header word l & 15 as loaded (the words the Plumtree phase leaves
 // alone are stored back from it)
 DEV void writeback_pt(Wv& w, uint32_t H) {
-    const RoundArgs& a = *w.a;
+    KArgs& a = kargs();
     const uint32_t l = lane_id();
     const size_t li = w.li;
     out_ext(w);
@@ -1513,7 +1524,7 @@ __global__ void __launch_bounds__(256, PSIM_PT_WAVES) k_pt(RoundArgs args) {
     __shared__ __attribute__((aligned(16))) uint32_t srecs[WAVES_PER_BLOCK][STAGE * 16];
     __shared__ uint32_t skeys[WAVES_PER_BLOCK][STAGE];
     __shared__ uint32_t sslots[2 * PSIM_MSG_SLOTS];
-    for (int i = threadIdx.x; i < 2 * PSIM_MSG_SLOTS; i += blockDim.x) sslots[i] = args.slots[i];
+    for (int i = threadIdx.x; i < 2 * PSIM_MSG_SLOTS; i += blockDim.x) sslots[i] = kargs().slots[i];
     for (int i = threadIdx.x; i < NST; i += blockDim.x) sst[i] = 0;
     __syncthreads();
     const uint32_t wid = threadIdx.x >> 6;
@@ -1533,26 +1544,26 @@ __global__ void __launch_bounds__(256, PSIM_PT_WAVES) k_pt(RoundArgs args) {
     w.t_last = __builtin_amdgcn_s_memtime();
 #endif
     w.st = sst;
-    w.round = args.round;
+    w.round = kargs().round;
     w.SC = 0;
     w.digest = 0;
-    const uint32_t na = *args.n_alist;
+    const uint32_t na = *kargs().n_alist;
     if (gw < na) {
         const uint32_t last = na - 1;
-        PtIn x = load_pt_node(args, load_desc(args, gw));
-        PtX y = load_pt_x(args, x);
-        PtIn xn = load_pt_node(args, load_desc(args, min(gw + nw, last)));
-        uint32_t d = load_desc(args, min(gw + 2 * nw, last));
+        PtIn x = load_pt_node(kargs(), load_desc(kargs(), gw));
+        PtX y = load_pt_x(kargs(), x);
+        PtIn xn = load_pt_node(kargs(), load_desc(kargs(), min(gw + nw, last)));
+        uint32_t d = load_desc(kargs(), min(gw + 2 * nw, last));
         for (uint32_t i = gw; i < na; i += nw) {
             STAMP(w, 31);
             begin_pt(w, x, y);
             STAMP(w, 29);
             body_pt(w, x);
-            PtX yn = load_pt_x(args, xn);
+            PtX yn = load_pt_x(kargs(), xn);
             writeback_pt(w, x.H);
             STAMP(w, 30);
-            PtIn xnn = load_pt_node(args, d);
-            d = load_desc(args, min(i + 3 * nw, last));
+            PtIn xnn = load_pt_node(kargs(), d);
+            d = load_desc(kargs(), min(i + 3 * nw, last));
             x = xn; y = yn; xn = xnn;
         }
     }
@@ -1562,8 +1573,8 @@ __global__ void __launch_bounds__(256, PSIM_PT_WAVES) k_pt(RoundArgs args) {
     flush_wave_stats(w, sst);
     __syncthreads();
     for (int i = threadIdx.x; i < NST; i += blockDim.x)
-        args.stat_part[(size_t)blockIdx.x * NST + i] = sst[i];
-    if (threadIdx.x == 0) atomicMax(&args.ktime[1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+        kargs().stat_part[(size_t)blockIdx.x * NST + i] = sst[i];
+    if (threadIdx.x == 0) atomicMax(&kargs().ktime[1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
 }
 
 // ------------------------------------------------ relays and lazy ticks --
@@ -1581,7 +1592,7 @@ __global__ void __launch_bounds__(256, PSIM_PT_WAVES) k_pt(RoundArgs args) {
 // tick too (an IHAVE per outstanding entry over live active connections).
 // The order of the lists does not matter (each node writes its own rows and
 // outbox region; the stats and the digest are sums).
-DEV uint64_t relay_emit(const RoundArgs& a, uint64_t slot, uint32_t dst, uint32_t me, uint32_t tt, uint32_t seq,
+DEV uint64_t relay_emit(KArgs& a, uint64_t slot, uint32_t dst, uint32_t me, uint32_t tt, uint32_t seq,
                         uint32_t a0, uint32_t a1, uint32_t a2, const uint32_t (&X)[8]) {
     const uint32_t W[16] = {dst, me, tt, seq, a0, a1, a2, 0u, X[0], X[1], X[2], X[3], X[4], X[5], X[6], X[7]};
     uint64_t dg = 0;
@@ -1617,20 +1628,21 @@ DEV void block_append(bool go, const uint4& D, uint4* desc, uint32_t* cnt, uint3
     }
 }
 
-__global__ void __launch_bounds__(256) k_relay(RoundArgs a) {
+__global__ void __launch_bounds__(256) k_relay(RoundArgs) {
     enum { R_PROC, R_DELIV, R_SHUF, R_IHAVE, R_FAIL, R_DIGEST, R_OVF, R_BOUND, R_DIH, R_DIGN, R_EIGN, R_N };
     __shared__ unsigned long long sst[R_N];
     __shared__ uint32_t sslots[2 * PSIM_MSG_SLOTS];
-    for (int i = threadIdx.x; i < 2 * PSIM_MSG_SLOTS; i += blockDim.x) sslots[i] = a.slots[i];
+    for (int i = threadIdx.x; i < 2 * PSIM_MSG_SLOTS; i += blockDim.x) sslots[i] = kargs().slots[i];
     __shared__ uint32_t wcnt[5];                      // per wave list counts, then the block's base
     if (threadIdx.x < R_N) sst[threadIdx.x] = 0;
-    if (threadIdx.x == 0) atomicMin(&a.ktime[0], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+    if (threadIdx.x == 0) atomicMin(&kargs().ktime[0], (unsigned long long)__builtin_amdgcn_s_memrealtime());
     __syncthreads();
     const uint32_t l = lane_id();
-    const uint32_t na = *a.n_alist;
+    const uint32_t na = *kargs().n_alist;
     const uint64_t two58 = 1ull << 58;
     unsigned long long v[R_N] = {};
     for (uint32_t base = blockIdx.x * blockDim.x; base < na; base += gridDim.x * blockDim.x) {
+        KArgs& a = kargs();                           // (re-read per step, not held in SGPRs)
         const uint32_t P = base + threadIdx.x;
         uint4 D = make_uint4(0, 0, 0, 0);
         bool heavy = false, to_pt = false, relay = false, pt_lane = false, maps = false;
@@ -1843,7 +1855,7 @@ __global__ void __launch_bounds__(256) k_relay(RoundArgs a) {
         for (int k = 0; k < R_N; k++)
             if (v[k]) atomicAdd(&sst[k], v[k]);
     __syncthreads();
-    uint64_t* row = a.stat_relay + (size_t)blockIdx.x * NST;
+    uint64_t* row = kargs().stat_relay + (size_t)blockIdx.x * NST;
     for (uint32_t k = threadIdx.x; k < NST; k += blockDim.x)
         row[k] = k == ST_PROC ? sst[R_PROC] : k == ST_DELIV + PSIM_MSG_SHUFFLE ? sst[R_DELIV]
                : k == ST_EMIT + PSIM_MSG_SHUFFLE ? sst[R_SHUF] : k == ST_EMIT + PSIM_MSG_PT_IHAVE ? sst[R_IHAVE]
