@@ -26,24 +26,13 @@
 
 namespace psim {
 
-// The launch's RoundArgs, read through an opaque constant-address pointer:
-// each helper re-reads the fields it needs with scalar loads, instead of the
-// kernel holding all 188 dwords of arguments in SGPRs (which spilled to VGPR
-// lanes: a v_readlane per reuse on the hot path).
-typedef const __attribute__((address_space(4))) RoundArgs KArgs;
-DEV KArgs& kargs() {
-    KArgs* p = (KArgs*)__builtin_amdgcn_kernarg_segment_ptr();
-    asm volatile("" : "+s"(p));
-    return *p;
-}
-
 #define ID_OF(e, n) (((uint32_t)(e) << 20) | (uint32_t)(n))
 #define ID_E(id) ((id) >> 20)
 #define ID_C(id) ((id)&0xFFFFFu)
 
 constexpr int WAVES_PER_BLOCK = 4;
 #ifndef PSIM_WAVES_PER_SIMD
-#define PSIM_WAVES_PER_SIMD 3
+#define PSIM_WAVES_PER_SIMD 4
 #endif
 
 // Diagnostic build only (-DPSIM_STAMPS): s_memtime between phase

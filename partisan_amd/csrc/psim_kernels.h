@@ -87,4 +87,16 @@ int debug_stamps(unsigned long long* out);
 uint32_t consume_grid();
 uint32_t pt_grid();
 
+// The launch's RoundArgs, read through an opaque constant-address pointer
+// (in a kernel whose only argument is a RoundArgs): each helper re-reads the
+// fields it needs with scalar loads, instead of the kernel holding all 188
+// dwords of arguments in SGPRs (which spilled to VGPR lanes: a v_readlane
+// per reuse on the hot path).
+typedef const __attribute__((address_space(4))) RoundArgs KArgs;
+__device__ __forceinline__ KArgs& kargs() {
+    KArgs* p = (KArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(p));
+    return *p;
+}
+
 }  // namespace psim

@@ -68,7 +68,7 @@ DEV uint32_t wave_sum(uint32_t v) {
 
 // ----------------------------------------------------------------- RNG --
 DEV void dc_fill(Pw& w, uint64_t base) {
-    uint64_t v = draw58_at(base + lane_id(), w.me, w.a->seed);
+    uint64_t v = draw58_at(base + lane_id(), w.me, kargs().seed);
     w.DCL = (uint32_t)v; w.DCH = (uint32_t)(v >> 32);
     w.dc_base = base;
 }
@@ -126,21 +126,21 @@ DEV void emit(Pw& w, uint32_t dst, uint32_t type, uint32_t a0, uint32_t slot) {
     uint32_t word = l == 0 ? dst : l == 1 ? w.me : l == 2 ? type : l == 3 ? s : l == 4 ? a0
                   : l == 7 ? slot : 0u;
     if (l < 16) {
-        reinterpret_cast<uint32_t*>(w.a->rec_out + at)[l] = word;
+        reinterpret_cast<uint32_t*>(kargs().rec_out + at)[l] = word;
         uint32_t hw = l == 7 ? 0u : word;
         w.digest += (uint64_t)hw * digest_mul(l);
     }
-    if (l == 0) w.a->okey[at] = dst;     // pluggable bounds come from k_node_prep
+    if (l == 0) kargs().okey[at] = dst;     // pluggable bounds come from k_node_prep
     st_add(w, ST_EMIT + type, 1);
 }
 
 // maybe_connect + find (partisan_util.erl:75-134): the peer runs and no
 // partition separates the two; view members answer from the cache
 DEV bool connect_ok(const Pw& w, uint32_t dst) {
-    if (dst >= w.a->n_nodes || dst == w.me) return false;
+    if (dst >= kargs().n_nodes || dst == w.me) return false;
     uint64_t m = ballot(w.CV == dst);
     uint32_t v = m ? rl(w.CF, ffs64(m))
-                   : ((uint32_t)w.a->flags[dst] | ((uint32_t)w.a->part[dst] << 8));
+                   : ((uint32_t)kargs().flags[dst] | ((uint32_t)kargs().part[dst] << 8));
     return (v & F_UP) && (v >> 8) == w.mypart;
 }
 
@@ -148,7 +148,7 @@ DEV bool connect_ok(const Pw& w, uint32_t dst) {
 // contact only.  The full strategy sends to members only (every target is
 // read from its own member row), so only SCAMP needs the check.
 DEV bool connected(const Pw& w, uint32_t p) {
-    if (w.a->strategy == PSIM_STRATEGY_FULL) return true;
+    if (kargs().strategy == PSIM_STRATEGY_FULL) return true;
     return ballot(lane_id() < w.vn && w.V == p) != 0 || p == w.h.join_contact;
 }
 
@@ -164,7 +164,7 @@ DEV void pl_send(Pw& w, uint32_t dst, uint32_t type, uint32_t a0, uint32_t slot)
 // ?SET:merge/2 into the row (full:49-55, :99-116); returns ?SET:equal/2 of
 // the two states before it
 DEV bool full_merge(Pw& w, const uint32_t* p) {
-    const uint32_t fw = w.a->tomb ? 2 * w.a->fw : w.a->fw;   // adds (+ removes)
+    const uint32_t fw = kargs().tomb ? 2 * kargs().fw : kargs().fw;   // adds (+ removes)
     bool neq = false, chg = false;
     for (uint32_t base = 0; base < fw; base += 256) {
         uint32_t i = base + 4 * lane_id();
@@ -187,15 +187,15 @@ DEV bool full_merge(Pw& w, const uint32_t* p) {
 // four member words (add & ~remove) of the node's row at word i
 DEV uint4 mem4(const Pw& w, uint32_t i) {
     uint4 o = *reinterpret_cast<const uint4*>(w.row + i);
-    if (w.a->tomb) {
-        const uint4 t = *reinterpret_cast<const uint4*>(w.row + w.a->fw + i);
+    if (kargs().tomb) {
+        const uint4 t = *reinterpret_cast<const uint4*>(w.row + kargs().fw + i);
         o = make_uint4(o.x & ~t.x, o.y & ~t.y, o.z & ~t.z, o.w & ~t.w);
     }
     return o;
 }
 
 DEV uint32_t full_count(const Pw& w) {
-    const uint32_t fw = w.a->fw;
+    const uint32_t fw = kargs().fw;
     uint32_t c = 0;
     for (uint32_t base = 0; base < fw; base += 256) {
         uint32_t i = base + 4 * lane_id();
@@ -210,7 +210,7 @@ DEV uint32_t full_count(const Pw& w) {
 
 // the k-th (0-based) member in id order
 DEV uint32_t full_nth(const Pw& w, uint32_t k) {
-    const uint32_t fw = w.a->fw;
+    const uint32_t fw = kargs().fw;
     const uint32_t l = lane_id();
     for (uint32_t base = 0; base < fw; base += 256) {
         uint32_t i = base + 4 * l;
@@ -247,11 +247,11 @@ DEV uint32_t full_nth(const Pw& w, uint32_t k) {
 DEV uint32_t full_snapshot(Pw& w) {
     if (w.snap != NONE && !w.dirty) return w.snap;
     uint32_t s = 0;
-    if (lane_id() == 0) s = atomicAdd(w.a->pay_top, 1u);
+    if (lane_id() == 0) s = atomicAdd(kargs().pay_top, 1u);
     s = rl(s, 0);
-    if (s >= w.a->pay_cap) { ovf(w, PSIM_OVF_STRATEGY); s = w.a->pay_cap - 1; }
-    const uint32_t fw = w.a->tomb ? 2 * w.a->fw : w.a->fw;   // adds (+ removes)
-    uint32_t* dst = w.a->pay_out + (size_t)s * 2 * w.a->fw;
+    if (s >= kargs().pay_cap) { ovf(w, PSIM_OVF_STRATEGY); s = kargs().pay_cap - 1; }
+    const uint32_t fw = kargs().tomb ? 2 * kargs().fw : kargs().fw;   // adds (+ removes)
+    uint32_t* dst = kargs().pay_out + (size_t)s * 2 * kargs().fw;
     for (uint32_t base = 0; base < fw; base += 256) {
         uint32_t i = base + 4 * lane_id();
         if (i < fw) *reinterpret_cast<uint4*>(dst + i) = *reinterpret_cast<const uint4*>(w.row + i);
@@ -268,8 +268,8 @@ DEV uint32_t full_snapshot(Pw& w) {
 // whole list is built before the manager sends any of it.
 DEV void full_gossip(Pw& w, uint32_t extra = NONE) {
     uint32_t slot = full_snapshot(w), cnt = full_count(w);
-    const uint32_t fw = w.a->fw;
-    if (w.a->fanout == 0) {
+    const uint32_t fw = kargs().fw;
+    if (kargs().fanout == 0) {
         for (uint32_t base = 0; base < fw; base += 256) {
             uint32_t i = base + 4 * lane_id();
             uint4 o = i < fw ? mem4(w, i) : make_uint4(0, 0, 0, 0);
@@ -290,11 +290,11 @@ DEV void full_gossip(Pw& w, uint32_t extra = NONE) {
         return;
     }
     uint32_t TG = 0;
-    for (uint32_t i = 0; i < w.a->fanout; i++) {
+    for (uint32_t i = 0; i < kargs().fanout; i++) {
         uint32_t t = full_nth(w, uniform_n(w, cnt) - 1);
         TG = lane_id() == i ? t : TG;
     }
-    for (uint32_t i = 0; i < w.a->fanout; i++) pl_send(w, rl(TG, i), PSIM_PL_GOSSIP, cnt, slot);
+    for (uint32_t i = 0; i < kargs().fanout; i++) pl_send(w, rl(TG, i), PSIM_PL_GOSSIP, cnt, slot);
 }
 
 // --------------------------------------------------------------- scamp --
@@ -308,11 +308,11 @@ DEV void scamp_add(Pw& w, uint32_t& L, uint32_t& n, uint32_t e, bool as_set) {
 
 // Strategy:join/3 at the joiner (sv1:52-99, sv2:64-113)
 DEV void scamp_join(Pw& w, uint32_t contact) {
-    const bool v1 = w.a->strategy == PSIM_STRATEGY_SCAMP_V1;
+    const bool v1 = kargs().strategy == PSIM_STRATEGY_SCAMP_V1;
     const uint32_t M0 = w.V, n0 = w.vn;
     scamp_add(w, w.V, w.vn, contact, v1);
     uint32_t SEL = 0;
-    uint32_t ns = sublist(w, M0, n0, v1 ? w.a->scamp_c : w.a->scamp_c - 1, SEL);
+    uint32_t ns = sublist(w, M0, n0, v1 ? kargs().scamp_c : kargs().scamp_c - 1, SEL);
     pl_send(w, contact, PSIM_PL_FWD_SUB, w.me, NONE);
     for (uint32_t i = 0; i < n0; i++)            // v1: sets:fold/3 = reverse of to_list
         pl_send(w, rl(M0, v1 ? n0 - 1 - i : i), PSIM_PL_FWD_SUB, contact, NONE);
@@ -333,7 +333,7 @@ DEV void scamp_periodic(Pw& w) {
 
 // handle_message(.., {forward_subscription, Node}) (sv1:212-252, sv2:284-327)
 DEV void scamp_fwd(Pw& w, uint32_t node) {
-    const bool v1 = w.a->strategy == PSIM_STRATEGY_SCAMP_V1;
+    const bool v1 = kargs().strategy == PSIM_STRATEGY_SCAMP_V1;
     const uint32_t rnd = uniform_n(w, 10) >= 5 ? 1u : 0u;    // random_0_or_1/0 sv1:272-279
     if (rnd == 0 && !has(w.V, w.vn, node)) {
         scamp_add(w, w.V, w.vn, node, v1);
@@ -349,7 +349,7 @@ DEV void scamp_fwd(Pw& w, uint32_t node) {
 // the old membership; v2 leave/2 (sv2:116-127) sends
 // {bootstrap_remove_subscription, t} to the partial view, state unchanged
 DEV void scamp_leave(Pw& w, uint32_t t) {
-    const bool v1 = w.a->strategy == PSIM_STRATEGY_SCAMP_V1;
+    const bool v1 = kargs().strategy == PSIM_STRATEGY_SCAMP_V1;
     const uint32_t M0 = w.V, n0 = w.vn;
     // the connections to the old members stay open (closed only on 'EXIT',
     // pl:971-984): the sends are judged on the old view
@@ -374,20 +374,20 @@ DEV void scamp_leave(Pw& w, uint32_t t) {
 // the OLD list (the target included); fanout > 0: the round's coalesced gossip
 DEV void full_leave(Pw& w, uint32_t t) {
     const uint32_t wi = t >> 5, bit = 1u << (t & 31u);
-    const bool was = (w.row[wi] & ~w.row[w.a->fw + wi] & bit) != 0;   // (tomb is on)
+    const bool was = (w.row[wi] & ~w.row[kargs().fw + wi] & bit) != 0;   // (tomb is on)
     __builtin_amdgcn_wave_barrier();
     if (was) {
-        if (lane_id() == 0) w.row[w.a->fw + wi] |= bit;
+        if (lane_id() == 0) w.row[kargs().fw + wi] |= bit;
         __builtin_amdgcn_wave_barrier();
         w.dirty = true;
     }
-    if (w.a->fanout) { w.gossip_due = true; return; }
+    if (kargs().fanout) { w.gossip_due = true; return; }
     full_gossip(w, was ? t : NONE);
 }
 
 // -------------------------------------------------------------- driver --
 DEV void pl_handle(Pw& w, uint32_t type, uint32_t src, uint32_t a0, uint32_t slot) {
-    const bool full = w.a->strategy == PSIM_STRATEGY_FULL;
+    const bool full = kargs().strategy == PSIM_STRATEGY_FULL;
     switch (type) {
     case PSIM_PL_HELLO:            // server: {state, Tag, get_local_state()} server:125-148
         if (!connect_ok(w, src)) { st_add(w, ST_FAIL, 1); w.nfail++; break; }
@@ -402,8 +402,8 @@ DEV void pl_handle(Pw& w, uint32_t type, uint32_t src, uint32_t a0, uint32_t slo
         if (w.h.join_contact != src) break;
         w.h.join_contact = NONE;
         if (full) {                // join/3 full:49-55
-            full_merge(w, w.a->pay_in + (size_t)slot * 2 * w.a->fw);
-            if (w.a->fanout) w.gossip_due = true;
+            full_merge(w, kargs().pay_in + (size_t)slot * 2 * kargs().fw);
+            if (kargs().fanout) w.gossip_due = true;
             else full_gossip(w);
         } else {
             scamp_join(w, src);
@@ -411,11 +411,11 @@ DEV void pl_handle(Pw& w, uint32_t type, uint32_t src, uint32_t a0, uint32_t slo
         break;
     case PSIM_PL_GOSSIP:           // handle_message/2 full:99-116
         if (!full) break;
-        if (!full_merge(w, w.a->pay_in + (size_t)slot * 2 * w.a->fw)) {
+        if (!full_merge(w, kargs().pay_in + (size_t)slot * 2 * kargs().fw)) {
             // a merged removal of ourselves: the manager stops (pl:1182-1188)
             // before the gossip it cast goes out
-            if (w.a->tomb && ((w.row[w.a->fw + (w.me >> 5)] >> (w.me & 31u)) & 1u)) { w.stop = true; break; }
-            if (w.a->fanout) w.gossip_due = true;
+            if (kargs().tomb && ((w.row[kargs().fw + (w.me >> 5)] >> (w.me & 31u)) & 1u)) { w.stop = true; break; }
+            if (kargs().fanout) w.gossip_due = true;
             else full_gossip(w);
         }
         break;
@@ -426,29 +426,29 @@ DEV void pl_handle(Pw& w, uint32_t type, uint32_t src, uint32_t a0, uint32_t slo
         if (!full) w.h.aux = w.round;
         break;
     case PSIM_PL_KEEP_SUB:         // sv2:328-338: InView = [Node | InView0]
-        if (w.a->strategy == PSIM_STRATEGY_SCAMP_V2) scamp_add(w, w.I, w.in_n, a0, false);
+        if (kargs().strategy == PSIM_STRATEGY_SCAMP_V2) scamp_add(w, w.I, w.in_n, a0, false);
         break;
     case PSIM_PL_REMOVE_SUB:       // sv1:190-211: a member Node hits the swapped
                                    // sets:del_element/2 arguments (App. A Q12): crash
-        if (w.a->strategy == PSIM_STRATEGY_SCAMP_V1 && has(w.V, w.vn, a0)) w.stop = true;
+        if (kargs().strategy == PSIM_STRATEGY_SCAMP_V1 && has(w.V, w.vn, a0)) w.stop = true;
         break;
     case PSIM_PL_BOOT_REMOVE:      // sv2:192-238: Node itself stops before its casts
                                    // go out (lists:nth(0, ..), or the self-less reset, pl:1182-1188)
-        if (w.a->strategy == PSIM_STRATEGY_SCAMP_V2 && a0 == w.me) w.stop = true;
+        if (kargs().strategy == PSIM_STRATEGY_SCAMP_V2 && a0 == w.me) w.stop = true;
         break;
     default:
         break;
     }
 }
 
-DEV uint32_t load_chunk(const RoundArgs& a, uint32_t ib, uint32_t ik, uint32_t c) {
+DEV uint32_t load_chunk(KArgs& a, uint32_t ib, uint32_t ik, uint32_t c) {
     uint32_t l = lane_id();
     return (c + (l >> 4) < ik) ? reinterpret_cast<const uint32_t*>(a.rec_in + ib + c + (l >> 4))[l & 15]
                                : 0u;
 }
 
 DEV void process_pl(Pw& w, uint32_t n, uint32_t ib, uint32_t ik, uint32_t ob) {
-    const RoundArgs& a = *w.a;
+    KArgs& a = kargs();
     const uint32_t l = lane_id();
     const uint32_t li = n - a.lo;
     const uint32_t r = a.round;
@@ -549,7 +549,7 @@ __global__ void __launch_bounds__(256) k_consume_pl(RoundArgs args) {
     __shared__ uint64_t sst[NST];
     __shared__ uint32_t scratch[PL_WAVES][64];
     for (int i = threadIdx.x; i < NST; i += blockDim.x) sst[i] = 0;
-    if (threadIdx.x == 0) atomicMin(&args.ktime[0], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+    if (threadIdx.x == 0) atomicMin(&kargs().ktime[0], (unsigned long long)__builtin_amdgcn_s_memrealtime());
     __syncthreads();
     const uint32_t wid = threadIdx.x >> 6;
     const uint32_t gw = uni(blockIdx.x * PL_WAVES + wid);
@@ -557,12 +557,12 @@ __global__ void __launch_bounds__(256) k_consume_pl(RoundArgs args) {
     Pw w;
     w.a = &args;
     w.lds = scratch[wid];
-    w.round = args.round;
+    w.round = kargs().round;
     w.SC = 0;
     w.digest = 0;
-    const uint32_t na = *args.n_alist;
+    const uint32_t na = *kargs().n_alist;
     for (uint32_t k = gw; k < na; k += nw) {
-        const uint4 d = args.desc[k];
+        const uint4 d = kargs().desc[k];
         process_pl(w, uni(d.x), uni(d.y), uni(d.z) & DESC_CNT_MASK, uni(d.w));
     }
     {
@@ -575,8 +575,8 @@ __global__ void __launch_bounds__(256) k_consume_pl(RoundArgs args) {
     }
     __syncthreads();
     for (int i = threadIdx.x; i < NST; i += blockDim.x)
-        args.stat_part[(size_t)blockIdx.x * NST + i] = sst[i];
-    if (threadIdx.x == 0) atomicMax(&args.ktime[1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+        kargs().stat_part[(size_t)blockIdx.x * NST + i] = sst[i];
+    if (threadIdx.x == 0) atomicMax(&kargs().ktime[1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
 }
 
 }  // namespace psim
