@@ -159,6 +159,43 @@ static ERL_NIF_TERM nif_broadcast(ErlNifEnv *env, int argc, const ERL_NIF_TERM a
     return rc ? err(env, rc) : enif_make_atom(env, "ok");
 }
 
+/* omission_nif(Ref, Kind, SrcBin, DstBin, On): install / remove
+ * {send_omission, Dst} funs at Src (Kind 0) or {receive_omission, Src} funs
+ * at Dst (Kind 1) -- add/remove_interposition_fun (pluggable:297-326) */
+static ERL_NIF_TERM nif_omission(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[]) {
+    sim_res *r; ErlNifBinary a, b; int kind, on;
+    if (!enif_get_resource(env, argv[0], SIM_RT, (void **)&r) || !enif_get_int(env, argv[1], &kind) ||
+        !enif_inspect_binary(env, argv[2], &a) || !enif_inspect_binary(env, argv[3], &b) ||
+        !enif_get_int(env, argv[4], &on) || a.size % 4 || a.size != b.size)
+        return enif_make_badarg(env);
+    LOCK_OR_BUSY(r);
+    int rc = psim_set_omission(r->h, kind, (const uint32_t *)a.data, (const uint32_t *)b.data, a.size / 4, on);
+    enif_mutex_unlock(r->mu);
+    return rc ? err(env, rc) : enif_make_atom(env, "ok");
+}
+
+/* faulted_nif(Ref, NodesBin, On): begin_omission / end_omission */
+static ERL_NIF_TERM nif_faulted(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[]) {
+    sim_res *r; ErlNifBinary a; int on;
+    if (!enif_get_resource(env, argv[0], SIM_RT, (void **)&r) || !enif_inspect_binary(env, argv[1], &a) ||
+        !enif_get_int(env, argv[2], &on) || a.size % 4)
+        return enif_make_badarg(env);
+    LOCK_OR_BUSY(r);
+    int rc = psim_set_faulted(r->h, (const uint32_t *)a.data, a.size / 4, on);
+    enif_mutex_unlock(r->mu);
+    return rc ? err(env, rc) : enif_make_atom(env, "ok");
+}
+
+/* clear_faults(Ref): resolve_all_faults_with_heal */
+static ERL_NIF_TERM nif_clear_faults(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[]) {
+    sim_res *r;
+    if (!enif_get_resource(env, argv[0], SIM_RT, (void **)&r)) return enif_make_badarg(env);
+    LOCK_OR_BUSY(r);
+    int rc = psim_clear_faults(r->h);
+    enif_mutex_unlock(r->mu);
+    return rc ? err(env, rc) : enif_make_atom(env, "ok");
+}
+
 /* step(Ref, Rounds) -> {ok, [{Round, Emitted, Delivered, FirstDeliveries}]} (dirty CPU) */
 static ERL_NIF_TERM nif_step(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[]) {
     sim_res *r; unsigned n;
@@ -379,6 +416,9 @@ static ErlNifFunc funcs[] = {
     {"histograms", 1, nif_histograms, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"set_partition_nif", 2, nif_set_partition, 0},
     {"clear_partition", 1, nif_clear_partition, 0},
+    {"omission_nif", 5, nif_omission, 0},
+    {"faulted_nif", 3, nif_faulted, 0},
+    {"clear_faults", 1, nif_clear_faults, 0},
     {"node", 2, nif_node, 0},
     {"snapshot", 1, nif_snapshot, ERL_NIF_DIRTY_JOB_IO_BOUND},
     {"restore", 2, nif_restore, ERL_NIF_DIRTY_JOB_IO_BOUND},

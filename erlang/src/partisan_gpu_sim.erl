@@ -3,7 +3,9 @@
 %% to the harness node_spec #{name => 'n<id>@sim', ...} (DESIGN.md section 2).
 -module(partisan_gpu_sim).
 -export([create/1, join/3, crash/2, revive/2, leave/2, leave_node/3, broadcast/3, step/2, active/2, members/3,
-         delivery/2, histograms/1, snapshot/1, restore/2, set_partition/2, clear_partition/1, node/2]).
+         delivery/2, histograms/1, snapshot/1, restore/2, set_partition/2, clear_partition/1, node/2,
+         begin_send_omission/3, end_send_omission/3, begin_receive_omission/3, end_receive_omission/3,
+         begin_omission/2, end_omission/2, clear_faults/1]).
 -on_load(init/0).
 
 init() ->
@@ -46,7 +48,21 @@ clear_partition(_Sim) -> erlang:nif_error(nif_not_loaded).
 %% one node: {ok, #{up, epoch, active, passive, have, round}}
 node(_Sim, _Node) -> erlang:nif_error(nif_not_loaded).
 
+%% omission faults of the pluggable manager's interposition layer (the
+%% crash-fault model's commands, test/prop_partisan_crash_fault_model.erl
+%% :93-229), pairwise over lists of ids; pluggable handles only
+begin_send_omission(Sim, Srcs, Dsts) -> omission_nif(Sim, 0, pack(Srcs), pack(Dsts), 1).
+end_send_omission(Sim, Srcs, Dsts) -> omission_nif(Sim, 0, pack(Srcs), pack(Dsts), 0).
+begin_receive_omission(Sim, Srcs, Dsts) -> omission_nif(Sim, 1, pack(Srcs), pack(Dsts), 1).
+end_receive_omission(Sim, Srcs, Dsts) -> omission_nif(Sim, 1, pack(Srcs), pack(Dsts), 0).
+begin_omission(Sim, Nodes) -> faulted_nif(Sim, pack(Nodes), 1).
+end_omission(Sim, Nodes) -> faulted_nif(Sim, pack(Nodes), 0).
+%% resolve_all_faults_with_heal
+clear_faults(_Sim) -> erlang:nif_error(nif_not_loaded).
+
 pack(Ids) -> << <<I:32/little>> || I <- Ids >>.
+omission_nif(_S, _K, _A, _B, _On) -> erlang:nif_error(nif_not_loaded).
+faulted_nif(_S, _N, _On) -> erlang:nif_error(nif_not_loaded).
 set_partition_nif(_S, _G) -> erlang:nif_error(nif_not_loaded).
 join_nif(_S, _N, _C) -> erlang:nif_error(nif_not_loaded).
 crash_nif(_S, _N) -> erlang:nif_error(nif_not_loaded).

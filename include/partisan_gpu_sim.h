@@ -64,7 +64,7 @@
 extern "C" {
 #endif
 
-#define PSIM_ABI_VERSION 5
+#define PSIM_ABI_VERSION 6
 
 /* error codes */
 #define PSIM_OK 0
@@ -200,6 +200,9 @@ typedef struct psim_round_stats {
     uint64_t digest;                         /* sum of per-message hashes of emitted messages */
     uint64_t state_bytes;                    /* algorithmic state bytes read+written */
     uint64_t overflow_by[PSIM_OVF_NKINDS];   /* overflow by table (PSIM_OVF_*), summing to overflow */
+    uint64_t omitted;                        /* pluggable: strategy messages an omission fault dropped
+                                                (at the sender: never sent, no draw; at the
+                                                receiver: never handled) -- psim_set_omission */
 } psim_round_stats;
 
 /* Canonical per-node view (inspection; unused slots zero). */
@@ -305,6 +308,33 @@ int psim_leave(psim_handle *h, const uint32_t *nodes, size_t n);
 int psim_leave_node(psim_handle *h, const uint32_t *actors, const uint32_t *targets, size_t n);
 int psim_set_partition(psim_handle *h, const uint8_t *group, size_t n);
 int psim_clear_partition(psim_handle *h);
+/* Omission faults of the pluggable manager's interposition layer
+ * (add_interposition_fun/2, remove_interposition_fun/1 pluggable:297-326;
+ * the folds in handle_cast({forward_message, ..}) :669-836 and
+ * handle_cast({receive_message, ..}) :634-667), as the crash-fault model
+ * installs them (test/prop_partisan_crash_fault_model.erl:93-196):
+ *   PSIM_OMIT_SEND     {send_omission, Dst} at Src (:158-196): a strategy
+ *                      message Src forwards to Dst becomes `undefined` -- not
+ *                      sent, no connection lookup, no dispatch draw;
+ *   PSIM_OMIT_RECEIVE  {receive_omission, Src} at Dst (:117-155): a strategy
+ *                      message Dst receives from Src is dropped unhandled.
+ * on = 1 installs (src[i], dst[i]) pairs, on = 0 removes them (installing a
+ * pair twice keeps one: the funs are a dict keyed by name).
+ * psim_set_faulted is the general omission begin_omission/end_omission
+ * (:93-114, `faulted` read by the interposition funs of
+ * partisan_trace_orchestrator:621-656): every strategy message the node
+ * sends or receives is dropped.  The hello/state handshake is the
+ * client/server processes' and passes.  psim_clear_faults removes all
+ * (resolve_all_faults_with_heal :198-229 removes every interposition fun,
+ * the `faulted` reader included).  Changes take effect at the start of
+ * the next round; dropped messages count in psim_round_stats.omitted.
+ * PSIM_EUNSUPPORTED for HyParView handles (that manager has no interposition
+ * layer). */
+#define PSIM_OMIT_SEND 0
+#define PSIM_OMIT_RECEIVE 1
+int psim_set_omission(psim_handle *h, int kind, const uint32_t *src, const uint32_t *dst, size_t n, int on);
+int psim_set_faulted(psim_handle *h, const uint32_t *nodes, size_t n, int on);
+int psim_clear_faults(psim_handle *h);
 /* broadcast/2 at `root` (plumtree:176-178) with the partisan_plumtree_backend
  * heartbeat semantics (backend:179-200), originated in the next round.  Any
  * node can be a root; per round at most one broadcast per root and per

@@ -123,6 +123,12 @@ struct psim_handle {
                                        removes (tombstones); member = add & ~rmv */
     uint32_t *pay_in, *pay_out;     /* full: gossip payload snapshots of rounds r-1 and r */
     size_t pay_out_n, pay_out_cap, pay_in_cap;
+    /* omission faults (interposition funs, pluggable:297-326): the pairs
+     * (src << 32 | dst) of the installed {send_omission, Dst} funs at Src and
+     * {receive_omission, Src} funs at Dst, and the generally omitting nodes;
+     * nx_* are the next round's (the API edits them, round_begin adopts them) */
+    struct fault_set { uint64_t *send, *recv; size_t send_n, recv_n; uint8_t *faulted; } flt, nx;
+    int faults_dirty;
 };
 
 /* per-node execution context */
@@ -135,6 +141,7 @@ typedef struct ctx {
     int dirty;                      /* full: state changed since that snapshot */
     int gossip_due;                 /* full, fanout > 0: a coalesced gossip is owed this round */
     int stop;                       /* the manager stopped in this round (leave, App. A Q12) */
+    uint32_t nomit_send;            /* sends an omission fault dropped this round */
 } ctx;
 
 /* a fixed-table overflow of kind PSIM_OVF_* */
@@ -831,7 +838,7 @@ static int timer_due(uint32_t period, uint64_t r, uint32_t start) {
 
 static void process_node(struct psim_handle *h, uint32_t n) {
     node *s = &h->nodes[n];
-    ctx c = {h, s, n, 0, PSIM_NONE, 0, 0, 0};
+    ctx c = {h, s, n, 0, PSIM_NONE, 0, 0, 0, 0};
     uint64_t r = h->round;
     size_t b = h->in_beg[n], e = h->in_beg[n + 1];
     /* a fresh incarnation has no connections: traffic addressed to the
@@ -942,7 +949,32 @@ static void pl_emit(ctx *c, uint32_t dst, uint32_t type, uint32_t a0, uint32_t s
  * keeps a connection to every member and pending node, so the send succeeds
  * iff Peer is one of them, runs and is not partitioned away; a successful
  * dispatch draws rand:uniform(1) (partisan_util:dispatch_pid/3 util:190-195). */
+static int pair_in(const uint64_t *l, size_t n, uint32_t src, uint32_t dst) {
+    uint64_t k = (uint64_t)src << 32 | dst;
+    for (size_t i = 0; i < n; i++) if (l[i] == k) return 1;
+    return 0;
+}
+
+/* the dict:fold of the interposition funs over a forwarded strategy message
+ * (handle_cast({forward_message, ..}) pluggable:669-684): {send_omission, Dst}
+ * (prop_partisan_crash_fault_model:166-177) and the `faulted` reader
+ * (partisan_trace_orchestrator:623-637) turn it into `undefined` */
+static int omit_send(ctx *c, uint32_t dst) {
+    struct psim_handle *h = c->h;
+    return h->flt.faulted[c->me] || pair_in(h->flt.send, h->flt.send_n, c->me, dst);
+}
+
+/* ... and over a received one (handle_cast({receive_message, ..}) :634-667):
+ * {receive_omission, Src} (crash_fault_model:125-135), `faulted` (:638-650) */
+static int omit_recv(ctx *c, uint32_t src) {
+    struct psim_handle *h = c->h;
+    return h->flt.faulted[c->me] || pair_in(h->flt.recv, h->flt.recv_n, src, c->me);
+}
+
 static int pl_send(ctx *c, uint32_t dst, uint32_t type, uint32_t a0, uint32_t slot) {
+    /* forward_message's interposition fold runs first: an omitted message
+     * is never looked up in the connections nor dispatched (pluggable:727-760) */
+    if (omit_send(c, dst)) { c->h->st->omitted++; c->nomit_send++; return 0; }
     /* full: every target comes from the node's own member row, or is an old
      * member whose connection is still open (leave/1) */
     int full = c->h->cfg.strategy == PSIM_STRATEGY_FULL;
@@ -1219,7 +1251,7 @@ int orc_crash(struct psim_handle *h, const uint32_t *nodes, size_t n);
 static void pl_process_node(struct psim_handle *h, uint32_t n) {
     node *s = &h->nodes[n];
     snode *q = &h->sn[n];
-    ctx c = {h, s, n, 0, PSIM_NONE, 0, 0, 0};
+    ctx c = {h, s, n, 0, PSIM_NONE, 0, 0, 0, 0};
     uint64_t r = h->round;
     size_t b = h->in_beg[n], e = h->in_beg[n + 1];
     if (s->start_round == r && e > b) { h->st->dropped += e - b; e = b; }
@@ -1243,6 +1275,12 @@ static void pl_process_node(struct psim_handle *h, uint32_t n) {
         else h->st->send_fail++;
     }
     for (size_t i = b; i < e && !c.stop; i++) {
+        /* strategy messages pass the receive interposition; hello / state
+         * are the client and server processes' */
+        if (h->inbox.v[i].type >= PSIM_PL_GOSSIP && omit_recv(&c, h->inbox.v[i].src)) {
+            h->st->omitted++;
+            continue;
+        }
         h->st->delivered[h->inbox.v[i].type]++;
         pl_handle(&c, &h->inbox.v[i]);
         if (c.stop) h->st->dropped += e - i - 1;
@@ -1251,6 +1289,9 @@ static void pl_process_node(struct psim_handle *h, uint32_t n) {
         h->out.n = out0;
         memcpy(h->st->emitted, em0, sizeof em0);
         h->st->digest = dig0; h->st->send_fail = fail0;
+        /* the receive-side omissions of the inbox before the stop stand;
+         * the send-side ones were casts to itself that never ran */
+        h->st->omitted -= c.nomit_send;
         orc_crash(h, &n, 1);
         return;
     }
@@ -1319,6 +1360,15 @@ static void round_begin(struct psim_handle *h, psim_round_stats *st) {
     h->pend_lv_n = 0;
     if (h->pend_part_clear) memset(h->part, 0, h->N);
     if (h->pend_part_set) memcpy(h->part, h->pend_part, h->N);
+    if (h->faults_dirty) {          /* interposition funs installed / removed */
+        memcpy(h->flt.faulted, h->nx.faulted, h->N);
+        h->flt.send = (uint64_t *)realloc(h->flt.send, (h->nx.send_n + 1) * 8);
+        h->flt.recv = (uint64_t *)realloc(h->flt.recv, (h->nx.recv_n + 1) * 8);
+        if (h->nx.send_n) memcpy(h->flt.send, h->nx.send, h->nx.send_n * 8);
+        if (h->nx.recv_n) memcpy(h->flt.recv, h->nx.recv, h->nx.recv_n * 8);
+        h->flt.send_n = h->nx.send_n; h->flt.recv_n = h->nx.recv_n;
+        h->faults_dirty = 0;
+    }
     /* broadcasts: each takes its message slot (the slot's previous id is
      * retired: its delivery bit cleared everywhere) and is originated this
      * round at its root if the root runs; the last one is the tracked one */
@@ -1434,7 +1484,9 @@ int orc_create(const psim_config *cfg, struct psim_handle **out) {
         }
     }
     h->origin = (uint32_t *)calloc(h->N, sizeof(uint32_t));
-    if (!h->origin) return PSIM_ENOMEM;
+    h->flt.faulted = (uint8_t *)calloc(h->N, 1);
+    h->nx.faulted = (uint8_t *)calloc(h->N, 1);
+    if (!h->origin || !h->flt.faulted || !h->nx.faulted) return PSIM_ENOMEM;
     for (int k = 0; k < PSIM_MSG_SLOTS; k++) h->slot_msg[k] = h->slot_root[k] = PSIM_NONE;
     h->tracked_msg = PSIM_NONE;
     *out = h;
@@ -1448,6 +1500,8 @@ void orc_destroy(struct psim_handle *h) {
     free(h->pend_crash); free(h->pend_join); free(h->pend_contact); free(h->pend_join_mark); free(h->origin);
     free(h->pend_lv_a); free(h->pend_lv_t);
     free(h->sn); free(h->fbits); free(h->pay_in); free(h->pay_out);
+    free(h->flt.send); free(h->flt.recv); free(h->flt.faulted);
+    free(h->nx.send); free(h->nx.recv); free(h->nx.faulted);
     free(h);
 }
 
@@ -1549,6 +1603,49 @@ int orc_set_partition(struct psim_handle *h, const uint8_t *group, size_t n) {
 
 int orc_clear_partition(struct psim_handle *h) {
     h->pend_part_clear = 1; h->pend_part_set = 0;
+    return PSIM_OK;
+}
+
+/* psim_set_omission: add_interposition_fun / remove_interposition_fun of
+ * {send_omission, Dst} at Src or {receive_omission, Src} at Dst
+ * (pluggable:297-310; prop_partisan_crash_fault_model:117-196).  The funs
+ * are a dict keyed by name: a pair is installed at most once. */
+int orc_set_omission(struct psim_handle *h, int kind, const uint32_t *src, const uint32_t *dst, size_t n, int on) {
+    if (!is_pl(h)) return PSIM_EUNSUPPORTED;      /* the HyParView manager has no interposition */
+    if (kind != PSIM_OMIT_SEND && kind != PSIM_OMIT_RECEIVE) return PSIM_EINVAL;
+    for (size_t i = 0; i < n; i++) if (src[i] >= h->N || dst[i] >= h->N) return PSIM_ERANGE;
+    uint64_t **l = kind == PSIM_OMIT_SEND ? &h->nx.send : &h->nx.recv;
+    size_t *ln = kind == PSIM_OMIT_SEND ? &h->nx.send_n : &h->nx.recv_n;
+    for (size_t i = 0; i < n; i++) {
+        uint64_t k = (uint64_t)src[i] << 32 | dst[i];
+        size_t j = 0;
+        while (j < *ln && (*l)[j] != k) j++;
+        if (on && j == *ln) {
+            *l = (uint64_t *)realloc(*l, (*ln + 1) * 8);
+            (*l)[(*ln)++] = k;
+        } else if (!on && j < *ln) {
+            (*l)[j] = (*l)[--(*ln)];
+        }
+    }
+    h->faults_dirty = 1;
+    return PSIM_OK;
+}
+
+/* psim_set_faulted: begin_omission / end_omission (crash_fault_model:93-114) */
+int orc_set_faulted(struct psim_handle *h, const uint32_t *nodes, size_t n, int on) {
+    if (!is_pl(h)) return PSIM_EUNSUPPORTED;
+    for (size_t i = 0; i < n; i++) if (nodes[i] >= h->N) return PSIM_ERANGE;
+    for (size_t i = 0; i < n; i++) h->nx.faulted[nodes[i]] = on ? 1 : 0;
+    h->faults_dirty = 1;
+    return PSIM_OK;
+}
+
+/* psim_clear_faults: resolve_all_faults_with_heal (crash_fault_model:198-229) */
+int orc_clear_faults(struct psim_handle *h) {
+    if (!is_pl(h)) return PSIM_EUNSUPPORTED;
+    h->nx.send_n = h->nx.recv_n = 0;
+    memset(h->nx.faulted, 0, h->N);
+    h->faults_dirty = 1;
     return PSIM_OK;
 }
 

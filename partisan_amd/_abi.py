@@ -8,7 +8,7 @@ import ctypes as C
 
 import numpy as np
 
-PSIM_ABI_VERSION = 5
+PSIM_ABI_VERSION = 6
 PSIM_MAP_BIT = 0x80000000
 PSIM_NONE = 0xFFFFFFFF
 ACTIVE_CAP, PASSIVE_CAP, IDMAP_CAP = 8, 32, 64
@@ -24,7 +24,8 @@ MSG_TYPES = [
     "NEIGHBOR_ACCEPTED", "NEIGHBOR_REJECTED", "SHUFFLE", "SHUFFLE_REPLY",
     "PT_BROADCAST", "PT_PRUNE", "PT_IHAVE", "PT_IGNORED_IHAVE", "PT_GRAFT",
 ]
-PL_MSG_TYPES = ["HELLO", "STATE", "GOSSIP", "FWD_SUB", "PING", "KEEP_SUB"]
+PL_MSG_TYPES = ["HELLO", "STATE", "GOSSIP", "FWD_SUB", "PING", "KEEP_SUB", "REMOVE_SUB", "BOOT_REMOVE"]
+OMIT_SEND, OMIT_RECEIVE = 0, 1
 HV_TYPES = list(range(0, 9))
 PT_TYPES = list(range(9, 14))
 
@@ -58,6 +59,7 @@ class PsimRoundStats(C.Structure):
         ("nodes_up", C.c_uint64), ("nodes_processed", C.c_uint64), ("exits", C.c_uint64),
         ("send_fail", C.c_uint64), ("first_deliveries", C.c_uint64), ("overflow", C.c_uint64),
         ("digest", C.c_uint64), ("state_bytes", C.c_uint64), ("overflow_by", C.c_uint64 * 4),
+        ("omitted", C.c_uint64),
     ]
 
 
@@ -127,6 +129,9 @@ SIGNATURES = {
     "leave_node": (C.c_int, [_H, _P32, _P32, C.c_size_t]),
     "set_partition": (C.c_int, [_H, C.POINTER(C.c_uint8), C.c_size_t]),
     "clear_partition": (C.c_int, [_H]),
+    "set_omission": (C.c_int, [_H, C.c_int, _P32, _P32, C.c_size_t, C.c_int]),
+    "set_faulted": (C.c_int, [_H, _P32, C.c_size_t, C.c_int]),
+    "clear_faults": (C.c_int, [_H]),
     "broadcast": (C.c_int, [_H, C.c_uint32, C.c_uint32]),
     "step": (C.c_int, [_H, C.c_uint32, C.POINTER(PsimRoundStats)]),
     "get_nodes": (C.c_int, [_H, C.c_uint32, C.c_uint32, C.POINTER(PsimNodeView)]),

@@ -114,6 +114,7 @@ enum {
     ST_EMIT = 0, ST_DELIV = 16, ST_DROPPED = 32, ST_UP, ST_PROC, ST_EXITS, ST_FAIL, ST_FIRST,
     ST_OVF, ST_DIGEST, ST_BYTES, ST_STOP,
     ST_BOUND,       // nodes that emitted more records than their outbox bound (an engine bug: fails the round)
+    ST_OMIT,        // pluggable: strategy messages an omission fault dropped
     ST_OVF_BY, NST = ST_OVF_BY + PSIM_OVF_NKINDS
 };
 

@@ -29,6 +29,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <new>
+#include <set>
 #include <vector>
 
 #include "psim_device.h"
@@ -1024,6 +1025,8 @@ struct Shard {
     // pluggable manager
     DBuf<uint32_t> sview, sinv, fbits, pay[2], pay_top;
     int pay_cur = 0;
+    DBuf<uint8_t> faulted;              // omission faults: generally omitting nodes (global id)
+    DBuf<uint64_t> omit;                // ... sorted send-omission pairs, then receive-omission pairs
     std::vector<uint64_t> soff, scnt;   // per destination shard (G + 1 offsets)
     uint32_t pgrid = 0, cgrid = 0, rgrid = 0, tgrid = 0;   // stats rows: prepare, consume, relay, plumtree blocks
     // pinned host words: NST stats and the consume span (stat_out), then the
@@ -1067,6 +1070,14 @@ struct psim_handle {
     uint32_t fw = 0;                    // full strategy: words per member row (adds; removes beside)
     bool tomb = false;                  // full: an ORSet remove exists (leave/1): kernels read remove rows
     std::vector<uint8_t> started;       // full strategy: ids ever started (no restarts)
+    // omission faults (pluggable): the next round's installed funs, edited by
+    // psim_set_omission / psim_set_faulted and uploaded when changed; the
+    // counts of the ones in force
+    std::set<uint64_t> nx_omit_s, nx_omit_r;
+    std::vector<uint8_t> nx_faulted;
+    size_t nx_nfaulted = 0;
+    bool faults_dirty = false;
+    uint32_t faults = 0, n_omit_s = 0, n_omit_r = 0;
     double kt_ms[KT_N] = {0};
     uint64_t kt_n[KT_N] = {0};
     // per-phase event timers (PSIM_PHASE_TIMERS=1): each event pair puts a
@@ -1112,6 +1123,8 @@ RoundArgs make_args(psim_handle* h, Shard* s) {
     a.desc_slow = s->desc_slow.p; a.n_slow = s->n_slow.p;
     a.desc_pt = s->desc_pt.p; a.n_pt = s->n_pt.p;
     a.stop_ids = s->stop_ids.p; a.n_stop = s->n_stop.p;
+    a.faults = h->faults; a.n_omit_s = h->n_omit_s; a.n_omit_r = h->n_omit_r;
+    a.faulted = s->faulted.p; a.omit = s->omit.p;
     return a;
 }
 
@@ -1276,6 +1289,16 @@ struct RoundCtl {
 // events + prepare for one shard; leaves `a` ready for k_consume
 int phase_events_prepare(psim_handle* h, Shard* s, const RoundCtl& ctl, RoundArgs& a) {
     const uint32_t n = s->n;
+    if (h->faults_dirty) {              // interposition funs installed / removed
+        std::vector<uint64_t> keys(h->nx_omit_s.begin(), h->nx_omit_s.end());
+        keys.insert(keys.end(), h->nx_omit_r.begin(), h->nx_omit_r.end());
+        TRY(s->faulted.ensure(h->N));
+        TRY(s->omit.ensure(std::max<size_t>(keys.size(), 1)));
+        HIP_TRY(hipMemcpyAsync(s->faulted.p, h->nx_faulted.data(), h->N, hipMemcpyHostToDevice, s->stream));
+        if (!keys.empty())
+            HIP_TRY(hipMemcpyAsync(s->omit.p, keys.data(), keys.size() * 8, hipMemcpyHostToDevice, s->stream));
+        HIP_TRY(hipStreamSynchronize(s->stream));   // (the host vector goes out of scope)
+    }
     a = make_args(h, s);
     a.crash_round = ctl.crashes;
     {
@@ -1619,6 +1642,12 @@ int run_round(psim_handle* h, uint64_t* st) {
         }
         h->tracked_msg = h->pend_b_msg.back();
     }
+    if (h->faults_dirty) {              // the funs in force from this round
+        if (h->nx_faulted.size() != h->N) h->nx_faulted.assign(h->N, 0);
+        h->n_omit_s = (uint32_t)h->nx_omit_s.size();
+        h->n_omit_r = (uint32_t)h->nx_omit_r.size();
+        h->faults = h->n_omit_s || h->n_omit_r || h->nx_nfaulted;
+    }
     for (Shard* s : h->shards) s->tn = 0;        // (timers of a round that failed)
     std::vector<RoundArgs> args(h->shards.size());   // (consume fills the payload arena fields)
     for (size_t i = 0; i < h->shards.size(); i++) TRY(phase_events_prepare(h, h->shards[i], ctl, args[i]));
@@ -1705,6 +1734,7 @@ int run_round(psim_handle* h, uint64_t* st) {
         h->pend_crash.insert(h->pend_crash.end(), ids.begin(), ids.end());
     }
     h->pend_part_set = h->pend_part_clear = false;
+    h->faults_dirty = false;
     h->pend_b_root.clear(); h->pend_b_msg.clear();
     h->round++;
     return PSIM_OK;
@@ -1721,6 +1751,7 @@ void fill_stats(const uint64_t* s, uint64_t round, psim_round_stats* o) {
     o->exits = s[ST_EXITS]; o->send_fail = s[ST_FAIL]; o->first_deliveries = s[ST_FIRST];
     o->overflow = s[ST_OVF]; o->digest = s[ST_DIGEST]; o->state_bytes = s[ST_BYTES];
     for (int k = 0; k < PSIM_OVF_NKINDS; k++) o->overflow_by[k] = s[ST_OVF_BY + k];
+    o->omitted = s[ST_OMIT];
 }
 
 int shard_alloc(psim_handle* h, Shard* s) {
@@ -2018,6 +2049,52 @@ int psim_set_partition(psim_handle* h, const uint8_t* group, size_t n) {
 int psim_clear_partition(psim_handle* h) {
     if (!h) return PSIM_EINVAL;
     h->pend_part_clear = true; h->pend_part_set = false;
+    return PSIM_OK;
+}
+
+// omission faults: add_interposition_fun / remove_interposition_fun
+// (pl:297-326) of the crash-fault model's {send_omission, Dst} and
+// {receive_omission, Src} funs (prop_partisan_crash_fault_model:117-196)
+int psim_set_omission(psim_handle* h, int kind, const uint32_t* src, const uint32_t* dst, size_t n, int on) {
+    if (!h || (n && (!src || !dst))) return PSIM_EINVAL;
+    if (h->cfg.manager != PSIM_MANAGER_PLUGGABLE) return PSIM_EUNSUPPORTED;
+    if (kind != PSIM_OMIT_SEND && kind != PSIM_OMIT_RECEIVE) return PSIM_EINVAL;
+    for (size_t i = 0; i < n; i++)
+        if (src[i] >= h->N || dst[i] >= h->N) return PSIM_ERANGE;
+    std::set<uint64_t>& l = kind == PSIM_OMIT_SEND ? h->nx_omit_s : h->nx_omit_r;
+    for (size_t i = 0; i < n; i++) {
+        const uint64_t k = (uint64_t)src[i] << 32 | dst[i];
+        if (on) l.insert(k);
+        else l.erase(k);
+    }
+    h->faults_dirty = true;
+    return PSIM_OK;
+}
+
+// begin_omission / end_omission (crash_fault_model:93-114)
+int psim_set_faulted(psim_handle* h, const uint32_t* nodes, size_t n, int on) {
+    if (!h || (n && !nodes)) return PSIM_EINVAL;
+    if (h->cfg.manager != PSIM_MANAGER_PLUGGABLE) return PSIM_EUNSUPPORTED;
+    for (size_t i = 0; i < n; i++)
+        if (nodes[i] >= h->N) return PSIM_ERANGE;
+    if (h->nx_faulted.size() != h->N) h->nx_faulted.assign(h->N, 0);
+    for (size_t i = 0; i < n; i++) {
+        const uint8_t v = on ? 1 : 0;
+        h->nx_nfaulted += (size_t)v - (size_t)h->nx_faulted[nodes[i]];
+        h->nx_faulted[nodes[i]] = v;
+    }
+    h->faults_dirty = true;
+    return PSIM_OK;
+}
+
+// resolve_all_faults_with_heal (crash_fault_model:198-229)
+int psim_clear_faults(psim_handle* h) {
+    if (!h) return PSIM_EINVAL;
+    if (h->cfg.manager != PSIM_MANAGER_PLUGGABLE) return PSIM_EUNSUPPORTED;
+    h->nx_omit_s.clear(); h->nx_omit_r.clear();
+    h->nx_faulted.assign(h->N, 0);
+    h->nx_nfaulted = 0;
+    h->faults_dirty = true;
     return PSIM_OK;
 }
 
@@ -2408,7 +2485,7 @@ static std::vector<Section> snap_sections(psim_handle* h, Shard* s, const ShardH
 int psim_snapshot(psim_handle* h, void* buf, size_t cap, size_t* need) {
     if (!h || !need) return PSIM_EINVAL;
     if (!h->pend_crash.empty() || !h->pend_join.empty() || !h->pend_lv_a.empty() || h->pend_part_set || h->pend_part_clear ||
-        !h->pend_b_root.empty())
+        !h->pend_b_root.empty() || h->faults || h->faults_dirty)   // (faults: host state, not snapshotted)
         return PSIM_ESTATE;
     if (hipSetDevice(h->device) != hipSuccess) return PSIM_EDEVICE;
     std::vector<ShardHead> heads;

@@ -72,6 +72,13 @@ struct RoundArgs {
     uint32_t* sinv;              // scamp v2: in_view rows
     uint32_t* stop_ids;          // pluggable: managers that stopped this round
     uint32_t* n_stop;            //   (their count, reset by k_node_prep)
+    // pluggable: omission faults (interposition funs, pl:297-326): the
+    // generally omitting nodes (global id) and the sorted pair keys
+    // src << 32 | dst of the send omissions, then those of the receive
+    // omissions; `faults` = any installed (else nothing is read)
+    uint32_t faults, n_omit_s, n_omit_r;
+    const uint8_t* faulted;
+    const uint64_t* omit;
 };
 
 __global__ void k_consume(RoundArgs args);

@@ -52,6 +52,7 @@ struct Pw {
     bool dirty, gossip_due;
     bool stop;                     // the manager stopped this round (leave, App. A Q12)
     uint32_t nfail;                // this node's failed sends this round (uniform)
+    uint32_t nomit;                // ... and its sends an omission fault dropped
 };
 
 DEV void st_add(Pw& w, int k, uint32_t v) { w.SC += lane_id() == (uint32_t)k ? v : 0u; }
@@ -152,9 +153,37 @@ DEV bool connected(const Pw& w, uint32_t p) {
     return ballot(lane_id() < w.vn && w.V == p) != 0 || p == w.h.join_contact;
 }
 
+// ---------------------------------------------------- omission faults --
+// the installed interposition funs (pl:297-326) as sorted pair keys
+// src << 32 | dst: a wave-uniform binary search
+DEV bool pair_in(const uint64_t* l, uint32_t n, uint64_t k) {
+    uint32_t lo = 0, hi = n;
+    while (lo < hi) {
+        const uint32_t m = (lo + hi) >> 1;
+        if (l[m] < k) lo = m + 1;
+        else hi = m;
+    }
+    return lo < n && l[lo] == k;
+}
+// the fold of handle_cast({forward_message, ..}) (pl:669-684) turns the
+// message into `undefined`: {send_omission, Dst} at the sender
+// (prop_partisan_crash_fault_model:166-177), the `faulted` reader
+// (partisan_trace_orchestrator:623-637)
+DEV bool omit_send(const Pw& w, uint32_t dst) {
+    return kargs().faulted[w.me] || pair_in(kargs().omit, kargs().n_omit_s, (uint64_t)w.me << 32 | dst);
+}
+// ... and that of handle_cast({receive_message, ..}) (pl:634-667):
+// {receive_omission, Src} at the receiver (crash_fault_model:125-135)
+DEV bool omit_recv(const Pw& w, uint32_t src) {
+    return kargs().faulted[w.me] ||
+           pair_in(kargs().omit + kargs().n_omit_s, kargs().n_omit_r, (uint64_t)src << 32 | w.me);
+}
+
 // do_send_message/7 (pl:1309-1363); success draws rand:uniform(1) in
-// partisan_util:dispatch_pid/3 (util:190-195)
+// partisan_util:dispatch_pid/3 (util:190-195).  The interposition fold runs
+// first: an omitted message meets no connection lookup and no draw (pl:727-760)
 DEV void pl_send(Pw& w, uint32_t dst, uint32_t type, uint32_t a0, uint32_t slot) {
+    if (kargs().faults && omit_send(w, dst)) { st_add(w, ST_OMIT, 1); w.nomit++; return; }
     if (!connect_ok(w, dst) || !connected(w, dst)) { st_add(w, ST_FAIL, 1); w.nfail++; return; }
     w.h.rng++;
     emit(w, dst, type, a0, slot);
@@ -480,7 +509,7 @@ DEV void process_pl(Pw& w, uint32_t n, uint32_t ib, uint32_t ik, uint32_t ob) {
     w.stop = false;
     // a manager that stops this round sends nothing: its sends are casts to
     // itself (schedule_self_message_delivery/6 pl:1585-1609)
-    w.nfail = 0;
+    w.nfail = 0; w.nomit = 0;
 
     if (leave) {                   // leave/1 (pl:502-515, :1390-1420)
         w.h.pad1[0] = 0;
@@ -502,6 +531,12 @@ DEV void process_pl(Pw& w, uint32_t n, uint32_t ib, uint32_t ik, uint32_t ob) {
         for (uint32_t q = 0; q < cm; q++) {
             uint32_t b = q * 16;
             uint32_t type = rl(R4, b + 2) & 0xFF;
+            // strategy messages pass the receive interposition (hello /
+            // state are the client and server processes')
+            if (kargs().faults && type >= PSIM_PL_GOSSIP && omit_recv(w, rl(R4, b + 1))) {
+                st_add(w, ST_OMIT, 1);
+                continue;
+            }
             st_add(w, ST_DELIV + type, 1);
             pl_handle(w, type, rl(R4, b + 1), rl(R4, b + 4), rl(R4, b + 7));
             if (w.stop) { st_add(w, ST_DROPPED, ik - (c + q) - 1); break; }
@@ -518,6 +553,7 @@ DEV void process_pl(Pw& w, uint32_t n, uint32_t ib, uint32_t ik, uint32_t ob) {
             st_add(w, ST_EMIT + rl(word, 2), (uint32_t)-1);
         }
         st_add(w, ST_FAIL, (uint32_t)-w.nfail);
+        st_add(w, ST_OMIT, (uint32_t)-w.nomit);   // (casts to itself that never ran)
         st_add(w, ST_STOP, 1);
         if (l2 == 0) a.stop_ids[atomicAdd(a.n_stop, 1u)] = n;
         w.seq = 0;

@@ -116,6 +116,44 @@ class _Driver:
     def clear_partition(self):
         self._check(self._api["clear_partition"](self._h), "clear_partition")
 
+    # ---- omission faults of the pluggable manager's interposition layer
+    # (add_interposition_fun/2, pluggable:297-326; the crash-fault model's
+    # begin/end_send_omission, begin/end_receive_omission, begin/end_omission,
+    # resolve_all_faults_with_heal: prop_partisan_crash_fault_model:93-229)
+    def _omission(self, kind, src, dst, on):
+        s = np.ascontiguousarray(np.atleast_1d(src), np.uint32)
+        d = np.ascontiguousarray(np.atleast_1d(dst), np.uint32)
+        if s.size != d.size:
+            raise ValueError("src and dst differ in length")
+        self._check(self._api["set_omission"](self._h, kind, _abi.u32p(s), _abi.u32p(d), s.size, int(on)),
+                    "set_omission")
+
+    def begin_send_omission(self, src, dst):
+        """Messages src forwards to dst are dropped at src (never sent)."""
+        self._omission(_abi.OMIT_SEND, src, dst, True)
+
+    def end_send_omission(self, src, dst):
+        self._omission(_abi.OMIT_SEND, src, dst, False)
+
+    def begin_receive_omission(self, src, dst):
+        """Messages dst receives from src are dropped at dst (never handled)."""
+        self._omission(_abi.OMIT_RECEIVE, src, dst, True)
+
+    def end_receive_omission(self, src, dst):
+        self._omission(_abi.OMIT_RECEIVE, src, dst, False)
+
+    def begin_omission(self, nodes):
+        """General omission: every strategy message the nodes send or receive."""
+        n = np.ascontiguousarray(np.atleast_1d(nodes), np.uint32)
+        self._check(self._api["set_faulted"](self._h, _abi.u32p(n), n.size, 1), "set_faulted")
+
+    def end_omission(self, nodes):
+        n = np.ascontiguousarray(np.atleast_1d(nodes), np.uint32)
+        self._check(self._api["set_faulted"](self._h, _abi.u32p(n), n.size, 0), "set_faulted")
+
+    def resolve_all_faults(self):
+        self._check(self._api["clear_faults"](self._h), "clear_faults")
+
     def broadcast(self, root, msg_id):
         self._check(self._api["broadcast"](self._h, root, msg_id), "broadcast")
 

@@ -7,7 +7,7 @@ from partisan_amd import workloads as W
 from partisan_amd.sim import default_config
 
 STAT_FIELDS = ["emitted", "delivered", "dropped", "nodes_up", "nodes_processed", "exits",
-               "send_fail", "first_deliveries", "overflow", "overflow_by", "digest"]
+               "send_fail", "first_deliveries", "overflow", "overflow_by", "digest", "omitted"]
 
 
 def _bcast_every(sim, period, first, root=0, count=None):
@@ -201,6 +201,53 @@ def pl_leave_remote(make, n, seed, rounds, strategy, leave_at=40, k=16, part_at=
             sim.clear_partition()
     st = sim.run_schedule(W.doubling_join(n, seed), rounds, extra=hook)
     return sim, st, np.array(picked["a"], np.uint32), np.array(picked["t"], np.uint32)
+
+
+def pl_omission(make, n, seed, rounds, strategy, fanout=0, begin=40, end=60, heal=75, k=None):
+    """The crash-fault model's omission faults (prop_partisan_crash_fault_model
+    :93-229) on a pluggable handle: a doubling bootstrap; at `begin` k nodes
+    start a general omission (begin_omission), k send omissions and k receive
+    omissions are installed on pairs drawn from the nodes' views (SCAMP; the
+    full strategy: random pairs); at `end` half of each kind ends; at `heal`
+    resolve_all_faults_with_heal.  Returns (sim, stats, faults) with faults =
+    dict(general=ids, send=(src, dst), recv=(src, dst))."""
+    sim = make(default_config(n_nodes=n, seed=seed, manager=1, strategy=strategy, fanout=fanout))
+    rng = np.random.Generator(np.random.PCG64([seed, 13]))
+    k = k or max(2, n // 32)
+    f = {}
+
+    def pairs():
+        if strategy == 0:
+            s = rng.choice(n, size=k, replace=False).astype(np.uint32)
+            d = ((s.astype(np.int64) + 1 + rng.integers(0, n - 1, size=k)) % n).astype(np.uint32)
+            return s, d
+        v = sim.strategy_nodes()
+        src, dst = [], []
+        for x in rng.permutation(n):
+            row = [int(y) for y in v["view"][x][: v["view_n"][x]] if int(y) != x]
+            if row:
+                src.append(int(x)); dst.append(row[int(rng.integers(0, len(row)))])
+            if len(src) == k:
+                break
+        return np.array(src, np.uint32), np.array(dst, np.uint32)
+
+    def hook(r):
+        if r == begin:
+            f["general"] = np.sort(rng.choice(np.arange(1, n), size=k, replace=False)).astype(np.uint32)
+            f["send"], f["recv"] = pairs(), pairs()
+            sim.begin_omission(f["general"])
+            sim.begin_send_omission(*f["send"])
+            sim.begin_receive_omission(*f["recv"])
+            sim.begin_send_omission(*f["send"])          # a second install keeps one fun
+        if r == end:
+            h = k // 2
+            sim.end_omission(f["general"][:h])
+            sim.end_send_omission(f["send"][0][:h], f["send"][1][:h])
+            sim.end_receive_omission(f["recv"][0][:h], f["recv"][1][:h])
+        if r == heal:
+            sim.resolve_all_faults()
+    st = sim.run_schedule(W.doubling_join(n, seed), rounds, extra=hook)
+    return sim, st, f
 
 
 def compare_strategy(a, b, full_bits=None):

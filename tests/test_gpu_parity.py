@@ -210,6 +210,22 @@ def test_strategy_remote_leave_parity(strategy):
         S.compare_strategy(gs, os_)
 
 
+@pytest.mark.parametrize("strategy,n,fanout", [(0, 32, 0), (0, 2048, 5), (1, 2048, 0), (2, 2048, 0)])
+def test_omission_fault_parity(strategy, n, fanout):
+    """The crash-fault model's omissions (general, send, receive; partly
+    ended, then healed) through the interposition layer: bit-identical to
+    the oracle, unsharded and over 4 virtual shards (SCAMP)."""
+    def sharded(cfg):
+        cfg.n_shards = 4
+        return _gpu(cfg)
+    os_, ost, _ = S.pl_omission(Oracle, n, 23, 100, strategy, fanout)
+    assert ost["omitted"].sum() > 0
+    for make in (_gpu, sharded) if strategy else (_gpu,):
+        gs, gst, _ = S.pl_omission(make, n, 23, 100, strategy, fanout)
+        S.compare_stats(gst, ost)
+        S.compare_strategy(gs, os_, full_bits=[0, 1, n // 2, n - 1] if strategy == 0 else None)
+
+
 @pytest.mark.parametrize("n,fanout", [(32, 0), (2048, 5)])
 def test_full_remote_leave_parity(n, fanout):
     """psim_leave_node under the full strategy: ORSet remove rows (tombstones)

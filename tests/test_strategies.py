@@ -212,3 +212,99 @@ def test_pluggable_rejects_broadcast():
     sim = Oracle(default_config(n_nodes=8, manager=1, strategy=1))
     with pytest.raises(Exception):
         sim.broadcast(0, 1)
+
+
+# ---------------------------------------------------------------- omission faults
+# The crash-fault model's omissions (prop_partisan_crash_fault_model:93-229)
+# through the pluggable manager's interposition funs (pluggable:297-326,
+# :634-836): a dropped send never reaches the connection lookup or the
+# dispatch draw, a dropped receive is never handled.
+
+@pytest.mark.parametrize("strategy,fanout", [(0, 5), (1, 0), (2, 0)])
+def test_omission_faults_drop_and_heal(strategy, fanout):
+    n = 1024
+    sim, st, f = S.pl_omission(Oracle, n, 21, 120, strategy, fanout)
+    assert st["omitted"][:40].sum() == 0
+    assert st["omitted"][40:75].sum() > 0
+    assert st["omitted"][76:].sum() == 0                  # healed (resolve_all_faults_with_heal)
+    assert st["overflow"].sum() == 0
+    if strategy == 0:                                     # the ORSet converges again after the heal
+        v = sim.strategy_nodes()
+        assert (v["members"] == n).all()
+    else:
+        assert _weakly_connected(_views(sim))
+
+
+def test_omission_that_never_matches_changes_nothing():
+    """installed funs whose pairs never carry a message (and a general
+    omission of nodes that never start) leave the run bit-identical"""
+    n = 1024
+
+    def quiet(make):
+        sim = make(default_config(n_nodes=n + 8, seed=4, manager=1, strategy=2))
+        ghosts = np.arange(n, n + 8, dtype=np.uint32)      # never started
+
+        def hook(r):
+            if r == 30:
+                sim.begin_omission(ghosts)
+                sim.begin_send_omission(ghosts, ghosts[::-1].copy())
+                sim.begin_receive_omission(np.zeros(8, np.uint32), ghosts)
+        return sim.run_schedule(S.W.doubling_join(n, 4), 80, extra=hook)
+
+    def plain(make):
+        sim = make(default_config(n_nodes=n + 8, seed=4, manager=1, strategy=2))
+        return sim.run_schedule(S.W.doubling_join(n, 4), 80)
+    S.compare_stats(quiet(Oracle), plain(Oracle))
+
+
+def test_general_omission_silences_a_node():
+    """begin_omission at x: x sends no strategy message and handles none
+    (full strategy, reference gossip-to-all on 16 nodes): its member set
+    stops growing and nobody learns of it (its join gossip never leaves),
+    while the others agree on the rest; after end_omission all converge."""
+    n = 16
+    sim = Oracle(default_config(n_nodes=n, seed=2, manager=1, strategy=0))
+    x = np.array([9], np.uint32)
+    sched = S.W.doubling_join(n, 2)
+    # node 9 starts in round 4 (ids [8, 16)); silence it from round 5
+    st = sim.run_schedule(sched, 5)
+    sim.begin_omission(x)
+    st = sim.step(40)
+    v = sim.strategy_nodes()
+    assert st["omitted"].sum() > 0
+    assert v["members"][9] < n
+    assert (np.delete(v["members"], 9) == n - 1).all()
+    sim.end_omission(x)
+    sim.step(30)
+    assert (sim.strategy_nodes()["members"] == n).all()
+
+
+def test_send_omission_counts_and_draws():
+    """a send omission costs no dispatch draw: the sender's draw counter
+    runs behind the same run without the fault by exactly the omitted count
+    when nothing else differs (SCAMP v1 pings to one omitted member)"""
+    n = 64
+    base = Oracle(default_config(n_nodes=n, seed=6, manager=1, strategy=1))
+    flt = Oracle(default_config(n_nodes=n, seed=6, manager=1, strategy=1))
+    for sim in (base, flt):
+        sim.run_schedule(S.W.doubling_join(n, 6), 30)
+    v = base.strategy_nodes()
+    x = next(i for i in range(n) if v["view_n"][i] >= 3)
+    y = int([j for j in v["view"][x][: v["view_n"][x]] if j != x][0])
+    flt.begin_send_omission(np.array([x], np.uint32), np.array([y], np.uint32))
+    # one periodic round of x (periodic every 10 rounds from its start)
+    a, b = base.step(1), flt.step(1)
+    while a["omitted"].sum() == b["omitted"].sum() == 0 and base.round < 60:
+        a, b = base.step(1), flt.step(1)
+    assert b["omitted"].sum() >= 1
+    ra, rb = base.strategy_nodes()["rng_ctr"][x], flt.strategy_nodes()["rng_ctr"][x]
+    assert ra - rb == b["omitted"].sum()
+
+
+def test_omission_rejections():
+    hv = Oracle(default_config(n_nodes=8))
+    with pytest.raises(Exception):                        # HyParView: no interposition layer
+        hv.begin_omission(np.array([1], np.uint32))
+    sv = Oracle(default_config(n_nodes=8, manager=1, strategy=1))
+    with pytest.raises(Exception):
+        sv.begin_send_omission(np.array([1], np.uint32), np.array([8], np.uint32))
