@@ -1634,7 +1634,7 @@ __global__ void __launch_bounds__(256) k_relay(RoundArgs) {
         KArgs& a = kargs();                           // (re-read per step, not held in SGPRs)
         const uint32_t P = base + threadIdx.x;
         uint4 D = make_uint4(0, 0, 0, 0);
-        bool heavy = false, to_pt = false, relay = false, pt_lane = false, maps = false;
+        bool heavy = false, to_pt = false, relay = false, pt_lane = false, maps = false, shuf = false;
         Hdr h;
         uint32_t ik = 0, oend = 0;
         uint4 act0 = make_uint4(0, 0, 0, 0), act1 = act0;
@@ -1680,8 +1680,10 @@ __global__ void __launch_bounds__(256) k_relay(RoundArgs) {
                 for (int j = 0; j < 8; j++)
                     exits |= (uint32_t)j < h.act_n && av[j] != id && av[j] < a.n_nodes && (a.flags[av[j]] & F_CRASHED);
             }
-            heavy = exits || fresh || (tf & DESC_SHUFFLE) || ((tf & DESC_PROMO) && h.act_n < a.min_active) ||
+            heavy = exits || fresh || ((tf & DESC_PROMO) && h.act_n < a.min_active) ||
                     (hvn && !(all_relay && h.act_n > 1));
+            // a due shuffle with nothing else heavy: k_shuf, after the relays
+            shuf = !heavy && (tf & DESC_SHUFFLE);
             maps = maps || exits || (tf & DESC_PROMO);        // move_to_active: current_id
             relay = !heavy && hvn > 0;
             const bool pt_msgs = !fresh && ik > hvn, origin = (tf & DESC_ORIGIN) != 0;
@@ -1689,13 +1691,15 @@ __global__ void __launch_bounds__(256) k_relay(RoundArgs) {
             // the Plumtree phase runs in the lane when the node's HyParView
             // phase does and its Plumtree work is IHAVE answers, acks and the
             // lazy tick; else in k_pt (after k_consume for a heavy node)
-            pt_lane = a.plumtree && !heavy && !origin && (pt_msgs ? pt_light : lazy);
-            to_pt = a.plumtree && (pt_msgs || origin || (heavy && lazy)) && !pt_lane;
-            if (!heavy && (relay || to_pt || pt_lane)) v[R_PROC]++;   // (k_consume counts its own)
+            // (after a shuffle start, the Plumtree phase waits for k_shuf: k_pt)
+            pt_lane = a.plumtree && !heavy && !shuf && !origin && (pt_msgs ? pt_light : lazy);
+            to_pt = a.plumtree && (pt_msgs || origin || ((heavy || shuf) && lazy)) && !pt_lane;
+            if (!heavy && (relay || to_pt || pt_lane || shuf)) v[R_PROC]++;   // (k_consume counts its own)
         }
         block_append(P < na && heavy, maps ? make_uint4(D.x, D.y, D.z | DESC_MAPS_BIT, D.w) : D, a.desc_slow, a.n_slow,
                      wcnt);
         block_append(P < na && to_pt, D, a.desc_pt, a.n_pt, wcnt);
+        block_append(P < na && shuf, D, a.desc_shuf, a.n_shuf, wcnt);
         if (P >= na || heavy) continue;
         const uint32_t id = D.x;
         const size_t li = id - a.lo;
@@ -1852,6 +1856,163 @@ __global__ void __launch_bounds__(256) k_relay(RoundArgs) {
                : k == ST_OVF_BY + PSIM_OVF_PT ? sst[R_OVF] : k == ST_BOUND ? sst[R_BOUND]
                : k == ST_DELIV + PSIM_MSG_PT_IHAVE ? sst[R_DIH] : k == ST_DELIV + PSIM_MSG_PT_IGNORED_IHAVE ? sst[R_DIGN]
                : k == ST_EMIT + PSIM_MSG_PT_IGNORED_IHAVE ? sst[R_EIGN] : 0ull;
+}
+
+// ------------------------------------------------------ shuffle starts --
+// k_shuf: one lane per node whose HyParView work this round is its due
+// passive_view_maintenance timer (hv:572-607), after any SHUFFLE relays
+// k_relay ran for it, with nothing else HyParView-heavy (k_relay's list).
+// The exchange is usort([Myself] ++ sublist(Active, k_active) ++
+// sublist(Passive, k_passive)) (hv:577-586): each sublist keys its
+// elements with consecutive draws in to_list order and keeps the K smallest
+// (key, element) pairs -- here a running top-K in registers, one element at
+// a time, exact on the full 53-bit keys -- then select_random(Active,
+// [Myself]) picks the target and do_send_message draws the dispatch value.
+// The view rows are only read: a shuffle start changes nothing but the
+// draw counter.  Same draws, record, sequence number, digest and stats as
+// k_consume's body; the node's Plumtree phase (if any) follows in k_pt.
+constexpr int SHUF_TOPK = PSIM_EXCHANGE_CAP - 1;   // k_active + k_passive <= 7
+
+// keep the K smallest (key, element) pairs in ascending order (slots >= K
+// hold ~0): the new pair enters at the end and bubbles up, unrolled
+DEV void topk_insert(uint64_t (&K)[SHUF_TOPK], uint32_t (&E)[SHUF_TOPK], uint64_t key, uint32_t e) {
+    uint64_t ck = key;
+    uint32_t ce = e;
+#pragma unroll
+    for (int i = 0; i < SHUF_TOPK; i++) {
+        const bool lt = ck < K[i] || (ck == K[i] && ce < E[i]);
+        const uint64_t tk = lt ? K[i] : ck;
+        const uint32_t te = lt ? E[i] : ce;
+        K[i] = lt ? ck : K[i];
+        E[i] = lt ? ce : E[i];
+        ck = tk;
+        ce = te;
+    }
+}
+
+__global__ void __launch_bounds__(256) k_shuf(RoundArgs) {
+    enum { S_SHUF, S_FAIL, S_DIGEST, S_BOUND, S_N };
+    __shared__ unsigned long long sst[S_N];
+    if (threadIdx.x < S_N) sst[threadIdx.x] = 0;
+    __syncthreads();
+    const uint32_t l = lane_id();
+    const uint32_t ns = *kargs().n_shuf;
+    const uint64_t two58 = 1ull << 58;
+    unsigned long long v[S_N] = {};
+    for (uint32_t P = blockIdx.x * blockDim.x + threadIdx.x; P < ns; P += gridDim.x * blockDim.x) {
+        KArgs& a = kargs();
+        const uint4 D = a.desc_shuf[P];
+        const uint32_t id = D.x;
+        const size_t li = id - a.lo;
+        const uint64_t rng0 = a.hdr[li].rng;
+        const uint32_t cnts = reinterpret_cast<const uint32_t*>(a.hdr + li)[9];   // act_n, pas_n, ..
+        const uint32_t act_n = cnts & 0xFF, pas_n = (cnts >> 8) & 0xFF;
+        const uint4* ar = reinterpret_cast<const uint4*>(a.act + li * PSIM_ACTIVE_CAP);
+        const uint4 a0 = ar[0], a1 = ar[1];
+        const uint32_t A[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+        uint32_t seq = a.ocnt[li];                    // after k_relay's relays
+        const uint32_t oend = (uint32_t)a.obase[li + 1];
+        const uint32_t me_part = a.part[id];
+        uint64_t rng = rng0;
+        // sublist(Active, k_active): keys rng .. rng + act_n - 1
+        uint64_t K[SHUF_TOPK];
+        uint32_t E[SHUF_TOPK];
+#pragma unroll
+        for (int i = 0; i < SHUF_TOPK; i++) { K[i] = ~0ull; E[i] = ~0u; }
+#pragma unroll
+        for (int j = 0; j < PSIM_ACTIVE_CAP; j++)
+            if ((uint32_t)j < act_n) topk_insert(K, E, draw58_at(rng + j, id, a.seed) >> 5, A[j]);
+        rng += act_n;
+        const uint32_t ka = min(act_n, a.k_active), kp = min(pas_n, a.k_passive);
+        uint32_t X[8];
+        X[0] = id;
+#pragma unroll
+        for (int i = 0; i < SHUF_TOPK; i++) X[1 + i] = (uint32_t)i < ka ? E[i] : ~0u;
+        // sublist(Passive, k_passive): keys rng .. rng + pas_n - 1, the
+        // passive row streamed 16 B at a time
+#pragma unroll
+        for (int i = 0; i < SHUF_TOPK; i++) { K[i] = ~0ull; E[i] = ~0u; }
+        const uint4* pr = reinterpret_cast<const uint4*>(a.pas + li * PSIM_PASSIVE_CAP);
+        for (uint32_t j0 = 0; j0 < pas_n; j0 += 4) {
+            const uint4 q = pr[j0 >> 2];
+            const uint32_t Q[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+            for (int c = 0; c < 4; c++)
+                if (j0 + c < pas_n) topk_insert(K, E, draw58_at(rng + j0 + c, id, a.seed) >> 5, Q[c]);
+        }
+        rng += pas_n;
+        // [Myself] ++ the active picks ++ the passive picks (slots past the
+        // picks hold ~0, which sorts last and is cut below)
+#pragma unroll
+        for (int i = 0; i < SHUF_TOPK; i++) {
+            const uint32_t e = (uint32_t)i < kp ? E[i] : ~0u;
+            // X[1 + ka + i] = e, as selects over the fixed slots
+#pragma unroll
+            for (int o = 1; o < 8; o++) X[o] = ((uint32_t)o == 1 + ka + (uint32_t)i) ? e : X[o];
+        }
+        // lists:usort/1: an 8-input sorting network, then the duplicates out
+#define CSW(i, j) { const uint32_t lo_ = min(X[i], X[j]), hi_ = max(X[i], X[j]); X[i] = lo_; X[j] = hi_; }
+        CSW(0, 1) CSW(2, 3) CSW(4, 5) CSW(6, 7)
+        CSW(0, 2) CSW(1, 3) CSW(4, 6) CSW(5, 7)
+        CSW(1, 2) CSW(5, 6) CSW(0, 4) CSW(3, 7)
+        CSW(1, 5) CSW(2, 6)
+        CSW(1, 4) CSW(3, 6)
+        CSW(2, 4) CSW(3, 5)
+        CSW(3, 4)
+#undef CSW
+        uint32_t U[8], nex = 0;
+#pragma unroll
+        for (int o = 0; o < 8; o++) U[o] = 0u;
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            const bool keep = X[i] != ~0u && (i == 0 || X[i] != X[i - 1]);
+#pragma unroll
+            for (int o = 0; o < 8; o++) U[o] = (keep && nex == (uint32_t)o) ? X[i] : U[o];
+            nex += keep ? 1u : 0u;
+        }
+        // select_random(Active, [Myself]) (hv:1346-1356)
+        uint32_t elig = 0;
+#pragma unroll
+        for (int j = 0; j < 8; j++) elig |= ((uint32_t)j < act_n && A[j] != id) ? (1u << j) : 0u;
+        const uint32_t cnt = __popc(elig);
+        if (cnt) {
+            uint32_t k;
+            for (;;) {                                // rand:uniform(cnt) - 1 (?uniform_range)
+                const uint64_t x = draw58_at(rng++, id, a.seed);
+                if (x < cnt) { k = (uint32_t)x; break; }
+                const uint32_t i = mod_small(x, cnt);
+                if (x - i <= two58 - cnt) { k = i; break; }
+            }
+            uint32_t e = elig;
+            for (uint32_t j = 0; j < k; j++) e &= e - 1;
+            const uint32_t t = A[__ffs(e) - 1];
+            // do_send_message: maybe_connect + find, then the dispatch draw
+            if (t < a.n_nodes && (a.flags[t] & F_UP) && a.part[t] == me_part) {
+                rng++;
+                v[S_DIGEST] += relay_emit(a, D.w + seq, t, id, PSIM_MSG_SHUFFLE | (a.arwl << 8) | (nex << 16), seq,
+                                          0u, 0u, 0u, U);
+                seq++;
+                v[S_SHUF]++;
+            } else {
+                v[S_FAIL]++;
+            }
+        }
+        a.hdr[li].rng = rng;
+        a.ocnt[li] = seq;
+        v[S_BOUND] += seq > oend - D.w ? 1u : 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < S_N; k++)
+        for (int o = 32; o > 0; o >>= 1) v[k] += __shfl_xor(v[k], o);
+    if (l == 0)
+        for (int k = 0; k < S_N; k++)
+            if (v[k]) atomicAdd(&sst[k], v[k]);
+    __syncthreads();
+    uint64_t* row = kargs().stat_shuf + (size_t)blockIdx.x * NST;
+    for (uint32_t k = threadIdx.x; k < NST; k += blockDim.x)
+        row[k] = k == ST_EMIT + PSIM_MSG_SHUFFLE ? sst[S_SHUF] : k == ST_FAIL ? sst[S_FAIL]
+               : k == ST_DIGEST ? sst[S_DIGEST] : k == ST_BOUND ? sst[S_BOUND] : 0ull;
+    if (threadIdx.x == 0) atomicMax(&kargs().ktime[1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
 }
 
 // one wave-slot per resident wave: the grid strides over the active list

@@ -45,6 +45,9 @@ struct RoundArgs {
     uint32_t* n_slow;
     uint4* desc_pt;             // ... and the nodes with Plumtree work, for k_pt
     uint32_t* n_pt;
+    uint4* desc_shuf;           // ... and the nodes whose HyParView phase ends in a shuffle start, for k_shuf
+    uint32_t* n_shuf;
+    uint64_t* stat_shuf;        // k_shuf's per-block stats rows
     uint64_t* stat_relay;
     uint64_t* stat_pt;          // k_pt's per-block stats rows
     const Msg* rec_in;          // dense, in inbox order (node runs at in_beg)
@@ -84,8 +87,11 @@ struct RoundArgs {
 __global__ void k_consume(RoundArgs args);
 // lane-per-node SHUFFLE relays ahead of k_consume (psim_consume.hip)
 constexpr uint32_t RELAY_MAX_BLOCKS = 8192;
+constexpr uint32_t SHUF_MAX_BLOCKS = 1024;     // k_shuf: grid-stride over its list
 __global__ void k_relay(RoundArgs args);
 __global__ void k_consume_pl(RoundArgs args);
+// lane-per-node shuffle starts of the nodes k_relay listed (psim_consume.hip)
+__global__ void k_shuf(RoundArgs args);
 // the Plumtree phase of the nodes k_relay listed (psim_consume.hip)
 __global__ void k_pt(RoundArgs args);
 // diagnostic builds (-DPSIM_STAMPS): per-phase cycle sums of k_consume, reset on read
