@@ -1019,13 +1019,16 @@ DEV uint32_t cache_flags(KArgs& a, uint32_t cv, uint32_t me) {
     return cv < a.n_nodes ? (f | (pt << 8)) : 0u;
 }
 
+template <bool LITE = false>
 DEV NodeX load_x(KArgs& a, const NodeIn& x) {
     uint32_t l = lane_id();
     NodeX y;
     const uint32_t hw9 = rl(x.H, 9);                 // act_n, pas_n, .. (Hdr word 9)
     const uint32_t act_n = hw9 & 0xFF, pas_n = (hw9 >> 8) & 0xFF;
     uint32_t av = shfl(x.A, (int)(l & 7));
-    uint32_t cv = l < 32 ? (l < pas_n ? x.P : NONE) : (l < 40 && l - 32 < act_n ? av : NONE);
+    // (LITE: k_consume_lite's handlers only send to active members and to
+    // senders -- no passive-member entries)
+    uint32_t cv = l < 32 ? (!LITE && l < pas_n ? x.P : NONE) : (l < 40 && l - 32 < act_n ? av : NONE);
     y.CV = cv;
     y.CF = cache_flags(a, cv, x.n);
     return y;
@@ -1357,6 +1360,130 @@ __global__ void __launch_bounds__(256, PSIM_WAVES_PER_SIMD) k_consume(RoundArgs 
     if (threadIdx.x == 0) atomicMax(&kargs().ktime[1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
 }
 
+// ------------------------------------------------ shuffle-exchange phase --
+// k_consume_lite: the same wave-per-node pipeline for the nodes k_relay
+// finds whose HyParView phase is SHUFFLE walks and their replies only -- a
+// SHUFFLE that ends here (hv:1095-1136 with TTL 0 or |active| = 1: the reply
+// sublist(Passive, |Exchange|), then merge_exchange), a SHUFFLE_REPLY
+// (hv:1091-1093: merge_exchange), any SHUFFLE relays among them, then a due
+// shuffle start (hv:572-607) -- with nothing else (no join, EXIT, promotion,
+// other message type).  These handlers change only the passive view and the
+// draw counter, never the active view (no notify) or an id map, and send
+// only to active members and to a message's sender, so the kernel carries
+// a fraction of k_consume's live state and runs at twice its occupancy: in
+// the rounds after a cohort's shuffle starts, most of k_consume's list was
+// these nodes.  Same handlers (hv_handle), draws, records and stats.
+DEV void body_lite(Wv& w, const NodeIn& x) {
+    KArgs& a = kargs();
+    const uint32_t l = lane_id();
+    w.work = true;
+    st_add(w, ST_PROC, 1);
+    for (uint32_t c = 0; c < x.ik; c += 4) {          // HyParView inbox, canonical order
+        uint32_t R4 = inbox_chunk(w, a, x.ib, x.ik, c, x.R0);
+        uint32_t cm = x.ik - c < 4 ? x.ik - c : 4;
+        for (uint32_t q = 0; q < cm; q++) {
+            uint32_t b = q * 16;
+            uint32_t tt = rl(R4, b + 2), type = tt & 0xFF;
+            if (type >= PSIM_MSG_PT_BROADCAST) continue;
+            st_add(w, ST_DELIV + type, 1);
+            uint32_t nex = (tt >> 16) & 0xFF;
+            uint32_t ex = shfl(R4, (int)((b + 8 + l) & 63));
+            ex = l < nex ? ex : 0u;
+            const uint32_t p = rl(R4, b + 1), ttl = (tt >> 8) & 0xFF;
+            if (type == PSIM_MSG_SHUFFLE_REPLY) {        // hv:1091-1093
+                merge_exchange(w, ex, nex);
+            } else if (ttl > 0 && w.act_n > 1) {         // hv:1095-1136: relay
+                uint32_t r = select_random(w, w.A, w.act_n, p, w.me, w.me);
+                if (r != NONE) hv_send(w, r, PSIM_MSG_SHUFFLE, ttl - 1, 0, 0, ex, nex);
+            } else {                                     // the walk ends here
+                uint32_t RESP = 0;
+                uint32_t nr = sublist(w, w.P, w.pas_n, nex, RESP, 0);
+                hv_send(w, p, PSIM_MSG_SHUFFLE_REPLY, 0, 0, 0, RESP, nr);
+                merge_exchange(w, ex, nex);
+            }
+        }
+    }
+    if (x.tf & DESC_SHUFFLE) {                        // hv:572-607
+        uint32_t EX;
+        uint32_t nex = build_exchange(w, EX);
+        uint32_t t = select_random(w, w.A, w.act_n, w.me, w.me, w.me);
+        if (t != NONE) hv_send(w, t, PSIM_MSG_SHUFFLE, a.arwl, 0, 0, EX, nex);
+    }
+}
+
+// the draw counter and passive size in the header, the passive row when it
+// changed, the outbox count and the records (the flag byte, the active row,
+// the id maps and the Plumtree rows are unchanged)
+DEV void writeback_lite(Wv& w) {
+    KArgs& a = kargs();
+    const uint32_t l = lane_id();
+    const size_t li = w.li;
+    uint32_t* hrow = reinterpret_cast<uint32_t*>(a.hdr + li);
+    const uint32_t k = l & 15;
+    // words 0-1: the draw counter; word 9: act_n | pas_n << 8 | sent_n << 16 | sent_head << 24
+    const uint32_t hw = k == 0 ? (uint32_t)w.rng : k == 1 ? (uint32_t)(w.rng >> 32)
+                      : (w.act_n | (w.pas_n << 8) | (w.sent_n << 16) | (w.sent_head << 24));
+    if (l < 16 && (k < 2 || k == 9)) hrow[k] = hw;
+    {
+        bool dirty = (w.vd & 2u) != 0;
+        uint32_t x = shfl(w.P, (int)(l & 31));
+        *(dirty ? a.pas + li * PSIM_PASSIVE_CAP + (l & 31) : hrow) = dirty ? x : (uint32_t)w.rng;
+    }
+    a.ocnt[li] = w.seq;
+    st_add(w, ST_BOUND, w.seq > a.obase[li + 1] - w.obase ? 1u : 0u);
+    flush_recs(w);
+}
+
+#ifndef PSIM_LITE_WAVES
+#define PSIM_LITE_WAVES 6
+#endif
+__global__ void __launch_bounds__(256, PSIM_LITE_WAVES) k_consume_lite(RoundArgs args) {
+    __shared__ uint64_t sst[NST];
+    __shared__ uint32_t scratch[WAVES_PER_BLOCK][64];
+    __shared__ __attribute__((aligned(16))) uint32_t srecs[WAVES_PER_BLOCK][STAGE * 16];
+    __shared__ uint32_t skeys[WAVES_PER_BLOCK][STAGE];
+    for (int i = threadIdx.x; i < NST; i += blockDim.x) sst[i] = 0;
+    __syncthreads();
+    const uint32_t wid = threadIdx.x >> 6;
+    const uint32_t gw = uni(blockIdx.x * WAVES_PER_BLOCK + wid);
+    const uint32_t nw = gridDim.x * WAVES_PER_BLOCK;
+    Wv w;
+    w.a = &args;
+    w.lds = scratch[wid];
+    w.nlog = nullptr;
+    w.srec = srecs[wid];
+    w.skey = skeys[wid];
+    w.slots = nullptr;
+    w.st = sst;
+    w.round = kargs().round;
+    w.SC = 0;
+    w.digest = 0;
+    w.KM = magic_lanes();
+    const uint32_t na = *kargs().n_lite;
+    if (gw < na) {
+        const uint32_t last = na - 1;
+        KArgs& a0 = kargs();
+        NodeIn x = load_node(a0, reinterpret_cast<const uint32_t*>(kargs().desc_lite + gw)[lane_id() & 3]);
+        NodeX y = load_x<true>(kargs(), x);
+        NodeIn xn = load_node(kargs(), reinterpret_cast<const uint32_t*>(kargs().desc_lite + min(gw + nw, last))[lane_id() & 3]);
+        uint32_t d = reinterpret_cast<const uint32_t*>(kargs().desc_lite + min(gw + 2 * nw, last))[lane_id() & 3];
+        for (uint32_t i = gw; i < na; i += nw) {
+            begin_node(w, x, y);
+            body_lite(w, x);
+            NodeX yn = load_x<true>(kargs(), xn);
+            writeback_lite(w);
+            NodeIn xnn = load_node(kargs(), d);
+            d = reinterpret_cast<const uint32_t*>(kargs().desc_lite + min(i + 3 * nw, last))[lane_id() & 3];
+            x = xn; y = yn; xn = xnn;
+        }
+    }
+    flush_wave_stats(w, sst);
+    __syncthreads();
+    for (int i = threadIdx.x; i < NST; i += blockDim.x)
+        kargs().stat_lite[(size_t)blockIdx.x * NST + i] = sst[i];
+    if (threadIdx.x == 0) atomicMax(&kargs().ktime[1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+}
+
 // ------------------------------------------------------- Plumtree phase --
 // k_pt: one wave per node with Plumtree work (k_relay's second list), after
 // the node's HyParView phase (k_relay's lane or k_consume): its Plumtree
@@ -1634,7 +1761,7 @@ __global__ void __launch_bounds__(256) k_relay(RoundArgs) {
         KArgs& a = kargs();                           // (re-read per step, not held in SGPRs)
         const uint32_t P = base + threadIdx.x;
         uint4 D = make_uint4(0, 0, 0, 0);
-        bool heavy = false, to_pt = false, relay = false, pt_lane = false, maps = false, shuf = false;
+        bool heavy = false, to_pt = false, relay = false, pt_lane = false, maps = false, shuf = false, lite = false;
         Hdr h;
         uint32_t ik = 0, oend = 0;
         uint4 act0 = make_uint4(0, 0, 0, 0), act1 = act0;
@@ -1655,7 +1782,7 @@ __global__ void __launch_bounds__(256) k_relay(RoundArgs) {
             // the inbox: how many HyParView messages, and whether each is a
             // SHUFFLE with TTL left (a relay while |active| > 1)
             uint32_t hvn = 0;
-            bool all_relay = true, pt_light = true;
+            bool all_relay = true, pt_light = true, all_shuf = true;
             for (uint32_t j = 0; j < ik; j++) {
                 const Msg& m = a.rec_in[D.y + j];
                 const uint32_t tt = m.tt, type = tt & 0xFF;
@@ -1663,6 +1790,7 @@ __global__ void __launch_bounds__(256) k_relay(RoundArgs) {
                     hvn++;
                     maps |= type <= PSIM_MSG_NEIGHBOR_ACCEPTED;   // id maps (hv:703-1089)
                     all_relay &= type == PSIM_MSG_SHUFFLE && ((tt >> 8) & 0xFF) > 0;
+                    all_shuf &= type == PSIM_MSG_SHUFFLE || type == PSIM_MSG_SHUFFLE_REPLY;
                 } else if (type == PSIM_MSG_PT_IHAVE) {
                     // an IHAVE of a delivered (or retired: stale) id only
                     // answers IGNORED_IHAVE (pt:380-386)
@@ -1680,27 +1808,31 @@ __global__ void __launch_bounds__(256) k_relay(RoundArgs) {
                 for (int j = 0; j < 8; j++)
                     exits |= (uint32_t)j < h.act_n && av[j] != id && av[j] < a.n_nodes && (a.flags[av[j]] & F_CRASHED);
             }
-            heavy = exits || fresh || ((tf & DESC_PROMO) && h.act_n < a.min_active) ||
-                    (hvn && !(all_relay && h.act_n > 1));
+            heavy = exits || fresh || ((tf & DESC_PROMO) && h.act_n < a.min_active) || (hvn && !all_shuf);
+            // SHUFFLE terminals and replies (with whatever relays and shuffle
+            // start come with them): k_consume_lite
+            lite = !heavy && hvn && !(all_relay && h.act_n > 1);
             // a due shuffle with nothing else heavy: k_shuf, after the relays
-            shuf = !heavy && (tf & DESC_SHUFFLE);
+            shuf = !heavy && !lite && (tf & DESC_SHUFFLE);
             maps = maps || exits || (tf & DESC_PROMO);        // move_to_active: current_id
-            relay = !heavy && hvn > 0;
+            relay = !heavy && !lite && hvn > 0;
             const bool pt_msgs = !fresh && ik > hvn, origin = (tf & DESC_ORIGIN) != 0;
             const bool lazy = (tf & DESC_LAZY) && h.out_n > 0;
             // the Plumtree phase runs in the lane when the node's HyParView
             // phase does and its Plumtree work is IHAVE answers, acks and the
             // lazy tick; else in k_pt (after k_consume for a heavy node)
             // (after a shuffle start, the Plumtree phase waits for k_shuf: k_pt)
-            pt_lane = a.plumtree && !heavy && !shuf && !origin && (pt_msgs ? pt_light : lazy);
-            to_pt = a.plumtree && (pt_msgs || origin || ((heavy || shuf) && lazy)) && !pt_lane;
-            if (!heavy && (relay || to_pt || pt_lane || shuf)) v[R_PROC]++;   // (k_consume counts its own)
+            pt_lane = a.plumtree && !heavy && !shuf && !lite && !origin && (pt_msgs ? pt_light : lazy);
+            to_pt = a.plumtree && (pt_msgs || origin || ((heavy || shuf || lite) && lazy)) && !pt_lane;
+            // (k_consume and k_consume_lite count their own)
+            if (!heavy && !lite && (relay || to_pt || pt_lane || shuf)) v[R_PROC]++;
         }
         block_append(P < na && heavy, maps ? make_uint4(D.x, D.y, D.z | DESC_MAPS_BIT, D.w) : D, a.desc_slow, a.n_slow,
                      wcnt);
         block_append(P < na && to_pt, D, a.desc_pt, a.n_pt, wcnt);
         block_append(P < na && shuf, D, a.desc_shuf, a.n_shuf, wcnt);
-        if (P >= na || heavy) continue;
+        block_append(P < na && lite, D, a.desc_lite, a.n_lite, wcnt);
+        if (P >= na || heavy || lite) continue;
         const uint32_t id = D.x;
         const size_t li = id - a.lo;
         const uint32_t A[8] = {act0.x, act0.y, act0.z, act0.w, act1.x, act1.y, act1.z, act1.w};
@@ -2026,6 +2158,7 @@ static uint32_t resident_grid(const void* k) {
     return (uint32_t)nb * (uint32_t)p.multiProcessorCount;
 }
 uint32_t consume_grid() { return resident_grid((const void*)k_consume); }
+uint32_t lite_grid() { return resident_grid((const void*)k_consume_lite); }
 uint32_t pt_grid() { return resident_grid((const void*)k_pt); }
 
 #ifdef PSIM_STAMPS

@@ -48,6 +48,9 @@ struct RoundArgs {
     uint4* desc_shuf;           // ... and the nodes whose HyParView phase ends in a shuffle start, for k_shuf
     uint32_t* n_shuf;
     uint64_t* stat_shuf;        // k_shuf's per-block stats rows
+    uint4* desc_lite;           // ... and the nodes with SHUFFLE terminals / replies, for k_consume_lite
+    uint32_t* n_lite;
+    uint64_t* stat_lite;        // k_consume_lite's per-block stats rows
     uint64_t* stat_relay;
     uint64_t* stat_pt;          // k_pt's per-block stats rows
     const Msg* rec_in;          // dense, in inbox order (node runs at in_beg)
@@ -92,12 +95,15 @@ __global__ void k_relay(RoundArgs args);
 __global__ void k_consume_pl(RoundArgs args);
 // lane-per-node shuffle starts of the nodes k_relay listed (psim_consume.hip)
 __global__ void k_shuf(RoundArgs args);
+// wave-per-node SHUFFLE terminals, replies and their merges (psim_consume.hip)
+__global__ void k_consume_lite(RoundArgs args);
 // the Plumtree phase of the nodes k_relay listed (psim_consume.hip)
 __global__ void k_pt(RoundArgs args);
 // diagnostic builds (-DPSIM_STAMPS): per-phase cycle sums of k_consume, reset on read
 int debug_stamps(unsigned long long* out);
 // resident-block count of k_consume on the current device
 uint32_t consume_grid();
+uint32_t lite_grid();
 uint32_t pt_grid();
 
 // The launch's RoundArgs, read through an opaque constant-address pointer
