@@ -5,7 +5,8 @@ profiles/pmc_records.json, which bench.py reads back by its pmc_key.
 
 Window: the `steps` timed rounds are the dispatches of each kernel before the
 overlay-drain rounds bench.py runs after its window (overlay.rounds_drained).
-Per round: the sum over k_relay, k_consume and k_pt.
+Per round: the sum over the node-round kernels (k_relay, k_shuf, k_consume_lite,
+k_consume, k_ptl, k_pt).
 
 Units and corrections (profiles/calib/, measured on this MI355X): FETCH_SIZE
 counts 64-B memory requests -- a random dword or a random 64-B record reads as
@@ -20,7 +21,7 @@ import json
 import os
 import sys
 
-KERNELS = ("k_relay(", "k_consume(", "k_pt(")
+KERNELS = ("k_relay(", "k_shuf(", "k_consume_lite(", "k_consume(", "k_ptl(", "k_pt(")
 
 
 def per_round(path, steps, tail):
@@ -44,7 +45,7 @@ def main():
            "traffic_upper_per_launch": 2 * fetch + write,
            "fetch_size_bytes": fetch, "write_size_bytes": write,
            "alg_bytes_per_launch": bench["roofline"]["alg_bytes_per_launch"],
-           "source": "FETCH_SIZE + WRITE_SIZE per timed round of k_relay + k_consume + k_pt, separate "
+           "source": "FETCH_SIZE + WRITE_SIZE per timed round of the node-round kernels, separate "
                      "rocprofv3 --pmc passes of this command (profiles/run_pmc.sh); FETCH_SIZE uncorrected: "
                      "random 64-B requests count exactly (profiles/calib/)"}
     path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "pmc_records.json")
