@@ -1733,7 +1733,8 @@ DEV void block_append(bool go, const uint4& D, uint4* desc, uint32_t* cnt, uint3
     if (lane_id() == 0) wcnt[wv] = popc(m);
     __syncthreads();
     if (threadIdx.x == 0) {
-        const uint32_t t = wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
+        uint32_t t = 0;
+        for (uint32_t k = 0; k < (blockDim.x >> 6); k++) t += wcnt[k];
         wcnt[4] = t ? atomicAdd(cnt, t) : 0u;
     }
     __syncthreads();
@@ -1829,7 +1830,11 @@ __global__ void __launch_bounds__(256) k_relay(RoundArgs) {
         }
         block_append(P < na && heavy, maps ? make_uint4(D.x, D.y, D.z | DESC_MAPS_BIT, D.w) : D, a.desc_slow, a.n_slow,
                      wcnt);
-        block_append(P < na && to_pt, D, a.desc_pt, a.n_pt, wcnt);
+        // (k_ptl takes the Plumtree phase of nodes without an origin, and
+        // hands k_pt the ones that do not fit a lane)
+        const bool origin_node = ((D.z >> 28) & DESC_ORIGIN) != 0;
+        block_append(P < na && to_pt && origin_node, D, a.desc_pt, a.n_pt, wcnt);
+        block_append(P < na && to_pt && !origin_node, D, a.desc_ptl, a.n_ptl, wcnt);
         block_append(P < na && shuf, D, a.desc_shuf, a.n_shuf, wcnt);
         block_append(P < na && lite, D, a.desc_lite, a.n_lite, wcnt);
         if (P >= na || heavy || lite) continue;
@@ -2144,6 +2149,371 @@ __global__ void __launch_bounds__(256) k_shuf(RoundArgs) {
     for (uint32_t k = threadIdx.x; k < NST; k += blockDim.x)
         row[k] = k == ST_EMIT + PSIM_MSG_SHUFFLE ? sst[S_SHUF] : k == ST_FAIL ? sst[S_FAIL]
                : k == ST_DIGEST ? sst[S_DIGEST] : k == ST_BOUND ? sst[S_BOUND] : 0ull;
+    if (threadIdx.x == 0) atomicMax(&kargs().ktime[1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+}
+
+// ---------------------------------------------------- Plumtree lanes --
+// k_ptl: one lane per node with Plumtree work (k_relay's list, origins
+// aside), after its HyParView phase.  In config C's steady state a node keeps
+// per-root sets for one root (the broadcaster) with a handful of eager and
+// lazy peers and a few outstanding entries, and its Plumtree phase is a
+// BROADCAST (first delivery: eager push + lazy adds; duplicate: PRUNE), some
+// PRUNEs, IHAVE answers and acks, then the lazy tick.  A lane holds slot 0's
+// eager and lazy sets (16 entries each) and the outstanding table (16
+// entries) in registers -- ordsets inserts / deletes as unrolled selects --
+// when the node's data fits that: no root in slots 1-3, every message's root
+// slot 0's (or slot 0 free and one root), the sets and the table far enough
+// below 16 that this round's adds fit, no outstanding extension row.  Any
+// other node is appended to k_pt's list and runs there (the wave path).
+// Same handlers as pt_handle / pt_push / the lazy tick (pt:288-313, :341-345,
+// :368-453, :562-631): the same records, sequence numbers, digest, stats.
+constexpr int PTL_CAP = 16;
+
+constexpr uint32_t PTL_BLK = 128;   // k_ptl block: 2 waves, 32 KiB of per-lane tables
+
+// A lane's tables in LDS, entry i of lane t at row i, column t (conflict-free):
+// unrolled scans read fixed offsets, run-time indexing is one access
+struct LdsCol {
+    uint32_t* p;
+    DEV uint32_t& operator[](uint32_t i) const { return p[i * PTL_BLK]; }
+};
+DEV bool col_has(const LdsCol& V, uint32_t n, uint32_t x) {
+    bool r = false;
+#pragma unroll
+    for (int i = 0; i < PTL_CAP; i++) r |= (uint32_t)i < n && V[i] == x;
+    return r;
+}
+// ordsets:del_element/2
+DEV void col_del(const LdsCol& V, uint32_t& n, uint32_t x) {
+    uint32_t at = n;
+    for (uint32_t i = 0; i < n; i++)
+        if (V[i] == x) { at = i; break; }
+    if (at == n) return;
+    for (uint32_t i = at; i + 1 < n; i++) V[i] = V[i + 1];
+    n--;
+    V[n] = 0u;
+}
+// ordsets:add_element/2 (the caller guarantees room)
+DEV void col_add(const LdsCol& V, uint32_t& n, uint32_t x) {
+    uint32_t pos = 0;
+    bool in = false;
+    for (uint32_t i = 0; i < n; i++) {
+        const uint32_t e = V[i];
+        in |= e == x;
+        pos += e < x ? 1u : 0u;
+    }
+    if (in) return;
+    for (uint32_t i = n; i > pos; i--) V[i] = V[i - 1];
+    V[pos] = x;
+    n++;
+}
+
+struct PtLane {
+    uint32_t id, me_part, act_n;
+    uint32_t A[PSIM_ACTIVE_CAP];
+    uint32_t root0;                // slot 0's root (NONE = free)
+    LdsCol EG, LZ, OL, OH;         // slot 0's eager / lazy sets; outstanding keys (low, high words)
+    uint32_t ne, nl, on;
+    uint64_t have;
+    bool sets_dirty, out_dirty;
+};
+
+// send/3 (pt:633-638): over an existing connection -- the peer in the active
+// view, running, same partition
+DEV bool ptl_conn(KArgs& a, const PtLane& n, uint32_t ident) {
+    const uint32_t p = ident & ~PSIM_MAP_BIT;
+    bool in = false;
+#pragma unroll
+    for (int j = 0; j < PSIM_ACTIVE_CAP; j++) in |= (uint32_t)j < n.act_n && n.A[j] == p;
+    return in && p != n.id && p < a.n_nodes && (a.flags[p] & F_UP) && a.part[p] == n.me_part;
+}
+
+// update_peers/5 + set_peers/4 (pt:593-609) on slot 0 (a new root takes it
+// with the common eagers, read here; the lane's preconditions leave no other
+// case)
+DEV void ptl_update(KArgs& a, PtLane& n, size_t li, uint32_t com_n, uint32_t from, uint32_t root, bool to_eager) {
+    n.sets_dirty = true;
+    if (n.root0 != root) {
+        n.root0 = root;
+        const uint4* cr = reinterpret_cast<const uint4*>(a.pt_com + li * PSIM_PT_MEMBERS_CAP);
+        const uint4 c0 = cr[0], c1 = cr[1];
+        const uint32_t C8[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+#pragma unroll
+        for (int i = 0; i < PTL_CAP; i++) { n.EG[i] = i < 8 && (uint32_t)i < com_n ? C8[i & 7] : 0u; n.LZ[i] = 0u; }
+        n.ne = com_n; n.nl = 0;
+    }
+    if (to_eager) {
+        col_add(n.EG, n.ne, from);
+        col_del(n.LZ, n.nl, from);
+    } else {
+        col_del(n.EG, n.ne, from);
+        col_add(n.LZ, n.nl, from);
+    }
+}
+
+DEV uint64_t out_at(const PtLane& n, uint32_t i) { return ((uint64_t)n.OH[i] << 32) | n.OL[i]; }
+// add_outstanding/6 (pt:574-579), ack_outstanding/6 (pt:562-567): the table
+// as sorted peer << 32 | msg << 16 | round keys
+DEV void ptl_add_out(PtLane& n, uint64_t key) {
+    uint32_t pos = 0;
+    bool in = false;
+    for (uint32_t i = 0; i < n.on; i++) {
+        const uint64_t e = out_at(n, i);
+        in |= e == key;
+        pos += e < key ? 1u : 0u;
+    }
+    if (in) return;
+    for (uint32_t i = n.on; i > pos; i--) { n.OL[i] = n.OL[i - 1]; n.OH[i] = n.OH[i - 1]; }
+    n.OL[pos] = (uint32_t)key; n.OH[pos] = (uint32_t)(key >> 32);
+    n.on++;
+    n.out_dirty = true;
+}
+DEV void ptl_ack_out(PtLane& n, uint64_t key) {
+    for (uint32_t i = 0; i < n.on; i++) {
+        if (out_at(n, i) != key) continue;
+        for (uint32_t j = i; j + 1 < n.on; j++) { n.OL[j] = n.OL[j + 1]; n.OH[j] = n.OH[j + 1]; }
+        n.on--;
+        n.OL[n.on] = 0u; n.OH[n.on] = 0u;
+        n.out_dirty = true;
+        return;
+    }
+}
+
+__global__ void __launch_bounds__(PTL_BLK) k_ptl(RoundArgs) {
+    enum { T_FIRST, T_FAIL, T_OVF, T_BOUND, T_DLV, T_EMT = T_DLV + 5, T_N = T_EMT + 5 };
+    __shared__ unsigned long long sst[T_N + 1];       // (+ the digest)
+    __shared__ uint32_t sslots[2 * PSIM_MSG_SLOTS];
+    __shared__ uint32_t wcnt[5];
+    __shared__ uint32_t tabs[4 * PTL_CAP * PTL_BLK];
+    for (int i = threadIdx.x; i < 2 * PSIM_MSG_SLOTS; i += blockDim.x) sslots[i] = kargs().slots[i];
+    if (threadIdx.x < T_N + 1) sst[threadIdx.x] = 0;
+    __syncthreads();
+    const uint32_t l = lane_id();
+    const uint32_t nq = *kargs().n_ptl;
+    uint32_t v[T_N] = {};
+    uint64_t dig = 0;
+    const uint32_t X0[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    PtLane n;
+    n.EG.p = tabs + threadIdx.x;
+    n.LZ.p = tabs + PTL_CAP * PTL_BLK + threadIdx.x;
+    n.OL.p = tabs + 2 * PTL_CAP * PTL_BLK + threadIdx.x;
+    n.OH.p = tabs + 3 * PTL_CAP * PTL_BLK + threadIdx.x;
+    for (uint32_t base = blockIdx.x * blockDim.x; base < nq; base += gridDim.x * blockDim.x) {
+        KArgs& a = kargs();
+        const uint32_t P = base + threadIdx.x;
+        bool go = false, fall = false;
+        uint4 D = make_uint4(0, 0, 0, 0);
+        uint32_t root0 = NONE, rtw4 = 0, rtw5 = 0, w10 = 0, w11 = 0, start = 0, act_n = 0;
+        if (P < nq) {
+            D = a.desc_ptl[P];
+            const size_t li = D.x - a.lo;
+            const uint32_t* hp = reinterpret_cast<const uint32_t*>(a.hdr + li);
+            const uint4 hq1 = reinterpret_cast<const uint4*>(hp)[1], hq2 = reinterpret_cast<const uint4*>(hp)[2];
+            start = hp[2];
+            act_n = hq2.y & 0xFF;                     // word 9
+            w10 = hq2.z; w11 = hq2.w;
+            const uint4* rr = reinterpret_cast<const uint4*>(a.pt_rt + li * RT_WORDS);
+            const uint4 r0 = rr[0], r1 = rr[1];
+            root0 = r0.x; rtw4 = r1.x; rtw5 = r1.y;
+            // the lane's preconditions over the inbox's Plumtree messages
+            const uint32_t ik = start == a.round ? 0u : (D.z & DESC_CNT_MASK);
+            uint32_t npt = 0, r0t = root0;
+            uint64_t bm = 0;                          // message slots of the BROADCASTs
+            // (an outstanding extension row taken earlier holds zeros while the
+            // table fits its own row: this round's adds must fit that row)
+            bool ok = r0.y == NONE && r0.z == NONE && r0.w == NONE &&
+                      (root0 == NONE || ((rtw4 >> 8) == 0 && (rtw5 >> 8) == 0));
+            for (uint32_t j = 0; ok && j < ik; j++) {
+                const Msg& m = a.rec_in[D.y + j];
+                const uint32_t type = m.tt & 0xFF;
+                if (type < PSIM_MSG_PT_BROADCAST || type > PSIM_MSG_PT_GRAFT) continue;
+                npt++;
+                if (type == PSIM_MSG_PT_BROADCAST) bm |= 1ull << (m.a0 % PSIM_MSG_SLOTS);
+                if (type != PSIM_MSG_PT_IGNORED_IHAVE) {
+                    if (r0t == NONE) r0t = m.a2;      // the root a first update would store
+                    ok &= m.a2 == r0t;
+                }
+            }
+            // first deliveries (lazy adds): the BROADCASTs' slots not delivered yet
+            const uint32_t nb = popc(bm & ~(((uint64_t)hq1.y << 32) | hq1.z));
+            const uint32_t com_n = w10 >> 24, out_n = (w11 >> 16) & 0xFF;
+            const uint32_t ne0 = root0 == NONE ? com_n : (rtw4 & 0xFF), nl0 = root0 == NONE ? 0u : (rtw5 & 0xFF);
+            ok &= ne0 + npt <= (uint32_t)PTL_CAP && nl0 + npt <= (uint32_t)PTL_CAP &&
+                  out_n + nb * (nl0 + npt) <= (uint32_t)PTL_CAP;
+            go = ok;
+            fall = !ok;
+        }
+        // nodes that do not fit go to k_pt's list (one atomic per block step)
+        block_append(fall, D, kargs().desc_pt, kargs().n_pt, wcnt);
+        if (!go) continue;
+        const uint32_t id = D.x;
+        const size_t li = id - a.lo;
+        n.id = id;
+        n.me_part = a.part[id];
+        n.act_n = act_n;
+        {
+            const uint4* ar = reinterpret_cast<const uint4*>(a.act + li * PSIM_ACTIVE_CAP);
+            const uint4 a0 = ar[0], a1 = ar[1];
+            n.A[0] = a0.x; n.A[1] = a0.y; n.A[2] = a0.z; n.A[3] = a0.w;
+            n.A[4] = a1.x; n.A[5] = a1.y; n.A[6] = a1.z; n.A[7] = a1.w;
+        }
+        n.root0 = root0;
+        n.ne = root0 == NONE ? 0u : (rtw4 & 0xFF);
+        n.nl = root0 == NONE ? 0u : (rtw5 & 0xFF);
+        {
+            const uint4* er = reinterpret_cast<const uint4*>(a.pt_eag + li * RT_SET);
+            const uint4* lr = reinterpret_cast<const uint4*>(a.pt_laz + li * RT_SET);
+            const uint4* orow = reinterpret_cast<const uint4*>(a.pt_out + li * OUT_IN);
+#pragma unroll
+            for (int q = 0; q < PTL_CAP / 4; q++) {
+                const uint4 e = er[q], z = lr[q];
+                n.EG[4 * q] = e.x; n.EG[4 * q + 1] = e.y; n.EG[4 * q + 2] = e.z; n.EG[4 * q + 3] = e.w;
+                n.LZ[4 * q] = z.x; n.LZ[4 * q + 1] = z.y; n.LZ[4 * q + 2] = z.z; n.LZ[4 * q + 3] = z.w;
+            }
+#pragma unroll
+            for (int q = 0; q < PTL_CAP / 2; q++) {
+                const uint4 o = orow[q];
+                n.OL[2 * q] = o.x; n.OH[2 * q] = o.y; n.OL[2 * q + 1] = o.z; n.OH[2 * q + 1] = o.w;
+            }
+        }
+        const uint32_t com_n = w10 >> 24;
+        const uint32_t* hp = reinterpret_cast<const uint32_t*>(a.hdr + li);
+        n.on = (w11 >> 16) & 0xFF;
+        n.have = ((uint64_t)hp[5] << 32) | hp[6];
+        n.sets_dirty = false; n.out_dirty = false;
+        uint32_t trk_round = hp[7], trk_hop = hp[8];
+        uint32_t seq = a.ocnt[li];
+        const uint32_t oend = (uint32_t)a.obase[li + 1];
+        const uint32_t ik = start == a.round ? 0u : (D.z & DESC_CNT_MASK);
+        for (uint32_t j = 0; j < ik; j++) {           // the Plumtree inbox, canonical order
+            const Msg* rp = a.rec_in + D.y + j;
+            const uint32_t type = rp->tt & 0xFF;
+            if (type < PSIM_MSG_PT_BROADCAST || type > PSIM_MSG_PT_GRAFT) continue;
+            const uint32_t src = rp->src, msg = rp->a0, rnd = rp->a1, root = rp->a2, from = src | PSIM_MAP_BIT;
+            v[T_DLV + type - PSIM_MSG_PT_BROADCAST]++;
+            // plumtree_backend is_stale/1 over the slots (a retired id: overflow, stale)
+            const uint32_t sk = msg % PSIM_MSG_SLOTS;
+            const bool live = sslots[sk] == msg;
+            const bool have = !live || ((n.have >> sk) & 1ull);
+            if (type != PSIM_MSG_PT_PRUNE && type != PSIM_MSG_PT_IGNORED_IHAVE && !live) v[T_OVF]++;
+            uint32_t sto = NONE, stt = 0, sa0 = 0, sa1 = 0;     // a single send of the handler
+            if (type == PSIM_MSG_PT_BROADCAST) {     // pt:288-293, :368-378
+                if (!have) {
+                    n.have |= 1ull << sk;
+                    v[T_FIRST]++;
+                    if (msg == a.tracked_msg) { trk_round = a.round; trk_hop = rnd + 1; }
+                    ptl_update(a, n, li, com_n, from, root, true);
+                    // eager_push/7 + schedule_lazy_push/6 over slot 0's sets
+                    for (uint32_t i = 0; i < n.ne; i++) {
+                        const uint32_t e = n.EG[i];
+                        if (e == from) continue;
+                        if (ptl_conn(a, n, e)) {
+                            dig += relay_emit(a, D.w + seq, e & ~PSIM_MAP_BIT, id, PSIM_MSG_PT_BROADCAST, seq, msg, rnd + 1,
+                                              root, X0);
+                            seq++;
+                            v[T_EMT + 0]++;
+                        } else {
+                            v[T_FAIL]++;
+                        }
+                    }
+                    for (uint32_t i = 0; i < n.nl; i++) {
+                        const uint32_t e = n.LZ[i];
+                        if (e != from) ptl_add_out(n, ((uint64_t)e << 32) | (msg << 16) | ((rnd + 1) & 0xFFFFu));
+                    }
+                } else {
+                    ptl_update(a, n, li, com_n, from, root, false);
+                    sto = from; stt = PSIM_MSG_PT_PRUNE;
+                }
+            } else if (type == PSIM_MSG_PT_PRUNE) {  // pt:294-298
+                ptl_update(a, n, li, com_n, from, root, false);
+            } else if (type == PSIM_MSG_PT_IHAVE) {  // pt:299-303, :380-386
+                sto = from; stt = have ? PSIM_MSG_PT_IGNORED_IHAVE : PSIM_MSG_PT_GRAFT; sa0 = msg; sa1 = rnd;
+                if (!have) ptl_update(a, n, li, com_n, from, root, true);
+            } else if (type == PSIM_MSG_PT_IGNORED_IHAVE) {   // pt:304-307
+                ptl_ack_out(n, ((uint64_t)from << 32) | (msg << 16) | (rnd & 0xFFFFu));
+            } else if (have) {                       // GRAFT pt:308-313, :388-402
+                ptl_update(a, n, li, com_n, from, root, true);
+                sto = from; stt = PSIM_MSG_PT_BROADCAST; sa0 = msg; sa1 = rnd;
+            }
+            if (sto != NONE) {                        // (the IHAVE answer goes before the update in
+                if (ptl_conn(a, n, sto)) {            //  the reference; the update sends nothing)
+                    dig += relay_emit(a, D.w + seq, src, id, stt, seq, sa0, sa1, root, X0);
+                    seq++;
+                    v[T_EMT + stt - PSIM_MSG_PT_BROADCAST]++;
+                } else {
+                    v[T_FAIL]++;
+                }
+            }
+        }
+        if (((D.z >> 28) & DESC_LAZY) && n.on > 0) {   // the lazy tick (pt:341-345, :443-453)
+            for (uint32_t i = 0; i < n.on; i++) {
+                const uint64_t o = out_at(n, i);
+                const uint32_t peer = (uint32_t)(o >> 32);
+                if (!ptl_conn(a, n, peer)) { v[T_FAIL]++; continue; }
+                const uint32_t msg = (uint32_t)(o >> 16) & 0xFFFFu, sk = msg % PSIM_MSG_SLOTS;
+                const bool live = sslots[sk] == msg;
+                v[T_OVF] += live ? 0u : 1u;
+                dig += relay_emit(a, D.w + seq, peer & ~PSIM_MAP_BIT, id, PSIM_MSG_PT_IHAVE, seq, msg,
+                                  (uint32_t)o & 0xFFFFu, live ? sslots[PSIM_MSG_SLOTS + sk] : NONE, X0);
+                seq++;
+                v[T_EMT + 2]++;
+            }
+        }
+        // write back: header words 5-8 and 11, the sets, the table, the flag byte
+        uint32_t* hw = reinterpret_cast<uint32_t*>(a.hdr + li);
+        reinterpret_cast<uint4*>(hw)[1] = make_uint4(hp[4], (uint32_t)(n.have >> 32), (uint32_t)n.have, trk_round);
+        hw[8] = trk_hop;
+        hw[11] = (w11 & ~0xFF0000u) | (n.on << 16);
+        if (n.sets_dirty) {
+            // (slots 1-3 stay free, the count words hold slot 0's counts only)
+            uint4* rr = reinterpret_cast<uint4*>(a.pt_rt + li * RT_WORDS);
+            rr[0] = make_uint4(n.root0, NONE, NONE, NONE);
+            rr[1].x = n.ne;
+            rr[1].y = n.nl;
+            uint4* er = reinterpret_cast<uint4*>(a.pt_eag + li * RT_SET);
+            uint4* lr = reinterpret_cast<uint4*>(a.pt_laz + li * RT_SET);
+#pragma unroll
+            for (int q = 0; q < PTL_CAP / 4; q++) {
+                er[q] = make_uint4(n.EG[4 * q], n.EG[4 * q + 1], n.EG[4 * q + 2], n.EG[4 * q + 3]);
+                lr[q] = make_uint4(n.LZ[4 * q], n.LZ[4 * q + 1], n.LZ[4 * q + 2], n.LZ[4 * q + 3]);
+            }
+        }
+        if (n.out_dirty) {
+            uint4* orow = reinterpret_cast<uint4*>(a.pt_out + li * OUT_IN);
+#pragma unroll
+            for (int q = 0; q < PTL_CAP / 2; q++)
+                orow[q] = make_uint4(n.OL[2 * q], n.OH[2 * q], n.OL[2 * q + 1], n.OH[2 * q + 1]);
+        }
+        a.ocnt[li] = seq;
+        v[T_BOUND] += seq > oend - D.w ? 1u : 0u;
+        const uint8_t fl = a.flags[id];
+        a.flags[id] = (uint8_t)((fl & (F_UP | F_CRASHED)) | (n.on ? F_LAZY : 0) | (min(n.on, 15u) << F_OUTN_SHIFT) |
+                                (act_n < a.min_active ? F_LOWACT : 0));
+    }
+#pragma unroll
+    for (int k = 0; k < T_N; k++)
+        for (int o = 32; o > 0; o >>= 1) v[k] += __shfl_xor(v[k], o);
+    for (int o = 32; o > 0; o >>= 1) dig += shfl64(dig, (int)((l + o) & 63));
+    if (l == 0) {
+        for (int k = 0; k < T_N; k++)
+            if (v[k]) atomicAdd(&sst[k], (unsigned long long)v[k]);
+        if (dig) atomicAdd(&sst[T_N], (unsigned long long)dig);
+    }
+    __syncthreads();
+    uint64_t* row = kargs().stat_ptl + (size_t)blockIdx.x * NST;
+    for (uint32_t k = threadIdx.x; k < NST; k += blockDim.x) {
+        uint64_t x = 0;
+        if (k == ST_FIRST) x = sst[T_FIRST];
+        else if (k == ST_FAIL) x = sst[T_FAIL];
+        else if (k == ST_OVF || k == ST_OVF_BY + PSIM_OVF_PT) x = sst[T_OVF];
+        else if (k == ST_DIGEST) x = sst[T_N];
+        else if (k == ST_BOUND) x = sst[T_BOUND];
+        else if (k >= ST_DELIV + PSIM_MSG_PT_BROADCAST && k <= ST_DELIV + PSIM_MSG_PT_GRAFT)
+            x = sst[T_DLV + k - ST_DELIV - PSIM_MSG_PT_BROADCAST];
+        else if (k >= ST_EMIT + PSIM_MSG_PT_BROADCAST && k <= ST_EMIT + PSIM_MSG_PT_GRAFT)
+            x = sst[T_EMT + k - ST_EMIT - PSIM_MSG_PT_BROADCAST];
+        row[k] = x;
+    }
     if (threadIdx.x == 0) atomicMax(&kargs().ktime[1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
 }
 

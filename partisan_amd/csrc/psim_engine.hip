@@ -586,6 +586,7 @@ __global__ void __launch_bounds__(256) k_node_prep(RoundArgs a, const unsigned l
         a.ktime[0] = ~0ull; a.ktime[1] = 0; *a.n_slow = 0; *a.n_pt = 0;
         if (a.n_shuf) *a.n_shuf = 0;
         if (a.n_lite) *a.n_lite = 0;
+        if (a.n_ptl) *a.n_ptl = 0;
         if (a.n_stop) *a.n_stop = 0;
     }
     __syncthreads();
@@ -1013,12 +1014,12 @@ struct Shard {
     DBuf<Msg> inbox;
     // per-round scratch
     DBuf<uint32_t> okey, ocnt, in_beg,
-        d_nact, n_slow, n_pt, n_shuf, n_lite, rank, long_list, n_long, tmp, hist, hoff;
+        d_nact, n_slow, n_pt, n_shuf, n_lite, n_ptl, rank, long_list, n_long, tmp, hist, hoff;
     DBuf<unsigned long long> bmask;     // per local node: message slots of its BROADCAST records
     DBuf<uint2> pairs;                  // route: (destination in bucket | class, source index)
     DBuf<unsigned long long> cb;        // per local node: inbox count | bound sum << 32 (n + 1)
     DBuf<unsigned long long> btot;      // this round's outbox total (k_node_prep)
-    DBuf<uint4> desc, desc_slow, desc_pt, desc_shuf, desc_lite;   // work descriptors; those k_relay leaves to k_consume / k_pt / k_shuf
+    DBuf<uint4> desc, desc_slow, desc_pt, desc_shuf, desc_lite, desc_ptl;   // work descriptors; those k_relay leaves to k_consume / k_pt / k_shuf
     DBuf<uint64_t> bound, pscan, obase, stat_part, stat_out, d_off;   // bound: packed (bound << 32 | work)
     DBuf<uint8_t> cub_tmp;              // the scan's tile totals
     DBuf<uint32_t> ev_ids, ev_contacts, stop_ids, n_stop;
@@ -1030,8 +1031,8 @@ struct Shard {
     DBuf<uint8_t> faulted;              // omission faults: generally omitting nodes (global id)
     DBuf<uint64_t> omit;                // ... sorted send-omission pairs, then receive-omission pairs
     std::vector<uint64_t> soff, scnt;   // per destination shard (G + 1 offsets)
-    uint32_t pgrid = 0, cgrid = 0, rgrid = 0, tgrid = 0, sgrid = 0, lgrid = 0;   // stats rows: prepare, consume,
-                                                                   // relay, plumtree, shuffle-start, lite blocks
+    uint32_t pgrid = 0, cgrid = 0, rgrid = 0, tgrid = 0, sgrid = 0, lgrid = 0, qgrid = 0;   // stats rows: prepare,
+                                   // consume, relay, plumtree, shuffle-start, lite, Plumtree-lane blocks
     // pinned host words: NST stats and the consume span (stat_out), then the
     // outbox total and the routed record count: the round's two read-backs
     uint64_t* pin = nullptr;
@@ -1128,6 +1129,7 @@ RoundArgs make_args(psim_handle* h, Shard* s) {
     a.desc_pt = s->desc_pt.p; a.n_pt = s->n_pt.p;
     a.desc_shuf = s->desc_shuf.p; a.n_shuf = s->n_shuf.p;
     a.desc_lite = s->desc_lite.p; a.n_lite = s->n_lite.p;
+    a.desc_ptl = s->desc_ptl.p; a.n_ptl = s->n_ptl.p;
     a.stop_ids = s->stop_ids.p; a.n_stop = s->n_stop.p;
     a.faults = h->faults; a.n_omit_s = h->n_omit_s; a.n_omit_r = h->n_omit_r;
     a.faulted = s->faulted.p; a.omit = s->omit.p;
@@ -1353,7 +1355,9 @@ int phase_events_prepare(psim_handle* h, Shard* s, const RoundCtl& ctl, RoundArg
         s->tgrid = hv && h->cfg.plumtree ? std::min<uint32_t>(grid_for(n), h->pt_blocks) : 0;
         s->sgrid = hv ? std::min<uint32_t>(grid_for(n), SHUF_MAX_BLOCKS) : 0;
         s->lgrid = hv ? std::min<uint32_t>(grid_for(n), h->lite_blocks) : 0;
-        TRY(s->stat_part.ensure((size_t)(s->pgrid + s->cgrid + s->rgrid + s->tgrid + s->sgrid + s->lgrid) * NST));
+        s->qgrid = hv && h->cfg.plumtree ? std::min<uint32_t>((n + PTL_BLOCK - 1) / PTL_BLOCK, PTL_MAX_BLOCKS) : 0;
+        TRY(s->stat_part.ensure((size_t)(s->pgrid + s->cgrid + s->rgrid + s->tgrid + s->sgrid + s->lgrid + s->qgrid) *
+                                NST));
         k_node_prep<<<s->pgrid, BLK, 0, s->stream>>>(a, s->bmask.p, s->bound.p, s->stat_part.p, s->ocnt.p,
                                                      s->btot.p);
         // bound[n] = 0: pscan[n] = (outbox total << 32) | active count;
@@ -1404,6 +1408,7 @@ int phase_events_prepare(psim_handle* h, Shard* s, const RoundCtl& ctl, RoundArg
     a.stat_pt = s->stat_part.p + (size_t)(s->pgrid + s->cgrid + s->rgrid) * NST;
     a.stat_shuf = s->stat_part.p + (size_t)(s->pgrid + s->cgrid + s->rgrid + s->tgrid) * NST;
     a.stat_lite = s->stat_part.p + (size_t)(s->pgrid + s->cgrid + s->rgrid + s->tgrid + s->sgrid) * NST;
+    a.stat_ptl = s->stat_part.p + (size_t)(s->pgrid + s->cgrid + s->rgrid + s->tgrid + s->sgrid + s->lgrid) * NST;
     return PSIM_OK;
 }
 
@@ -1441,6 +1446,7 @@ int phase_consume(psim_handle* h, Shard* s, RoundArgs& a) {
         b.desc = s->desc_slow.p;
         b.n_alist = s->n_slow.p;
         k_consume<<<s->cgrid, BLK, 0, s->stream>>>(b);
+        if (s->qgrid) k_ptl<<<s->qgrid, PTL_BLOCK, 0, s->stream>>>(a);
         if (s->tgrid) {
             RoundArgs c = a;
             c.desc = s->desc_pt.p;
@@ -1630,7 +1636,7 @@ int exchange_rccl(psim_handle* h) {
 int phase_stats(psim_handle* h, Shard* s, const std::vector<uint32_t>& crashed) {
     KTimer t(h, s, KT_STATS);
     k_stats_reduce<<<NST, BLK, 0, s->stream>>>(s->stat_part.p, s->pgrid + s->cgrid + s->rgrid + s->tgrid + s->sgrid +
-                                                   s->lgrid,
+                                                   s->lgrid + s->qgrid,
                                                s->stat_out.p,
                                                 s->pin_dev);
     if (!crashed.empty()) {
@@ -1707,9 +1713,9 @@ int run_round(psim_handle* h, uint64_t* st) {
             uint64_t em = 0;
             for (int k = 0; k < PSIM_MSG_NTYPES; k++) em += s->pin[ST_EMIT + k];
             std::fprintf(stderr, "psim: round %llu shard %u: %u nodes with work, %u to k_consume, %u to k_pt, "
-                         "%u to k_shuf, %u to k_consume_lite, outbox bound %llu, emitted %llu\n",
+                         "%u to k_shuf, %u to k_consume_lite, %u to k_ptl, outbox bound %llu, emitted %llu\n",
                          (unsigned long long)h->round, s->idx, read1(s, s->d_nact.p), read1(s, s->n_slow.p),
-                         read1(s, s->n_pt.p), read1(s, s->n_shuf.p), read1(s, s->n_lite.p),
+                         read1(s, s->n_pt.p), read1(s, s->n_shuf.p), read1(s, s->n_lite.p), read1(s, s->n_ptl.p),
                          (unsigned long long)s->pin[PIN_TOTAL], (unsigned long long)em);
         }
         if (s->pin[NST] != ~0ull && s->pin[NST + 1] > s->pin[NST]) {   // 100 MHz ticks
@@ -1808,6 +1814,7 @@ int shard_alloc(psim_handle* h, Shard* s) {
     rc |= s->desc_pt.alloc(n); rc |= s->n_pt.alloc(1);
     rc |= s->desc_shuf.alloc(n); rc |= s->n_shuf.alloc(1);
     rc |= s->desc_lite.alloc(n); rc |= s->n_lite.alloc(1);
+    rc |= s->desc_ptl.alloc(n); rc |= s->n_ptl.alloc(1);
     if (h->cfg.manager == PSIM_MANAGER_PLUGGABLE) { rc |= s->stop_ids.alloc(n); rc |= s->n_stop.alloc(1); }
     rc |= s->stat_out.alloc(NST + 2);   // + the consume span
     rc |= s->ikeys.alloc(1024); rc |= s->ivals.alloc(1024);
@@ -1848,7 +1855,7 @@ void shard_free(Shard* s) {
     s->rank.release(); s->long_list.release(); s->bmask.release(); s->btot.release();
     s->hist.release(); s->hoff.release(); s->pairs.release(); s->n_long.release(); s->tmp.release();
     s->stop_ids.release(); s->n_stop.release();
-    s->desc.release(); s->d_nact.release(); s->desc_slow.release(); s->n_slow.release(); s->desc_pt.release(); s->n_pt.release(); s->desc_shuf.release(); s->n_shuf.release(); s->desc_lite.release(); s->n_lite.release(); s->bound.release(); s->pscan.release();
+    s->desc.release(); s->d_nact.release(); s->desc_slow.release(); s->n_slow.release(); s->desc_pt.release(); s->n_pt.release(); s->desc_shuf.release(); s->n_shuf.release(); s->desc_lite.release(); s->n_lite.release(); s->desc_ptl.release(); s->n_ptl.release(); s->bound.release(); s->pscan.release();
     s->obase.release(); s->stat_part.release(); s->stat_out.release(); s->d_off.release();
     s->cub_tmp.release(); s->ev_ids.release(); s->ev_contacts.release(); s->sendbuf.release();
     s->sview.release(); s->sinv.release(); s->fbits.release(); s->pay[0].release(); s->pay[1].release();

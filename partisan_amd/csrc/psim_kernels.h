@@ -51,6 +51,9 @@ struct RoundArgs {
     uint4* desc_lite;           // ... and the nodes with SHUFFLE terminals / replies, for k_consume_lite
     uint32_t* n_lite;
     uint64_t* stat_lite;        // k_consume_lite's per-block stats rows
+    uint4* desc_ptl;            // ... and the nodes with Plumtree work and no origin, for k_ptl
+    uint32_t* n_ptl;
+    uint64_t* stat_ptl;         // k_ptl's per-block stats rows
     uint64_t* stat_relay;
     uint64_t* stat_pt;          // k_pt's per-block stats rows
     const Msg* rec_in;          // dense, in inbox order (node runs at in_beg)
@@ -91,12 +94,16 @@ __global__ void k_consume(RoundArgs args);
 // lane-per-node SHUFFLE relays ahead of k_consume (psim_consume.hip)
 constexpr uint32_t RELAY_MAX_BLOCKS = 8192;
 constexpr uint32_t SHUF_MAX_BLOCKS = 1024;     // k_shuf: grid-stride over its list
+constexpr uint32_t PTL_MAX_BLOCKS = 1024;      // k_ptl: grid-stride over its list
+constexpr uint32_t PTL_BLOCK = 128;            // k_ptl's block (psim_consume.hip PTL_BLK)
 __global__ void k_relay(RoundArgs args);
 __global__ void k_consume_pl(RoundArgs args);
 // lane-per-node shuffle starts of the nodes k_relay listed (psim_consume.hip)
 __global__ void k_shuf(RoundArgs args);
 // wave-per-node SHUFFLE terminals, replies and their merges (psim_consume.hip)
 __global__ void k_consume_lite(RoundArgs args);
+// lane-per-node Plumtree phases (psim_consume.hip); hands k_pt what does not fit
+__global__ void k_ptl(RoundArgs args);
 // the Plumtree phase of the nodes k_relay listed (psim_consume.hip)
 __global__ void k_pt(RoundArgs args);
 // diagnostic builds (-DPSIM_STAMPS): per-phase cycle sums of k_consume, reset on read

@@ -6,7 +6,7 @@ for r in rows:
     n=r['Kernel_Name']; d=(int(r['End_Timestamp'])-int(r['Start_Timestamp']))/1000
     if 'k_relay' in n: cur={'relay':d}; out.append(cur)
     elif cur is not None:
-        for k,tag in (('shuf','k_shuf'),('lite','k_consume_lite'),('merge','k_merge'),('cons','k_consume('),('pt','k_pt(')):
+        for k,tag in (('shuf','k_shuf'),('lite','k_consume_lite'),('ptl','k_ptl('),('merge','k_merge'),('cons','k_consume('),('pt','k_pt(')):
             if tag in n: cur[k]=d
 last=out[-int(sys.argv[2]) if len(sys.argv)>2 else -20:]
 for i,c in enumerate(last):
