@@ -1303,7 +1303,6 @@ __global__ void __launch_bounds__(256, PSIM_WAVES_PER_SIMD) k_consume(RoundArgs 
     __shared__ __attribute__((aligned(16))) uint32_t srecs[WAVES_PER_BLOCK][STAGE * 16];
     __shared__ uint32_t skeys[WAVES_PER_BLOCK][STAGE];
     for (int i = threadIdx.x; i < NST; i += blockDim.x) sst[i] = 0;
-    if (threadIdx.x == 0) atomicMin(&kargs().ktime[0], (unsigned long long)__builtin_amdgcn_s_memrealtime());
     __syncthreads();
 
     const uint32_t wid = threadIdx.x >> 6;
@@ -1357,7 +1356,6 @@ __global__ void __launch_bounds__(256, PSIM_WAVES_PER_SIMD) k_consume(RoundArgs 
     __syncthreads();
     for (int i = threadIdx.x; i < NST; i += blockDim.x)
         kargs().stat_part[(size_t)blockIdx.x * NST + i] = sst[i];
-    if (threadIdx.x == 0) atomicMax(&kargs().ktime[1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
 }
 
 // ------------------------------------------------ shuffle-exchange phase --
@@ -1481,7 +1479,6 @@ __global__ void __launch_bounds__(256, PSIM_LITE_WAVES) k_consume_lite(RoundArgs
     __syncthreads();
     for (int i = threadIdx.x; i < NST; i += blockDim.x)
         kargs().stat_lite[(size_t)blockIdx.x * NST + i] = sst[i];
-    if (threadIdx.x == 0) atomicMax(&kargs().ktime[1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
 }
 
 // ------------------------------------------------------- Plumtree phase --
@@ -1690,7 +1687,6 @@ __global__ void __launch_bounds__(256, PSIM_PT_WAVES) k_pt(RoundArgs args) {
     __syncthreads();
     for (int i = threadIdx.x; i < NST; i += blockDim.x)
         kargs().stat_part[(size_t)blockIdx.x * NST + i] = sst[i];
-    if (threadIdx.x == 0) atomicMax(&kargs().ktime[1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
 }
 
 // ------------------------------------------------ relays and lazy ticks --
@@ -1752,7 +1748,6 @@ __global__ void __launch_bounds__(256) k_relay(RoundArgs) {
     for (int i = threadIdx.x; i < 2 * PSIM_MSG_SLOTS; i += blockDim.x) sslots[i] = kargs().slots[i];
     __shared__ uint32_t wcnt[5];                      // per wave list counts, then the block's base
     if (threadIdx.x < R_N) sst[threadIdx.x] = 0;
-    if (threadIdx.x == 0) atomicMin(&kargs().ktime[0], (unsigned long long)__builtin_amdgcn_s_memrealtime());
     __syncthreads();
     const uint32_t l = lane_id();
     const uint32_t na = *kargs().n_alist;
@@ -2149,7 +2144,6 @@ __global__ void __launch_bounds__(256) k_shuf(RoundArgs) {
     for (uint32_t k = threadIdx.x; k < NST; k += blockDim.x)
         row[k] = k == ST_EMIT + PSIM_MSG_SHUFFLE ? sst[S_SHUF] : k == ST_FAIL ? sst[S_FAIL]
                : k == ST_DIGEST ? sst[S_DIGEST] : k == ST_BOUND ? sst[S_BOUND] : 0ull;
-    if (threadIdx.x == 0) atomicMax(&kargs().ktime[1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
 }
 
 // ---------------------------------------------------- Plumtree lanes --
@@ -2514,7 +2508,14 @@ __global__ void __launch_bounds__(PTL_BLK) k_ptl(RoundArgs) {
             x = sst[T_EMT + k - ST_EMIT - PSIM_MSG_PT_BROADCAST];
         row[k] = x;
     }
-    if (threadIdx.x == 0) atomicMax(&kargs().ktime[1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+}
+
+// the node-round phase's span: s_memrealtime (100 MHz) before k_relay
+// (slot 0) and after the last node-round kernel (slot 1), on the same
+// stream -- one wave each instead of a same-address atomic from every block
+// of every kernel (~10^4 per round)
+__global__ void k_mark(unsigned long long* t, int slot) {
+    if (threadIdx.x == 0) t[slot] = __builtin_amdgcn_s_memrealtime();
 }
 
 // one wave-slot per resident wave: the grid strides over the active list

@@ -1439,6 +1439,7 @@ int phase_consume(psim_handle* h, Shard* s, RoundArgs& a) {
         // k_relay sorts the nodes with work: a lone SHUFFLE relay (and a
         // lazy tick) one lane each, more HyParView work one k_consume wave,
         // Plumtree work one k_pt wave after the node's HyParView phase
+        k_mark<<<1, 64, 0, s->stream>>>(a.ktime, 0);
         k_relay<<<s->rgrid, BLK, 0, s->stream>>>(a);
         k_shuf<<<s->sgrid, BLK, 0, s->stream>>>(a);
         k_consume_lite<<<s->lgrid, BLK, 0, s->stream>>>(a);
@@ -1454,6 +1455,7 @@ int phase_consume(psim_handle* h, Shard* s, RoundArgs& a) {
             c.stat_part = a.stat_pt;
             k_pt<<<s->tgrid, BLK, 0, s->stream>>>(c);
         }
+        k_mark<<<1, 64, 0, s->stream>>>(a.ktime, 1);
     }
     HIP_TRY(hipGetLastError());
     s->pay_cur ^= 1;

@@ -104,6 +104,8 @@ __global__ void k_shuf(RoundArgs args);
 __global__ void k_consume_lite(RoundArgs args);
 // lane-per-node Plumtree phases (psim_consume.hip); hands k_pt what does not fit
 __global__ void k_ptl(RoundArgs args);
+// a timestamp into t[slot] (the node-round span, RoundArgs::ktime)
+__global__ void k_mark(unsigned long long* t, int slot);
 // the Plumtree phase of the nodes k_relay listed (psim_consume.hip)
 __global__ void k_pt(RoundArgs args);
 // diagnostic builds (-DPSIM_STAMPS): per-phase cycle sums of k_consume, reset on read
