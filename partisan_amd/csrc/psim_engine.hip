@@ -16,7 +16,7 @@
 //            G  > 1: stable partition by owner shard -> gather records ->
 //                    all-to-all (counts, then records) -> the same grouping
 //                    of the shard-ordered concatenation by dst
-//   stats    k_stats_reduce (+ sum over shards / ncclAllReduce)
+//   stats    k_stats_tiles + k_stats_final (+ sum over shards / ncclAllReduce)
 // Grouping a (src, seq)-ordered stream -- or a concatenation ordered by
 // source shard -- by dst, each group in stream order, yields each inbox in
 // canonical (src, seq) order,
@@ -614,7 +614,7 @@ __global__ void __launch_bounds__(256) k_node_prep(RoundArgs a, const unsigned l
                 w = c > 0 || (pending && !x.have) || per || leave;
             } else {
                 bool origin = a.origin[i] != 0;
-                const Hdr& x = a.hdr[i];
+                const Hdr& x = a.hdr[i];      // (read only where needed: a fresh start, a full nibble)
                 // the due timers' sends: the JOIN of a fresh start, a
                 // promotion's NEIGHBOR_REQUEST (the active view may shrink
                 // during the round: any due promotion), a shuffle
@@ -652,7 +652,13 @@ __global__ void __launch_bounds__(256) k_node_prep(RoundArgs a, const unsigned l
                 // a due lazy tick sends every outstanding entry: those left
                 // from last round and those this round's pushes add, at most
                 // PT_OUT_CAP
-                if (lazy) b += min((uint32_t)PSIM_PT_OUT_CAP, (uint32_t)x.out_n + lazy_add);
+                // (the flag byte's nibble is min(out_n, 15) after the node's
+                // last round: the header only when it saturates)
+                if (lazy) {
+                    const uint32_t fo = (uint32_t)f >> F_OUTN_SHIFT;
+                    const uint32_t on = fo < 15 ? fo : (uint32_t)x.out_n;
+                    b += min((uint32_t)PSIM_PT_OUT_CAP, on + lazy_add);
+                }
                 // a crash round: a NEIGHBOR_REQUEST per crashed active member
                 if (a.crash_round) {
                     const uint4* ar = reinterpret_cast<const uint4*>(a.act + (size_t)i * PSIM_ACTIVE_CAP);
@@ -741,26 +747,53 @@ __global__ void k_gather_dev(const Msg* __restrict__ rec, const uint32_t* __rest
     }
 }
 
-// one block per stats slot; lanes stride over the per-block partials.  The
-// sums (and the consume span, out[NST..NST+1]) are also stored straight
-// into the shard's pinned host words, so the host reads them after its
-// end-of-round wait without a copy.
-__global__ void k_stats_reduce(const uint64_t* part, uint32_t nblocks, uint64_t* out, uint64_t* hout) {
-    __shared__ uint64_t red[BLK];
-    uint32_t k = blockIdx.x;
-    uint64_t s = 0;
-    for (uint32_t b = threadIdx.x; b < nblocks; b += blockDim.x) s += part[(size_t)b * NST + k];
-    red[threadIdx.x] = s;
+// The round's stats: every kernel block left a row of NST partial sums.
+// k_stats_tiles: block b sums a contiguous range of rows, 4 rows at a time
+// with one lane per column (coalesced 384-B rows), into tile row b;
+// k_stats_final: one wave sums the tile rows.  The sums (and the node-round
+// span, out[NST..NST+1]) are also stored straight into the shard's pinned
+// host words, so the host reads them after its end-of-round wait without a
+// copy.
+constexpr uint32_t STAT_TILES = 256;
+__global__ void __launch_bounds__(BLK) k_stats_tiles(const uint64_t* __restrict__ part, uint32_t nrows,
+                                                    uint64_t* __restrict__ tiles) {
+    __shared__ uint64_t red[BLK / 64][64];
+    const uint32_t c = threadIdx.x & 63, g = threadIdx.x >> 6;
+    const uint32_t per = (nrows + gridDim.x - 1) / gridDim.x;
+    const uint32_t r0 = blockIdx.x * per, r1 = min(nrows, r0 + per);
+    uint64_t v = 0;
+    if (c < NST) {
+#pragma unroll 4
+        for (uint32_t r = r0 + g; r < r1; r += BLK / 64) v += part[(size_t)r * NST + c];
+    }
+    red[g][c] = v;
     __syncthreads();
-    for (uint32_t w = blockDim.x / 2; w > 0; w >>= 1) {
-        if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
-        __syncthreads();
+    if (g == 0 && c < NST) {
+        uint64_t t = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < BLK / 64; k++) t += red[k][c];
+        tiles[(size_t)blockIdx.x * NST + c] = t;
     }
-    if (threadIdx.x == 0) {
-        out[k] = red[0];
-        hout[k] = red[0];
-        if (k == 0) { hout[NST] = out[NST]; hout[NST + 1] = out[NST + 1]; }
+}
+__global__ void __launch_bounds__(BLK) k_stats_final(const uint64_t* __restrict__ tiles, uint32_t nt, uint64_t* out,
+                                                    uint64_t* hout) {
+    __shared__ uint64_t red[BLK / 64][64];
+    const uint32_t c = threadIdx.x & 63, g = threadIdx.x >> 6;
+    uint64_t v = 0;
+    if (c < NST) {
+#pragma unroll 4
+        for (uint32_t b = g; b < nt; b += BLK / 64) v += tiles[(size_t)b * NST + c];
     }
+    red[g][c] = v;
+    __syncthreads();
+    if (g == 0 && c < NST) {
+        uint64_t t = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < BLK / 64; k++) t += red[k][c];
+        out[c] = t;
+        hout[c] = t;
+    }
+    if (threadIdx.x == 0) { hout[NST] = out[NST]; hout[NST + 1] = out[NST + 1]; }
 }
 
 // --------------------------------------------------------- overlay stats --
@@ -1020,7 +1053,7 @@ struct Shard {
     DBuf<unsigned long long> cb;        // per local node: inbox count | bound sum << 32 (n + 1)
     DBuf<unsigned long long> btot;      // this round's outbox total (k_node_prep)
     DBuf<uint4> desc, desc_slow, desc_pt, desc_shuf, desc_lite, desc_ptl;   // work descriptors; those k_relay leaves to k_consume / k_pt / k_shuf
-    DBuf<uint64_t> bound, pscan, obase, stat_part, stat_out, d_off;   // bound: packed (bound << 32 | work)
+    DBuf<uint64_t> bound, pscan, obase, stat_part, stat_out, stat_tile, d_off;   // bound: packed (bound << 32 | work)
     DBuf<uint8_t> cub_tmp;              // the scan's tile totals
     DBuf<uint32_t> ev_ids, ev_contacts, stop_ids, n_stop;
     bool tomb_live = false;             // full: snapshots carry their remove rows
@@ -1637,10 +1670,10 @@ int exchange_rccl(psim_handle* h) {
 
 int phase_stats(psim_handle* h, Shard* s, const std::vector<uint32_t>& crashed) {
     KTimer t(h, s, KT_STATS);
-    k_stats_reduce<<<NST, BLK, 0, s->stream>>>(s->stat_part.p, s->pgrid + s->cgrid + s->rgrid + s->tgrid + s->sgrid +
-                                                   s->lgrid + s->qgrid,
-                                               s->stat_out.p,
-                                                s->pin_dev);
+    const uint32_t rows = s->pgrid + s->cgrid + s->rgrid + s->tgrid + s->sgrid + s->lgrid + s->qgrid;
+    const uint32_t nt = std::min<uint32_t>(STAT_TILES, std::max<uint32_t>(1, rows / 32));
+    k_stats_tiles<<<nt, BLK, 0, s->stream>>>(s->stat_part.p, rows, s->stat_tile.p);
+    k_stats_final<<<1, BLK, 0, s->stream>>>(s->stat_tile.p, nt, s->stat_out.p, s->pin_dev);
     if (!crashed.empty()) {
         TRY(upload(s, s->ev_ids, crashed));
         k_uncrash<<<grid_for(crashed.size()), BLK, 0, s->stream>>>(s->flags.p, s->ev_ids.p,
@@ -1819,6 +1852,7 @@ int shard_alloc(psim_handle* h, Shard* s) {
     rc |= s->desc_ptl.alloc(n); rc |= s->n_ptl.alloc(1);
     if (h->cfg.manager == PSIM_MANAGER_PLUGGABLE) { rc |= s->stop_ids.alloc(n); rc |= s->n_stop.alloc(1); }
     rc |= s->stat_out.alloc(NST + 2);   // + the consume span
+    rc |= s->stat_tile.alloc((size_t)STAT_TILES * NST);
     rc |= s->ikeys.alloc(1024); rc |= s->ivals.alloc(1024);
     rc |= s->recvbuf.alloc(1024); rc |= s->inbox.alloc(1024); rc |= s->outbox.alloc(1024);
     if (h->cfg.manager == PSIM_MANAGER_PLUGGABLE) {
@@ -1858,7 +1892,7 @@ void shard_free(Shard* s) {
     s->hist.release(); s->hoff.release(); s->pairs.release(); s->n_long.release(); s->tmp.release();
     s->stop_ids.release(); s->n_stop.release();
     s->desc.release(); s->d_nact.release(); s->desc_slow.release(); s->n_slow.release(); s->desc_pt.release(); s->n_pt.release(); s->desc_shuf.release(); s->n_shuf.release(); s->desc_lite.release(); s->n_lite.release(); s->desc_ptl.release(); s->n_ptl.release(); s->bound.release(); s->pscan.release();
-    s->obase.release(); s->stat_part.release(); s->stat_out.release(); s->d_off.release();
+    s->obase.release(); s->stat_part.release(); s->stat_out.release(); s->stat_tile.release(); s->d_off.release();
     s->cub_tmp.release(); s->ev_ids.release(); s->ev_contacts.release(); s->sendbuf.release();
     s->sview.release(); s->sinv.release(); s->fbits.release(); s->pay[0].release(); s->pay[1].release();
     s->pay_top.release();
