@@ -1695,15 +1695,14 @@ __global__ void __launch_bounds__(256, PSIM_PT_WAVES) k_pt(RoundArgs args) {
 // SHUFFLEs of their inbox (hv:1095-1136 with TTL > 0 and |active| > 1: a
 // select_random over active -- [Sender, Myself], then do_send_message) --
 // and such a lane does it here, exactly as k_consume's body and writeback
-// would (the same draws, records, sequence numbers, digest and stats).  A
-// node with more HyParView work (another message type, a due timer that can
-// act, a join, a crashed active member) goes to k_consume's list.  A node with Plumtree
-// work (Plumtree messages, an origin, a due lazy tick with entries
-// outstanding) goes to k_pt's list -- unless its only Plumtree work is the
-// lazy tick and its HyParView work is done here: then the lane runs the
-// tick too (an IHAVE per outstanding entry over live active connections).
-// The order of the lists does not matter (each node writes its own rows and
-// outbox region; the stats and the digest are sums).
+// would (the same draws, records, sequence numbers, digest and stats).  The
+// other lists: a due shuffle start with nothing else heavy -> k_shuf (after
+// the relays); SHUFFLE terminals / replies -> k_consume_lite; any other
+// HyParView work (another message type, a promotion that can act, a join, a
+// crashed active member) -> k_consume; Plumtree work (messages, a due lazy
+// tick with entries outstanding) -> k_ptl, an origin -> k_pt, after the
+// HyParView phase.  The order within a list does not matter (each node
+// writes its own rows and outbox region; the stats and the digest are sums).
 DEV uint64_t relay_emit(KArgs& a, uint64_t slot, uint32_t dst, uint32_t me, uint32_t tt, uint32_t seq,
                         uint32_t a0, uint32_t a1, uint32_t a2, const uint32_t (&X)[8]) {
     const uint32_t W[16] = {dst, me, tt, seq, a0, a1, a2, 0u, X[0], X[1], X[2], X[3], X[4], X[5], X[6], X[7]};
@@ -1741,11 +1740,12 @@ DEV void block_append(bool go, const uint4& D, uint4* desc, uint32_t* cnt, uint3
     }
 }
 
-__global__ void __launch_bounds__(256) k_relay(RoundArgs) {
-    enum { R_PROC, R_DELIV, R_SHUF, R_IHAVE, R_FAIL, R_DIGEST, R_OVF, R_BOUND, R_DIH, R_DIGN, R_EIGN, R_N };
+#ifndef PSIM_RELAY_WAVES
+#define PSIM_RELAY_WAVES 4
+#endif
+__global__ void __launch_bounds__(256, PSIM_RELAY_WAVES) k_relay(RoundArgs) {
+    enum { R_PROC, R_DELIV, R_SHUF, R_FAIL, R_DIGEST, R_BOUND, R_N };
     __shared__ unsigned long long sst[R_N];
-    __shared__ uint32_t sslots[2 * PSIM_MSG_SLOTS];
-    for (int i = threadIdx.x; i < 2 * PSIM_MSG_SLOTS; i += blockDim.x) sslots[i] = kargs().slots[i];
     __shared__ uint32_t wcnt[5];                      // per wave list counts, then the block's base
     if (threadIdx.x < R_N) sst[threadIdx.x] = 0;
     __syncthreads();
@@ -1757,7 +1757,7 @@ __global__ void __launch_bounds__(256) k_relay(RoundArgs) {
         KArgs& a = kargs();                           // (re-read per step, not held in SGPRs)
         const uint32_t P = base + threadIdx.x;
         uint4 D = make_uint4(0, 0, 0, 0);
-        bool heavy = false, to_pt = false, relay = false, pt_lane = false, maps = false, shuf = false, lite = false;
+        bool heavy = false, to_pt = false, relay = false, maps = false, shuf = false, lite = false;
         Hdr h;
         uint32_t ik = 0, oend = 0;
         uint4 act0 = make_uint4(0, 0, 0, 0), act1 = act0;
@@ -1778,7 +1778,7 @@ __global__ void __launch_bounds__(256) k_relay(RoundArgs) {
             // the inbox: how many HyParView messages, and whether each is a
             // SHUFFLE with TTL left (a relay while |active| > 1)
             uint32_t hvn = 0;
-            bool all_relay = true, pt_light = true, all_shuf = true;
+            bool all_relay = true, all_shuf = true;
             for (uint32_t j = 0; j < ik; j++) {
                 const Msg& m = a.rec_in[D.y + j];
                 const uint32_t tt = m.tt, type = tt & 0xFF;
@@ -1787,13 +1787,6 @@ __global__ void __launch_bounds__(256) k_relay(RoundArgs) {
                     maps |= type <= PSIM_MSG_NEIGHBOR_ACCEPTED;   // id maps (hv:703-1089)
                     all_relay &= type == PSIM_MSG_SHUFFLE && ((tt >> 8) & 0xFF) > 0;
                     all_shuf &= type == PSIM_MSG_SHUFFLE || type == PSIM_MSG_SHUFFLE_REPLY;
-                } else if (type == PSIM_MSG_PT_IHAVE) {
-                    // an IHAVE of a delivered (or retired: stale) id only
-                    // answers IGNORED_IHAVE (pt:380-386)
-                    const uint32_t k = m.a0 % PSIM_MSG_SLOTS;
-                    pt_light &= sslots[k] != m.a0 || (((k < 32 ? h.have : h.aux) >> (k & 31)) & 1u);
-                } else {
-                    pt_light &= type == PSIM_MSG_PT_IGNORED_IHAVE;   // an ack (pt:304-307)
                 }
             }
             const bool fresh = h.start_round == a.round;
@@ -1814,14 +1807,12 @@ __global__ void __launch_bounds__(256) k_relay(RoundArgs) {
             relay = !heavy && !lite && hvn > 0;
             const bool pt_msgs = !fresh && ik > hvn, origin = (tf & DESC_ORIGIN) != 0;
             const bool lazy = (tf & DESC_LAZY) && h.out_n > 0;
-            // the Plumtree phase runs in the lane when the node's HyParView
-            // phase does and its Plumtree work is IHAVE answers, acks and the
-            // lazy tick; else in k_pt (after k_consume for a heavy node)
-            // (after a shuffle start, the Plumtree phase waits for k_shuf: k_pt)
-            pt_lane = a.plumtree && !heavy && !shuf && !lite && !origin && (pt_msgs ? pt_light : lazy);
-            to_pt = a.plumtree && (pt_msgs || origin || ((heavy || shuf || lite) && lazy)) && !pt_lane;
+            // the Plumtree phase (messages, an origin, a due lazy tick with
+            // entries outstanding) runs after the HyParView phase: k_ptl, or
+            // k_pt for an origin
+            to_pt = a.plumtree && (pt_msgs || origin || lazy);
             // (k_consume and k_consume_lite count their own)
-            if (!heavy && !lite && (relay || to_pt || pt_lane || shuf)) v[R_PROC]++;
+            if (!heavy && !lite && (relay || to_pt || shuf)) v[R_PROC]++;
         }
         block_append(P < na && heavy, maps ? make_uint4(D.x, D.y, D.z | DESC_MAPS_BIT, D.w) : D, a.desc_slow, a.n_slow,
                      wcnt);
@@ -1877,98 +1868,13 @@ __global__ void __launch_bounds__(256) k_relay(RoundArgs) {
                 }
             }
         }
-        uint32_t out_n = h.out_n;
-        if (pt_lane) {
-            const uint32_t X[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-            uint64_t* own = a.pt_out + li * OUT_IN;   // outstanding: own row, then the extension row
-            uint64_t* ext = a.outx + (size_t)(h.pad1[3] ? h.pad1[3] - 1 : 0) * OUT_EXT;
-            // the Plumtree inbox in canonical order: IHAVE -> IGNORED_IHAVE
-            // over an active connection (pt:380-386, send/3 pt:633-638),
-            // IGNORED_IHAVE -> the outstanding entry acked (pt:562-567)
-            uint64_t gone = 0;
-            for (uint32_t j = 0; j < ik; j++) {
-                const Msg* rp = a.rec_in + D.y + j;
-                const uint32_t tt = rp->tt, type = tt & 0xFF;
-                if (type < PSIM_MSG_PT_BROADCAST) continue;
-                const uint32_t p = rp->src, msg = rp->a0, rnd = rp->a1;
-                if (type == PSIM_MSG_PT_IHAVE) {
-                    v[R_DIH]++;
-                    v[R_OVF] += sslots[msg % PSIM_MSG_SLOTS] != msg ? 1u : 0u;   // a retired id (pt_have)
-                    bool in = false;
-#pragma unroll
-                    for (int q = 0; q < 8; q++) in |= q < h.act_n && A[q] == p;
-                    if (in && p != id && p < a.n_nodes && (a.flags[p] & F_UP) && a.part[p] == me_part) {
-                        v[R_DIGEST] += relay_emit(a, D.w + seq, p, id, PSIM_MSG_PT_IGNORED_IHAVE, seq, msg, rnd, rp->a2, X);
-                        seq++;
-                        v[R_EIGN]++;
-                    } else {
-                        v[R_FAIL]++;
-                    }
-                } else {
-                    v[R_DIGN]++;
-                    const uint64_t key = ((uint64_t)(p | PSIM_MAP_BIT) << 32) | (msg << 16) | (rnd & 0xFFFFu);
-                    for (uint32_t e = 0; e < out_n; e++)
-                        if (!((gone >> e) & 1u) && (e < OUT_IN ? own[e] : ext[e - OUT_IN]) == key) {
-                            gone |= 1ull << e;
-                            break;
-                        }
-                }
-            }
-            if (gone) {                               // the acked entries out, order kept
-                uint32_t k = 0;
-                for (uint32_t e = 0; e < out_n; e++) {
-                    if ((gone >> e) & 1u) continue;
-                    if (k != e) {
-                        const uint64_t o = e < OUT_IN ? own[e] : ext[e - OUT_IN];
-                        (k < OUT_IN ? own[k] : ext[k - OUT_IN]) = o;
-                    }
-                    k++;
-                }
-                for (uint32_t e = k; e < out_n; e++) (e < OUT_IN ? own[e] : ext[e - OUT_IN]) = 0ull;
-                out_n = k;
-                reinterpret_cast<uint32_t*>(a.hdr + li)[11] = out_n << 16;   // Hdr word 11: out_n
-            }
-            // the lazy tick: an IHAVE per outstanding entry, in order (send_lazy
-            // pt:443-453) -- rows in chunks of 4 entries, two 16-B loads in flight
-            for (uint32_t i0 = 0; ((D.z >> 28) & DESC_LAZY) && i0 < out_n; i0 += 4) {
-                const uint4* orow = reinterpret_cast<const uint4*>(i0 < OUT_IN ? own + i0 : ext + (i0 - OUT_IN));
-                const uint4 q0 = orow[0], q1 = orow[1];
-                const uint64_t O[4] = {((uint64_t)q0.y << 32) | q0.x, ((uint64_t)q0.w << 32) | q0.z,
-                                       ((uint64_t)q1.y << 32) | q1.x, ((uint64_t)q1.w << 32) | q1.z};
-                bool in[4];
-#pragma unroll
-                for (int c = 0; c < 4; c++) {         // send/3: an existing connection (member of Active)
-                    const uint32_t p = (uint32_t)(O[c] >> 32) & ~PSIM_MAP_BIT;
-                    bool x = false;
-#pragma unroll
-                    for (int j = 0; j < 8; j++) x |= j < h.act_n && A[j] == p;
-                    in[c] = x && p != id && i0 + c < out_n;
-                }
-                for (int c = 0; c < 4 && i0 + c < out_n; c++) {
-                    const uint64_t o = O[c];
-                    const uint32_t p = (uint32_t)(o >> 32) & ~PSIM_MAP_BIT;
-                    if (!(in[c] && p < a.n_nodes && (a.flags[p] & F_UP) && a.part[p] == me_part)) {
-                        v[R_FAIL]++;
-                        continue;
-                    }
-                    // the message's root from its slot (a retired id: overflow, PSIM_NONE)
-                    const uint32_t msg = (uint32_t)(o >> 16) & 0xFFFFu, sk = msg % PSIM_MSG_SLOTS;
-                    const bool live = sslots[sk] == msg;
-                    v[R_OVF] += live ? 0u : 1u;
-                    v[R_DIGEST] += relay_emit(a, D.w + seq, p, id, PSIM_MSG_PT_IHAVE, seq, msg, (uint32_t)o & 0xFFFFu,
-                                              live ? sslots[PSIM_MSG_SLOTS + sk] : PSIM_NONE, X);
-                    seq++;
-                    v[R_IHAVE]++;
-                }
-            }
-        }
         if (rng != h.rng) a.hdr[li].rng = rng;
         a.ocnt[li] = seq;
         v[R_BOUND] += seq > oend - D.w ? 1u : 0u;
-        if (!to_pt) {                                 // (k_pt writes the byte of its nodes)
+        if (!to_pt) {                                 // (k_ptl / k_pt write the byte of their nodes)
             const uint8_t fl = a.flags[id];
-            a.flags[id] = (uint8_t)((fl & (F_UP | F_CRASHED)) | (out_n ? F_LAZY : 0) |
-                                    (min(out_n, 15u) << F_OUTN_SHIFT) |
+            a.flags[id] = (uint8_t)((fl & (F_UP | F_CRASHED)) | (h.out_n ? F_LAZY : 0) |
+                                    (min((uint32_t)h.out_n, 15u) << F_OUTN_SHIFT) |
                                     (h.act_n < a.min_active ? F_LOWACT : 0));
         }
     }
@@ -1983,11 +1889,8 @@ __global__ void __launch_bounds__(256) k_relay(RoundArgs) {
     uint64_t* row = kargs().stat_relay + (size_t)blockIdx.x * NST;
     for (uint32_t k = threadIdx.x; k < NST; k += blockDim.x)
         row[k] = k == ST_PROC ? sst[R_PROC] : k == ST_DELIV + PSIM_MSG_SHUFFLE ? sst[R_DELIV]
-               : k == ST_EMIT + PSIM_MSG_SHUFFLE ? sst[R_SHUF] : k == ST_EMIT + PSIM_MSG_PT_IHAVE ? sst[R_IHAVE]
-               : k == ST_FAIL ? sst[R_FAIL] : k == ST_DIGEST ? sst[R_DIGEST] : k == ST_OVF ? sst[R_OVF]
-               : k == ST_OVF_BY + PSIM_OVF_PT ? sst[R_OVF] : k == ST_BOUND ? sst[R_BOUND]
-               : k == ST_DELIV + PSIM_MSG_PT_IHAVE ? sst[R_DIH] : k == ST_DELIV + PSIM_MSG_PT_IGNORED_IHAVE ? sst[R_DIGN]
-               : k == ST_EMIT + PSIM_MSG_PT_IGNORED_IHAVE ? sst[R_EIGN] : 0ull;
+               : k == ST_EMIT + PSIM_MSG_SHUFFLE ? sst[R_SHUF] : k == ST_FAIL ? sst[R_FAIL]
+               : k == ST_DIGEST ? sst[R_DIGEST] : k == ST_BOUND ? sst[R_BOUND] : 0ull;
 }
 
 // ------------------------------------------------------ shuffle starts --
