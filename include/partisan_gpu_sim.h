@@ -64,7 +64,7 @@
 extern "C" {
 #endif
 
-#define PSIM_ABI_VERSION 6
+#define PSIM_ABI_VERSION 7
 
 /* error codes */
 #define PSIM_OK 0
@@ -114,7 +114,7 @@ enum psim_pl_msg_type {
 #define PSIM_STRATEGY_FULL 0       /* partisan_full_membership_strategy */
 #define PSIM_STRATEGY_SCAMP_V1 1   /* partisan_scamp_v1_membership_strategy */
 #define PSIM_STRATEGY_SCAMP_V2 2   /* partisan_scamp_v2_membership_strategy */
-#define PSIM_SVIEW_CAP 64          /* SCAMP membership / partial_view / in_view slots */
+#define PSIM_SVIEW_CAP 128         /* SCAMP membership / partial_view / in_view slots */
 
 /* Plumtree peer identities: an atom name is the bare node id; a node_spec
  * map (myself(), From, Root) has this bit set.  Erlang term order puts every
@@ -180,9 +180,9 @@ typedef struct psim_config {
     uint32_t manager;            /* PSIM_MANAGER_*, 0 = HyParView */
     uint32_t strategy;           /* PSIM_STRATEGY_* when manager = PLUGGABLE */
     uint32_t periodic_interval;  /* rounds; periodic_interval 10000 ms (partisan_config.erl:130) */
-    uint32_t scamp_c;            /* scamp_c, ?SCAMP_C_VALUE = 5 (partisan.hrl:31) */
+    uint32_t scamp_c;            /* scamp_c, ?SCAMP_C_VALUE = 5 (partisan.hrl:31); <= 64 */
     uint32_t fanout;             /* full: 0 = gossip to every member (reference);
-                                    k > 0 = k uniformly drawn members (config B extension) */
+                                    k > 0 = k uniformly drawn members (config B extension); <= 64 */
     uint32_t reserved[3];
 } psim_config;
 

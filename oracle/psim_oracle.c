@@ -1452,8 +1452,8 @@ int orc_create(const psim_config *cfg, struct psim_handle **out) {
         cfg->max_active_size > PSIM_ACTIVE_CAP || cfg->max_passive_size < 1 ||
         cfg->max_passive_size > 30 || 1 + cfg->k_active + cfg->k_passive > PSIM_EXCHANGE_CAP ||
         cfg->arwl > 255 || cfg->prwl > 255 || cfg->manager > PSIM_MANAGER_PLUGGABLE ||
-        cfg->strategy > PSIM_STRATEGY_SCAMP_V2 || cfg->scamp_c < 1 || cfg->scamp_c > PSIM_SVIEW_CAP ||
-        cfg->fanout > PSIM_SVIEW_CAP)
+        cfg->strategy > PSIM_STRATEGY_SCAMP_V2 || cfg->scamp_c < 1 || cfg->scamp_c > 64 ||
+        cfg->fanout > 64)
         return PSIM_EINVAL;
     int full = cfg->manager == PSIM_MANAGER_PLUGGABLE && cfg->strategy == PSIM_STRATEGY_FULL;
     if (full && cfg->shard_world > 1) return PSIM_EUNSUPPORTED;   /* payloads are shard-local */

@@ -8,14 +8,14 @@ import ctypes as C
 
 import numpy as np
 
-PSIM_ABI_VERSION = 6
+PSIM_ABI_VERSION = 7
 PSIM_MAP_BIT = 0x80000000
 PSIM_NONE = 0xFFFFFFFF
 ACTIVE_CAP, PASSIVE_CAP, IDMAP_CAP = 8, 32, 64
 PT_MEMBERS_CAP, PT_SET_POOL, PT_OUT_CAP, EXCHANGE_CAP = 8, 64, 64, 8
 PT_ROOTS, MSG_SLOTS = 4, 64
 NTYPES = 16
-SVIEW_CAP = 64
+SVIEW_CAP = 128
 MANAGER_HYPARVIEW, MANAGER_PLUGGABLE = 0, 1
 STRATEGY_FULL, STRATEGY_SCAMP_V1, STRATEGY_SCAMP_V2 = 0, 1, 2
 

@@ -2064,7 +2064,10 @@ __global__ void __launch_bounds__(256) k_shuf(RoundArgs) {
 // other node is appended to k_pt's list and runs there (the wave path).
 // Same handlers as pt_handle / pt_push / the lazy tick (pt:288-313, :341-345,
 // :368-453, :562-631): the same records, sequence numbers, digest, stats.
-constexpr int PTL_CAP = 16;
+#ifndef PSIM_PTL_CAP
+#define PSIM_PTL_CAP 16
+#endif
+constexpr int PTL_CAP = PSIM_PTL_CAP;
 
 constexpr uint32_t PTL_BLK = 128;   // k_ptl block: 2 waves, 32 KiB of per-lane tables
 
@@ -2176,7 +2179,10 @@ DEV void ptl_ack_out(PtLane& n, uint64_t key) {
     }
 }
 
-__global__ void __launch_bounds__(PTL_BLK) k_ptl(RoundArgs) {
+#ifndef PSIM_PTL_BLOCKS_PER_CU
+#define PSIM_PTL_BLOCKS_PER_CU 2
+#endif
+__global__ void __launch_bounds__(PTL_BLK, PSIM_PTL_BLOCKS_PER_CU) k_ptl(RoundArgs) {
     enum { T_FIRST, T_FAIL, T_OVF, T_BOUND, T_DLV, T_EMT = T_DLV + 5, T_N = T_EMT + 5 };
     __shared__ unsigned long long sst[T_N + 1];       // (+ the digest)
     __shared__ uint32_t sslots[2 * PSIM_MSG_SLOTS];

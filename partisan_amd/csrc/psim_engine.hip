@@ -609,8 +609,15 @@ __global__ void __launch_bounds__(256) k_node_prep(RoundArgs a, const unsigned l
                     b = a.fanout ? (uint64_t)c + a.fanout + 1
                                  : ((uint64_t)c + 2 + (leave ? 1 : 0)) * (a.n_nodes + 1);
                 else
-                    b = (uint64_t)c + (pending ? 2 + PSIM_SVIEW_CAP + a.scamp_c : 0) +
-                        (per ? 1 + PSIM_SVIEW_CAP : 0) + (leave ? PSIM_SVIEW_CAP : 0) + 1;
+                {
+                    // the view at round start, grown by at most one id per
+                    // inbox message (a kept subscription) and the contact:
+                    // join = contact + members + picks, periodic = a
+                    // resubscription + a ping per member, leave/1 (before
+                    // the inbox) = one per member, any message = one send
+                    const uint64_t vn = x.act_n, vg = vn + c + 1;
+                    b = (uint64_t)c + (pending ? 1 + 2 * vg : 0) + (per ? 1 + vg : 0) + (leave ? vn : 0) + 1;
+                }
                 w = c > 0 || (pending && !x.have) || per || leave;
             } else {
                 bool origin = a.origin[i] != 0;
@@ -1948,8 +1955,8 @@ int psim_create(const psim_config* cfg, psim_handle** out) {
         cfg->max_active_size > PSIM_ACTIVE_CAP || cfg->max_passive_size < 1 ||
         cfg->max_passive_size > 30 || 1 + cfg->k_active + cfg->k_passive > PSIM_EXCHANGE_CAP ||
         cfg->arwl > 255 || cfg->prwl > 255 || cfg->manager > PSIM_MANAGER_PLUGGABLE ||
-        cfg->strategy > PSIM_STRATEGY_SCAMP_V2 || cfg->scamp_c < 1 || cfg->scamp_c > PSIM_SVIEW_CAP ||
-        cfg->fanout > PSIM_SVIEW_CAP)
+        cfg->strategy > PSIM_STRATEGY_SCAMP_V2 || cfg->scamp_c < 1 || cfg->scamp_c > 64 ||
+        cfg->fanout > 64)   /* (picks land in one 64-lane register) */
         return PSIM_EINVAL;
     const bool full = cfg->manager == PSIM_MANAGER_PLUGGABLE && cfg->strategy == PSIM_STRATEGY_FULL;
     uint32_t world = std::max<uint32_t>(cfg->shard_world, 1);

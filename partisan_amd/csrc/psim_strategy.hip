@@ -29,17 +29,45 @@ constexpr int PL_WAVES = 4;        // waves per block
 constexpr uint32_t NONE = PSIM_NONE;
 constexpr uint64_t NONE64 = ~0ull;
 
+// A SCAMP list of up to PSIM_SVIEW_CAP = 128 ids in two registers: entry l
+// in lane l of `a`, entry 64 + l in lane l of `b` (entries past the count 0)
+static_assert(PSIM_SVIEW_CAP == 128, "a SCAMP list is two 64-lane registers");
+struct L2 { uint32_t a, b; };
+DEV bool has2(const L2& V, uint32_t n, uint32_t e) {
+    const uint32_t l = lane_id();
+    return (ballot(l < n && V.a == e) | ballot(64 + l < n && V.b == e)) != 0;
+}
+DEV uint32_t get2(const L2& V, uint32_t i) { return i < 64 ? rl(V.a, (int)i) : rl(V.b, (int)(i - 64)); }
+// insert e at position pos (entries from pos move up one)
+DEV void ins2(L2& V, uint32_t& n, uint32_t pos, uint32_t e) {
+    const uint32_t l = lane_id();
+    const uint32_t carry = rl(V.a, 63);
+    const uint32_t pa = from_prev(V.a);
+    uint32_t pb = from_prev(V.b);
+    pb = l == 0 ? carry : pb;
+    V.a = l < pos ? V.a : (l == pos ? e : (l <= n ? pa : 0u));
+    const uint32_t j = 64 + l;
+    V.b = j < pos ? V.b : (j == pos ? e : (j <= n ? pb : 0u));
+    n++;
+}
+// sets:add_element/2 in sets:to_list/1 order (after every entry of a bucket <= e's)
+DEV void add_set2(L2& V, uint32_t& n, uint32_t e) {
+    const uint32_t l = lane_id(), b = bucket16(e);
+    const uint32_t pos = popc(ballot(l < n && bucket16(V.a) <= b)) + popc(ballot(64 + l < n && bucket16(V.b) <= b));
+    ins2(V, n, pos, e);
+}
+
 // Hdr fields of a pluggable node (see RoundArgs): join_contact = pending
 // contact, aux = round of the last ping, have = hello sent,
 // act_n = view length, pas_n = in_view length.
 struct Pw {
     const RoundArgs* a;
-    uint32_t* lds;                 // 64 words of per-wave scratch
+    uint32_t* lds;                 // 128 words of per-wave scratch
     uint32_t me, li, mypart, round;
     Hdr h;
-    uint32_t V, I;                 // scamp: view / in_view, one id per lane
+    L2 V, I;                       // scamp: view / in_view, entries l and 64 + l in lane l
     uint32_t vn, in_n;
-    uint32_t CV, CF;               // connection cache: view ids at node start and
+    L2 CV, CF;                     // connection cache: view ids at node start and
                                    // flags | part << 8 of each
     uint32_t seq;
     uint64_t obase;
@@ -91,24 +119,29 @@ DEV uint32_t uniform_n(Pw& w, uint32_t n) {
 }
 
 // lists:sublist(shuffle(L), K) (sv1:263-269, sv2:345-350) over a list of up
-// to 64 ids: element l keys on counter rng + l; its rank among the (key, id)
-// pairs is its position after lists:sort; the first K land in OUT lanes 0..
-DEV uint32_t sublist(Pw& w, uint32_t V, uint32_t n, uint32_t k, uint32_t& OUT) {
-    uint32_t l = lane_id();
-    uint64_t base = w.h.rng;
-    if (base < w.dc_base || base + n - w.dc_base > 64) dc_fill(w, base);
-    uint32_t off = (uint32_t)(base - w.dc_base);
-    uint32_t src = (l + off) & 63;
-    uint32_t kl = shfl(w.DCL, (int)src), kh = shfl(w.DCH, (int)src);
-    uint64_t key = l < n ? ((((uint64_t)kh) << 32) | kl) >> 5 : ~0ull;
-    uint32_t m = n < k ? n : k;
-    uint32_t rank = 0;
-    for (uint32_t j = 0; j < n; j++) {
-        uint64_t kj = rl64(key, j);
-        uint32_t ej = rl(V, j);
-        rank += (kj < key || (kj == key && ej < V)) ? 1u : 0u;
+// to 128 ids: element j keys on counter rng + j (two draw-cache fills past 64
+// entries); its rank among the (key, id) pairs is its position after
+// lists:sort; the first K (<= 64) land in OUT lanes 0..
+DEV uint32_t sublist(Pw& w, const L2& V, uint32_t n, uint32_t k, uint32_t& OUT) {
+    const uint32_t l = lane_id();
+    const uint64_t base = w.h.rng;
+    dc_fill(w, base);
+    const uint64_t ka = l < n ? ((((uint64_t)w.DCH) << 32) | w.DCL) >> 5 : ~0ull;
+    uint64_t kb = ~0ull;
+    if (n > 64) {
+        dc_fill(w, base + 64);
+        kb = 64 + l < n ? ((((uint64_t)w.DCH) << 32) | w.DCL) >> 5 : ~0ull;
     }
-    if (l < n && rank < m) w.lds[rank] = V;
+    const uint32_t m = n < k ? n : k;
+    uint32_t ra = 0, rb = 0;
+    for (uint32_t j = 0; j < n; j++) {
+        const uint64_t kj = j < 64 ? rl64(ka, (int)j) : rl64(kb, (int)(j - 64));
+        const uint32_t ej = get2(V, j);
+        ra += (kj < ka || (kj == ka && ej < V.a)) ? 1u : 0u;
+        rb += (kj < kb || (kj == kb && ej < V.b)) ? 1u : 0u;
+    }
+    if (l < n && ra < m) w.lds[ra] = V.a;
+    if (64 + l < n && rb < m) w.lds[rb] = V.b;
     __builtin_amdgcn_wave_barrier();
     uint32_t got = l < m ? w.lds[l] : 0u;
     __builtin_amdgcn_wave_barrier();
@@ -139,9 +172,9 @@ DEV void emit(Pw& w, uint32_t dst, uint32_t type, uint32_t a0, uint32_t slot) {
 // partition separates the two; view members answer from the cache
 DEV bool connect_ok(const Pw& w, uint32_t dst) {
     if (dst >= kargs().n_nodes || dst == w.me) return false;
-    uint64_t m = ballot(w.CV == dst);
-    uint32_t v = m ? rl(w.CF, ffs64(m))
-                   : ((uint32_t)kargs().flags[dst] | ((uint32_t)kargs().part[dst] << 8));
+    const uint64_t ma = ballot(w.CV.a == dst), mb = ballot(w.CV.b == dst);
+    uint32_t v = ma ? rl(w.CF.a, ffs64(ma)) : mb ? rl(w.CF.b, ffs64(mb))
+               : ((uint32_t)kargs().flags[dst] | ((uint32_t)kargs().part[dst] << 8));
     return (v & F_UP) && (v >> 8) == w.mypart;
 }
 
@@ -150,7 +183,7 @@ DEV bool connect_ok(const Pw& w, uint32_t dst) {
 // read from its own member row), so only SCAMP needs the check.
 DEV bool connected(const Pw& w, uint32_t p) {
     if (kargs().strategy == PSIM_STRATEGY_FULL) return true;
-    return ballot(lane_id() < w.vn && w.V == p) != 0 || p == w.h.join_contact;
+    return has2(w.V, w.vn, p) || p == w.h.join_contact;
 }
 
 // ---------------------------------------------------- omission faults --
@@ -328,43 +361,45 @@ DEV void full_gossip(Pw& w, uint32_t extra = NONE) {
 
 // --------------------------------------------------------------- scamp --
 // sets:add_element/2 (v1, sets:to_list order) or [E | L] (v2) into a fixed table
-DEV void scamp_add(Pw& w, uint32_t& L, uint32_t& n, uint32_t e, bool as_set) {
-    if (as_set && has(L, n, e)) return;
+DEV void scamp_add(Pw& w, L2& L, uint32_t& n, uint32_t e, bool as_set) {
+    if (as_set && has2(L, n, e)) return;
     if (n >= PSIM_SVIEW_CAP) { ovf(w, PSIM_OVF_STRATEGY); return; }
-    if (as_set) view_add(L, n, e);
-    else vins(L, n, 0, e);
+    if (as_set) add_set2(L, n, e);
+    else ins2(L, n, 0, e);
 }
 
 // Strategy:join/3 at the joiner (sv1:52-99, sv2:64-113)
 DEV void scamp_join(Pw& w, uint32_t contact) {
     const bool v1 = kargs().strategy == PSIM_STRATEGY_SCAMP_V1;
-    const uint32_t M0 = w.V, n0 = w.vn;
+    const L2 M0 = w.V;
+    const uint32_t n0 = w.vn;
     scamp_add(w, w.V, w.vn, contact, v1);
     uint32_t SEL = 0;
     uint32_t ns = sublist(w, M0, n0, v1 ? kargs().scamp_c : kargs().scamp_c - 1, SEL);
     pl_send(w, contact, PSIM_PL_FWD_SUB, w.me, NONE);
     for (uint32_t i = 0; i < n0; i++)            // v1: sets:fold/3 = reverse of to_list
-        pl_send(w, rl(M0, v1 ? n0 - 1 - i : i), PSIM_PL_FWD_SUB, contact, NONE);
+        pl_send(w, get2(M0, v1 ? n0 - 1 - i : i), PSIM_PL_FWD_SUB, contact, NONE);
     for (uint32_t i = 0; i < ns; i++) pl_send(w, rl(SEL, i), PSIM_PL_FWD_SUB, contact, NONE);
 }
 
 // periodic/1 (sv1:125-174, sv2:130-178); "isolated" = a ping was received
 // and not this round (App. A Q12: 100000 us against 1-s rounds)
 DEV void scamp_periodic(Pw& w) {
-    const uint32_t M = w.V, n = w.vn;
+    const L2 M = w.V;
+    const uint32_t n = w.vn;
     const bool isolated = w.h.aux != NONE && w.round > w.h.aux;
     if (isolated) {
         uint32_t SEL = 0;
         if (sublist(w, M, n, 1, SEL)) pl_send(w, rl(SEL, 0), PSIM_PL_FWD_SUB, w.me, NONE);
     }
-    for (uint32_t i = 0; i < n; i++) pl_send(w, rl(M, i), PSIM_PL_PING, w.me, NONE);
+    for (uint32_t i = 0; i < n; i++) pl_send(w, get2(M, i), PSIM_PL_PING, w.me, NONE);
 }
 
 // handle_message(.., {forward_subscription, Node}) (sv1:212-252, sv2:284-327)
 DEV void scamp_fwd(Pw& w, uint32_t node) {
     const bool v1 = kargs().strategy == PSIM_STRATEGY_SCAMP_V1;
     const uint32_t rnd = uniform_n(w, 10) >= 5 ? 1u : 0u;    // random_0_or_1/0 sv1:272-279
-    if (rnd == 0 && !has(w.V, w.vn, node)) {
+    if (rnd == 0 && !has2(w.V, w.vn, node)) {
         scamp_add(w, w.V, w.vn, node, v1);
         if (!v1) pl_send(w, node, PSIM_PL_KEEP_SUB, w.me, NONE);
         return;
@@ -379,20 +414,23 @@ DEV void scamp_fwd(Pw& w, uint32_t node) {
 // {bootstrap_remove_subscription, t} to the partial view, state unchanged
 DEV void scamp_leave(Pw& w, uint32_t t) {
     const bool v1 = kargs().strategy == PSIM_STRATEGY_SCAMP_V1;
-    const uint32_t M0 = w.V, n0 = w.vn;
+    const L2 M0 = w.V;
+    const uint32_t n0 = w.vn;
     // the connections to the old members stay open (closed only on 'EXIT',
     // pl:971-984): the sends are judged on the old view
     for (uint32_t i = 0; i < n0; i++)
-        pl_send(w, rl(M0, i), v1 ? PSIM_PL_REMOVE_SUB : PSIM_PL_BOOT_REMOVE, t, NONE);
+        pl_send(w, get2(M0, i), v1 ? PSIM_PL_REMOVE_SUB : PSIM_PL_BOOT_REMOVE, t, NONE);
     if (v1) {
         const uint32_t l = lane_id();
-        const bool keep = l < w.vn && w.V != t;
-        const uint64_t km = ballot(keep);
-        const uint32_t pos = __popcll(km & ((1ull << l) - 1));
-        if (keep) w.lds[pos] = w.V;
+        const bool keep_a = l < w.vn && w.V.a != t, keep_b = 64 + l < w.vn && w.V.b != t;
+        const uint64_t ma = ballot(keep_a), mb = ballot(keep_b);
+        const uint32_t ca = (uint32_t)__popcll(ma);
+        if (keep_a) w.lds[__popcll(ma & ((1ull << l) - 1))] = w.V.a;
+        if (keep_b) w.lds[ca + __popcll(mb & ((1ull << l) - 1))] = w.V.b;
         __builtin_amdgcn_wave_barrier();
-        const uint32_t k = (uint32_t)__popcll(km);
-        w.V = l < k ? w.lds[l] : 0u;
+        const uint32_t k = ca + (uint32_t)__popcll(mb);
+        w.V.a = l < k ? w.lds[l] : 0u;
+        w.V.b = 64 + l < k ? w.lds[64 + l] : 0u;
         __builtin_amdgcn_wave_barrier();
         w.vn = k;
     }
@@ -459,7 +497,7 @@ DEV void pl_handle(Pw& w, uint32_t type, uint32_t src, uint32_t a0, uint32_t slo
         break;
     case PSIM_PL_REMOVE_SUB:       // sv1:190-211: a member Node hits the swapped
                                    // sets:del_element/2 arguments (App. A Q12): crash
-        if (kargs().strategy == PSIM_STRATEGY_SCAMP_V1 && has(w.V, w.vn, a0)) w.stop = true;
+        if (kargs().strategy == PSIM_STRATEGY_SCAMP_V1 && has2(w.V, w.vn, a0)) w.stop = true;
         break;
     case PSIM_PL_BOOT_REMOVE:      // sv2:192-238: Node itself stops before its casts
                                    // go out (lists:nth(0, ..), or the self-less reset, pl:1182-1188)
@@ -497,11 +535,18 @@ DEV void process_pl(Pw& w, uint32_t n, uint32_t ib, uint32_t ik, uint32_t ob) {
     st_add(w, ST_PROC, 1);
     const bool full = a.strategy == PSIM_STRATEGY_FULL;
     w.vn = w.h.act_n; w.in_n = w.h.pas_n;
-    w.V = full ? 0u : a.sview[(size_t)li * PSIM_SVIEW_CAP + l];
-    w.I = a.strategy == PSIM_STRATEGY_SCAMP_V2 ? a.sinv[(size_t)li * PSIM_SVIEW_CAP + l] : 0u;
-    const uint32_t V0 = w.V, I0 = w.I;
-    w.CV = l < w.vn ? w.V : NONE;
-    w.CF = w.CV < a.n_nodes ? ((uint32_t)a.flags[w.CV] | ((uint32_t)a.part[w.CV] << 8)) : 0u;
+    const uint32_t* vrow = a.sview + (size_t)li * PSIM_SVIEW_CAP;
+    const uint32_t* irow = a.sinv + (size_t)li * PSIM_SVIEW_CAP;
+    w.V.a = full ? 0u : vrow[l];
+    w.V.b = full || w.vn <= 64 ? 0u : vrow[64 + l];
+    const bool v2 = a.strategy == PSIM_STRATEGY_SCAMP_V2;
+    w.I.a = v2 ? irow[l] : 0u;
+    w.I.b = v2 && w.in_n > 64 ? irow[64 + l] : 0u;
+    const L2 V0 = w.V, I0 = w.I;
+    w.CV.a = l < w.vn ? w.V.a : NONE;
+    w.CV.b = 64 + l < w.vn ? w.V.b : NONE;
+    w.CF.a = w.CV.a < a.n_nodes ? ((uint32_t)a.flags[w.CV.a] | ((uint32_t)a.part[w.CV.a] << 8)) : 0u;
+    w.CF.b = w.CV.b < a.n_nodes ? ((uint32_t)a.flags[w.CV.b] | ((uint32_t)a.part[w.CV.b] << 8)) : 0u;
     w.row = full ? a.fbits + (size_t)li * 2 * a.fw : nullptr;
     w.seq = 0; w.obase = ob;
     w.snap = NONE; w.dirty = false; w.gossip_due = false;
@@ -566,9 +611,10 @@ DEV void process_pl(Pw& w, uint32_t n, uint32_t ib, uint32_t ik, uint32_t ob) {
 
     // ---- write back
     w.h.act_n = (uint8_t)w.vn; w.h.pas_n = (uint8_t)w.in_n;
-    if (!full && ballot(w.V != V0)) a.sview[(size_t)li * PSIM_SVIEW_CAP + l] = w.V;
-    if (a.strategy == PSIM_STRATEGY_SCAMP_V2 && ballot(w.I != I0))
-        a.sinv[(size_t)li * PSIM_SVIEW_CAP + l] = w.I;
+    if (!full && ballot(w.V.a != V0.a)) a.sview[(size_t)li * PSIM_SVIEW_CAP + l] = w.V.a;
+    if (!full && ballot(w.V.b != V0.b)) a.sview[(size_t)li * PSIM_SVIEW_CAP + 64 + l] = w.V.b;
+    if (v2 && ballot(w.I.a != I0.a)) a.sinv[(size_t)li * PSIM_SVIEW_CAP + l] = w.I.a;
+    if (v2 && ballot(w.I.b != I0.b)) a.sinv[(size_t)li * PSIM_SVIEW_CAP + 64 + l] = w.I.b;
     {
         const uint32_t* hw = reinterpret_cast<const uint32_t*>(&w.h);
         uint32_t v = 0;
@@ -583,7 +629,7 @@ DEV void process_pl(Pw& w, uint32_t n, uint32_t ib, uint32_t ik, uint32_t ob) {
 
 __global__ void __launch_bounds__(256) k_consume_pl(RoundArgs args) {
     __shared__ uint64_t sst[NST];
-    __shared__ uint32_t scratch[PL_WAVES][64];
+    __shared__ uint32_t scratch[PL_WAVES][128];
     for (int i = threadIdx.x; i < NST; i += blockDim.x) sst[i] = 0;
     if (threadIdx.x == 0) atomicMin(&kargs().ktime[0], (unsigned long long)__builtin_amdgcn_s_memrealtime());
     __syncthreads();
