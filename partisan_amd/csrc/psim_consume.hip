@@ -2206,7 +2206,7 @@ __global__ void __launch_bounds__(PTL_BLK, PSIM_PTL_BLOCKS_PER_CU) k_ptl(RoundAr
         const uint32_t P = base + threadIdx.x;
         bool go = false, fall = false;
         uint4 D = make_uint4(0, 0, 0, 0);
-        uint32_t root0 = NONE, rtw4 = 0, rtw5 = 0, w10 = 0, w11 = 0, start = 0, act_n = 0;
+        uint32_t root0 = NONE, rtw4 = 0, rtw5 = 0, w10 = 0, w11 = 0, start = 0, act_n = 0, tmask = 0;
         if (P < nq) {
             D = a.desc_ptl[P];
             const size_t li = D.x - a.lo;
@@ -2231,6 +2231,7 @@ __global__ void __launch_bounds__(PTL_BLK, PSIM_PTL_BLOCKS_PER_CU) k_ptl(RoundAr
                 const uint32_t type = m.tt & 0xFF;
                 if (type < PSIM_MSG_PT_BROADCAST || type > PSIM_MSG_PT_GRAFT) continue;
                 npt++;
+                tmask |= 1u << type;
                 if (type == PSIM_MSG_PT_BROADCAST) bm |= 1ull << (m.a0 % PSIM_MSG_SLOTS);
                 if (type != PSIM_MSG_PT_IGNORED_IHAVE) {
                     if (r0t == NONE) r0t = m.a2;      // the root a first update would store
@@ -2263,16 +2264,24 @@ __global__ void __launch_bounds__(PTL_BLK, PSIM_PTL_BLOCKS_PER_CU) k_ptl(RoundAr
         n.root0 = root0;
         n.ne = root0 == NONE ? 0u : (rtw4 & 0xFF);
         n.nl = root0 == NONE ? 0u : (rtw5 & 0xFF);
-        {
+        // the sets only for messages that may update them, the table only for
+        // lazy adds, acks or a lazy tick (the rest is never read, nor stored)
+        const bool need_sets = (tmask & ((1u << PSIM_MSG_PT_BROADCAST) | (1u << PSIM_MSG_PT_PRUNE) |
+                                         (1u << PSIM_MSG_PT_IHAVE) | (1u << PSIM_MSG_PT_GRAFT))) != 0;
+        const bool need_out = (tmask & ((1u << PSIM_MSG_PT_BROADCAST) | (1u << PSIM_MSG_PT_IGNORED_IHAVE))) != 0 ||
+                              (((D.z >> 28) & DESC_LAZY) && ((w11 >> 16) & 0xFF) > 0);
+        if (need_sets) {
             const uint4* er = reinterpret_cast<const uint4*>(a.pt_eag + li * RT_SET);
             const uint4* lr = reinterpret_cast<const uint4*>(a.pt_laz + li * RT_SET);
-            const uint4* orow = reinterpret_cast<const uint4*>(a.pt_out + li * OUT_IN);
 #pragma unroll
             for (int q = 0; q < PTL_CAP / 4; q++) {
                 const uint4 e = er[q], z = lr[q];
                 n.EG[4 * q] = e.x; n.EG[4 * q + 1] = e.y; n.EG[4 * q + 2] = e.z; n.EG[4 * q + 3] = e.w;
                 n.LZ[4 * q] = z.x; n.LZ[4 * q + 1] = z.y; n.LZ[4 * q + 2] = z.z; n.LZ[4 * q + 3] = z.w;
             }
+        }
+        if (need_out) {
+            const uint4* orow = reinterpret_cast<const uint4*>(a.pt_out + li * OUT_IN);
 #pragma unroll
             for (int q = 0; q < PTL_CAP / 2; q++) {
                 const uint4 o = orow[q];
