@@ -2067,7 +2067,11 @@ __global__ void __launch_bounds__(256) k_shuf(RoundArgs) {
 #ifndef PSIM_PTL_CAP
 #define PSIM_PTL_CAP 16
 #endif
-constexpr int PTL_CAP = PSIM_PTL_CAP;
+#ifndef PSIM_PTL_SET_CAP
+#define PSIM_PTL_SET_CAP 16
+#endif
+constexpr int PTL_CAP = PSIM_PTL_CAP;           // outstanding entries a lane holds
+constexpr int PTL_SET = PSIM_PTL_SET_CAP;       // eager / lazy entries a lane holds
 
 constexpr uint32_t PTL_BLK = 128;   // k_ptl block: 2 waves, 32 KiB of per-lane tables
 
@@ -2080,7 +2084,7 @@ struct LdsCol {
 DEV bool col_has(const LdsCol& V, uint32_t n, uint32_t x) {
     bool r = false;
 #pragma unroll
-    for (int i = 0; i < PTL_CAP; i++) r |= (uint32_t)i < n && V[i] == x;
+    for (int i = 0; i < PTL_SET; i++) r |= (uint32_t)i < n && V[i] == x;
     return r;
 }
 // ordsets:del_element/2
@@ -2139,7 +2143,7 @@ DEV void ptl_update(KArgs& a, PtLane& n, size_t li, uint32_t com_n, uint32_t fro
         const uint4 c0 = cr[0], c1 = cr[1];
         const uint32_t C8[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
 #pragma unroll
-        for (int i = 0; i < PTL_CAP; i++) { n.EG[i] = i < 8 && (uint32_t)i < com_n ? C8[i & 7] : 0u; n.LZ[i] = 0u; }
+        for (int i = 0; i < PTL_SET; i++) { n.EG[i] = i < 8 && (uint32_t)i < com_n ? C8[i & 7] : 0u; n.LZ[i] = 0u; }
         n.ne = com_n; n.nl = 0;
     }
     if (to_eager) {
@@ -2187,7 +2191,7 @@ __global__ void __launch_bounds__(PTL_BLK, PSIM_PTL_BLOCKS_PER_CU) k_ptl(RoundAr
     __shared__ unsigned long long sst[T_N + 1];       // (+ the digest)
     __shared__ uint32_t sslots[2 * PSIM_MSG_SLOTS];
     __shared__ uint32_t wcnt[5];
-    __shared__ uint32_t tabs[4 * PTL_CAP * PTL_BLK];
+    __shared__ uint32_t tabs[(2 * PTL_SET + 2 * PTL_CAP) * PTL_BLK];
     for (int i = threadIdx.x; i < 2 * PSIM_MSG_SLOTS; i += blockDim.x) sslots[i] = kargs().slots[i];
     if (threadIdx.x < T_N + 1) sst[threadIdx.x] = 0;
     __syncthreads();
@@ -2198,9 +2202,9 @@ __global__ void __launch_bounds__(PTL_BLK, PSIM_PTL_BLOCKS_PER_CU) k_ptl(RoundAr
     const uint32_t X0[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     PtLane n;
     n.EG.p = tabs + threadIdx.x;
-    n.LZ.p = tabs + PTL_CAP * PTL_BLK + threadIdx.x;
-    n.OL.p = tabs + 2 * PTL_CAP * PTL_BLK + threadIdx.x;
-    n.OH.p = tabs + 3 * PTL_CAP * PTL_BLK + threadIdx.x;
+    n.LZ.p = tabs + PTL_SET * PTL_BLK + threadIdx.x;
+    n.OL.p = tabs + 2 * PTL_SET * PTL_BLK + threadIdx.x;
+    n.OH.p = tabs + (2 * PTL_SET + PTL_CAP) * PTL_BLK + threadIdx.x;
     for (uint32_t base = blockIdx.x * blockDim.x; base < nq; base += gridDim.x * blockDim.x) {
         KArgs& a = kargs();
         const uint32_t P = base + threadIdx.x;
@@ -2227,22 +2231,23 @@ __global__ void __launch_bounds__(PTL_BLK, PSIM_PTL_BLOCKS_PER_CU) k_ptl(RoundAr
             bool ok = r0.y == NONE && r0.z == NONE && r0.w == NONE &&
                       (root0 == NONE || ((rtw4 >> 8) == 0 && (rtw5 >> 8) == 0));
             for (uint32_t j = 0; ok && j < ik; j++) {
-                const Msg& m = a.rec_in[D.y + j];
-                const uint32_t type = m.tt & 0xFF;
+                const uint4* rq = reinterpret_cast<const uint4*>(a.rec_in + D.y + j);
+                const uint4 q0 = rq[0], q1 = rq[1];
+                const uint32_t type = q0.z & 0xFF;
                 if (type < PSIM_MSG_PT_BROADCAST || type > PSIM_MSG_PT_GRAFT) continue;
                 npt++;
                 tmask |= 1u << type;
-                if (type == PSIM_MSG_PT_BROADCAST) bm |= 1ull << (m.a0 % PSIM_MSG_SLOTS);
+                if (type == PSIM_MSG_PT_BROADCAST) bm |= 1ull << (q1.x % PSIM_MSG_SLOTS);
                 if (type != PSIM_MSG_PT_IGNORED_IHAVE) {
-                    if (r0t == NONE) r0t = m.a2;      // the root a first update would store
-                    ok &= m.a2 == r0t;
+                    if (r0t == NONE) r0t = q1.z;      // the root a first update would store
+                    ok &= q1.z == r0t;
                 }
             }
             // first deliveries (lazy adds): the BROADCASTs' slots not delivered yet
             const uint32_t nb = popc(bm & ~(((uint64_t)hq1.y << 32) | hq1.z));
             const uint32_t com_n = w10 >> 24, out_n = (w11 >> 16) & 0xFF;
             const uint32_t ne0 = root0 == NONE ? com_n : (rtw4 & 0xFF), nl0 = root0 == NONE ? 0u : (rtw5 & 0xFF);
-            ok &= ne0 + npt <= (uint32_t)PTL_CAP && nl0 + npt <= (uint32_t)PTL_CAP &&
+            ok &= ne0 + npt <= (uint32_t)PTL_SET && nl0 + npt <= (uint32_t)PTL_SET &&
                   out_n + nb * (nl0 + npt) <= (uint32_t)PTL_CAP;
             go = ok;
             fall = !ok;
@@ -2274,7 +2279,7 @@ __global__ void __launch_bounds__(PTL_BLK, PSIM_PTL_BLOCKS_PER_CU) k_ptl(RoundAr
             const uint4* er = reinterpret_cast<const uint4*>(a.pt_eag + li * RT_SET);
             const uint4* lr = reinterpret_cast<const uint4*>(a.pt_laz + li * RT_SET);
 #pragma unroll
-            for (int q = 0; q < PTL_CAP / 4; q++) {
+            for (int q = 0; q < PTL_SET / 4; q++) {
                 const uint4 e = er[q], z = lr[q];
                 n.EG[4 * q] = e.x; n.EG[4 * q + 1] = e.y; n.EG[4 * q + 2] = e.z; n.EG[4 * q + 3] = e.w;
                 n.LZ[4 * q] = z.x; n.LZ[4 * q + 1] = z.y; n.LZ[4 * q + 2] = z.z; n.LZ[4 * q + 3] = z.w;
@@ -2298,10 +2303,13 @@ __global__ void __launch_bounds__(PTL_BLK, PSIM_PTL_BLOCKS_PER_CU) k_ptl(RoundAr
         const uint32_t oend = (uint32_t)a.obase[li + 1];
         const uint32_t ik = start == a.round ? 0u : (D.z & DESC_CNT_MASK);
         for (uint32_t j = 0; j < ik; j++) {           // the Plumtree inbox, canonical order
-            const Msg* rp = a.rec_in + D.y + j;
-            const uint32_t type = rp->tt & 0xFF;
+            // (the record's first 32 B as two 16-B loads: field-wise reads were
+            // re-issued per branch, 40 more VGPRs)
+            const uint4* rq = reinterpret_cast<const uint4*>(a.rec_in + D.y + j);
+            const uint4 q0 = rq[0], q1 = rq[1];
+            const uint32_t type = q0.z & 0xFF;
             if (type < PSIM_MSG_PT_BROADCAST || type > PSIM_MSG_PT_GRAFT) continue;
-            const uint32_t src = rp->src, msg = rp->a0, rnd = rp->a1, root = rp->a2, from = src | PSIM_MAP_BIT;
+            const uint32_t src = q0.y, msg = q1.x, rnd = q1.y, root = q1.z, from = src | PSIM_MAP_BIT;
             v[T_DLV + type - PSIM_MSG_PT_BROADCAST]++;
             // plumtree_backend is_stale/1 over the slots (a retired id: overflow, stale)
             const uint32_t sk = msg % PSIM_MSG_SLOTS;
@@ -2385,7 +2393,7 @@ __global__ void __launch_bounds__(PTL_BLK, PSIM_PTL_BLOCKS_PER_CU) k_ptl(RoundAr
             uint4* er = reinterpret_cast<uint4*>(a.pt_eag + li * RT_SET);
             uint4* lr = reinterpret_cast<uint4*>(a.pt_laz + li * RT_SET);
 #pragma unroll
-            for (int q = 0; q < PTL_CAP / 4; q++) {
+            for (int q = 0; q < PTL_SET / 4; q++) {
                 er[q] = make_uint4(n.EG[4 * q], n.EG[4 * q + 1], n.EG[4 * q + 2], n.EG[4 * q + 3]);
                 lr[q] = make_uint4(n.LZ[4 * q], n.LZ[4 * q + 1], n.LZ[4 * q + 2], n.LZ[4 * q + 3]);
             }
