@@ -1433,7 +1433,7 @@ DEV void writeback_lite(Wv& w) {
 }
 
 #ifndef PSIM_LITE_WAVES
-#define PSIM_LITE_WAVES 6
+#define PSIM_LITE_WAVES 8
 #endif
 __global__ void __launch_bounds__(256, PSIM_LITE_WAVES) k_consume_lite(RoundArgs args) {
     __shared__ uint64_t sst[NST];
@@ -1779,14 +1779,22 @@ __global__ void __launch_bounds__(256, PSIM_RELAY_WAVES) k_relay(RoundArgs) {
             // SHUFFLE with TTL left (a relay while |active| > 1)
             uint32_t hvn = 0;
             bool all_relay = true, all_shuf = true;
-            for (uint32_t j = 0; j < ik; j++) {
-                const Msg& m = a.rec_in[D.y + j];
-                const uint32_t tt = m.tt, type = tt & 0xFF;
-                if (type < PSIM_MSG_PT_BROADCAST) {
-                    hvn++;
-                    maps |= type <= PSIM_MSG_NEIGHBOR_ACCEPTED;   // id maps (hv:703-1089)
-                    all_relay &= type == PSIM_MSG_SHUFFLE && ((tt >> 8) & 0xFF) > 0;
-                    all_shuf &= type == PSIM_MSG_SHUFFLE || type == PSIM_MSG_SHUFFLE_REPLY;
+            // (four type words issued before any is waited on: a loop of
+            // single loads waits one memory latency per record)
+            for (uint32_t j = 0; j < ik; j += 4) {
+                uint32_t T[4];
+#pragma unroll
+                for (int q = 0; q < 4; q++)
+                    T[q] = j + q < ik ? a.rec_in[D.y + j + q].tt : (uint32_t)PSIM_MSG_PT_BROADCAST;
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const uint32_t tt = T[q], type = tt & 0xFF;
+                    if (type < PSIM_MSG_PT_BROADCAST) {
+                        hvn++;
+                        maps |= type <= PSIM_MSG_NEIGHBOR_ACCEPTED;   // id maps (hv:703-1089)
+                        all_relay &= type == PSIM_MSG_SHUFFLE && ((tt >> 8) & 0xFF) > 0;
+                        all_shuf &= type == PSIM_MSG_SHUFFLE || type == PSIM_MSG_SHUFFLE_REPLY;
+                    }
                 }
             }
             const bool fresh = h.start_round == a.round;
@@ -2224,7 +2232,11 @@ __global__ void __launch_bounds__(PTL_BLK, PSIM_PTL_BLOCKS_PER_CU) k_ptl(RoundAr
             root0 = r0.x; rtw4 = r1.x; rtw5 = r1.y;
             // the lane's preconditions over the inbox's Plumtree messages
             const uint32_t ik = start == a.round ? 0u : (D.z & DESC_CNT_MASK);
-            uint32_t npt = 0, r0t = root0;
+            // eager / lazy adds this inbox can make: a BROADCAST adds its
+            // sender to one of them (first delivery: eager, else lazy), an
+            // IHAVE of a missing id and a GRAFT to eager, a PRUNE to lazy
+            // (plumtree:288-313; an IGNORED_I_HAVE to neither)
+            uint32_t n_eg = 0, n_lz = 0, r0t = root0;
             uint64_t bm = 0;                          // message slots of the BROADCASTs
             // (an outstanding extension row taken earlier holds zeros while the
             // table fits its own row: this round's adds must fit that row)
@@ -2235,7 +2247,8 @@ __global__ void __launch_bounds__(PTL_BLK, PSIM_PTL_BLOCKS_PER_CU) k_ptl(RoundAr
                 const uint4 q0 = rq[0], q1 = rq[1];
                 const uint32_t type = q0.z & 0xFF;
                 if (type < PSIM_MSG_PT_BROADCAST || type > PSIM_MSG_PT_GRAFT) continue;
-                npt++;
+                n_eg += type == PSIM_MSG_PT_BROADCAST || type == PSIM_MSG_PT_IHAVE || type == PSIM_MSG_PT_GRAFT;
+                n_lz += type == PSIM_MSG_PT_BROADCAST || type == PSIM_MSG_PT_PRUNE;
                 tmask |= 1u << type;
                 if (type == PSIM_MSG_PT_BROADCAST) bm |= 1ull << (q1.x % PSIM_MSG_SLOTS);
                 if (type != PSIM_MSG_PT_IGNORED_IHAVE) {
@@ -2247,8 +2260,8 @@ __global__ void __launch_bounds__(PTL_BLK, PSIM_PTL_BLOCKS_PER_CU) k_ptl(RoundAr
             const uint32_t nb = popc(bm & ~(((uint64_t)hq1.y << 32) | hq1.z));
             const uint32_t com_n = w10 >> 24, out_n = (w11 >> 16) & 0xFF;
             const uint32_t ne0 = root0 == NONE ? com_n : (rtw4 & 0xFF), nl0 = root0 == NONE ? 0u : (rtw5 & 0xFF);
-            ok &= ne0 + npt <= (uint32_t)PTL_SET && nl0 + npt <= (uint32_t)PTL_SET &&
-                  out_n + nb * (nl0 + npt) <= (uint32_t)PTL_CAP;
+            ok &= ne0 + n_eg <= (uint32_t)PTL_SET && nl0 + n_lz <= (uint32_t)PTL_SET &&
+                  out_n + nb * (nl0 + n_lz) <= (uint32_t)PTL_CAP;
             go = ok;
             fall = !ok;
         }
