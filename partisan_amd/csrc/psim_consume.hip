@@ -1433,7 +1433,7 @@ DEV void writeback_lite(Wv& w) {
 }
 
 #ifndef PSIM_LITE_WAVES
-#define PSIM_LITE_WAVES 8
+#define PSIM_LITE_WAVES 6
 #endif
 __global__ void __launch_bounds__(256, PSIM_LITE_WAVES) k_consume_lite(RoundArgs args) {
     __shared__ uint64_t sst[NST];
@@ -2081,7 +2081,7 @@ __global__ void __launch_bounds__(256) k_shuf(RoundArgs) {
 constexpr int PTL_CAP = PSIM_PTL_CAP;           // outstanding entries a lane holds
 constexpr int PTL_SET = PSIM_PTL_SET_CAP;       // eager / lazy entries a lane holds
 
-constexpr uint32_t PTL_BLK = 128;   // k_ptl block: 2 waves, 32 KiB of per-lane tables
+constexpr uint32_t PTL_BLK = PTL_BLOCK;   // k_ptl block: one wave, 16 KiB of per-lane tables
 
 // A lane's tables in LDS, entry i of lane t at row i, column t (conflict-free):
 // unrolled scans read fixed offsets, run-time indexing is one access
@@ -2192,7 +2192,7 @@ DEV void ptl_ack_out(PtLane& n, uint64_t key) {
 }
 
 #ifndef PSIM_PTL_BLOCKS_PER_CU
-#define PSIM_PTL_BLOCKS_PER_CU 2
+#define PSIM_PTL_BLOCKS_PER_CU 3
 #endif
 __global__ void __launch_bounds__(PTL_BLK, PSIM_PTL_BLOCKS_PER_CU) k_ptl(RoundArgs) {
     enum { T_FIRST, T_FAIL, T_OVF, T_BOUND, T_DLV, T_EMT = T_DLV + 5, T_N = T_EMT + 5 };
@@ -2292,10 +2292,12 @@ __global__ void __launch_bounds__(PTL_BLK, PSIM_PTL_BLOCKS_PER_CU) k_ptl(RoundAr
             const uint4* er = reinterpret_cast<const uint4*>(a.pt_eag + li * RT_SET);
             const uint4* lr = reinterpret_cast<const uint4*>(a.pt_laz + li * RT_SET);
 #pragma unroll
-            for (int q = 0; q < PTL_SET / 4; q++) {
+            for (int q = 0; q < (PTL_SET + 3) / 4; q++) {  // (a capacity not a multiple of 4: the tail quad's first words)
                 const uint4 e = er[q], z = lr[q];
-                n.EG[4 * q] = e.x; n.EG[4 * q + 1] = e.y; n.EG[4 * q + 2] = e.z; n.EG[4 * q + 3] = e.w;
-                n.LZ[4 * q] = z.x; n.LZ[4 * q + 1] = z.y; n.LZ[4 * q + 2] = z.z; n.LZ[4 * q + 3] = z.w;
+                const uint32_t E4[4] = {e.x, e.y, e.z, e.w}, Z4[4] = {z.x, z.y, z.z, z.w};
+#pragma unroll
+                for (int k = 0; k < 4; k++)
+                    if (4 * q + k < PTL_SET) { n.EG[4 * q + k] = E4[k]; n.LZ[4 * q + k] = Z4[k]; }
             }
         }
         if (need_out) {
@@ -2410,6 +2412,11 @@ __global__ void __launch_bounds__(PTL_BLK, PSIM_PTL_BLOCKS_PER_CU) k_ptl(RoundAr
                 er[q] = make_uint4(n.EG[4 * q], n.EG[4 * q + 1], n.EG[4 * q + 2], n.EG[4 * q + 3]);
                 lr[q] = make_uint4(n.LZ[4 * q], n.LZ[4 * q + 1], n.LZ[4 * q + 2], n.LZ[4 * q + 3]);
             }
+#pragma unroll
+            for (int i = PTL_SET & ~3; i < PTL_SET; i++) {     // (the rest of the row is left as it was)
+                a.pt_eag[li * RT_SET + i] = n.EG[i];
+                a.pt_laz[li * RT_SET + i] = n.LZ[i];
+            }
         }
         if (n.out_dirty) {
             uint4* orow = reinterpret_cast<uint4*>(a.pt_out + li * OUT_IN);
@@ -2459,17 +2466,18 @@ __global__ void k_mark(unsigned long long* t, int slot) {
 
 // one wave-slot per resident wave: the grid strides over the active list
 // with no second generation of waves (a partial generation is a tail)
-static uint32_t resident_grid(const void* k) {
+static uint32_t resident_grid(const void* k, int block = WAVES_PER_BLOCK * 64) {
     int dev = 0, nb = 0;
     hipDeviceProp_t p;
     if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&p, dev) != hipSuccess ||
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, WAVES_PER_BLOCK * 64, 0) != hipSuccess || nb <= 0)
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, block, 0) != hipSuccess || nb <= 0)
         return 1024;
     return (uint32_t)nb * (uint32_t)p.multiProcessorCount;
 }
 uint32_t consume_grid() { return resident_grid((const void*)k_consume); }
 uint32_t lite_grid() { return resident_grid((const void*)k_consume_lite); }
 uint32_t pt_grid() { return resident_grid((const void*)k_pt); }
+uint32_t ptl_grid() { return resident_grid((const void*)k_ptl, PTL_BLK); }
 
 #ifdef PSIM_STAMPS
 int debug_stamps(unsigned long long* out) {

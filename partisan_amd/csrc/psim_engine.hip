@@ -1098,6 +1098,7 @@ struct psim_handle {
     uint32_t consume_blocks = 1024;     // resident k_consume blocks on the device
     uint32_t pt_blocks = 1024;          // ... and k_pt blocks
     uint32_t lite_blocks = 1024;        // ... and k_consume_lite blocks
+    uint32_t ptl_blocks = 1024;         // ... and k_ptl blocks
     uint64_t round = 0;
     std::vector<Shard*> shards;         // shards owned by this process
     int rank = 0, world = 1;
@@ -1395,7 +1396,7 @@ int phase_events_prepare(psim_handle* h, Shard* s, const RoundCtl& ctl, RoundArg
         s->tgrid = hv && h->cfg.plumtree ? std::min<uint32_t>(grid_for(n), h->pt_blocks) : 0;
         s->sgrid = hv ? std::min<uint32_t>(grid_for(n), SHUF_MAX_BLOCKS) : 0;
         s->lgrid = hv ? std::min<uint32_t>(grid_for(n), h->lite_blocks) : 0;
-        s->qgrid = hv && h->cfg.plumtree ? std::min<uint32_t>((n + PTL_BLOCK - 1) / PTL_BLOCK, PTL_MAX_BLOCKS) : 0;
+        s->qgrid = hv && h->cfg.plumtree ? std::min<uint32_t>((n + PTL_BLOCK - 1) / PTL_BLOCK, h->ptl_blocks) : 0;
         TRY(s->stat_part.ensure((size_t)(s->pgrid + s->cgrid + s->rgrid + s->tgrid + s->sgrid + s->lgrid + s->qgrid) *
                                 NST));
         k_node_prep<<<s->pgrid, BLK, 0, s->stream>>>(a, s->bmask.p, s->bound.p, s->stat_part.p, s->ocnt.p,
@@ -1984,6 +1985,7 @@ int psim_create(const psim_config* cfg, psim_handle** out) {
     h->consume_blocks = psim::consume_grid();
     h->pt_blocks = psim::pt_grid();
     h->lite_blocks = psim::lite_grid();
+    h->ptl_blocks = psim::ptl_grid();
     {
         const char* e = getenv("PSIM_PHASE_TIMERS");
         h->phase_timers = e && *e && *e != '0';

@@ -94,8 +94,14 @@ __global__ void k_consume(RoundArgs args);
 // lane-per-node SHUFFLE relays ahead of k_consume (psim_consume.hip)
 constexpr uint32_t RELAY_MAX_BLOCKS = 8192;
 constexpr uint32_t SHUF_MAX_BLOCKS = 1024;     // k_shuf: grid-stride over its list
-constexpr uint32_t PTL_MAX_BLOCKS = 1024;      // k_ptl: grid-stride over its list
-constexpr uint32_t PTL_BLOCK = 128;            // k_ptl's block (psim_consume.hip PTL_BLK)
+#ifndef PSIM_PTL_BLOCK
+#define PSIM_PTL_BLOCK 64
+#endif
+// k_ptl's block (psim_consume.hip PTL_BLK): one wave, so that its 256 B of
+// LDS per lane leave no block-sized hole (9 resident blocks per CU against 4
+// of 128 lanes, measured 2 % faster); the grid strides over its list with
+// the resident blocks (ptl_grid())
+constexpr uint32_t PTL_BLOCK = PSIM_PTL_BLOCK;
 __global__ void k_relay(RoundArgs args);
 __global__ void k_consume_pl(RoundArgs args);
 // lane-per-node shuffle starts of the nodes k_relay listed (psim_consume.hip)
@@ -114,6 +120,7 @@ int debug_stamps(unsigned long long* out);
 uint32_t consume_grid();
 uint32_t lite_grid();
 uint32_t pt_grid();
+uint32_t ptl_grid();
 
 // The launch's RoundArgs, read through an opaque constant-address pointer
 // (in a kernel whose only argument is a RoundArgs): each helper re-reads the
