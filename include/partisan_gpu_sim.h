@@ -304,7 +304,9 @@ int psim_leave(psim_handle *h, const uint32_t *nodes, size_t n);
  *       node that merges a removal of itself stops (pluggable:1182-1188).
  * A stopping manager sends nothing in that round (its sends are casts to
  * itself) and is down from the next round on.  One call per actor per
- * round.  PSIM_EUNSUPPORTED for HyParView handles and multi-rank handles. */
+ * round.  Multi-rank handles: every rank makes the same calls; a stop
+ * reported by the target's rank is all-gathered after the round.
+ * PSIM_EUNSUPPORTED for HyParView handles. */
 int psim_leave_node(psim_handle *h, const uint32_t *actors, const uint32_t *targets, size_t n);
 int psim_set_partition(psim_handle *h, const uint8_t *group, size_t n);
 int psim_clear_partition(psim_handle *h);

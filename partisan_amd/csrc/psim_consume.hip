@@ -1746,7 +1746,7 @@ DEV void block_append(bool go, const uint4& D, uint4* desc, uint32_t* cnt, uint3
 __global__ void __launch_bounds__(256, PSIM_RELAY_WAVES) k_relay(RoundArgs) {
     enum { R_PROC, R_DELIV, R_SHUF, R_FAIL, R_DIGEST, R_BOUND, R_N };
     __shared__ unsigned long long sst[R_N];
-    __shared__ uint32_t wcnt[5];                      // per wave list counts, then the block's base
+    __shared__ uint32_t wc5[5][5];                    // per list: the wave counts, then the block's base
     if (threadIdx.x < R_N) sst[threadIdx.x] = 0;
     __syncthreads();
     const uint32_t l = lane_id();
@@ -1822,15 +1822,43 @@ __global__ void __launch_bounds__(256, PSIM_RELAY_WAVES) k_relay(RoundArgs) {
             // (k_consume and k_consume_lite count their own)
             if (!heavy && !lite && (relay || to_pt || shuf)) v[R_PROC]++;
         }
-        block_append(P < na && heavy, maps ? make_uint4(D.x, D.y, D.z | DESC_MAPS_BIT, D.w) : D, a.desc_slow, a.n_slow,
-                     wcnt);
         // (k_ptl takes the Plumtree phase of nodes without an origin, and
         // hands k_pt the ones that do not fit a lane)
         const bool origin_node = ((D.z >> 28) & DESC_ORIGIN) != 0;
-        block_append(P < na && to_pt && origin_node, D, a.desc_pt, a.n_pt, wcnt);
-        block_append(P < na && to_pt && !origin_node, D, a.desc_ptl, a.n_ptl, wcnt);
-        block_append(P < na && shuf, D, a.desc_shuf, a.n_shuf, wcnt);
-        block_append(P < na && lite, D, a.desc_lite, a.n_lite, wcnt);
+        {
+            // the five lists at once: one barrier-separated count, the five
+            // block atomics from five lanes of one instruction (one after
+            // another they were five serial L2 round trips per block step)
+            const bool g[5] = {P < na && heavy, P < na && to_pt && origin_node, P < na && to_pt && !origin_node,
+                               P < na && shuf, P < na && lite};
+            uint64_t m[5];
+#pragma unroll
+            for (int k = 0; k < 5; k++) m[k] = ballot(g[k]);
+            const uint32_t wv = threadIdx.x >> 6, nwv = blockDim.x >> 6;
+            __syncthreads();                          // the previous step's readers of wc5 are done
+            if (l == 0)
+#pragma unroll
+                for (int k = 0; k < 5; k++) wc5[k][wv] = popc(m[k]);
+            __syncthreads();
+            if (threadIdx.x < 5) {
+                const uint32_t k = threadIdx.x;
+                uint32_t t = 0;
+                for (uint32_t j = 0; j < nwv; j++) t += wc5[k][j];
+                uint32_t* cnt = k == 0 ? a.n_slow : k == 1 ? a.n_pt : k == 2 ? a.n_ptl : k == 3 ? a.n_shuf : a.n_lite;
+                wc5[k][4] = t ? atomicAdd(cnt, t) : 0u;
+            }
+            __syncthreads();
+#pragma unroll
+            for (int k = 0; k < 5; k++)
+                if (g[k]) {
+                    uint32_t b0 = wc5[k][4];
+                    for (uint32_t j = 0; j < wv; j++) b0 += wc5[k][j];
+                    uint4* desc = k == 0 ? a.desc_slow : k == 1 ? a.desc_pt : k == 2 ? a.desc_ptl
+                                : k == 3 ? a.desc_shuf : a.desc_lite;
+                    desc[b0 + popc(m[k] & lt_mask())] =
+                        k == 0 && maps ? make_uint4(D.x, D.y, D.z | DESC_MAPS_BIT, D.w) : D;
+                }
+        }
         if (P >= na || heavy || lite) continue;
         const uint32_t id = D.x;
         const size_t li = id - a.lo;

@@ -1784,7 +1784,9 @@ int run_round(psim_handle* h, uint64_t* st) {
     h->pend_lv_a.clear(); h->pend_lv_t.clear();
     if (st[ST_STOP]) {
         // managers that stopped this round (psim_leave_node) are down from the
-        // next round on: the next round's crash events (single-rank handles)
+        // next round on: the next round's crash events, on every rank (the
+        // count is the all-reduced one, so every rank of an RCCL handle is
+        // here: its shard's list is all-gathered, padded to the longest)
         std::vector<uint32_t> ids;
         for (Shard* s : h->shards) {
             const size_t k = s->pin[ST_STOP];
@@ -1793,6 +1795,29 @@ int run_round(psim_handle* h, uint64_t* st) {
             ids.resize(at + k);
             HIP_TRY(hipMemcpyAsync(ids.data() + at, s->stop_ids.p, k * 4, hipMemcpyDeviceToHost, s->stream));
             TRY(stream_wait(s));
+        }
+        if (h->world > 1) {
+            Shard* s = h->shards[0];
+            const uint32_t W = h->world;
+            std::vector<uint64_t> cnt(W), mine(ids.begin(), ids.end());
+            const uint64_t k = mine.size();
+            TRY(h->comm_cnt.ensure(W + 1));
+            HIP_TRY(hipMemcpyAsync(h->comm_cnt.p + W, &k, 8, hipMemcpyHostToDevice, s->stream));
+            NCCL_TRY(ncclAllGather(h->comm_cnt.p + W, h->comm_cnt.p, 1, ncclUint64, h->comm, s->stream));
+            HIP_TRY(hipMemcpyAsync(cnt.data(), h->comm_cnt.p, W * 8, hipMemcpyDeviceToHost, s->stream));
+            TRY(stream_wait(s));
+            const uint64_t mk = *std::max_element(cnt.begin(), cnt.end());
+            mine.resize(mk, 0);
+            std::vector<uint64_t> all((size_t)W * mk);
+            TRY(h->comm_cnt.ensure((size_t)W * mk + mk));
+            HIP_TRY(hipMemcpyAsync(h->comm_cnt.p + (size_t)W * mk, mine.data(), mk * 8, hipMemcpyHostToDevice,
+                                   s->stream));
+            NCCL_TRY(ncclAllGather(h->comm_cnt.p + (size_t)W * mk, h->comm_cnt.p, mk, ncclUint64, h->comm, s->stream));
+            HIP_TRY(hipMemcpyAsync(all.data(), h->comm_cnt.p, all.size() * 8, hipMemcpyDeviceToHost, s->stream));
+            TRY(stream_wait(s));
+            ids.clear();
+            for (uint32_t r = 0; r < W; r++)
+                for (uint64_t j = 0; j < cnt[r]; j++) ids.push_back((uint32_t)all[(size_t)r * mk + j]);
         }
         std::sort(ids.begin(), ids.end());
         h->pend_crash.insert(h->pend_crash.end(), ids.begin(), ids.end());
@@ -2090,11 +2115,12 @@ int psim_leave(psim_handle* h, const uint32_t* nodes, size_t n) {
 }
 
 // leave/1: actors[i] removes targets[i] (pl:502-515 -> internal_leave/2
-// :1390-1420); actor == target is leave/0.  Single-rank handles (a stop is
-// learned from the owner shard's list after the round).
+// :1390-1420); actor == target is leave/0.  A stop is learned from the
+// owner shard's list after the round (RCCL ranks: all-gathered; every rank
+// makes the same calls).
 int psim_leave_node(psim_handle* h, const uint32_t* actors, const uint32_t* targets, size_t n) {
     if (!h || (n && (!actors || !targets))) return PSIM_EINVAL;
-    if (h->cfg.manager != PSIM_MANAGER_PLUGGABLE || h->world > 1) return PSIM_EUNSUPPORTED;
+    if (h->cfg.manager != PSIM_MANAGER_PLUGGABLE) return PSIM_EUNSUPPORTED;
     for (size_t i = 0; i < n; i++) {
         if (actors[i] >= h->N || targets[i] >= h->N) return PSIM_ERANGE;
         for (uint32_t a : h->pend_lv_a) if (a == actors[i]) return PSIM_EINVAL;

@@ -1,5 +1,7 @@
-"""Two RCCL ranks of the simulator on ONE device (diagnostic: exercises the
-RCCL exchange path of psim_engine.hip where no second GPU is available).
+"""Two RCCL ranks of the simulator (diagnostic: the RCCL exchange path of
+psim_engine.hip).  Needs two devices: RCCL 7.2 refuses two ranks on one
+("Duplicate GPU detected", ncclInvalidUsage, measured on the one-GPU box),
+so set HIP_VISIBLE_DEVICES per rank or run it on a node with two GPUs.
 Compares the 2-rank run with a 1-shard run on the same device, bit for bit.
 Usage: torchrun --nproc-per-node 2 profiles/rccl_pair.py"""
 import os

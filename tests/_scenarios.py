@@ -203,6 +203,19 @@ def pl_leave_remote(make, n, seed, rounds, strategy, leave_at=40, k=16, part_at=
     return sim, st, np.array(picked["a"], np.uint32), np.array(picked["t"], np.uint32)
 
 
+def pl_leave_fixed(make, n, seed, rounds, strategy, leave_at, actors, targets, fanout=0):
+    """pl_leave_remote's schedule with the leave/1 pairs given (the pairs a
+    run of pl_leave_remote picked): for handles that cannot pick them
+    themselves, e.g. RCCL ranks that see only their own rows."""
+    sim = make(default_config(n_nodes=n, seed=seed, manager=1, strategy=strategy, fanout=fanout))
+
+    def hook(r):
+        if r == leave_at:
+            sim.leave_node(np.asarray(actors, np.uint32), np.asarray(targets, np.uint32))
+    st = sim.run_schedule(W.doubling_join(n, seed), rounds, extra=hook)
+    return sim, st
+
+
 def pl_omission(make, n, seed, rounds, strategy, fanout=0, begin=40, end=60, heal=75, k=None):
     """The crash-fault model's omission faults (prop_partisan_crash_fault_model
     :93-229) on a pluggable handle: a doubling bootstrap; at `begin` k nodes
