@@ -2011,6 +2011,10 @@ int psim_create(const psim_config* cfg, psim_handle** out) {
     h->pt_blocks = psim::pt_grid();
     h->lite_blocks = psim::lite_grid();
     h->ptl_blocks = psim::ptl_grid();
+    if (const char* e = getenv("PSIM_PTL_GRID")) {      // (a smaller k_ptl grid, for measurements)
+        const long v = strtol(e, nullptr, 10);
+        if (v > 0 && (uint32_t)v < h->ptl_blocks) h->ptl_blocks = (uint32_t)v;
+    }
     {
         const char* e = getenv("PSIM_PHASE_TIMERS");
         h->phase_timers = e && *e && *e != '0';
