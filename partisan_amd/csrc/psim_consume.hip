@@ -2151,6 +2151,7 @@ DEV void col_add(const LdsCol& V, uint32_t& n, uint32_t x) {
 struct PtLane {
     uint32_t id, me_part, act_n;
     uint32_t A[PSIM_ACTIVE_CAP];
+    uint32_t cmask;                // bit j: A[j] is a live connection (ptl_conn's test, per member)
     uint32_t root0;                // slot 0's root (NONE = free)
     LdsCol EG, LZ, OL, OH;         // slot 0's eager / lazy sets; outstanding keys (low, high words)
     uint32_t ne, nl, on;
@@ -2160,12 +2161,30 @@ struct PtLane {
 
 // send/3 (pt:633-638): over an existing connection -- the peer in the active
 // view, running, same partition
+// (the members' up and partition bytes are read once per node, all eight
+// loads in flight together: read per send they were one dependent memory
+// latency per send; no kernel of the phase changes them)
+DEV uint32_t ptl_conn_mask(KArgs& a, const PtLane& n) {
+    uint8_t fl[PSIM_ACTIVE_CAP], pt[PSIM_ACTIVE_CAP];
+#pragma unroll
+    for (int j = 0; j < PSIM_ACTIVE_CAP; j++) {
+        const uint32_t q = (uint32_t)j < n.act_n && n.A[j] < a.n_nodes ? n.A[j] : n.id;
+        fl[j] = a.flags[q];
+        pt[j] = a.part[q];
+    }
+    uint32_t m = 0;
+#pragma unroll
+    for (int j = 0; j < PSIM_ACTIVE_CAP; j++)
+        m |= ((uint32_t)j < n.act_n && n.A[j] < a.n_nodes && n.A[j] != n.id && (fl[j] & F_UP) &&
+              pt[j] == n.me_part) ? 1u << j : 0u;
+    return m;
+}
 DEV bool ptl_conn(KArgs& a, const PtLane& n, uint32_t ident) {
     const uint32_t p = ident & ~PSIM_MAP_BIT;
-    bool in = false;
+    bool c = false;
 #pragma unroll
-    for (int j = 0; j < PSIM_ACTIVE_CAP; j++) in |= (uint32_t)j < n.act_n && n.A[j] == p;
-    return in && p != n.id && p < a.n_nodes && (a.flags[p] & F_UP) && a.part[p] == n.me_part;
+    for (int j = 0; j < PSIM_ACTIVE_CAP; j++) c |= ((n.cmask >> j) & 1u) && n.A[j] == p;
+    return c;
 }
 
 // update_peers/5 + set_peers/4 (pt:593-609) on slot 0 (a new root takes it
@@ -2307,6 +2326,7 @@ __global__ void __launch_bounds__(PTL_BLK, PSIM_PTL_BLOCKS_PER_CU) k_ptl(RoundAr
             n.A[0] = a0.x; n.A[1] = a0.y; n.A[2] = a0.z; n.A[3] = a0.w;
             n.A[4] = a1.x; n.A[5] = a1.y; n.A[6] = a1.z; n.A[7] = a1.w;
         }
+        n.cmask = ptl_conn_mask(a, n);
         n.root0 = root0;
         n.ne = root0 == NONE ? 0u : (rtw4 & 0xFF);
         n.nl = root0 == NONE ? 0u : (rtw5 & 0xFF);
