@@ -2365,11 +2365,20 @@ __global__ void __launch_bounds__(PTL_BLK, PSIM_PTL_BLOCKS_PER_CU) k_ptl(RoundAr
         uint32_t seq = a.ocnt[li];
         const uint32_t oend = (uint32_t)a.obase[li + 1];
         const uint32_t ik = start == a.round ? 0u : (D.z & DESC_CNT_MASK);
+        // (each record's first 32 B as two 16-B loads -- field-wise reads were
+        // re-issued per branch, 40 more VGPRs -- and the next record's issued
+        // before this one is handled)
+        uint4 nq0 = make_uint4(0, 0, 0, 0), nq1 = nq0;
+        if (ik) {
+            const uint4* rq = reinterpret_cast<const uint4*>(a.rec_in + D.y);
+            nq0 = rq[0]; nq1 = rq[1];
+        }
         for (uint32_t j = 0; j < ik; j++) {           // the Plumtree inbox, canonical order
-            // (the record's first 32 B as two 16-B loads: field-wise reads were
-            // re-issued per branch, 40 more VGPRs)
-            const uint4* rq = reinterpret_cast<const uint4*>(a.rec_in + D.y + j);
-            const uint4 q0 = rq[0], q1 = rq[1];
+            const uint4 q0 = nq0, q1 = nq1;
+            {
+                const uint4* rq = reinterpret_cast<const uint4*>(a.rec_in + D.y + min(j + 1, ik - 1));
+                nq0 = rq[0]; nq1 = rq[1];
+            }
             const uint32_t type = q0.z & 0xFF;
             if (type < PSIM_MSG_PT_BROADCAST || type > PSIM_MSG_PT_GRAFT) continue;
             const uint32_t src = q0.y, msg = q1.x, rnd = q1.y, root = q1.z, from = src | PSIM_MAP_BIT;
