@@ -54,7 +54,7 @@ def parse():
     p.add_argument("--nodes", type=int, default=1 << 20, help="nodes per GPU (weak scaling)")
     p.add_argument("--seed", type=int, default=1)
     p.add_argument("--settle", type=int, default=60, help="untimed rounds after bootstrap")
-    p.add_argument("--cpu-sample-nodes", type=int, default=1 << 16)
+    p.add_argument("--cpu-sample-nodes", type=int, default=1 << 17)
     p.add_argument("--cpu-sample-rounds", type=int, default=40)
     p.add_argument("--cpu-workers", type=int, default=16,
                    help="processes of the all-cores CPU baseline (the GPU box's CPU share is 16)")
@@ -66,6 +66,11 @@ def parse():
     p.add_argument("--vshards", type=int, default=1,
                    help="diagnostic: G virtual shards of --nodes each on this one GPU (the sharded "
                         "partition / exchange / receive path with device copies instead of RCCL)")
+    p.add_argument("--schedule", default="survey", choices=["survey", "doubling"],
+                   help="config C's event schedule.  survey (default): SURVEY 8(d) -- joins spread "
+                        "over a 64-round ramp, 100 warm-up rounds, then ONE broadcast from node 0 at the "
+                        "first timed round; doubling: the round-2 line -- doubling bootstrap, --settle "
+                        "rounds, a broadcast from node 0 every 10 rounds throughout")
     p.add_argument("--workload", default="C", choices=["C", "B", "D", "E"],
                    help="C (default, the headline line): HyParView+Plumtree; "
                         "B: full-membership strategy, fanout 5; D: SCAMP v2 (c=5); "
@@ -128,9 +133,12 @@ def launch_ranks(args):
 
 
 # -------------------------------------------------------- CPU baseline --
-def _cpu_sample(n, seed, rounds, barrier=None):
+SURVEY_WARM = 100               # warm-up rounds after the 64-round join ramp
+
+
+def _cpu_sample(n, seed, rounds, schedule, barrier=None):
     """The CPU oracle (a port of the reference handlers, 1 thread) on a
-    bounded sample of the workload: same bootstrap, same broadcast cadence.
+    bounded sample of the workload: same bootstrap, same broadcast schedule.
     Returns (node-rounds, msgs, seconds)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from _oracle import Oracle
@@ -138,13 +146,16 @@ def _cpu_sample(n, seed, rounds, barrier=None):
     from partisan_amd.sim import default_config
 
     o = Oracle(default_config(n_nodes=n, seed=seed))
-    o.run_schedule(W.doubling_join(n, seed), 40)
+    if schedule == "survey":
+        o.run_schedule(W.survey_join(n, seed), W.SURVEY_RAMP + SURVEY_WARM)
+    else:
+        o.run_schedule(W.doubling_join(n, seed), 40)
     k, msgs = 0, 0
     if barrier is not None:                   # all workers time their rounds together
         barrier.wait()
     t0 = time.perf_counter()
     for r in range(rounds):
-        if r % BCAST_PERIOD == 0:
+        if (r == 0) if schedule == "survey" else (r % BCAST_PERIOD == 0):
             o.broadcast(0, k)
             k += 1
         msgs += int(o.step(1)["emitted"].sum())
@@ -165,6 +176,25 @@ def cpu_model():
     return None
 
 
+def reference_probe():
+    """the reference Erlang path is timed only where an
+    Erlang VM exists on this box (`command -v erl`)."""
+    import shutil
+    erl = shutil.which("erl")
+    if erl is None:
+        return {"available": False, "erl": None,
+                "note": "unavailable: no erl on this box (no Erlang VM); the CPU baseline is the port"}
+    try:
+        otp = subprocess.run([erl, "-noshell", "-eval",
+                              "io:format(\"~s\", [erlang:system_info(otp_release)]), halt()."],
+                             capture_output=True, text=True, timeout=60).stdout.strip()
+    except (OSError, subprocess.SubprocessError):
+        otp = None
+    return {"available": True, "erl": erl, "otp_release": otp,
+            "note": "an Erlang VM exists here: erlang/harness/README.md runs config A through the "
+                    "reference modules and compare_trace.py"}
+
+
 def cpu_baseline(args):
     """Run before the GPU is touched (worker processes are forked).  One
     thread, then `workers` independent oracle processes on the same sample
@@ -173,11 +203,11 @@ def cpu_baseline(args):
     import multiprocessing as mp
 
     n, rounds = args.cpu_sample_nodes, args.cpu_sample_rounds
-    nr, msgs, dt = _cpu_sample(n, args.seed, rounds)
+    nr, msgs, dt = _cpu_sample(n, args.seed, rounds, args.schedule)
     workers = max(1, min(args.cpu_workers, len(os.sched_getaffinity(0))))
     ctx = mp.get_context("fork")
     barrier, q = ctx.Barrier(workers), ctx.Queue()
-    procs = [ctx.Process(target=_cpu_worker, args=((n, args.seed + i, rounds), barrier, q))
+    procs = [ctx.Process(target=_cpu_worker, args=((n, args.seed + i, rounds, args.schedule), barrier, q))
              for i in range(workers)]
     for p in procs:
         p.start()
@@ -188,13 +218,17 @@ def cpu_baseline(args):
     tot = sum(r[0] for r in res)
     return {"value": nr / dt, "unit": "node-rounds/s", "cores": 1, "kind": "port",
             "msgs_per_sec": msgs / dt,
-            "sample": f"oracle/psim_oracle.c, {n} nodes, {rounds} steady-state rounds after a doubling "
-                      f"bootstrap, broadcast every {BCAST_PERIOD} rounds, 1 thread",
+            "sample": (f"oracle/psim_oracle.c, {n} nodes, {rounds} rounds from one broadcast after the "
+                       f"survey bootstrap (64-round ramp + {SURVEY_WARM} rounds), 1 thread"
+                       if args.schedule == "survey" else
+                       f"oracle/psim_oracle.c, {n} nodes, {rounds} steady-state rounds after a doubling "
+                       f"bootstrap, broadcast every {BCAST_PERIOD} rounds, 1 thread"),
             "all_cores": {"value": tot / wall, "unit": "node-rounds/s", "cores": workers,
                           "msgs_per_sec": sum(r[1] for r in res) / wall,
                           "sample": f"{workers} oracle processes at once, each the 1-thread sample "
                                     f"with its own seed, timed rounds started together (barrier); "
                                     f"node-rounds of all / the slowest one's time"},
+            "reference": reference_probe(),
             "cpu_model": cpu_model(), "nproc": os.cpu_count(),
             "affinity_cpus": len(os.sched_getaffinity(0))}
 
@@ -307,7 +341,8 @@ def src_hash():
 
 def pmc_key(args, world, n):
     return {"workload": args.workload, "nodes": n, "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "seed": args.seed, "schedule": SCHEDULE_VERSION, "src": src_hash()}
+            "warmup": args.warmup, "seed": args.seed, "schedule": SCHEDULE_VERSION,
+            "events": args.schedule if args.workload == "C" else "doubling", "src": src_hash()}
 
 
 def pmc_traffic(key):
@@ -477,15 +512,23 @@ def main():
         ovf_run[:] += s_["overflow_by"].sum(axis=0).astype(np.uint64)
         return s_
 
-    boot = W.doubling_join(n, args.seed)
-    ovf_run[:] += sim.run_schedule(boot, boot[-1][0] + 1 + args.settle)["overflow_by"].sum(axis=0).astype(np.uint64)
+    survey = args.workload == "C" and args.schedule == "survey"
+    if survey:
+        # the 64-round join ramp and 100 warm-up rounds; the
+        # --warmup rounds follow, then the one broadcast opens the window
+        boot = W.survey_join(n, args.seed)
+        ovf_run[:] += sim.run_schedule(boot, W.SURVEY_RAMP + SURVEY_WARM)["overflow_by"].sum(axis=0).astype(np.uint64)
+    else:
+        boot = W.doubling_join(n, args.seed)
+        ovf_run[:] += sim.run_schedule(boot, boot[-1][0] + 1 + args.settle)["overflow_by"].sum(axis=0).astype(np.uint64)
 
     # event index i counts rounds from the start of the broadcast phase:
-    # STEADY_ROUNDS untimed broadcast rounds (whatever --warmup is), the
-    # warmup rounds, then the timed window
+    # doubling: STEADY_ROUNDS untimed broadcast rounds (whatever --warmup is),
+    # the warmup rounds, then the timed window; survey: the warmup rounds,
+    # then the timed window, whose first round carries the broadcast
     state = {"k": 0, "last_bcast": None}
     churn = {}
-    t_start = STEADY_ROUNDS + args.warmup
+    t_start = args.warmup if survey else STEADY_ROUNDS + args.warmup
     if args.workload == "E":
         # config E: 0.2*N crashes spread over 100 rounds, each
         # victim restarts the next round and rejoins; ids [0, N/2) | [N/2, N)
@@ -495,8 +538,11 @@ def main():
         part = W.half_partition(n)
         p_on, p_off = t_start + 20, t_start + 40
 
+    def bcast_round(i):
+        return i == t_start if survey else i % BCAST_PERIOD == 0
+
     def round_events(i):
-        if i % BCAST_PERIOD == 0:
+        if bcast_round(i):
             sim.broadcast(0, state["k"] % 0x10000)
             state["k"] += 1
             state["last_bcast"] = i
@@ -511,7 +557,7 @@ def main():
                 sim.clear_partition()
 
     def has_events(i):
-        return i % BCAST_PERIOD == 0 or (args.workload == "E" and (i in churn or i - 1 in churn or i in (p_on, p_off)))
+        return bcast_round(i) or (args.workload == "E" and (i in churn or i - 1 in churn or i in (p_on, p_off)))
 
     for i in range(t_start):
         round_events(i)
@@ -555,10 +601,13 @@ def main():
     per_launch_bytes = alg_bytes / max(1, c_n)
     per_launch_s = (c_ms / 1e3) / max(1, c_n)
     achieved = per_launch_bytes / per_launch_s / 1e9 if per_launch_s > 0 else 0.0
+    # the same algorithmic bytes over the whole step (node-round phase, route,
+    # gather, prepare, stats, host syncs): the whole-step roofline fraction
+    step_achieved = alg_bytes / dt / 1e9 if dt > 0 else 0.0
     key = pmc_key(args, world, n)
     traffic, trec = pmc_traffic(key)
     tsrc = trec.get("source") if trec else None
-    n_bc = sum(1 for j in range(t_start, t_start + args.steps) if j % BCAST_PERIOD == 0)
+    n_bc = sum(1 for j in range(t_start, t_start + args.steps) if bcast_round(j))
     out = {
         "metric": "simulated node-rounds/sec (+ msgs/sec), 1M-node HyParView+Plumtree"
                   + ("" if args.workload == "C" else " (config E: churn + partition)"),
@@ -569,13 +618,20 @@ def main():
         "ms_per_step": dt / args.steps * 1e3,
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": "u32", "data": "synthetic",
-        "config": {"workload": ("C: HyParView+Plumtree, doubling bootstrap, steady state, "
-                                "broadcast from node 0 every 10 rounds") if args.workload == "C" else
+        "config": {"workload": ("C: HyParView+Plumtree, SURVEY 8(d) schedule: joins over a 64-round ramp "
+                                "(node i at round 64*i/N, contact uniform among earlier rounds), 100 warm-up "
+                                "rounds, --warmup rounds, then one broadcast from node 0 at the first timed "
+                                "round; the window is that broadcast's propagation") if survey else
+                               ("C: HyParView+Plumtree, doubling bootstrap, steady state, "
+                                "broadcast from node 0 every 10 rounds (not SURVEY 8(d)'s schedule: the doubling "
+                                "ramp starts half the overlay in one round, aligning its shuffle timers)")
+                               if args.workload == "C" else
                                ("E: HyParView+Plumtree, 20% churn over 100 rounds (crash, restart, rejoin), "
                                 "half/half partition for rounds 20-39, broadcast every 10 rounds"),
                    "nodes": n, "nodes_per_gpu": args.nodes, "seed": args.seed,
-                   "untimed_broadcast_rounds": STEADY_ROUNDS + args.warmup,
-                   "broadcasts_before_window": (t_start + BCAST_PERIOD - 1) // BCAST_PERIOD,
+                   "schedule": "survey" if survey else "doubling",
+                   "untimed_broadcast_rounds": 0 if survey else STEADY_ROUNDS + args.warmup,
+                   "broadcasts_before_window": 0 if survey else (t_start + BCAST_PERIOD - 1) // BCAST_PERIOD,
                    "broadcasts_in_window": n_bc,
                    "parallelism": (f"node-range sharded x{world}, RCCL all-to-all" if world > 1 else
                                    f"1 GPU, {args.vshards} virtual shards" if args.vshards > 1 else "1 GPU")},
@@ -587,7 +643,9 @@ def main():
                                "kernels launched just before k_relay and just after k_pt)",
                      "alg_bytes_per_launch": per_launch_bytes,
                      "alg_bytes_formula": ALG_FORMULA,
-                     "avg_launch_ms": per_launch_s * 1e3},
+                     "avg_launch_ms": per_launch_s * 1e3,
+                     "step_achieved": step_achieved,
+                     "step_frac": step_achieved / HBM_PEAK_GBS},
         "kernel_ms_per_step": {k: v[0] / args.steps for k, v in kt.items() if v[1]},
         "overflow": int(st["overflow"].sum()),
         "pmc_key": key,

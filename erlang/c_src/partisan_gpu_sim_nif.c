@@ -10,7 +10,9 @@
  * mutex (the ABI is thread-compatible, not thread-safe).  psim_step and the
  * other long calls run on dirty schedulers and wait for the mutex; the short
  * NIFs run on normal schedulers and never block one: when the handle is busy
- * (a step in progress) they return {error, busy} and the caller retries.
+ * (a step in progress) they return {error, busy}; the wrappers in
+ * partisan_gpu_sim.erl retry those with a bounded back-off (call/1 there),
+ * so a caller sees {error, busy} only after ~10 s of steps.
  */
 #include <erl_nif.h>
 #include <string.h>
@@ -408,18 +410,18 @@ static ErlNifFunc funcs[] = {
     {"revive_nif", 2, nif_revive, 0},
     {"leave_nif", 2, nif_leave, 0},
     {"leave_node_nif", 3, nif_leave_node, 0},
-    {"broadcast", 3, nif_broadcast, 0},
+    {"broadcast_nif", 3, nif_broadcast, 0},
     {"step", 2, nif_step, ERL_NIF_DIRTY_JOB_CPU_BOUND},
-    {"active", 2, nif_active, 0},
-    {"members", 3, nif_members, 0},
-    {"delivery", 2, nif_delivery, 0},
+    {"active_nif", 2, nif_active, 0},
+    {"members_nif", 3, nif_members, 0},
+    {"delivery_nif", 2, nif_delivery, 0},
     {"histograms", 1, nif_histograms, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"set_partition_nif", 2, nif_set_partition, 0},
-    {"clear_partition", 1, nif_clear_partition, 0},
+    {"clear_partition_nif", 1, nif_clear_partition, 0},
     {"omission_nif", 5, nif_omission, 0},
     {"faulted_nif", 3, nif_faulted, 0},
-    {"clear_faults", 1, nif_clear_faults, 0},
-    {"node", 2, nif_node, 0},
+    {"clear_faults_nif", 1, nif_clear_faults, 0},
+    {"node_nif", 2, nif_node, 0},
     {"snapshot", 1, nif_snapshot, ERL_NIF_DIRTY_JOB_IO_BOUND},
     {"restore", 2, nif_restore, ERL_NIF_DIRTY_JOB_IO_BOUND},
 };

@@ -1,12 +1,20 @@
 %% partisan_gpu_sim -- NIF bindings of the MI355X simulator
 %% (include/partisan_gpu_sim.h).  Node ids are the simulated nodes; an id maps
 %% to the harness node_spec #{name => 'n<id>@sim', ...} (DESIGN.md section 2).
+%%
+%% The short NIFs run on normal schedulers and answer {error, busy} while
+%% another process holds the handle inside a step (dirty scheduler).  Every
+%% wrapper below goes through call/1, which retries a busy answer with a
+%% bounded back-off, so callers may match on success directly.
 -module(partisan_gpu_sim).
 -export([create/1, join/3, crash/2, revive/2, leave/2, leave_node/3, broadcast/3, step/2, active/2, members/3,
          delivery/2, histograms/1, snapshot/1, restore/2, set_partition/2, clear_partition/1, node/2,
          begin_send_omission/3, end_send_omission/3, begin_receive_omission/3, end_receive_omission/3,
          begin_omission/2, end_omission/2, clear_faults/1]).
 -on_load(init/0).
+
+%% back-off of a busy handle: 1 ms sleeps, at most ~10 s in all
+-define(BUSY_TRIES, 10000).
 
 init() ->
     Priv = case code:priv_dir(partisan_gpu_sim) of
@@ -19,46 +27,66 @@ init() ->
 create(_Config) -> erlang:nif_error(nif_not_loaded).
 
 %% Nodes/Contacts: lists of ids, packed as little-endian u32 binaries.
-join(Sim, Nodes, Contacts) -> join_nif(Sim, pack(Nodes), pack(Contacts)).
-crash(Sim, Nodes) -> crash_nif(Sim, pack(Nodes)).
+join(Sim, Nodes, Contacts) -> call(fun() -> join_nif(Sim, pack(Nodes), pack(Contacts)) end).
+crash(Sim, Nodes) -> call(fun() -> crash_nif(Sim, pack(Nodes)) end).
 %% restart without a join (init/1 state; reached through passive views)
-revive(Sim, Nodes) -> revive_nif(Sim, pack(Nodes)).
+revive(Sim, Nodes) -> call(fun() -> revive_nif(Sim, pack(Nodes)) end).
 %% leave/0 at each node (pluggable manager handles; {error, unsupported} on HyParView)
-leave(Sim, Nodes) -> leave_nif(Sim, pack(Nodes)).
+leave(Sim, Nodes) -> call(fun() -> leave_nif(Sim, pack(Nodes)) end).
 %% leave/1 at each actor: Actors[i] removes Targets[i] (SCAMP v1 / v2 handles)
-leave_node(Sim, Actors, Targets) -> leave_node_nif(Sim, pack(Actors), pack(Targets)).
-broadcast(_Sim, _Root, _Id) -> erlang:nif_error(nif_not_loaded).
+leave_node(Sim, Actors, Targets) -> call(fun() -> leave_node_nif(Sim, pack(Actors), pack(Targets)) end).
+broadcast(Sim, Root, Id) -> call(fun() -> broadcast_nif(Sim, Root, Id) end).
+%% a dirty NIF: waits for the handle's mutex itself
 step(_Sim, _Rounds) -> erlang:nif_error(nif_not_loaded).
-active(_Sim, _Node) -> erlang:nif_error(nif_not_loaded).
+active(Sim, Node) -> call(fun() -> active_nif(Sim, Node) end).
 %% pluggable manager handles: the strategy membership of Node (N = n_nodes)
-members(_Sim, _Node, _N) -> erlang:nif_error(nif_not_loaded).
+members(Sim, Node, N) -> call(fun() -> members_nif(Sim, Node, N) end).
 %% the tracked broadcast at Node: {ok, {Have, FirstRound, Hop}}
-delivery(_Sim, _Node) -> erlang:nif_error(nif_not_loaded).
-%% overlay statistics (psim_histograms) as a map
+delivery(Sim, Node) -> call(fun() -> delivery_nif(Sim, Node) end).
+%% overlay statistics (psim_histograms) as a map (dirty NIF)
 histograms(_Sim) -> erlang:nif_error(nif_not_loaded).
-%% whole-simulation state as a binary, and back into a handle of the same config
+%% whole-simulation state as a binary, and back into a handle of the same config (dirty NIFs)
 snapshot(_Sim) -> erlang:nif_error(nif_not_loaded).
 restore(_Sim, _Bin) -> erlang:nif_error(nif_not_loaded).
 
 %% the partition group of every node (a list of N small integers): an
 %% injected partition as a network partition (DESIGN.md section 2);
 %% clear_partition/1 resolves it
-set_partition(Sim, Groups) -> set_partition_nif(Sim, << <<G:8>> || G <- Groups >>).
-clear_partition(_Sim) -> erlang:nif_error(nif_not_loaded).
-%% one node: {ok, #{up, epoch, active, passive, have, round}}
-node(_Sim, _Node) -> erlang:nif_error(nif_not_loaded).
+set_partition(Sim, Groups) ->
+    Bin = << <<G:8>> || G <- Groups >>,
+    call(fun() -> set_partition_nif(Sim, Bin) end).
+clear_partition(Sim) -> call(fun() -> clear_partition_nif(Sim) end).
+%% one node: {ok, #{up, epoch, active, passive, have, slots, round}}
+node(Sim, Node) -> call(fun() -> node_nif(Sim, Node) end).
 
 %% omission faults of the pluggable manager's interposition layer (the
 %% crash-fault model's commands, test/prop_partisan_crash_fault_model.erl
 %% :93-229), pairwise over lists of ids; pluggable handles only
-begin_send_omission(Sim, Srcs, Dsts) -> omission_nif(Sim, 0, pack(Srcs), pack(Dsts), 1).
-end_send_omission(Sim, Srcs, Dsts) -> omission_nif(Sim, 0, pack(Srcs), pack(Dsts), 0).
-begin_receive_omission(Sim, Srcs, Dsts) -> omission_nif(Sim, 1, pack(Srcs), pack(Dsts), 1).
-end_receive_omission(Sim, Srcs, Dsts) -> omission_nif(Sim, 1, pack(Srcs), pack(Dsts), 0).
-begin_omission(Sim, Nodes) -> faulted_nif(Sim, pack(Nodes), 1).
-end_omission(Sim, Nodes) -> faulted_nif(Sim, pack(Nodes), 0).
+begin_send_omission(Sim, Srcs, Dsts) -> omission(Sim, 0, Srcs, Dsts, 1).
+end_send_omission(Sim, Srcs, Dsts) -> omission(Sim, 0, Srcs, Dsts, 0).
+begin_receive_omission(Sim, Srcs, Dsts) -> omission(Sim, 1, Srcs, Dsts, 1).
+end_receive_omission(Sim, Srcs, Dsts) -> omission(Sim, 1, Srcs, Dsts, 0).
+begin_omission(Sim, Nodes) -> call(fun() -> faulted_nif(Sim, pack(Nodes), 1) end).
+end_omission(Sim, Nodes) -> call(fun() -> faulted_nif(Sim, pack(Nodes), 0) end).
 %% resolve_all_faults_with_heal
-clear_faults(_Sim) -> erlang:nif_error(nif_not_loaded).
+clear_faults(Sim) -> call(fun() -> clear_faults_nif(Sim) end).
+
+omission(Sim, Kind, Srcs, Dsts, On) ->
+    S = pack(Srcs),
+    D = pack(Dsts),
+    call(fun() -> omission_nif(Sim, Kind, S, D, On) end).
+
+%% a short NIF, retried while the handle is inside another process's step
+call(F) -> call(F, ?BUSY_TRIES).
+
+call(F, Tries) ->
+    case F() of
+        {error, busy} when Tries > 1 ->
+            timer:sleep(1),
+            call(F, Tries - 1);
+        Result ->
+            Result
+    end.
 
 pack(Ids) -> << <<I:32/little>> || I <- Ids >>.
 omission_nif(_S, _K, _A, _B, _On) -> erlang:nif_error(nif_not_loaded).
@@ -69,3 +97,10 @@ crash_nif(_S, _N) -> erlang:nif_error(nif_not_loaded).
 revive_nif(_S, _N) -> erlang:nif_error(nif_not_loaded).
 leave_nif(_S, _N) -> erlang:nif_error(nif_not_loaded).
 leave_node_nif(_S, _A, _T) -> erlang:nif_error(nif_not_loaded).
+broadcast_nif(_S, _R, _I) -> erlang:nif_error(nif_not_loaded).
+active_nif(_S, _N) -> erlang:nif_error(nif_not_loaded).
+members_nif(_S, _N, _K) -> erlang:nif_error(nif_not_loaded).
+delivery_nif(_S, _N) -> erlang:nif_error(nif_not_loaded).
+clear_partition_nif(_S) -> erlang:nif_error(nif_not_loaded).
+clear_faults_nif(_S) -> erlang:nif_error(nif_not_loaded).
+node_nif(_S, _N) -> erlang:nif_error(nif_not_loaded).

@@ -14,6 +14,7 @@
 -behaviour(partisan_membership_strategy).
 
 -export([init/1, join/3, leave/2, periodic/1, handle_message/2]).
+-export([start_seed/1]).
 
 -record(sim_strategy, {sim, me :: non_neg_integer(), n :: pos_integer(), driver :: boolean(),
                        started = false :: boolean()}).
@@ -21,9 +22,15 @@
 -define(NONE, 16#FFFFFFFF).
 
 %% The node starts in the simulator exactly once: at join/3 with its contact,
-%% or -- a seed that never joins -- at its first periodic/1 without one.
-%% (psim_join refuses a second start of a node in one round, and a full-
-%% strategy node cannot restart at all.)
+%% or -- a seed that never joins -- at init/1 when partisan_config's
+%% `sim_seed_node` is true (or later through start_seed/1).  Until then it is
+%% inert: periodic/1 and handle_message/2 answer [Myself] and start nothing,
+%% so a periodic tick that comes before the user's join (the pluggable
+%% manager schedules periodic from init, pl:363) cannot turn a joiner into a
+%% singleton.  join/3 on a node already started (a seed, or a second join)
+%% cannot be expressed in the simulator -- psim_join would restart the node,
+%% and a full-strategy node cannot restart at all -- so it raises
+%% {already_started, Me} instead of reporting a join that did not happen.
 init(_Identity) ->
     N = partisan_config:get(sim_nodes, 32),
     Me = partisan_config:get(sim_node, 0),
@@ -39,15 +46,26 @@ init(_Identity) ->
                                                   periodic_interval => 10});
                     H -> {ok, H}
                 end,
-    State = #sim_strategy{sim = Sim, me = Me, n = N,
-                          driver = partisan_config:get(sim_driver, false)},
+    State0 = #sim_strategy{sim = Sim, me = Me, n = N,
+                           driver = partisan_config:get(sim_driver, false)},
+    State = case partisan_config:get(sim_seed_node, false) of
+                true -> start_seed(State0);
+                false -> State0
+            end,
     {ok, membership(State), State}.
 
+%% a seed: the node starts alone (no contact) in the next round
+start_seed(State = #sim_strategy{started = false, sim = Sim, me = Me}) ->
+    ok = partisan_gpu_sim:join(Sim, [Me], [?NONE]),
+    State#sim_strategy{started = true};
+start_seed(State) ->
+    State.
+
 %% Strategy:join/3 at the joiner: the simulated hello/state handshake and the
-%% strategy's join happen in the next rounds of the simulator.  A second
-%% join of a running node is not forwarded (the node keeps its state).
-join(State = #sim_strategy{started = true}, _Node, _RemoteState) ->
-    {ok, membership(State), [], State};
+%% strategy's join happen in the next rounds of the simulator.  A join of a
+%% node already started is refused loudly (see the header).
+join(#sim_strategy{started = true, me = Me}, _Node, _RemoteState) ->
+    erlang:error({already_started, Me});
 join(State = #sim_strategy{sim = Sim, me = Me}, #{name := Name}, _RemoteState) ->
     ok = partisan_gpu_sim:join(Sim, [Me], [id(Name)]),
     State1 = State#sim_strategy{started = true},
@@ -63,9 +81,6 @@ leave(State = #sim_strategy{sim = Sim, me = Me}, #{name := Name}) ->
          end,
     {ok, membership(State), [], State}.
 
-periodic(State = #sim_strategy{started = false, sim = Sim, me = Me}) ->
-    ok = partisan_gpu_sim:join(Sim, [Me], [?NONE]),          % a seed: starts alone
-    periodic(State#sim_strategy{started = true});
 periodic(State = #sim_strategy{sim = Sim, driver = true}) ->
     {ok, _Stats} = partisan_gpu_sim:step(Sim, 1),
     {ok, membership(State), [], State};

@@ -23,6 +23,11 @@
 %%                                  views are cut off from the rest (a network
 %%                                  partition, DESIGN.md section 2; hv:244-246,
 %%                                  :1731-1769 floods the same TTL)
+%%                                  one partition at a time per simulator handle:
+%%                                  a second injection before the first is
+%%                                  resolved answers {error, already_partitioned}
+%%                                  (managers sharing a handle through sim_handle
+%%                                  share that one cut)
 %%   resolve_partition/1, partitions/0   hv:249-255, :1771-1797
 %%   send_message/2, forward_message/2..5, cast_message/3..5, receive_message/2
 %%                                  application traffic is not simulated (only
@@ -145,6 +150,11 @@ handle_call(partitions, _From, S = #state{partition = {Ref, Cut}}) ->
     Mine = lists:member(S#state.me, Cut),
     Peers = [{Ref, name(P)} || P <- view(S), P =/= S#state.me, lists:member(P, Cut) =/= Mine],
     {reply, {ok, Peers}, S};
+handle_call({inject_partition, _, _}, _From, S = #state{partition = {_, _}}) ->
+    %% one partition per handle: the network keeps a single cut, so a second
+    %% injection would silently replace the first (the reference accumulates
+    %% {Ref, Peer} entries per injection, hv:1766-1770)
+    {reply, {error, already_partitioned}, S};
 handle_call({inject_partition, Origin, TTL}, _From, S = #state{sim = Sim, n = N}) ->
     %% the flood of hv:1731-1769 reaches the nodes within TTL hops of Origin
     %% over active views; they form one side of a network partition

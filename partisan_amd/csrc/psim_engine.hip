@@ -939,7 +939,9 @@ struct DBuf {
     // grow to the next power of two (per-round sizes peak on broadcast
     // rounds; a 25 % step re-allocated -- 1 ms each -- for many rounds),
     // contents not kept
-    // headroom: grow to the power of two at or above want * (1 + headroom / 4)
+    // headroom: grow to the power of two at or above want * (1 + headroom / 4);
+    // headroom < 0: exactly want, rounded up to 64 MiB past 1 GiB (an
+    // up-front reservation sized against the free device memory)
     int ensure(size_t want, int headroom = 0) {
         if (want <= n) return PSIM_OK;
         static const bool trace = getenv("PSIM_TRACE_GROW") != nullptr;
@@ -947,15 +949,16 @@ struct DBuf {
             std::fprintf(stderr, "psim: grow %zu -> %zu (want) x %zu B\n", n, want, sizeof(T));
         if (p) (void)hipFree(p);
         p = nullptr; n = 0;
-        const size_t goal = want + want / 4 * (size_t)headroom;
+        const size_t goal = want + want / 4 * (size_t)(headroom > 0 ? headroom : 0);
         size_t cap = 1024;
         while (cap < goal) cap <<= 1;
         // past 1 GiB a power of two (or the caller's headroom) may waste up
         // to half: 1/8 headroom in 64 MiB steps instead (at 2^26 nodes the
         // message buffers are tens of GB)
+        if (headroom < 0) cap = want;
         if (cap * sizeof(T) > (1ull << 30)) {
             const size_t step = (64ull << 20) / sizeof(T);
-            cap = (want + want / 8 + step - 1) / step * step;
+            cap = (want + (headroom < 0 ? 0 : want / 8) + step - 1) / step * step;
         }
         if (hipMalloc(&p, cap * sizeof(T)) != hipSuccess) {
             size_t fr = 0, tot = 0;
@@ -1025,8 +1028,20 @@ int bits_for(uint64_t n) {
     return b;
 }
 
-constexpr uint64_t RESERVE_PER_NODE = 24;   // outbox slots per node reserved up front
+// Up-front reservations (the first round of a handle): a buffer that grows
+// mid-run is a hipFree + hipMalloc, and the driver clears fresh device memory
+// -- at 2^26 nodes one growth of the ~100 GB outbox took 2.3-3.1 s inside a
+// timed window (profiles/r03/e26_attrib.txt) -- so the message buffers take
+// their working size once, against the free device memory:
+//   the route's records: RCAP_RESERVE per node where that takes at most
+//   RCAP_FREE_FRAC of the free memory (else RCAP_PER_NODE, growing);
+//   the outbox: RESERVE_PER_NODE slots per node, or what is left after the
+//   route, less OUTBOX_SPARE (a growth past it still works, slowly)
+constexpr uint64_t RESERVE_PER_NODE = 32;   // outbox slots per node reserved up front
 constexpr uint64_t RCAP_PER_NODE = 4;       // initial route capacity (records) per node
+constexpr uint64_t RCAP_RESERVE = 8;        // ... reserved up front where it fits
+constexpr double RCAP_FREE_FRAC = 0.30;
+constexpr double OUTBOX_SPARE = 0.12;
 
 struct Shard {
     uint32_t idx = 0, lo = 0, n = 0;    // global shard index, owned [lo, lo + n)
@@ -1387,7 +1402,10 @@ int phase_events_prepare(psim_handle* h, Shard* s, const RoundCtl& ctl, RoundArg
     {
         KTimer t(h, s, KT_PREPARE);
         a.in_cb = s->cb.p;
-        s->pgrid = std::min<uint32_t>(grid_for(n), 512);   // grid-stride: few partials
+        // grid-stride; 4096 blocks (16 waves per CU) keep the crash rounds'
+        // dependent loads (active row -> members' flag bytes) in flight --
+        // 512 blocks left 2 waves per SIMD and took 6.8 ms at 2^26 nodes
+        s->pgrid = std::min<uint32_t>(grid_for(n), 4096);
         s->cgrid = std::min<uint32_t>(grid_for(n), h->consume_blocks);
         // one lane per possible working node (up to RELAY_MAX_BLOCKS, then grid-stride):
         // the relays are chains of dependent random loads, so latency wants lanes
@@ -1411,32 +1429,47 @@ int phase_events_prepare(psim_handle* h, Shard* s, const RoundCtl& ctl, RoundArg
         const uint64_t total = s->pin[PIN_TOTAL];
         if (total >= 0xFFFFFFFFull) return PSIM_ENOMEM;
         // the bound peaks on broadcast rounds and creeps up for many rounds:
-        // each growth (a free + malloc, ~2 ms at GB sizes) reserves 1.5x;
-        // the first round reserves RESERVE_PER_NODE slots per node instead,
-        // where that takes at most a quarter of the free device memory
+        // each growth reserves 1.5x; the first round reserves the working
+        // sizes instead (the constants above RESERVE_PER_NODE)
         uint64_t want = total + 1;
         int headroom = 2;
+        const char* rcap_init = getenv("PSIM_RCAP_INIT");   // (test hook: a small route capacity
+                                                            // exercises the regrow + reroute)
+        if (h->G == 1 && !s->rcap) {
+            s->rcap = 4096;
+            while (s->rcap < (uint64_t)n * RCAP_PER_NODE) s->rcap <<= 1;
+            if (rcap_init) s->rcap = std::max<uint64_t>(16, strtoull(rcap_init, nullptr, 10));
+        }
         if (!s->reserved) {
             s->reserved = true;
             size_t fr = 0, tot = 0;
-            const uint64_t r = (uint64_t)n * RESERVE_PER_NODE;
-            const uint64_t per_slot = sizeof(Msg) + sizeof(uint32_t);
-            if (hipMemGetInfo(&fr, &tot) == hipSuccess && r * per_slot <= fr / 4 && r > want) {
-                want = r;
-                headroom = 0;
+            if (hipMemGetInfo(&fr, &tot) == hipSuccess) {
+                const uint64_t per_rec = sizeof(Msg) + 3 * sizeof(uint32_t) + sizeof(uint2);
+                const uint64_t per_slot = sizeof(Msg) + sizeof(uint32_t);
+                // (memory the current buffers hold comes back when they regrow)
+                uint64_t avail = fr + (uint64_t)s->outbox.n * sizeof(Msg) + (uint64_t)s->okey.n * 4;
+                if (h->G == 1 && !rcap_init) {
+                    const uint64_t rc = (uint64_t)n * RCAP_RESERVE;
+                    if (rc > s->rcap && (double)(rc * per_rec) <= RCAP_FREE_FRAC * (double)avail) s->rcap = rc;
+                    const uint64_t held = s->rcap * per_rec;
+                    avail = avail > held ? avail - held : 0;
+                }
+                const uint64_t r = std::min<uint64_t>((uint64_t)n * RESERVE_PER_NODE,
+                                                      (uint64_t)((1.0 - OUTBOX_SPARE) * (double)avail) / per_slot);
+                if (r > want) {
+                    want = r;
+                    headroom = -1;
+                    s->outbox.release();            // (its memory is part of avail)
+                    s->okey.release();
+                }
             }
+        } else if (want > s->outbox.n && s->outbox.n * sizeof(Msg) > (1ull << 30)) {
+            std::fprintf(stderr, "psim: round %llu: outbox grows past its reservation (%zu -> %llu slots)\n",
+                         (unsigned long long)h->round, s->outbox.n, (unsigned long long)want);
         }
         TRY(s->outbox.ensure(want, headroom));
         TRY(s->okey.ensure(want, headroom));
-        if (h->G == 1) {            // the route runs without a host sync, checking its capacity
-            if (!s->rcap) {
-                s->rcap = 4096;
-                while (s->rcap < (uint64_t)n * RCAP_PER_NODE) s->rcap <<= 1;
-                // (test hook: a small start capacity exercises the regrow + reroute)
-                if (const char* e = getenv("PSIM_RCAP_INIT")) s->rcap = std::max<uint64_t>(16, strtoull(e, nullptr, 10));
-            }
-            TRY(route_buffers(s, s->m_in == 0));
-        }
+        if (h->G == 1) TRY(route_buffers(s, s->m_in == 0));   // the route checks its capacity on the device
     }
     a.in_beg = s->in_beg.p;
     a.desc = s->desc.p; a.n_alist = s->d_nact.p;

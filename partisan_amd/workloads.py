@@ -43,6 +43,36 @@ def doubling_join(n_nodes, seed, max_per_round=MAX_JOINS_PER_ROUND):
     return sched
 
 
+SURVEY_RAMP = 64
+
+
+def survey_join(n_nodes, seed, ramp=SURVEY_RAMP):
+    """Config C's bootstrap as SURVEY.md section 8(d) defines it: node i
+    joins at round floor(ramp * i / N), each joiner contacting a uniformly
+    drawn node among those started in an earlier round.  Node 0 is the seed
+    (started alone at round 0); the rest of round 0's batch joins node 0.
+    Start rounds -- and so the shuffle and promotion timer phases -- spread
+    evenly over the ramp, unlike the doubling ramp, which starts half the
+    overlay in its last round."""
+    rng = _rng(seed, 3)
+    ids = np.arange(n_nodes, dtype=np.uint64)
+    rnd = (ids * ramp // n_nodes).astype(np.int64)
+    sched = [(0, np.array([0], np.uint32), np.array([NONE], np.uint32))]
+    for r in range(ramp):
+        lo = int(np.searchsorted(rnd, r, "left"))
+        hi = int(np.searchsorted(rnd, r, "right"))
+        if r == 0:
+            lo = 1
+        if hi <= lo:
+            continue
+        batch = np.arange(lo, hi, dtype=np.uint32)
+        first = int(np.searchsorted(rnd, r, "left"))
+        contacts = (np.zeros(hi - lo, np.uint32) if r == 0 else
+                    rng.integers(0, first, size=hi - lo, dtype=np.uint64).astype(np.uint32))
+        sched.append((r, batch, contacts))
+    return sched
+
+
 def star_join(n_nodes, at_round=1):
     """Hot-spot case: every node joins node 0 in the same round."""
     ids = np.arange(1, n_nodes, dtype=np.uint32)
