@@ -38,7 +38,7 @@ S_MSG = 64                      # message record bytes
 CHECK_NODES = 1 << 14           # the built-in sharding check
 CHECK_ROUNDS = 90
 SCHEDULE_VERSION = 2            # bumps when the event schedule of a run changes (PMC keys)
-OVF_KINDS = ("idmap", "pt_outstanding", "pt_sets_roots_msgs", "strategy")   # PSIM_OVF_*
+OVF_KINDS = ("idmap", "pt_outstanding", "pt_sets_roots_msgs", "strategy", "conn")   # PSIM_OVF_*
 ALG_FORMULA = ("B = N_proc * 2 * 416 + M_in * 64 + M_out * 68 per round, N_proc = nodes with work "
                "(stats nodes_processed), M_in / M_out = delivered / emitted records.  Departs from "
                "SURVEY 8(d) (every node's 416 B read, touched nodes' written, 32-B Plumtree records): "
@@ -505,7 +505,7 @@ def main():
     if world > 1:
         cfg.shard_world, cfg.shard_rank = world, rank
     sim = Simulator(cfg, comm=comm)
-    ovf_run = np.zeros(4, np.uint64)          # overflows by table over every round of the run
+    ovf_run = np.zeros(len(OVF_KINDS), np.uint64)          # overflows by table over every round of the run
 
     def step(k):
         s_ = sim.step(k)

@@ -64,7 +64,7 @@
 extern "C" {
 #endif
 
-#define PSIM_ABI_VERSION 7
+#define PSIM_ABI_VERSION 8
 
 /* error codes */
 #define PSIM_OK 0
@@ -75,6 +75,7 @@ extern "C" {
 #define PSIM_ERANGE -5      /* node id out of range                   */
 #define PSIM_ECOMM -6       /* RCCL / transport error                 */
 #define PSIM_EUNSUPPORTED -7
+#define PSIM_ECAPACITY -8   /* cfg.strict: a fixed table overflowed this round */
 
 /* message types (the record `type` field; also stats indices) */
 enum psim_msg_type {
@@ -128,6 +129,18 @@ enum psim_pl_msg_type {
 #define PSIM_PASSIVE_CAP 32
 #define PSIM_IDMAP_CAP 64   /* sent_message_map / recv_message_map slots */
 #define PSIM_PT_MEMBERS_CAP 8
+/* Connections of a node's HyParView manager beyond its active view
+ * (SURVEY App. A Q11): partisan_util:maybe_connect/2 opens one before every
+ * send and only disconnect/2 (hyparview:1237-1258) or the peer's death
+ * (EXIT, :609-654) closes it, so a shuffle terminal keeps the connection to
+ * its Sender (:1127-1131), a neighbor_request receiver to a rejected
+ * requester (:987), a promoting node to the passive peer it asked (:1701),
+ * a joiner to its contact (:506).  The table holds those lingering peers and,
+ * with PSIM_CONN_DOWN set, the rare active members whose connection a
+ * neighbor_rejected closed (:1063) -- an add to a full table counts an
+ * overflow (PSIM_OVF_CONN) and is dropped. */
+#define PSIM_CONN_CAP 8
+#define PSIM_CONN_DOWN 0x80000000u
 #define PSIM_PT_OUT_CAP 64
 #define PSIM_EXCHANGE_CAP 8
 /* Plumtree roots a node keeps per-root eager/lazy sets for at once
@@ -148,7 +161,8 @@ enum psim_pl_msg_type {
 #define PSIM_OVF_PT_OUT 1    /* Plumtree outstanding IHAVE entries (the new entry dropped) */
 #define PSIM_OVF_PT 2        /* Plumtree members, per-root sets, root slots, retired message ids */
 #define PSIM_OVF_STRATEGY 3  /* pluggable: SCAMP views, full-membership snapshot payload */
-#define PSIM_OVF_NKINDS 4
+#define PSIM_OVF_CONN 4      /* HyParView connections beyond the active view (the new one dropped) */
+#define PSIM_OVF_NKINDS 5
 
 typedef struct psim_config {
     uint32_t abi_version;        /* must be PSIM_ABI_VERSION */
@@ -183,7 +197,11 @@ typedef struct psim_config {
     uint32_t scamp_c;            /* scamp_c, ?SCAMP_C_VALUE = 5 (partisan.hrl:31); <= 64 */
     uint32_t fanout;             /* full: 0 = gossip to every member (reference);
                                     k > 0 = k uniformly drawn members (config B extension); <= 64 */
-    uint32_t reserved[3];
+    uint32_t strict;             /* 0: a fixed-table overflow is counted (stats.overflow_by) and the
+                                    round goes on; 1: psim_step fails with PSIM_ECAPACITY after the
+                                    round in which any overflow happened (e.g. a fifth live Plumtree
+                                    root at a node, or a 65th live message id) */
+    uint32_t reserved[2];
 } psim_config;
 
 typedef struct psim_round_stats {
@@ -207,7 +225,8 @@ typedef struct psim_round_stats {
 
 /* Canonical per-node view (inspection; unused slots zero). */
 typedef struct psim_node_view {
-    uint32_t up, epoch, start_round, pad0;
+    uint32_t up, epoch, start_round;
+    uint32_t conn_n;                         /* entries of conn[] */
     uint64_t rng_ctr;
     uint32_t act_n, pas_n;
     uint32_t act[PSIM_ACTIVE_CAP];           /* sets:to_list order, self included */
@@ -225,6 +244,9 @@ typedef struct psim_node_view {
     uint32_t pt_out_peer[PSIM_PT_OUT_CAP], pt_out_msg[PSIM_PT_OUT_CAP], pt_out_round[PSIM_PT_OUT_CAP];
     uint64_t have;                           /* delivered: bit (msg id mod PSIM_MSG_SLOTS) */
     uint32_t trk_round, trk_hop;
+    /* connections beyond the active view (lingering peers), and active
+     * members without one (| PSIM_CONN_DOWN), in insertion order */
+    uint32_t conn[PSIM_CONN_CAP];
 } psim_node_view;
 
 /* Per-node state of a PLUGGABLE handle (inspection; unused slots zero). */
@@ -371,6 +393,13 @@ int psim_get_histograms(psim_handle *h, psim_histograms *out);
  * follow are identical to the original's (HyParView handles). */
 int psim_snapshot(psim_handle *h, void *buf, size_t cap, size_t *need);
 int psim_restore(psim_handle *h, const void *buf, size_t size);
+
+/* The live Plumtree message slots (plumtree_backend's ETS set keyed by
+ * message id, :140-167): ids[k] = the message id owning slot k (PSIM_NONE =
+ * free) and roots[k] its root (node_spec identity, | PSIM_MAP_BIT), for
+ * k < PSIM_MSG_SLOTS; cap must be >= PSIM_MSG_SLOTS.  A node's delivery bit
+ * k (psim_node_view.have) answers is_stale/1 for ids[k] only. */
+int psim_get_msg_slots(psim_handle *h, uint32_t *ids, uint32_t *roots, size_t cap);
 
 /* Per-kernel device time (ms) accumulated over the last psim_step call:
  * names[i] is a static string; returns the number of entries. */

@@ -72,6 +72,10 @@ typedef struct node {
     uint32_t out_peer[PSIM_PT_OUT_CAP], out_msg[PSIM_PT_OUT_CAP], out_round[PSIM_PT_OUT_CAP], out_n;
     uint64_t have;                  /* plumtree_backend ETS: bit (msg id mod PSIM_MSG_SLOTS) */
     uint32_t trk_round, trk_hop;
+    /* the manager's connections (partisan_peer_service_connections) beyond
+     * the active view: lingering peers, and | PSIM_CONN_DOWN the active
+     * members without one; insertion order */
+    uint32_t conn[PSIM_CONN_CAP], conn_n;
 } node;
 
 typedef struct omsg {
@@ -308,20 +312,67 @@ static void emit(ctx *c, uint32_t dst, uint32_t type, uint32_t ttl, uint32_t a0,
     c->h->st->digest += msg_hash(&m);
 }
 
-/* maybe_connect + find: the connection attempt succeeds iff the peer's
- * manager is running and no network partition separates the two
- * (partisan_util.erl:75-134; partition model DESIGN.md). */
+/* A connection attempt (partisan_util:maybe_connect/2, util.erl:75-134)
+ * succeeds iff the peer's manager is running and no network partition
+ * separates the two (partition model DESIGN.md). */
 static int connect_ok(ctx *c, uint32_t dst) {
     struct psim_handle *h = c->h;
     if (dst >= h->N || dst == c->me) return 0;
     return h->nodes[dst].up && h->part[dst] == h->part[c->me];
 }
 
-/* do_send_message/3 after maybe_connect (hyparview:1274-1343): on success
- * partisan_util:dispatch_pid/1 draws rand:uniform(1) (util:190-195). */
+/* ------------------------------------------------------ connections -- */
+/* The Connections dict of the manager as the active view
+ * plus the table of node.conn: a peer outside the active view is connected
+ * iff it is in the table; an active member is connected unless the table
+ * holds it | PSIM_CONN_DOWN.  maybe_connect/2 opens a connection before every
+ * HyParView send; only disconnect/2 (hyparview:1237-1258) and the peer's
+ * death (EXIT, :609-654) close one; leaving the active view always goes
+ * through one of those. */
+static int conn_find(const node *s, uint32_t e) {
+    for (uint32_t i = 0; i < s->conn_n; i++)
+        if (s->conn[i] == e) return (int)i;
+    return -1;
+}
+static void conn_add(ctx *c, uint32_t e) {
+    node *s = c->s;
+    if (conn_find(s, e) >= 0) return;
+    if (s->conn_n >= PSIM_CONN_CAP) { ovf(c, PSIM_OVF_CONN); return; }
+    s->conn[s->conn_n++] = e;
+}
+static void conn_del(node *s, uint32_t e) {
+    int i = conn_find(s, e);
+    if (i < 0) return;
+    for (uint32_t j = (uint32_t)i; j + 1 < s->conn_n; j++) s->conn[j] = s->conn[j + 1];
+    s->conn[--s->conn_n] = 0;
+}
+/* partisan_peer_service_connections:find/2 succeeds */
+static int conn_has(ctx *c, uint32_t p) {
+    node *s = c->s;
+    if (list_member(s->act, s->act_n, p)) return conn_find(s, p | PSIM_CONN_DOWN) < 0;
+    return conn_find(s, p) >= 0;
+}
+/* partisan_util:maybe_connect/2: 1 iff connected afterwards */
+static int maybe_connect(ctx *c, uint32_t p) {
+    if (!connect_ok(c, p)) return 0;
+    if (list_member(c->s->act, c->s->act_n, p)) conn_del(c->s, p | PSIM_CONN_DOWN);
+    else conn_add(c, p);
+    return 1;
+}
+/* disconnect/2 (hyparview:1237-1258) */
+static void disconnect(ctx *c, uint32_t p) {
+    if (list_member(c->s->act, c->s->act_n, p)) conn_add(c, p | PSIM_CONN_DOWN);
+    else conn_del(c->s, p);
+}
+
+/* maybe_connect, then do_send_message/3 (hyparview:1274-1343): on success
+ * partisan_util:dispatch_pid/1 draws rand:uniform(1) (util:190-195).  Every
+ * HyParView send of the reference is preceded by a maybe_connect of its
+ * destination (:506, :594, :721, :743, :784, :830, :878, :906, :987, :1110,
+ * :1127, :1493, :1701). */
 static int hv_send(ctx *c, uint32_t dst, uint32_t type, uint32_t ttl, uint32_t a0, uint32_t a1,
                    const uint32_t *ex, uint32_t nex) {
-    if (!connect_ok(c, dst)) { c->h->st->send_fail++; return 0; }
+    if (!maybe_connect(c, dst)) { c->h->st->send_fail++; return 0; }
     (void)uniform_n(c, 1);
     emit(c, dst, type, ttl, a0, a1, 0, ex, nex);
     return 1;
@@ -409,19 +460,27 @@ static void drop_random_active(ctx *c) {
     uint32_t p = select_random(c, s->act, s->act_n, omit, 1);
     if (p == PSIM_NONE) return;
     set_del(s->act, &s->act_n, p);
+    conn_del(s, p | PSIM_CONN_DOWN);
     add_to_passive(c, p);
     uint32_t nid = next_id(c, p);
     map_store(c, s->sent_peer, s->sent_id, &s->sent_n, &s->sent_head, p, nid);
-    hv_send(c, p, PSIM_MSG_DISCONNECT, 0, nid, 0, NULL, 0);
+    hv_send(c, p, PSIM_MSG_DISCONNECT, 0, nid, 0, NULL, 0);   /* maybe_connect (:1493), send */
+    disconnect(c, p);                                         /* (:1506) */
 }
 
-/* add_to_active_view/3, hyparview:1371-1420 (tag/reserved ignored) */
+/* add_to_active_view/3, hyparview:1371-1420 (tag/reserved ignored).  The
+ * connection the caller opened (every caller but neighbor_accepted runs
+ * maybe_connect first) moves with the peer into the active view; without one
+ * the peer is an active member without a connection. */
 static void add_to_active(ctx *c, uint32_t p) {
     node *s = c->s;
     if (p == c->me || list_member(s->act, s->act_n, p)) return;
     set_del(s->pas, &s->pas_n, p);
     if (s->act_n >= c->h->cfg.max_active_size) drop_random_active(c);
+    int had = conn_find(s, p) >= 0;
+    conn_del(s, p);
     set_add(s->act, &s->act_n, p);
+    if (!had) conn_add(c, p | PSIM_CONN_DOWN);
 }
 
 /* [Myself] ++ select_random_sublist(Active, k_active) ++
@@ -587,12 +646,14 @@ static void pt_update(ctx *c, uint32_t from, uint32_t root, int to_eager) {
     }
 }
 
-/* send/3 (plumtree:633-638) -> cast_message -> forward_message: succeeds only
- * over an existing connection of this node's manager. */
+/* send/3 (plumtree:633-638) -> cast_message -> forward_message
+ * (hyparview:441-460) -> do_send_message/4 without maybe_connect: succeeds
+ * only over an existing connection of this node's manager -- an active member
+ * or a lingering peer (App. A Q11) -- to a running peer in the same partition
+ * group. */
 static int pt_conn(ctx *c, uint32_t ident) {
     uint32_t id = ident & ~PSIM_MAP_BIT;
-    node *s = c->s;
-    return !(id == c->me || !list_member(s->act, s->act_n, id) || !c->h->nodes[id].up ||
+    return !(id == c->me || id >= c->h->N || !conn_has(c, id) || !c->h->nodes[id].up ||
              c->h->part[id] != c->h->part[c->me]);
 }
 
@@ -719,7 +780,7 @@ static void hv_handle(ctx *c, const omsg *m) {
     case PSIM_MSG_JOIN: {                         /* hyparview:703-771 */
         uint32_t p = m->src, pe = m->a0;
         if (addable_epoch(c, pe, p) && !list_member(s->act, s->act_n, p)) {
-            if (connect_ok(c, p)) {
+            if (maybe_connect(c, p)) {                /* :721-723 */
                 add_to_active(c, p);
                 hv_send(c, p, PSIM_MSG_NEIGHBOR, 0, current_id(c, p), 0, NULL, 0);
                 uint32_t omit[2] = {me, p}, peers[PSIM_ACTIVE_CAP];
@@ -733,14 +794,14 @@ static void hv_handle(ctx *c, const omsg *m) {
     }
     case PSIM_MSG_NEIGHBOR: {                     /* hyparview:774-805 */
         uint32_t p = m->src;
-        if (addable_id(c, m->a0, p) && connect_ok(c, p)) add_to_active(c, p);
+        if (addable_id(c, m->a0, p) && maybe_connect(c, p)) add_to_active(c, p);   /* :784-786 */
         notify(c);
         break;
     }
     case PSIM_MSG_FORWARD_JOIN: {                 /* hyparview:808-923 */
         uint32_t p = m->a0, pe = m->a1, ttl = m->ttl, sender = m->src;
         if (ttl == 0 || s->act_n == 1) {
-            if (addable_epoch(c, pe, p) && !list_member(s->act, s->act_n, p) && connect_ok(c, p)) {
+            if (addable_epoch(c, pe, p) && !list_member(s->act, s->act_n, p) && maybe_connect(c, p)) {
                 add_to_active(c, p);
                 hv_send(c, p, PSIM_MSG_NEIGHBOR, 0, current_id(c, p), 0, NULL, 0);
             }
@@ -754,7 +815,7 @@ static void hv_handle(ctx *c, const omsg *m) {
             uint32_t r = select_random(c, act0, n0, omit, 3);
             if (r == PSIM_NONE) {
                 if (addable_epoch(c, pe, p) && !list_member(act0, n0, p)) {
-                    if (connect_ok(c, p)) {
+                    if (maybe_connect(c, p)) {        /* :878-880 */
                         add_to_active(c, p);
                         hv_send(c, p, PSIM_MSG_NEIGHBOR, 0, current_id(c, p), 0, NULL, 0);
                     } else {
@@ -778,8 +839,10 @@ static void hv_handle(ctx *c, const omsg *m) {
         uint32_t pas0[PSIM_PASSIVE_CAP], np0 = s->pas_n;
         memcpy(pas0, s->pas, sizeof pas0);
         set_del(s->act, &s->act_n, p);
+        conn_del(s, p | PSIM_CONN_DOWN);
         add_to_passive(c, p);
         map_store(c, s->recv_peer, s->recv_id, &s->recv_n, &s->recv_head, p, d);
+        disconnect(c, p);                         /* :952 */
         if (s->act_n == 1) {
             uint32_t omit[2] = {me, p};
             move_to_active(c, select_random(c, pas0, np0, omit, 2));
@@ -789,9 +852,10 @@ static void hv_handle(ctx *c, const omsg *m) {
     case PSIM_MSG_NEIGHBOR_REQUEST: {             /* hyparview:975-1053 */
         uint32_t p = m->src, d = m->a0;
         uint32_t ack[PSIM_EXCHANGE_CAP];
+        int conn = maybe_connect(c, p);           /* :987, kept in both branches */
         uint32_t nack = build_exchange(c, ack);
         if (addable_id(c, d, p)) {               /* priority is always high (:1706) */
-            if (connect_ok(c, p)) {
+            if (conn) {
                 hv_send(c, p, PSIM_MSG_NEIGHBOR_ACCEPTED, 0, current_id(c, p), 0, ack, nack);
                 add_to_active(c, p);
             }
@@ -803,6 +867,7 @@ static void hv_handle(ctx *c, const omsg *m) {
         break;
     }
     case PSIM_MSG_NEIGHBOR_REJECTED:              /* hyparview:1056-1067 */
+        disconnect(c, m->src);                    /* :1063 */
         merge_exchange(c, m->ex, m->nex);
         break;
     case PSIM_MSG_NEIGHBOR_ACCEPTED:              /* hyparview:1070-1089 */
@@ -851,9 +916,16 @@ static void process_node(struct psim_handle *h, uint32_t n) {
     int origin = h->origin[n] != 0 && h->cfg.plumtree;
     int lazy_due = h->cfg.plumtree && timer_due(h->cfg.lazy_tick_period, r, s->start_round);
     int lazy = lazy_due && s->out_n > 0;
-    uint32_t exits[PSIM_ACTIVE_CAP], nexit = 0;
+    /* EXIT at every holder of a connection to a peer that crashed this round
+     * (App. A Q11): the connected active members in to_list order, then the
+     * lingering peers in table order (their EXITs only edit the passive view
+     * and the table) */
+    uint32_t exits[PSIM_ACTIVE_CAP + PSIM_CONN_CAP], nexit = 0;
     for (uint32_t i = 0; i < s->act_n; i++)
-        if (s->act[i] != n && h->crashed_now[s->act[i]]) exits[nexit++] = s->act[i];
+        if (s->act[i] != n && h->crashed_now[s->act[i]] && conn_find(s, s->act[i] | PSIM_CONN_DOWN) < 0)
+            exits[nexit++] = s->act[i];
+    for (uint32_t i = 0; i < s->conn_n; i++)
+        if (!(s->conn[i] & PSIM_CONN_DOWN) && h->crashed_now[s->conn[i]]) exits[nexit++] = s->conn[i];
     int joining = (s->start_round == r && s->join_contact != PSIM_NONE);
     if (!(e > b || joining || nexit || promo_work || shuf || origin || lazy)) return;
     h->st->nodes_processed++;
@@ -861,10 +933,12 @@ static void process_node(struct psim_handle *h, uint32_t n) {
     /* handle_cast({join, Peer}), hyparview:500-515 */
     if (joining) hv_send(&c, s->join_contact, PSIM_MSG_JOIN, 0, s->epoch, 0, NULL, 0);
 
-    /* handle_info({'EXIT', ..}), hyparview:609-654 */
+    /* handle_info({'EXIT', ..}), hyparview:609-654: the connection is pruned,
+     * the peer leaves the passive view, and the active view with a promotion */
     for (uint32_t i = 0; i < nexit; i++) {
         uint32_t d = exits[i];
         h->st->exits++;
+        conn_del(s, d);
         if (list_member(s->pas, s->pas_n, d)) set_del(s->pas, &s->pas_n, d);
         if (list_member(s->act, s->act_n, d)) {
             set_del(s->act, &s->act_n, d);
@@ -1453,7 +1527,7 @@ int orc_create(const psim_config *cfg, struct psim_handle **out) {
         cfg->max_passive_size > 30 || 1 + cfg->k_active + cfg->k_passive > PSIM_EXCHANGE_CAP ||
         cfg->arwl > 255 || cfg->prwl > 255 || cfg->manager > PSIM_MANAGER_PLUGGABLE ||
         cfg->strategy > PSIM_STRATEGY_SCAMP_V2 || cfg->scamp_c < 1 || cfg->scamp_c > 64 ||
-        cfg->fanout > 64)
+        cfg->fanout > 64 || cfg->strict > 1)
         return PSIM_EINVAL;
     int full = cfg->manager == PSIM_MANAGER_PLUGGABLE && cfg->strategy == PSIM_STRATEGY_FULL;
     if (full && cfg->shard_world > 1) return PSIM_EUNSUPPORTED;   /* payloads are shard-local */
@@ -1662,7 +1736,11 @@ int orc_broadcast(struct psim_handle *h, uint32_t root, uint32_t msg_id) {
 
 int orc_step(struct psim_handle *h, uint32_t n_rounds, psim_round_stats *stats) {
     psim_round_stats tmp;
-    for (uint32_t i = 0; i < n_rounds; i++) run_round(h, stats ? &stats[i] : &tmp);
+    for (uint32_t i = 0; i < n_rounds; i++) {
+        psim_round_stats *st = stats ? &stats[i] : &tmp;
+        run_round(h, st);
+        if (h->cfg.strict && st->overflow) return PSIM_ECAPACITY;   /* cfg.strict: fail loudly */
+    }
     return PSIM_OK;
 }
 
@@ -1695,7 +1773,16 @@ int orc_get_nodes(struct psim_handle *h, uint32_t first, uint32_t count, psim_no
         memcpy(v->pt_out_msg, s->out_msg, sizeof v->pt_out_msg);
         memcpy(v->pt_out_round, s->out_round, sizeof v->pt_out_round);
         v->have = s->have; v->trk_round = s->trk_round; v->trk_hop = s->trk_hop;
+        v->conn_n = s->conn_n;
+        memcpy(v->conn, s->conn, sizeof v->conn);
     }
+    return PSIM_OK;
+}
+
+/* psim_get_msg_slots: the live message slots (plumtree_backend's ETS set) */
+int orc_get_msg_slots(struct psim_handle *h, uint32_t *ids, uint32_t *roots, size_t cap) {
+    if (!h || !ids || !roots || cap < PSIM_MSG_SLOTS) return PSIM_EINVAL;
+    for (int k = 0; k < PSIM_MSG_SLOTS; k++) { ids[k] = h->slot_msg[k]; roots[k] = h->slot_root[k]; }
     return PSIM_OK;
 }
 

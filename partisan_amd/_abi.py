@@ -8,12 +8,14 @@ import ctypes as C
 
 import numpy as np
 
-PSIM_ABI_VERSION = 7
+PSIM_ABI_VERSION = 8
 PSIM_MAP_BIT = 0x80000000
 PSIM_NONE = 0xFFFFFFFF
 ACTIVE_CAP, PASSIVE_CAP, IDMAP_CAP = 8, 32, 64
 PT_MEMBERS_CAP, PT_SET_POOL, PT_OUT_CAP, EXCHANGE_CAP = 8, 64, 64, 8
 PT_ROOTS, MSG_SLOTS = 4, 64
+CONN_CAP, CONN_DOWN = 8, 0x80000000
+OVF_NKINDS = 5
 NTYPES = 16
 SVIEW_CAP = 128
 MANAGER_HYPARVIEW, MANAGER_PLUGGABLE = 0, 1
@@ -32,6 +34,7 @@ PT_TYPES = list(range(9, 14))
 ERRORS = {
     0: "PSIM_OK", -1: "PSIM_EINVAL", -2: "PSIM_ENOMEM", -3: "PSIM_EDEVICE",
     -4: "PSIM_ESTATE", -5: "PSIM_ERANGE", -6: "PSIM_ECOMM", -7: "PSIM_EUNSUPPORTED",
+    -8: "PSIM_ECAPACITY",
 }
 
 
@@ -48,7 +51,8 @@ class PsimConfig(C.Structure):
         ("shard_world", C.c_uint32), ("comm_id", C.c_void_p),
         ("max_msgs_per_round", C.c_uint64),
         ("manager", C.c_uint32), ("strategy", C.c_uint32), ("periodic_interval", C.c_uint32),
-        ("scamp_c", C.c_uint32), ("fanout", C.c_uint32), ("reserved", C.c_uint32 * 3),
+        ("scamp_c", C.c_uint32), ("fanout", C.c_uint32), ("strict", C.c_uint32),
+        ("reserved", C.c_uint32 * 2),
     ]
 
 
@@ -58,7 +62,7 @@ class PsimRoundStats(C.Structure):
         ("delivered", C.c_uint64 * NTYPES), ("dropped", C.c_uint64),
         ("nodes_up", C.c_uint64), ("nodes_processed", C.c_uint64), ("exits", C.c_uint64),
         ("send_fail", C.c_uint64), ("first_deliveries", C.c_uint64), ("overflow", C.c_uint64),
-        ("digest", C.c_uint64), ("state_bytes", C.c_uint64), ("overflow_by", C.c_uint64 * 4),
+        ("digest", C.c_uint64), ("state_bytes", C.c_uint64), ("overflow_by", C.c_uint64 * OVF_NKINDS),
         ("omitted", C.c_uint64),
     ]
 
@@ -66,7 +70,7 @@ class PsimRoundStats(C.Structure):
 class PsimNodeView(C.Structure):
     _fields_ = [
         ("up", C.c_uint32), ("epoch", C.c_uint32), ("start_round", C.c_uint32),
-        ("pad0", C.c_uint32), ("rng_ctr", C.c_uint64),
+        ("conn_n", C.c_uint32), ("rng_ctr", C.c_uint64),
         ("act_n", C.c_uint32), ("pas_n", C.c_uint32),
         ("act", C.c_uint32 * ACTIVE_CAP), ("pas", C.c_uint32 * PASSIVE_CAP),
         ("sent_n", C.c_uint32), ("sent_head", C.c_uint32),
@@ -82,6 +86,7 @@ class PsimNodeView(C.Structure):
         ("pt_out_peer", C.c_uint32 * PT_OUT_CAP), ("pt_out_msg", C.c_uint32 * PT_OUT_CAP),
         ("pt_out_round", C.c_uint32 * PT_OUT_CAP),
         ("have", C.c_uint64), ("trk_round", C.c_uint32), ("trk_hop", C.c_uint32),
+        ("conn", C.c_uint32 * CONN_CAP),
     ]
 
 
@@ -140,6 +145,7 @@ SIGNATURES = {
     "get_member_bits": (C.c_int, [_H, C.c_uint32, _P32, C.c_size_t]),
     "get_delivery": (C.c_int, [_H, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint8), _P32, _P32]),
     "get_histograms": (C.c_int, [_H, C.POINTER(PsimHistograms)]),
+    "get_msg_slots": (C.c_int, [_H, _P32, _P32, C.c_size_t]),
 }
 # symbols only the GPU library exports
 GPU_ONLY = {

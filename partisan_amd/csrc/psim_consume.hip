@@ -79,8 +79,13 @@ struct Wv {
     bool maps, pt, maps_dirty, pt_dirty;
     uint64_t obase;
     uint32_t seq;
-    uint32_t CV, CF;     // connection cache: ids of Passive (lanes 0-31) and Active
-                         // (32-39) at node start; CF = flags | part << 8 of each
+    uint32_t CV, CF;     // connection cache: ids of Passive (lanes 0-31), Active (32-39)
+                         // and the connection table (40-47) at node start; CF = flags |
+                         // part << 8 of each
+    uint32_t CN;         // the connection table (lanes 0 .. conn_n - 1): lingering peers, and
+                         // | PSIM_CONN_DOWN the active members without a connection
+    uint32_t conn_n, conn_dn;   // its entries, and those marked PSIM_CONN_DOWN
+    bool cn_dirty;
     uint64_t digest;     // per-lane partial: lane j sums the hashes of record word j
     uint32_t SC;         // per-lane stats counter: lane k counts stats slot k (< NST)
     // draw cache: lane l holds the 58-bit draw of counter dc_base + l, filled
@@ -341,11 +346,56 @@ DEV bool connect_ok(const Wv& w, uint32_t dst) {
     return (v & F_UP) && (v >> 8) == w.mypart;
 }
 
-// do_send_message/3 (hv:1274-1343); success draws rand:uniform(1) in
-// partisan_util:dispatch_pid/1 (util:190-195), always exactly one value
+// -------------------------------------------------------- connections --
+// The manager's Connections dict (the oracle's conn_*):
+// the active view plus the table CN -- lingering peers outside the active
+// view, and | PSIM_CONN_DOWN the active members without a connection.
+// maybe_connect/2 opens one before every HyParView send; only disconnect/2
+// (hv:1237-1258) and the peer's death (EXIT, hv:609-654) close one.
+DEV int conn_find(const Wv& w, uint32_t e) { return idx_of(w.CN, w.conn_n, e); }
+DEV void conn_add(Wv& w, uint32_t e) {
+    if (conn_find(w, e) >= 0) return;
+    if (w.conn_n >= PSIM_CONN_CAP) { ovf(w, PSIM_OVF_CONN); return; }
+    w.CN = lane_id() == w.conn_n ? e : w.CN;
+    w.conn_n++;
+    w.conn_dn += (e & PSIM_CONN_DOWN) ? 1u : 0u;
+    w.cn_dirty = true;
+}
+DEV void conn_del(Wv& w, uint32_t e) {
+    const int k = conn_find(w, e);
+    if (k < 0) return;
+    vdel(w.CN, w.conn_n, (uint32_t)k);
+    w.conn_dn -= (e & PSIM_CONN_DOWN) ? 1u : 0u;
+    w.cn_dirty = true;
+}
+// partisan_peer_service_connections:find/2 succeeds
+DEV bool conn_has(const Wv& w, uint32_t p) {
+    if (has(w.A, w.act_n, p)) return !w.conn_dn || conn_find(w, p | PSIM_CONN_DOWN) < 0;
+    return w.conn_n && conn_find(w, p) >= 0;
+}
+// partisan_util:maybe_connect/2 (util.erl:75-134): connected afterwards
+DEV bool maybe_connect(Wv& w, uint32_t p) {
+    if (!connect_ok(w, p)) return false;
+    if (has(w.A, w.act_n, p)) {
+        if (w.conn_dn) conn_del(w, p | PSIM_CONN_DOWN);
+    } else {
+        conn_add(w, p);
+    }
+    return true;
+}
+// disconnect/2 (hv:1237-1258)
+DEV void disconnect(Wv& w, uint32_t p) {
+    if (has(w.A, w.act_n, p)) conn_add(w, p | PSIM_CONN_DOWN);
+    else if (w.conn_n) conn_del(w, p);
+}
+
+// maybe_connect, then do_send_message/3 (hv:1274-1343); success draws
+// rand:uniform(1) in partisan_util:dispatch_pid/1 (util:190-195), always
+// exactly one value.  Every HyParView send of the reference is preceded by
+// a maybe_connect of its destination.
 DEV void hv_send(Wv& w, uint32_t dst, uint32_t type, uint32_t ttl, uint32_t a0, uint32_t a1,
                  uint32_t EX, uint32_t nex) {
-    if (!connect_ok(w, dst)) { st_add(w, ST_FAIL, 1); return; }
+    if (!maybe_connect(w, dst)) { st_add(w, ST_FAIL, 1); return; }
     w.rng++;
     emit(w, dst, type, ttl, a0, a1, 0, EX, nex);
 }
@@ -435,19 +485,27 @@ DEV void drop_random_active(Wv& w) {                     // hv:1467-1512
     uint32_t p = select_random(w, w.A, w.act_n, w.me, w.me, w.me);
     if (p == NONE) return;
     vdel_val(w.A, w.act_n, p);
+    if (w.conn_dn) conn_del(w, p | PSIM_CONN_DOWN);
     w.vd |= 1u;
     add_to_passive(w, p);
     uint32_t nid = next_id(w, p);
     map_store(w, w.SP, w.SI, w.sent_n, w.sent_head, p, nid);
-    hv_send(w, p, PSIM_MSG_DISCONNECT, 0, nid, 0, 0, 0);
+    hv_send(w, p, PSIM_MSG_DISCONNECT, 0, nid, 0, 0, 0);   // maybe_connect (hv:1493), send
+    disconnect(w, p);                                     // (hv:1506)
 }
 
+// (the connection the caller opened -- every caller but neighbor_accepted
+// runs maybe_connect first -- moves with the peer into the active view;
+// without one the peer is an active member without a connection)
 DEV void add_to_active(Wv& w, uint32_t p) {              // hv:1371-1420
     if (p == w.me || has(w.A, w.act_n, p)) return;
     if (vdel_val(w.P, w.pas_n, p)) w.vd |= 2u;
     if (w.act_n >= kargs().max_active) drop_random_active(w);
+    const bool had = w.conn_n && conn_find(w, p) >= 0;
+    if (had) conn_del(w, p);
     view_add(w.A, w.act_n, p);
     w.vd |= 1u;
+    if (!had) conn_add(w, p | PSIM_CONN_DOWN);
 }
 
 // usort([Myself] ++ sublist(Active, k_active) ++ sublist(Passive, k_passive))
@@ -673,10 +731,12 @@ DEV void pt_update(Wv& w, uint32_t from, uint32_t root, bool to_eager) {
     }
 }
 
-// send/3 (pt:633-638): only over an existing connection of the manager
+// send/3 (pt:633-638) -> forward_message (hv:441-460) -> do_send_message
+// without maybe_connect: only over an existing connection of the manager (an
+// active member, or a lingering peer)
 DEV bool pt_conn(const Wv& w, uint32_t ident) {
     uint32_t id = ident & ~PSIM_MAP_BIT;
-    return id != w.me && has(w.A, w.act_n, id) && connect_ok(w, id);
+    return id != w.me && conn_has(w, id) && connect_ok(w, id);
 }
 DEV void pt_send(Wv& w, uint32_t ident, uint32_t type, uint32_t msg, uint32_t rnd, uint32_t root) {
     if (!pt_conn(w, ident)) {
@@ -698,6 +758,16 @@ DEV uint64_t pt_conn_mask(Wv& w, uint64_t cand, uint32_t IDENT) {
     for (uint32_t j = 0; j < w.act_n; j++) {          // (has/3 + the cache lookup of connect_ok)
         const uint32_t aj = rl(w.A, j), cj = rl(w.CF, 32 + j);
         const bool hit = aj == id;
+        in |= hit;
+        fl = hit ? cj : fl;
+    }
+    // the connection table (cache lanes 40..: its entries at phase start,
+    // unchanged in the Plumtree phase): an active member marked down has no
+    // connection, a lingering peer has one
+    for (uint32_t j = 0; j < w.conn_n; j++) {
+        const uint32_t ej = rl(w.CN, j), cj = rl(w.CF, 40 + j);
+        in = ej == (id | PSIM_CONN_DOWN) ? false : in;
+        const bool hit = ej == id;
         in |= hit;
         fl = hit ? cj : fl;
     }
@@ -850,7 +920,7 @@ DEV void hv_handle(Wv& w, uint32_t type, uint32_t p, uint32_t ttl, uint32_t a0, 
     uint32_t me = w.me;
     switch (type) {
     case PSIM_MSG_JOIN:                                // hv:703-771
-        if (addable_epoch(w, a0, p) && !has(w.A, w.act_n, p) && connect_ok(w, p)) {
+        if (addable_epoch(w, a0, p) && !has(w.A, w.act_n, p) && maybe_connect(w, p)) {   // :721-723
             add_to_active(w, p);
             hv_send(w, p, PSIM_MSG_NEIGHBOR, 0, current_id(w, p), 0, 0, 0);
             // (members(Active) -- [Myself]) -- [Peer], in to_list order
@@ -862,13 +932,13 @@ DEV void hv_handle(Wv& w, uint32_t type, uint32_t p, uint32_t ttl, uint32_t a0, 
         }
         break;
     case PSIM_MSG_NEIGHBOR:                            // hv:774-805
-        if (addable_id(w, a0, p) && connect_ok(w, p)) add_to_active(w, p);
+        if (addable_id(w, a0, p) && maybe_connect(w, p)) add_to_active(w, p);   // :784-786
         notify(w);
         break;
     case PSIM_MSG_FORWARD_JOIN: {                      // hv:808-923
         uint32_t q = a0, pe = a1, sender = p;
         if (ttl == 0 || w.act_n == 1) {
-            if (addable_epoch(w, pe, q) && !has(w.A, w.act_n, q) && connect_ok(w, q)) {
+            if (addable_epoch(w, pe, q) && !has(w.A, w.act_n, q) && maybe_connect(w, q)) {
                 add_to_active(w, q);
                 hv_send(w, q, PSIM_MSG_NEIGHBOR, 0, current_id(w, q), 0, 0, 0);
             }
@@ -880,7 +950,7 @@ DEV void hv_handle(Wv& w, uint32_t type, uint32_t p, uint32_t ttl, uint32_t a0, 
             uint32_t r = select_random(w, w.A, w.act_n, sender, me, q);
             if (r == NONE) {
                 if (addable_epoch(w, pe, q) && !has(w.A, w.act_n, q)) {
-                    if (connect_ok(w, q)) {
+                    if (maybe_connect(w, q)) {                 // :878-880
                         add_to_active(w, q);
                         hv_send(w, q, PSIM_MSG_NEIGHBOR, 0, current_id(w, q), 0, 0, 0);
                     } else {
@@ -899,18 +969,21 @@ DEV void hv_handle(Wv& w, uint32_t type, uint32_t p, uint32_t ttl, uint32_t a0, 
     case PSIM_MSG_DISCONNECT: {                        // hv:926-972
         if (!valid_disconnect(w, p, a0)) break;
         vdel_val(w.A, w.act_n, p);
+        if (w.conn_dn) conn_del(w, p | PSIM_CONN_DOWN);
         w.vd |= 1u;
         uint32_t P0 = w.P, np0 = w.pas_n;              // Passive before the add
         add_to_passive(w, p);
         map_store(w, w.RP, w.RI, w.recv_n, w.recv_head, p, a0);
+        disconnect(w, p);                              // :952
         if (w.act_n == 1) move_to_active(w, select_random(w, P0, np0, me, p, me));
         break;
     }
     case PSIM_MSG_NEIGHBOR_REQUEST: {                  // hv:975-1053
         uint32_t ACK;
+        const bool conn = maybe_connect(w, p);         // :987, kept in both branches
         uint32_t nack = build_exchange(w, ACK);
         if (addable_id(w, a0, p)) {                    // priority is always high (:1706)
-            if (connect_ok(w, p)) {
+            if (conn) {
                 hv_send(w, p, PSIM_MSG_NEIGHBOR_ACCEPTED, 0, current_id(w, p), 0, ACK, nack);
                 add_to_active(w, p);
             }
@@ -922,6 +995,7 @@ DEV void hv_handle(Wv& w, uint32_t type, uint32_t p, uint32_t ttl, uint32_t a0, 
         break;
     }
     case PSIM_MSG_NEIGHBOR_REJECTED:                   // hv:1056-1067
+        disconnect(w, p);                              // :1063
         merge_exchange(w, EX, nex);
         break;
     case PSIM_MSG_NEIGHBOR_ACCEPTED:                   // hv:1070-1089
@@ -985,10 +1059,12 @@ struct NodeIn {
     bool maps;                     // DESC_MAPS_BIT (k_relay)
     uint32_t H;                    // header word l & 15
     uint32_t A, P, R0;
+    uint32_t CN;                   // connection-table entry l & 7 (k_consume_lite: 0)
     uint32_t fl, part;
 };
 struct NodeX {
-    uint32_t CV, CF;               // view ids (passive 0-31, active 32-39), their flags | part << 8
+    uint32_t CV, CF;               // view ids (passive 0-31, active 32-39, connection table
+                                   // 40-47), their flags | part << 8
 };
 
 DEV uint32_t load_desc(KArgs& a, uint32_t k) {
@@ -996,6 +1072,7 @@ DEV uint32_t load_desc(KArgs& a, uint32_t k) {
     return reinterpret_cast<const uint32_t*>(a.desc + k)[l & 3];
 }
 
+template <bool CONN = true>
 DEV NodeIn load_node(KArgs& a, uint32_t D) {
     uint32_t l = lane_id();
     NodeIn x;
@@ -1007,9 +1084,18 @@ DEV NodeIn load_node(KArgs& a, uint32_t D) {
     x.P = a.pas[li * PSIM_PASSIVE_CAP + (l & 31)];
     uint32_t m = x.ik ? min(l >> 4, x.ik - 1) : 0u;  // record ib exists (the inbox has one spare)
     x.R0 = reinterpret_cast<const uint32_t*>(a.rec_in + x.ib + m)[l & 15];
+    x.CN = CONN ? a.conn[li * PSIM_CONN_CAP + (l & 7)] : 0u;
     x.fl = a.flags[x.n];
     x.part = a.part[x.n];
     return x;
+}
+
+// the connection-table entry in cache lane 40 + j (j < conn_n, else NONE):
+// the peer of a lingering connection; NONE for a member marked down
+DEV uint32_t conn_cache_id(uint32_t CN, uint32_t H) {
+    const uint32_t l = lane_id(), cn = rl(H, HW_CONN) & 0xFF;
+    const uint32_t e = shfl(CN, (int)(l & 7));
+    return l >= 40 && l < 48 && l - 40 < cn && !(e & PSIM_CONN_DOWN) ? e : NONE;
 }
 
 // flag | partition << 8 of the view members in CV (the connection cache)
@@ -1029,6 +1115,7 @@ DEV NodeX load_x(KArgs& a, const NodeIn& x) {
     // (LITE: k_consume_lite's handlers only send to active members and to
     // senders -- no passive-member entries)
     uint32_t cv = l < 32 ? (!LITE && l < pas_n ? x.P : NONE) : (l < 40 && l - 32 < act_n ? av : NONE);
+    if (!LITE && l >= 40) cv = conn_cache_id(x.CN, x.H);
     y.CV = cv;
     y.CF = cache_flags(a, cv, x.n);
     return y;
@@ -1077,6 +1164,7 @@ DEV void begin_header(Wv& w, uint32_t H) {
     w.act_n = w9 & 0xFF; w.pas_n = (w9 >> 8) & 0xFF; w.sent_n = (w9 >> 16) & 0xFF; w.sent_head = w9 >> 24;
     w.recv_n = w10 & 0xFF; w.recv_head = (w10 >> 8) & 0xFF; w.all_n = (w10 >> 16) & 0xFF; w.com_n = w10 >> 24;
     w.out_n = (w11 >> 16) & 0xFF;
+    w.conn_n = w11 & 0xFF; w.conn_dn = (w11 >> 8) & 0xFF;
     w.sx = rl(H, HW_SENT_EXT); w.rx = rl(H, HW_RECV_EXT); w.ox = rl(H, HW_OUT_EXT);
 }
 
@@ -1093,6 +1181,8 @@ DEV void begin_node(Wv& w, const NodeIn& x, const NodeX& y) {
     w.obase = x.ob;
     w.mypart = x.part;
     w.CV = y.CV; w.CF = y.CF;
+    w.CN = l < w.conn_n ? x.CN : 0u;
+    w.cn_dirty = false;
     w.maps = false; w.pt = false; w.maps_dirty = false; w.pt_dirty = false;
     w.seq = 0; w.flushed = 0;
     w.nlog_n = 0;
@@ -1120,13 +1210,18 @@ DEV void body_hv(Wv& w, const NodeIn& x) {
     bool origin = (x.tf & DESC_ORIGIN) != 0;
     bool lazy = (x.tf & DESC_LAZY) != 0 && w.out_n > 0;
     bool joining = hw_start(w) == r && hw_contact(w) != NONE;
-    uint64_t exits = 0;
-    if (a.crash_round) {                        // F_CRASHED of the active members (cache lanes 32-39)
-        bool dead = l >= 32 && l - 32 < w.act_n && w.CV != n && (w.CF & F_CRASHED);
-        exits = ballot(dead) >> 32;
+    // EXIT (hv:609-654) at every holder of a connection to a peer that
+    // crashed this round (App. A Q11): the connected active members (cache
+    // lanes 32-39, less those marked down), then the lingering peers (40-47)
+    uint64_t exits = 0, lexits = 0;
+    if (a.crash_round) {
+        bool dead = l >= 32 && l < 40 && l - 32 < w.act_n && w.CV != n && (w.CF & F_CRASHED);
+        for (uint32_t j = 0; j < w.conn_n && w.conn_dn; j++) dead &= rl(w.CN, j) != (w.CV | PSIM_CONN_DOWN);
+        exits = (ballot(dead) >> 32) & 0xFFull;
+        lexits = (ballot(l >= 40 && l < 48 && w.CV != NONE && (w.CF & F_CRASHED)) >> 40) & 0xFFull;
     }
     bool promo_work = promo && w.act_n < a.min_active;
-    if (!(ik || joining || exits || promo_work || shuf || origin || lazy)) { STAMP(w, 0); return; }
+    if (!(ik || joining || exits || lexits || promo_work || shuf || origin || lazy)) { STAMP(w, 0); return; }
     w.work = true;
     st_add(w, ST_PROC, 1);
     if (x.maps) load_maps(w);                         // (k_relay: a handler here may use them)
@@ -1135,12 +1230,19 @@ DEV void body_hv(Wv& w, const NodeIn& x) {
     if (joining)                                      // hv:500-515
         hv_send(w, hw_contact(w), PSIM_MSG_JOIN, 0, hw_epoch(w), 0, 0, 0);
 
-    if (exits) {                                      // hv:609-654
+    if (exits | lexits) {                             // hv:609-654
+        // the crashed peers, listed before any handler runs: the active
+        // members in to_list order, then the lingering peers in table order
         uint32_t D = compact(w, w.A, exits);
-        uint32_t nd = popc(exits);
+        const uint32_t na = popc(exits);
+        const uint32_t LV = shfl(w.CV, (int)((l + 40) & 63));
+        const uint32_t LD = compact(w, LV, lexits);
+        D = l >= na ? shfl(LD, (int)((l - na) & 63)) : D;
+        const uint32_t nd = na + popc(lexits);
         for (uint32_t i = 0; i < nd; i++) {
             uint32_t d = rl(D, i);
             st_add(w, ST_EXITS, 1);
+            if (w.conn_n) conn_del(w, d);             // the connection is pruned
             if (vdel_val(w.P, w.pas_n, d)) w.vd |= 2u;
             if (vdel_val(w.A, w.act_n, d)) {
                 w.vd |= 1u;
@@ -1196,7 +1298,7 @@ DEV uint32_t header_word(const Wv& w, uint32_t k) {
     v = k == 8 ? w.trk_hop : v;
     v = k == 9 ? (w.act_n | (w.pas_n << 8) | (w.sent_n << 16) | (w.sent_head << 24)) : v;
     v = k == 10 ? (w.recv_n | (w.recv_head << 8) | (w.all_n << 16) | (w.com_n << 24)) : v;
-    v = k == 11 ? (w.out_n << 16) : v;
+    v = k == 11 ? (w.conn_n | (w.conn_dn << 8) | (w.out_n << 16)) : v;
     v = k == HW_SENT_EXT ? w.sx : v;
     v = k == HW_RECV_EXT ? w.rx : v;
     v = k == HW_OUT_EXT ? w.ox : v;
@@ -1282,6 +1384,12 @@ DEV void writeback(Wv& w) {
         uint64_t* h64 = reinterpret_cast<uint64_t*>(hrow);   // (the draw counter, rewritten)
         *(ds ? (own ? a.sentm + io : a.mapx + so) : h64) = ds ? (((uint64_t)w.SI << 32) | w.SP) : w.rng;
         *(dr ? (own ? a.recvm + io : a.mapx + ro) : h64) = dr ? (((uint64_t)w.RI << 32) | w.RP) : w.rng;
+    }
+    {
+        // the connection table (a fixed store: unchanged, it rewrites the
+        // header's word 0)
+        const uint32_t x = shfl(w.CN, (int)(l & 7));
+        *(w.cn_dirty ? a.conn + li * PSIM_CONN_CAP + (l & 7) : hrow) = w.cn_dirty ? x : h0;
     }
     if (w.pt_dirty) store_pt_rows(w);
     a.ocnt[li] = w.seq;
@@ -1374,6 +1482,11 @@ __global__ void __launch_bounds__(256, PSIM_WAVES_PER_SIMD) k_consume(RoundArgs 
 DEV void body_lite(Wv& w, const NodeIn& x) {
     KArgs& a = kargs();
     const uint32_t l = lane_id();
+    // (k_relay sends here only nodes with no active member marked down whose
+    // walks end at a Sender in the active view: every send goes to an active
+    // member over its connection, so the connection table is neither read
+    // nor written -- nor is header word 11)
+    w.conn_n = 0; w.conn_dn = 0;
     w.work = true;
     st_add(w, ST_PROC, 1);
     for (uint32_t c = 0; c < x.ik; c += 4) {          // HyParView inbox, canonical order
@@ -1461,16 +1574,16 @@ __global__ void __launch_bounds__(256, PSIM_LITE_WAVES) k_consume_lite(RoundArgs
     if (gw < na) {
         const uint32_t last = na - 1;
         KArgs& a0 = kargs();
-        NodeIn x = load_node(a0, reinterpret_cast<const uint32_t*>(kargs().desc_lite + gw)[lane_id() & 3]);
+        NodeIn x = load_node<false>(a0, reinterpret_cast<const uint32_t*>(kargs().desc_lite + gw)[lane_id() & 3]);
         NodeX y = load_x<true>(kargs(), x);
-        NodeIn xn = load_node(kargs(), reinterpret_cast<const uint32_t*>(kargs().desc_lite + min(gw + nw, last))[lane_id() & 3]);
+        NodeIn xn = load_node<false>(kargs(), reinterpret_cast<const uint32_t*>(kargs().desc_lite + min(gw + nw, last))[lane_id() & 3]);
         uint32_t d = reinterpret_cast<const uint32_t*>(kargs().desc_lite + min(gw + 2 * nw, last))[lane_id() & 3];
         for (uint32_t i = gw; i < na; i += nw) {
             begin_node(w, x, y);
             body_lite(w, x);
             NodeX yn = load_x<true>(kargs(), xn);
             writeback_lite(w);
-            NodeIn xnn = load_node(kargs(), d);
+            NodeIn xnn = load_node<false>(kargs(), d);
             d = reinterpret_cast<const uint32_t*>(kargs().desc_lite + min(i + 3 * nw, last))[lane_id() & 3];
             x = xn; y = yn; xn = xnn;
         }
@@ -1493,7 +1606,7 @@ __global__ void __launch_bounds__(256, PSIM_LITE_WAVES) k_consume_lite(RoundArgs
 //   PtX    flag / partition bytes of the active members, the Plumtree rows
 struct PtIn {
     uint32_t n, ib, ik, ob, tf;
-    uint32_t H, A, R0;
+    uint32_t H, A, R0, CN;
     uint32_t fl, part, oc;
 };
 struct PtX {
@@ -1510,17 +1623,19 @@ DEV PtIn load_pt_node(KArgs& a, uint32_t D) {
     x.A = a.act[li * PSIM_ACTIVE_CAP + (l & 7)];
     const uint32_t m = x.ik ? min(l >> 4, x.ik - 1) : 0u;
     x.R0 = reinterpret_cast<const uint32_t*>(a.rec_in + x.ib + m)[l & 15];
+    x.CN = a.conn[li * PSIM_CONN_CAP + (l & 7)];
     x.fl = a.flags[x.n];
     x.part = a.part[x.n];
     x.oc = a.ocnt[li];
     return x;
 }
 
-// the active members' ids in cache lanes 32-39 (connect_ok)
+// the active members' ids in cache lanes 32-39 and the connection table's
+// lingering peers in 40-47 (connect_ok, pt_conn_mask)
 DEV uint32_t act_cache(const PtIn& x) {
     const uint32_t l = lane_id(), act_n = rl(x.H, 9) & 0xFF;
     const uint32_t av = shfl(x.A, (int)(l & 7));
-    return l >= 32 && l < 40 && l - 32 < act_n ? av : NONE;
+    return l >= 32 && l < 40 && l - 32 < act_n ? av : (l >= 40 ? conn_cache_id(x.CN, x.H) : NONE);
 }
 
 DEV PtX load_pt_x(KArgs& a, const PtIn& x) {
@@ -1553,6 +1668,9 @@ DEV void begin_pt(Wv& w, const PtIn& x, const PtX& y) {
     w.obase = x.ob;
     w.mypart = x.part;
     w.CV = act_cache(x); w.CF = y.CF;
+    const uint32_t w11 = rl(x.H, HW_CONN);
+    w.conn_n = w11 & 0xFF; w.conn_dn = (w11 >> 8) & 0xFF;
+    w.CN = l < w.conn_n ? x.CN : 0u;
     load_pt_regs(w, y.PA, y.PG, y.PL, y.PO);
     w.pt_dirty = false;
     w.seq = x.oc; w.flushed = x.oc;                  // after the HyParView phase's records
@@ -1778,34 +1896,66 @@ __global__ void __launch_bounds__(256, PSIM_RELAY_WAVES) k_relay(RoundArgs) {
             // the inbox: how many HyParView messages, and whether each is a
             // SHUFFLE with TTL left (a relay while |active| > 1)
             uint32_t hvn = 0;
-            bool all_relay = true, all_shuf = true;
-            // (four type words issued before any is waited on: a loop of
-            // single loads waits one memory latency per record)
+            bool all_relay = true, all_shuf = true, term_out = false;
+            const uint32_t av[8] = {act0.x, act0.y, act0.z, act0.w, act1.x, act1.y, act1.z, act1.w};
+            // (four records' first 16 B issued before any is waited on: a
+            // loop of single loads waits one memory latency per record)
             for (uint32_t j = 0; j < ik; j += 4) {
-                uint32_t T[4];
-#pragma unroll
-                for (int q = 0; q < 4; q++)
-                    T[q] = j + q < ik ? a.rec_in[D.y + j + q].tt : (uint32_t)PSIM_MSG_PT_BROADCAST;
+                uint2 T[4];                                   // (src, type word)
 #pragma unroll
                 for (int q = 0; q < 4; q++) {
-                    const uint32_t tt = T[q], type = tt & 0xFF;
+                    const uint4 r4 = j + q < ik ? *reinterpret_cast<const uint4*>(a.rec_in + D.y + j + q)
+                                                : make_uint4(0, 0, (uint32_t)PSIM_MSG_PT_BROADCAST, 0);
+                    T[q] = make_uint2(r4.y, r4.z);
+                }
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const uint32_t tt = T[q].y, type = tt & 0xFF;
                     if (type < PSIM_MSG_PT_BROADCAST) {
                         hvn++;
                         maps |= type <= PSIM_MSG_NEIGHBOR_ACCEPTED;   // id maps (hv:703-1089)
+                        const bool relays = ((tt >> 8) & 0xFF) > 0 && h.act_n > 1;
                         all_relay &= type == PSIM_MSG_SHUFFLE && ((tt >> 8) & 0xFF) > 0;
                         all_shuf &= type == PSIM_MSG_SHUFFLE || type == PSIM_MSG_SHUFFLE_REPLY;
+                        // a walk that ends here replies to its Sender: maybe_connect
+                        // (hv:1127) opens a lingering connection to a Sender outside
+                        // the active view -- the connection table's path, k_consume
+                        if (type == PSIM_MSG_SHUFFLE && !relays) {
+                            bool in = false;
+#pragma unroll
+                            for (int k = 0; k < 8; k++) in |= (uint32_t)k < h.act_n && av[k] == T[q].x;
+                            term_out |= !in;
+                        }
                     }
                 }
             }
             const bool fresh = h.start_round == a.round;
-            bool exits = false;                       // a crashed active member: EXIT events
+            bool exits = false;                       // a crashed peer held over a connection: EXIT events
             if (a.crash_round) {
-                const uint32_t av[8] = {act0.x, act0.y, act0.z, act0.w, act1.x, act1.y, act1.z, act1.w};
+                uint32_t cv[PSIM_CONN_CAP] = {};
+                if (h.conn_n) {
+                    const uint4* cr = reinterpret_cast<const uint4*>(a.conn + li * PSIM_CONN_CAP);
+                    const uint4 c0 = cr[0], c1 = cr[1];
+                    cv[0] = c0.x; cv[1] = c0.y; cv[2] = c0.z; cv[3] = c0.w;
+                    cv[4] = c1.x; cv[5] = c1.y; cv[6] = c1.z; cv[7] = c1.w;
+                }
 #pragma unroll
-                for (int j = 0; j < 8; j++)
-                    exits |= (uint32_t)j < h.act_n && av[j] != id && av[j] < a.n_nodes && (a.flags[av[j]] & F_CRASHED);
+                for (int j = 0; j < 8; j++) {
+                    bool down = false;
+#pragma unroll
+                    for (int k = 0; k < PSIM_CONN_CAP; k++) down |= (uint32_t)k < h.conn_n && cv[k] == (av[j] | PSIM_CONN_DOWN);
+                    exits |= (uint32_t)j < h.act_n && av[j] != id && av[j] < a.n_nodes && !down &&
+                             (a.flags[av[j]] & F_CRASHED);
+                }
+#pragma unroll
+                for (int k = 0; k < PSIM_CONN_CAP; k++)
+                    exits |= (uint32_t)k < h.conn_n && !(cv[k] & PSIM_CONN_DOWN) && (a.flags[cv[k] & KEY_DST_MASK] & F_CRASHED);
             }
-            heavy = exits || fresh || ((tf & DESC_PROMO) && h.act_n < a.min_active) || (hvn && !all_shuf);
+            // an active member without a connection (conn_dn): the next send
+            // to it reconnects (maybe_connect) -- the connection table's path
+            const bool cdown = h.conn_dn != 0 && (hvn > 0 || (tf & DESC_SHUFFLE));
+            heavy = exits || fresh || ((tf & DESC_PROMO) && h.act_n < a.min_active) || (hvn && !all_shuf) ||
+                    term_out || cdown;
             // SHUFFLE terminals and replies (with whatever relays and shuffle
             // start come with them): k_consume_lite
             lite = !heavy && hvn && !(all_relay && h.act_n > 1);
@@ -2287,7 +2437,9 @@ __global__ void __launch_bounds__(PTL_BLK, PSIM_PTL_BLOCKS_PER_CU) k_ptl(RoundAr
             uint64_t bm = 0;                          // message slots of the BROADCASTs
             // (an outstanding extension row taken earlier holds zeros while the
             // table fits its own row: this round's adds must fit that row)
-            bool ok = r0.y == NONE && r0.z == NONE && r0.w == NONE &&
+            // (a node with a connection table -- lingering peers, or active
+            // members without a connection -- tests its sends in k_pt)
+            bool ok = r0.y == NONE && r0.z == NONE && r0.w == NONE && (w11 & 0xFFFFu) == 0 &&
                       (root0 == NONE || ((rtw4 >> 8) == 0 && (rtw5 >> 8) == 0));
             for (uint32_t j = 0; ok && j < ik; j++) {
                 const uint4* rq = reinterpret_cast<const uint4*>(a.rec_in + D.y + j);

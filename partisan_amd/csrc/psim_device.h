@@ -22,7 +22,8 @@ struct __attribute__((aligned(16))) Hdr {
     uint32_t trk_hop;      // plumtree Round + 1 at that delivery (0 at the root)
     uint8_t act_n, pas_n, sent_n, sent_head;
     uint8_t recv_n, recv_head, all_n, com_n;
-    uint8_t pad2, pad3, out_n, pad0;
+    uint8_t conn_n, conn_dn, out_n, pad0;   // connection table (RoundArgs::conn): entries, of
+                                            // which | PSIM_CONN_DOWN (active members without one)
     uint32_t pad1[4];      // pluggable: pad1[0] = leave/1 target of this round + 1, 0 = none;
                            // HyParView: pad1[1] / pad1[2] = the sent / recv id map's
                            // extension row + 1 (0 = none), words HW_SENT_EXT / HW_RECV_EXT;
@@ -70,6 +71,9 @@ constexpr uint32_t HW_SENT_EXT = 13, HW_RECV_EXT = 14;   // header words (Hdr pa
 constexpr uint32_t OUT_IN = 16;
 constexpr uint32_t OUT_EXT = PSIM_PT_OUT_CAP - OUT_IN;
 constexpr uint32_t HW_OUT_EXT = 15;
+// the connection table's counts: header word 11, bytes 0 (entries) and 1
+// (PSIM_CONN_DOWN entries); byte 2 is the outstanding count
+constexpr uint32_t HW_CONN = 11;
 
 // route key: dst in the low 27 bits, the sender-side emission bound of the
 // message type in the top 5 (used to size the receiver's next outbox).

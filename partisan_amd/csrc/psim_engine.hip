@@ -143,6 +143,8 @@ __global__ void k_join(RoundArgs a, uint32_t* start, const uint32_t* ids, const 
     }
     for (uint32_t k = 0; k < RT_WORDS; k++) a.pt_rt[(size_t)li * RT_WORDS + k] = k < PSIM_PT_ROOTS ? PSIM_NONE : 0u;
     for (uint32_t k = 0; k < OUT_IN; k++) a.pt_out[(size_t)li * OUT_IN + k] = 0;
+    if (a.conn)                    // a fresh incarnation has no connections
+        for (uint32_t k = 0; k < PSIM_CONN_CAP; k++) a.conn[(size_t)li * PSIM_CONN_CAP + k] = 0;
     if (ox)
         for (uint32_t k = 0; k < OUT_EXT; k++) a.outx[(size_t)(ox - 1) * OUT_EXT + k] = 0;
     if (a.pl) {                    // the pluggable manager's init/1 (pl:346-402) + Strategy:init/1
@@ -667,15 +669,37 @@ __global__ void __launch_bounds__(256) k_node_prep(RoundArgs a, const unsigned l
                     b += min((uint32_t)PSIM_PT_OUT_CAP, on + lazy_add);
                 }
                 // a crash round: a NEIGHBOR_REQUEST per crashed active member
+                // (bounded over every crashed member); EXIT work for a
+                // crashed member held over a connection -- an active member
+                // not marked PSIM_CONN_DOWN, or a lingering peer (App. A Q11)
+                bool exits = false;
                 if (a.crash_round) {
                     const uint4* ar = reinterpret_cast<const uint4*>(a.act + (size_t)i * PSIM_ACTIVE_CAP);
                     const uint4 a0 = ar[0], a1 = ar[1];
                     const uint32_t av[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+                    uint32_t cv[PSIM_CONN_CAP] = {};
+                    const uint32_t cn = x.conn_n;
+                    if (cn) {
+                        const uint4* cr = reinterpret_cast<const uint4*>(a.conn + (size_t)i * PSIM_CONN_CAP);
+                        const uint4 c0 = cr[0], c1 = cr[1];
+                        cv[0] = c0.x; cv[1] = c0.y; cv[2] = c0.z; cv[3] = c0.w;
+                        cv[4] = c1.x; cv[5] = c1.y; cv[6] = c1.z; cv[7] = c1.w;
+                    }
 #pragma unroll
                     for (int k = 0; k < PSIM_ACTIVE_CAP; k++)
-                        if ((uint32_t)k < x.act_n && av[k] < a.n_nodes && (a.flags[av[k]] & F_CRASHED)) b++;
+                        if ((uint32_t)k < x.act_n && av[k] < a.n_nodes && av[k] != a.lo + i &&
+                            (a.flags[av[k]] & F_CRASHED)) {
+                            b++;
+                            bool down = false;
+#pragma unroll
+                            for (int j = 0; j < PSIM_CONN_CAP; j++) down |= (uint32_t)j < cn && cv[j] == (av[k] | PSIM_CONN_DOWN);
+                            exits |= !down;
+                        }
+#pragma unroll
+                    for (int j = 0; j < PSIM_CONN_CAP; j++)
+                        exits |= (uint32_t)j < cn && !(cv[j] & PSIM_CONN_DOWN) && (a.flags[cv[j] & KEY_DST_MASK] & F_CRASHED);
                 }
-                w = c > 0 || st == r || a.crash_round || (f & F_LAZY) || origin ||
+                w = c > 0 || st == r || exits || (f & F_LAZY) || origin ||
                     (a.random_promotion && (f & F_LOWACT) && due(a.promotion_period, r, st)) ||
                     due(a.shuffle_period, r, st);
                 // a working node's first slot is reserved: a wave that emits
@@ -1057,6 +1081,7 @@ struct Shard {
     DBuf<uint32_t> slots;               // the message slots (msg ids, then roots), a copy of the host's
     DBuf<uint32_t> bc_roots, bc_msgs;   // this round's broadcasts
     DBuf<uint64_t> pt_out, outx;        // outstanding: own rows, extension rows (pool)
+    DBuf<uint32_t> conn;                // connection tables (PSIM_CONN_CAP per node; HyParView)
     DBuf<uint32_t> outx_top;
     // inbox of the next round: sorted (local dst | bound, record index) pairs
     DBuf<uint32_t> ikeys, ivals;
@@ -1174,6 +1199,7 @@ RoundArgs make_args(psim_handle* h, Shard* s) {
     a.pt_all = s->pt_all.p; a.pt_com = s->pt_com.p; a.pt_eag = s->pt_eag.p; a.pt_laz = s->pt_laz.p;
     a.pt_rt = s->pt_rt.p;
     a.pt_out = s->pt_out.p; a.outx = s->outx.p; a.outx_top = s->outx_top.p;
+    a.conn = s->conn.p;
     a.outx_rows = (uint32_t)(s->outx.n / OUT_EXT);
     a.start = s->start.p;
     a.pl = c.manager == PSIM_MANAGER_PLUGGABLE;
@@ -1905,6 +1931,7 @@ int shard_alloc(psim_handle* h, Shard* s) {
     rc |= s->pt_eag.alloc(n * RT_SET); rc |= s->pt_laz.alloc(n * RT_SET); rc |= s->pt_rt.alloc(n * RT_WORDS);
     rc |= s->origin.alloc(n); rc |= s->slots.alloc(2 * PSIM_MSG_SLOTS);
     rc |= s->pt_out.alloc(n * OUT_IN); rc |= s->start.alloc(n);
+    if (h->cfg.manager != PSIM_MANAGER_PLUGGABLE) rc |= s->conn.alloc(n * PSIM_CONN_CAP);
     if (h->cfg.manager != PSIM_MANAGER_PLUGGABLE) rc |= s->outx.alloc(std::max<size_t>(1024, n / 32) * OUT_EXT);
     rc |= s->outx_top.alloc(1);
     rc |= s->ocnt.alloc(n); rc |= s->cb.alloc(n + 1);
@@ -1944,7 +1971,7 @@ void shard_free(Shard* s) {
     s->act.release(); s->pas.release(); s->sentm.release(); s->recvm.release();
     s->pt_all.release(); s->pt_com.release();
     s->mapx.release(); s->mapx_top.release();
-    s->pt_eag.release(); s->pt_laz.release(); s->pt_out.release(); s->start.release();
+    s->pt_eag.release(); s->pt_laz.release(); s->pt_out.release(); s->start.release(); s->conn.release();
     s->outx.release(); s->outx_top.release();
     s->pt_rt.release(); s->origin.release(); s->slots.release(); s->bc_roots.release(); s->bc_msgs.release();
     s->ikeys.release(); s->ivals.release(); s->recvbuf.release(); s->inbox.release();
@@ -1988,6 +2015,7 @@ const char* psim_strerror(int code) {
     case PSIM_ERANGE: return "node id out of range";
     case PSIM_ECOMM: return "communication error";
     case PSIM_EUNSUPPORTED: return "unsupported";
+    case PSIM_ECAPACITY: return "a fixed table overflowed (strict)";
     default: return "unknown error";
     }
 }
@@ -2015,7 +2043,7 @@ int psim_create(const psim_config* cfg, psim_handle** out) {
         cfg->max_passive_size > 30 || 1 + cfg->k_active + cfg->k_passive > PSIM_EXCHANGE_CAP ||
         cfg->arwl > 255 || cfg->prwl > 255 || cfg->manager > PSIM_MANAGER_PLUGGABLE ||
         cfg->strategy > PSIM_STRATEGY_SCAMP_V2 || cfg->scamp_c < 1 || cfg->scamp_c > 64 ||
-        cfg->fanout > 64)   /* (picks land in one 64-lane register) */
+        cfg->fanout > 64 || cfg->strict > 1)   /* (picks land in one 64-lane register) */
         return PSIM_EINVAL;
     const bool full = cfg->manager == PSIM_MANAGER_PLUGGABLE && cfg->strategy == PSIM_STRATEGY_FULL;
     uint32_t world = std::max<uint32_t>(cfg->shard_world, 1);
@@ -2253,6 +2281,16 @@ int psim_step(psim_handle* h, uint32_t n_rounds, psim_round_stats* stats) {
         int rc = run_round(h, st);
         if (rc) return rc;
         if (stats) fill_stats(st, r, &stats[i]);
+        if (h->cfg.strict && st[ST_OVF]) return PSIM_ECAPACITY;   // cfg.strict: fail loudly
+    }
+    return PSIM_OK;
+}
+
+int psim_get_msg_slots(psim_handle* h, uint32_t* ids, uint32_t* roots, size_t cap) {
+    if (!h || !ids || !roots || cap < PSIM_MSG_SLOTS) return PSIM_EINVAL;
+    for (int k = 0; k < PSIM_MSG_SLOTS; k++) {
+        ids[k] = h->slot_tab[k];
+        roots[k] = h->slot_tab[PSIM_MSG_SLOTS + k];
     }
     return PSIM_OK;
 }
@@ -2271,6 +2309,7 @@ static int get_shard_nodes(Shard* s, uint32_t first, uint32_t count, psim_node_v
     std::vector<uint32_t> all((size_t)count * PSIM_PT_MEMBERS_CAP), com(all.size());
     std::vector<uint32_t> eag((size_t)count * RT_SET), laz(eag.size()), rt((size_t)count * RT_WORDS);
     std::vector<uint64_t> po((size_t)count * OUT_IN);
+    std::vector<uint32_t> cn((size_t)count * PSIM_CONN_CAP, 0u);
     const size_t li = first - s->lo;
     auto cp = [&](void* dst, const void* src, size_t bytes) {
         return hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, s->stream);
@@ -2291,6 +2330,7 @@ static int get_shard_nodes(Shard* s, uint32_t first, uint32_t count, psim_node_v
     HIP_TRY(cp(laz.data(), s->pt_laz.p + li * RT_SET, laz.size() * 4));
     HIP_TRY(cp(rt.data(), s->pt_rt.p + li * RT_WORDS, rt.size() * 4));
     HIP_TRY(cp(po.data(), s->pt_out.p + li * OUT_IN, po.size() * 8));
+    if (s->conn.p) HIP_TRY(cp(cn.data(), s->conn.p + li * PSIM_CONN_CAP, cn.size() * 4));
     const uint32_t otop = s->outx.p ? std::min<uint32_t>(read1(s, s->outx_top.p), (uint32_t)(s->outx.n / OUT_EXT)) : 0u;
     std::vector<uint64_t> xo((size_t)otop * OUT_EXT);
     if (otop) HIP_TRY(cp(xo.data(), s->outx.p, xo.size() * 8));
@@ -2334,6 +2374,8 @@ static int get_shard_nodes(Shard* s, uint32_t first, uint32_t count, psim_node_v
             v->pt_out_round[j] = (uint32_t)o & 0xFFFFu;
         }
         v->have = ((uint64_t)x.aux << 32) | x.have; v->trk_round = x.trk_round; v->trk_hop = x.trk_hop;
+        v->conn_n = x.conn_n;
+        for (uint32_t j = 0; j < x.conn_n && j < PSIM_CONN_CAP; j++) v->conn[j] = cn[(size_t)k * PSIM_CONN_CAP + j];
     }
     return PSIM_OK;
 }
@@ -2603,6 +2645,7 @@ static std::vector<Section> snap_sections(psim_handle* h, Shard* s, const ShardH
         {s->pt_all.p, n * PSIM_PT_MEMBERS_CAP * 4}, {s->pt_com.p, n * PSIM_PT_MEMBERS_CAP * 4},
         {s->pt_eag.p, n * RT_SET * 4}, {s->pt_laz.p, n * RT_SET * 4}, {s->pt_rt.p, n * RT_WORDS * 4},
         {s->pt_out.p, n * OUT_IN * 8}, {s->outx.p, (size_t)sh.out_rows * OUT_EXT * 8}, {s->start.p, n * 4},
+        {s->conn.p, s->conn.p ? n * PSIM_CONN_CAP * 4 : 0},
         {s->cb.p, (n + 1) * 8}, {s->bmask.p, n * 8}, {s->in_beg.p, (n + 1) * 4},
         {s->inbox.p, (size_t)sh.m_in * sizeof(Msg)},
     };

@@ -24,6 +24,8 @@ struct RoundArgs {
     uint32_t* mapx_top;         // pool rows taken
     uint32_t mapx_rows;         // pool rows
     uint32_t *pt_all, *pt_com, *pt_eag, *pt_laz, *pt_rt;
+    uint32_t* conn;             // connections beyond the active view: PSIM_CONN_CAP per node
+                                // (Hdr conn_n / conn_dn)
     uint64_t* pt_out;           // outstanding: the OUT_IN own entries
     uint64_t* outx;             // outstanding extension rows (OUT_EXT entries), a shared pool
     uint32_t* outx_top;

@@ -78,6 +78,46 @@ def joiner_crash(make, n=2048, seed=3, rounds=40, **cfg):
     return sim, st
 
 
+def lingering_exits(make, n=2048, seed=5, extra_rounds=6, k=16):
+    """churn_partition, then a crash of the k peers held by the most
+    lingering connections: their EXITs reach holders
+    outside their active views; then a few rounds more."""
+    sim, st = churn_partition(make, n=n, seed=seed)
+    v = sim.nodes()
+    holders = {}
+    for i in np.nonzero(v["up"])[0]:
+        for e in v["conn"][i][: v["conn_n"][i]]:
+            if not int(e) & 0x80000000:
+                holders[int(e)] = holders.get(int(e), 0) + 1
+    victims = sorted(holders, key=lambda p: (-holders[p], p))[:k]
+    sim.crash(np.array(victims, np.uint32))
+    sim.broadcast(1, 999)
+    st2 = sim.step(extra_rounds)
+    return sim, np.concatenate([st, st2]), victims
+
+
+def e_miniature(make, n=1 << 14, seed=101, rounds=90):
+    """Config E in miniature, as bench.py's built-in sharding check runs it:
+    doubling bootstrap, 20% churn over rounds 30-49 (crash, restart and
+    rejoin), a half/half partition for rounds 55-64, a broadcast from node 0
+    every 10 rounds from round 20."""
+    sim = make(default_config(n_nodes=n, seed=seed))
+    ch = {r: (v, c) for r, v, c in W.churn_schedule(n, seed, 0.2, 30, 20)}
+
+    def hook(r):
+        if r in ch:
+            sim.crash(ch[r][0])
+            sim.join(ch[r][0], ch[r][1])
+        if r == 55:
+            sim.set_partition(W.half_partition(n))
+        if r == 65:
+            sim.clear_partition()
+        if r >= 20 and r % 10 == 0:
+            sim.broadcast(0, (r // 10) % 0x10000)
+    st = sim.run_schedule(W.doubling_join(n, seed), rounds, extra=hook)
+    return sim, st
+
+
 VARIANT = dict(max_active_size=8, max_passive_size=20, arwl=6, prwl=6, persist_epoch=1)
 
 

@@ -47,6 +47,26 @@ def test_churn_partition_parity():
     S.compare_nodes(gs.nodes(), os_.nodes())
 
 
+def test_lingering_connections_parity():
+    """connections beyond the active view -- shuffle
+    terminals' Senders, rejected and pending neighbor requests, a joiner's
+    contact -- in the connection table, EXIT at every holder, Plumtree sends
+    over them: the crash of the most-held lingering peers, GPU == oracle."""
+    (gs, gst, gv), (os_, ost, ov) = _both(S.lingering_exits)
+    assert gv == ov and ov
+    S.compare_stats(gst, ost)
+    S.compare_nodes(gs.nodes(), os_.nodes())
+    assert int((os_.nodes()["conn_n"] > 0).sum()) > 0
+
+
+def test_e_miniature_parity():
+    """Config E in miniature (bench.py's sharding-check schedule) at 2^14
+    nodes: churn, restarts, a partition and broadcasts, GPU == oracle."""
+    (gs, gst), (os_, ost) = _both(S.e_miniature)
+    S.compare_stats(gst, ost)
+    S.compare_nodes(gs.nodes(), os_.nodes())
+
+
 def test_crash_parity():
     (gs, gst, _), (os_, ost, _) = _both(S.crash_only)
     S.compare_stats(gst, ost)
