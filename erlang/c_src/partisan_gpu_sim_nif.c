@@ -72,7 +72,7 @@ static ERL_NIF_TERM nif_create(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv
         !get_u32(env, argv[0], "plumtree", &c.plumtree) ||
         !get_u32(env, argv[0], "manager", &c.manager) ||
         !get_u32(env, argv[0], "strategy", &c.strategy) ||
-        !get_u32(env, argv[0], "fanout", &c.fanout) ||
+        !get_u32(env, argv[0], "fanout", &c.fanout) || !get_u32(env, argv[0], "strict", &c.strict) ||
         !get_u32(env, argv[0], "scamp_c", &c.scamp_c) ||
         !get_u32(env, argv[0], "periodic_interval", &c.periodic_interval))
         return enif_make_badarg(env);
@@ -159,6 +159,25 @@ static ERL_NIF_TERM nif_broadcast(ErlNifEnv *env, int argc, const ERL_NIF_TERM a
     int rc = psim_broadcast(r->h, root, id);
     enif_mutex_unlock(r->mu);
     return rc ? err(env, rc) : enif_make_atom(env, "ok");
+}
+
+/* msg_slots_nif(Ref) -> {ok, [{Slot, Id, Root}]}: the live message slots
+ * (psim_get_msg_slots; plumtree_backend's ETS set, :140-167) */
+static ERL_NIF_TERM nif_msg_slots(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[]) {
+    sim_res *r;
+    uint32_t ids[PSIM_MSG_SLOTS], roots[PSIM_MSG_SLOTS];
+    if (!enif_get_resource(env, argv[0], SIM_RT, (void **)&r)) return enif_make_badarg(env);
+    LOCK_OR_BUSY(r);
+    int rc = psim_get_msg_slots(r->h, ids, roots, PSIM_MSG_SLOTS);
+    enif_mutex_unlock(r->mu);
+    if (rc) return err(env, rc);
+    ERL_NIF_TERM l = enif_make_list(env, 0);
+    for (int k = PSIM_MSG_SLOTS - 1; k >= 0; k--)
+        if (ids[k] != PSIM_NONE)
+            l = enif_make_list_cell(env, enif_make_tuple3(env, enif_make_uint(env, (unsigned)k),
+                                                          enif_make_uint(env, ids[k]),
+                                                          enif_make_uint(env, roots[k] & ~PSIM_MAP_BIT)), l);
+    return enif_make_tuple2(env, enif_make_atom(env, "ok"), l);
 }
 
 /* omission_nif(Ref, Kind, SrcBin, DstBin, On): install / remove
@@ -422,6 +441,7 @@ static ErlNifFunc funcs[] = {
     {"faulted_nif", 3, nif_faulted, 0},
     {"clear_faults_nif", 1, nif_clear_faults, 0},
     {"node_nif", 2, nif_node, 0},
+    {"msg_slots_nif", 1, nif_msg_slots, 0},
     {"snapshot", 1, nif_snapshot, ERL_NIF_DIRTY_JOB_IO_BOUND},
     {"restore", 2, nif_restore, ERL_NIF_DIRTY_JOB_IO_BOUND},
 };

@@ -1,7 +1,8 @@
 """Reference parity through the in-BEAM harness (erlang/harness/README.md).
 
   python erlang/harness/compare_trace.py scenario config_a DIR
-      writes DIR/config_a.terms (the event script psim_harness:run/2 reads)
+      writes DIR/config_a.terms (the event script psim_harness:run/2 -- or,
+      for the *_pl scenarios, psim_strategy_harness:run/2 -- reads)
       and DIR/config_a.oracle (the CPU oracle's record stream of the same
       scenario: one line per emitted message, in the harness's format)
   python erlang/harness/compare_trace.py compare DIR/config_a.harness DIR/config_a.oracle
@@ -36,16 +37,28 @@ SCENARIOS = {
     # a doubling bootstrap with crashes (EXIT handling) and broadcasts
     "doubling_crash_256": dict(n=256, seed=3, rounds=80, joins=lambda n, s: W.doubling_join(n, s),
                                bcast=[(30, 0, 1), (60, 0, 2)], crash={40: list(range(5, 256, 17))}),
+    # the pluggable manager's strategies (erlang/harness/psim_strategy_harness.erl;
+    # pl:384, :881-903, :986-1044, :1153-1195): configs B and D in miniature,
+    # reference semantics (fanout 0), with crashes, a partition and leave/1
+    "full_16_pl": dict(n=16, seed=11, rounds=80, joins=lambda n, s: W.doubling_join(n, s), bcast=[],
+                       crash={40: [5]}, strategy="full"),
+    "scamp_v1_128_pl": dict(n=128, seed=11, rounds=100, joins=lambda n, s: W.doubling_join(n, s), bcast=[],
+                            crash={40: [3, 77]}, part=(60, 70), leave={50: [(9, 10)]}, strategy="scamp_v1"),
+    "scamp_v2_128_pl": dict(n=128, seed=11, rounds=100, joins=lambda n, s: W.doubling_join(n, s), bcast=[],
+                            crash={40: [3, 77]}, part=(60, 70), leave={50: [(9, 10)]}, strategy="scamp_v2"),
 }
+STRATEGIES = {"full": 0, "scamp_v1": 1, "scamp_v2": 2}
 
 
 def scenario(name, out_dir):
     sc = SCENARIOS[name]
     n, seed, rounds = sc["n"], sc["seed"], sc["rounds"]
     joins = sc["joins"](n, seed)
+    strategy = sc.get("strategy")
     os.makedirs(out_dir, exist_ok=True)
     with open(os.path.join(out_dir, name + ".terms"), "w") as f:
-        f.write(f"{{config, #{{n_nodes => {n}, seed => {seed}, rounds => {rounds}}}}}.\n")
+        extra = f", strategy => {strategy}, periodic_interval => 10, scamp_c => 5" if strategy else ""
+        f.write(f"{{config, #{{n_nodes => {n}, seed => {seed}, rounds => {rounds}{extra}}}}}.\n")
         for r, ids, contacts in joins:
             pairs = ", ".join(f"{{{int(i)}, {'none' if int(c) == NONE else int(c)}}}" for i, c in zip(ids, contacts))
             f.write(f"{{join, {r}, [{pairs}]}}.\n")
@@ -53,15 +66,25 @@ def scenario(name, out_dir):
             f.write(f"{{crash, {r}, [{', '.join(str(i) for i in ids)}]}}.\n")
         for r, root, msg in sc["bcast"]:
             f.write(f"{{broadcast, {r}, {root}, {msg}}}.\n")
-    lines = oracle_stream(n, seed, rounds, joins, sc["bcast"], sc["crash"])
+        if "part" in sc:
+            g = ", ".join(str(int(x)) for x in W.half_partition(n))
+            f.write(f"{{partition, {sc['part'][0]}, [{g}]}}.\n{{clear_partition, {sc['part'][1]}}}.\n")
+        for r, pairs in sc.get("leave", {}).items():
+            f.write(f"{{leave, {r}, [{', '.join(f'{{{a}, {t}}}' for a, t in pairs)}]}}.\n")
+    lines = oracle_stream(n, seed, rounds, joins, sc["bcast"], sc["crash"], strategy=strategy,
+                          part=sc.get("part"), leave=sc.get("leave", {}))
     with open(os.path.join(out_dir, name + ".oracle"), "w") as f:
         f.write("\n".join(lines) + "\n")
     print(f"wrote {name}.terms and {name}.oracle ({len(lines)} records)")
 
 
-def oracle_stream(n, seed, rounds, joins, bcast, crash):
+def oracle_stream(n, seed, rounds, joins, bcast, crash, strategy=None, part=None, leave=None):
     from _oracle import Oracle
-    o = Oracle(default_config(n_nodes=n, seed=seed))
+    if strategy:
+        o = Oracle(default_config(n_nodes=n, seed=seed, manager=_abi.MANAGER_PLUGGABLE,
+                                  strategy=STRATEGIES[strategy], fanout=0, scamp_c=5, periodic_interval=10))
+    else:
+        o = Oracle(default_config(n_nodes=n, seed=seed))
     lib = o._lib
     ev = {}
     for r, ids, contacts in joins:
@@ -75,6 +98,12 @@ def oracle_stream(n, seed, rounds, joins, bcast, crash):
             o.crash(np.array(crash[r], np.uint32))
         if r in bc:
             o.broadcast(*bc[r])
+        if part and r == part[0]:
+            o.set_partition(W.half_partition(n))
+        if part and r == part[1]:
+            o.clear_partition()
+        if leave and r in leave:
+            o.leave_node([a for a, _ in leave[r]], [t for _, t in leave[r]])
         st = np.zeros(1, _abi.STATS_DTYPE)
         assert lib.orc_round_emit(o._h, st.ctypes.data) == 0
         k = C.c_size_t()

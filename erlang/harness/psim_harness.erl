@@ -26,7 +26,7 @@
 %% and Plumtree's (pt = src/partisan_plumtree_broadcast.erl): init/1
 %% (:251-264), handle_cast/2 (:282-336), handle_info(lazy_tick) (:341-345).
 -module(psim_harness).
--export([main/1, run/2, spec/1, id_of/1, reachable/2, register_conn/3, record/3,
+-export([main/1, run/2, spec/1, name/1, id_of/1, reachable/2, register_conn/3, record/3,
          pt_update/1, pt_send/4, have/1, have_add/1]).
 
 -define(HV, partisan_hyparview_peer_service_manager).
@@ -119,7 +119,16 @@ node_round(Id, Node0, R, Crashed, Msgs, Origin) ->
               true -> noreply(?HV:handle_cast({join, spec(Contact)}, HV0));
               false -> HV0
           end,
-    %% b. EXIT for every active member that crashed this round, to_list order (Q11)
+    %% b. EXIT at every holder of a connection to a peer that crashed this
+    %% round (App. A Q11): the active members holding one, in to_list order,
+    %% then the node's other connections (lingering ones: a shuffle reply's
+    %% Sender, a rejected requester, a pending promotion, the join contact),
+    %% in id order -- their EXITs only edit the passive view and the
+    %% connections, so their order among themselves does not matter; the
+    %% oracle (psim_oracle.c process_node) runs them in the same sequence
+    Active1 = [P || P <- sets:to_list(element(?ST_ACTIVE, HV1)), id_of(P) =/= Id],
+    Others = lists:usort([D || {{S, D}, _} <- maps:to_list(get(psim_h_conn_map, #{})), S =:= Id,
+                               not lists:member(D, [id_of(P) || P <- Active1])]),
     HV2 = lists:foldl(fun(P, H) ->
                               case lists:member(id_of(P), Crashed) of
                                   true ->
@@ -130,10 +139,11 @@ node_round(Id, Node0, R, Crashed, Msgs, Origin) ->
                                       end;
                                   false -> H
                               end
-                      end, HV1, [P || P <- sets:to_list(element(?ST_ACTIVE, HV1)), id_of(P) =/= Id]),
-    %% connections to nodes that are down or across the partition fail at
-    %% send time (R0: the connect rule is evaluated when a message is sent)
-    HV3 = prune_unreachable(Id, HV2),
+                      end, HV1, Active1 ++ [spec(D) || D <- Others]),
+    %% connections to peers across the partition stay open but carry nothing
+    %% this round (R0: the connect rule is evaluated when a message is sent):
+    %% they are set aside for the node's round and put back after it
+    {HV3, SetAside} = set_aside_unreachable(Id, HV2),
     Fresh = Start =:= R,                                      % a fresh incarnation drops its inbox
     {HvMsgs, PtMsgs} = lists:partition(fun is_hv/1, case Fresh of true -> []; false -> Msgs end),
     %% c. HyParView inbox
@@ -165,7 +175,7 @@ node_round(Id, Node0, R, Crashed, Msgs, Origin) ->
               false -> PT2
           end,
     {_, _, Ctr} = psim_philox:state(),
-    Node0#{hv := HV6, pt := PT3, ctr := Ctr, have := get(psim_h_have)}.
+    Node0#{hv := put_back(SetAside, get(psim_h_hv)), pt := PT3, ctr := Ctr, have := get(psim_h_have)}.
 
 noreply({noreply, S}) -> S.
 
@@ -177,13 +187,29 @@ is_hv(M) when is_tuple(M) ->
 
 conns(HV) -> element(?ST_CONNECTIONS, HV).
 
-prune_unreachable(Id, HV) ->
-    Conns = lists:foldl(fun(P, C) ->
-                                case reachable(Id, P) of
-                                    true -> C;
-                                    false -> partisan_peer_service_connections:erase(name(P), C)
+set_aside_unreachable(Id, HV) ->
+    {Conns, Aside} =
+        lists:foldl(fun(P, {C, A}) ->
+                            case {reachable(Id, P), partisan_peer_service_connections:find(name(P), C)} of
+                                {false, {ok, Entries}} when Entries =/= [] ->
+                                    {partisan_peer_service_connections:erase(name(P), C), [{P, Entries} | A]};
+                                _ -> {C, A}
+                            end
+                    end, {conns(HV), []}, known_peers(Id)),
+    {setelement(?ST_CONNECTIONS, HV, Conns), Aside}.
+
+%% the set-aside connections back, unless the round made a new one to the
+%% same peer (residual, unpinned: a disconnect/2 of a set-aside peer during
+%% the round is not replayed on it)
+put_back(Aside, HV) ->
+    Conns = lists:foldl(fun({P, Entries}, C) ->
+                                case partisan_peer_service_connections:find(name(P), C) of
+                                    {ok, E} when E =/= [] -> C;
+                                    _ -> lists:foldl(fun({A, Ch, Pid}, C1) ->
+                                                             partisan_peer_service_connections:store(spec(P), {A, Ch, Pid}, C1)
+                                                     end, C, Entries)
                                 end
-                        end, conns(HV), known_peers(Id)),
+                        end, conns(HV), Aside),
     setelement(?ST_CONNECTIONS, HV, Conns).
 
 known_peers(Id) -> [D || {{S, D}, _} <- maps:to_list(get(psim_h_conn_map, #{})), S =:= Id].
@@ -251,14 +277,18 @@ record(Src, Dst, Msg) ->
 pt_update(Names) ->
     put(psim_h_pt, noreply(?PT:handle_cast({update, Names}, get(psim_h_pt)))).
 
-%% Plumtree send/3 over the node's HyParView connections (R0: the target is
-%% in the active view, running and reachable; a self-addressed atom finds
-%% no connection, App. A Q6)
+%% Plumtree send/3 over the node's HyParView connections (forward_message,
+%% hv:441-460 -> do_send_message/4 without maybe_connect): any connection of
+%% the manager -- an active member's or a lingering one (App. A Q11) -- to a
+%% running, reachable peer; a self-addressed atom finds no connection (Q6)
 pt_send(Src, Name, _Kind, Msg) ->
     Dst = id_of(Name),
     HV = get(psim_h_hv),
-    InActive = lists:any(fun(P) -> id_of(P) =:= Dst end, sets:to_list(element(?ST_ACTIVE, HV))),
-    case InActive andalso reachable(Src, Dst) of
+    Conn = case partisan_peer_service_connections:find(name(Dst), conns(HV)) of
+               {ok, [_ | _]} -> true;
+               _ -> false
+           end,
+    case Conn andalso reachable(Src, Dst) of
         true -> record(Src, Dst, Msg);
         false -> {error, disconnected}
     end.

@@ -10,7 +10,7 @@
 -export([create/1, join/3, crash/2, revive/2, leave/2, leave_node/3, broadcast/3, step/2, active/2, members/3,
          delivery/2, histograms/1, snapshot/1, restore/2, set_partition/2, clear_partition/1, node/2,
          begin_send_omission/3, end_send_omission/3, begin_receive_omission/3, end_receive_omission/3,
-         begin_omission/2, end_omission/2, clear_faults/1]).
+         begin_omission/2, end_omission/2, clear_faults/1, msg_slots/1]).
 -on_load(init/0).
 
 %% back-off of a busy handle: 1 ms sleeps, at most ~10 s in all
@@ -56,8 +56,11 @@ set_partition(Sim, Groups) ->
     Bin = << <<G:8>> || G <- Groups >>,
     call(fun() -> set_partition_nif(Sim, Bin) end).
 clear_partition(Sim) -> call(fun() -> clear_partition_nif(Sim) end).
-%% one node: {ok, #{up, epoch, active, passive, have, slots, round}}
+%% one node: {ok, #{up, epoch, active, passive, have, round}}
 node(Sim, Node) -> call(fun() -> node_nif(Sim, Node) end).
+%% the live message slots: {ok, [{Slot, MsgId, RootId}]} -- delivery bit
+%% Slot of node/2's `have` answers for MsgId only (psim_get_msg_slots)
+msg_slots(Sim) -> call(fun() -> msg_slots_nif(Sim) end).
 
 %% omission faults of the pluggable manager's interposition layer (the
 %% crash-fault model's commands, test/prop_partisan_crash_fault_model.erl
@@ -104,3 +107,4 @@ delivery_nif(_S, _N) -> erlang:nif_error(nif_not_loaded).
 clear_partition_nif(_S) -> erlang:nif_error(nif_not_loaded).
 clear_faults_nif(_S) -> erlang:nif_error(nif_not_loaded).
 node_nif(_S, _N) -> erlang:nif_error(nif_not_loaded).
+msg_slots_nif(_S) -> erlang:nif_error(nif_not_loaded).

@@ -38,15 +38,33 @@ broadcast_data(#sim_broadcast{root = Root, counter = C}) ->
 merge(Id, _Payload) ->
     not is_stale(Id).
 
+%% Counter's slot must still hold Counter: a retired id (its slot taken by
+%% a newer broadcast, Counter - 64k) is one the backend no longer knows --
+%% stale for is_stale/1 (the engine treats it so, counting an overflow) and
+%% not graftable
 is_stale({_Root, Counter}) ->
-    {Sim, Me} = handle(),
-    {ok, #{have := Have}} = partisan_gpu_sim:node(Sim, Me),
-    (Have bsr (Counter rem 64)) band 1 =:= 1.
+    case delivered(Counter) of
+        retired -> true;
+        Have -> Have
+    end.
 
-graft(Id) ->
-    case is_stale(Id) of
+graft(Id = {_Root, Counter}) ->
+    case delivered(Counter) of
         true -> {ok, Id};
-        false -> {error, {not_found, Id}}
+        _ -> {error, {not_found, Id}}
+    end.
+
+%% true / false: the simulated node's delivery bit of a live id; retired
+delivered(Counter) ->
+    {Sim, Me} = handle(),
+    Slot = Counter rem 64,
+    {ok, Slots} = partisan_gpu_sim:msg_slots(Sim),
+    case lists:keyfind(Slot, 1, Slots) of
+        {Slot, Counter, _Root} ->
+            {ok, #{have := Have}} = partisan_gpu_sim:node(Sim, Me),
+            (Have bsr Slot) band 1 =:= 1;
+        _ ->
+            retired
     end.
 
 exchange(_Peer) ->

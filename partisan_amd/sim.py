@@ -191,6 +191,15 @@ class _Driver:
                                               _abi.u32p(rnd), _abi.u32p(hop)), "get_delivery")
         return have, rnd, hop
 
+    def msg_slots(self):
+        """The live Plumtree message slots (psim_get_msg_slots): per slot k the
+        message id owning it (NONE = free) and its root identity."""
+        ids = np.zeros(_abi.MSG_SLOTS, np.uint32)
+        roots = np.zeros(_abi.MSG_SLOTS, np.uint32)
+        self._check(self._api["get_msg_slots"](self._h, _abi.u32p(ids), _abi.u32p(roots), ids.size),
+                    "get_msg_slots")
+        return ids, roots
+
     def histograms(self):
         """Overlay statistics (psim_histograms) as a dict of ints / arrays."""
         h = _abi.PsimHistograms()

@@ -439,3 +439,16 @@ def test_snapshot_restore_continues_identically():
     b = other.step(40)
     S.compare_stats(a, b)
     S.compare_nodes(sim.nodes(), other.nodes())
+
+
+def test_msg_slots_and_strict_gpu():
+    """psim_get_msg_slots and cfg.strict on the GPU: six live roots overflow
+    the four root slots -- counted identically to the oracle by default, a
+    failed step (PSIM_ECAPACITY) with strict = 1."""
+    from partisan_amd.sim import SimError
+    (gs, gst, _), (os_, ost, _) = _both(S.multi_root, n=512, roots=6, rounds=60)
+    S.compare_stats(gst, ost)
+    for a, b in zip(gs.msg_slots(), os_.msg_slots()):
+        assert np.array_equal(a, b)
+    with pytest.raises(SimError, match="overflowed"):
+        S.multi_root(_gpu, n=512, roots=6, rounds=60, strict=1)

@@ -37,3 +37,25 @@ def test_scenario_and_compare(tmp_path):
     open(bad, "w").write("\n".join(mod) + "\n")
     r = _run("compare", bad, stream)
     assert r.returncode == 1 and "record 500 differs" in r.stdout
+
+
+def test_strategy_scenarios(tmp_path):
+    """The pluggable-manager scenarios of psim_strategy_harness.erl (configs
+    B and D in miniature): the event script names the strategy, its leave/1
+    and partition events, and the oracle's stream carries the handshake and
+    the strategy's own message types in the harness's record format."""
+    d = str(tmp_path)
+    for name, types in (("scamp_v1_128_pl", {0, 1, 3, 4, 6}), ("scamp_v2_128_pl", {0, 1, 3, 4, 5, 7}),
+                        ("full_16_pl", {0, 1, 2})):
+        r = _run("scenario", name, d)
+        assert r.returncode == 0, r.stderr
+        terms = open(os.path.join(d, name + ".terms")).read()
+        strategy = name.rsplit("_", 2)[0] if name.startswith("full") else name[:8]
+        assert f"strategy => {strategy}" in terms and "periodic_interval => 10" in terms
+        if name.startswith("scamp"):
+            assert "{leave, 50, [{9, 10}]}." in terms and "{clear_partition, 70}." in terms
+        lines = open(os.path.join(d, name + ".oracle")).read().splitlines()
+        got = {int(l.split()[5]) for l in lines}
+        assert types <= got, (name, sorted(got))
+        assert all(len(l.split()) == 11 and l.split()[6] == "0" for l in lines)   # ttl 0, no exchange ids
+        assert _run("compare", os.path.join(d, name + ".oracle"), os.path.join(d, name + ".oracle")).returncode == 0

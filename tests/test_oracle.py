@@ -363,3 +363,22 @@ def test_lingering_exits_prune_every_holder():
     # (a passive view may take a victim back in the same round from an
     # exchange already in flight, so only the EXITs are counted here)
     assert int(st["exits"].sum()) >= sum(len(holders[p]) for p in victims)
+
+
+def test_msg_slots_and_strict_capacity():
+    """psim_get_msg_slots names the id and root owning each message slot; with
+    cfg.strict a fixed-table overflow -- here a fifth live Plumtree root at a
+    node (PSIM_PT_ROOTS = 4, the heartbeat case of plumtree_backend:179-200)
+    -- fails the step loudly instead of being counted."""
+    from partisan_amd import _abi
+    from partisan_amd.sim import SimError
+    sim, st, roots = S.multi_root(Oracle, n=512, roots=6, rounds=60)
+    ids, rts = sim.msg_slots()
+    live = ids != _abi.PSIM_NONE
+    assert live.sum() > 0 and all(int(i) % _abi.MSG_SLOTS == k for k, i in enumerate(ids) if i != _abi.PSIM_NONE)
+    assert set(int(r) & ~_abi.PSIM_MAP_BIT for r in rts[live]) <= set(roots)
+    assert int(st["overflow_by"][:, 2].sum()) > 0             # counted (strict = 0)
+    with pytest.raises(SimError, match="ECAPACITY"):
+        S.multi_root(Oracle, n=512, roots=6, rounds=60, strict=1)
+    _, st4, _ = S.multi_root(Oracle, n=512, roots=4, rounds=60, strict=1)   # four roots fit
+    assert int(st4["overflow"].sum()) == 0
