@@ -512,52 +512,16 @@ def main():
         ovf_run[:] += s_["overflow_by"].sum(axis=0).astype(np.uint64)
         return s_
 
-    survey = args.workload == "C" and args.schedule == "survey"
-    if survey:
-        # the 64-round join ramp and 100 warm-up rounds; the
-        # --warmup rounds follow, then the one broadcast opens the window
-        boot = W.survey_join(n, args.seed)
-        ovf_run[:] += sim.run_schedule(boot, W.SURVEY_RAMP + SURVEY_WARM)["overflow_by"].sum(axis=0).astype(np.uint64)
-    else:
-        boot = W.doubling_join(n, args.seed)
-        ovf_run[:] += sim.run_schedule(boot, boot[-1][0] + 1 + args.settle)["overflow_by"].sum(axis=0).astype(np.uint64)
-
-    # event index i counts rounds from the start of the broadcast phase:
-    # doubling: STEADY_ROUNDS untimed broadcast rounds (whatever --warmup is),
-    # the warmup rounds, then the timed window; survey: the warmup rounds,
-    # then the timed window, whose first round carries the broadcast
-    state = {"k": 0, "last_bcast": None}
-    churn = {}
-    t_start = args.warmup if survey else STEADY_ROUNDS + args.warmup
-    if args.workload == "E":
-        # config E: 0.2*N crashes spread over 100 rounds, each
-        # victim restarts the next round and rejoins; ids [0, N/2) | [N/2, N)
-        # partitioned for 20 rounds from round 20 of the measured window
-        for r, v, c in W.churn_schedule(n, args.seed, 0.2, STEADY_ROUNDS, 100):
-            churn[r] = (v, c)
-        part = W.half_partition(n)
-        p_on, p_off = t_start + 20, t_start + 40
-
-    def bcast_round(i):
-        return i == t_start if survey else i % BCAST_PERIOD == 0
-
-    def round_events(i):
-        if bcast_round(i):
-            sim.broadcast(0, state["k"] % 0x10000)
-            state["k"] += 1
-            state["last_bcast"] = i
-        if args.workload == "E":
-            if i in churn:
-                sim.crash(churn[i][0])
-            if i - 1 in churn:
-                sim.join(churn[i - 1][0], churn[i - 1][1])
-            if i == p_on:
-                sim.set_partition(part)
-            if i == p_off:
-                sim.clear_partition()
-
-    def has_events(i):
-        return bcast_round(i) or (args.workload == "E" and (i in churn or i - 1 in churn or i in (p_on, p_off)))
+    sched = W.BenchSchedule(args.workload, args.schedule, n, args.seed, args.warmup, args.settle)
+    survey = sched.survey
+    boot, until = sched.bootstrap()
+    ovf_run[:] += sim.run_schedule(boot, until)["overflow_by"].sum(axis=0).astype(np.uint64)
+    # phase-round i counts from the end of the bootstrap; the timed window
+    # starts at t_start (workloads.BenchSchedule)
+    t_start = sched.t_start
+    round_events = lambda i: sched.apply(sim, i)      # noqa: E731
+    has_events = sched.has_events
+    bcast_round = sched.bcast_round
 
     for i in range(t_start):
         round_events(i)
@@ -655,7 +619,7 @@ def main():
     # overlay statistics (psim_get_histograms; outside the measurement):
     # drain rounds without new broadcasts until the tracked (last) broadcast
     # has had at least its last hop + 5 rounds and OVERLAY_DRAIN rounds
-    since = t_start + args.steps - state["last_bcast"]
+    since = t_start + args.steps - sched.last_bcast
     step(OVERLAY_DRAIN)
     drained = OVERLAY_DRAIN
     while True:

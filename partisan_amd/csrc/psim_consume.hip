@@ -1091,7 +1091,9 @@ DEV NodeIn load_node(KArgs& a, uint32_t D) {
 }
 
 // the connection-table entry in cache lane 40 + j (j < conn_n, else NONE):
-// the peer of a lingering connection; NONE for a member marked down
+// the peer of a lingering connection; NONE for a member marked down.  Every
+// lane must call it (a shuffle reads lanes 0-7: a lane outside the exec
+// mask reads as 0)
 DEV uint32_t conn_cache_id(uint32_t CN, uint32_t H) {
     const uint32_t l = lane_id(), cn = rl(H, HW_CONN) & 0xFF;
     const uint32_t e = shfl(CN, (int)(l & 7));
@@ -1115,7 +1117,10 @@ DEV NodeX load_x(KArgs& a, const NodeIn& x) {
     // (LITE: k_consume_lite's handlers only send to active members and to
     // senders -- no passive-member entries)
     uint32_t cv = l < 32 ? (!LITE && l < pas_n ? x.P : NONE) : (l < 40 && l - 32 < act_n ? av : NONE);
-    if (!LITE && l >= 40) cv = conn_cache_id(x.CN, x.H);
+    if (!LITE) {                                     // (uniform: every lane runs the shuffle)
+        const uint32_t cc = conn_cache_id(x.CN, x.H);
+        cv = l >= 40 ? cc : cv;
+    }
     y.CV = cv;
     y.CF = cache_flags(a, cv, x.n);
     return y;
@@ -1635,7 +1640,8 @@ DEV PtIn load_pt_node(KArgs& a, uint32_t D) {
 DEV uint32_t act_cache(const PtIn& x) {
     const uint32_t l = lane_id(), act_n = rl(x.H, 9) & 0xFF;
     const uint32_t av = shfl(x.A, (int)(l & 7));
-    return l >= 32 && l < 40 && l - 32 < act_n ? av : (l >= 40 ? conn_cache_id(x.CN, x.H) : NONE);
+    const uint32_t cc = conn_cache_id(x.CN, x.H);    // (every lane: it shuffles)
+    return l >= 32 && l < 40 && l - 32 < act_n ? av : (l >= 40 ? cc : NONE);
 }
 
 DEV PtX load_pt_x(KArgs& a, const PtIn& x) {

@@ -107,3 +107,67 @@ def half_partition(n_nodes):
     g = np.zeros(n_nodes, np.uint8)
     g[n_nodes // 2:] = 1
     return g
+
+
+class BenchSchedule:
+    """The event schedule of bench.py's config C and E lines -- one source for
+    the bench, the bench-scale parity fixtures (tests/golden/gen_bench_fixtures.py)
+    and their GPU test.
+
+    C, schedule "survey" (SURVEY.md 8(d)): survey_join's 64-round ramp and
+    SURVEY_WARM warm-up rounds, then `warmup` rounds, then the timed window,
+    whose first round carries the one broadcast from node 0.
+    C / E, schedule "doubling": doubling_join, `settle` rounds, STEADY_ROUNDS
+    untimed broadcast rounds, `warmup` rounds, the window; a broadcast from
+    node 0 every BCAST_PERIOD rounds throughout.  E adds 0.2 N crashes over
+    100 rounds from STEADY_ROUNDS (each victim restarts and rejoins the next
+    round) and the half/half partition for rounds 20-39 of the window.
+    Phase-round i counts from the end of the bootstrap; the window starts at
+    i = t_start."""
+    STEADY_ROUNDS = 40
+    BCAST_PERIOD = 10
+    SURVEY_WARM = 100
+
+    def __init__(self, workload, schedule, n, seed, warmup, settle=60):
+        self.workload, self.n, self.seed = workload, n, seed
+        self.survey = workload == "C" and schedule == "survey"
+        self.settle = settle
+        self.t_start = warmup if self.survey else self.STEADY_ROUNDS + warmup
+        self.k = 0
+        self.last_bcast = None
+        self.churn = {}
+        if workload == "E":
+            for r, v, c in churn_schedule(n, seed, 0.2, self.STEADY_ROUNDS, 100):
+                self.churn[r] = (v, c)
+            self.part = half_partition(n)
+            self.p_on, self.p_off = self.t_start + 20, self.t_start + 40
+
+    def bootstrap(self):
+        """(join schedule, the round run_schedule runs to)"""
+        if self.survey:
+            return survey_join(self.n, self.seed), SURVEY_RAMP + self.SURVEY_WARM
+        boot = doubling_join(self.n, self.seed)
+        return boot, boot[-1][0] + 1 + self.settle
+
+    def bcast_round(self, i):
+        return i == self.t_start if self.survey else i % self.BCAST_PERIOD == 0
+
+    def has_events(self, i):
+        return self.bcast_round(i) or (self.workload == "E" and (i in self.churn or i - 1 in self.churn or
+                                                                 i in (self.p_on, self.p_off)))
+
+    def apply(self, sim, i):
+        """the events of phase-round i, before it runs"""
+        if self.bcast_round(i):
+            sim.broadcast(0, self.k % 0x10000)
+            self.k += 1
+            self.last_bcast = i
+        if self.workload == "E":
+            if i in self.churn:
+                sim.crash(self.churn[i][0])
+            if i - 1 in self.churn:
+                sim.join(self.churn[i - 1][0], self.churn[i - 1][1])
+            if i == self.p_on:
+                sim.set_partition(self.part)
+            if i == self.p_off:
+                sim.clear_partition()

@@ -78,6 +78,26 @@ def joiner_crash(make, n=2048, seed=3, rounds=40, **cfg):
     return sim, st
 
 
+def heartbeat(make, n=64, seed=23, rounds=120, period=10, first=40, **cfg):
+    """plumtree_backend's heartbeat (backend:179-200, :221-228): every live
+    node broadcasts {mynode(), unique_integer} every `period` rounds, so every
+    node is a root (p8).  Each node beats at its own phase (id mod period);
+    message ids count up and wrap the 64 slots.  With more live roots than a
+    node's PSIM_PT_ROOTS slots and more live ids than PSIM_MSG_SLOTS, the
+    overflows are counted (cfg.strict = 0) or fail the step (strict = 1)."""
+    sim = make(default_config(n_nodes=n, seed=seed, **cfg))
+    state = {"k": 0}
+
+    def hook(r):
+        if r >= first:
+            for root in range(n):
+                if (r + root) % period == 0:
+                    sim.broadcast(root, state["k"] % 0x10000)
+                    state["k"] += 1
+    st = sim.run_schedule(W.doubling_join(n, seed), rounds, extra=hook)
+    return sim, st
+
+
 def lingering_exits(make, n=2048, seed=5, extra_rounds=6, k=16):
     """churn_partition, then a crash of the k peers held by the most
     lingering connections: their EXITs reach holders

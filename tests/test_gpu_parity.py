@@ -452,3 +452,41 @@ def test_msg_slots_and_strict_gpu():
         assert np.array_equal(a, b)
     with pytest.raises(SimError, match="overflowed"):
         S.multi_root(_gpu, n=512, roots=6, rounds=60, strict=1)
+
+
+def test_heartbeat_parity():
+    """Every node a root (plumtree_backend's heartbeat, backend:179-200):
+    64 nodes beating every 10 rounds overflow the 4 root slots; GPU and
+    oracle count the same overflows (strict = 0) and both fail the step with
+    strict = 1 (the test above covers the GPU's error)."""
+    (gs, gst), (os_, ost) = _both(S.heartbeat)
+    S.compare_stats(gst, ost)
+    S.compare_nodes(gs.nodes(), os_.nodes())
+    assert int(ost["overflow_by"][:, 2].sum()) > 0
+
+
+@pytest.mark.parametrize("name", ["C_survey", "C_doubling"])
+def test_bench_schedule_parity(name):
+    """bench.py's exact schedules (workloads.BenchSchedule) at the bench's
+    2^20 nodes, into the timed window -- the survey line's broadcast round,
+    or two broadcasts and a cohort merge round of the doubling line --
+    against the oracle's committed run of the same schedule
+    (tests/golden/gen_bench_fixtures.py): every round's digest and counts,
+    and the hash of every node's final view."""
+    import hashlib
+    import json
+    import os
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, os.path.join(here, "golden"))
+    import gen_bench_fixtures as G
+    fx = json.load(open(os.path.join(here, "golden", "bench_fixtures.json")))
+    want = fx["fixtures"][name]
+    st, nodes = G.run(_gpu, name, n=fx["nodes"], seed=fx["seed"], warmup=fx["warmup"], window=fx["window"][name])
+    assert len(st) == want["rounds"]
+    for f in G.FIELDS:
+        got = st[f].tolist()
+        if got != want[f]:
+            bad = next(i for i, (a, b) in enumerate(zip(got, want[f])) if a != b)
+            raise AssertionError(f"{name}: {f} differs first at round {bad}")
+    assert hashlib.sha256(nodes.tobytes()).hexdigest() == want["state_sha256"]

@@ -382,3 +382,13 @@ def test_msg_slots_and_strict_capacity():
         S.multi_root(Oracle, n=512, roots=6, rounds=60, strict=1)
     _, st4, _ = S.multi_root(Oracle, n=512, roots=4, rounds=60, strict=1)   # four roots fit
     assert int(st4["overflow"].sum()) == 0
+
+
+def test_heartbeat_fails_loudly_when_strict():
+    """More live Plumtree roots than a node's slots: counted by default,
+    PSIM_ECAPACITY with cfg.strict (no silent protocol change)."""
+    from partisan_amd.sim import SimError
+    _, st = S.heartbeat(Oracle)
+    assert int(st["overflow"].sum()) > 0
+    with pytest.raises(SimError, match="ECAPACITY"):
+        S.heartbeat(Oracle, strict=1)
