@@ -1410,6 +1410,7 @@ DEV void writeback(Wv& w) {
 // one HyParView-phase wave per node of the list (k_relay leaves here every
 // node whose HyParView work is more than one SHUFFLE relay)
 __global__ void __launch_bounds__(256, PSIM_WAVES_PER_SIMD) k_consume(RoundArgs args) {
+    if (*kargs().ctl) return;                         // an aborted batch (run_batch)
     __shared__ uint64_t sst[NST];
     __shared__ uint32_t scratch[WAVES_PER_BLOCK][64];
     __shared__ uint32_t nlogs[WAVES_PER_BLOCK][NLOG * (PSIM_ACTIVE_CAP + 1)];
@@ -1554,6 +1555,7 @@ DEV void writeback_lite(Wv& w) {
 #define PSIM_LITE_WAVES 6
 #endif
 __global__ void __launch_bounds__(256, PSIM_LITE_WAVES) k_consume_lite(RoundArgs args) {
+    if (*kargs().ctl) return;                         // an aborted batch (run_batch)
     __shared__ uint64_t sst[NST];
     __shared__ uint32_t scratch[WAVES_PER_BLOCK][64];
     __shared__ __attribute__((aligned(16))) uint32_t srecs[WAVES_PER_BLOCK][STAGE * 16];
@@ -1756,6 +1758,7 @@ DEV void writeback_pt(Wv& w, uint32_t H) {
 #define PSIM_PT_WAVES 5
 #endif
 __global__ void __launch_bounds__(256, PSIM_PT_WAVES) k_pt(RoundArgs args) {
+    if (*kargs().ctl) return;                         // an aborted batch (run_batch)
     __shared__ uint64_t sst[NST];
     __shared__ uint32_t scratch[WAVES_PER_BLOCK][64];
     __shared__ __attribute__((aligned(16))) uint32_t srecs[WAVES_PER_BLOCK][STAGE * 16];
@@ -1868,6 +1871,7 @@ DEV void block_append(bool go, const uint4& D, uint4* desc, uint32_t* cnt, uint3
 #define PSIM_RELAY_WAVES 4
 #endif
 __global__ void __launch_bounds__(256, PSIM_RELAY_WAVES) k_relay(RoundArgs) {
+    if (*kargs().ctl) return;                         // an aborted batch (run_batch)
     enum { R_PROC, R_DELIV, R_SHUF, R_FAIL, R_DIGEST, R_BOUND, R_N };
     __shared__ unsigned long long sst[R_N];
     __shared__ uint32_t wc5[5][5];                    // per list: the wave counts, then the block's base
@@ -2118,6 +2122,7 @@ DEV void topk_insert(uint64_t (&K)[SHUF_TOPK], uint32_t (&E)[SHUF_TOPK], uint64_
 }
 
 __global__ void __launch_bounds__(256) k_shuf(RoundArgs) {
+    if (*kargs().ctl) return;                         // an aborted batch (run_batch)
     enum { S_SHUF, S_FAIL, S_DIGEST, S_BOUND, S_N };
     __shared__ unsigned long long sst[S_N];
     if (threadIdx.x < S_N) sst[threadIdx.x] = 0;
@@ -2398,6 +2403,7 @@ DEV void ptl_ack_out(PtLane& n, uint64_t key) {
 #define PSIM_PTL_BLOCKS_PER_CU 3
 #endif
 __global__ void __launch_bounds__(PTL_BLK, PSIM_PTL_BLOCKS_PER_CU) k_ptl(RoundArgs) {
+    if (*kargs().ctl) return;                         // an aborted batch (run_batch)
     enum { T_FIRST, T_FAIL, T_OVF, T_BOUND, T_DLV, T_EMT = T_DLV + 5, T_N = T_EMT + 5 };
     __shared__ unsigned long long sst[T_N + 1];       // (+ the digest)
     __shared__ uint32_t sslots[2 * PSIM_MSG_SLOTS];
@@ -2675,8 +2681,8 @@ __global__ void __launch_bounds__(PTL_BLK, PSIM_PTL_BLOCKS_PER_CU) k_ptl(RoundAr
 // (slot 0) and after the last node-round kernel (slot 1), on the same
 // stream -- one wave each instead of a same-address atomic from every block
 // of every kernel (~10^4 per round)
-__global__ void k_mark(unsigned long long* t, int slot) {
-    if (threadIdx.x == 0) t[slot] = __builtin_amdgcn_s_memrealtime();
+__global__ void k_mark(unsigned long long* t, int slot, const uint32_t* ctl) {
+    if (threadIdx.x == 0 && !*ctl) t[slot] = __builtin_amdgcn_s_memrealtime();
 }
 
 // one wave-slot per resident wave: the grid strides over the active list

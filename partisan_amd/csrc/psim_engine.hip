@@ -43,6 +43,10 @@ constexpr int BLK = 256;
 // pinned host words per shard (Shard::pin): NST stats, the consume span, the
 // outbox total, the routed record count -- stored by kernels, read by the host
 enum { PIN_TOTAL = NST + 2, PIN_M = NST + 3, PIN_OVF = NST + 4, PIN_BIGIN = NST + 5 };
+// the pinned words: slot 0 holds the above (and a single round's stats);
+// slot j + 1 the stats and node-round span of round j of a batch (run_batch)
+constexpr uint32_t PIN_STRIDE = NST + 8;
+constexpr uint32_t BATCH_MAX = 64;
 
 #define HIP_TRY(x)                                                       \
     do {                                                                 \
@@ -89,9 +93,9 @@ __global__ void k_leave_set(Hdr* hdr, uint32_t lo, uint32_t n_local, const uint3
     if (id >= lo && id < lo + n_local) hdr[id - lo].pad1[0] = targets[i] + 1;
 }
 
-__global__ void k_uncrash(uint8_t* flags, const uint32_t* ids, uint32_t n) {
+__global__ void k_uncrash(uint8_t* flags, const uint32_t* ids, uint32_t n, const uint32_t* ctl) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
+    if (i >= n || *ctl) return;
     flags[ids[i]] &= (uint8_t)~F_CRASHED;
 }
 
@@ -179,9 +183,9 @@ __global__ void k_bcast_reset(Hdr* hdr, uint32_t n, uint32_t lo, uint32_t hi) {
 // start events, which precede this on the stream) originate them:
 // origin[root - lo] = msg + 1; clear = true resets the same entries
 __global__ void k_origin(uint32_t* origin, uint32_t lo, uint32_t n_local, const uint32_t* roots,
-                         const uint32_t* msgs, uint32_t k, const uint8_t* flags, bool clear) {
+                         const uint32_t* msgs, uint32_t k, const uint8_t* flags, bool clear, const uint32_t* ctl) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= k) return;
+    if (i >= k || *ctl) return;
     const uint32_t r = roots[i];
     if (r < lo || r >= lo + n_local) return;
     if (clear) origin[r - lo] = 0;
@@ -273,7 +277,8 @@ __device__ __forceinline__ void route_step(const RouteIn& in, uint32_t step, uin
 template <bool DENSE>
 __global__ void __launch_bounds__(RB_STEP) k_bucket_hist(RouteIn in, uint32_t nsteps, uint32_t nb,
                                                          uint32_t wshift, uint32_t* hist, uint32_t* n_long,
-                                                         unsigned long long* btot) {
+                                                         unsigned long long* btot, const uint32_t* ctl) {
+    if (*ctl) return;                                 // an aborted batch (run_batch)
     extern __shared__ uint32_t hcnt[];                // nb bucket counters
     __shared__ uint32_t spre[4][65];
     __shared__ uint64_t sbase[4][64];
@@ -294,11 +299,18 @@ __global__ void __launch_bounds__(RB_STEP) k_bucket_hist(RouteIn in, uint32_t ns
 template <bool DENSE>
 __global__ void __launch_bounds__(RB_STEP) k_bucket_scatter(RouteIn in, uint32_t nsteps, uint32_t nb,
                                                             uint32_t wshift, const uint32_t* __restrict__ off,
-                                                            uint2* pairs, uint64_t cap, uint64_t* hovf) {
+                                                            uint2* pairs, uint64_t cap, uint64_t* hovf,
+                                                            uint32_t* ctl, uint32_t round1) {
+    if (*ctl) return;                                 // an aborted batch (run_batch)
     extern __shared__ uint32_t hcnt[];                // nb rank counters
     const uint32_t m = off[(size_t)nb * gridDim.x];   // the record count
     if (m > cap) {                                    // the route buffers are too small:
-        if (blockIdx.x == 0 && threadIdx.x == 0) *hovf = m;   // the host grows them and reruns
+        if (blockIdx.x == 0 && threadIdx.x == 0) {    // the host grows them and reruns
+            *hovf = m;
+            // (a batch: this round's route and every later kernel of the
+            // batch stand still -- round round1 - 1, code 2)
+            if (round1) { ctl[1] = round1 - 1; __threadfence(); ctl[0] = 2; }
+        }
         return;
     }
     __shared__ uint32_t spre[4][65];
@@ -428,7 +440,8 @@ __global__ void __launch_bounds__(RR_THREADS) k_bucket_route(
     uint32_t n, uint32_t wshift, uint32_t nblk, const uint32_t* __restrict__ off,
     const uint2* __restrict__ pairs, const Msg* __restrict__ rec, uint32_t* rank, unsigned long long* cb,
     unsigned long long* bmask, uint32_t* in_beg, uint32_t* idx, uint32_t* long_list, uint32_t* n_long, uint64_t* hm,
-    uint64_t cap) {
+    uint64_t cap, const uint32_t* ctl) {
+    if (*ctl) return;                                 // an aborted batch (run_batch)
     extern __shared__ uint32_t sm[];
     __shared__ uint32_t spart[RR_THREADS];
     const uint32_t W = 1u << wshift, wmask = W - 1, b = blockIdx.x;
@@ -546,7 +559,8 @@ __device__ void block_sort_lds(uint32_t* sv, uint32_t* p, uint32_t k) {
 __global__ void __launch_bounds__(256) k_run_sort_long(const uint32_t* __restrict__ in_beg,
                                                        const unsigned long long* __restrict__ cb, uint32_t* idx,
                                                        uint32_t* tmp, const uint32_t* __restrict__ long_list,
-                                                       const uint32_t* n_long) {
+                                                       const uint32_t* n_long, const uint32_t* ctl) {
+    if (*ctl) return;                                 // an aborted batch (run_batch)
     __shared__ uint32_t sv[RUN_LDS];
     const uint32_t nl = *n_long;
     for (uint32_t q = blockIdx.x; q < nl; q += gridDim.x) {
@@ -582,6 +596,7 @@ __device__ __forceinline__ bool due(uint32_t period, uint32_t r, uint32_t start)
 // messages addressed to dead ones.
 __global__ void __launch_bounds__(256) k_node_prep(RoundArgs a, const unsigned long long* bmask, uint64_t* packed,
                                                    uint64_t* part, uint32_t* ocnt, unsigned long long* btot) {
+    if (*a.ctl) return;                               // an aborted batch (run_batch)
     __shared__ unsigned long long s_up, s_drop, s_b;
     if (threadIdx.x == 0) { s_up = 0; s_drop = 0; s_b = 0; }
     if (blockIdx.x == 0 && threadIdx.x == 0) {
@@ -744,15 +759,18 @@ __global__ void k_desc(const uint64_t* __restrict__ packed, const uint64_t* __re
                        const uint32_t* __restrict__ in_beg, const unsigned long long* __restrict__ cb,
                        const uint32_t* __restrict__ start, RoundArgs a, uint4* __restrict__ desc,
                        uint64_t* __restrict__ obase, uint32_t* nact, const unsigned long long* btot,
-                       uint64_t* hout) {
+                       uint64_t* hout, uint64_t cap, uint32_t* ctl) {
     const uint32_t li = blockIdx.x * blockDim.x + threadIdx.x;
-    if (li > a.n_local) return;
+    if (li > a.n_local || *ctl) return;
     const uint64_t P = pscan[li];
     obase[li] = P >> 32;
     if (li == a.n_local) {
         *nact = (uint32_t)P;
         obase[li] = *btot;
         hout[PIN_TOTAL] = *btot;                      // the host's one mid-round read
+        // a batch (cap > 0) checks the outbox here instead: a total past its
+        // capacity stops the rest of the batch (code 1, this round)
+        if (cap && *btot + 1 > cap) { ctl[1] = a.round; __threadfence(); ctl[0] = 1; }
         return;
     }
     if (!(packed[li] & 1u)) return;
@@ -767,8 +785,9 @@ __global__ void k_desc(const uint64_t* __restrict__ packed, const uint64_t* __re
 
 // records src[slots[i]] -> out[i] for i < *pm, grid-stride, 4 lanes x 16 B
 __global__ void k_gather_dev(const Msg* __restrict__ rec, const uint32_t* __restrict__ slots,
-                             const uint32_t* __restrict__ pm, Msg* __restrict__ out, uint64_t cap) {
-    if (*pm > cap) return;                            // the route overflowed: redone by the host
+                             const uint32_t* __restrict__ pm, Msg* __restrict__ out, uint64_t cap,
+                             const uint32_t* ctl) {
+    if (*ctl || *pm > cap) return;                    // the route overflowed: redone by the host
     const uint64_t m4 = (uint64_t)*pm * 4;
     for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < m4;
          t += (uint64_t)gridDim.x * blockDim.x) {
@@ -1127,6 +1146,14 @@ struct Shard {
     bool ev_live = false;
     bool reserved = false;              // first-round capacity reservation done
     uint64_t rcap = 0;                  // records the route's buffers hold (G == 1: checked on the device)
+    // batches of rounds without host waits (run_batch): the abort word
+    // (code, round) in device memory; while a batch is enqueued, k_desc
+    // checks the outbox against desc_cap and the route flags its overflow
+    // for round batch_round1 - 1; round j's stats go to pinned slot j + 1
+    DBuf<uint32_t> ctl;
+    uint64_t desc_cap = 0;
+    uint32_t batch_round1 = 0;
+    uint32_t stat_slot = 0;
 };
 
 }  // namespace
@@ -1207,6 +1234,7 @@ RoundArgs make_args(psim_handle* h, Shard* s) {
     a.fanout = c.fanout; a.fw = h->fw; a.tomb = h->tomb;
     a.fbits = s->fbits.p; a.sview = s->sview.p; a.sinv = s->sinv.p;
     a.ktime = reinterpret_cast<unsigned long long*>(s->stat_out.p + NST);
+    a.ctl = s->ctl.p;
     a.desc_slow = s->desc_slow.p; a.n_slow = s->n_slow.p;
     a.desc_pt = s->desc_pt.p; a.n_pt = s->n_pt.p;
     a.desc_shuf = s->desc_shuf.p; a.n_shuf = s->n_shuf.p;
@@ -1376,10 +1404,14 @@ struct RoundCtl {
     uint64_t bcast_clear = 0;           // message slots this round's broadcasts retire
 };
 
-// events + prepare for one shard; leaves `a` ready for k_consume
-int phase_events_prepare(psim_handle* h, Shard* s, const RoundCtl& ctl, RoundArgs& a) {
+// events + prepare for one shard; leaves `a` ready for k_consume.
+// events = false: the round's events were applied already (the redo of a
+// batch round, run_batch); batched: no host wait -- the outbox and route
+// capacities stand and k_desc checks the outbox on the device (desc_cap)
+int phase_events_prepare(psim_handle* h, Shard* s, const RoundCtl& ctl, RoundArgs& a, bool events = true,
+                         bool batched = false) {
     const uint32_t n = s->n;
-    if (h->faults_dirty) {              // interposition funs installed / removed
+    if (events && h->faults_dirty) {    // interposition funs installed / removed
         std::vector<uint64_t> keys(h->nx_omit_s.begin(), h->nx_omit_s.end());
         keys.insert(keys.end(), h->nx_omit_r.begin(), h->nx_omit_r.end());
         TRY(s->faulted.ensure(h->N));
@@ -1391,7 +1423,7 @@ int phase_events_prepare(psim_handle* h, Shard* s, const RoundCtl& ctl, RoundArg
     }
     a = make_args(h, s);
     a.crash_round = ctl.crashes;
-    {
+    if (events) {
         KTimer t(h, s, KT_EVENTS);
         if (ctl.crashes) {
             TRY(upload(s, s->ev_ids, h->pend_crash));
@@ -1422,7 +1454,7 @@ int phase_events_prepare(psim_handle* h, Shard* s, const RoundCtl& ctl, RoundArg
             TRY(upload(s, s->bc_msgs, h->pend_b_msg));
             HIP_TRY(hipMemcpyAsync(s->slots.p, h->slot_tab, sizeof h->slot_tab, hipMemcpyHostToDevice, s->stream));
             k_origin<<<grid_for(k), BLK, 0, s->stream>>>(s->origin.p, s->lo, n, s->bc_roots.p, s->bc_msgs.p, k,
-                                                          s->flags.p, false);
+                                                          s->flags.p, false, s->ctl.p);
         }
     }
     {
@@ -1449,9 +1481,11 @@ int phase_events_prepare(psim_handle* h, Shard* s, const RoundCtl& ctl, RoundArg
         // obase[n] = the exact total (btot, summed by k_node_prep)
         TRY(scan_excl(s, s->bound.p, s->pscan.p, n + 1));
         k_desc<<<grid_for(n + 1), BLK, 0, s->stream>>>(s->bound.p, s->pscan.p, s->in_beg.p, s->cb.p, s->start.p, a,
-                                                        s->desc.p, s->obase.p, s->d_nact.p, s->btot.p, s->pin_dev);
-        if (s->pin[PIN_BIGIN]) return PSIM_ENOMEM;    // a node's inbox count must fit 27 bits
+                                                        s->desc.p, s->obase.p, s->d_nact.p, s->btot.p, s->pin_dev,
+                                                        s->desc_cap, s->ctl.p);
+        if (batched) goto args;
         TRY(stream_wait(s));                          // (k_desc stored the total in pin)
+        if (s->pin[PIN_BIGIN]) return PSIM_ENOMEM;    // a node's inbox count must fit 27 bits
         const uint64_t total = s->pin[PIN_TOTAL];
         if (total >= 0xFFFFFFFFull) return PSIM_ENOMEM;
         // the bound peaks on broadcast rounds and creeps up for many rounds:
@@ -1469,7 +1503,9 @@ int phase_events_prepare(psim_handle* h, Shard* s, const RoundCtl& ctl, RoundArg
         if (!s->reserved) {
             s->reserved = true;
             size_t fr = 0, tot = 0;
-            if (hipMemGetInfo(&fr, &tot) == hipSuccess) {
+            // (test hook: no reservation -- the outbox grows round by round,
+            // inside batches through the abort word)
+            if (!getenv("PSIM_NO_RESERVE") && hipMemGetInfo(&fr, &tot) == hipSuccess) {
                 const uint64_t per_rec = sizeof(Msg) + 3 * sizeof(uint32_t) + sizeof(uint2);
                 const uint64_t per_slot = sizeof(Msg) + sizeof(uint32_t);
                 // (memory the current buffers hold comes back when they regrow)
@@ -1497,6 +1533,7 @@ int phase_events_prepare(psim_handle* h, Shard* s, const RoundCtl& ctl, RoundArg
         TRY(s->okey.ensure(want, headroom));
         if (h->G == 1) TRY(route_buffers(s, s->m_in == 0));   // the route checks its capacity on the device
     }
+args:
     a.in_beg = s->in_beg.p;
     a.desc = s->desc.p; a.n_alist = s->d_nact.p;
     a.rec_in = s->inbox.p;
@@ -1539,7 +1576,7 @@ int phase_consume(psim_handle* h, Shard* s, RoundArgs& a) {
         // k_relay sorts the nodes with work: a lone SHUFFLE relay (and a
         // lazy tick) one lane each, more HyParView work one k_consume wave,
         // Plumtree work one k_pt wave after the node's HyParView phase
-        k_mark<<<1, 64, 0, s->stream>>>(a.ktime, 0);
+        k_mark<<<1, 64, 0, s->stream>>>(a.ktime, 0, s->ctl.p);
         k_relay<<<s->rgrid, BLK, 0, s->stream>>>(a);
         k_shuf<<<s->sgrid, BLK, 0, s->stream>>>(a);
         k_consume_lite<<<s->lgrid, BLK, 0, s->stream>>>(a);
@@ -1555,7 +1592,7 @@ int phase_consume(psim_handle* h, Shard* s, RoundArgs& a) {
             c.stat_part = a.stat_pt;
             k_pt<<<s->tgrid, BLK, 0, s->stream>>>(c);
         }
-        k_mark<<<1, 64, 0, s->stream>>>(a.ktime, 1);
+        k_mark<<<1, 64, 0, s->stream>>>(a.ktime, 1, s->ctl.p);
     }
     HIP_TRY(hipGetLastError());
     s->pay_cur ^= 1;
@@ -1569,7 +1606,7 @@ int gather_inbox(psim_handle* h, Shard* s, const Msg* src, const uint32_t* dev_m
     KTimer t(h, s, KT_GATHER);
     if (max_m)
         k_gather_dev<<<std::min<uint32_t>(grid_for((uint64_t)max_m * 4), 8192), BLK, 0, s->stream>>>(
-            src, s->ivals.p, dev_m, s->inbox.p, s->rcap);
+            src, s->ivals.p, dev_m, s->inbox.p, s->rcap, s->ctl.p);
     return PSIM_OK;
 }
 
@@ -1593,22 +1630,25 @@ int route_group(psim_handle* h, Shard* s, const Msg* dense, uint32_t m) {
     KTimer t(h, s, KT_SORT);
     if (dense)
         k_bucket_hist<true><<<nblk, RB_STEP, lds_h, s->stream>>>(in, nsteps, nb, wshift, s->hist.p, s->n_long.p,
-                                                                 s->btot.p);
+                                                                 s->btot.p, s->ctl.p);
     else
         k_bucket_hist<false><<<nblk, RB_STEP, lds_h, s->stream>>>(in, nsteps, nb, wshift, s->hist.p, s->n_long.p,
-                                                                  s->btot.p);
+                                                                  s->btot.p, s->ctl.p);
     TRY(scan_excl(s, s->hist.p, s->hoff.p, (uint32_t)nh));
     if (dense)
         k_bucket_scatter<true><<<nblk, RB_STEP, lds_h, s->stream>>>(in, nsteps, nb, wshift, s->hoff.p, s->pairs.p,
-                                                                    s->rcap, s->pin_dev + PIN_OVF);
+                                                                    s->rcap, s->pin_dev + PIN_OVF, s->ctl.p,
+                                                                    s->batch_round1);
     else
         k_bucket_scatter<false><<<nblk, RB_STEP, lds_h, s->stream>>>(in, nsteps, nb, wshift, s->hoff.p,
-                                                                     s->pairs.p, s->rcap, s->pin_dev + PIN_OVF);
+                                                                     s->pairs.p, s->rcap, s->pin_dev + PIN_OVF,
+                                                                     s->ctl.p, s->batch_round1);
     k_bucket_route<<<nb, RR_THREADS, lds_r, s->stream>>>(n, wshift, nblk, s->hoff.p, s->pairs.p, in.rec, s->rank.p,
                                                           s->cb.p, s->bmask.p, s->in_beg.p, s->ivals.p,
-                                                          s->long_list.p, s->n_long.p, s->pin_dev + PIN_M, s->rcap);
+                                                          s->long_list.p, s->n_long.p, s->pin_dev + PIN_M, s->rcap,
+                                                          s->ctl.p);
     k_run_sort_long<<<std::min<uint32_t>(n, 512), 256, 0, s->stream>>>(s->in_beg.p, s->cb.p, s->ivals.p, s->tmp.p,
-                                                                       s->long_list.p, s->n_long.p);
+                                                                       s->long_list.p, s->n_long.p, s->ctl.p);
     HIP_TRY(hipGetLastError());
     return PSIM_OK;
 }
@@ -1630,8 +1670,9 @@ int phase_route_local(psim_handle* h, Shard* s) {
     TRY(route_group(h, s, nullptr, 0));
     // (m_in: read back with the round's stats; ivals, pairs, rank, tmp and the
     // inbox were sized in prepare by the outbox total, which bounds it)
+    // (a batch has no outbox total on the host: the capacity sizes the grid)
     return gather_inbox(h, s, s->outbox.p, s->in_beg.p + s->n,
-                        (uint32_t)std::min<uint64_t>(s->pin[PIN_TOTAL], s->rcap));
+                        (uint32_t)(s->batch_round1 ? s->rcap : std::min<uint64_t>(s->pin[PIN_TOTAL], s->rcap)));
 }
 
 // G > 1, sender side: the outbox partitioned by owner shard into the send
@@ -1740,18 +1781,17 @@ int phase_stats(psim_handle* h, Shard* s, const std::vector<uint32_t>& crashed) 
     const uint32_t rows = s->pgrid + s->cgrid + s->rgrid + s->tgrid + s->sgrid + s->lgrid + s->qgrid;
     const uint32_t nt = std::min<uint32_t>(STAT_TILES, std::max<uint32_t>(1, rows / 32));
     k_stats_tiles<<<nt, BLK, 0, s->stream>>>(s->stat_part.p, rows, s->stat_tile.p);
-    k_stats_final<<<1, BLK, 0, s->stream>>>(s->stat_tile.p, nt, s->stat_out.p, s->pin_dev);
+    k_stats_final<<<1, BLK, 0, s->stream>>>(s->stat_tile.p, nt, s->stat_out.p, s->pin_dev + (size_t)s->stat_slot * PIN_STRIDE);
     if (!crashed.empty()) {
         TRY(upload(s, s->ev_ids, crashed));
         k_uncrash<<<grid_for(crashed.size()), BLK, 0, s->stream>>>(s->flags.p, s->ev_ids.p,
-                                                                  (uint32_t)crashed.size());
+                                                                  (uint32_t)crashed.size(), s->ctl.p);
     }
     return PSIM_OK;
 }
 
-int run_round(psim_handle* h, uint64_t* st) {
-    RoundCtl ctl;
-    ctl.crashes = !h->pend_crash.empty();
+// the host side of a round's broadcast events: message slots, the tracked id
+void bcast_slots(psim_handle* h, RoundCtl& ctl) {
     if (!h->pend_b_root.empty()) {
         // each broadcast takes its message slot (the previous id of the slot
         // retires); the roots' origin entries are set on the device after the
@@ -1764,6 +1804,15 @@ int run_round(psim_handle* h, uint64_t* st) {
         }
         h->tracked_msg = h->pend_b_msg.back();
     }
+}
+
+// One round, waited for.  events_applied: the pending events went to the
+// device already (the redo of an aborted batch round): only their
+// round-end halves run (crash-round EXIT checks, k_uncrash, origins spent).
+int run_round(psim_handle* h, uint64_t* st, bool events_applied = false) {
+    RoundCtl ctl;
+    ctl.crashes = !h->pend_crash.empty();
+    if (!events_applied) bcast_slots(h, ctl);
     if (h->faults_dirty) {              // the funs in force from this round
         if (h->nx_faulted.size() != h->N) h->nx_faulted.assign(h->N, 0);
         h->n_omit_s = (uint32_t)h->nx_omit_s.size();
@@ -1772,7 +1821,8 @@ int run_round(psim_handle* h, uint64_t* st) {
     }
     for (Shard* s : h->shards) s->tn = 0;        // (timers of a round that failed)
     std::vector<RoundArgs> args(h->shards.size());   // (consume fills the payload arena fields)
-    for (size_t i = 0; i < h->shards.size(); i++) TRY(phase_events_prepare(h, h->shards[i], ctl, args[i]));
+    for (size_t i = 0; i < h->shards.size(); i++)
+        TRY(phase_events_prepare(h, h->shards[i], ctl, args[i], !events_applied));
     for (size_t i = 0; i < h->shards.size(); i++) TRY(phase_consume(h, h->shards[i], args[i]));
     if (h->G == 1) {
         TRY(phase_route_local(h, h->shards[0]));
@@ -1786,7 +1836,7 @@ int run_round(psim_handle* h, uint64_t* st) {
         if (!h->pend_b_root.empty())        // this round's origins are spent
             k_origin<<<grid_for(h->pend_b_root.size()), BLK, 0, s->stream>>>(
                 s->origin.p, s->lo, s->n, s->bc_roots.p, s->bc_msgs.p, (uint32_t)h->pend_b_root.size(), s->flags.p,
-                true);
+                true, s->ctl.p);
     }
     memset(st, 0, NST * 8);
     for (Shard* s : h->shards) {
@@ -1902,15 +1952,146 @@ void fill_stats(const uint64_t* s, uint64_t round, psim_round_stats* o) {
     o->omitted = s[ST_OMIT];
 }
 
+// Whether psim_step may run its rounds as batches (run_batch): one RCCL-free
+// HyParView shard past its first round, no diagnostic mode that reads the
+// device between kernels, no strict mode (it stops at the overflowing round)
+bool batchable(psim_handle* h) {
+    static const bool trace = getenv("PSIM_TRACE_RELAY") != nullptr;
+    static const bool off = getenv("PSIM_NO_BATCH") != nullptr;
+    if (off || trace || h->G != 1 || h->world != 1 || h->phase_timers || h->cfg.strict ||
+        h->cfg.manager == PSIM_MANAGER_PLUGGABLE || !h->pend_lv_a.empty())
+        return false;
+    Shard* s = h->shards[0];
+    return s->reserved && s->rcap && s->outbox.n;
+}
+
+// Up to BATCH_MAX rounds enqueued back to back with no host wait between
+// them (the pending events go with the first), then one wait.  A round
+// whose outbox bound passes the outbox capacity (k_desc, code 1) or whose
+// records pass the route's (k_bucket_scatter, code 2) sets the abort word:
+// every later kernel of the batch returns at once, the host grows the
+// buffer and finishes that round waited for -- from prepare (code 1: nothing
+// of it ran past k_desc) or from the route (code 2: its node phases ran).
+// Returns the rounds done (>= 1) in *done; their stats in st_out.
+int run_batch(psim_handle* h, uint32_t nb, psim_round_stats* st_out, uint32_t* done_out) {
+    Shard* s = h->shards[0];
+    const uint64_t r0 = h->round;
+    RoundCtl ctl0;
+    ctl0.crashes = !h->pend_crash.empty();
+    bcast_slots(h, ctl0);
+    const std::vector<uint32_t> crashed0 = h->pend_crash;
+    const std::vector<uint32_t> none;
+    const bool bc0 = !h->pend_b_root.empty();
+    s->tn = 0;
+    s->desc_cap = std::min<uint64_t>(s->outbox.n, s->okey.n);
+    for (uint32_t j = 0; j < nb; j++) {
+        s->stat_slot = j + 1;
+        s->batch_round1 = (uint32_t)h->round + 1;
+        RoundArgs a;
+        const RoundCtl ctl = j == 0 ? ctl0 : RoundCtl{};
+        TRY(phase_events_prepare(h, s, ctl, a, j == 0, true));
+        TRY(phase_consume(h, s, a));
+        TRY(phase_route_local(h, s));
+        TRY(phase_stats(h, s, j == 0 ? crashed0 : none));
+        if (j == 0 && bc0)                  // the first round's origins are spent
+            k_origin<<<grid_for(h->pend_b_root.size()), BLK, 0, s->stream>>>(
+                s->origin.p, s->lo, s->n, s->bc_roots.p, s->bc_msgs.p, (uint32_t)h->pend_b_root.size(), s->flags.p,
+                true, s->ctl.p);
+        HIP_TRY(hipGetLastError());
+        h->round++;
+    }
+    s->stat_slot = 0; s->batch_round1 = 0; s->desc_cap = 0;
+    uint32_t cw[2] = {0, 0};
+    HIP_TRY(hipMemcpyAsync(cw, s->ctl.p, sizeof cw, hipMemcpyDeviceToHost, s->stream));
+    TRY(stream_wait(s));
+    if (s->pin[PIN_BIGIN]) return PSIM_ENOMEM;        // a node's inbox count must fit 27 bits
+    const uint32_t done = cw[0] ? (uint32_t)(cw[1] - r0) : nb;
+    if (cw[0] && (cw[1] < r0 || done >= nb)) return PSIM_EDEVICE;
+    for (uint32_t j = 0; j < done; j++) {
+        const uint64_t* p = s->pin + (size_t)(j + 1) * PIN_STRIDE;
+        if (p[ST_BOUND]) {
+            std::fprintf(stderr, "psim: round %llu: %llu nodes emitted past their outbox bound (engine bug)\n",
+                         (unsigned long long)(r0 + j), (unsigned long long)p[ST_BOUND]);
+            return PSIM_EDEVICE;
+        }
+        if (st_out) fill_stats(p, r0 + j, &st_out[j]);
+        if (p[NST] != ~0ull && p[NST + 1] > p[NST]) {     // 100 MHz ticks
+            h->kt_ms[KT_CONSUME] += (double)(p[NST + 1] - p[NST]) * 1e-5;
+            h->kt_n[KT_CONSUME]++;
+        }
+    }
+    if (done > 0) {                           // the first round's events are spent
+        for (uint32_t j : h->pend_join) h->pend_join_mark[j] = 0;
+        h->pend_crash.clear(); h->pend_join.clear(); h->pend_contact.clear();
+        h->pend_part_set = h->pend_part_clear = false;
+        h->pend_b_root.clear(); h->pend_b_msg.clear();
+        h->faults_dirty = false;
+    }
+    s->m_in = (uint32_t)s->pin[PIN_M];         // (the last route that ran)
+    *done_out = done;
+    if (!cw[0]) {
+        h->round = r0 + nb;
+        return PSIM_OK;
+    }
+    // round r0 + done stopped the batch: reset the word, grow, finish it
+    HIP_TRY(hipMemsetAsync(s->ctl.p, 0, sizeof cw, s->stream));
+    h->round = r0 + done;
+    uint64_t st[NST];
+    if (cw[0] == 1) {
+        const uint64_t total = s->pin[PIN_TOTAL];
+        if (total >= 0xFFFFFFFFull) return PSIM_ENOMEM;
+        std::fprintf(stderr, "psim: round %llu: outbox grows past its capacity (%zu -> %llu slots)\n",
+                     (unsigned long long)h->round, s->outbox.n, (unsigned long long)total + 1);
+        TRY(s->outbox.ensure(total + 1, 2));
+        TRY(s->okey.ensure(total + 1, 2));
+        TRY(stream_wait(s));
+        TRY(run_round(h, st, done == 0));     // (the first round's events are applied)
+    } else {
+        // its node phases ran: grow the route's buffers, route it again,
+        // then its stats and round-end halves
+        const uint64_t m = s->pin[PIN_OVF];
+        s->pin[PIN_OVF] = 0;
+        const uint64_t want = m + m / 2;
+        if (want <= (1ull << 26)) while (s->rcap < want) s->rcap <<= 1;
+        else s->rcap = (want + (1ull << 20) - 1) >> 20 << 20;
+        TRY(route_buffers(s, false));
+        TRY(phase_route_local(h, s));
+        TRY(phase_stats(h, s, done == 0 ? crashed0 : none));
+        if (done == 0 && bc0)
+            k_origin<<<grid_for(h->pend_b_root.size()), BLK, 0, s->stream>>>(
+                s->origin.p, s->lo, s->n, s->bc_roots.p, s->bc_msgs.p, (uint32_t)h->pend_b_root.size(), s->flags.p,
+                true, s->ctl.p);
+        TRY(stream_wait(s));
+        for (int k = 0; k < NST; k++) st[k] = s->pin[k];
+        if (st[ST_BOUND]) return PSIM_EDEVICE;
+        s->m_in = (uint32_t)s->pin[PIN_M];
+        if (s->pin[NST] != ~0ull && s->pin[NST + 1] > s->pin[NST]) {
+            h->kt_ms[KT_CONSUME] += (double)(s->pin[NST + 1] - s->pin[NST]) * 1e-5;
+            h->kt_n[KT_CONSUME]++;
+        }
+        if (done == 0) {
+            for (uint32_t j : h->pend_join) h->pend_join_mark[j] = 0;
+            h->pend_crash.clear(); h->pend_join.clear(); h->pend_contact.clear();
+            h->pend_part_set = h->pend_part_clear = false;
+            h->pend_b_root.clear(); h->pend_b_msg.clear();
+            h->faults_dirty = false;
+        }
+        h->round++;
+    }
+    if (st_out) fill_stats(st, r0 + done, &st_out[done]);
+    *done_out = done + 1;
+    return PSIM_OK;
+}
+
 int shard_alloc(psim_handle* h, Shard* s) {
     HIP_TRY(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
     HIP_TRY(hipEventCreateWithFlags(&s->wait_ev, hipEventDisableTiming));
     if (s->n > (1u << 26))      // route buckets of 8192 destinations: 128 KiB of LDS per block
         HIP_TRY(hipFuncSetAttribute((const void*)k_bucket_route, hipFuncAttributeMaxDynamicSharedMemorySize,
                                     8192 * 16));
-    HIP_TRY(hipHostMalloc((void**)&s->pin, (NST + 8) * sizeof(uint64_t), hipHostMallocMapped));
+    HIP_TRY(hipHostMalloc((void**)&s->pin, (size_t)PIN_STRIDE * (1 + BATCH_MAX) * sizeof(uint64_t), hipHostMallocMapped));
     HIP_TRY(hipHostGetDevicePointer((void**)&s->pin_dev, s->pin, 0));
-    memset(s->pin, 0, (NST + 8) * sizeof(uint64_t));
+    memset(s->pin, 0, (size_t)PIN_STRIDE * (1 + BATCH_MAX) * sizeof(uint64_t));
     for (int k = 0; k < Shard::MAXT; k++) {
         HIP_TRY(hipEventCreate(&s->ev[k][0]));
         HIP_TRY(hipEventCreate(&s->ev[k][1]));
@@ -1945,6 +2126,7 @@ int shard_alloc(psim_handle* h, Shard* s) {
     rc |= s->desc_ptl.alloc(n); rc |= s->n_ptl.alloc(1);
     if (h->cfg.manager == PSIM_MANAGER_PLUGGABLE) { rc |= s->stop_ids.alloc(n); rc |= s->n_stop.alloc(1); }
     rc |= s->stat_out.alloc(NST + 2);   // + the consume span
+    rc |= s->ctl.alloc(2);
     rc |= s->stat_tile.alloc((size_t)STAT_TILES * NST);
     rc |= s->ikeys.alloc(1024); rc |= s->ivals.alloc(1024);
     rc |= s->recvbuf.alloc(1024); rc |= s->inbox.alloc(1024); rc |= s->outbox.alloc(1024);
@@ -1986,7 +2168,7 @@ void shard_free(Shard* s) {
     s->stop_ids.release(); s->n_stop.release();
     s->desc.release(); s->d_nact.release(); s->desc_slow.release(); s->n_slow.release(); s->desc_pt.release(); s->n_pt.release(); s->desc_shuf.release(); s->n_shuf.release(); s->desc_lite.release(); s->n_lite.release(); s->desc_ptl.release(); s->n_ptl.release(); s->bound.release(); s->pscan.release();
     s->obase.release(); s->stat_part.release(); s->stat_out.release(); s->stat_tile.release(); s->d_off.release();
-    s->cub_tmp.release(); s->ev_ids.release(); s->ev_contacts.release(); s->sendbuf.release();
+    s->cub_tmp.release(); s->ev_ids.release(); s->ev_contacts.release(); s->sendbuf.release(); s->ctl.release();
     s->sview.release(); s->sinv.release(); s->fbits.release(); s->pay[0].release(); s->pay[1].release();
     s->pay_top.release();
     if (s->ev_live)
@@ -2275,13 +2457,21 @@ int psim_step(psim_handle* h, uint32_t n_rounds, psim_round_stats* stats) {
     if (!h) return PSIM_EINVAL;
     if (hipSetDevice(h->device) != hipSuccess) return PSIM_EDEVICE;
     for (int k = 0; k < KT_N; k++) { h->kt_ms[k] = 0; h->kt_n[k] = 0; }
-    for (uint32_t i = 0; i < n_rounds; i++) {
+    for (uint32_t i = 0; i < n_rounds;) {
+        if (batchable(h)) {                   // rounds back to back, one wait per batch
+            uint32_t done = 0;
+            int rc = run_batch(h, std::min<uint32_t>(n_rounds - i, BATCH_MAX), stats ? stats + i : nullptr, &done);
+            if (rc) return rc;
+            i += done;
+            continue;
+        }
         uint64_t st[NST];
         uint64_t r = h->round;
         int rc = run_round(h, st);
         if (rc) return rc;
         if (stats) fill_stats(st, r, &stats[i]);
         if (h->cfg.strict && st[ST_OVF]) return PSIM_ECAPACITY;   // cfg.strict: fail loudly
+        i++;
     }
     return PSIM_OK;
 }

@@ -67,6 +67,10 @@ struct RoundArgs {
     // consume kernel span: min block-start and max block-end s_memrealtime
     // (100 MHz), reset by k_node_prep
     unsigned long long* ktime;
+    // the batch's abort word (psim_engine.hip run_batch): nonzero once a round
+    // of the batch has overflowed a buffer; every kernel that reads or writes
+    // round state returns at once (uniformly, before any barrier)
+    const uint32_t* ctl;
     // pluggable manager (k_consume_pl); Hdr fields are reused as
     // join_contact = pending contact, aux = last ping round,
     // have = hello sent, act_n = view length, pas_n = in_view length
@@ -113,7 +117,7 @@ __global__ void k_consume_lite(RoundArgs args);
 // lane-per-node Plumtree phases (psim_consume.hip); hands k_pt what does not fit
 __global__ void k_ptl(RoundArgs args);
 // a timestamp into t[slot] (the node-round span, RoundArgs::ktime)
-__global__ void k_mark(unsigned long long* t, int slot);
+__global__ void k_mark(unsigned long long* t, int slot, const uint32_t* ctl);
 // the Plumtree phase of the nodes k_relay listed (psim_consume.hip)
 __global__ void k_pt(RoundArgs args);
 // diagnostic builds (-DPSIM_STAMPS): per-phase cycle sums of k_consume, reset on read

@@ -628,6 +628,7 @@ DEV void process_pl(Pw& w, uint32_t n, uint32_t ib, uint32_t ik, uint32_t ob) {
 }  // namespace
 
 __global__ void __launch_bounds__(256) k_consume_pl(RoundArgs args) {
+    if (*kargs().ctl) return;                         // an aborted batch (run_batch)
     __shared__ uint64_t sst[NST];
     __shared__ uint32_t scratch[PL_WAVES][128];
     for (int i = threadIdx.x; i < NST; i += blockDim.x) sst[i] = 0;

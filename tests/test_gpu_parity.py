@@ -315,6 +315,28 @@ def test_route_regrow_parity(monkeypatch):
     S.compare_nodes(gs.nodes(), os_.nodes())
 
 
+def test_batch_regrow_parity(monkeypatch):
+    """Batched rounds (run_batch, psim_engine.hip) whose outbox and route
+    outgrow their buffers mid-batch: with no up-front reservation and a
+    route capacity of 16 records the abort word stops batches at k_desc
+    (code 1) and at the route (code 2); the host grows the buffer, finishes
+    that round and starts the next batch.  Results stay bit-identical."""
+    monkeypatch.setenv("PSIM_NO_RESERVE", "1")
+    monkeypatch.setenv("PSIM_RCAP_INIT", "16")
+
+    def run(make):
+        sim, _ = S.doubling(make, 4096, 9, 30, bcast_period=0, bcast_first=0)
+        sim.broadcast(7, 1)
+        out = [sim.step(60)]                      # one step call: batches, growth inside
+        sim.crash(np.arange(3, 4096, 37, dtype=np.uint32))
+        out.append(sim.step(40))
+        return sim, out
+    (gs, gst), (os_, ost) = run(_gpu), run(Oracle)
+    for a, b in zip(gst, ost):
+        S.compare_stats(a, b)
+    S.compare_nodes(gs.nodes(), os_.nodes())
+
+
 def test_histograms_delivery_parity():
     """psim_get_histograms / psim_get_delivery: the GPU's device kernels
     (in-degree atomics, reverse-link test, label propagation) against the
