@@ -37,7 +37,7 @@ S_NODE = 416                    # algorithmic state bytes per processed node (SU
 S_MSG = 64                      # message record bytes
 CHECK_NODES = 1 << 14           # the built-in sharding check
 CHECK_ROUNDS = 90
-SCHEDULE_VERSION = 2            # bumps when the event schedule of a run changes (PMC keys)
+SCHEDULE_VERSION = 3            # bumps when the event schedule of a run changes (PMC keys)
 OVF_KINDS = ("idmap", "pt_outstanding", "pt_sets_roots_msgs", "strategy", "conn")   # PSIM_OVF_*
 ALG_FORMULA = ("B = N_proc * 2 * 416 + M_in * 64 + M_out * 68 per round, N_proc = nodes with work "
                "(stats nodes_processed), M_in / M_out = delivered / emitted records.  Departs from "

@@ -1242,7 +1242,8 @@ DEV void body_hv(Wv& w, const NodeIn& x) {
         const uint32_t na = popc(exits);
         const uint32_t LV = shfl(w.CV, (int)((l + 40) & 63));
         const uint32_t LD = compact(w, LV, lexits);
-        D = l >= na ? shfl(LD, (int)((l - na) & 63)) : D;
+        const uint32_t LS = shfl(LD, (int)((l - na) & 63));   // (every lane: a lane outside
+        D = l >= na ? LS : D;                                    //  the exec mask reads as 0)
         const uint32_t nd = na + popc(lexits);
         for (uint32_t i = 0; i < nd; i++) {
             uint32_t d = rl(D, i);

@@ -48,12 +48,16 @@ SURVEY_RAMP = 64
 
 def survey_join(n_nodes, seed, ramp=SURVEY_RAMP):
     """Config C's bootstrap as SURVEY.md section 8(d) defines it: node i
-    joins at round floor(ramp * i / N), each joiner contacting a uniformly
-    drawn node among those started in an earlier round.  Node 0 is the seed
-    (started alone at round 0); the rest of round 0's batch joins node 0.
-    Start rounds -- and so the shuffle and promotion timer phases -- spread
-    evenly over the ramp, unlike the doubling ramp, which starts half the
-    overlay in its last round."""
+    joins at round floor(ramp * i / N) a uniformly drawn already-joined
+    node: one among those started in an earlier round.  Round 0 has no
+    earlier round: node 0 is the seed and node i of round 0's batch joins a
+    uniformly drawn node of [0, i) (all started in round 0, up when the JOIN
+    arrives) -- a random recursive tree (~ln(N/ramp) JOINs at node 0) rather
+    than a star of N/ramp JOINs at node 0, which would overrun node 0's
+    disconnect-id maps and connection table (the caps) on the
+    first round.  Start rounds -- and so the shuffle and promotion timer
+    phases -- spread evenly over the ramp, unlike the doubling ramp, which
+    starts half the overlay in its last round."""
     rng = _rng(seed, 3)
     ids = np.arange(n_nodes, dtype=np.uint64)
     rnd = (ids * ramp // n_nodes).astype(np.int64)
@@ -67,8 +71,10 @@ def survey_join(n_nodes, seed, ramp=SURVEY_RAMP):
             continue
         batch = np.arange(lo, hi, dtype=np.uint32)
         first = int(np.searchsorted(rnd, r, "left"))
-        contacts = (np.zeros(hi - lo, np.uint32) if r == 0 else
-                    rng.integers(0, first, size=hi - lo, dtype=np.uint64).astype(np.uint32))
+        if r == 0:                            # node i: uniform over [0, i)
+            contacts = np.floor(rng.random(hi - lo) * batch).astype(np.uint32)
+        else:
+            contacts = rng.integers(0, first, size=hi - lo, dtype=np.uint64).astype(np.uint32)
         sched.append((r, batch, contacts))
     return sched
 
