@@ -64,7 +64,7 @@
 extern "C" {
 #endif
 
-#define PSIM_ABI_VERSION 8
+#define PSIM_ABI_VERSION 9
 
 /* error codes */
 #define PSIM_OK 0
@@ -93,7 +93,17 @@ enum psim_msg_type {
     PSIM_MSG_PT_IHAVE = 11,         /* {i_have, Id, Mod, Round, Root, From}      plumtree:299  */
     PSIM_MSG_PT_IGNORED_IHAVE = 12, /* {ignored_i_have, ...}                     plumtree:304  */
     PSIM_MSG_PT_GRAFT = 13,         /* {graft, Id, Mod, Round, Root, From}       plumtree:308  */
-    PSIM_MSG_NTYPES = 16
+    /* X-BOT (cfg.manager = PSIM_MANAGER_XBOT): the record carries
+     * a0 = OldNode, a1 = InitiatorNode, a2 = CandidateNode, word 7 (a3) =
+     * DisconnectNode (PSIM_NONE = undefined), ttl = the reply's answer (1 true,
+     * 0 false); xbot = src/partisan_hyparview_xbot_peer_service_manager.erl */
+    PSIM_MSG_XBOT_OPTIMIZATION = 16,       /* {optimization, _, Old, I, C, undefined}       xbot:1205 */
+    PSIM_MSG_XBOT_OPTIMIZATION_REPLY = 17, /* {optimization_reply, Ans, Old, I, C, D}       xbot:1171 */
+    PSIM_MSG_XBOT_REPLACE = 18,            /* {replace, _, Old, I, C, D}                    xbot:1252 */
+    PSIM_MSG_XBOT_REPLACE_REPLY = 19,      /* {replace_reply, Ans, Old, I, C, D}            xbot:1227 */
+    PSIM_MSG_XBOT_SWITCH = 20,             /* {switch, _, Old, I, C, D}                     xbot:1295 */
+    PSIM_MSG_XBOT_SWITCH_REPLY = 21,       /* {switch_reply, Ans, Old, I, C, D}             xbot:1270 */
+    PSIM_MSG_NTYPES = 24
 };
 
 /* message types of a PLUGGABLE handle (same record and stats slots) */
@@ -111,6 +121,7 @@ enum psim_pl_msg_type {
 /* cfg.manager */
 #define PSIM_MANAGER_HYPARVIEW 0   /* partisan_hyparview_peer_service_manager (+ Plumtree) */
 #define PSIM_MANAGER_PLUGGABLE 1   /* partisan_pluggable_peer_service_manager + cfg.strategy */
+#define PSIM_MANAGER_XBOT 2        /* partisan_hyparview_xbot_peer_service_manager (+ Plumtree) */
 /* cfg.strategy (PLUGGABLE) */
 #define PSIM_STRATEGY_FULL 0       /* partisan_full_membership_strategy */
 #define PSIM_STRATEGY_SCAMP_V1 1   /* partisan_scamp_v1_membership_strategy */
@@ -141,6 +152,12 @@ enum psim_pl_msg_type {
  * overflow (PSIM_OVF_CONN) and is dropped. */
 #define PSIM_CONN_CAP 8
 #define PSIM_CONN_DOWN 0x80000000u
+/* X-BOT handles: an active member whose connection do_disconnect/2 stopped
+ * while the state that pruned it was thrown away (xbot:1367-1379 -- every
+ * optimization handler discards it), so the dead pid stays in the dict until
+ * its 'EXIT' (xbot:608-653) is handled at the start of the next round; sends
+ * to it draw the dispatch value and fail.  At most one per member. */
+#define PSIM_CONN_CLOSING 0x40000000u
 #define PSIM_PT_OUT_CAP 64
 #define PSIM_EXCHANGE_CAP 8
 /* Plumtree roots a node keeps per-root eager/lazy sets for at once
@@ -201,7 +218,10 @@ typedef struct psim_config {
                                     round goes on; 1: psim_step fails with PSIM_ECAPACITY after the
                                     round in which any overflow happened (e.g. a fifth live Plumtree
                                     root at a node, or a 65th live message id) */
-    uint32_t reserved[2];
+    uint32_t xbot_period;        /* rounds; xbot_interval (partisan_config.erl:100, :145: 5000 +
+                                    uniform(60000) ms, drawn per VM from an unseeded generator --
+                                    a fixed period here, default 35); X-BOT handles */
+    uint32_t reserved1;
 } psim_config;
 
 typedef struct psim_round_stats {
@@ -400,6 +420,14 @@ int psim_restore(psim_handle *h, const void *buf, size_t size);
  * k < PSIM_MSG_SLOTS; cap must be >= PSIM_MSG_SLOTS.  A node's delivery bit
  * k (psim_node_view.have) answers is_stale/1 for ids[k] only. */
 int psim_get_msg_slots(psim_handle *h, uint32_t *ids, uint32_t *roots, size_t cap);
+
+/* X-BOT's latency oracle (is_better/3 + is_better_node_by_latency/2,
+ * xbot:1318-1333: timer:tc of net_adm:ping from the deciding node).  The
+ * simulator places every node on a 1024 x 1024 torus from a hash of (seed,
+ * id) and takes the ping time from a to b as their toroidal L1 distance
+ * (0 for a == b); a crashed or never-started node answers pang.  Exported so
+ * hosts and tests can read the same metric. */
+uint32_t psim_xbot_latency(uint64_t seed, uint32_t a, uint32_t b);
 
 /* Per-kernel device time (ms) accumulated over the last psim_step call:
  * names[i] is a static string; returns the number of entries. */

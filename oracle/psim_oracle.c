@@ -81,7 +81,7 @@ typedef struct node {
 typedef struct omsg {
     uint32_t dst, src, seq;
     uint32_t type, ttl, nex;
-    uint32_t a0, a1, a2;
+    uint32_t a0, a1, a2, a3;        /* a3: record word 7 (X-BOT's DisconnectNode, else 0) */
     uint32_t ex[PSIM_EXCHANGE_CAP];
     uint32_t slot;                  /* full strategy: payload snapshot (not part of the record digest) */
 } omsg;
@@ -276,7 +276,7 @@ static uint64_t mix64(uint64_t z) {
 }
 
 /* Digest of one message: the sum over the 16 words of its 64-B record
- * image [dst, src, type|ttl<<8|nex<<16, seq, a0, a1, a2, 0, ex0..ex7] of
+ * image [dst, src, type|ttl<<8|nex<<16, seq, a0, a1, a2, a3, ex0..ex7] of
  * word_j * (0x9E3779B1 + 2j * 0x632BE5AB) mod 2^64 (odd multipliers).
  * Position-sensitive, order-free across messages (the round digest is a sum),
  * and one multiply-add per lane on the GPU. */
@@ -284,7 +284,7 @@ static uint64_t digest_mul(uint32_t j) { return (uint64_t)(uint32_t)(0x9E3779B1u
 
 static uint64_t msg_hash(const omsg *m) {
     uint32_t w[16] = {m->dst, m->src, m->type | (m->ttl << 8) | (m->nex << 16), m->seq,
-                      m->a0, m->a1, m->a2, 0};
+                      m->a0, m->a1, m->a2, m->a3};
     for (uint32_t i = 0; i < m->nex; i++) w[8 + i] = m->ex[i];
     uint64_t h = 0;
     for (uint32_t j = 0; j < 16; j++) h += (uint64_t)w[j] * digest_mul(j);
@@ -299,17 +299,22 @@ static void vec_push(msgvec *v, const omsg *m) {
     v->v[v->n++] = *m;
 }
 
-static void emit(ctx *c, uint32_t dst, uint32_t type, uint32_t ttl, uint32_t a0, uint32_t a1,
-                 uint32_t a2, const uint32_t *ex, uint32_t nex) {
+static void emit4(ctx *c, uint32_t dst, uint32_t type, uint32_t ttl, uint32_t a0, uint32_t a1,
+                  uint32_t a2, uint32_t a3, const uint32_t *ex, uint32_t nex) {
     omsg m;
     memset(&m, 0, sizeof m);
     m.dst = dst; m.src = c->me; m.seq = c->seq++;
     m.type = type; m.ttl = ttl; m.nex = nex;
-    m.a0 = a0; m.a1 = a1; m.a2 = a2;
+    m.a0 = a0; m.a1 = a1; m.a2 = a2; m.a3 = a3;
     for (uint32_t i = 0; i < nex; i++) m.ex[i] = ex[i];
     vec_push(&c->h->out, &m);
     c->h->st->emitted[type]++;
     c->h->st->digest += msg_hash(&m);
+}
+
+static void emit(ctx *c, uint32_t dst, uint32_t type, uint32_t ttl, uint32_t a0, uint32_t a1,
+                 uint32_t a2, const uint32_t *ex, uint32_t nex) {
+    emit4(c, dst, type, ttl, a0, a1, a2, 0, ex, nex);
 }
 
 /* A connection attempt (partisan_util:maybe_connect/2, util.erl:75-134)
@@ -346,21 +351,30 @@ static void conn_del(node *s, uint32_t e) {
     for (uint32_t j = (uint32_t)i; j + 1 < s->conn_n; j++) s->conn[j] = s->conn[j + 1];
     s->conn[--s->conn_n] = 0;
 }
-/* partisan_peer_service_connections:find/2 succeeds */
+/* X-BOT: the member's connection pid was stopped by a do_disconnect whose
+ * state was discarded -- the dead pid is still in the dict (PSIM_CONN_CLOSING) */
+static int conn_closing(const node *s, uint32_t p) { return s->conn_n && conn_find(s, p | PSIM_CONN_CLOSING) >= 0; }
+/* partisan_peer_service_connections:find/2 succeeds over a live pid */
 static int conn_has(ctx *c, uint32_t p) {
     node *s = c->s;
-    if (list_member(s->act, s->act_n, p)) return conn_find(s, p | PSIM_CONN_DOWN) < 0;
+    if (list_member(s->act, s->act_n, p))
+        return conn_find(s, p | PSIM_CONN_DOWN) < 0 && !conn_closing(s, p);
     return conn_find(s, p) >= 0;
 }
-/* partisan_util:maybe_connect/2: 1 iff connected afterwards */
+/* partisan_util:maybe_connect/2: 1 iff connected afterwards (a dead pid in
+ * the dict counts as found: maybe_connect opens nothing, util.erl:111-115) */
 static int maybe_connect(ctx *c, uint32_t p) {
+    if (conn_closing(c->s, p)) return 1;
     if (!connect_ok(c, p)) return 0;
     if (list_member(c->s->act, c->s->act_n, p)) conn_del(c->s, p | PSIM_CONN_DOWN);
     else conn_add(c, p);
     return 1;
 }
-/* disconnect/2 (hyparview:1237-1258) */
+/* disconnect/2 (hyparview:1237-1258).  X-BOT: stopping a pid that is already
+ * dead (PSIM_CONN_CLOSING) raises noproc in gen_server:stop/1 and would take
+ * the manager down; here the entry is pruned like a live one */
 static void disconnect(ctx *c, uint32_t p) {
+    if (conn_closing(c->s, p)) conn_del(c->s, p | PSIM_CONN_CLOSING);
     if (list_member(c->s->act, c->s->act_n, p)) conn_add(c, p | PSIM_CONN_DOWN);
     else conn_del(c->s, p);
 }
@@ -372,6 +386,11 @@ static void disconnect(ctx *c, uint32_t p) {
  * :1127, :1493, :1701). */
 static int hv_send(ctx *c, uint32_t dst, uint32_t type, uint32_t ttl, uint32_t a0, uint32_t a1,
                    const uint32_t *ex, uint32_t nex) {
+    if (conn_closing(c->s, dst)) {                /* X-BOT: dispatch_pid draws, the call to the */
+        (void)uniform_n(c, 1);                    /* dead pid fails (hyparview:1507-1514) */
+        c->h->st->send_fail++;
+        return 0;
+    }
     if (!maybe_connect(c, dst)) { c->h->st->send_fail++; return 0; }
     (void)uniform_n(c, 1);
     emit(c, dst, type, ttl, a0, a1, 0, ex, nex);
@@ -515,6 +534,148 @@ static void move_to_active(ctx *c, uint32_t p) {
     uint32_t ex[PSIM_EXCHANGE_CAP];
     uint32_t nex = build_exchange(c, ex);
     hv_send(c, p, PSIM_MSG_NEIGHBOR_REQUEST, 0, current_id(c, p), 0, ex, nex);
+}
+
+/* ------------------------------------------------------------- X-BOT -- */
+/* partisan_hyparview_xbot_peer_service_manager (xbot below): HyParView with
+ * the X-BOT optimization rounds (xbot:586-606, :691-716, :1171-1346).  Round
+ * model R0-X, DESIGN.md section 2c. */
+static int is_xbot(const struct psim_handle *h) { return h->cfg.manager == PSIM_MANAGER_XBOT; }
+
+/* the latency oracle: toroidal L1 distance on a 1024 x 1024 grid of
+ * hash-placed nodes (psim_xbot_latency in include/partisan_gpu_sim.h) */
+static uint32_t xb_coord(uint64_t seed, uint32_t id) {
+    return (uint32_t)mix64(seed ^ ((uint64_t)id * 0x9E3779B97F4A7C15ull)) & 0xFFFFFu;
+}
+static uint32_t xb_axis(uint32_t a, uint32_t b) {
+    uint32_t d = a > b ? a - b : b - a;
+    return d < 1024u - d ? d : 1024u - d;
+}
+uint32_t orc_xbot_latency(uint64_t seed, uint32_t a, uint32_t b) {
+    if (a == b) return 0;
+    uint32_t p = xb_coord(seed, a), q = xb_coord(seed, b);
+    return xb_axis(p & 1023u, q & 1023u) + xb_axis(p >> 10, q >> 10);
+}
+
+/* net_adm:ping/1 answers pong: the node runs (pings go over distributed
+ * Erlang, not partisan: a partition does not stop them) */
+static int xb_pong(ctx *c, uint32_t p) { return p == c->me || (p < c->h->N && c->h->nodes[p].up); }
+
+/* is_better(latency, New, Old) at the deciding node (xbot:1318-1333) */
+static int xb_better(ctx *c, uint32_t nw, uint32_t old) {
+    if (!xb_pong(c, nw)) return 0;
+    if (!xb_pong(c, old)) return 1;
+    uint64_t sd = c->h->cfg.seed;
+    return orc_xbot_latency(sd, c->me, nw) < orc_xbot_latency(sd, c->me, old);
+}
+
+/* select_disconnect_node/1 + select_worst_in_active_view/2 (xbot:1336-1346)
+ * over sets:to_list(Active) */
+static uint32_t xb_worst(ctx *c) {
+    node *s = c->s;
+    uint32_t worst = s->act[0];
+    for (uint32_t i = 1; i < s->act_n; i++)
+        if (!xb_better(c, s->act[i], worst)) worst = s->act[i];
+    return worst;
+}
+
+/* do_send_message over the Connections of a maybe_connect whose result the
+ * handler throws away (send_join/2 xbot:1349-1363, every optimization send):
+ * the send goes out iff the peer can be reached; the dict is not changed */
+static int xb_send(ctx *c, uint32_t dst, uint32_t type, uint32_t ttl, uint32_t a0, uint32_t a1,
+                   uint32_t a2, uint32_t a3) {
+    if (conn_closing(c->s, dst)) {                /* the dead pid: a draw, a failed call */
+        (void)uniform_n(c, 1);
+        c->h->st->send_fail++;
+        return 0;
+    }
+    if (!connect_ok(c, dst)) { c->h->st->send_fail++; return 0; }
+    (void)uniform_n(c, 1);
+    emit4(c, dst, type, ttl, a0, a1, a2, a3, NULL, 0);
+    return 1;
+}
+static void xb_join(ctx *c, uint32_t p) { xb_send(c, p, PSIM_MSG_JOIN, 0, c->s->epoch, 0, 0, 0); }
+
+/* do_disconnect/2 (xbot:1367-1379) with its result discarded by every caller:
+ * the passive add's eviction draw is consumed (the rand state lives in the
+ * process dictionary) and a live connection's pid is stopped, but the
+ * views and the dict stay as they were -- the pid's 'EXIT' removes the peer
+ * next round (process_node) */
+static void xb_do_disconnect(ctx *c, uint32_t p) {
+    node *s = c->s;
+    if (!list_member(s->act, s->act_n, p)) return;
+    if (p != c->me && !list_member(s->pas, s->pas_n, p) && s->pas_n >= c->h->cfg.max_passive_size)
+        (void)uniform_n(c, s->pas_n);             /* select_random(Passive, [Myself]) */
+    if (conn_find(s, p | PSIM_CONN_DOWN) < 0 && !conn_closing(s, p)) conn_add(c, p | PSIM_CONN_CLOSING);
+}
+
+/* the optimization messages (xbot:1171-1314); a0 Old, a1 Initiator, a2
+ * Candidate, a3 Disconnect (PSIM_NONE = undefined), ttl the answer */
+static void xb_handle(ctx *c, const omsg *m) {
+    node *s = c->s;
+    uint32_t old = m->a0, ini = m->a1, cand = m->a2, dis = m->a3, ans = m->ttl;
+    switch (m->type) {
+    case PSIM_MSG_XBOT_OPTIMIZATION:              /* xbot:1205-1224 (at the candidate) */
+        if (s->act_n < c->h->cfg.max_active_size) {
+            xb_join(c, ini);
+            xb_send(c, ini, PSIM_MSG_XBOT_OPTIMIZATION_REPLY, 1, old, ini, cand, PSIM_NONE);
+        } else {
+            uint32_t d = xb_worst(c);
+            xb_send(c, d, PSIM_MSG_XBOT_REPLACE, 0, old, ini, cand, d);
+        }
+        break;
+    case PSIM_MSG_XBOT_REPLACE:                   /* xbot:1252-1267 (at the disconnect node) */
+        if (!xb_better(c, old, cand)) xb_send(c, cand, PSIM_MSG_XBOT_REPLACE_REPLY, 0, old, ini, cand, dis);
+        else xb_send(c, old, PSIM_MSG_XBOT_SWITCH, 0, old, ini, cand, dis);
+        break;
+    case PSIM_MSG_XBOT_SWITCH:                    /* xbot:1295-1314 (at the old node) */
+        if (list_member(s->act, s->act_n, ini)) {
+            xb_do_disconnect(c, ini);
+            xb_join(c, dis);
+            xb_send(c, dis, PSIM_MSG_XBOT_SWITCH_REPLY, 1, old, ini, cand, dis);
+        } else {
+            xb_send(c, dis, PSIM_MSG_XBOT_SWITCH_REPLY, 0, old, ini, cand, dis);
+        }
+        break;
+    case PSIM_MSG_XBOT_SWITCH_REPLY:              /* xbot:1270-1292 (at the disconnect node) */
+        if (ans) {
+            xb_do_disconnect(c, cand);
+            xb_join(c, old);
+        }
+        xb_send(c, cand, PSIM_MSG_XBOT_REPLACE_REPLY, ans, old, ini, cand, dis);
+        break;
+    case PSIM_MSG_XBOT_REPLACE_REPLY:             /* xbot:1227-1249 (at the candidate) */
+        if (ans) {
+            xb_do_disconnect(c, dis);
+            xb_join(c, ini);
+        }
+        xb_send(c, ini, PSIM_MSG_XBOT_OPTIMIZATION_REPLY, ans, old, ini, cand, dis);
+        break;
+    case PSIM_MSG_XBOT_OPTIMIZATION_REPLY:        /* xbot:1171-1202 (at the initiator) */
+        if (!ans) break;
+        if (dis != PSIM_NONE && list_member(s->act, s->act_n, old)) xb_do_disconnect(c, old);
+        xb_join(c, cand);
+        break;
+    default:
+        break;
+    }
+}
+
+/* handle_info(xbot_execution) (xbot:587-606, :691-716): with a full active
+ * view, two passive candidates, each checked against the active members in
+ * to_list order; the first member it beats gets an optimization message */
+static void xb_execute(ctx *c) {
+    node *s = c->s;
+    if (s->act_n < c->h->cfg.max_active_size) return;
+    uint32_t cand[2], act[PSIM_ACTIVE_CAP], na = s->act_n;
+    memcpy(act, s->act, sizeof act);
+    uint32_t nc = select_random_sublist(c, s->pas, s->pas_n, 2, cand);
+    for (uint32_t i = 0; i < nc; i++)
+        for (uint32_t j = 0; j < na; j++)
+            if (xb_better(c, cand[i], act[j])) {
+                xb_send(c, cand[i], PSIM_MSG_XBOT_OPTIMIZATION, 0, act[j], c->me, cand[i], PSIM_NONE);
+                break;
+            }
 }
 
 /* --------------------------------------------------------- plumtree -- */
@@ -786,7 +947,11 @@ static void hv_handle(ctx *c, const omsg *m) {
                 uint32_t omit[2] = {me, p}, peers[PSIM_ACTIVE_CAP];
                 uint32_t np = list_subtract(s->act, s->act_n, omit, 2, peers);
                 for (uint32_t i = 0; i < np; i++)
-                    hv_send(c, peers[i], PSIM_MSG_FORWARD_JOIN, h->cfg.arwl, p, pe, NULL, 0);
+                    if (is_xbot(h))                   /* xbot:765-786: the fold's connections are
+                                                         dropped, State1 is kept */
+                        xb_send(c, peers[i], PSIM_MSG_FORWARD_JOIN, h->cfg.arwl, p, pe, 0, 0);
+                    else
+                        hv_send(c, peers[i], PSIM_MSG_FORWARD_JOIN, h->cfg.arwl, p, pe, NULL, 0);
                 notify(c);
             }
         }
@@ -818,10 +983,11 @@ static void hv_handle(ctx *c, const omsg *m) {
                     if (maybe_connect(c, p)) {        /* :878-880 */
                         add_to_active(c, p);
                         hv_send(c, p, PSIM_MSG_NEIGHBOR, 0, current_id(c, p), 0, NULL, 0);
-                    } else {
+                    } else if (!is_xbot(h)) {
                         /* {error, not_found} -> State0 (:896-897): the passive
                          * insert is discarded; its eviction draw stays consumed
-                         * (the rand state lives in the process dictionary) */
+                         * (the rand state lives in the process dictionary).
+                         * X-BOT keeps State2 (xbot:921-922) */
                         memcpy(s->pas, pas0, sizeof pas0);
                         s->pas_n = np0;
                     }
@@ -855,7 +1021,7 @@ static void hv_handle(ctx *c, const omsg *m) {
         int conn = maybe_connect(c, p);           /* :987, kept in both branches */
         uint32_t nack = build_exchange(c, ack);
         if (addable_id(c, d, p)) {               /* priority is always high (:1706) */
-            if (conn) {
+            if (conn || is_xbot(h)) {             /* X-BOT accepts without the find (xbot:1026-1045) */
                 hv_send(c, p, PSIM_MSG_NEIGHBOR_ACCEPTED, 0, current_id(c, p), 0, ack, nack);
                 add_to_active(c, p);
             }
@@ -893,6 +1059,7 @@ static void hv_handle(ctx *c, const omsg *m) {
         break;
     }
     default:
+        if (m->type >= PSIM_MSG_XBOT_OPTIMIZATION && is_xbot(h)) xb_handle(c, m);
         break;
     }
 }
@@ -916,18 +1083,25 @@ static void process_node(struct psim_handle *h, uint32_t n) {
     int origin = h->origin[n] != 0 && h->cfg.plumtree;
     int lazy_due = h->cfg.plumtree && timer_due(h->cfg.lazy_tick_period, r, s->start_round);
     int lazy = lazy_due && s->out_n > 0;
+    int xbot = is_xbot(h) && timer_due(h->cfg.xbot_period, r, s->start_round);
+    /* X-BOT: the 'EXIT' of every connection pid a discarded do_disconnect
+     * stopped last round (xbot:608-653), in table order */
+    uint32_t closed[PSIM_CONN_CAP], nclosed = 0;
+    for (uint32_t i = 0; i < s->conn_n; i++)
+        if (s->conn[i] & PSIM_CONN_CLOSING) closed[nclosed++] = s->conn[i] & ~PSIM_CONN_CLOSING;
     /* EXIT at every holder of a connection to a peer that crashed this round
      * (App. A Q11): the connected active members in to_list order, then the
      * lingering peers in table order (their EXITs only edit the passive view
      * and the table) */
     uint32_t exits[PSIM_ACTIVE_CAP + PSIM_CONN_CAP], nexit = 0;
     for (uint32_t i = 0; i < s->act_n; i++)
-        if (s->act[i] != n && h->crashed_now[s->act[i]] && conn_find(s, s->act[i] | PSIM_CONN_DOWN) < 0)
+        if (s->act[i] != n && h->crashed_now[s->act[i]] && conn_find(s, s->act[i] | PSIM_CONN_DOWN) < 0 &&
+            !conn_closing(s, s->act[i]))
             exits[nexit++] = s->act[i];
     for (uint32_t i = 0; i < s->conn_n; i++)
         if (!(s->conn[i] & PSIM_CONN_DOWN) && h->crashed_now[s->conn[i]]) exits[nexit++] = s->conn[i];
     int joining = (s->start_round == r && s->join_contact != PSIM_NONE);
-    if (!(e > b || joining || nexit || promo_work || shuf || origin || lazy)) return;
+    if (!(e > b || joining || nexit || nclosed || promo_work || shuf || xbot || origin || lazy)) return;
     h->st->nodes_processed++;
 
     /* handle_cast({join, Peer}), hyparview:500-515 */
@@ -935,6 +1109,17 @@ static void process_node(struct psim_handle *h, uint32_t n) {
 
     /* handle_info({'EXIT', ..}), hyparview:609-654: the connection is pruned,
      * the peer leaves the passive view, and the active view with a promotion */
+    for (uint32_t i = 0; i < nclosed; i++) {       /* X-BOT: the stopped pids' EXITs first */
+        uint32_t d = closed[i];
+        h->st->exits++;
+        conn_del(s, d | PSIM_CONN_CLOSING);
+        if (list_member(s->pas, s->pas_n, d)) set_del(s->pas, &s->pas_n, d);
+        if (list_member(s->act, s->act_n, d)) {
+            set_del(s->act, &s->act_n, d);
+            uint32_t omit[1] = {n};
+            move_to_active(&c, select_random(&c, s->pas, s->pas_n, omit, 1));
+        }
+    }
     for (uint32_t i = 0; i < nexit; i++) {
         uint32_t d = exits[i];
         h->st->exits++;
@@ -948,7 +1133,7 @@ static void process_node(struct psim_handle *h, uint32_t n) {
     }
 
     for (size_t i = b; i < e; i++)
-        if (h->inbox.v[i].type < PSIM_MSG_PT_BROADCAST) {
+        if (h->inbox.v[i].type < PSIM_MSG_PT_BROADCAST || h->inbox.v[i].type >= PSIM_MSG_XBOT_OPTIMIZATION) {
             h->st->delivered[h->inbox.v[i].type]++;
             hv_handle(&c, &h->inbox.v[i]);
         }
@@ -965,6 +1150,8 @@ static void process_node(struct psim_handle *h, uint32_t n) {
         uint32_t r2 = select_random(&c, s->act, s->act_n, omit, 1);
         if (r2 != PSIM_NONE) hv_send(&c, r2, PSIM_MSG_SHUFFLE, h->cfg.arwl, 0, 0, ex, nex);
     }
+
+    if (xbot) xb_execute(&c);                     /* xbot:587-606 */
 
     if (!h->cfg.plumtree) return;
     for (size_t i = b; i < e; i++)
@@ -1518,6 +1705,7 @@ void orc_default_config(psim_config *cfg) {
     cfg->device = -1; cfg->n_shards = 1; cfg->shard_world = 1;
     cfg->manager = PSIM_MANAGER_HYPARVIEW; cfg->strategy = PSIM_STRATEGY_FULL;
     cfg->periodic_interval = 10; cfg->scamp_c = 5; cfg->fanout = 0;
+    cfg->xbot_period = 35;
 }
 
 int orc_create(const psim_config *cfg, struct psim_handle **out) {
@@ -1525,7 +1713,7 @@ int orc_create(const psim_config *cfg, struct psim_handle **out) {
         cfg->n_nodes >= PSIM_MAP_BIT || cfg->max_active_size < 2 ||
         cfg->max_active_size > PSIM_ACTIVE_CAP || cfg->max_passive_size < 1 ||
         cfg->max_passive_size > 30 || 1 + cfg->k_active + cfg->k_passive > PSIM_EXCHANGE_CAP ||
-        cfg->arwl > 255 || cfg->prwl > 255 || cfg->manager > PSIM_MANAGER_PLUGGABLE ||
+        cfg->arwl > 255 || cfg->prwl > 255 || cfg->manager > PSIM_MANAGER_XBOT ||
         cfg->strategy > PSIM_STRATEGY_SCAMP_V2 || cfg->scamp_c < 1 || cfg->scamp_c > 64 ||
         cfg->fanout > 64 || cfg->strict > 1)
         return PSIM_EINVAL;
@@ -1906,7 +2094,7 @@ int orc_get_inbox(struct psim_handle *h, uint32_t *out, size_t cap, size_t *n) {
         const omsg *m = &h->inbox.v[i];
         uint32_t *o = out + i * 16;
         o[0] = m->dst; o[1] = m->src; o[2] = m->seq; o[3] = m->type | (m->ttl << 8) | (m->nex << 16);
-        o[4] = m->a0; o[5] = m->a1; o[6] = m->a2; o[7] = 0;
+        o[4] = m->a0; o[5] = m->a1; o[6] = m->a2; o[7] = m->a3;
         for (int k = 0; k < 8; k++) o[8 + k] = k < (int)m->nex ? m->ex[k] : 0;
     }
     return PSIM_OK;
@@ -1926,7 +2114,7 @@ uint32_t orc_bucket16(uint32_t id) { return bucket16(id); }
  * then orc_round_absorb with every message addressed to the owned range. */
 static void pack(const omsg *m, uint32_t *o) {
     o[0] = m->dst; o[1] = m->src; o[2] = m->seq; o[3] = m->type | (m->ttl << 8) | (m->nex << 16);
-    o[4] = m->a0; o[5] = m->a1; o[6] = m->a2; o[7] = 0;
+    o[4] = m->a0; o[5] = m->a1; o[6] = m->a2; o[7] = m->a3;
     for (int k = 0; k < 8; k++) o[8 + k] = k < (int)m->nex ? m->ex[k] : 0;
 }
 
@@ -1950,7 +2138,7 @@ int orc_round_absorb(struct psim_handle *h, const uint32_t *recs, size_t n) {
         memset(&m, 0, sizeof m);
         m.dst = o[0]; m.src = o[1]; m.seq = o[2];
         m.type = o[3] & 0xFF; m.ttl = (o[3] >> 8) & 0xFF; m.nex = (o[3] >> 16) & 0xFF;
-        m.a0 = o[4]; m.a1 = o[5]; m.a2 = o[6];
+        m.a0 = o[4]; m.a1 = o[5]; m.a2 = o[6]; m.a3 = o[7];
         for (int k = 0; k < 8; k++) m.ex[k] = o[8 + k];
         if (m.dst < h->lo || m.dst >= h->hi) { free(in.v); return PSIM_ERANGE; }
         vec_push(&in, &m);

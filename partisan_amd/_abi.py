@@ -8,28 +8,31 @@ import ctypes as C
 
 import numpy as np
 
-PSIM_ABI_VERSION = 8
+PSIM_ABI_VERSION = 9
 PSIM_MAP_BIT = 0x80000000
 PSIM_NONE = 0xFFFFFFFF
 ACTIVE_CAP, PASSIVE_CAP, IDMAP_CAP = 8, 32, 64
 PT_MEMBERS_CAP, PT_SET_POOL, PT_OUT_CAP, EXCHANGE_CAP = 8, 64, 64, 8
 PT_ROOTS, MSG_SLOTS = 4, 64
-CONN_CAP, CONN_DOWN = 8, 0x80000000
+CONN_CAP, CONN_DOWN, CONN_CLOSING = 8, 0x80000000, 0x40000000
 OVF_NKINDS = 5
-NTYPES = 16
+NTYPES = 24
 SVIEW_CAP = 128
-MANAGER_HYPARVIEW, MANAGER_PLUGGABLE = 0, 1
+MANAGER_HYPARVIEW, MANAGER_PLUGGABLE, MANAGER_XBOT = 0, 1, 2
 STRATEGY_FULL, STRATEGY_SCAMP_V1, STRATEGY_SCAMP_V2 = 0, 1, 2
 
 MSG_TYPES = [
     "JOIN", "FORWARD_JOIN", "NEIGHBOR", "DISCONNECT", "NEIGHBOR_REQUEST",
     "NEIGHBOR_ACCEPTED", "NEIGHBOR_REJECTED", "SHUFFLE", "SHUFFLE_REPLY",
-    "PT_BROADCAST", "PT_PRUNE", "PT_IHAVE", "PT_IGNORED_IHAVE", "PT_GRAFT",
+    "PT_BROADCAST", "PT_PRUNE", "PT_IHAVE", "PT_IGNORED_IHAVE", "PT_GRAFT", "", "",
+    "XBOT_OPTIMIZATION", "XBOT_OPTIMIZATION_REPLY", "XBOT_REPLACE", "XBOT_REPLACE_REPLY",
+    "XBOT_SWITCH", "XBOT_SWITCH_REPLY",
 ]
 PL_MSG_TYPES = ["HELLO", "STATE", "GOSSIP", "FWD_SUB", "PING", "KEEP_SUB", "REMOVE_SUB", "BOOT_REMOVE"]
 OMIT_SEND, OMIT_RECEIVE = 0, 1
 HV_TYPES = list(range(0, 9))
 PT_TYPES = list(range(9, 14))
+XBOT_TYPES = list(range(16, 22))
 
 ERRORS = {
     0: "PSIM_OK", -1: "PSIM_EINVAL", -2: "PSIM_ENOMEM", -3: "PSIM_EDEVICE",
@@ -52,7 +55,7 @@ class PsimConfig(C.Structure):
         ("max_msgs_per_round", C.c_uint64),
         ("manager", C.c_uint32), ("strategy", C.c_uint32), ("periodic_interval", C.c_uint32),
         ("scamp_c", C.c_uint32), ("fanout", C.c_uint32), ("strict", C.c_uint32),
-        ("reserved", C.c_uint32 * 2),
+        ("xbot_period", C.c_uint32), ("reserved1", C.c_uint32),
     ]
 
 
@@ -146,6 +149,7 @@ SIGNATURES = {
     "get_delivery": (C.c_int, [_H, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint8), _P32, _P32]),
     "get_histograms": (C.c_int, [_H, C.POINTER(PsimHistograms)]),
     "get_msg_slots": (C.c_int, [_H, _P32, _P32, C.c_size_t]),
+    "xbot_latency": (C.c_uint32, [C.c_uint64, C.c_uint32, C.c_uint32]),
 }
 # symbols only the GPU library exports
 GPU_ONLY = {

@@ -115,7 +115,8 @@ constexpr uint32_t DESC_MAPS_BIT = 1u << 27;
 
 // stats slots in the per-block partial arrays
 enum {
-    ST_EMIT = 0, ST_DELIV = 16, ST_DROPPED = 32, ST_UP, ST_PROC, ST_EXITS, ST_FAIL, ST_FIRST,
+    ST_EMIT = 0, ST_DELIV = PSIM_MSG_NTYPES, ST_DROPPED = 2 * PSIM_MSG_NTYPES, ST_UP, ST_PROC, ST_EXITS,
+    ST_FAIL, ST_FIRST,
     ST_OVF, ST_DIGEST, ST_BYTES, ST_STOP,
     ST_BOUND,       // nodes that emitted more records than their outbox bound (an engine bug: fails the round)
     ST_OMIT,        // pluggable: strategy messages an omission fault dropped
@@ -157,11 +158,24 @@ __device__ __forceinline__ uint64_t digest_mul(uint32_t j) {
     return (uint64_t)(uint32_t)(0x9E3779B1u + 2u * j * 0x632BE5ABu);
 }
 
-__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+__host__ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
     z ^= z >> 30; z *= 0xBF58476D1CE4E5B9ull;
     z ^= z >> 27; z *= 0x94D049BB133111EBull;
     z ^= z >> 31;
     return z;
+}
+
+// X-BOT's ping time from a to b (psim_xbot_latency): nodes hash-placed on a
+// 1024 x 1024 torus, toroidal L1 distance
+__host__ __device__ __forceinline__ uint32_t xbot_axis(uint32_t a, uint32_t b) {
+    const uint32_t d = a > b ? a - b : b - a;
+    return d < 1024u - d ? d : 1024u - d;
+}
+__host__ __device__ __forceinline__ uint32_t xbot_latency(uint64_t seed, uint32_t a, uint32_t b) {
+    if (a == b) return 0;
+    const uint32_t p = (uint32_t)mix64(seed ^ ((uint64_t)a * 0x9E3779B97F4A7C15ull)) & 0xFFFFFu;
+    const uint32_t q = (uint32_t)mix64(seed ^ ((uint64_t)b * 0x9E3779B97F4A7C15ull)) & 0xFFFFFu;
+    return xbot_axis(p & 1023u, q & 1023u) + xbot_axis(p >> 10, q >> 10);
 }
 
 }  // namespace psim

@@ -2214,7 +2214,10 @@ void psim_default_config(psim_config* cfg) {
     cfg->device = -1; cfg->n_shards = 1; cfg->shard_world = 1;
     cfg->manager = PSIM_MANAGER_HYPARVIEW; cfg->strategy = PSIM_STRATEGY_FULL;
     cfg->periodic_interval = 10; cfg->scamp_c = 5; cfg->fanout = 0;
+    cfg->xbot_period = 35;
 }
+
+uint32_t psim_xbot_latency(uint64_t seed, uint32_t a, uint32_t b) { return psim::xbot_latency(seed, a, b); }
 
 void psim_destroy(psim_handle* h);
 

@@ -33,6 +33,8 @@ def default_config(**kw):
     # pluggable manager (partisan_config.erl:129-130, partisan.hrl:31)
     cfg.manager, cfg.strategy = _abi.MANAGER_HYPARVIEW, _abi.STRATEGY_FULL
     cfg.periodic_interval, cfg.scamp_c, cfg.fanout = 10, 5, 0
+    # X-BOT: xbot_interval, 5000 + uniform(60000) ms (partisan_config.erl:100) -> its mean
+    cfg.xbot_period = 35
     for k, v in kw.items():
         if not hasattr(cfg, k):
             raise KeyError(k)
