@@ -85,6 +85,7 @@ struct Wv {
     uint32_t CN;         // the connection table (lanes 0 .. conn_n - 1): lingering peers, and
                          // | PSIM_CONN_DOWN the active members without a connection
     uint32_t conn_n, conn_dn;   // its entries, and those marked PSIM_CONN_DOWN
+    uint32_t conn_cl;           // X-BOT: ... and those marked PSIM_CONN_CLOSING (stopped pids)
     bool cn_dirty;
     uint64_t digest;     // per-lane partial: lane j sums the hashes of record word j
     uint32_t SC;         // per-lane stats counter: lane k counts stats slot k (< NST)
@@ -272,8 +273,8 @@ DEV uint32_t sublist(Wv& w, uint32_t V, uint32_t n, uint32_t k, uint32_t& OUT, u
 DEV void flush_recs(Wv& w);
 DEV void flush_full(Wv& w);
 
-DEV void emit(Wv& w, uint32_t dst, uint32_t type, uint32_t ttl, uint32_t a0, uint32_t a1,
-              uint32_t a2, uint32_t EX, uint32_t nex) {
+DEV void emit4(Wv& w, uint32_t dst, uint32_t type, uint32_t ttl, uint32_t a0, uint32_t a1,
+               uint32_t a2, uint32_t a3, uint32_t EX, uint32_t nex) {
     uint32_t l = lane_id();
     uint32_t s = w.seq++;
     uint32_t k = s - w.flushed;                      // staging slot
@@ -281,7 +282,7 @@ DEV void emit(Wv& w, uint32_t dst, uint32_t type, uint32_t ttl, uint32_t a0, uin
     // lanes 8..15 take the exchange ids of lanes 0..7 (DPP row_shr:8)
     uint32_t exv = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)EX, 0x118, 0xF, 0xF, true);
     uint32_t word = l == 0 ? dst : l == 1 ? w.me : l == 2 ? tt : l == 3 ? s : l == 4 ? a0
-                  : l == 5 ? a1 : l == 6 ? a2 : l == 7 ? 0u : (l - 8 < nex ? exv : 0u);
+                  : l == 5 ? a1 : l == 6 ? a2 : l == 7 ? a3 : (l - 8 < nex ? exv : 0u);
     if (l < 16) {
         w.srec[k * 16 + l] = word;
         w.digest += (uint64_t)word * digest_mul(l);   // the oracle's msg_hash, word l
@@ -289,6 +290,10 @@ DEV void emit(Wv& w, uint32_t dst, uint32_t type, uint32_t ttl, uint32_t a0, uin
     if (l == 0) w.skey[k] = dst | (max_emit(type) << KEY_DST_BITS);
     st_add(w, ST_EMIT + type, 1);
     if (k + 1 == STAGE) flush_full(w);               // a node with > STAGE emissions
+}
+DEV void emit(Wv& w, uint32_t dst, uint32_t type, uint32_t ttl, uint32_t a0, uint32_t a1,
+              uint32_t a2, uint32_t EX, uint32_t nex) {
+    emit4(w, dst, type, ttl, a0, a1, a2, 0u, EX, nex);
 }
 
 // The staged records [flushed, seq) to outbox slots obase + flushed..: one
@@ -359,6 +364,7 @@ DEV void conn_add(Wv& w, uint32_t e) {
     w.CN = lane_id() == w.conn_n ? e : w.CN;
     w.conn_n++;
     w.conn_dn += (e & PSIM_CONN_DOWN) ? 1u : 0u;
+    w.conn_cl += (e & PSIM_CONN_CLOSING) ? 1u : 0u;
     w.cn_dirty = true;
 }
 DEV void conn_del(Wv& w, uint32_t e) {
@@ -366,15 +372,22 @@ DEV void conn_del(Wv& w, uint32_t e) {
     if (k < 0) return;
     vdel(w.CN, w.conn_n, (uint32_t)k);
     w.conn_dn -= (e & PSIM_CONN_DOWN) ? 1u : 0u;
+    w.conn_cl -= (e & PSIM_CONN_CLOSING) ? 1u : 0u;
     w.cn_dirty = true;
 }
-// partisan_peer_service_connections:find/2 succeeds
+// X-BOT: the member's connection pid was stopped by a do_disconnect whose
+// state was discarded; the dead pid stays in the dict until its 'EXIT'
+DEV bool conn_closing(const Wv& w, uint32_t p) { return w.conn_cl && conn_find(w, p | PSIM_CONN_CLOSING) >= 0; }
+// partisan_peer_service_connections:find/2 succeeds over a live pid
 DEV bool conn_has(const Wv& w, uint32_t p) {
-    if (has(w.A, w.act_n, p)) return !w.conn_dn || conn_find(w, p | PSIM_CONN_DOWN) < 0;
+    if (has(w.A, w.act_n, p))
+        return (!w.conn_dn || conn_find(w, p | PSIM_CONN_DOWN) < 0) && !conn_closing(w, p);
     return w.conn_n && conn_find(w, p) >= 0;
 }
-// partisan_util:maybe_connect/2 (util.erl:75-134): connected afterwards
+// partisan_util:maybe_connect/2 (util.erl:75-134): connected afterwards (a
+// dead pid in the dict counts as found: nothing is opened)
 DEV bool maybe_connect(Wv& w, uint32_t p) {
+    if (conn_closing(w, p)) return true;
     if (!connect_ok(w, p)) return false;
     if (has(w.A, w.act_n, p)) {
         if (w.conn_dn) conn_del(w, p | PSIM_CONN_DOWN);
@@ -383,8 +396,10 @@ DEV bool maybe_connect(Wv& w, uint32_t p) {
     }
     return true;
 }
-// disconnect/2 (hv:1237-1258)
+// disconnect/2 (hv:1237-1258); X-BOT: a stopped pid is pruned like a live
+// one (the reference's second gen_server:stop raises noproc)
 DEV void disconnect(Wv& w, uint32_t p) {
+    if (conn_closing(w, p)) conn_del(w, p | PSIM_CONN_CLOSING);
     if (has(w.A, w.act_n, p)) conn_add(w, p | PSIM_CONN_DOWN);
     else if (w.conn_n) conn_del(w, p);
 }
@@ -395,6 +410,7 @@ DEV void disconnect(Wv& w, uint32_t p) {
 // a maybe_connect of its destination.
 DEV void hv_send(Wv& w, uint32_t dst, uint32_t type, uint32_t ttl, uint32_t a0, uint32_t a1,
                  uint32_t EX, uint32_t nex) {
+    if (conn_closing(w, dst)) { w.rng++; st_add(w, ST_FAIL, 1); return; }   // X-BOT: a dead pid (draw, fail)
     if (!maybe_connect(w, dst)) { st_add(w, ST_FAIL, 1); return; }
     w.rng++;
     emit(w, dst, type, ttl, a0, a1, 0, EX, nex);
@@ -766,7 +782,7 @@ DEV uint64_t pt_conn_mask(Wv& w, uint64_t cand, uint32_t IDENT) {
     // connection, a lingering peer has one
     for (uint32_t j = 0; j < w.conn_n; j++) {
         const uint32_t ej = rl(w.CN, j), cj = rl(w.CF, 40 + j);
-        in = ej == (id | PSIM_CONN_DOWN) ? false : in;
+        in = ej == (id | PSIM_CONN_DOWN) || ej == (id | PSIM_CONN_CLOSING) ? false : in;
         const bool hit = ej == id;
         in |= hit;
         fl = hit ? cj : fl;
@@ -913,9 +929,128 @@ DEV void pt_handle(Wv& w, uint32_t type, uint32_t src, uint32_t msg, uint32_t rn
     }
 }
 
+// --------------------------------------------------------------- X-BOT --
+// partisan_hyparview_xbot_peer_service_manager (xbot): HyParView plus the
+// optimization rounds (xbot:586-606, :691-716, :1171-1346), round model R0-X
+// (the oracle's xb_*).  Every X-BOT node with X-BOT work runs
+// here, in k_consume.
+// net_adm:ping/1 answers pong iff the node runs (pings go over distributed
+// Erlang, so a partition does not stop them); F_UP of another node does not
+// change during the phase
+DEV bool xb_pong(const Wv& w, uint32_t p) {
+    if (p == w.me) return true;
+    if (p >= kargs().n_nodes) return false;
+    const uint64_t m = ballot(w.CV == p);
+    const uint32_t f = m ? rl(w.CF, ffs64(m)) : (uint32_t)kargs().flags[p];
+    return (f & F_UP) != 0;
+}
+// is_better(latency, New, Old) at this node (xbot:1318-1333)
+DEV bool xb_better(const Wv& w, uint32_t nw, uint32_t old) {
+    if (!xb_pong(w, nw)) return false;
+    if (!xb_pong(w, old)) return true;
+    const uint64_t sd = kargs().seed;
+    return xbot_latency(sd, w.me, nw) < xbot_latency(sd, w.me, old);
+}
+// select_disconnect_node/1 + select_worst_in_active_view/2 (xbot:1336-1346)
+DEV uint32_t xb_worst(const Wv& w) {
+    uint32_t worst = rl(w.A, 0);
+    for (uint32_t i = 1; i < w.act_n; i++) {
+        const uint32_t h = rl(w.A, i);
+        if (!xb_better(w, h, worst)) worst = h;
+    }
+    return worst;
+}
+// do_send_message over a maybe_connect whose result the handler drops
+// (send_join/2 xbot:1349-1363 and every optimization send): out iff the peer
+// can be reached, the connection table unchanged
+DEV void xb_send(Wv& w, uint32_t dst, uint32_t type, uint32_t ans, uint32_t a0, uint32_t a1, uint32_t a2,
+                 uint32_t a3) {
+    if (conn_closing(w, dst)) { w.rng++; st_add(w, ST_FAIL, 1); return; }
+    if (!connect_ok(w, dst)) { st_add(w, ST_FAIL, 1); return; }
+    w.rng++;
+    emit4(w, dst, type, ans, a0, a1, a2, a3, 0, 0);
+}
+DEV void xb_join(Wv& w, uint32_t p) { xb_send(w, p, PSIM_MSG_JOIN, 0, hw_epoch(w), 0, 0, 0); }
+// do_disconnect/2 (xbot:1367-1379), its state discarded by every caller: the
+// passive add's eviction draw is consumed and a live connection's pid
+// stopped (PSIM_CONN_CLOSING); its 'EXIT' removes the peer next round
+DEV void xb_do_disconnect(Wv& w, uint32_t p) {
+    if (!has(w.A, w.act_n, p)) return;
+    if (p != w.me && !has(w.P, w.pas_n, p) && w.pas_n >= kargs().max_passive) (void)uniform_n(w, w.pas_n);
+    if ((!w.conn_dn || conn_find(w, p | PSIM_CONN_DOWN) < 0) && !conn_closing(w, p)) conn_add(w, p | PSIM_CONN_CLOSING);
+}
+// the optimization messages: a0 Old, a1 Initiator, a2 Candidate, a3
+// Disconnect (NONE = undefined), ttl the answer
+DEV void xb_handle(Wv& w, uint32_t type, uint32_t ans, uint32_t old, uint32_t ini, uint32_t cand, uint32_t dis) {
+    switch (type) {
+    case PSIM_MSG_XBOT_OPTIMIZATION:                   // xbot:1205-1224, at the candidate
+        if (w.act_n < kargs().max_active) {
+            xb_join(w, ini);
+            xb_send(w, ini, PSIM_MSG_XBOT_OPTIMIZATION_REPLY, 1, old, ini, cand, NONE);
+        } else {
+            const uint32_t d = xb_worst(w);
+            xb_send(w, d, PSIM_MSG_XBOT_REPLACE, 0, old, ini, cand, d);
+        }
+        break;
+    case PSIM_MSG_XBOT_REPLACE:                        // xbot:1252-1267, at the disconnect node
+        if (!xb_better(w, old, cand)) xb_send(w, cand, PSIM_MSG_XBOT_REPLACE_REPLY, 0, old, ini, cand, dis);
+        else xb_send(w, old, PSIM_MSG_XBOT_SWITCH, 0, old, ini, cand, dis);
+        break;
+    case PSIM_MSG_XBOT_SWITCH:                         // xbot:1295-1314, at the old node
+        if (has(w.A, w.act_n, ini)) {
+            xb_do_disconnect(w, ini);
+            xb_join(w, dis);
+            xb_send(w, dis, PSIM_MSG_XBOT_SWITCH_REPLY, 1, old, ini, cand, dis);
+        } else {
+            xb_send(w, dis, PSIM_MSG_XBOT_SWITCH_REPLY, 0, old, ini, cand, dis);
+        }
+        break;
+    case PSIM_MSG_XBOT_SWITCH_REPLY:                   // xbot:1270-1292, at the disconnect node
+        if (ans) {
+            xb_do_disconnect(w, cand);
+            xb_join(w, old);
+        }
+        xb_send(w, cand, PSIM_MSG_XBOT_REPLACE_REPLY, ans, old, ini, cand, dis);
+        break;
+    case PSIM_MSG_XBOT_REPLACE_REPLY:                  // xbot:1227-1249, at the candidate
+        if (ans) {
+            xb_do_disconnect(w, dis);
+            xb_join(w, ini);
+        }
+        xb_send(w, ini, PSIM_MSG_XBOT_OPTIMIZATION_REPLY, ans, old, ini, cand, dis);
+        break;
+    case PSIM_MSG_XBOT_OPTIMIZATION_REPLY:             // xbot:1171-1202, at the initiator
+        if (!ans) break;
+        if (dis != NONE && has(w.A, w.act_n, old)) xb_do_disconnect(w, old);
+        xb_join(w, cand);
+        break;
+    default:
+        break;
+    }
+}
+// handle_info(xbot_execution) (xbot:587-606, :691-716): with a full active
+// view, two passive candidates, each checked against the active members in
+// to_list order; the first one it beats gets an optimization message
+DEV void xb_execute(Wv& w) {
+    if (w.act_n < kargs().max_active) return;
+    uint32_t C = 0;
+    const uint32_t nc = sublist(w, w.P, w.pas_n, 2, C, 0);
+    const uint32_t A0 = w.A, na = w.act_n;
+    for (uint32_t i = 0; i < nc; i++) {
+        const uint32_t c = rl(C, i);
+        for (uint32_t j = 0; j < na; j++) {
+            const uint32_t old = rl(A0, j);
+            if (xb_better(w, c, old)) {
+                xb_send(w, c, PSIM_MSG_XBOT_OPTIMIZATION, 0, old, w.me, c, NONE);
+                break;
+            }
+        }
+    }
+}
+
 // ----------------------------------------------------------- hyparview --
 DEV void hv_handle(Wv& w, uint32_t type, uint32_t p, uint32_t ttl, uint32_t a0, uint32_t a1,
-                   uint32_t EX, uint32_t nex) {
+                   uint32_t a2, uint32_t a3, uint32_t EX, uint32_t nex) {
     KArgs& a = kargs();
     uint32_t me = w.me;
     switch (type) {
@@ -926,7 +1061,9 @@ DEV void hv_handle(Wv& w, uint32_t type, uint32_t p, uint32_t ttl, uint32_t a0, 
             // (members(Active) -- [Myself]) -- [Peer], in to_list order
             for (uint32_t i = 0; i < w.act_n; i++) {
                 uint32_t q = rl(w.A, i);
-                if (q != me && q != p) hv_send(w, q, PSIM_MSG_FORWARD_JOIN, a.arwl, p, a0, 0, 0);
+                if (q == me || q == p) continue;
+                if (a.xbot) xb_send(w, q, PSIM_MSG_FORWARD_JOIN, a.arwl, p, a0, 0, 0);   // xbot:765-786:
+                else hv_send(w, q, PSIM_MSG_FORWARD_JOIN, a.arwl, p, a0, 0, 0);          // the fold's dict dropped
             }
             notify(w);
         }
@@ -953,9 +1090,10 @@ DEV void hv_handle(Wv& w, uint32_t type, uint32_t p, uint32_t ttl, uint32_t a0, 
                     if (maybe_connect(w, q)) {                 // :878-880
                         add_to_active(w, q);
                         hv_send(w, q, PSIM_MSG_NEIGHBOR, 0, current_id(w, q), 0, 0, 0);
-                    } else {
+                    } else if (!a.xbot) {
                         // {error, not_found} -> State0 (hv:896-897): the insert
                         // is discarded, its eviction draw stays consumed
+                        // (X-BOT keeps State2, xbot:921-922)
                         w.P = P_s; w.pas_n = np_s;
                     }
                 }
@@ -983,7 +1121,7 @@ DEV void hv_handle(Wv& w, uint32_t type, uint32_t p, uint32_t ttl, uint32_t a0, 
         const bool conn = maybe_connect(w, p);         // :987, kept in both branches
         uint32_t nack = build_exchange(w, ACK);
         if (addable_id(w, a0, p)) {                    // priority is always high (:1706)
-            if (conn) {
+            if (conn || a.xbot) {                      // (X-BOT: no find, xbot:1026-1045)
                 hv_send(w, p, PSIM_MSG_NEIGHBOR_ACCEPTED, 0, current_id(w, p), 0, ACK, nack);
                 add_to_active(w, p);
             }
@@ -1022,6 +1160,7 @@ DEV void hv_handle(Wv& w, uint32_t type, uint32_t p, uint32_t ttl, uint32_t a0, 
         }
         break;
     default:
+        if (type >= PSIM_MSG_XBOT_OPTIMIZATION && a.xbot) xb_handle(w, type, ttl, a0, a1, a2, a3);
         break;
     }
 }
@@ -1057,6 +1196,7 @@ DEV uint32_t inbox_chunk(const Wv& w, KArgs& a, uint32_t ib, uint32_t ik, uint32
 struct NodeIn {
     uint32_t n, ib, ik, ob, tf;    // tf: due timers (DESC_* bits, k_desc)
     bool maps;                     // DESC_MAPS_BIT (k_relay)
+    bool xb;                       // DESC_XBOT_BIT: X-BOT's xbot_execution is due (k_desc)
     uint32_t H;                    // header word l & 15
     uint32_t A, P, R0;
     uint32_t CN;                   // connection-table entry l & 7 (k_consume_lite: 0)
@@ -1078,6 +1218,7 @@ DEV NodeIn load_node(KArgs& a, uint32_t D) {
     NodeIn x;
     x.n = rl(D, 0); x.ib = rl(D, 1); x.ik = rl(D, 2) & DESC_CNT_MASK; x.tf = rl(D, 2) >> 28; x.ob = rl(D, 3);
     x.maps = (rl(D, 2) & DESC_MAPS_BIT) != 0;
+    x.xb = (rl(D, 2) & DESC_XBOT_BIT) != 0;
     const size_t li = x.n - a.lo;
     x.H = reinterpret_cast<const uint32_t*>(a.hdr + li)[l & 15];
     x.A = a.act[li * PSIM_ACTIVE_CAP + (l & 7)];
@@ -1097,7 +1238,7 @@ DEV NodeIn load_node(KArgs& a, uint32_t D) {
 DEV uint32_t conn_cache_id(uint32_t CN, uint32_t H) {
     const uint32_t l = lane_id(), cn = rl(H, HW_CONN) & 0xFF;
     const uint32_t e = shfl(CN, (int)(l & 7));
-    return l >= 40 && l < 48 && l - 40 < cn && !(e & PSIM_CONN_DOWN) ? e : NONE;
+    return l >= 40 && l < 48 && l - 40 < cn && !(e & (PSIM_CONN_DOWN | PSIM_CONN_CLOSING)) ? e : NONE;
 }
 
 // flag | partition << 8 of the view members in CV (the connection cache)
@@ -1169,7 +1310,7 @@ DEV void begin_header(Wv& w, uint32_t H) {
     w.act_n = w9 & 0xFF; w.pas_n = (w9 >> 8) & 0xFF; w.sent_n = (w9 >> 16) & 0xFF; w.sent_head = w9 >> 24;
     w.recv_n = w10 & 0xFF; w.recv_head = (w10 >> 8) & 0xFF; w.all_n = (w10 >> 16) & 0xFF; w.com_n = w10 >> 24;
     w.out_n = (w11 >> 16) & 0xFF;
-    w.conn_n = w11 & 0xFF; w.conn_dn = (w11 >> 8) & 0xFF;
+    w.conn_n = w11 & 0xFF; w.conn_dn = (w11 >> 8) & 0xFF; w.conn_cl = w11 >> 24;
     w.sx = rl(H, HW_SENT_EXT); w.rx = rl(H, HW_RECV_EXT); w.ox = rl(H, HW_OUT_EXT);
 }
 
@@ -1221,12 +1362,14 @@ DEV void body_hv(Wv& w, const NodeIn& x) {
     uint64_t exits = 0, lexits = 0;
     if (a.crash_round) {
         bool dead = l >= 32 && l < 40 && l - 32 < w.act_n && w.CV != n && (w.CF & F_CRASHED);
-        for (uint32_t j = 0; j < w.conn_n && w.conn_dn; j++) dead &= rl(w.CN, j) != (w.CV | PSIM_CONN_DOWN);
+        for (uint32_t j = 0; j < w.conn_n && (w.conn_dn || w.conn_cl); j++)
+            dead &= rl(w.CN, j) != (w.CV | PSIM_CONN_DOWN) && rl(w.CN, j) != (w.CV | PSIM_CONN_CLOSING);
         exits = (ballot(dead) >> 32) & 0xFFull;
         lexits = (ballot(l >= 40 && l < 48 && w.CV != NONE && (w.CF & F_CRASHED)) >> 40) & 0xFFull;
     }
     bool promo_work = promo && w.act_n < a.min_active;
-    if (!(ik || joining || exits || lexits || promo_work || shuf || origin || lazy)) { STAMP(w, 0); return; }
+    const uint32_t ncl = w.conn_cl;                   // X-BOT: connection pids stopped last round
+    if (!(ik || joining || exits || lexits || ncl || promo_work || shuf || x.xb || origin || lazy)) { STAMP(w, 0); return; }
     w.work = true;
     st_add(w, ST_PROC, 1);
     if (x.maps) load_maps(w);                         // (k_relay: a handler here may use them)
@@ -1234,6 +1377,22 @@ DEV void body_hv(Wv& w, const NodeIn& x) {
 
     if (joining)                                      // hv:500-515
         hv_send(w, hw_contact(w), PSIM_MSG_JOIN, 0, hw_epoch(w), 0, 0, 0);
+
+    if (ncl) {                                        // X-BOT: their 'EXIT's (xbot:608-653), table order
+        const uint64_t cm = ballot(l < w.conn_n && (w.CN & PSIM_CONN_CLOSING));
+        const uint32_t D = compact(w, w.CN & ~PSIM_CONN_CLOSING, cm);
+        const uint32_t nd = popc(cm);
+        for (uint32_t i = 0; i < nd; i++) {
+            const uint32_t d = rl(D, i);
+            st_add(w, ST_EXITS, 1);
+            conn_del(w, d | PSIM_CONN_CLOSING);
+            if (vdel_val(w.P, w.pas_n, d)) w.vd |= 2u;
+            if (vdel_val(w.A, w.act_n, d)) {
+                w.vd |= 1u;
+                move_to_active(w, select_random(w, w.P, w.pas_n, n, n, n));
+            }
+        }
+    }
 
     if (exits | lexits) {                             // hv:609-654
         // the crashed peers, listed before any handler runs: the active
@@ -1264,13 +1423,14 @@ DEV void body_hv(Wv& w, const NodeIn& x) {
         for (uint32_t q = 0; q < cm; q++) {
             uint32_t b = q * 16;
             uint32_t tt = rl(R4, b + 2), type = tt & 0xFF;
-            if (type >= PSIM_MSG_PT_BROADCAST) continue;
+            if (type >= PSIM_MSG_PT_BROADCAST && type < PSIM_MSG_XBOT_OPTIMIZATION) continue;
             st_add(w, ST_DELIV + type, 1);
             uint32_t nex = (tt >> 16) & 0xFF;
             uint32_t ex = shfl(R4, (int)((b + 8 + l) & 63));
             ex = l < nex ? ex : 0u;
             STAMP(w, 3);
-            hv_handle(w, type, rl(R4, b + 1), (tt >> 8) & 0xFF, rl(R4, b + 4), rl(R4, b + 5), ex, nex);
+            hv_handle(w, type, rl(R4, b + 1), (tt >> 8) & 0xFF, rl(R4, b + 4), rl(R4, b + 5), rl(R4, b + 6),
+                      rl(R4, b + 7), ex, nex);
             STAMP(w, 4 + type);
         }
     }
@@ -1285,6 +1445,7 @@ DEV void body_hv(Wv& w, const NodeIn& x) {
         uint32_t t = select_random(w, w.A, w.act_n, n, n, n);
         if (t != NONE) hv_send(w, t, PSIM_MSG_SHUFFLE, a.arwl, 0, 0, EX, nex);
     }
+    if (x.xb) xb_execute(w);                          // xbot:587-606
     STAMP(w, 14);
     if (a.plumtree) replay_notifies(w);
     STAMP(w, 15);
@@ -1304,7 +1465,7 @@ DEV uint32_t header_word(const Wv& w, uint32_t k) {
     v = k == 8 ? w.trk_hop : v;
     v = k == 9 ? (w.act_n | (w.pas_n << 8) | (w.sent_n << 16) | (w.sent_head << 24)) : v;
     v = k == 10 ? (w.recv_n | (w.recv_head << 8) | (w.all_n << 16) | (w.com_n << 24)) : v;
-    v = k == 11 ? (w.conn_n | (w.conn_dn << 8) | (w.out_n << 16)) : v;
+    v = k == 11 ? (w.conn_n | (w.conn_dn << 8) | (w.out_n << 16) | (w.conn_cl << 24)) : v;
     v = k == HW_SENT_EXT ? w.sx : v;
     v = k == HW_RECV_EXT ? w.rx : v;
     v = k == HW_OUT_EXT ? w.ox : v;
@@ -1493,7 +1654,7 @@ DEV void body_lite(Wv& w, const NodeIn& x) {
     // walks end at a Sender in the active view: every send goes to an active
     // member over its connection, so the connection table is neither read
     // nor written -- nor is header word 11)
-    w.conn_n = 0; w.conn_dn = 0;
+    w.conn_n = 0; w.conn_dn = 0; w.conn_cl = 0;
     w.work = true;
     st_add(w, ST_PROC, 1);
     for (uint32_t c = 0; c < x.ik; c += 4) {          // HyParView inbox, canonical order
@@ -1678,7 +1839,7 @@ DEV void begin_pt(Wv& w, const PtIn& x, const PtX& y) {
     w.mypart = x.part;
     w.CV = act_cache(x); w.CF = y.CF;
     const uint32_t w11 = rl(x.H, HW_CONN);
-    w.conn_n = w11 & 0xFF; w.conn_dn = (w11 >> 8) & 0xFF;
+    w.conn_n = w11 & 0xFF; w.conn_dn = (w11 >> 8) & 0xFF; w.conn_cl = w11 >> 24;
     w.CN = l < w.conn_n ? x.CN : 0u;
     load_pt_regs(w, y.PA, y.PG, y.PL, y.PO);
     w.pt_dirty = false;
@@ -1922,7 +2083,7 @@ __global__ void __launch_bounds__(256, PSIM_RELAY_WAVES) k_relay(RoundArgs) {
 #pragma unroll
                 for (int q = 0; q < 4; q++) {
                     const uint32_t tt = T[q].y, type = tt & 0xFF;
-                    if (type < PSIM_MSG_PT_BROADCAST) {
+                    if (type < PSIM_MSG_PT_BROADCAST || type >= PSIM_MSG_XBOT_OPTIMIZATION) {   // (X-BOT's: heavy)
                         hvn++;
                         maps |= type <= PSIM_MSG_NEIGHBOR_ACCEPTED;   // id maps (hv:703-1089)
                         const bool relays = ((tt >> 8) & 0xFF) > 0 && h.act_n > 1;
@@ -1965,14 +2126,17 @@ __global__ void __launch_bounds__(256, PSIM_RELAY_WAVES) k_relay(RoundArgs) {
             // an active member without a connection (conn_dn): the next send
             // to it reconnects (maybe_connect) -- the connection table's path
             const bool cdown = h.conn_dn != 0 && (hvn > 0 || (tf & DESC_SHUFFLE));
+            // X-BOT: a due xbot_execution, or connection pids stopped last
+            // round (their 'EXIT's): k_consume
+            const bool xwork = a.xbot && (h.conn_cl || (D.z & DESC_XBOT_BIT));
             heavy = exits || fresh || ((tf & DESC_PROMO) && h.act_n < a.min_active) || (hvn && !all_shuf) ||
-                    term_out || cdown;
+                    term_out || cdown || xwork;
             // SHUFFLE terminals and replies (with whatever relays and shuffle
             // start come with them): k_consume_lite
             lite = !heavy && hvn && !(all_relay && h.act_n > 1);
             // a due shuffle with nothing else heavy: k_shuf, after the relays
             shuf = !heavy && !lite && (tf & DESC_SHUFFLE);
-            maps = maps || exits || (tf & DESC_PROMO);        // move_to_active: current_id
+            maps = maps || exits || (tf & DESC_PROMO) || h.conn_cl;   // move_to_active: current_id
             relay = !heavy && !lite && hvn > 0;
             const bool pt_msgs = !fresh && ik > hvn, origin = (tf & DESC_ORIGIN) != 0;
             const bool lazy = (tf & DESC_LAZY) && h.out_n > 0;

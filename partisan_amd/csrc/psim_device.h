@@ -22,8 +22,9 @@ struct __attribute__((aligned(16))) Hdr {
     uint32_t trk_hop;      // plumtree Round + 1 at that delivery (0 at the root)
     uint8_t act_n, pas_n, sent_n, sent_head;
     uint8_t recv_n, recv_head, all_n, com_n;
-    uint8_t conn_n, conn_dn, out_n, pad0;   // connection table (RoundArgs::conn): entries, of
-                                            // which | PSIM_CONN_DOWN (active members without one)
+    uint8_t conn_n, conn_dn, out_n, conn_cl; // connection table (RoundArgs::conn): entries, of
+                                             // which | PSIM_CONN_DOWN (active members without one);
+                                             // X-BOT: of which | PSIM_CONN_CLOSING (stopped pids)
     uint32_t pad1[4];      // pluggable: pad1[0] = leave/1 target of this round + 1, 0 = none;
                            // HyParView: pad1[1] / pad1[2] = the sent / recv id map's
                            // extension row + 1 (0 = none), words HW_SENT_EXT / HW_RECV_EXT;
@@ -71,8 +72,9 @@ constexpr uint32_t HW_SENT_EXT = 13, HW_RECV_EXT = 14;   // header words (Hdr pa
 constexpr uint32_t OUT_IN = 16;
 constexpr uint32_t OUT_EXT = PSIM_PT_OUT_CAP - OUT_IN;
 constexpr uint32_t HW_OUT_EXT = 15;
-// the connection table's counts: header word 11, bytes 0 (entries) and 1
-// (PSIM_CONN_DOWN entries); byte 2 is the outstanding count
+// the connection table's counts: header word 11, bytes 0 (entries), 1
+// (PSIM_CONN_DOWN entries) and 3 (PSIM_CONN_CLOSING entries); byte 2 is the
+// outstanding count
 constexpr uint32_t HW_CONN = 11;
 
 // route key: dst in the low 27 bits, the sender-side emission bound of the
@@ -98,6 +100,13 @@ __host__ __device__ constexpr uint32_t max_emit(uint32_t type) {
          : type == PSIM_MSG_PT_BROADCAST ? KEY_BCAST
          : type == PSIM_MSG_PT_IHAVE ? 1
          : type == PSIM_MSG_PT_GRAFT ? 1
+         // X-BOT: a send_join and a reply at most (xbot:1171-1314)
+         : type == PSIM_MSG_XBOT_OPTIMIZATION ? 2
+         : type == PSIM_MSG_XBOT_OPTIMIZATION_REPLY ? 1
+         : type == PSIM_MSG_XBOT_REPLACE ? 1
+         : type == PSIM_MSG_XBOT_REPLACE_REPLY ? 2
+         : type == PSIM_MSG_XBOT_SWITCH ? 2
+         : type == PSIM_MSG_XBOT_SWITCH_REPLY ? 2
          : 0;
 }
 static_assert(PSIM_ACTIVE_CAP < KEY_BCAST, "max_emit must fit the 5-bit key field below the marker");
@@ -106,22 +115,28 @@ static_assert(PSIM_ACTIVE_CAP < KEY_BCAST, "max_emit must fit the 5-bit key fiel
 
 // work descriptor (id, inbox begin, inbox count | due timers << 28, outbox
 // base): the timers k_desc found due this round for the node
-constexpr uint32_t DESC_CNT_MASK = (1u << 27) - 1;
+constexpr uint32_t DESC_CNT_MASK = (1u << 26) - 1;
 enum : uint32_t { DESC_PROMO = 1, DESC_SHUFFLE = 2, DESC_LAZY = 4, DESC_ORIGIN = 8 };
+// bit 26: X-BOT's xbot_execution timer is due (xbot:587-606, k_desc)
+constexpr uint32_t DESC_XBOT_BIT = 1u << 26;
 // bit 27 of k_consume's descriptors (k_relay): the node's HyParView phase may
 // read or write its disconnect-id maps (a JOIN .. NEIGHBOR_ACCEPTED message,
 // an EXIT, a promotion)
 constexpr uint32_t DESC_MAPS_BIT = 1u << 27;
 
-// stats slots in the per-block partial arrays
+// stats slots in the per-block partial arrays (a wave counts slot k in lane
+// k of one register, so there are at most 64): the message types with a
+// slot are 0 .. PSIM_MSG_XBOT_SWITCH_REPLY (PSIM_MSG_NTYPES rounds up)
+constexpr int ST_NTYPES = PSIM_MSG_XBOT_SWITCH_REPLY + 1;
 enum {
-    ST_EMIT = 0, ST_DELIV = PSIM_MSG_NTYPES, ST_DROPPED = 2 * PSIM_MSG_NTYPES, ST_UP, ST_PROC, ST_EXITS,
+    ST_EMIT = 0, ST_DELIV = ST_NTYPES, ST_DROPPED = 2 * ST_NTYPES, ST_UP, ST_PROC, ST_EXITS,
     ST_FAIL, ST_FIRST,
     ST_OVF, ST_DIGEST, ST_BYTES, ST_STOP,
     ST_BOUND,       // nodes that emitted more records than their outbox bound (an engine bug: fails the round)
     ST_OMIT,        // pluggable: strategy messages an omission fault dropped
     ST_OVF_BY, NST = ST_OVF_BY + PSIM_OVF_NKINDS
 };
+static_assert(NST <= 64, "a wave's stats counter holds one slot per lane");
 
 // ------------------------------------------------------------------ RNG --
 // Philox4x32-10; key = seed, counter = (draw#, node id, stream).

@@ -717,6 +717,15 @@ __global__ void __launch_bounds__(256) k_node_prep(RoundArgs a, const unsigned l
                 w = c > 0 || st == r || exits || (f & F_LAZY) || origin ||
                     (a.random_promotion && (f & F_LOWACT) && due(a.promotion_period, r, st)) ||
                     due(a.shuffle_period, r, st);
+                if (a.xbot) {
+                    // X-BOT: a due xbot_execution sends to two candidates at
+                    // most; the 'EXIT' of each connection pid stopped last
+                    // round may promote (a NEIGHBOR_REQUEST each)
+                    const bool xb = due(a.xbot_period, r, st);
+                    const uint32_t cl = x.conn_cl;
+                    b += (xb ? 2u : 0u) + cl;
+                    w = w || xb || cl;
+                }
                 // a working node's first slot is reserved: a wave that emits
                 // nothing rewrites it (flush_recs' fixed store)
                 if (w && b == 0) b = 1;
@@ -774,13 +783,14 @@ __global__ void k_desc(const uint64_t* __restrict__ packed, const uint64_t* __re
         return;
     }
     if (!(packed[li] & 1u)) return;
-    if ((uint32_t)cb[li] > DESC_CNT_MASK) hout[PIN_BIGIN] = 1;   // (the descriptor packs it in 27 bits)
+    if ((uint32_t)cb[li] > DESC_CNT_MASK) hout[PIN_BIGIN] = 1;   // (the descriptor packs it in 26 bits)
     const uint32_t st = start[li], r = a.round;
     const uint32_t tf = (a.random_promotion && due(a.promotion_period, r, st) ? DESC_PROMO : 0u) |
                         (due(a.shuffle_period, r, st) ? DESC_SHUFFLE : 0u) |
                         (a.plumtree && due(a.lazy_tick_period, r, st) ? DESC_LAZY : 0u) |
                         (a.plumtree && !a.pl && a.origin[li] ? DESC_ORIGIN : 0u);
-    desc[(uint32_t)P] = make_uint4(a.lo + li, in_beg[li], (uint32_t)cb[li] | (tf << 28), (uint32_t)(P >> 32));
+    const uint32_t xb = a.xbot && due(a.xbot_period, r, st) ? DESC_XBOT_BIT : 0u;
+    desc[(uint32_t)P] = make_uint4(a.lo + li, in_beg[li], (uint32_t)cb[li] | xb | (tf << 28), (uint32_t)(P >> 32));
 }
 
 // records src[slots[i]] -> out[i] for i < *pm, grid-stride, 4 lanes x 16 B
@@ -1230,6 +1240,7 @@ RoundArgs make_args(psim_handle* h, Shard* s) {
     a.outx_rows = (uint32_t)(s->outx.n / OUT_EXT);
     a.start = s->start.p;
     a.pl = c.manager == PSIM_MANAGER_PLUGGABLE;
+    a.xbot = c.manager == PSIM_MANAGER_XBOT; a.xbot_period = c.xbot_period;
     a.strategy = c.strategy; a.periodic = c.periodic_interval; a.scamp_c = c.scamp_c;
     a.fanout = c.fanout; a.fw = h->fw; a.tomb = h->tomb;
     a.fbits = s->fbits.p; a.sview = s->sview.p; a.sinv = s->sinv.p;
@@ -1863,7 +1874,7 @@ int run_round(psim_handle* h, uint64_t* st, bool events_applied = false) {
         if (trace_relay && s->rgrid)
         {
             uint64_t em = 0;
-            for (int k = 0; k < PSIM_MSG_NTYPES; k++) em += s->pin[ST_EMIT + k];
+            for (int k = 0; k < ST_NTYPES; k++) em += s->pin[ST_EMIT + k];
             std::fprintf(stderr, "psim: round %llu shard %u: %u nodes with work, %u to k_consume, %u to k_pt, "
                          "%u to k_shuf, %u to k_consume_lite, %u to k_ptl, outbox bound %llu, emitted %llu\n",
                          (unsigned long long)h->round, s->idx, read1(s, s->d_nact.p), read1(s, s->n_slow.p),
@@ -1941,7 +1952,7 @@ int run_round(psim_handle* h, uint64_t* st, bool events_applied = false) {
 void fill_stats(const uint64_t* s, uint64_t round, psim_round_stats* o) {
     memset(o, 0, sizeof *o);
     o->round = round;
-    for (int i = 0; i < PSIM_MSG_NTYPES; i++) {
+    for (int i = 0; i < ST_NTYPES; i++) {          // (types 22, 23: no slot, always 0)
         o->emitted[i] = s[ST_EMIT + i];
         o->delivered[i] = s[ST_DELIV + i];
     }
@@ -2226,7 +2237,7 @@ int psim_create(const psim_config* cfg, psim_handle** out) {
         cfg->n_nodes > KEY_DST_MASK || cfg->max_active_size < 2 ||
         cfg->max_active_size > PSIM_ACTIVE_CAP || cfg->max_passive_size < 1 ||
         cfg->max_passive_size > 30 || 1 + cfg->k_active + cfg->k_passive > PSIM_EXCHANGE_CAP ||
-        cfg->arwl > 255 || cfg->prwl > 255 || cfg->manager > PSIM_MANAGER_PLUGGABLE ||
+        cfg->arwl > 255 || cfg->prwl > 255 || cfg->manager > PSIM_MANAGER_XBOT ||
         cfg->strategy > PSIM_STRATEGY_SCAMP_V2 || cfg->scamp_c < 1 || cfg->scamp_c > 64 ||
         cfg->fanout > 64 || cfg->strict > 1)   /* (picks land in one 64-lane register) */
         return PSIM_EINVAL;

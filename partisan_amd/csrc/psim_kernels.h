@@ -11,6 +11,7 @@ struct RoundArgs {
     uint64_t seed;
     uint32_t max_active, min_active, max_passive, arwl, prwl, k_active, k_passive;
     uint32_t shuffle_period, promotion_period, random_promotion, plumtree, lazy_tick_period;
+    uint32_t xbot, xbot_period;   // X-BOT manager (PSIM_MANAGER_XBOT) and its xbot_execution period
     // per-round scalars
     uint32_t crash_round, tracked_msg;
     // node state: flags/part are replicated and indexed by global id;

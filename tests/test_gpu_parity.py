@@ -512,3 +512,35 @@ def test_bench_schedule_parity(name):
             bad = next(i for i, (a, b) in enumerate(zip(got, want[f])) if a != b)
             raise AssertionError(f"{name}: {f} differs first at round {bad}")
     assert hashlib.sha256(nodes.tobytes()).hexdigest() == want["state_sha256"]
+
+
+# ---- X-BOT (partisan_hyparview_xbot_peer_service_manager)
+@pytest.mark.parametrize("period", [35, 10])
+def test_xbot_parity(period):
+    """X-BOT's optimization rounds (xbot:586-606, :691-716, :1171-1346) under
+    churn and a partition: the discarded-state connects and disconnects,
+    the stopped pids' EXITs one round later, the JOIN / FORWARD_JOIN /
+    NEIGHBOR_REQUEST variants -- GPU == oracle (period 10: a busier overlay
+    whose id-map and connection-table overflows are counted identically)."""
+    (gs, gst), (os_, ost) = _both(S.churn_partition, n=2048, manager=2, xbot_period=period)
+    assert ost["emitted"][:, 16:22].sum() > 1000
+    S.compare_stats(gst, ost)
+    S.compare_nodes(gs.nodes(), os_.nodes())
+
+
+def test_xbot_shard_invariance():
+    def gpu_sharded(cfg):
+        cfg.n_shards = 3
+        return _gpu(cfg)
+    gs, gst = S.churn_partition(gpu_sharded, n=2048, manager=2, xbot_period=20)
+    os_, ost = S.churn_partition(Oracle, n=2048, manager=2, xbot_period=20)
+    S.compare_stats(gst, ost)
+    S.compare_nodes(gs.nodes(), os_.nodes())
+
+
+def test_xbot_64k_parity():
+    (gs, gst), (os_, ost) = _both(S.doubling, 1 << 16, 31, 70, bcast_period=10, bcast_first=30,
+                                  manager=2, xbot_period=12)
+    assert ost["emitted"][:, 16:22].sum() > 10000
+    S.compare_stats(gst, ost)
+    S.compare_nodes(gs.nodes(), os_.nodes())
