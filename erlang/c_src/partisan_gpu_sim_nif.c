@@ -55,9 +55,10 @@ static int get_u32(ErlNifEnv *env, ERL_NIF_TERM map, const char *k, uint32_t *ou
 }
 
 /* create(#{n_nodes => N, seed => S, max_active_size => .., ...,
- *         manager => 0 | 1, strategy => 0 | 1 | 2, fanout => K, scamp_c => C,
- *         periodic_interval => Rounds}) -> {ok, Ref}
- * manager 1 = the pluggable manager with strategy 0 full, 1 scamp v1, 2 scamp v2 */
+ *         manager => 0 | 1 | 2, strategy => 0 | 1 | 2, fanout => K, scamp_c => C,
+ *         periodic_interval => Rounds, xbot_period => Rounds}) -> {ok, Ref}
+ * manager 1 = the pluggable manager with strategy 0 full, 1 scamp v1, 2 scamp v2;
+ * manager 2 = partisan_hyparview_xbot_peer_service_manager (X-BOT) */
 static ERL_NIF_TERM nif_create(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[]) {
     psim_config c;
     ErlNifUInt64 seed;
@@ -74,7 +75,8 @@ static ERL_NIF_TERM nif_create(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv
         !get_u32(env, argv[0], "strategy", &c.strategy) ||
         !get_u32(env, argv[0], "fanout", &c.fanout) || !get_u32(env, argv[0], "strict", &c.strict) ||
         !get_u32(env, argv[0], "scamp_c", &c.scamp_c) ||
-        !get_u32(env, argv[0], "periodic_interval", &c.periodic_interval))
+        !get_u32(env, argv[0], "periodic_interval", &c.periodic_interval) ||
+        !get_u32(env, argv[0], "xbot_period", &c.xbot_period))
         return enif_make_badarg(env);
     if (enif_get_map_value(env, argv[0], enif_make_atom(env, "seed"), &v) &&
         enif_get_uint64(env, v, &seed))

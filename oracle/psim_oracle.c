@@ -1099,7 +1099,8 @@ static void process_node(struct psim_handle *h, uint32_t n) {
             !conn_closing(s, s->act[i]))
             exits[nexit++] = s->act[i];
     for (uint32_t i = 0; i < s->conn_n; i++)
-        if (!(s->conn[i] & PSIM_CONN_DOWN) && h->crashed_now[s->conn[i]]) exits[nexit++] = s->conn[i];
+        if (!(s->conn[i] & (PSIM_CONN_DOWN | PSIM_CONN_CLOSING)) && h->crashed_now[s->conn[i]])
+            exits[nexit++] = s->conn[i];
     int joining = (s->start_round == r && s->join_contact != PSIM_NONE);
     if (!(e > b || joining || nexit || nclosed || promo_work || shuf || xbot || origin || lazy)) return;
     h->st->nodes_processed++;
