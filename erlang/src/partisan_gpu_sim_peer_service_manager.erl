@@ -107,7 +107,11 @@ init([]) ->
             max_active_size => partisan_config:get(max_active_size, 6),
             min_active_size => partisan_config:get(min_active_size, 3),
             max_passive_size => partisan_config:get(max_passive_size, 30),
-            arwl => partisan_config:get(arwl, 5), prwl => partisan_config:get(prwl, 30)},
+            arwl => partisan_config:get(arwl, 5), prwl => partisan_config:get(prwl, 30),
+            %% sim_xbot = true: partisan_hyparview_xbot_peer_service_manager's
+            %% semantics (optimization rounds every xbot_period rounds)
+            manager => case partisan_config:get(sim_xbot, false) of true -> 2; _ -> 0 end,
+            xbot_period => partisan_config:get(sim_xbot_period, 35)},
     {ok, Sim} = case partisan_config:get(sim_handle, undefined) of
                     undefined -> partisan_gpu_sim:create(Cfg);
                     H -> {ok, H}

@@ -9,7 +9,7 @@ for r in rows:
     n=r['Kernel_Name']; d=(int(r['End_Timestamp'])-int(r['Start_Timestamp']))/1000
     if 'k_relay' in n: cur={'relay':d}; out.append(cur)
     elif cur is not None:
-        for k,tag in (('shuf','k_shuf'),('lite','k_consume_lite'),('ptl','k_ptl('),('merge','k_merge'),('cons','k_consume('),('pt','k_pt(')):
+        for k,tag in (('shuf','k_shuf'),('lite','k_consume_lite'),('lite','k_term'),('ptl','k_ptl('),('merge','k_merge'),('cons','k_consume('),('pt','k_pt(')):
             if tag in n: cur[k]=d
 tail=int(sys.argv[sys.argv.index('--tail')+1]) if '--tail' in sys.argv else 0
 if tail: out=out[:-tail]

@@ -5,7 +5,7 @@ profiles/pmc_records.json, which bench.py reads back by its pmc_key.
 
 Window: the `steps` timed rounds are the dispatches of each kernel before the
 overlay-drain rounds bench.py runs after its window (overlay.rounds_drained).
-Per round: the sum over the node-round kernels (k_relay, k_shuf, k_consume_lite,
+Per round: the sum over the node-round kernels (k_relay, k_shuf, k_term or k_consume_lite,
 k_consume, k_ptl, k_pt).
 
 Units and corrections (profiles/calib/, measured on this MI355X): FETCH_SIZE
@@ -21,7 +21,7 @@ import json
 import os
 import sys
 
-KERNELS = ("k_relay(", "k_shuf(", "k_consume_lite(", "k_consume(", "k_ptl(", "k_pt(")
+KERNELS = ("k_relay(", "k_shuf(", "k_consume_lite(", "k_term(", "k_consume(", "k_ptl(", "k_pt(")
 
 
 def per_round(path, steps, tail):
