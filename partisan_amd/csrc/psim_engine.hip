@@ -285,7 +285,6 @@ __global__ void __launch_bounds__(RB_STEP) k_bucket_hist(RouteIn in, uint32_t ns
     for (uint32_t j = threadIdx.x; j < nb; j += blockDim.x) hcnt[j] = 0;
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         *n_long = 0;
-        *btot = 0;                                    // summed again by the next k_node_prep
         hist[(size_t)nb * gridDim.x] = 0;             // the scan's extra entry
     }
     __syncthreads();
@@ -752,8 +751,9 @@ __global__ void __launch_bounds__(256) k_node_prep(RoundArgs a, const unsigned l
     }
     __syncthreads();
     // the exact total (the packed scan's high word wraps past 2^32 slots):
-    // one global add per block, few blocks
-    if (threadIdx.x == 0 && s_b) atomicAdd(btot, s_b);
+    // the block's sum in its own word, summed by k_desc's last block (one
+    // same-address atomic per block serialised 4096 adds at L2 every round)
+    if (threadIdx.x == 0) btot[blockIdx.x] = s_b;
     if (threadIdx.x < NST) {
         uint64_t v = threadIdx.x == ST_UP ? s_up : threadIdx.x == ST_DROPPED ? s_drop : 0ull;
         part[(size_t)blockIdx.x * NST + threadIdx.x] = v;
@@ -768,18 +768,34 @@ __global__ void k_desc(const uint64_t* __restrict__ packed, const uint64_t* __re
                        const uint32_t* __restrict__ in_beg, const unsigned long long* __restrict__ cb,
                        const uint32_t* __restrict__ start, RoundArgs a, uint4* __restrict__ desc,
                        uint64_t* __restrict__ obase, uint32_t* nact, const unsigned long long* btot,
-                       uint64_t* hout, uint64_t cap, uint32_t* ctl) {
+                       uint32_t nbt, uint64_t* hout, uint64_t cap, uint32_t* ctl) {
     const uint32_t li = blockIdx.x * blockDim.x + threadIdx.x;
-    if (li > a.n_local || *ctl) return;
+    if (*ctl) return;                                 // (uniform)
+    __shared__ unsigned long long s_w[BLK / 64], s_tot;
+    if (blockIdx.x == gridDim.x - 1) {                // the outbox total: k_node_prep's nbt block sums
+        unsigned long long t = 0;
+        for (uint32_t j = threadIdx.x; j < nbt; j += blockDim.x) t += btot[j];
+        for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o);
+        if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = t;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            unsigned long long u = 0;
+            for (uint32_t k = 0; k < blockDim.x / 64; k++) u += s_w[k];
+            s_tot = u;
+        }
+        __syncthreads();
+    }
+    if (li > a.n_local) return;
     const uint64_t P = pscan[li];
     obase[li] = P >> 32;
     if (li == a.n_local) {
+        const unsigned long long tot = s_tot;
         *nact = (uint32_t)P;
-        obase[li] = *btot;
-        hout[PIN_TOTAL] = *btot;                      // the host's one mid-round read
+        obase[li] = tot;
+        hout[PIN_TOTAL] = tot;                        // the host's one mid-round read
         // a batch (cap > 0) checks the outbox here instead: a total past its
         // capacity stops the rest of the batch (code 1, this round)
-        if (cap && *btot + 1 > cap) { ctl[1] = a.round; __threadfence(); ctl[0] = 1; }
+        if (cap && tot + 1 > cap) { ctl[1] = a.round; __threadfence(); ctl[0] = 1; }
         return;
     }
     if (!(packed[li] & 1u)) return;
@@ -1496,7 +1512,7 @@ int phase_events_prepare(psim_handle* h, Shard* s, const RoundCtl& ctl, RoundArg
         // obase[n] = the exact total (btot, summed by k_node_prep)
         TRY(scan_excl(s, s->bound.p, s->pscan.p, n + 1));
         k_desc<<<grid_for(n + 1), BLK, 0, s->stream>>>(s->bound.p, s->pscan.p, s->in_beg.p, s->cb.p, s->start.p, a,
-                                                        s->desc.p, s->obase.p, s->d_nact.p, s->btot.p, s->pin_dev,
+                                                        s->desc.p, s->obase.p, s->d_nact.p, s->btot.p, s->pgrid, s->pin_dev,
                                                         s->desc_cap, s->ctl.p);
         if (batched) goto args;
         TRY(stream_wait(s));                          // (k_desc stored the total in pin)
@@ -2135,7 +2151,7 @@ int shard_alloc(psim_handle* h, Shard* s) {
     rc |= s->outx_top.alloc(1);
     rc |= s->ocnt.alloc(n); rc |= s->cb.alloc(n + 1);
     rc |= s->in_beg.alloc(n + 1); rc |= s->bound.alloc(n + 1); rc |= s->pscan.alloc(n + 1); rc |= s->obase.alloc(n + 1);
-    rc |= s->long_list.alloc(n); rc |= s->bmask.alloc(n); rc |= s->btot.alloc(1); rc |= s->n_long.alloc(1);
+    rc |= s->long_list.alloc(n); rc |= s->bmask.alloc(n); rc |= s->btot.alloc(4096); rc |= s->n_long.alloc(1);
     rc |= s->desc.alloc(n); rc |= s->d_nact.alloc(1);
     rc |= s->desc_slow.alloc(n); rc |= s->n_slow.alloc(1);
     rc |= s->desc_pt.alloc(n); rc |= s->n_pt.alloc(1);
