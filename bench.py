@@ -602,7 +602,7 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": tsrc,
                      "traffic_upper": trec.get("traffic_upper_per_launch") if trec else None,
-                     "kernel": "k_relay + k_shuf + k_term + k_consume + k_ptl + k_pt (the node-round "
+                     "kernel": "k_relay + k_shuf + k_consume_lite + k_consume + k_ptl + k_pt (the node-round "
                                "phase: one launch of each per round on one stream, timed by s_memrealtime marker "
                                "kernels launched just before k_relay and just after k_pt)",
                      "alg_bytes_per_launch": per_launch_bytes,

@@ -1397,7 +1397,10 @@ DEV void body_hv(Wv& w, const NodeIn& x) {
     if (exits | lexits) {                             // hv:609-654
         // the crashed peers, listed before any handler runs: the active
         // members in to_list order, then the lingering peers in table order
-        uint32_t D = compact(w, w.A, exits);
+        // (from the cache's copy of the active view at node start: the
+        // X-BOT EXITs above may have shifted w.A)
+        const uint32_t AV = shfl(w.CV, (int)((l + 32) & 63));
+        uint32_t D = compact(w, AV, exits);
         const uint32_t na = popc(exits);
         const uint32_t LV = shfl(w.CV, (int)((l + 40) & 63));
         const uint32_t LD = compact(w, LV, lexits);
@@ -2411,325 +2414,6 @@ __global__ void __launch_bounds__(256) k_shuf(RoundArgs) {
                : k == ST_DIGEST ? sst[S_DIGEST] : k == ST_BOUND ? sst[S_BOUND] : 0ull;
 }
 
-// ------------------------------------------ shuffle terminals, lanes --
-// k_term: one lane per node of k_relay's lite list -- SHUFFLE terminals
-// (hv:1115-1136: sublist(Passive, |Exchange|) back to the Sender, then
-// merge_exchange), SHUFFLE_REPLYs (hv:1091-1093: merge_exchange), the relays
-// among them and a due shuffle start (hv:572-607), nothing else.  These
-// handlers touch only the passive view and the draw counter, and send only
-// to active members (k_relay's precondition: every walk ending here ends at
-// a Sender in the active view, no member is marked down), so a lane carries
-// the whole node: the active view in registers, the passive view in an LDS
-// column.  In config C's steady state a tenth of the nodes start a shuffle
-// every round and the walks end at as many terminals, whose replies reach as
-// many nodes the round after: ~2 x 10^5 nodes a round at 2^20, each a chain
-// of dependent loads and ~40 draws -- as one wave per node (k_consume_lite)
-// that was 65 % of the round.  Same handlers, draws, records, sequence
-// numbers, digest and stats as k_consume_lite / hv_handle.
-constexpr uint32_t TERM_BLK = 64;
-constexpr int TERM_K = PSIM_EXCHANGE_CAP;       // a terminal's reply: |Exchange| <= 8 ids
-
-// keep the N smallest (key, element) pairs in ascending order (the K and E
-// of slots past the inserted pairs hold ~0): topk_insert for any N
-template <int N>
-DEV void topk_ins(uint64_t (&K)[N], uint32_t (&E)[N], uint64_t key, uint32_t e) {
-    uint64_t ck = key;
-    uint32_t ce = e;
-#pragma unroll
-    for (int i = 0; i < N; i++) {
-        const bool lt = ck < K[i] || (ck == K[i] && ce < E[i]);
-        const uint64_t tk = lt ? K[i] : ck;
-        const uint32_t te = lt ? E[i] : ce;
-        K[i] = lt ? ck : K[i];
-        E[i] = lt ? ce : E[i];
-        ck = tk;
-        ce = te;
-    }
-}
-
-// rand:uniform(n) - 1 with a 58-bit generator (OTP ?uniform_range), n <= 64
-DEV uint32_t lane_uniform(uint64_t& rng, uint32_t id, uint64_t seed, uint32_t n) {
-    const uint64_t two58 = 1ull << 58;
-    for (;;) {
-        const uint64_t x = draw58_at(rng++, id, seed);
-        if (x < n) return (uint32_t)x;
-        const uint32_t i = mod_small(x, n);
-        if (x - i <= two58 - n) return i;
-    }
-}
-
-// lists:usort/1 of eight ids (~0 = none: sorts last, dropped): a sorting
-// network, then the duplicates out; returns the count, U ascending
-DEV uint32_t usort8(uint32_t (&X)[8], uint32_t (&U)[8]) {
-#define CSW(i, j) { const uint32_t lo_ = min(X[i], X[j]), hi_ = max(X[i], X[j]); X[i] = lo_; X[j] = hi_; }
-    CSW(0, 1) CSW(2, 3) CSW(4, 5) CSW(6, 7)
-    CSW(0, 2) CSW(1, 3) CSW(4, 6) CSW(5, 7)
-    CSW(1, 2) CSW(5, 6) CSW(0, 4) CSW(3, 7)
-    CSW(1, 5) CSW(2, 6)
-    CSW(1, 4) CSW(3, 6)
-    CSW(2, 4) CSW(3, 5)
-    CSW(3, 4)
-#undef CSW
-    uint32_t n = 0;
-#pragma unroll
-    for (int o = 0; o < 8; o++) U[o] = 0u;
-#pragma unroll
-    for (int i = 0; i < 8; i++) {
-        const bool keep = X[i] != ~0u && (i == 0 || X[i] != X[i - 1]);
-#pragma unroll
-        for (int o = 0; o < 8; o++) U[o] = (keep && n == (uint32_t)o) ? X[i] : U[o];
-        n += keep ? 1u : 0u;
-    }
-    return n;
-}
-
-// A lane's node.  The passive view: entry i at LDS row i of the lane's
-// column, as bucket16(id) << 28 | id (ids < 2^27, the route key's limit), so
-// that the sets v1 position of an insert is a count over the top nibble
-struct TermNode {
-    uint32_t id, me_part, act_n, pas_n;
-    uint32_t A[PSIM_ACTIVE_CAP];
-    uint32_t* P;                   // P[i * TERM_BLK]
-    uint64_t rng;
-    bool dirty;
-};
-constexpr uint32_t TERM_ID = (1u << 28) - 1;
-
-// merge_exchange/2 (hv:1590-1595): add_to_passive (hv:1423-1448) for each of
-// usort(Exchange -- Active -- [Myself]), an eviction draw whenever full
-DEV void term_merge(const TermNode& n0, TermNode& n, const uint32_t (&EX)[8], uint32_t nex, uint32_t maxp,
-                    uint64_t seed) {
-    uint32_t X[8], T[8];
-#pragma unroll
-    for (int i = 0; i < 8; i++) {
-        const uint32_t e = EX[i];
-        bool keep = (uint32_t)i < nex && e != n.id;
-#pragma unroll
-        for (int j = 0; j < PSIM_ACTIVE_CAP; j++) keep &= !((uint32_t)j < n.act_n && n.A[j] == e);
-        X[i] = keep ? e : ~0u;
-    }
-    const uint32_t mt = usort8(X, T);
-    for (uint32_t i = 0; i < mt; i++) {
-        uint32_t t = 0;
-#pragma unroll
-        for (int o = 0; o < 8; o++) t = (uint32_t)o == i ? T[o] : t;
-        bool in = false;
-        for (uint32_t j = 0; j < n.pas_n; j++) in |= (n.P[j * TERM_BLK] & TERM_ID) == t;
-        if (in) continue;
-        if (n.pas_n >= maxp) {                        // select_random(Passive, [Myself]) + delete
-            const uint32_t k = lane_uniform(n.rng, n.id, seed, n.pas_n);
-            for (uint32_t j = k; j + 1 < n.pas_n; j++) n.P[j * TERM_BLK] = n.P[(j + 1) * TERM_BLK];
-            n.pas_n--;
-        }
-        const uint32_t b = bucket16(t);
-        uint32_t pos = 0;
-        for (uint32_t j = 0; j < n.pas_n; j++) pos += (n.P[j * TERM_BLK] >> 28) <= b ? 1u : 0u;
-        for (uint32_t j = n.pas_n; j > pos; j--) n.P[j * TERM_BLK] = n.P[(j - 1) * TERM_BLK];
-        n.P[pos * TERM_BLK] = (b << 28) | t;
-        n.pas_n++;
-        n.dirty = true;
-    }
-    (void)n0;
-}
-
-#ifndef PSIM_TERM_BLOCKS_PER_CU
-#define PSIM_TERM_BLOCKS_PER_CU 4
-#endif
-__global__ void __launch_bounds__(TERM_BLK, PSIM_TERM_BLOCKS_PER_CU) k_term(RoundArgs) {
-    if (*kargs().ctl) return;                         // an aborted batch (run_batch)
-    enum { S_PROC, S_DSHUF, S_DREPLY, S_ESHUF, S_EREPLY, S_FAIL, S_DIGEST, S_BOUND, S_N };
-    __shared__ unsigned long long sst[S_N];
-    __shared__ uint32_t pcol[PSIM_PASSIVE_CAP * TERM_BLK];
-    if (threadIdx.x < S_N) sst[threadIdx.x] = 0;
-    __syncthreads();
-    const uint32_t l = lane_id();
-    const uint32_t nq = *kargs().n_lite;
-    unsigned long long v[S_N] = {};
-    TermNode n;
-    n.P = pcol + threadIdx.x;
-    for (uint32_t Q = blockIdx.x * TERM_BLK + threadIdx.x; Q < nq; Q += gridDim.x * TERM_BLK) {
-        KArgs& a = kargs();
-        const uint4 D = a.desc_lite[Q];
-        const uint32_t id = D.x, ik = D.z & DESC_CNT_MASK, tf = D.z >> 28;
-        const size_t li = id - a.lo;
-        const uint64_t seed = a.seed;
-        // the header's draw counter and counts, the active row, the passive
-        // row and the partition byte: independent, issued together
-        const uint4* hq = reinterpret_cast<const uint4*>(a.hdr + li);
-        const uint4 h0 = hq[0], h2 = hq[2];
-        const uint4* ar = reinterpret_cast<const uint4*>(a.act + li * PSIM_ACTIVE_CAP);
-        const uint4 a0 = ar[0], a1 = ar[1];
-        const uint4* pr = reinterpret_cast<const uint4*>(a.pas + li * PSIM_PASSIVE_CAP);
-        uint4 pq[PSIM_PASSIVE_CAP / 4];
-#pragma unroll
-        for (int q = 0; q < PSIM_PASSIVE_CAP / 4; q++) pq[q] = pr[q];
-        n.me_part = a.part[id];
-        n.id = id;
-        n.rng = ((uint64_t)h0.y << 32) | h0.x;
-        const uint32_t w9 = h2.y;                     // act_n | pas_n << 8 | sent_n << 16 | sent_head << 24
-        n.act_n = w9 & 0xFF; n.pas_n = (w9 >> 8) & 0xFF;
-        n.A[0] = a0.x; n.A[1] = a0.y; n.A[2] = a0.z; n.A[3] = a0.w;
-        n.A[4] = a1.x; n.A[5] = a1.y; n.A[6] = a1.z; n.A[7] = a1.w;
-#pragma unroll
-        for (int q = 0; q < PSIM_PASSIVE_CAP / 4; q++) {
-            const uint32_t Pq[4] = {pq[q].x, pq[q].y, pq[q].z, pq[q].w};
-#pragma unroll
-            for (int c = 0; c < 4; c++) n.P[(4 * q + c) * TERM_BLK] = (bucket16(Pq[c]) << 28) | Pq[c];
-        }
-        n.dirty = false;
-        const uint32_t maxp = a.max_passive;
-        uint32_t seq = 0;
-        const uint32_t oend = (uint32_t)a.obase[li + 1];
-        v[S_PROC]++;
-        // (src, type word) and the exchange of the next record, issued
-        // before the current one is handled
-        const Msg* rb = a.rec_in + D.y;
-        for (uint32_t j = 0; j < ik; j++) {            // the HyParView inbox, canonical order
-            const uint4 r0 = *reinterpret_cast<const uint4*>(rb + j);
-            const uint32_t tt = r0.z, type = tt & 0xFF, src = r0.y;
-            if (type != PSIM_MSG_SHUFFLE && type != PSIM_MSG_SHUFFLE_REPLY) continue;   // (Plumtree: k_ptl / k_pt)
-            const uint32_t ttl = (tt >> 8) & 0xFF, nex = (tt >> 16) & 0xFF;
-            const uint4* ex = reinterpret_cast<const uint4*>(rb[j].ex);
-            const uint4 e0 = ex[0], e1 = ex[1];
-            uint32_t EX[8] = {e0.x, e0.y, e0.z, e0.w, e1.x, e1.y, e1.z, e1.w};
-#pragma unroll
-            for (int k = 0; k < 8; k++) EX[k] = (uint32_t)k < nex ? EX[k] : 0u;
-            if (type == PSIM_MSG_SHUFFLE_REPLY) {    // hv:1091-1093
-                v[S_DREPLY]++;
-                term_merge(n, n, EX, nex, maxp, seed);
-                continue;
-            }
-            v[S_DSHUF]++;
-            if (ttl > 0 && n.act_n > 1) {             // hv:1095-1113: relay to select_random(Active, [Sender, Myself])
-                uint32_t elig = 0;
-#pragma unroll
-                for (int k = 0; k < 8; k++) elig |= ((uint32_t)k < n.act_n && n.A[k] != src && n.A[k] != id) ? (1u << k) : 0u;
-                const uint32_t cnt = __popc(elig);
-                if (!cnt) continue;
-                const uint32_t kk = lane_uniform(n.rng, id, seed, cnt);
-                uint32_t e = elig;
-                for (uint32_t q = 0; q < kk; q++) e &= e - 1;
-                uint32_t r = 0;
-#pragma unroll
-                for (int k = 0; k < 8; k++) r = (__ffs(e) - 1 == k) ? n.A[k] : r;
-                if (r < a.n_nodes && (a.flags[r] & F_UP) && a.part[r] == n.me_part) {
-                    n.rng++;                          // dispatch_pid/1 (util:190-195)
-                    v[S_DIGEST] += relay_emit(a, D.w + seq, r, id, PSIM_MSG_SHUFFLE | ((ttl - 1) << 8) | (nex << 16),
-                                              seq, 0u, 0u, 0u, EX);
-                    seq++;
-                    v[S_ESHUF]++;
-                } else {
-                    v[S_FAIL]++;
-                }
-                continue;
-            }
-            // the walk ends here (hv:1115-1136): sublist(Passive, |Exchange|)
-            // to the Sender, then merge_exchange
-            uint64_t K[TERM_K];
-            uint32_t E[TERM_K];
-#pragma unroll
-            for (int k = 0; k < TERM_K; k++) { K[k] = ~0ull; E[k] = ~0u; }
-            for (uint32_t q = 0; q < n.pas_n; q++)
-                topk_ins(K, E, draw58_at(n.rng + q, id, seed) >> 5, n.P[q * TERM_BLK] & TERM_ID);
-            n.rng += n.pas_n;
-            const uint32_t nr = min(n.pas_n, nex);
-            uint32_t RESP[8];
-#pragma unroll
-            for (int k = 0; k < 8; k++) RESP[k] = (uint32_t)k < nr ? E[k] : 0u;
-            if (src < a.n_nodes && (a.flags[src] & F_UP) && a.part[src] == n.me_part) {
-                n.rng++;
-                v[S_DIGEST] += relay_emit(a, D.w + seq, src, id, PSIM_MSG_SHUFFLE_REPLY | (nr << 16), seq,
-                                          0u, 0u, 0u, RESP);
-                seq++;
-                v[S_EREPLY]++;
-            } else {
-                v[S_FAIL]++;
-            }
-            term_merge(n, n, EX, nex, maxp, seed);
-        }
-        if (tf & DESC_SHUFFLE) {                      // hv:572-607: the shuffle start, over the merged views
-            uint64_t K[SHUF_TOPK];
-            uint32_t E[SHUF_TOPK];
-#pragma unroll
-            for (int k = 0; k < SHUF_TOPK; k++) { K[k] = ~0ull; E[k] = ~0u; }
-#pragma unroll
-            for (int k = 0; k < PSIM_ACTIVE_CAP; k++)
-                if ((uint32_t)k < n.act_n) topk_ins(K, E, draw58_at(n.rng + k, id, seed) >> 5, n.A[k]);
-            n.rng += n.act_n;
-            const uint32_t ka = min(n.act_n, a.k_active), kp = min(n.pas_n, a.k_passive);
-            uint32_t X[8];
-            X[0] = id;
-#pragma unroll
-            for (int k = 0; k < SHUF_TOPK; k++) X[1 + k] = (uint32_t)k < ka ? E[k] : ~0u;
-#pragma unroll
-            for (int k = 0; k < SHUF_TOPK; k++) { K[k] = ~0ull; E[k] = ~0u; }
-            for (uint32_t q = 0; q < n.pas_n; q++)
-                topk_ins(K, E, draw58_at(n.rng + q, id, seed) >> 5, n.P[q * TERM_BLK] & TERM_ID);
-            n.rng += n.pas_n;
-#pragma unroll
-            for (int k = 0; k < SHUF_TOPK; k++) {
-                const uint32_t e = (uint32_t)k < kp ? E[k] : ~0u;
-#pragma unroll
-                for (int o = 1; o < 8; o++) X[o] = ((uint32_t)o == 1 + ka + (uint32_t)k) ? e : X[o];
-            }
-            uint32_t U[8];
-            const uint32_t nx = usort8(X, U);
-            uint32_t elig = 0;                        // select_random(Active, [Myself])
-#pragma unroll
-            for (int k = 0; k < 8; k++) elig |= ((uint32_t)k < n.act_n && n.A[k] != id) ? (1u << k) : 0u;
-            const uint32_t cnt = __popc(elig);
-            if (cnt) {
-                const uint32_t kk = lane_uniform(n.rng, id, seed, cnt);
-                uint32_t e = elig;
-                for (uint32_t q = 0; q < kk; q++) e &= e - 1;
-                uint32_t t = 0;
-#pragma unroll
-                for (int k = 0; k < 8; k++) t = (__ffs(e) - 1 == k) ? n.A[k] : t;
-                if (t < a.n_nodes && (a.flags[t] & F_UP) && a.part[t] == n.me_part) {
-                    n.rng++;
-                    v[S_DIGEST] += relay_emit(a, D.w + seq, t, id, PSIM_MSG_SHUFFLE | (a.arwl << 8) | (nx << 16), seq,
-                                              0u, 0u, 0u, U);
-                    seq++;
-                    v[S_ESHUF]++;
-                } else {
-                    v[S_FAIL]++;
-                }
-            }
-        }
-        // write back: the draw counter, pas_n in word 9, the passive row if
-        // it changed, the outbox count
-        uint32_t* hw = reinterpret_cast<uint32_t*>(a.hdr + li);
-        reinterpret_cast<uint2*>(hw)[0] = make_uint2((uint32_t)n.rng, (uint32_t)(n.rng >> 32));
-        if (n.dirty) {
-            hw[9] = (w9 & ~0xFF00u) | (n.pas_n << 8);
-            uint4* pw = reinterpret_cast<uint4*>(a.pas + li * PSIM_PASSIVE_CAP);
-#pragma unroll
-            for (int q = 0; q < PSIM_PASSIVE_CAP / 4; q++) {
-                uint32_t o[4];
-#pragma unroll
-                for (int c = 0; c < 4; c++)
-                    o[c] = (uint32_t)(4 * q + c) < n.pas_n ? (n.P[(4 * q + c) * TERM_BLK] & TERM_ID) : 0u;
-                pw[q] = make_uint4(o[0], o[1], o[2], o[3]);
-            }
-        }
-        a.ocnt[li] = seq;
-        v[S_BOUND] += seq > oend - D.w ? 1u : 0u;
-    }
-#pragma unroll
-    for (int k = 0; k < S_N; k++)
-        for (int o = 32; o > 0; o >>= 1) v[k] += __shfl_xor(v[k], o);
-    if (l == 0)
-        for (int k = 0; k < S_N; k++)
-            if (v[k]) atomicAdd(&sst[k], v[k]);
-    __syncthreads();
-    uint64_t* row = kargs().stat_lite + (size_t)blockIdx.x * NST;
-    for (uint32_t k = threadIdx.x; k < NST; k += blockDim.x)
-        row[k] = k == ST_PROC ? sst[S_PROC] : k == ST_DELIV + PSIM_MSG_SHUFFLE ? sst[S_DSHUF]
-               : k == ST_DELIV + PSIM_MSG_SHUFFLE_REPLY ? sst[S_DREPLY] : k == ST_EMIT + PSIM_MSG_SHUFFLE ? sst[S_ESHUF]
-               : k == ST_EMIT + PSIM_MSG_SHUFFLE_REPLY ? sst[S_EREPLY] : k == ST_FAIL ? sst[S_FAIL]
-               : k == ST_DIGEST ? sst[S_DIGEST] : k == ST_BOUND ? sst[S_BOUND] : 0ull;
-}
-
 // ---------------------------------------------------- Plumtree lanes --
 // k_ptl: one lane per node with Plumtree work (k_relay's list, origins
 // aside), after its HyParView phase.  In config C's steady state a node keeps
@@ -3181,7 +2865,6 @@ static uint32_t resident_grid(const void* k, int block = WAVES_PER_BLOCK * 64) {
 }
 uint32_t consume_grid() { return resident_grid((const void*)k_consume); }
 uint32_t lite_grid() { return resident_grid((const void*)k_consume_lite); }
-uint32_t term_grid() { return resident_grid((const void*)k_term, TERM_BLK); }
 uint32_t pt_grid() { return resident_grid((const void*)k_pt); }
 uint32_t ptl_grid() { return resident_grid((const void*)k_ptl, PTL_BLK); }
 

@@ -1191,8 +1191,6 @@ struct psim_handle {
     uint32_t consume_blocks = 1024;     // resident k_consume blocks on the device
     uint32_t pt_blocks = 1024;          // ... and k_pt blocks
     uint32_t lite_blocks = 1024;        // ... and k_consume_lite blocks
-    uint32_t term_blocks = 1024;        // ... and k_term's (64 lanes)
-    bool lite_wave = false;             // PSIM_LITE_WAVE=1: k_consume_lite instead of k_term
     uint32_t ptl_blocks = 1024;         // ... and k_ptl blocks
     uint64_t round = 0;
     std::vector<Shard*> shards;         // shards owned by this process
@@ -1500,9 +1498,7 @@ int phase_events_prepare(psim_handle* h, Shard* s, const RoundCtl& ctl, RoundArg
         s->rgrid = hv ? std::min<uint32_t>(grid_for(n), RELAY_MAX_BLOCKS) : 0;
         s->tgrid = hv && h->cfg.plumtree ? std::min<uint32_t>(grid_for(n), h->pt_blocks) : 0;
         s->sgrid = hv ? std::min<uint32_t>(grid_for(n), SHUF_MAX_BLOCKS) : 0;
-        s->lgrid = !hv ? 0
-                 : h->lite_wave ? std::min<uint32_t>(grid_for(n), h->lite_blocks)
-                                : std::min<uint32_t>((n + TERM_BLOCK - 1) / TERM_BLOCK, h->term_blocks);
+        s->lgrid = hv ? std::min<uint32_t>(grid_for(n), h->lite_blocks) : 0;
         s->qgrid = hv && h->cfg.plumtree ? std::min<uint32_t>((n + PTL_BLOCK - 1) / PTL_BLOCK, h->ptl_blocks) : 0;
         TRY(s->stat_part.ensure((size_t)(s->pgrid + s->cgrid + s->rgrid + s->tgrid + s->sgrid + s->lgrid + s->qgrid) *
                                 NST));
@@ -1610,10 +1606,7 @@ int phase_consume(psim_handle* h, Shard* s, RoundArgs& a) {
         k_mark<<<1, 64, 0, s->stream>>>(a.ktime, 0, s->ctl.p);
         k_relay<<<s->rgrid, BLK, 0, s->stream>>>(a);
         k_shuf<<<s->sgrid, BLK, 0, s->stream>>>(a);
-        // SHUFFLE terminals and replies: one lane per node (k_term), or one
-        // wave per node (k_consume_lite, PSIM_LITE_WAVE=1)
-        if (h->lite_wave) k_consume_lite<<<s->lgrid, BLK, 0, s->stream>>>(a);
-        else k_term<<<s->lgrid, TERM_BLOCK, 0, s->stream>>>(a);
+        k_consume_lite<<<s->lgrid, BLK, 0, s->stream>>>(a);
         RoundArgs b = a;
         b.desc = s->desc_slow.p;
         b.n_alist = s->n_slow.p;
@@ -2290,11 +2283,7 @@ int psim_create(const psim_config* cfg, psim_handle** out) {
     h->consume_blocks = psim::consume_grid();
     h->pt_blocks = psim::pt_grid();
     h->lite_blocks = psim::lite_grid();
-    h->term_blocks = psim::term_grid();
-    {
-        const char* e = getenv("PSIM_LITE_WAVE");
-        h->lite_wave = e && atoi(e) != 0;
-    }
+
     h->ptl_blocks = psim::ptl_grid();
     if (const char* e = getenv("PSIM_PTL_GRID")) {      // (a smaller k_ptl grid, for measurements)
         const long v = strtol(e, nullptr, 10);

@@ -115,10 +115,6 @@ __global__ void k_consume_pl(RoundArgs args);
 __global__ void k_shuf(RoundArgs args);
 // wave-per-node SHUFFLE terminals, replies and their merges (psim_consume.hip)
 __global__ void k_consume_lite(RoundArgs args);
-// lane-per-node SHUFFLE terminals, replies and their merges (psim_consume.hip):
-// k_consume_lite's list one lane per node (64-lane blocks)
-__global__ void k_term(RoundArgs args);
-constexpr uint32_t TERM_BLOCK = 64;
 // lane-per-node Plumtree phases (psim_consume.hip); hands k_pt what does not fit
 __global__ void k_ptl(RoundArgs args);
 // a timestamp into t[slot] (the node-round span, RoundArgs::ktime)
@@ -130,7 +126,6 @@ int debug_stamps(unsigned long long* out);
 // resident-block count of k_consume on the current device
 uint32_t consume_grid();
 uint32_t lite_grid();
-uint32_t term_grid();
 uint32_t pt_grid();
 uint32_t ptl_grid();
 

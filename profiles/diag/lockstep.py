@@ -73,7 +73,7 @@ class Lockstep:
                     print(f"    peers up before/after: {[(q, int(prev['up'][q]), int(o['up'][q])) for q in sorted(peers) if q < self.n]}")
                     for m in ib[ib[:, 0] == i]:
                         print(f"    in: src {m[1]} seq {m[2]} type {m[3] & 0xFF} ttl {(m[3] >> 8) & 0xFF} "
-                              f"a0 {m[4]} a1 {m[5]} a2 {m[6]} ex {m[8:8 + ((m[3] >> 16) & 0xFF)].tolist()}")
+                              f"a0 {m[4]} a1 {m[5]} a2 {m[6]} a3 {m[7]} ex {m[8:8 + ((m[3] >> 16) & 0xFF)].tolist()}")
                 raise Diverged(r)
         return np.concatenate(out)
 

@@ -61,6 +61,12 @@ def churn_partition(make, n=2048, seed=5, rounds=140, **cfg):
     return sim, st
 
 
+def xbot_churn(make, n=2048, seed=5, rounds=140, period=10):
+    """churn_partition under the X-BOT manager: optimization
+    rounds every `period` rounds through the churn and the partition."""
+    return churn_partition(make, n=n, seed=seed, rounds=rounds, manager=2, xbot_period=period)
+
+
 def joiner_crash(make, n=2048, seed=3, rounds=40, **cfg):
     """A doubling bootstrap where a third of each round's joiners crash two
     rounds after they start, while their FORWARD_JOINs are still walking.
