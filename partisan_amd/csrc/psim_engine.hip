@@ -2130,8 +2130,11 @@ int shard_alloc(psim_handle* h, Shard* s) {
     rc |= s->act.alloc(n * PSIM_ACTIVE_CAP); rc |= s->pas.alloc(n * PSIM_PASSIVE_CAP);
     rc |= s->sentm.alloc(n * IDMAP_IN); rc |= s->recvm.alloc(n * IDMAP_IN);
     if (h->cfg.manager != PSIM_MANAGER_PLUGGABLE) {
-        // extension rows for 1/32 of the nodes (~1/1700 used at 2^23 under config E)
-        const size_t rows = std::max<size_t>(1024, n / 32);
+        // extension rows for 1/32 of the nodes (~1/1700 used at 2^23 under config E);
+        // X-BOT's optimization rounds disconnect and rejoin peers all the time
+        // (most nodes' maps pass 16 entries within 50 rounds at a 10-round
+        // period): one row per map and node, the oracle's full 64 entries
+        const size_t rows = h->cfg.manager == PSIM_MANAGER_XBOT ? 2 * n : std::max<size_t>(1024, n / 32);
         rc |= s->mapx.alloc(rows * IDMAP_EXT);
     }
     rc |= s->mapx_top.alloc(1);
