@@ -39,6 +39,7 @@ constexpr int WAVES_PER_BLOCK = 4;
 // boundaries, summed per phase over all waves (psim::debug_stamps).
 #ifdef PSIM_STAMPS
 __device__ unsigned long long g_stamps[32];
+__device__ unsigned long long g_stamps_lite[32];   // k_consume_lite's phases (profiles/stamps.py --lite)
 #define STAMP(w, k)                                                                  \
     do {                                                                             \
         uint64_t t_ = __builtin_amdgcn_s_memtime();                                  \
@@ -1660,6 +1661,7 @@ DEV void body_lite(Wv& w, const NodeIn& x) {
     w.conn_n = 0; w.conn_dn = 0; w.conn_cl = 0;
     w.work = true;
     st_add(w, ST_PROC, 1);
+    STAMP(w, 1);
     for (uint32_t c = 0; c < x.ik; c += 4) {          // HyParView inbox, canonical order
         uint32_t R4 = inbox_chunk(w, a, x.ib, x.ik, c, x.R0);
         uint32_t cm = x.ik - c < 4 ? x.ik - c : 4;
@@ -1672,24 +1674,32 @@ DEV void body_lite(Wv& w, const NodeIn& x) {
             uint32_t ex = shfl(R4, (int)((b + 8 + l) & 63));
             ex = l < nex ? ex : 0u;
             const uint32_t p = rl(R4, b + 1), ttl = (tt >> 8) & 0xFF;
+            STAMP(w, 2);
             if (type == PSIM_MSG_SHUFFLE_REPLY) {        // hv:1091-1093
                 merge_exchange(w, ex, nex);
+                STAMP(w, 3);
             } else if (ttl > 0 && w.act_n > 1) {         // hv:1095-1136: relay
                 uint32_t r = select_random(w, w.A, w.act_n, p, w.me, w.me);
                 if (r != NONE) hv_send(w, r, PSIM_MSG_SHUFFLE, ttl - 1, 0, 0, ex, nex);
+                STAMP(w, 4);
             } else {                                     // the walk ends here
                 uint32_t RESP = 0;
                 uint32_t nr = sublist(w, w.P, w.pas_n, nex, RESP, 0);
+                STAMP(w, 5);
                 hv_send(w, p, PSIM_MSG_SHUFFLE_REPLY, 0, 0, 0, RESP, nr);
+                STAMP(w, 6);
                 merge_exchange(w, ex, nex);
+                STAMP(w, 7);
             }
         }
     }
+    STAMP(w, 2);
     if (x.tf & DESC_SHUFFLE) {                        // hv:572-607
         uint32_t EX;
         uint32_t nex = build_exchange(w, EX);
         uint32_t t = select_random(w, w.A, w.act_n, w.me, w.me, w.me);
         if (t != NONE) hv_send(w, t, PSIM_MSG_SHUFFLE, a.arwl, 0, 0, EX, nex);
+        STAMP(w, 8);
     }
 }
 
@@ -1737,6 +1747,12 @@ __global__ void __launch_bounds__(256, PSIM_LITE_WAVES) k_consume_lite(RoundArgs
     w.srec = srecs[wid];
     w.skey = skeys[wid];
     w.slots = nullptr;
+#ifdef PSIM_STAMPS
+    __shared__ uint64_t stamps[WAVES_PER_BLOCK][32];
+    if ((threadIdx.x & 63) < 32) stamps[wid][threadIdx.x & 63] = 0;
+    w.stl = stamps[wid];
+    w.t_last = __builtin_amdgcn_s_memtime();
+#endif
     w.st = sst;
     w.round = kargs().round;
     w.SC = 0;
@@ -1751,15 +1767,22 @@ __global__ void __launch_bounds__(256, PSIM_LITE_WAVES) k_consume_lite(RoundArgs
         NodeIn xn = load_node<false>(kargs(), reinterpret_cast<const uint32_t*>(kargs().desc_lite + min(gw + nw, last))[lane_id() & 3]);
         uint32_t d = reinterpret_cast<const uint32_t*>(kargs().desc_lite + min(gw + 2 * nw, last))[lane_id() & 3];
         for (uint32_t i = gw; i < na; i += nw) {
+            STAMP(w, 0);
             begin_node(w, x, y);
             body_lite(w, x);
             NodeX yn = load_x<true>(kargs(), xn);
+            STAMP(w, 9);
             writeback_lite(w);
+            STAMP(w, 10);
             NodeIn xnn = load_node<false>(kargs(), d);
             d = reinterpret_cast<const uint32_t*>(kargs().desc_lite + min(i + 3 * nw, last))[lane_id() & 3];
             x = xn; y = yn; xn = xnn;
+            STAMP(w, 11);
         }
     }
+#ifdef PSIM_STAMPS
+    if (lane_id() < 32) atomicAdd(&g_stamps_lite[lane_id()], (unsigned long long)w.stl[lane_id()]);
+#endif
     flush_wave_stats(w, sst);
     __syncthreads();
     for (int i = threadIdx.x; i < NST; i += blockDim.x)
@@ -2870,10 +2893,14 @@ uint32_t ptl_grid() { return resident_grid((const void*)k_ptl, PTL_BLK); }
 
 #ifdef PSIM_STAMPS
 int debug_stamps(unsigned long long* out) {
+    // k_consume / k_pt phases in out[0..31], k_consume_lite's in out[32..63]
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 32) != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(out + 32, HIP_SYMBOL(g_stamps_lite), sizeof(unsigned long long) * 32) != hipSuccess)
+        return -1;
     unsigned long long z[32] = {0};
     if (hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), z, sizeof z) != hipSuccess) return -1;
-    return 32;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_stamps_lite), z, sizeof z) != hipSuccess) return -1;
+    return 64;
 }
 #else
 int debug_stamps(unsigned long long*) { return 0; }

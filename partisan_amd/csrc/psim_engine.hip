@@ -2981,7 +2981,7 @@ int psim_kernel_times(psim_handle* h, const char** names, double* ms, uint64_t* 
 
 // diagnostic: per-phase s_memtime sums of k_consume (zeros unless built with -DPSIM_STAMPS)
 int psim_debug_stamps(unsigned long long* out, int cap) {
-    if (!out || cap < 32) return PSIM_EINVAL;
+    if (!out || cap < 64) return PSIM_EINVAL;
     return psim::debug_stamps(out);
 }
 

@@ -1,8 +1,11 @@
-"""Per-phase cycle breakdown of k_consume (diagnostic builds, -DPSIM_STAMPS).
+"""Per-phase cycle breakdown of the wave-per-node kernels (diagnostic
+builds, -DPSIM_STAMPS: `make -C partisan_amd/csrc stamps`, loaded with
+PSIM_LIB=stamps).
 
-Runs config C like bench.py and prints the summed s_memtime deltas per phase
-of the wave-per-node consume kernel over the timed rounds.
-Usage: python profiles/stamps.py [--nodes N] [--steps K]
+Runs bench.py's config C schedule (workloads.BenchSchedule, survey by
+default) and prints the summed s_memtime deltas per phase of k_consume /
+k_pt and of k_consume_lite over the timed rounds.
+Usage: PSIM_LIB=stamps python profiles/stamps.py [--nodes N] [--steps K] [--schedule survey|doubling]
 """
 import argparse
 import ctypes as C
@@ -25,12 +28,27 @@ for i, n in enumerate(HV):
     NAMES[4 + i] = "hv:" + n
 for i, n in enumerate(PT):
     NAMES[16 + i] = "pt:" + n
+LITE = {0: "wait for the node's loads", 1: "begin_node", 2: "inbox chunk / record parse", 3: "SHUFFLE_REPLY merge",
+        4: "SHUFFLE relay", 5: "terminal: sublist", 6: "terminal: reply send", 7: "terminal: merge",
+        8: "shuffle start", 9: "next node's 2nd-stage loads", 10: "writeback", 11: "next node's loads"}
+
+
+def table(v, names, steps):
+    tot = v.sum()
+    if tot == 0:
+        return
+    print(f"  total wave-ticks {tot:.4g} ({tot / steps:.4g}/round)")
+    for k in np.argsort(-v):
+        if v[k]:
+            print(f"    {names.get(int(k), str(k)):30s} {v[k] / tot * 100:6.2f}%  {v[k] / steps:.4g}/round")
 
 
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("--nodes", type=int, default=1 << 20)
     p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--schedule", default="survey")
     a = p.parse_args()
     from partisan_amd import Simulator, _lib
     from partisan_amd import workloads as W
@@ -39,40 +57,32 @@ def main():
     lib = _lib.load()
     lib.psim_debug_stamps.restype = C.c_int
     lib.psim_debug_stamps.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
-    buf = (C.c_ulonglong * 32)()
+    buf = (C.c_ulonglong * 64)()
     sim = Simulator(default_config(n_nodes=a.nodes, seed=1))
-    boot = W.doubling_join(a.nodes, 1)
-    sim.run_schedule(boot, boot[-1][0] + 61)
-    # bench.py's schedule: 45 untimed broadcast rounds (steady state), then
-    # the measured rounds, a broadcast from node 0 every 10 rounds
-    k = 0
-    for i in range(45):
-        if i % 10 == 0:
-            sim.broadcast(0, k)
-            k += 1
+    sched = W.BenchSchedule("C", a.schedule, a.nodes, 1, a.warmup)
+    boot, until = sched.bootstrap()
+    sim.run_schedule(boot, until)
+    for i in range(sched.t_start):
+        sched.apply(sim, i)
         sim.step(1)
-    if lib.psim_debug_stamps(buf, 32) != 32:
-        print("library built without -DPSIM_STAMPS")
+    if lib.psim_debug_stamps(buf, 64) != 64:
+        print("library built without -DPSIM_STAMPS (make -C partisan_amd/csrc stamps; PSIM_LIB=stamps)")
         return
     st = []
-    for i in range(45, 45 + a.steps):
-        if i % 10 == 0:
-            sim.broadcast(0, k)
-            k += 1
+    for i in range(sched.t_start, sched.t_start + a.steps):
+        sched.apply(sim, i)
         st.append(sim.step(1))
-    lib.psim_debug_stamps(buf, 32)
+    lib.psim_debug_stamps(buf, 64)
     st = np.concatenate(st)
     v = np.array(buf[:], np.float64)
-    tot = v.sum()
-    print(f"rounds {a.steps}  processed {int(st['nodes_processed'].sum())}  "
-          f"delivered {int(st['delivered'].sum())}  emitted {int(st['emitted'].sum())}")
-    print(f"total wave-ticks {tot:.4g} (s_memtime: shader clock)")
+    print(f"{a.schedule} schedule, {a.nodes} nodes, rounds {a.steps}: processed {int(st['nodes_processed'].sum())} "
+          f"delivered {int(st['delivered'].sum())} emitted {int(st['emitted'].sum())} (s_memtime ticks)")
     dl = st["delivered"].sum(axis=0) / a.steps
     print("delivered/round: " + ", ".join(f"{n}={int(dl[i])}" for i, n in enumerate(HV + PT) if dl[i]))
-    for k in np.argsort(-v):
-        if v[k] == 0:
-            continue
-        print(f"  {NAMES.get(int(k), str(k)):18s} {v[k] / tot * 100:6.2f}%  {v[k] / a.steps:.4g}/round")
+    print("k_consume / k_pt:")
+    table(v[:32], NAMES, a.steps)
+    print("k_consume_lite:")
+    table(v[32:], LITE, a.steps)
 
 
 if __name__ == "__main__":
