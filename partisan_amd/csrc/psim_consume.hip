@@ -1651,61 +1651,9 @@ __global__ void __launch_bounds__(256, PSIM_WAVES_PER_SIMD) k_consume(RoundArgs 
 // a fraction of k_consume's live state and runs at twice its occupancy: in
 // the rounds after a cohort's shuffle starts, most of k_consume's list was
 // these nodes.  Same handlers (hv_handle), draws, records and stats.
-// k_consume_lite keeps the passive view tagged: entry = bucket16(id) << 28 |
-// id (ids < 2^27, the route key's limit), so a sets-v1 insert position is a
-// count over the top nibble and a membership test one compare
-constexpr uint32_t PID_MASK = (1u << 28) - 1;
-
-// merge_exchange/2 (hv:1590-1595) over the tagged passive view: add_to_passive
-// for each of usort(Exchange -- Active -- [Myself]).  An exchange never holds
-// an id twice (build_exchange usorts, a terminal's reply is a sublist of a
-// set), so the usort is a rank by value.  With the view full (the steady
-// state) each add evicts the draw's index and inserts by bucket in one lane
-// shift.  Same draws and result as merge_exchange.
-DEV void merge_lite(Wv& w, uint32_t EX, uint32_t nex) {
-    const uint32_t l = lane_id();
-    bool in_act = false;
-    for (uint32_t j = 0; j < w.act_n; j++) in_act |= (EX == rl(w.A, j));
-    const uint64_t valid = ballot(l < nex && EX != w.me && !in_act);
-    if (!valid) return;
-    const uint32_t mt = popc(valid);
-    uint32_t rank = 0;
-    for (uint64_t m = valid; m; m &= m - 1) rank += rl(EX, ffs64(m)) < EX ? 1u : 0u;
-    if ((valid >> l) & 1ull) w.lds[rank] = EX;
-    __builtin_amdgcn_wave_barrier();
-    const uint32_t T = l < mt ? w.lds[l] : 0u;
-    __builtin_amdgcn_wave_barrier();
-    const uint32_t maxp = kargs().max_passive;
-    const uint64_t c0 = w.rng;
-    if (c0 < w.dc_base || c0 + mt - w.dc_base > 64) dc_fill(w, c0);   // cover [c0, c0 + mt)
-    const uint32_t off = (uint32_t)(c0 - w.dc_base);
-    const uint32_t src = (off + l) & 63;
-    const uint64_t v = ((uint64_t)shfl(w.DCH, (int)src) << 32) | shfl(w.DCL, (int)src);
-    const uint32_t KI = mod_small_m(v, maxp, rl(w.KM, maxp & 63));
-    const bool rej = v >= maxp && v - KI > (1ull << 58) - maxp;
-    uint32_t used = 0;
-    const bool seq_draws = maxp > 64 || ballot(l < mt && rej);   // (p ~ 2^-53: draw one at a time)
-    for (uint32_t i = 0; i < mt; i++) {
-        const uint32_t t = rl(T, i), b = bucket16(t), tb = (b << 28) | t;
-        if (ballot(l < w.pas_n && w.P == tb)) continue;
-        w.vd |= 2u;
-        if (w.pas_n >= maxp) {                       // select_random(Passive, [Myself]) + delete, then insert
-            const uint32_t k = seq_draws ? uniform_n(w, w.pas_n) - 1 : rl(KI, used++);
-            const uint32_t pos = popc(ballot(l < w.pas_n && (w.P >> 28) <= b)) - ((rl(w.P, k) >> 28) <= b ? 1u : 0u);
-            const uint32_t nx = from_next(w.P), pv = from_prev(w.P);
-            w.P = k <= pos ? (l < k ? w.P : l < pos ? nx : l == pos ? tb : w.P)
-                           : (l < pos ? w.P : l == pos ? tb : l <= k ? pv : w.P);
-        } else {
-            vins(w.P, w.pas_n, popc(ballot(l < w.pas_n && (w.P >> 28) <= b)), tb);
-        }
-    }
-    if (!seq_draws) w.rng = c0 + used;
-}
-
 DEV void body_lite(Wv& w, const NodeIn& x) {
     KArgs& a = kargs();
     const uint32_t l = lane_id();
-    w.P = l < w.pas_n ? (bucket16(w.P) << 28) | w.P : 0u;   // the tagged view (merge_lite)
     // (k_relay sends here only nodes with no active member marked down whose
     // walks end at a Sender in the active view: every send goes to an active
     // member over its connection, so the connection table is neither read
@@ -1728,7 +1676,7 @@ DEV void body_lite(Wv& w, const NodeIn& x) {
             const uint32_t p = rl(R4, b + 1), ttl = (tt >> 8) & 0xFF;
             STAMP(w, 2);
             if (type == PSIM_MSG_SHUFFLE_REPLY) {        // hv:1091-1093
-                merge_lite(w, ex, nex);
+                merge_exchange(w, ex, nex);
                 STAMP(w, 3);
             } else if (ttl > 0 && w.act_n > 1) {         // hv:1095-1136: relay
                 uint32_t r = select_random(w, w.A, w.act_n, p, w.me, w.me);
@@ -1736,17 +1684,16 @@ DEV void body_lite(Wv& w, const NodeIn& x) {
                 STAMP(w, 4);
             } else {                                     // the walk ends here
                 uint32_t RESP = 0;
-                uint32_t nr = sublist(w, w.P & PID_MASK, w.pas_n, nex, RESP, 0);
+                uint32_t nr = sublist(w, w.P, w.pas_n, nex, RESP, 0);
                 STAMP(w, 5);
                 hv_send(w, p, PSIM_MSG_SHUFFLE_REPLY, 0, 0, 0, RESP, nr);
                 STAMP(w, 6);
-                merge_lite(w, ex, nex);
+                merge_exchange(w, ex, nex);
                 STAMP(w, 7);
             }
         }
     }
     STAMP(w, 2);
-    w.P &= PID_MASK;                                  // (the ids again)
     if (x.tf & DESC_SHUFFLE) {                        // hv:572-607
         uint32_t EX;
         uint32_t nex = build_exchange(w, EX);
