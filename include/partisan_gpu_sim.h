@@ -429,6 +429,36 @@ int psim_get_msg_slots(psim_handle *h, uint32_t *ids, uint32_t *roots, size_t ca
  * hosts and tests can read the same metric. */
 uint32_t psim_xbot_latency(uint64_t seed, uint32_t a, uint32_t b);
 
+/* Wire format of a partisan peer connection, for mixed
+ * clusters of real and simulated nodes: a frame is {packet, 4} -- a 4-byte
+ * big-endian length (peer_service_client.erl:214) -- around term_to_binary/1
+ * of the message (client:253-257, peer_service_server.erl:172-182).  A
+ * record is the engine's 64-B message record (words: dst, src,
+ * type | ttl << 8 | nex << 16, seq, a0, a1, a2, a3, ex[0..8)); its term is
+ * the one the reference's handler sends (HyParView hv:506-1131, Plumtree as
+ * {forward_message, partisan_plumtree_broadcast, Msg} hv:441-460 with the
+ * backend's heartbeat ids {RootName, Counter}, X-BOT xbot:1171-1314; the
+ * table is in partisan_amd/csrc/psim_wire.cpp).  Node id i is the node_spec
+ * #{name => '<prefix><i>@<host>', listen_addrs => [#{ip => ip_base + i,
+ * port => port}], channels => [undefined], parallelism => 1}
+ * (partisan_peer_service_manager.erl:71-76). */
+typedef struct psim_wire_names {
+    const char *prefix;          /* node name prefix, e.g. "n" */
+    const char *host;            /* node name host part, e.g. "127.0.0.1" */
+    uint32_t ip_base;            /* IPv4 of node 0 (host order); node i has ip_base + i */
+    uint32_t port;               /* listen port (PEER_PORT 9090, partisan.hrl:3) */
+} psim_wire_names;
+/* One record to one frame (*len bytes).  With buf == NULL or cap < *len only
+ * *len is set.  PSIM_EINVAL for a record no handler sends (an IHAVE of a
+ * retired id: no root). */
+int psim_wire_encode(const uint32_t rec[16], const psim_wire_names *names, uint8_t *buf, size_t cap, size_t *len);
+/* The first frame of buf back to a record (dst = the connection's peer,
+ * passed in; seq = 0: the order of a connection is its sequence); *used =
+ * the frame's bytes.  PSIM_ERANGE: buf holds no complete frame yet;
+ * PSIM_EINVAL: not one of the messages above. */
+int psim_wire_decode(const uint8_t *buf, size_t len, const psim_wire_names *names, uint32_t dst, uint32_t rec[16],
+                     size_t *used);
+
 /* Per-kernel device time (ms) accumulated over the last psim_step call:
  * names[i] is a static string; returns the number of entries. */
 int psim_kernel_times(psim_handle *h, const char **names, double *ms, uint64_t *launches, int cap);
