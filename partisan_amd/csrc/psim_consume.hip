@@ -1729,17 +1729,21 @@ DEV void writeback_lite(Wv& w) {
 #ifndef PSIM_LITE_WAVES
 #define PSIM_LITE_WAVES 6
 #endif
-__global__ void __launch_bounds__(256, PSIM_LITE_WAVES) k_consume_lite(RoundArgs args) {
+#ifndef PSIM_LITE_WPB
+#define PSIM_LITE_WPB 4
+#endif
+constexpr uint32_t LITE_WPB = PSIM_LITE_WPB;        // waves per k_consume_lite block
+__global__ void __launch_bounds__(64 * PSIM_LITE_WPB, PSIM_LITE_WAVES) k_consume_lite(RoundArgs args) {
     if (*kargs().ctl) return;                         // an aborted batch (run_batch)
     __shared__ uint64_t sst[NST];
-    __shared__ uint32_t scratch[WAVES_PER_BLOCK][64];
-    __shared__ __attribute__((aligned(16))) uint32_t srecs[WAVES_PER_BLOCK][STAGE * 16];
-    __shared__ uint32_t skeys[WAVES_PER_BLOCK][STAGE];
+    __shared__ uint32_t scratch[LITE_WPB][64];
+    __shared__ __attribute__((aligned(16))) uint32_t srecs[LITE_WPB][STAGE * 16];
+    __shared__ uint32_t skeys[LITE_WPB][STAGE];
     for (int i = threadIdx.x; i < NST; i += blockDim.x) sst[i] = 0;
     __syncthreads();
     const uint32_t wid = threadIdx.x >> 6;
-    const uint32_t gw = uni(blockIdx.x * WAVES_PER_BLOCK + wid);
-    const uint32_t nw = gridDim.x * WAVES_PER_BLOCK;
+    const uint32_t gw = uni(blockIdx.x * LITE_WPB + wid);
+    const uint32_t nw = gridDim.x * LITE_WPB;
     Wv w;
     w.a = &args;
     w.lds = scratch[wid];
@@ -1748,7 +1752,7 @@ __global__ void __launch_bounds__(256, PSIM_LITE_WAVES) k_consume_lite(RoundArgs
     w.skey = skeys[wid];
     w.slots = nullptr;
 #ifdef PSIM_STAMPS
-    __shared__ uint64_t stamps[WAVES_PER_BLOCK][32];
+    __shared__ uint64_t stamps[LITE_WPB][32];
     if ((threadIdx.x & 63) < 32) stamps[wid][threadIdx.x & 63] = 0;
     w.stl = stamps[wid];
     w.t_last = __builtin_amdgcn_s_memtime();
@@ -2887,7 +2891,8 @@ static uint32_t resident_grid(const void* k, int block = WAVES_PER_BLOCK * 64) {
     return (uint32_t)nb * (uint32_t)p.multiProcessorCount;
 }
 uint32_t consume_grid() { return resident_grid((const void*)k_consume); }
-uint32_t lite_grid() { return resident_grid((const void*)k_consume_lite); }
+uint32_t lite_grid() { return resident_grid((const void*)k_consume_lite, 64 * LITE_WPB); }
+uint32_t lite_block() { return 64 * LITE_WPB; }
 uint32_t pt_grid() { return resident_grid((const void*)k_pt); }
 uint32_t ptl_grid() { return resident_grid((const void*)k_ptl, PTL_BLK); }
 

@@ -1498,7 +1498,7 @@ int phase_events_prepare(psim_handle* h, Shard* s, const RoundCtl& ctl, RoundArg
         s->rgrid = hv ? std::min<uint32_t>(grid_for(n), RELAY_MAX_BLOCKS) : 0;
         s->tgrid = hv && h->cfg.plumtree ? std::min<uint32_t>(grid_for(n), h->pt_blocks) : 0;
         s->sgrid = hv ? std::min<uint32_t>(grid_for(n), SHUF_MAX_BLOCKS) : 0;
-        s->lgrid = hv ? std::min<uint32_t>(grid_for(n), h->lite_blocks) : 0;
+        s->lgrid = hv ? std::min<uint32_t>((uint32_t)((n + psim::lite_block() - 1) / psim::lite_block()), h->lite_blocks) : 0;
         s->qgrid = hv && h->cfg.plumtree ? std::min<uint32_t>((n + PTL_BLOCK - 1) / PTL_BLOCK, h->ptl_blocks) : 0;
         TRY(s->stat_part.ensure((size_t)(s->pgrid + s->cgrid + s->rgrid + s->tgrid + s->sgrid + s->lgrid + s->qgrid) *
                                 NST));
@@ -1606,7 +1606,7 @@ int phase_consume(psim_handle* h, Shard* s, RoundArgs& a) {
         k_mark<<<1, 64, 0, s->stream>>>(a.ktime, 0, s->ctl.p);
         k_relay<<<s->rgrid, BLK, 0, s->stream>>>(a);
         k_shuf<<<s->sgrid, BLK, 0, s->stream>>>(a);
-        k_consume_lite<<<s->lgrid, BLK, 0, s->stream>>>(a);
+        k_consume_lite<<<s->lgrid, psim::lite_block(), 0, s->stream>>>(a);
         RoundArgs b = a;
         b.desc = s->desc_slow.p;
         b.n_alist = s->n_slow.p;
@@ -2286,6 +2286,10 @@ int psim_create(const psim_config* cfg, psim_handle** out) {
     h->consume_blocks = psim::consume_grid();
     h->pt_blocks = psim::pt_grid();
     h->lite_blocks = psim::lite_grid();
+    if (const char* e = getenv("PSIM_LITE_GRID")) {     // (another k_consume_lite grid, for measurements)
+        const long v = strtol(e, nullptr, 10);
+        if (v > 0) h->lite_blocks = (uint32_t)v;
+    }
 
     h->ptl_blocks = psim::ptl_grid();
     if (const char* e = getenv("PSIM_PTL_GRID")) {      // (a smaller k_ptl grid, for measurements)

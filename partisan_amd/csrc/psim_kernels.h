@@ -126,6 +126,7 @@ int debug_stamps(unsigned long long* out);
 // resident-block count of k_consume on the current device
 uint32_t consume_grid();
 uint32_t lite_grid();
+uint32_t lite_block();
 uint32_t pt_grid();
 uint32_t ptl_grid();
 
