@@ -2285,16 +2285,28 @@ int psim_create(const psim_config* cfg, psim_handle** out) {
     if (hipSetDevice(dev) != hipSuccess) { delete h; return PSIM_EDEVICE; }
     h->consume_blocks = psim::consume_grid();
     h->pt_blocks = psim::pt_grid();
-    h->lite_blocks = psim::lite_grid();
+    if (const char* e = getenv("PSIM_PT_GRID")) {       // (another k_pt grid, for measurements)
+        const long v = strtol(e, nullptr, 10);
+        if (v > 0) h->pt_blocks = (uint32_t)v;
+    }
+    if (const char* e = getenv("PSIM_CONSUME_GRID")) {  // (another k_consume grid, for measurements)
+        const long v = strtol(e, nullptr, 10);
+        if (v > 0) h->consume_blocks = (uint32_t)v;
+    }
+    // four times the resident blocks: the dispatcher hands freed slots new
+    // blocks, which evens out the waves' uneven node mixes (the resident grid
+    // left 4.1 of 6 waves/SIMD busy on average; 300 -> 272 us a round on the
+    // survey line, profiles/r03/p10)
+    h->lite_blocks = 4 * psim::lite_grid();
     if (const char* e = getenv("PSIM_LITE_GRID")) {     // (another k_consume_lite grid, for measurements)
         const long v = strtol(e, nullptr, 10);
         if (v > 0) h->lite_blocks = (uint32_t)v;
     }
 
     h->ptl_blocks = psim::ptl_grid();
-    if (const char* e = getenv("PSIM_PTL_GRID")) {      // (a smaller k_ptl grid, for measurements)
+    if (const char* e = getenv("PSIM_PTL_GRID")) {      // (another k_ptl grid, for measurements)
         const long v = strtol(e, nullptr, 10);
-        if (v > 0 && (uint32_t)v < h->ptl_blocks) h->ptl_blocks = (uint32_t)v;
+        if (v > 0) h->ptl_blocks = (uint32_t)v;
     }
     {
         const char* e = getenv("PSIM_PHASE_TIMERS");

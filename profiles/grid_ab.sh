@@ -1,6 +1,35 @@
-O=gpurun_out/ab_grid; mkdir -p $O
-for rep in 1 2; do for g in 0 2048 1792 1536 1280; do
-  if [ $g = 0 ]; then E=""; else E="PSIM_PTL_GRID=$g"; fi
-  env $E timeout -k 10 200 python bench.py --no-cpu-baseline --no-check --steps 20 --warmup 5 > $O/b_${g}_$rep.json 2> $O/b_${g}_$rep.err || { echo FAIL $g; exit 1; }
-  python -c "import json; d=json.load(open('$O/b_${g}_$rep.json')); print('grid $g', $rep, 'ms/step %.3f node-round %.3f' % (d['ms_per_step'], d['roofline']['avg_launch_ms']))"
-done; done
+#!/bin/bash
+# Grids (and library variants) of the node-round kernels on the driver's bench
+# command (survey schedule, --steps 20 --warmup 5): per entry the bench line
+# and, from a kernel trace, each node-round kernel's average time.
+# Usage (repo root): bash profiles/grid_ab.sh TAG ENTRY ...
+#   ENTRY = VARIANT[:NAME=VALUE[,NAME=VALUE...]], VARIANT "base" =
+#   libpartisan_gpu_sim.so, NAME e.g. PSIM_LITE_GRID, PSIM_PTL_GRID,
+#   PSIM_PT_GRID, PSIM_CONSUME_GRID
+set -o pipefail
+TAG=$1; shift
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+O=$R/gpurun_out/$TAG
+mkdir -p $O
+cd /tmp && export TMPDIR=/tmp
+k=0
+for e in "$@"; do
+  k=$((k + 1))
+  v=${e%%:*}; envs=""
+  [ "$e" != "$v" ] && envs=${e#*:}
+  if [ "$v" = base ]; then L=""; else L=$v; fi
+  ( export PSIM_LIB=$L; IFS=','; for kv in $envs; do export "$kv"; done
+    timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $O/t$k -o run --output-format csv -- \
+      python3 $R/bench.py --no-cpu-baseline --no-check --steps 20 --warmup 5 > $O/bench_$k.json 2> $O/bench_$k.err ) \
+    || { echo "BENCH FAILED $e"; tail -5 $O/bench_$k.err; exit 1; }
+  S=$(find $O/t$k -name "*kernel_stats.csv" | head -1)
+  python3 -c "
+import csv, json
+d = json.load(open('$O/bench_$k.json'))
+ks = {r['Name']: float(r['AverageNs']) / 1e3 for r in csv.DictReader(open('$S'))}
+pick = lambda s: next((round(v, 1) for n, v in ks.items() if s in n), None)
+print('$e', round(d['ms_per_step'], 3), 'ms/step phase', round(d['roofline']['avg_launch_ms'], 3),
+      'lite', pick('k_consume_lite'), 'ptl', pick('k_ptl('), 'pt', pick('k_pt('), 'relay', pick('k_relay'), 'cons', pick('k_consume('))"
+  rm -rf $O/t$k
+done
+echo AB DONE
