@@ -2283,31 +2283,24 @@ int psim_create(const psim_config* cfg, psim_handle** out) {
     int dev = cfg->device;
     if (dev < 0 && hipGetDevice(&dev) != hipSuccess) { delete h; return PSIM_EDEVICE; }
     if (hipSetDevice(dev) != hipSuccess) { delete h; return PSIM_EDEVICE; }
-    h->consume_blocks = psim::consume_grid();
-    h->pt_blocks = psim::pt_grid();
-    if (const char* e = getenv("PSIM_PT_GRID")) {       // (another k_pt grid, for measurements)
-        const long v = strtol(e, nullptr, 10);
-        if (v > 0) h->pt_blocks = (uint32_t)v;
-    }
-    if (const char* e = getenv("PSIM_CONSUME_GRID")) {  // (another k_consume grid, for measurements)
-        const long v = strtol(e, nullptr, 10);
-        if (v > 0) h->consume_blocks = (uint32_t)v;
-    }
-    // four times the resident blocks: the dispatcher hands freed slots new
-    // blocks, which evens out the waves' uneven node mixes (the resident grid
-    // left 4.1 of 6 waves/SIMD busy on average; 300 -> 272 us a round on the
-    // survey line, profiles/r03/p10)
-    h->lite_blocks = 4 * psim::lite_grid();
-    if (const char* e = getenv("PSIM_LITE_GRID")) {     // (another k_consume_lite grid, for measurements)
-        const long v = strtol(e, nullptr, 10);
-        if (v > 0) h->lite_blocks = (uint32_t)v;
-    }
-
-    h->ptl_blocks = psim::ptl_grid();
-    if (const char* e = getenv("PSIM_PTL_GRID")) {      // (another k_ptl grid, for measurements)
-        const long v = strtol(e, nullptr, 10);
-        if (v > 0) h->ptl_blocks = (uint32_t)v;
-    }
+    // grids: PSIM_<KERNEL>_GRID=N (blocks) or =xK (K times the resident grid)
+    // override them for measurements (profiles/grid_ab.sh)
+    auto grid = [](const char* env, uint32_t resident, uint32_t dflt) -> uint32_t {
+        const char* e = getenv(env);
+        if (!e) return dflt;
+        const bool mul = e[0] == 'x';
+        const long v = strtol(e + (mul ? 1 : 0), nullptr, 10);
+        if (v <= 0) return dflt;
+        return mul ? (uint32_t)v * resident : (uint32_t)v;
+    };
+    h->consume_blocks = grid("PSIM_CONSUME_GRID", psim::consume_grid(), psim::consume_grid());
+    h->pt_blocks = grid("PSIM_PT_GRID", psim::pt_grid(), psim::pt_grid());
+    // k_consume_lite: four times the resident blocks -- the dispatcher hands
+    // freed slots new blocks, which evens out the waves' uneven node mixes (the
+    // resident grid left 4.1 of 6 waves/SIMD busy on average; 300 -> 272 us a
+    // round on the survey line, profiles/r03/p10)
+    h->lite_blocks = grid("PSIM_LITE_GRID", psim::lite_grid(), 4 * psim::lite_grid());
+    h->ptl_blocks = grid("PSIM_PTL_GRID", psim::ptl_grid(), psim::ptl_grid());
     {
         const char* e = getenv("PSIM_PHASE_TIMERS");
         h->phase_timers = e && *e && *e != '0';

@@ -5,7 +5,8 @@
 # Usage (repo root): bash profiles/grid_ab.sh TAG ENTRY ...
 #   ENTRY = VARIANT[:NAME=VALUE[,NAME=VALUE...]], VARIANT "base" =
 #   libpartisan_gpu_sim.so, NAME e.g. PSIM_LITE_GRID, PSIM_PTL_GRID,
-#   PSIM_PT_GRID, PSIM_CONSUME_GRID
+#   PSIM_PT_GRID, PSIM_CONSUME_GRID;
+#   VALUE = blocks, or xK = K times the resident grid
 set -o pipefail
 TAG=$1; shift
 R=${GRAFT_REPO_ROOT:-$(pwd)}
