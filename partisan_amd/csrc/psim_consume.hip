@@ -2147,11 +2147,11 @@ __global__ void __launch_bounds__(256, PSIM_RELAY_WAVES) k_relay(RoundArgs) {
 #pragma unroll
                     for (int k = 0; k < PSIM_CONN_CAP; k++) down |= (uint32_t)k < h.conn_n && cv[k] == (av[j] | PSIM_CONN_DOWN);
                     exits |= (uint32_t)j < h.act_n && av[j] != id && av[j] < a.n_nodes && !down &&
-                             (a.flags[av[j]] & F_CRASHED);
+                             crashed_now(a, av[j]);
                 }
 #pragma unroll
                 for (int k = 0; k < PSIM_CONN_CAP; k++)
-                    exits |= (uint32_t)k < h.conn_n && !(cv[k] & PSIM_CONN_DOWN) && (a.flags[cv[k] & KEY_DST_MASK] & F_CRASHED);
+                    exits |= (uint32_t)k < h.conn_n && !(cv[k] & PSIM_CONN_DOWN) && crashed_now(a, cv[k] & KEY_DST_MASK);
             }
             // an active member without a connection (conn_dn): the next send
             // to it reconnects (maybe_connect) -- the connection table's path

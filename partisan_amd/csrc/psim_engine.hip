@@ -75,12 +75,16 @@ constexpr uint32_t BATCH_MAX = 64;
     } while (0)
 
 // ------------------------------------------------------------ kernels --
-__global__ void k_crash(uint8_t* flags, const uint32_t* ids, uint32_t n) {
+__global__ void k_crash(uint8_t* flags, uint32_t* crash_bits, const uint32_t* ids, uint32_t n) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     uint32_t id = ids[i];
     uint8_t f = flags[id];
-    if (f & F_UP) flags[id] = (uint8_t)((f & ~F_UP) | F_CRASHED);
+    if (f & F_UP) {
+        flags[id] = (uint8_t)((f & ~F_UP) | F_CRASHED);
+        const uint32_t g = id >> CRASH_GRAIN_SHIFT;
+        atomicOr(crash_bits + (g >> 5), 1u << (g & 31));
+    }
 }
 
 // leave/1 calls of this round (pluggable): Hdr pad1[0] = target + 1 at
@@ -93,10 +97,11 @@ __global__ void k_leave_set(Hdr* hdr, uint32_t lo, uint32_t n_local, const uint3
     if (id >= lo && id < lo + n_local) hdr[id - lo].pad1[0] = targets[i] + 1;
 }
 
-__global__ void k_uncrash(uint8_t* flags, const uint32_t* ids, uint32_t n, const uint32_t* ctl) {
+__global__ void k_uncrash(uint8_t* flags, uint32_t* crash_bits, const uint32_t* ids, uint32_t n, const uint32_t* ctl) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n || *ctl) return;
     flags[ids[i]] &= (uint8_t)~F_CRASHED;
+    crash_bits[ids[i] >> (CRASH_GRAIN_SHIFT + 5)] = 0;   // (every bit of the word is this round's)
 }
 
 // node start: init/1 of the manager (hv:289-354) and of the broadcast
@@ -702,7 +707,7 @@ __global__ void __launch_bounds__(256) k_node_prep(RoundArgs a, const unsigned l
 #pragma unroll
                     for (int k = 0; k < PSIM_ACTIVE_CAP; k++)
                         if ((uint32_t)k < x.act_n && av[k] < a.n_nodes && av[k] != a.lo + i &&
-                            (a.flags[av[k]] & F_CRASHED)) {
+                            crashed_now(a, av[k])) {
                             b++;
                             bool down = false;
 #pragma unroll
@@ -711,7 +716,7 @@ __global__ void __launch_bounds__(256) k_node_prep(RoundArgs a, const unsigned l
                         }
 #pragma unroll
                     for (int j = 0; j < PSIM_CONN_CAP; j++)
-                        exits |= (uint32_t)j < cn && !(cv[j] & PSIM_CONN_DOWN) && (a.flags[cv[j] & KEY_DST_MASK] & F_CRASHED);
+                        exits |= (uint32_t)j < cn && !(cv[j] & PSIM_CONN_DOWN) && crashed_now(a, cv[j] & KEY_DST_MASK);
                 }
                 w = c > 0 || st == r || exits || (f & F_LAZY) || origin ||
                     (a.random_promotion && (f & F_LOWACT) && due(a.promotion_period, r, st)) ||
@@ -1117,6 +1122,7 @@ struct Shard {
     hipStream_t stream = nullptr;
     // replicated (global id)
     DBuf<uint8_t> flags, part;
+    DBuf<uint32_t> crash_bits;   // RoundArgs::crash_bits
     // local rows
     DBuf<Hdr> hdr;
     DBuf<uint32_t> act, pas, pt_all, pt_com, pt_eag, pt_laz, pt_rt, start;
@@ -1245,7 +1251,7 @@ RoundArgs make_args(psim_handle* h, Shard* s) {
     a.tracked_msg = h->tracked_msg;
     a.origin = s->origin.p;
     a.slots = s->slots.p;
-    a.flags = s->flags.p; a.part = s->part.p; a.hdr = s->hdr.p;
+    a.flags = s->flags.p; a.part = s->part.p; a.hdr = s->hdr.p; a.crash_bits = s->crash_bits.p;
     a.act = s->act.p; a.pas = s->pas.p; a.sentm = s->sentm.p; a.recvm = s->recvm.p;
     a.mapx = s->mapx.p; a.mapx_top = s->mapx_top.p;
     a.mapx_rows = (uint32_t)(s->mapx.n / IDMAP_EXT);
@@ -1455,7 +1461,7 @@ int phase_events_prepare(psim_handle* h, Shard* s, const RoundCtl& ctl, RoundArg
         if (ctl.crashes) {
             TRY(upload(s, s->ev_ids, h->pend_crash));
             k_crash<<<grid_for(h->pend_crash.size()), BLK, 0, s->stream>>>(
-                s->flags.p, s->ev_ids.p, (uint32_t)h->pend_crash.size());
+                s->flags.p, s->crash_bits.p, s->ev_ids.p, (uint32_t)h->pend_crash.size());
         }
         if (!h->pend_join.empty()) {
             TRY(upload(s, s->ev_ids, h->pend_join));
@@ -1811,7 +1817,7 @@ int phase_stats(psim_handle* h, Shard* s, const std::vector<uint32_t>& crashed) 
     k_stats_final<<<1, BLK, 0, s->stream>>>(s->stat_tile.p, nt, s->stat_out.p, s->pin_dev + (size_t)s->stat_slot * PIN_STRIDE);
     if (!crashed.empty()) {
         TRY(upload(s, s->ev_ids, crashed));
-        k_uncrash<<<grid_for(crashed.size()), BLK, 0, s->stream>>>(s->flags.p, s->ev_ids.p,
+        k_uncrash<<<grid_for(crashed.size()), BLK, 0, s->stream>>>(s->flags.p, s->crash_bits.p, s->ev_ids.p,
                                                                   (uint32_t)crashed.size(), s->ctl.p);
     }
     return PSIM_OK;
@@ -2127,6 +2133,7 @@ int shard_alloc(psim_handle* h, Shard* s) {
     const size_t N = h->N, n = std::max<uint32_t>(s->n, 1);
     int rc = 0;
     rc |= s->flags.alloc(N); rc |= s->part.alloc(N); rc |= s->hdr.alloc(n);
+    rc |= s->crash_bits.alloc((N >> (CRASH_GRAIN_SHIFT + 5)) + 1);
     rc |= s->act.alloc(n * PSIM_ACTIVE_CAP); rc |= s->pas.alloc(n * PSIM_PASSIVE_CAP);
     rc |= s->sentm.alloc(n * IDMAP_IN); rc |= s->recvm.alloc(n * IDMAP_IN);
     if (h->cfg.manager != PSIM_MANAGER_PLUGGABLE) {
@@ -2179,7 +2186,7 @@ int shard_alloc(psim_handle* h, Shard* s) {
 
 void shard_free(Shard* s) {
     if (s->stream) (void)hipStreamSynchronize(s->stream);
-    s->flags.release(); s->part.release(); s->hdr.release();
+    s->flags.release(); s->part.release(); s->hdr.release(); s->crash_bits.release();
     s->act.release(); s->pas.release(); s->sentm.release(); s->recvm.release();
     s->pt_all.release(); s->pt_com.release();
     s->mapx.release(); s->mapx_top.release();
