@@ -221,7 +221,11 @@ __global__ void k_origin(uint32_t* origin, uint32_t lo, uint32_t n_local, const 
 // source index makes the inbox deterministic.
 constexpr uint32_t RUN_SHORT = 16;
 constexpr uint32_t RUN_LDS = 2048;
-constexpr uint32_t RB_STEP = 256;          // source nodes (or dense records) per block step
+#ifndef PSIM_RB_STEP
+#define PSIM_RB_STEP 256
+#endif
+constexpr uint32_t RB_STEP = PSIM_RB_STEP;  // source nodes (or dense records) per block step = the block
+constexpr uint32_t RB_WAVES = RB_STEP / 64;
 constexpr uint32_t RB_MAX_BLOCKS = 1024;   // blocks of the two passes over the sources
 constexpr uint32_t RR_THREADS = 512;       // k_bucket_route block
 
@@ -285,8 +289,8 @@ __global__ void __launch_bounds__(RB_STEP) k_bucket_hist(RouteIn in, uint32_t ns
                                                          unsigned long long* btot, const uint32_t* ctl) {
     if (*ctl) return;                                 // an aborted batch (run_batch)
     extern __shared__ uint32_t hcnt[];                // nb bucket counters
-    __shared__ uint32_t spre[4][65];
-    __shared__ uint64_t sbase[4][64];
+    __shared__ uint32_t spre[RB_WAVES][65];
+    __shared__ uint64_t sbase[RB_WAVES][64];
     for (uint32_t j = threadIdx.x; j < nb; j += blockDim.x) hcnt[j] = 0;
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         *n_long = 0;
@@ -317,16 +321,16 @@ __global__ void __launch_bounds__(RB_STEP) k_bucket_scatter(RouteIn in, uint32_t
         }
         return;
     }
-    __shared__ uint32_t spre[4][65];
-    __shared__ uint64_t sbase[4][64];
-    for (uint32_t j = threadIdx.x; j < nb; j += blockDim.x) hcnt[j] = 0;
+    __shared__ uint32_t spre[RB_WAVES][65];
+    __shared__ uint64_t sbase[RB_WAVES][64];
+    // each bucket's counter starts at this block's place in it: the returned
+    // count is the pair's position (no per-record read of the offset matrix)
+    for (uint32_t j = threadIdx.x; j < nb; j += blockDim.x) hcnt[j] = off[(size_t)j * gridDim.x + blockIdx.x];
     __syncthreads();
     const uint32_t wmask = (1u << wshift) - 1;
     for (uint32_t step = blockIdx.x; step < nsteps; step += gridDim.x)
         route_step<DENSE>(in, step, spre, sbase, [&](uint32_t g, uint32_t d, uint32_t cls) {
-            const uint32_t b = d >> wshift;
-            const uint32_t r = atomicAdd(&hcnt[b], 1u);
-            pairs[off[(size_t)b * gridDim.x + blockIdx.x] + r] = make_uint2((d & wmask) | (cls << 16), g);
+            pairs[atomicAdd(&hcnt[d >> wshift], 1u)] = make_uint2((d & wmask) | (cls << 16), g);
         });
 }
 
@@ -348,9 +352,9 @@ template <bool WRITE>
 __global__ void __launch_bounds__(RB_STEP) k_owner_part(RouteIn in, uint32_t nsteps, uint32_t spb, uint32_t G,
                                                         uint32_t per, uint32_t* hist,
                                                         const uint32_t* __restrict__ off, Msg* __restrict__ out) {
-    __shared__ uint32_t spre[4][65];
-    __shared__ uint64_t sbase[4][64];
-    __shared__ uint32_t wc[4][64];                    // per wave and owner: records in this step
+    __shared__ uint32_t spre[RB_WAVES][65];
+    __shared__ uint64_t sbase[RB_WAVES][64];
+    __shared__ uint32_t wc[RB_WAVES][64];             // per wave and owner: records in this step
     __shared__ uint32_t run[64];                      // per owner: the block's next position
     const uint32_t w = threadIdx.x >> 6, l = threadIdx.x & 63, nblk = gridDim.x;
     if (threadIdx.x < 64) run[threadIdx.x] = (WRITE && threadIdx.x < G) ? off[threadIdx.x * nblk + blockIdx.x] : 0u;
@@ -421,8 +425,8 @@ __global__ void __launch_bounds__(RB_STEP) k_owner_part(RouteIn in, uint32_t nst
             }
         }
         __syncthreads();
-        if (threadIdx.x < G) run[threadIdx.x] += wc[0][threadIdx.x] + wc[1][threadIdx.x] + wc[2][threadIdx.x] +
-                                                 wc[3][threadIdx.x];
+        if (threadIdx.x < G)
+            for (uint32_t v = 0; v < RB_WAVES; v++) run[threadIdx.x] += wc[v][threadIdx.x];
     }
     if (!WRITE) {
         __syncthreads();
