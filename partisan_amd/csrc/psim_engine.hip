@@ -1157,6 +1157,9 @@ struct Shard {
     DBuf<uint4> desc, desc_slow, desc_pt, desc_shuf, desc_lite, desc_ptl;   // work descriptors; those k_relay leaves to k_consume / k_pt / k_shuf
     DBuf<uint64_t> bound, pscan, obase, stat_part, stat_out, stat_tile, d_off;   // bound: packed (bound << 32 | work)
     DBuf<uint8_t> cub_tmp;              // the scan's tile totals
+    DBuf<uint32_t> scan_stat;           // single-pass scan: [0] ticket counter, then a status per tile
+    DBuf<uint64_t> scan_val;            //   and two values per tile (k_scan_lb)
+    uint32_t scan_tick = 0, scan_epoch = 0;
     DBuf<uint32_t> ev_ids, ev_contacts, stop_ids, n_stop;
     bool tomb_live = false;             // full: snapshots carry their remove rows
     DBuf<Msg> sendbuf;
@@ -1388,11 +1391,105 @@ __global__ void __launch_bounds__(BLK) k_scan_apply(const T* __restrict__ in, T*
     }
 }
 
+// Single pass (decoupled look-back): a block takes the next tile through a
+// ticket counter (tiles start in launch order, so a block only ever waits on
+// tiles of blocks already running), publishes the tile total, then finds its
+// prefix by summing its predecessors' published values a wave at a time,
+// back to the nearest inclusive prefix, and publishes that.  stat[t] =
+// epoch << 2 | 1 (the total is in val[2t]) or | 2 (the inclusive prefix is
+// in val[2t + 1]); a status of another epoch (an earlier scan) reads as not
+// yet published.  One launch and one read of the input where the
+// reduce-then-scan took three launches (~5 us each at 2^20 nodes).
+template <typename T>
+__global__ void __launch_bounds__(BLK) k_scan_lb(const T* __restrict__ in, T* __restrict__ out, uint32_t n,
+                                                 uint32_t* tick, uint32_t base, uint32_t* stat, T* val,
+                                                 uint32_t epoch) {
+    __shared__ uint32_t s_tile;
+    __shared__ T s_pre;
+    if (threadIdx.x == 0) s_tile = atomicAdd(tick, 1u) - base;
+    __syncthreads();
+    const uint32_t t = s_tile;
+    const size_t b0 = (size_t)t * SCAN_TILE + (size_t)threadIdx.x * SCAN_ITEMS;
+    T x[SCAN_ITEMS], v = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < SCAN_ITEMS; k++) {
+        x[k] = b0 + k < n ? in[b0 + k] : T(0);
+        v += x[k];
+    }
+    T tot;
+    T run = block_excl(v, &tot);
+    if (threadIdx.x < 64) {
+        const uint32_t l = threadIdx.x;
+        if (l == 0) {
+            __hip_atomic_store(&val[2 * t + (t == 0)], tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&stat[t], epoch << 2 | (t == 0 ? 2u : 1u), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        T pre = 0;
+        for (uint32_t hi = t; hi > 0;) {                // lane l: tile hi - 1 - l
+            const int64_t j = (int64_t)hi - 1 - (int64_t)l;
+            uint32_t st = 2;                            // (before tile 0: an inclusive 0)
+            if (j >= 0) {
+                st = __hip_atomic_load(&stat[j], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+                st = (st >> 2) == epoch ? (st & 3u) : 0u;
+            }
+            const uint64_t inc = __ballot(st == 2), ready = __ballot(st != 0);
+            const uint32_t lim = inc ? (uint32_t)__ffsll((long long)inc) - 1 : 63;   // lanes 0..lim count
+            const uint64_t need = lim == 63 ? ~0ull : ((2ull << lim) - 1);
+            if ((ready & need) != need) {               // a predecessor has not published yet
+                __builtin_amdgcn_s_sleep(1);
+                continue;
+            }
+            T vv = 0;
+            if (l <= lim && j >= 0)
+                vv = __hip_atomic_load(&val[2 * j + (st == 2)], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+            for (int d = 32; d > 0; d >>= 1) vv += __shfl_xor(vv, d);
+            pre += vv;
+            if (inc) break;
+            hi = hi > 64 ? hi - 64 : 0;
+        }
+        if (l == 0) {
+            if (t > 0) {
+                __hip_atomic_store(&val[2 * t + 1], pre + tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(&stat[t], epoch << 2 | 2u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            s_pre = pre;
+        }
+    }
+    __syncthreads();
+    run += s_pre;
+#pragma unroll
+    for (uint32_t k = 0; k < SCAN_ITEMS; k++) {
+        if (b0 + k < n) out[b0 + k] = run;
+        run += x[k];
+    }
+}
+
+// the look-back state for nt tiles (zeroed when it grows: no epoch is 0)
+int scan_state(Shard* s, uint32_t nt) {
+    if (s->scan_stat.n >= (size_t)nt + 1 && s->scan_val.n >= 2 * (size_t)nt) return PSIM_OK;
+    HIP_TRY(hipStreamSynchronize(s->stream));
+    TRY(s->scan_stat.ensure((size_t)nt + 1));
+    TRY(s->scan_val.ensure(2 * (size_t)nt));
+    HIP_TRY(hipMemsetAsync(s->scan_stat.p, 0, s->scan_stat.n * sizeof(uint32_t), s->stream));
+    s->scan_tick = 0;
+    return PSIM_OK;
+}
+
 template <typename T>
 int scan_excl(Shard* s, const T* in, T* out, uint32_t n) {
+    static const bool three = getenv("PSIM_SCAN_3PASS") != nullptr;   // (the reduce-then-scan, for A/B)
     const uint32_t nt = (uint32_t)(((uint64_t)n + SCAN_TILE - 1) / SCAN_TILE);
     if (nt <= 1) {
         k_scan_apply<T><<<1, BLK, 0, s->stream>>>(in, out, n, nullptr);
+    } else if (!three) {
+        TRY(scan_state(s, nt));
+        s->scan_epoch = (s->scan_epoch + 1) & 0x3FFFFFFFu;
+        if (!s->scan_epoch) s->scan_epoch = 1;
+        static_assert(sizeof(T) <= sizeof(uint64_t), "scan values are at most 64 bits");
+        k_scan_lb<T><<<nt, BLK, 0, s->stream>>>(in, out, n, s->scan_stat.p, s->scan_tick, s->scan_stat.p + 1,
+                                                reinterpret_cast<T*>(s->scan_val.p), s->scan_epoch);
+        s->scan_tick += nt;
     } else {
         TRY(s->cub_tmp.ensure((size_t)nt * sizeof(T)));
         T* sums = reinterpret_cast<T*>(s->cub_tmp.p);
@@ -2221,7 +2318,7 @@ void shard_free(Shard* s) {
     s->stop_ids.release(); s->n_stop.release();
     s->desc.release(); s->d_nact.release(); s->desc_slow.release(); s->n_slow.release(); s->desc_pt.release(); s->n_pt.release(); s->desc_shuf.release(); s->n_shuf.release(); s->desc_lite.release(); s->n_lite.release(); s->desc_ptl.release(); s->n_ptl.release(); s->bound.release(); s->pscan.release();
     s->obase.release(); s->stat_part.release(); s->stat_out.release(); s->stat_tile.release(); s->d_off.release();
-    s->cub_tmp.release(); s->ev_ids.release(); s->ev_contacts.release(); s->sendbuf.release(); s->ctl.release();
+    s->cub_tmp.release(); s->scan_stat.release(); s->scan_val.release(); s->ev_ids.release(); s->ev_contacts.release(); s->sendbuf.release(); s->ctl.release();
     s->sview.release(); s->sinv.release(); s->fbits.release(); s->pay[0].release(); s->pay[1].release();
     s->pay_top.release();
     if (s->ev_live)
