@@ -1157,8 +1157,8 @@ struct Shard {
     DBuf<uint4> desc, desc_slow, desc_pt, desc_shuf, desc_lite, desc_ptl;   // work descriptors; those k_relay leaves to k_consume / k_pt / k_shuf
     DBuf<uint64_t> bound, pscan, obase, stat_part, stat_out, stat_tile, d_off;   // bound: packed (bound << 32 | work)
     DBuf<uint8_t> cub_tmp;              // the scan's tile totals
-    DBuf<uint32_t> scan_stat;           // single-pass scan: [0] ticket counter, then a status per tile
-    DBuf<uint64_t> scan_val;            //   and two values per tile (k_scan_lb)
+    DBuf<uint32_t> scan_stat;           // single-pass scan (k_scan_lb): [0] the ticket counter, [1] give-ups,
+    DBuf<uint64_t> scan_val;            //   the epoch-tagged words per tile
     uint32_t scan_tick = 0, scan_epoch = 0;
     DBuf<uint32_t> ev_ids, ev_contacts, stop_ids, n_stop;
     bool tomb_live = false;             // full: snapshots carry their remove rows
@@ -1395,15 +1395,43 @@ __global__ void __launch_bounds__(BLK) k_scan_apply(const T* __restrict__ in, T*
 // ticket counter (tiles start in launch order, so a block only ever waits on
 // tiles of blocks already running), publishes the tile total, then finds its
 // prefix by summing its predecessors' published values a wave at a time,
-// back to the nearest inclusive prefix, and publishes that.  stat[t] =
-// epoch << 2 | 1 (the total is in val[2t]) or | 2 (the inclusive prefix is
-// in val[2t + 1]); a status of another epoch (an earlier scan) reads as not
-// yet published.  One launch and one read of the input where the
+// back to the nearest inclusive prefix, and publishes that.  Every published
+// word is self-validating -- 32 bits of the value under the scan's epoch in
+// the high half, stored and loaded as one device-coherent 64-bit word -- so no
+// release/acquire fence is needed (on gfx950 an agent-scope release writes
+// back the whole L2: 60 us a scan, measured).  Slot (t, kind) holds
+// sizeof(T) / 4 words at val[((2 t + kind) * NW + w]; kind 0 = the tile
+// total, 1 = the inclusive prefix; a word of another epoch (an earlier scan)
+// reads as not yet published.  One launch and one read of the input where the
 // reduce-then-scan took three launches (~5 us each at 2^20 nodes).
 template <typename T>
+struct ScanSlot {
+    static constexpr uint32_t NW = sizeof(T) / 4;
+    __device__ static void put(uint64_t* val, uint32_t t, uint32_t kind, T v, uint32_t epoch) {
+#pragma unroll
+        for (uint32_t w = 0; w < NW; w++)
+            __hip_atomic_store(&val[(2 * (size_t)t + kind) * NW + w],
+                               (uint64_t)epoch << 32 | (uint32_t)((uint64_t)v >> (32 * w)), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __device__ static bool get(const uint64_t* val, uint32_t t, uint32_t kind, T& v, uint32_t epoch) {
+        uint64_t x = 0;
+        bool ok = true;
+#pragma unroll
+        for (uint32_t w = 0; w < NW; w++) {
+            const uint64_t y = __hip_atomic_load(&val[(2 * (size_t)t + kind) * NW + w], __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+            ok &= (uint32_t)(y >> 32) == epoch;
+            x |= (uint64_t)(uint32_t)y << (32 * w);
+        }
+        v = (T)x;
+        return ok;
+    }
+};
+
+template <typename T>
 __global__ void __launch_bounds__(BLK) k_scan_lb(const T* __restrict__ in, T* __restrict__ out, uint32_t n,
-                                                 uint32_t* tick, uint32_t base, uint32_t* stat, T* val,
-                                                 uint32_t epoch) {
+                                                 uint32_t* tick, uint32_t base, uint64_t* val, uint32_t epoch) {
     __shared__ uint32_t s_tile;
     __shared__ T s_pre;
     if (threadIdx.x == 0) s_tile = atomicAdd(tick, 1u) - base;
@@ -1420,28 +1448,31 @@ __global__ void __launch_bounds__(BLK) k_scan_lb(const T* __restrict__ in, T* __
     T run = block_excl(v, &tot);
     if (threadIdx.x < 64) {
         const uint32_t l = threadIdx.x;
-        if (l == 0) {
-            __hip_atomic_store(&val[2 * t + (t == 0)], tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&stat[t], epoch << 2 | (t == 0 ? 2u : 1u), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-        }
+        if (l == 0) ScanSlot<T>::put(val, t, t == 0 ? 1u : 0u, tot, epoch);
         T pre = 0;
+        uint32_t spins = 0;
         for (uint32_t hi = t; hi > 0;) {                // lane l: tile hi - 1 - l
             const int64_t j = (int64_t)hi - 1 - (int64_t)l;
             uint32_t st = 2;                            // (before tile 0: an inclusive 0)
+            T vv = 0;
             if (j >= 0) {
-                st = __hip_atomic_load(&stat[j], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-                st = (st >> 2) == epoch ? (st & 3u) : 0u;
+                st = ScanSlot<T>::get(val, (uint32_t)j, 1, vv, epoch) ? 2u
+                   : ScanSlot<T>::get(val, (uint32_t)j, 0, vv, epoch) ? 1u : 0u;
             }
             const uint64_t inc = __ballot(st == 2), ready = __ballot(st != 0);
             const uint32_t lim = inc ? (uint32_t)__ffsll((long long)inc) - 1 : 63;   // lanes 0..lim count
             const uint64_t need = lim == 63 ? ~0ull : ((2ull << lim) - 1);
             if ((ready & need) != need) {               // a predecessor has not published yet
+                // (never past ~1 s: a lost word would hang the device -- give up
+                // loudly instead: tick[1] counts it, the prefix is wrong)
+                if (++spins > (1u << 22)) {
+                    if (l == 0) atomicAdd(tick + 1, 1u);
+                    break;
+                }
                 __builtin_amdgcn_s_sleep(1);
                 continue;
             }
-            T vv = 0;
-            if (l <= lim && j >= 0)
-                vv = __hip_atomic_load(&val[2 * j + (st == 2)], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (l > lim) vv = 0;
 #pragma unroll
             for (int d = 32; d > 0; d >>= 1) vv += __shfl_xor(vv, d);
             pre += vv;
@@ -1449,10 +1480,7 @@ __global__ void __launch_bounds__(BLK) k_scan_lb(const T* __restrict__ in, T* __
             hi = hi > 64 ? hi - 64 : 0;
         }
         if (l == 0) {
-            if (t > 0) {
-                __hip_atomic_store(&val[2 * t + 1], pre + tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(&stat[t], epoch << 2 | 2u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-            }
+            if (t > 0) ScanSlot<T>::put(val, t, 1, pre + tot, epoch);
             s_pre = pre;
         }
     }
@@ -1467,11 +1495,12 @@ __global__ void __launch_bounds__(BLK) k_scan_lb(const T* __restrict__ in, T* __
 
 // the look-back state for nt tiles (zeroed when it grows: no epoch is 0)
 int scan_state(Shard* s, uint32_t nt) {
-    if (s->scan_stat.n >= (size_t)nt + 1 && s->scan_val.n >= 2 * (size_t)nt) return PSIM_OK;
+    if (s->scan_stat.n >= 2 && s->scan_val.n >= 4 * (size_t)nt) return PSIM_OK;
     HIP_TRY(hipStreamSynchronize(s->stream));
-    TRY(s->scan_stat.ensure((size_t)nt + 1));
-    TRY(s->scan_val.ensure(2 * (size_t)nt));
+    TRY(s->scan_stat.ensure(2));
+    TRY(s->scan_val.ensure(4 * (size_t)nt));
     HIP_TRY(hipMemsetAsync(s->scan_stat.p, 0, s->scan_stat.n * sizeof(uint32_t), s->stream));
+    HIP_TRY(hipMemsetAsync(s->scan_val.p, 0, s->scan_val.n * sizeof(uint64_t), s->stream));
     s->scan_tick = 0;
     return PSIM_OK;
 }
@@ -1484,11 +1513,10 @@ int scan_excl(Shard* s, const T* in, T* out, uint32_t n) {
         k_scan_apply<T><<<1, BLK, 0, s->stream>>>(in, out, n, nullptr);
     } else if (!three) {
         TRY(scan_state(s, nt));
-        s->scan_epoch = (s->scan_epoch + 1) & 0x3FFFFFFFu;
-        if (!s->scan_epoch) s->scan_epoch = 1;
-        static_assert(sizeof(T) <= sizeof(uint64_t), "scan values are at most 64 bits");
-        k_scan_lb<T><<<nt, BLK, 0, s->stream>>>(in, out, n, s->scan_stat.p, s->scan_tick, s->scan_stat.p + 1,
-                                                reinterpret_cast<T*>(s->scan_val.p), s->scan_epoch);
+        if (!++s->scan_epoch) s->scan_epoch = 1;        // (0: the zeroed state, never an epoch)
+        static_assert(sizeof(T) == 4 || sizeof(T) == 8, "scan values are 32 or 64 bits");
+        k_scan_lb<T><<<nt, BLK, 0, s->stream>>>(in, out, n, s->scan_stat.p, s->scan_tick, s->scan_val.p,
+                                                s->scan_epoch);
         s->scan_tick += nt;
     } else {
         TRY(s->cub_tmp.ensure((size_t)nt * sizeof(T)));
