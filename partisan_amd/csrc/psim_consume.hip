@@ -1727,7 +1727,7 @@ DEV void writeback_lite(Wv& w) {
 }
 
 #ifndef PSIM_LITE_WAVES
-#define PSIM_LITE_WAVES 6
+#define PSIM_LITE_WAVES 7
 #endif
 #ifndef PSIM_LITE_WPB
 #define PSIM_LITE_WPB 4
