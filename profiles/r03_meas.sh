@@ -18,6 +18,7 @@ gunzip -k $(find $O/steady/trace -name "*kernel_trace.csv.gz" | head -1) 2>/dev/
 F=$(find $O/steady/trace -name "*kernel_trace.csv" | head -1)
 python profiles/per_round.py $F 20 --tail $(python -c "import json,sys; print(json.load(open(sys.argv[1]))['overlay']['rounds_drained'])" $O/steady/bench.json) > $O/steady/per_round.txt
 python profiles/gaps.py $F --steps 20 > $O/steady/gaps.txt
+python profiles/round_kernels.py $F 20 --tail $(python -c "import json,sys; print(json.load(open(sys.argv[1]))['overlay']['rounds_drained'])" $O/steady/bench.json) > $O/steady/round_kernels.txt
 rm -f $F
 tail -1 $O/steady/per_round.txt; head -12 $O/steady/steady.txt
 bash profiles/sq_kernels.sh $TAG/sq --steps 20 --warmup 5 > /dev/null || exit 1
