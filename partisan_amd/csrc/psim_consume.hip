@@ -2597,7 +2597,12 @@ DEV void ptl_ack_out(PtLane& n, uint64_t key) {
 #ifndef PSIM_PTL_BLOCKS_PER_CU
 #define PSIM_PTL_BLOCKS_PER_CU 3
 #endif
-__global__ void __launch_bounds__(PTL_BLK, PSIM_PTL_BLOCKS_PER_CU) k_ptl(RoundArgs) {
+#ifdef PSIM_PTL_WPE      // (a waves-per-SIMD floor for the register allocator, for A/B builds)
+#define PTL_BOUNDS __launch_bounds__(PTL_BLK) __attribute__((amdgpu_waves_per_eu(PSIM_PTL_WPE)))
+#else
+#define PTL_BOUNDS __launch_bounds__(PTL_BLK, PSIM_PTL_BLOCKS_PER_CU)
+#endif
+__global__ void PTL_BOUNDS k_ptl(RoundArgs) {
     if (*kargs().ctl) return;                         // an aborted batch (run_batch)
     enum { T_FIRST, T_FAIL, T_OVF, T_BOUND, T_DLV, T_EMT = T_DLV + 5, T_N = T_EMT + 5 };
     __shared__ unsigned long long sst[T_N + 1];       // (+ the digest)
