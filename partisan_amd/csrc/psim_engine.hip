@@ -222,9 +222,13 @@ __global__ void k_origin(uint32_t* origin, uint32_t lo, uint32_t n_local, const 
 constexpr uint32_t RUN_SHORT = 16;
 constexpr uint32_t RUN_LDS = 2048;
 #ifndef PSIM_RB_STEP
-#define PSIM_RB_STEP 256
+#define PSIM_RB_STEP 1024
 #endif
-constexpr uint32_t RB_STEP = PSIM_RB_STEP;  // source nodes (or dense records) per block step = the block
+// source nodes (or dense records) per block step = the block: 1024 threads
+// keep 16 waves per CU on the two passes' load chains at 2^26 nodes, where the
+// 64 KB LDS histograms (16 K buckets) allow two blocks per CU (k_bucket_hist
+// 2.20 -> 0.85 ms a round, profiles/r03/p16; no change at 2^20)
+constexpr uint32_t RB_STEP = PSIM_RB_STEP;
 constexpr uint32_t RB_WAVES = RB_STEP / 64;
 constexpr uint32_t RB_MAX_BLOCKS = 1024;   // blocks of the two passes over the sources
 constexpr uint32_t RR_THREADS = 512;       // k_bucket_route block
