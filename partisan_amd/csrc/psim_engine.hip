@@ -438,10 +438,13 @@ __global__ void __launch_bounds__(RB_STEP) k_owner_part(RouteIn in, uint32_t nst
     }
 }
 
-// each owner's first send-buffer position (G + 1 entries: the last is the total)
-__global__ void k_owner_offsets(const uint32_t* hoff, uint32_t nblk, uint32_t G, uint64_t* d_off) {
+// each owner's first send-buffer position (G + 1 entries: the last is the
+// total) and, on RCCL ranks, each owner's record count straight into the send
+// half of the count all-to-all (so the round reads both back at once)
+__global__ void k_owner_offsets(const uint32_t* hoff, uint32_t nblk, uint32_t G, uint64_t* d_off, uint64_t* cnt) {
     const uint32_t q = threadIdx.x;
     if (q <= G) d_off[q] = hoff[q * nblk];
+    if (cnt && q < G) cnt[q] = (uint64_t)(hoff[(q + 1) * nblk] - hoff[q * nblk]);
 }
 
 
@@ -1866,6 +1869,8 @@ int phase_partition(psim_handle* h, Shard* s) {
     TRY(s->hoff.ensure(nh));
     TRY(s->sendbuf.ensure(s->pin[PIN_TOTAL] + 1, 2));   // the outbox bound bounds the records
     TRY(s->d_off.ensure(G + 1));
+    const bool rccl = h->world > 1;
+    if (rccl) TRY(h->comm_cnt.ensure(2 * G));
     s->soff.assign(G + 1, 0);
     {
         KTimer t(h, s, KT_SORT);
@@ -1874,8 +1879,11 @@ int phase_partition(psim_handle* h, Shard* s) {
         TRY(scan_excl(s, s->hist.p, s->hoff.p, (uint32_t)nh));
         k_owner_part<true><<<nblk, RB_STEP, 0, s->stream>>>(in, nsteps, spb, G, h->per, nullptr, s->hoff.p,
                                                              s->sendbuf.p);
-        k_owner_offsets<<<1, 128, 0, s->stream>>>(s->hoff.p, nblk, G, s->d_off.p);
+        k_owner_offsets<<<1, 128, 0, s->stream>>>(s->hoff.p, nblk, G, s->d_off.p, rccl ? h->comm_cnt.p : nullptr);
         HIP_TRY(hipGetLastError());
+        // an RCCL rank reads the offsets back with the received counts, after
+        // the count all-to-all (exchange_rccl): one host wait a round, not two
+        if (rccl) return PSIM_OK;
         HIP_TRY(hipMemcpyAsync(s->soff.data(), s->d_off.p, (G + 1) * 8, hipMemcpyDeviceToHost, s->stream));
         TRY(stream_wait(s));
     }
@@ -1926,12 +1934,14 @@ int exchange_rccl(psim_handle* h) {
     uint64_t m = 0;
     {
         KTimer t(h, s, KT_EXCHANGE);
-        TRY(h->comm_cnt.ensure(2 * G));
-        HIP_TRY(hipMemcpyAsync(h->comm_cnt.p, s->scnt.data(), G * 8, hipMemcpyHostToDevice, s->stream));
+        // (k_owner_offsets wrote this rank's counts into comm_cnt[0, G))
         NCCL_TRY(ncclAllToAll(h->comm_cnt.p, h->comm_cnt.p + G, 1, ncclUint64, h->comm, s->stream));
         std::vector<uint64_t> rcnt(G);
         HIP_TRY(hipMemcpyAsync(rcnt.data(), h->comm_cnt.p + G, G * 8, hipMemcpyDeviceToHost, s->stream));
+        HIP_TRY(hipMemcpyAsync(s->soff.data(), s->d_off.p, (G + 1) * 8, hipMemcpyDeviceToHost, s->stream));
         TRY(stream_wait(s));
+        s->scnt.resize(G);
+        for (uint32_t g = 0; g < G; g++) s->scnt[g] = s->soff[g + 1] - s->soff[g];
         std::vector<uint64_t> roff(G);
         for (uint32_t g = 0; g < G; g++) { roff[g] = m; m += rcnt[g]; }
         TRY(s->recvbuf.ensure(m + 1));
