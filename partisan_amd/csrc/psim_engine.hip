@@ -776,6 +776,53 @@ __global__ void __launch_bounds__(256) k_node_prep(RoundArgs a, const unsigned l
     }
 }
 
+// node li's entry of k_desc (li == n_local: the totals), from its prefix P
+// of the packed words and its own packed word pk
+__device__ __forceinline__ void desc_entry(const RoundArgs& a, uint32_t li, uint64_t P, uint64_t pk,
+                                           const uint32_t* __restrict__ in_beg,
+                                           const unsigned long long* __restrict__ cb,
+                                           const uint32_t* __restrict__ start, uint4* __restrict__ desc,
+                                           uint64_t* __restrict__ obase, uint32_t* nact, unsigned long long tot,
+                                           uint64_t* hout, uint64_t cap, uint32_t* ctl) {
+    obase[li] = P >> 32;
+    if (li == a.n_local) {
+        *nact = (uint32_t)P;
+        obase[li] = tot;
+        hout[PIN_TOTAL] = tot;                        // the host's one mid-round read
+        // a batch (cap > 0) checks the outbox here instead: a total past its
+        // capacity stops the rest of the batch (code 1, this round)
+        if (cap && tot + 1 > cap) { ctl[1] = a.round; __threadfence(); ctl[0] = 1; }
+        return;
+    }
+    if (!(pk & 1u)) return;
+    if ((uint32_t)cb[li] > DESC_CNT_MASK) hout[PIN_BIGIN] = 1;   // (the descriptor packs it in 26 bits)
+    const uint32_t st = start[li], r = a.round;
+    const uint32_t tf = (a.random_promotion && due(a.promotion_period, r, st) ? DESC_PROMO : 0u) |
+                        (due(a.shuffle_period, r, st) ? DESC_SHUFFLE : 0u) |
+                        (a.plumtree && due(a.lazy_tick_period, r, st) ? DESC_LAZY : 0u) |
+                        (a.plumtree && !a.pl && a.origin[li] ? DESC_ORIGIN : 0u);
+    const uint32_t xb = a.xbot && due(a.xbot_period, r, st) ? DESC_XBOT_BIT : 0u;
+    desc[(uint32_t)P] = make_uint4(a.lo + li, in_beg[li], (uint32_t)cb[li] | xb | (tf << 28), (uint32_t)(P >> 32));
+}
+
+// the outbox total: the sum of k_node_prep's nbt block sums (every thread of
+// the block calls it)
+__device__ unsigned long long btot_sum(const unsigned long long* btot, uint32_t nbt) {
+    __shared__ unsigned long long s_w[BLK / 64], s_tot;
+    unsigned long long t = 0;
+    for (uint32_t j = threadIdx.x; j < nbt; j += blockDim.x) t += btot[j];
+    for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o);
+    if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = t;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long u = 0;
+        for (uint32_t k = 0; k < blockDim.x / 64; k++) u += s_w[k];
+        s_tot = u;
+    }
+    __syncthreads();
+    return s_tot;
+}
+
 // Per node, from the scan of the packed (bound, work) words: the outbox
 // base, and for a node with work its descriptor at its active-list position
 // -- every address k_consume needs first and which of the node's timers are
@@ -787,42 +834,9 @@ __global__ void k_desc(const uint64_t* __restrict__ packed, const uint64_t* __re
                        uint32_t nbt, uint64_t* hout, uint64_t cap, uint32_t* ctl) {
     const uint32_t li = blockIdx.x * blockDim.x + threadIdx.x;
     if (*ctl) return;                                 // (uniform)
-    __shared__ unsigned long long s_w[BLK / 64], s_tot;
-    if (blockIdx.x == gridDim.x - 1) {                // the outbox total: k_node_prep's nbt block sums
-        unsigned long long t = 0;
-        for (uint32_t j = threadIdx.x; j < nbt; j += blockDim.x) t += btot[j];
-        for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o);
-        if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = t;
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            unsigned long long u = 0;
-            for (uint32_t k = 0; k < blockDim.x / 64; k++) u += s_w[k];
-            s_tot = u;
-        }
-        __syncthreads();
-    }
+    const unsigned long long tot = blockIdx.x == gridDim.x - 1 ? btot_sum(btot, nbt) : 0ull;   // (uniform)
     if (li > a.n_local) return;
-    const uint64_t P = pscan[li];
-    obase[li] = P >> 32;
-    if (li == a.n_local) {
-        const unsigned long long tot = s_tot;
-        *nact = (uint32_t)P;
-        obase[li] = tot;
-        hout[PIN_TOTAL] = tot;                        // the host's one mid-round read
-        // a batch (cap > 0) checks the outbox here instead: a total past its
-        // capacity stops the rest of the batch (code 1, this round)
-        if (cap && tot + 1 > cap) { ctl[1] = a.round; __threadfence(); ctl[0] = 1; }
-        return;
-    }
-    if (!(packed[li] & 1u)) return;
-    if ((uint32_t)cb[li] > DESC_CNT_MASK) hout[PIN_BIGIN] = 1;   // (the descriptor packs it in 26 bits)
-    const uint32_t st = start[li], r = a.round;
-    const uint32_t tf = (a.random_promotion && due(a.promotion_period, r, st) ? DESC_PROMO : 0u) |
-                        (due(a.shuffle_period, r, st) ? DESC_SHUFFLE : 0u) |
-                        (a.plumtree && due(a.lazy_tick_period, r, st) ? DESC_LAZY : 0u) |
-                        (a.plumtree && !a.pl && a.origin[li] ? DESC_ORIGIN : 0u);
-    const uint32_t xb = a.xbot && due(a.xbot_period, r, st) ? DESC_XBOT_BIT : 0u;
-    desc[(uint32_t)P] = make_uint4(a.lo + li, in_beg[li], (uint32_t)cb[li] | xb | (tf << 28), (uint32_t)(P >> 32));
+    desc_entry(a, li, pscan[li], packed[li], in_beg, cb, start, desc, obase, nact, tot, hout, cap, ctl);
 }
 
 // records src[slots[i]] -> out[i] for i < *pm, grid-stride, 4 lanes x 16 B
@@ -1436,16 +1450,21 @@ struct ScanSlot {
     }
 };
 
+// One tile of the single-pass scan (every thread of the block): loads the
+// thread's SCAN_ITEMS consecutive inputs into x, returns the exclusive prefix
+// of the first of them; *b0 = that element's index, *tile = the tile
 template <typename T>
-__global__ void __launch_bounds__(BLK) k_scan_lb(const T* __restrict__ in, T* __restrict__ out, uint32_t n,
-                                                 uint32_t* tick, uint32_t base, uint64_t* val, uint32_t epoch) {
+__device__ T scan_tile_lb(const T* __restrict__ in, uint32_t n, uint32_t* tick, uint32_t base, uint64_t* val,
+                          uint32_t epoch, T (&x)[SCAN_ITEMS], size_t* b0_out, uint32_t* tile) {
     __shared__ uint32_t s_tile;
     __shared__ T s_pre;
     if (threadIdx.x == 0) s_tile = atomicAdd(tick, 1u) - base;
     __syncthreads();
     const uint32_t t = s_tile;
     const size_t b0 = (size_t)t * SCAN_TILE + (size_t)threadIdx.x * SCAN_ITEMS;
-    T x[SCAN_ITEMS], v = 0;
+    *b0_out = b0;
+    *tile = t;
+    T v = 0;
 #pragma unroll
     for (uint32_t k = 0; k < SCAN_ITEMS; k++) {
         x[k] = b0 + k < n ? in[b0 + k] : T(0);
@@ -1492,10 +1511,47 @@ __global__ void __launch_bounds__(BLK) k_scan_lb(const T* __restrict__ in, T* __
         }
     }
     __syncthreads();
-    run += s_pre;
+    return run + s_pre;
+}
+
+template <typename T>
+__global__ void __launch_bounds__(BLK) k_scan_lb(const T* __restrict__ in, T* __restrict__ out, uint32_t n,
+                                                 uint32_t* tick, uint32_t base, uint64_t* val, uint32_t epoch) {
+    T x[SCAN_ITEMS];
+    size_t b0;
+    uint32_t t;
+    T run = scan_tile_lb<T>(in, n, tick, base, val, epoch, x, &b0, &t);
 #pragma unroll
     for (uint32_t k = 0; k < SCAN_ITEMS; k++) {
         if (b0 + k < n) out[b0 + k] = run;
+        run += x[k];
+    }
+}
+
+// prepare's scan and k_desc in one pass: the packed (bound << 32 | work)
+// words of nodes [0, n_local] scanned in a single pass (k_scan_lb's tile) and
+// each node's outbox base and descriptor written from its prefix at once --
+// no pscan array, one launch instead of two (same entries as k_desc)
+__global__ void __launch_bounds__(BLK) k_scan_desc(const uint64_t* __restrict__ packed, uint32_t* tick, uint32_t base,
+                                                   uint64_t* val, uint32_t epoch,
+                                                   const uint32_t* __restrict__ in_beg,
+                                                   const unsigned long long* __restrict__ cb,
+                                                   const uint32_t* __restrict__ start, RoundArgs a,
+                                                   uint4* __restrict__ desc, uint64_t* __restrict__ obase,
+                                                   uint32_t* nact, const unsigned long long* btot, uint32_t nbt,
+                                                   uint64_t* hout, uint64_t cap, uint32_t* ctl) {
+    uint64_t x[SCAN_ITEMS];
+    size_t b0;
+    uint32_t t;
+    // (every block takes its ticket and publishes, an aborted batch too: the
+    // look-back of the later tiles waits on it)
+    uint64_t run = scan_tile_lb<uint64_t>(packed, a.n_local + 1, tick, base, val, epoch, x, &b0, &t);
+    const unsigned long long tot = t == a.n_local / SCAN_TILE ? btot_sum(btot, nbt) : 0ull;   // (uniform)
+    if (*ctl) return;
+#pragma unroll
+    for (uint32_t k = 0; k < SCAN_ITEMS; k++) {
+        if (b0 + k <= a.n_local)
+            desc_entry(a, (uint32_t)(b0 + k), run, x[k], in_beg, cb, start, desc, obase, nact, tot, hout, cap, ctl);
         run += x[k];
     }
 }
@@ -1531,6 +1587,29 @@ int scan_excl(Shard* s, const T* in, T* out, uint32_t n) {
         k_scan_tiles<T><<<nt, BLK, 0, s->stream>>>(in, n, sums);
         k_scan_sums<T><<<1, BLK, 0, s->stream>>>(sums, nt);
         k_scan_apply<T><<<nt, BLK, 0, s->stream>>>(in, out, n, sums);
+    }
+    HIP_TRY(hipGetLastError());
+    return PSIM_OK;
+}
+
+// prepare's scan + descriptors: k_scan_desc, or (PSIM_SCAN_3PASS, for A/B)
+// the scan then k_desc
+int scan_desc(Shard* s, const RoundArgs& a) {
+    static const bool three = getenv("PSIM_SCAN_3PASS") != nullptr;
+    const uint32_t n1 = a.n_local + 1;
+    const uint32_t nt = (n1 + SCAN_TILE - 1) / SCAN_TILE;
+    if (three) {
+        TRY(scan_excl(s, s->bound.p, s->pscan.p, n1));
+        k_desc<<<grid_for(n1), BLK, 0, s->stream>>>(s->bound.p, s->pscan.p, s->in_beg.p, s->cb.p, s->start.p, a,
+                                                     s->desc.p, s->obase.p, s->d_nact.p, s->btot.p, s->pgrid, s->pin_dev,
+                                                     s->desc_cap, s->ctl.p);
+    } else {
+        TRY(scan_state(s, nt));
+        if (!++s->scan_epoch) s->scan_epoch = 1;
+        k_scan_desc<<<nt, BLK, 0, s->stream>>>(s->bound.p, s->scan_stat.p, s->scan_tick, s->scan_val.p, s->scan_epoch,
+                                               s->in_beg.p, s->cb.p, s->start.p, a, s->desc.p, s->obase.p,
+                                               s->d_nact.p, s->btot.p, s->pgrid, s->pin_dev, s->desc_cap, s->ctl.p);
+        s->scan_tick += nt;
     }
     HIP_TRY(hipGetLastError());
     return PSIM_OK;
@@ -1648,10 +1727,7 @@ int phase_events_prepare(psim_handle* h, Shard* s, const RoundCtl& ctl, RoundArg
                                                      s->btot.p);
         // bound[n] = 0: pscan[n] = (outbox total << 32) | active count;
         // obase[n] = the exact total (btot, summed by k_node_prep)
-        TRY(scan_excl(s, s->bound.p, s->pscan.p, n + 1));
-        k_desc<<<grid_for(n + 1), BLK, 0, s->stream>>>(s->bound.p, s->pscan.p, s->in_beg.p, s->cb.p, s->start.p, a,
-                                                        s->desc.p, s->obase.p, s->d_nact.p, s->btot.p, s->pgrid, s->pin_dev,
-                                                        s->desc_cap, s->ctl.p);
+        TRY(scan_desc(s, a));
         if (batched) goto args;
         TRY(stream_wait(s));                          // (k_desc stored the total in pin)
         if (s->pin[PIN_BIGIN]) return PSIM_ENOMEM;    // a node's inbox count must fit 27 bits
