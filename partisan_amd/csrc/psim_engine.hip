@@ -1570,7 +1570,10 @@ int scan_state(Shard* s, uint32_t nt) {
 
 template <typename T>
 int scan_excl(Shard* s, const T* in, T* out, uint32_t n) {
-    static const bool three = getenv("PSIM_SCAN_3PASS") != nullptr;   // (the reduce-then-scan, for A/B)
+    // the reduce-then-scan by default: the single-pass look-back (PSIM_SCAN_LB=1)
+    // measured 1.5 % slower a step at 2^20 (profiles/r03/p25: its device-coherent
+    // status loads cost more than the two launches it saves)
+    static const bool three = getenv("PSIM_SCAN_LB") == nullptr;
     const uint32_t nt = (uint32_t)(((uint64_t)n + SCAN_TILE - 1) / SCAN_TILE);
     if (nt <= 1) {
         k_scan_apply<T><<<1, BLK, 0, s->stream>>>(in, out, n, nullptr);
@@ -1592,10 +1595,10 @@ int scan_excl(Shard* s, const T* in, T* out, uint32_t n) {
     return PSIM_OK;
 }
 
-// prepare's scan + descriptors: k_scan_desc, or (PSIM_SCAN_3PASS, for A/B)
-// the scan then k_desc
+// prepare's scan + descriptors: the scan then k_desc, or (PSIM_SCAN_LB=1)
+// k_scan_desc
 int scan_desc(Shard* s, const RoundArgs& a) {
-    static const bool three = getenv("PSIM_SCAN_3PASS") != nullptr;
+    static const bool three = getenv("PSIM_SCAN_LB") == nullptr;
     const uint32_t n1 = a.n_local + 1;
     const uint32_t nt = (n1 + SCAN_TILE - 1) / SCAN_TILE;
     if (three) {
