@@ -1865,15 +1865,12 @@ int gather_inbox(psim_handle* h, Shard* s, const Msg* src, const uint32_t* dev_m
 // source indices in ivals.  No host synchronisation.
 int route_group(psim_handle* h, Shard* s, const Msg* dense, uint32_t m) {
     const uint32_t n = s->n;
-    // buckets of 2^wshift destinations, one k_bucket_route block each: at
-    // least ~1024 of them for the 256 CUs (fewer, larger buckets at 2^20 left
-    // 8 waves per CU on the route's chains), at most 16 K (the two passes'
-    // LDS histograms: 4 B per bucket)
+    // buckets of 2^wshift destinations, one k_bucket_route block each, at
+    // most 16 K of them (the two passes' LDS histograms: 4 B per bucket).
+    // At 2^20 more, smaller buckets (1024 nodes) cut k_bucket_route 36 -> 21
+    // us but cost as much in the histogram passes and their scan, and the
+    // step measured 1 % slower (profiles/r03/ab_log.txt, p17)
     uint32_t wshift = n > (1u << 26) ? 13 : 12;
-    if (n <= (1u << 22)) {
-        wshift = 9;                                    // (W >= RR_THREADS)
-        while (wshift < 12 && (n >> wshift) > 1024) wshift++;
-    }
     if (const char* e = getenv("PSIM_ROUTE_WSHIFT")) {  // (another bucket width, for measurements)
         const int v = atoi(e);
         if (v >= 9 && v <= 13) wshift = (uint32_t)v;
