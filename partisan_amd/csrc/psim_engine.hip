@@ -231,7 +231,10 @@ constexpr uint32_t RUN_LDS = 2048;
 constexpr uint32_t RB_STEP = PSIM_RB_STEP;
 constexpr uint32_t RB_WAVES = RB_STEP / 64;
 constexpr uint32_t RB_MAX_BLOCKS = 1024;   // blocks of the two passes over the sources
-constexpr uint32_t RR_THREADS = 512;       // k_bucket_route block
+#ifndef PSIM_RR_THREADS
+#define PSIM_RR_THREADS 512
+#endif
+constexpr uint32_t RR_THREADS = PSIM_RR_THREADS;   // k_bucket_route block
 
 // the sources of one route: the outbox runs of this shard's nodes (G == 1),
 // or a dense receive buffer (G > 1)
