@@ -232,9 +232,11 @@ constexpr uint32_t RB_STEP = PSIM_RB_STEP;
 constexpr uint32_t RB_WAVES = RB_STEP / 64;
 constexpr uint32_t RB_MAX_BLOCKS = 1024;   // blocks of the two passes over the sources
 #ifndef PSIM_RR_THREADS
-#define PSIM_RR_THREADS 512
+#define PSIM_RR_THREADS 1024
 #endif
-constexpr uint32_t RR_THREADS = PSIM_RR_THREADS;   // k_bucket_route block
+// k_bucket_route block: 1024 threads keep 16 waves per CU on its one block
+// per bucket (512: route 36 -> 31 us a round at 2^20, profiles/r03 p26)
+constexpr uint32_t RR_THREADS = PSIM_RR_THREADS;
 
 // the sources of one route: the outbox runs of this shard's nodes (G == 1),
 // or a dense receive buffer (G > 1)
@@ -1876,7 +1878,7 @@ int route_group(psim_handle* h, Shard* s, const Msg* dense, uint32_t m) {
     uint32_t wshift = n > (1u << 26) ? 13 : 12;
     if (const char* e = getenv("PSIM_ROUTE_WSHIFT")) {  // (another bucket width, for measurements)
         const int v = atoi(e);
-        if (v >= 9 && v <= 13) wshift = (uint32_t)v;
+        if ((1u << v) >= RR_THREADS && v <= 13) wshift = (uint32_t)v;
     }
     const uint32_t W = 1u << wshift, nb = (n + W - 1) >> wshift;
     const RouteIn in{dense ? dense : s->outbox.p, s->okey.p, s->obase.p, s->ocnt.p, dense ? m : n, s->lo,
