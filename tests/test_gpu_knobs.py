@@ -1,0 +1,26 @@
+"""The engine's measurement knobs change launch shapes and algorithms, never
+results: the single-pass look-back scans and the fused scan + descriptor
+kernel (PSIM_SCAN_LB), another route bucket width (PSIM_ROUTE_WSHIFT) and
+other grids for every node-round kernel (PSIM_*_GRID) must reproduce the
+oracle bit for bit.  The knobs are read once per process, so each set runs in
+a child process (tests/_knob_run.py)."""
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+@pytest.mark.parametrize("knobs", [
+    {"PSIM_SCAN_LB": "1", "PSIM_ROUTE_WSHIFT": "10"},
+    {"PSIM_LITE_GRID": "x1", "PSIM_PTL_GRID": "x2", "PSIM_PT_GRID": "x2", "PSIM_CONSUME_GRID": "x2"},
+])
+def test_knobs_keep_parity(knobs):
+    env = dict(os.environ, **knobs)
+    r = subprocess.run([sys.executable, "-u", os.path.join(HERE, "_knob_run.py")], env=env,
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    assert "identical" in r.stdout
