@@ -195,6 +195,42 @@ def reference_probe():
                     "reference modules and compare_trace.py"}
 
 
+def _cpu_rows():
+    """the CPU restatement on configs A and B as well (1
+    thread): A at its size (32 nodes, 200 bootstrap rounds + one broadcast and
+    40 rounds; seeds 1-5, the survey's list), B on a bounded sample (the full
+    strategy with fanout 5, gossip every round, 16384 nodes after a doubling
+    bootstrap + 20 settle rounds, 20 timed rounds)."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import _scenarios as S
+    from _oracle import Oracle
+    from partisan_amd import workloads as W
+    from partisan_amd.sim import default_config
+
+    t0 = time.perf_counter()
+    nr = msgs = 0
+    for seed in range(1, 6):
+        _, st = S.config_a(Oracle, seed=seed)
+        nr += 32 * len(st)
+        msgs += int(st["emitted"].sum())
+    dt = time.perf_counter() - t0
+    rows = {"A": {"value": nr / dt, "unit": "node-rounds/s", "cores": 1, "msgs_per_sec": msgs / dt,
+                  "sample": "config A (32 nodes join node 0 one per round, 200 rounds, a broadcast, 40 rounds), "
+                            "seeds 1-5, oracle, 1 thread"}}
+    n, rounds = 16384, 20
+    o = Oracle(default_config(n_nodes=n, seed=1, manager=1, strategy=0, fanout=5, periodic_interval=1))
+    boot = W.doubling_join(n, 1)
+    o.run_schedule(boot, boot[-1][0] + 1 + 20)
+    t0 = time.perf_counter()
+    st = o.step(rounds)
+    dt = time.perf_counter() - t0
+    rows["B"] = {"value": n * rounds / dt, "unit": "node-rounds/s", "cores": 1,
+                 "msgs_per_sec": int(st["emitted"].sum()) / dt,
+                 "sample": f"config B sample: full-membership strategy (ORSet bitsets), fanout 5, {n} nodes "
+                           f"(B is 10^5), doubling bootstrap + 20 rounds, {rounds} timed rounds, oracle, 1 thread"}
+    return rows
+
+
 def cpu_baseline(args):
     """Run before the GPU is touched (worker processes are forked).  One
     thread, then `workers` independent oracle processes on the same sample
@@ -228,6 +264,7 @@ def cpu_baseline(args):
                           "sample": f"{workers} oracle processes at once, each the 1-thread sample "
                                     f"with its own seed, timed rounds started together (barrier); "
                                     f"node-rounds of all / the slowest one's time"},
+            "rows": _cpu_rows(),
             "reference": reference_probe(),
             "cpu_model": cpu_model(), "nproc": os.cpu_count(),
             "affinity_cpus": len(os.sched_getaffinity(0))}
