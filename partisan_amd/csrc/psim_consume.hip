@@ -2064,6 +2064,9 @@ DEV void block_append(bool go, const uint4& D, uint4* desc, uint32_t* cnt, uint3
 #endif
 __global__ void __launch_bounds__(256, PSIM_RELAY_WAVES) k_relay(RoundArgs) {
     if (*kargs().ctl) return;                         // an aborted batch (run_batch)
+    // the node-round phase starts here: its span's first stamp (the last is
+    // taken by the first kernel after the phase, RoundArgs::ktime)
+    if (blockIdx.x == 0 && threadIdx.x == 0) kargs().ktime[0] = __builtin_amdgcn_s_memrealtime();
     enum { R_PROC, R_DELIV, R_SHUF, R_FAIL, R_DIGEST, R_BOUND, R_N };
     __shared__ unsigned long long sst[R_N];
     __shared__ uint32_t wc5[5][5];                    // per list: the wave counts, then the block's base
@@ -2875,14 +2878,6 @@ __global__ void PTL_BOUNDS k_ptl(RoundArgs) {
             x = sst[T_EMT + k - ST_EMIT - PSIM_MSG_PT_BROADCAST];
         row[k] = x;
     }
-}
-
-// the node-round phase's span: s_memrealtime (100 MHz) before k_relay
-// (slot 0) and after the last node-round kernel (slot 1), on the same
-// stream -- one wave each instead of a same-address atomic from every block
-// of every kernel (~10^4 per round)
-__global__ void k_mark(unsigned long long* t, int slot, const uint32_t* ctl) {
-    if (threadIdx.x == 0 && !*ctl) t[slot] = __builtin_amdgcn_s_memrealtime();
 }
 
 // one wave-slot per resident wave: the grid strides over the active list

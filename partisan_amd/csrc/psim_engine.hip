@@ -295,8 +295,10 @@ __device__ __forceinline__ void route_step(const RouteIn& in, uint32_t step, uin
 template <bool DENSE>
 __global__ void __launch_bounds__(RB_STEP) k_bucket_hist(RouteIn in, uint32_t nsteps, uint32_t nb,
                                                          uint32_t wshift, uint32_t* hist, uint32_t* n_long,
-                                                         unsigned long long* btot, const uint32_t* ctl) {
+                                                         unsigned long long* btot, const uint32_t* ctl,
+                                                         unsigned long long* mark) {
     if (*ctl) return;                                 // an aborted batch (run_batch)
+    if (mark && blockIdx.x == 0 && threadIdx.x == 0) *mark = __builtin_amdgcn_s_memrealtime();   // (phase end)
     extern __shared__ uint32_t hcnt[];                // nb bucket counters
     __shared__ uint32_t spre[RB_WAVES][65];
     __shared__ uint64_t sbase[RB_WAVES][64];
@@ -360,7 +362,9 @@ __global__ void __launch_bounds__(RB_STEP) k_bucket_scatter(RouteIn in, uint32_t
 template <bool WRITE>
 __global__ void __launch_bounds__(RB_STEP) k_owner_part(RouteIn in, uint32_t nsteps, uint32_t spb, uint32_t G,
                                                         uint32_t per, uint32_t* hist,
-                                                        const uint32_t* __restrict__ off, Msg* __restrict__ out) {
+                                                        const uint32_t* __restrict__ off, Msg* __restrict__ out,
+                                                        unsigned long long* mark) {
+    if (mark && blockIdx.x == 0 && threadIdx.x == 0) *mark = __builtin_amdgcn_s_memrealtime();   // (phase end)
     __shared__ uint32_t spre[RB_WAVES][65];
     __shared__ uint64_t sbase[RB_WAVES][64];
     __shared__ uint32_t wc[RB_WAVES][64];             // per wave and owner: records in this step
@@ -1829,7 +1833,6 @@ int phase_consume(psim_handle* h, Shard* s, RoundArgs& a) {
         // k_relay sorts the nodes with work: a lone SHUFFLE relay (and a
         // lazy tick) one lane each, more HyParView work one k_consume wave,
         // Plumtree work one k_pt wave after the node's HyParView phase
-        k_mark<<<1, 64, 0, s->stream>>>(a.ktime, 0, s->ctl.p);
         k_relay<<<s->rgrid, BLK, 0, s->stream>>>(a);
         k_shuf<<<s->sgrid, BLK, 0, s->stream>>>(a);
         k_consume_lite<<<s->lgrid, psim::lite_block(), 0, s->stream>>>(a);
@@ -1845,7 +1848,6 @@ int phase_consume(psim_handle* h, Shard* s, RoundArgs& a) {
             c.stat_part = a.stat_pt;
             k_pt<<<s->tgrid, BLK, 0, s->stream>>>(c);
         }
-        k_mark<<<1, 64, 0, s->stream>>>(a.ktime, 1, s->ctl.p);
     }
     HIP_TRY(hipGetLastError());
     s->pay_cur ^= 1;
@@ -1868,6 +1870,13 @@ int gather_inbox(psim_handle* h, Shard* s, const Msg* src, const uint32_t* dev_m
 // runs (dense == nullptr) or the m records of `dense`; leaves cb, bmask,
 // in_beg[0..n] (in_beg[n] = the record count) and the sorted runs of
 // source indices in ivals.  No host synchronisation.
+// where the first kernel after the HyParView node-round phase stamps the
+// phase's end (RoundArgs::ktime[1]); the pluggable kernel keeps its own span
+unsigned long long* phase_end_mark(psim_handle* h, Shard* s) {
+    return h->cfg.manager == PSIM_MANAGER_PLUGGABLE ? nullptr
+                                                    : reinterpret_cast<unsigned long long*>(s->stat_out.p + NST) + 1;
+}
+
 int route_group(psim_handle* h, Shard* s, const Msg* dense, uint32_t m) {
     const uint32_t n = s->n;
     // buckets of 2^wshift destinations, one k_bucket_route block each, at
@@ -1892,10 +1901,10 @@ int route_group(psim_handle* h, Shard* s, const Msg* dense, uint32_t m) {
     KTimer t(h, s, KT_SORT);
     if (dense)
         k_bucket_hist<true><<<nblk, RB_STEP, lds_h, s->stream>>>(in, nsteps, nb, wshift, s->hist.p, s->n_long.p,
-                                                                 s->btot.p, s->ctl.p);
-    else
+                                                                 s->btot.p, s->ctl.p, nullptr);
+    else    // (G == 1: the first kernel after the node-round phase stamps its end)
         k_bucket_hist<false><<<nblk, RB_STEP, lds_h, s->stream>>>(in, nsteps, nb, wshift, s->hist.p, s->n_long.p,
-                                                                  s->btot.p, s->ctl.p);
+                                                                  s->btot.p, s->ctl.p, phase_end_mark(h, s));
     TRY(scan_excl(s, s->hist.p, s->hoff.p, (uint32_t)nh));
     if (dense)
         k_bucket_scatter<true><<<nblk, RB_STEP, lds_h, s->stream>>>(in, nsteps, nb, wshift, s->hoff.p, s->pairs.p,
@@ -1956,10 +1965,10 @@ int phase_partition(psim_handle* h, Shard* s) {
     {
         KTimer t(h, s, KT_SORT);
         k_owner_part<false><<<nblk, RB_STEP, 0, s->stream>>>(in, nsteps, spb, G, h->per, s->hist.p, nullptr,
-                                                              nullptr);
+                                                              nullptr, phase_end_mark(h, s));
         TRY(scan_excl(s, s->hist.p, s->hoff.p, (uint32_t)nh));
         k_owner_part<true><<<nblk, RB_STEP, 0, s->stream>>>(in, nsteps, spb, G, h->per, nullptr, s->hoff.p,
-                                                             s->sendbuf.p);
+                                                             s->sendbuf.p, nullptr);
         k_owner_offsets<<<1, 128, 0, s->stream>>>(s->hoff.p, nblk, G, s->d_off.p, rccl ? h->comm_cnt.p : nullptr);
         HIP_TRY(hipGetLastError());
         // an RCCL rank reads the offsets back with the received counts, after

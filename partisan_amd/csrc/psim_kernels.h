@@ -68,8 +68,12 @@ struct RoundArgs {
     uint32_t* okey;
     uint32_t* ocnt;
     uint64_t* stat_part;   // [gridDim.x][NST]
-    // consume kernel span: min block-start and max block-end s_memrealtime
-    // (100 MHz), reset by k_node_prep
+    // the node-round phase's span (s_memrealtime, 100 MHz): [0] stamped by
+    // k_relay's first block as it starts, [1] by the first kernel after the
+    // phase (the route's first pass) as it starts -- two stores a round on
+    // the shard's stream, no marker launches and no same-address atomics
+    // (the pluggable kernel takes its own min start / max end); reset by
+    // k_node_prep
     unsigned long long* ktime;
     // the batch's abort word (psim_engine.hip run_batch): nonzero once a round
     // of the batch has overflowed a buffer; every kernel that reads or writes
@@ -120,8 +124,6 @@ __global__ void k_shuf(RoundArgs args);
 __global__ void k_consume_lite(RoundArgs args);
 // lane-per-node Plumtree phases (psim_consume.hip); hands k_pt what does not fit
 __global__ void k_ptl(RoundArgs args);
-// a timestamp into t[slot] (the node-round span, RoundArgs::ktime)
-__global__ void k_mark(unsigned long long* t, int slot, const uint32_t* ctl);
 // the Plumtree phase of the nodes k_relay listed (psim_consume.hip)
 __global__ void k_pt(RoundArgs args);
 // diagnostic builds (-DPSIM_STAMPS): per-phase cycle sums of k_consume, reset on read
