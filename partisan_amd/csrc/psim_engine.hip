@@ -1604,58 +1604,13 @@ int scan_excl(Shard* s, const T* in, T* out, uint32_t n) {
     return PSIM_OK;
 }
 
-// the reduce-then-scan's last pass fused with k_desc: each tile scans itself
-// from its total's prefix and writes every node's outbox base and descriptor
-// straight from it (no pscan array, one launch fewer than scan + k_desc)
-__global__ void __launch_bounds__(BLK) k_scan_apply_desc(const uint64_t* __restrict__ packed,
-                                                         const uint64_t* __restrict__ sums,
-                                                         const uint32_t* __restrict__ in_beg,
-                                                         const unsigned long long* __restrict__ cb,
-                                                         const uint32_t* __restrict__ start, RoundArgs a,
-                                                         uint4* __restrict__ desc, uint64_t* __restrict__ obase,
-                                                         uint32_t* nact, const unsigned long long* btot, uint32_t nbt,
-                                                         uint64_t* hout, uint64_t cap, uint32_t* ctl) {
-    if (*ctl) return;                                 // (uniform)
-    const uint32_t n1 = a.n_local + 1;
-    const size_t b0 = (size_t)blockIdx.x * SCAN_TILE + (size_t)threadIdx.x * SCAN_ITEMS;
-    uint64_t x[SCAN_ITEMS], v = 0;
-#pragma unroll
-    for (uint32_t k = 0; k < SCAN_ITEMS; k++) {
-        x[k] = b0 + k < n1 ? packed[b0 + k] : 0ull;
-        v += x[k];
-    }
-    uint64_t tot;
-    uint64_t run = block_excl(v, &tot) + (sums ? sums[blockIdx.x] : 0ull);
-    const unsigned long long otot = blockIdx.x == a.n_local / SCAN_TILE ? btot_sum(btot, nbt) : 0ull;  // (uniform)
-#pragma unroll
-    for (uint32_t k = 0; k < SCAN_ITEMS; k++) {
-        if (b0 + k < n1)
-            desc_entry(a, (uint32_t)(b0 + k), run, x[k], in_beg, cb, start, desc, obase, nact, otot, hout, cap, ctl);
-        run += x[k];
-    }
-}
-
-// prepare's scan + descriptors: the reduce-then-scan with k_desc fused into
-// its last pass; PSIM_SCAN_LB=1: the single-pass k_scan_desc; PSIM_SCAN_DESC=0
-// (for A/B): the scan, then k_desc
+// prepare's scan + descriptors: the scan then k_desc, or (PSIM_SCAN_LB=1)
+// k_scan_desc
 int scan_desc(Shard* s, const RoundArgs& a) {
     static const bool three = getenv("PSIM_SCAN_LB") == nullptr;
-    static const bool split = getenv("PSIM_SCAN_DESC") && atoi(getenv("PSIM_SCAN_DESC")) == 0;
     const uint32_t n1 = a.n_local + 1;
     const uint32_t nt = (n1 + SCAN_TILE - 1) / SCAN_TILE;
-    if (three && !split) {
-        const uint64_t* sums = nullptr;
-        if (nt > 1) {
-            TRY(s->cub_tmp.ensure((size_t)nt * sizeof(uint64_t)));
-            uint64_t* t = reinterpret_cast<uint64_t*>(s->cub_tmp.p);
-            k_scan_tiles<uint64_t><<<nt, BLK, 0, s->stream>>>(s->bound.p, n1, t);
-            k_scan_sums<uint64_t><<<1, BLK, 0, s->stream>>>(t, nt);
-            sums = t;
-        }
-        k_scan_apply_desc<<<nt, BLK, 0, s->stream>>>(s->bound.p, sums, s->in_beg.p, s->cb.p, s->start.p, a, s->desc.p,
-                                                     s->obase.p, s->d_nact.p, s->btot.p, s->pgrid, s->pin_dev,
-                                                     s->desc_cap, s->ctl.p);
-    } else if (three) {
+    if (three) {
         TRY(scan_excl(s, s->bound.p, s->pscan.p, n1));
         k_desc<<<grid_for(n1), BLK, 0, s->stream>>>(s->bound.p, s->pscan.p, s->in_beg.p, s->cb.p, s->start.p, a,
                                                      s->desc.p, s->obase.p, s->d_nact.p, s->btot.p, s->pgrid, s->pin_dev,

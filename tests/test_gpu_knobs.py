@@ -1,7 +1,6 @@
 """The engine's measurement knobs change launch shapes and algorithms, never
 results: the single-pass look-back scans and the fused scan + descriptor
-kernel (PSIM_SCAN_LB), the scan and k_desc as separate launches
-(PSIM_SCAN_DESC=0), another route bucket width (PSIM_ROUTE_WSHIFT) and
+kernel (PSIM_SCAN_LB), another route bucket width (PSIM_ROUTE_WSHIFT) and
 other grids for every node-round kernel (PSIM_*_GRID) must reproduce the
 oracle bit for bit.  The knobs are read once per process, so each set runs in
 a child process (tests/_knob_run.py)."""
@@ -17,7 +16,6 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 
 @pytest.mark.parametrize("knobs", [
     {"PSIM_SCAN_LB": "1", "PSIM_ROUTE_WSHIFT": "10"},
-    {"PSIM_SCAN_DESC": "0"},
     {"PSIM_LITE_GRID": "x1", "PSIM_PTL_GRID": "x2", "PSIM_PT_GRID": "x2", "PSIM_CONSUME_GRID": "x2"},
 ])
 def test_knobs_keep_parity(knobs):
