@@ -2319,23 +2319,6 @@ DEV void topk_insert(uint64_t (&K)[SHUF_TOPK], uint32_t (&E)[SHUF_TOPK], uint64_
     }
 }
 
-// the quad's four top-K lists merged: every lane of the quad ends with the K
-// smallest (key, element) pairs of all four (two butterfly steps)
-DEV void topk_quad(uint64_t (&K)[SHUF_TOPK], uint32_t (&E)[SHUF_TOPK]) {
-#pragma unroll
-    for (int m = 1; m <= 2; m <<= 1) {
-        uint64_t OK[SHUF_TOPK];
-        uint32_t OE[SHUF_TOPK];
-#pragma unroll
-        for (int i = 0; i < SHUF_TOPK; i++) {
-            OK[i] = __shfl_xor(K[i], m);
-            OE[i] = (uint32_t)__shfl_xor((int)E[i], m);
-        }
-#pragma unroll
-        for (int i = 0; i < SHUF_TOPK; i++) topk_insert(K, E, OK[i], OE[i]);
-    }
-}
-
 __global__ void __launch_bounds__(256) k_shuf(RoundArgs) {
     if (*kargs().ctl) return;                         // an aborted batch (run_batch)
     enum { S_SHUF, S_FAIL, S_DIGEST, S_BOUND, S_N };
@@ -2346,12 +2329,7 @@ __global__ void __launch_bounds__(256) k_shuf(RoundArgs) {
     const uint32_t ns = *kargs().n_shuf;
     const uint64_t two58 = 1ull << 58;
     unsigned long long v[S_N] = {};
-    // four lanes per node (a quad): lane q of the quad draws the sublist keys
-    // of the view entries j = q (mod 4) and keeps their top K; the quad merges
-    // its four top-K lists, and its lane 0 finishes the node (the per-node
-    // chain of ~35 Philox draws was k_shuf's whole latency, one lane each)
-    const uint32_t q = l & 3;
-    for (uint32_t P = (blockIdx.x * blockDim.x + threadIdx.x) >> 2; P < ns; P += (gridDim.x * blockDim.x) >> 2) {
+    for (uint32_t P = blockIdx.x * blockDim.x + threadIdx.x; P < ns; P += gridDim.x * blockDim.x) {
         KArgs& a = kargs();
         const uint4 D = a.desc_shuf[P];
         const uint32_t id = D.x;
@@ -2373,8 +2351,7 @@ __global__ void __launch_bounds__(256) k_shuf(RoundArgs) {
         for (int i = 0; i < SHUF_TOPK; i++) { K[i] = ~0ull; E[i] = ~0u; }
 #pragma unroll
         for (int j = 0; j < PSIM_ACTIVE_CAP; j++)
-            if ((uint32_t)j % 4 == q && (uint32_t)j < act_n) topk_insert(K, E, draw58_at(rng + j, id, a.seed) >> 5, A[j]);
-        topk_quad(K, E);
+            if ((uint32_t)j < act_n) topk_insert(K, E, draw58_at(rng + j, id, a.seed) >> 5, A[j]);
         rng += act_n;
         const uint32_t ka = min(act_n, a.k_active), kp = min(pas_n, a.k_passive);
         uint32_t X[8];
@@ -2385,11 +2362,15 @@ __global__ void __launch_bounds__(256) k_shuf(RoundArgs) {
         // passive row streamed 16 B at a time
 #pragma unroll
         for (int i = 0; i < SHUF_TOPK; i++) { K[i] = ~0ull; E[i] = ~0u; }
-        const uint32_t* pr = a.pas + li * PSIM_PASSIVE_CAP;
-        for (uint32_t j = q; j < pas_n; j += 4) topk_insert(K, E, draw58_at(rng + j, id, a.seed) >> 5, pr[j]);
-        topk_quad(K, E);
+        const uint4* pr = reinterpret_cast<const uint4*>(a.pas + li * PSIM_PASSIVE_CAP);
+        for (uint32_t j0 = 0; j0 < pas_n; j0 += 4) {
+            const uint4 q = pr[j0 >> 2];
+            const uint32_t Q[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+            for (int c = 0; c < 4; c++)
+                if (j0 + c < pas_n) topk_insert(K, E, draw58_at(rng + j0 + c, id, a.seed) >> 5, Q[c]);
+        }
         rng += pas_n;
-        if (q) continue;                              // (the quad's lane 0 finishes the node)
         // [Myself] ++ the active picks ++ the passive picks (slots past the
         // picks hold ~0, which sorts last and is cut below)
 #pragma unroll
