@@ -1212,6 +1212,11 @@ struct Shard {
     int tk[MAXT];
     int tn = 0;
     hipEvent_t wait_ev = nullptr;
+    // the three HyParView kernels after k_relay take disjoint node lists and
+    // run concurrently: k_shuf and k_consume on two side streams forked from
+    // and joined back into `stream` (fork_ev, join_ev)
+    hipStream_t side[2] = {nullptr, nullptr};
+    hipEvent_t fork_ev = nullptr, join_ev[2] = {nullptr, nullptr};
     bool ev_live = false;
     bool reserved = false;              // first-round capacity reservation done
     uint64_t rcap = 0;                  // records the route's buffers hold (G == 1: checked on the device)
@@ -1834,12 +1839,31 @@ int phase_consume(psim_handle* h, Shard* s, RoundArgs& a) {
         // lazy tick) one lane each, more HyParView work one k_consume wave,
         // Plumtree work one k_pt wave after the node's HyParView phase
         k_relay<<<s->rgrid, BLK, 0, s->stream>>>(a);
-        k_shuf<<<s->sgrid, BLK, 0, s->stream>>>(a);
-        k_consume_lite<<<s->lgrid, psim::lite_block(), 0, s->stream>>>(a);
         RoundArgs b = a;
         b.desc = s->desc_slow.p;
         b.n_alist = s->n_slow.p;
-        k_consume<<<s->cgrid, BLK, 0, s->stream>>>(b);
+        // k_shuf, k_consume_lite and k_consume take k_relay's disjoint lists
+        // and write only their own nodes' rows, records and stats rows: they
+        // run side by side (k_shuf and k_consume, latency-bound at ~1 and
+        // ~0.5 waves/SIMD, fill k_consume_lite's tail), then join before the
+        // Plumtree phase.  PSIM_SERIAL_PHASE=1: one after another (A/B)
+        static const bool serial = getenv("PSIM_SERIAL_PHASE") != nullptr;
+        if (serial) {
+            k_shuf<<<s->sgrid, BLK, 0, s->stream>>>(a);
+            k_consume_lite<<<s->lgrid, psim::lite_block(), 0, s->stream>>>(a);
+            k_consume<<<s->cgrid, BLK, 0, s->stream>>>(b);
+        } else {
+            HIP_TRY(hipEventRecord(s->fork_ev, s->stream));
+            HIP_TRY(hipStreamWaitEvent(s->side[0], s->fork_ev, 0));
+            HIP_TRY(hipStreamWaitEvent(s->side[1], s->fork_ev, 0));
+            k_consume<<<s->cgrid, BLK, 0, s->side[0]>>>(b);
+            k_shuf<<<s->sgrid, BLK, 0, s->side[1]>>>(a);
+            k_consume_lite<<<s->lgrid, psim::lite_block(), 0, s->stream>>>(a);
+            for (int k = 0; k < 2; k++) {
+                HIP_TRY(hipEventRecord(s->join_ev[k], s->side[k]));
+                HIP_TRY(hipStreamWaitEvent(s->stream, s->join_ev[k], 0));
+            }
+        }
         if (s->qgrid) k_ptl<<<s->qgrid, PTL_BLOCK, 0, s->stream>>>(a);
         if (s->tgrid) {
             RoundArgs c = a;
@@ -2364,6 +2388,11 @@ int run_batch(psim_handle* h, uint32_t nb, psim_round_stats* st_out, uint32_t* d
 int shard_alloc(psim_handle* h, Shard* s) {
     HIP_TRY(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
     HIP_TRY(hipEventCreateWithFlags(&s->wait_ev, hipEventDisableTiming));
+    for (int k = 0; k < 2; k++) {
+        HIP_TRY(hipStreamCreateWithFlags(&s->side[k], hipStreamNonBlocking));
+        HIP_TRY(hipEventCreateWithFlags(&s->join_ev[k], hipEventDisableTiming));
+    }
+    HIP_TRY(hipEventCreateWithFlags(&s->fork_ev, hipEventDisableTiming));
     if (s->n > (1u << 26))      // route buckets of 8192 destinations: 128 KiB of LDS per block
         HIP_TRY(hipFuncSetAttribute((const void*)k_bucket_route, hipFuncAttributeMaxDynamicSharedMemorySize,
                                     8192 * 16));
@@ -2442,6 +2471,14 @@ void shard_free(Shard* s) {
     if (s->pin) (void)hipHostFree(s->pin);
     if (s->wait_ev) (void)hipEventDestroy(s->wait_ev);
     s->wait_ev = nullptr;
+    for (int k = 0; k < 2; k++) {
+        if (s->join_ev[k]) (void)hipEventDestroy(s->join_ev[k]);
+        if (s->side[k]) (void)hipStreamDestroy(s->side[k]);
+        s->join_ev[k] = nullptr;
+        s->side[k] = nullptr;
+    }
+    if (s->fork_ev) (void)hipEventDestroy(s->fork_ev);
+    s->fork_ev = nullptr;
     s->pin = nullptr;
     s->outbox.release(); s->okey.release(); s->ocnt.release();
     s->cb.release(); s->in_beg.release();
