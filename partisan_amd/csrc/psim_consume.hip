@@ -2069,7 +2069,7 @@ __global__ void __launch_bounds__(256, PSIM_RELAY_WAVES) k_relay(RoundArgs) {
     if (blockIdx.x == 0 && threadIdx.x == 0) kargs().ktime[0] = __builtin_amdgcn_s_memrealtime();
     enum { R_PROC, R_DELIV, R_SHUF, R_FAIL, R_DIGEST, R_BOUND, R_N };
     __shared__ unsigned long long sst[R_N];
-    __shared__ uint32_t wc5[6][5];                    // per list: the wave counts, then the block's base
+    __shared__ uint32_t wc5[5][5];                    // per list: the wave counts, then the block's base
     if (threadIdx.x < R_N) sst[threadIdx.x] = 0;
     __syncthreads();
     const uint32_t l = lane_id();
@@ -2187,38 +2187,32 @@ __global__ void __launch_bounds__(256, PSIM_RELAY_WAVES) k_relay(RoundArgs) {
             // the five lists at once: one barrier-separated count, the five
             // block atomics from five lanes of one instruction (one after
             // another they were five serial L2 round trips per block step)
-            // (k_ptl's nodes in two lists: those whose HyParView phase is
-            // done in this lane -- k_ptl runs them beside the HyParView
-            // kernels -- and those of k_consume, k_consume_lite and k_shuf)
-            const bool hv_after = heavy || lite || shuf;
-            const bool g[6] = {P < na && heavy, P < na && to_pt && origin_node,
-                               P < na && to_pt && !origin_node && !hv_after, P < na && shuf, P < na && lite,
-                               P < na && to_pt && !origin_node && hv_after};
-            uint64_t m[6];
+            const bool g[5] = {P < na && heavy, P < na && to_pt && origin_node, P < na && to_pt && !origin_node,
+                               P < na && shuf, P < na && lite};
+            uint64_t m[5];
 #pragma unroll
-            for (int k = 0; k < 6; k++) m[k] = ballot(g[k]);
+            for (int k = 0; k < 5; k++) m[k] = ballot(g[k]);
             const uint32_t wv = threadIdx.x >> 6, nwv = blockDim.x >> 6;
             __syncthreads();                          // the previous step's readers of wc5 are done
             if (l == 0)
 #pragma unroll
-                for (int k = 0; k < 6; k++) wc5[k][wv] = popc(m[k]);
+                for (int k = 0; k < 5; k++) wc5[k][wv] = popc(m[k]);
             __syncthreads();
-            if (threadIdx.x < 6) {
+            if (threadIdx.x < 5) {
                 const uint32_t k = threadIdx.x;
                 uint32_t t = 0;
                 for (uint32_t j = 0; j < nwv; j++) t += wc5[k][j];
-                uint32_t* cnt = k == 0 ? a.n_slow : k == 1 ? a.n_pt : k == 2 ? a.n_ptl : k == 3 ? a.n_shuf
-                              : k == 4 ? a.n_lite : a.n_ptl2;
+                uint32_t* cnt = k == 0 ? a.n_slow : k == 1 ? a.n_pt : k == 2 ? a.n_ptl : k == 3 ? a.n_shuf : a.n_lite;
                 wc5[k][4] = t ? atomicAdd(cnt, t) : 0u;
             }
             __syncthreads();
 #pragma unroll
-            for (int k = 0; k < 6; k++)
+            for (int k = 0; k < 5; k++)
                 if (g[k]) {
                     uint32_t b0 = wc5[k][4];
                     for (uint32_t j = 0; j < wv; j++) b0 += wc5[k][j];
                     uint4* desc = k == 0 ? a.desc_slow : k == 1 ? a.desc_pt : k == 2 ? a.desc_ptl
-                                : k == 3 ? a.desc_shuf : k == 4 ? a.desc_lite : a.desc_ptl2;
+                                : k == 3 ? a.desc_shuf : a.desc_lite;
                     desc[b0 + popc(m[k] & lt_mask())] =
                         k == 0 && maps ? make_uint4(D.x, D.y, D.z | DESC_MAPS_BIT, D.w) : D;
                 }

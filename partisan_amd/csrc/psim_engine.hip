@@ -628,7 +628,6 @@ __global__ void __launch_bounds__(256) k_node_prep(RoundArgs a, const unsigned l
         if (a.n_shuf) *a.n_shuf = 0;
         if (a.n_lite) *a.n_lite = 0;
         if (a.n_ptl) *a.n_ptl = 0;
-        if (a.n_ptl2) *a.n_ptl2 = 0;
         if (a.n_stop) *a.n_stop = 0;
     }
     __syncthreads();
@@ -1180,12 +1179,12 @@ struct Shard {
     DBuf<Msg> inbox;
     // per-round scratch
     DBuf<uint32_t> okey, ocnt, in_beg,
-        d_nact, n_slow, n_pt, n_shuf, n_lite, n_ptl, n_ptl2, rank, long_list, n_long, tmp, hist, hoff;
+        d_nact, n_slow, n_pt, n_shuf, n_lite, n_ptl, rank, long_list, n_long, tmp, hist, hoff;
     DBuf<unsigned long long> bmask;     // per local node: message slots of its BROADCAST records
     DBuf<uint2> pairs;                  // route: (destination in bucket | class, source index)
     DBuf<unsigned long long> cb;        // per local node: inbox count | bound sum << 32 (n + 1)
     DBuf<unsigned long long> btot;      // this round's outbox total (k_node_prep)
-    DBuf<uint4> desc, desc_slow, desc_pt, desc_shuf, desc_lite, desc_ptl, desc_ptl2;   // work descriptors; those k_relay leaves to k_consume / k_pt / k_shuf
+    DBuf<uint4> desc, desc_slow, desc_pt, desc_shuf, desc_lite, desc_ptl;   // work descriptors; those k_relay leaves to k_consume / k_pt / k_shuf
     DBuf<uint64_t> bound, pscan, obase, stat_part, stat_out, stat_tile, d_off;   // bound: packed (bound << 32 | work)
     DBuf<uint8_t> cub_tmp;              // the scan's tile totals
     DBuf<uint32_t> scan_stat;           // single-pass scan (k_scan_lb): [0] the ticket counter, [1] give-ups,
@@ -1216,9 +1215,8 @@ struct Shard {
     // the three HyParView kernels after k_relay take disjoint node lists and
     // run concurrently: k_shuf and k_consume on two side streams forked from
     // and joined back into `stream` (fork_ev, join_ev)
-    static constexpr int NSIDE = 3;     // k_consume, k_shuf, the first k_ptl launch
-    hipStream_t side[NSIDE] = {};
-    hipEvent_t fork_ev = nullptr, join_ev[NSIDE] = {};
+    hipStream_t side[2] = {nullptr, nullptr};
+    hipEvent_t fork_ev = nullptr, join_ev[2] = {nullptr, nullptr};
     bool ev_live = false;
     bool reserved = false;              // first-round capacity reservation done
     uint64_t rcap = 0;                  // records the route's buffers hold (G == 1: checked on the device)
@@ -1317,7 +1315,6 @@ RoundArgs make_args(psim_handle* h, Shard* s) {
     a.desc_shuf = s->desc_shuf.p; a.n_shuf = s->n_shuf.p;
     a.desc_lite = s->desc_lite.p; a.n_lite = s->n_lite.p;
     a.desc_ptl = s->desc_ptl.p; a.n_ptl = s->n_ptl.p;
-    a.desc_ptl2 = s->desc_ptl2.p; a.n_ptl2 = s->n_ptl2.p;
     a.stop_ids = s->stop_ids.p; a.n_stop = s->n_stop.p;
     a.faults = h->faults; a.n_omit_s = h->n_omit_s; a.n_omit_r = h->n_omit_r;
     a.faulted = s->faulted.p; a.omit = s->omit.p;
@@ -1741,7 +1738,7 @@ int phase_events_prepare(psim_handle* h, Shard* s, const RoundCtl& ctl, RoundArg
         s->sgrid = hv ? std::min<uint32_t>(grid_for(n), SHUF_MAX_BLOCKS) : 0;
         s->lgrid = hv ? std::min<uint32_t>((uint32_t)((n + psim::lite_block() - 1) / psim::lite_block()), h->lite_blocks) : 0;
         s->qgrid = hv && h->cfg.plumtree ? std::min<uint32_t>((n + PTL_BLOCK - 1) / PTL_BLOCK, h->ptl_blocks) : 0;
-        TRY(s->stat_part.ensure((size_t)(s->pgrid + s->cgrid + s->rgrid + s->tgrid + s->sgrid + s->lgrid + 2 * s->qgrid) *
+        TRY(s->stat_part.ensure((size_t)(s->pgrid + s->cgrid + s->rgrid + s->tgrid + s->sgrid + s->lgrid + s->qgrid) *
                                 NST));
         k_node_prep<<<s->pgrid, BLK, 0, s->stream>>>(a, s->bmask.p, s->bound.p, s->stat_part.p, s->ocnt.p,
                                                      s->btot.p);
@@ -1850,32 +1847,24 @@ int phase_consume(psim_handle* h, Shard* s, RoundArgs& a) {
         // run side by side (k_shuf and k_consume, latency-bound at ~1 and
         // ~0.5 waves/SIMD, fill k_consume_lite's tail), then join before the
         // Plumtree phase.  PSIM_SERIAL_PHASE=1: one after another (A/B)
-        // k_ptl in two launches: the nodes whose HyParView phase ran in
-        // k_relay's lane (desc_ptl) beside the HyParView kernels, the others
-        // (desc_ptl2, stats rows after the first launch's) once they are done
-        RoundArgs d = a;
-        d.desc_ptl = s->desc_ptl2.p;
-        d.n_ptl = s->n_ptl2.p;
-        d.stat_ptl = a.stat_ptl + (size_t)s->qgrid * NST;
         static const bool serial = getenv("PSIM_SERIAL_PHASE") != nullptr;
         if (serial) {
             k_shuf<<<s->sgrid, BLK, 0, s->stream>>>(a);
             k_consume_lite<<<s->lgrid, psim::lite_block(), 0, s->stream>>>(a);
             k_consume<<<s->cgrid, BLK, 0, s->stream>>>(b);
-            if (s->qgrid) k_ptl<<<s->qgrid, PTL_BLOCK, 0, s->stream>>>(a);
         } else {
             HIP_TRY(hipEventRecord(s->fork_ev, s->stream));
-            for (int k = 0; k < Shard::NSIDE; k++) HIP_TRY(hipStreamWaitEvent(s->side[k], s->fork_ev, 0));
+            HIP_TRY(hipStreamWaitEvent(s->side[0], s->fork_ev, 0));
+            HIP_TRY(hipStreamWaitEvent(s->side[1], s->fork_ev, 0));
             k_consume<<<s->cgrid, BLK, 0, s->side[0]>>>(b);
             k_shuf<<<s->sgrid, BLK, 0, s->side[1]>>>(a);
-            if (s->qgrid) k_ptl<<<s->qgrid, PTL_BLOCK, 0, s->side[2]>>>(a);
             k_consume_lite<<<s->lgrid, psim::lite_block(), 0, s->stream>>>(a);
-            for (int k = 0; k < Shard::NSIDE; k++) {
+            for (int k = 0; k < 2; k++) {
                 HIP_TRY(hipEventRecord(s->join_ev[k], s->side[k]));
                 HIP_TRY(hipStreamWaitEvent(s->stream, s->join_ev[k], 0));
             }
         }
-        if (s->qgrid) k_ptl<<<s->qgrid, PTL_BLOCK, 0, s->stream>>>(d);
+        if (s->qgrid) k_ptl<<<s->qgrid, PTL_BLOCK, 0, s->stream>>>(a);
         if (s->tgrid) {
             RoundArgs c = a;
             c.desc = s->desc_pt.p;
@@ -2091,7 +2080,7 @@ int exchange_rccl(psim_handle* h) {
 
 int phase_stats(psim_handle* h, Shard* s, const std::vector<uint32_t>& crashed) {
     KTimer t(h, s, KT_STATS);
-    const uint32_t rows = s->pgrid + s->cgrid + s->rgrid + s->tgrid + s->sgrid + s->lgrid + 2 * s->qgrid;   // (two k_ptl launches)
+    const uint32_t rows = s->pgrid + s->cgrid + s->rgrid + s->tgrid + s->sgrid + s->lgrid + s->qgrid;
     const uint32_t nt = std::min<uint32_t>(STAT_TILES, std::max<uint32_t>(1, rows / 32));
     k_stats_tiles<<<nt, BLK, 0, s->stream>>>(s->stat_part.p, rows, s->stat_tile.p);
     k_stats_final<<<1, BLK, 0, s->stream>>>(s->stat_tile.p, nt, s->stat_out.p, s->pin_dev + (size_t)s->stat_slot * PIN_STRIDE);
@@ -2399,7 +2388,7 @@ int run_batch(psim_handle* h, uint32_t nb, psim_round_stats* st_out, uint32_t* d
 int shard_alloc(psim_handle* h, Shard* s) {
     HIP_TRY(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
     HIP_TRY(hipEventCreateWithFlags(&s->wait_ev, hipEventDisableTiming));
-    for (int k = 0; k < Shard::NSIDE; k++) {
+    for (int k = 0; k < 2; k++) {
         HIP_TRY(hipStreamCreateWithFlags(&s->side[k], hipStreamNonBlocking));
         HIP_TRY(hipEventCreateWithFlags(&s->join_ev[k], hipEventDisableTiming));
     }
@@ -2446,7 +2435,6 @@ int shard_alloc(psim_handle* h, Shard* s) {
     rc |= s->desc_shuf.alloc(n); rc |= s->n_shuf.alloc(1);
     rc |= s->desc_lite.alloc(n); rc |= s->n_lite.alloc(1);
     rc |= s->desc_ptl.alloc(n); rc |= s->n_ptl.alloc(1);
-    rc |= s->desc_ptl2.alloc(n); rc |= s->n_ptl2.alloc(1);
     if (h->cfg.manager == PSIM_MANAGER_PLUGGABLE) { rc |= s->stop_ids.alloc(n); rc |= s->n_stop.alloc(1); }
     rc |= s->stat_out.alloc(NST + 2);   // + the consume span
     rc |= s->ctl.alloc(2);
@@ -2483,7 +2471,7 @@ void shard_free(Shard* s) {
     if (s->pin) (void)hipHostFree(s->pin);
     if (s->wait_ev) (void)hipEventDestroy(s->wait_ev);
     s->wait_ev = nullptr;
-    for (int k = 0; k < Shard::NSIDE; k++) {
+    for (int k = 0; k < 2; k++) {
         if (s->join_ev[k]) (void)hipEventDestroy(s->join_ev[k]);
         if (s->side[k]) (void)hipStreamDestroy(s->side[k]);
         s->join_ev[k] = nullptr;
@@ -2497,7 +2485,7 @@ void shard_free(Shard* s) {
     s->rank.release(); s->long_list.release(); s->bmask.release(); s->btot.release();
     s->hist.release(); s->hoff.release(); s->pairs.release(); s->n_long.release(); s->tmp.release();
     s->stop_ids.release(); s->n_stop.release();
-    s->desc.release(); s->d_nact.release(); s->desc_slow.release(); s->n_slow.release(); s->desc_pt.release(); s->n_pt.release(); s->desc_shuf.release(); s->n_shuf.release(); s->desc_lite.release(); s->n_lite.release(); s->desc_ptl.release(); s->n_ptl.release(); s->desc_ptl2.release(); s->n_ptl2.release(); s->bound.release(); s->pscan.release();
+    s->desc.release(); s->d_nact.release(); s->desc_slow.release(); s->n_slow.release(); s->desc_pt.release(); s->n_pt.release(); s->desc_shuf.release(); s->n_shuf.release(); s->desc_lite.release(); s->n_lite.release(); s->desc_ptl.release(); s->n_ptl.release(); s->bound.release(); s->pscan.release();
     s->obase.release(); s->stat_part.release(); s->stat_out.release(); s->stat_tile.release(); s->d_off.release();
     s->cub_tmp.release(); s->scan_stat.release(); s->scan_val.release(); s->ev_ids.release(); s->ev_contacts.release(); s->sendbuf.release(); s->ctl.release();
     s->sview.release(); s->sinv.release(); s->fbits.release(); s->pay[0].release(); s->pay[1].release();

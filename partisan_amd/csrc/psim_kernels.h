@@ -59,11 +59,6 @@ struct RoundArgs {
     uint64_t* stat_lite;        // k_consume_lite's per-block stats rows
     uint4* desc_ptl;            // ... and the nodes with Plumtree work and no origin, for k_ptl
     uint32_t* n_ptl;
-    // k_relay splits k_ptl's nodes: those whose HyParView phase ran in its
-    // lane (or had none) in desc_ptl -- k_ptl takes them beside the HyParView
-    // kernels -- and the rest here, for the k_ptl launch after them
-    uint4* desc_ptl2;
-    uint32_t* n_ptl2;
     uint64_t* stat_ptl;         // k_ptl's per-block stats rows
     uint64_t* stat_relay;
     uint64_t* stat_pt;          // k_pt's per-block stats rows
