@@ -1847,7 +1847,13 @@ int phase_consume(psim_handle* h, Shard* s, RoundArgs& a) {
         // run side by side (k_shuf and k_consume, latency-bound at ~1 and
         // ~0.5 waves/SIMD, fill k_consume_lite's tail), then join before the
         // Plumtree phase.  PSIM_SERIAL_PHASE=1: one after another (A/B)
-        static const bool serial = getenv("PSIM_SERIAL_PHASE") != nullptr;
+        // Serial in crash rounds: there k_consume carries the EXIT scans and
+        // the crashed members' replacements of every holder (config E at
+        // 2^26: 15 ms of wave work a round) and side by side with
+        // k_consume_lite the two took longer than one after the other
+        // (node-round phase 61.0 -> 68.3 ms, profiles/r03/p36)
+        static const bool serial_env = getenv("PSIM_SERIAL_PHASE") != nullptr;
+        const bool serial = serial_env || a.crash_round;
         if (serial) {
             k_shuf<<<s->sgrid, BLK, 0, s->stream>>>(a);
             k_consume_lite<<<s->lgrid, psim::lite_block(), 0, s->stream>>>(a);
