@@ -31,7 +31,7 @@ ks = {r['Name']: float(r['AverageNs']) / 1e3 for r in csv.DictReader(open('$S'))
 pick = lambda s: next((round(v, 1) for n, v in ks.items() if s in n), None)
 print('$e', round(d['ms_per_step'], 3), 'ms/step phase', round(d['roofline']['avg_launch_ms'], 3),
       'lite', pick('k_consume_lite'), 'ptl', pick('k_ptl('), 'pt', pick('k_pt('), 'relay', pick('k_relay'), 'cons', pick('k_consume('),
-      '| hist', pick('k_bucket_hist'), 'scat', pick('k_bucket_scatter'), 'route', pick('k_bucket_route'), 'gath', pick('k_gather_dev'))" | tee -a $O/ab.txt
+      '| hist', pick('k_bucket_hist'), 'scat', pick('k_bucket_scatter'), 'route', pick('k_bucket_route'), 'gath', pick('k_gather'))" | tee -a $O/ab.txt
   rm -rf $O/t$k
 done
 echo AB DONE
