@@ -848,22 +848,6 @@ __global__ void k_desc(const uint64_t* __restrict__ packed, const uint64_t* __re
     desc_entry(a, li, pscan[li], packed[li], in_beg, cb, start, desc, obase, nact, tot, hout, cap, ctl);
 }
 
-// records src[slots[i]] -> out[i] for i < *pm, grid-stride, one lane per
-// record: its slot, then all four 16-B loads in flight before the stores
-// (A/B against the 4-lanes-per-record form below: PSIM_GATHER4=1)
-__global__ void k_gather_rec(const Msg* __restrict__ rec, const uint32_t* __restrict__ slots,
-                             const uint32_t* __restrict__ pm, Msg* __restrict__ out, uint64_t cap,
-                             const uint32_t* ctl) {
-    if (*ctl || *pm > cap) return;                    // the route overflowed: redone by the host
-    const uint64_t m = *pm;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (uint64_t)gridDim.x * blockDim.x) {
-        const uint4* sp = reinterpret_cast<const uint4*>(&rec[slots[i]]);
-        const uint4 x0 = sp[0], x1 = sp[1], x2 = sp[2], x3 = sp[3];
-        uint4* dp = reinterpret_cast<uint4*>(&out[i]);
-        dp[0] = x0; dp[1] = x1; dp[2] = x2; dp[3] = x3;
-    }
-}
-
 // records src[slots[i]] -> out[i] for i < *pm, grid-stride, 4 lanes x 16 B
 __global__ void k_gather_dev(const Msg* __restrict__ rec, const uint32_t* __restrict__ slots,
                              const uint32_t* __restrict__ pm, Msg* __restrict__ out, uint64_t cap,
@@ -1905,12 +1889,8 @@ int phase_consume(psim_handle* h, Shard* s, RoundArgs& a) {
 // record count is read on the device (in_beg[n] for G == 1).
 int gather_inbox(psim_handle* h, Shard* s, const Msg* src, const uint32_t* dev_m, uint32_t max_m) {
     KTimer t(h, s, KT_GATHER);
-    static const bool four = getenv("PSIM_GATHER4") != nullptr;
-    if (max_m && four)
+    if (max_m)
         k_gather_dev<<<std::min<uint32_t>(grid_for((uint64_t)max_m * 4), 8192), BLK, 0, s->stream>>>(
-            src, s->ivals.p, dev_m, s->inbox.p, s->rcap, s->ctl.p);
-    else if (max_m)
-        k_gather_rec<<<std::min<uint32_t>(grid_for((uint64_t)max_m), 8192), BLK, 0, s->stream>>>(
             src, s->ivals.p, dev_m, s->inbox.p, s->rcap, s->ctl.p);
     return PSIM_OK;
 }
