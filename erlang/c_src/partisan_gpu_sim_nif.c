@@ -385,6 +385,20 @@ static ERL_NIF_TERM nif_set_partition(ErlNifEnv *env, int argc, const ERL_NIF_TE
     return rc ? err(env, rc) : enif_make_atom(env, "ok");
 }
 
+/* set_bucket_table(Ref, BucketsBin): one byte per node, erlang:phash(NodeSpec,
+ * 16) - 1 -- the sets v1 order of every view; before the
+ * first step only */
+static ERL_NIF_TERM nif_set_bucket_table(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[]) {
+    sim_res *r; ErlNifBinary b;
+    if (!enif_get_resource(env, argv[0], SIM_RT, (void **)&r) || !enif_inspect_binary(env, argv[1], &b) ||
+        b.size != r->n_nodes)
+        return enif_make_badarg(env);
+    LOCK_OR_BUSY(r);
+    int rc = psim_set_bucket_table(r->h, (const uint8_t *)b.data, b.size);
+    enif_mutex_unlock(r->mu);
+    return rc ? err(env, rc) : enif_make_atom(env, "ok");
+}
+
 static ERL_NIF_TERM nif_clear_partition(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[]) {
     sim_res *r;
     if (!enif_get_resource(env, argv[0], SIM_RT, (void **)&r)) return enif_make_badarg(env);
@@ -439,6 +453,7 @@ static ErlNifFunc funcs[] = {
     {"histograms", 1, nif_histograms, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"set_partition_nif", 2, nif_set_partition, 0},
     {"clear_partition_nif", 1, nif_clear_partition, 0},
+    {"set_bucket_table_nif", 2, nif_set_bucket_table, 0},
     {"omission_nif", 5, nif_omission, 0},
     {"faulted_nif", 3, nif_faulted, 0},
     {"clear_faults_nif", 1, nif_clear_faults, 0},

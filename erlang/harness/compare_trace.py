@@ -1,15 +1,21 @@
 """Reference parity through the in-BEAM harness (erlang/harness/README.md).
 
-  python erlang/harness/compare_trace.py scenario config_a DIR
+  python erlang/harness/compare_trace.py scenario config_a DIR [BUCKETS]
       writes DIR/config_a.terms (the event script psim_harness:run/2 -- or,
       for the *_pl scenarios, psim_strategy_harness:run/2 -- reads)
       and DIR/config_a.oracle (the CPU oracle's record stream of the same
-      scenario: one line per emitted message, in the harness's format)
+      scenario: one line per emitted message, in the harness's format; its
+      first line `S config_a` names the scenario).  With BUCKETS (a file of
+      `B id bucket` or `id bucket` lines) the oracle orders views by that
+      sets v1 table (psim_set_bucket_table) instead of its stand-in.
   python erlang/harness/compare_trace.py compare DIR/config_a.harness DIR/config_a.oracle
       diffs the two streams round by round; exit status 1 at the first
-      differing record.  Bucket lines (B id phash16) of the harness output
-      are also written to DIR/bucket16.txt: the sets v1 order the engine's
-      bucket16() stands in for (psim_device.h).
+      differing record.  The harness writes the real view order -- a line
+      `B id bucket` per node, bucket = erlang:phash(NodeSpec, 16) - 1 (App.
+      A Q1) -- which compare copies to DIR/bucket16.txt and, when it differs
+      from the table the oracle stream was made with, uses to regenerate that
+      stream (DIR/config_a.oracle_b) before diffing: one harness run is a
+      complete comparison.
 
 The oracle is the checker (test infrastructure); the GPU engine is pinned to
 it bit for bit by tests/test_gpu_parity.py, so harness == oracle extends to
@@ -50,7 +56,27 @@ SCENARIOS = {
 STRATEGIES = {"full": 0, "scamp_v1": 1, "scamp_v2": 2}
 
 
-def scenario(name, out_dir):
+def read_buckets(path, n=None):
+    """`B id bucket` (harness output) or `id bucket` lines -> uint8 table"""
+    rows = []
+    for l in open(path):
+        f = l.split()
+        if f and f[0] == "B":
+            f = f[1:]
+        if len(f) == 2:
+            rows.append((int(f[0]), int(f[1])))
+    m = n if n is not None else (max(i for i, _ in rows) + 1 if rows else 0)
+    tab = np.zeros(m, np.uint8)
+    seen = np.zeros(m, bool)
+    for i, b in rows:
+        if i < m:
+            tab[i], seen[i] = b, True
+    if not seen.all() or (tab > 15).any():
+        raise ValueError(f"{path}: not a bucket table of {m} nodes")
+    return tab
+
+
+def scenario(name, out_dir, buckets=None):
     sc = SCENARIOS[name]
     n, seed, rounds = sc["n"], sc["seed"], sc["rounds"]
     joins = sc["joins"](n, seed)
@@ -71,20 +97,34 @@ def scenario(name, out_dir):
             f.write(f"{{partition, {sc['part'][0]}, [{g}]}}.\n{{clear_partition, {sc['part'][1]}}}.\n")
         for r, pairs in sc.get("leave", {}).items():
             f.write(f"{{leave, {r}, [{', '.join(f'{{{a}, {t}}}' for a, t in pairs)}]}}.\n")
-    lines = oracle_stream(n, seed, rounds, joins, sc["bcast"], sc["crash"], strategy=strategy,
-                          part=sc.get("part"), leave=sc.get("leave", {}))
-    with open(os.path.join(out_dir, name + ".oracle"), "w") as f:
+    tab = read_buckets(buckets, n) if buckets else None
+    write_stream(name, os.path.join(out_dir, name + ".oracle"), tab)
+    print(f"wrote {name}.terms and {name}.oracle")
+
+
+def write_stream(name, path, tab=None):
+    sc = SCENARIOS[name]
+    n, seed, rounds = sc["n"], sc["seed"], sc["rounds"]
+    lines = oracle_stream(n, seed, rounds, sc["joins"](n, seed), sc["bcast"], sc["crash"],
+                          strategy=sc.get("strategy"), part=sc.get("part"), leave=sc.get("leave", {}),
+                          buckets=tab)
+    with open(path, "w") as f:
+        f.write(f"S {name}\n")
+        if tab is not None:
+            f.write("".join(f"B {i} {int(b)}\n" for i, b in enumerate(tab)))
         f.write("\n".join(lines) + "\n")
-    print(f"wrote {name}.terms and {name}.oracle ({len(lines)} records)")
+    return len(lines)
 
 
-def oracle_stream(n, seed, rounds, joins, bcast, crash, strategy=None, part=None, leave=None):
+def oracle_stream(n, seed, rounds, joins, bcast, crash, strategy=None, part=None, leave=None, buckets=None):
     from _oracle import Oracle
     if strategy:
         o = Oracle(default_config(n_nodes=n, seed=seed, manager=_abi.MANAGER_PLUGGABLE,
                                   strategy=STRATEGIES[strategy], fanout=0, scamp_c=5, periodic_interval=10))
     else:
         o = Oracle(default_config(n_nodes=n, seed=seed))
+    if buckets is not None:
+        o.set_bucket_table(buckets)
     lib = o._lib
     ev = {}
     for r, ids, contacts in joins:
@@ -125,8 +165,19 @@ def compare(harness, oracle):
     o = [l.rstrip("\n") for l in open(oracle) if l.startswith("R ")]
     buckets = [l for l in open(harness) if l.startswith("B ")]
     if buckets:
-        with open(os.path.join(os.path.dirname(os.path.abspath(harness)), "bucket16.txt"), "w") as f:
+        path = os.path.join(os.path.dirname(os.path.abspath(harness)), "bucket16.txt")
+        with open(path, "w") as f:
             f.writelines(buckets)
+        names = [l.split()[1] for l in open(oracle) if l.startswith("S ")]
+        used = [l for l in open(oracle) if l.startswith("B ")]
+        if names and names[0] in SCENARIOS and sorted(used) != sorted(buckets):
+            # the stream was made with another view order: remake it with the
+            # harness's erlang:phash table, then diff against that
+            tab = read_buckets(path, SCENARIOS[names[0]]["n"])
+            regen = os.path.splitext(oracle)[0] + ".oracle_b"
+            write_stream(names[0], regen, tab)
+            print(f"oracle stream regenerated with the harness's bucket table: {regen}")
+            o = [l.rstrip("\n") for l in open(regen) if l.startswith("R ")]
     for i, (a, b) in enumerate(zip(h, o)):
         if a != b:
             print(f"record {i} differs:\n  harness {a}\n  oracle  {b}")
@@ -140,6 +191,6 @@ def compare(harness, oracle):
 
 if __name__ == "__main__":
     if sys.argv[1] == "scenario":
-        scenario(sys.argv[2], sys.argv[3])
+        scenario(sys.argv[2], sys.argv[3], sys.argv[4] if len(sys.argv) > 4 else None)
     else:
         sys.exit(compare(sys.argv[2], sys.argv[3]))

@@ -27,7 +27,7 @@
 %% (:251-264), handle_cast/2 (:282-336), handle_info(lazy_tick) (:341-345).
 -module(psim_harness).
 -export([main/1, run/2, spec/1, name/1, id_of/1, reachable/2, register_conn/3, record/3,
-         pt_update/1, pt_send/4, have/1, have_add/1]).
+         pt_update/1, pt_send/4, have/1, have_add/1, write_buckets/2]).
 
 -define(HV, partisan_hyparview_peer_service_manager).
 -define(PT, partisan_plumtree_broadcast).

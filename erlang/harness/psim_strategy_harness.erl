@@ -75,6 +75,8 @@ run(Events, OutFile) ->
     put({psim_h_cfg, random_seed_int}, Seed),
     {ok, F} = file:open(OutFile, [write]),
     Nodes = lists:foldl(fun(R, Acc) -> round(R, Events, Acc, F) end, #{}, lists:seq(0, Rounds - 1)),
+    %% the sets v1 buckets SCAMP v1's membership set is ordered by (App. A Q1)
+    ok = psim_harness:write_buckets(F, N),
     [io:format(F, "V ~b ~s~n", [Id, string:join([integer_to_list(psim_harness:id_of(P)) || P <- M], " ")])
      || {Id, #{up := true, members := M}} <- lists:sort(maps:to_list(Nodes))],
     file:close(F).

@@ -10,7 +10,7 @@
 -export([create/1, join/3, crash/2, revive/2, leave/2, leave_node/3, broadcast/3, step/2, active/2, members/3,
          delivery/2, histograms/1, snapshot/1, restore/2, set_partition/2, clear_partition/1, node/2,
          begin_send_omission/3, end_send_omission/3, begin_receive_omission/3, end_receive_omission/3,
-         begin_omission/2, end_omission/2, clear_faults/1, msg_slots/1]).
+         begin_omission/2, end_omission/2, clear_faults/1, msg_slots/1, set_bucket_table/2, phash_buckets/2]).
 -on_load(init/0).
 
 %% back-off of a busy handle: 1 ms sleeps, at most ~10 s in all
@@ -56,6 +56,13 @@ set_partition(Sim, Groups) ->
     Bin = << <<G:8>> || G <- Groups >>,
     call(fun() -> set_partition_nif(Sim, Bin) end).
 clear_partition(Sim) -> call(fun() -> clear_partition_nif(Sim) end).
+%% the sets v1 order of every view (SURVEY App. A Q1): one bucket per node,
+%% erlang:phash(NodeSpec, 16) - 1, before the first step
+set_bucket_table(Sim, Buckets) ->
+    Bin = << <<B:8>> || B <- Buckets >>,
+    call(fun() -> set_bucket_table_nif(Sim, Bin) end).
+%% that table for node specs Spec(0) .. Spec(N - 1), computed by this VM
+phash_buckets(N, Spec) -> [erlang:phash(Spec(I), 16) - 1 || I <- lists:seq(0, N - 1)].
 %% one node: {ok, #{up, epoch, active, passive, have, round}}
 node(Sim, Node) -> call(fun() -> node_nif(Sim, Node) end).
 %% the live message slots: {ok, [{Slot, MsgId, RootId}]} -- delivery bit
@@ -105,6 +112,7 @@ active_nif(_S, _N) -> erlang:nif_error(nif_not_loaded).
 members_nif(_S, _N, _K) -> erlang:nif_error(nif_not_loaded).
 delivery_nif(_S, _N) -> erlang:nif_error(nif_not_loaded).
 clear_partition_nif(_S) -> erlang:nif_error(nif_not_loaded).
+set_bucket_table_nif(_S, _B) -> erlang:nif_error(nif_not_loaded).
 clear_faults_nif(_S) -> erlang:nif_error(nif_not_loaded).
 node_nif(_S, _N) -> erlang:nif_error(nif_not_loaded).
 msg_slots_nif(_S) -> erlang:nif_error(nif_not_loaded).

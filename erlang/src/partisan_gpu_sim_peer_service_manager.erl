@@ -113,7 +113,12 @@ init([]) ->
             manager => case partisan_config:get(sim_xbot, false) of true -> 2; _ -> 0 end,
             xbot_period => partisan_config:get(sim_xbot_period, 35)},
     {ok, Sim} = case partisan_config:get(sim_handle, undefined) of
-                    undefined -> partisan_gpu_sim:create(Cfg);
+                    undefined ->
+                        {ok, H0} = partisan_gpu_sim:create(Cfg),
+                        %% views in this VM's sets v1 order (SURVEY App. A Q1):
+                        %% erlang:phash/2 of every simulated node_spec
+                        ok = partisan_gpu_sim:set_bucket_table(H0, partisan_gpu_sim:phash_buckets(N, fun spec/1)),
+                        {ok, H0};
                     H -> {ok, H}
                 end,
     %% the node starts at join/1 (or start_seed/0): one start per node
@@ -232,6 +237,11 @@ flood(Seen, Frontier, TTL, Sim) ->
     flood(Seen ++ Next, Next, TTL - 1, Sim).
 
 name(Id) -> list_to_atom(lists:flatten(io_lib:format("n~10..0B@sim", [Id]))).
+%% the node_spec of simulated node Id (the harness's, DESIGN.md section 2)
+spec(Id) ->
+    #{name => name(Id),
+      listen_addrs => [#{ip => {10, (Id bsr 16) band 255, (Id bsr 8) band 255, Id band 255}, port => 9090}],
+      channels => [undefined], parallelism => 1}.
 id(Name) when is_atom(Name) ->
     [$n | Rest] = atom_to_list(Name),
     list_to_integer(lists:takewhile(fun(C) -> C >= $0 andalso C =< $9 end, Rest));

@@ -34,6 +34,9 @@
  *       one BSP round of every node's timers and inbox:
  *       hyparview handle_message/2 (:693-1166), handle_info timers (:542-607),
  *       plumtree handle_cast/2 (:282-336), lazy_tick (:341-345)
+ *   psim_set_bucket_table
+ *       the sets v1 order of every view: sets:to_list/1 yields bucket
+ *       erlang:phash(NodeSpec, 16) 1..16, oldest first   (hyparview:1230-1231, :1346-1361)
  *   psim_get_nodes
  *       debug getters active/0, passive/0 (hyparview:261-281),
  *       plumtree debug_get_peers/2,3 (:222-231), broadcast_members/0 (:188-195)
@@ -64,7 +67,7 @@
 extern "C" {
 #endif
 
-#define PSIM_ABI_VERSION 9
+#define PSIM_ABI_VERSION 10
 
 /* error codes */
 #define PSIM_OK 0
@@ -351,6 +354,19 @@ int psim_leave(psim_handle *h, const uint32_t *nodes, size_t n);
  * PSIM_EUNSUPPORTED for HyParView handles. */
 int psim_leave_node(psim_handle *h, const uint32_t *actors, const uint32_t *targets, size_t n);
 int psim_set_partition(psim_handle *h, const uint8_t *group, size_t n);
+/* View order.  Views are kept in sets:to_list/1 order of
+ * OTP's sets v1 (<= 80 elements: 16 buckets, yielded bucket 1..16, oldest
+ * first within a bucket), so every select_random index and every shuffle
+ * key pairing (hyparview:1230-1231, :1346-1361; scamp_v1's membership) depends
+ * on the bucket of each element, erlang:phash(NodeSpec, 16).  buckets[i] =
+ * that bucket - 1 (0..15) for node i, n = n_nodes -- e.g. the table the
+ * in-BEAM harness exports (erlang/harness, `B id bucket` lines).  Without a
+ * table the handle uses a stand-in (low 4 bits of murmur3 fmix32(id)).
+ * Valid only before the first round (PSIM_ESTATE after); buckets == NULL
+ * restores the stand-in.  Multi-rank handles: every rank passes the same
+ * table.  Not part of psim_snapshot: set it on the new handle before
+ * psim_restore. */
+int psim_set_bucket_table(psim_handle *h, const uint8_t *buckets, size_t n);
 int psim_clear_partition(psim_handle *h);
 /* Omission faults of the pluggable manager's interposition layer
  * (add_interposition_fun/2, remove_interposition_fun/1 pluggable:297-326;
@@ -431,12 +447,15 @@ uint32_t psim_xbot_latency(uint64_t seed, uint32_t a, uint32_t b);
 
 /* Wire format of a partisan peer connection, for mixed
  * clusters of real and simulated nodes: a frame is {packet, 4} -- a 4-byte
- * big-endian length (peer_service_client.erl:214) -- around term_to_binary/1
- * of the message (client:253-257, peer_service_server.erl:172-182).  A
+ * big-endian length (peer_service_client.erl:214) -- around
+ * partisan_util:term_to_iolist/1 of the message -- what the connection's
+ * send path writes (client:95, :130, :275; util:235-297; the receiver,
+ * peer_service_server.erl:172-182, takes any term encoding).  A
  * record is the engine's 64-B message record (words: dst, src,
  * type | ttl << 8 | nex << 16, seq, a0, a1, a2, a3, ex[0..8)); its term is
  * the one the reference's handler sends (HyParView hv:506-1131, Plumtree as
- * {forward_message, partisan_plumtree_broadcast, Msg} hv:441-460 with the
+ * {forward_message, partisan_plumtree_broadcast, {'$gen_cast', Msg}}
+ * (cast_message/3 hv:147-154, forward_message hv:441-460) with the
  * backend's heartbeat ids {RootName, Counter}, X-BOT xbot:1171-1314; the
  * table is in partisan_amd/csrc/psim_wire.cpp).  Node id i is the node_spec
  * #{name => '<prefix><i>@<host>', listen_addrs => [#{ip => ip_base + i,
@@ -466,6 +485,15 @@ int psim_kernel_times(psim_handle *h, const char **names, double *ms, uint64_t *
 /* RCCL bootstrap for multi-process sharding (rank 0 creates, all pass it in cfg). */
 int psim_comm_id_size(void);
 int psim_get_comm_id(void *buf, size_t cap);
+/* TEST VEHICLE, not a product backend: the id of a new loopback world
+ * (psim_comm_id_size() bytes).  Handles created with it as cfg.comm_id
+ * (shard_world = W, shard_rank = r, all on one device, in this process) run
+ * the multi-rank code path -- owner partition, count all-to-all, record
+ * exchange, stats reduce, leave/1 stop-list gather, overlay gathers -- with
+ * device copies and a host barrier in place of RCCL, so it can run where
+ * RCCL cannot (one GPU).  The W ranks are W host threads, each making the
+ * same calls as RCCL ranks would (collective calls must be concurrent). */
+int psim_loopback_comm_id(void *buf, size_t cap);
 
 #ifdef __cplusplus
 }

@@ -133,6 +133,7 @@ struct psim_handle {
      * nx_* are the next round's (the API edits them, round_begin adopts them) */
     struct fault_set { uint64_t *send, *recv; size_t send_n, recv_n; uint8_t *faulted; } flt, nx;
     int faults_dirty;
+    uint8_t *btab;                  /* sets v1 bucket per node (orc_set_bucket_table), NULL = stand-in */
 };
 
 /* per-node execution context */
@@ -180,11 +181,16 @@ static uint64_t uniform_key(ctx *c) { return draw58(c) >> 5; }
 /* ------------------------------------------------------- sets v1 order -- */
 /* OTP sets (v1) with <= 80 elements: 16 buckets, element prepended in its
  * bucket, to_list yields bucket 1..16, oldest first.
- * bucket16() stands in for erlang:phash(NodeSpec, 16): see DESIGN.md. */
-static uint32_t bucket16(uint32_t id) {
+ * bucket16() is erlang:phash(NodeSpec, 16) - 1 from the handle's table
+ * (orc_set_bucket_table, e.g. exported by the in-BEAM harness); without one
+ * the stand-in below (murmur3 fmix32 of the id): see DESIGN.md. */
+static uint32_t bucket16_default(uint32_t id) {
     uint32_t h = id;
     h ^= h >> 16; h *= 0x85EBCA6Bu; h ^= h >> 13; h *= 0xC2B2AE35u; h ^= h >> 16;
     return h & 15u;
+}
+static uint32_t bucket16(const struct psim_handle *h, uint32_t id) {
+    return h->btab ? h->btab[id] : bucket16_default(id);
 }
 
 static int list_member(const uint32_t *l, uint32_t n, uint32_t e) {
@@ -194,11 +200,11 @@ static int list_member(const uint32_t *l, uint32_t n, uint32_t e) {
 }
 
 /* sets:add_element/2 */
-static void set_add(uint32_t *l, uint32_t *n, uint32_t e) {
+static void set_add(const struct psim_handle *h, uint32_t *l, uint32_t *n, uint32_t e) {
     if (list_member(l, *n, e)) return;
-    uint32_t b = bucket16(e), pos = *n;
+    uint32_t b = bucket16(h, e), pos = *n;
     for (uint32_t i = 0; i < *n; i++)
-        if (bucket16(l[i]) > b) { pos = i; break; }
+        if (bucket16(h, l[i]) > b) { pos = i; break; }
     for (uint32_t i = *n; i > pos; i--) l[i] = l[i - 1];
     l[pos] = e;
     (*n)++;
@@ -469,7 +475,7 @@ static void add_to_passive(ctx *c, uint32_t p) {
         uint32_t r = select_random(c, s->pas, s->pas_n, omit, 1);
         if (r != PSIM_NONE) set_del(s->pas, &s->pas_n, r);
     }
-    set_add(s->pas, &s->pas_n, p);
+    set_add(c->h, s->pas, &s->pas_n, p);
 }
 
 /* drop_random_element_from_active_view/1, hyparview:1467-1512 (no reservations) */
@@ -498,7 +504,7 @@ static void add_to_active(ctx *c, uint32_t p) {
     if (s->act_n >= c->h->cfg.max_active_size) drop_random_active(c);
     int had = conn_find(s, p) >= 0;
     conn_del(s, p);
-    set_add(s->act, &s->act_n, p);
+    set_add(c->h, s->act, &s->act_n, p);
     if (!had) conn_add(c, p | PSIM_CONN_DOWN);
 }
 
@@ -1348,7 +1354,7 @@ static uint32_t random_0_or_1(ctx *c) { return uniform_n(c, 10) >= 5 ? 1u : 0u; 
 static void scamp_add(ctx *c, uint32_t *l, uint32_t *n, uint32_t e, int as_set) {
     if (as_set && list_member(l, *n, e)) return;
     if (*n >= PSIM_SVIEW_CAP) { ovf(c, PSIM_OVF_STRATEGY); return; }
-    if (as_set) { set_add(l, n, e); return; }
+    if (as_set) { set_add(c->h, l, n, e); return; }
     for (uint32_t i = *n; i > 0; i--) l[i] = l[i - 1];
     l[0] = e;
     (*n)++;
@@ -1765,6 +1771,7 @@ void orc_destroy(struct psim_handle *h) {
     free(h->sn); free(h->fbits); free(h->pay_in); free(h->pay_out);
     free(h->flt.send); free(h->flt.recv); free(h->flt.faulted);
     free(h->nx.send); free(h->nx.recv); free(h->nx.faulted);
+    free(h->btab);
     free(h);
 }
 
@@ -2106,7 +2113,20 @@ void orc_philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0,
                 uint32_t out[4]) {
     philox(c0, c1, c2, c3, k0, k1, out);
 }
-uint32_t orc_bucket16(uint32_t id) { return bucket16(id); }
+uint32_t orc_bucket16(uint32_t id) { return bucket16_default(id); }
+
+/* psim_set_bucket_table */
+int orc_set_bucket_table(struct psim_handle *h, const uint8_t *buckets, size_t n) {
+    if (!h) return PSIM_EINVAL;
+    if (h->round != 0) return PSIM_ESTATE;
+    if (!buckets) { free(h->btab); h->btab = NULL; return PSIM_OK; }
+    if (n != h->N) return PSIM_EINVAL;
+    for (size_t i = 0; i < n; i++)
+        if (buckets[i] > 15) return PSIM_EINVAL;
+    if (!h->btab && !(h->btab = (uint8_t *)malloc(n))) return PSIM_ENOMEM;
+    memcpy(h->btab, buckets, n);
+    return PSIM_OK;
+}
 
 /* ---------------------------------------------- sharded protocol (tests) --
  * One oracle per rank owns [lo, hi); a round is orc_round_emit (events +

@@ -8,7 +8,7 @@ import ctypes as C
 
 import numpy as np
 
-PSIM_ABI_VERSION = 9
+PSIM_ABI_VERSION = 10
 PSIM_MAP_BIT = 0x80000000
 PSIM_NONE = 0xFFFFFFFF
 ACTIVE_CAP, PASSIVE_CAP, IDMAP_CAP = 8, 32, 64
@@ -137,6 +137,7 @@ SIGNATURES = {
     "leave_node": (C.c_int, [_H, _P32, _P32, C.c_size_t]),
     "set_partition": (C.c_int, [_H, C.POINTER(C.c_uint8), C.c_size_t]),
     "clear_partition": (C.c_int, [_H]),
+    "set_bucket_table": (C.c_int, [_H, C.POINTER(C.c_uint8), C.c_size_t]),
     "set_omission": (C.c_int, [_H, C.c_int, _P32, _P32, C.c_size_t, C.c_int]),
     "set_faulted": (C.c_int, [_H, _P32, C.c_size_t, C.c_int]),
     "clear_faults": (C.c_int, [_H]),
@@ -159,6 +160,7 @@ GPU_ONLY = {
                                C.POINTER(C.c_uint64), C.c_int]),
     "comm_id_size": (C.c_int, []),
     "get_comm_id": (C.c_int, [C.c_void_p, C.c_size_t]),
+    "loopback_comm_id": (C.c_int, [C.c_void_p, C.c_size_t]),
     "snapshot": (C.c_int, [_H, C.c_void_p, C.c_size_t, C.POINTER(C.c_size_t)]),
     "restore": (C.c_int, [_H, C.c_void_p, C.c_size_t]),
 }

@@ -494,7 +494,7 @@ DEV void add_to_passive(Wv& w, uint32_t p) {             // hv:1423-1448
         uint32_t k = uniform_n(w, w.pas_n) - 1;
         vdel(w.P, w.pas_n, k);
     }
-    view_add(w.P, w.pas_n, p);
+    view_add(kargs().btab, w.P, w.pas_n, p);
     w.vd |= 2u;
 }
 
@@ -520,7 +520,7 @@ DEV void add_to_active(Wv& w, uint32_t p) {              // hv:1371-1420
     if (w.act_n >= kargs().max_active) drop_random_active(w);
     const bool had = w.conn_n && conn_find(w, p) >= 0;
     if (had) conn_del(w, p);
-    view_add(w.A, w.act_n, p);
+    view_add(kargs().btab, w.A, w.act_n, p);
     w.vd |= 1u;
     if (!had) conn_add(w, p | PSIM_CONN_DOWN);
 }
@@ -560,7 +560,8 @@ DEV void merge_exchange(Wv& w, uint32_t EX, uint32_t nex) {
         for (uint32_t i = 0; i < mt; i++) add_to_passive(w, rl(T, i));
         return;
     }
-    uint32_t PB = l < w.pas_n ? bucket16(w.P) : 0u;
+    const uint8_t* bt = kargs().btab;
+    uint32_t PB = l < w.pas_n ? bucket16(bt, w.P) : 0u;
     uint32_t used = 0;
     for (uint32_t i = 0; i < mt; i++) {
         const uint32_t t = rl(T, i);
@@ -571,7 +572,7 @@ DEV void merge_exchange(Wv& w, uint32_t EX, uint32_t nex) {
             vdel(PB, n2, k);
             vdel(w.P, w.pas_n, k);
         }
-        const uint32_t b = bucket16(t);
+        const uint32_t b = bucket16(bt, t);
         const uint32_t pos = popc(ballot(l < w.pas_n && PB <= b));
         uint32_t n2 = w.pas_n;
         vins(PB, n2, pos, b);

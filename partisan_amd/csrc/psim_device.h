@@ -161,11 +161,17 @@ __device__ __forceinline__ uint64_t draw58_at(uint64_t ctr, uint32_t node, uint6
     return ((((uint64_t)o1) << 32) | o0) >> 6;
 }
 
-// sets v1 bucket of an element (stand-in for erlang:phash(NodeSpec, 16))
-__host__ __device__ __forceinline__ uint32_t bucket16(uint32_t id) {
+// sets v1 bucket of an element: erlang:phash(NodeSpec, 16) - 1 from the
+// handle's bucket table (psim_set_bucket_table: one byte per global id,
+// replicated on every shard), or, without one, the default stand-in -- the
+// low 4 bits of murmur3's fmix32 of the id
+__host__ __device__ __forceinline__ uint32_t bucket16_default(uint32_t id) {
     uint32_t h = id;
     h ^= h >> 16; h *= 0x85EBCA6Bu; h ^= h >> 13; h *= 0xC2B2AE35u; h ^= h >> 16;
     return h & 15u;
+}
+__host__ __device__ __forceinline__ uint32_t bucket16(const uint8_t* tab, uint32_t id) {
+    return tab ? (uint32_t)tab[id] : bucket16_default(id);
 }
 
 // digest multiplier of record word j (oracle msg_hash): odd, position-distinct

@@ -16,7 +16,8 @@
 //            G  > 1: stable partition by owner shard -> gather records ->
 //                    all-to-all (counts, then records) -> the same grouping
 //                    of the shard-ordered concatenation by dst
-//   stats    k_stats_tiles + k_stats_final (+ sum over shards / ncclAllReduce)
+//   stats    k_stats_tiles + k_stats_final (+ sum over shards / the ranks' all-reduce)
+// Ranks exchange through psim_comm.h: RCCL, or the loopback test vehicle.
 // Grouping a (src, seq)-ordered stream -- or a concatenation ordered by
 // source shard -- by dst, each group in stream order, yields each inbox in
 // canonical (src, seq) order,
@@ -32,6 +33,7 @@
 #include <set>
 #include <vector>
 
+#include "psim_comm.h"
 #include "psim_device.h"
 #include "psim_kernels.h"
 
@@ -55,16 +57,6 @@ constexpr uint32_t BATCH_MAX = 64;
             std::fprintf(stderr, "psim: %s failed: %s (%s:%d)\n", #x,    \
                          hipGetErrorString(e_), __FILE__, __LINE__);     \
             return PSIM_EDEVICE;                                         \
-        }                                                                \
-    } while (0)
-
-#define NCCL_TRY(x)                                                      \
-    do {                                                                 \
-        ncclResult_t r_ = (x);                                           \
-        if (r_ != ncclSuccess) {                                         \
-            std::fprintf(stderr, "psim: %s failed: %s (%s:%d)\n", #x,    \
-                         ncclGetErrorString(r_), __FILE__, __LINE__);    \
-            return PSIM_ECOMM;                                           \
         }                                                                \
     } while (0)
 
@@ -1157,6 +1149,7 @@ struct Shard {
     // replicated (global id)
     DBuf<uint8_t> flags, part;
     DBuf<uint32_t> crash_bits;   // RoundArgs::crash_bits
+    DBuf<uint8_t> btab;          // RoundArgs::btab (psim_set_bucket_table), global id
     // local rows
     DBuf<Hdr> hdr;
     DBuf<uint32_t> act, pas, pt_all, pt_com, pt_eag, pt_laz, pt_rt, start;
@@ -1187,9 +1180,6 @@ struct Shard {
     DBuf<uint4> desc, desc_slow, desc_pt, desc_shuf, desc_lite, desc_ptl;   // work descriptors; those k_relay leaves to k_consume / k_pt / k_shuf
     DBuf<uint64_t> bound, pscan, obase, stat_part, stat_out, stat_tile, d_off;   // bound: packed (bound << 32 | work)
     DBuf<uint8_t> cub_tmp;              // the scan's tile totals
-    DBuf<uint32_t> scan_stat;           // single-pass scan (k_scan_lb): [0] the ticket counter, [1] give-ups,
-    DBuf<uint64_t> scan_val;            //   the epoch-tagged words per tile
-    uint32_t scan_tick = 0, scan_epoch = 0;
     DBuf<uint32_t> ev_ids, ev_contacts, stop_ids, n_stop;
     bool tomb_live = false;             // full: snapshots carry their remove rows
     DBuf<Msg> sendbuf;
@@ -1241,9 +1231,13 @@ struct psim_handle {
     uint32_t lite_blocks = 1024;        // ... and k_consume_lite blocks
     uint32_t ptl_blocks = 1024;         // ... and k_ptl blocks
     uint64_t round = 0;
+    // a round failed half-way (psim_step returned an error from inside a
+    // round or batch): the state is not a round boundary any more, so every
+    // later psim_step answers PSIM_ESTATE instead of running on it
+    bool failed = false;
     std::vector<Shard*> shards;         // shards owned by this process
     int rank = 0, world = 1;
-    ncclComm_t comm = nullptr;
+    Comm* comm = nullptr;               // world > 1: RCCL (or the loopback test vehicle), psim_comm.h
     DBuf<uint64_t> comm_cnt;            // RCCL: [send counts | recv counts]
     // pending events
     std::vector<uint32_t> pend_crash, pend_join, pend_contact;
@@ -1254,6 +1248,7 @@ struct psim_handle {
     std::vector<uint32_t> pend_b_root, pend_b_msg;    // broadcasts of the next round, in call order
     uint32_t slot_tab[2 * PSIM_MSG_SLOTS];            // slot k: msg id [k], root [PSIM_MSG_SLOTS + k]
     uint32_t tracked_msg = PSIM_NONE;
+    bool btab = false;                  // psim_set_bucket_table: the shards' btab rows are in use
     uint32_t fw = 0;                    // full strategy: words per member row (adds; removes beside)
     bool tomb = false;                  // full: an ORSet remove exists (leave/1): kernels read remove rows
     std::vector<uint8_t> started;       // full strategy: ids ever started (no restarts)
@@ -1294,6 +1289,7 @@ RoundArgs make_args(psim_handle* h, Shard* s) {
     a.origin = s->origin.p;
     a.slots = s->slots.p;
     a.flags = s->flags.p; a.part = s->part.p; a.hdr = s->hdr.p; a.crash_bits = s->crash_bits.p;
+    a.btab = h->btab ? s->btab.p : nullptr;
     a.act = s->act.p; a.pas = s->pas.p; a.sentm = s->sentm.p; a.recvm = s->recvm.p;
     a.mapx = s->mapx.p; a.mapx_top = s->mapx_top.p;
     a.mapx_rows = (uint32_t)(s->mapx.n / IDMAP_EXT);
@@ -1426,178 +1422,14 @@ __global__ void __launch_bounds__(BLK) k_scan_apply(const T* __restrict__ in, T*
     }
 }
 
-// Single pass (decoupled look-back): a block takes the next tile through a
-// ticket counter (tiles start in launch order, so a block only ever waits on
-// tiles of blocks already running), publishes the tile total, then finds its
-// prefix by summing its predecessors' published values a wave at a time,
-// back to the nearest inclusive prefix, and publishes that.  Every published
-// word is self-validating -- 32 bits of the value under the scan's epoch in
-// the high half, stored and loaded as one device-coherent 64-bit word -- so no
-// release/acquire fence is needed (on gfx950 an agent-scope release writes
-// back the whole L2: 60 us a scan, measured).  Slot (t, kind) holds
-// sizeof(T) / 4 words at val[((2 t + kind) * NW + w]; kind 0 = the tile
-// total, 1 = the inclusive prefix; a word of another epoch (an earlier scan)
-// reads as not yet published.  One launch and one read of the input where the
-// reduce-then-scan took three launches (~5 us each at 2^20 nodes).
-template <typename T>
-struct ScanSlot {
-    static constexpr uint32_t NW = sizeof(T) / 4;
-    __device__ static void put(uint64_t* val, uint32_t t, uint32_t kind, T v, uint32_t epoch) {
-#pragma unroll
-        for (uint32_t w = 0; w < NW; w++)
-            __hip_atomic_store(&val[(2 * (size_t)t + kind) * NW + w],
-                               (uint64_t)epoch << 32 | (uint32_t)((uint64_t)v >> (32 * w)), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-    }
-    __device__ static bool get(const uint64_t* val, uint32_t t, uint32_t kind, T& v, uint32_t epoch) {
-        uint64_t x = 0;
-        bool ok = true;
-#pragma unroll
-        for (uint32_t w = 0; w < NW; w++) {
-            const uint64_t y = __hip_atomic_load(&val[(2 * (size_t)t + kind) * NW + w], __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_AGENT);
-            ok &= (uint32_t)(y >> 32) == epoch;
-            x |= (uint64_t)(uint32_t)y << (32 * w);
-        }
-        v = (T)x;
-        return ok;
-    }
-};
-
-// One tile of the single-pass scan (every thread of the block): loads the
-// thread's SCAN_ITEMS consecutive inputs into x, returns the exclusive prefix
-// of the first of them; *b0 = that element's index, *tile = the tile
-template <typename T>
-__device__ T scan_tile_lb(const T* __restrict__ in, uint32_t n, uint32_t* tick, uint32_t base, uint64_t* val,
-                          uint32_t epoch, T (&x)[SCAN_ITEMS], size_t* b0_out, uint32_t* tile) {
-    __shared__ uint32_t s_tile;
-    __shared__ T s_pre;
-    if (threadIdx.x == 0) s_tile = atomicAdd(tick, 1u) - base;
-    __syncthreads();
-    const uint32_t t = s_tile;
-    const size_t b0 = (size_t)t * SCAN_TILE + (size_t)threadIdx.x * SCAN_ITEMS;
-    *b0_out = b0;
-    *tile = t;
-    T v = 0;
-#pragma unroll
-    for (uint32_t k = 0; k < SCAN_ITEMS; k++) {
-        x[k] = b0 + k < n ? in[b0 + k] : T(0);
-        v += x[k];
-    }
-    T tot;
-    T run = block_excl(v, &tot);
-    if (threadIdx.x < 64) {
-        const uint32_t l = threadIdx.x;
-        if (l == 0) ScanSlot<T>::put(val, t, t == 0 ? 1u : 0u, tot, epoch);
-        T pre = 0;
-        uint32_t spins = 0;
-        for (uint32_t hi = t; hi > 0;) {                // lane l: tile hi - 1 - l
-            const int64_t j = (int64_t)hi - 1 - (int64_t)l;
-            uint32_t st = 2;                            // (before tile 0: an inclusive 0)
-            T vv = 0;
-            if (j >= 0) {
-                st = ScanSlot<T>::get(val, (uint32_t)j, 1, vv, epoch) ? 2u
-                   : ScanSlot<T>::get(val, (uint32_t)j, 0, vv, epoch) ? 1u : 0u;
-            }
-            const uint64_t inc = __ballot(st == 2), ready = __ballot(st != 0);
-            const uint32_t lim = inc ? (uint32_t)__ffsll((long long)inc) - 1 : 63;   // lanes 0..lim count
-            const uint64_t need = lim == 63 ? ~0ull : ((2ull << lim) - 1);
-            if ((ready & need) != need) {               // a predecessor has not published yet
-                // (never past ~1 s: a lost word would hang the device -- give up
-                // loudly instead: tick[1] counts it, the prefix is wrong)
-                if (++spins > (1u << 22)) {
-                    if (l == 0) atomicAdd(tick + 1, 1u);
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(1);
-                continue;
-            }
-            if (l > lim) vv = 0;
-#pragma unroll
-            for (int d = 32; d > 0; d >>= 1) vv += __shfl_xor(vv, d);
-            pre += vv;
-            if (inc) break;
-            hi = hi > 64 ? hi - 64 : 0;
-        }
-        if (l == 0) {
-            if (t > 0) ScanSlot<T>::put(val, t, 1, pre + tot, epoch);
-            s_pre = pre;
-        }
-    }
-    __syncthreads();
-    return run + s_pre;
-}
-
-template <typename T>
-__global__ void __launch_bounds__(BLK) k_scan_lb(const T* __restrict__ in, T* __restrict__ out, uint32_t n,
-                                                 uint32_t* tick, uint32_t base, uint64_t* val, uint32_t epoch) {
-    T x[SCAN_ITEMS];
-    size_t b0;
-    uint32_t t;
-    T run = scan_tile_lb<T>(in, n, tick, base, val, epoch, x, &b0, &t);
-#pragma unroll
-    for (uint32_t k = 0; k < SCAN_ITEMS; k++) {
-        if (b0 + k < n) out[b0 + k] = run;
-        run += x[k];
-    }
-}
-
-// prepare's scan and k_desc in one pass: the packed (bound << 32 | work)
-// words of nodes [0, n_local] scanned in a single pass (k_scan_lb's tile) and
-// each node's outbox base and descriptor written from its prefix at once --
-// no pscan array, one launch instead of two (same entries as k_desc)
-__global__ void __launch_bounds__(BLK) k_scan_desc(const uint64_t* __restrict__ packed, uint32_t* tick, uint32_t base,
-                                                   uint64_t* val, uint32_t epoch,
-                                                   const uint32_t* __restrict__ in_beg,
-                                                   const unsigned long long* __restrict__ cb,
-                                                   const uint32_t* __restrict__ start, RoundArgs a,
-                                                   uint4* __restrict__ desc, uint64_t* __restrict__ obase,
-                                                   uint32_t* nact, const unsigned long long* btot, uint32_t nbt,
-                                                   uint64_t* hout, uint64_t cap, uint32_t* ctl) {
-    uint64_t x[SCAN_ITEMS];
-    size_t b0;
-    uint32_t t;
-    // (every block takes its ticket and publishes, an aborted batch too: the
-    // look-back of the later tiles waits on it)
-    uint64_t run = scan_tile_lb<uint64_t>(packed, a.n_local + 1, tick, base, val, epoch, x, &b0, &t);
-    const unsigned long long tot = t == a.n_local / SCAN_TILE ? btot_sum(btot, nbt) : 0ull;   // (uniform)
-    if (*ctl) return;
-#pragma unroll
-    for (uint32_t k = 0; k < SCAN_ITEMS; k++) {
-        if (b0 + k <= a.n_local)
-            desc_entry(a, (uint32_t)(b0 + k), run, x[k], in_beg, cb, start, desc, obase, nact, tot, hout, cap, ctl);
-        run += x[k];
-    }
-}
-
-// the look-back state for nt tiles (zeroed when it grows: no epoch is 0)
-int scan_state(Shard* s, uint32_t nt) {
-    if (s->scan_stat.n >= 2 && s->scan_val.n >= 4 * (size_t)nt) return PSIM_OK;
-    HIP_TRY(hipStreamSynchronize(s->stream));
-    TRY(s->scan_stat.ensure(2));
-    TRY(s->scan_val.ensure(4 * (size_t)nt));
-    HIP_TRY(hipMemsetAsync(s->scan_stat.p, 0, s->scan_stat.n * sizeof(uint32_t), s->stream));
-    HIP_TRY(hipMemsetAsync(s->scan_val.p, 0, s->scan_val.n * sizeof(uint64_t), s->stream));
-    s->scan_tick = 0;
-    return PSIM_OK;
-}
-
 template <typename T>
 int scan_excl(Shard* s, const T* in, T* out, uint32_t n) {
-    // the reduce-then-scan by default: the single-pass look-back (PSIM_SCAN_LB=1)
-    // measured 1.5 % slower a step at 2^20 (profiles/r03/p25: its device-coherent
-    // status loads cost more than the two launches it saves)
-    static const bool three = getenv("PSIM_SCAN_LB") == nullptr;
+    // (a single-pass decoupled look-back measured 1.5 % slower a step at
+    // 2^20, profiles/r03/p25: its device-coherent status loads cost more than
+    // the two launches it saves; removed in round 4)
     const uint32_t nt = (uint32_t)(((uint64_t)n + SCAN_TILE - 1) / SCAN_TILE);
     if (nt <= 1) {
         k_scan_apply<T><<<1, BLK, 0, s->stream>>>(in, out, n, nullptr);
-    } else if (!three) {
-        TRY(scan_state(s, nt));
-        if (!++s->scan_epoch) s->scan_epoch = 1;        // (0: the zeroed state, never an epoch)
-        static_assert(sizeof(T) == 4 || sizeof(T) == 8, "scan values are 32 or 64 bits");
-        k_scan_lb<T><<<nt, BLK, 0, s->stream>>>(in, out, n, s->scan_stat.p, s->scan_tick, s->scan_val.p,
-                                                s->scan_epoch);
-        s->scan_tick += nt;
     } else {
         TRY(s->cub_tmp.ensure((size_t)nt * sizeof(T)));
         T* sums = reinterpret_cast<T*>(s->cub_tmp.p);
@@ -1609,25 +1441,13 @@ int scan_excl(Shard* s, const T* in, T* out, uint32_t n) {
     return PSIM_OK;
 }
 
-// prepare's scan + descriptors: the scan then k_desc, or (PSIM_SCAN_LB=1)
-// k_scan_desc
+// prepare's scan + descriptors: the scan, then k_desc
 int scan_desc(Shard* s, const RoundArgs& a) {
-    static const bool three = getenv("PSIM_SCAN_LB") == nullptr;
     const uint32_t n1 = a.n_local + 1;
-    const uint32_t nt = (n1 + SCAN_TILE - 1) / SCAN_TILE;
-    if (three) {
-        TRY(scan_excl(s, s->bound.p, s->pscan.p, n1));
-        k_desc<<<grid_for(n1), BLK, 0, s->stream>>>(s->bound.p, s->pscan.p, s->in_beg.p, s->cb.p, s->start.p, a,
-                                                     s->desc.p, s->obase.p, s->d_nact.p, s->btot.p, s->pgrid, s->pin_dev,
-                                                     s->desc_cap, s->ctl.p);
-    } else {
-        TRY(scan_state(s, nt));
-        if (!++s->scan_epoch) s->scan_epoch = 1;
-        k_scan_desc<<<nt, BLK, 0, s->stream>>>(s->bound.p, s->scan_stat.p, s->scan_tick, s->scan_val.p, s->scan_epoch,
-                                               s->in_beg.p, s->cb.p, s->start.p, a, s->desc.p, s->obase.p,
-                                               s->d_nact.p, s->btot.p, s->pgrid, s->pin_dev, s->desc_cap, s->ctl.p);
-        s->scan_tick += nt;
-    }
+    TRY(scan_excl(s, s->bound.p, s->pscan.p, n1));
+    k_desc<<<grid_for(n1), BLK, 0, s->stream>>>(s->bound.p, s->pscan.p, s->in_beg.p, s->cb.p, s->start.p, a,
+                                                 s->desc.p, s->obase.p, s->d_nact.p, s->btot.p, s->pgrid, s->pin_dev,
+                                                 s->desc_cap, s->ctl.p);
     HIP_TRY(hipGetLastError());
     return PSIM_OK;
 }
@@ -1747,7 +1567,7 @@ int phase_events_prepare(psim_handle* h, Shard* s, const RoundCtl& ctl, RoundArg
         TRY(scan_desc(s, a));
         if (batched) goto args;
         TRY(stream_wait(s));                          // (k_desc stored the total in pin)
-        if (s->pin[PIN_BIGIN]) return PSIM_ENOMEM;    // a node's inbox count must fit 27 bits
+        if (s->pin[PIN_BIGIN]) { s->pin[PIN_BIGIN] = 0; return PSIM_ENOMEM; }   // an inbox count must fit 27 bits
         const uint64_t total = s->pin[PIN_TOTAL];
         if (total >= 0xFFFFFFFFull) return PSIM_ENOMEM;
         // the bound peaks on broadcast rounds and creeps up for many rounds:
@@ -2055,7 +1875,7 @@ int exchange_rccl(psim_handle* h) {
     {
         KTimer t(h, s, KT_EXCHANGE);
         // (k_owner_offsets wrote this rank's counts into comm_cnt[0, G))
-        NCCL_TRY(ncclAllToAll(h->comm_cnt.p, h->comm_cnt.p + G, 1, ncclUint64, h->comm, s->stream));
+        TRY(h->comm->all_to_all_u64(h->comm_cnt.p, h->comm_cnt.p + G, 1, s->stream));
         std::vector<uint64_t> rcnt(G);
         HIP_TRY(hipMemcpyAsync(rcnt.data(), h->comm_cnt.p + G, G * 8, hipMemcpyDeviceToHost, s->stream));
         HIP_TRY(hipMemcpyAsync(s->soff.data(), s->d_off.p, (G + 1) * 8, hipMemcpyDeviceToHost, s->stream));
@@ -2066,17 +1886,13 @@ int exchange_rccl(psim_handle* h) {
         for (uint32_t g = 0; g < G; g++) { roff[g] = m; m += rcnt[g]; }
         TRY(s->recvbuf.ensure(m + 1));
         Msg* rb = s->recvbuf.p;
-        NCCL_TRY(ncclGroupStart());
+        std::vector<Xfer> sends, recvs;
         for (uint32_t g = 0; g < G; g++) {
             if (g == s->idx) continue;
-            if (s->scnt[g])
-                NCCL_TRY(ncclSend(s->sendbuf.p + s->soff[g], s->scnt[g] * sizeof(Msg), ncclUint8, (int)g,
-                                  h->comm, s->stream));
-            if (rcnt[g])
-                NCCL_TRY(ncclRecv(rb + roff[g], rcnt[g] * sizeof(Msg), ncclUint8, (int)g, h->comm,
-                                  s->stream));
+            if (s->scnt[g]) sends.push_back({(int)g, s->sendbuf.p + s->soff[g], s->scnt[g] * sizeof(Msg)});
+            if (rcnt[g]) recvs.push_back({(int)g, rb + roff[g], rcnt[g] * sizeof(Msg)});
         }
-        NCCL_TRY(ncclGroupEnd());
+        TRY(h->comm->exchange(sends, recvs, s->stream));
         if (rcnt[s->idx])
             HIP_TRY(hipMemcpyAsync(rb + roff[s->idx], s->sendbuf.p + s->soff[s->idx],
                                    rcnt[s->idx] * sizeof(Msg), hipMemcpyDeviceToDevice, s->stream));
@@ -2187,7 +2003,7 @@ int run_round(psim_handle* h, uint64_t* st, bool events_applied = false) {
         Shard* s = h->shards[0];
         TRY(h->comm_cnt.ensure(NST));
         HIP_TRY(hipMemcpyAsync(h->comm_cnt.p, st, NST * 8, hipMemcpyHostToDevice, s->stream));
-        NCCL_TRY(ncclAllReduce(h->comm_cnt.p, h->comm_cnt.p, NST, ncclUint64, ncclSum, h->comm, s->stream));
+        TRY(h->comm->all_reduce(h->comm_cnt.p, NST, CType::U64, COp::SUM, s->stream));
         HIP_TRY(hipMemcpyAsync(st, h->comm_cnt.p, NST * 8, hipMemcpyDeviceToHost, s->stream));
         TRY(stream_wait(s));
     }
@@ -2220,7 +2036,7 @@ int run_round(psim_handle* h, uint64_t* st, bool events_applied = false) {
             const uint64_t k = mine.size();
             TRY(h->comm_cnt.ensure(W + 1));
             HIP_TRY(hipMemcpyAsync(h->comm_cnt.p + W, &k, 8, hipMemcpyHostToDevice, s->stream));
-            NCCL_TRY(ncclAllGather(h->comm_cnt.p + W, h->comm_cnt.p, 1, ncclUint64, h->comm, s->stream));
+            TRY(h->comm->all_gather(h->comm_cnt.p + W, h->comm_cnt.p, 8, s->stream));
             HIP_TRY(hipMemcpyAsync(cnt.data(), h->comm_cnt.p, W * 8, hipMemcpyDeviceToHost, s->stream));
             TRY(stream_wait(s));
             const uint64_t mk = *std::max_element(cnt.begin(), cnt.end());
@@ -2229,7 +2045,7 @@ int run_round(psim_handle* h, uint64_t* st, bool events_applied = false) {
             TRY(h->comm_cnt.ensure((size_t)W * mk + mk));
             HIP_TRY(hipMemcpyAsync(h->comm_cnt.p + (size_t)W * mk, mine.data(), mk * 8, hipMemcpyHostToDevice,
                                    s->stream));
-            NCCL_TRY(ncclAllGather(h->comm_cnt.p + (size_t)W * mk, h->comm_cnt.p, mk, ncclUint64, h->comm, s->stream));
+            TRY(h->comm->all_gather(h->comm_cnt.p + (size_t)W * mk, h->comm_cnt.p, mk * 8, s->stream));
             HIP_TRY(hipMemcpyAsync(all.data(), h->comm_cnt.p, all.size() * 8, hipMemcpyDeviceToHost, s->stream));
             TRY(stream_wait(s));
             ids.clear();
@@ -2312,7 +2128,11 @@ int run_batch(psim_handle* h, uint32_t nb, psim_round_stats* st_out, uint32_t* d
     uint32_t cw[2] = {0, 0};
     HIP_TRY(hipMemcpyAsync(cw, s->ctl.p, sizeof cw, hipMemcpyDeviceToHost, s->stream));
     TRY(stream_wait(s));
-    if (s->pin[PIN_BIGIN]) return PSIM_ENOMEM;        // a node's inbox count must fit 27 bits
+    if (s->pin[PIN_BIGIN]) {                          // a node's inbox count must fit 27 bits
+        s->pin[PIN_BIGIN] = 0;
+        HIP_TRY(hipMemsetAsync(s->ctl.p, 0, sizeof cw, s->stream));
+        return PSIM_ENOMEM;                           // (psim_step marks the handle failed)
+    }
     const uint32_t done = cw[0] ? (uint32_t)(cw[1] - r0) : nb;
     if (cw[0] && (cw[1] < r0 || done >= nb)) return PSIM_EDEVICE;
     for (uint32_t j = 0; j < done; j++) {
@@ -2466,7 +2286,7 @@ int shard_alloc(psim_handle* h, Shard* s) {
 
 void shard_free(Shard* s) {
     if (s->stream) (void)hipStreamSynchronize(s->stream);
-    s->flags.release(); s->part.release(); s->hdr.release(); s->crash_bits.release();
+    s->flags.release(); s->part.release(); s->hdr.release(); s->crash_bits.release(); s->btab.release();
     s->act.release(); s->pas.release(); s->sentm.release(); s->recvm.release();
     s->pt_all.release(); s->pt_com.release();
     s->mapx.release(); s->mapx_top.release();
@@ -2493,7 +2313,7 @@ void shard_free(Shard* s) {
     s->stop_ids.release(); s->n_stop.release();
     s->desc.release(); s->d_nact.release(); s->desc_slow.release(); s->n_slow.release(); s->desc_pt.release(); s->n_pt.release(); s->desc_shuf.release(); s->n_shuf.release(); s->desc_lite.release(); s->n_lite.release(); s->desc_ptl.release(); s->n_ptl.release(); s->bound.release(); s->pscan.release();
     s->obase.release(); s->stat_part.release(); s->stat_out.release(); s->stat_tile.release(); s->d_off.release();
-    s->cub_tmp.release(); s->scan_stat.release(); s->scan_val.release(); s->ev_ids.release(); s->ev_contacts.release(); s->sendbuf.release(); s->ctl.release();
+    s->cub_tmp.release(); s->ev_ids.release(); s->ev_contacts.release(); s->sendbuf.release(); s->ctl.release();
     s->sview.release(); s->sinv.release(); s->fbits.release(); s->pay[0].release(); s->pay[1].release();
     s->pay_top.release();
     if (s->ev_live)
@@ -2617,15 +2437,22 @@ int psim_create(const psim_config* cfg, psim_handle** out) {
         if (rc) { psim_destroy(h); return rc; }
     }
     if (world > 1) {
-        ncclUniqueId id;
-        memcpy(&id, cfg->comm_id, sizeof id);
-        ncclResult_t r = ncclCommInitRank(&h->comm, (int)world, id, (int)cfg->shard_rank);
-        if (r != ncclSuccess) {
-            std::fprintf(stderr, "psim: ncclCommInitRank(world %u, rank %u) failed: %s\n", world,
-                         cfg->shard_rank, ncclGetErrorString(r));
-            h->comm = nullptr;
+        // RCCL; an id from psim_loopback_comm_id selects the loopback test
+        // vehicle instead (ranks as threads of this process, psim_comm.h)
+        int rc;
+        if (LoopbackComm::is_loopback_id(cfg->comm_id)) {
+            LoopbackComm* c = new (std::nothrow) LoopbackComm();
+            h->comm = c;
+            rc = c ? c->init(cfg->comm_id, (int)cfg->shard_rank, (int)world) : PSIM_ENOMEM;
+        } else {
+            RcclComm* c = new (std::nothrow) RcclComm();
+            h->comm = c;
+            rc = c ? c->init(cfg->comm_id, (int)cfg->shard_rank, (int)world) : PSIM_ENOMEM;
+            if (rc) std::fprintf(stderr, "psim: RCCL world %u, rank %u: no communicator\n", world, cfg->shard_rank);
+        }
+        if (rc) {
             psim_destroy(h);
-            return PSIM_ECOMM;
+            return rc;
         }
     }
     *out = h;
@@ -2638,7 +2465,7 @@ void psim_destroy(psim_handle* h) {
     for (Shard* s : h->shards) shard_free(s);
     h->shards.clear();
     h->comm_cnt.release();
-    if (h->comm) ncclCommDestroy(h->comm);
+    delete h->comm;
     delete h;
 }
 
@@ -2727,6 +2554,27 @@ int psim_set_partition(psim_handle* h, const uint8_t* group, size_t n) {
     return PSIM_OK;
 }
 
+// The sets v1 bucket of every node_spec, erlang:phash(NodeSpec, 16) - 1
+// (SURVEY App. A Q1): the order sets:to_list/1 yields views in, which every
+// select_random index and every shuffle key pairing follows (hv:1230-1231,
+// :1346-1361).  Before the first round only (the views already built would
+// be in the old order); buckets == NULL restores the default table.
+int psim_set_bucket_table(psim_handle* h, const uint8_t* buckets, size_t n) {
+    if (!h) return PSIM_EINVAL;
+    if (h->round != 0) return PSIM_ESTATE;
+    if (!buckets) { h->btab = false; return PSIM_OK; }
+    if (n != h->N) return PSIM_EINVAL;
+    for (size_t i = 0; i < n; i++)
+        if (buckets[i] > 15) return PSIM_EINVAL;
+    if (hipSetDevice(h->device) != hipSuccess) return PSIM_EDEVICE;
+    for (Shard* s : h->shards) {
+        if (!s->btab.p && s->btab.alloc(h->N)) return PSIM_ENOMEM;
+        if (hipMemcpy(s->btab.p, buckets, n, hipMemcpyHostToDevice) != hipSuccess) return PSIM_EDEVICE;
+    }
+    h->btab = true;
+    return PSIM_OK;
+}
+
 int psim_clear_partition(psim_handle* h) {
     if (!h) return PSIM_EINVAL;
     h->pend_part_clear = true; h->pend_part_set = false;
@@ -2793,20 +2641,21 @@ int psim_broadcast(psim_handle* h, uint32_t root, uint32_t msg_id) {
 
 int psim_step(psim_handle* h, uint32_t n_rounds, psim_round_stats* stats) {
     if (!h) return PSIM_EINVAL;
+    if (h->failed) return PSIM_ESTATE;
     if (hipSetDevice(h->device) != hipSuccess) return PSIM_EDEVICE;
     for (int k = 0; k < KT_N; k++) { h->kt_ms[k] = 0; h->kt_n[k] = 0; }
     for (uint32_t i = 0; i < n_rounds;) {
         if (batchable(h)) {                   // rounds back to back, one wait per batch
             uint32_t done = 0;
             int rc = run_batch(h, std::min<uint32_t>(n_rounds - i, BATCH_MAX), stats ? stats + i : nullptr, &done);
-            if (rc) return rc;
+            if (rc) { h->failed = true; return rc; }
             i += done;
             continue;
         }
         uint64_t st[NST];
         uint64_t r = h->round;
         int rc = run_round(h, st);
-        if (rc) return rc;
+        if (rc) { h->failed = true; return rc; }
         if (stats) fill_stats(st, r, &stats[i]);
         if (h->cfg.strict && st[ST_OVF]) return PSIM_ECAPACITY;   // cfg.strict: fail loudly
         i++;
@@ -3072,7 +2921,7 @@ int psim_get_histograms(psim_handle* h, psim_histograms* out) {
         k_hist_out<<<grid_for(s->n), BLK, 0, st>>>(s->hdr.p, s->act.p, s->pas.p, s->flags.p, s->lo, s->n, tbit,
                                                    ind.p, ind.p + N, hist.p);
     if (h->world > 1) {
-        NCCL_TRY(ncclAllReduce(ind.p, ind.p, 2 * N, ncclUint32, ncclSum, h->comm, st));
+        TRY(h->comm->all_reduce(ind.p, 2 * N, CType::U32, COp::SUM, st));
     }
     for (Shard* s : h->shards)
         k_hist_in<<<grid_for(s->n), BLK, 0, st>>>(ind.p, ind.p + N, s->flags.p, s->lo, s->n, hist.p);
@@ -3083,8 +2932,8 @@ int psim_get_histograms(psim_handle* h, psim_histograms* out) {
         hv[H_N] = hv[H_LAST];
         TRY(h->comm_cnt.ensure(H_N + 4));
         HIP_TRY(hipMemcpyAsync(h->comm_cnt.p, hv.data(), (H_N + 4) * 8, hipMemcpyHostToDevice, st));
-        NCCL_TRY(ncclAllReduce(h->comm_cnt.p, h->comm_cnt.p, H_N, ncclUint64, ncclSum, h->comm, st));
-        NCCL_TRY(ncclAllReduce(h->comm_cnt.p + H_N, h->comm_cnt.p + H_N, 1, ncclUint64, ncclMax, h->comm, st));
+        TRY(h->comm->all_reduce(h->comm_cnt.p, H_N, CType::U64, COp::SUM, st));
+        TRY(h->comm->all_reduce(h->comm_cnt.p + H_N, 1, CType::U64, COp::MAX, st));
         HIP_TRY(hipMemcpyAsync(hv.data(), h->comm_cnt.p, (H_N + 4) * 8, hipMemcpyDeviceToHost, st));
         HIP_TRY(hipStreamSynchronize(st));
         hv[H_LAST] = hv[H_N];
@@ -3116,9 +2965,8 @@ int psim_get_histograms(psim_handle* h, psim_histograms* out) {
                                                            gact.p + (size_t)s->lo * PSIM_ACTIVE_CAP, gan.p + s->lo);
         if (h->world > 1) {
             const size_t off = (size_t)h->rank * per;
-            NCCL_TRY(ncclAllGather(gact.p + off * PSIM_ACTIVE_CAP, gact.p, (size_t)per * PSIM_ACTIVE_CAP, ncclUint32,
-                                   h->comm, st));
-            NCCL_TRY(ncclAllGather(gan.p + off, gan.p, per, ncclUint8, h->comm, st));
+            TRY(h->comm->all_gather(gact.p + off * PSIM_ACTIVE_CAP, gact.p, (size_t)per * PSIM_ACTIVE_CAP * 4, st));
+            TRY(h->comm->all_gather(gan.p + off, gan.p, per, st));
         }
         const uint8_t* fl = s0->flags.p;         // replicated: every shard holds all N
         TRY(L.alloc_on(n, st)); TRY(sz.alloc_on(n, st)); TRY(flag.alloc_on(1, st)); TRY(r.alloc_on(3, st));
@@ -3290,6 +3138,9 @@ int psim_debug_stamps(unsigned long long* out, int cap) {
 }
 
 int psim_comm_id_size(void) { return (int)sizeof(ncclUniqueId); }
+
+// a loopback world's id (test vehicle of the rank code path, psim_comm.h)
+int psim_loopback_comm_id(void* buf, size_t cap) { return psim::loopback_new_id(buf, cap); }
 
 int psim_get_comm_id(void* buf, size_t cap) {
     if (!buf || cap < sizeof(ncclUniqueId)) return PSIM_EINVAL;

@@ -21,6 +21,9 @@ struct RoundArgs {
     // this round's crashed ids, one bit per CRASH_GRAIN ids (replicated,
     // zero outside crash rounds): a filter in L2 in front of the flag bytes
     const uint32_t* crash_bits;
+    // the sets v1 bucket of every global id (psim_set_bucket_table), or
+    // nullptr for the default (bucket16_default): the view order of App. A Q1
+    const uint8_t* btab;
     Hdr* hdr;
     uint32_t *act, *pas;
     uint64_t *sentm, *recvm;    // id maps: the IDMAP_IN own entries, id << 32 | peer

@@ -52,8 +52,9 @@ DEV void ins2(L2& V, uint32_t& n, uint32_t pos, uint32_t e) {
 }
 // sets:add_element/2 in sets:to_list/1 order (after every entry of a bucket <= e's)
 DEV void add_set2(L2& V, uint32_t& n, uint32_t e) {
-    const uint32_t l = lane_id(), b = bucket16(e);
-    const uint32_t pos = popc(ballot(l < n && bucket16(V.a) <= b)) + popc(ballot(64 + l < n && bucket16(V.b) <= b));
+    const uint8_t* bt = kargs().btab;
+    const uint32_t l = lane_id(), b = bucket16(bt, e);
+    const uint32_t pos = popc(ballot(l < n && bucket16(bt, V.a) <= b)) + popc(ballot(64 + l < n && bucket16(bt, V.b) <= b));
     ins2(V, n, pos, e);
 }
 

@@ -91,10 +91,11 @@ DEV bool vdel_val(uint32_t& V, uint32_t& n, uint32_t e) {
     return true;
 }
 // sets:add_element/2 in sets:to_list/1 order: after every element whose
-// bucket is <= the new element's bucket (new = youngest of its bucket)
-DEV void view_add(uint32_t& V, uint32_t& n, uint32_t e) {
-    uint32_t b = bucket16(e);
-    uint32_t pos = popc(ballot(lane_id() < n && bucket16(V) <= b));
+// bucket is <= the new element's bucket (new = youngest of its bucket);
+// `bt` = the handle's bucket table (RoundArgs::btab, nullptr = default)
+DEV void view_add(const uint8_t* bt, uint32_t& V, uint32_t& n, uint32_t e) {
+    uint32_t b = bucket16(bt, e);
+    uint32_t pos = popc(ballot(lane_id() < n && bucket16(bt, V) <= b));
     vins(V, n, pos, e);
 }
 

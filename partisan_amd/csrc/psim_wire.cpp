@@ -1,10 +1,18 @@
 // psim_wire.cpp -- the wire format of a partisan peer connection (SURVEY.md
 // 8(f) rank 4), so simulated nodes can exchange messages with real partisan
 // nodes: every frame is {packet, 4} -- a 4-byte big-endian length
-// (peer_service_client:214, the socket options of connect/2) -- around
-// term_to_binary/1 of the message the manager hands its connection
-// (client:253-257 encode/1 on the send path, server:172-182 decode on the
-// receive path): Erlang's external term format, version byte 131.
+// (peer_service_client:214, the socket options of connect/2) -- around the
+// encoding the connection's send path writes: handle_call({send_message, M})
+// sends encode(M) (client:95, :130) = partisan_util:term_to_iolist/1
+// (client:275-276, util:235-297) -- Erlang's external term format, version
+// byte 131, with its own rules above the maps: atoms as SMALL_ATOM_EXT (115,
+// a 1-byte length), tuples as SMALL_TUPLE_EXT, lists of bytes as STRING_EXT,
+// other lists as LIST_EXT, and every other term -- the node_spec maps and
+// everything inside them, integers -- through term_to_binary/1 (OTP 19-22:
+// latin-1 atoms as ATOM_EXT, small maps with their keys in term order).  The
+// receiver (server:172-182) takes any form; so does the decoder here.  (The
+// client's hello, client:253-257, is default_encode = term_to_binary/1, and
+// is not a record.)
 //
 // A message is the engine's 64-B record (psim_device.h Msg: dst, src,
 // type | ttl << 8 | nex << 16, seq, a0, a1, a2, a3, ex[8]); the term is the
@@ -19,7 +27,11 @@
 //   NEIGHBOR_REJECTED  {neighbor_rejected, Myself, Exchange}               hv:1041-1043
 //   SHUFFLE            {shuffle, Exchange, TTL, Sender}                    hv:594-597, :1110-1113
 //   SHUFFLE_REPLY      {shuffle_reply, Exchange, Myself}                   hv:1127-1131
-//   Plumtree           {forward_message, partisan_plumtree_broadcast, Msg} hv:441-460, pt:633-638
+//   Plumtree           {forward_message, partisan_plumtree_broadcast, {'$gen_cast', Msg}}:
+//                      send/3 (pt:633-638) calls cast_message/3, which wraps
+//                      Msg as {'$gen_cast', Msg} (hv:147-154) for
+//                      forward_message (hv:441-460); the receiver's
+//                      process_forward sends it on as is (util:385-399)
 //     BROADCAST        {broadcast, Id, Payload, Mod, Round, Root, From}    pt:398, :431
 //     PRUNE            {prune, Root, From}                                 pt:372
 //     IHAVE / IGNORED_IHAVE / GRAFT
@@ -35,10 +47,7 @@
 // [#{ip => ip_base + i, port => port}], channels => [undefined],
 // parallelism => 1} (partisan_peer_service_manager:myself/0 :71-76,
 // partisan.hrl:14-19) -- a Plumtree identity without PSIM_MAP_BIT is the name
-// atom alone.  term_to_binary/1 of OTP 19-22 (the
-// reference's targets) writes latin-1 atoms as ATOM_EXT and small maps with
-// their keys in term order; the decoder also takes the UTF-8 and small atom
-// forms and any integer form.
+// atom alone.
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
@@ -69,10 +78,18 @@ const char* const kPlumtreeBackend = "partisan_plumtree_backend";
 // ------------------------------------------------------------- encoder --
 struct Enc {
     std::vector<uint8_t> b;
+    // inside a term term_to_iolist/1 hands to term_to_binary/1 (a map)
+    int in_map = 0;
     void u8(uint32_t v) { b.push_back((uint8_t)v); }
     void u16(uint32_t v) { u8(v >> 8); u8(v); }
     void u32(uint32_t v) { u16(v >> 16); u16(v); }
-    void atom(const std::string& s) { u8(T_ATOM); u16((uint32_t)s.size()); b.insert(b.end(), s.begin(), s.end()); }
+    // term_to_iolist_/1's atom clause (util:243-252): SMALL_ATOM_EXT up to
+    // 255 characters; term_to_binary/1 inside a map: ATOM_EXT
+    void atom(const std::string& s) {
+        if (!in_map && s.size() <= 255) { u8(T_SMALL_ATOM); u8((uint32_t)s.size()); }
+        else { u8(T_ATOM); u16((uint32_t)s.size()); }
+        b.insert(b.end(), s.begin(), s.end());
+    }
     void integer(int64_t v) {
         if (v >= 0 && v <= 255) { u8(T_SMALL_INTEGER); u8((uint32_t)v); return; }
         if (v >= INT32_MIN && v <= INT32_MAX) { u8(T_INTEGER); u32((uint32_t)(int32_t)v); return; }
@@ -114,6 +131,7 @@ struct Names {
 // node_spec(): a map with its keys in term order (channels < listen_addrs <
 // name < parallelism; ip < port)
 void node_spec(Enc& e, const Names& nm, uint32_t id) {
+    e.in_map++;                                       // (term_to_iolist_'s fallback clause, util:288-291)
     e.map(4);
     e.atom("channels"); e.list(1); e.atom("undefined"); e.nil();
     e.atom("listen_addrs"); e.list(1);
@@ -124,6 +142,7 @@ void node_spec(Enc& e, const Names& nm, uint32_t id) {
     e.nil();
     e.atom("name"); e.atom(nm.name(id));
     e.atom("parallelism"); e.integer(1);
+    e.in_map--;
 }
 // a Plumtree peer identity: a node_spec map (PSIM_MAP_BIT) or the name atom
 void identity(Enc& e, const Names& nm, uint32_t ident) {
@@ -184,6 +203,7 @@ bool encode_term(Enc& e, const Names& nm, const uint32_t* r) {
         if (a2 == PSIM_NONE) return false;               // (an IHAVE of a retired id has no root)
         const std::string root_name = nm.name(a2 & ~PSIM_MAP_BIT);
         e.tuple(3); e.atom("forward_message"); e.atom(kPlumtreeServer);
+        e.tuple(2); e.atom("$gen_cast");                 // cast_message/3 (hv:147-154)
         const auto id = [&] { e.tuple(2); e.atom(root_name); e.integer(a0); };
         if (type == PSIM_MSG_PT_PRUNE) {
             e.tuple(3); e.atom(kPtTags[1]); identity(e, nm, a2); node_spec(e, nm, src);
@@ -377,10 +397,12 @@ bool decode_term(const Term& t, const Names& nm, uint32_t dst, uint32_t* r) {
         }
     }
     if (tag == "forward_message") {
-        if (m != 3 || !is_atom(k[1], kPlumtreeServer) || k[2].kind != Term::TUPLE || k[2].k.empty() ||
-            k[2].k[0].kind != Term::ATOM)
+        // {forward_message, partisan_plumtree_broadcast, {'$gen_cast', Msg}}
+        if (m != 3 || !is_atom(k[1], kPlumtreeServer) || k[2].kind != Term::TUPLE || k[2].k.size() != 2 ||
+            !is_atom(k[2].k[0], "$gen_cast") || k[2].k[1].kind != Term::TUPLE || k[2].k[1].k.empty() ||
+            k[2].k[1].k[0].kind != Term::ATOM)
             return false;
-        const auto& q = k[2].k;
+        const auto& q = k[2].k[1].k;
         const std::string& pt = q[0].a;
         uint32_t root = 0, ctr = 0;
         if (pt == kPtTags[1]) {

@@ -118,6 +118,17 @@ class _Driver:
     def clear_partition(self):
         self._check(self._api["clear_partition"](self._h), "clear_partition")
 
+    def set_bucket_table(self, buckets):
+        """The sets v1 bucket (erlang:phash(NodeSpec, 16) - 1, 0..15) of every
+        node: the view order of SURVEY App. A Q1.  Before the first round;
+        None restores the built-in stand-in."""
+        if buckets is None:
+            self._check(self._api["set_bucket_table"](self._h, None, 0), "set_bucket_table")
+            return
+        b = np.ascontiguousarray(buckets, np.uint8)
+        self._check(self._api["set_bucket_table"](
+            self._h, b.ctypes.data_as(C.POINTER(C.c_uint8)), b.size), "set_bucket_table")
+
     # ---- omission faults of the pluggable manager's interposition layer
     # (add_interposition_fun/2, pluggable:297-326; the crash-fault model's
     # begin/end_send_omission, begin/end_receive_omission, begin/end_omission,
@@ -276,6 +287,21 @@ def comm_id():
     rc = extra["get_comm_id"](buf, n)
     if rc != 0:
         raise SimError(f"get_comm_id: {extra['strerror'](rc).decode()}")
+    return buf.raw
+
+
+def loopback_comm_id():
+    """TEST VEHICLE: the id of a new loopback world (psim_loopback_comm_id):
+    ranks as threads of this process on one device, in place of RCCL."""
+    from . import _lib
+
+    lib = _lib.load()
+    extra = _abi.bind(lib, "psim_", _abi.GPU_ONLY)
+    n = extra["comm_id_size"]()
+    buf = C.create_string_buffer(n)
+    rc = extra["loopback_comm_id"](buf, n)
+    if rc != 0:
+        raise SimError(f"loopback_comm_id: {extra['strerror'](rc).decode()}")
     return buf.raw
 
 

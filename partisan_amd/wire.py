@@ -1,6 +1,7 @@
 """Wire format of a partisan peer connection (include/partisan_gpu_sim.h
 psim_wire_encode / psim_wire_decode): {packet, 4} frames
-around term_to_binary/1 of the manager's messages, so simulated nodes can
+around partisan_util:term_to_iolist/1 of the manager's messages (what a
+partisan connection writes, peer_service_client:95, :275), so simulated nodes can
 talk to real partisan nodes.  Records are the engine's 64-B message records
 as 16 uint32 words (dst, src, type | ttl << 8 | nex << 16, seq, a0, a1, a2,
 a3, ex[8])."""

@@ -54,6 +54,40 @@ def _enc(t, out):
         raise TypeError(t)
 
 
+def _iolist(t, out):
+    """partisan_util:term_to_iolist_/1 (util:238-291), restated: atoms as
+    SMALL_ATOM_EXT, tuples as SMALL_TUPLE_EXT, lists of bytes as STRING_EXT,
+    other lists as LIST_EXT, anything else (maps, integers) via
+    term_to_binary/1."""
+    if isinstance(t, Atom) and len(str(t)) <= 255:
+        b = str(t).encode("latin-1")
+        out += bytes([115, len(b)]) + b
+    elif isinstance(t, tuple):
+        out += bytes([104, len(t)])
+        for x in t:
+            _iolist(x, out)
+    elif isinstance(t, list):
+        if not t:
+            out += bytes([106])
+        elif all(isinstance(x, int) and not isinstance(x, bool) and 0 <= x <= 255 for x in t):
+            out += bytes([107]) + struct.pack(">H", len(t)) + bytes(t)
+        else:
+            out += bytes([108]) + struct.pack(">I", len(t))
+            for x in t:
+                _iolist(x, out)
+            out += bytes([106])
+    else:
+        _enc(t, out)
+
+
+def term_to_iolist(t):
+    """The bytes of partisan_util:term_to_iolist/1: what a partisan
+    connection writes for a message (peer_service_client:95, :130, :275)."""
+    out = bytearray([131])
+    _iolist(t, out)
+    return bytes(out)
+
+
 def term_to_binary(t):
     out = bytearray([131])
     _enc(t, out)

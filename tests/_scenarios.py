@@ -10,6 +10,22 @@ STAT_FIELDS = ["emitted", "delivered", "dropped", "nodes_up", "nodes_processed",
                "send_fail", "first_deliveries", "overflow", "overflow_by", "digest", "omitted"]
 
 
+def random_buckets(n, seed):
+    """A sets v1 bucket table (0..15 per node) unrelated to the built-in
+    stand-in: what an in-BEAM harness export of erlang:phash(NodeSpec, 16)
+    looks like to the engine (psim_set_bucket_table)."""
+    return np.random.Generator(np.random.PCG64([seed, 0xB16])).integers(0, 16, n).astype(np.uint8)
+
+
+def with_buckets(make, seed=7, table=None):
+    """`make` with a bucket table installed before the first round."""
+    def mk(cfg):
+        sim = make(cfg)
+        sim.set_bucket_table(random_buckets(cfg.n_nodes, seed) if table is None else table)
+        return sim
+    return mk
+
+
 def _bcast_every(sim, period, first, root=0, count=None):
     state = {"k": 0}
 

@@ -490,8 +490,10 @@ def test_heartbeat_parity():
 @pytest.mark.parametrize("name", ["C_survey", "C_doubling"])
 def test_bench_schedule_parity(name):
     """bench.py's exact schedules (workloads.BenchSchedule) at the bench's
-    2^20 nodes, into the timed window -- the survey line's broadcast round,
-    or two broadcasts and a cohort merge round of the doubling line --
+    2^20 nodes, into the timed window -- for the survey line the driver's
+    whole window (--warmup 5, the 20 timed rounds of the broadcast's
+    propagation, 5 more), or two broadcasts and a cohort merge round of the
+    doubling line --
     against the oracle's committed run of the same schedule
     (tests/golden/gen_bench_fixtures.py): every round's digest and counts,
     and the hash of every node's final view."""
@@ -504,7 +506,8 @@ def test_bench_schedule_parity(name):
     import gen_bench_fixtures as G
     fx = json.load(open(os.path.join(here, "golden", "bench_fixtures.json")))
     want = fx["fixtures"][name]
-    st, nodes = G.run(_gpu, name, n=fx["nodes"], seed=fx["seed"], warmup=fx["warmup"], window=fx["window"][name])
+    wu = fx["warmup"][name] if isinstance(fx["warmup"], dict) else fx["warmup"]
+    st, nodes = G.run(_gpu, name, n=fx["nodes"], seed=fx["seed"], warmup=wu, window=fx["window"][name])
     assert len(st) == want["rounds"]
     for f in G.FIELDS:
         got = st[f].tolist()
@@ -544,3 +547,39 @@ def test_xbot_64k_parity():
     assert ost["emitted"][:, 16:22].sum() > 10000
     S.compare_stats(gst, ost)
     S.compare_nodes(gs.nodes(), os_.nodes())
+
+
+def _both_tab(fn, seed, *a, **kw):
+    return fn(S.with_buckets(_gpu, seed), *a, **kw), fn(S.with_buckets(Oracle, seed), *a, **kw)
+
+
+@pytest.mark.parametrize("case", ["config_a", "churn_partition", "doubling_64k", "xbot", "scamp_v1"])
+def test_bucket_table_parity(case):
+    """App. A Q1: a sets v1 bucket table that is not the built-in stand-in
+    (psim_set_bucket_table, what an in-BEAM harness export of
+    erlang:phash(NodeSpec, 16) supplies) -- GPU == oracle bit for bit, and
+    the views follow the table."""
+    if case == "config_a":
+        (gs, gst), (os_, ost) = _both_tab(S.config_a, 11)
+    elif case == "churn_partition":
+        (gs, gst), (os_, ost) = _both_tab(S.churn_partition, 12, n=2048)
+    elif case == "doubling_64k":
+        def run(make):
+            sim, st = S.doubling(make, 1 << 16, 21, 60)
+            sim.broadcast(0, 5)
+            return sim, np.concatenate([st, sim.step(30)])
+        (gs, gst), (os_, ost) = _both_tab(run, 13)
+    elif case == "xbot":
+        (gs, gst), (os_, ost) = _both_tab(S.xbot_churn, 14, n=1024, rounds=100)
+    else:
+        (gs, gst), (os_, ost) = _both_tab(S.pl_doubling, 15, 2048, 5, 60, 1, crash_at=30, part_at=40)
+        S.compare_stats(gst, ost)
+        S.compare_strategy(gs, os_)
+        return
+    S.compare_stats(gst, ost)
+    v = gs.nodes()
+    S.compare_nodes(v, os_.nodes())
+    tab = S.random_buckets(len(v), {"config_a": 11, "churn_partition": 12, "doubling_64k": 13, "xbot": 14}[case])
+    for i in np.nonzero(v["up"])[0][:4096]:
+        row = v["pas"][i][: v["pas_n"][i]]
+        assert (np.diff(tab[row].astype(int)) >= 0).all(), i

@@ -21,7 +21,8 @@ def test_scenario_and_compare(tmp_path):
     terms = open(os.path.join(d, "doubling_crash_256.terms")).read()
     assert terms.startswith("{config, #{n_nodes => 256") and "{crash, 40, [5, 22" in terms
     stream = os.path.join(d, "doubling_crash_256.oracle")
-    lines = open(stream).read().splitlines()
+    head, *lines = open(stream).read().splitlines()
+    assert head == "S doubling_crash_256"
     assert len(lines) > 1000 and all(l.startswith("R ") for l in lines)
     # (src, seq) numbering: per round and source, seq runs 0, 1, 2, ...
     seen = {}
@@ -32,8 +33,8 @@ def test_scenario_and_compare(tmp_path):
         seen[key] = int(f[3])
     assert _run("compare", stream, stream).returncode == 0
     bad = os.path.join(d, "bad")
-    mod = lines[:]
-    mod[500] = mod[500].rsplit(" ", 1)[0] + " 999"
+    mod = [head] + lines
+    mod[501] = mod[501].rsplit(" ", 1)[0] + " 999"
     open(bad, "w").write("\n".join(mod) + "\n")
     r = _run("compare", bad, stream)
     assert r.returncode == 1 and "record 500 differs" in r.stdout
@@ -54,8 +55,43 @@ def test_strategy_scenarios(tmp_path):
         assert f"strategy => {strategy}" in terms and "periodic_interval => 10" in terms
         if name.startswith("scamp"):
             assert "{leave, 50, [{9, 10}]}." in terms and "{clear_partition, 70}." in terms
-        lines = open(os.path.join(d, name + ".oracle")).read().splitlines()
+        lines = [l for l in open(os.path.join(d, name + ".oracle")).read().splitlines() if l.startswith("R ")]
         got = {int(l.split()[5]) for l in lines}
         assert types <= got, (name, sorted(got))
         assert all(len(l.split()) == 11 and l.split()[6] == "0" for l in lines)   # ttl 0, no exchange ids
         assert _run("compare", os.path.join(d, name + ".oracle"), os.path.join(d, name + ".oracle")).returncode == 0
+
+
+def test_compare_takes_the_harness_bucket_table(tmp_path):
+    """App. A Q1: the harness writes erlang:phash(NodeSpec, 16) of every node
+    (`B id bucket`); compare regenerates the oracle stream with that table
+    (psim_set_bucket_table) before diffing, so a harness run whose sets order
+    is not the oracle's stand-in still compares record for record.  Here the
+    "harness output" is the oracle's own stream under a random table."""
+    sys.path.insert(0, os.path.dirname(TOOL))
+    import compare_trace as CT
+    import numpy as np
+    import _scenarios as S
+    d = str(tmp_path)
+    assert _run("scenario", "config_a", d).returncode == 0
+    default = os.path.join(d, "config_a.oracle")
+    tab = S.random_buckets(32, 5)
+    fake = os.path.join(d, "config_a.harness")
+    CT.write_stream("config_a", fake, tab)
+    assert open(fake).read().count("\nB ") == 32
+    r = _run("compare", fake, default)
+    assert r.returncode == 0 and "regenerated" in r.stdout and "records identical" in r.stdout, r.stdout
+    assert np.array_equal(CT.read_buckets(os.path.join(d, "bucket16.txt"), 32), tab)
+    # the default stream differs from the table's: without the table the diff fails
+    h = [l for l in open(fake) if l.startswith("R ")]
+    o = [l for l in open(default) if l.startswith("R ")]
+    assert h != o
+    plain = os.path.join(d, "plain.harness")
+    open(plain, "w").writelines(h)
+    assert _run("compare", plain, default).returncode == 1
+    # a scenario made with the table from the start compares without regenerating
+    bt = os.path.join(d, "tab.txt")
+    open(bt, "w").write("".join(f"{i} {int(b)}\n" for i, b in enumerate(tab)))
+    assert _run("scenario", "config_a", d, bt).returncode == 0
+    r = _run("compare", fake, default)
+    assert r.returncode == 0 and "regenerated" not in r.stdout

@@ -392,3 +392,57 @@ def test_heartbeat_fails_loudly_when_strict():
     assert int(st["overflow"].sum()) > 0
     with pytest.raises(SimError, match="ECAPACITY"):
         S.heartbeat(Oracle, strict=1)
+
+
+def _views_in_bucket_order(v, tab):
+    for i in np.nonzero(v["up"])[0]:
+        for f, nf in (("act", "act_n"), ("pas", "pas_n")):
+            row = v[f][i][: v[nf][i]]
+            b = tab[row]
+            assert (np.diff(b.astype(int)) >= 0).all(), (i, f, row.tolist(), b.tolist())
+
+
+def test_bucket_table_sets_view_order():
+    """App. A Q1: with a table installed (psim_set_bucket_table) every view
+    is in sets:to_list order of that table -- ascending bucket -- and the run
+    differs from the stand-in's; the stand-in's own table reproduces the
+    default run bit for bit."""
+    tab = S.random_buckets(32, 7)
+    sim, st = S.config_a(S.with_buckets(Oracle, table=tab))
+    _views_in_bucket_order(sim.nodes(), tab)
+    assert S.connected(S.active_graph(sim.nodes()))
+    base, bst = S.config_a(Oracle)
+    assert not np.array_equal(st["digest"], bst["digest"])
+    lib = load()
+    own = np.array([lib.orc_bucket16(i) for i in range(32)], np.uint8)
+    same, sst = S.config_a(S.with_buckets(Oracle, table=own))
+    S.compare_stats(sst, bst)
+    S.compare_nodes(same.nodes(), base.nodes())
+    _views_in_bucket_order(base.nodes(), own)
+
+
+def test_bucket_table_scamp_v1_order():
+    """SCAMP v1's membership is a sets v1 set too (scamp_v1:45-279): its
+    view follows the table (views of <= 80 entries)."""
+    n = 512
+    tab = S.random_buckets(n, 3)
+    sim, _ = S.pl_doubling(S.with_buckets(Oracle, table=tab), n, 5, 40, 1)
+    v = sim.strategy_nodes()
+    for i in range(n):
+        row = v["view"][i][: v["view_n"][i]]
+        if 0 < len(row) <= 80:
+            assert (np.diff(tab[row].astype(int)) >= 0).all(), i
+
+
+def test_bucket_table_checks():
+    from partisan_amd.sim import SimError
+    sim = Oracle(default_config(n_nodes=32))
+    with pytest.raises(SimError):
+        sim.set_bucket_table(np.full(32, 16, np.uint8))      # buckets are 0..15
+    with pytest.raises(SimError):
+        sim.set_bucket_table(np.zeros(31, np.uint8))          # one per node
+    sim.set_bucket_table(np.zeros(32, np.uint8))
+    sim.set_bucket_table(None)
+    sim.step(1)
+    with pytest.raises(SimError):
+        sim.set_bucket_table(np.zeros(32, np.uint8))          # before the first round only

@@ -1,8 +1,10 @@
 """The wire format (psim_wire_encode / psim_wire_decode):
-{packet, 4} frames around term_to_binary/1 of the reference handlers'
-messages.  Pinned three ways:
+{packet, 4} frames around partisan_util:term_to_iolist/1 (util:235-297) of
+the reference handlers' messages -- what the connection's send path writes
+(peer_service_client:95, :130, :275).  Pinned three ways:
   * tests/_etf.py (an independent encoder of the published external term
-    format) against known term_to_binary/1 outputs of OTP 19-22;
+    format, and of term_to_iolist's own rules above it) against known
+    term_to_binary/1 outputs of OTP 19-22 and term_to_iolist outputs;
   * every message type's frame, byte for byte, against that encoder applied
     to the tuple the reference handler builds (cited per type);
   * decode(encode(r)) == r for each of them and over every record of real
@@ -13,7 +15,7 @@ import pytest
 
 import _scenarios as S
 from _etf import Atom as A
-from _etf import packet4, term_to_binary
+from _etf import packet4, term_to_binary, term_to_iolist
 from _oracle import Oracle
 from partisan_amd import wire
 
@@ -34,6 +36,19 @@ def test_etf_known_answers():
     assert term_to_binary({A("a"): 1}) == bytes([131, 116, 0, 0, 0, 1, 100, 0, 1, 97, 97, 1])
     # flatmap keys in term order
     assert term_to_binary({A("b"): 2, A("a"): 1}) == term_to_binary({A("a"): 1, A("b"): 2})
+
+
+def test_iolist_known_answers():
+    """partisan_util:term_to_iolist/1 (util:235-297): small atoms above the
+    maps, term_to_binary/1 inside them and for integers."""
+    assert term_to_iolist(A("ok")) == bytes([131, 115, 2, 111, 107])
+    assert term_to_iolist((A("a"), 1)) == bytes([131, 104, 2, 115, 1, 97, 97, 1])
+    assert term_to_iolist([A("a")]) == bytes([131, 108, 0, 0, 0, 1, 115, 1, 97, 106])
+    assert term_to_iolist([]) == bytes([131, 106])
+    assert term_to_iolist([1, 2]) == bytes([131, 107, 0, 2, 1, 2])
+    assert term_to_iolist(256) == term_to_binary(256)
+    assert term_to_iolist({A("a"): [A("b")]}) == term_to_binary({A("a"): [A("b")]})
+    assert term_to_iolist((A("x"), {A("a"): 1})) == bytes([131, 104, 2, 115, 1, 120]) + term_to_binary({A("a"): 1})[1:]
 
 
 def name(i):
@@ -78,7 +93,9 @@ MOD = A("partisan_plumtree_backend")
 
 
 def fwd(msg):
-    return (A("forward_message"), PT, msg)                                                        # hv:441-460
+    # send/3 (pt:633-638) -> cast_message/3 wraps {'$gen_cast', Msg} (hv:147-154)
+    # -> forward_message (hv:441-460)
+    return (A("forward_message"), PT, (A("$gen_cast"), msg))
 
 
 CASES += [
@@ -105,7 +122,7 @@ CASES += [
 @pytest.mark.parametrize("k", range(len(CASES)))
 def test_frame_matches_reference_term(k):
     r, term = CASES[k]
-    assert wire.encode(r, NM) == packet4(term_to_binary(term))
+    assert wire.encode(r, NM) == packet4(term_to_iolist(term))
 
 
 @pytest.mark.parametrize("k", range(len(CASES)))
@@ -131,7 +148,8 @@ def test_stream_of_frames_and_partial_reads():
 
 def test_decoder_accepts_other_term_encodings():
     """binary_to_term/1 takes any form: UTF-8 / small atoms, INTEGER_EXT for a
-    small integer -- so must the decoder (a newer OTP writes ATOM_UTF8_EXT)."""
+    small integer -- so must the decoder (a newer OTP writes ATOM_UTF8_EXT;
+    a plain term_to_binary/1 frame writes ATOM_EXT everywhere)."""
     r, term = CASES[3]
     b = term_to_binary(term)
     # every ATOM_EXT (100, len16) -> SMALL_ATOM_UTF8_EXT (119, len8)
@@ -159,7 +177,9 @@ def test_decoder_accepts_other_term_encodings():
 
 
 def test_rejects_unknown_terms():
-    for term in [A("ok"), (A("join"), spec(2), U), (A("hello"), name(1)), (A("neighbor"), spec(2), U, (1, 3), spec(5))]:
+    no_cast = (A("forward_message"), PT, (A("prune"), spec(6), spec(2)))          # (no gen_cast wrapper)
+    for term in [A("ok"), (A("join"), spec(2), U), (A("hello"), name(1)), (A("neighbor"), spec(2), U, (1, 3), spec(5)),
+                 no_cast]:
         with pytest.raises(wire.WireError):
             wire.decode(packet4(term_to_binary(term)), NM, 1)
     with pytest.raises(wire.WireError):
