@@ -16,8 +16,6 @@ from partisan_amd.sim import _Driver, loopback_comm_id
 
 class LoopbackRanks:
     def __init__(self, cfg, world, device=0):
-        import copy
-
         from partisan_amd import Simulator
 
         self.world, self.n = world, cfg.n_nodes
@@ -26,7 +24,7 @@ class LoopbackRanks:
         cid = loopback_comm_id()
         self.ranks = []
         for r in range(world):
-            c = copy.copy(cfg)
+            c = type(cfg).from_buffer_copy(cfg)
             c.shard_world, c.shard_rank, c.n_shards, c.device = world, r, 1, device
             self.ranks.append(Simulator(c, comm=cid))
 
