@@ -1228,7 +1228,10 @@ struct psim_handle {
     int device = 0;
     uint32_t consume_blocks = 1024;     // resident k_consume blocks on the device
     uint32_t pt_blocks = 1024;          // ... and k_pt blocks
-    uint32_t lite_blocks = 1024;        // ... and k_consume_lite blocks
+    uint32_t lite_blocks = 1024;        // ... and k_consume_lite (k_lite_half) blocks
+    // the lite list's kernel: k_lite_half, two nodes per wave (psim_lite.hip);
+    // PSIM_LITE_WAVE=1 keeps the wave-per-node k_consume_lite (A/B)
+    bool lite_half = true;
     uint32_t ptl_blocks = 1024;         // ... and k_ptl blocks
     uint64_t round = 0;
     // a round failed half-way (psim_step returned an error from inside a
@@ -1556,7 +1559,9 @@ int phase_events_prepare(psim_handle* h, Shard* s, const RoundCtl& ctl, RoundArg
         s->rgrid = hv ? std::min<uint32_t>(grid_for(n), RELAY_MAX_BLOCKS) : 0;
         s->tgrid = hv && h->cfg.plumtree ? std::min<uint32_t>(grid_for(n), h->pt_blocks) : 0;
         s->sgrid = hv ? std::min<uint32_t>(grid_for(n), SHUF_MAX_BLOCKS) : 0;
-        s->lgrid = hv ? std::min<uint32_t>((uint32_t)((n + psim::lite_block() - 1) / psim::lite_block()), h->lite_blocks) : 0;
+        // (k_lite_half: two nodes per wave)
+        const uint32_t lnodes = h->lite_half ? psim::lite_half_block() * 2 : psim::lite_block();
+        s->lgrid = hv ? std::min<uint32_t>((uint32_t)((n + lnodes - 1) / lnodes), h->lite_blocks) : 0;
         s->qgrid = hv && h->cfg.plumtree ? std::min<uint32_t>((n + PTL_BLOCK - 1) / PTL_BLOCK, h->ptl_blocks) : 0;
         TRY(s->stat_part.ensure((size_t)(s->pgrid + s->cgrid + s->rgrid + s->tgrid + s->sgrid + s->lgrid + s->qgrid) *
                                 NST));
@@ -1631,6 +1636,11 @@ args:
     return PSIM_OK;
 }
 
+void launch_lite(psim_handle* h, Shard* s, const RoundArgs& a, hipStream_t st) {
+    if (h->lite_half) k_lite_half<<<s->lgrid, psim::lite_half_block(), 0, st>>>(a);
+    else k_consume_lite<<<s->lgrid, psim::lite_block(), 0, st>>>(a);
+}
+
 int phase_consume(psim_handle* h, Shard* s, RoundArgs& a) {
     if (a.pl && a.strategy == PSIM_STRATEGY_FULL) {
         // snapshots: at most one per node plus one per inbox message
@@ -1676,7 +1686,7 @@ int phase_consume(psim_handle* h, Shard* s, RoundArgs& a) {
         const bool serial = serial_env || a.crash_round;
         if (serial) {
             k_shuf<<<s->sgrid, BLK, 0, s->stream>>>(a);
-            k_consume_lite<<<s->lgrid, psim::lite_block(), 0, s->stream>>>(a);
+            launch_lite(h, s, a, s->stream);
             k_consume<<<s->cgrid, BLK, 0, s->stream>>>(b);
         } else {
             HIP_TRY(hipEventRecord(s->fork_ev, s->stream));
@@ -1684,7 +1694,7 @@ int phase_consume(psim_handle* h, Shard* s, RoundArgs& a) {
             HIP_TRY(hipStreamWaitEvent(s->side[1], s->fork_ev, 0));
             k_consume<<<s->cgrid, BLK, 0, s->side[0]>>>(b);
             k_shuf<<<s->sgrid, BLK, 0, s->side[1]>>>(a);
-            k_consume_lite<<<s->lgrid, psim::lite_block(), 0, s->stream>>>(a);
+            launch_lite(h, s, a, s->stream);
             for (int k = 0; k < 2; k++) {
                 HIP_TRY(hipEventRecord(s->join_ev[k], s->side[k]));
                 HIP_TRY(hipStreamWaitEvent(s->stream, s->join_ev[k], 0));
@@ -2414,7 +2424,9 @@ int psim_create(const psim_config* cfg, psim_handle** out) {
     // freed slots new blocks, which evens out the waves' uneven node mixes (the
     // resident grid left 4.1 of 6 waves/SIMD busy on average; 300 -> 272 us a
     // round on the survey line, profiles/r03/p10)
-    h->lite_blocks = grid("PSIM_LITE_GRID", psim::lite_grid(), 4 * psim::lite_grid());
+    h->lite_half = getenv("PSIM_LITE_WAVE") == nullptr;
+    h->lite_blocks = h->lite_half ? grid("PSIM_LITE_GRID", psim::lite_half_grid(), 4 * psim::lite_half_grid())
+                                  : grid("PSIM_LITE_GRID", psim::lite_grid(), 4 * psim::lite_grid());
     h->ptl_blocks = grid("PSIM_PTL_GRID", psim::ptl_grid(), psim::ptl_grid());
     {
         const char* e = getenv("PSIM_PHASE_TIMERS");

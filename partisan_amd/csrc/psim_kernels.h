@@ -125,6 +125,10 @@ __global__ void k_consume_pl(RoundArgs args);
 __global__ void k_shuf(RoundArgs args);
 // wave-per-node SHUFFLE terminals, replies and their merges (psim_consume.hip)
 __global__ void k_consume_lite(RoundArgs args);
+// the same with two nodes per wave, one per 32-lane half (psim_lite.hip)
+__global__ void k_lite_half(RoundArgs args);
+uint32_t lite_half_grid();
+uint32_t lite_half_block();
 // lane-per-node Plumtree phases (psim_consume.hip); hands k_pt what does not fit
 __global__ void k_ptl(RoundArgs args);
 // the Plumtree phase of the nodes k_relay listed (psim_consume.hip)

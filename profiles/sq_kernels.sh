@@ -12,7 +12,7 @@ O=$R/gpurun_out/$TAG
 mkdir -p $O
 cd /tmp && export TMPDIR=/tmp
 timeout -s KILL 150 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS GRBM_GUI_ACTIVE \
-  --kernel-include-regex "k_consume|k_pt|k_relay|k_shuf|k_term" -d $O/pmc -o run --output-format csv -- \
+  --kernel-include-regex "k_consume|k_pt|k_relay|k_shuf|k_term|k_lite" -d $O/pmc -o run --output-format csv -- \
   python3 $R/bench.py --no-cpu-baseline --no-check "$@" > $O/bench.json 2> $O/pmc.err || { echo "pmc failed"; tail -3 $O/pmc.err; exit 1; }
 cd $R
 F=$(find $O/pmc -name "*counter_collection.csv" | head -1)

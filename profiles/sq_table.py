@@ -8,7 +8,7 @@ import json
 import sys
 from collections import defaultdict
 
-KERNELS = ["k_relay", "k_shuf", "k_consume_lite", "k_term", "k_consume", "k_ptl", "k_pt"]
+KERNELS = ["k_relay", "k_shuf", "k_consume_lite", "k_lite_half", "k_term", "k_consume", "k_ptl", "k_pt"]
 
 
 def kname(s):

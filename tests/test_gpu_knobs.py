@@ -1,9 +1,9 @@
 """The engine's measurement knobs change launch shapes and algorithms, never
-results: the single-pass look-back scans and the fused scan + descriptor
-kernel (PSIM_SCAN_LB), another route bucket width (PSIM_ROUTE_WSHIFT), other
-grids for every node-round kernel (PSIM_*_GRID) and the HyParView kernels
-one after another instead of side by side (PSIM_SERIAL_PHASE) must reproduce the
-oracle bit for bit.  The knobs are read once per process, so each set runs in
+results: another route bucket width (PSIM_ROUTE_WSHIFT), other grids for
+every node-round kernel (PSIM_*_GRID), the HyParView kernels one after
+another instead of side by side (PSIM_SERIAL_PHASE) and the wave-per-node
+lite kernel instead of the two-nodes-per-wave one (PSIM_LITE_WAVE) must
+reproduce the oracle bit for bit.  The knobs are read once per process, so each set runs in
 a child process (tests/_knob_run.py)."""
 import os
 import subprocess
@@ -16,7 +16,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 
 
 @pytest.mark.parametrize("knobs", [
-    {"PSIM_SCAN_LB": "1", "PSIM_ROUTE_WSHIFT": "10"},
+    {"PSIM_ROUTE_WSHIFT": "10"},
+    {"PSIM_LITE_WAVE": "1"},
     {"PSIM_LITE_GRID": "x1", "PSIM_PTL_GRID": "x2", "PSIM_PT_GRID": "x2", "PSIM_CONSUME_GRID": "x2"},
     {"PSIM_SERIAL_PHASE": "1"},
 ])
