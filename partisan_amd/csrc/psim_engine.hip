@@ -1682,8 +1682,14 @@ int phase_consume(psim_handle* h, Shard* s, RoundArgs& a) {
         // 2^26: 15 ms of wave work a round) and side by side with
         // k_consume_lite the two took longer than one after the other
         // (node-round phase 61.0 -> 68.3 ms, profiles/r03/p36)
+        // Since round 4 (k_lite_half) the kernels run one after another by
+        // default: side by side with k_lite_half's 128-VGPR waves the phase
+        // took 0.61 ms against 0.58 serially, and the step 0.84 against 0.77
+        // (profiles/r04/p8); PSIM_CONCURRENT_PHASE=1 restores the side streams
+        // outside crash rounds (and, with the wave kernel, PSIM_LITE_WAVE=1)
+        static const bool conc_env = getenv("PSIM_CONCURRENT_PHASE") != nullptr;
         static const bool serial_env = getenv("PSIM_SERIAL_PHASE") != nullptr;
-        const bool serial = serial_env || a.crash_round;
+        const bool serial = serial_env || a.crash_round || !(conc_env || !h->lite_half);
         if (serial) {
             k_shuf<<<s->sgrid, BLK, 0, s->stream>>>(a);
             launch_lite(h, s, a, s->stream);
