@@ -37,7 +37,7 @@ S_NODE = 416                    # algorithmic state bytes per processed node (SU
 S_MSG = 64                      # message record bytes
 CHECK_NODES = 1 << 14           # the built-in sharding check
 CHECK_ROUNDS = 90
-SCHEDULE_VERSION = 3            # bumps when the event schedule of a run changes (PMC keys)
+SCHEDULE_VERSION = 4            # bumps when the event schedule of a run changes (PMC keys)
 OVF_KINDS = ("idmap", "pt_outstanding", "pt_sets_roots_msgs", "strategy", "conn")   # PSIM_OVF_*
 ALG_FORMULA = ("B = N_proc * 2 * 416 + M_in * 64 + M_out * 68 per round, N_proc = nodes with work "
                "(stats nodes_processed), M_in / M_out = delivered / emitted records.  Departs from "
@@ -59,6 +59,9 @@ def parse():
     p.add_argument("--cpu-workers", type=int, default=16,
                    help="processes of the all-cores CPU baseline (the GPU box's CPU share is 16)")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-baseline-only", action="store_true",
+                   help="print the cpu_baseline object alone (no GPU): e.g. a 2^20 sample with "
+                        "--cpu-sample-nodes 1048576, which takes minutes of bootstrap")
     p.add_argument("--no-check", action="store_true", help="skip the built-in sharding check")
     p.add_argument("--dry-run", action="store_true",
                    help="launcher test on CPU: the ranks rendezvous (gloo), time a host loop with the "
@@ -67,10 +70,13 @@ def parse():
                    help="diagnostic: G virtual shards of --nodes each on this one GPU (the sharded "
                         "partition / exchange / receive path with device copies instead of RCCL)")
     p.add_argument("--schedule", default="survey", choices=["survey", "doubling"],
-                   help="config C's event schedule.  survey (default): SURVEY 8(d) -- joins spread "
+                   help="the event schedule.  C, survey (default): SURVEY 8(d) -- joins spread "
                         "over a 64-round ramp, 100 warm-up rounds, then ONE broadcast from node 0 at the "
                         "first timed round; doubling: the round-2 line -- doubling bootstrap, --settle "
-                        "rounds, a broadcast from node 0 every 10 rounds throughout")
+                        "rounds, a broadcast from node 0 every 10 rounds throughout.  E, survey "
+                        "(default): the half/half partition at phase rounds 150-169, after the churn "
+                        "(SURVEY 8(d) E); doubling: round 3's E line, the partition at window rounds "
+                        "20-39, inside the churn")
     p.add_argument("--workload", default="C", choices=["C", "B", "D", "E"],
                    help="C (default, the headline line): HyParView+Plumtree; "
                         "B: full-membership strategy, fanout 5; D: SCAMP v2 (c=5); "
@@ -231,6 +237,36 @@ def _cpu_rows():
     return rows
 
 
+def cpu_share():
+    """What bounds this process's CPUs: the cgroup quota (v2 cpu.max, v1
+    cfs_quota_us / cfs_period_us), the affinity mask and the thread knobs the
+    box exports (OMP_NUM_THREADS etc.; 16 on the one-GPU box)."""
+    out = {"affinity_cpus": len(os.sched_getaffinity(0)), "nproc": os.cpu_count()}
+    raw = None
+    for path in ("/sys/fs/cgroup/cpu.max", "/sys/fs/cgroup/cpu/cpu.cfs_quota_us"):
+        try:
+            raw = open(path).read().strip()
+        except OSError:
+            continue
+        if path.endswith("cpu.max"):
+            q, _, per = raw.partition(" ")
+        else:
+            try:
+                per = open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read().strip()
+            except OSError:
+                per = ""
+            q = raw
+            raw = f"{q} {per}"
+        out["cgroup_cpu_max"] = {"file": path, "value": raw,
+                                 "quota_cpus": (int(q) / int(per)) if q.lstrip("-").isdigit() and int(q) > 0
+                                 and per.isdigit() else None}
+        break
+    if raw is None:
+        out["cgroup_cpu_max"] = None
+    out["env"] = {k: os.environ[k] for k in ("OMP_NUM_THREADS", "MAX_JOBS") if k in os.environ}
+    return out
+
+
 def cpu_baseline(args):
     """Run before the GPU is touched (worker processes are forked).  One
     thread, then `workers` independent oracle processes on the same sample
@@ -267,7 +303,7 @@ def cpu_baseline(args):
             "rows": _cpu_rows(),
             "reference": reference_probe(),
             "cpu_model": cpu_model(), "nproc": os.cpu_count(),
-            "affinity_cpus": len(os.sched_getaffinity(0))}
+            "affinity_cpus": len(os.sched_getaffinity(0)), "cpu_share": cpu_share()}
 
 
 # --------------------------------------------------------- shard check --
@@ -379,7 +415,7 @@ def src_hash():
 def pmc_key(args, world, n):
     return {"workload": args.workload, "nodes": n, "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "seed": args.seed, "schedule": SCHEDULE_VERSION,
-            "events": args.schedule if args.workload == "C" else "doubling", "src": src_hash()}
+            "events": args.schedule if args.workload in ("C", "E") else "doubling", "src": src_hash()}
 
 
 def pmc_traffic(key):
@@ -503,6 +539,10 @@ def main():
         raise SystemExit("bench: --vshards is a single-GPU diagnostic")
 
     # the CPU baseline first, while no GPU has been touched (it forks)
+    if args.cpu_baseline_only:
+        print(json.dumps({"cpu_baseline": cpu_baseline(args), "workload": args.workload,
+                          "schedule": args.schedule, "rounds": args.cpu_sample_rounds}), flush=True)
+        return
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.workload == "C":
         cpu = cpu_baseline(args)
@@ -627,10 +667,16 @@ def main():
                                 "broadcast from node 0 every 10 rounds (not SURVEY 8(d)'s schedule: the doubling "
                                 "ramp starts half the overlay in one round, aligning its shuffle timers)")
                                if args.workload == "C" else
-                               ("E: HyParView+Plumtree, 20% churn over 100 rounds (crash, restart, rejoin), "
-                                "half/half partition for rounds 20-39, broadcast every 10 rounds"),
+                               ("E: HyParView+Plumtree, doubling bootstrap, 20% churn over phase rounds 40-139 "
+                                "(crash, restart, rejoin the next round), half/half partition for phase rounds "
+                                + (f"{sched.p_on}-{sched.p_off - 1} (SURVEY 8(d) E: after the churn)"
+                                   if args.schedule == "survey" else
+                                   f"{sched.p_on}-{sched.p_off - 1} (window rounds 20-39, inside the churn: "
+                                   "round 3's line)")
+                                + ", broadcast from node 0 every 10 rounds; the window starts at phase round "
+                                f"{t_start}"),
                    "nodes": n, "nodes_per_gpu": args.nodes, "seed": args.seed,
-                   "schedule": "survey" if survey else "doubling",
+                   "schedule": args.schedule if args.workload in ("C", "E") else "doubling",
                    "untimed_broadcast_rounds": 0 if survey else STEADY_ROUNDS + args.warmup,
                    "broadcasts_before_window": 0 if survey else (t_start + BCAST_PERIOD - 1) // BCAST_PERIOD,
                    "broadcasts_in_window": n_bc,

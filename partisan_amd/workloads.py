@@ -89,9 +89,13 @@ def star_join(n_nodes, at_round=1):
 def churn_schedule(n_nodes, seed, frac, first_round, n_rounds, protect=(0,)):
     """Config E churn: frac*N crashes spread uniformly over n_rounds starting
     at first_round; each crashed node restarts the next round and rejoins a
-    uniformly drawn node that is up when the JOIN is sent (SURVEY.md section
-    8(d) E): not one of the restarting nodes, nor one crashing in that round.
-    The contacts of round k's victims are used at round k + 1."""
+    uniformly drawn node that is up when the JOIN is sent and when it arrives
+    (crashes "replaced by as many fresh joins"): not
+    one of the restarting nodes, nor one crashing in the round the JOIN is
+    sent (k + 1) or delivered (k + 2) -- a JOIN that meets a crashed contact
+    is dropped and HyParView never retries it (hv:500-515), which left each
+    such rejoiner isolated until round 4.  The contacts of round k's victims
+    are used at round k + 1."""
     rng = _rng(seed, 2)
     total = int(frac * n_nodes)
     cand = np.setdiff1d(np.arange(n_nodes, dtype=np.uint32), np.array(protect, np.uint32))
@@ -99,7 +103,7 @@ def churn_schedule(n_nodes, seed, frac, first_round, n_rounds, protect=(0,)):
     per = np.array_split(victims, n_rounds)
     out = []
     for k, v in enumerate(per):
-        down = np.concatenate([v, per[k + 1]]) if k + 1 < len(per) else v
+        down = np.concatenate([v] + [per[j] for j in (k + 1, k + 2) if j < len(per)])
         contacts = rng.integers(0, n_nodes, size=v.size, dtype=np.uint64).astype(np.uint32)
         bad = np.isin(contacts, down)
         while bad.any():                      # redraw (uniform over the nodes up)
@@ -127,12 +131,18 @@ class BenchSchedule:
     untimed broadcast rounds, `warmup` rounds, the window; a broadcast from
     node 0 every BCAST_PERIOD rounds throughout.  E adds 0.2 N crashes over
     100 rounds from STEADY_ROUNDS (each victim restarts and rejoins the next
-    round) and the half/half partition for rounds 20-39 of the window.
+    round) and the half/half partition for rounds 20-39 of the window: in the
+    middle of the churn (round 3's E line).
+    E, schedule "survey": the same bootstrap, broadcasts and churn, and the
+    partition where SURVEY 8(d) E puts it -- 20 rounds from phase round
+    E_PARTITION (150), ten rounds after the last churn rejoin (round 140),
+    whatever the window.
     Phase-round i counts from the end of the bootstrap; the window starts at
     i = t_start."""
     STEADY_ROUNDS = 40
     BCAST_PERIOD = 10
     SURVEY_WARM = 100
+    E_PARTITION = 150
 
     def __init__(self, workload, schedule, n, seed, warmup, settle=60):
         self.workload, self.n, self.seed = workload, n, seed
@@ -146,7 +156,10 @@ class BenchSchedule:
             for r, v, c in churn_schedule(n, seed, 0.2, self.STEADY_ROUNDS, 100):
                 self.churn[r] = (v, c)
             self.part = half_partition(n)
-            self.p_on, self.p_off = self.t_start + 20, self.t_start + 40
+            if schedule == "survey":
+                self.p_on, self.p_off = self.E_PARTITION, self.E_PARTITION + 20
+            else:
+                self.p_on, self.p_off = self.t_start + 20, self.t_start + 40
 
     def bootstrap(self):
         """(join schedule, the round run_schedule runs to)"""

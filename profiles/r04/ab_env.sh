@@ -8,7 +8,7 @@ for pass in 1 2; do
   for spec in "$@"; do
     name=${spec%%:*}; vars=${spec#*:}
     [ "$vars" = "$spec" ] && vars=""
-    timeout -k 10 300 env $vars python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-check > $O/bench_${name}_$pass.json 2> $O/bench_${name}_$pass.err || { echo "bench $name failed"; tail -3 $O/bench_${name}_$pass.err; exit 1; }
+    timeout -k 10 300 env $vars python bench.py ${BENCH_ARGS:---steps 20 --warmup 5} --no-cpu-baseline --no-check > $O/bench_${name}_$pass.json 2> $O/bench_${name}_$pass.err || { echo "bench $name failed"; tail -3 $O/bench_${name}_$pass.err; exit 1; }
     python - $O/bench_${name}_$pass.json $name $pass <<'PY'
 import json, sys
 d = json.load(open(sys.argv[1]))

@@ -7,7 +7,7 @@ mkdir -p $O
 for pass in 1 2; do
   for v in "$@"; do
     if [ "$v" = base ]; then unset PSIM_LIB; else export PSIM_LIB=$v; fi
-    timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-check > $O/bench_${v}_$pass.json 2> $O/bench_${v}_$pass.err || { echo "bench $v failed"; tail -3 $O/bench_${v}_$pass.err; exit 1; }
+    timeout -k 10 300 python bench.py ${BENCH_ARGS:---steps 20 --warmup 5} --no-cpu-baseline --no-check > $O/bench_${v}_$pass.json 2> $O/bench_${v}_$pass.err || { echo "bench $v failed"; tail -3 $O/bench_${v}_$pass.err; exit 1; }
     python - $O/bench_${v}_$pass.json $v $pass <<'PY'
 import json, sys
 d = json.load(open(sys.argv[1]))

@@ -129,8 +129,8 @@ def reliability(sim, sched, i, marks=(10, 20, 40)):
     return out
 
 
-def run(make, n, seed=1, warmup=10, points=POINTS):
-    sched = W.BenchSchedule("E", "doubling", n, seed, warmup)
+def run(make, n, seed=1, warmup=10, points=POINTS, schedule="doubling"):
+    sched = W.BenchSchedule("E", schedule, n, seed, warmup)
     sim = make(default_config(n_nodes=n, seed=seed))
     boot, until = sched.bootstrap()
     sim.run_schedule(boot, until)
@@ -155,6 +155,7 @@ def main():
     p.add_argument("--backend", choices=["gpu", "oracle"], required=True)
     p.add_argument("--nodes", type=int, nargs="+", required=True)
     p.add_argument("--seed", type=int, default=1)
+    p.add_argument("--schedule", choices=["doubling", "survey"], default="doubling")
     a = p.parse_args()
     if a.backend == "gpu":
         from partisan_amd import Simulator as make
@@ -162,8 +163,9 @@ def main():
         from _oracle import Oracle as make
     for n in a.nodes:
         t = time.time()
-        rows, rel = run(make, n, a.seed)
-        print(json.dumps({"backend": a.backend, "nodes": n, "seed": a.seed, "wall_s": round(time.time() - t, 1),
+        rows, rel = run(make, n, a.seed, schedule=a.schedule)
+        print(json.dumps({"backend": a.backend, "nodes": n, "seed": a.seed, "schedule": a.schedule,
+                          "wall_s": round(time.time() - t, 1),
                           "points": rows, "reliability": rel}), flush=True)
 
 

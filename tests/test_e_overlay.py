@@ -12,7 +12,12 @@ on the oracle here and on the GPU at 2^18 nodes.
   * a broadcast after the churn reaches the whole giant component within
     20 rounds (Plumtree reliability = the overlay's connectivity).
 The bounds: outside <= lost joins (every outside node is explained by one
-lost join, directly or through its contact) and >= 60% lost-join nodes."""
+lost join, directly or through its contact) and >= 60% lost-join nodes.
+
+With the partition where SURVEY 8(d) E puts it -- phase rounds 150-169,
+after the churn (schedule "survey", bench.py --workload E's default) -- no
+rejoin meets it: the overlay heals to one component within 49 rounds of the
+last rejoin and a broadcast then reaches every live node."""
 import pytest
 
 import e_overlay as E
@@ -41,3 +46,23 @@ def test_e_overlay_gpu():
     rows, rel = E.run(Simulator, 1 << 18)
     check(rows, rel)
     assert rows[-1]["outside_frac"] < 0.03, rows[-1]
+
+
+def check_survey(rows, rel):
+    for r in rows:
+        assert r["lost_joins"] == 0 and r["outside_victims"] == r["outside"], r
+        assert r["outside_frac"] < 0.002, r
+    assert rows[1]["outside"] == 0 and rows[2]["outside"] == 0, rows
+    assert rel["delivered_20"] == 1.0 and rel["delivered_40"] == 1.0, rel
+
+
+def test_e_overlay_survey_oracle():
+    rows, rel = E.run(Oracle, 16384, schedule="survey")
+    check_survey(rows, rel)
+
+
+@pytest.mark.gpu
+def test_e_overlay_survey_gpu():
+    from partisan_amd import Simulator
+    rows, rel = E.run(Simulator, 1 << 18, schedule="survey")
+    check_survey(rows, rel)
