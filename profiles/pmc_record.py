@@ -5,8 +5,9 @@ profiles/pmc_records.json, which bench.py reads back by its pmc_key.
 
 Window: the `steps` timed rounds are the dispatches of each kernel before the
 overlay-drain rounds bench.py runs after its window (overlay.rounds_drained).
-Per round: the sum over the node-round kernels (k_relay, k_shuf, k_term or k_consume_lite,
-k_consume, k_ptl, k_pt).
+Per round: the sum over the node-round kernels (k_relay, k_shuf, k_lite_half
+or k_consume_lite, k_consume, k_ptq or k_ptl, k_pt; k_consume_pl for the
+pluggable lines B and D, which drain no rounds after their window).
 
 Units and corrections (profiles/calib/, measured on this MI355X): FETCH_SIZE
 counts 64-B memory requests -- a random dword or a random 64-B record reads as
@@ -21,7 +22,8 @@ import json
 import os
 import sys
 
-KERNELS = ("k_relay(", "k_shuf(", "k_consume_lite(", "k_term(", "k_consume(", "k_ptl(", "k_pt(")
+KERNELS = ("k_relay(", "k_shuf(", "k_consume_lite(", "k_lite_half(", "k_term(", "k_consume(", "k_ptl(", "k_ptq(",
+           "k_pt(", "k_consume_pl(")
 
 
 def per_round(path, steps, tail):
@@ -37,7 +39,7 @@ def per_round(path, steps, tail):
 
 def main():
     bench = json.load(open(sys.argv[1]))
-    steps, tail = bench["steps"], bench["overlay"]["rounds_drained"]
+    steps, tail = bench["steps"], bench.get("overlay", {}).get("rounds_drained", 0)
     fetch = per_round(sys.argv[2], steps, tail)
     write = per_round(sys.argv[3], steps, tail)
     rec = {"key": bench["pmc_key"],

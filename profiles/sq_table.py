@@ -8,7 +8,8 @@ import json
 import sys
 from collections import defaultdict
 
-KERNELS = ["k_relay", "k_shuf", "k_consume_lite", "k_lite_half", "k_term", "k_consume", "k_ptl", "k_pt"]
+KERNELS = ["k_relay", "k_shuf", "k_consume_lite", "k_lite_half", "k_term", "k_consume", "k_ptl", "k_ptq", "k_pt",
+           "k_consume_pl"]
 
 
 def kname(s):
@@ -20,7 +21,7 @@ def kname(s):
 def main():
     rows = list(csv.DictReader(open(sys.argv[1])))
     b = json.loads(open(sys.argv[2]).read().strip().splitlines()[-1])
-    steps, tail = b["steps"], b["overlay"]["rounds_drained"]
+    steps, tail = b["steps"], b.get("overlay", {}).get("rounds_drained", 0)
     per = defaultdict(lambda: defaultdict(dict))       # kernel -> dispatch -> counter -> value
     for r in rows:
         k = kname(r["Kernel_Name"])

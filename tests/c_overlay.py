@@ -105,6 +105,7 @@ def run(make, n, seed=1, points=POINTS):
         r, s = classify(sim)
         rows.append(r)
         sets.append(s)
+    sim.run_schedule(boot, until)
     for i in range(sched.t_start + WINDOW):
         sched.apply(sim, i)
         sim.step(1)
@@ -115,6 +116,8 @@ def run(make, n, seed=1, points=POINTS):
     rows.append(r)
     sets.append(s)
     stable = next(rows[k]["round"] for k in range(len(sets)) if all(sets[j] == s for j in range(k, len(sets))))
+    if not points:
+        stable = None                             # (no earlier report point to compare with)
     return {"rows": rows, "stable_since": stable}
 
 
@@ -123,6 +126,8 @@ def main():
     p.add_argument("--backend", choices=["gpu", "oracle"], required=True)
     p.add_argument("--nodes", type=int, nargs="+", required=True)
     p.add_argument("--seed", type=int, default=1)
+    p.add_argument("--points", type=int, nargs="*", default=list(POINTS),
+                   help="bootstrap rounds to classify at before the window's end (none: the end only)")
     a = p.parse_args()
     if a.backend == "gpu":
         from partisan_amd import Simulator as make
@@ -130,7 +135,7 @@ def main():
         from _oracle import Oracle as make
     for n in a.nodes:
         t = time.time()
-        r = run(make, n, a.seed)
+        r = run(make, n, a.seed, tuple(a.points))
         print(json.dumps({"backend": a.backend, "nodes": n, "seed": a.seed, "wall_s": round(time.time() - t, 1)} | r),
               flush=True)
 
