@@ -685,10 +685,10 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": tsrc,
                      "traffic_upper": trec.get("traffic_upper_per_launch") if trec else None,
-                     "kernel": "k_relay + k_shuf + k_consume_lite + k_consume + k_ptl + k_pt (the node-round "
-                               "phase: one launch of each per round on one stream, timed by s_memrealtime stamps "
-                               "stored as k_relay's first block starts and as the first kernel after k_pt "
-                               "starts)",
+                     "kernel": "k_relay + k_shuf + k_lite_half + k_consume + k_ptl + k_pt (the node-round "
+                               "phase: one launch of each per round, one after another on the shard's stream, "
+                               "timed by s_memrealtime stamps stored as k_relay's first block starts and as the "
+                               "first kernel after k_pt starts)",
                      "alg_bytes_per_launch": per_launch_bytes,
                      "alg_bytes_formula": ALG_FORMULA,
                      "avg_launch_ms": per_launch_s * 1e3,

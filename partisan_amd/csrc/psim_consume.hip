@@ -1763,14 +1763,14 @@ __global__ void __launch_bounds__(64 * PSIM_LITE_WPB, PSIM_LITE_WAVES) k_consume
     w.SC = 0;
     w.digest = 0;
     w.KM = magic_lanes();
-    const uint32_t na = *kargs().n_lite;
+    const uint32_t n0 = kargs().n_lite[0], na = n0 + kargs().n_lite[1];
     if (gw < na) {
         const uint32_t last = na - 1;
         KArgs& a0 = kargs();
-        NodeIn x = load_node<false>(a0, reinterpret_cast<const uint32_t*>(kargs().desc_lite + gw)[lane_id() & 3]);
+        NodeIn x = load_node<false>(a0, reinterpret_cast<const uint32_t*>(kargs().desc_lite + lite_at(a0, n0, gw))[lane_id() & 3]);
         NodeX y = load_x<true>(kargs(), x);
-        NodeIn xn = load_node<false>(kargs(), reinterpret_cast<const uint32_t*>(kargs().desc_lite + min(gw + nw, last))[lane_id() & 3]);
-        uint32_t d = reinterpret_cast<const uint32_t*>(kargs().desc_lite + min(gw + 2 * nw, last))[lane_id() & 3];
+        NodeIn xn = load_node<false>(kargs(), reinterpret_cast<const uint32_t*>(kargs().desc_lite + lite_at(a0, n0, min(gw + nw, last)))[lane_id() & 3]);
+        uint32_t d = reinterpret_cast<const uint32_t*>(kargs().desc_lite + lite_at(a0, n0, min(gw + 2 * nw, last)))[lane_id() & 3];
         for (uint32_t i = gw; i < na; i += nw) {
             STAMP(w, 0);
             begin_node(w, x, y);
@@ -1780,7 +1780,7 @@ __global__ void __launch_bounds__(64 * PSIM_LITE_WPB, PSIM_LITE_WAVES) k_consume
             writeback_lite(w);
             STAMP(w, 10);
             NodeIn xnn = load_node<false>(kargs(), d);
-            d = reinterpret_cast<const uint32_t*>(kargs().desc_lite + min(i + 3 * nw, last))[lane_id() & 3];
+            d = reinterpret_cast<const uint32_t*>(kargs().desc_lite + lite_at(kargs(), n0, min(i + 3 * nw, last)))[lane_id() & 3];
             x = xn; y = yn; xn = xnn;
             STAMP(w, 11);
         }
@@ -2063,6 +2063,12 @@ DEV void block_append(bool go, const uint4& D, uint4* desc, uint32_t* cnt, uint3
 #ifndef PSIM_RELAY_WAVES
 #define PSIM_RELAY_WAVES 4
 #endif
+#ifndef PSIM_PTL_BIN          // k_ptl's list binned by BROADCAST presence (0: one list, for A/B)
+#define PSIM_PTL_BIN 1
+#endif
+#ifndef PSIM_LITE_BIN         // the lite list binned by SHUFFLE terminals (0: one list, for A/B)
+#define PSIM_LITE_BIN 1
+#endif
 __global__ void __launch_bounds__(256, PSIM_RELAY_WAVES) k_relay(RoundArgs) {
     if (*kargs().ctl) return;                         // an aborted batch (run_batch)
     // the node-round phase starts here: its span's first stamp (the last is
@@ -2070,7 +2076,7 @@ __global__ void __launch_bounds__(256, PSIM_RELAY_WAVES) k_relay(RoundArgs) {
     if (blockIdx.x == 0 && threadIdx.x == 0) kargs().ktime[0] = __builtin_amdgcn_s_memrealtime();
     enum { R_PROC, R_DELIV, R_SHUF, R_FAIL, R_DIGEST, R_BOUND, R_N };
     __shared__ unsigned long long sst[R_N];
-    __shared__ uint32_t wc5[5][5];                    // per list: the wave counts, then the block's base
+    __shared__ uint32_t wc5[7][5];                    // per list: the wave counts, then the block's base
     if (threadIdx.x < R_N) sst[threadIdx.x] = 0;
     __syncthreads();
     const uint32_t l = lane_id();
@@ -2081,7 +2087,7 @@ __global__ void __launch_bounds__(256, PSIM_RELAY_WAVES) k_relay(RoundArgs) {
         KArgs& a = kargs();                           // (re-read per step, not held in SGPRs)
         const uint32_t P = base + threadIdx.x;
         uint4 D = make_uint4(0, 0, 0, 0);
-        bool heavy = false, to_pt = false, relay = false, maps = false, shuf = false, lite = false;
+        bool heavy = false, to_pt = false, relay = false, maps = false, shuf = false, lite = false, bcast = false, term = false;
         Hdr h;
         uint32_t ik = 0, oend = 0;
         uint4 act0 = make_uint4(0, 0, 0, 0), act1 = act0;
@@ -2103,6 +2109,7 @@ __global__ void __launch_bounds__(256, PSIM_RELAY_WAVES) k_relay(RoundArgs) {
             // SHUFFLE with TTL left (a relay while |active| > 1)
             uint32_t hvn = 0;
             bool all_relay = true, all_shuf = true, term_out = false;
+            bcast = false; term = false;
             const uint32_t av[8] = {act0.x, act0.y, act0.z, act0.w, act1.x, act1.y, act1.z, act1.w};
             // (four records' first 16 B issued before any is waited on: a
             // loop of single loads waits one memory latency per record)
@@ -2117,6 +2124,7 @@ __global__ void __launch_bounds__(256, PSIM_RELAY_WAVES) k_relay(RoundArgs) {
 #pragma unroll
                 for (int q = 0; q < 4; q++) {
                     const uint32_t tt = T[q].y, type = tt & 0xFF;
+                    bcast |= j + q < ik && type == PSIM_MSG_PT_BROADCAST;
                     if (type < PSIM_MSG_PT_BROADCAST || type >= PSIM_MSG_XBOT_OPTIMIZATION) {   // (X-BOT's: heavy)
                         hvn++;
                         maps |= type <= PSIM_MSG_NEIGHBOR_ACCEPTED;   // id maps (hv:703-1089)
@@ -2126,6 +2134,7 @@ __global__ void __launch_bounds__(256, PSIM_RELAY_WAVES) k_relay(RoundArgs) {
                         // a walk that ends here replies to its Sender: maybe_connect
                         // (hv:1127) opens a lingering connection to a Sender outside
                         // the active view -- the connection table's path, k_consume
+                        term |= type == PSIM_MSG_SHUFFLE && !relays;
                         if (type == PSIM_MSG_SHUFFLE && !relays) {
                             bool in = false;
 #pragma unroll
@@ -2185,36 +2194,43 @@ __global__ void __launch_bounds__(256, PSIM_RELAY_WAVES) k_relay(RoundArgs) {
         // hands k_pt the ones that do not fit a lane)
         const bool origin_node = ((D.z >> 28) & DESC_ORIGIN) != 0;
         {
-            // the five lists at once: one barrier-separated count, the five
-            // block atomics from five lanes of one instruction (one after
-            // another they were five serial L2 round trips per block step)
-            const bool g[5] = {P < na && heavy, P < na && to_pt && origin_node, P < na && to_pt && !origin_node,
-                               P < na && shuf, P < na && lite};
-            uint64_t m[5];
+            // the seven lists at once: one barrier-separated count, the
+            // block atomics from seven lanes of one instruction (one after
+            // another they were serial L2 round trips per block step); k_ptl's
+            // list as two, BROADCAST nodes from its front, the others from
+            // its back (ptl_desc), and the lite list likewise by SHUFFLE
+            // terminals (lite_at)
+            const bool ptl = P < na && to_pt && !origin_node, lt = P < na && lite;
+            const bool g[7] = {P < na && heavy, P < na && to_pt && origin_node, ptl && (bcast || !PSIM_PTL_BIN),
+                               P < na && shuf, lt && (term || !PSIM_LITE_BIN), ptl && !(bcast || !PSIM_PTL_BIN),
+                               lt && !(term || !PSIM_LITE_BIN)};
+            uint64_t m[7];
 #pragma unroll
-            for (int k = 0; k < 5; k++) m[k] = ballot(g[k]);
+            for (int k = 0; k < 7; k++) m[k] = ballot(g[k]);
             const uint32_t wv = threadIdx.x >> 6, nwv = blockDim.x >> 6;
             __syncthreads();                          // the previous step's readers of wc5 are done
             if (l == 0)
 #pragma unroll
-                for (int k = 0; k < 5; k++) wc5[k][wv] = popc(m[k]);
+                for (int k = 0; k < 7; k++) wc5[k][wv] = popc(m[k]);
             __syncthreads();
-            if (threadIdx.x < 5) {
+            if (threadIdx.x < 7) {
                 const uint32_t k = threadIdx.x;
                 uint32_t t = 0;
                 for (uint32_t j = 0; j < nwv; j++) t += wc5[k][j];
-                uint32_t* cnt = k == 0 ? a.n_slow : k == 1 ? a.n_pt : k == 2 ? a.n_ptl : k == 3 ? a.n_shuf : a.n_lite;
+                uint32_t* cnt = k == 0 ? a.n_slow : k == 1 ? a.n_pt : k == 2 ? a.n_ptl : k == 3 ? a.n_shuf
+                              : k == 4 ? a.n_lite : k == 5 ? a.n_ptl + 1 : a.n_lite + 1;
                 wc5[k][4] = t ? atomicAdd(cnt, t) : 0u;
             }
             __syncthreads();
 #pragma unroll
-            for (int k = 0; k < 5; k++)
+            for (int k = 0; k < 7; k++)
                 if (g[k]) {
                     uint32_t b0 = wc5[k][4];
                     for (uint32_t j = 0; j < wv; j++) b0 += wc5[k][j];
-                    uint4* desc = k == 0 ? a.desc_slow : k == 1 ? a.desc_pt : k == 2 ? a.desc_ptl
+                    const uint32_t at = b0 + popc(m[k] & lt_mask());
+                    uint4* desc = k == 0 ? a.desc_slow : k == 1 ? a.desc_pt : k == 2 || k == 5 ? a.desc_ptl
                                 : k == 3 ? a.desc_shuf : a.desc_lite;
-                    desc[b0 + popc(m[k] & lt_mask())] =
+                    desc[k >= 5 ? a.n_local - 1 - at : at] =
                         k == 0 && maps ? make_uint4(D.x, D.y, D.z | DESC_MAPS_BIT, D.w) : D;
                 }
         }
@@ -2452,16 +2468,17 @@ __global__ void __launch_bounds__(256) k_shuf(RoundArgs) {
 // lazy peers and a few outstanding entries, and its Plumtree phase is a
 // BROADCAST (first delivery: eager push + lazy adds; duplicate: PRUNE), some
 // PRUNEs, IHAVE answers and acks, then the lazy tick.  A lane holds slot 0's
-// eager and lazy sets (16 entries each) and the outstanding table (16
-// entries) in registers -- ordsets inserts / deletes as unrolled selects --
-// when the node's data fits that: no root in slots 1-3, every message's root
-// slot 0's (or slot 0 free and one root), the sets and the table far enough
-// below 16 that this round's adds fit, no outstanding extension row.  Any
-// other node is appended to k_pt's list and runs there (the wave path).
+// eager and lazy sets (16 entries each) and the outstanding table (PTL_CAP
+// entries) in LDS columns when the node's data fits that: no root in slots
+// 1-3, every message's root slot 0's (or slot 0 free and one root), the sets
+// and the table far enough below their capacity that this round's adds fit,
+// no outstanding extension row.  Any other node is appended to k_pt's list
+// and runs there (the wave path).  k_relay orders the list: nodes with a
+// BROADCAST first, so most waves run one kind of node (ptl_desc).
 // Same handlers as pt_handle / pt_push / the lazy tick (pt:288-313, :341-345,
 // :368-453, :562-631): the same records, sequence numbers, digest, stats.
-#ifndef PSIM_PTL_CAP
-#define PSIM_PTL_CAP 16
+#ifndef PSIM_PTL_CAP          // (12: 14 KiB of LDS a block, 11 per CU; 16 took 16 KiB, 9 per CU --
+#define PSIM_PTL_CAP 12       //  at 2^26 12 measured 0.8 ms a round faster, profiles/r04/ab3e)
 #endif
 #ifndef PSIM_PTL_SET_CAP
 #define PSIM_PTL_SET_CAP 16
@@ -2469,7 +2486,7 @@ __global__ void __launch_bounds__(256) k_shuf(RoundArgs) {
 constexpr int PTL_CAP = PSIM_PTL_CAP;           // outstanding entries a lane holds
 constexpr int PTL_SET = PSIM_PTL_SET_CAP;       // eager / lazy entries a lane holds
 
-constexpr uint32_t PTL_BLK = PTL_BLOCK;   // k_ptl block: one wave, 16 KiB of per-lane tables
+constexpr uint32_t PTL_BLK = PTL_BLOCK;   // k_ptl block: one wave, 14 KiB of per-lane tables
 
 // A lane's tables in LDS, entry i of lane t at row i, column t (conflict-free):
 // unrolled scans read fixed offsets, run-time indexing is one access
@@ -2617,7 +2634,7 @@ __global__ void PTL_BOUNDS k_ptl(RoundArgs) {
     if (threadIdx.x < T_N + 1) sst[threadIdx.x] = 0;
     __syncthreads();
     const uint32_t l = lane_id();
-    const uint32_t nq = *kargs().n_ptl;
+    const uint32_t nq0 = kargs().n_ptl[0], nq = nq0 + kargs().n_ptl[1];
     uint32_t v[T_N] = {};
     uint64_t dig = 0;
     const uint32_t X0[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -2633,7 +2650,7 @@ __global__ void PTL_BOUNDS k_ptl(RoundArgs) {
         uint4 D = make_uint4(0, 0, 0, 0);
         uint32_t root0 = NONE, rtw4 = 0, rtw5 = 0, w10 = 0, w11 = 0, start = 0, act_n = 0, tmask = 0;
         if (P < nq) {
-            D = a.desc_ptl[P];
+            D = ptl_desc(a, nq0, P);
             const size_t li = D.x - a.lo;
             const uint32_t* hp = reinterpret_cast<const uint32_t*>(a.hdr + li);
             const uint4 hq1 = reinterpret_cast<const uint4*>(hp)[1], hq2 = reinterpret_cast<const uint4*>(hp)[2];
@@ -2906,7 +2923,9 @@ int debug_stamps(unsigned long long* out) {
     unsigned long long z[32] = {0};
     if (hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), z, sizeof z) != hipSuccess) return -1;
     if (hipMemcpyToSymbol(HIP_SYMBOL(g_stamps_lite), z, sizeof z) != hipSuccess) return -1;
-    return 64;
+    // k_lite_half's, when it ran (psim_lite.hip): 96 entries
+    if (debug_stamps_half(out + 64) != 32) return -1;
+    return 96;
 }
 #else
 int debug_stamps(unsigned long long*) { return 0; }

@@ -618,8 +618,8 @@ __global__ void __launch_bounds__(256) k_node_prep(RoundArgs a, const unsigned l
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         a.ktime[0] = ~0ull; a.ktime[1] = 0; *a.n_slow = 0; *a.n_pt = 0;
         if (a.n_shuf) *a.n_shuf = 0;
-        if (a.n_lite) *a.n_lite = 0;
-        if (a.n_ptl) *a.n_ptl = 0;
+        if (a.n_lite) { a.n_lite[0] = 0; a.n_lite[1] = 0; }
+        if (a.n_ptl) { a.n_ptl[0] = 0; a.n_ptl[1] = 0; }
         if (a.n_stop) *a.n_stop = 0;
     }
     __syncthreads();
@@ -1232,7 +1232,8 @@ struct psim_handle {
     // the lite list's kernel: k_lite_half, two nodes per wave (psim_lite.hip);
     // PSIM_LITE_WAVE=1 keeps the wave-per-node k_consume_lite (A/B)
     bool lite_half = true;
-    uint32_t ptl_blocks = 1024;         // ... and k_ptl blocks
+    uint32_t ptl_blocks = 1024;         // ... and k_ptl / k_ptq blocks
+    bool ptl_quarter = false;           // k_ptq (PSIM_PTL_QUARTER=1) or k_ptl
     uint64_t round = 0;
     // a round failed half-way (psim_step returned an error from inside a
     // round or batch): the state is not a round boundary any more, so every
@@ -1562,7 +1563,9 @@ int phase_events_prepare(psim_handle* h, Shard* s, const RoundCtl& ctl, RoundArg
         // (k_lite_half: two nodes per wave)
         const uint32_t lnodes = h->lite_half ? psim::lite_half_block() * 2 : psim::lite_block();
         s->lgrid = hv ? std::min<uint32_t>((uint32_t)((n + lnodes - 1) / lnodes), h->lite_blocks) : 0;
-        s->qgrid = hv && h->cfg.plumtree ? std::min<uint32_t>((n + PTL_BLOCK - 1) / PTL_BLOCK, h->ptl_blocks) : 0;
+        // (k_ptq: four nodes per wave)
+        const uint32_t qnodes = h->ptl_quarter ? psim::ptq_nodes() : PTL_BLOCK;
+        s->qgrid = hv && h->cfg.plumtree ? std::min<uint32_t>((uint32_t)((n + qnodes - 1) / qnodes), h->ptl_blocks) : 0;
         TRY(s->stat_part.ensure((size_t)(s->pgrid + s->cgrid + s->rgrid + s->tgrid + s->sgrid + s->lgrid + s->qgrid) *
                                 NST));
         k_node_prep<<<s->pgrid, BLK, 0, s->stream>>>(a, s->bmask.p, s->bound.p, s->stat_part.p, s->ocnt.p,
@@ -1706,7 +1709,10 @@ int phase_consume(psim_handle* h, Shard* s, RoundArgs& a) {
                 HIP_TRY(hipStreamWaitEvent(s->stream, s->join_ev[k], 0));
             }
         }
-        if (s->qgrid) k_ptl<<<s->qgrid, PTL_BLOCK, 0, s->stream>>>(a);
+        if (s->qgrid) {
+            if (h->ptl_quarter) k_ptq<<<s->qgrid, psim::ptq_block(), 0, s->stream>>>(a);
+            else k_ptl<<<s->qgrid, PTL_BLOCK, 0, s->stream>>>(a);
+        }
         if (s->tgrid) {
             RoundArgs c = a;
             c.desc = s->desc_pt.p;
@@ -2007,7 +2013,8 @@ int run_round(psim_handle* h, uint64_t* st, bool events_applied = false) {
             std::fprintf(stderr, "psim: round %llu shard %u: %u nodes with work, %u to k_consume, %u to k_pt, "
                          "%u to k_shuf, %u to k_consume_lite, %u to k_ptl, outbox bound %llu, emitted %llu\n",
                          (unsigned long long)h->round, s->idx, read1(s, s->d_nact.p), read1(s, s->n_slow.p),
-                         read1(s, s->n_pt.p), read1(s, s->n_shuf.p), read1(s, s->n_lite.p), read1(s, s->n_ptl.p),
+                         read1(s, s->n_pt.p), read1(s, s->n_shuf.p), read1(s, s->n_lite.p) + read1(s, s->n_lite.p + 1),
+                         read1(s, s->n_ptl.p) + read1(s, s->n_ptl.p + 1),
                          (unsigned long long)s->pin[PIN_TOTAL], (unsigned long long)em);
         }
         if (s->pin[NST] != ~0ull && s->pin[NST + 1] > s->pin[NST]) {   // 100 MHz ticks
@@ -2266,7 +2273,14 @@ int shard_alloc(psim_handle* h, Shard* s) {
     rc |= s->origin.alloc(n); rc |= s->slots.alloc(2 * PSIM_MSG_SLOTS);
     rc |= s->pt_out.alloc(n * OUT_IN); rc |= s->start.alloc(n);
     if (h->cfg.manager != PSIM_MANAGER_PLUGGABLE) rc |= s->conn.alloc(n * PSIM_CONN_CAP);
-    if (h->cfg.manager != PSIM_MANAGER_PLUGGABLE) rc |= s->outx.alloc(std::max<size_t>(1024, n / 32) * OUT_EXT);
+    // outstanding extension rows for 1/8 of the nodes: a lazy peer that is no
+    // member (update_peers adds a PRUNE's or IHAVE's sender after its
+    // neighbors_down) collects one entry per broadcast that no ack clears
+    // (pt:443-453, :562-579), so tables grow for as long as broadcasts run --
+    // under config E with the partition after the churn ~10 % of the nodes
+    // pass 16 entries by phase round 230 (oracle, 2^16); at 1/32 the pool ran
+    // out at 2^26
+    if (h->cfg.manager != PSIM_MANAGER_PLUGGABLE) rc |= s->outx.alloc(std::max<size_t>(1024, n / 8) * OUT_EXT);
     rc |= s->outx_top.alloc(1);
     rc |= s->ocnt.alloc(n); rc |= s->cb.alloc(n + 1);
     rc |= s->in_beg.alloc(n + 1); rc |= s->bound.alloc(n + 1); rc |= s->pscan.alloc(n + 1); rc |= s->obase.alloc(n + 1);
@@ -2275,8 +2289,8 @@ int shard_alloc(psim_handle* h, Shard* s) {
     rc |= s->desc_slow.alloc(n); rc |= s->n_slow.alloc(1);
     rc |= s->desc_pt.alloc(n); rc |= s->n_pt.alloc(1);
     rc |= s->desc_shuf.alloc(n); rc |= s->n_shuf.alloc(1);
-    rc |= s->desc_lite.alloc(n); rc |= s->n_lite.alloc(1);
-    rc |= s->desc_ptl.alloc(n); rc |= s->n_ptl.alloc(1);
+    rc |= s->desc_lite.alloc(n); rc |= s->n_lite.alloc(2);
+    rc |= s->desc_ptl.alloc(n); rc |= s->n_ptl.alloc(2);
     if (h->cfg.manager == PSIM_MANAGER_PLUGGABLE) { rc |= s->stop_ids.alloc(n); rc |= s->n_stop.alloc(1); }
     rc |= s->stat_out.alloc(NST + 2);   // + the consume span
     rc |= s->ctl.alloc(2);
@@ -2433,7 +2447,13 @@ int psim_create(const psim_config* cfg, psim_handle** out) {
     h->lite_half = getenv("PSIM_LITE_WAVE") == nullptr;
     h->lite_blocks = h->lite_half ? grid("PSIM_LITE_GRID", psim::lite_half_grid(), 4 * psim::lite_half_grid())
                                   : grid("PSIM_LITE_GRID", psim::lite_grid(), 4 * psim::lite_grid());
-    h->ptl_blocks = grid("PSIM_PTL_GRID", psim::ptl_grid(), psim::ptl_grid());
+    // k_ptl (a lane per node); PSIM_PTL_QUARTER=1: k_ptq (four nodes per wave,
+    // parity-exact, slower: 0.602 against 0.584 ms a phase at 2^20 and 79.3
+    // against 68.1 ms at 2^26, profiles/r04/pq2 -- a row per node runs each
+    // handler for 4 nodes where a lane per node runs it for 64)
+    h->ptl_quarter = getenv("PSIM_PTL_QUARTER") != nullptr;
+    h->ptl_blocks = h->ptl_quarter ? grid("PSIM_PTL_GRID", psim::ptq_grid(), 2 * psim::ptq_grid())
+                                   : grid("PSIM_PTL_GRID", psim::ptl_grid(), psim::ptl_grid());
     {
         const char* e = getenv("PSIM_PHASE_TIMERS");
         h->phase_timers = e && *e && *e != '0';
@@ -3149,9 +3169,10 @@ int psim_kernel_times(psim_handle* h, const char** names, double* ms, uint64_t* 
     return k;
 }
 
-// diagnostic: per-phase s_memtime sums of k_consume (zeros unless built with -DPSIM_STAMPS)
+// diagnostic: per-phase s_memtime sums of k_consume / k_pt, k_consume_lite and
+// k_lite_half (96 entries; 0 returned unless built with -DPSIM_STAMPS)
 int psim_debug_stamps(unsigned long long* out, int cap) {
-    if (!out || cap < 64) return PSIM_EINVAL;
+    if (!out || cap < 96) return PSIM_EINVAL;
     return psim::debug_stamps(out);
 }
 

@@ -57,11 +57,12 @@ struct RoundArgs {
     uint4* desc_shuf;           // ... and the nodes whose HyParView phase ends in a shuffle start, for k_shuf
     uint32_t* n_shuf;
     uint64_t* stat_shuf;        // k_shuf's per-block stats rows
-    uint4* desc_lite;           // ... and the nodes with SHUFFLE terminals / replies, for k_consume_lite
-    uint32_t* n_lite;
+    uint4* desc_lite;           // ... and the nodes with SHUFFLE terminals / replies, for k_lite_half:
+    uint32_t* n_lite;           // [0] from the front, those with a terminal, [1] from the back (lite_at)
     uint64_t* stat_lite;        // k_consume_lite's per-block stats rows
-    uint4* desc_ptl;            // ... and the nodes with Plumtree work and no origin, for k_ptl
-    uint32_t* n_ptl;
+    uint4* desc_ptl;            // ... and the nodes with Plumtree work and no origin, for k_ptl:
+    uint32_t* n_ptl;            // [0] from the front, those with a BROADCAST in their inbox, [1] from
+                                // the back (desc_ptl[n_local - 1 - i]), the others (ptl_desc)
     uint64_t* stat_ptl;         // k_ptl's per-block stats rows
     uint64_t* stat_relay;
     uint64_t* stat_pt;          // k_pt's per-block stats rows
@@ -114,7 +115,7 @@ constexpr uint32_t SHUF_MAX_BLOCKS = 1024;     // k_shuf: grid-stride over its l
 #ifndef PSIM_PTL_BLOCK
 #define PSIM_PTL_BLOCK 64
 #endif
-// k_ptl's block (psim_consume.hip PTL_BLK): one wave, so that its 256 B of
+// k_ptl's block (psim_consume.hip PTL_BLK): one wave, so that its 224 B of
 // LDS per lane leave no block-sized hole (9 resident blocks per CU against 4
 // of 128 lanes, measured 2 % faster); the grid strides over its list with
 // the resident blocks (ptl_grid())
@@ -131,10 +132,16 @@ uint32_t lite_half_grid();
 uint32_t lite_half_block();
 // lane-per-node Plumtree phases (psim_consume.hip); hands k_pt what does not fit
 __global__ void k_ptl(RoundArgs args);
+// the same with four nodes per wave, one per 16-lane row (psim_ptq.hip)
+__global__ void k_ptq(RoundArgs args);
+uint32_t ptq_grid();
+uint32_t ptq_block();
+uint32_t ptq_nodes();
 // the Plumtree phase of the nodes k_relay listed (psim_consume.hip)
 __global__ void k_pt(RoundArgs args);
 // diagnostic builds (-DPSIM_STAMPS): per-phase cycle sums of k_consume, reset on read
 int debug_stamps(unsigned long long* out);
+int debug_stamps_half(unsigned long long* out);   // k_lite_half's 32 (psim_lite.hip)
 // resident-block count of k_consume on the current device
 uint32_t consume_grid();
 uint32_t lite_grid();
@@ -162,6 +169,23 @@ __device__ __forceinline__ bool crashed_now(Args& a, uint32_t id) {
 }
 
 typedef const __attribute__((address_space(4))) RoundArgs KArgs;
+
+// entry i of k_ptl's list: the BROADCAST nodes k_relay put at the front, then
+// the others it put at the back -- so a wave's lanes mostly run the same
+// handlers (a first delivery's eager push and lazy adds, or the light IHAVE
+// answers, acks and lazy ticks), not the union of both
+template <class Args>
+__device__ __forceinline__ uint4 ptl_desc(Args& a, uint32_t n0, uint32_t i) {
+    return a.desc_ptl[i < n0 ? i : a.n_local - 1 - (i - n0)];
+}
+// entry i of the lite list: the nodes with a SHUFFLE terminal (a sublist of
+// the passive view, a reply and a merge) at the front, the others (replies'
+// merges, relays, shuffle starts) at the back -- k_lite_half pairs adjacent
+// entries in a wave's two halves, so most pairs share the terminal's sublist
+template <class Args>
+__device__ __forceinline__ uint32_t lite_at(Args& a, uint32_t n0, uint32_t i) {
+    return i < n0 ? i : a.n_local - 1 - (i - n0);
+}
 __device__ __forceinline__ KArgs& kargs() {
     KArgs* p = (KArgs*)__builtin_amdgcn_kernarg_segment_ptr();
     asm volatile("" : "+s"(p));

@@ -43,6 +43,23 @@ constexpr uint32_t HSTAGE = 16;                 // staged records per half
 #endif
 constexpr uint32_t HWPB = PSIM_HALF_WPB;        // waves per block
 
+// Diagnostic build only (-DPSIM_STAMPS, `make stamps`): s_memtime between
+// phase boundaries, per half (slot half * 16 + phase), summed over all waves
+// into g_stamps_half (debug_stamps_half; profiles/stamps.py).  A phase both
+// halves run is charged to each; one only the other half runs goes to this
+// half's next stamp.
+#ifdef PSIM_STAMPS
+__device__ unsigned long long g_stamps_half[32];
+#define HSTAMP(w, k)                                                                 \
+    do {                                                                             \
+        const uint64_t t_ = __builtin_amdgcn_s_memtime();                            \
+        if (hl_id() == 0) (w).stl[(hb_id() >> 1) + (k)] += t_ - (w).t_last;          \
+        (w).t_last = t_;                                                             \
+    } while (0)
+#else
+#define HSTAMP(w, k) do { } while (0)
+#endif
+
 DEV uint32_t hl_id() { return __lane_id() & 31u; }
 DEV uint32_t hb_id() { return __lane_id() & 32u; }
 
@@ -104,10 +121,12 @@ DEV uint32_t hdel(uint32_t V, uint32_t n, uint32_t k) {
 struct Hn {
     uint32_t me, ob, ib, ik;
     uint32_t fl;                     // the due timers (DESC_* bits, k_desc) | HF_PDIRTY | partition << 8
+                                     // | header word 9's bytes 2-3 << 16 (kept for the writeback)
     uint32_t act_n, pas_n;
     uint64_t rng;                    // the Philox draw counter
     uint32_t A, P;                   // lane hl: active[hl] (hl < 8), passive[hl]
-    uint32_t AF;                     // flags | partition << 8 of A (the connection cache)
+    uint32_t AF;                     // flags | partition << 8 of A (the connection cache); lane 31:
+                                     // the outbox's slots, obase[row + 1] - ob (out_cap)
     uint32_t seq, flushed;
     uint64_t dcb;                    // draw cache: lane hl holds the draw of counter dcb + hl
     uint32_t DCL, DCH;
@@ -116,13 +135,17 @@ constexpr uint32_t HF_PDIRTY = 16;  // Hn::fl: the passive view changed
 DEV uint32_t local_row(const Hn& x) { return x.me - kargs().lo; }
 // the node's outbox slots: no store goes past them (a record past the bound
 // is not stored -- the engine fails the round on the bound check)
-DEV uint32_t out_cap(const Hn& x) { return (uint32_t)(kargs().obase[local_row(x) + 1] - x.ob); }
+DEV uint32_t out_cap(const Hn& x) {
+    const uint32_t a = __builtin_amdgcn_readlane(x.AF, 31), b = __builtin_amdgcn_readlane(x.AF, 63);
+    return hb_id() ? b : a;
+}
 
 // a node's counters (each half counts its own node's; lane 0 of the half
 // adds them to the block's stats at the node's end), and the wave's digest
-struct Hc {
+struct Hc {                           // (summed over the half's nodes: < 2^16 each)
     uint32_t dl;                     // SHUFFLE | SHUFFLE_REPLY << 16 delivered
     uint32_t em;                     // SHUFFLE | SHUFFLE_REPLY << 16 emitted
+    uint32_t pb;                     // nodes | bound violations << 16
     uint32_t fail;
     uint64_t digest;                 // lane j < 16 of a half sums word j of its records
 };
@@ -134,6 +157,10 @@ struct Hw {                          // the wave's LDS
     uint32_t* scr;                   // 2 halves x 32 words of scratch
     uint32_t KM;                     // lane hl: kMagic[hl] (exact modulo, n < 32)
     uint32_t DM;                     // lane hl < 16: the digest multiplier of record word hl
+#ifdef PSIM_STAMPS
+    unsigned long long* stl;         // 2 halves x 16 phase sums (LDS)
+    uint64_t t_last;
+#endif
 };
 
 // ------------------------------------------------------------------ RNG --
@@ -292,7 +319,7 @@ DEV bool connect_ok(const Hn& x, uint32_t dst) {
     const uint32_t m = hmask(hl_id() < x.act_n && x.A == dst);
     const uint32_t c = hget(x.AF, (uint32_t)__ffs(m) - 1);
     const uint32_t v = m ? c : ((uint32_t)a.flags[dst] | ((uint32_t)a.part[dst] << 8));
-    return (v & F_UP) && (v >> 8) == (x.fl >> 8);
+    return (v & F_UP) && (v >> 8) == ((x.fl >> 8) & 0xFFu);
 }
 
 // do_send_message/3 (hv:1274-1343) after maybe_connect: the dispatch draw of
@@ -405,10 +432,10 @@ struct HIn {
     uint32_t EX4;                    // lane hl: exchange id hl & 7 of inbox record hl >> 3
 };
 
-DEV HIn load_in(KArgs& a, uint32_t i, bool live) {
+DEV HIn load_in(KArgs& a, uint32_t n0, uint32_t i, bool live) {
     const uint32_t l = hl_id();
     HIn in;
-    in.D = live ? a.desc_lite[i] : make_uint4(0, 0, 0, 0);
+    in.D = live ? a.desc_lite[lite_at(a, n0, i)] : make_uint4(0, 0, 0, 0);
     const size_t li = live ? in.D.x - a.lo : 0;
     const uint32_t* hrow = reinterpret_cast<const uint32_t*>(a.hdr + li);
     in.r0 = hrow[0]; in.r1 = hrow[1]; in.w9 = hrow[9];
@@ -427,11 +454,10 @@ DEV HIn load_in(KArgs& a, uint32_t i, bool live) {
 }
 
 DEV void begin(Hn& x, const HIn& in) {
-    KArgs& a = kargs();
     const uint32_t l = hl_id();
     x.me = in.D.x; x.ib = in.D.y;
     x.ik = in.D.z & DESC_CNT_MASK; x.ob = in.D.w;
-    x.fl = (in.D.z >> 28) | (in.part << 8);
+    x.fl = (in.D.z >> 28) | (in.part << 8) | (in.w9 & 0xFFFF0000u);
     x.rng = ((uint64_t)in.r1 << 32) | in.r0;
     x.act_n = in.w9 & 0xFF; x.pas_n = (in.w9 >> 8) & 0xFF;
     x.A = l < x.act_n ? in.A : 0u;
@@ -469,16 +495,21 @@ DEV void body(Hn& x, Hw& w, Hc& c, const HIn& in) {
         const bool reply = type == PSIM_MSG_SHUFFLE_REPLY;          // hv:1091-1093
         const bool relay = !reply && ttl > 0 && x.act_n > 1;         // hv:1095-1136
         c.dl += reply ? 0x10000u : 1u;
+        HSTAMP(w, 6);
         if (relay) {
             const uint32_t r = select_random(x, w, x.A, x.act_n, p, x.me);
             if (r != PSIM_NONE) hv_send(x, w, c, r, PSIM_MSG_SHUFFLE, ttl - 1, ex, nex);
+            HSTAMP(w, 1);
         } else {
             if (!reply) {                             // the walk ends here: reply to Sender
                 uint32_t RESP = 0;
                 const uint32_t nr = sublist<PSIM_PASSIVE_CAP - 2>(x, w, x.P, x.pas_n, nex, RESP, 0);
+                HSTAMP(w, 2);
                 hv_send(x, w, c, p, PSIM_MSG_SHUFFLE_REPLY, 0, RESP, nr);
+                HSTAMP(w, 3);
             }
             merge_exchange(x, w, ex, nex);
+            HSTAMP(w, 4);
         }
       }
     }
@@ -490,7 +521,22 @@ DEV void body(Hn& x, Hw& w, Hc& c, const HIn& in) {
         const uint32_t nex = husort(w, EX, l < m);
         const uint32_t t = select_random(x, w, x.A, x.act_n, x.me, x.me);
         if (t != PSIM_NONE) hv_send(x, w, c, t, PSIM_MSG_SHUFFLE, a.arwl, EX, nex);
+        HSTAMP(w, 5);
     }
+}
+
+// a half's counters into the block's stats (once, at the kernel's end: the
+// per-node LDS atomics cost a writeback's worth of issue slots)
+DEV void count(Hw& w, const Hc& c) {
+    if (hl_id() != 0) return;
+    unsigned long long* st = w.sst;
+    if (c.pb & 0xFFFFu) atomicAdd(&st[ST_PROC], (unsigned long long)(c.pb & 0xFFFFu));
+    if (c.pb >> 16) atomicAdd(&st[ST_BOUND], (unsigned long long)(c.pb >> 16));
+    if (c.dl & 0xFFFFu) atomicAdd(&st[ST_DELIV + PSIM_MSG_SHUFFLE], (unsigned long long)(c.dl & 0xFFFFu));
+    if (c.dl >> 16) atomicAdd(&st[ST_DELIV + PSIM_MSG_SHUFFLE_REPLY], (unsigned long long)(c.dl >> 16));
+    if (c.em & 0xFFFFu) atomicAdd(&st[ST_EMIT + PSIM_MSG_SHUFFLE], (unsigned long long)(c.em & 0xFFFFu));
+    if (c.em >> 16) atomicAdd(&st[ST_EMIT + PSIM_MSG_SHUFFLE_REPLY], (unsigned long long)(c.em >> 16));
+    if (c.fail) atomicAdd(&st[ST_FAIL], (unsigned long long)c.fail);
 }
 
 // the draw counter and passive size in the header, the passive row when it
@@ -501,23 +547,18 @@ DEV void writeback(Hn& x, Hw& w, Hc& c) {
     const uint32_t l = hl_id();
     const uint32_t li = local_row(x);
     uint32_t* hrow = reinterpret_cast<uint32_t*>(a.hdr + li);
-    const uint32_t w9 = (hrow[9] & ~0xFF00u) | (x.pas_n << 8);
+    const uint32_t w9 = (x.fl & 0xFFFF0000u) | (x.pas_n << 8) | x.act_n;
     if (l < 3) hrow[l == 2 ? 9 : l] = l == 0 ? (uint32_t)x.rng : l == 1 ? (uint32_t)(x.rng >> 32) : w9;
     if (x.fl & HF_PDIRTY) a.pas[(size_t)li * PSIM_PASSIVE_CAP + l] = x.P;
     flush(x, w);
-    if (l == 0) {
-        a.ocnt[li] = x.seq;
-        unsigned long long* st = w.sst;
-        atomicAdd(&st[ST_PROC], 1ull);
-        if (c.dl & 0xFFFFu) atomicAdd(&st[ST_DELIV + PSIM_MSG_SHUFFLE], (unsigned long long)(c.dl & 0xFFFFu));
-        if (c.dl >> 16) atomicAdd(&st[ST_DELIV + PSIM_MSG_SHUFFLE_REPLY], (unsigned long long)(c.dl >> 16));
-        if (c.em & 0xFFFFu) atomicAdd(&st[ST_EMIT + PSIM_MSG_SHUFFLE], (unsigned long long)(c.em & 0xFFFFu));
-        if (c.em >> 16) atomicAdd(&st[ST_EMIT + PSIM_MSG_SHUFFLE_REPLY], (unsigned long long)(c.em >> 16));
-        if (c.fail) atomicAdd(&st[ST_FAIL], (unsigned long long)c.fail);
-        if (x.seq > out_cap(x)) atomicAdd(&st[ST_BOUND], 1ull);
+    if (l == 0) a.ocnt[li] = x.seq;
+    c.pb += 1u + (x.seq > out_cap(x) ? 0x10000u : 0u);
+    if ((c.dl | c.em | c.pb) & 0x80008000u) {        // (a 16-bit half past 2^15: flush early)
+        count(w, c);
+        c.dl = 0; c.em = 0; c.pb = 0; c.fail = 0;
     }
-    c.dl = 0; c.em = 0; c.fail = 0;
 }
+
 
 }  // namespace
 
@@ -527,6 +568,10 @@ __global__ void __launch_bounds__(64 * PSIM_HALF_WPB, PSIM_HALF_WAVES) k_lite_ha
     __shared__ __attribute__((aligned(16))) uint32_t srecs[HWPB][2 * HSTAGE * 16];
     __shared__ uint32_t skeys[HWPB][2 * HSTAGE];
     __shared__ uint32_t scrs[HWPB][64];
+#ifdef PSIM_STAMPS
+    __shared__ unsigned long long stls[HWPB][32];
+    for (int i = threadIdx.x; i < (int)(HWPB * 32); i += blockDim.x) (&stls[0][0])[i] = 0;
+#endif
     for (int i = threadIdx.x; i < NST; i += blockDim.x) sst[i] = 0;
     __syncthreads();
     const uint32_t wid = threadIdx.x >> 6, l = hl_id();
@@ -534,29 +579,40 @@ __global__ void __launch_bounds__(64 * PSIM_HALF_WPB, PSIM_HALF_WAVES) k_lite_ha
     w.sst = sst; w.srec = srecs[wid]; w.skey = skeys[wid]; w.scr = scrs[wid];
     w.KM = kMagic[l == 0 ? 64 : l];
     w.DM = (uint32_t)digest_mul(l & 15);
+#ifdef PSIM_STAMPS
+    w.stl = stls[wid];
+    w.t_last = __builtin_amdgcn_s_memtime();
+#endif
     Hc c = {};
     // half h of global wave gw takes list entries 2 gw + h, + 2 nw, ...
     const uint32_t nw = gridDim.x * HWPB;
     const uint32_t first = 2 * (blockIdx.x * HWPB + wid) + (hb_id() >> 5);
-    const uint32_t na = *kargs().n_lite;
+    const uint32_t n0 = kargs().n_lite[0], na = n0 + kargs().n_lite[1];
     if (first < na) {
         Hn x;
-        HIn in = load_in(kargs(), first, true);
+        HIn in = load_in(kargs(), n0, first, true);
         for (uint32_t i = first; i < na; i += 2 * nw) {
+            HSTAMP(w, 8);
             begin(x, in);
             // the connection cache: flag and partition bytes of the active members
             {
                 KArgs& a = kargs();
                 const uint32_t ca = l < x.act_n && x.A < a.n_nodes ? x.A : x.me;
-                x.AF = (uint32_t)a.flags[ca] | ((uint32_t)a.part[ca] << 8);
+                // (the outbox bound's load issued with the two bytes: one wait)
+                const uint32_t cap = (uint32_t)(a.obase[x.me - a.lo + 1] - x.ob);
+                const uint32_t af = (uint32_t)a.flags[ca] | ((uint32_t)a.part[ca] << 8);
+                x.AF = l == 31 ? cap : af;
             }
             // the next node's inputs, in flight while this one runs
             const uint32_t nx = i + 2 * nw;
-            const HIn inn = load_in(kargs(), nx < na ? nx : i, nx < na);
+            const HIn inn = load_in(kargs(), n0, nx < na ? nx : i, nx < na);
+            HSTAMP(w, 0);
             body(x, w, c, in);
             writeback(x, w, c);
+            HSTAMP(w, 7);
             in = inn;
         }
+        count(w, c);
     }
     // the digest partials of every lane
     {
@@ -568,6 +624,13 @@ __global__ void __launch_bounds__(64 * PSIM_HALF_WPB, PSIM_HALF_WAVES) k_lite_ha
     __syncthreads();
     for (int i = threadIdx.x; i < NST; i += blockDim.x)
         kargs().stat_lite[(size_t)blockIdx.x * NST + i] = sst[i];
+#ifdef PSIM_STAMPS
+    if (threadIdx.x < 32) {
+        unsigned long long t = 0;
+        for (uint32_t k = 0; k < HWPB; k++) t += stls[k][threadIdx.x];
+        if (t) atomicAdd(&g_stamps_half[threadIdx.x], t);
+    }
+#endif
 }
 
 static uint32_t half_resident_grid() {
@@ -582,4 +645,17 @@ static uint32_t half_resident_grid() {
 uint32_t lite_half_grid() { return half_resident_grid(); }
 uint32_t lite_half_block() { return 64 * HWPB; }
 
+}  // namespace psim
+
+namespace psim {
+#ifdef PSIM_STAMPS
+int debug_stamps_half(unsigned long long* out) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps_half), sizeof(unsigned long long) * 32) != hipSuccess) return -1;
+    unsigned long long z[32] = {0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_stamps_half), z, sizeof z) != hipSuccess) return -1;
+    return 32;
+}
+#else
+int debug_stamps_half(unsigned long long*) { return 0; }
+#endif
 }  // namespace psim

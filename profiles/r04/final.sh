@@ -32,3 +32,4 @@ gzip -c $T > $O/kernel_trace.csv.gz && rm -rf $O/prof
 bash profiles/sq_kernels.sh $TAG/sq --steps 20 --warmup 5 > /dev/null || exit 1
 tail -8 $O/sq/sq_kernels.txt
 bash profiles/run_pmc.sh $TAG --steps 20 --warmup 5 --no-check | tail -1
+PSIM_LIB=stamps timeout -k 10 300 python3 profiles/stamps.py --steps 20 > $O/stamps.txt 2>&1 && tail -12 $O/stamps.txt

@@ -28,6 +28,9 @@ for i, n in enumerate(HV):
     NAMES[4 + i] = "hv:" + n
 for i, n in enumerate(PT):
     NAMES[16 + i] = "pt:" + n
+HALF = {8: "loop / wait for the node's loads", 0: "begin + connection cache", 6: "inbox record parse",
+        1: "SHUFFLE relay", 2: "terminal: sublist", 3: "terminal: reply send", 4: "merge_exchange",
+        5: "shuffle start", 7: "writeback + flush"}
 LITE = {0: "wait for the node's loads", 1: "begin_node", 2: "inbox chunk / record parse", 3: "SHUFFLE_REPLY merge",
         4: "SHUFFLE relay", 5: "terminal: sublist", 6: "terminal: reply send", 7: "terminal: merge",
         8: "shuffle start", 9: "next node's 2nd-stage loads", 10: "writeback", 11: "next node's loads"}
@@ -57,7 +60,7 @@ def main():
     lib = _lib.load()
     lib.psim_debug_stamps.restype = C.c_int
     lib.psim_debug_stamps.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
-    buf = (C.c_ulonglong * 64)()
+    buf = (C.c_ulonglong * 96)()
     sim = Simulator(default_config(n_nodes=a.nodes, seed=1))
     sched = W.BenchSchedule("C", a.schedule, a.nodes, 1, a.warmup)
     boot, until = sched.bootstrap()
@@ -65,14 +68,14 @@ def main():
     for i in range(sched.t_start):
         sched.apply(sim, i)
         sim.step(1)
-    if lib.psim_debug_stamps(buf, 64) != 64:
+    if lib.psim_debug_stamps(buf, 96) != 96:
         print("library built without -DPSIM_STAMPS (make -C partisan_amd/csrc stamps; PSIM_LIB=stamps)")
         return
     st = []
     for i in range(sched.t_start, sched.t_start + a.steps):
         sched.apply(sim, i)
         st.append(sim.step(1))
-    lib.psim_debug_stamps(buf, 64)
+    lib.psim_debug_stamps(buf, 96)
     st = np.concatenate(st)
     v = np.array(buf[:], np.float64)
     print(f"{a.schedule} schedule, {a.nodes} nodes, rounds {a.steps}: processed {int(st['nodes_processed'].sum())} "
@@ -81,8 +84,12 @@ def main():
     print("delivered/round: " + ", ".join(f"{n}={int(dl[i])}" for i, n in enumerate(HV + PT) if dl[i]))
     print("k_consume / k_pt:")
     table(v[:32], NAMES, a.steps)
-    print("k_consume_lite:")
-    table(v[32:], LITE, a.steps)
+    if v[32:64].any():
+        print("k_consume_lite:")
+        table(v[32:64], LITE, a.steps)
+    if v[64:].any():
+        print("k_lite_half (each half's phases; both halves summed):")
+        table(v[64:80] + v[80:96], HALF, a.steps)
 
 
 if __name__ == "__main__":
