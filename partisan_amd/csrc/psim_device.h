@@ -170,8 +170,20 @@ __host__ __device__ __forceinline__ uint32_t bucket16_default(uint32_t id) {
     h ^= h >> 16; h *= 0x85EBCA6Bu; h ^= h >> 13; h *= 0xC2B2AE35u; h ^= h >> 16;
     return h & 15u;
 }
-__host__ __device__ __forceinline__ uint32_t bucket16(const uint8_t* tab, uint32_t id) {
-    return tab ? (uint32_t)tab[id] : bucket16_default(id);
+// (the table's byte load waited for on its own branch: merged with the
+// default branch, the load left its register "pending" at the join and the
+// compiler's path-insensitive wait there became an s_waitcnt vmcnt(0) on the
+// default branch too -- draining every load and store in flight, a node's
+// prefetched rows among them, twice per k_lite_half merge)
+__device__ __forceinline__ uint32_t bucket16(const uint8_t* tab, uint32_t id) {
+    uint32_t b;
+    if (tab) {
+        b = tab[id];
+        __builtin_amdgcn_s_waitcnt(0x0F70);      // vmcnt(0), expcnt / lgkmcnt untouched
+    } else {
+        b = bucket16_default(id);
+    }
+    return b;
 }
 
 // digest multiplier of record word j (oracle msg_hash): odd, position-distinct

@@ -156,7 +156,6 @@ struct Hw {                          // the wave's LDS
     uint32_t* skey;                  // 2 halves x HSTAGE route keys
     uint32_t* scr;                   // 2 halves x 32 words of scratch
     uint32_t KM;                     // lane hl: kMagic[hl] (exact modulo, n < 32)
-    uint32_t DM;                     // lane hl < 16: the digest multiplier of record word hl
 #ifdef PSIM_STAMPS
     unsigned long long* stl;         // 2 halves x 16 phase sums (LDS)
     uint64_t t_last;
@@ -301,7 +300,7 @@ DEV void emit(Hn& x, Hw& w, Hc& c, uint32_t dst, uint32_t type, uint32_t ttl, ui
                         : l < 8 ? 0u : (l - 8 < nex ? exv : 0u);
     if (l < 16) {
         w.srec[(h * HSTAGE + k) * 16 + l] = word;
-        c.digest += (uint64_t)word * w.DM;
+        c.digest += (uint64_t)word * digest_mul(l);      // (l < 16: record word l's multiplier)
     }
     if (l == 0) w.skey[h * HSTAGE + k] = dst | (max_emit(type) << KEY_DST_BITS);
     x.seq++;
@@ -432,10 +431,16 @@ struct HIn {
     uint32_t EX4;                    // lane hl: exchange id hl & 7 of inbox record hl >> 3
 };
 
-DEV HIn load_in(KArgs& a, uint32_t n0, uint32_t i, bool live) {
+// (the descriptor comes from a load issued before the previous node's
+// writeback: issued after those stores, its wait drained them -- the memory
+// counter is in order -- at every node)
+DEV uint4 load_desc(KArgs& a, uint32_t n0, uint32_t i, bool live) {
+    return live ? a.desc_lite[lite_at(a, n0, i)] : make_uint4(0, 0, 0, 0);
+}
+DEV HIn load_in(KArgs& a, const uint4& D, bool live) {
     const uint32_t l = hl_id();
     HIn in;
-    in.D = live ? a.desc_lite[lite_at(a, n0, i)] : make_uint4(0, 0, 0, 0);
+    in.D = D;
     const size_t li = live ? in.D.x - a.lo : 0;
     const uint32_t* hrow = reinterpret_cast<const uint32_t*>(a.hdr + li);
     in.r0 = hrow[0]; in.r1 = hrow[1]; in.w9 = hrow[9];
@@ -578,7 +583,6 @@ __global__ void __launch_bounds__(64 * PSIM_HALF_WPB, PSIM_HALF_WAVES) k_lite_ha
     Hw w;
     w.sst = sst; w.srec = srecs[wid]; w.skey = skeys[wid]; w.scr = scrs[wid];
     w.KM = kMagic[l == 0 ? 64 : l];
-    w.DM = (uint32_t)digest_mul(l & 15);
 #ifdef PSIM_STAMPS
     w.stl = stls[wid];
     w.t_last = __builtin_amdgcn_s_memtime();
@@ -590,7 +594,8 @@ __global__ void __launch_bounds__(64 * PSIM_HALF_WPB, PSIM_HALF_WAVES) k_lite_ha
     const uint32_t n0 = kargs().n_lite[0], na = n0 + kargs().n_lite[1];
     if (first < na) {
         Hn x;
-        HIn in = load_in(kargs(), n0, first, true);
+        HIn in = load_in(kargs(), load_desc(kargs(), n0, first, true), true);
+        uint4 Dn = load_desc(kargs(), n0, first + 2 * nw < na ? first + 2 * nw : first, first + 2 * nw < na);
         for (uint32_t i = first; i < na; i += 2 * nw) {
             HSTAMP(w, 8);
             begin(x, in);
@@ -604,10 +609,11 @@ __global__ void __launch_bounds__(64 * PSIM_HALF_WPB, PSIM_HALF_WAVES) k_lite_ha
                 x.AF = l == 31 ? cap : af;
             }
             // the next node's inputs, in flight while this one runs
-            const uint32_t nx = i + 2 * nw;
-            const HIn inn = load_in(kargs(), n0, nx < na ? nx : i, nx < na);
+            const uint32_t nx = i + 2 * nw, nnx = i + 4 * nw;
+            const HIn inn = load_in(kargs(), Dn, nx < na);
             HSTAMP(w, 0);
             body(x, w, c, in);
+            Dn = load_desc(kargs(), n0, nnx < na ? nnx : i, nnx < na);
             writeback(x, w, c);
             HSTAMP(w, 7);
             in = inn;
