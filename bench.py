@@ -472,7 +472,8 @@ def main_strategy(args):
         state = int(st["nodes_processed"].sum()) * 2 * (64 + 4 * 64 * 2)
     alg = state + int(st["delivered"].sum()) * S_MSG + msgs * (S_MSG + 4)
     achieved = alg / (c_ms / 1e3) / 1e9 if c_ms > 0 else 0.0
-    traffic, trec = pmc_traffic(pmc_key(args, 1, n))
+    key = pmc_key(args, 1, n)
+    traffic, trec = pmc_traffic(key)
     tsrc = trec.get("source") if trec else None
     out = {
         "metric": "simulated node-rounds/sec (+ msgs/sec), pluggable manager " + args.workload,
@@ -483,11 +484,13 @@ def main_strategy(args):
         "config": {"workload": name, "nodes": n, "seed": args.seed, "parallelism": "1 GPU"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": tsrc,
+                     "traffic_upper": trec.get("traffic_upper_per_launch") if trec else None,
                      "kernel": "k_consume_pl",
                      "alg_bytes_per_launch": alg / max(1, c_n), "avg_launch_ms": c_ms / max(1, c_n)},
         "kernel_ms_per_step": {k: v[0] / args.steps for k, v in kt.items() if v[1]},
         "overflow": int(st["overflow"].sum()),
         "members_min": int(sim.strategy_nodes(0, min(n, 4096))["members"].min()) if args.workload == "B" else None,
+        "pmc_key": key,
     }
     print(json.dumps(out), flush=True)
 

@@ -26,27 +26,34 @@ KERNELS = ("k_relay(", "k_shuf(", "k_consume_lite(", "k_lite_half(", "k_term(", 
            "k_pt(", "k_consume_pl(")
 
 
-def per_round(path, steps, tail):
+def per_round(path, steps, tail, by=None):
+    """bytes per timed round over the node-round kernels; `by` collects them
+    per kernel"""
     rows = list(csv.DictReader(open(path)))
     tot = 0.0
     for k in KERNELS:
         kr = [r for r in rows if k in r["Kernel_Name"]]
         ids = sorted({int(r["Dispatch_Id"]) for r in kr})
         keep = set(ids[len(ids) - tail - steps:len(ids) - tail])
-        tot += sum(float(r["Counter_Value"]) for r in kr if int(r["Dispatch_Id"]) in keep)
-    return tot * 1024 / steps          # KiB -> bytes, per round
+        b = sum(float(r["Counter_Value"]) for r in kr if int(r["Dispatch_Id"]) in keep) * 1024 / steps
+        tot += b
+        if by is not None and b:
+            by[k.rstrip("(")] = by.get(k.rstrip("("), 0.0) + b
+    return tot                         # (KiB counts -> bytes, per round)
 
 
 def main():
     bench = json.load(open(sys.argv[1]))
     steps, tail = bench["steps"], bench.get("overlay", {}).get("rounds_drained", 0)
-    fetch = per_round(sys.argv[2], steps, tail)
-    write = per_round(sys.argv[3], steps, tail)
+    by = {}
+    fetch = per_round(sys.argv[2], steps, tail, by)
+    write = per_round(sys.argv[3], steps, tail, by)
     rec = {"key": bench["pmc_key"],
            "traffic_per_launch": fetch + write,
            "traffic_upper_per_launch": 2 * fetch + write,
            "fetch_size_bytes": fetch, "write_size_bytes": write,
            "alg_bytes_per_launch": bench["roofline"]["alg_bytes_per_launch"],
+           "per_kernel": by,              # FETCH_SIZE + WRITE_SIZE per round, by kernel
            "source": "FETCH_SIZE + WRITE_SIZE per timed round of the node-round kernels, separate "
                      "rocprofv3 --pmc passes of this command (profiles/run_pmc.sh); FETCH_SIZE uncorrected: "
                      "random 64-B requests count exactly (profiles/calib/)"}
