@@ -15,18 +15,18 @@ at report points through the run:
   stable_since        the first report point from which the outside set is the
                       same set of nodes as at the end
 
-The finding (DESIGN.md section 6): no outside node is isolated.  Each sits in
+The finding (DESIGN.md section 5): no outside node is isolated.  Each sits in
 a closed component of >= 2 nodes that formed during the join ramp, when
 eviction DISCONNECTs (add_to_active_view on a full view, hv:1371-1386,
-:1467-1510) cut its last links to the rest, and it holds >= 2 active
-peers -- at or above
-min_active_size (3 with the node itself), so random_promotion
-(hv:542-556, has_reached_the_limit) never fires, and shuffles walk only its
-own active links.  Their passive views hold giant members, but HyParView
-promotes from the passive view only below min_active_size or on a failure.
-Nothing in the protocol merges such a component again; the oracle (the
-reference's handlers) shows the same components, and the GPU equals it bit
-for bit (test_bench_schedule_parity at 2^20).
+:1467-1510) cut its last links to the rest.  With >= 2 active peers (all of
+them at 2^18 and 2^20) a node is at min_active_size (3 with the node
+itself), so random_promotion (hv:542-556, has_reached_the_limit) never
+fires; with 1 (a few at 2^24) its low-priority NEIGHBOR requests meet full
+views; shuffles walk only the component's own active links, and the passive
+view is promoted only on a failure.  Nothing in the protocol merges such a
+component again; the oracle (the reference's handlers) shows the same
+components, and the GPU equals it bit for bit (test_bench_schedule_parity
+at 2^20).
 
 Usage (GPU box):  python tests/c_overlay.py --backend gpu --nodes 262144 1048576
        (CPU here): python tests/c_overlay.py --backend oracle --nodes 16384 65536
