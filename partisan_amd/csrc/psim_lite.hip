@@ -437,16 +437,24 @@ struct HIn {
 DEV uint4 load_desc(KArgs& a, uint32_t n0, uint32_t i, bool live) {
     return live ? a.desc_lite[lite_at(a, n0, i)] : make_uint4(0, 0, 0, 0);
 }
-DEV HIn load_in(KArgs& a, const uint4& D, bool live) {
+// the node's rows: header words, active and passive rows, partition byte
+// (for the next node issued after this one's body, so that they are not
+// held in registers across it)
+DEV void load_rows(KArgs& a, HIn& in, bool live) {
     const uint32_t l = hl_id();
-    HIn in;
-    in.D = D;
     const size_t li = live ? in.D.x - a.lo : 0;
     const uint32_t* hrow = reinterpret_cast<const uint32_t*>(a.hdr + li);
     in.r0 = hrow[0]; in.r1 = hrow[1]; in.w9 = hrow[9];
     in.A = l < PSIM_ACTIVE_CAP ? a.act[li * PSIM_ACTIVE_CAP + l] : 0u;
     in.P = a.pas[li * PSIM_PASSIVE_CAP + l];
     in.part = a.part[live ? in.D.x : 0];
+}
+// the descriptor's inbox heads (issued a node ahead)
+DEV HIn load_in(KArgs& a, const uint4& D) {
+    const uint32_t l = hl_id();
+    HIn in;
+    in.D = D;
+    in.r0 = in.r1 = in.w9 = in.A = in.P = in.part = 0;
     // the first 32 records' senders and type words, the first four's
     // exchanges (one load instruction each, issued a node ahead)
     const uint32_t ik = in.D.z & DESC_CNT_MASK;
@@ -594,7 +602,8 @@ __global__ void __launch_bounds__(64 * PSIM_HALF_WPB, PSIM_HALF_WAVES) k_lite_ha
     const uint32_t n0 = kargs().n_lite[0], na = n0 + kargs().n_lite[1];
     if (first < na) {
         Hn x;
-        HIn in = load_in(kargs(), load_desc(kargs(), n0, first, true), true);
+        HIn in = load_in(kargs(), load_desc(kargs(), n0, first, true));
+        load_rows(kargs(), in, true);
         uint4 Dn = load_desc(kargs(), n0, first + 2 * nw < na ? first + 2 * nw : first, first + 2 * nw < na);
         for (uint32_t i = first; i < na; i += 2 * nw) {
             HSTAMP(w, 8);
@@ -610,10 +619,11 @@ __global__ void __launch_bounds__(64 * PSIM_HALF_WPB, PSIM_HALF_WAVES) k_lite_ha
             }
             // the next node's inputs, in flight while this one runs
             const uint32_t nx = i + 2 * nw, nnx = i + 4 * nw;
-            const HIn inn = load_in(kargs(), Dn, nx < na);
+            HIn inn = load_in(kargs(), Dn);
             HSTAMP(w, 0);
             body(x, w, c, in);
             Dn = load_desc(kargs(), n0, nnx < na ? nnx : i, nnx < na);
+            load_rows(kargs(), inn, nx < na);
             writeback(x, w, c);
             HSTAMP(w, 7);
             in = inn;
