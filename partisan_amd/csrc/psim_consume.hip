@@ -2263,7 +2263,7 @@ __global__ void __launch_bounds__(256, PSIM_RELAY_WAVES) k_relay(RoundArgs) {
                 for (uint32_t j = 0; j < k; j++) e &= e - 1;
                 const uint32_t r = A[__ffs(e) - 1];
                 // do_send_message: maybe_connect + find, then the dispatch draw
-                if (r < a.n_nodes && (a.flags[r] & F_UP) && a.part[r] == me_part) {
+                if (r < a.n_nodes && a.upart[r] == me_part) {
                     rng++;
                     const uint4* ex = reinterpret_cast<const uint4*>(rp->ex);
                     const uint4 e0 = ex[0], e1 = ex[1];
@@ -2434,7 +2434,7 @@ __global__ void __launch_bounds__(256) k_shuf(RoundArgs) {
             for (uint32_t j = 0; j < k; j++) e &= e - 1;
             const uint32_t t = A[__ffs(e) - 1];
             // do_send_message: maybe_connect + find, then the dispatch draw
-            if (t < a.n_nodes && (a.flags[t] & F_UP) && a.part[t] == me_part) {
+            if (t < a.n_nodes && a.upart[t] == me_part) {
                 rng++;
                 v[S_DIGEST] += relay_emit(a, D.w + seq, t, id, PSIM_MSG_SHUFFLE | (a.arwl << 8) | (nex << 16), seq,
                                           0u, 0u, 0u, U);
@@ -2538,22 +2538,20 @@ struct PtLane {
 
 // send/3 (pt:633-638): over an existing connection -- the peer in the active
 // view, running, same partition
-// (the members' up and partition bytes are read once per node, all eight
+// (the members' up-and-partition pairs are read once per node, all eight
 // loads in flight together: read per send they were one dependent memory
 // latency per send; no kernel of the phase changes them)
 DEV uint32_t ptl_conn_mask(KArgs& a, const PtLane& n) {
-    uint8_t fl[PSIM_ACTIVE_CAP], pt[PSIM_ACTIVE_CAP];
+    uint16_t up[PSIM_ACTIVE_CAP];                     // (k_node_prep's up-and-partition pairs)
 #pragma unroll
     for (int j = 0; j < PSIM_ACTIVE_CAP; j++) {
         const uint32_t q = (uint32_t)j < n.act_n && n.A[j] < a.n_nodes ? n.A[j] : n.id;
-        fl[j] = a.flags[q];
-        pt[j] = a.part[q];
+        up[j] = a.upart[q];
     }
     uint32_t m = 0;
 #pragma unroll
     for (int j = 0; j < PSIM_ACTIVE_CAP; j++)
-        m |= ((uint32_t)j < n.act_n && n.A[j] < a.n_nodes && n.A[j] != n.id && (fl[j] & F_UP) &&
-              pt[j] == n.me_part) ? 1u << j : 0u;
+        m |= ((uint32_t)j < n.act_n && n.A[j] < a.n_nodes && n.A[j] != n.id && up[j] == n.me_part) ? 1u << j : 0u;
     return m;
 }
 DEV bool ptl_conn(KArgs& a, const PtLane& n, uint32_t ident) {

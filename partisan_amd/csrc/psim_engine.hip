@@ -623,6 +623,11 @@ __global__ void __launch_bounds__(256) k_node_prep(RoundArgs a, const unsigned l
         if (a.n_stop) *a.n_stop = 0;
     }
     __syncthreads();
+    // the peers' up-and-partition pairs for k_ptl's connection tests (every
+    // global id: the flag and partition arrays are replicated)
+    if (a.upart)
+        for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g < a.n_nodes; g += gridDim.x * blockDim.x)
+            a.upart[g] = (a.flags[g] & F_UP) ? (uint16_t)a.part[g] : UPART_DOWN;
     unsigned long long up = 0, drop = 0, bs = 0;        // this thread's sums (wave-summed below)
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < a.n_local; i += gridDim.x * blockDim.x) {
         uint32_t id = a.lo + i;
@@ -1148,6 +1153,7 @@ struct Shard {
     hipStream_t stream = nullptr;
     // replicated (global id)
     DBuf<uint8_t> flags, part;
+    DBuf<uint16_t> upart;               // k_node_prep's up-and-partition pairs (RoundArgs::upart)
     DBuf<uint32_t> crash_bits;   // RoundArgs::crash_bits
     DBuf<uint8_t> btab;          // RoundArgs::btab (psim_set_bucket_table), global id
     // local rows
@@ -1293,6 +1299,7 @@ RoundArgs make_args(psim_handle* h, Shard* s) {
     a.origin = s->origin.p;
     a.slots = s->slots.p;
     a.flags = s->flags.p; a.part = s->part.p; a.hdr = s->hdr.p; a.crash_bits = s->crash_bits.p;
+    a.upart = s->upart.p;
     a.btab = h->btab ? s->btab.p : nullptr;
     a.act = s->act.p; a.pas = s->pas.p; a.sentm = s->sentm.p; a.recvm = s->recvm.p;
     a.mapx = s->mapx.p; a.mapx_top = s->mapx_top.p;
@@ -2256,6 +2263,7 @@ int shard_alloc(psim_handle* h, Shard* s) {
     const size_t N = h->N, n = std::max<uint32_t>(s->n, 1);
     int rc = 0;
     rc |= s->flags.alloc(N); rc |= s->part.alloc(N); rc |= s->hdr.alloc(n);
+    if (h->cfg.manager != PSIM_MANAGER_PLUGGABLE) rc |= s->upart.alloc(N);
     rc |= s->crash_bits.alloc((N >> (CRASH_GRAIN_SHIFT + 5)) + 1);
     rc |= s->act.alloc(n * PSIM_ACTIVE_CAP); rc |= s->pas.alloc(n * PSIM_PASSIVE_CAP);
     rc |= s->sentm.alloc(n * IDMAP_IN); rc |= s->recvm.alloc(n * IDMAP_IN);
@@ -2316,7 +2324,7 @@ int shard_alloc(psim_handle* h, Shard* s) {
 
 void shard_free(Shard* s) {
     if (s->stream) (void)hipStreamSynchronize(s->stream);
-    s->flags.release(); s->part.release(); s->hdr.release(); s->crash_bits.release(); s->btab.release();
+    s->flags.release(); s->part.release(); s->upart.release(); s->hdr.release(); s->crash_bits.release(); s->btab.release();
     s->act.release(); s->pas.release(); s->sentm.release(); s->recvm.release();
     s->pt_all.release(); s->pt_com.release();
     s->mapx.release(); s->mapx_top.release();

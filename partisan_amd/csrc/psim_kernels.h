@@ -18,6 +18,13 @@ struct RoundArgs {
     // every other row is local (index = id - lo)
     uint8_t* flags;
     const uint8_t* part;
+    // per global id: its partition group while it is up, UPART_DOWN if not --
+    // built by k_node_prep after the round's events (F_UP and the groups
+    // change only there), so a connection test of a peer reads one byte pair
+    // instead of a flag byte and a partition byte on two random lines (k_ptl:
+    // eight members a node, 63 GB a round at 2^26 before; k_relay, k_shuf,
+    // k_lite_half likewise; HyParView / X-BOT handles only)
+    uint16_t* upart;
     // this round's crashed ids, one bit per CRASH_GRAIN ids (replicated,
     // zero outside crash rounds): a filter in L2 in front of the flag bytes
     const uint32_t* crash_bits;
@@ -159,6 +166,7 @@ uint32_t ptl_grid();
 // loads per node from HBM, 5 ms a crash round at 2^26 nodes; the 512 KB
 // filter answers ~97 % of them from L2 -- 134k crashes in 4M grains)
 constexpr uint32_t CRASH_GRAIN_SHIFT = 4;
+constexpr uint16_t UPART_DOWN = 0x100;
 __device__ __forceinline__ bool crash_filter(const uint32_t* bits, uint32_t id) {
     const uint32_t g = id >> CRASH_GRAIN_SHIFT;
     return (bits[g >> 5] >> (g & 31)) & 1u;

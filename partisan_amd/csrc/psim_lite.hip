@@ -125,7 +125,8 @@ struct Hn {
     uint32_t act_n, pas_n;
     uint64_t rng;                    // the Philox draw counter
     uint32_t A, P;                   // lane hl: active[hl] (hl < 8), passive[hl]
-    uint32_t AF;                     // flags | partition << 8 of A (the connection cache); lane 31:
+    uint32_t AF;                     // A's up-and-partition pairs (RoundArgs::upart: the connection
+                                     // cache, partition if up, UPART_DOWN if not); lane 31:
                                      // the outbox's slots, obase[row + 1] - ob (out_cap)
     uint32_t seq, flushed;
     uint64_t dcb;                    // draw cache: lane hl holds the draw of counter dcb + hl
@@ -311,14 +312,14 @@ DEV void emit(Hn& x, Hw& w, Hc& c, uint32_t dst, uint32_t type, uint32_t ttl, ui
 // maybe_connect + find (partisan_util.erl:75-134): the peer runs and no
 // partition separates the two.  Every lite send goes to an active member
 // (k_relay sends a walk that ends at a Sender outside the active view to
-// k_consume), read from the connection cache; others from the flag bytes.
+// k_consume), read from the connection cache; others from the pair array.
 DEV bool connect_ok(const Hn& x, uint32_t dst) {
     KArgs& a = kargs();
     if (dst >= a.n_nodes || dst == x.me) return false;
     const uint32_t m = hmask(hl_id() < x.act_n && x.A == dst);
     const uint32_t c = hget(x.AF, (uint32_t)__ffs(m) - 1);
-    const uint32_t v = m ? c : ((uint32_t)a.flags[dst] | ((uint32_t)a.part[dst] << 8));
-    return (v & F_UP) && (v >> 8) == ((x.fl >> 8) & 0xFFu);
+    const uint32_t v = m ? c : (uint32_t)a.upart[dst];
+    return v == ((x.fl >> 8) & 0xFFu);
 }
 
 // do_send_message/3 (hv:1274-1343) after maybe_connect: the dispatch draw of
@@ -608,13 +609,13 @@ __global__ void __launch_bounds__(64 * PSIM_HALF_WPB, PSIM_HALF_WAVES) k_lite_ha
         for (uint32_t i = first; i < na; i += 2 * nw) {
             HSTAMP(w, 8);
             begin(x, in);
-            // the connection cache: flag and partition bytes of the active members
+            // the connection cache: the active members' up-and-partition pairs
             {
                 KArgs& a = kargs();
                 const uint32_t ca = l < x.act_n && x.A < a.n_nodes ? x.A : x.me;
-                // (the outbox bound's load issued with the two bytes: one wait)
+                // (the outbox bound's load issued with the pair: one wait)
                 const uint32_t cap = (uint32_t)(a.obase[x.me - a.lo + 1] - x.ob);
-                const uint32_t af = (uint32_t)a.flags[ca] | ((uint32_t)a.part[ca] << 8);
+                const uint32_t af = a.upart[ca];
                 x.AF = l == 31 ? cap : af;
             }
             // the next node's inputs, in flight while this one runs

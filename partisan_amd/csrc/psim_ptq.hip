@@ -339,8 +339,8 @@ k_ptq(RoundArgs) {
             n.A = l < PSIM_ACTIVE_CAP ? a.act[li * PSIM_ACTIVE_CAP + l] : NONE;
             const bool mem = l < act_n && l < PSIM_ACTIVE_CAP && n.A < a.n_nodes;
             const uint32_t q = mem ? n.A : id;
-            const uint8_t f = a.flags[q], p = a.part[q];
-            setf(n.G, G_CMASK, qmask(mem && n.A != id && (f & F_UP) && p == me_part));
+            const uint32_t up = a.upart[q];
+            setf(n.G, G_CMASK, qmask(mem && n.A != id && up == me_part));
         }
         // the sets only for messages that may update them, the table only for
         // lazy adds, acks or a lazy tick
