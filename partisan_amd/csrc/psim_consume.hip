@@ -1763,14 +1763,15 @@ __global__ void __launch_bounds__(64 * PSIM_LITE_WPB, PSIM_LITE_WAVES) k_consume
     w.SC = 0;
     w.digest = 0;
     w.KM = magic_lanes();
-    const uint32_t n0 = kargs().n_lite[0], na = n0 + kargs().n_lite[1];
+    uint32_t lc[4], na;
+    lite_counts(kargs(), lc, na);
     if (gw < na) {
         const uint32_t last = na - 1;
         KArgs& a0 = kargs();
-        NodeIn x = load_node<false>(a0, reinterpret_cast<const uint32_t*>(kargs().desc_lite + lite_at(a0, n0, gw))[lane_id() & 3]);
+        NodeIn x = load_node<false>(a0, reinterpret_cast<const uint32_t*>(kargs().desc_lite + lite_at(a0, lc, gw))[lane_id() & 3]);
         NodeX y = load_x<true>(kargs(), x);
-        NodeIn xn = load_node<false>(kargs(), reinterpret_cast<const uint32_t*>(kargs().desc_lite + lite_at(a0, n0, min(gw + nw, last)))[lane_id() & 3]);
-        uint32_t d = reinterpret_cast<const uint32_t*>(kargs().desc_lite + lite_at(a0, n0, min(gw + 2 * nw, last)))[lane_id() & 3];
+        NodeIn xn = load_node<false>(kargs(), reinterpret_cast<const uint32_t*>(kargs().desc_lite + lite_at(a0, lc, min(gw + nw, last)))[lane_id() & 3]);
+        uint32_t d = reinterpret_cast<const uint32_t*>(kargs().desc_lite + lite_at(a0, lc, min(gw + 2 * nw, last)))[lane_id() & 3];
         for (uint32_t i = gw; i < na; i += nw) {
             STAMP(w, 0);
             begin_node(w, x, y);
@@ -1780,7 +1781,7 @@ __global__ void __launch_bounds__(64 * PSIM_LITE_WPB, PSIM_LITE_WAVES) k_consume
             writeback_lite(w);
             STAMP(w, 10);
             NodeIn xnn = load_node<false>(kargs(), d);
-            d = reinterpret_cast<const uint32_t*>(kargs().desc_lite + lite_at(kargs(), n0, min(i + 3 * nw, last)))[lane_id() & 3];
+            d = reinterpret_cast<const uint32_t*>(kargs().desc_lite + lite_at(kargs(), lc, min(i + 3 * nw, last)))[lane_id() & 3];
             x = xn; y = yn; xn = xnn;
             STAMP(w, 11);
         }
@@ -2076,7 +2077,7 @@ __global__ void __launch_bounds__(256, PSIM_RELAY_WAVES) k_relay(RoundArgs) {
     if (blockIdx.x == 0 && threadIdx.x == 0) kargs().ktime[0] = __builtin_amdgcn_s_memrealtime();
     enum { R_PROC, R_DELIV, R_SHUF, R_FAIL, R_DIGEST, R_BOUND, R_N };
     __shared__ unsigned long long sst[R_N];
-    __shared__ uint32_t wc5[7][5];                    // per list: the wave counts, then the block's base
+    __shared__ uint32_t wc5[9][5];                    // per list: the wave counts, then the block's base
     if (threadIdx.x < R_N) sst[threadIdx.x] = 0;
     __syncthreads();
     const uint32_t l = lane_id();
@@ -2087,7 +2088,8 @@ __global__ void __launch_bounds__(256, PSIM_RELAY_WAVES) k_relay(RoundArgs) {
         KArgs& a = kargs();                           // (re-read per step, not held in SGPRs)
         const uint32_t P = base + threadIdx.x;
         uint4 D = make_uint4(0, 0, 0, 0);
-        bool heavy = false, to_pt = false, relay = false, maps = false, shuf = false, lite = false, bcast = false, term = false;
+        bool heavy = false, to_pt = false, relay = false, maps = false, shuf = false, lite = false, bcast = false, term = false,
+             extra = false;
         Hdr h;
         uint32_t ik = 0, oend = 0;
         uint4 act0 = make_uint4(0, 0, 0, 0), act1 = act0;
@@ -2109,7 +2111,7 @@ __global__ void __launch_bounds__(256, PSIM_RELAY_WAVES) k_relay(RoundArgs) {
             // SHUFFLE with TTL left (a relay while |active| > 1)
             uint32_t hvn = 0;
             bool all_relay = true, all_shuf = true, term_out = false;
-            bcast = false; term = false;
+            bcast = false; term = false; extra = (tf & DESC_SHUFFLE) != 0;
             const uint32_t av[8] = {act0.x, act0.y, act0.z, act0.w, act1.x, act1.y, act1.z, act1.w};
             // (four records' first 16 B issued before any is waited on: a
             // loop of single loads waits one memory latency per record)
@@ -2135,6 +2137,7 @@ __global__ void __launch_bounds__(256, PSIM_RELAY_WAVES) k_relay(RoundArgs) {
                         // (hv:1127) opens a lingering connection to a Sender outside
                         // the active view -- the connection table's path, k_consume
                         term |= type == PSIM_MSG_SHUFFLE && !relays;
+                        extra |= type == PSIM_MSG_SHUFFLE && relays;
                         if (type == PSIM_MSG_SHUFFLE && !relays) {
                             bool in = false;
 #pragma unroll
@@ -2201,36 +2204,39 @@ __global__ void __launch_bounds__(256, PSIM_RELAY_WAVES) k_relay(RoundArgs) {
             // its back (ptl_desc), and the lite list likewise by SHUFFLE
             // terminals (lite_at)
             const bool ptl = P < na && to_pt && !origin_node, lt = P < na && lite;
-            const bool g[7] = {P < na && heavy, P < na && to_pt && origin_node, ptl && (bcast || !PSIM_PTL_BIN),
-                               P < na && shuf, lt && (term || !PSIM_LITE_BIN), ptl && !(bcast || !PSIM_PTL_BIN),
-                               lt && !(term || !PSIM_LITE_BIN)};
-            uint64_t m[7];
+            const bool lt0 = lt && !(extra && PSIM_LITE_BIN), lt1 = lt && extra && PSIM_LITE_BIN;
+            const bool tb = term || !PSIM_LITE_BIN;
+            const bool g[9] = {P < na && heavy, P < na && to_pt && origin_node, ptl && (bcast || !PSIM_PTL_BIN),
+                               P < na && shuf, lt0 && tb, ptl && !(bcast || !PSIM_PTL_BIN), lt0 && !tb,
+                               lt1 && tb, lt1 && !tb};
+            uint64_t m[9];
 #pragma unroll
-            for (int k = 0; k < 7; k++) m[k] = ballot(g[k]);
+            for (int k = 0; k < 9; k++) m[k] = ballot(g[k]);
             const uint32_t wv = threadIdx.x >> 6, nwv = blockDim.x >> 6;
             __syncthreads();                          // the previous step's readers of wc5 are done
             if (l == 0)
 #pragma unroll
-                for (int k = 0; k < 7; k++) wc5[k][wv] = popc(m[k]);
+                for (int k = 0; k < 9; k++) wc5[k][wv] = popc(m[k]);
             __syncthreads();
-            if (threadIdx.x < 7) {
+            if (threadIdx.x < 9) {
                 const uint32_t k = threadIdx.x;
                 uint32_t t = 0;
                 for (uint32_t j = 0; j < nwv; j++) t += wc5[k][j];
                 uint32_t* cnt = k == 0 ? a.n_slow : k == 1 ? a.n_pt : k == 2 ? a.n_ptl : k == 3 ? a.n_shuf
-                              : k == 4 ? a.n_lite : k == 5 ? a.n_ptl + 1 : a.n_lite + 1;
+                              : k == 4 ? a.n_lite : k == 5 ? a.n_ptl + 1 : a.n_lite + (k - 5);
                 wc5[k][4] = t ? atomicAdd(cnt, t) : 0u;
             }
             __syncthreads();
 #pragma unroll
-            for (int k = 0; k < 7; k++)
+            for (int k = 0; k < 9; k++)
                 if (g[k]) {
                     uint32_t b0 = wc5[k][4];
                     for (uint32_t j = 0; j < wv; j++) b0 += wc5[k][j];
                     const uint32_t at = b0 + popc(m[k] & lt_mask());
                     uint4* desc = k == 0 ? a.desc_slow : k == 1 ? a.desc_pt : k == 2 || k == 5 ? a.desc_ptl
                                 : k == 3 ? a.desc_shuf : a.desc_lite;
-                    desc[k >= 5 ? a.n_local - 1 - at : at] =
+                    const uint32_t nl = a.n_local;
+                    desc[k == 5 || k == 6 ? nl - 1 - at : k == 7 ? nl + at : k == 8 ? 2 * nl - 1 - at : at] =
                         k == 0 && maps ? make_uint4(D.x, D.y, D.z | DESC_MAPS_BIT, D.w) : D;
                 }
         }

@@ -618,7 +618,7 @@ __global__ void __launch_bounds__(256) k_node_prep(RoundArgs a, const unsigned l
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         a.ktime[0] = ~0ull; a.ktime[1] = 0; *a.n_slow = 0; *a.n_pt = 0;
         if (a.n_shuf) *a.n_shuf = 0;
-        if (a.n_lite) { a.n_lite[0] = 0; a.n_lite[1] = 0; }
+        if (a.n_lite) { a.n_lite[0] = 0; a.n_lite[1] = 0; a.n_lite[2] = 0; a.n_lite[3] = 0; }
         if (a.n_ptl) { a.n_ptl[0] = 0; a.n_ptl[1] = 0; }
         if (a.n_stop) *a.n_stop = 0;
     }
@@ -2020,7 +2020,7 @@ int run_round(psim_handle* h, uint64_t* st, bool events_applied = false) {
             std::fprintf(stderr, "psim: round %llu shard %u: %u nodes with work, %u to k_consume, %u to k_pt, "
                          "%u to k_shuf, %u to k_consume_lite, %u to k_ptl, outbox bound %llu, emitted %llu\n",
                          (unsigned long long)h->round, s->idx, read1(s, s->d_nact.p), read1(s, s->n_slow.p),
-                         read1(s, s->n_pt.p), read1(s, s->n_shuf.p), read1(s, s->n_lite.p) + read1(s, s->n_lite.p + 1),
+                         read1(s, s->n_pt.p), read1(s, s->n_shuf.p), read1(s, s->n_lite.p) + read1(s, s->n_lite.p + 1) + read1(s, s->n_lite.p + 2) + read1(s, s->n_lite.p + 3),
                          read1(s, s->n_ptl.p) + read1(s, s->n_ptl.p + 1),
                          (unsigned long long)s->pin[PIN_TOTAL], (unsigned long long)em);
         }
@@ -2297,7 +2297,7 @@ int shard_alloc(psim_handle* h, Shard* s) {
     rc |= s->desc_slow.alloc(n); rc |= s->n_slow.alloc(1);
     rc |= s->desc_pt.alloc(n); rc |= s->n_pt.alloc(1);
     rc |= s->desc_shuf.alloc(n); rc |= s->n_shuf.alloc(1);
-    rc |= s->desc_lite.alloc(n); rc |= s->n_lite.alloc(2);
+    rc |= s->desc_lite.alloc(2 * n); rc |= s->n_lite.alloc(4);
     rc |= s->desc_ptl.alloc(n); rc |= s->n_ptl.alloc(2);
     if (h->cfg.manager == PSIM_MANAGER_PLUGGABLE) { rc |= s->stop_ids.alloc(n); rc |= s->n_stop.alloc(1); }
     rc |= s->stat_out.alloc(NST + 2);   // + the consume span

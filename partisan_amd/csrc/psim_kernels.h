@@ -65,7 +65,8 @@ struct RoundArgs {
     uint32_t* n_shuf;
     uint64_t* stat_shuf;        // k_shuf's per-block stats rows
     uint4* desc_lite;           // ... and the nodes with SHUFFLE terminals / replies, for k_lite_half:
-    uint32_t* n_lite;           // [0] from the front, those with a terminal, [1] from the back (lite_at)
+    uint32_t* n_lite;           // 2 n_local slots, four bins (lite_at): [0] and [1] from the first
+                                // half's front and back, [2] and [3] from the second's
     uint64_t* stat_lite;        // k_consume_lite's per-block stats rows
     uint4* desc_ptl;            // ... and the nodes with Plumtree work and no origin, for k_ptl:
     uint32_t* n_ptl;            // [0] from the front, those with a BROADCAST in their inbox, [1] from
@@ -186,13 +187,24 @@ template <class Args>
 __device__ __forceinline__ uint4 ptl_desc(Args& a, uint32_t n0, uint32_t i) {
     return a.desc_ptl[i < n0 ? i : a.n_local - 1 - (i - n0)];
 }
-// entry i of the lite list: the nodes with a SHUFFLE terminal (a sublist of
-// the passive view, a reply and a merge) at the front, the others (replies'
-// merges, relays, shuffle starts) at the back -- k_lite_half pairs adjacent
-// entries in a wave's two halves, so most pairs share the terminal's sublist
+// entry i of the lite list, in four bins k_relay fills: nodes with a SHUFFLE
+// terminal (a sublist of the passive view, a reply and a merge) and nothing
+// else, nodes with only replies' merges, then the same two with more work
+// beside (SHUFFLE relays in the inbox, a due shuffle start) -- k_lite_half
+// pairs adjacent entries in a wave's two halves, so most pairs run the same
+// handlers and neither half waits on the other's extra work
 template <class Args>
-__device__ __forceinline__ uint32_t lite_at(Args& a, uint32_t n0, uint32_t i) {
-    return i < n0 ? i : a.n_local - 1 - (i - n0);
+__device__ __forceinline__ uint32_t lite_at(Args& a, const uint32_t (&c)[4], uint32_t i) {
+    const uint32_t n = a.n_local;
+    return i < c[0] ? i
+         : i < c[0] + c[1] ? n - 1 - (i - c[0])
+         : i < c[0] + c[1] + c[2] ? n + (i - c[0] - c[1])
+         : 2 * n - 1 - (i - c[0] - c[1] - c[2]);
+}
+template <class Args>
+__device__ __forceinline__ void lite_counts(Args& a, uint32_t (&c)[4], uint32_t& na) {
+    c[0] = a.n_lite[0]; c[1] = a.n_lite[1]; c[2] = a.n_lite[2]; c[3] = a.n_lite[3];
+    na = c[0] + c[1] + c[2] + c[3];
 }
 __device__ __forceinline__ KArgs& kargs() {
     KArgs* p = (KArgs*)__builtin_amdgcn_kernarg_segment_ptr();

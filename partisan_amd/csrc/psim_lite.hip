@@ -435,8 +435,8 @@ struct HIn {
 // (the descriptor comes from a load issued before the previous node's
 // writeback: issued after those stores, its wait drained them -- the memory
 // counter is in order -- at every node)
-DEV uint4 load_desc(KArgs& a, uint32_t n0, uint32_t i, bool live) {
-    return live ? a.desc_lite[lite_at(a, n0, i)] : make_uint4(0, 0, 0, 0);
+DEV uint4 load_desc(KArgs& a, const uint32_t (&lc)[4], uint32_t i, bool live) {
+    return live ? a.desc_lite[lite_at(a, lc, i)] : make_uint4(0, 0, 0, 0);
 }
 // the node's rows: header words, active and passive rows, partition byte
 // (for the next node issued after this one's body, so that they are not
@@ -600,12 +600,13 @@ __global__ void __launch_bounds__(64 * PSIM_HALF_WPB, PSIM_HALF_WAVES) k_lite_ha
     // half h of global wave gw takes list entries 2 gw + h, + 2 nw, ...
     const uint32_t nw = gridDim.x * HWPB;
     const uint32_t first = 2 * (blockIdx.x * HWPB + wid) + (hb_id() >> 5);
-    const uint32_t n0 = kargs().n_lite[0], na = n0 + kargs().n_lite[1];
+    uint32_t lc[4], na;
+    lite_counts(kargs(), lc, na);
     if (first < na) {
         Hn x;
-        HIn in = load_in(kargs(), load_desc(kargs(), n0, first, true));
+        HIn in = load_in(kargs(), load_desc(kargs(), lc, first, true));
         load_rows(kargs(), in, true);
-        uint4 Dn = load_desc(kargs(), n0, first + 2 * nw < na ? first + 2 * nw : first, first + 2 * nw < na);
+        uint4 Dn = load_desc(kargs(), lc, first + 2 * nw < na ? first + 2 * nw : first, first + 2 * nw < na);
         for (uint32_t i = first; i < na; i += 2 * nw) {
             HSTAMP(w, 8);
             begin(x, in);
@@ -623,7 +624,8 @@ __global__ void __launch_bounds__(64 * PSIM_HALF_WPB, PSIM_HALF_WAVES) k_lite_ha
             HIn inn = load_in(kargs(), Dn);
             HSTAMP(w, 0);
             body(x, w, c, in);
-            Dn = load_desc(kargs(), n0, nnx < na ? nnx : i, nnx < na);
+            HSTAMP(w, 9);
+            Dn = load_desc(kargs(), lc, nnx < na ? nnx : i, nnx < na);
             load_rows(kargs(), inn, nx < na);
             writeback(x, w, c);
             HSTAMP(w, 7);

@@ -30,7 +30,7 @@ for i, n in enumerate(PT):
     NAMES[16 + i] = "pt:" + n
 HALF = {8: "loop / wait for the node's loads", 0: "begin + connection cache", 6: "inbox record parse",
         1: "SHUFFLE relay", 2: "terminal: sublist", 3: "terminal: reply send", 4: "merge_exchange",
-        5: "shuffle start", 7: "writeback + flush"}
+        5: "shuffle start", 7: "writeback + flush", 9: "body's end (the other half's work)"}
 LITE = {0: "wait for the node's loads", 1: "begin_node", 2: "inbox chunk / record parse", 3: "SHUFFLE_REPLY merge",
         4: "SHUFFLE relay", 5: "terminal: sublist", 6: "terminal: reply send", 7: "terminal: merge",
         8: "shuffle start", 9: "next node's 2nd-stage loads", 10: "writeback", 11: "next node's loads"}
