@@ -2061,8 +2061,8 @@ DEV void block_append(bool go, const uint4& D, uint4* desc, uint32_t* cnt, uint3
     }
 }
 
-#ifndef PSIM_RELAY_WAVES
-#define PSIM_RELAY_WAVES 4
+#ifndef PSIM_RELAY_WAVES       // (5: 95 VGPRs, no spills; 0.532 -> 0.527 ms a phase against 4, profiles/r04 ab6)
+#define PSIM_RELAY_WAVES 5
 #endif
 #ifndef PSIM_PTL_BIN          // k_ptl's list binned by BROADCAST presence (0: one list, for A/B)
 #define PSIM_PTL_BIN 1
