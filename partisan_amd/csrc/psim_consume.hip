@@ -2193,6 +2193,20 @@ __global__ void __launch_bounds__(256, PSIM_RELAY_WAVES) k_relay(RoundArgs) {
             // (k_consume and k_consume_lite count their own)
             if (!heavy && !lite && (relay || to_pt || shuf)) v[R_PROC]++;
         }
+        // a relaying lane's members' up-and-partition pairs, issued before
+        // the list appends' barriers so that their latency hides behind them
+        // (read per relay, after its draw, they were one dependent load each)
+        uint32_t upm[4] = {NONE, NONE, NONE, NONE};   // member j's pair in bits 16 (j & 1) of word j >> 1
+        if (P < na && relay) {
+            const uint32_t av[8] = {act0.x, act0.y, act0.z, act0.w, act1.x, act1.y, act1.z, act1.w};
+            KArgs& a = kargs();
+#pragma unroll
+            for (int j = 0; j < 8; j += 2) {
+                const uint32_t q0 = (uint32_t)j < h.act_n && av[j] < a.n_nodes ? av[j] : D.x;
+                const uint32_t q1 = (uint32_t)j + 1 < h.act_n && av[j + 1] < a.n_nodes ? av[j + 1] : D.x;
+                upm[j >> 1] = (uint32_t)a.upart[q0] | ((uint32_t)a.upart[q1] << 16);
+            }
+        }
         // (k_ptl takes the Plumtree phase of nodes without an origin, and
         // hands k_pt the ones that do not fit a lane)
         const bool origin_node = ((D.z >> 28) & DESC_ORIGIN) != 0;
@@ -2267,9 +2281,14 @@ __global__ void __launch_bounds__(256, PSIM_RELAY_WAVES) k_relay(RoundArgs) {
                 }
                 uint32_t e = elig;
                 for (uint32_t j = 0; j < k; j++) e &= e - 1;
-                const uint32_t r = A[__ffs(e) - 1];
+                const uint32_t jr_ = (uint32_t)__ffs(e) - 1;
+                const uint32_t r = A[jr_];
+                uint32_t up = 0;
+#pragma unroll
+                for (int j = 0; j < 8; j++)
+                    if ((uint32_t)j == jr_) up = (upm[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
                 // do_send_message: maybe_connect + find, then the dispatch draw
-                if (r < a.n_nodes && a.upart[r] == me_part) {
+                if (r < a.n_nodes && up == me_part) {
                     rng++;
                     const uint4* ex = reinterpret_cast<const uint4*>(rp->ex);
                     const uint4 e0 = ex[0], e1 = ex[1];
