@@ -1935,6 +1935,14 @@ int phase_stats(psim_handle* h, Shard* s, const std::vector<uint32_t>& crashed) 
     const uint32_t nt = std::min<uint32_t>(STAT_TILES, std::max<uint32_t>(1, rows / 32));
     k_stats_tiles<<<nt, BLK, 0, s->stream>>>(s->stat_part.p, rows, s->stat_tile.p);
     k_stats_final<<<1, BLK, 0, s->stream>>>(s->stat_tile.p, nt, s->stat_out.p, s->pin_dev + (size_t)s->stat_slot * PIN_STRIDE);
+    if (h->world > 1) {
+        // the ranks' sums reduced on the device, on the shard's stream, and
+        // stored over the pinned words: the end of the round waits once
+        // (a host copy, an all-reduce and a second wait after it before)
+        TRY(h->comm->all_reduce(s->stat_out.p, NST, CType::U64, COp::SUM, s->stream));
+        HIP_TRY(hipMemcpyAsync(s->pin_dev + (size_t)s->stat_slot * PIN_STRIDE, s->stat_out.p, NST * 8,
+                               hipMemcpyDeviceToDevice, s->stream));
+    }
     if (!crashed.empty()) {
         TRY(upload(s, s->ev_ids, crashed));
         k_uncrash<<<grid_for(crashed.size()), BLK, 0, s->stream>>>(s->flags.p, s->crash_bits.p, s->ev_ids.p,
@@ -2029,14 +2037,7 @@ int run_round(psim_handle* h, uint64_t* st, bool events_applied = false) {
             h->kt_n[KT_CONSUME]++;
         }
     }
-    if (h->world > 1) {
-        Shard* s = h->shards[0];
-        TRY(h->comm_cnt.ensure(NST));
-        HIP_TRY(hipMemcpyAsync(h->comm_cnt.p, st, NST * 8, hipMemcpyHostToDevice, s->stream));
-        TRY(h->comm->all_reduce(h->comm_cnt.p, NST, CType::U64, COp::SUM, s->stream));
-        HIP_TRY(hipMemcpyAsync(st, h->comm_cnt.p, NST * 8, hipMemcpyDeviceToHost, s->stream));
-        TRY(stream_wait(s));
-    }
+    // (an RCCL rank's st[] is already the all-reduced sum: phase_stats)
     if (st[ST_BOUND]) {
         std::fprintf(stderr, "psim: round %llu: %llu nodes emitted past their outbox bound (engine bug)\n",
                      (unsigned long long)h->round, (unsigned long long)st[ST_BOUND]);
@@ -2052,7 +2053,7 @@ int run_round(psim_handle* h, uint64_t* st, bool events_applied = false) {
         // here: its shard's list is all-gathered, padded to the longest)
         std::vector<uint32_t> ids;
         for (Shard* s : h->shards) {
-            const size_t k = s->pin[ST_STOP];
+            const size_t k = read1(s, s->n_stop.p);   // this shard's own (pin[] is the ranks' sum)
             if (!k) continue;
             const size_t at = ids.size();
             ids.resize(at + k);
