@@ -2641,6 +2641,32 @@ DEV void ptl_ack_out(PtLane& n, uint64_t key) {
 #ifndef PSIM_PTL_BLOCKS_PER_CU
 #define PSIM_PTL_BLOCKS_PER_CU 3
 #endif
+#ifndef PSIM_PTL_RREG
+#define PSIM_PTL_RREG 6       // 4: 61.75, 6: 60.89 ms a phase at 2^26 (profiles/r04/ab_rreg.sh); 8 spills
+#endif
+// the first PTL_RREG Plumtree records of a k_ptl node, kept in registers from
+// the precondition pass: a record load issued after the node's emissions
+// waits for those stores too (one vector memory counter, in order), so the
+// handler loop loads none of them
+constexpr int PTL_RREG = PSIM_PTL_RREG;
+struct PtlRecs {
+    uint32_t src[PTL_RREG > 0 ? PTL_RREG : 1], tt[PTL_RREG > 0 ? PTL_RREG : 1], msg[PTL_RREG > 0 ? PTL_RREG : 1],
+        rnd[PTL_RREG > 0 ? PTL_RREG : 1], root[PTL_RREG > 0 ? PTL_RREG : 1];
+};
+// record j's source, type word, message id, round and root
+DEV void ptl_rec(const KArgs& a, const PtlRecs& R, uint32_t base, uint32_t j, uint32_t& src, uint32_t& tt,
+                 uint32_t& msg, uint32_t& rnd, uint32_t& root) {
+    if (j < (uint32_t)PTL_RREG) {
+        src = R.src[0]; tt = R.tt[0]; msg = R.msg[0]; rnd = R.rnd[0]; root = R.root[0];
+#pragma unroll
+        for (int k = 1; k < PTL_RREG; k++)
+            if (j == (uint32_t)k) { src = R.src[k]; tt = R.tt[k]; msg = R.msg[k]; rnd = R.rnd[k]; root = R.root[k]; }
+    } else {
+        const uint4* rq = reinterpret_cast<const uint4*>(a.rec_in + base + j);
+        const uint4 q0 = rq[0], q1 = rq[1];
+        src = q0.y; tt = q0.z; msg = q1.x; rnd = q1.y; root = q1.z;
+    }
+}
 #ifdef PSIM_PTL_WPE      // (a waves-per-SIMD floor for the register allocator, for A/B builds)
 #define PTL_BOUNDS __launch_bounds__(PTL_BLK) __attribute__((amdgpu_waves_per_eu(PSIM_PTL_WPE)))
 #else
@@ -2671,6 +2697,7 @@ __global__ void PTL_BOUNDS k_ptl(RoundArgs) {
         const uint32_t P = base + threadIdx.x;
         bool go = false, fall = false;
         uint4 D = make_uint4(0, 0, 0, 0);
+        PtlRecs R;
         uint32_t root0 = NONE, rtw4 = 0, rtw5 = 0, w10 = 0, w11 = 0, start = 0, act_n = 0, tmask = 0;
         if (P < nq) {
             D = ptl_desc(a, nq0, P);
@@ -2697,18 +2724,27 @@ __global__ void PTL_BOUNDS k_ptl(RoundArgs) {
             // members without a connection -- tests its sends in k_pt)
             bool ok = r0.y == NONE && r0.z == NONE && r0.w == NONE && (w11 & 0xFFFFu) == 0 &&
                       (root0 == NONE || ((rtw4 >> 8) == 0 && (rtw5 >> 8) == 0));
+#pragma unroll
+            for (int j = 0; j < PTL_RREG; j++) {      // (all issued before the first is used)
+                uint4 q0 = make_uint4(0, 0, 0, 0), q1 = q0;
+                if ((uint32_t)j < ik) {
+                    const uint4* rq = reinterpret_cast<const uint4*>(a.rec_in + D.y + j);
+                    q0 = rq[0]; q1 = rq[1];
+                }
+                R.src[j] = q0.y; R.tt[j] = q0.z; R.msg[j] = q1.x; R.rnd[j] = q1.y; R.root[j] = q1.z;
+            }
             for (uint32_t j = 0; ok && j < ik; j++) {
-                const uint4* rq = reinterpret_cast<const uint4*>(a.rec_in + D.y + j);
-                const uint4 q0 = rq[0], q1 = rq[1];
-                const uint32_t type = q0.z & 0xFF;
+                uint32_t src, tt, msg, rnd, root;
+                ptl_rec(a, R, D.y, j, src, tt, msg, rnd, root);
+                const uint32_t type = tt & 0xFF;
                 if (type < PSIM_MSG_PT_BROADCAST || type > PSIM_MSG_PT_GRAFT) continue;
                 n_eg += type == PSIM_MSG_PT_BROADCAST || type == PSIM_MSG_PT_IHAVE || type == PSIM_MSG_PT_GRAFT;
                 n_lz += type == PSIM_MSG_PT_BROADCAST || type == PSIM_MSG_PT_PRUNE;
                 tmask |= 1u << type;
-                if (type == PSIM_MSG_PT_BROADCAST) bm |= 1ull << (q1.x % PSIM_MSG_SLOTS);
+                if (type == PSIM_MSG_PT_BROADCAST) bm |= 1ull << (msg % PSIM_MSG_SLOTS);
                 if (type != PSIM_MSG_PT_IGNORED_IHAVE) {
-                    if (r0t == NONE) r0t = q1.z;      // the root a first update would store
-                    ok &= q1.z == r0t;
+                    if (r0t == NONE) r0t = root;      // the root a first update would store
+                    ok &= root == r0t;
                 }
             }
             // first deliveries (lazy adds): the BROADCASTs' slots not delivered yet
@@ -2770,26 +2806,17 @@ __global__ void PTL_BOUNDS k_ptl(RoundArgs) {
         n.have = ((uint64_t)hp[5] << 32) | hp[6];
         n.sets_dirty = false; n.out_dirty = false;
         uint32_t trk_round = hp[7], trk_hop = hp[8];
+        const uint32_t hw4 = hp[4];
+        const uint8_t fl0 = a.flags[id];              // (read before the emissions' stores: see PtlRecs)
         uint32_t seq = a.ocnt[li];
         const uint32_t oend = (uint32_t)a.obase[li + 1];
         const uint32_t ik = start == a.round ? 0u : (D.z & DESC_CNT_MASK);
-        // (each record's first 32 B as two 16-B loads -- field-wise reads were
-        // re-issued per branch, 40 more VGPRs -- and the next record's issued
-        // before this one is handled)
-        uint4 nq0 = make_uint4(0, 0, 0, 0), nq1 = nq0;
-        if (ik) {
-            const uint4* rq = reinterpret_cast<const uint4*>(a.rec_in + D.y);
-            nq0 = rq[0]; nq1 = rq[1];
-        }
         for (uint32_t j = 0; j < ik; j++) {           // the Plumtree inbox, canonical order
-            const uint4 q0 = nq0, q1 = nq1;
-            {
-                const uint4* rq = reinterpret_cast<const uint4*>(a.rec_in + D.y + min(j + 1, ik - 1));
-                nq0 = rq[0]; nq1 = rq[1];
-            }
-            const uint32_t type = q0.z & 0xFF;
+            uint32_t src, tt, msg, rnd, root;
+            ptl_rec(a, R, D.y, j, src, tt, msg, rnd, root);
+            const uint32_t type = tt & 0xFF;
             if (type < PSIM_MSG_PT_BROADCAST || type > PSIM_MSG_PT_GRAFT) continue;
-            const uint32_t src = q0.y, msg = q1.x, rnd = q1.y, root = q1.z, from = src | PSIM_MAP_BIT;
+            const uint32_t from = src | PSIM_MAP_BIT;
             v[T_DLV + type - PSIM_MSG_PT_BROADCAST]++;
             // plumtree_backend is_stale/1 over the slots (a retired id: overflow, stale)
             const uint32_t sk = msg % PSIM_MSG_SLOTS;
@@ -2861,7 +2888,7 @@ __global__ void PTL_BOUNDS k_ptl(RoundArgs) {
         }
         // write back: header words 5-8 and 11, the sets, the table, the flag byte
         uint32_t* hw = reinterpret_cast<uint32_t*>(a.hdr + li);
-        reinterpret_cast<uint4*>(hw)[1] = make_uint4(hp[4], (uint32_t)(n.have >> 32), (uint32_t)n.have, trk_round);
+        reinterpret_cast<uint4*>(hw)[1] = make_uint4(hw4, (uint32_t)(n.have >> 32), (uint32_t)n.have, trk_round);
         hw[8] = trk_hop;
         hw[11] = (w11 & ~0xFF0000u) | (n.on << 16);
         if (n.sets_dirty) {
@@ -2891,8 +2918,7 @@ __global__ void PTL_BOUNDS k_ptl(RoundArgs) {
         }
         a.ocnt[li] = seq;
         v[T_BOUND] += seq > oend - D.w ? 1u : 0u;
-        const uint8_t fl = a.flags[id];
-        a.flags[id] = (uint8_t)((fl & (F_UP | F_CRASHED)) | (n.on ? F_LAZY : 0) | (min(n.on, 15u) << F_OUTN_SHIFT) |
+        a.flags[id] = (uint8_t)((fl0 & (F_UP | F_CRASHED)) | (n.on ? F_LAZY : 0) | (min(n.on, 15u) << F_OUTN_SHIFT) |
                                 (act_n < a.min_active ? F_LOWACT : 0));
     }
 #pragma unroll
