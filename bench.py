@@ -2,13 +2,18 @@
 
 A step is one BSP round of the hot path (HyParView handlers + timers,
 Plumtree broadcast, message route) over every node of a 2^20-node overlay
-per GPU (steady state after a doubling bootstrap; a broadcast from node 0
+per GPU.  The default schedule is SURVEY 8(d)'s: joins spread over a
+64-round ramp, 100 warm-up rounds, --warmup rounds, then one broadcast from
+node 0 at the first timed round, whose propagation the window measures
+(--schedule doubling keeps round 2's line: doubling bootstrap, a broadcast
 every 10 rounds).  Prints ONE JSON line (rank 0).  See DESIGN.md section 5.
 
   python bench.py                      1 GPU (config C)
   python bench.py --gpus N             N GPUs: N ranks are started here, one
                                        per GPU, node-range sharded over RCCL
   torchrun --nproc-per-node N bench.py --gpus N   the same, ranks by torchrun
+  python bench.py --rank-path          1 GPU through the RCCL rank path (a
+                                       one-rank communicator; diagnostic)
 
 Every run first checks the sharded round against the one-shard engine on a
 small churn + partition scenario (digest of every emitted record, every
@@ -69,6 +74,10 @@ def parse():
     p.add_argument("--vshards", type=int, default=1,
                    help="diagnostic: G virtual shards of --nodes each on this one GPU (the sharded "
                         "partition / exchange / receive path with device copies instead of RCCL)")
+    p.add_argument("--rank-path", action="store_true",
+                   help="diagnostic at --gpus 1: run the RCCL rank path with a one-rank communicator "
+                        "(owner partition, ncclAllToAll of the counts, grouped self ncclSend/ncclRecv of "
+                        "the records, the stats ncclAllReduce, the overlay ncclAllGathers)")
     p.add_argument("--schedule", default="survey", choices=["survey", "doubling"],
                    help="the event schedule.  C, survey (default): SURVEY 8(d) -- joins spread "
                         "over a 64-round ramp, 100 warm-up rounds, then ONE broadcast from node 0 at the "
@@ -350,7 +359,7 @@ def shard_check(args, world, rank, dist, comm):
     # size (>= 2^19 nodes per shard) -- the small check covers that path too
     os.environ["PSIM_ROUTE_BLOCKS"] = "3"
     try:
-        if world > 1:
+        if world > 1 or comm is not None:
             cfg.shard_world, cfg.shard_rank = world, rank
             sh = Simulator(cfg, comm=comm)
             shards = world
@@ -391,6 +400,7 @@ def shard_check(args, world, rank, dist, comm):
     if bad:
         raise SystemExit(f"bench: sharding check failed on rank {rank}: {bad[:4]}")
     return {"nodes": n, "rounds": CHECK_ROUNDS, "shards": shards,
+            "rank_path": comm is not None,
             "against": "the one-shard engine on this GPU",
             "scenario": "doubling bootstrap, 20% churn rounds 30-49, half/half partition 55-64, "
                         "broadcast every 10 rounds",
@@ -540,6 +550,8 @@ def main():
         return main_strategy(args)
     if world > 1 and args.vshards > 1:
         raise SystemExit("bench: --vshards is a single-GPU diagnostic")
+    if args.rank_path and (world > 1 or args.vshards > 1):
+        raise SystemExit("bench: --rank-path is the one-GPU diagnostic of the RCCL path (ranks > 1 use it anyway)")
 
     # the CPU baseline first, while no GPU has been touched (it forks)
     if args.cpu_baseline_only:
@@ -566,7 +578,7 @@ def main():
 
     def shared_comm():
         if world == 1:
-            return None
+            return comm_id() if args.rank_path else None
         obj = [comm_id() if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
         return obj[0]
@@ -684,6 +696,7 @@ def main():
                    "broadcasts_before_window": 0 if survey else (t_start + BCAST_PERIOD - 1) // BCAST_PERIOD,
                    "broadcasts_in_window": n_bc,
                    "parallelism": (f"node-range sharded x{world}, RCCL all-to-all" if world > 1 else
+                                   "1 GPU, the RCCL rank path with a one-rank communicator" if args.rank_path else
                                    f"1 GPU, {args.vshards} virtual shards" if args.vshards > 1 else "1 GPU")},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": tsrc,

@@ -67,7 +67,7 @@
 extern "C" {
 #endif
 
-#define PSIM_ABI_VERSION 10
+#define PSIM_ABI_VERSION 11
 
 /* error codes */
 #define PSIM_OK 0
@@ -208,7 +208,11 @@ typedef struct psim_config {
     uint32_t n_shards;           /* node-range shards of this process (virtual shards), 1 */
     uint32_t shard_rank;         /* RCCL rank (multi-process), 0 */
     uint32_t shard_world;        /* RCCL world size, 1 */
-    const void *comm_id;         /* ncclUniqueId bytes when shard_world > 1, else NULL */
+    const void *comm_id;         /* ncclUniqueId bytes when shard_world > 1; with shard_world = 1
+                                    a non-NULL id selects the rank path on a one-rank communicator
+                                    (the 1-GPU diagnostic of the RCCL path: owner partition,
+                                    ncclAllToAll, self ncclSend/ncclRecv, ncclAllReduce,
+                                    ncclAllGather); NULL = the in-place route */
     uint64_t max_msgs_per_round; /* 0 = auto */
     /* pluggable manager */
     uint32_t manager;            /* PSIM_MANAGER_*, 0 = HyParView */
@@ -282,7 +286,10 @@ typedef struct psim_strategy_view {
     uint32_t view[PSIM_SVIEW_CAP];           /* scamp v1 membership (sets:to_list order) /
                                                 scamp v2 partial_view (list order) */
     uint32_t in_view[PSIM_SVIEW_CAP];        /* scamp v2 in_view (list order) */
-    uint32_t members, pad;                   /* full: size of query(ORSet) */
+    uint32_t members;                        /* full: size of query(ORSet) */
+    uint32_t view_slots;                     /* scamp v1: active slots of the membership set
+                                                (OTP sets v1: 16, one more past each 5 per slot;
+                                                0 for an empty view and other strategies) */
     uint64_t members_hash;                   /* full: sum of mix64(id + 1) over members */
 } psim_strategy_view;
 
@@ -355,18 +362,27 @@ int psim_leave(psim_handle *h, const uint32_t *nodes, size_t n);
 int psim_leave_node(psim_handle *h, const uint32_t *actors, const uint32_t *targets, size_t n);
 int psim_set_partition(psim_handle *h, const uint8_t *group, size_t n);
 /* View order.  Views are kept in sets:to_list/1 order of
- * OTP's sets v1 (<= 80 elements: 16 buckets, yielded bucket 1..16, oldest
- * first within a bucket), so every select_random index and every shuffle
- * key pairing (hyparview:1230-1231, :1346-1361; scamp_v1's membership) depends
- * on the bucket of each element, erlang:phash(NodeSpec, 16).  buckets[i] =
- * that bucket - 1 (0..15) for node i, n = n_nodes -- e.g. the table the
- * in-BEAM harness exports (erlang/harness, `B id bucket` lines).  Without a
- * table the handle uses a stand-in (low 4 bits of murmur3 fmix32(id)).
- * Valid only before the first round (PSIM_ESTATE after); buckets == NULL
- * restores the stand-in.  Multi-rank handles: every rank passes the same
- * table.  Not part of psim_snapshot: set it on the new handle before
- * psim_restore. */
+ * OTP's sets v1, a linear hash table (stdlib sets.erl: 16 slots up to 80
+ * elements, yielded slot 1..n, oldest first within a slot; one more slot
+ * each time the size passes 5 n, one fewer when it drops below 3 n), so every
+ * select_random index and every shuffle key pairing (hyparview:1230-1231,
+ * :1346-1361; scamp_v1's membership, scamp_v1:45-279) depends on the slot of
+ * each element, erlang:phash(NodeSpec, MaxN) with MaxN = 16, 32, ...
+ * psim_set_phash_table takes the whole hash: phash[i] =
+ * erlang:phash(NodeSpec_i, 4294967296) - 1 for node i (phash(T, R) - 1 is
+ * that value mod R for every power of two R), n = n_nodes -- e.g. the table
+ * the in-BEAM harness exports (erlang/harness, `B id hash` lines).  The
+ * engine keeps its low 8 bits: every set it holds (views of <= 128 ids) has
+ * MaxN <= 32.  psim_set_bucket_table takes the 16-slot bucket alone
+ * (phash(NodeSpec, 16) - 1, 0..15): enough for every HyParView view; a SCAMP
+ * v1 view past 80 ids then reads the missing bits as 0.  Without a table the
+ * handle uses a stand-in hash (murmur3 fmix32(id)).  Valid only before the
+ * first round (PSIM_ESTATE after); NULL restores the stand-in.  Multi-rank
+ * handles: every rank passes the same table.  The table is not part of
+ * psim_snapshot, but a snapshot records its hash: set the same table on the
+ * new handle before psim_restore (PSIM_EINVAL otherwise). */
 int psim_set_bucket_table(psim_handle *h, const uint8_t *buckets, size_t n);
+int psim_set_phash_table(psim_handle *h, const uint32_t *phash, size_t n);
 int psim_clear_partition(psim_handle *h);
 /* Omission faults of the pluggable manager's interposition layer
  * (add_interposition_fun/2, remove_interposition_fun/1 pluggable:297-326;
@@ -402,7 +418,12 @@ int psim_clear_faults(psim_handle *h);
  * names the tracked broadcast of psim_get_delivery / psim_get_histograms. */
 int psim_broadcast(psim_handle *h, uint32_t root, uint32_t msg_id);
 
-/* Run n_rounds BSP rounds; stats (may be NULL) receives one entry per round. */
+/* Run n_rounds BSP rounds; stats (may be NULL) receives one entry per round.
+ * An error from inside a round (PSIM_ENOMEM, PSIM_EDEVICE, PSIM_ECOMM) leaves
+ * the state off a round boundary: the handle is unusable -- every later
+ * psim_step answers PSIM_ESTATE -- until psim_restore loads a snapshot into
+ * it.  PSIM_ECAPACITY (cfg.strict) is returned after a whole round and does
+ * not poison the handle. */
 int psim_step(psim_handle *h, uint32_t n_rounds, psim_round_stats *stats);
 
 /* Inspection: views of nodes [first, first+count) into caller buffers. */
@@ -425,8 +446,12 @@ int psim_get_histograms(psim_handle *h, psim_histograms *out);
 /* Snapshot of the whole simulation state of this process (node rows,
  * in-flight messages, round, events not yet applied are not included):
  * with buf == NULL (or cap too small) only *need is set.  psim_restore
- * loads it into a handle created with the same config; the rounds that
- * follow are identical to the original's (HyParView handles). */
+ * loads it into a handle created with the same config (and the same
+ * view-order table, whose hash the snapshot records: PSIM_EINVAL otherwise);
+ * the rounds that follow are identical to the original's (HyParView
+ * handles).  A restore replaces the whole state -- events queued and not yet
+ * applied are dropped -- and puts a handle a failed psim_step left unusable
+ * back into service. */
 int psim_snapshot(psim_handle *h, void *buf, size_t cap, size_t *need);
 int psim_restore(psim_handle *h, const void *buf, size_t size);
 

@@ -92,6 +92,7 @@ typedef struct snode {
     uint32_t pending, hello_sent;   /* internal_join/3: Pending = [Contact] until the handshake */
     uint32_t last_ping;             /* scamp last_message_time as a round, PSIM_NONE = undefined */
     uint32_t view[PSIM_SVIEW_CAP], view_n;   /* scamp v1 membership / v2 partial_view */
+    uint32_t view_slots;            /* scamp v1: active slots of the membership set (sets v1, >= 16) */
     uint32_t inv[PSIM_SVIEW_CAP], inv_n;     /* scamp v2 in_view */
     uint32_t leave_tgt;             /* leave/1 call of this round: target + 1, 0 = none */
 } snode;
@@ -133,7 +134,8 @@ struct psim_handle {
      * nx_* are the next round's (the API edits them, round_begin adopts them) */
     struct fault_set { uint64_t *send, *recv; size_t send_n, recv_n; uint8_t *faulted; } flt, nx;
     int faults_dirty;
-    uint8_t *btab;                  /* sets v1 bucket per node (orc_set_bucket_table), NULL = stand-in */
+    uint8_t *btab;                  /* low 8 bits of erlang:phash(NodeSpec, 2^32) - 1 per node
+                                       (orc_set_phash_table / orc_set_bucket_table), NULL = stand-in */
 };
 
 /* per-node execution context */
@@ -179,18 +181,51 @@ static uint32_t uniform_n(ctx *c, uint32_t n) {
 static uint64_t uniform_key(ctx *c) { return draw58(c) >> 5; }
 
 /* ------------------------------------------------------- sets v1 order -- */
-/* OTP sets (v1) with <= 80 elements: 16 buckets, element prepended in its
- * bucket, to_list yields bucket 1..16, oldest first.
- * bucket16() is erlang:phash(NodeSpec, 16) - 1 from the handle's table
- * (orc_set_bucket_table, e.g. exported by the in-BEAM harness); without one
- * the stand-in below (murmur3 fmix32 of the id): see DESIGN.md. */
-static uint32_t bucket16_default(uint32_t id) {
+/* OTP sets (v1, stdlib sets.erl; the default `sets` before OTP 24 and the
+ * one the reference's strategies use) is a linear hash table: `n` active
+ * slots (16 at sets:new/0), MaxN the power of two >= n, an element's slot
+ * get_slot/2 = phash(E, MaxN), or that minus MaxN/2 past n (the buddy slot).
+ * add_element/2 prepends to the slot's bucket; past 5 n elements
+ * maybe_expand/2 opens slot n + 1 and rehashes its buddy's bucket into the
+ * two (order kept); del_element/2 below 3 n elements (n > 16) closes slot n
+ * with maybe_contract/2, its bucket put in front of its buddy's (B2 ++ B1).
+ * to_list/1 folds slot n..1, each bucket head first, prepending: slot 1..n,
+ * oldest first within a slot.  Up to 80 elements that
+ * is 16 buckets, erlang:phash(NodeSpec, 16) - 1.  The hash is
+ * erlang:phash(NodeSpec, 2^32) - 1 from the handle's table (orc_set_phash_table,
+ * e.g. exported by the in-BEAM harness; its low 8 bits: MaxN <= 256 covers
+ * every set of <= 128 ids the engine holds); without one the stand-in below
+ * (murmur3 fmix32 of the id): see DESIGN.md.  Restated from OTP's published
+ * sets.erl; no OTP is present here, so the order past 80 is unpinned. */
+static uint32_t phash_default(uint32_t id) {
     uint32_t h = id;
     h ^= h >> 16; h *= 0x85EBCA6Bu; h ^= h >> 13; h *= 0xC2B2AE35u; h ^= h >> 16;
-    return h & 15u;
+    return h;
 }
-static uint32_t bucket16(const struct psim_handle *h, uint32_t id) {
-    return h->btab ? h->btab[id] : bucket16_default(id);
+static uint32_t bucket16_default(uint32_t id) { return phash_default(id) & 15u; }
+static uint32_t phash8(const struct psim_handle *h, uint32_t id) {
+    return h->btab ? h->btab[id] : (phash_default(id) & 255u);
+}
+static uint32_t set_maxn(uint32_t ns) {
+    uint32_t m = 16;
+    while (m < ns) m <<= 1;
+    return m;
+}
+/* get_slot/2, 0-based */
+static uint32_t set_slot(const struct psim_handle *h, uint32_t e, uint32_t ns) {
+    uint32_t m = set_maxn(ns), x = phash8(h, e) & (m - 1);
+    return x < ns ? x : x - m / 2;
+}
+/* the list re-ordered by slot under ns slots, stably: after a slot opens
+ * (its entries, from the buddy slot, go to the end) or closes (its entries,
+ * at the end, go after the buddy slot's own) */
+static void set_reslot(const struct psim_handle *h, uint32_t *l, uint32_t n, uint32_t ns) {
+    for (uint32_t i = 1; i < n; i++) {
+        uint32_t e = l[i], k = set_slot(h, e, ns);
+        int j = (int)i - 1;
+        while (j >= 0 && set_slot(h, l[j], ns) > k) { l[j + 1] = l[j]; j--; }
+        l[j + 1] = e;
+    }
 }
 
 static int list_member(const uint32_t *l, uint32_t n, uint32_t e) {
@@ -199,18 +234,38 @@ static int list_member(const uint32_t *l, uint32_t n, uint32_t e) {
     return 0;
 }
 
-/* sets:add_element/2 */
-static void set_add(const struct psim_handle *h, uint32_t *l, uint32_t *n, uint32_t e) {
+/* sets:add_element/2 of a set with *ns active slots (NULL: 16, a set that
+ * never grows past 80 elements -- every HyParView view) */
+static void set_add(const struct psim_handle *h, uint32_t *l, uint32_t *n, uint32_t e, uint32_t *ns) {
     if (list_member(l, *n, e)) return;
-    uint32_t b = bucket16(h, e), pos = *n;
+    uint32_t slots = ns ? *ns : 16, b = set_slot(h, e, slots), pos = *n;
     for (uint32_t i = 0; i < *n; i++)
-        if (bucket16(h, l[i]) > b) { pos = i; break; }
+        if (set_slot(h, l[i], slots) > b) { pos = i; break; }
     for (uint32_t i = *n; i > pos; i--) l[i] = l[i - 1];
     l[pos] = e;
     (*n)++;
+    if (ns && *n > 5 * *ns) {           /* maybe_expand/2: size + 1 > exp_size */
+        (*ns)++;
+        set_reslot(h, l, *n, *ns);
+    }
 }
 
-/* sets:del_element/2 */
+/* sets:del_element/2 of a set with *ns active slots: maybe_contract/2 below
+ * 3 n elements */
+static void set_del_slots(const struct psim_handle *h, uint32_t *l, uint32_t *n, uint32_t e, uint32_t *ns) {
+    uint32_t j = 0;
+    for (uint32_t i = 0; i < *n; i++)
+        if (l[i] != e) l[j++] = l[i];
+    if (j == *n) return;                /* Dc = 0 */
+    for (uint32_t i = j; i < *n; i++) l[i] = 0;
+    *n = j;
+    if (*n < 3 * *ns && *ns > 16) {
+        (*ns)--;
+        set_reslot(h, l, *n, *ns);
+    }
+}
+
+/* sets:del_element/2 of a set that never grew past 16 slots */
 static void set_del(uint32_t *l, uint32_t *n, uint32_t e) {
     uint32_t j = 0;
     for (uint32_t i = 0; i < *n; i++)
@@ -475,7 +530,7 @@ static void add_to_passive(ctx *c, uint32_t p) {
         uint32_t r = select_random(c, s->pas, s->pas_n, omit, 1);
         if (r != PSIM_NONE) set_del(s->pas, &s->pas_n, r);
     }
-    set_add(c->h, s->pas, &s->pas_n, p);
+    set_add(c->h, s->pas, &s->pas_n, p, NULL);
 }
 
 /* drop_random_element_from_active_view/1, hyparview:1467-1512 (no reservations) */
@@ -504,7 +559,7 @@ static void add_to_active(ctx *c, uint32_t p) {
     if (s->act_n >= c->h->cfg.max_active_size) drop_random_active(c);
     int had = conn_find(s, p) >= 0;
     conn_del(s, p);
-    set_add(c->h, s->act, &s->act_n, p);
+    set_add(c->h, s->act, &s->act_n, p, NULL);
     if (!had) conn_add(c, p | PSIM_CONN_DOWN);
 }
 
@@ -1354,7 +1409,7 @@ static uint32_t random_0_or_1(ctx *c) { return uniform_n(c, 10) >= 5 ? 1u : 0u; 
 static void scamp_add(ctx *c, uint32_t *l, uint32_t *n, uint32_t e, int as_set) {
     if (as_set && list_member(l, *n, e)) return;
     if (*n >= PSIM_SVIEW_CAP) { ovf(c, PSIM_OVF_STRATEGY); return; }
-    if (as_set) { set_add(c->h, l, n, e); return; }
+    if (as_set) { set_add(c->h, l, n, e, &c->h->sn[c->me].view_slots); return; }
     for (uint32_t i = *n; i > 0; i--) l[i] = l[i - 1];
     l[0] = e;
     (*n)++;
@@ -1429,12 +1484,7 @@ static void scamp_leave(ctx *c, uint32_t t) {
      * 'EXIT', pluggable:971-984), so the sends are judged on the old view */
     for (uint32_t i = 0; i < n0; i++)
         pl_send(c, m0[i], v1 ? PSIM_PL_REMOVE_SUB : PSIM_PL_BOOT_REMOVE, t, PSIM_NONE);
-    if (v1) {
-        uint32_t k = 0;
-        for (uint32_t i = 0; i < q->view_n; i++) if (q->view[i] != t) q->view[k++] = q->view[i];
-        for (uint32_t i = k; i < q->view_n; i++) q->view[i] = 0;
-        q->view_n = k;
-    }
+    if (v1) set_del_slots(c->h, q->view, &q->view_n, t, &q->view_slots);   /* sets:del_element/2 (sv1:111) */
 }
 
 /* leave/1 of the full strategy at the actor, NameToRemove = t (full:58-89):
@@ -1577,6 +1627,7 @@ static void pl_node_init(struct psim_handle *h, uint32_t n, uint32_t contact) {
     q->pending = contact;
     q->last_ping = PSIM_NONE;
     q->view[0] = n; q->view_n = 1;               /* init/1: Myself only */
+    q->view_slots = 16;                          /* sets:new/0 */
     if (h->cfg.strategy == PSIM_STRATEGY_FULL) {
         q->view_n = 0; q->view[0] = 0;
         uint32_t *b = fb_row(h, n);
@@ -2077,6 +2128,7 @@ int orc_get_strategy_nodes(struct psim_handle *h, uint32_t first, uint32_t count
         v->view_n = q->view_n; v->in_n = q->inv_n;
         memcpy(v->view, q->view, sizeof v->view);
         memcpy(v->in_view, q->inv, sizeof v->in_view);
+        if (h->cfg.strategy == PSIM_STRATEGY_SCAMP_V1 && q->view_n) v->view_slots = q->view_slots;
         if (h->fbits) {
             v->members = full_count(h, fb_row(h, n));
             v->members_hash = members_hash(h, fb_row(h, n));
@@ -2115,7 +2167,7 @@ void orc_philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0,
 }
 uint32_t orc_bucket16(uint32_t id) { return bucket16_default(id); }
 
-/* psim_set_bucket_table */
+/* psim_set_bucket_table: the 16-slot bucket alone (the hash's bits 4-7 read as 0) */
 int orc_set_bucket_table(struct psim_handle *h, const uint8_t *buckets, size_t n) {
     if (!h) return PSIM_EINVAL;
     if (h->round != 0) return PSIM_ESTATE;
@@ -2125,6 +2177,45 @@ int orc_set_bucket_table(struct psim_handle *h, const uint8_t *buckets, size_t n
         if (buckets[i] > 15) return PSIM_EINVAL;
     if (!h->btab && !(h->btab = (uint8_t *)malloc(n))) return PSIM_ENOMEM;
     memcpy(h->btab, buckets, n);
+    return PSIM_OK;
+}
+
+/* The sets v1 restatement alone (tests/test_strategies.py pins it against a
+ * bucket-level model of OTP's sets.erl): ops[i] = e adds element e, ~e
+ * deletes it, in a fresh set over the hash table `phash` (n entries); the
+ * final sets:to_list/1 into out (cap >= its size), *out_n, *slots. */
+int orc_sets_run(const uint32_t *phash, size_t n, const uint32_t *ops, size_t n_ops, uint32_t *out, size_t cap,
+                 uint32_t *out_n, uint32_t *slots) {
+    struct psim_handle h;
+    memset(&h, 0, sizeof h);
+    h.N = (uint32_t)n;
+    uint8_t *tab = (uint8_t *)malloc(n ? n : 1);
+    if (!tab) return PSIM_ENOMEM;
+    for (size_t i = 0; i < n; i++) tab[i] = (uint8_t)phash[i];
+    h.btab = tab;
+    uint32_t *l = (uint32_t *)calloc(n_ops + 1, sizeof(uint32_t)), k = 0, ns = 16;
+    if (!l) { free(tab); return PSIM_ENOMEM; }
+    int rc = PSIM_OK;
+    for (size_t i = 0; i < n_ops && !rc; i++) {
+        uint32_t e = ops[i] >> 31 ? ~ops[i] : ops[i];
+        if (e >= n) { rc = PSIM_ERANGE; break; }
+        if (ops[i] >> 31) set_del_slots(&h, l, &k, e, &ns);
+        else set_add(&h, l, &k, e, &ns);
+    }
+    if (!rc && cap < k) rc = PSIM_EINVAL;
+    if (!rc) { memcpy(out, l, k * sizeof(uint32_t)); *out_n = k; *slots = ns; }
+    free(l); free(tab);
+    return rc;
+}
+
+/* psim_set_phash_table: erlang:phash(NodeSpec, 2^32) - 1 per node */
+int orc_set_phash_table(struct psim_handle *h, const uint32_t *phash, size_t n) {
+    if (!h) return PSIM_EINVAL;
+    if (h->round != 0) return PSIM_ESTATE;
+    if (!phash) { free(h->btab); h->btab = NULL; return PSIM_OK; }
+    if (n != h->N) return PSIM_EINVAL;
+    if (!h->btab && !(h->btab = (uint8_t *)malloc(n))) return PSIM_ENOMEM;
+    for (size_t i = 0; i < n; i++) h->btab[i] = (uint8_t)phash[i];
     return PSIM_OK;
 }
 

@@ -8,7 +8,7 @@ import ctypes as C
 
 import numpy as np
 
-PSIM_ABI_VERSION = 10
+PSIM_ABI_VERSION = 11
 PSIM_MAP_BIT = 0x80000000
 PSIM_NONE = 0xFFFFFFFF
 ACTIVE_CAP, PASSIVE_CAP, IDMAP_CAP = 8, 32, 64
@@ -99,7 +99,7 @@ class PsimStrategyView(C.Structure):
         ("last_ping", C.c_uint32), ("rng_ctr", C.c_uint64),
         ("view_n", C.c_uint32), ("in_n", C.c_uint32),
         ("view", C.c_uint32 * SVIEW_CAP), ("in_view", C.c_uint32 * SVIEW_CAP),
-        ("members", C.c_uint32), ("pad", C.c_uint32), ("members_hash", C.c_uint64),
+        ("members", C.c_uint32), ("view_slots", C.c_uint32), ("members_hash", C.c_uint64),
     ]
 
 
@@ -138,6 +138,7 @@ SIGNATURES = {
     "set_partition": (C.c_int, [_H, C.POINTER(C.c_uint8), C.c_size_t]),
     "clear_partition": (C.c_int, [_H]),
     "set_bucket_table": (C.c_int, [_H, C.POINTER(C.c_uint8), C.c_size_t]),
+    "set_phash_table": (C.c_int, [_H, _P32, C.c_size_t]),
     "set_omission": (C.c_int, [_H, C.c_int, _P32, _P32, C.c_size_t, C.c_int]),
     "set_faulted": (C.c_int, [_H, _P32, C.c_size_t, C.c_int]),
     "clear_faults": (C.c_int, [_H]),

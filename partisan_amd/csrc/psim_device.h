@@ -26,6 +26,7 @@ struct __attribute__((aligned(16))) Hdr {
                                              // which | PSIM_CONN_DOWN (active members without one);
                                              // X-BOT: of which | PSIM_CONN_CLOSING (stopped pids)
     uint32_t pad1[4];      // pluggable: pad1[0] = leave/1 target of this round + 1, 0 = none;
+                           // pad1[1] = the SCAMP v1 membership set's active slots - 16;
                            // HyParView: pad1[1] / pad1[2] = the sent / recv id map's
                            // extension row + 1 (0 = none), words HW_SENT_EXT / HW_RECV_EXT;
                            // pad1[3] = the outstanding table's, word HW_OUT_EXT
@@ -161,29 +162,51 @@ __device__ __forceinline__ uint64_t draw58_at(uint64_t ctr, uint32_t node, uint6
     return ((((uint64_t)o1) << 32) | o0) >> 6;
 }
 
-// sets v1 bucket of an element: erlang:phash(NodeSpec, 16) - 1 from the
-// handle's bucket table (psim_set_bucket_table: one byte per global id,
-// replicated on every shard), or, without one, the default stand-in -- the
-// low 4 bits of murmur3's fmix32 of the id
-__host__ __device__ __forceinline__ uint32_t bucket16_default(uint32_t id) {
+// sets v1 slots of an element (OTP sets.erl get_slot/2: erlang:phash(E,
+// MaxN), MaxN = 16, 32, ..) come from the low bits of its 32-bit hash
+// erlang:phash(NodeSpec, 2^32) - 1.  The handle's table
+// (psim_set_phash_table / psim_set_bucket_table: one byte per global id, the
+// hash's low 8 bits, replicated on every shard) or, without one, the default
+// stand-in -- murmur3's fmix32 of the id
+__host__ __device__ __forceinline__ uint32_t phash_default(uint32_t id) {
     uint32_t h = id;
     h ^= h >> 16; h *= 0x85EBCA6Bu; h ^= h >> 13; h *= 0xC2B2AE35u; h ^= h >> 16;
-    return h & 15u;
+    return h;
 }
+__host__ __device__ __forceinline__ uint32_t bucket16_default(uint32_t id) { return phash_default(id) & 15u; }
 // (the table's byte load waited for on its own branch: merged with the
 // default branch, the load left its register "pending" at the join and the
 // compiler's path-insensitive wait there became an s_waitcnt vmcnt(0) on the
 // default branch too -- draining every load and store in flight, a node's
-// prefetched rows among them, twice per k_lite_half merge)
-__device__ __forceinline__ uint32_t bucket16(const uint8_t* tab, uint32_t id) {
+// prefetched rows among them, twice per k_lite_half merge.  The immediate is
+// gfx9's field layout -- vmcnt in bits 3:0 and 15:14 -- so other targets take
+// the plain load)
+__device__ __forceinline__ uint32_t phash8(const uint8_t* tab, uint32_t id) {
     uint32_t b;
     if (tab) {
         b = tab[id];
+#if defined(__gfx950__) || defined(__gfx942__) || defined(__gfx940__) || defined(__gfx90a__)
         __builtin_amdgcn_s_waitcnt(0x0F70);      // vmcnt(0), expcnt / lgkmcnt untouched
+#endif
     } else {
-        b = bucket16_default(id);
+        b = phash_default(id) & 255u;
     }
     return b;
+}
+// the 16-slot bucket, erlang:phash(NodeSpec, 16) - 1: every set of <= 80
+// elements (every HyParView view)
+__device__ __forceinline__ uint32_t bucket16(const uint8_t* tab, uint32_t id) { return phash8(tab, id) & 15u; }
+// the slot of an element in a sets v1 set with ns active slots (16 <= ns <=
+// 256): H = phash(E, MaxN) - 1 for MaxN the power of two >= ns; H >= ns ->
+// H - MaxN / 2 (the buddy slot, sets.erl get_slot/2)
+__host__ __device__ __forceinline__ uint32_t set_maxn(uint32_t ns) {
+    uint32_t m = 16;
+    while (m < ns) m <<= 1;
+    return m;
+}
+__device__ __forceinline__ uint32_t set_slot(const uint8_t* tab, uint32_t id, uint32_t ns) {
+    const uint32_t m = set_maxn(ns), x = phash8(tab, id) & (m - 1);
+    return x < ns ? x : x - m / 2;
 }
 
 // digest multiplier of record word j (oracle msg_hash): odd, position-distinct

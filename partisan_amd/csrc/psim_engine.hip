@@ -1247,7 +1247,12 @@ struct psim_handle {
     bool failed = false;
     std::vector<Shard*> shards;         // shards owned by this process
     int rank = 0, world = 1;
-    Comm* comm = nullptr;               // world > 1: RCCL (or the loopback test vehicle), psim_comm.h
+    // the rank path (one shard per rank, the owner partition, the exchange
+    // and the collectives of psim_comm.h): world > 1, or a one-rank world
+    // whose cfg.comm_id was given (the 1-GPU diagnostic of the RCCL path:
+    // every collective, the self send/recv included, runs through the library)
+    bool ranked = false;
+    Comm* comm = nullptr;               // ranked: RCCL (or the loopback test vehicle), psim_comm.h
     DBuf<uint64_t> comm_cnt;            // RCCL: [send counts | recv counts]
     // pending events
     std::vector<uint32_t> pend_crash, pend_join, pend_contact;
@@ -1259,6 +1264,7 @@ struct psim_handle {
     uint32_t slot_tab[2 * PSIM_MSG_SLOTS];            // slot k: msg id [k], root [PSIM_MSG_SLOTS + k]
     uint32_t tracked_msg = PSIM_NONE;
     bool btab = false;                  // psim_set_bucket_table: the shards' btab rows are in use
+    uint32_t btab_hash = 0;             // ... their FNV-1a | 1 (0 = the default table), in snapshots
     uint32_t fw = 0;                    // full strategy: words per member row (adds; removes beside)
     bool tomb = false;                  // full: an ORSet remove exists (leave/1): kernels read remove rows
     std::vector<uint8_t> started;       // full strategy: ids ever started (no restarts)
@@ -1282,6 +1288,11 @@ struct psim_handle {
 };
 
 namespace {
+
+// one shard in this process and no rank path: the round's emissions are
+// grouped by destination in place (phase_route_local); otherwise they go
+// through the owner partition and an exchange
+inline bool local_route(const psim_handle* h) { return h->G == 1 && !h->ranked; }
 
 RoundArgs make_args(psim_handle* h, Shard* s) {
     RoundArgs a;
@@ -1592,7 +1603,7 @@ int phase_events_prepare(psim_handle* h, Shard* s, const RoundCtl& ctl, RoundArg
         int headroom = 2;
         const char* rcap_init = getenv("PSIM_RCAP_INIT");   // (test hook: a small route capacity
                                                             // exercises the regrow + reroute)
-        if (h->G == 1 && !s->rcap) {
+        if (local_route(h) && !s->rcap) {
             s->rcap = 4096;
             while (s->rcap < (uint64_t)n * RCAP_PER_NODE) s->rcap <<= 1;
             if (rcap_init) s->rcap = std::max<uint64_t>(16, strtoull(rcap_init, nullptr, 10));
@@ -1607,7 +1618,7 @@ int phase_events_prepare(psim_handle* h, Shard* s, const RoundCtl& ctl, RoundArg
                 const uint64_t per_slot = sizeof(Msg) + sizeof(uint32_t);
                 // (memory the current buffers hold comes back when they regrow)
                 uint64_t avail = fr + (uint64_t)s->outbox.n * sizeof(Msg) + (uint64_t)s->okey.n * 4;
-                if (h->G == 1 && !rcap_init) {
+                if (local_route(h) && !rcap_init) {
                     const uint64_t rc = (uint64_t)n * RCAP_RESERVE;
                     if (rc > s->rcap && (double)(rc * per_rec) <= RCAP_FREE_FRAC * (double)avail) s->rcap = rc;
                     const uint64_t held = s->rcap * per_rec;
@@ -1628,7 +1639,7 @@ int phase_events_prepare(psim_handle* h, Shard* s, const RoundCtl& ctl, RoundArg
         }
         TRY(s->outbox.ensure(want, headroom));
         TRY(s->okey.ensure(want, headroom));
-        if (h->G == 1) TRY(route_buffers(s, s->m_in == 0));   // the route checks its capacity on the device
+        if (local_route(h)) TRY(route_buffers(s, s->m_in == 0));   // the route checks its capacity on the device
     }
 args:
     a.in_beg = s->in_beg.p;
@@ -1838,7 +1849,7 @@ int phase_partition(psim_handle* h, Shard* s) {
     TRY(s->hoff.ensure(nh));
     TRY(s->sendbuf.ensure(s->pin[PIN_TOTAL] + 1, 2));   // the outbox bound bounds the records
     TRY(s->d_off.ensure(G + 1));
-    const bool rccl = h->world > 1;
+    const bool rccl = h->ranked;
     if (rccl) TRY(h->comm_cnt.ensure(2 * G));
     s->soff.assign(G + 1, 0);
     {
@@ -1916,13 +1927,17 @@ int exchange_rccl(psim_handle* h) {
         TRY(s->recvbuf.ensure(m + 1));
         Msg* rb = s->recvbuf.p;
         std::vector<Xfer> sends, recvs;
+        // a rank's own records: a device copy, except in a one-rank world
+        // (the diagnostic of the RCCL path), where the self send / receive
+        // pair goes through the library like any other peer's
+        const bool self_comm = h->world == 1;
         for (uint32_t g = 0; g < G; g++) {
-            if (g == s->idx) continue;
+            if (g == s->idx && !self_comm) continue;
             if (s->scnt[g]) sends.push_back({(int)g, s->sendbuf.p + s->soff[g], s->scnt[g] * sizeof(Msg)});
             if (rcnt[g]) recvs.push_back({(int)g, rb + roff[g], rcnt[g] * sizeof(Msg)});
         }
         TRY(h->comm->exchange(sends, recvs, s->stream));
-        if (rcnt[s->idx])
+        if (rcnt[s->idx] && !self_comm)
             HIP_TRY(hipMemcpyAsync(rb + roff[s->idx], s->sendbuf.p + s->soff[s->idx],
                                    rcnt[s->idx] * sizeof(Msg), hipMemcpyDeviceToDevice, s->stream));
     }
@@ -1935,7 +1950,7 @@ int phase_stats(psim_handle* h, Shard* s, const std::vector<uint32_t>& crashed) 
     const uint32_t nt = std::min<uint32_t>(STAT_TILES, std::max<uint32_t>(1, rows / 32));
     k_stats_tiles<<<nt, BLK, 0, s->stream>>>(s->stat_part.p, rows, s->stat_tile.p);
     k_stats_final<<<1, BLK, 0, s->stream>>>(s->stat_tile.p, nt, s->stat_out.p, s->pin_dev + (size_t)s->stat_slot * PIN_STRIDE);
-    if (h->world > 1) {
+    if (h->ranked) {
         // the ranks' sums reduced on the device, on the shard's stream, and
         // stored over the pinned words: the end of the round waits once
         // (a host copy, an all-reduce and a second wait after it before)
@@ -1984,12 +1999,19 @@ int run_round(psim_handle* h, uint64_t* st, bool events_applied = false) {
     std::vector<RoundArgs> args(h->shards.size());   // (consume fills the payload arena fields)
     for (size_t i = 0; i < h->shards.size(); i++)
         TRY(phase_events_prepare(h, h->shards[i], ctl, args[i], !events_applied));
+    // (test hook: this round fails half-way, after its events went to the
+    // device, as an allocation failure inside a round would)
+    static const long long fail_round = getenv("PSIM_TEST_FAIL_ROUND") ? atoll(getenv("PSIM_TEST_FAIL_ROUND")) : -1;
+    if (fail_round >= 0 && h->round == (uint64_t)fail_round) {
+        for (Shard* s : h->shards) (void)hipStreamSynchronize(s->stream);
+        return PSIM_ENOMEM;
+    }
     for (size_t i = 0; i < h->shards.size(); i++) TRY(phase_consume(h, h->shards[i], args[i]));
-    if (h->G == 1) {
+    if (local_route(h)) {
         TRY(phase_route_local(h, h->shards[0]));
     } else {
         for (Shard* s : h->shards) TRY(phase_partition(h, s));
-        if (h->world > 1) TRY(exchange_rccl(h));
+        if (h->ranked) TRY(exchange_rccl(h));
         else TRY(exchange_local(h));
     }
     for (Shard* s : h->shards) {
@@ -2004,7 +2026,7 @@ int run_round(psim_handle* h, uint64_t* st, bool events_applied = false) {
         TRY(stream_wait(s));
         flush_timers(h, s);
         for (int k = 0; k < NST; k++) st[k] += s->pin[k];
-        if (h->G == 1 && s->pin[PIN_OVF]) {
+        if (local_route(h) && s->pin[PIN_OVF]) {
             // the route found more records than its buffers hold: grow them
             // (1.5x, power of two) and route this round's outbox again
             const uint64_t m = s->pin[PIN_OVF];
@@ -2019,7 +2041,7 @@ int run_round(psim_handle* h, uint64_t* st, bool events_applied = false) {
             TRY(phase_route_local(h, s));
             TRY(stream_wait(s));
         }
-        if (h->G == 1) s->m_in = (uint32_t)s->pin[PIN_M];   // routed this round
+        if (local_route(h)) s->m_in = (uint32_t)s->pin[PIN_M];   // routed this round
         static const bool trace_relay = getenv("PSIM_TRACE_RELAY") != nullptr;
         if (trace_relay && s->rgrid)
         {
@@ -2060,7 +2082,7 @@ int run_round(psim_handle* h, uint64_t* st, bool events_applied = false) {
             HIP_TRY(hipMemcpyAsync(ids.data() + at, s->stop_ids.p, k * 4, hipMemcpyDeviceToHost, s->stream));
             TRY(stream_wait(s));
         }
-        if (h->world > 1) {
+        if (h->ranked) {
             Shard* s = h->shards[0];
             const uint32_t W = h->world;
             std::vector<uint64_t> cnt(W), mine(ids.begin(), ids.end());
@@ -2112,8 +2134,8 @@ void fill_stats(const uint64_t* s, uint64_t round, psim_round_stats* o) {
 // device between kernels, no strict mode (it stops at the overflowing round)
 bool batchable(psim_handle* h) {
     static const bool trace = getenv("PSIM_TRACE_RELAY") != nullptr;
-    static const bool off = getenv("PSIM_NO_BATCH") != nullptr;
-    if (off || trace || h->G != 1 || h->world != 1 || h->phase_timers || h->cfg.strict ||
+    static const bool off = getenv("PSIM_NO_BATCH") != nullptr || getenv("PSIM_TEST_FAIL_ROUND") != nullptr;
+    if (off || trace || h->G != 1 || h->ranked || h->phase_timers || h->cfg.strict ||
         h->cfg.manager == PSIM_MANAGER_PLUGGABLE || !h->pend_lv_a.empty())
         return false;
     Shard* s = h->shards[0];
@@ -2417,8 +2439,11 @@ int psim_create(const psim_config* cfg, psim_handle** out) {
     const bool full = cfg->manager == PSIM_MANAGER_PLUGGABLE && cfg->strategy == PSIM_STRATEGY_FULL;
     uint32_t world = std::max<uint32_t>(cfg->shard_world, 1);
     uint32_t local = std::max<uint32_t>(cfg->n_shards, 1);
-    if (world > 1 && (local != 1 || !cfg->comm_id || cfg->shard_rank >= world)) return PSIM_EINVAL;
-    uint32_t G = world > 1 ? world : local;
+    // the rank path: world > 1, or one rank with a communicator id (the
+    // 1-GPU diagnostic of the RCCL path)
+    const bool ranked = world > 1 || cfg->comm_id != nullptr;
+    if (ranked && (local != 1 || !cfg->comm_id || cfg->shard_rank >= world)) return PSIM_EINVAL;
+    uint32_t G = ranked ? world : local;
     if (G > 64 || G > cfg->n_nodes) return PSIM_EINVAL;
     if (full && G > 1) return PSIM_EUNSUPPORTED;      // gossip payloads are shard-local
     psim_handle* h = new (std::nothrow) psim_handle();
@@ -2433,6 +2458,7 @@ int psim_create(const psim_config* cfg, psim_handle** out) {
     for (uint32_t k = 0; k < 2 * PSIM_MSG_SLOTS; k++) h->slot_tab[k] = PSIM_NONE;
     h->per = (h->N + G - 1) / G;
     h->world = (int)world;
+    h->ranked = ranked;
     h->rank = (int)cfg->shard_rank;
     int dev = cfg->device;
     if (dev < 0 && hipGetDevice(&dev) != hipSuccess) { delete h; return PSIM_EDEVICE; }
@@ -2471,7 +2497,7 @@ int psim_create(const psim_config* cfg, psim_handle** out) {
     }
     h->device = dev;
     for (uint32_t g = 0; g < G; g++) {
-        if (world > 1 && g != cfg->shard_rank) continue;
+        if (ranked && g != cfg->shard_rank) continue;
         Shard* s = new (std::nothrow) Shard();
         if (!s) { psim_destroy(h); return PSIM_ENOMEM; }
         s->idx = g;
@@ -2483,7 +2509,7 @@ int psim_create(const psim_config* cfg, psim_handle** out) {
             rc = PSIM_EDEVICE;
         if (rc) { psim_destroy(h); return rc; }
     }
-    if (world > 1) {
+    if (ranked) {
         // RCCL; an id from psim_loopback_comm_id selects the loopback test
         // vehicle instead (ranks as threads of this process, psim_comm.h)
         int rc;
@@ -2601,25 +2627,47 @@ int psim_set_partition(psim_handle* h, const uint8_t* group, size_t n) {
     return PSIM_OK;
 }
 
-// The sets v1 bucket of every node_spec, erlang:phash(NodeSpec, 16) - 1
-// (SURVEY App. A Q1): the order sets:to_list/1 yields views in, which every
-// select_random index and every shuffle key pairing follows (hv:1230-1231,
-// :1346-1361).  Before the first round only (the views already built would
-// be in the old order); buckets == NULL restores the default table.
-int psim_set_bucket_table(psim_handle* h, const uint8_t* buckets, size_t n) {
-    if (!h) return PSIM_EINVAL;
-    if (h->round != 0) return PSIM_ESTATE;
-    if (!buckets) { h->btab = false; return PSIM_OK; }
-    if (n != h->N) return PSIM_EINVAL;
-    for (size_t i = 0; i < n; i++)
-        if (buckets[i] > 15) return PSIM_EINVAL;
+// The view-order table: the low 8 bits of every
+// node_spec's erlang:phash(NodeSpec, 2^32) - 1, from which sets v1's slots
+// follow (psim_device.h set_slot: 16 buckets for every HyParView view, the
+// linear hash's wider tables for SCAMP v1 memberships past 80 ids): the order
+// sets:to_list/1 yields views in, which every select_random index and every
+// shuffle key pairing follows (hv:1230-1231, :1346-1361; sv1:45-279).  Before
+// the first round only (the views already built would be in the old order);
+// NULL restores the default table.
+static int install_table(psim_handle* h, const std::vector<uint8_t>& tab) {
     if (hipSetDevice(h->device) != hipSuccess) return PSIM_EDEVICE;
     for (Shard* s : h->shards) {
         if (!s->btab.p && s->btab.alloc(h->N)) return PSIM_ENOMEM;
-        if (hipMemcpy(s->btab.p, buckets, n, hipMemcpyHostToDevice) != hipSuccess) return PSIM_EDEVICE;
+        if (hipMemcpy(s->btab.p, tab.data(), tab.size(), hipMemcpyHostToDevice) != hipSuccess) return PSIM_EDEVICE;
     }
+    // (FNV-1a of the bytes, recorded in snapshots: psim_restore refuses a
+    // snapshot made under another table)
+    uint32_t x = 0x811C9DC5u;
+    for (uint8_t b : tab) x = (x ^ b) * 0x01000193u;
     h->btab = true;
+    h->btab_hash = x | 1u;
     return PSIM_OK;
+}
+
+int psim_set_bucket_table(psim_handle* h, const uint8_t* buckets, size_t n) {
+    if (!h) return PSIM_EINVAL;
+    if (h->round != 0) return PSIM_ESTATE;
+    if (!buckets) { h->btab = false; h->btab_hash = 0; return PSIM_OK; }
+    if (n != h->N) return PSIM_EINVAL;
+    for (size_t i = 0; i < n; i++)
+        if (buckets[i] > 15) return PSIM_EINVAL;
+    return install_table(h, std::vector<uint8_t>(buckets, buckets + n));
+}
+
+int psim_set_phash_table(psim_handle* h, const uint32_t* phash, size_t n) {
+    if (!h) return PSIM_EINVAL;
+    if (h->round != 0) return PSIM_ESTATE;
+    if (!phash) { h->btab = false; h->btab_hash = 0; return PSIM_OK; }
+    if (n != h->N) return PSIM_EINVAL;
+    std::vector<uint8_t> tab(n);
+    for (size_t i = 0; i < n; i++) tab[i] = (uint8_t)phash[i];
+    return install_table(h, tab);
 }
 
 int psim_clear_partition(psim_handle* h) {
@@ -2898,6 +2946,7 @@ int psim_get_strategy_nodes(psim_handle* h, uint32_t first, uint32_t count, psim
                 v->members_hash = members_hash(mem.data(), h->fw);
             } else {
                 memcpy(v->view, &view[(size_t)j * PSIM_SVIEW_CAP], sizeof v->view);
+                if (h->cfg.strategy == PSIM_STRATEGY_SCAMP_V1 && x.act_n) v->view_slots = 16 + x.pad1[1];
                 if (!inv.empty()) memcpy(v->in_view, &inv[(size_t)j * PSIM_SVIEW_CAP], sizeof v->in_view);
             }
         }
@@ -2967,7 +3016,7 @@ int psim_get_histograms(psim_handle* h, psim_histograms* out) {
     for (Shard* s : h->shards)
         k_hist_out<<<grid_for(s->n), BLK, 0, st>>>(s->hdr.p, s->act.p, s->pas.p, s->flags.p, s->lo, s->n, tbit,
                                                    ind.p, ind.p + N, hist.p);
-    if (h->world > 1) {
+    if (h->ranked) {
         TRY(h->comm->all_reduce(ind.p, 2 * N, CType::U32, COp::SUM, st));
     }
     for (Shard* s : h->shards)
@@ -2975,7 +3024,7 @@ int psim_get_histograms(psim_handle* h, psim_histograms* out) {
     std::vector<unsigned long long> hv(H_N + 4, 0);
     HIP_TRY(hipMemcpyAsync(hv.data(), hist.p, (H_N + 4) * 8, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
-    if (h->world > 1) {                          // sums over ranks; the latest round: max
+    if (h->ranked) {                             // sums over ranks; the latest round: max
         hv[H_N] = hv[H_LAST];
         TRY(h->comm_cnt.ensure(H_N + 4));
         HIP_TRY(hipMemcpyAsync(h->comm_cnt.p, hv.data(), (H_N + 4) * 8, hipMemcpyHostToDevice, st));
@@ -3010,7 +3059,7 @@ int psim_get_histograms(psim_handle* h, psim_histograms* out) {
             if (s->n)
                 k_pack_act<<<grid_for(s->n), BLK, 0, st>>>(s->hdr.p, s->act.p, s->n,
                                                            gact.p + (size_t)s->lo * PSIM_ACTIVE_CAP, gan.p + s->lo);
-        if (h->world > 1) {
+        if (h->ranked) {
             const size_t off = (size_t)h->rank * per;
             TRY(h->comm->all_gather(gact.p + off * PSIM_ACTIVE_CAP, gact.p, (size_t)per * PSIM_ACTIVE_CAP * 4, st));
             TRY(h->comm->all_gather(gan.p + off, gan.p, per, st));
@@ -3046,7 +3095,7 @@ int psim_get_histograms(psim_handle* h, psim_histograms* out) {
 struct SnapHead {
     uint32_t magic, abi, n_nodes, n_local_shards, manager, strategy, fw, started_n;
     uint64_t round;
-    uint32_t tracked_msg, pad, G, world;
+    uint32_t tracked_msg, btab_hash, G, world;
     uint32_t slot_tab[2 * PSIM_MSG_SLOTS];
 };
 struct ShardHead {
@@ -3105,7 +3154,7 @@ int psim_snapshot(psim_handle* h, void* buf, size_t cap, size_t* need) {
     if (!buf || cap < total) return PSIM_OK;
     char* o = static_cast<char*>(buf);
     SnapHead hd{SNAP_MAGIC, PSIM_ABI_VERSION, h->N, (uint32_t)h->shards.size(), h->cfg.manager, h->cfg.strategy,
-                h->fw, (uint32_t)h->started.size(), h->round, h->tracked_msg, 0, h->G, (uint32_t)h->world, {}};
+                h->fw, (uint32_t)h->started.size(), h->round, h->tracked_msg, h->btab_hash, h->G, (uint32_t)h->world, {}};
     memcpy(hd.slot_tab, h->slot_tab, sizeof h->slot_tab);
     memcpy(o, &hd, sizeof hd); o += sizeof hd;
     if (!h->started.empty()) { memcpy(o, h->started.data(), h->started.size()); o += h->started.size(); }
@@ -3131,6 +3180,7 @@ int psim_restore(psim_handle* h, const void* buf, size_t size) {
         hd.n_local_shards != h->shards.size() || hd.manager != h->cfg.manager || hd.strategy != h->cfg.strategy ||
         hd.fw != h->fw || hd.G != h->G || hd.world != (uint32_t)h->world)
         return PSIM_EINVAL;
+    if (hd.btab_hash != h->btab_hash) return PSIM_EINVAL;   // another view-order table
     if (hd.started_n) {
         if ((size_t)(end - o) < hd.started_n) return PSIM_EINVAL;
         h->started.assign(o, o + hd.started_n); o += hd.started_n;
@@ -3164,6 +3214,13 @@ int psim_restore(psim_handle* h, const void* buf, size_t size) {
     for (Shard* s : h->shards)
         HIP_TRY(hipMemcpy(s->slots.p, h->slot_tab, sizeof h->slot_tab, hipMemcpyHostToDevice));
     HIP_TRY(hipDeviceSynchronize());
+    // back on a round boundary: a handle a failed step poisoned runs again
+    h->failed = false;
+    h->pend_crash.clear(); h->pend_join.clear(); h->pend_contact.clear();
+    h->pend_lv_a.clear(); h->pend_lv_t.clear();
+    h->pend_join_mark.assign(h->pend_join_mark.size(), 0);
+    h->pend_part_set = h->pend_part_clear = false;
+    h->pend_b_root.clear(); h->pend_b_msg.clear();
     return PSIM_OK;
 }
 

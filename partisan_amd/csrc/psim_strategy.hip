@@ -50,17 +50,83 @@ DEV void ins2(L2& V, uint32_t& n, uint32_t pos, uint32_t e) {
     V.b = j < pos ? V.b : (j == pos ? e : (j <= n ? pb : 0u));
     n++;
 }
-// sets:add_element/2 in sets:to_list/1 order (after every entry of a bucket <= e's)
-DEV void add_set2(L2& V, uint32_t& n, uint32_t e) {
+// every entry moves to its position: entry l of the list to PA (lane l),
+// entry 64 + l to PB, through the wave's 128 scratch words
+DEV void permute2(uint32_t* lds, L2& V, uint32_t n, uint32_t PA, uint32_t PB) {
+    const uint32_t l = lane_id();
+    if (l < n) lds[PA] = V.a;
+    if (64 + l < n) lds[PB] = V.b;
+    __builtin_amdgcn_wave_barrier();
+    V.a = l < n ? lds[l] : 0u;
+    V.b = 64 + l < n ? lds[64 + l] : 0u;
+    __builtin_amdgcn_wave_barrier();
+}
+
+// A SCAMP v1 membership is an OTP sets v1 linear hash table (sets.erl) of
+// `ns` active slots; the list holds sets:to_list/1 order: slot 0..ns-1,
+// oldest first within a slot (an element is prepended to its bucket, and
+// to_list's fold reverses it).  sets:add_element/2: after every entry of a
+// slot <= e's; then maybe_expand/2 -- past 5 ns elements slot ns opens and
+// the entries of its buddy slot ns - MaxN/2 whose phash(E, MaxN') is ns + 1
+// move into it, order kept: to the list's end (MaxN doubles when ns reaches
+// it).
+DEV void add_set2(uint32_t* lds, L2& V, uint32_t& n, uint32_t e, uint32_t& ns) {
     const uint8_t* bt = kargs().btab;
-    const uint32_t l = lane_id(), b = bucket16(bt, e);
-    const uint32_t pos = popc(ballot(l < n && bucket16(bt, V.a) <= b)) + popc(ballot(64 + l < n && bucket16(bt, V.b) <= b));
+    const uint32_t l = lane_id(), b = set_slot(bt, e, ns);
+    const uint32_t pos = popc(ballot(l < n && set_slot(bt, V.a, ns) <= b)) +
+                         popc(ballot(64 + l < n && set_slot(bt, V.b, ns) <= b));
     ins2(V, n, pos, e);
+    if (n <= 5 * ns) return;
+    ns++;                                       // maybe_expand/2: one slot more
+    const bool ma = l < n && set_slot(bt, V.a, ns) == ns - 1;
+    const bool mb = 64 + l < n && set_slot(bt, V.b, ns) == ns - 1;
+    const uint64_t lt = (1ull << l) - 1;
+    const uint64_t bma = ballot(ma), bmb = ballot(mb);
+    const uint64_t sa = ballot(l < n && !ma), sb = ballot(64 + l < n && !mb);
+    const uint32_t stay = popc(sa) + popc(sb);
+    const uint32_t PA = ma ? stay + popc(bma & lt) : popc(sa & lt);
+    const uint32_t PB = mb ? stay + popc(bma) + popc(bmb & lt) : popc(sa) + popc(sb & lt);
+    permute2(lds, V, n, PA, PB);
+}
+
+// sets:del_element/2 of a member at list position i, then maybe_contract/2:
+// below 3 ns elements (ns > 16) slot ns - 1 closes and its entries join its
+// buddy slot ns - 1 - MaxN/2, after that slot's own entries (B2 ++ B1 in
+// bucket order, whose to_list is B1's entries, then B2's)
+DEV void del_set2(uint32_t* lds, L2& V, uint32_t& n, uint32_t e, uint32_t& ns) {
+    const uint8_t* bt = kargs().btab;
+    const uint32_t l = lane_id();
+    const uint64_t lt = (1ull << l) - 1;
+    {
+        const bool ka = l < n && V.a != e, kb = 64 + l < n && V.b != e;
+        const uint64_t ba = ballot(ka), bb = ballot(kb);
+        const uint32_t k = popc(ba) + popc(bb);
+        if (k == n) return;                     // not a member: Dc = 0
+        permute2(lds, V, n, ka ? popc(ba & lt) : k, kb ? popc(ba) + popc(bb & lt) : k);
+        V.a = l < k ? V.a : 0u;                 // (entries past the count are 0)
+        V.b = 64 + l < k ? V.b : 0u;
+        n = k;
+    }
+    if (!(n < 3 * ns && ns > 16)) return;
+    const uint32_t top = ns - 1, to = top - set_maxn(ns) / 2;
+    // the closing slot's entries (at the list's end) go after every other
+    // entry of a slot <= `to`
+    const bool ga = l < n && set_slot(bt, V.a, ns) == top, gb = 64 + l < n && set_slot(bt, V.b, ns) == top;
+    const bool ea = l < n && !ga && set_slot(bt, V.a, ns) <= to, eb = 64 + l < n && !gb && set_slot(bt, V.b, ns) <= to;
+    const uint64_t bga = ballot(ga), bgb = ballot(gb);
+    const uint32_t p = popc(ballot(ea)) + popc(ballot(eb)), g = popc(bga) + popc(bgb);
+    const uint64_t na = ballot(l < n && !ga), nb = ballot(64 + l < n && !gb);
+    const uint32_t ra = popc(na & lt), rb = popc(na) + popc(nb & lt);
+    const uint32_t PA = ga ? p + popc(bga & lt) : ra + (ra >= p ? g : 0u);
+    const uint32_t PB = gb ? p + popc(bga) + popc(bgb & lt) : rb + (rb >= p ? g : 0u);
+    permute2(lds, V, n, PA, PB);
+    ns--;
 }
 
 // Hdr fields of a pluggable node (see RoundArgs): join_contact = pending
 // contact, aux = round of the last ping, have = hello sent,
-// act_n = view length, pas_n = in_view length.
+// act_n = view length, pas_n = in_view length, pad1[1] = SCAMP v1's set
+// slots - 16 (sets v1 linear hashing, add_set2).
 struct Pw {
     const RoundArgs* a;
     uint32_t* lds;                 // 128 words of per-wave scratch
@@ -68,6 +134,7 @@ struct Pw {
     Hdr h;
     L2 V, I;                       // scamp: view / in_view, entries l and 64 + l in lane l
     uint32_t vn, in_n;
+    uint32_t vs;                   // scamp v1: the membership set's active slots (sets v1, 16..)
     L2 CV, CF;                     // connection cache: view ids at node start and
                                    // flags | part << 8 of each
     uint32_t seq;
@@ -365,7 +432,7 @@ DEV void full_gossip(Pw& w, uint32_t extra = NONE) {
 DEV void scamp_add(Pw& w, L2& L, uint32_t& n, uint32_t e, bool as_set) {
     if (as_set && has2(L, n, e)) return;
     if (n >= PSIM_SVIEW_CAP) { ovf(w, PSIM_OVF_STRATEGY); return; }
-    if (as_set) add_set2(L, n, e);
+    if (as_set) add_set2(w.lds, L, n, e, w.vs);
     else ins2(L, n, 0, e);
 }
 
@@ -421,20 +488,7 @@ DEV void scamp_leave(Pw& w, uint32_t t) {
     // pl:971-984): the sends are judged on the old view
     for (uint32_t i = 0; i < n0; i++)
         pl_send(w, get2(M0, i), v1 ? PSIM_PL_REMOVE_SUB : PSIM_PL_BOOT_REMOVE, t, NONE);
-    if (v1) {
-        const uint32_t l = lane_id();
-        const bool keep_a = l < w.vn && w.V.a != t, keep_b = 64 + l < w.vn && w.V.b != t;
-        const uint64_t ma = ballot(keep_a), mb = ballot(keep_b);
-        const uint32_t ca = (uint32_t)__popcll(ma);
-        if (keep_a) w.lds[__popcll(ma & ((1ull << l) - 1))] = w.V.a;
-        if (keep_b) w.lds[ca + __popcll(mb & ((1ull << l) - 1))] = w.V.b;
-        __builtin_amdgcn_wave_barrier();
-        const uint32_t k = ca + (uint32_t)__popcll(mb);
-        w.V.a = l < k ? w.lds[l] : 0u;
-        w.V.b = 64 + l < k ? w.lds[64 + l] : 0u;
-        __builtin_amdgcn_wave_barrier();
-        w.vn = k;
-    }
+    if (v1) del_set2(w.lds, w.V, w.vn, t, w.vs);    // sets:del_element/2 (sv1:111)
 }
 
 // leave/1 of the full strategy at the actor (full:58-89): the target's add is
@@ -536,6 +590,7 @@ DEV void process_pl(Pw& w, uint32_t n, uint32_t ib, uint32_t ik, uint32_t ob) {
     st_add(w, ST_PROC, 1);
     const bool full = a.strategy == PSIM_STRATEGY_FULL;
     w.vn = w.h.act_n; w.in_n = w.h.pas_n;
+    w.vs = 16 + w.h.pad1[1];
     const uint32_t* vrow = a.sview + (size_t)li * PSIM_SVIEW_CAP;
     const uint32_t* irow = a.sinv + (size_t)li * PSIM_SVIEW_CAP;
     w.V.a = full ? 0u : vrow[l];
@@ -612,6 +667,7 @@ DEV void process_pl(Pw& w, uint32_t n, uint32_t ib, uint32_t ik, uint32_t ob) {
 
     // ---- write back
     w.h.act_n = (uint8_t)w.vn; w.h.pas_n = (uint8_t)w.in_n;
+    w.h.pad1[1] = w.vs - 16;
     if (!full && ballot(w.V.a != V0.a)) a.sview[(size_t)li * PSIM_SVIEW_CAP + l] = w.V.a;
     if (!full && ballot(w.V.b != V0.b)) a.sview[(size_t)li * PSIM_SVIEW_CAP + 64 + l] = w.V.b;
     if (v2 && ballot(w.I.a != I0.a)) a.sinv[(size_t)li * PSIM_SVIEW_CAP + l] = w.I.a;

@@ -129,6 +129,18 @@ class _Driver:
         self._check(self._api["set_bucket_table"](
             self._h, b.ctypes.data_as(C.POINTER(C.c_uint8)), b.size), "set_bucket_table")
 
+    def set_phash_table(self, phash):
+        """erlang:phash(NodeSpec, 2^32) - 1 of every node (uint32): the sets
+        v1 slots of every set the handle keeps -- 16 buckets for HyParView
+        views, the linear hash's wider tables for SCAMP v1 memberships past
+        80 ids.  Before the first round; None restores
+        the built-in stand-in."""
+        if phash is None:
+            self._check(self._api["set_phash_table"](self._h, None, 0), "set_phash_table")
+            return
+        p = np.ascontiguousarray(phash, np.uint32)
+        self._check(self._api["set_phash_table"](self._h, _abi.u32p(p), p.size), "set_phash_table")
+
     # ---- omission faults of the pluggable manager's interposition layer
     # (add_interposition_fun/2, pluggable:297-326; the crash-fault model's
     # begin/end_send_omission, begin/end_receive_omission, begin/end_omission,
