@@ -385,6 +385,21 @@ static ERL_NIF_TERM nif_set_partition(ErlNifEnv *env, int argc, const ERL_NIF_TE
     return rc ? err(env, rc) : enif_make_atom(env, "ok");
 }
 
+/* set_phash_table(Ref, HashesBin): one native-endian uint32 per node,
+ * erlang:phash(NodeSpec, 2^32) - 1 -- the sets v1 slots of every set the
+ * engine keeps (16 buckets, or the linear hash's wider tables for SCAMP v1
+ * memberships past 80 ids); before the first step only */
+static ERL_NIF_TERM nif_set_phash_table(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[]) {
+    sim_res *r; ErlNifBinary b;
+    if (!enif_get_resource(env, argv[0], SIM_RT, (void **)&r) || !enif_inspect_binary(env, argv[1], &b) ||
+        b.size != (size_t)r->n_nodes * 4)
+        return enif_make_badarg(env);
+    LOCK_OR_BUSY(r);
+    int rc = psim_set_phash_table(r->h, (const uint32_t *)b.data, r->n_nodes);
+    enif_mutex_unlock(r->mu);
+    return rc ? err(env, rc) : enif_make_atom(env, "ok");
+}
+
 /* set_bucket_table(Ref, BucketsBin): one byte per node, erlang:phash(NodeSpec,
  * 16) - 1 -- the sets v1 order of every view; before the
  * first step only */
@@ -454,6 +469,7 @@ static ErlNifFunc funcs[] = {
     {"set_partition_nif", 2, nif_set_partition, 0},
     {"clear_partition_nif", 1, nif_clear_partition, 0},
     {"set_bucket_table_nif", 2, nif_set_bucket_table, 0},
+    {"set_phash_table_nif", 2, nif_set_phash_table, 0},
     {"omission_nif", 5, nif_omission, 0},
     {"faulted_nif", 3, nif_faulted, 0},
     {"clear_faults_nif", 1, nif_clear_faults, 0},

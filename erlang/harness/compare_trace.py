@@ -6,12 +6,12 @@
       and DIR/config_a.oracle (the CPU oracle's record stream of the same
       scenario: one line per emitted message, in the harness's format; its
       first line `S config_a` names the scenario).  With BUCKETS (a file of
-      `B id bucket` or `id bucket` lines) the oracle orders views by that
-      sets v1 table (psim_set_bucket_table) instead of its stand-in.
+      `B id hash` or `id hash` lines) the oracle orders views by that
+      sets v1 table (psim_set_phash_table) instead of its stand-in.
   python erlang/harness/compare_trace.py compare DIR/config_a.harness DIR/config_a.oracle
       diffs the two streams round by round; exit status 1 at the first
       differing record.  The harness writes the real view order -- a line
-      `B id bucket` per node, bucket = erlang:phash(NodeSpec, 16) - 1 (App.
+      `B id hash` per node, hash = erlang:phash(NodeSpec, 2^32) - 1 (App.
       A Q1) -- which compare copies to DIR/bucket16.txt and, when it differs
       from the table the oracle stream was made with, uses to regenerate that
       stream (DIR/config_a.oracle_b) before diffing: one harness run is a
@@ -57,7 +57,9 @@ STRATEGIES = {"full": 0, "scamp_v1": 1, "scamp_v2": 2}
 
 
 def read_buckets(path, n=None):
-    """`B id bucket` (harness output) or `id bucket` lines -> uint8 table"""
+    """`B id hash` (harness output: erlang:phash(NodeSpec, 2^32) - 1) or
+    `id hash` lines -> uint32 table; a 16-slot bucket table (0..15) reads
+    the same way (psim_set_phash_table takes it as a hash with zero high bits)"""
     rows = []
     for l in open(path):
         f = l.split()
@@ -66,13 +68,13 @@ def read_buckets(path, n=None):
         if len(f) == 2:
             rows.append((int(f[0]), int(f[1])))
     m = n if n is not None else (max(i for i, _ in rows) + 1 if rows else 0)
-    tab = np.zeros(m, np.uint8)
+    tab = np.zeros(m, np.uint32)
     seen = np.zeros(m, bool)
     for i, b in rows:
         if i < m:
             tab[i], seen[i] = b, True
-    if not seen.all() or (tab > 15).any():
-        raise ValueError(f"{path}: not a bucket table of {m} nodes")
+    if not seen.all():
+        raise ValueError(f"{path}: not a hash table of {m} nodes")
     return tab
 
 
@@ -124,7 +126,7 @@ def oracle_stream(n, seed, rounds, joins, bcast, crash, strategy=None, part=None
     else:
         o = Oracle(default_config(n_nodes=n, seed=seed))
     if buckets is not None:
-        o.set_bucket_table(buckets)
+        o.set_phash_table(buckets)
     lib = o._lib
     ev = {}
     for r, ids, contacts in joins:

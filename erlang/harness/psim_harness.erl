@@ -5,8 +5,9 @@
 %% node's `rand` state.  It writes every emitted message of every round as a
 %% record line in the engine's encoding, so erlang/harness/compare_trace.py
 %% can diff it against the CPU oracle (and through it the GPU engine),
-%% seed for seed.  It also exports erlang:phash(NodeSpec, 16) of every node
-%% -- the sets v1 bucket order the engine's bucket16() stands in for.
+%% seed for seed.  It also exports erlang:phash(NodeSpec, 2^32) - 1 of every
+%% node -- the sets v1 slots (16 buckets, or the linear hash's wider tables
+%% past 80 elements) the engine's stand-in hash replaces.
 %%
 %% NOT RUN HERE: this image has no Erlang VM (SURVEY 8(c)).  Run recipe:
 %% erlang/harness/README.md.
@@ -239,10 +240,16 @@ crash(Id, Nodes) ->
 %% ------------------------------------------------------ shim callbacks
 spec(Id) ->
     #{name => name(Id),
-      listen_addrs => [#{ip => {10, (Id bsr 16) band 255, (Id bsr 8) band 255, Id band 255}, port => 9090}],
+      listen_addrs => [#{ip => ip(Id), port => 9090}],
       channels => [undefined], parallelism => 1}.
 
 name(Id) -> list_to_atom(lists:flatten(io_lib:format("n~10..0B@sim", [Id]))).
+
+%% 10.0.0.0 + Id: term order of the specs is id order below 2^27 (the
+%% listen address decides it before the name), as psim_wire.cpp's ip_base + id
+ip(Id) ->
+    Ip = 16#0A000000 + Id,
+    {Ip bsr 24, (Ip bsr 16) band 255, (Ip bsr 8) band 255, Ip band 255}.
 
 id_of(#{name := Name}) -> id_of(Name);
 id_of(Name) when is_atom(Name) ->
@@ -321,7 +328,7 @@ ident(N) when is_atom(N) -> id_of(N).
 
 %% ------------------------------------------------------ exports
 write_buckets(F, N) ->
-    [io:format(F, "B ~b ~b~n", [Id, erlang:phash(spec(Id), 16) - 1]) || Id <- lists:seq(0, N - 1)],
+    [io:format(F, "B ~b ~b~n", [Id, erlang:phash(spec(Id), 4294967296) - 1]) || Id <- lists:seq(0, N - 1)],
     ok.
 
 write_views(F, Nodes) ->

@@ -10,7 +10,8 @@
 -export([create/1, join/3, crash/2, revive/2, leave/2, leave_node/3, broadcast/3, step/2, active/2, members/3,
          delivery/2, histograms/1, snapshot/1, restore/2, set_partition/2, clear_partition/1, node/2,
          begin_send_omission/3, end_send_omission/3, begin_receive_omission/3, end_receive_omission/3,
-         begin_omission/2, end_omission/2, clear_faults/1, msg_slots/1, set_bucket_table/2, phash_buckets/2]).
+         begin_omission/2, end_omission/2, clear_faults/1, msg_slots/1, set_bucket_table/2, phash_buckets/2,
+         set_phash_table/2, phash_table/2, spec_ip/1]).
 -on_load(init/0).
 
 %% back-off of a busy handle: 1 ms sleeps, at most ~10 s in all
@@ -63,6 +64,19 @@ set_bucket_table(Sim, Buckets) ->
     call(fun() -> set_bucket_table_nif(Sim, Bin) end).
 %% that table for node specs Spec(0) .. Spec(N - 1), computed by this VM
 phash_buckets(N, Spec) -> [erlang:phash(Spec(I), 16) - 1 || I <- lists:seq(0, N - 1)].
+%% the whole hash, erlang:phash(NodeSpec, 2^32) - 1 per node: the slots of
+%% every sets v1 set the engine keeps, SCAMP v1 memberships past 80 ids
+%% included (OTP's linear hash, psim_set_phash_table); before the first step
+set_phash_table(Sim, Hashes) ->
+    Bin = << <<H:32/native>> || H <- Hashes >>,
+    call(fun() -> set_phash_table_nif(Sim, Bin) end).
+phash_table(N, Spec) -> [erlang:phash(Spec(I), 4294967296) - 1 || I <- lists:seq(0, N - 1)].
+%% the simulated node_spec's listen address: 10.0.0.0 + Id, so that term
+%% order (the ip tuple decides it: listen_addrs precedes name) is id order for
+%% every id below 2^27 (psim_wire.cpp's ip_base + id)
+spec_ip(Id) ->
+    Ip = 16#0A000000 + Id,
+    {Ip bsr 24, (Ip bsr 16) band 255, (Ip bsr 8) band 255, Ip band 255}.
 %% one node: {ok, #{up, epoch, active, passive, have, round}}
 node(Sim, Node) -> call(fun() -> node_nif(Sim, Node) end).
 %% the live message slots: {ok, [{Slot, MsgId, RootId}]} -- delivery bit
@@ -113,6 +127,7 @@ members_nif(_S, _N, _K) -> erlang:nif_error(nif_not_loaded).
 delivery_nif(_S, _N) -> erlang:nif_error(nif_not_loaded).
 clear_partition_nif(_S) -> erlang:nif_error(nif_not_loaded).
 set_bucket_table_nif(_S, _B) -> erlang:nif_error(nif_not_loaded).
+set_phash_table_nif(_S, _B) -> erlang:nif_error(nif_not_loaded).
 clear_faults_nif(_S) -> erlang:nif_error(nif_not_loaded).
 node_nif(_S, _N) -> erlang:nif_error(nif_not_loaded).
 msg_slots_nif(_S) -> erlang:nif_error(nif_not_loaded).

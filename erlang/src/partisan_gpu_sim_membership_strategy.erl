@@ -39,11 +39,15 @@ init(_Identity) ->
                end,
     {ok, Sim} = case partisan_config:get(sim_handle, undefined) of
                     undefined ->
-                        partisan_gpu_sim:create(#{n_nodes => N, seed => partisan_config:get(sim_seed, 1),
-                                                  manager => 1, strategy => Strategy,
-                                                  fanout => partisan_config:get(sim_fanout, 0),
-                                                  scamp_c => partisan_config:get(scamp_c, 5),
-                                                  periodic_interval => 10});
+                        {ok, H0} = partisan_gpu_sim:create(#{n_nodes => N, seed => partisan_config:get(sim_seed, 1),
+                                                             manager => 1, strategy => Strategy,
+                                                             fanout => partisan_config:get(sim_fanout, 0),
+                                                             scamp_c => partisan_config:get(scamp_c, 5),
+                                                             periodic_interval => 10}),
+                        %% SCAMP v1's membership in this VM's sets v1 order
+                        %% (SURVEY App. A Q1; OTP's linear hash past 80 ids)
+                        ok = partisan_gpu_sim:set_phash_table(H0, partisan_gpu_sim:phash_table(N, fun spec/1)),
+                        {ok, H0};
                     H -> {ok, H}
                 end,
     State0 = #sim_strategy{sim = Sim, me = Me, n = N,
@@ -98,8 +102,7 @@ membership(#sim_strategy{sim = Sim, me = Me, n = N}) ->
     [spec(I) || I <- Ids].
 
 spec(I) ->
-    #{name => name(I), listen_addrs => [#{ip => {10, (I bsr 16) band 255, (I bsr 8) band 255, I band 255},
-                                           port => 9090}],
+    #{name => name(I), listen_addrs => [#{ip => partisan_gpu_sim:spec_ip(I), port => 9090}],
        channels => [undefined], parallelism => 1}.
 
 name(Id) -> list_to_atom(lists:flatten(io_lib:format("n~10..0B@sim", [Id]))).

@@ -117,7 +117,7 @@ init([]) ->
                         {ok, H0} = partisan_gpu_sim:create(Cfg),
                         %% views in this VM's sets v1 order (SURVEY App. A Q1):
                         %% erlang:phash/2 of every simulated node_spec
-                        ok = partisan_gpu_sim:set_bucket_table(H0, partisan_gpu_sim:phash_buckets(N, fun spec/1)),
+                        ok = partisan_gpu_sim:set_phash_table(H0, partisan_gpu_sim:phash_table(N, fun spec/1)),
                         {ok, H0};
                     H -> {ok, H}
                 end,
@@ -240,7 +240,7 @@ name(Id) -> list_to_atom(lists:flatten(io_lib:format("n~10..0B@sim", [Id]))).
 %% the node_spec of simulated node Id (the harness's, DESIGN.md section 2)
 spec(Id) ->
     #{name => name(Id),
-      listen_addrs => [#{ip => {10, (Id bsr 16) band 255, (Id bsr 8) band 255, Id band 255}, port => 9090}],
+      listen_addrs => [#{ip => partisan_gpu_sim:spec_ip(Id), port => 9090}],
       channels => [undefined], parallelism => 1}.
 id(Name) when is_atom(Name) ->
     [$n | Rest] = atom_to_list(Name),

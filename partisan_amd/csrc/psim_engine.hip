@@ -206,9 +206,12 @@ __global__ void k_origin(uint32_t* origin, uint32_t lo, uint32_t n_local, const 
 //                      returned count is the record's rank in its run), the
 //                      run starts (block scan), each source index into its
 //                      run, and every run of <= RUN_SHORT sorted in registers
-//   k_run_sort_long    runs longer than RUN_SHORT, one block each: bitonic
-//                      in LDS up to RUN_LDS, LDS-sorted chunks merged through
-//                      `tmp` beyond
+//                      -- then, in the same block, the runs of RUN_SHORT + 1
+//                      .. 64 (a wave each, bitonic over the lanes) and the
+//                      longer ones (the whole block: bitonic in LDS up to
+//                      RUN_LDS, LDS-sorted chunks merged through `tmp`
+//                      beyond), and the bucket's records copied into the
+//                      inbox in run order (the gather, 128 B a record)
 // Run order before the sort depends on atomic timing; sorting each run by
 // source index makes the inbox deterministic.
 constexpr uint32_t RUN_SHORT = 16;
@@ -284,21 +287,74 @@ __device__ __forceinline__ void route_step(const RouteIn& in, uint32_t step, uin
     }
 }
 
+// The round's stats: every kernel block left a row of NST partial sums,
+// summed inside the route (no launches of their own: two small kernels cost
+// ~12 us a round in launch and drain): block t < nt of k_bucket_hist sums a
+// contiguous range of rows, one lane per column (coalesced rows), into tile
+// row t; block 0 of k_bucket_scatter sums the tile rows.  The sums (and the
+// node-round span, out[NST..NST+1]) are also stored straight into the
+// shard's pinned host words, so the host reads them after its end-of-round
+// wait without a copy.
+constexpr uint32_t STAT_TILES = 256;
+struct StatsIn {
+    const uint64_t* part;      // nrows rows of NST partial sums
+    uint32_t nrows, nt;        // nt tiles (<= STAT_TILES, <= the hist grid)
+    uint64_t* tiles;
+    uint64_t* out;             // the shard's stat_out (NST sums, then the span)
+    uint64_t* hout;            // its pinned words
+};
+// (red: the block's [waves][64] words of LDS; every thread calls these)
+__device__ __forceinline__ void stats_tile(const StatsIn& st, uint32_t t, uint64_t (*red)[64]) {
+    const uint32_t c = threadIdx.x & 63, g = threadIdx.x >> 6, ng = blockDim.x >> 6;
+    const uint32_t per = (st.nrows + st.nt - 1) / st.nt;
+    const uint32_t r0 = t * per, r1 = min(st.nrows, r0 + per);
+    uint64_t v = 0;
+    if (c < NST) {
+#pragma unroll 4
+        for (uint32_t r = r0 + g; r < r1; r += ng) v += st.part[(size_t)r * NST + c];
+    }
+    __syncthreads();                                  // (red's previous readers are done)
+    red[g][c] = v;
+    __syncthreads();
+    if (g == 0 && c < NST) {
+        uint64_t u = 0;
+        for (uint32_t k = 0; k < ng; k++) u += red[k][c];
+        st.tiles[(size_t)t * NST + c] = u;
+    }
+    __syncthreads();
+}
+__device__ __forceinline__ void stats_final(const StatsIn& st, uint64_t (*red)[64]) {
+    const uint32_t c = threadIdx.x & 63, g = threadIdx.x >> 6, ng = blockDim.x >> 6;
+    uint64_t v = 0;
+    if (c < NST) {
+#pragma unroll 4
+        for (uint32_t b = g; b < st.nt; b += ng) v += st.tiles[(size_t)b * NST + c];
+    }
+    __syncthreads();
+    red[g][c] = v;
+    __syncthreads();
+    if (g == 0 && c < NST) {
+        uint64_t u = 0;
+        for (uint32_t k = 0; k < ng; k++) u += red[k][c];
+        st.out[c] = u;
+        st.hout[c] = u;
+    }
+    if (threadIdx.x == 0) { st.hout[NST] = st.out[NST]; st.hout[NST + 1] = st.out[NST + 1]; }
+    __syncthreads();
+}
+
 template <bool DENSE>
 __global__ void __launch_bounds__(RB_STEP) k_bucket_hist(RouteIn in, uint32_t nsteps, uint32_t nb,
-                                                         uint32_t wshift, uint32_t* hist, uint32_t* n_long,
-                                                         unsigned long long* btot, const uint32_t* ctl,
-                                                         unsigned long long* mark) {
+                                                         uint32_t wshift, uint32_t* hist, const uint32_t* ctl,
+                                                         unsigned long long* mark, StatsIn st) {
     if (*ctl) return;                                 // an aborted batch (run_batch)
     if (mark && blockIdx.x == 0 && threadIdx.x == 0) *mark = __builtin_amdgcn_s_memrealtime();   // (phase end)
     extern __shared__ uint32_t hcnt[];                // nb bucket counters
     __shared__ uint32_t spre[RB_WAVES][65];
     __shared__ uint64_t sbase[RB_WAVES][64];
+    if (blockIdx.x < st.nt) stats_tile(st, blockIdx.x, sbase);   // (uniform)
     for (uint32_t j = threadIdx.x; j < nb; j += blockDim.x) hcnt[j] = 0;
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        *n_long = 0;
-        hist[(size_t)nb * gridDim.x] = 0;             // the scan's extra entry
-    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) hist[(size_t)nb * gridDim.x] = 0;   // the scan's extra entry
     __syncthreads();
     for (uint32_t step = blockIdx.x; step < nsteps; step += gridDim.x)
         route_step<DENSE>(in, step, spre, sbase,
@@ -311,9 +367,12 @@ template <bool DENSE>
 __global__ void __launch_bounds__(RB_STEP) k_bucket_scatter(RouteIn in, uint32_t nsteps, uint32_t nb,
                                                             uint32_t wshift, const uint32_t* __restrict__ off,
                                                             uint2* pairs, uint64_t cap, uint64_t* hovf,
-                                                            uint32_t* ctl, uint32_t round1) {
+                                                            uint32_t* ctl, uint32_t round1, StatsIn st) {
     if (*ctl) return;                                 // an aborted batch (run_batch)
     extern __shared__ uint32_t hcnt[];                // nb rank counters
+    __shared__ uint32_t spre[RB_WAVES][65];
+    __shared__ uint64_t sbase[RB_WAVES][64];
+    if (blockIdx.x == 0) stats_final(st, sbase);      // (the tiles are k_bucket_hist's; before any return)
     const uint32_t m = off[(size_t)nb * gridDim.x];   // the record count
     if (m > cap) {                                    // the route buffers are too small:
         if (blockIdx.x == 0 && threadIdx.x == 0) {    // the host grows them and reruns
@@ -324,8 +383,6 @@ __global__ void __launch_bounds__(RB_STEP) k_bucket_scatter(RouteIn in, uint32_t
         }
         return;
     }
-    __shared__ uint32_t spre[RB_WAVES][65];
-    __shared__ uint64_t sbase[RB_WAVES][64];
     // each bucket's counter starts at this block's place in it: the returned
     // count is the pair's position (no per-record read of the offset matrix)
     for (uint32_t j = threadIdx.x; j < nb; j += blockDim.x) hcnt[j] = off[(size_t)j * gridDim.x + blockIdx.x];
@@ -449,17 +506,81 @@ __global__ void k_owner_offsets(const uint32_t* hoff, uint32_t nblk, uint32_t G,
 }
 
 
+// bitonic sort of p[0..k) (k <= RUN_LDS) through LDS, whole block
+__device__ __forceinline__ void block_sort_lds(uint32_t* sv, uint32_t* p, uint32_t k) {
+    uint32_t P = 1;
+    while (P < k) P <<= 1;
+    for (uint32_t t = threadIdx.x; t < P; t += blockDim.x) sv[t] = t < k ? p[t] : 0xFFFFFFFFu;
+    __syncthreads();
+    for (uint32_t kk = 2; kk <= P; kk <<= 1) {
+        for (uint32_t jj = kk >> 1; jj > 0; jj >>= 1) {
+            for (uint32_t t = threadIdx.x; t < P; t += blockDim.x) {
+                const uint32_t u = t ^ jj;
+                if (u > t) {
+                    const uint32_t a = sv[t], b = sv[u];
+                    if ((a > b) == ((t & kk) == 0)) { sv[t] = b; sv[u] = a; }
+                }
+            }
+            __syncthreads();
+        }
+    }
+    for (uint32_t t = threadIdx.x; t < k; t += blockDim.x) p[t] = sv[t];
+    __syncthreads();
+}
+
+// a run longer than 64, whole block: RUN_LDS chunks sorted in LDS, then
+// merged pairwise through y (the run's own range of the scratch)
+__device__ __forceinline__ void sort_run_block(uint32_t* p, uint32_t k, uint32_t* y, uint32_t* sv) {
+    for (uint32_t c0 = 0; c0 < k; c0 += RUN_LDS) block_sort_lds(sv, p + c0, min(RUN_LDS, k - c0));
+    uint32_t* x = p;
+    for (uint32_t wd = RUN_LDS; wd < k; wd *= 2) {
+        for (uint32_t a0 = threadIdx.x * 2 * wd; a0 < k; a0 += blockDim.x * 2 * wd) {
+            const uint32_t m0 = min(a0 + wd, k), e0 = min(a0 + 2 * wd, k);
+            uint32_t u = a0, v = m0, o = a0;
+            while (u < m0 && v < e0) y[o++] = x[u] <= x[v] ? x[u++] : x[v++];
+            while (u < m0) y[o++] = x[u++];
+            while (v < e0) y[o++] = x[v++];
+        }
+        __syncthreads();
+        uint32_t* z = x; x = y; y = z;
+    }
+    if (x != p)
+        for (uint32_t t = threadIdx.x; t < k; t += blockDim.x) p[t] = x[t];
+    __syncthreads();
+}
+
+// p[0..k), RUN_SHORT < k <= 64, sorted by one wave: a bitonic network over
+// the lanes (lane l holds element l; the missing ones sort last)
+__device__ __forceinline__ void wave_sort64(uint32_t* p, uint32_t k) {
+    const uint32_t l = threadIdx.x & 63;
+    uint32_t v = l < k ? p[l] : 0xFFFFFFFFu;
+#pragma unroll
+    for (uint32_t kk = 2; kk <= 64; kk <<= 1) {
+#pragma unroll
+        for (uint32_t j = kk >> 1; j > 0; j >>= 1) {
+            const uint32_t u = (uint32_t)__shfl_xor((int)v, (int)j);
+            const bool keep_min = ((l & j) == 0) == ((l & kk) == 0);
+            v = keep_min ? min(v, u) : max(v, u);
+        }
+    }
+    if (l < k) p[l] = v;
+}
+
 // One block per bucket of W destinations; LDS holds per destination the
 // count, the bound sum (later the run start, in the same words) and the
 // BROADCAST message-slot mask (64 bits): 4 x W words.
 __global__ void __launch_bounds__(RR_THREADS) k_bucket_route(
     uint32_t n, uint32_t wshift, uint32_t nblk, const uint32_t* __restrict__ off,
     const uint2* __restrict__ pairs, const Msg* __restrict__ rec, uint32_t* rank, unsigned long long* cb,
-    unsigned long long* bmask, uint32_t* in_beg, uint32_t* idx, uint32_t* long_list, uint32_t* n_long, uint64_t* hm,
+    unsigned long long* bmask, uint32_t* in_beg, uint32_t* idx, uint32_t* tmp, Msg* __restrict__ inbox, uint64_t* hm,
     uint64_t cap, const uint32_t* ctl) {
     if (*ctl) return;                                 // an aborted batch (run_batch)
-    extern __shared__ uint32_t sm[];
-    __shared__ uint32_t spart[RR_THREADS];
+    // (the dynamic words hold 64-bit masks: 8-byte aligned -- a 4-byte static
+    // word in front of them misaligned ds_or_b64 and faulted; the long-run
+    // count lives in spart's spare words instead)
+    extern __shared__ __attribute__((aligned(16))) uint32_t sm[];
+    __shared__ __attribute__((aligned(16))) uint32_t spart[RR_THREADS + 4];
+    uint32_t& s_nl = spart[RR_THREADS];
     const uint32_t W = 1u << wshift, wmask = W - 1, b = blockIdx.x;
     uint32_t* cnt = sm;
     uint32_t* bs = sm + W;
@@ -468,6 +589,7 @@ __global__ void __launch_bounds__(RR_THREADS) k_bucket_route(
     const uint32_t s0 = off[(size_t)b * nblk], s1 = off[(size_t)(b + 1) * nblk];
     if (off[(size_t)gridDim.x * nblk] > cap) return;  // overflow (k_bucket_scatter flagged it)
     for (uint32_t j = threadIdx.x; j < 4 * W; j += blockDim.x) sm[j] = 0;
+    if (threadIdx.x == 0) s_nl = 0;
     __syncthreads();
     for (uint32_t p = s0 + threadIdx.x; p < s1; p += blockDim.x) {
         const uint2 x = pairs[p];
@@ -521,11 +643,15 @@ __global__ void __launch_bounds__(RR_THREADS) k_bucket_route(
         idx[s0 + pre[x.x & wmask] + rank[p]] = x.y;
     }
     __syncthreads();                                  // the runs are in place (same block)
+    // the bucket's longer runs, listed in LDS (the BROADCAST masks are out:
+    // their words hold the list and the block sort's buffer)
+    uint32_t* sv = reinterpret_cast<uint32_t*>(mk);   // RUN_LDS words
+    uint32_t* ll = sv + RUN_LDS;                      // <= W destinations (2 W words in all, W >= 4096)
     for (uint32_t dl = threadIdx.x; dl < W; dl += blockDim.x) {
         const uint32_t k = cnt[dl];
         if (k < 2) continue;
         if (k > RUN_SHORT) {
-            long_list[atomicAdd(n_long, 1u)] = (b << wshift) + dl;
+            ll[atomicAdd(&s_nl, 1u)] = dl;
             continue;
         }
         uint32_t* q = idx + s0 + pre[dl];
@@ -545,60 +671,30 @@ __global__ void __launch_bounds__(RR_THREADS) k_bucket_route(
         for (uint32_t t = 0; t < RUN_SHORT; t++)
             if (t < k) q[t] = v[t];
     }
-}
-
-// bitonic sort of p[0..k) (k <= RUN_LDS) through LDS, whole block
-__device__ void block_sort_lds(uint32_t* sv, uint32_t* p, uint32_t k) {
-    uint32_t P = 1;
-    while (P < k) P <<= 1;
-    for (uint32_t t = threadIdx.x; t < P; t += blockDim.x) sv[t] = t < k ? p[t] : 0xFFFFFFFFu;
     __syncthreads();
-    for (uint32_t kk = 2; kk <= P; kk <<= 1) {
-        for (uint32_t jj = kk >> 1; jj > 0; jj >>= 1) {
-            for (uint32_t t = threadIdx.x; t < P; t += blockDim.x) {
-                const uint32_t u = t ^ jj;
-                if (u > t) {
-                    const uint32_t a = sv[t], b = sv[u];
-                    if ((a > b) == ((t & kk) == 0)) { sv[t] = b; sv[u] = a; }
-                }
-            }
-            __syncthreads();
-        }
+    // runs of RUN_SHORT + 1 .. 64: one wave each (a bitonic network over the
+    // lanes); longer ones -- a join storm on one contact -- the whole block
+    const uint32_t nl = s_nl, wv = threadIdx.x >> 6, nwv = blockDim.x >> 6;
+    for (uint32_t q = wv; q < nl; q += nwv) {
+        const uint32_t dl = ll[q], k = cnt[dl];
+        if (k <= 64) wave_sort64(idx + s0 + pre[dl], k);
     }
-    for (uint32_t t = threadIdx.x; t < k; t += blockDim.x) p[t] = sv[t];
     __syncthreads();
-}
-
-// one block per listed run; a run longer than RUN_LDS (a join storm on one
-// contact) is sorted in RUN_LDS chunks, then merged pairwise through tmp
-// (the run's own range of it) -- slow, and only for such rounds
-__global__ void __launch_bounds__(256) k_run_sort_long(const uint32_t* __restrict__ in_beg,
-                                                       const unsigned long long* __restrict__ cb, uint32_t* idx,
-                                                       uint32_t* tmp, const uint32_t* __restrict__ long_list,
-                                                       const uint32_t* n_long, const uint32_t* ctl) {
-    if (*ctl) return;                                 // an aborted batch (run_batch)
-    __shared__ uint32_t sv[RUN_LDS];
-    const uint32_t nl = *n_long;
-    for (uint32_t q = blockIdx.x; q < nl; q += gridDim.x) {
-        const uint32_t d = long_list[q], k = (uint32_t)cb[d];
-        uint32_t* p = idx + in_beg[d];
-        for (uint32_t c0 = 0; c0 < k; c0 += RUN_LDS) block_sort_lds(sv, p + c0, min(RUN_LDS, k - c0));
-        uint32_t* x = p;
-        uint32_t* y = tmp + in_beg[d];
-        for (uint32_t wd = RUN_LDS; wd < k; wd *= 2) {
-            for (uint32_t a0 = threadIdx.x * 2 * wd; a0 < k; a0 += blockDim.x * 2 * wd) {
-                const uint32_t m0 = min(a0 + wd, k), e0 = min(a0 + 2 * wd, k);
-                uint32_t u = a0, v = m0, o = a0;
-                while (u < m0 && v < e0) y[o++] = x[u] <= x[v] ? x[u++] : x[v++];
-                while (u < m0) y[o++] = x[u++];
-                while (v < e0) y[o++] = x[v++];
-            }
-            __syncthreads();
-            uint32_t* z = x; x = y; y = z;
-        }
-        if (x != p)
-            for (uint32_t t = threadIdx.x; t < k; t += blockDim.x) p[t] = x[t];
-        __syncthreads();
+    for (uint32_t q = 0; q < nl; q++) {               // (uniform)
+        const uint32_t dl = ll[q], k = cnt[dl];
+        if (k > 64) sort_run_block(idx + s0 + pre[dl], k, tmp + s0 + pre[dl], sv);
+    }
+    __syncthreads();
+    // the bucket's records into the inbox in run order (16 B a lane; two
+    // records' pieces in flight per thread)
+    const uint32_t m4 = (s1 - s0) * 4, bd = blockDim.x;
+    for (uint32_t t = threadIdx.x; t < m4; t += 2 * bd) {
+        const uint32_t t2 = t + bd;
+        const uint4 a = reinterpret_cast<const uint4*>(&rec[idx[s0 + (t >> 2)]])[t & 3];
+        uint4 c = make_uint4(0, 0, 0, 0);
+        if (t2 < m4) c = reinterpret_cast<const uint4*>(&rec[idx[s0 + (t2 >> 2)]])[t2 & 3];
+        reinterpret_cast<uint4*>(&inbox[s0 + (t >> 2)])[t & 3] = a;
+        if (t2 < m4) reinterpret_cast<uint4*>(&inbox[s0 + (t2 >> 2)])[t2 & 3] = c;
     }
 }
 
@@ -843,69 +939,6 @@ __global__ void k_desc(const uint64_t* __restrict__ packed, const uint64_t* __re
     const unsigned long long tot = blockIdx.x == gridDim.x - 1 ? btot_sum(btot, nbt) : 0ull;   // (uniform)
     if (li > a.n_local) return;
     desc_entry(a, li, pscan[li], packed[li], in_beg, cb, start, desc, obase, nact, tot, hout, cap, ctl);
-}
-
-// records src[slots[i]] -> out[i] for i < *pm, grid-stride, 4 lanes x 16 B
-__global__ void k_gather_dev(const Msg* __restrict__ rec, const uint32_t* __restrict__ slots,
-                             const uint32_t* __restrict__ pm, Msg* __restrict__ out, uint64_t cap,
-                             const uint32_t* ctl) {
-    if (*ctl || *pm > cap) return;                    // the route overflowed: redone by the host
-    const uint64_t m4 = (uint64_t)*pm * 4;
-    for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < m4;
-         t += (uint64_t)gridDim.x * blockDim.x) {
-        const uint64_t i = t >> 2;
-        const uint4* sp = reinterpret_cast<const uint4*>(&rec[slots[i]]);
-        reinterpret_cast<uint4*>(&out[i])[t & 3] = sp[t & 3];
-    }
-}
-
-// The round's stats: every kernel block left a row of NST partial sums.
-// k_stats_tiles: block b sums a contiguous range of rows, 4 rows at a time
-// with one lane per column (coalesced 384-B rows), into tile row b;
-// k_stats_final: one wave sums the tile rows.  The sums (and the node-round
-// span, out[NST..NST+1]) are also stored straight into the shard's pinned
-// host words, so the host reads them after its end-of-round wait without a
-// copy.
-constexpr uint32_t STAT_TILES = 256;
-__global__ void __launch_bounds__(BLK) k_stats_tiles(const uint64_t* __restrict__ part, uint32_t nrows,
-                                                    uint64_t* __restrict__ tiles) {
-    __shared__ uint64_t red[BLK / 64][64];
-    const uint32_t c = threadIdx.x & 63, g = threadIdx.x >> 6;
-    const uint32_t per = (nrows + gridDim.x - 1) / gridDim.x;
-    const uint32_t r0 = blockIdx.x * per, r1 = min(nrows, r0 + per);
-    uint64_t v = 0;
-    if (c < NST) {
-#pragma unroll 4
-        for (uint32_t r = r0 + g; r < r1; r += BLK / 64) v += part[(size_t)r * NST + c];
-    }
-    red[g][c] = v;
-    __syncthreads();
-    if (g == 0 && c < NST) {
-        uint64_t t = 0;
-#pragma unroll
-        for (uint32_t k = 0; k < BLK / 64; k++) t += red[k][c];
-        tiles[(size_t)blockIdx.x * NST + c] = t;
-    }
-}
-__global__ void __launch_bounds__(BLK) k_stats_final(const uint64_t* __restrict__ tiles, uint32_t nt, uint64_t* out,
-                                                    uint64_t* hout) {
-    __shared__ uint64_t red[BLK / 64][64];
-    const uint32_t c = threadIdx.x & 63, g = threadIdx.x >> 6;
-    uint64_t v = 0;
-    if (c < NST) {
-#pragma unroll 4
-        for (uint32_t b = g; b < nt; b += BLK / 64) v += tiles[(size_t)b * NST + c];
-    }
-    red[g][c] = v;
-    __syncthreads();
-    if (g == 0 && c < NST) {
-        uint64_t t = 0;
-#pragma unroll
-        for (uint32_t k = 0; k < BLK / 64; k++) t += red[k][c];
-        out[c] = t;
-        hout[c] = t;
-    }
-    if (threadIdx.x == 0) { hout[NST] = out[NST]; hout[NST + 1] = out[NST + 1]; }
 }
 
 // --------------------------------------------------------- overlay stats --
@@ -1178,7 +1211,7 @@ struct Shard {
     DBuf<Msg> inbox;
     // per-round scratch
     DBuf<uint32_t> okey, ocnt, in_beg,
-        d_nact, n_slow, n_pt, n_shuf, n_lite, n_ptl, rank, long_list, n_long, tmp, hist, hoff;
+        d_nact, n_slow, n_pt, n_shuf, n_lite, n_ptl, rank, tmp, hist, hoff;
     DBuf<unsigned long long> bmask;     // per local node: message slots of its BROADCAST records
     DBuf<uint2> pairs;                  // route: (destination in bucket | class, source index)
     DBuf<unsigned long long> cb;        // per local node: inbox count | bound sum << 32 (n + 1)
@@ -1744,22 +1777,12 @@ int phase_consume(psim_handle* h, Shard* s, RoundArgs& a) {
     return PSIM_OK;
 }
 
-// records of the grouped source indices, gathered into the other inbox:
-// k_consume then reads each node's messages as one contiguous run.  The
-// record count is read on the device (in_beg[n] for G == 1).
-int gather_inbox(psim_handle* h, Shard* s, const Msg* src, const uint32_t* dev_m, uint32_t max_m) {
-    KTimer t(h, s, KT_GATHER);
-    if (max_m)
-        k_gather_dev<<<std::min<uint32_t>(grid_for((uint64_t)max_m * 4), 8192), BLK, 0, s->stream>>>(
-            src, s->ivals.p, dev_m, s->inbox.p, s->rcap, s->ctl.p);
-    return PSIM_OK;
-}
-
-// dense emission list in (src, seq) order: keys = dst | bound, vals = slot
 // The route (section comment above the kernels) over this shard's outbox
 // runs (dense == nullptr) or the m records of `dense`; leaves cb, bmask,
-// in_beg[0..n] (in_beg[n] = the record count) and the sorted runs of
-// source indices in ivals.  No host synchronisation.
+// in_beg[0..n] (in_beg[n] = the record count), the sorted runs of source
+// indices in ivals and the records themselves in the inbox in run order:
+// k_consume reads each node's messages as one contiguous run.  No host
+// synchronisation.
 // where the first kernel after the HyParView node-round phase stamps the
 // phase's end (RoundArgs::ktime[1]); the pluggable kernel keeps its own span
 unsigned long long* phase_end_mark(psim_handle* h, Shard* s) {
@@ -1777,7 +1800,9 @@ int route_group(psim_handle* h, Shard* s, const Msg* dense, uint32_t m) {
     uint32_t wshift = n > (1u << 26) ? 13 : 12;
     if (const char* e = getenv("PSIM_ROUTE_WSHIFT")) {  // (another bucket width, for measurements)
         const int v = atoi(e);
-        if ((1u << v) >= RR_THREADS && v <= 13) wshift = (uint32_t)v;
+        // (k_bucket_route's long-run list and sort buffer share the 2 W
+        // words of its BROADCAST masks: W >= 2048)
+        if ((1u << v) >= RR_THREADS && v >= 11 && v <= 13) wshift = (uint32_t)v;
     }
     const uint32_t W = 1u << wshift, nb = (n + W - 1) >> wshift;
     const RouteIn in{dense ? dense : s->outbox.p, s->okey.p, s->obase.p, s->ocnt.p, dense ? m : n, s->lo,
@@ -1788,28 +1813,30 @@ int route_group(psim_handle* h, Shard* s, const Msg* dense, uint32_t m) {
     TRY(s->hist.ensure(nh));
     TRY(s->hoff.ensure(nh));
     const size_t lds_h = (size_t)nb * 4, lds_r = (size_t)W * 16;
+    // the round's stats rows (every node-phase kernel's blocks) are complete
+    const uint32_t rows = s->pgrid + s->cgrid + s->rgrid + s->tgrid + s->sgrid + s->lgrid + s->qgrid;
+    const StatsIn st{s->stat_part.p, rows,
+                     std::min<uint32_t>(nblk, std::min<uint32_t>(STAT_TILES, std::max<uint32_t>(1, rows / 32))),
+                     s->stat_tile.p, s->stat_out.p, s->pin_dev + (size_t)s->stat_slot * PIN_STRIDE};
     KTimer t(h, s, KT_SORT);
     if (dense)
-        k_bucket_hist<true><<<nblk, RB_STEP, lds_h, s->stream>>>(in, nsteps, nb, wshift, s->hist.p, s->n_long.p,
-                                                                 s->btot.p, s->ctl.p, nullptr);
+        k_bucket_hist<true><<<nblk, RB_STEP, lds_h, s->stream>>>(in, nsteps, nb, wshift, s->hist.p, s->ctl.p,
+                                                                 nullptr, st);
     else    // (G == 1: the first kernel after the node-round phase stamps its end)
-        k_bucket_hist<false><<<nblk, RB_STEP, lds_h, s->stream>>>(in, nsteps, nb, wshift, s->hist.p, s->n_long.p,
-                                                                  s->btot.p, s->ctl.p, phase_end_mark(h, s));
+        k_bucket_hist<false><<<nblk, RB_STEP, lds_h, s->stream>>>(in, nsteps, nb, wshift, s->hist.p, s->ctl.p,
+                                                                  phase_end_mark(h, s), st);
     TRY(scan_excl(s, s->hist.p, s->hoff.p, (uint32_t)nh));
     if (dense)
         k_bucket_scatter<true><<<nblk, RB_STEP, lds_h, s->stream>>>(in, nsteps, nb, wshift, s->hoff.p, s->pairs.p,
                                                                     s->rcap, s->pin_dev + PIN_OVF, s->ctl.p,
-                                                                    s->batch_round1);
+                                                                    s->batch_round1, st);
     else
         k_bucket_scatter<false><<<nblk, RB_STEP, lds_h, s->stream>>>(in, nsteps, nb, wshift, s->hoff.p,
                                                                      s->pairs.p, s->rcap, s->pin_dev + PIN_OVF,
-                                                                     s->ctl.p, s->batch_round1);
+                                                                     s->ctl.p, s->batch_round1, st);
     k_bucket_route<<<nb, RR_THREADS, lds_r, s->stream>>>(n, wshift, nblk, s->hoff.p, s->pairs.p, in.rec, s->rank.p,
-                                                          s->cb.p, s->bmask.p, s->in_beg.p, s->ivals.p,
-                                                          s->long_list.p, s->n_long.p, s->pin_dev + PIN_M, s->rcap,
-                                                          s->ctl.p);
-    k_run_sort_long<<<std::min<uint32_t>(n, 512), 256, 0, s->stream>>>(s->in_beg.p, s->cb.p, s->ivals.p, s->tmp.p,
-                                                                       s->long_list.p, s->n_long.p, s->ctl.p);
+                                                          s->cb.p, s->bmask.p, s->in_beg.p, s->ivals.p, s->tmp.p,
+                                                          s->inbox.p, s->pin_dev + PIN_M, s->rcap, s->ctl.p);
     HIP_TRY(hipGetLastError());
     return PSIM_OK;
 }
@@ -1827,14 +1854,9 @@ int route_buffers(Shard* s, bool both_inboxes) {
 }
 
 // G == 1: the outbox runs grouped by destination are the whole route
-int phase_route_local(psim_handle* h, Shard* s) {
-    TRY(route_group(h, s, nullptr, 0));
-    // (m_in: read back with the round's stats; ivals, pairs, rank, tmp and the
-    // inbox were sized in prepare by the outbox total, which bounds it)
-    // (a batch has no outbox total on the host: the capacity sizes the grid)
-    return gather_inbox(h, s, s->outbox.p, s->in_beg.p + s->n,
-                        (uint32_t)(s->batch_round1 ? s->rcap : std::min<uint64_t>(s->pin[PIN_TOTAL], s->rcap)));
-}
+// (m_in: read back with the round's stats; ivals, pairs, rank, tmp and the
+// inbox were sized in prepare by the outbox total, which bounds it)
+int phase_route_local(psim_handle* h, Shard* s) { return route_group(h, s, nullptr, 0); }
 
 // G > 1, sender side: the outbox partitioned by owner shard into the send
 // buffer (k_owner_part); per-owner counts/offsets on the host
@@ -1878,7 +1900,7 @@ int phase_receive(psim_handle* h, Shard* s, uint32_t m) {
     TRY(route_buffers(s, false));
     TRY(route_group(h, s, s->recvbuf.p, m));
     s->m_in = m;
-    return gather_inbox(h, s, s->recvbuf.p, s->in_beg.p + s->n, m);
+    return PSIM_OK;
 }
 
 // virtual shards of this process: device copies between shard buffers
@@ -1944,12 +1966,9 @@ int exchange_rccl(psim_handle* h) {
     return phase_receive(h, s, (uint32_t)m);
 }
 
+// the round's end after its route (which summed the stats: StatsIn)
 int phase_stats(psim_handle* h, Shard* s, const std::vector<uint32_t>& crashed) {
     KTimer t(h, s, KT_STATS);
-    const uint32_t rows = s->pgrid + s->cgrid + s->rgrid + s->tgrid + s->sgrid + s->lgrid + s->qgrid;
-    const uint32_t nt = std::min<uint32_t>(STAT_TILES, std::max<uint32_t>(1, rows / 32));
-    k_stats_tiles<<<nt, BLK, 0, s->stream>>>(s->stat_part.p, rows, s->stat_tile.p);
-    k_stats_final<<<1, BLK, 0, s->stream>>>(s->stat_tile.p, nt, s->stat_out.p, s->pin_dev + (size_t)s->stat_slot * PIN_STRIDE);
     if (h->ranked) {
         // the ranks' sums reduced on the device, on the shard's stream, and
         // stored over the pinned words: the end of the round waits once
@@ -2315,7 +2334,7 @@ int shard_alloc(psim_handle* h, Shard* s) {
     rc |= s->outx_top.alloc(1);
     rc |= s->ocnt.alloc(n); rc |= s->cb.alloc(n + 1);
     rc |= s->in_beg.alloc(n + 1); rc |= s->bound.alloc(n + 1); rc |= s->pscan.alloc(n + 1); rc |= s->obase.alloc(n + 1);
-    rc |= s->long_list.alloc(n); rc |= s->bmask.alloc(n); rc |= s->btot.alloc(4096); rc |= s->n_long.alloc(1);
+    rc |= s->bmask.alloc(n); rc |= s->btot.alloc(4096);
     rc |= s->desc.alloc(n); rc |= s->d_nact.alloc(1);
     rc |= s->desc_slow.alloc(n); rc |= s->n_slow.alloc(1);
     rc |= s->desc_pt.alloc(n); rc |= s->n_pt.alloc(1);
@@ -2369,8 +2388,8 @@ void shard_free(Shard* s) {
     s->pin = nullptr;
     s->outbox.release(); s->okey.release(); s->ocnt.release();
     s->cb.release(); s->in_beg.release();
-    s->rank.release(); s->long_list.release(); s->bmask.release(); s->btot.release();
-    s->hist.release(); s->hoff.release(); s->pairs.release(); s->n_long.release(); s->tmp.release();
+    s->rank.release(); s->bmask.release(); s->btot.release();
+    s->hist.release(); s->hoff.release(); s->pairs.release(); s->tmp.release();
     s->stop_ids.release(); s->n_stop.release();
     s->desc.release(); s->d_nact.release(); s->desc_slow.release(); s->n_slow.release(); s->desc_pt.release(); s->n_pt.release(); s->desc_shuf.release(); s->n_shuf.release(); s->desc_lite.release(); s->n_lite.release(); s->desc_ptl.release(); s->n_ptl.release(); s->bound.release(); s->pscan.release();
     s->obase.release(); s->stat_part.release(); s->stat_out.release(); s->stat_tile.release(); s->d_off.release();
@@ -3207,6 +3226,13 @@ int psim_restore(psim_handle* h, const void* buf, size_t size) {
             if (x.bytes) HIP_TRY(hipMemcpy(x.p, o, x.bytes, hipMemcpyHostToDevice));
             o += x.bytes;
         }
+        // the per-round words a round that failed half-way may have left set
+        // (a broadcast's origin entries, crashed-this-round bits, the batch
+        // abort word, the stop list): a round boundary has them clear
+        if (s->origin.p) HIP_TRY(hipMemset(s->origin.p, 0, s->origin.n * sizeof(uint32_t)));
+        if (s->crash_bits.p) HIP_TRY(hipMemset(s->crash_bits.p, 0, s->crash_bits.n * sizeof(uint32_t)));
+        if (s->ctl.p) HIP_TRY(hipMemset(s->ctl.p, 0, s->ctl.n * sizeof(uint32_t)));
+        if (s->n_stop.p) HIP_TRY(hipMemset(s->n_stop.p, 0, s->n_stop.n * sizeof(uint32_t)));
         s->reserved = false;
     }
     h->round = hd.round; h->tracked_msg = hd.tracked_msg;

@@ -376,32 +376,38 @@ DEV void merge_exchange(Hn& x, Hw& w, uint32_t EX, uint32_t nex) {
     if (par) {
         // branch-free steps, unrolled: candidate I of the half (a no-op past
         // mt or when already a member) evicts the index in K's lane 0 when
-        // the view is full, then goes in at its bucket's position
+        // the view is full, then goes in at its bucket's position.  An entry
+        // and its bucket are one tag, bucket << 27 | id (ids < 2^27,
+        // KEY_DST_MASK), lanes past the count hold TSENT: the entries of a
+        // bucket <= t's are the tags <= t's bucket | 0x07FFFFFF (a prefix),
+        // membership is tag equality (a candidate past mt is TSENT and
+        // matches the empty lanes: a no-op), and eviction + insertion is one
+        // select per lane among its own, its predecessor's and its
+        // successor's tag and t's
+        constexpr uint32_t TSENT = 0xFFFFFFFFu, IDM = (1u << 27) - 1;
+        uint32_t PT = l < x.pas_n ? (PB << 27) | x.P : TSENT;
+        const uint32_t TG = l < mt ? (TB << 27) | T : TSENT;
         uint32_t K = KI;                             // the next eviction's index in the half's lane 0
-        uint32_t dirty = 0;
+        uint32_t n = x.pas_n, dirty = 0;
         unroll<PSIM_EXCHANGE_CAP>([&](auto I) {
-            const uint32_t t = hgetc<I>(T), tb = hgetc<I>(TB);
-            const uint32_t n0 = x.pas_n;
-            const bool inP = hany(l < n0 && x.P == t);
-            const bool mem = ((uint32_t)I >= mt) | inP;
-            const bool ev = !mem && n0 >= maxp;
+            const uint32_t tt = hgetc<I>(TG);
+            const bool mem = hany(PT == tt);
+            const bool ev = !mem && n >= maxp;       // select_random(Passive, [Myself]) + remove
             const uint32_t k = hget_c0(K);
-            const uint32_t pn = from_next(x.P), pbn = from_next(PB), kn = from_next(K);
-            const bool sh = ev && l >= k;            // select_random(Passive, [Myself]) + remove
-            x.P = sh ? (l + 1 < n0 ? pn : 0u) : x.P;
-            PB = sh ? (l + 1 < n0 ? pbn : 0u) : PB;
+            const uint32_t kn = from_next(K), pv = from_prev(PT), nx = from_next(PT);
             K = ev ? kn : K;
             used += ev ? 1u : 0u;
-            const uint32_t n1 = n0 - (ev ? 1u : 0u);
-            const bool le = l < n1 && PB <= tb;      // a prefix of the half
-            const uint32_t lep = from_prev(le ? 1u : 0u), pv = from_prev(x.P), pbv = from_prev(PB);
-            const bool at = l <= n1 && (l == 0 || lep);
-            const bool keep = mem || le;
-            x.P = keep ? x.P : at ? t : (l <= n1 ? pv : 0u);
-            PB = keep ? PB : at ? tb : (l <= n1 ? pbv : 0u);
-            x.pas_n = n1 + (mem ? 0u : 1u);
+            // entries of a bucket <= t's, then t's position once lane k is gone
+            const uint32_t c = (uint32_t)__popc(hmask(PT <= (tt | IDM)));
+            const uint32_t p = c - ((ev && k < c) ? 1u : 0u);
+            const bool gone = ev && l >= k, gone1 = ev && l >= k + 1;   // (l - 1 >= k)
+            const uint32_t F = l < p ? (gone ? nx : PT) : l == p ? tt : (gone1 ? PT : pv);
+            PT = mem ? PT : F;
+            n += (mem ? 0u : 1u) - (ev ? 1u : 0u);
             dirty |= mem ? 0u : 1u;
         });
+        x.pas_n = n;
+        x.P = PT == TSENT ? 0u : PT & IDM;
         x.fl |= dirty ? HF_PDIRTY : 0u;
     } else {
         for (uint32_t i = 0; i < mt; i++) {          // step by step, with ?uniform_range redraws

@@ -60,6 +60,7 @@ class LoopbackRanks:
     def clear_partition(self): self._all("clear_partition")
     def broadcast(self, root, msg_id): self._all("broadcast", root, msg_id)
     def set_bucket_table(self, buckets): self._all("set_bucket_table", buckets)
+    def set_phash_table(self, phash): self._all("set_phash_table", phash)
 
     # ---- collectives: one thread per rank; every rank's stats are the
     # all-reduced ones

@@ -389,3 +389,45 @@ def connected(adj):
 
 def asymmetric(adj):
     return [(i, j) for i in adj for j in adj[i] if j in adj and i not in adj[j]]
+
+
+def random_phash(n, seed):
+    """erlang:phash(NodeSpec, 2^32) - 1 per node as an in-BEAM export would
+    give it (psim_set_phash_table): random 32-bit values"""
+    return np.random.Generator(np.random.PCG64([seed, 0xFA5])).integers(0, 1 << 32, n, dtype=np.uint64).astype(
+        np.uint32)
+
+
+def with_phash(make, seed=7):
+    """`make` with a 32-bit phash table installed before the first round."""
+    def mk(cfg):
+        sim = make(cfg)
+        sim.set_phash_table(random_phash(cfg.n_nodes, seed))
+        return sim
+    return mk
+
+
+def pl_v1_large_view(make, n=180, seed=29, per_round=20, leave_from=40, leave_to=140, rounds=160):
+    """SCAMP v1 with a membership past 80 ids (OTP sets v1 linear hashing,
+    SURVEY App. A Q1): every node joins node 0, per_round a round, so node 0
+    keeps ~40 % of the N forward_subscriptions (sv1:212-252) and its view
+    grows past 80 (expansions at 81, 86, ...); from leave_from node 0
+    removes one member a round with leave/1 (sv1:102-122: sets:del_element)
+    until its view drops below 3 n (contractions).  The leave targets are
+    read from the handle's own view."""
+    sim = make(default_config(n_nodes=n, seed=seed, manager=1, strategy=1))
+    sched = [(0, np.array([0], np.uint32), np.array([W.NONE], np.uint32))]
+    for r, lo in enumerate(range(1, n, per_round), start=1):
+        ids = np.arange(lo, min(n, lo + per_round), dtype=np.uint32)
+        sched.append((r, ids, np.zeros(ids.size, np.uint32)))
+    trace = []
+
+    def hook(r):
+        v = sim.strategy_nodes(0, 1)[0]
+        trace.append((int(v["view_n"]), int(v["view_slots"])))
+        if leave_from <= r < leave_to and v["up"]:
+            row = [int(x) for x in v["view"][: v["view_n"]] if int(x) != 0]
+            if row:
+                sim.leave_node(np.array([0], np.uint32), np.array([row[len(row) // 2]], np.uint32))
+    st = sim.run_schedule(sched, rounds, extra=hook)
+    return sim, st, trace

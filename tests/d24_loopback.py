@@ -1,0 +1,108 @@
+"""Config D at its full size through the rank path:
+SCAMP v2 (c = 5) over 2^24 nodes, node-range sharded over 8 loopback ranks
+(psim_loopback_comm_id: the multi-rank code path of DESIGN.md section 7 --
+owner partition, count all-to-all, record exchange, stats all-reduce -- on
+one GPU, the ranks as threads) against the one-shard engine on the same GPU,
+bit for bit: every round's stats and record digest, and every node's
+strategy row (hashed in chunks) at the end; then D's own properties.
+Schedule: the doubling bootstrap to 2^24 (2^23 joiners in its last round),
+10 settle rounds, 1 % of the nodes crash (restart + rejoin a random live
+node 5 rounds later), a half/half partition for 8 rounds, 8 more rounds.
+
+Run directly (prints progress) or from tests/test_gpu_d24.py.  Exit 0 = equal."""
+import hashlib
+import os
+import sys
+import time
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+sys.path.insert(0, os.path.dirname(HERE))
+
+import numpy as np  # noqa: E402
+
+import _scenarios as S  # noqa: E402
+from _loopback import LoopbackRanks  # noqa: E402
+from partisan_amd import Simulator  # noqa: E402
+from partisan_amd import workloads as W  # noqa: E402
+from partisan_amd.sim import default_config  # noqa: E402
+
+N = int(os.environ.get("PSIM_D24_NODES", 1 << 24))
+RANKS = 8
+SEED = 31
+T0 = time.time()
+
+
+def log(*a):
+    print(f"[{time.time() - T0:7.1f}s]", *a, file=sys.stderr, flush=True)
+
+
+def run(sim, label):
+    boot = W.doubling_join(N, SEED)
+    b_end = boot[-1][0] + 1
+    crash_at, part_at, end = b_end + 10, b_end + 20, b_end + 36
+    rng = np.random.Generator(np.random.PCG64([SEED, 41]))
+    victims = np.sort(rng.choice(np.arange(1, N, dtype=np.uint32), size=N // 100, replace=False)).astype(np.uint32)
+    # each rejoins a uniformly drawn node that stayed up (one contact for all
+    # would overflow its 128-id in-view: PSIM_SVIEW_CAP)
+    alive = np.setdiff1d(np.arange(N, dtype=np.uint32), victims)
+    contacts = alive[rng.integers(0, alive.size, size=victims.size)].astype(np.uint32)
+
+    def hook(r):
+        if r == crash_at:
+            sim.crash(victims)
+        if r == crash_at + 5:
+            sim.join(victims, contacts)
+        if r == part_at:
+            sim.set_partition(W.half_partition(N))
+        if r == part_at + 8:
+            sim.clear_partition()
+        if r % 8 == 0:
+            log(label, "round", r)
+    st = sim.run_schedule(boot, end, extra=hook)
+    log(label, "done,", len(st), "rounds")
+    return st
+
+
+def row_hashes(sim, chunk=1 << 18):
+    out = []
+    for lo in range(0, N, chunk):
+        v = sim.strategy_nodes(lo, min(chunk, N - lo))
+        out.append(hashlib.sha1(v.tobytes()).hexdigest())
+    return out
+
+
+def main():
+    cfg = default_config(n_nodes=N, seed=SEED, manager=1, strategy=2, scamp_c=5, device=0)
+    one = Simulator(cfg)
+    st1 = run(one, "one shard")
+    v = one.strategy_nodes()
+    props = {"view_mean": float(v["view_n"][v["up"] == 1].mean()), "in_mean": float(v["in_n"][v["up"] == 1].mean()),
+             "up": int(v["up"].sum())}
+    del v
+    h1 = row_hashes(one)
+    one.close()
+    log("one shard rows hashed", props)
+    ranks = LoopbackRanks(default_config(n_nodes=N, seed=SEED, manager=1, strategy=2, scamp_c=5), RANKS)
+    st8 = run(ranks, f"{RANKS} loopback ranks")
+    S.compare_stats(st8, st1)
+    log("stats and digests equal over", len(st1), "rounds")
+    h8 = row_hashes(ranks)
+    ranks.close()
+    bad = [i for i, (a, b) in enumerate(zip(h1, h8)) if a != b]
+    assert not bad, f"strategy rows differ in chunks {bad[:8]}"
+    log("strategy rows equal (", len(h1), "chunks )")
+    # D's properties: every live node holds a partial view (SCAMP's
+    # log-sized views: (c + 1) ln N scale), nothing overflowed, messages
+    # conserved round to round
+    assert int(st1["overflow"].sum()) == 0
+    em = st1["emitted"].sum(axis=1)
+    got = st1["delivered"].sum(axis=1) + st1["dropped"] + st1["omitted"]
+    assert np.array_equal(em[:-1], got[1:]), "messages not conserved"
+    assert 1.0 < props["view_mean"] < 6 * np.log(N), props
+    print("D24 OK", {"nodes": N, "ranks": RANKS, "rounds": len(st1), **props,
+                     "msgs": int(st1["emitted"].sum()), "seconds": round(time.time() - T0, 1)}, flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -463,6 +463,21 @@ def test_snapshot_restore_continues_identically():
     S.compare_nodes(sim.nodes(), other.nodes())
 
 
+def test_failed_step_poisons_until_restore():
+    """a round that fails half-way leaves the handle answering PSIM_ESTATE
+    until psim_restore puts it back on a round boundary; a snapshot made
+    under one view-order table is refused under another (tests/_fail_run.py,
+    a child process: the failure hook is read once per process)"""
+    import os
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    env = dict(os.environ, PSIM_TEST_FAIL_ROUND="50")
+    r = subprocess.run([sys.executable, "-u", os.path.join(here, "_fail_run.py")], env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+
+
 def test_msg_slots_and_strict_gpu():
     """psim_get_msg_slots and cfg.strict on the GPU: six live roots overflow
     the four root slots -- counted identically to the oracle by default, a
