@@ -74,6 +74,8 @@ def parse():
     p.add_argument("--vshards", type=int, default=1,
                    help="diagnostic: G virtual shards of --nodes each on this one GPU (the sharded "
                         "partition / exchange / receive path with device copies instead of RCCL)")
+    p.add_argument("--strict", action="store_true",
+                   help="cfg.strict = 1: a fixed-table overflow fails the round (PSIM_ECAPACITY) and the run")
     p.add_argument("--rank-path", action="store_true",
                    help="diagnostic at --gpus 1: run the RCCL rank path with a one-rank communicator "
                         "(owner partition, ncclAllToAll of the counts, grouped self ncclSend/ncclRecv of "
@@ -495,6 +497,11 @@ def main_strategy(args):
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": tsrc,
                      "traffic_upper": trec.get("traffic_upper_per_launch") if trec else None,
+                     # the counted HBM bytes over the same time: B's ORSet rows are
+                     # re-read from L2 / MALL, so its algorithmic fraction is above
+                     # what the memory moved (state both)
+                     "traffic_frac": (traffic / (c_ms / max(1, c_n) / 1e3) / 1e9 / HBM_PEAK_GBS)
+                                     if traffic and c_ms > 0 else None,
                      "kernel": "k_consume_pl",
                      "alg_bytes_per_launch": alg / max(1, c_n), "avg_launch_ms": c_ms / max(1, c_n)},
         "kernel_ms_per_step": {k: v[0] / args.steps for k, v in kt.items() if v[1]},
@@ -592,6 +599,7 @@ def main():
     n = args.nodes * world * args.vshards
     cfg = default_config(n_nodes=n, seed=args.seed)
     cfg.n_shards = args.vshards
+    cfg.strict = 1 if args.strict else 0
     cfg.device = int(os.environ.get("PSIM_DEVICE", os.environ.get("LOCAL_RANK", "0")))
     comm = shared_comm()
     if world > 1:
@@ -752,7 +760,7 @@ def main():
                            "ok": bool(np.array_equal(em[:-1], got[1:]))}
     out["device_mem_used_gb"] = device_mem_used_gb()
     out["overflow_run"] = {"rounds": sim.round, **{k: int(v) for k, v in zip(OVF_KINDS, ovf_run)},
-                           "total": int(ovf_run.sum())}
+                           "total": int(ovf_run.sum()), "strict": bool(args.strict)}
     if cpu is not None:
         out["cpu_baseline"] = cpu
     if rank == 0:

@@ -67,7 +67,7 @@
 extern "C" {
 #endif
 
-#define PSIM_ABI_VERSION 11
+#define PSIM_ABI_VERSION 12
 
 /* error codes */
 #define PSIM_OK 0
@@ -161,7 +161,7 @@ enum psim_pl_msg_type {
  * its 'EXIT' (xbot:608-653) is handled at the start of the next round; sends
  * to it draw the dispatch value and fail.  At most one per member. */
 #define PSIM_CONN_CLOSING 0x40000000u
-#define PSIM_PT_OUT_CAP 64
+#define PSIM_PT_OUT_CAP 128
 #define PSIM_EXCHANGE_CAP 8
 /* Plumtree roots a node keeps per-root eager/lazy sets for at once
  * (eager_sets / lazy_sets orddicts, plumtree:76-84, :599-631): a root

@@ -8,11 +8,11 @@ import ctypes as C
 
 import numpy as np
 
-PSIM_ABI_VERSION = 11
+PSIM_ABI_VERSION = 12
 PSIM_MAP_BIT = 0x80000000
 PSIM_NONE = 0xFFFFFFFF
 ACTIVE_CAP, PASSIVE_CAP, IDMAP_CAP = 8, 32, 64
-PT_MEMBERS_CAP, PT_SET_POOL, PT_OUT_CAP, EXCHANGE_CAP = 8, 64, 64, 8
+PT_MEMBERS_CAP, PT_SET_POOL, PT_OUT_CAP, EXCHANGE_CAP = 8, 64, 128, 8
 PT_ROOTS, MSG_SLOTS = 4, 64
 CONN_CAP, CONN_DOWN, CONN_CLOSING = 8, 0x80000000, 0x40000000
 OVF_NKINDS = 5

@@ -639,6 +639,48 @@ DEV void slot_del(Wv& w, uint32_t& V, uint32_t which, uint32_t k, uint32_t e) {
     rt_set_count(w, which, k, n - 1);
 }
 
+DEV uint32_t take_ext_row(Wv& w, uint32_t* top, uint32_t rows, int kind);
+
+// The outstanding table's tail (entries OUT_HEAD.. of a table past one
+// register, psim_device.h): lane l holds entry OUT_HEAD + l, in place in the
+// extension row (a tail implies one: pt_add_out takes it before the first
+// tail entry)
+DEV uint64_t* out_tail(const Wv& w) {
+    return kargs().outx + (size_t)(w.ox - 1) * OUT_EXT + OUT_TAIL_AT + lane_id();
+}
+DEV uint64_t load_out_tail(const Wv& w) {
+    return lane_id() < w.out_n - OUT_HEAD ? *out_tail(w) : 0ull;
+}
+
+// neighbors_down/2's outstanding filter (pt:414-416): the entries to peer e
+// leave, the order kept across the register and the tail
+DEV void out_drop_peer(Wv& w, uint32_t e) {
+    const uint32_t l = lane_id();
+    const uint64_t keep = ballot(l < w.out_n && (uint32_t)(w.OUT >> 32) != e);
+    if (w.out_n <= OUT_HEAD) {
+        if (popc(keep) != w.out_n) {
+            w.OUT = compact64(w, w.OUT, keep);
+            w.out_n = popc(keep);
+        }
+        return;
+    }
+    const uint32_t nt = w.out_n - OUT_HEAD;
+    uint64_t T = load_out_tail(w);
+    const uint64_t kt = ballot(l < nt && (uint32_t)(T >> 32) != e);
+    const uint32_t k1 = popc(keep), k2 = popc(kt);
+    if (k1 + k2 == w.out_n) return;
+    const uint64_t H = compact64(w, w.OUT, keep);
+    T = compact64(w, T, kt);
+    // the register: its k1 kept entries, then the tail's first 64 - k1
+    const uint64_t up = shfl64(T, (int)((l - k1) & 63));
+    w.OUT = l < k1 ? H : (l - k1 < k2 ? up : 0ull);
+    const uint32_t sh = OUT_HEAD - k1;
+    const uint64_t rest = shfl64(T, (int)((l + sh) & 63));
+    T = l + sh < k2 ? rest : 0ull;
+    w.out_n = k1 + k2;
+    if (w.out_n > OUT_HEAD) *out_tail(w) = T;
+}
+
 // notify/1 (hv:1598-1599) -> plumtree update/1 -> handle_cast({update, ..})
 // (pt:314-336), reset_peers/4 (:652-659), neighbors_down/2 (:404-423)
 DEV void apply_notify(Wv& w, uint32_t SNAP, uint32_t sn) {
@@ -678,11 +720,7 @@ DEV void apply_notify(Wv& w, uint32_t SNAP, uint32_t sn) {
             slot_del(w, w.EAG, RT_EN, k, e);
             slot_del(w, w.LAZ, RT_LN, k, e);
         }
-        uint64_t keep = ballot(l < w.out_n && (uint32_t)(w.OUT >> 32) != e);
-        if (popc(keep) != w.out_n) {
-            w.OUT = compact64(w, w.OUT, keep);
-            w.out_n = popc(keep);
-        }
+        out_drop_peer(w, e);
     }
 }
 
@@ -839,14 +877,59 @@ DEV void pt_add_out(Wv& w, uint32_t peer, uint32_t msg, uint32_t rnd) {   // pt:
     uint64_t key = ((uint64_t)peer << 32) | (msg << 16) | (rnd & 0xFFFFu);
     w.pt_dirty = true;
     if (ballot(l < w.out_n && w.OUT == key)) return;
+    if (w.out_n < OUT_HEAD) {
+        vins64(w.OUT, w.out_n, popc(ballot(l < w.out_n && w.OUT < key)), key);
+        return;
+    }
+    // a full register: the sorted order continues in the tail
+    const uint32_t nt = w.out_n - OUT_HEAD;
+    uint64_t T = nt ? load_out_tail(w) : 0ull;
+    if (ballot(l < nt && T == key)) return;
     if (w.out_n >= PSIM_PT_OUT_CAP) { ovf(w, PSIM_OVF_PT_OUT); return; }
-    vins64(w.OUT, w.out_n, popc(ballot(l < w.out_n && w.OUT < key)), key);
+    if (!w.ox) {
+        w.ox = take_ext_row(w, kargs().outx_top, kargs().outx_rows, PSIM_OVF_PT_OUT);
+        if (!w.ox) return;
+    }
+    uint32_t pos = popc(ballot(w.OUT < key));
+    uint64_t into = key;
+    if (pos < OUT_HEAD) {                 // the register's last entry moves to the tail's front
+        into = rl64(w.OUT, OUT_HEAD - 1);
+        uint32_t n = OUT_HEAD - 1;
+        vins64(w.OUT, n, pos, key);
+        pos = 0;
+    } else {
+        pos = popc(ballot(l < nt && T < key));
+    }
+    uint32_t n = nt;
+    vins64(T, n, pos, into);
+    *out_tail(w) = T;
+    w.out_n++;
 }
 
 DEV void pt_ack_out(Wv& w, uint32_t peer, uint32_t msg, uint32_t rnd) {   // pt:562-567
+    const uint32_t l = lane_id();
     uint64_t key = ((uint64_t)peer << 32) | (msg << 16) | (rnd & 0xFFFFu);
-    int k = ffs64(ballot(lane_id() < w.out_n && w.OUT == key));
-    if (k >= 0) { vdel64(w.OUT, w.out_n, (uint32_t)k); w.pt_dirty = true; }
+    int k = ffs64(ballot(l < w.out_n && w.OUT == key));
+    if (w.out_n <= OUT_HEAD) {
+        if (k >= 0) { vdel64(w.OUT, w.out_n, (uint32_t)k); w.pt_dirty = true; }
+        return;
+    }
+    uint32_t nt = w.out_n - OUT_HEAD;
+    uint64_t T = load_out_tail(w);
+    if (k >= 0) {                         // the tail's front moves up into the register
+        const uint64_t t0 = rl64(T, 0);
+        uint32_t n = OUT_HEAD;
+        vdel64(w.OUT, n, (uint32_t)k);
+        w.OUT = l == OUT_HEAD - 1 ? t0 : w.OUT;
+        k = 0;
+    } else {
+        k = ffs64(ballot(l < nt && T == key));
+        if (k < 0) return;
+    }
+    vdel64(T, nt, (uint32_t)k);
+    *out_tail(w) = T;
+    w.out_n--;
+    w.pt_dirty = true;
 }
 
 // eager_push/7 + schedule_lazy_push/6 (pt:428-441) over all_peers/3: the
@@ -1508,9 +1591,13 @@ DEV uint32_t take_ext_row(Wv& w, uint32_t* top, uint32_t rows, int kind) {
     if (r >= rows) { ovf(w, kind); return 0; }
     return r + 1;
 }
-// the outstanding table outgrew its own row
+// the outstanding table outgrew its own row (the pool exhausted: the
+// overflow is counted and the entries past the row are dropped)
 DEV void out_ext(Wv& w) {
-    if (w.pt_dirty && w.out_n > OUT_IN && !w.ox) w.ox = take_ext_row(w, kargs().outx_top, kargs().outx_rows, PSIM_OVF_PT_OUT);
+    if (w.pt_dirty && w.out_n > OUT_IN && !w.ox) {
+        w.ox = take_ext_row(w, kargs().outx_top, kargs().outx_rows, PSIM_OVF_PT_OUT);
+        if (!w.ox) w.out_n = OUT_IN;
+    }
 }
 
 DEV uint8_t flag_byte(const Wv& w) {
@@ -1878,6 +1965,22 @@ DEV void begin_pt(Wv& w, const PtIn& x, const PtX& y) {
     w.seq = x.oc; w.flushed = x.oc;                  // after the HyParView phase's records
 }
 
+// the lazy tick's IHAVEs for the outstanding table's tail (entries
+// OUT_HEAD.., after the register's: the table's order)
+DEV void lazy_tick_tail(Wv& w) {
+    const uint32_t l = lane_id();
+    const uint64_t T = load_out_tail(w);
+    const uint32_t peer = (uint32_t)(T >> 32), msg = ((uint32_t)T >> 16) & 0xFFFFu;
+    const uint64_t ok = pt_conn_mask(w, ballot(l < w.out_n - OUT_HEAD), peer);
+    const uint32_t sk = msg % PSIM_MSG_SLOTS;
+    const bool live = w.slots[sk] == msg;
+    const uint32_t root = live ? w.slots[PSIM_MSG_SLOTS + sk] : NONE;
+    const uint32_t dead = popc(ok & ballot(!live));
+    st_add(w, ST_OVF, dead);
+    st_add(w, ST_OVF_BY + PSIM_OVF_PT, dead);
+    emit_batch<true>(w, ok, PSIM_MSG_PT_IHAVE, peer & ~PSIM_MAP_BIT, msg, (uint32_t)T & 0xFFFFu, root);
+}
+
 DEV void body_pt(Wv& w, const PtIn& x) {
     KArgs& a = kargs();
     const uint32_t r = a.round, n = x.n;
@@ -1918,6 +2021,7 @@ DEV void body_pt(Wv& w, const PtIn& x) {
         st_add(w, ST_OVF, dead);
         st_add(w, ST_OVF_BY + PSIM_OVF_PT, dead);
         emit_batch<true>(w, ok, PSIM_MSG_PT_IHAVE, peer & ~PSIM_MAP_BIT, msg, (uint32_t)w.OUT & 0xFFFFu, root);
+        if (w.out_n > OUT_HEAD) lazy_tick_tail(w);
         STAMP(w, 22);
     }
 }
@@ -2525,6 +2629,9 @@ DEV bool col_has(const LdsCol& V, uint32_t n, uint32_t x) {
     for (int i = 0; i < PTL_SET; i++) r |= (uint32_t)i < n && V[i] == x;
     return r;
 }
+#ifndef PSIM_PTL_PF           // k_ptl's set / table loops read one entry ahead (0: A/B)
+#define PSIM_PTL_PF 1
+#endif
 // ordsets:del_element/2
 DEV void col_del(const LdsCol& V, uint32_t& n, uint32_t x) {
     uint32_t at = n;
@@ -2566,6 +2673,10 @@ struct PtLane {
 // (the members' up-and-partition pairs are read once per node, all eight
 // loads in flight together: read per send they were one dependent memory
 // latency per send; no kernel of the phase changes them)
+// (loading only the members a send of this node may go to -- the senders
+// its answers go to, its lazy tick's peers -- measured slower at 2^20 and
+// at 2^26: the loads then wait for the records and the table, and the
+// random lines come from the MALL, profiles/r05/ab_log.txt r5k / r5l)
 DEV uint32_t ptl_conn_mask(KArgs& a, const PtLane& n) {
     uint16_t up[PSIM_ACTIVE_CAP];                     // (k_node_prep's up-and-partition pairs)
 #pragma unroll
@@ -2579,6 +2690,7 @@ DEV uint32_t ptl_conn_mask(KArgs& a, const PtLane& n) {
         m |= ((uint32_t)j < n.act_n && n.A[j] < a.n_nodes && n.A[j] != n.id && up[j] == n.me_part) ? 1u << j : 0u;
     return m;
 }
+
 DEV bool ptl_conn(KArgs& a, const PtLane& n, uint32_t ident) {
     const uint32_t p = ident & ~PSIM_MAP_BIT;
     bool c = false;
@@ -2831,8 +2943,18 @@ __global__ void PTL_BOUNDS k_ptl(RoundArgs) {
                     if (msg == a.tracked_msg) { trk_round = a.round; trk_hop = rnd + 1; }
                     ptl_update(a, n, li, com_n, from, root, true);
                     // eager_push/7 + schedule_lazy_push/6 over slot 0's sets
+                    // (each entry's LDS read issued an iteration ahead of its
+                    // use: the loop waited one LDS latency per member)
+#if PSIM_PTL_PF
+                    uint32_t e_nx = n.EG[0];
+#endif
                     for (uint32_t i = 0; i < n.ne; i++) {
+#if PSIM_PTL_PF
+                        const uint32_t e = e_nx;
+                        e_nx = n.EG[(i + 1) % PTL_SET];
+#else
                         const uint32_t e = n.EG[i];
+#endif
                         if (e == from) continue;
                         if (ptl_conn(a, n, e)) {
                             dig += relay_emit(a, D.w + seq, e & ~PSIM_MAP_BIT, id, PSIM_MSG_PT_BROADCAST, seq, msg, rnd + 1,
@@ -2843,8 +2965,16 @@ __global__ void PTL_BOUNDS k_ptl(RoundArgs) {
                             v[T_FAIL]++;
                         }
                     }
+#if PSIM_PTL_PF
+                    uint32_t z_nx = n.LZ[0];
+#endif
                     for (uint32_t i = 0; i < n.nl; i++) {
+#if PSIM_PTL_PF
+                        const uint32_t e = z_nx;
+                        z_nx = n.LZ[(i + 1) % PTL_SET];
+#else
                         const uint32_t e = n.LZ[i];
+#endif
                         if (e != from) ptl_add_out(n, ((uint64_t)e << 32) | (msg << 16) | ((rnd + 1) & 0xFFFFu));
                     }
                 } else {
@@ -2873,8 +3003,16 @@ __global__ void PTL_BOUNDS k_ptl(RoundArgs) {
             }
         }
         if (((D.z >> 28) & DESC_LAZY) && n.on > 0) {   // the lazy tick (pt:341-345, :443-453)
+#if PSIM_PTL_PF
+            uint64_t o_nx = out_at(n, 0);
+#endif
             for (uint32_t i = 0; i < n.on; i++) {
+#if PSIM_PTL_PF
+                const uint64_t o = o_nx;
+                o_nx = out_at(n, (i + 1) % PTL_CAP);
+#else
                 const uint64_t o = out_at(n, i);
+#endif
                 const uint32_t peer = (uint32_t)(o >> 32);
                 if (!ptl_conn(a, n, peer)) { v[T_FAIL]++; continue; }
                 const uint32_t msg = (uint32_t)(o >> 16) & 0xFFFFu, sk = msg % PSIM_MSG_SLOTS;

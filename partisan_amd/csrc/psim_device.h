@@ -69,9 +69,16 @@ constexpr uint32_t IDMAP_IN = 16;
 constexpr uint32_t IDMAP_EXT = PSIM_IDMAP_CAP - IDMAP_IN;
 constexpr uint32_t HW_SENT_EXT = 13, HW_RECV_EXT = 14;   // header words (Hdr pad1[1], pad1[2])
 // Plumtree outstanding table (PSIM_PT_OUT_CAP entries): likewise OUT_IN in
-// the node's row, the rest in an extension row of another pool
+// the node's row, the rest in an extension row of another pool.  A wave holds
+// the first OUT_HEAD entries in one 64-lane register; the tail (entries
+// OUT_HEAD.., a node with more than 64 lazy pushes outstanding -- rare, the
+// ramp of a 2^26-node broadcast) is read and written in place in the
+// extension row, from offset OUT_TAIL_AT
 constexpr uint32_t OUT_IN = 16;
 constexpr uint32_t OUT_EXT = PSIM_PT_OUT_CAP - OUT_IN;
+constexpr uint32_t OUT_HEAD = 64;
+constexpr uint32_t OUT_TAIL_AT = OUT_HEAD - OUT_IN;
+static_assert(PSIM_PT_OUT_CAP <= 2 * OUT_HEAD, "the tail is one 64-lane register");
 constexpr uint32_t HW_OUT_EXT = 15;
 // the connection table's counts: header word 11, bytes 0 (entries), 1
 // (PSIM_CONN_DOWN entries) and 3 (PSIM_CONN_CLOSING entries); byte 2 is the

@@ -707,10 +707,11 @@ __device__ __forceinline__ bool due(uint32_t period, uint32_t r, uint32_t start)
 // scan, origin, outstanding lazy pushes).  Also counts live nodes and
 // messages addressed to dead ones.
 __global__ void __launch_bounds__(256) k_node_prep(RoundArgs a, const unsigned long long* bmask, uint64_t* packed,
-                                                   uint64_t* part, uint32_t* ocnt, unsigned long long* btot) {
+                                                   uint64_t* part, uint32_t* ocnt, unsigned long long* btot,
+                                                   uint32_t per, uint64_t* tiles) {
     if (*a.ctl) return;                               // an aborted batch (run_batch)
-    __shared__ unsigned long long s_up, s_drop, s_b;
-    if (threadIdx.x == 0) { s_up = 0; s_drop = 0; s_b = 0; }
+    __shared__ unsigned long long s_up, s_drop, s_b, s_w;
+    if (threadIdx.x == 0) { s_up = 0; s_drop = 0; s_b = 0; s_w = 0; }
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         a.ktime[0] = ~0ull; a.ktime[1] = 0; *a.n_slow = 0; *a.n_pt = 0;
         if (a.n_shuf) *a.n_shuf = 0;
@@ -721,11 +722,14 @@ __global__ void __launch_bounds__(256) k_node_prep(RoundArgs a, const unsigned l
     __syncthreads();
     // the peers' up-and-partition pairs for k_ptl's connection tests (every
     // global id: the flag and partition arrays are replicated)
-    if (a.upart)
+    if (a.upart && a.upart_dirty)
         for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g < a.n_nodes; g += gridDim.x * blockDim.x)
             a.upart[g] = (a.flags[g] & F_UP) ? (uint16_t)a.part[g] : UPART_DOWN;
-    unsigned long long up = 0, drop = 0, bs = 0;        // this thread's sums (wave-summed below)
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < a.n_local; i += gridDim.x * blockDim.x) {
+    unsigned long long up = 0, drop = 0, bs = 0, ws = 0;   // this thread's sums (wave-summed below)
+    // block b takes the nodes [b * per, (b + 1) * per), blockDim at a time
+    // (coalesced), so that its sums are a contiguous tile of the scan below
+    const uint32_t i0 = blockIdx.x * per, i1 = min(a.n_local, i0 + per);
+    for (uint32_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
         uint32_t id = a.lo + i;
         uint8_t f = a.flags[id];
         uint64_t b = 0;
@@ -856,18 +860,28 @@ __global__ void __launch_bounds__(256) k_node_prep(RoundArgs a, const unsigned l
         packed[i] = (b << 32) | w;
         ocnt[i] = 0;               // consume writes the count of every node it runs
         bs += b;
+        ws += w;
     }
     for (int o = 32; o > 0; o >>= 1) {
         up += __shfl_xor(up, o);
         drop += __shfl_xor(drop, o);
         bs += __shfl_xor(bs, o);
+        ws += __shfl_xor(ws, o);
     }
     if ((threadIdx.x & 63) == 0) {
         if (up) atomicAdd(&s_up, up);
         if (drop) atomicAdd(&s_drop, drop);
         if (bs) atomicAdd(&s_b, bs);
+        if (ws) atomicAdd(&s_w, ws);
     }
     __syncthreads();
+    // the tile's sum of the packed words (wrapping like them past 2^32
+    // slots) for the scan; the extra tile after the last is 0 (its prefix
+    // becomes the total)
+    if (threadIdx.x == 0) {
+        tiles[blockIdx.x] = (s_b << 32) + s_w;
+        if (blockIdx.x == gridDim.x - 1) tiles[gridDim.x] = 0;
+    }
     // the exact total (the packed scan's high word wraps past 2^32 slots):
     // the block's sum in its own word, summed by k_desc's last block (one
     // same-address atomic per block serialised 4096 adds at L2 every round)
@@ -925,20 +939,39 @@ __device__ unsigned long long btot_sum(const unsigned long long* btot, uint32_t 
     return s_tot;
 }
 
+template <typename T>
+__device__ T block_excl(T v, T* total);   // (the exclusive-scan section below)
+
 // Per node, from the scan of the packed (bound, work) words: the outbox
 // base, and for a node with work its descriptor at its active-list position
 // -- every address k_consume needs first and which of the node's timers are
 // due (hv:542-607, pt:341-345).  Entry n: the outbox total and the count.
-__global__ void k_desc(const uint64_t* __restrict__ packed, const uint64_t* __restrict__ pscan,
-                       const uint32_t* __restrict__ in_beg, const unsigned long long* __restrict__ cb,
-                       const uint32_t* __restrict__ start, RoundArgs a, uint4* __restrict__ desc,
-                       uint64_t* __restrict__ obase, uint32_t* nact, const unsigned long long* btot,
-                       uint32_t nbt, uint64_t* hout, uint64_t cap, uint32_t* ctl) {
-    const uint32_t li = blockIdx.x * blockDim.x + threadIdx.x;
+// Block b walks k_node_prep's range of block b again, BLK nodes a pass: a
+// block scan of their packed words on top of the tile's prefix (tiles: the
+// exclusive scan of k_node_prep's tile sums, k_scan_sums) -- one launch in
+// place of a tile-sum and an apply pass over the whole array.
+__global__ void __launch_bounds__(BLK) k_desc(const uint64_t* __restrict__ packed, const uint64_t* __restrict__ tiles,
+                                             uint32_t per, const uint32_t* __restrict__ in_beg,
+                                             const unsigned long long* __restrict__ cb,
+                                             const uint32_t* __restrict__ start, RoundArgs a, uint4* __restrict__ desc,
+                                             uint64_t* __restrict__ obase, uint32_t* nact,
+                                             const unsigned long long* btot, uint64_t* hout, uint64_t cap,
+                                             uint32_t* ctl) {
     if (*ctl) return;                                 // (uniform)
-    const unsigned long long tot = blockIdx.x == gridDim.x - 1 ? btot_sum(btot, nbt) : 0ull;   // (uniform)
-    if (li > a.n_local) return;
-    desc_entry(a, li, pscan[li], packed[li], in_beg, cb, start, desc, obase, nact, tot, hout, cap, ctl);
+    const bool last = blockIdx.x == gridDim.x - 1;
+    const unsigned long long tot = last ? btot_sum(btot, gridDim.x) : 0ull;   // (uniform)
+    const uint32_t i0 = blockIdx.x * per, i1 = min(a.n_local, i0 + per);
+    uint64_t carry = tiles[blockIdx.x];
+    for (uint32_t k = i0; k < i1; k += BLK) {         // (uniform)
+        const uint32_t li = k + threadIdx.x;
+        const uint64_t pk = li < i1 ? packed[li] : 0ull;
+        uint64_t pass;
+        const uint64_t e = block_excl(pk, &pass);
+        if (li < i1) desc_entry(a, li, carry + e, pk, in_beg, cb, start, desc, obase, nact, 0ull, hout, cap, ctl);
+        carry += pass;
+    }
+    if (last && threadIdx.x == 0)                     // entry n: the totals
+        desc_entry(a, a.n_local, tiles[gridDim.x], 0ull, in_beg, cb, start, desc, obase, nact, tot, hout, cap, ctl);
 }
 
 // --------------------------------------------------------- overlay stats --
@@ -1228,6 +1261,7 @@ struct Shard {
     DBuf<uint8_t> faulted;              // omission faults: generally omitting nodes (global id)
     DBuf<uint64_t> omit;                // ... sorted send-omission pairs, then receive-omission pairs
     std::vector<uint64_t> soff, scnt;   // per destination shard (G + 1 offsets)
+    uint32_t pper = BLK;               // k_node_prep / k_desc: nodes per block (a multiple of BLK)
     uint32_t pgrid = 0, cgrid = 0, rgrid = 0, tgrid = 0, sgrid = 0, lgrid = 0, qgrid = 0;   // stats rows: prepare,
                                    // consume, relay, plumtree, shuffle-start, lite, Plumtree-lane blocks
     // pinned host words: NST stats and the consume span (stat_out), then the
@@ -1248,6 +1282,7 @@ struct Shard {
     hipEvent_t fork_ev = nullptr, join_ev[2] = {nullptr, nullptr};
     bool ev_live = false;
     bool reserved = false;              // first-round capacity reservation done
+    bool upart_valid = false;           // upart holds this state's pairs (RoundArgs::upart_dirty)
     uint64_t rcap = 0;                  // records the route's buffers hold (G == 1: checked on the device)
     // batches of rounds without host waits (run_batch): the abort word
     // (code, round) in device memory; while a batch is enqueued, k_desc
@@ -1444,17 +1479,21 @@ __global__ void __launch_bounds__(BLK) k_scan_tiles(const T* __restrict__ in, ui
     if (threadIdx.x == 0) sums[blockIdx.x] = tot;
 }
 
-// one block: exclusive scan of the nt tile totals in place, in chunks of BLK
+// one block: exclusive scan of the nt tile totals in place -- each thread a
+// contiguous run of ceil(nt / BLK) of them, one block scan of the run sums
+// (a block scan per BLK chunk took 12.7 us for 4097 totals: 17 serial
+// barrier pairs)
 template <typename T>
 __global__ void __launch_bounds__(BLK) k_scan_sums(T* sums, uint32_t nt) {
-    T carry = 0;
-    for (uint32_t c = 0; c < nt; c += BLK) {
-        const uint32_t i = c + threadIdx.x;
-        const T v = i < nt ? sums[i] : T(0);
-        T tot;
-        const T e = block_excl(v, &tot);
-        if (i < nt) sums[i] = carry + e;
-        carry += tot;
+    const uint32_t per = (nt + BLK - 1) / BLK, i0 = threadIdx.x * per, i1 = min(nt, i0 + per);
+    T v = 0;
+    for (uint32_t i = i0; i < i1; i++) v += sums[i];
+    T tot;
+    T run = block_excl(v, &tot);
+    for (uint32_t i = i0; i < i1; i++) {
+        const T x = sums[i];
+        sums[i] = run;
+        run += x;
     }
 }
 
@@ -1496,13 +1535,14 @@ int scan_excl(Shard* s, const T* in, T* out, uint32_t n) {
     return PSIM_OK;
 }
 
-// prepare's scan + descriptors: the scan, then k_desc
+// prepare's scan + descriptors: k_node_prep left its blocks' tile sums in
+// pscan[0..pgrid] (pgrid + 1: the extra one is 0); one block scans them,
+// then k_desc walks the ranges again
 int scan_desc(Shard* s, const RoundArgs& a) {
-    const uint32_t n1 = a.n_local + 1;
-    TRY(scan_excl(s, s->bound.p, s->pscan.p, n1));
-    k_desc<<<grid_for(n1), BLK, 0, s->stream>>>(s->bound.p, s->pscan.p, s->in_beg.p, s->cb.p, s->start.p, a,
-                                                 s->desc.p, s->obase.p, s->d_nact.p, s->btot.p, s->pgrid, s->pin_dev,
-                                                 s->desc_cap, s->ctl.p);
+    k_scan_sums<uint64_t><<<1, BLK, 0, s->stream>>>(s->pscan.p, s->pgrid + 1);
+    k_desc<<<s->pgrid, BLK, 0, s->stream>>>(s->bound.p, s->pscan.p, s->pper, s->in_beg.p, s->cb.p, s->start.p, a,
+                                             s->desc.p, s->obase.p, s->d_nact.p, s->btot.p, s->pin_dev, s->desc_cap,
+                                             s->ctl.p);
     HIP_TRY(hipGetLastError());
     return PSIM_OK;
 }
@@ -1563,6 +1603,11 @@ int phase_events_prepare(psim_handle* h, Shard* s, const RoundCtl& ctl, RoundArg
     }
     a = make_args(h, s);
     a.crash_round = ctl.crashes;
+    // the up-and-partition pairs change only with crash, start and partition
+    // events (k_crash, k_join, the partition copy): rebuilt only then
+    a.upart_dirty = !s->upart_valid ||
+                    (events && (ctl.crashes || !h->pend_join.empty() || h->pend_part_set || h->pend_part_clear));
+    s->upart_valid = true;
     if (events) {
         KTimer t(h, s, KT_EVENTS);
         if (ctl.crashes) {
@@ -1603,7 +1648,12 @@ int phase_events_prepare(psim_handle* h, Shard* s, const RoundCtl& ctl, RoundArg
         // grid-stride; 4096 blocks (16 waves per CU) keep the crash rounds'
         // dependent loads (active row -> members' flag bytes) in flight --
         // 512 blocks left 2 waves per SIMD and took 6.8 ms at 2^26 nodes
-        s->pgrid = std::min<uint32_t>(grid_for(n), 4096);
+        // (contiguous ranges of pper nodes, a multiple of BLK: k_desc's tiles)
+        {
+            const uint32_t g = std::min<uint32_t>(grid_for(n), 4096);
+            s->pper = BLK * (uint32_t)(((uint64_t)n + (uint64_t)g * BLK - 1) / ((uint64_t)g * BLK));
+            s->pgrid = std::max<uint32_t>(1, (uint32_t)(((uint64_t)n + s->pper - 1) / s->pper));
+        }
         s->cgrid = std::min<uint32_t>(grid_for(n), h->consume_blocks);
         // one lane per possible working node (up to RELAY_MAX_BLOCKS, then grid-stride):
         // the relays are chains of dependent random loads, so latency wants lanes
@@ -1620,9 +1670,9 @@ int phase_events_prepare(psim_handle* h, Shard* s, const RoundCtl& ctl, RoundArg
         TRY(s->stat_part.ensure((size_t)(s->pgrid + s->cgrid + s->rgrid + s->tgrid + s->sgrid + s->lgrid + s->qgrid) *
                                 NST));
         k_node_prep<<<s->pgrid, BLK, 0, s->stream>>>(a, s->bmask.p, s->bound.p, s->stat_part.p, s->ocnt.p,
-                                                     s->btot.p);
-        // bound[n] = 0: pscan[n] = (outbox total << 32) | active count;
-        // obase[n] = the exact total (btot, summed by k_node_prep)
+                                                     s->btot.p, s->pper, s->pscan.p);
+        // pscan[pgrid] becomes (outbox total << 32) | active count;
+        // obase[n] = the exact total (btot, summed by k_desc's last block)
         TRY(scan_desc(s, a));
         if (batched) goto args;
         TRY(stream_wait(s));                          // (k_desc stored the total in pin)
@@ -2333,7 +2383,7 @@ int shard_alloc(psim_handle* h, Shard* s) {
     if (h->cfg.manager != PSIM_MANAGER_PLUGGABLE) rc |= s->outx.alloc(std::max<size_t>(1024, n / 8) * OUT_EXT);
     rc |= s->outx_top.alloc(1);
     rc |= s->ocnt.alloc(n); rc |= s->cb.alloc(n + 1);
-    rc |= s->in_beg.alloc(n + 1); rc |= s->bound.alloc(n + 1); rc |= s->pscan.alloc(n + 1); rc |= s->obase.alloc(n + 1);
+    rc |= s->in_beg.alloc(n + 1); rc |= s->bound.alloc(n + 1); rc |= s->pscan.alloc(4097); rc |= s->obase.alloc(n + 1);
     rc |= s->bmask.alloc(n); rc |= s->btot.alloc(4096);
     rc |= s->desc.alloc(n); rc |= s->d_nact.alloc(1);
     rc |= s->desc_slow.alloc(n); rc |= s->n_slow.alloc(1);
@@ -3234,6 +3284,7 @@ int psim_restore(psim_handle* h, const void* buf, size_t size) {
         if (s->ctl.p) HIP_TRY(hipMemset(s->ctl.p, 0, s->ctl.n * sizeof(uint32_t)));
         if (s->n_stop.p) HIP_TRY(hipMemset(s->n_stop.p, 0, s->n_stop.n * sizeof(uint32_t)));
         s->reserved = false;
+        s->upart_valid = false;
     }
     h->round = hd.round; h->tracked_msg = hd.tracked_msg;
     memcpy(h->slot_tab, hd.slot_tab, sizeof h->slot_tab);

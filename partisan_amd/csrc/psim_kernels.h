@@ -14,6 +14,7 @@ struct RoundArgs {
     uint32_t xbot, xbot_period;   // X-BOT manager (PSIM_MANAGER_XBOT) and its xbot_execution period
     // per-round scalars
     uint32_t crash_round, tracked_msg;
+    uint32_t upart_dirty;       // this round's events changed F_UP or a partition: k_node_prep rebuilds upart
     // node state: flags/part are replicated and indexed by global id;
     // every other row is local (index = id - lo)
     uint8_t* flags;

@@ -195,8 +195,10 @@ DEV uint32_t select_random(Hn& x, const Hw& w, uint32_t V, uint32_t n, uint32_t 
     const uint32_t cnt = (uint32_t)__popc(M);
     if (cnt == 0) return PSIM_NONE;
     const uint32_t k = uniform_n(x, w, cnt) - 1;
-    for (uint32_t j = 0; j < k; j++) M &= M - 1;      // the k-th eligible lane
-    return hget(V, (uint32_t)__ffs(M) - 1);
+    // the k-th eligible lane: the one with k eligible lanes below it (no
+    // loop of up to k steps, whose count differs between the halves)
+    const bool hit = ((M >> l) & 1u) && (uint32_t)__popc(M & ((1u << l) - 1u)) == k;
+    return hget(V, (uint32_t)__ffs(hmask(hit)) - 1);
 }
 
 // lists:sublist(shuffle(to_list(View)), K) (hv:1359-1361, :1586-1587): one
@@ -389,8 +391,14 @@ DEV void merge_exchange(Hn& x, Hw& w, uint32_t EX, uint32_t nex) {
         const uint32_t TG = l < mt ? (TB << 27) | T : TSENT;
         uint32_t K = KI;                             // the next eviction's index in the half's lane 0
         uint32_t n = x.pas_n, dirty = 0;
+        // every candidate's tag fetched up front: one LDS wait, not one a
+        // step (the half's step chain waited on its swizzle each step;
+        // phase 0.505 -> 0.502 ms, profiles/r05/ab_log.txt)
+        uint32_t TT8[PSIM_EXCHANGE_CAP];
+        unroll<PSIM_EXCHANGE_CAP>([&](auto I) { TT8[I] = hgetc<I>(TG); });
+        __builtin_amdgcn_sched_barrier(0);
         unroll<PSIM_EXCHANGE_CAP>([&](auto I) {
-            const uint32_t tt = hgetc<I>(TG);
+            const uint32_t tt = TT8[I];
             const bool mem = hany(PT == tt);
             const bool ev = !mem && n >= maxp;       // select_random(Passive, [Myself]) + remove
             const uint32_t k = hget_c0(K);

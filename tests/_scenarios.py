@@ -160,6 +160,32 @@ def e_miniature(make, n=1 << 14, seed=101, rounds=90):
     return sim, st
 
 
+def out_tail(make, n=512, seed=3, period=2, part_on=40, part_off=80, rounds=110, snap_at=(60, 79, 81)):
+    """Plumtree outstanding tables past one 64-entry register (pt:574-579
+    adds, :562-567 acks): a broadcast from node 0 every `period` rounds
+    from round 30, and a half/half partition over rounds part_on..part_off
+    - 1 that leaves the lazy pushes across it unacked (up to 88 entries on a
+    node at the defaults, none dropped; period=1 fills tables to
+    PSIM_PT_OUT_CAP and drops).  The heal acks them.  Returns the node
+    views at the rounds in `snap_at` too (the tables at their largest)."""
+    sim = make(default_config(n_nodes=n, seed=seed))
+    snaps = {}
+    state = {"k": 0}
+
+    def hook(r):
+        if r in snap_at:
+            snaps[r] = sim.nodes()
+        if r == part_on:
+            sim.set_partition(W.half_partition(n))
+        if r == part_off:
+            sim.clear_partition()
+        if r >= 30 and r % period == 0:
+            sim.broadcast(0, state["k"] % 0x10000)
+            state["k"] += 1
+    st = sim.run_schedule(W.doubling_join(n, seed), rounds, extra=hook)
+    return sim, st, snaps
+
+
 VARIANT = dict(max_active_size=8, max_passive_size=20, arwl=6, prwl=6, persist_epoch=1)
 
 

@@ -47,6 +47,22 @@ def test_churn_partition_parity():
     S.compare_nodes(gs.nodes(), os_.nodes())
 
 
+@pytest.mark.parametrize("kw", [dict(), dict(period=1, snap_at=(60, 79))], ids=["tail", "at_cap"])
+def test_outstanding_tail_parity(kw):
+    """Outstanding tables past one 64-lane register (up to PSIM_PT_OUT_CAP
+    128; tests/test_out_tail.py shows the oracle fills them): adds, acks
+    and lazy ticks over the extension row's tail, GPU == oracle, the tables
+    compared while at their largest.  (neighbors_down/2's filter over a
+    tail, out_drop_peer, is not reached: the entries are lazy-set peers,
+    node_spec identities, and the filter drops bare ids -- DESIGN.md 2's
+    leak.)"""
+    (gs, gst, gsn), (os_, ost, osn) = _both(S.out_tail, **kw)
+    S.compare_stats(gst, ost)
+    for r in osn:
+        S.compare_nodes(gsn[r], osn[r])
+    S.compare_nodes(gs.nodes(), os_.nodes())
+
+
 def test_lingering_connections_parity():
     """connections beyond the active view -- shuffle
     terminals' Senders, rejected and pending neighbor requests, a joiner's
