@@ -153,7 +153,7 @@ def launch_ranks(args):
 SURVEY_WARM = 100               # warm-up rounds after the 64-round join ramp
 
 
-def _cpu_sample(n, seed, rounds, schedule, barrier=None):
+def _cpu_sample(n, seed, rounds, schedule, barrier=None, progress=True):
     """The CPU oracle (a port of the reference handlers, 1 thread) on a
     bounded sample of the workload: same bootstrap, same broadcast schedule.
     Returns (node-rounds, msgs, seconds)."""
@@ -163,10 +163,15 @@ def _cpu_sample(n, seed, rounds, schedule, barrier=None):
     from partisan_amd.sim import default_config
 
     o = Oracle(default_config(n_nodes=n, seed=seed))
+    # (a progress line every 32 bootstrap rounds on stderr from the 1-thread
+    # sample and the first worker at 2^19 nodes and more: minutes of CPU work
+    # print nothing else)
+    tick = (lambda r: r % 32 or print(f"cpu_baseline: bootstrap round {r}", file=sys.stderr, flush=True)) \
+        if progress and n >= (1 << 19) else None
     if schedule == "survey":
-        o.run_schedule(W.survey_join(n, seed), W.SURVEY_RAMP + SURVEY_WARM)
+        o.run_schedule(W.survey_join(n, seed), W.SURVEY_RAMP + SURVEY_WARM, extra=tick)
     else:
-        o.run_schedule(W.doubling_join(n, seed), 40)
+        o.run_schedule(W.doubling_join(n, seed), 40, extra=tick)
     k, msgs = 0, 0
     if barrier is not None:                   # all workers time their rounds together
         barrier.wait()
@@ -179,8 +184,8 @@ def _cpu_sample(n, seed, rounds, schedule, barrier=None):
     return n * rounds, msgs, time.perf_counter() - t0
 
 
-def _cpu_worker(a, barrier, q):
-    q.put(_cpu_sample(*a, barrier=barrier))
+def _cpu_worker(a, barrier, q, progress):
+    q.put(_cpu_sample(*a, barrier=barrier, progress=progress))
 
 
 def cpu_model():
@@ -290,7 +295,7 @@ def cpu_baseline(args):
     workers = max(1, min(args.cpu_workers, len(os.sched_getaffinity(0))))
     ctx = mp.get_context("fork")
     barrier, q = ctx.Barrier(workers), ctx.Queue()
-    procs = [ctx.Process(target=_cpu_worker, args=((n, args.seed + i, rounds, args.schedule), barrier, q))
+    procs = [ctx.Process(target=_cpu_worker, args=((n, args.seed + i, rounds, args.schedule), barrier, q, i == 0))
              for i in range(workers)]
     for p in procs:
         p.start()
