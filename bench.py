@@ -633,6 +633,7 @@ def main():
         step(1)
     if world > 1:
         dist.barrier()
+    x0 = sim.exchange_stats()
     t0 = time.perf_counter()
     stats = []
     kt = {}
@@ -651,6 +652,7 @@ def main():
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
+    x1 = sim.exchange_stats()
     st = np.concatenate(stats)
     dt = t1 - t0
     if world > 1:
@@ -727,6 +729,13 @@ def main():
         "overflow": int(st["overflow"].sum()),
         "pmc_key": key,
     }
+    if world > 1 or args.vshards > 1 or args.rank_path:
+        # the cross-shard exchange over the window, this rank's shards: records
+        # sent to another shard and their wire bytes (32 B a record, 32 more
+        # for one with exchange ids; 64 B a record in memory)
+        xr, xb = x1[0] - x0[0], x1[1] - x0[1]
+        out["exchange"] = {"records_per_round": xr / args.steps, "wire_bytes_per_round": xb / args.steps,
+                           "wire_bytes_per_record": xb / max(1, xr), "record_bytes_in_memory": 64}
     if check is not None:
         out["check"] = check
     # overlay statistics (psim_get_histograms; outside the measurement):

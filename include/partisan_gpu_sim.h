@@ -507,6 +507,13 @@ int psim_wire_decode(const uint8_t *buf, size_t len, const psim_wire_names *name
  * names[i] is a static string; returns the number of entries. */
 int psim_kernel_times(psim_handle *h, const char **names, double *ms, uint64_t *launches, int cap);
 
+/* The cross-shard exchange since psim_create (G > 1: virtual shards or RCCL
+ * ranks; this process's shards): *records = records sent to another shard,
+ * *bytes = their bytes on the wire -- 32 B a record (dst, src, type word, seq,
+ * a0-a2, word 7) plus 32 B for one with exchange ids (nex > 0), against 64 B
+ * a record in memory.  Both 0 on one shard. */
+int psim_get_exchange_stats(psim_handle *h, uint64_t *records, uint64_t *bytes);
+
 /* RCCL bootstrap for multi-process sharding (rank 0 creates, all pass it in cfg). */
 int psim_comm_id_size(void);
 int psim_get_comm_id(void *buf, size_t cap);

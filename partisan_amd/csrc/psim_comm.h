@@ -221,10 +221,14 @@ struct LoopbackComm : Comm {
         LoopWorld::Post p;
         p.sends = sends;
         return frame(st, p, [&] {
+            // the k-th receive from a peer takes the peer's k-th send to this
+            // rank (point-to-point order, as RCCL matches a group's messages)
+            std::map<int, int> nth;
             for (const Xfer& r : recvs) {
                 const Xfer* m = nullptr;
+                int k = nth[r.peer]++;
                 for (const Xfer& s : w->posts[r.peer].sends)
-                    if (s.peer == rank) m = &s;
+                    if (s.peer == rank && k-- == 0) { m = &s; break; }
                 if (!m || m->bytes != r.bytes) {
                     std::fprintf(stderr, "psim: loopback: rank %d expects %zu B from %d, which sends %zu\n", rank,
                                  r.bytes, r.peer, m ? m->bytes : (size_t)0);

@@ -42,6 +42,8 @@ using namespace psim;
 namespace {
 
 constexpr int BLK = 256;
+constexpr uint32_t PREP_BLK = 1024;   // k_desc blocks (at most PREP_BLK of them)
+constexpr uint32_t DESC_RANGES = 4;   // k_node_prep ranges a k_desc block takes (at most DESC_RANGES * PREP_BLK)
 // pinned host words per shard (Shard::pin): NST stats, the consume span, the
 // outbox total, the routed record count -- stored by kernels, read by the host
 enum { PIN_TOTAL = NST + 2, PIN_M = NST + 3, PIN_OVF = NST + 4, PIN_BIGIN = NST + 5 };
@@ -233,8 +235,26 @@ constexpr uint32_t RB_MAX_BLOCKS = 1024;   // blocks of the two passes over the 
 // per bucket (512: route 36 -> 31 us a round at 2^20, profiles/r03 p26)
 constexpr uint32_t RR_THREADS = PSIM_RR_THREADS;
 
+// The exchange's wire format (G > 1): a record's first 32 B -- dst, src, type
+// word, seq, a0-a2 and word 7 -- is its head; a record with exchange ids
+// (nex > 0 in its type word: SHUFFLE, SHUFFLE_REPLY, X-BOT's) also sends its
+// last 32 B, the tail.  Every other record's last 32 B are zeros, so 32 B
+// of the 64 cross xGMI.  A sender writes, per owner shard, the heads of its
+// records in (src, seq) order, then the tails in the same order, and puts a
+// long record's tail index (among that owner's tails) in the head's word 7
+// -- zero in every record that crosses shards: the full strategy's payload
+// slot lives there, and that strategy runs on one shard (psim_create).  The
+// receiver's heads and tails arrive in source-shard order; k_bucket_hist adds
+// the source's tail base to each long head's word 7, and k_bucket_route
+// gathers head + tail (or zeros) into the 64-B inbox record, word 7 zeroed.
+struct __attribute__((aligned(16))) Wire {
+    uint4 q[2];
+};
+static_assert(sizeof(Wire) == 32, "a wire unit is half a record");
+__host__ __device__ __forceinline__ bool wire_long(uint32_t tt) { return ((tt >> 16) & 0xFFu) != 0u; }
+
 // the sources of one route: the outbox runs of this shard's nodes (G == 1),
-// or a dense receive buffer (G > 1)
+// or the received heads and tails (G > 1)
 struct RouteIn {
     const Msg* rec;
     const uint32_t* okey;      // runs: route key of every outbox slot
@@ -243,22 +263,39 @@ struct RouteIn {
     uint32_t n_src;            // runs: source nodes; dense: records
     uint32_t lo;               // first local node id
     uint32_t pl;               // dense: pluggable manager (bound class 0)
+    Wire* wire;                // dense: the heads (word 7 of a long one fixed up by k_bucket_hist)
+    const Wire* tails;         // dense: the tails
+    const uint32_t* seg;       // dense: per source shard its first head, then its first tail (2 (nseg + 1))
+    uint32_t nseg;
 };
+
+// the source shard of received head i (seg: nseg + 1 increasing starts)
+__device__ __forceinline__ uint32_t wire_source(const RouteIn& in, uint32_t i) {
+    uint32_t a = 0, b = in.nseg;
+    while (b - a > 1) {
+        const uint32_t m = (a + b) >> 1;
+        if (in.seg[m] <= i) a = m; else b = m;
+    }
+    return a;
+}
 
 // Calls f(g, d, cls) for every record of block step `step`: source index g,
 // local destination d, bound class cls.  The runs form has a wave expand 64
 // consecutive source nodes' runs into consecutive record numbers (lane l
 // takes records l, l + 64, ..., so okey is read in slot order); every thread
 // of the block must call it.
-template <bool DENSE, typename F>
+template <bool DENSE, bool FIX = false, typename F>
 __device__ __forceinline__ void route_step(const RouteIn& in, uint32_t step, uint32_t (*spre)[65],
                                            uint64_t (*sbase)[64], F f) {
     const uint32_t w = threadIdx.x >> 6, l = threadIdx.x & 63;
     const uint32_t i = step * RB_STEP + threadIdx.x;
     if (DENSE) {
         if (i < in.n_src) {
-            const Msg& r = in.rec[i];
-            f(i, r.dst - in.lo, in.pl ? 0u : max_emit(r.tt & 0xFF));
+            const uint4 h0 = in.wire[i].q[0];        // dst, src, type word, seq
+            // (FIX, k_bucket_hist: a long head's tail index becomes the
+            // index among every received tail)
+            if (FIX && wire_long(h0.z)) in.wire[i].q[1].w += in.seg[in.nseg + 1 + wire_source(in, i)];
+            f(i, h0.x - in.lo, in.pl ? 0u : max_emit(h0.z & 0xFF));
         }
         return;
     }
@@ -357,8 +394,8 @@ __global__ void __launch_bounds__(RB_STEP) k_bucket_hist(RouteIn in, uint32_t ns
     if (blockIdx.x == 0 && threadIdx.x == 0) hist[(size_t)nb * gridDim.x] = 0;   // the scan's extra entry
     __syncthreads();
     for (uint32_t step = blockIdx.x; step < nsteps; step += gridDim.x)
-        route_step<DENSE>(in, step, spre, sbase,
-                          [&](uint32_t, uint32_t d, uint32_t) { atomicAdd(&hcnt[d >> wshift], 1u); });
+        route_step<DENSE, DENSE>(in, step, spre, sbase,
+                                 [&](uint32_t, uint32_t d, uint32_t) { atomicAdd(&hcnt[d >> wshift], 1u); });
     __syncthreads();
     for (uint32_t j = threadIdx.x; j < nb; j += blockDim.x) hist[(size_t)j * gridDim.x + blockIdx.x] = hcnt[j];
 }
@@ -395,32 +432,43 @@ __global__ void __launch_bounds__(RB_STEP) k_bucket_scatter(RouteIn in, uint32_t
 }
 
 // G > 1, sender side: this shard's outbox runs stably partitioned by owner
-// shard (owner = dst / per) straight into the send buffer, so each owner's
-// records stay in (src, seq) order -- the receiver's route relies on it.
-// Two passes; block blk takes the consecutive block steps [blk * spb,
+// shard (owner = dst / per) straight into the send buffer in the wire format
+// (Wire: the heads of every owner, then the tails of every owner), so each
+// owner's records stay in (src, seq) order -- the receiver's route relies on
+// it.  Two passes; block blk takes the consecutive block steps [blk * spb,
 // (blk + 1) * spb), so block order is source order (a grid-stride step
 // assignment would put a block's later steps before the next block's
 // earlier ones and break the (src, seq) order once a block runs two steps):
-//   WRITE = false  per block and owner the record count -> hist[q * nblk + blk]
-//                  (hist[G * nblk] = 0: the scan's extra entry, the total)
-//   WRITE = true   after the scan, each record's 64 B to off[q * nblk + blk]
-//                  + its rank among the block's records of owner q
+//   WRITE = false  per block and owner the record count -> hist[q * nblk +
+//                  blk] and the long records' count -> hist[(G + q) * nblk +
+//                  blk] (hist[2 G nblk] = 0: the scan's extra entry, the total)
+//   WRITE = true   after the scan, each record's head to off[q * nblk + blk]
+//                  + its rank among the block's records of owner q, a long
+//                  record's tail to off[(G + q) * nblk + blk] + its rank among
+//                  the block's long records of owner q, and that tail's index
+//                  among owner q's tails into the head's word 7
 // A wave walks its 64 nodes' records in slot order, 64 at a time; the rank
 // within a batch is a ballot over the lanes of the same owner, one ballot
 // per distinct owner in the batch (<= G).
 template <bool WRITE>
 __global__ void __launch_bounds__(RB_STEP) k_owner_part(RouteIn in, uint32_t nsteps, uint32_t spb, uint32_t G,
                                                         uint32_t per, uint32_t* hist,
-                                                        const uint32_t* __restrict__ off, Msg* __restrict__ out,
+                                                        const uint32_t* __restrict__ off, Wire* __restrict__ out,
                                                         unsigned long long* mark) {
     if (mark && blockIdx.x == 0 && threadIdx.x == 0) *mark = __builtin_amdgcn_s_memrealtime();   // (phase end)
     __shared__ uint32_t spre[RB_WAVES][65];
     __shared__ uint64_t sbase[RB_WAVES][64];
-    __shared__ uint32_t wc[RB_WAVES][64];             // per wave and owner: records in this step
-    __shared__ uint32_t run[64];                      // per owner: the block's next position
+    __shared__ uint32_t wc[RB_WAVES][64], wl[RB_WAVES][64];   // per wave and owner: records / long ones this step
+    __shared__ uint32_t run[64], runl[64];            // per owner: the block's next head / tail position
+    __shared__ uint32_t tb[64];                       // per owner: its first tail (WRITE)
     const uint32_t w = threadIdx.x >> 6, l = threadIdx.x & 63, nblk = gridDim.x;
-    if (threadIdx.x < 64) run[threadIdx.x] = (WRITE && threadIdx.x < G) ? off[threadIdx.x * nblk + blockIdx.x] : 0u;
-    if (!WRITE && blockIdx.x == 0 && threadIdx.x == 0) hist[G * nblk] = 0;
+    if (threadIdx.x < 64) {
+        const bool q = WRITE && threadIdx.x < G;
+        run[threadIdx.x] = q ? off[threadIdx.x * nblk + blockIdx.x] : 0u;
+        runl[threadIdx.x] = q ? off[(G + threadIdx.x) * nblk + blockIdx.x] : 0u;
+        tb[threadIdx.x] = q ? off[(G + threadIdx.x) * nblk] : 0u;
+    }
+    if (!WRITE && blockIdx.x == 0 && threadIdx.x == 0) hist[2 * G * nblk] = 0;
     const uint32_t s_end = min(nsteps, (blockIdx.x + 1) * spb);
     for (uint32_t step = blockIdx.x * spb; step < s_end; step++) {
         const uint32_t i = step * RB_STEP + threadIdx.x;
@@ -448,61 +496,86 @@ __global__ void __launch_bounds__(RB_STEP) k_owner_part(RouteIn in, uint32_t nst
             g = sbase[w][a] + (t - pre[a]);
             return (in.okey[g] & KEY_DST_MASK) / per;
         };
-        uint32_t cnt = 0;                             // lane q: this wave's records of owner q
+        uint32_t cnt = 0, cntl = 0;                   // lane q: this wave's records / long records of owner q
         for (uint32_t t0 = 0; t0 < T; t0 += 64) {
             uint64_t g = 0;
             const uint32_t o = rec_at(t0 + l, g);
+            const bool lg = o != 0xFFFFFFFFu && wire_long(in.rec[g].tt);
             for (uint64_t todo = __ballot(o != 0xFFFFFFFFu); todo;) {
                 const uint32_t q = __builtin_amdgcn_readlane(o, __ffsll((long long)todo) - 1);
-                const uint64_t m = __ballot(o == q);
+                const uint64_t m = __ballot(o == q), ml = __ballot(o == q && lg);
                 cnt += l == q ? (uint32_t)__popcll(m) : 0u;
+                cntl += l == q ? (uint32_t)__popcll(ml) : 0u;
                 todo &= ~m;
             }
         }
         wc[w][l] = cnt;
+        wl[w][l] = cntl;
         __syncthreads();
         if (WRITE) {
-            uint32_t B = 0;                           // lane q: where this wave's next owner-q record goes
+            uint32_t B = 0, BL = 0;                   // lane q: where this wave's next owner-q head / tail goes
             if (l < G) {
                 B = run[l];
-                for (uint32_t v = 0; v < w; v++) B += wc[v][l];
+                BL = runl[l];
+                for (uint32_t v = 0; v < w; v++) { B += wc[v][l]; BL += wl[v][l]; }
             }
             for (uint32_t t0 = 0; t0 < T; t0 += 64) {
                 uint64_t g = 0;
                 const uint32_t o = rec_at(t0 + l, g);
-                uint32_t pos = 0;
+                uint4 x0 = make_uint4(0, 0, 0, 0), x1 = x0, x2 = x0, x3 = x0;
+                if (o != 0xFFFFFFFFu) {
+                    const uint4* sp = reinterpret_cast<const uint4*>(&in.rec[g]);
+                    x0 = sp[0]; x1 = sp[1]; x2 = sp[2]; x3 = sp[3];
+                }
+                const bool lg = o != 0xFFFFFFFFu && wire_long(x0.z);
+                uint32_t pos = 0, lpos = 0;
                 for (uint64_t todo = __ballot(o != 0xFFFFFFFFu); todo;) {
                     const uint32_t q = __builtin_amdgcn_readlane(o, __ffsll((long long)todo) - 1);
-                    const uint64_t m = __ballot(o == q);
-                    if (o == q) pos = __builtin_amdgcn_readlane(B, q) + (uint32_t)__popcll(m & ((1ull << l) - 1ull));
+                    const uint64_t m = __ballot(o == q), ml = __ballot(o == q && lg);
+                    const uint64_t below = (1ull << l) - 1ull;
+                    if (o == q) {
+                        pos = __builtin_amdgcn_readlane(B, q) + (uint32_t)__popcll(m & below);
+                        lpos = __builtin_amdgcn_readlane(BL, q) + (uint32_t)__popcll(ml & below);
+                    }
                     B += l == q ? (uint32_t)__popcll(m) : 0u;
+                    BL += l == q ? (uint32_t)__popcll(ml) : 0u;
                     todo &= ~m;
                 }
                 if (o != 0xFFFFFFFFu) {
-                    const uint4* sp = reinterpret_cast<const uint4*>(&in.rec[g]);
-                    uint4* dp = reinterpret_cast<uint4*>(&out[pos]);
-                    const uint4 x0 = sp[0], x1 = sp[1], x2 = sp[2], x3 = sp[3];
-                    dp[0] = x0; dp[1] = x1; dp[2] = x2; dp[3] = x3;
+                    if (lg) {
+                        x1.w = lpos - tb[o];          // the tail's index among owner o's tails
+                        out[lpos].q[0] = x2;
+                        out[lpos].q[1] = x3;
+                    }
+                    out[pos].q[0] = x0;
+                    out[pos].q[1] = x1;
                 }
             }
         }
         __syncthreads();
         if (threadIdx.x < G)
-            for (uint32_t v = 0; v < RB_WAVES; v++) run[threadIdx.x] += wc[v][threadIdx.x];
+            for (uint32_t v = 0; v < RB_WAVES; v++) { run[threadIdx.x] += wc[v][threadIdx.x]; runl[threadIdx.x] += wl[v][threadIdx.x]; }
     }
     if (!WRITE) {
         __syncthreads();
-        if (threadIdx.x < G) hist[threadIdx.x * nblk + blockIdx.x] = run[threadIdx.x];
+        if (threadIdx.x < G) {
+            hist[threadIdx.x * nblk + blockIdx.x] = run[threadIdx.x];
+            hist[(G + threadIdx.x) * nblk + blockIdx.x] = runl[threadIdx.x];
+        }
     }
 }
 
-// each owner's first send-buffer position (G + 1 entries: the last is the
-// total) and, on RCCL ranks, each owner's record count straight into the send
-// half of the count all-to-all (so the round reads both back at once)
+// each owner's first head and first tail in the send buffer (2 G + 1
+// entries: heads of owners 0.., tails of owners 0.., the total) and, on RCCL
+// ranks, each owner's record count | its long records' count << 32 straight
+// into the send half of the count all-to-all (so the round reads both back
+// at once)
 __global__ void k_owner_offsets(const uint32_t* hoff, uint32_t nblk, uint32_t G, uint64_t* d_off, uint64_t* cnt) {
     const uint32_t q = threadIdx.x;
-    if (q <= G) d_off[q] = hoff[q * nblk];
-    if (cnt && q < G) cnt[q] = (uint64_t)(hoff[(q + 1) * nblk] - hoff[q * nblk]);
+    if (q <= 2 * G) d_off[q] = hoff[q * nblk];
+    if (cnt && q < G)
+        cnt[q] = (uint64_t)(hoff[(q + 1) * nblk] - hoff[q * nblk]) |
+                 ((uint64_t)(hoff[(G + q + 1) * nblk] - hoff[(G + q) * nblk]) << 32);
 }
 
 
@@ -566,12 +639,27 @@ __device__ __forceinline__ void wave_sort64(uint32_t* p, uint32_t k) {
     if (l < k) p[l] = v;
 }
 
+// 16-B piece p of received record k rebuilt from the wire: the head's two
+// pieces (word 7, the tail index, back to 0 on a long record), then the
+// tail's -- or zeros
+__device__ __forceinline__ uint4 wire_piece(const Wire* __restrict__ heads, const Wire* __restrict__ tails,
+                                            uint32_t k, uint32_t p) {
+    if (p == 0) return heads[k].q[0];
+    const uint32_t tt = heads[k].q[0].z;
+    const uint4 h1 = heads[k].q[1];
+    const bool lng = wire_long(tt);
+    if (p == 1) return make_uint4(h1.x, h1.y, h1.z, lng ? 0u : h1.w);
+    return lng ? tails[h1.w].q[p - 2] : make_uint4(0, 0, 0, 0);
+}
+
 // One block per bucket of W destinations; LDS holds per destination the
 // count, the bound sum (later the run start, in the same words) and the
 // BROADCAST message-slot mask (64 bits): 4 x W words.
+template <bool WIRE>
 __global__ void __launch_bounds__(RR_THREADS) k_bucket_route(
     uint32_t n, uint32_t wshift, uint32_t nblk, const uint32_t* __restrict__ off,
-    const uint2* __restrict__ pairs, const Msg* __restrict__ rec, uint32_t* rank, unsigned long long* cb,
+    const uint2* __restrict__ pairs, const Msg* __restrict__ rec, const Wire* __restrict__ heads,
+    const Wire* __restrict__ tails, uint32_t* rank, unsigned long long* cb,
     unsigned long long* bmask, uint32_t* in_beg, uint32_t* idx, uint32_t* tmp, Msg* __restrict__ inbox, uint64_t* hm,
     uint64_t cap, const uint32_t* ctl) {
     if (*ctl) return;                                 // an aborted batch (run_batch)
@@ -597,7 +685,8 @@ __global__ void __launch_bounds__(RR_THREADS) k_bucket_route(
         rank[p] = atomicAdd(&cnt[dl], 1u);
         if (cls == KEY_BCAST) {                       // 1 (a duplicate's PRUNE) + the slot bit
             atomicAdd(&bs[dl], 1u);
-            atomicOr(&mk[dl], 1ull << (rec[x.y].a0 % PSIM_MSG_SLOTS));
+            const uint32_t a0 = WIRE ? heads[x.y].q[1].x : rec[x.y].a0;
+            atomicOr(&mk[dl], 1ull << (a0 % PSIM_MSG_SLOTS));
         } else if (cls) {
             atomicAdd(&bs[dl], cls);
         }
@@ -690,9 +779,14 @@ __global__ void __launch_bounds__(RR_THREADS) k_bucket_route(
     const uint32_t m4 = (s1 - s0) * 4, bd = blockDim.x;
     for (uint32_t t = threadIdx.x; t < m4; t += 2 * bd) {
         const uint32_t t2 = t + bd;
-        const uint4 a = reinterpret_cast<const uint4*>(&rec[idx[s0 + (t >> 2)]])[t & 3];
-        uint4 c = make_uint4(0, 0, 0, 0);
-        if (t2 < m4) c = reinterpret_cast<const uint4*>(&rec[idx[s0 + (t2 >> 2)]])[t2 & 3];
+        uint4 a, c = make_uint4(0, 0, 0, 0);
+        if (WIRE) {
+            a = wire_piece(heads, tails, idx[s0 + (t >> 2)], t & 3);
+            if (t2 < m4) c = wire_piece(heads, tails, idx[s0 + (t2 >> 2)], t2 & 3);
+        } else {
+            a = reinterpret_cast<const uint4*>(&rec[idx[s0 + (t >> 2)]])[t & 3];
+            if (t2 < m4) c = reinterpret_cast<const uint4*>(&rec[idx[s0 + (t2 >> 2)]])[t2 & 3];
+        }
         reinterpret_cast<uint4*>(&inbox[s0 + (t >> 2)])[t & 3] = a;
         if (t2 < m4) reinterpret_cast<uint4*>(&inbox[s0 + (t2 >> 2)])[t2 & 3] = c;
     }
@@ -706,7 +800,7 @@ __device__ __forceinline__ bool due(uint32_t period, uint32_t r, uint32_t start)
 // outbox region) and whether it has any work (inbox, join, timers, EXIT
 // scan, origin, outstanding lazy pushes).  Also counts live nodes and
 // messages addressed to dead ones.
-__global__ void __launch_bounds__(256) k_node_prep(RoundArgs a, const unsigned long long* bmask, uint64_t* packed,
+__global__ void __launch_bounds__(BLK) k_node_prep(RoundArgs a, const unsigned long long* bmask, uint64_t* packed,
                                                    uint64_t* part, uint32_t* ocnt, unsigned long long* btot,
                                                    uint32_t per, uint64_t* tiles) {
     if (*a.ctl) return;                               // an aborted batch (run_batch)
@@ -736,8 +830,13 @@ __global__ void __launch_bounds__(256) k_node_prep(RoundArgs a, const unsigned l
         uint32_t w = 0;
         const unsigned long long cbi = a.in_cb[i];       // inbox count | bound sum << 32
         uint32_t c = (uint32_t)cbi;
+        // (the row words every live node reads, issued with the flag byte:
+        // read under its test, they were a second dependent memory wait)
+        const uint32_t st_ = a.start[i];
+        const uint32_t org_ = a.pl ? 0u : a.origin[i];
+        const unsigned long long bm_ = a.pl ? 0ull : bmask[i];
         if (f & F_UP) {
-            uint32_t st = a.start[i], r = a.round;
+            uint32_t st = st_, r = a.round;
             if (a.pl) {            // emission bounds of the pluggable round (R0-P)
                 const Hdr& x = a.hdr[i];
                 bool pending = x.join_contact != PSIM_NONE;
@@ -758,7 +857,7 @@ __global__ void __launch_bounds__(256) k_node_prep(RoundArgs a, const unsigned l
                 }
                 w = c > 0 || (pending && !x.have) || per || leave;
             } else {
-                bool origin = a.origin[i] != 0;
+                bool origin = org_ != 0;
                 const Hdr& x = a.hdr[i];      // (read only where needed: a fresh start, a full nibble)
                 // the due timers' sends: the JOIN of a fresh start, a
                 // promotion's NEIGHBOR_REQUEST (the active view may shrink
@@ -772,7 +871,7 @@ __global__ void __launch_bounds__(256) k_node_prep(RoundArgs a, const unsigned l
                 // reset -- plus one per message handled before; the push's
                 // sends need an active connection: at most two per active
                 // member (its atom and its node_spec identity, App. A Q6)
-                const unsigned long long bm = c ? bmask[i] : 0ull;
+                const unsigned long long bm = c ? bm_ : 0ull;
                 const uint32_t pushes = (uint32_t)__popcll(bm) + (origin ? 1u : 0u);
                 const bool lazy = a.plumtree && due(a.lazy_tick_period, r, st);
                 uint32_t lazy_add = 0;
@@ -892,14 +991,31 @@ __global__ void __launch_bounds__(256) k_node_prep(RoundArgs a, const unsigned l
     }
 }
 
+// the per-node inputs of a k_desc entry, loaded before the block scan (the
+// scan's barriers then overlap their latency; loaded after it, they were a
+// second dependent memory wait a pass)
+struct DescIn {
+    uint32_t in_beg, cnt, start, origin;
+};
+__device__ __forceinline__ DescIn desc_in(const RoundArgs& a, uint32_t li, uint64_t pk,
+                                          const uint32_t* __restrict__ in_beg,
+                                          const unsigned long long* __restrict__ cb,
+                                          const uint32_t* __restrict__ start) {
+    DescIn d{0, 0, 0, 0};
+    if (pk & 1u) {
+        d.in_beg = in_beg[li];
+        d.cnt = (uint32_t)cb[li];
+        d.start = start[li];
+        d.origin = a.plumtree && !a.pl ? a.origin[li] : 0u;
+    }
+    return d;
+}
+
 // node li's entry of k_desc (li == n_local: the totals), from its prefix P
-// of the packed words and its own packed word pk
-__device__ __forceinline__ void desc_entry(const RoundArgs& a, uint32_t li, uint64_t P, uint64_t pk,
-                                           const uint32_t* __restrict__ in_beg,
-                                           const unsigned long long* __restrict__ cb,
-                                           const uint32_t* __restrict__ start, uint4* __restrict__ desc,
-                                           uint64_t* __restrict__ obase, uint32_t* nact, unsigned long long tot,
-                                           uint64_t* hout, uint64_t cap, uint32_t* ctl) {
+// of the packed words, its own packed word pk and its inputs
+__device__ __forceinline__ void desc_entry(const RoundArgs& a, uint32_t li, uint64_t P, uint64_t pk, const DescIn& d,
+                                           uint4* __restrict__ desc, uint64_t* __restrict__ obase, uint32_t* nact,
+                                           unsigned long long tot, uint64_t* hout, uint64_t cap, uint32_t* ctl) {
     obase[li] = P >> 32;
     if (li == a.n_local) {
         *nact = (uint32_t)P;
@@ -911,20 +1027,20 @@ __device__ __forceinline__ void desc_entry(const RoundArgs& a, uint32_t li, uint
         return;
     }
     if (!(pk & 1u)) return;
-    if ((uint32_t)cb[li] > DESC_CNT_MASK) hout[PIN_BIGIN] = 1;   // (the descriptor packs it in 26 bits)
-    const uint32_t st = start[li], r = a.round;
+    if (d.cnt > DESC_CNT_MASK) hout[PIN_BIGIN] = 1;   // (the descriptor packs it in 26 bits)
+    const uint32_t st = d.start, r = a.round;
     const uint32_t tf = (a.random_promotion && due(a.promotion_period, r, st) ? DESC_PROMO : 0u) |
                         (due(a.shuffle_period, r, st) ? DESC_SHUFFLE : 0u) |
                         (a.plumtree && due(a.lazy_tick_period, r, st) ? DESC_LAZY : 0u) |
-                        (a.plumtree && !a.pl && a.origin[li] ? DESC_ORIGIN : 0u);
+                        (d.origin ? DESC_ORIGIN : 0u);
     const uint32_t xb = a.xbot && due(a.xbot_period, r, st) ? DESC_XBOT_BIT : 0u;
-    desc[(uint32_t)P] = make_uint4(a.lo + li, in_beg[li], (uint32_t)cb[li] | xb | (tf << 28), (uint32_t)(P >> 32));
+    desc[(uint32_t)P] = make_uint4(a.lo + li, d.in_beg, d.cnt | xb | (tf << 28), (uint32_t)(P >> 32));
 }
 
 // the outbox total: the sum of k_node_prep's nbt block sums (every thread of
 // the block calls it)
 __device__ unsigned long long btot_sum(const unsigned long long* btot, uint32_t nbt) {
-    __shared__ unsigned long long s_w[BLK / 64], s_tot;
+    __shared__ unsigned long long s_w[PREP_BLK / 64], s_tot;
     unsigned long long t = 0;
     for (uint32_t j = threadIdx.x; j < nbt; j += blockDim.x) t += btot[j];
     for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o);
@@ -939,39 +1055,58 @@ __device__ unsigned long long btot_sum(const unsigned long long* btot, uint32_t 
     return s_tot;
 }
 
-template <typename T>
+template <typename T, uint32_t NT = BLK>
 __device__ T block_excl(T v, T* total);   // (the exclusive-scan section below)
 
 // Per node, from the scan of the packed (bound, work) words: the outbox
 // base, and for a node with work its descriptor at its active-list position
 // -- every address k_consume needs first and which of the node's timers are
 // due (hv:542-607, pt:341-345).  Entry n: the outbox total and the count.
-// Block b walks k_node_prep's range of block b again, BLK nodes a pass: a
-// block scan of their packed words on top of the tile's prefix (tiles: the
-// exclusive scan of k_node_prep's tile sums, k_scan_sums) -- one launch in
-// place of a tile-sum and an apply pass over the whole array.
-__global__ void __launch_bounds__(BLK) k_desc(const uint64_t* __restrict__ packed, const uint64_t* __restrict__ tiles,
-                                             uint32_t per, const uint32_t* __restrict__ in_beg,
-                                             const unsigned long long* __restrict__ cb,
-                                             const uint32_t* __restrict__ start, RoundArgs a, uint4* __restrict__ desc,
-                                             uint64_t* __restrict__ obase, uint32_t* nact,
-                                             const unsigned long long* btot, uint64_t* hout, uint64_t cap,
-                                             uint32_t* ctl) {
+// Block b walks k_node_prep's range of block b again, PREP_BLK nodes a pass:
+// a block scan of their packed words on top of the range's prefix, which the
+// block sums itself from k_node_prep's range sums (one per thread: the grid
+// has at most PREP_BLK blocks) -- one launch in place of a tile-sum, a
+// tile-scan and an apply pass (the one-block scan of the range sums alone
+// took 8.5 us a round at 2^20 nodes over 4096 ranges)
+__global__ void __launch_bounds__(PREP_BLK) k_desc(const uint64_t* __restrict__ packed,
+                                                  const uint64_t* __restrict__ tiles, uint32_t per,
+                                                  const uint32_t* __restrict__ in_beg,
+                                                  const unsigned long long* __restrict__ cb,
+                                                  const uint32_t* __restrict__ start, RoundArgs a,
+                                                  uint4* __restrict__ desc, uint64_t* __restrict__ obase,
+                                                  uint32_t* nact, const unsigned long long* btot,
+                                                  uint32_t nranges, uint64_t* hout, uint64_t cap, uint32_t* ctl) {
     if (*ctl) return;                                 // (uniform)
     const bool last = blockIdx.x == gridDim.x - 1;
-    const unsigned long long tot = last ? btot_sum(btot, gridDim.x) : 0ull;   // (uniform)
-    const uint32_t i0 = blockIdx.x * per, i1 = min(a.n_local, i0 + per);
-    uint64_t carry = tiles[blockIdx.x];
-    for (uint32_t k = i0; k < i1; k += BLK) {         // (uniform)
-        const uint32_t li = k + threadIdx.x;
-        const uint64_t pk = li < i1 ? packed[li] : 0ull;
+    const uint32_t r0 = blockIdx.x * DESC_RANGES;     // this block's first k_node_prep range
+    const uint32_t i0 = r0 * per, i1 = min(a.n_local, i0 + DESC_RANGES * per);
+    // (the sums of the ranges before this block's and the first pass's
+    // inputs issued before either is used)
+    uint64_t tp = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < DESC_RANGES; k++) {
+        const uint32_t j = threadIdx.x + k * PREP_BLK;
+        tp += j < r0 ? tiles[j] : 0ull;
+    }
+    uint32_t li = i0 + threadIdx.x;
+    uint64_t pk = li < i1 ? packed[li] : 0ull;
+    DescIn d = desc_in(a, li, pk, in_beg, cb, start);
+    const unsigned long long tot = last ? btot_sum(btot, nranges) : 0ull;   // (uniform)
+    uint64_t carry;
+    (void)block_excl<uint64_t, PREP_BLK>(tp, &carry);
+    for (uint32_t k = i0; k < i1; k += PREP_BLK) {    // (uniform)
+        if (k != i0) {
+            li = k + threadIdx.x;
+            pk = li < i1 ? packed[li] : 0ull;
+            d = desc_in(a, li, pk, in_beg, cb, start);
+        }
         uint64_t pass;
-        const uint64_t e = block_excl(pk, &pass);
-        if (li < i1) desc_entry(a, li, carry + e, pk, in_beg, cb, start, desc, obase, nact, 0ull, hout, cap, ctl);
+        const uint64_t e = block_excl<uint64_t, PREP_BLK>(pk, &pass);
+        if (li < i1) desc_entry(a, li, carry + e, pk, d, desc, obase, nact, 0ull, hout, cap, ctl);
         carry += pass;
     }
-    if (last && threadIdx.x == 0)                     // entry n: the totals
-        desc_entry(a, a.n_local, tiles[gridDim.x], 0ull, in_beg, cb, start, desc, obase, nact, tot, hout, cap, ctl);
+    if (last && threadIdx.x == 0)                     // entry n: the totals (carry: every range's sum)
+        desc_entry(a, a.n_local, carry, 0ull, DescIn{0, 0, 0, 0}, desc, obase, nact, tot, hout, cap, ctl);
 }
 
 // --------------------------------------------------------- overlay stats --
@@ -1237,7 +1372,12 @@ struct Shard {
     DBuf<uint32_t> ikeys, ivals;
     uint32_t m_in = 0;
     DBuf<Msg> outbox;                   // this round's emissions (holes between node regions)
-    DBuf<Msg> recvbuf;                  // G > 1: received records, in source-shard order
+    // G > 1: the received records in the wire format, in source-shard order:
+    // their heads, the long ones' tails, and per source its first head and
+    // first tail (wseg, 2 (G + 1) words; its host copy until the next round)
+    DBuf<Wire> recvh, recvt;
+    DBuf<uint32_t> wseg;
+    std::vector<uint32_t> wseg_host;
     // records by node run, in inbox order: read by this round's node-round
     // kernels, then (same stream) overwritten by the route with the next
     // round's -- one buffer, nothing reads a round's inbox after its consume
@@ -1254,13 +1394,15 @@ struct Shard {
     DBuf<uint8_t> cub_tmp;              // the scan's tile totals
     DBuf<uint32_t> ev_ids, ev_contacts, stop_ids, n_stop;
     bool tomb_live = false;             // full: snapshots carry their remove rows
-    DBuf<Msg> sendbuf;
+    DBuf<Wire> sendbuf;                 // G > 1: the outbox in the wire format, by owner (k_owner_part)
     // pluggable manager
     DBuf<uint32_t> sview, sinv, fbits, pay[2], pay_top;
     int pay_cur = 0;
     DBuf<uint8_t> faulted;              // omission faults: generally omitting nodes (global id)
     DBuf<uint64_t> omit;                // ... sorted send-omission pairs, then receive-omission pairs
-    std::vector<uint64_t> soff, scnt;   // per destination shard (G + 1 offsets)
+    // per destination shard: the send buffer's offsets (2 G + 1: heads of
+    // each owner, tails of each owner, the end), heads and tails sent
+    std::vector<uint64_t> soff, scnt, lcnt;
     uint32_t pper = BLK;               // k_node_prep / k_desc: nodes per block (a multiple of BLK)
     uint32_t pgrid = 0, cgrid = 0, rgrid = 0, tgrid = 0, sgrid = 0, lgrid = 0, qgrid = 0;   // stats rows: prepare,
                                    // consume, relay, plumtree, shuffle-start, lite, Plumtree-lane blocks
@@ -1322,6 +1464,9 @@ struct psim_handle {
     bool ranked = false;
     Comm* comm = nullptr;               // ranked: RCCL (or the loopback test vehicle), psim_comm.h
     DBuf<uint64_t> comm_cnt;            // RCCL: [send counts | recv counts]
+    // the exchange since creation (psim_get_exchange_stats): records sent to
+    // another shard, and their wire bytes (heads + tails)
+    uint64_t x_records = 0, x_bytes = 0;
     // pending events
     std::vector<uint32_t> pend_crash, pend_join, pend_contact;
     std::vector<uint8_t> pend_join_mark;   // ids in pend_join (a node starts at most once per round)
@@ -1445,9 +1590,9 @@ constexpr uint32_t SCAN_ITEMS = 8, SCAN_TILE = BLK * SCAN_ITEMS;
 
 // exclusive scan of one value per thread across the block; returns the
 // block total in *total (every thread)
-template <typename T>
+template <typename T, uint32_t NT>
 __device__ T block_excl(T v, T* total) {
-    __shared__ T wsum[BLK / 64];
+    __shared__ T wsum[NT / 64];
     const uint32_t l = threadIdx.x & 63, wv = threadIdx.x >> 6;
     T x = v;                                          // inclusive scan within the wave
 #pragma unroll
@@ -1459,7 +1604,7 @@ __device__ T block_excl(T v, T* total) {
     __syncthreads();
     T base = 0, tot = 0;
 #pragma unroll
-    for (uint32_t k = 0; k < BLK / 64; k++) {
+    for (uint32_t k = 0; k < NT / 64; k++) {
         base += k < wv ? wsum[k] : T(0);
         tot += wsum[k];
     }
@@ -1482,18 +1627,32 @@ __global__ void __launch_bounds__(BLK) k_scan_tiles(const T* __restrict__ in, ui
 // one block: exclusive scan of the nt tile totals in place -- each thread a
 // contiguous run of ceil(nt / BLK) of them, one block scan of the run sums
 // (a block scan per BLK chunk took 12.7 us for 4097 totals: 17 serial
-// barrier pairs)
+// barrier pairs).  Up to SUMS_LDS totals go through LDS, loaded and stored
+// coalesced (the runs read straight from memory were ceil(nt / BLK)
+// dependent strided loads a thread: 8.6 us for 4097 totals)
+constexpr uint32_t SUMS_LDS = 4096 + 2 * BLK;
 template <typename T>
 __global__ void __launch_bounds__(BLK) k_scan_sums(T* sums, uint32_t nt) {
+    __shared__ T buf[SUMS_LDS];
+    const bool lds = nt <= SUMS_LDS;                  // (uniform)
+    T* p = lds ? buf : sums;
+    if (lds) {
+        for (uint32_t i = threadIdx.x; i < nt; i += BLK) buf[i] = sums[i];
+        __syncthreads();
+    }
     const uint32_t per = (nt + BLK - 1) / BLK, i0 = threadIdx.x * per, i1 = min(nt, i0 + per);
     T v = 0;
-    for (uint32_t i = i0; i < i1; i++) v += sums[i];
+    for (uint32_t i = i0; i < i1; i++) v += p[i];
     T tot;
     T run = block_excl(v, &tot);
     for (uint32_t i = i0; i < i1; i++) {
-        const T x = sums[i];
-        sums[i] = run;
+        const T x = p[i];
+        p[i] = run;
         run += x;
+    }
+    if (lds) {
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < nt; i += BLK) sums[i] = buf[i];
     }
 }
 
@@ -1535,14 +1694,13 @@ int scan_excl(Shard* s, const T* in, T* out, uint32_t n) {
     return PSIM_OK;
 }
 
-// prepare's scan + descriptors: k_node_prep left its blocks' tile sums in
-// pscan[0..pgrid] (pgrid + 1: the extra one is 0); one block scans them,
-// then k_desc walks the ranges again
+// prepare's scan + descriptors: k_node_prep left its blocks' range sums in
+// pscan[0..pgrid); k_desc sums the ones before its range and walks the range
+// again
 int scan_desc(Shard* s, const RoundArgs& a) {
-    k_scan_sums<uint64_t><<<1, BLK, 0, s->stream>>>(s->pscan.p, s->pgrid + 1);
-    k_desc<<<s->pgrid, BLK, 0, s->stream>>>(s->bound.p, s->pscan.p, s->pper, s->in_beg.p, s->cb.p, s->start.p, a,
-                                             s->desc.p, s->obase.p, s->d_nact.p, s->btot.p, s->pin_dev, s->desc_cap,
-                                             s->ctl.p);
+    k_desc<<<(s->pgrid + DESC_RANGES - 1) / DESC_RANGES, PREP_BLK, 0, s->stream>>>(
+        s->bound.p, s->pscan.p, s->pper, s->in_beg.p, s->cb.p, s->start.p, a, s->desc.p, s->obase.p, s->d_nact.p,
+        s->btot.p, s->pgrid, s->pin_dev, s->desc_cap, s->ctl.p);
     HIP_TRY(hipGetLastError());
     return PSIM_OK;
 }
@@ -1648,9 +1806,11 @@ int phase_events_prepare(psim_handle* h, Shard* s, const RoundCtl& ctl, RoundArg
         // grid-stride; 4096 blocks (16 waves per CU) keep the crash rounds'
         // dependent loads (active row -> members' flag bytes) in flight --
         // 512 blocks left 2 waves per SIMD and took 6.8 ms at 2^26 nodes
-        // (contiguous ranges of pper nodes, a multiple of BLK: k_desc's tiles)
+        // (contiguous ranges of pper nodes, a multiple of BLK: k_desc takes
+        // DESC_RANGES consecutive ranges a block; 1024-thread blocks here
+        // took 27.6 us against 21.5 at 2^20, profiles/r05/ab_log.txt r5r)
         {
-            const uint32_t g = std::min<uint32_t>(grid_for(n), 4096);
+            const uint32_t g = std::min<uint32_t>(grid_for(n), DESC_RANGES * PREP_BLK);
             s->pper = BLK * (uint32_t)(((uint64_t)n + (uint64_t)g * BLK - 1) / ((uint64_t)g * BLK));
             s->pgrid = std::max<uint32_t>(1, (uint32_t)(((uint64_t)n + s->pper - 1) / s->pper));
         }
@@ -1671,7 +1831,7 @@ int phase_events_prepare(psim_handle* h, Shard* s, const RoundCtl& ctl, RoundArg
                                 NST));
         k_node_prep<<<s->pgrid, BLK, 0, s->stream>>>(a, s->bmask.p, s->bound.p, s->stat_part.p, s->ocnt.p,
                                                      s->btot.p, s->pper, s->pscan.p);
-        // pscan[pgrid] becomes (outbox total << 32) | active count;
+        // (pscan: the ranges' sums of packed words; k_desc's last block sums them all)
         // obase[n] = the exact total (btot, summed by k_desc's last block)
         TRY(scan_desc(s, a));
         if (batched) goto args;
@@ -1840,14 +2000,16 @@ unsigned long long* phase_end_mark(psim_handle* h, Shard* s) {
                                                     : reinterpret_cast<unsigned long long*>(s->stat_out.p + NST) + 1;
 }
 
-int route_group(psim_handle* h, Shard* s, const Msg* dense, uint32_t m) {
+int route_group(psim_handle* h, Shard* s, bool dense, uint32_t m) {
     const uint32_t n = s->n;
     // buckets of 2^wshift destinations, one k_bucket_route block each, at
     // most 16 K of them (the two passes' LDS histograms: 4 B per bucket).
-    // At 2^20 more, smaller buckets (1024 nodes) cut k_bucket_route 36 -> 21
-    // us but cost as much in the histogram passes and their scan, and the
-    // step measured 1 % slower (profiles/r03/ab_log.txt, p17)
-    uint32_t wshift = n > (1u << 26) ? 13 : 12;
+    // Up to 2^22 nodes 2048-node buckets: twice the route's blocks (one per
+    // CU at 2^20 with 4096) -- k_bucket_route 64 -> 56 us, the histogram
+    // passes +4 us, the step 0.667 -> 0.663 ms (profiles/r05/ab_log.txt r5o);
+    // in round 3, before the gather moved into the route, 1024-node buckets
+    // measured 1 % slower a step (profiles/r03/ab_log.txt, p17)
+    uint32_t wshift = n > (1u << 26) ? 13 : n > (1u << 22) ? 12 : 11;
     if (const char* e = getenv("PSIM_ROUTE_WSHIFT")) {  // (another bucket width, for measurements)
         const int v = atoi(e);
         // (k_bucket_route's long-run list and sort buffer share the 2 W
@@ -1855,8 +2017,9 @@ int route_group(psim_handle* h, Shard* s, const Msg* dense, uint32_t m) {
         if ((1u << v) >= RR_THREADS && v >= 11 && v <= 13) wshift = (uint32_t)v;
     }
     const uint32_t W = 1u << wshift, nb = (n + W - 1) >> wshift;
-    const RouteIn in{dense ? dense : s->outbox.p, s->okey.p, s->obase.p, s->ocnt.p, dense ? m : n, s->lo,
-                     h->cfg.manager == PSIM_MANAGER_PLUGGABLE};
+    const RouteIn in{s->outbox.p, s->okey.p, s->obase.p, s->ocnt.p, dense ? m : n, s->lo,
+                     h->cfg.manager == PSIM_MANAGER_PLUGGABLE, dense ? s->recvh.p : nullptr,
+                     dense ? s->recvt.p : nullptr, dense ? s->wseg.p : nullptr, dense ? h->G : 0u};
     const uint32_t nsteps = std::max<uint32_t>(1, (in.n_src + RB_STEP - 1) / RB_STEP);
     const uint32_t nblk = std::min<uint32_t>(nsteps, h->rb_blocks);
     const size_t nh = (size_t)nb * nblk + 1;
@@ -1884,9 +2047,14 @@ int route_group(psim_handle* h, Shard* s, const Msg* dense, uint32_t m) {
         k_bucket_scatter<false><<<nblk, RB_STEP, lds_h, s->stream>>>(in, nsteps, nb, wshift, s->hoff.p,
                                                                      s->pairs.p, s->rcap, s->pin_dev + PIN_OVF,
                                                                      s->ctl.p, s->batch_round1, st);
-    k_bucket_route<<<nb, RR_THREADS, lds_r, s->stream>>>(n, wshift, nblk, s->hoff.p, s->pairs.p, in.rec, s->rank.p,
-                                                          s->cb.p, s->bmask.p, s->in_beg.p, s->ivals.p, s->tmp.p,
-                                                          s->inbox.p, s->pin_dev + PIN_M, s->rcap, s->ctl.p);
+    if (dense)
+        k_bucket_route<true><<<nb, RR_THREADS, lds_r, s->stream>>>(
+            n, wshift, nblk, s->hoff.p, s->pairs.p, nullptr, in.wire, in.tails, s->rank.p, s->cb.p, s->bmask.p,
+            s->in_beg.p, s->ivals.p, s->tmp.p, s->inbox.p, s->pin_dev + PIN_M, s->rcap, s->ctl.p);
+    else
+        k_bucket_route<false><<<nb, RR_THREADS, lds_r, s->stream>>>(
+            n, wshift, nblk, s->hoff.p, s->pairs.p, in.rec, nullptr, nullptr, s->rank.p, s->cb.p, s->bmask.p,
+            s->in_beg.p, s->ivals.p, s->tmp.p, s->inbox.p, s->pin_dev + PIN_M, s->rcap, s->ctl.p);
     HIP_TRY(hipGetLastError());
     return PSIM_OK;
 }
@@ -1906,24 +2074,27 @@ int route_buffers(Shard* s, bool both_inboxes) {
 // G == 1: the outbox runs grouped by destination are the whole route
 // (m_in: read back with the round's stats; ivals, pairs, rank, tmp and the
 // inbox were sized in prepare by the outbox total, which bounds it)
-int phase_route_local(psim_handle* h, Shard* s) { return route_group(h, s, nullptr, 0); }
+int phase_route_local(psim_handle* h, Shard* s) { return route_group(h, s, false, 0); }
+
+void send_counts(Shard* s, uint32_t G);
 
 // G > 1, sender side: the outbox partitioned by owner shard into the send
-// buffer (k_owner_part); per-owner counts/offsets on the host
+// buffer in the wire format (k_owner_part); per-owner counts/offsets on the host
 int phase_partition(psim_handle* h, Shard* s) {
     const uint32_t G = h->G;
-    const RouteIn in{s->outbox.p, s->okey.p, s->obase.p, s->ocnt.p, s->n, 0, 0};
+    RouteIn in{};
+    in.rec = s->outbox.p; in.okey = s->okey.p; in.obase = s->obase.p; in.ocnt = s->ocnt.p; in.n_src = s->n;
     const uint32_t nsteps = std::max<uint32_t>(1, (s->n + RB_STEP - 1) / RB_STEP);
     const uint32_t spb = (nsteps + h->rb_blocks - 1) / h->rb_blocks;    // consecutive steps per block
     const uint32_t nblk = (nsteps + spb - 1) / spb;
-    const size_t nh = (size_t)G * nblk + 1;
+    const size_t nh = (size_t)2 * G * nblk + 1;
     TRY(s->hist.ensure(nh));
     TRY(s->hoff.ensure(nh));
-    TRY(s->sendbuf.ensure(s->pin[PIN_TOTAL] + 1, 2));   // the outbox bound bounds the records
-    TRY(s->d_off.ensure(G + 1));
+    TRY(s->sendbuf.ensure(2 * (s->pin[PIN_TOTAL] + 1), 2));   // (the outbox bound bounds the records)
+    TRY(s->d_off.ensure(2 * G + 1));
     const bool rccl = h->ranked;
     if (rccl) TRY(h->comm_cnt.ensure(2 * G));
-    s->soff.assign(G + 1, 0);
+    s->soff.assign(2 * G + 1, 0);
     {
         KTimer t(h, s, KT_SORT);
         k_owner_part<false><<<nblk, RB_STEP, 0, s->stream>>>(in, nsteps, spb, G, h->per, s->hist.p, nullptr,
@@ -1931,89 +2102,146 @@ int phase_partition(psim_handle* h, Shard* s) {
         TRY(scan_excl(s, s->hist.p, s->hoff.p, (uint32_t)nh));
         k_owner_part<true><<<nblk, RB_STEP, 0, s->stream>>>(in, nsteps, spb, G, h->per, nullptr, s->hoff.p,
                                                              s->sendbuf.p, nullptr);
-        k_owner_offsets<<<1, 128, 0, s->stream>>>(s->hoff.p, nblk, G, s->d_off.p, rccl ? h->comm_cnt.p : nullptr);
+        k_owner_offsets<<<1, 256, 0, s->stream>>>(s->hoff.p, nblk, G, s->d_off.p, rccl ? h->comm_cnt.p : nullptr);
         HIP_TRY(hipGetLastError());
         // an RCCL rank reads the offsets back with the received counts, after
         // the count all-to-all (exchange_rccl): one host wait a round, not two
         if (rccl) return PSIM_OK;
-        HIP_TRY(hipMemcpyAsync(s->soff.data(), s->d_off.p, (G + 1) * 8, hipMemcpyDeviceToHost, s->stream));
+        HIP_TRY(hipMemcpyAsync(s->soff.data(), s->d_off.p, (2 * G + 1) * 8, hipMemcpyDeviceToHost, s->stream));
         TRY(stream_wait(s));
     }
-    s->scnt.resize(G);
-    for (uint32_t g = 0; g < G; g++) s->scnt[g] = s->soff[g + 1] - s->soff[g];
+    send_counts(s, G);
     return PSIM_OK;
 }
 
-// G > 1, receiver side: the shard-ordered concatenation grouped by dst
-int phase_receive(psim_handle* h, Shard* s, uint32_t m) {
+// per owner the heads and the tails this shard sends (from soff)
+void send_counts(Shard* s, uint32_t G) {
+    s->scnt.resize(G);
+    s->lcnt.resize(G);
+    for (uint32_t g = 0; g < G; g++) {
+        s->scnt[g] = s->soff[g + 1] - s->soff[g];
+        s->lcnt[g] = s->soff[G + g + 1] - s->soff[G + g];
+    }
+}
+
+// G > 1, receiver side: heads and tails from the G sources (hc[g] / lc[g]
+// each), already in recvh / recvt in source order; the source table, then
+// the route over the heads
+int phase_receive(psim_handle* h, Shard* s, const std::vector<uint64_t>& hc, const std::vector<uint64_t>& lc) {
+    const uint32_t G = h->G;
+    s->wseg_host.assign(2 * (G + 1), 0);
+    uint64_t m = 0, ml = 0;
+    for (uint32_t g = 0; g < G; g++) {
+        s->wseg_host[g] = (uint32_t)m;
+        s->wseg_host[G + 1 + g] = (uint32_t)ml;
+        m += hc[g];
+        ml += lc[g];
+    }
+    s->wseg_host[G] = (uint32_t)m;
+    s->wseg_host[2 * G + 1] = (uint32_t)ml;
+    TRY(s->wseg.ensure(2 * (G + 1)));
+    // (the host vector lives until the next round's receive: the copy is
+    // ordered on the stream before the route reads it)
+    HIP_TRY(hipMemcpyAsync(s->wseg.p, s->wseg_host.data(), s->wseg_host.size() * 4, hipMemcpyHostToDevice,
+                           s->stream));
     s->rcap = std::max<uint64_t>(s->rcap, m);   // exact: the count is on the host here
     TRY(route_buffers(s, false));
-    TRY(route_group(h, s, s->recvbuf.p, m));
-    s->m_in = m;
+    TRY(route_group(h, s, true, (uint32_t)m));
+    s->m_in = (uint32_t)m;
     return PSIM_OK;
 }
 
 // virtual shards of this process: device copies between shard buffers
 int exchange_local(psim_handle* h) {
     const uint32_t G = h->G;
-    std::vector<uint64_t> m(G, 0);
     for (Shard* d : h->shards) {
-        for (Shard* s : h->shards) m[d->idx] += s->scnt[d->idx];
-        TRY(d->recvbuf.ensure(m[d->idx] + 1));
-    }
-    for (Shard* d : h->shards) {
+        std::vector<uint64_t> hc(G), lc(G);
+        uint64_t m = 0, ml = 0;
+        for (Shard* s : h->shards) {
+            hc[s->idx] = s->scnt[d->idx];
+            lc[s->idx] = s->lcnt[d->idx];
+            m += hc[s->idx];
+            ml += lc[s->idx];
+        }
+        TRY(d->recvh.ensure(m + 1));
+        TRY(d->recvt.ensure(ml + 1));
         {
             KTimer t(h, d, KT_EXCHANGE);
-            uint64_t off = 0;
+            uint64_t oh = 0, ot = 0;
             for (uint32_t g = 0; g < G; g++) {  // concatenation in source-shard order
                 Shard* s = h->shards[g];
-                uint64_t c = s->scnt[d->idx];
-                if (c)
-                    HIP_TRY(hipMemcpyAsync(d->recvbuf.p + off, s->sendbuf.p + s->soff[d->idx],
-                                           c * sizeof(Msg), hipMemcpyDeviceToDevice, d->stream));
-                off += c;
+                if (hc[g])
+                    HIP_TRY(hipMemcpyAsync(d->recvh.p + oh, s->sendbuf.p + s->soff[d->idx], hc[g] * sizeof(Wire),
+                                           hipMemcpyDeviceToDevice, d->stream));
+                if (lc[g])
+                    HIP_TRY(hipMemcpyAsync(d->recvt.p + ot, s->sendbuf.p + s->soff[G + d->idx], lc[g] * sizeof(Wire),
+                                           hipMemcpyDeviceToDevice, d->stream));
+                if (g != d->idx) {
+                    h->x_records += hc[g];
+                    h->x_bytes += (hc[g] + lc[g]) * sizeof(Wire);
+                }
+                oh += hc[g];
+                ot += lc[g];
             }
         }
-        TRY(phase_receive(h, d, (uint32_t)m[d->idx]));
+        TRY(phase_receive(h, d, hc, lc));
     }
     return PSIM_OK;
 }
 
 // one shard per RCCL rank: counts by all-to-all, records by grouped send/recv
+// (per peer its heads, then its tails)
 int exchange_rccl(psim_handle* h) {
     Shard* s = h->shards[0];
     const uint32_t G = h->G;
-    uint64_t m = 0;
+    std::vector<uint64_t> hc(G), lc(G);
     {
         KTimer t(h, s, KT_EXCHANGE);
         // (k_owner_offsets wrote this rank's counts into comm_cnt[0, G))
         TRY(h->comm->all_to_all_u64(h->comm_cnt.p, h->comm_cnt.p + G, 1, s->stream));
         std::vector<uint64_t> rcnt(G);
         HIP_TRY(hipMemcpyAsync(rcnt.data(), h->comm_cnt.p + G, G * 8, hipMemcpyDeviceToHost, s->stream));
-        HIP_TRY(hipMemcpyAsync(s->soff.data(), s->d_off.p, (G + 1) * 8, hipMemcpyDeviceToHost, s->stream));
+        HIP_TRY(hipMemcpyAsync(s->soff.data(), s->d_off.p, (2 * G + 1) * 8, hipMemcpyDeviceToHost, s->stream));
         TRY(stream_wait(s));
-        s->scnt.resize(G);
-        for (uint32_t g = 0; g < G; g++) s->scnt[g] = s->soff[g + 1] - s->soff[g];
-        std::vector<uint64_t> roff(G);
-        for (uint32_t g = 0; g < G; g++) { roff[g] = m; m += rcnt[g]; }
-        TRY(s->recvbuf.ensure(m + 1));
-        Msg* rb = s->recvbuf.p;
+        send_counts(s, G);
+        uint64_t m = 0, ml = 0;
+        std::vector<uint64_t> roh(G), rot(G);
+        for (uint32_t g = 0; g < G; g++) {
+            hc[g] = rcnt[g] & 0xFFFFFFFFull;
+            lc[g] = rcnt[g] >> 32;
+            roh[g] = m;
+            rot[g] = ml;
+            m += hc[g];
+            ml += lc[g];
+        }
+        TRY(s->recvh.ensure(m + 1));
+        TRY(s->recvt.ensure(ml + 1));
         std::vector<Xfer> sends, recvs;
-        // a rank's own records: a device copy, except in a one-rank world
+        // a rank's own records: device copies, except in a one-rank world
         // (the diagnostic of the RCCL path), where the self send / receive
-        // pair goes through the library like any other peer's
+        // pairs go through the library like any other peer's
         const bool self_comm = h->world == 1;
         for (uint32_t g = 0; g < G; g++) {
             if (g == s->idx && !self_comm) continue;
-            if (s->scnt[g]) sends.push_back({(int)g, s->sendbuf.p + s->soff[g], s->scnt[g] * sizeof(Msg)});
-            if (rcnt[g]) recvs.push_back({(int)g, rb + roff[g], rcnt[g] * sizeof(Msg)});
+            if (s->scnt[g]) sends.push_back({(int)g, s->sendbuf.p + s->soff[g], s->scnt[g] * sizeof(Wire)});
+            if (s->lcnt[g]) sends.push_back({(int)g, s->sendbuf.p + s->soff[G + g], s->lcnt[g] * sizeof(Wire)});
+            if (hc[g]) recvs.push_back({(int)g, s->recvh.p + roh[g], hc[g] * sizeof(Wire)});
+            if (lc[g]) recvs.push_back({(int)g, s->recvt.p + rot[g], lc[g] * sizeof(Wire)});
+            h->x_records += s->scnt[g];
+            h->x_bytes += (s->scnt[g] + s->lcnt[g]) * sizeof(Wire);
         }
         TRY(h->comm->exchange(sends, recvs, s->stream));
-        if (rcnt[s->idx] && !self_comm)
-            HIP_TRY(hipMemcpyAsync(rb + roff[s->idx], s->sendbuf.p + s->soff[s->idx],
-                                   rcnt[s->idx] * sizeof(Msg), hipMemcpyDeviceToDevice, s->stream));
+        if (!self_comm) {
+            const uint32_t g = s->idx;
+            if (hc[g])
+                HIP_TRY(hipMemcpyAsync(s->recvh.p + roh[g], s->sendbuf.p + s->soff[g], hc[g] * sizeof(Wire),
+                                       hipMemcpyDeviceToDevice, s->stream));
+            if (lc[g])
+                HIP_TRY(hipMemcpyAsync(s->recvt.p + rot[g], s->sendbuf.p + s->soff[G + g], lc[g] * sizeof(Wire),
+                                       hipMemcpyDeviceToDevice, s->stream));
+        }
     }
-    return phase_receive(h, s, (uint32_t)m);
+    return phase_receive(h, s, hc, lc);
 }
 
 // the round's end after its route (which summed the stats: StatsIn)
@@ -2341,9 +2569,12 @@ int shard_alloc(psim_handle* h, Shard* s) {
         HIP_TRY(hipEventCreateWithFlags(&s->join_ev[k], hipEventDisableTiming));
     }
     HIP_TRY(hipEventCreateWithFlags(&s->fork_ev, hipEventDisableTiming));
-    if (s->n > (1u << 26))      // route buckets of 8192 destinations: 128 KiB of LDS per block
-        HIP_TRY(hipFuncSetAttribute((const void*)k_bucket_route, hipFuncAttributeMaxDynamicSharedMemorySize,
+    if (s->n > (1u << 26)) {    // route buckets of 8192 destinations: 128 KiB of LDS per block
+        HIP_TRY(hipFuncSetAttribute((const void*)k_bucket_route<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                     8192 * 16));
+        HIP_TRY(hipFuncSetAttribute((const void*)k_bucket_route<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    8192 * 16));
+    }
     HIP_TRY(hipHostMalloc((void**)&s->pin, (size_t)PIN_STRIDE * (1 + BATCH_MAX) * sizeof(uint64_t), hipHostMallocMapped));
     HIP_TRY(hipHostGetDevicePointer((void**)&s->pin_dev, s->pin, 0));
     memset(s->pin, 0, (size_t)PIN_STRIDE * (1 + BATCH_MAX) * sizeof(uint64_t));
@@ -2396,7 +2627,7 @@ int shard_alloc(psim_handle* h, Shard* s) {
     rc |= s->ctl.alloc(2);
     rc |= s->stat_tile.alloc((size_t)STAT_TILES * NST);
     rc |= s->ikeys.alloc(1024); rc |= s->ivals.alloc(1024);
-    rc |= s->recvbuf.alloc(1024); rc |= s->inbox.alloc(1024); rc |= s->outbox.alloc(1024);
+    rc |= s->recvh.alloc(1024); rc |= s->recvt.alloc(1024); rc |= s->wseg.alloc(130); rc |= s->inbox.alloc(1024); rc |= s->outbox.alloc(1024);
     if (h->cfg.manager == PSIM_MANAGER_PLUGGABLE) {
         if (h->cfg.strategy == PSIM_STRATEGY_FULL) {
             rc |= s->fbits.alloc(n * 2 * h->fw);     // [adds | removes] per node
@@ -2423,7 +2654,7 @@ void shard_free(Shard* s) {
     s->pt_eag.release(); s->pt_laz.release(); s->pt_out.release(); s->start.release(); s->conn.release();
     s->outx.release(); s->outx_top.release();
     s->pt_rt.release(); s->origin.release(); s->slots.release(); s->bc_roots.release(); s->bc_msgs.release();
-    s->ikeys.release(); s->ivals.release(); s->recvbuf.release(); s->inbox.release();
+    s->ikeys.release(); s->ivals.release(); s->recvh.release(); s->recvt.release(); s->wseg.release(); s->inbox.release();
     if (s->pin) (void)hipHostFree(s->pin);
     if (s->wait_ev) (void)hipEventDestroy(s->wait_ev);
     s->wait_ev = nullptr;
@@ -3298,6 +3529,13 @@ int psim_restore(psim_handle* h, const void* buf, size_t size) {
     h->pend_join_mark.assign(h->pend_join_mark.size(), 0);
     h->pend_part_set = h->pend_part_clear = false;
     h->pend_b_root.clear(); h->pend_b_msg.clear();
+    return PSIM_OK;
+}
+
+int psim_get_exchange_stats(psim_handle* h, uint64_t* records, uint64_t* bytes) {
+    if (!h || !records || !bytes) return PSIM_EINVAL;
+    *records = h->x_records;
+    *bytes = h->x_bytes;
     return PSIM_OK;
 }
 

@@ -351,6 +351,13 @@ class Simulator(_Driver):
         buf = C.create_string_buffer(bytes(data), len(data))
         self._check(self._extra["restore"](self._h, buf, len(data)), "restore")
 
+    def exchange_stats(self):
+        """(records, wire bytes) this process's shards sent to other shards
+        since creation (psim_get_exchange_stats)."""
+        r, b = C.c_uint64(), C.c_uint64()
+        self._check(self._extra["get_exchange_stats"](self._h, C.byref(r), C.byref(b)), "get_exchange_stats")
+        return r.value, b.value
+
     def kernel_times(self):
         cap = 64
         names = (C.c_char_p * cap)()

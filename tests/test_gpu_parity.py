@@ -175,6 +175,11 @@ def test_shard_count_invariance(shards):
     os_, ost = S.churn_partition(Oracle, n=2048)
     S.compare_stats(gst, ost)
     S.compare_nodes(gs.nodes(), os_.nodes())
+    # the wire format: 32 B a record, 32 more for one with exchange ids
+    # (SHUFFLE / SHUFFLE_REPLY) -- fewer bytes than the 64-B records, and
+    # at least every record's head
+    xr, xb = gs.exchange_stats()
+    assert xr > 0 and 32 * xr < xb < 64 * xr
 
 
 @pytest.mark.parametrize("shards", [2, 4])
