@@ -347,12 +347,8 @@ DEV void flush_full(Wv& w) {
 DEV bool connect_ok(const Wv& w, uint32_t dst) {
     if (dst >= kargs().n_nodes || dst == w.me) return false;
     uint64_t m = ballot(w.CV == dst);
-    if (m) {
-        const uint32_t v = rl(w.CF, ffs64(m));
-        return (v & F_UP) && (v >> 8) == w.mypart;
-    }
-    if (kargs().upart) return kargs().upart[dst] == w.mypart;   // (UPART_DOWN matches no group)
-    const uint32_t v = (uint32_t)kargs().flags[dst] | ((uint32_t)kargs().part[dst] << 8);
+    uint32_t v = m ? rl(w.CF, ffs64(m))
+                   : ((uint32_t)kargs().flags[dst] | ((uint32_t)kargs().part[dst] << 8));
     return (v & F_UP) && (v >> 8) == w.mypart;
 }
 
@@ -1330,20 +1326,14 @@ DEV uint32_t conn_cache_id(uint32_t CN, uint32_t H) {
     return l >= 40 && l < 48 && l - 40 < cn && !(e & (PSIM_CONN_DOWN | PSIM_CONN_CLOSING)) ? e : NONE;
 }
 
-// flag | partition << 8 of the view members in CV (the connection cache):
-// F_UP and the partition from the up-and-partition pair (one 2-B read on one
-// random line, not a flag byte and a partition byte on two: at 2^26 nodes a
-// k_consume node read 96 random lines for its 48 cache lanes), F_CRASHED in
-// a crash round behind the L2 crash filter -- the only flag bits a handler
-// reads from the cache
+// flag | partition << 8 of the view members in CV (the connection cache)
+// (the passive lanes from the up-and-partition pairs, one 2-B read each
+// instead of a flag byte and a partition byte, measured slower at 2^26: E
+// 75.6 -> 76.1 ms a round, k_consume +0.3 ms, k_pt +0.2 -- the 128 MB pair
+// array caches worse than the flag bytes every kernel reads;
+// profiles/r05/ab_log.txt r5v)
 DEV uint32_t cache_flags(KArgs& a, uint32_t cv, uint32_t me) {
     const uint32_t ca = cv < a.n_nodes ? cv : me;
-    if (a.upart) {
-        const uint32_t u = a.upart[ca];
-        uint32_t v = u == UPART_DOWN ? 0u : (F_UP | (u << 8));
-        if (a.crash_round && crashed_now(a, ca)) v |= F_CRASHED;
-        return cv < a.n_nodes ? v : 0u;
-    }
     const uint32_t f = a.flags[ca], pt = a.part[ca];
     return cv < a.n_nodes ? (f | (pt << 8)) : 0u;
 }
