@@ -360,6 +360,10 @@ int psim_leave(psim_handle *h, const uint32_t *nodes, size_t n);
  * reported by the target's rank is all-gathered after the round.
  * PSIM_EUNSUPPORTED for HyParView handles. */
 int psim_leave_node(psim_handle *h, const uint32_t *actors, const uint32_t *targets, size_t n);
+/* group[i]: node i's partition group, 0..PSIM_PARTITION_MAX (PSIM_EINVAL for
+ * any other value); nodes in different groups cannot exchange messages from
+ * the next round on (partisan_SUITE's partition injection). */
+#define PSIM_PARTITION_MAX 254
 int psim_set_partition(psim_handle *h, const uint8_t *group, size_t n);
 /* View order.  Views are kept in sets:to_list/1 order of
  * OTP's sets v1, a linear hash table (stdlib sets.erl: 16 slots up to 80

@@ -1917,6 +1917,8 @@ int orc_leave_node(struct psim_handle *h, const uint32_t *actors, const uint32_t
 
 int orc_set_partition(struct psim_handle *h, const uint8_t *group, size_t n) {
     if (n != h->N) return PSIM_EINVAL;
+    for (size_t i = 0; i < n; i++)
+        if (group[i] > PSIM_PARTITION_MAX) return PSIM_EINVAL;
     memcpy(h->pend_part, group, n);
     h->pend_part_set = 1; h->pend_part_clear = 0;
     return PSIM_OK;

@@ -818,7 +818,7 @@ __global__ void __launch_bounds__(BLK) k_node_prep(RoundArgs a, const unsigned l
     // global id: the flag and partition arrays are replicated)
     if (a.upart && a.upart_dirty)
         for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g < a.n_nodes; g += gridDim.x * blockDim.x)
-            a.upart[g] = (a.flags[g] & F_UP) ? (uint16_t)a.part[g] : UPART_DOWN;
+            a.upart[g] = (a.flags[g] & F_UP) ? (upart_t)a.part[g] : UPART_DOWN;
     unsigned long long up = 0, drop = 0, bs = 0, ws = 0;   // this thread's sums (wave-summed below)
     // block b takes the nodes [b * per, (b + 1) * per), blockDim at a time
     // (coalesced), so that its sums are a contiguous tile of the scan below
@@ -1354,7 +1354,7 @@ struct Shard {
     hipStream_t stream = nullptr;
     // replicated (global id)
     DBuf<uint8_t> flags, part;
-    DBuf<uint16_t> upart;               // k_node_prep's up-and-partition pairs (RoundArgs::upart)
+    DBuf<upart_t> upart;                // k_node_prep's up-and-partition pairs (RoundArgs::upart)
     DBuf<uint32_t> crash_bits;   // RoundArgs::crash_bits
     DBuf<uint8_t> btab;          // RoundArgs::btab (psim_set_bucket_table), global id
     // local rows
@@ -2922,6 +2922,8 @@ int psim_leave_node(psim_handle* h, const uint32_t* actors, const uint32_t* targ
 
 int psim_set_partition(psim_handle* h, const uint8_t* group, size_t n) {
     if (!h || !group || n != h->N) return PSIM_EINVAL;
+    for (size_t i = 0; i < n; i++)
+        if (group[i] == PSIM_PARTITION_MAX + 1) return PSIM_EINVAL;   // (255: the pair array's "down")
     h->pend_part.assign(group, group + n);
     h->pend_part_set = true; h->pend_part_clear = false;
     return PSIM_OK;

@@ -4,6 +4,20 @@
 
 namespace psim {
 
+// the up-and-partition pair of a node (RoundArgs::upart): its partition
+// group while it is up, UPART_DOWN if not -- one byte (groups 0..254:
+// psim_set_partition), so the array is the size of the flag bytes (64 MB at
+// 2^26 nodes) and caches as well; PSIM_UPART8=0 keeps round 4's 2-byte pairs
+// (A/B builds)
+#ifndef PSIM_UPART8
+#define PSIM_UPART8 1
+#endif
+#if PSIM_UPART8
+typedef uint8_t upart_t;
+#else
+typedef uint16_t upart_t;
+#endif
+
 struct RoundArgs {
     // config
     uint32_t n_nodes, round;
@@ -25,7 +39,7 @@ struct RoundArgs {
     // instead of a flag byte and a partition byte on two random lines (k_ptl:
     // eight members a node, 63 GB a round at 2^26 before; k_relay, k_shuf,
     // k_lite_half likewise; HyParView / X-BOT handles only)
-    uint16_t* upart;
+    upart_t* upart;
     // this round's crashed ids, one bit per CRASH_GRAIN ids (replicated,
     // zero outside crash rounds): a filter in L2 in front of the flag bytes
     const uint32_t* crash_bits;
@@ -168,7 +182,7 @@ uint32_t ptl_grid();
 // loads per node from HBM, 5 ms a crash round at 2^26 nodes; the 512 KB
 // filter answers ~97 % of them from L2 -- 134k crashes in 4M grains)
 constexpr uint32_t CRASH_GRAIN_SHIFT = 4;
-constexpr uint16_t UPART_DOWN = 0x100;
+constexpr upart_t UPART_DOWN = (upart_t)(PSIM_UPART8 ? 0xFFu : 0x100u);
 __device__ __forceinline__ bool crash_filter(const uint32_t* bits, uint32_t id) {
     const uint32_t g = id >> CRASH_GRAIN_SHIFT;
     return (bits[g >> 5] >> (g & 31)) & 1u;

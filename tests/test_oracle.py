@@ -193,6 +193,19 @@ def test_plumtree_off():
     assert S.connected(S.active_graph(sim.nodes()))
 
 
+def test_partition_groups_0_to_254():
+    """psim_set_partition takes groups 0..PSIM_PARTITION_MAX (254): 255 is
+    the engine's down mark in its one-byte up-and-partition pairs"""
+    from partisan_amd.sim import SimError
+    n = 64
+    sim = Oracle(default_config(n_nodes=n, seed=3))
+    g = np.full(n, 254, np.uint8)
+    sim.set_partition(g)
+    g[5] = 255
+    with pytest.raises(SimError):
+        sim.set_partition(g)
+
+
 def test_partition_blocks_cross_traffic():
     n = 512
     sim = Oracle(default_config(n_nodes=n, seed=3))
