@@ -1327,11 +1327,10 @@ DEV uint32_t conn_cache_id(uint32_t CN, uint32_t H) {
 }
 
 // flag | partition << 8 of the view members in CV (the connection cache)
-// (the passive lanes from the up-and-partition pairs, one 2-B read each
+// (the passive lanes from the up-and-partition pairs, one read each
 // instead of a flag byte and a partition byte, measured slower at 2^26: E
-// 75.6 -> 76.1 ms a round, k_consume +0.3 ms, k_pt +0.2 -- the 128 MB pair
-// array caches worse than the flag bytes every kernel reads;
-// profiles/r05/ab_log.txt r5v)
+// 75.6 -> 76.1 ms a round with 2-B pairs, 75.0 -> 75.4 with 1-B pairs
+// (k_consume -0.1 ms, k_pt +0.2); profiles/r05/ab_log.txt r5v, r5x)
 DEV uint32_t cache_flags(KArgs& a, uint32_t cv, uint32_t me) {
     const uint32_t ca = cv < a.n_nodes ? cv : me;
     const uint32_t f = a.flags[ca], pt = a.part[ca];
