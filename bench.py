@@ -74,6 +74,9 @@ def parse():
     p.add_argument("--vshards", type=int, default=1,
                    help="diagnostic: G virtual shards of --nodes each on this one GPU (the sharded "
                         "partition / exchange / receive path with device copies instead of RCCL)")
+    p.add_argument("--kernel-counts", action="store_true",
+                   help="diagnostic (profiles/run_pmc.sh): one round per step call, and each node-round kernel's "
+                        "nodes, deliveries and emissions (psim_debug_kernel_counts) -> per_kernel_alg")
     p.add_argument("--strict", action="store_true",
                    help="cfg.strict = 1: a fixed-table overflow fails the round (PSIM_ECAPACITY) and the run")
     p.add_argument("--rank-path", action="store_true",
@@ -638,14 +641,18 @@ def main():
     stats = []
     kt = {}
     i = 0
+    kc = {}                                           # --kernel-counts: per kernel (nodes, in, out)
     while i < args.steps:
         # rounds up to the next one with host events run in one step call
         round_events(t_start + i)
         k = 1
-        while i + k < args.steps and not has_events(t_start + i + k):
+        while i + k < args.steps and not has_events(t_start + i + k) and not args.kernel_counts:
             k += 1
         stats.append(step(k))
         i += k
+        if args.kernel_counts:
+            for name, v in sim.kernel_counts().items():
+                kc[name] = tuple(a + b for a, b in zip(kc.get(name, (0, 0, 0)), v))
         for name, (ms, cnt) in sim.kernel_times().items():
             a, b = kt.get(name, (0.0, 0))
             kt[name] = (a + ms, b + cnt)
@@ -729,6 +736,13 @@ def main():
         "overflow": int(st["overflow"].sum()),
         "pmc_key": key,
     }
+    if kc:
+        # each node-round kernel's share of the algorithmic bytes (the formula
+        # above, with the kernel's own counts: its nodes processed, records
+        # delivered and emitted), per round
+        out["per_kernel_alg"] = {k: (v[0] * 2 * S_NODE + v[1] * S_MSG + v[2] * (S_MSG + 4)) / args.steps
+                                 for k, v in kc.items()}
+        out["per_kernel_counts"] = {k: [x / args.steps for x in v] for k, v in kc.items()}
     if world > 1 or args.vshards > 1 or args.rank_path:
         # the cross-shard exchange over the window, this rank's shards: records
         # sent to another shard and their wire bytes (32 B a record, 32 more

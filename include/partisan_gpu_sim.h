@@ -507,6 +507,13 @@ int psim_wire_encode(const uint32_t rec[16], const psim_wire_names *names, uint8
 int psim_wire_decode(const uint8_t *buf, size_t len, const psim_wire_names *names, uint32_t dst, uint32_t rec[16],
                      size_t *used);
 
+/* Diagnostic: per node-round kernel of the last round (k_relay, k_shuf,
+ * k_lite_half, k_consume, k_ptl, k_pt; this process's first shard), 4 words
+ * each: nodes processed, records delivered, records emitted, 0 -- the
+ * kernel's share of the algorithmic bytes (bench.py --kernel-counts,
+ * profiles/pmc_record.py).  Returns 6 (0 under the pluggable manager). */
+int psim_debug_kernel_counts(psim_handle *h, uint64_t *out, int cap);
+
 /* Per-kernel device time (ms) accumulated over the last psim_step call:
  * names[i] is a static string; returns the number of entries. */
 int psim_kernel_times(psim_handle *h, const char **names, double *ms, uint64_t *launches, int cap);

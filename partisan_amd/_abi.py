@@ -165,6 +165,7 @@ GPU_ONLY = {
     "snapshot": (C.c_int, [_H, C.c_void_p, C.c_size_t, C.POINTER(C.c_size_t)]),
     "restore": (C.c_int, [_H, C.c_void_p, C.c_size_t]),
     "get_exchange_stats": (C.c_int, [_H, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
+    "debug_kernel_counts": (C.c_int, [_H, C.POINTER(C.c_uint64), C.c_int]),
 }
 
 

@@ -3552,6 +3552,36 @@ int psim_kernel_times(psim_handle* h, const char** names, double* ms, uint64_t* 
     return k;
 }
 
+// diagnostic: per node-round kernel of the last round (shard 0's blocks; the
+// stats rows every block leaves, before the route sums them), in the order
+// k_relay, k_shuf, k_lite_half / k_consume_lite, k_consume, k_ptl / k_ptq,
+// k_pt: out[4 k] nodes processed (stats nodes_processed), out[4 k + 1]
+// records delivered, out[4 k + 2] records emitted, out[4 k + 3] 0.  Returns
+// the number of kernels (6); 0 for the pluggable manager's one kernel.
+int psim_debug_kernel_counts(psim_handle* h, uint64_t* out, int cap) {
+    if (!h || !out || cap < 24) return PSIM_EINVAL;
+    if (h->cfg.manager == PSIM_MANAGER_PLUGGABLE) return 0;
+    Shard* s = h->shards[0];
+    const uint32_t rows = s->pgrid + s->cgrid + s->rgrid + s->tgrid + s->sgrid + s->lgrid + s->qgrid;
+    std::vector<uint64_t> st((size_t)rows * NST);
+    HIP_TRY(hipStreamSynchronize(s->stream));
+    HIP_TRY(hipMemcpy(st.data(), s->stat_part.p, st.size() * 8, hipMemcpyDeviceToHost));
+    // row ranges (make_args: prepare, consume, relay, pt, shuf, lite, ptl)
+    const uint32_t b_cons = s->pgrid, b_rel = b_cons + s->cgrid, b_pt = b_rel + s->rgrid, b_sh = b_pt + s->tgrid,
+                   b_li = b_sh + s->sgrid, b_pl = b_li + s->lgrid, b_end = b_pl + s->qgrid;
+    const uint32_t rng[6][2] = {{b_rel, b_pt}, {b_sh, b_li}, {b_li, b_pl}, {b_cons, b_rel}, {b_pl, b_end}, {b_pt, b_sh}};
+    for (int k = 0; k < 6; k++) {
+        uint64_t v[3] = {0, 0, 0};
+        for (uint32_t r = rng[k][0]; r < rng[k][1]; r++) {
+            const uint64_t* row = st.data() + (size_t)r * NST;
+            v[0] += row[ST_PROC];
+            for (int t = 0; t < ST_NTYPES; t++) { v[1] += row[ST_DELIV + t]; v[2] += row[ST_EMIT + t]; }
+        }
+        out[4 * k] = v[0]; out[4 * k + 1] = v[1]; out[4 * k + 2] = v[2]; out[4 * k + 3] = 0;
+    }
+    return 6;
+}
+
 // diagnostic: per-phase s_memtime sums of k_consume / k_pt, k_consume_lite and
 // k_lite_half (96 entries; 0 returned unless built with -DPSIM_STAMPS)
 int psim_debug_stamps(unsigned long long* out, int cap) {

@@ -54,6 +54,11 @@ def main():
            "fetch_size_bytes": fetch, "write_size_bytes": write,
            "alg_bytes_per_launch": bench["roofline"]["alg_bytes_per_launch"],
            "per_kernel": by,              # FETCH_SIZE + WRITE_SIZE per round, by kernel
+           # each kernel's algorithmic bytes per round (bench.py --kernel-counts:
+           # its own nodes processed, deliveries, emissions) and counted / algorithmic
+           "per_kernel_alg": bench.get("per_kernel_alg"),
+           "per_kernel_excess": ({k: by[k] / a for k, a in bench["per_kernel_alg"].items() if a and k in by}
+                                 if bench.get("per_kernel_alg") else None),
            "source": "FETCH_SIZE + WRITE_SIZE per timed round of the node-round kernels, separate "
                      "rocprofv3 --pmc passes of this command (profiles/run_pmc.sh); FETCH_SIZE uncorrected: "
                      "random 64-B requests count exactly (profiles/calib/)"}

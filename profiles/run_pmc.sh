@@ -12,7 +12,7 @@ mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
 for c in FETCH_SIZE WRITE_SIZE; do
   timeout -s KILL 300 rocprofv3 --pmc $c --kernel-include-regex "k_relay|k_shuf|k_consume|k_lite|k_term|k_pt" -d $OUT/$c -o run \
-    --output-format csv -- python3 $R/bench.py --no-cpu-baseline "$@" > $OUT/$c.json 2> $OUT/$c.err \
+    --output-format csv -- python3 $R/bench.py --no-cpu-baseline --kernel-counts "$@" > $OUT/$c.json 2> $OUT/$c.err \
     || { echo "$c pass failed"; tail -3 $OUT/$c.err; exit 1; }
 done
 cd $R
