@@ -353,7 +353,14 @@ DEV void pas_insert(Hn& x, uint32_t& PB, uint32_t t, uint32_t b) {
 // eviction the draws are taken together (lane i: the i-th eviction's index);
 // one the ?uniform_range test would reject (p ~ 2^-53) sends the half down
 // the step-by-step draws instead.
-DEV void merge_exchange(Hn& x, Hw& w, uint32_t EX, uint32_t nex) {
+// sorted: EX is already usort'ed -- a SHUFFLE's exchange (hv:586: every
+// shuffle start sends lists:usort(Exchange0), and relays pass it on
+// unchanged) -- so the candidates are its valid lanes in order, compacted
+// through LDS (no 8 x 8 swizzle rank: terminals are half of the merges)
+#ifndef PSIM_MERGE_SORTED     // (0: every merge through husort, for A/B)
+#define PSIM_MERGE_SORTED 1
+#endif
+DEV void merge_exchange(Hn& x, Hw& w, uint32_t EX, uint32_t nex, bool sorted) {
     KArgs& a = kargs();
     const uint32_t l = hl_id();
     bool in_act = false;
@@ -362,7 +369,20 @@ DEV void merge_exchange(Hn& x, Hw& w, uint32_t EX, uint32_t nex) {
         in_act |= ((uint32_t)J < x.act_n) & (aj == EX);
     });
     uint32_t T = EX;
-    const uint32_t mt = husort(w, T, l < nex && EX != x.me && !in_act);
+    const bool valid = l < nex && EX != x.me && !in_act;
+    uint32_t mt;
+    if (PSIM_MERGE_SORTED && sorted) {
+        const uint32_t vm = hmask(valid);
+        uint32_t* sc = w.scr + hb_id();
+        if (valid) sc[__popc(vm & ((1u << l) - 1u))] = EX;
+        __builtin_amdgcn_wave_barrier();
+        mt = (uint32_t)__popc(vm);
+        const uint32_t got = sc[l];
+        __builtin_amdgcn_wave_barrier();
+        T = l < mt ? got : 0u;
+    } else {
+        mt = husort(w, T, valid);
+    }
     if (!mt) return;
     const uint32_t maxp = a.max_passive;
     const uint8_t* bt = a.btab;
@@ -536,7 +556,7 @@ DEV void body(Hn& x, Hw& w, Hc& c, const HIn& in) {
                 hv_send(x, w, c, p, PSIM_MSG_SHUFFLE_REPLY, 0, RESP, nr);
                 HSTAMP(w, 3);
             }
-            merge_exchange(x, w, ex, nex);
+            merge_exchange(x, w, ex, nex, !reply);
             HSTAMP(w, 4);
         }
       }
