@@ -678,7 +678,7 @@ DEV void out_drop_peer(Wv& w, uint32_t e) {
     const uint64_t rest = shfl64(T, (int)((l + sh) & 63));
     T = l + sh < k2 ? rest : 0ull;
     w.out_n = k1 + k2;
-    if (w.out_n > OUT_HEAD) *out_tail(w) = T;
+    *out_tail(w) = T;                                 // (zeros past the table: a getter reads the row)
 }
 
 // notify/1 (hv:1598-1599) -> plumtree update/1 -> handle_cast({update, ..})

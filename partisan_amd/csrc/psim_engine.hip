@@ -46,7 +46,7 @@ constexpr uint32_t PREP_BLK = 1024;   // k_desc blocks (at most PREP_BLK of them
 constexpr uint32_t DESC_RANGES = 4;   // k_node_prep ranges a k_desc block takes (at most DESC_RANGES * PREP_BLK)
 // pinned host words per shard (Shard::pin): NST stats, the consume span, the
 // outbox total, the routed record count -- stored by kernels, read by the host
-enum { PIN_TOTAL = NST + 2, PIN_M = NST + 3, PIN_OVF = NST + 4, PIN_BIGIN = NST + 5 };
+enum { PIN_TOTAL = NST + 2, PIN_M = NST + 3, PIN_OVF = NST + 4, PIN_BIGIN = NST + 5, PIN_OUTX = NST + 6 };
 // the pinned words: slot 0 holds the above (and a single round's stats);
 // slot j + 1 the stats and node-round span of round j of a batch (run_batch)
 constexpr uint32_t PIN_STRIDE = NST + 8;
@@ -339,6 +339,8 @@ struct StatsIn {
     uint64_t* tiles;
     uint64_t* out;             // the shard's stat_out (NST sums, then the span)
     uint64_t* hout;            // its pinned words
+    const uint32_t* outx_top;  // the outstanding pool's rows taken (-> pinned slot 0, PIN_OUTX; may be null)
+    uint64_t* hout0;           // pinned slot 0
 };
 // (red: the block's [waves][64] words of LDS; every thread calls these)
 __device__ __forceinline__ void stats_tile(const StatsIn& st, uint32_t t, uint64_t (*red)[64]) {
@@ -376,7 +378,11 @@ __device__ __forceinline__ void stats_final(const StatsIn& st, uint64_t (*red)[6
         st.out[c] = u;
         st.hout[c] = u;
     }
-    if (threadIdx.x == 0) { st.hout[NST] = st.out[NST]; st.hout[NST + 1] = st.out[NST + 1]; }
+    if (threadIdx.x == 0) {
+        st.hout[NST] = st.out[NST];
+        st.hout[NST + 1] = st.out[NST + 1];
+        if (st.outx_top) st.hout0[PIN_OUTX] = *st.outx_top;
+    }
     __syncthreads();
 }
 
@@ -2030,7 +2036,8 @@ int route_group(psim_handle* h, Shard* s, bool dense, uint32_t m) {
     const uint32_t rows = s->pgrid + s->cgrid + s->rgrid + s->tgrid + s->sgrid + s->lgrid + s->qgrid;
     const StatsIn st{s->stat_part.p, rows,
                      std::min<uint32_t>(nblk, std::min<uint32_t>(STAT_TILES, std::max<uint32_t>(1, rows / 32))),
-                     s->stat_tile.p, s->stat_out.p, s->pin_dev + (size_t)s->stat_slot * PIN_STRIDE};
+                     s->stat_tile.p, s->stat_out.p, s->pin_dev + (size_t)s->stat_slot * PIN_STRIDE,
+                     s->outx.p ? s->outx_top.p : nullptr, s->pin_dev};
     KTimer t(h, s, KT_SORT);
     if (dense)
         k_bucket_hist<true><<<nblk, RB_STEP, lds_h, s->stream>>>(in, nsteps, nb, wshift, s->hist.p, s->ctl.p,
@@ -2611,7 +2618,13 @@ int shard_alloc(psim_handle* h, Shard* s) {
     // under config E with the partition after the churn ~10 % of the nodes
     // pass 16 entries by phase round 230 (oracle, 2^16); at 1/32 the pool ran
     // out at 2^26
-    if (h->cfg.manager != PSIM_MANAGER_PLUGGABLE) rc |= s->outx.alloc(std::max<size_t>(1024, n / 8) * OUT_EXT);
+    if (h->cfg.manager != PSIM_MANAGER_PLUGGABLE) {
+        // rows for 1/8 of the nodes to start with (grow_outx doubles it);
+        // PSIM_OUTX_ROWS sets another start (tests of the growth)
+        size_t rows = std::max<size_t>(1024, n / 8);
+        if (const char* e = getenv("PSIM_OUTX_ROWS")) rows = std::max<size_t>(1, (size_t)atoll(e));
+        rc |= s->outx.alloc(rows * OUT_EXT);
+    }
     rc |= s->outx_top.alloc(1);
     rc |= s->ocnt.alloc(n); rc |= s->cb.alloc(n + 1);
     rc |= s->in_beg.alloc(n + 1); rc |= s->bound.alloc(n + 1); rc |= s->pscan.alloc(4097); rc |= s->obase.alloc(n + 1);
@@ -3036,6 +3049,28 @@ int psim_broadcast(psim_handle* h, uint32_t root, uint32_t msg_id) {
     return PSIM_OK;
 }
 
+// The outstanding tables' extension pool: a node takes a row for good the
+// first time its table outgrows its own row, so the pool doubles at a round
+// boundary once half of it is taken (read from the pinned word the route's
+// stats pass leaves) -- up to a row per node, which never runs out.  A failed
+// growth is reported once and leaves the pool as it is (a table that then
+// finds no row counts a PSIM_OVF_PT_OUT overflow; cfg.strict fails the step).
+int grow_outx(Shard* s) {
+    if (!s->outx.p) return PSIM_OK;
+    const uint64_t rows = s->outx.n / OUT_EXT, used = std::min<uint64_t>(s->pin[PIN_OUTX], rows);
+    if (rows >= s->n || used * 2 < rows) return PSIM_OK;
+    const uint64_t want = std::min<uint64_t>(std::max<uint64_t>(2 * rows, used + 1024), s->n);
+    if (s->outx.ensure_keep(want * OUT_EXT, used * OUT_EXT, s->stream) != PSIM_OK) {
+        static bool told = false;
+        if (!told) std::fprintf(stderr, "psim: the outstanding pool could not grow past %llu rows\n",
+                                (unsigned long long)rows);
+        told = true;
+        return PSIM_OK;
+    }
+    HIP_TRY(hipMemsetAsync(s->outx.p + used * OUT_EXT, 0, (s->outx.n - used * OUT_EXT) * 8, s->stream));
+    return PSIM_OK;
+}
+
 int psim_step(psim_handle* h, uint32_t n_rounds, psim_round_stats* stats) {
     if (!h) return PSIM_EINVAL;
     if (h->failed) return PSIM_ESTATE;
@@ -3046,6 +3081,8 @@ int psim_step(psim_handle* h, uint32_t n_rounds, psim_round_stats* stats) {
             uint32_t done = 0;
             int rc = run_batch(h, std::min<uint32_t>(n_rounds - i, BATCH_MAX), stats ? stats + i : nullptr, &done);
             if (rc) { h->failed = true; return rc; }
+            for (Shard* s : h->shards)
+                if ((rc = grow_outx(s))) { h->failed = true; return rc; }
             i += done;
             continue;
         }
@@ -3053,6 +3090,8 @@ int psim_step(psim_handle* h, uint32_t n_rounds, psim_round_stats* stats) {
         uint64_t r = h->round;
         int rc = run_round(h, st);
         if (rc) { h->failed = true; return rc; }
+        for (Shard* s : h->shards)
+            if ((rc = grow_outx(s))) { h->failed = true; return rc; }
         if (stats) fill_stats(st, r, &stats[i]);
         if (h->cfg.strict && st[ST_OVF]) return PSIM_ECAPACITY;   // cfg.strict: fail loudly
         i++;
@@ -3141,7 +3180,8 @@ static int get_shard_nodes(Shard* s, uint32_t first, uint32_t count, psim_node_v
         memcpy(v->pt_lazy, &laz[(size_t)k * RT_SET], sizeof v->pt_lazy);
         const uint32_t ox = x.pad1[3];
         for (uint32_t j = 0; j < PSIM_PT_OUT_CAP; j++) {
-            const uint64_t o = j < OUT_IN ? po[(size_t)k * OUT_IN + j]
+            const uint64_t o = j >= x.out_n ? 0ull
+                             : j < OUT_IN ? po[(size_t)k * OUT_IN + j]
                              : ox && ox <= otop ? xo[(size_t)(ox - 1) * OUT_EXT + j - OUT_IN] : 0ull;
             v->pt_out_peer[j] = (uint32_t)(o >> 32);
             v->pt_out_msg[j] = (uint32_t)(o >> 16) & 0xFFFFu;
@@ -3502,7 +3542,15 @@ int psim_restore(psim_handle* h, const void* buf, size_t size) {
             HIP_TRY(hipMemcpy(s->pay_top.p, &sh.pay_rows, 4, hipMemcpyHostToDevice));
         if ((size_t)sh.pad[1] * IDMAP_EXT > s->mapx.n) return PSIM_EINVAL;
         HIP_TRY(hipMemcpy(s->mapx_top.p, &sh.pad[1], 4, hipMemcpyHostToDevice));
-        if ((size_t)sh.out_rows * OUT_EXT > s->outx.n) return PSIM_EINVAL;
+        if (sh.out_rows && !s->outx.p) return PSIM_EINVAL;
+        if (s->outx.p) {
+            // (a grown pool: this handle's grows to hold the snapshot's rows;
+            // the rows past them zeroed, as a fresh pool's are)
+            TRY(s->outx.ensure((size_t)sh.out_rows * OUT_EXT));
+            HIP_TRY(hipMemset(s->outx.p + (size_t)sh.out_rows * OUT_EXT, 0,
+                              (s->outx.n - (size_t)sh.out_rows * OUT_EXT) * 8));
+            s->pin[PIN_OUTX] = sh.out_rows;
+        }
         HIP_TRY(hipMemcpy(s->outx_top.p, &sh.out_rows, 4, hipMemcpyHostToDevice));
         for (const Section& x : snap_sections(h, s, sh)) {
             if ((size_t)(end - o) < x.bytes) return PSIM_EINVAL;

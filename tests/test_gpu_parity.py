@@ -63,6 +63,27 @@ def test_outstanding_tail_parity(kw):
     S.compare_nodes(gs.nodes(), os_.nodes())
 
 
+def test_outstanding_pool_growth(monkeypatch):
+    """The outstanding tables' extension pool starting at 8 rows
+    (PSIM_OUTX_ROWS): grow_outx doubles it at round boundaries as nodes take
+    rows, with no overflow and GPU == oracle through the tables' largest
+    (a snapshot of the grown pool restores into a fresh handle)"""
+    monkeypatch.setenv("PSIM_OUTX_ROWS", "8")
+    gs, gst, gsn = S.out_tail(_gpu)
+    os_, ost, osn = S.out_tail(Oracle)
+    S.compare_stats(gst, ost)
+    for r in osn:
+        S.compare_nodes(gsn[r], osn[r])
+    assert int(gst["overflow"].sum()) == 0
+    assert int((osn[79]["pt_out_n"] > 16).sum()) > 8      # more rows than the pool started with
+    snap = gs.snapshot()
+    monkeypatch.setenv("PSIM_OUTX_ROWS", "8")
+    from partisan_amd.sim import default_config
+    fresh = _gpu(default_config(n_nodes=512, seed=3))
+    fresh.restore(snap)
+    S.compare_nodes(fresh.nodes(), os_.nodes())
+
+
 def test_lingering_connections_parity():
     """connections beyond the active view -- shuffle
     terminals' Senders, rejected and pending neighbor requests, a joiner's
