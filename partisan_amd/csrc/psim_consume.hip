@@ -2305,7 +2305,7 @@ __global__ void __launch_bounds__(256, PSIM_RELAY_WAVES) k_relay(RoundArgs) {
         // the list appends' barriers so that their latency hides behind them
         // (read per relay, after its draw, they were one dependent load each)
         uint32_t upm[4] = {NONE, NONE, NONE, NONE};   // member j's pair in bits 16 (j & 1) of word j >> 1
-        if (P < na && relay) {
+        if (P < na && (relay || lite)) {
             const uint32_t av[8] = {act0.x, act0.y, act0.z, act0.w, act1.x, act1.y, act1.z, act1.w};
             KArgs& a = kargs();
 #pragma unroll
@@ -2361,6 +2361,14 @@ __global__ void __launch_bounds__(256, PSIM_RELAY_WAVES) k_relay(RoundArgs) {
                     desc[k == 5 || k == 6 ? nl - 1 - at : k == 7 ? nl + at : k == 8 ? 2 * nl - 1 - at : at] =
                         k == 0 && maps ? make_uint4(D.x, D.y, D.z | DESC_MAPS_BIT, D.w) : D;
                 }
+        }
+        if (P < na && lite && !heavy) {
+            // the lite node's connection bits (k_lite_half's connect_ok)
+            uint32_t cm = 0;
+#pragma unroll
+            for (int j = 0; j < 8; j++)
+                cm |= ((upm[j >> 1] >> (16 * (j & 1))) & 0xFFFFu) == me_part ? 1u << j : 0u;
+            kargs().lite_cm[D.x - kargs().lo] = (uint8_t)cm;
         }
         if (P >= na || heavy || lite) continue;
         const uint32_t id = D.x;

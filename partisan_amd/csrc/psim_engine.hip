@@ -1361,6 +1361,7 @@ struct Shard {
     // replicated (global id)
     DBuf<uint8_t> flags, part;
     DBuf<upart_t> upart;                // k_node_prep's up-and-partition pairs (RoundArgs::upart)
+    DBuf<uint8_t> lite_cm;              // k_relay's connection bits of lite-list nodes (RoundArgs::lite_cm)
     DBuf<uint32_t> crash_bits;   // RoundArgs::crash_bits
     DBuf<uint8_t> btab;          // RoundArgs::btab (psim_set_bucket_table), global id
     // local rows
@@ -1530,6 +1531,7 @@ RoundArgs make_args(psim_handle* h, Shard* s) {
     a.slots = s->slots.p;
     a.flags = s->flags.p; a.part = s->part.p; a.hdr = s->hdr.p; a.crash_bits = s->crash_bits.p;
     a.upart = s->upart.p;
+    a.lite_cm = s->lite_cm.p;
     a.btab = h->btab ? s->btab.p : nullptr;
     a.act = s->act.p; a.pas = s->pas.p; a.sentm = s->sentm.p; a.recvm = s->recvm.p;
     a.mapx = s->mapx.p; a.mapx_top = s->mapx_top.p;
@@ -2593,7 +2595,7 @@ int shard_alloc(psim_handle* h, Shard* s) {
     const size_t N = h->N, n = std::max<uint32_t>(s->n, 1);
     int rc = 0;
     rc |= s->flags.alloc(N); rc |= s->part.alloc(N); rc |= s->hdr.alloc(n);
-    if (h->cfg.manager != PSIM_MANAGER_PLUGGABLE) rc |= s->upart.alloc(N);
+    if (h->cfg.manager != PSIM_MANAGER_PLUGGABLE) { rc |= s->upart.alloc(N); rc |= s->lite_cm.alloc(n); }
     rc |= s->crash_bits.alloc((N >> (CRASH_GRAIN_SHIFT + 5)) + 1);
     rc |= s->act.alloc(n * PSIM_ACTIVE_CAP); rc |= s->pas.alloc(n * PSIM_PASSIVE_CAP);
     rc |= s->sentm.alloc(n * IDMAP_IN); rc |= s->recvm.alloc(n * IDMAP_IN);
@@ -2660,7 +2662,7 @@ int shard_alloc(psim_handle* h, Shard* s) {
 
 void shard_free(Shard* s) {
     if (s->stream) (void)hipStreamSynchronize(s->stream);
-    s->flags.release(); s->part.release(); s->upart.release(); s->hdr.release(); s->crash_bits.release(); s->btab.release();
+    s->flags.release(); s->part.release(); s->upart.release(); s->lite_cm.release(); s->hdr.release(); s->crash_bits.release(); s->btab.release();
     s->act.release(); s->pas.release(); s->sentm.release(); s->recvm.release();
     s->pt_all.release(); s->pt_com.release();
     s->mapx.release(); s->mapx_top.release();

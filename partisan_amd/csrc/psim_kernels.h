@@ -40,6 +40,11 @@ struct RoundArgs {
     // eight members a node, 63 GB a round at 2^26 before; k_relay, k_shuf,
     // k_lite_half likewise; HyParView / X-BOT handles only)
     upart_t* upart;
+    // per local node of k_relay's lite list: bit j = active member j is up in
+    // this node's partition group (k_relay reads the pairs for it before its
+    // list appends; k_lite_half reads the byte with the node's rows, a node
+    // ahead, instead of eight dependent pair loads as the node starts)
+    uint8_t* lite_cm;
     // this round's crashed ids, one bit per CRASH_GRAIN ids (replicated,
     // zero outside crash rounds): a filter in L2 in front of the flag bytes
     const uint32_t* crash_bits;

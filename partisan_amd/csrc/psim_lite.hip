@@ -125,9 +125,9 @@ struct Hn {
     uint32_t act_n, pas_n;
     uint64_t rng;                    // the Philox draw counter
     uint32_t A, P;                   // lane hl: active[hl] (hl < 8), passive[hl]
-    uint32_t AF;                     // A's up-and-partition pairs (RoundArgs::upart: the connection
-                                     // cache, partition if up, UPART_DOWN if not); lane 31:
-                                     // the outbox's slots, obase[row + 1] - ob (out_cap)
+    uint32_t AF;                     // bit j: active member j is up in this node's group (k_relay's
+                                     // RoundArgs::lite_cm); bits 8..: the outbox's slots,
+                                     // obase[row + 1] - ob (out_cap), saturating at 2^24 - 1
     uint32_t seq, flushed;
     uint64_t dcb;                    // draw cache: lane hl holds the draw of counter dcb + hl
     uint32_t DCL, DCH;
@@ -136,10 +136,7 @@ constexpr uint32_t HF_PDIRTY = 16;  // Hn::fl: the passive view changed
 DEV uint32_t local_row(const Hn& x) { return x.me - kargs().lo; }
 // the node's outbox slots: no store goes past them (a record past the bound
 // is not stored -- the engine fails the round on the bound check)
-DEV uint32_t out_cap(const Hn& x) {
-    const uint32_t a = __builtin_amdgcn_readlane(x.AF, 31), b = __builtin_amdgcn_readlane(x.AF, 63);
-    return hb_id() ? b : a;
-}
+DEV uint32_t out_cap(const Hn& x) { return x.AF >> 8; }
 
 // a node's counters (each half counts its own node's; lane 0 of the half
 // adds them to the block's stats at the node's end), and the wave's digest
@@ -319,9 +316,8 @@ DEV bool connect_ok(const Hn& x, uint32_t dst) {
     KArgs& a = kargs();
     if (dst >= a.n_nodes || dst == x.me) return false;
     const uint32_t m = hmask(hl_id() < x.act_n && x.A == dst);
-    const uint32_t c = hget(x.AF, (uint32_t)__ffs(m) - 1);
-    const uint32_t v = m ? c : (uint32_t)a.upart[dst];
-    return v == ((x.fl >> 8) & 0xFFu);
+    if (m) return (x.AF >> (__ffs(m) - 1)) & 1u;
+    return (uint32_t)a.upart[dst] == ((x.fl >> 8) & 0xFFu);
 }
 
 // do_send_message/3 (hv:1274-1343) after maybe_connect: the dispatch draw of
@@ -462,6 +458,7 @@ DEV void merge_exchange(Hn& x, Hw& w, uint32_t EX, uint32_t nex, bool sorted) {
 struct HIn {
     uint4 D;
     uint32_t r0, r1, w9, A, P, part;
+    uint32_t cm, oe;                 // k_relay's connection bits; obase[row + 1] (low word)
     uint32_t SRC, TT;                // lane hl: sender and type word of inbox record hl
     uint32_t EX4;                    // lane hl: exchange id hl & 7 of inbox record hl >> 3
 };
@@ -483,13 +480,15 @@ DEV void load_rows(KArgs& a, HIn& in, bool live) {
     in.A = l < PSIM_ACTIVE_CAP ? a.act[li * PSIM_ACTIVE_CAP + l] : 0u;
     in.P = a.pas[li * PSIM_PASSIVE_CAP + l];
     in.part = a.part[live ? in.D.x : 0];
+    in.cm = a.lite_cm[li];
+    in.oe = reinterpret_cast<const uint32_t*>(a.obase + li + 1)[0];   // (totals < 2^32 slots)
 }
 // the descriptor's inbox heads (issued a node ahead)
 DEV HIn load_in(KArgs& a, const uint4& D) {
     const uint32_t l = hl_id();
     HIn in;
     in.D = D;
-    in.r0 = in.r1 = in.w9 = in.A = in.P = in.part = 0;
+    in.r0 = in.r1 = in.w9 = in.A = in.P = in.part = in.cm = in.oe = 0;
     // the first 32 records' senders and type words, the first four's
     // exchanges (one load instruction each, issued a node ahead)
     const uint32_t ik = in.D.z & DESC_CNT_MASK;
@@ -644,15 +643,8 @@ __global__ void __launch_bounds__(64 * PSIM_HALF_WPB, PSIM_HALF_WAVES) k_lite_ha
         for (uint32_t i = first; i < na; i += 2 * nw) {
             HSTAMP(w, 8);
             begin(x, in);
-            // the connection cache: the active members' up-and-partition pairs
-            {
-                KArgs& a = kargs();
-                const uint32_t ca = l < x.act_n && x.A < a.n_nodes ? x.A : x.me;
-                // (the outbox bound's load issued with the pair: one wait)
-                const uint32_t cap = (uint32_t)(a.obase[x.me - a.lo + 1] - x.ob);
-                const uint32_t af = a.upart[ca];
-                x.AF = l == 31 ? cap : af;
-            }
+            // the connection bits and the outbox bound, loaded with the rows
+            x.AF = in.cm | (min(in.oe - x.ob, 0xFFFFFFu) << 8);
             // the next node's inputs, in flight while this one runs
             const uint32_t nx = i + 2 * nw, nnx = i + 4 * nw;
             HIn inn = load_in(kargs(), Dn);
