@@ -21,6 +21,7 @@ round; node rows; overlay statistics): N RCCL ranks against one GPU, or, on
 one GPU, two virtual shards against one.  A mismatch fails the run.
 """
 import argparse
+import contextlib
 import hashlib
 import json
 import os
@@ -50,6 +51,22 @@ ALG_FORMULA = ("B = N_proc * 2 * 416 + M_in * 64 + M_out * 68 per round, N_proc 
                "idle nodes are not read by the kernels and are not counted; every record is the "
                "64-B record the engine moves, plus its 4-B route key")
 
+
+
+@contextlib.contextmanager
+def c_stdout_to_stderr():
+    """C-level writes to stdout (RCCL prints its version banner there as a
+    communicator starts) go to stderr meanwhile: rank 0's stdout carries the
+    one JSON line only"""
+    sys.stdout.flush()
+    saved = os.dup(1)
+    os.dup2(2, 1)
+    try:
+        yield
+    finally:
+        sys.stdout.flush()
+        os.dup2(saved, 1)
+        os.close(saved)
 
 def parse():
     p = argparse.ArgumentParser()
@@ -371,7 +388,8 @@ def shard_check(args, world, rank, dist, comm):
     try:
         if world > 1 or comm is not None:
             cfg.shard_world, cfg.shard_rank = world, rank
-            sh = Simulator(cfg, comm=comm)
+            with c_stdout_to_stderr():
+                sh = Simulator(cfg, comm=comm)
             shards = world
         else:
             cfg.n_shards = 2
@@ -612,7 +630,8 @@ def main():
     comm = shared_comm()
     if world > 1:
         cfg.shard_world, cfg.shard_rank = world, rank
-    sim = Simulator(cfg, comm=comm)
+    with c_stdout_to_stderr():
+        sim = Simulator(cfg, comm=comm)
     ovf_run = np.zeros(len(OVF_KINDS), np.uint64)          # overflows by table over every round of the run
 
     def step(k):
