@@ -84,6 +84,29 @@ def test_outstanding_pool_growth(monkeypatch):
     S.compare_nodes(fresh.nodes(), os_.nodes())
 
 
+def test_kernel_counts_sum_to_the_round():
+    """psim_debug_kernel_counts: the node-round kernels' own nodes processed,
+    deliveries and emissions add up to the round's stats (every one of them
+    is counted by exactly one kernel), round after round of a churn +
+    partition run with broadcasts"""
+    from partisan_amd.sim import default_config
+    from partisan_amd import workloads as W
+    n = 2048
+    sim = _gpu(default_config(n_nodes=n, seed=5))
+    sim.run_schedule(W.doubling_join(n, 5), 40)
+    for r in range(40):
+        if r % 10 == 0:
+            sim.broadcast(0, r)
+        if r == 20:
+            sim.crash(np.arange(100, 140, dtype=np.uint32))
+        st = sim.step(1)
+        kc = sim.kernel_counts()
+        assert set(kc) == set(sim.KERNELS)
+        assert sum(v[0] for v in kc.values()) == int(st["nodes_processed"][0])
+        assert sum(v[1] for v in kc.values()) == int(st["delivered"][0].sum())
+        assert sum(v[2] for v in kc.values()) == int(st["emitted"][0].sum())
+
+
 def test_lingering_connections_parity():
     """connections beyond the active view -- shuffle
     terminals' Senders, rejected and pending neighbor requests, a joiner's
