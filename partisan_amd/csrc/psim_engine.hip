@@ -199,10 +199,13 @@ __global__ void k_origin(uint32_t* origin, uint32_t lo, uint32_t n_local, const 
 // nodes, and everything per destination happens in one block's LDS:
 //   k_bucket_hist<>    a block takes fixed steps of source records and
 //                      histograms their buckets in LDS -> hist[b * nblk + blk]
-//   scan               over hist: where block blk's records of bucket b go;
-//                      the extra last entry becomes the record count
-//   k_bucket_scatter<> the same steps again: each record's (destination in
-//                      bucket | bound class, source index) pair to its place
+//   k_bucket_offsets   a block per bucket: the scan of its row of hist --
+//                      where block blk's records go within bucket b -- and
+//                      the bucket's total
+//   k_bucket_scatter<> the scan of the totals (each block; block 0 stores
+//                      the bucket bases), then the same steps again: each
+//                      record's (destination in bucket | bound class, source
+//                      index) pair to its place
 //   k_bucket_route     one block per bucket: per destination the count, the
 //                      bound sum and the BROADCAST id mask (LDS atomics; the
 //                      returned count is the record's rank in its run), the
@@ -397,7 +400,6 @@ __global__ void __launch_bounds__(RB_STEP) k_bucket_hist(RouteIn in, uint32_t ns
     __shared__ uint64_t sbase[RB_WAVES][64];
     if (blockIdx.x < st.nt) stats_tile(st, blockIdx.x, sbase);   // (uniform)
     for (uint32_t j = threadIdx.x; j < nb; j += blockDim.x) hcnt[j] = 0;
-    if (blockIdx.x == 0 && threadIdx.x == 0) hist[(size_t)nb * gridDim.x] = 0;   // the scan's extra entry
     __syncthreads();
     for (uint32_t step = blockIdx.x; step < nsteps; step += gridDim.x)
         route_step<DENSE, DENSE>(in, step, spre, sbase,
@@ -406,9 +408,29 @@ __global__ void __launch_bounds__(RB_STEP) k_bucket_hist(RouteIn in, uint32_t ns
     for (uint32_t j = threadIdx.x; j < nb; j += blockDim.x) hist[(size_t)j * gridDim.x + blockIdx.x] = hcnt[j];
 }
 
+template <typename T, uint32_t NT = BLK>
+__device__ T block_excl(T v, T* total);   // (the exclusive-scan section below)
+
+// Block b: row b of hist (nblk <= RB_MAX_BLOCKS counts, one a thread) scanned
+// into hoff, the row's sum into tot[b].  One launch where a scan over the
+// whole matrix took three (k_scan_tiles / _sums / _apply, ~15 us a round at
+// 2^20 nodes, mostly launch and drain)
+__global__ void __launch_bounds__(RB_MAX_BLOCKS) k_bucket_offsets(const uint32_t* __restrict__ hist, uint32_t nblk,
+                                                                 uint32_t* __restrict__ hoff,
+                                                                 uint32_t* __restrict__ tot, const uint32_t* ctl) {
+    if (*ctl) return;                                 // an aborted batch (run_batch)
+    const size_t r = (size_t)blockIdx.x * nblk;
+    const uint32_t v = threadIdx.x < nblk ? hist[r + threadIdx.x] : 0u;
+    uint32_t t;
+    const uint32_t e = block_excl<uint32_t, RB_MAX_BLOCKS>(v, &t);
+    if (threadIdx.x < nblk) hoff[r + threadIdx.x] = e;
+    if (threadIdx.x == 0) tot[blockIdx.x] = t;
+}
+
 template <bool DENSE>
 __global__ void __launch_bounds__(RB_STEP) k_bucket_scatter(RouteIn in, uint32_t nsteps, uint32_t nb,
                                                             uint32_t wshift, const uint32_t* __restrict__ off,
+                                                            const uint32_t* __restrict__ tot, uint32_t* base,
                                                             uint2* pairs, uint64_t cap, uint64_t* hovf,
                                                             uint32_t* ctl, uint32_t round1, StatsIn st) {
     if (*ctl) return;                                 // an aborted batch (run_batch)
@@ -416,7 +438,16 @@ __global__ void __launch_bounds__(RB_STEP) k_bucket_scatter(RouteIn in, uint32_t
     __shared__ uint32_t spre[RB_WAVES][65];
     __shared__ uint64_t sbase[RB_WAVES][64];
     if (blockIdx.x == 0) stats_final(st, sbase);      // (the tiles are k_bucket_hist's; before any return)
-    const uint32_t m = off[(size_t)nb * gridDim.x];   // the record count
+    // the buckets' bases: the totals through LDS (coalesced), a run of them a
+    // thread, one block scan of the run sums
+    for (uint32_t j = threadIdx.x; j < nb; j += blockDim.x) hcnt[j] = tot[j];
+    __syncthreads();
+    const uint32_t per = (nb + RB_STEP - 1) / RB_STEP, j0 = min(nb, threadIdx.x * per), j1 = min(nb, j0 + per);
+    uint32_t v = 0;
+    for (uint32_t j = j0; j < j1; j++) v += hcnt[j];
+    uint32_t m;                                       // the record count
+    uint32_t run = block_excl<uint32_t, RB_STEP>(v, &m);
+    if (blockIdx.x == 0 && threadIdx.x == 0) base[nb] = m;   // (k_bucket_route's overflow test too)
     if (m > cap) {                                    // the route buffers are too small:
         if (blockIdx.x == 0 && threadIdx.x == 0) {    // the host grows them and reruns
             *hovf = m;
@@ -426,9 +457,19 @@ __global__ void __launch_bounds__(RB_STEP) k_bucket_scatter(RouteIn in, uint32_t
         }
         return;
     }
+    for (uint32_t j = j0; j < j1; j++) {
+        const uint32_t x = hcnt[j];
+        hcnt[j] = run;
+        run += x;
+    }
+    __syncthreads();
     // each bucket's counter starts at this block's place in it: the returned
     // count is the pair's position (no per-record read of the offset matrix)
-    for (uint32_t j = threadIdx.x; j < nb; j += blockDim.x) hcnt[j] = off[(size_t)j * gridDim.x + blockIdx.x];
+    for (uint32_t j = threadIdx.x; j < nb; j += blockDim.x) {
+        const uint32_t b0 = hcnt[j];
+        if (blockIdx.x == 0) base[j] = b0;
+        hcnt[j] = b0 + off[(size_t)j * gridDim.x + blockIdx.x];
+    }
     __syncthreads();
     const uint32_t wmask = (1u << wshift) - 1;
     for (uint32_t step = blockIdx.x; step < nsteps; step += gridDim.x)
@@ -663,7 +704,7 @@ __device__ __forceinline__ uint4 wire_piece(const Wire* __restrict__ heads, cons
 // BROADCAST message-slot mask (64 bits): 4 x W words.
 template <bool WIRE>
 __global__ void __launch_bounds__(RR_THREADS) k_bucket_route(
-    uint32_t n, uint32_t wshift, uint32_t nblk, const uint32_t* __restrict__ off,
+    uint32_t n, uint32_t wshift, const uint32_t* __restrict__ base,
     const uint2* __restrict__ pairs, const Msg* __restrict__ rec, const Wire* __restrict__ heads,
     const Wire* __restrict__ tails, uint32_t* rank, unsigned long long* cb,
     unsigned long long* bmask, uint32_t* in_beg, uint32_t* idx, uint32_t* tmp, Msg* __restrict__ inbox, uint64_t* hm,
@@ -680,8 +721,8 @@ __global__ void __launch_bounds__(RR_THREADS) k_bucket_route(
     uint32_t* bs = sm + W;
     unsigned long long* mk = reinterpret_cast<unsigned long long*>(sm + 2 * W);
     uint32_t* pre = bs;                               // (after the bound sums are written out)
-    const uint32_t s0 = off[(size_t)b * nblk], s1 = off[(size_t)(b + 1) * nblk];
-    if (off[(size_t)gridDim.x * nblk] > cap) return;  // overflow (k_bucket_scatter flagged it)
+    const uint32_t s0 = base[b], s1 = base[b + 1];
+    if (base[gridDim.x] > cap) return;                // overflow (k_bucket_scatter flagged it)
     for (uint32_t j = threadIdx.x; j < 4 * W; j += blockDim.x) sm[j] = 0;
     if (threadIdx.x == 0) s_nl = 0;
     __syncthreads();
@@ -1061,8 +1102,6 @@ __device__ unsigned long long btot_sum(const unsigned long long* btot, uint32_t 
     return s_tot;
 }
 
-template <typename T, uint32_t NT = BLK>
-__device__ T block_excl(T v, T* total);   // (the exclusive-scan section below)
 
 // Per node, from the scan of the packed (bound, work) words: the outbox
 // base, and for a node with work its descriptor at its active-list position
@@ -1392,6 +1431,7 @@ struct Shard {
     // per-round scratch
     DBuf<uint32_t> okey, ocnt, in_beg,
         d_nact, n_slow, n_pt, n_shuf, n_lite, n_ptl, rank, tmp, hist, hoff;
+    DBuf<uint32_t> rtot, rbase;         // route: per bucket its record count, and its first pair
     DBuf<unsigned long long> bmask;     // per local node: message slots of its BROADCAST records
     DBuf<uint2> pairs;                  // route: (destination in bucket | class, source index)
     DBuf<unsigned long long> cb;        // per local node: inbox count | bound sum << 32 (n + 1)
@@ -2030,9 +2070,11 @@ int route_group(psim_handle* h, Shard* s, bool dense, uint32_t m) {
                      dense ? s->recvt.p : nullptr, dense ? s->wseg.p : nullptr, dense ? h->G : 0u};
     const uint32_t nsteps = std::max<uint32_t>(1, (in.n_src + RB_STEP - 1) / RB_STEP);
     const uint32_t nblk = std::min<uint32_t>(nsteps, h->rb_blocks);
-    const size_t nh = (size_t)nb * nblk + 1;
+    const size_t nh = (size_t)nb * nblk;
     TRY(s->hist.ensure(nh));
     TRY(s->hoff.ensure(nh));
+    TRY(s->rtot.ensure(nb));
+    TRY(s->rbase.ensure(nb + 1));
     const size_t lds_h = (size_t)nb * 4, lds_r = (size_t)W * 16;
     // the round's stats rows (every node-phase kernel's blocks) are complete
     const uint32_t rows = s->pgrid + s->cgrid + s->rgrid + s->tgrid + s->sgrid + s->lgrid + s->qgrid;
@@ -2047,22 +2089,24 @@ int route_group(psim_handle* h, Shard* s, bool dense, uint32_t m) {
     else    // (G == 1: the first kernel after the node-round phase stamps its end)
         k_bucket_hist<false><<<nblk, RB_STEP, lds_h, s->stream>>>(in, nsteps, nb, wshift, s->hist.p, s->ctl.p,
                                                                   phase_end_mark(h, s), st);
-    TRY(scan_excl(s, s->hist.p, s->hoff.p, (uint32_t)nh));
+    k_bucket_offsets<<<nb, RB_MAX_BLOCKS, 0, s->stream>>>(s->hist.p, nblk, s->hoff.p, s->rtot.p, s->ctl.p);
     if (dense)
-        k_bucket_scatter<true><<<nblk, RB_STEP, lds_h, s->stream>>>(in, nsteps, nb, wshift, s->hoff.p, s->pairs.p,
-                                                                    s->rcap, s->pin_dev + PIN_OVF, s->ctl.p,
+        k_bucket_scatter<true><<<nblk, RB_STEP, lds_h, s->stream>>>(in, nsteps, nb, wshift, s->hoff.p, s->rtot.p,
+                                                                    s->rbase.p, s->pairs.p, s->rcap,
+                                                                    s->pin_dev + PIN_OVF, s->ctl.p,
                                                                     s->batch_round1, st);
     else
-        k_bucket_scatter<false><<<nblk, RB_STEP, lds_h, s->stream>>>(in, nsteps, nb, wshift, s->hoff.p,
-                                                                     s->pairs.p, s->rcap, s->pin_dev + PIN_OVF,
-                                                                     s->ctl.p, s->batch_round1, st);
+        k_bucket_scatter<false><<<nblk, RB_STEP, lds_h, s->stream>>>(in, nsteps, nb, wshift, s->hoff.p, s->rtot.p,
+                                                                     s->rbase.p, s->pairs.p, s->rcap,
+                                                                     s->pin_dev + PIN_OVF, s->ctl.p,
+                                                                     s->batch_round1, st);
     if (dense)
         k_bucket_route<true><<<nb, RR_THREADS, lds_r, s->stream>>>(
-            n, wshift, nblk, s->hoff.p, s->pairs.p, nullptr, in.wire, in.tails, s->rank.p, s->cb.p, s->bmask.p,
+            n, wshift, s->rbase.p, s->pairs.p, nullptr, in.wire, in.tails, s->rank.p, s->cb.p, s->bmask.p,
             s->in_beg.p, s->ivals.p, s->tmp.p, s->inbox.p, s->pin_dev + PIN_M, s->rcap, s->ctl.p);
     else
         k_bucket_route<false><<<nb, RR_THREADS, lds_r, s->stream>>>(
-            n, wshift, nblk, s->hoff.p, s->pairs.p, in.rec, nullptr, nullptr, s->rank.p, s->cb.p, s->bmask.p,
+            n, wshift, s->rbase.p, s->pairs.p, in.rec, nullptr, nullptr, s->rank.p, s->cb.p, s->bmask.p,
             s->in_beg.p, s->ivals.p, s->tmp.p, s->inbox.p, s->pin_dev + PIN_M, s->rcap, s->ctl.p);
     HIP_TRY(hipGetLastError());
     return PSIM_OK;
@@ -2685,7 +2729,7 @@ void shard_free(Shard* s) {
     s->outbox.release(); s->okey.release(); s->ocnt.release();
     s->cb.release(); s->in_beg.release();
     s->rank.release(); s->bmask.release(); s->btot.release();
-    s->hist.release(); s->hoff.release(); s->pairs.release(); s->tmp.release();
+    s->hist.release(); s->hoff.release(); s->rtot.release(); s->rbase.release(); s->pairs.release(); s->tmp.release();
     s->stop_ids.release(); s->n_stop.release();
     s->desc.release(); s->d_nact.release(); s->desc_slow.release(); s->n_slow.release(); s->desc_pt.release(); s->n_pt.release(); s->desc_shuf.release(); s->n_shuf.release(); s->desc_lite.release(); s->n_lite.release(); s->desc_ptl.release(); s->n_ptl.release(); s->bound.release(); s->pscan.release();
     s->obase.release(); s->stat_part.release(); s->stat_out.release(); s->stat_tile.release(); s->d_off.release();
