@@ -46,8 +46,21 @@ __device__ unsigned long long g_stamps_lite[32];   // k_consume_lite's phases (p
         if (lane_id() == 0) (w).stl[(k)] += t_ - (w).t_last;                         \
         (w).t_last = t_;                                                             \
     } while (0)
+// k_ptl (a lane per node, divergent): the first active lane adds the time
+// since the wave's last stamp (both in LDS) to phase k -- the branches of a
+// divergent handler run one after another, each charged its own time --
+// into g_stamps_lite[16 + k] at the kernel's end
+#define PTL_STAMP(k)                                                                 \
+    do {                                                                             \
+        const uint64_t t_ = __builtin_amdgcn_s_memtime();                            \
+        if (lane_id() == (uint32_t)__ffsll((long long)__builtin_amdgcn_read_exec()) - 1) { \
+            ptl_st[(k)] += t_ - ptl_st[15];                                          \
+            ptl_st[15] = t_;                                                         \
+        }                                                                            \
+    } while (0)
 #else
 #define STAMP(w, k) do { } while (0)
+#define PTL_STAMP(k) do { } while (0)
 #endif
 constexpr uint32_t NONE = PSIM_NONE;
 
@@ -2644,28 +2657,47 @@ DEV bool col_has(const LdsCol& V, uint32_t n, uint32_t x) {
 #ifndef PSIM_PTL_PF           // k_ptl's set / table loops read one entry ahead (0: A/B)
 #define PSIM_PTL_PF 1
 #endif
-// ordsets:del_element/2
+// ordsets:del_element/2: the search stops at the first entry >= x (the set
+// is ascending), the entries after x move down one; each LDS read is issued
+// an iteration ahead of its use
 DEV void col_del(const LdsCol& V, uint32_t& n, uint32_t x) {
-    uint32_t at = n;
-    for (uint32_t i = 0; i < n; i++)
-        if (V[i] == x) { at = i; break; }
+    uint32_t at = n, e = n ? V[0] : 0u;
+    for (uint32_t i = 0; i < n; i++) {
+        const uint32_t en = i + 1 < n ? V[i + 1] : 0u;
+        if (e >= x) {
+            if (e == x) at = i;
+            break;
+        }
+        e = en;
+    }
     if (at == n) return;
-    for (uint32_t i = at; i + 1 < n; i++) V[i] = V[i + 1];
+    uint32_t nx = at + 1 < n ? V[at + 1] : 0u;
+    for (uint32_t i = at; i + 1 < n; i++) {
+        const uint32_t m = nx;
+        nx = i + 2 < n ? V[i + 2] : 0u;
+        V[i] = m;
+    }
     n--;
     V[n] = 0u;
 }
-// ordsets:add_element/2 (the caller guarantees room)
+// ordsets:add_element/2 (the caller guarantees room): from the back, the
+// entries above x move up one -- one pass, no separate search -- and a
+// member found below them moves them back (x already in the set)
 DEV void col_add(const LdsCol& V, uint32_t& n, uint32_t x) {
-    uint32_t pos = 0;
-    bool in = false;
-    for (uint32_t i = 0; i < n; i++) {
-        const uint32_t e = V[i];
-        in |= e == x;
-        pos += e < x ? 1u : 0u;
+    const uint32_t top = V[n];                        // (restored when x is a member)
+    uint32_t i = n, e = n ? V[n - 1] : 0u;
+    while (i && e > x) {
+        const uint32_t e2 = i > 1 ? V[i - 2] : 0u;
+        V[i] = e;
+        i--;
+        e = e2;
     }
-    if (in) return;
-    for (uint32_t i = n; i > pos; i--) V[i] = V[i - 1];
-    V[pos] = x;
+    if (i && e == x) {
+        for (uint32_t k = i; k < n; k++) V[k] = V[k + 1];
+        V[n] = top;
+        return;
+    }
+    V[i] = x;
     n++;
 }
 
@@ -2725,13 +2757,17 @@ DEV void ptl_update(KArgs& a, PtLane& n, size_t li, uint32_t com_n, uint32_t fro
         for (int i = 0; i < PTL_SET; i++) { n.EG[i] = i < 8 && (uint32_t)i < com_n ? C8[i & 7] : 0u; n.LZ[i] = 0u; }
         n.ne = com_n; n.nl = 0;
     }
-    if (to_eager) {
-        col_add(n.EG, n.ne, from);
-        col_del(n.LZ, n.nl, from);
-    } else {
-        col_del(n.EG, n.ne, from);
-        col_add(n.LZ, n.nl, from);
-    }
+    // the set `from` joins and the one it leaves, selected per lane: every
+    // lane of the wave runs the one add and the one delete together, whatever
+    // its message (the two directions as branches ran one after the other)
+    LdsCol A, D;
+    A.p = to_eager ? n.EG.p : n.LZ.p;
+    D.p = to_eager ? n.LZ.p : n.EG.p;
+    uint32_t na = to_eager ? n.ne : n.nl, nd = to_eager ? n.nl : n.ne;
+    col_add(A, na, from);
+    col_del(D, nd, from);
+    n.ne = to_eager ? na : nd;
+    n.nl = to_eager ? nd : na;
 }
 
 DEV uint64_t out_at(const PtLane& n, uint32_t i) { return ((uint64_t)n.OH[i] << 32) | n.OL[i]; }
@@ -2805,6 +2841,10 @@ __global__ void PTL_BOUNDS k_ptl(RoundArgs) {
     __shared__ uint32_t tabs[(2 * PTL_SET + 2 * PTL_CAP) * PTL_BLK];
     for (int i = threadIdx.x; i < 2 * PSIM_MSG_SLOTS; i += blockDim.x) sslots[i] = kargs().slots[i];
     if (threadIdx.x < T_N + 1) sst[threadIdx.x] = 0;
+#ifdef PSIM_STAMPS
+    __shared__ unsigned long long ptl_st[16];
+    if (threadIdx.x < 16) ptl_st[threadIdx.x] = threadIdx.x == 15 ? __builtin_amdgcn_s_memtime() : 0ull;
+#endif
     __syncthreads();
     const uint32_t l = lane_id();
     const uint32_t nq0 = kargs().n_ptl[0], nq = nq0 + kargs().n_ptl[1];
@@ -2880,8 +2920,10 @@ __global__ void PTL_BOUNDS k_ptl(RoundArgs) {
             go = ok;
             fall = !ok;
         }
+        PTL_STAMP(0);
         // nodes that do not fit go to k_pt's list (one atomic per block step)
         block_append(fall, D, kargs().desc_pt, kargs().n_pt, wcnt);
+        PTL_STAMP(1);
         if (!go) continue;
         const uint32_t id = D.x;
         const size_t li = id - a.lo;
@@ -2895,6 +2937,7 @@ __global__ void PTL_BOUNDS k_ptl(RoundArgs) {
             n.A[4] = a1.x; n.A[5] = a1.y; n.A[6] = a1.z; n.A[7] = a1.w;
         }
         n.cmask = ptl_conn_mask(a, n);
+        PTL_STAMP(2);
         n.root0 = root0;
         n.ne = root0 == NONE ? 0u : (rtw4 & 0xFF);
         n.nl = root0 == NONE ? 0u : (rtw5 & 0xFF);
@@ -2934,6 +2977,13 @@ __global__ void PTL_BOUNDS k_ptl(RoundArgs) {
         const uint8_t fl0 = a.flags[id];              // (read before the emissions' stores: see PtlRecs)
         uint32_t seq = a.ocnt[li];
         const uint32_t oend = (uint32_t)a.obase[li + 1];
+#ifdef PSIM_STAMPS
+        {   // (the loads above waited for here, as the first handler would)
+            volatile uint32_t sink_ = n.EG[0] + n.OL[0] + hw4 + fl0 + seq + oend;
+            (void)sink_;
+        }
+#endif
+        PTL_STAMP(3);
         const uint32_t ik = start == a.round ? 0u : (D.z & DESC_CNT_MASK);
         for (uint32_t j = 0; j < ik; j++) {           // the Plumtree inbox, canonical order
             uint32_t src, tt, msg, rnd, root;
@@ -2948,12 +2998,20 @@ __global__ void PTL_BOUNDS k_ptl(RoundArgs) {
             const bool have = !live || ((n.have >> sk) & 1ull);
             if (type != PSIM_MSG_PT_PRUNE && type != PSIM_MSG_PT_IGNORED_IHAVE && !live) v[T_OVF]++;
             uint32_t sto = NONE, stt = 0, sa0 = 0, sa1 = 0;     // a single send of the handler
+            // update_peers/5 (pt:593-609) at one call site for every message:
+            // to eager -- a first delivery, an IHAVE of a missing id, a GRAFT
+            // of a held one; to lazy -- a duplicate, a PRUNE (a wave whose
+            // lanes hold different messages ran one update per branch)
+            const bool first = type == PSIM_MSG_PT_BROADCAST && !have;
+            const bool to_eager = first || (type == PSIM_MSG_PT_IHAVE && !have) || (type == PSIM_MSG_PT_GRAFT && have);
+            const bool to_lazy = (type == PSIM_MSG_PT_BROADCAST && have) || type == PSIM_MSG_PT_PRUNE;
+            if (to_eager || to_lazy) ptl_update(a, n, li, com_n, from, root, to_eager);
+            PTL_STAMP(4);
             if (type == PSIM_MSG_PT_BROADCAST) {     // pt:288-293, :368-378
                 if (!have) {
                     n.have |= 1ull << sk;
                     v[T_FIRST]++;
                     if (msg == a.tracked_msg) { trk_round = a.round; trk_hop = rnd + 1; }
-                    ptl_update(a, n, li, com_n, from, root, true);
                     // eager_push/7 + schedule_lazy_push/6 over slot 0's sets
                     // (each entry's LDS read issued an iteration ahead of its
                     // use: the loop waited one LDS latency per member)
@@ -2989,21 +3047,18 @@ __global__ void PTL_BOUNDS k_ptl(RoundArgs) {
 #endif
                         if (e != from) ptl_add_out(n, ((uint64_t)e << 32) | (msg << 16) | ((rnd + 1) & 0xFFFFu));
                     }
-                } else {
-                    ptl_update(a, n, li, com_n, from, root, false);
+                    PTL_STAMP(5);
+                } else {                             // a duplicate: PRUNE back
                     sto = from; stt = PSIM_MSG_PT_PRUNE;
                 }
-            } else if (type == PSIM_MSG_PT_PRUNE) {  // pt:294-298
-                ptl_update(a, n, li, com_n, from, root, false);
             } else if (type == PSIM_MSG_PT_IHAVE) {  // pt:299-303, :380-386
                 sto = from; stt = have ? PSIM_MSG_PT_IGNORED_IHAVE : PSIM_MSG_PT_GRAFT; sa0 = msg; sa1 = rnd;
-                if (!have) ptl_update(a, n, li, com_n, from, root, true);
             } else if (type == PSIM_MSG_PT_IGNORED_IHAVE) {   // pt:304-307
                 ptl_ack_out(n, ((uint64_t)from << 32) | (msg << 16) | (rnd & 0xFFFFu));
-            } else if (have) {                       // GRAFT pt:308-313, :388-402
-                ptl_update(a, n, li, com_n, from, root, true);
+                PTL_STAMP(9);
+            } else if (type == PSIM_MSG_PT_GRAFT && have) {   // pt:308-313, :388-402
                 sto = from; stt = PSIM_MSG_PT_BROADCAST; sa0 = msg; sa1 = rnd;
-            }
+            }                                        // (PRUNE pt:294-298: the update only)
             if (sto != NONE) {                        // (the IHAVE answer goes before the update in
                 if (ptl_conn(a, n, sto)) {            //  the reference; the update sends nothing)
                     dig += relay_emit(a, D.w + seq, src, id, stt, seq, sa0, sa1, root, X0);
@@ -3012,8 +3067,10 @@ __global__ void PTL_BOUNDS k_ptl(RoundArgs) {
                 } else {
                     v[T_FAIL]++;
                 }
+                PTL_STAMP(10);
             }
         }
+        PTL_STAMP(11);
         if (((D.z >> 28) & DESC_LAZY) && n.on > 0) {   // the lazy tick (pt:341-345, :443-453)
 #if PSIM_PTL_PF
             uint64_t o_nx = out_at(n, 0);
@@ -3036,6 +3093,7 @@ __global__ void PTL_BOUNDS k_ptl(RoundArgs) {
                 v[T_EMT + 2]++;
             }
         }
+        PTL_STAMP(12);
         // write back: header words 5-8 and 11, the sets, the table, the flag byte
         uint32_t* hw = reinterpret_cast<uint32_t*>(a.hdr + li);
         reinterpret_cast<uint4*>(hw)[1] = make_uint4(hw4, (uint32_t)(n.have >> 32), (uint32_t)n.have, trk_round);
@@ -3070,7 +3128,12 @@ __global__ void PTL_BOUNDS k_ptl(RoundArgs) {
         v[T_BOUND] += seq > oend - D.w ? 1u : 0u;
         a.flags[id] = (uint8_t)((fl0 & (F_UP | F_CRASHED)) | (n.on ? F_LAZY : 0) | (min(n.on, 15u) << F_OUTN_SHIFT) |
                                 (act_n < a.min_active ? F_LOWACT : 0));
+        PTL_STAMP(13);
     }
+#ifdef PSIM_STAMPS
+    PTL_STAMP(14);
+    if (threadIdx.x < 15) atomicAdd(&g_stamps_lite[16 + threadIdx.x], ptl_st[threadIdx.x]);
+#endif
 #pragma unroll
     for (int k = 0; k < T_N; k++)
         for (int o = 32; o > 0; o >>= 1) v[k] += __shfl_xor(v[k], o);

@@ -31,6 +31,10 @@ for i, n in enumerate(PT):
 HALF = {8: "loop / wait for the node's loads", 0: "begin + connection cache", 6: "inbox record parse",
         1: "SHUFFLE relay", 2: "terminal: sublist", 3: "terminal: reply send", 4: "merge_exchange",
         5: "shuffle start", 7: "writeback + flush", 9: "body's end (the other half's work)"}
+PTL = {0: "list entry, rows, records, preconditions", 1: "k_pt list append", 2: "active row + connection mask",
+       3: "sets / table loads", 4: "update_peers (every message)", 5: "BROADCAST first: eager push + lazy adds",
+       9: "IGNORED_IHAVE ack", 10: "answer send",
+       11: "handler loop control", 12: "lazy tick", 13: "writeback", 14: "kernel end"}
 LITE = {0: "wait for the node's loads", 1: "begin_node", 2: "inbox chunk / record parse", 3: "SHUFFLE_REPLY merge",
         4: "SHUFFLE relay", 5: "terminal: sublist", 6: "terminal: reply send", 7: "terminal: merge",
         8: "shuffle start", 9: "next node's 2nd-stage loads", 10: "writeback", 11: "next node's loads"}
@@ -84,9 +88,12 @@ def main():
     print("delivered/round: " + ", ".join(f"{n}={int(dl[i])}" for i, n in enumerate(HV + PT) if dl[i]))
     print("k_consume / k_pt:")
     table(v[:32], NAMES, a.steps)
-    if v[32:64].any():
+    if v[32:48].any():
         print("k_consume_lite:")
-        table(v[32:64], LITE, a.steps)
+        table(v[32:48], LITE, a.steps)
+    if v[48:64].any():
+        print("k_ptl (wave time by phase; a divergent handler's branches each charged their own):")
+        table(v[48:64], PTL, a.steps)
     if v[64:].any():
         print("k_lite_half (each half's phases; both halves summed):")
         table(v[64:80] + v[80:96], HALF, a.steps)
