@@ -2154,8 +2154,10 @@ DEV uint64_t relay_emit(KArgs& a, uint64_t slot, uint32_t dst, uint32_t me, uint
     uint4* o = reinterpret_cast<uint4*>(a.rec_out + slot);
     o[0] = make_uint4(dst, me, tt, seq);
     o[1] = make_uint4(a0, a1, a2, 0u);
-    o[2] = make_uint4(X[0], X[1], X[2], X[3]);
-    o[3] = make_uint4(X[4], X[5], X[6], X[7]);
+    if (!PSIM_SHORT_TAIL || ((tt >> 16) & 0xFFu)) {   // (a short record's tail: zeros, by the route)
+        o[2] = make_uint4(X[0], X[1], X[2], X[3]);
+        o[3] = make_uint4(X[4], X[5], X[6], X[7]);
+    }
     a.okey[slot] = dst | (max_emit(tt & 0xFF) << KEY_DST_BITS);
     return dg;
 }
@@ -2721,13 +2723,16 @@ struct PtLane {
 // its answers go to, its lazy tick's peers -- measured slower at 2^20 and
 // at 2^26: the loads then wait for the records and the table, and the
 // random lines come from the MALL, profiles/r05/ab_log.txt r5k / r5l)
-DEV uint32_t ptl_conn_mask(KArgs& a, const PtLane& n) {
-    uint16_t up[PSIM_ACTIVE_CAP];                     // (k_node_prep's up-and-partition pairs)
+// (the pairs are loaded as soon as the active row arrives, before the
+// node's precondition pass, whose work then covers their latency)
+DEV void ptl_load_pairs(KArgs& a, const PtLane& n, uint16_t (&up)[PSIM_ACTIVE_CAP]) {
 #pragma unroll
     for (int j = 0; j < PSIM_ACTIVE_CAP; j++) {
         const uint32_t q = (uint32_t)j < n.act_n && n.A[j] < a.n_nodes ? n.A[j] : n.id;
         up[j] = a.upart[q];
     }
+}
+DEV uint32_t ptl_conn_mask(KArgs& a, const PtLane& n, const uint16_t (&up)[PSIM_ACTIVE_CAP]) {
     uint32_t m = 0;
 #pragma unroll
     for (int j = 0; j < PSIM_ACTIVE_CAP; j++)
@@ -2787,6 +2792,43 @@ DEV void ptl_add_out(PtLane& n, uint64_t key) {
     n.on++;
     n.out_dirty = true;
 }
+// schedule_lazy_push/6 over slot 0's lazy set (pt:368-378): the keys
+// peer << 32 | lo of its members other than `from` -- ascending with the
+// set -- merged into the ascending table: a forward pass counts the keys
+// the table lacks, a backward pass moves the table's larger entries up and
+// places the new keys (add_outstanding per member searched the whole table
+// and shifted its tail for each key)
+#ifndef PSIM_PTL_LAZYM        // (0: add_outstanding per member, for A/B)
+#define PSIM_PTL_LAZYM 1
+#endif
+DEV void ptl_add_lazy(PtLane& n, uint32_t from, uint32_t lo) {
+    uint32_t add = 0;
+    for (uint32_t j = 0, i = 0; j < n.nl; j++) {
+        const uint32_t e = n.LZ[j];
+        if (e == from) continue;
+        const uint64_t key = ((uint64_t)e << 32) | lo;
+        while (i < n.on && out_at(n, i) < key) i++;
+        add += (i < n.on && out_at(n, i) == key) ? 0u : 1u;
+    }
+    if (!add) return;
+    int i = (int)n.on - 1, d = (int)(n.on + add) - 1;
+    for (int j = (int)n.nl - 1; j >= 0; j--) {
+        const uint32_t e = n.LZ[j];
+        if (e == from) continue;
+        const uint64_t key = ((uint64_t)e << 32) | lo;
+        uint64_t t = i >= 0 ? out_at(n, i) : 0ull;
+        while (i >= 0 && t > key) {
+            n.OL[d] = (uint32_t)t; n.OH[d] = (uint32_t)(t >> 32);
+            d--; i--;
+            t = i >= 0 ? out_at(n, i) : 0ull;
+        }
+        if (i >= 0 && t == key) continue;             // (already outstanding)
+        n.OL[d] = (uint32_t)key; n.OH[d] = e;
+        d--;
+    }
+    n.on += add;
+    n.out_dirty = true;
+}
 DEV void ptl_ack_out(PtLane& n, uint64_t key) {
     for (uint32_t i = 0; i < n.on; i++) {
         if (out_at(n, i) != key) continue;
@@ -2837,7 +2879,6 @@ __global__ void PTL_BOUNDS k_ptl(RoundArgs) {
     enum { T_FIRST, T_FAIL, T_OVF, T_BOUND, T_DLV, T_EMT = T_DLV + 5, T_N = T_EMT + 5 };
     __shared__ unsigned long long sst[T_N + 1];       // (+ the digest)
     __shared__ uint32_t sslots[2 * PSIM_MSG_SLOTS];
-    __shared__ uint32_t wcnt[5];
     __shared__ uint32_t tabs[(2 * PTL_SET + 2 * PTL_CAP) * PTL_BLK];
     for (int i = threadIdx.x; i < 2 * PSIM_MSG_SLOTS; i += blockDim.x) sslots[i] = kargs().slots[i];
     if (threadIdx.x < T_N + 1) sst[threadIdx.x] = 0;
@@ -2863,10 +2904,17 @@ __global__ void PTL_BOUNDS k_ptl(RoundArgs) {
         uint4 D = make_uint4(0, 0, 0, 0);
         PtlRecs R;
         uint32_t root0 = NONE, rtw4 = 0, rtw5 = 0, w10 = 0, w11 = 0, start = 0, act_n = 0, tmask = 0;
+        uint16_t up[PSIM_ACTIVE_CAP];
         if (P < nq) {
             D = ptl_desc(a, nq0, P);
             const size_t li = D.x - a.lo;
             const uint32_t* hp = reinterpret_cast<const uint32_t*>(a.hdr + li);
+            // (the active row and the partition byte with the node's rows:
+            // loaded after its precondition pass, they and the members' pairs
+            // were two more dependent memory waits before its handlers)
+            const uint4* ar = reinterpret_cast<const uint4*>(a.act + li * PSIM_ACTIVE_CAP);
+            const uint4 a0 = ar[0], a1 = ar[1];
+            n.me_part = a.part[D.x];
             const uint4 hq1 = reinterpret_cast<const uint4*>(hp)[1], hq2 = reinterpret_cast<const uint4*>(hp)[2];
             start = hp[2];
             act_n = hq2.y & 0xFF;                     // word 9
@@ -2874,6 +2922,11 @@ __global__ void PTL_BOUNDS k_ptl(RoundArgs) {
             const uint4* rr = reinterpret_cast<const uint4*>(a.pt_rt + li * RT_WORDS);
             const uint4 r0 = rr[0], r1 = rr[1];
             root0 = r0.x; rtw4 = r1.x; rtw5 = r1.y;
+            n.id = D.x;
+            n.act_n = act_n;
+            n.A[0] = a0.x; n.A[1] = a0.y; n.A[2] = a0.z; n.A[3] = a0.w;
+            n.A[4] = a1.x; n.A[5] = a1.y; n.A[6] = a1.z; n.A[7] = a1.w;
+            ptl_load_pairs(a, n, up);
             // the lane's preconditions over the inbox's Plumtree messages
             const uint32_t ik = start == a.round ? 0u : (D.z & DESC_CNT_MASK);
             // eager / lazy adds this inbox can make: a BROADCAST adds its
@@ -2921,22 +2974,17 @@ __global__ void PTL_BOUNDS k_ptl(RoundArgs) {
             fall = !ok;
         }
         PTL_STAMP(0);
-        // nodes that do not fit go to k_pt's list (one atomic per block step)
-        block_append(fall, D, kargs().desc_pt, kargs().n_pt, wcnt);
+        // nodes that do not fit go to k_pt's list: one atomic a wave (a block
+        // is one wave), its return waited for only where the list entries are
+        // written, after the node's handlers
+        const uint64_t fm = ballot(fall);
+        uint32_t fbase = 0;
+        if (fm && lane_id() == 0) fbase = atomicAdd(kargs().n_pt, (uint32_t)popc(fm));
         PTL_STAMP(1);
-        if (!go) continue;
+        if (go) {
         const uint32_t id = D.x;
         const size_t li = id - a.lo;
-        n.id = id;
-        n.me_part = a.part[id];
-        n.act_n = act_n;
-        {
-            const uint4* ar = reinterpret_cast<const uint4*>(a.act + li * PSIM_ACTIVE_CAP);
-            const uint4 a0 = ar[0], a1 = ar[1];
-            n.A[0] = a0.x; n.A[1] = a0.y; n.A[2] = a0.z; n.A[3] = a0.w;
-            n.A[4] = a1.x; n.A[5] = a1.y; n.A[6] = a1.z; n.A[7] = a1.w;
-        }
-        n.cmask = ptl_conn_mask(a, n);
+        n.cmask = ptl_conn_mask(a, n, up);
         PTL_STAMP(2);
         n.root0 = root0;
         n.ne = root0 == NONE ? 0u : (rtw4 & 0xFF);
@@ -3035,6 +3083,9 @@ __global__ void PTL_BOUNDS k_ptl(RoundArgs) {
                             v[T_FAIL]++;
                         }
                     }
+#if PSIM_PTL_LAZYM
+                    ptl_add_lazy(n, from, (msg << 16) | ((rnd + 1) & 0xFFFFu));
+#else
 #if PSIM_PTL_PF
                     uint32_t z_nx = n.LZ[0];
 #endif
@@ -3047,6 +3098,7 @@ __global__ void PTL_BOUNDS k_ptl(RoundArgs) {
 #endif
                         if (e != from) ptl_add_out(n, ((uint64_t)e << 32) | (msg << 16) | ((rnd + 1) & 0xFFFFu));
                     }
+#endif
                     PTL_STAMP(5);
                 } else {                             // a duplicate: PRUNE back
                     sto = from; stt = PSIM_MSG_PT_PRUNE;
@@ -3129,6 +3181,11 @@ __global__ void PTL_BOUNDS k_ptl(RoundArgs) {
         a.flags[id] = (uint8_t)((fl0 & (F_UP | F_CRASHED)) | (n.on ? F_LAZY : 0) | (min(n.on, 15u) << F_OUTN_SHIFT) |
                                 (act_n < a.min_active ? F_LOWACT : 0));
         PTL_STAMP(13);
+        }
+        if (fm) {
+            fbase = (uint32_t)__shfl((int)fbase, 0);
+            if (fall) kargs().desc_pt[fbase + popc(fm & ((1ull << lane_id()) - 1ull))] = D;
+        }
     }
 #ifdef PSIM_STAMPS
     PTL_STAMP(14);

@@ -699,6 +699,17 @@ __device__ __forceinline__ uint4 wire_piece(const Wire* __restrict__ heads, cons
     return lng ? tails[h1.w].q[p - 2] : make_uint4(0, 0, 0, 0);
 }
 
+// 16-B piece p of outbox record k for the inbox, p = the lane's index in its
+// quad (the quad's lanes take one record's four pieces): a short record's
+// tail (nex == 0: its emitter may leave it unwritten, PSIM_SHORT_TAIL) as
+// zeros -- the type word from the quad's first lane (DPP quad_perm 0,0,0,0)
+__device__ __forceinline__ uint4 rec_piece(const Msg* __restrict__ rec, uint32_t k, uint32_t p) {
+    const uint4 v = reinterpret_cast<const uint4*>(&rec[k])[p];
+    if (!PSIM_SHORT_TAIL) return v;
+    const uint32_t tt = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v.z, 0x00, 0xF, 0xF, false);
+    return p < 2 || wire_long(tt) ? v : make_uint4(0, 0, 0, 0);
+}
+
 // One block per bucket of W destinations; LDS holds per destination the
 // count, the bound sum (later the run start, in the same words) and the
 // BROADCAST message-slot mask (64 bits): 4 x W words.
@@ -823,7 +834,7 @@ __global__ void __launch_bounds__(RR_THREADS) k_bucket_route(
     __syncthreads();
     // the bucket's records into the inbox in run order (16 B a lane; two
     // records' pieces in flight per thread)
-    const uint32_t m4 = (s1 - s0) * 4, bd = blockDim.x;
+    const uint32_t m4 = (s1 - s0) * 4, bd = blockDim.x;   // (bd: a multiple of 4 -- piece t & 3 = lane & 3)
     for (uint32_t t = threadIdx.x; t < m4; t += 2 * bd) {
         const uint32_t t2 = t + bd;
         uint4 a, c = make_uint4(0, 0, 0, 0);
@@ -831,8 +842,8 @@ __global__ void __launch_bounds__(RR_THREADS) k_bucket_route(
             a = wire_piece(heads, tails, idx[s0 + (t >> 2)], t & 3);
             if (t2 < m4) c = wire_piece(heads, tails, idx[s0 + (t2 >> 2)], t2 & 3);
         } else {
-            a = reinterpret_cast<const uint4*>(&rec[idx[s0 + (t >> 2)]])[t & 3];
-            if (t2 < m4) c = reinterpret_cast<const uint4*>(&rec[idx[s0 + (t2 >> 2)]])[t2 & 3];
+            a = rec_piece(rec, idx[s0 + (t >> 2)], t & 3);
+            if (t2 < m4) c = rec_piece(rec, idx[s0 + (t2 >> 2)], t2 & 3);
         }
         reinterpret_cast<uint4*>(&inbox[s0 + (t >> 2)])[t & 3] = a;
         if (t2 < m4) reinterpret_cast<uint4*>(&inbox[s0 + (t2 >> 2)])[t2 & 3] = c;

@@ -226,6 +226,14 @@ __device__ __forceinline__ void lite_counts(Args& a, uint32_t (&c)[4], uint32_t&
     c[0] = a.n_lite[0]; c[1] = a.n_lite[1]; c[2] = a.n_lite[2]; c[3] = a.n_lite[3];
     na = c[0] + c[1] + c[2] + c[3];
 }
+// A record without exchange ids (nex == 0 in its type word: Plumtree,
+// DISCONNECT, NEIGHBOR_*) leaves its last 32 B unwritten in the outbox; the
+// route's gather writes zeros there (as the exchange's wire format does)
+// (PSIM_SHORT_TAIL=0: every tail written and copied, for A/B)
+#ifndef PSIM_SHORT_TAIL
+#define PSIM_SHORT_TAIL 1
+#endif
+
 __device__ __forceinline__ KArgs& kargs() {
     KArgs* p = (KArgs*)__builtin_amdgcn_kernarg_segment_ptr();
     asm volatile("" : "+s"(p));
