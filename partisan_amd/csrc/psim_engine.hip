@@ -43,6 +43,10 @@ namespace {
 
 constexpr int BLK = 256;
 constexpr uint32_t PREP_BLK = 1024;   // k_desc blocks (at most PREP_BLK of them)
+#ifndef PSIM_PREP_NPT
+#define PSIM_PREP_NPT 2
+#endif
+constexpr uint32_t PREP_NPT = PSIM_PREP_NPT;   // k_node_prep: nodes a thread (loads a node ahead)
 constexpr uint32_t DESC_RANGES = 4;   // k_node_prep ranges a k_desc block takes (at most DESC_RANGES * PREP_BLK)
 // pinned host words per shard (Shard::pin): NST stats, the consume span, the
 // outbox total, the routed record count -- stored by kernels, read by the host
@@ -881,18 +885,39 @@ __global__ void __launch_bounds__(BLK) k_node_prep(RoundArgs a, const unsigned l
     // block b takes the nodes [b * per, (b + 1) * per), blockDim at a time
     // (coalesced), so that its sums are a contiguous tile of the scan below
     const uint32_t i0 = blockIdx.x * per, i1 = min(a.n_local, i0 + per);
+    // (the row words every live node reads, issued with the flag byte --
+    // read under its test, they were a second dependent memory wait -- and
+    // for the thread's next node before this one's work: PREP_NPT nodes a
+    // thread, their loads overlapped)
+    struct PrepIn {
+        uint8_t f;
+        unsigned long long cbi;                           // inbox count | bound sum << 32
+        uint32_t st, org;
+        unsigned long long bm;
+    };
+    auto prep_in = [&](uint32_t i) {
+        PrepIn q{0, 0ull, 0u, 0u, 0ull};
+        if (i < i1) {
+            q.f = a.flags[a.lo + i];
+            q.cbi = a.in_cb[i];
+            q.st = a.start[i];
+            q.org = a.pl ? 0u : a.origin[i];
+            q.bm = a.pl ? 0ull : bmask[i];
+        }
+        return q;
+    };
+    PrepIn nx = prep_in(i0 + threadIdx.x);
     for (uint32_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
-        uint32_t id = a.lo + i;
-        uint8_t f = a.flags[id];
+        const PrepIn cur = nx;
+        nx = prep_in(i + blockDim.x);
+        uint8_t f = cur.f;
         uint64_t b = 0;
         uint32_t w = 0;
-        const unsigned long long cbi = a.in_cb[i];       // inbox count | bound sum << 32
+        const unsigned long long cbi = cur.cbi;
         uint32_t c = (uint32_t)cbi;
-        // (the row words every live node reads, issued with the flag byte:
-        // read under its test, they were a second dependent memory wait)
-        const uint32_t st_ = a.start[i];
-        const uint32_t org_ = a.pl ? 0u : a.origin[i];
-        const unsigned long long bm_ = a.pl ? 0ull : bmask[i];
+        const uint32_t st_ = cur.st;
+        const uint32_t org_ = cur.org;
+        const unsigned long long bm_ = cur.bm;
         if (f & F_UP) {
             uint32_t st = st_, r = a.round;
             if (a.pl) {            // emission bounds of the pluggable round (R0-P)
@@ -1869,7 +1894,7 @@ int phase_events_prepare(psim_handle* h, Shard* s, const RoundCtl& ctl, RoundArg
         // DESC_RANGES consecutive ranges a block; 1024-thread blocks here
         // took 27.6 us against 21.5 at 2^20, profiles/r05/ab_log.txt r5r)
         {
-            const uint32_t g = std::min<uint32_t>(grid_for(n), DESC_RANGES * PREP_BLK);
+            const uint32_t g = std::min<uint32_t>(std::max<uint32_t>(1, grid_for(n) / PREP_NPT), DESC_RANGES * PREP_BLK);
             s->pper = BLK * (uint32_t)(((uint64_t)n + (uint64_t)g * BLK - 1) / ((uint64_t)g * BLK));
             s->pgrid = std::max<uint32_t>(1, (uint32_t)(((uint64_t)n + s->pper - 1) / s->pper));
         }
