@@ -44,7 +44,7 @@ namespace {
 constexpr int BLK = 256;
 constexpr uint32_t PREP_BLK = 1024;   // k_desc blocks (at most PREP_BLK of them)
 #ifndef PSIM_PREP_NPT
-#define PSIM_PREP_NPT 2
+#define PSIM_PREP_NPT 4       // (2: step 0.620 -> 0.615 ms at 2^20 against 1 node a thread, profiles/r05/ab_log.txt r6m, r6n)
 #endif
 constexpr uint32_t PREP_NPT = PSIM_PREP_NPT;   // k_node_prep: nodes a thread (loads a node ahead)
 constexpr uint32_t DESC_RANGES = 4;   // k_node_prep ranges a k_desc block takes (at most DESC_RANGES * PREP_BLK)
@@ -235,6 +235,10 @@ constexpr uint32_t RUN_LDS = 2048;
 constexpr uint32_t RB_STEP = PSIM_RB_STEP;
 constexpr uint32_t RB_WAVES = RB_STEP / 64;
 constexpr uint32_t RB_MAX_BLOCKS = 1024;   // blocks of the two passes over the sources
+// ... by default: one resident generation (two 1024-thread blocks a CU) --
+// 1024 blocks were two generations of latency-bound steps at 2^20 (step
+// 0.619 -> 0.615 ms, profiles/r05/ab_log.txt r6n)
+constexpr uint32_t RB_BLOCKS = 512;
 #ifndef PSIM_RR_THREADS
 #define PSIM_RR_THREADS 1024
 #endif
@@ -1580,7 +1584,7 @@ struct psim_handle {
     bool phase_timers = false;
     // blocks of the route / owner-partition passes (RB_MAX_BLOCKS; a test
     // hook, PSIM_ROUTE_BLOCKS, lowers it so small runs take several steps per block)
-    uint32_t rb_blocks = RB_MAX_BLOCKS;
+    uint32_t rb_blocks = RB_BLOCKS;
 };
 
 namespace {
