@@ -245,6 +245,10 @@ constexpr uint32_t RB_BLOCKS = 512;
 // k_bucket_route block: 1024 threads keep 16 waves per CU on its one block
 // per bucket (512: route 36 -> 31 us a round at 2^20, profiles/r03 p26)
 constexpr uint32_t RR_THREADS = PSIM_RR_THREADS;
+#ifndef PSIM_RR_REG
+#define PSIM_RR_REG 6
+#endif
+constexpr uint32_t RR_REG = PSIM_RR_REG;   // k_bucket_route: pairs a thread holds in registers
 
 // The exchange's wire format (G > 1): a record's first 32 B -- dst, src, type
 // word, seq, a0-a2 and word 7 -- is its head; a record with exchange ids
@@ -745,10 +749,13 @@ __global__ void __launch_bounds__(RR_THREADS) k_bucket_route(
     for (uint32_t j = threadIdx.x; j < 4 * W; j += blockDim.x) sm[j] = 0;
     if (threadIdx.x == 0) s_nl = 0;
     __syncthreads();
-    for (uint32_t p = s0 + threadIdx.x; p < s1; p += blockDim.x) {
-        const uint2 x = pairs[p];
+    // each pair's rank in its run (LDS atomics), the bound sums and masks; a
+    // bucket of at most RR_REG pairs a thread keeps its pairs and ranks in
+    // registers for the run placement below (all its loads issued at once;
+    // no rank array written and read back, no second read of the pairs)
+    auto count = [&](const uint2& x) {
         const uint32_t dl = x.x & wmask, cls = x.x >> 16;
-        rank[p] = atomicAdd(&cnt[dl], 1u);
+        const uint32_t r = atomicAdd(&cnt[dl], 1u);
         if (cls == KEY_BCAST) {                       // 1 (a duplicate's PRUNE) + the slot bit
             atomicAdd(&bs[dl], 1u);
             const uint32_t a0 = WIRE ? heads[x.y].q[1].x : rec[x.y].a0;
@@ -756,6 +763,22 @@ __global__ void __launch_bounds__(RR_THREADS) k_bucket_route(
         } else if (cls) {
             atomicAdd(&bs[dl], cls);
         }
+        return r;
+    };
+    const bool inreg = s1 - s0 <= RR_REG * blockDim.x;   // (uniform)
+    uint2 px[RR_REG];
+    uint32_t pr[RR_REG];
+    if (inreg) {
+#pragma unroll
+        for (uint32_t k = 0; k < RR_REG; k++) {
+            const uint32_t p = s0 + threadIdx.x + k * blockDim.x;
+            px[k] = p < s1 ? pairs[p] : make_uint2(0, 0);
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < RR_REG; k++)
+            if (s0 + threadIdx.x + k * blockDim.x < s1) pr[k] = count(px[k]);
+    } else {
+        for (uint32_t p = s0 + threadIdx.x; p < s1; p += blockDim.x) rank[p] = count(pairs[p]);
     }
     __syncthreads();
     // run starts: each thread scans W / RR_THREADS consecutive counts, then
@@ -763,13 +786,9 @@ __global__ void __launch_bounds__(RR_THREADS) k_bucket_route(
     const uint32_t per = W / RR_THREADS, j0 = threadIdx.x * per;
     uint32_t sum = 0;
     for (uint32_t j = 0; j < per; j++) sum += cnt[j0 + j];
-    spart[threadIdx.x] = sum;
-    __syncthreads();
-    for (uint32_t o = 1; o < RR_THREADS; o <<= 1) {   // Hillis-Steele inclusive scan
-        const uint32_t v = threadIdx.x >= o ? spart[threadIdx.x - o] : 0u;
-        __syncthreads();
-        spart[threadIdx.x] += v;
-        __syncthreads();
+    {
+        uint32_t tot;
+        spart[threadIdx.x] = block_excl<uint32_t, RR_THREADS>(sum, &tot) + sum;   // (inclusive)
     }
     for (uint32_t dl = threadIdx.x; dl < W; dl += blockDim.x) {
         const uint32_t d = (b << wshift) + dl;
@@ -793,9 +812,15 @@ __global__ void __launch_bounds__(RR_THREADS) k_bucket_route(
         in_beg[n] = s1;
         *hm = s1;
     }
-    for (uint32_t p = s0 + threadIdx.x; p < s1; p += blockDim.x) {
-        const uint2 x = pairs[p];
-        idx[s0 + pre[x.x & wmask] + rank[p]] = x.y;
+    if (inreg) {
+#pragma unroll
+        for (uint32_t k = 0; k < RR_REG; k++)
+            if (s0 + threadIdx.x + k * blockDim.x < s1) idx[s0 + pre[px[k].x & wmask] + pr[k]] = px[k].y;
+    } else {
+        for (uint32_t p = s0 + threadIdx.x; p < s1; p += blockDim.x) {
+            const uint2 x = pairs[p];
+            idx[s0 + pre[x.x & wmask] + rank[p]] = x.y;
+        }
     }
     __syncthreads();                                  // the runs are in place (same block)
     // the bucket's longer runs, listed in LDS (the BROADCAST masks are out:
