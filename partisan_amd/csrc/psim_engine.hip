@@ -1560,8 +1560,7 @@ struct psim_handle {
     // the lite list's kernel: k_lite_half, two nodes per wave (psim_lite.hip);
     // PSIM_LITE_WAVE=1 keeps the wave-per-node k_consume_lite (A/B)
     bool lite_half = true;
-    uint32_t ptl_blocks = 1024;         // ... and k_ptl / k_ptq blocks
-    bool ptl_quarter = false;           // k_ptq (PSIM_PTL_QUARTER=1) or k_ptl
+    uint32_t ptl_blocks = 1024;         // ... and k_ptl blocks
     uint64_t round = 0;
     // a round failed half-way (psim_step returned an error from inside a
     // round or batch): the state is not a round boundary any more, so every
@@ -1937,8 +1936,7 @@ int phase_events_prepare(psim_handle* h, Shard* s, const RoundCtl& ctl, RoundArg
         // (k_lite_half: two nodes per wave)
         const uint32_t lnodes = h->lite_half ? psim::lite_half_block() * 2 : psim::lite_block();
         s->lgrid = hv ? std::min<uint32_t>((uint32_t)((n + lnodes - 1) / lnodes), h->lite_blocks) : 0;
-        // (k_ptq: four nodes per wave)
-        const uint32_t qnodes = h->ptl_quarter ? psim::ptq_nodes() : PTL_BLOCK;
+        const uint32_t qnodes = PTL_BLOCK;
         s->qgrid = hv && h->cfg.plumtree ? std::min<uint32_t>((uint32_t)((n + qnodes - 1) / qnodes), h->ptl_blocks) : 0;
         TRY(s->stat_part.ensure((size_t)(s->pgrid + s->cgrid + s->rgrid + s->tgrid + s->sgrid + s->lgrid + s->qgrid) *
                                 NST));
@@ -2084,8 +2082,7 @@ int phase_consume(psim_handle* h, Shard* s, RoundArgs& a) {
             }
         }
         if (s->qgrid) {
-            if (h->ptl_quarter) k_ptq<<<s->qgrid, psim::ptq_block(), 0, s->stream>>>(a);
-            else k_ptl<<<s->qgrid, PTL_BLOCK, 0, s->stream>>>(a);
+            k_ptl<<<s->qgrid, PTL_BLOCK, 0, s->stream>>>(a);
         }
         if (s->tgrid) {
             RoundArgs c = a;
@@ -2906,13 +2903,12 @@ int psim_create(const psim_config* cfg, psim_handle** out) {
     h->lite_half = getenv("PSIM_LITE_WAVE") == nullptr;
     h->lite_blocks = h->lite_half ? grid("PSIM_LITE_GRID", psim::lite_half_grid(), 4 * psim::lite_half_grid())
                                   : grid("PSIM_LITE_GRID", psim::lite_grid(), 4 * psim::lite_grid());
-    // k_ptl (a lane per node); PSIM_PTL_QUARTER=1: k_ptq (four nodes per wave,
-    // parity-exact, slower: 0.602 against 0.584 ms a phase at 2^20 and 79.3
-    // against 68.1 ms at 2^26, profiles/r04/pq2 -- a row per node runs each
-    // handler for 4 nodes where a lane per node runs it for 64)
-    h->ptl_quarter = getenv("PSIM_PTL_QUARTER") != nullptr;
-    h->ptl_blocks = h->ptl_quarter ? grid("PSIM_PTL_GRID", psim::ptq_grid(), 2 * psim::ptq_grid())
-                                   : grid("PSIM_PTL_GRID", psim::ptl_grid(), psim::ptl_grid());
+    // k_ptl (a lane per node; round 4's four-nodes-per-wave k_ptq was
+    // parity-exact but slower -- 0.602 against 0.584 ms a phase at 2^20, 79.3
+    // against 68.1 ms at 2^26, profiles/r04/pq2: a row per node runs each
+    // handler for 4 nodes where a lane per node runs it for 64 -- and was
+    // removed in round 5)
+    h->ptl_blocks = grid("PSIM_PTL_GRID", psim::ptl_grid(), psim::ptl_grid());
     {
         const char* e = getenv("PSIM_PHASE_TIMERS");
         h->phase_timers = e && *e && *e != '0';
@@ -3713,7 +3709,7 @@ int psim_kernel_times(psim_handle* h, const char** names, double* ms, uint64_t* 
 
 // diagnostic: per node-round kernel of the last round (shard 0's blocks; the
 // stats rows every block leaves, before the route sums them), in the order
-// k_relay, k_shuf, k_lite_half / k_consume_lite, k_consume, k_ptl / k_ptq,
+// k_relay, k_shuf, k_lite_half / k_consume_lite, k_consume, k_ptl,
 // k_pt: out[4 k] nodes processed (stats nodes_processed), out[4 k + 1]
 // records delivered, out[4 k + 2] records emitted, out[4 k + 3] 0.  Returns
 // the number of kernels (6); 0 for the pluggable manager's one kernel.

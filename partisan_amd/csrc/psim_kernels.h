@@ -160,11 +160,6 @@ uint32_t lite_half_grid();
 uint32_t lite_half_block();
 // lane-per-node Plumtree phases (psim_consume.hip); hands k_pt what does not fit
 __global__ void k_ptl(RoundArgs args);
-// the same with four nodes per wave, one per 16-lane row (psim_ptq.hip)
-__global__ void k_ptq(RoundArgs args);
-uint32_t ptq_grid();
-uint32_t ptq_block();
-uint32_t ptq_nodes();
 // the Plumtree phase of the nodes k_relay listed (psim_consume.hip)
 __global__ void k_pt(RoundArgs args);
 // diagnostic builds (-DPSIM_STAMPS): per-phase cycle sums of k_consume, reset on read

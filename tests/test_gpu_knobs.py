@@ -2,9 +2,8 @@
 results: another route bucket width (PSIM_ROUTE_WSHIFT), other grids for
 every node-round kernel (PSIM_*_GRID), the HyParView kernels one after
 another or side by side (PSIM_CONCURRENT_PHASE), the wave-per-node
-lite kernel instead of the two-nodes-per-wave one (PSIM_LITE_WAVE) and the
-four-nodes-per-wave Plumtree kernel instead of the lane-per-node one
-(PSIM_PTL_QUARTER) must reproduce the oracle bit for bit.  The knobs are read once per process, so each set runs in
+lite kernel instead of the two-nodes-per-wave one (PSIM_LITE_WAVE) must
+reproduce the oracle bit for bit.  The knobs are read once per process, so each set runs in
 a child process (tests/_knob_run.py)."""
 import os
 import subprocess
@@ -17,12 +16,11 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 
 
 @pytest.mark.parametrize("knobs", [
-    {"PSIM_ROUTE_WSHIFT": "10"},
+    {"PSIM_ROUTE_WSHIFT": "12"},
     {"PSIM_LITE_WAVE": "1"},
     {"PSIM_LITE_GRID": "x1", "PSIM_PTL_GRID": "x2", "PSIM_PT_GRID": "x2", "PSIM_CONSUME_GRID": "x2"},
     {"PSIM_CONCURRENT_PHASE": "1"},
-    {"PSIM_PTL_QUARTER": "1"},
-    {"PSIM_PTL_QUARTER": "1", "PSIM_PTL_GRID": "x1"},
+    {"PSIM_PTL_GRID": "x1"},
 ])
 def test_knobs_keep_parity(knobs):
     env = dict(os.environ, **knobs)
