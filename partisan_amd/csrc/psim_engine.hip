@@ -727,7 +727,7 @@ __device__ __forceinline__ uint4 rec_piece(const Msg* __restrict__ rec, uint32_t
 // BROADCAST message-slot mask (64 bits): 4 x W words.
 template <bool WIRE>
 __global__ void __launch_bounds__(RR_THREADS) k_bucket_route(
-    uint32_t n, uint32_t wshift, const uint32_t* __restrict__ base,
+    uint32_t n, uint32_t wshift, uint32_t regcap, const uint32_t* __restrict__ base,
     const uint2* __restrict__ pairs, const Msg* __restrict__ rec, const Wire* __restrict__ heads,
     const Wire* __restrict__ tails, uint32_t* rank, unsigned long long* cb,
     unsigned long long* bmask, uint32_t* in_beg, uint32_t* idx, uint32_t* tmp, Msg* __restrict__ inbox, uint64_t* hm,
@@ -765,7 +765,7 @@ __global__ void __launch_bounds__(RR_THREADS) k_bucket_route(
         }
         return r;
     };
-    const bool inreg = s1 - s0 <= RR_REG * blockDim.x;   // (uniform)
+    const bool inreg = s1 - s0 <= regcap * blockDim.x;   // (uniform; regcap <= RR_REG)
     uint2 px[RR_REG];
     uint32_t pr[RR_REG];
     if (inreg) {
@@ -1609,6 +1609,7 @@ struct psim_handle {
     // blocks of the route / owner-partition passes (RB_MAX_BLOCKS; a test
     // hook, PSIM_ROUTE_BLOCKS, lowers it so small runs take several steps per block)
     uint32_t rb_blocks = RB_BLOCKS;
+    uint32_t rr_reg = RR_REG;           // k_bucket_route: pairs a thread may hold (PSIM_ROUTE_REG=0: the array path)
 };
 
 namespace {
@@ -2164,11 +2165,11 @@ int route_group(psim_handle* h, Shard* s, bool dense, uint32_t m) {
                                                                      s->batch_round1, st);
     if (dense)
         k_bucket_route<true><<<nb, RR_THREADS, lds_r, s->stream>>>(
-            n, wshift, s->rbase.p, s->pairs.p, nullptr, in.wire, in.tails, s->rank.p, s->cb.p, s->bmask.p,
+            n, wshift, h->rr_reg, s->rbase.p, s->pairs.p, nullptr, in.wire, in.tails, s->rank.p, s->cb.p, s->bmask.p,
             s->in_beg.p, s->ivals.p, s->tmp.p, s->inbox.p, s->pin_dev + PIN_M, s->rcap, s->ctl.p);
     else
         k_bucket_route<false><<<nb, RR_THREADS, lds_r, s->stream>>>(
-            n, wshift, s->rbase.p, s->pairs.p, in.rec, nullptr, nullptr, s->rank.p, s->cb.p, s->bmask.p,
+            n, wshift, h->rr_reg, s->rbase.p, s->pairs.p, in.rec, nullptr, nullptr, s->rank.p, s->cb.p, s->bmask.p,
             s->in_beg.p, s->ivals.p, s->tmp.p, s->inbox.p, s->pin_dev + PIN_M, s->rcap, s->ctl.p);
     HIP_TRY(hipGetLastError());
     return PSIM_OK;
@@ -2914,6 +2915,8 @@ int psim_create(const psim_config* cfg, psim_handle** out) {
         h->phase_timers = e && *e && *e != '0';
         const char* b = getenv("PSIM_ROUTE_BLOCKS");
         if (b && *b) h->rb_blocks = std::max<uint32_t>(1, std::min<uint32_t>(RB_MAX_BLOCKS, (uint32_t)atoi(b)));
+        const char* g = getenv("PSIM_ROUTE_REG");     // (test hook: the large-bucket path everywhere)
+        if (g && *g) h->rr_reg = std::min<uint32_t>(RR_REG, (uint32_t)atoi(g));
     }
     h->device = dev;
     for (uint32_t g = 0; g < G; g++) {

@@ -1,5 +1,6 @@
 """The engine's measurement knobs change launch shapes and algorithms, never
-results: another route bucket width (PSIM_ROUTE_WSHIFT), other grids for
+results: another route bucket width (PSIM_ROUTE_WSHIFT), the route's
+large-bucket path for every bucket (PSIM_ROUTE_REG=0), other grids for
 every node-round kernel (PSIM_*_GRID), the HyParView kernels one after
 another or side by side (PSIM_CONCURRENT_PHASE), the wave-per-node
 lite kernel instead of the two-nodes-per-wave one (PSIM_LITE_WAVE) must
@@ -17,6 +18,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 
 @pytest.mark.parametrize("knobs", [
     {"PSIM_ROUTE_WSHIFT": "12"},
+    {"PSIM_ROUTE_REG": "0", "PSIM_ROUTE_BLOCKS": "7"},
     {"PSIM_LITE_WAVE": "1"},
     {"PSIM_LITE_GRID": "x1", "PSIM_PTL_GRID": "x2", "PSIM_PT_GRID": "x2", "PSIM_CONSUME_GRID": "x2"},
     {"PSIM_CONCURRENT_PHASE": "1"},
