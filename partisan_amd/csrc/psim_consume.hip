@@ -2703,10 +2703,18 @@ DEV void col_add(const LdsCol& V, uint32_t& n, uint32_t x) {
     n++;
 }
 
+#ifndef PSIM_PTL_CONN         // k_ptl takes nodes with a connection table (0: k_pt does, for A/B)
+#define PSIM_PTL_CONN 1
+#endif
+constexpr uint32_t PTL_CN = 4;  // ... of at most 4 entries (a lane's registers; more: k_pt)
 struct PtLane {
     uint32_t id, me_part, act_n;
     uint32_t A[PSIM_ACTIVE_CAP];
     uint32_t cmask;                // bit j: A[j] is a live connection (ptl_conn's test, per member)
+#if PSIM_PTL_CONN
+    uint32_t L[PTL_CN];            // the connection table's lingering peers (entries without a flag)
+    uint32_t lmask;                // bit k: L[k] is outside the active view, running, same partition
+#endif
     uint32_t root0;                // slot 0's root (NONE = free)
     LdsCol EG, LZ, OL, OH;         // slot 0's eager / lazy sets; outstanding keys (low, high words)
     uint32_t ne, nl, on;
@@ -2745,6 +2753,12 @@ DEV bool ptl_conn(KArgs& a, const PtLane& n, uint32_t ident) {
     bool c = false;
 #pragma unroll
     for (int j = 0; j < PSIM_ACTIVE_CAP; j++) c |= ((n.cmask >> j) & 1u) && n.A[j] == p;
+#if PSIM_PTL_CONN
+    // conn_has: a lingering peer's connection (lmask holds none of the
+    // active members: for those the active test alone decides)
+#pragma unroll
+    for (int k = 0; k < (int)PTL_CN; k++) c |= ((n.lmask >> k) & 1u) && n.L[k] == p;
+#endif
     return c;
 }
 
@@ -2937,9 +2951,13 @@ __global__ void PTL_BOUNDS k_ptl(RoundArgs) {
             uint64_t bm = 0;                          // message slots of the BROADCASTs
             // (an outstanding extension row taken earlier holds zeros while the
             // table fits its own row: this round's adds must fit that row)
-            // (a node with a connection table -- lingering peers, or active
-            // members without a connection -- tests its sends in k_pt)
-            bool ok = r0.y == NONE && r0.z == NONE && r0.w == NONE && (w11 & 0xFFFFu) == 0 &&
+            // (a connection table -- lingering peers, or active members
+            // without a connection -- of at most PTL_CN entries is read below
+            // for the sends' tests; a larger one, or X-BOT's closing entries,
+            // go to k_pt: at the C line's broadcast peak every node k_pt took
+            // held one, profiles/r05/ab_log.txt r6u)
+            bool ok = r0.y == NONE && r0.z == NONE && r0.w == NONE &&
+                      (PSIM_PTL_CONN ? (w11 >> 24) == 0 && (w11 & 0xFFu) <= PTL_CN : (w11 & 0xFFFFu) == 0) &&
                       (root0 == NONE || ((rtw4 >> 8) == 0 && (rtw5 >> 8) == 0));
 #pragma unroll
             for (int j = 0; j < PTL_RREG; j++) {      // (all issued before the first is used)
@@ -2985,6 +3003,45 @@ __global__ void PTL_BOUNDS k_ptl(RoundArgs) {
         const uint32_t id = D.x;
         const size_t li = id - a.lo;
         n.cmask = ptl_conn_mask(a, n, up);
+#if PSIM_PTL_CONN
+        n.lmask = 0;
+        {
+            // the connection table (k_pt's conn_has, pt:633-638): an active
+            // member marked PSIM_CONN_DOWN has no connection; an entry without
+            // a flag is a lingering peer with one (no closing entries here:
+            // X-BOT's go to k_pt)
+            const uint32_t cn = w11 & 0xFFu;
+            uint32_t CN[PTL_CN] = {};
+            if (cn) {
+                const uint4 c0 = *reinterpret_cast<const uint4*>(a.conn + li * PSIM_CONN_CAP);
+                CN[0] = c0.x; CN[1] = c0.y; CN[2] = c0.z; CN[3] = c0.w;
+            }
+            uint32_t down = 0, inA = 0;
+#pragma unroll
+            for (int k = 0; k < (int)PTL_CN; k++) {
+                const uint32_t e = CN[k];
+                bool ina = false;
+#pragma unroll
+                for (int j = 0; j < PSIM_ACTIVE_CAP; j++) {
+                    down |= ((uint32_t)k < cn && (uint32_t)j < act_n && e == (n.A[j] | PSIM_CONN_DOWN)) ? 1u << j : 0u;
+                    ina |= (uint32_t)j < act_n && n.A[j] == e;
+                }
+                inA |= ina ? 1u << k : 0u;
+            }
+            n.cmask &= ~down;
+            upart_t lup[PTL_CN];
+#pragma unroll
+            for (int k = 0; k < (int)PTL_CN; k++) {
+                const bool lg = (uint32_t)k < cn && !(CN[k] & (PSIM_CONN_DOWN | PSIM_CONN_CLOSING)) && CN[k] < a.n_nodes;
+                n.L[k] = lg ? CN[k] : NONE;
+                lup[k] = lg ? a.upart[CN[k]] : UPART_DOWN;
+            }
+#pragma unroll
+            for (int k = 0; k < (int)PTL_CN; k++)
+                n.lmask |= (n.L[k] != NONE && n.L[k] != id && !((inA >> k) & 1u) && (uint32_t)lup[k] == n.me_part)
+                               ? 1u << k : 0u;
+        }
+#endif
         PTL_STAMP(2);
         n.root0 = root0;
         n.ne = root0 == NONE ? 0u : (rtw4 & 0xFF);
