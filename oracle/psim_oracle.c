@@ -188,7 +188,8 @@ static uint64_t uniform_key(ctx *c) { return draw58(c) >> 5; }
  * add_element/2 prepends to the slot's bucket; past 5 n elements
  * maybe_expand/2 opens slot n + 1 and rehashes its buddy's bucket into the
  * two (order kept); del_element/2 below 3 n elements (n > 16) closes slot n
- * with maybe_contract/2, its bucket put in front of its buddy's (B2 ++ B1).
+ * with maybe_contract/2, its bucket appended to its buddy's
+ * (put_bucket_s(Segs0, Slot1, B1 ++ B2), B1 the buddy's bucket).
  * to_list/1 folds slot n..1, each bucket head first, prepending: slot 1..n,
  * oldest first within a slot.  Up to 80 elements that
  * is 16 buckets, erlang:phash(NodeSpec, 16) - 1.  The hash is
@@ -217,13 +218,19 @@ static uint32_t set_slot(const struct psim_handle *h, uint32_t e, uint32_t ns) {
     return x < ns ? x : x - m / 2;
 }
 /* the list re-ordered by slot under ns slots, stably: after a slot opens
- * (its entries, from the buddy slot, go to the end) or closes (its entries,
- * at the end, go after the buddy slot's own) */
-static void set_reslot(const struct psim_handle *h, uint32_t *l, uint32_t n, uint32_t ns) {
+ * (its entries, from the buddy slot, go to the end: rehash/4 keeps order).
+ * `closing` (a slot index under ns + 1, or ~0u): the slot maybe_contract/2
+ * just closed; its entries, at the list's end, go in front of the buddy
+ * slot's own -- the merged bucket B1 ++ B2 read back by to_list's reversing
+ * fold */
+static void set_reslot(const struct psim_handle *h, uint32_t *l, uint32_t n, uint32_t ns, uint32_t closing) {
     for (uint32_t i = 1; i < n; i++) {
-        uint32_t e = l[i], k = set_slot(h, e, ns);
+        uint32_t e = l[i], k = 2 * set_slot(h, e, ns) + (set_slot(h, e, ns + 1) == closing ? 0u : 1u);
         int j = (int)i - 1;
-        while (j >= 0 && set_slot(h, l[j], ns) > k) { l[j + 1] = l[j]; j--; }
+        while (j >= 0 && 2 * set_slot(h, l[j], ns) + (set_slot(h, l[j], ns + 1) == closing ? 0u : 1u) > k) {
+            l[j + 1] = l[j];
+            j--;
+        }
         l[j + 1] = e;
     }
 }
@@ -246,7 +253,7 @@ static void set_add(const struct psim_handle *h, uint32_t *l, uint32_t *n, uint3
     (*n)++;
     if (ns && *n > 5 * *ns) {           /* maybe_expand/2: size + 1 > exp_size */
         (*ns)++;
-        set_reslot(h, l, *n, *ns);
+        set_reslot(h, l, *n, *ns, ~0u);
     }
 }
 
@@ -261,7 +268,7 @@ static void set_del_slots(const struct psim_handle *h, uint32_t *l, uint32_t *n,
     *n = j;
     if (*n < 3 * *ns && *ns > 16) {
         (*ns)--;
-        set_reslot(h, l, *n, *ns);
+        set_reslot(h, l, *n, *ns, *ns);
     }
 }
 

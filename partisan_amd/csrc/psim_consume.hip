@@ -3307,4 +3307,7 @@ int debug_stamps(unsigned long long* out) {
 int debug_stamps(unsigned long long*) { return 0; }
 #endif
 
+// this TU's layout (psim_kernels.h layout_sig, checked by psim_create)
+uint32_t layout_sig_consume() { return layout_sig(); }
+
 }  // namespace psim

@@ -249,6 +249,15 @@ constexpr uint32_t RR_THREADS = PSIM_RR_THREADS;
 #define PSIM_RR_REG 6
 #endif
 constexpr uint32_t RR_REG = PSIM_RR_REG;   // k_bucket_route: pairs a thread holds in registers
+// bucket widths 2^11 .. 2^13 (route_group): k_bucket_route's LDS holds 4 W
+// words -- counts, bound sums, and W 64-bit BROADCAST masks whose 2 W words
+// then carry the block sort's RUN_LDS-word buffer and the long-run list (at
+// most W destinations), so W >= RUN_LDS; its run-start scan gives each
+// thread W / RR_THREADS counts
+constexpr uint32_t WSHIFT_MIN = 11, WSHIFT_MAX = 13;
+static_assert((1u << WSHIFT_MIN) >= RUN_LDS, "k_bucket_route: the sort buffer and the long-run list share 2 W words");
+static_assert((1u << WSHIFT_MIN) % RR_THREADS == 0, "k_bucket_route: W / RR_THREADS counts a thread");
+static_assert((1u << WSHIFT_MAX) * 16 <= 160 * 1024, "k_bucket_route: 16 W bytes of LDS");
 
 // The exchange's wire format (G > 1): a record's first 32 B -- dst, src, type
 // word, seq, a0-a2 and word 7 -- is its head; a record with exchange ids
@@ -826,7 +835,7 @@ __global__ void __launch_bounds__(RR_THREADS) k_bucket_route(
     // the bucket's longer runs, listed in LDS (the BROADCAST masks are out:
     // their words hold the list and the block sort's buffer)
     uint32_t* sv = reinterpret_cast<uint32_t*>(mk);   // RUN_LDS words
-    uint32_t* ll = sv + RUN_LDS;                      // <= W destinations (2 W words in all, W >= 4096)
+    uint32_t* ll = sv + RUN_LDS;                      // <= W destinations (2 W words in all: W >= RUN_LDS)
     for (uint32_t dl = threadIdx.x; dl < W; dl += blockDim.x) {
         const uint32_t k = cnt[dl];
         if (k < 2) continue;
@@ -1546,6 +1555,7 @@ struct Shard {
     uint64_t desc_cap = 0;
     uint32_t batch_round1 = 0;
     uint32_t stat_slot = 0;
+    bool outx_short = false;            // the outstanding pool failed to grow (reported once per shard)
 };
 
 }  // namespace
@@ -2123,9 +2133,7 @@ int route_group(psim_handle* h, Shard* s, bool dense, uint32_t m) {
     uint32_t wshift = n > (1u << 26) ? 13 : n > (1u << 22) ? 12 : 11;
     if (const char* e = getenv("PSIM_ROUTE_WSHIFT")) {  // (another bucket width, for measurements)
         const int v = atoi(e);
-        // (k_bucket_route's long-run list and sort buffer share the 2 W
-        // words of its BROADCAST masks: W >= 2048)
-        if ((1u << v) >= RR_THREADS && v >= 11 && v <= 13) wshift = (uint32_t)v;
+        if (v >= (int)WSHIFT_MIN && v <= (int)WSHIFT_MAX) wshift = (uint32_t)v;
     }
     const uint32_t W = 1u << wshift, nb = (n + W - 1) >> wshift;
     const RouteIn in{s->outbox.p, s->okey.p, s->obase.p, s->ocnt.p, dense ? m : n, s->lo,
@@ -2858,6 +2866,16 @@ int psim_create(const psim_config* cfg, psim_handle** out) {
         cfg->strategy > PSIM_STRATEGY_SCAMP_V2 || cfg->scamp_c < 1 || cfg->scamp_c > 64 ||
         cfg->fanout > 64 || cfg->strict > 1)   /* (picks land in one 64-lane register) */
         return PSIM_EINVAL;
+    {
+        // every kernel TU compiled against the same layout (psim_kernels.h
+        // layout_sig): a mixed A/B library is refused here, not in a kernel
+        const uint32_t e = layout_sig(), c = layout_sig_consume(), l = layout_sig_lite(), st = layout_sig_strategy();
+        if (c != e || l != e || st != e) {
+            std::fprintf(stderr, "psim: library TUs built with different layouts (engine %08x, consume %08x, "
+                         "lite %08x, strategy %08x): rebuild every TU with the same macros\n", e, c, l, st);
+            return PSIM_ESTATE;
+        }
+    }
     const bool full = cfg->manager == PSIM_MANAGER_PLUGGABLE && cfg->strategy == PSIM_STRATEGY_FULL;
     uint32_t world = std::max<uint32_t>(cfg->shard_world, 1);
     uint32_t local = std::max<uint32_t>(cfg->n_shards, 1);
@@ -3171,10 +3189,12 @@ int grow_outx(Shard* s) {
     if (rows >= s->n || used * 2 < rows) return PSIM_OK;
     const uint64_t want = std::min<uint64_t>(std::max<uint64_t>(2 * rows, used + 1024), s->n);
     if (s->outx.ensure_keep(want * OUT_EXT, used * OUT_EXT, s->stream) != PSIM_OK) {
-        static bool told = false;
-        if (!told) std::fprintf(stderr, "psim: the outstanding pool could not grow past %llu rows\n",
-                                (unsigned long long)rows);
-        told = true;
+        // (per shard: every handle in the process reports its own; the
+        // tables that then find no row count PSIM_OVF_PT_OUT overflows in the
+        // round's stats, and cfg.strict fails the step on the first)
+        if (!s->outx_short) std::fprintf(stderr, "psim: shard %u: the outstanding pool could not grow past %llu rows\n",
+                                         s->idx, (unsigned long long)rows);
+        s->outx_short = true;
         return PSIM_OK;
     }
     HIP_TRY(hipMemsetAsync(s->outx.p + used * OUT_EXT, 0, (s->outx.n - used * OUT_EXT) * 8, s->stream));
@@ -3633,16 +3653,37 @@ int psim_restore(psim_handle* h, const void* buf, size_t size) {
         hd.fw != h->fw || hd.G != h->G || hd.world != (uint32_t)h->world)
         return PSIM_EINVAL;
     if (hd.btab_hash != h->btab_hash) return PSIM_EINVAL;   // another view-order table
+    // the whole layout is checked before any state changes: every shard head
+    // and every section must lie inside the buffer, so a short or mismatched
+    // snapshot leaves the handle as it was
+    {
+        const char* q = o;
+        if ((size_t)(end - q) < hd.started_n) return PSIM_EINVAL;
+        q += hd.started_n;
+        for (Shard* s : h->shards) {
+            if ((size_t)(end - q) < sizeof(ShardHead)) return PSIM_EINVAL;
+            ShardHead sh;
+            memcpy(&sh, q, sizeof sh); q += sizeof sh;
+            if (sh.lo != s->lo || sh.n != s->n || sh.pay_cur > 1) return PSIM_EINVAL;
+            if ((size_t)sh.pad[1] * IDMAP_EXT > s->mapx.n) return PSIM_EINVAL;
+            if (sh.out_rows && !s->outx.p) return PSIM_EINVAL;
+            for (const Section& x : snap_sections(h, s, sh)) {
+                if ((size_t)(end - q) < x.bytes) return PSIM_EINVAL;
+                q += x.bytes;
+            }
+        }
+    }
+    // from here on a failure (an allocation, a copy) leaves a half-restored
+    // state: the handle stays failed (psim_step answers PSIM_ESTATE) until a
+    // restore succeeds
+    h->failed = true;
     if (hd.started_n) {
-        if ((size_t)(end - o) < hd.started_n) return PSIM_EINVAL;
         h->started.assign(o, o + hd.started_n); o += hd.started_n;
     }
     for (Shard* s : h->shards) {
         HIP_TRY(hipStreamSynchronize(s->stream));
-        if ((size_t)(end - o) < sizeof(ShardHead)) return PSIM_EINVAL;
         ShardHead sh;
         memcpy(&sh, o, sizeof sh); o += sizeof sh;
-        if (sh.lo != s->lo || sh.n != s->n) return PSIM_EINVAL;
         s->m_in = sh.m_in; s->pay_cur = (int)sh.pay_cur;
         s->tomb_live = sh.pad[0] != 0;
         if (s->tomb_live) h->tomb = true;
@@ -3650,9 +3691,7 @@ int psim_restore(psim_handle* h, const void* buf, size_t size) {
         if (sh.pay_rows) TRY(s->pay[s->pay_cur ^ 1].ensure((size_t)sh.pay_rows * 2 * h->fw));
         if (h->cfg.manager == PSIM_MANAGER_PLUGGABLE && s->pay_top.p)
             HIP_TRY(hipMemcpy(s->pay_top.p, &sh.pay_rows, 4, hipMemcpyHostToDevice));
-        if ((size_t)sh.pad[1] * IDMAP_EXT > s->mapx.n) return PSIM_EINVAL;
         HIP_TRY(hipMemcpy(s->mapx_top.p, &sh.pad[1], 4, hipMemcpyHostToDevice));
-        if (sh.out_rows && !s->outx.p) return PSIM_EINVAL;
         if (s->outx.p) {
             // (a grown pool: this handle's grows to hold the snapshot's rows;
             // the rows past them zeroed, as a fresh pool's are)
@@ -3663,7 +3702,6 @@ int psim_restore(psim_handle* h, const void* buf, size_t size) {
         }
         HIP_TRY(hipMemcpy(s->outx_top.p, &sh.out_rows, 4, hipMemcpyHostToDevice));
         for (const Section& x : snap_sections(h, s, sh)) {
-            if ((size_t)(end - o) < x.bytes) return PSIM_EINVAL;
             if (x.bytes) HIP_TRY(hipMemcpy(x.p, o, x.bytes, hipMemcpyHostToDevice));
             o += x.bytes;
         }

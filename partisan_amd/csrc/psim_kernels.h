@@ -1,5 +1,7 @@
 // psim_kernels.h -- kernel argument blocks shared by the kernel TUs and the host.
 #pragma once
+#include <stddef.h>
+
 #include "psim_device.h"
 
 namespace psim {
@@ -228,6 +230,35 @@ __device__ __forceinline__ void lite_counts(Args& a, uint32_t (&c)[4], uint32_t&
 #ifndef PSIM_SHORT_TAIL
 #define PSIM_SHORT_TAIL 1
 #endif
+
+// The layout every kernel TU was compiled against: the shared structs' sizes
+// and field offsets, the record-format and table macros a -D can change, the
+// ABI.  Each TU returns its own value (layout_sig_consume/lite/strategy, and
+// the engine's) and psim_create refuses a library whose TUs disagree: an A/B
+// build that recompiles one TU with a layout macro (make variant / lvariant /
+// evariant X=...) and links it against the other TUs' objects would otherwise
+// hand the route records and keys in another format (round 5's r4lite fault
+// in k_bucket_route, profiles/r05/ab_log.txt).
+constexpr uint32_t layout_mix(uint32_t h, uint64_t v) {
+    return ((h ^ (uint32_t)v) * 0x01000193u ^ (uint32_t)(v >> 32)) * 0x01000193u;
+}
+constexpr uint32_t layout_sig() {
+    uint32_t h = 0x811C9DC5u;
+    const uint64_t v[] = {
+        PSIM_ABI_VERSION, sizeof(RoundArgs), offsetof(RoundArgs, flags), offsetof(RoundArgs, upart),
+        offsetof(RoundArgs, hdr), offsetof(RoundArgs, conn), offsetof(RoundArgs, outx_rows),
+        offsetof(RoundArgs, desc), offsetof(RoundArgs, desc_lite), offsetof(RoundArgs, stat_pt),
+        offsetof(RoundArgs, rec_out), offsetof(RoundArgs, okey), offsetof(RoundArgs, ktime),
+        offsetof(RoundArgs, ctl), offsetof(RoundArgs, fbits), offsetof(RoundArgs, omit),
+        sizeof(Hdr), sizeof(Msg), sizeof(upart_t), PSIM_SHORT_TAIL, PTL_BLOCK, KEY_DST_BITS, KEY_BCAST,
+        PSIM_ACTIVE_CAP, PSIM_PASSIVE_CAP, PSIM_EXCHANGE_CAP, PSIM_PT_ROOTS, PSIM_PT_OUT_CAP, PSIM_IDMAP_CAP,
+        PSIM_CONN_CAP, PSIM_SVIEW_CAP, OUT_IN, IDMAP_IN, RT_SET, RT_WORDS, NST, CRASH_GRAIN_SHIFT};
+    for (uint64_t x : v) h = layout_mix(h, x);
+    return h;
+}
+uint32_t layout_sig_consume();
+uint32_t layout_sig_lite();
+uint32_t layout_sig_strategy();
 
 __device__ __forceinline__ KArgs& kargs() {
     KArgs* p = (KArgs*)__builtin_amdgcn_kernarg_segment_ptr();

@@ -703,4 +703,7 @@ int debug_stamps_half(unsigned long long* out) {
 #else
 int debug_stamps_half(unsigned long long*) { return 0; }
 #endif
+// this TU's layout (psim_kernels.h layout_sig, checked by psim_create)
+uint32_t layout_sig_lite() { return layout_sig(); }
+
 }  // namespace psim

@@ -91,8 +91,9 @@ DEV void add_set2(uint32_t* lds, L2& V, uint32_t& n, uint32_t e, uint32_t& ns) {
 
 // sets:del_element/2 of a member at list position i, then maybe_contract/2:
 // below 3 ns elements (ns > 16) slot ns - 1 closes and its entries join its
-// buddy slot ns - 1 - MaxN/2, after that slot's own entries (B2 ++ B1 in
-// bucket order, whose to_list is B1's entries, then B2's)
+// buddy slot ns - 1 - MaxN/2 as put_bucket_s(Segs0, Slot1, B1 ++ B2) stores
+// them (B1 the buddy's bucket, B2 the closing slot's); to_list's reversing
+// fold then yields the closing slot's entries first, then the buddy's own
 DEV void del_set2(uint32_t* lds, L2& V, uint32_t& n, uint32_t e, uint32_t& ns) {
     const uint8_t* bt = kargs().btab;
     const uint32_t l = lane_id();
@@ -109,10 +110,10 @@ DEV void del_set2(uint32_t* lds, L2& V, uint32_t& n, uint32_t e, uint32_t& ns) {
     }
     if (!(n < 3 * ns && ns > 16)) return;
     const uint32_t top = ns - 1, to = top - set_maxn(ns) / 2;
-    // the closing slot's entries (at the list's end) go after every other
-    // entry of a slot <= `to`
+    // the closing slot's entries (at the list's end) go after every entry of
+    // a slot < `to`, in front of the buddy slot's own
     const bool ga = l < n && set_slot(bt, V.a, ns) == top, gb = 64 + l < n && set_slot(bt, V.b, ns) == top;
-    const bool ea = l < n && !ga && set_slot(bt, V.a, ns) <= to, eb = 64 + l < n && !gb && set_slot(bt, V.b, ns) <= to;
+    const bool ea = l < n && !ga && set_slot(bt, V.a, ns) < to, eb = 64 + l < n && !gb && set_slot(bt, V.b, ns) < to;
     const uint64_t bga = ballot(ga), bgb = ballot(gb);
     const uint32_t p = popc(ballot(ea)) + popc(ballot(eb)), g = popc(bga) + popc(bgb);
     const uint64_t na = ballot(l < n && !ga), nb = ballot(64 + l < n && !gb);
@@ -718,5 +719,8 @@ __global__ void __launch_bounds__(256) k_consume_pl(RoundArgs args) {
         kargs().stat_part[(size_t)blockIdx.x * NST + i] = sst[i];
     if (threadIdx.x == 0) atomicMax(&kargs().ktime[1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
 }
+
+// this TU's layout (psim_kernels.h layout_sig, checked by psim_create)
+uint32_t layout_sig_strategy() { return layout_sig(); }
 
 }  // namespace psim

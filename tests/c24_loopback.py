@@ -1,0 +1,118 @@
+"""Config D's HyParView half (BASELINE.json configs[3]: "HyParView 16M nodes
+... node-range sharded across 8 GPUs") through the rank path, VERDICT r5
+item 1a: HyParView + Plumtree on config C's survey schedule at 2^24 nodes,
+node-range sharded over 8 loopback ranks (psim_loopback_comm_id: the
+multi-rank code path of DESIGN.md section 7 -- owner partition, count
+all-to-all, the 32-B wire exchange, stats all-reduce, overlay all-gathers --
+on one GPU, the ranks as threads), against the one-shard engine on the same
+GPU, bit for bit: every round's stats and record digest, the overlay
+statistics, and every node's row (hashed in chunks) at the end.  Then C's
+overlay properties on that state (tests/c_overlay.py's classification, as
+test_c_overlay holds them at 2^18 and 2^20): no isolated node, the outside
+set small (2.8e-4 at 2^24), the tracked broadcast
+reaching exactly the giant component, active links symmetric, and messages
+conserved round to round.
+Schedule (partisan_amd.workloads.BenchSchedule "C"/"survey", bench.py's
+headline line at 16x the nodes): survey_join's 64-round ramp, 100 warm-up
+rounds, 5 more, then the broadcast from node 0 and 40 rounds (its last hop
+at 2^24 is ~28).
+
+Run directly (prints progress) or from tests/test_gpu_c24.py.  Exit 0 = equal."""
+import hashlib
+import os
+import sys
+import time
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+sys.path.insert(0, os.path.dirname(HERE))
+
+import numpy as np  # noqa: E402
+
+import _scenarios as S  # noqa: E402
+import c_overlay  # noqa: E402
+from _loopback import LoopbackRanks  # noqa: E402
+from partisan_amd import Simulator  # noqa: E402
+from partisan_amd import workloads as W  # noqa: E402
+from partisan_amd.sim import default_config  # noqa: E402
+
+N = int(os.environ.get("PSIM_C24_NODES", 1 << 24))
+RANKS = 8
+SEED = 1
+WARMUP, WINDOW = 5, 40
+T0 = time.time()
+
+
+def log(*a):
+    print(f"[{time.time() - T0:7.1f}s]", *a, file=sys.stderr, flush=True)
+
+
+def run(sim, label):
+    sched = W.BenchSchedule("C", "survey", N, SEED, WARMUP)
+    boot, until = sched.bootstrap()
+
+    def hook(r):
+        if r % 16 == 0:
+            log(label, "round", r)
+    st = [sim.run_schedule(boot, until, extra=hook)]
+    for i in range(sched.t_start + WINDOW):
+        sched.apply(sim, i)
+        st.append(sim.step(1))
+    st = np.concatenate(st)
+    log(label, "done,", len(st), "rounds")
+    return st
+
+
+def row_hashes(sim, chunk=1 << 18):
+    out = []
+    for lo in range(0, N, chunk):
+        v = sim.nodes(lo, min(chunk, N - lo))
+        out.append(hashlib.sha1(v.tobytes()).hexdigest())
+    return out
+
+
+def main():
+    one = Simulator(default_config(n_nodes=N, seed=SEED, device=0))
+    st1 = run(one, "one shard")
+    h1 = one.histograms()
+    cls, _ = c_overlay.classify(one)
+    log("one shard classified", cls)
+    rows1 = row_hashes(one)
+    one.close()
+    log("one shard rows hashed")
+    ranks = LoopbackRanks(default_config(n_nodes=N, seed=SEED), RANKS)
+    st8 = run(ranks, f"{RANKS} loopback ranks")
+    S.compare_stats(st8, st1)
+    log("stats and digests equal over", len(st1), "rounds")
+    h8 = ranks.histograms()
+    for k in h1:
+        assert np.array_equal(np.asarray(h1[k]), np.asarray(h8[k])), f"overlay statistic {k} differs"
+    rows8 = row_hashes(ranks)
+    ranks.close()
+    bad = [i for i, (a, b) in enumerate(zip(rows1, rows8)) if a != b]
+    assert not bad, f"node rows differ in chunks {bad[:8]}"
+    log("node rows equal (", len(rows1), "chunks ) and overlay statistics equal")
+    # C's properties (test_c_overlay's, at 2^24)
+    assert int(st1["overflow"].sum()) == 0
+    em = st1["emitted"].sum(axis=1)
+    got = st1["delivered"].sum(axis=1) + st1["dropped"]
+    assert np.array_equal(em[:-1], got[1:]), "messages not conserved"
+    assert cls["n_up"] == N and cls["isolated"] == 0, cls
+    assert cls["outside"] == 0 or cls["min_peers_outside"] >= 1, cls
+    assert cls["outside_frac"] <= 0.002, cls
+    assert all(x >= 2 for x in cls["comp_sizes"]), cls
+    assert cls["components"] == h1["components"] and cls["giant"] == h1["largest_component"], (cls, h1["components"])
+    # the window's broadcast (40 rounds on: past its last hop, ~28 at 2^24)
+    # reaches exactly the giant component
+    rel = h1["delivered"] / N
+    assert h1["delivered"] == cls["giant"] and rel >= 0.999, (rel, cls["giant"])
+    sym = h1["symmetric_links"] / max(1, h1["active_links"])
+    assert sym >= 0.999, sym
+    print("C24 OK", {"nodes": N, "ranks": RANKS, "rounds": len(st1), "components": cls["components"],
+                     "outside": cls["outside"], "isolated": cls["isolated"], "reliability": round(rel, 6),
+                     "symmetric": round(sym, 6), "msgs": int(st1["emitted"].sum()),
+                     "seconds": round(time.time() - T0, 1)}, flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -520,6 +520,13 @@ def test_snapshot_restore_continues_identically():
     sim.broadcast(0, 7)
     a = sim.step(40)
     other = Simulator(default_config(n_nodes=4096, seed=2))
+    # a short snapshot (its last section cut) is refused before anything
+    # changes: the fresh handle still steps as a fresh handle
+    from partisan_amd.sim import SimError
+    with pytest.raises(SimError):
+        other.restore(snap[:-64])
+    assert other.round == 0
+    other.step(1)
     other.restore(snap)
     assert other.round == 60
     other.broadcast(0, 7)

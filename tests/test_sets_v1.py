@@ -4,7 +4,7 @@ list in to_list order, re-slotted stably when the linear hash opens or
 closes a slot) against a bucket-level model of stdlib's sets.erl written
 here from its published algorithm -- #set{size, n, maxn, bso, exp_size,
 con_size, segs}, get_slot/2, add_element/2 + maybe_expand/2 (rehash of the
-buddy bucket), del_element/2 + maybe_contract/2 (B2 ++ B1), to_list/1 as the
+buddy bucket), del_element/2 + maybe_contract/2 (B1 ++ B2), to_list/1 as the
 fold over slots n..1.  No OTP is present here, so the model is a
 restatement, not a pin: parity of this order with the reference is
 unpinned.  The phash tables are random 32-bit values,
@@ -71,7 +71,7 @@ class OtpSetsV1:
         if self.size - dc < self.con_size and self.n > self.SEG:
             N = self.n
             s1, s2 = N - self.bso, N
-            self.bkt[s1] = self.bkt[s2] + self.bkt[s1]          # B2 ++ B1
+            self.bkt[s1] = self.bkt[s1] + self.bkt[s2]          # put_bucket_s(Segs0, Slot1, B1 ++ B2)
             self.bkt[s2] = []
             n1 = N - 1
             self.size -= dc
@@ -176,3 +176,28 @@ def test_sets_v1_expansion_points():
     ops = list(range(81)) + [~i & 0xFFFFFFFF for i in range(30)]   # 51 left
     _, s = _oracle_run(ph, ops)
     assert s == 17
+
+
+def test_sets_v1_contract_merges_b1_then_b2():
+    """A fixed expand-then-contract sequence worked by hand from sets.erl:
+    a1, b1, a2, b2 share 16-slot bucket 1 (phash(E, 16) = 1); the 81st add
+    opens slot 17 and rehash/4 moves b1, b2 there (phash(E, 32) = 17).  Then
+    31 deletes take the size below 3 * 17: maybe_contract/2 stores slot 1 as
+    B1 ++ B2 = [a2, a1] ++ [b2, b1] (buckets newest first), which to_list/1's
+    reversing fold yields as b1, b2, a1, a2."""
+    a1, b1, a2, b2 = 0, 1, 2, 3
+    ph = np.zeros(128, np.uint32)
+    ph[a1], ph[a2] = 0 + 32 * 5, 0 + 32 * 9            # low 5 bits 0: slot 1 at MaxN 16 and 32
+    ph[b1], ph[b2] = 16 + 32 * 3, 16 + 32 * 7          # low 5 bits 16: slot 1, then slot 17
+    fill = list(range(4, 81))
+    for i in fill:
+        ph[i] = (i % 15) + 1 + 32 * i                 # never bucket 1
+    ops = [a1, b1, a2, b2] + fill
+    got, slots = _oracle_run(ph, ops)
+    assert slots == 17 and got[:2] == [a1, a2] and got[-2:] == [b1, b2]
+    ops += [~i & 0xFFFFFFFF for i in fill[:31]]
+    got, slots = _oracle_run(ph, ops)
+    assert slots == 16
+    assert got[:4] == [b1, b2, a1, a2]
+    want, _ = _model_run(ph, ops)
+    assert got == want
