@@ -303,6 +303,26 @@ def cpu_share():
     return out
 
 
+CPU_FULL_SIZE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r05", "cpu20", "cpu20.json")
+
+
+def _cpu_full_size(n):
+    """The same oracle at the headline's full 2^20 nodes, measured once on a
+    box's host by `bench.py --cpu-baseline-only --cpu-sample-nodes 1048576
+    --cpu-sample-rounds 20` (its bootstrap takes minutes, so the default
+    line times the bounded sample above) -- quoted from the committed record
+    beside the sample, with its source, not re-measured here"""
+    if n >= 1 << 20 or not os.path.exists(CPU_FULL_SIZE):
+        return None
+    try:
+        d = json.load(open(CPU_FULL_SIZE))["cpu_baseline"]
+    except (OSError, ValueError, KeyError):
+        return None
+    return {"value": d["value"], "unit": d["unit"], "cores": d["cores"], "all_cores_value": d["all_cores"]["value"],
+            "all_cores": d["all_cores"]["cores"], "sample": d["sample"],
+            "source": "profiles/r05/cpu20/cpu20.json (measured, not re-run by this command)"}
+
+
 def cpu_baseline(args):
     """Run before the GPU is touched (worker processes are forked).  One
     thread, then `workers` independent oracle processes on the same sample
@@ -337,6 +357,7 @@ def cpu_baseline(args):
                                     f"with its own seed, timed rounds started together (barrier); "
                                     f"node-rounds of all / the slowest one's time"},
             "rows": _cpu_rows(),
+            "full_size": _cpu_full_size(n),
             "reference": reference_probe(),
             "cpu_model": cpu_model(), "nproc": os.cpu_count(),
             "affinity_cpus": len(os.sched_getaffinity(0)), "cpu_share": cpu_share()}

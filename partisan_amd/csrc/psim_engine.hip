@@ -51,9 +51,20 @@ constexpr uint32_t DESC_RANGES = 4;   // k_node_prep ranges a k_desc block takes
 // pinned host words per shard (Shard::pin): NST stats, the consume span, the
 // outbox total, the routed record count -- stored by kernels, read by the host
 enum { PIN_TOTAL = NST + 2, PIN_M = NST + 3, PIN_OVF = NST + 4, PIN_BIGIN = NST + 5, PIN_OUTX = NST + 6 };
+// the rank path's words of a round (RCCL ranks; all-reduced, so every rank
+// reads the same): PIN_XAB ranks whose round aborted (a batch's capacity
+// checks, exchange_fixed), PIN_XMH / PIN_XMT the ranks' largest per-owner head
+// / tail counts, summed; then this rank's per-owner send counts (G words)
+enum { PIN_XAB = NST + 8, PIN_XMH = NST + 9, PIN_XMT = NST + 10, PIN_XCNT = NST + 16 };
+// slot 0 only: the largest outbox total (k_desc) and routed count (the
+// route) since the host last cleared them (PSIM_TRACE_BOUND, psim_step)
+enum { PIN_TMAX = NST + 7, PIN_MMAX = NST + 11 };
+// stat_out: NST sums, the node-round span (2), the three x-words of the
+// rank path (all-reduced with the sums)
+constexpr uint32_t STAT_OUT_X = NST + 2, STAT_OUT_N = NST + 5;
 // the pinned words: slot 0 holds the above (and a single round's stats);
 // slot j + 1 the stats and node-round span of round j of a batch (run_batch)
-constexpr uint32_t PIN_STRIDE = NST + 8;
+constexpr uint32_t PIN_STRIDE = PIN_XCNT + 64;
 constexpr uint32_t BATCH_MAX = 64;
 
 #define HIP_TRY(x)                                                       \
@@ -291,6 +302,12 @@ struct RouteIn {
     const Wire* tails;         // dense: the tails
     const uint32_t* seg;       // dense: per source shard its first head, then its first tail (2 (nseg + 1))
     uint32_t nseg;
+    // dense, a batched rank round (exchange_fixed): source g's heads at
+    // [g capH, g capH + its count), its tails at [g capT, ..), the counts
+    // (heads | tails << 32) received by the count all-to-all; capH = 0: the
+    // packed layout above
+    uint32_t capH, capT;
+    const uint64_t* rcnt;
 };
 
 // the source shard of received head i (seg: nseg + 1 increasing starts)
@@ -314,11 +331,22 @@ __device__ __forceinline__ void route_step(const RouteIn& in, uint32_t step, uin
     const uint32_t w = threadIdx.x >> 6, l = threadIdx.x & 63;
     const uint32_t i = step * RB_STEP + threadIdx.x;
     if (DENSE) {
-        if (i < in.n_src) {
+        uint32_t g = 0;
+        bool ok = i < in.n_src;
+        if (in.capH && ok) {                          // (the fixed layout: a slot past its source's count is empty)
+            g = i / in.capH;
+            ok = i - g * in.capH < min((uint32_t)in.rcnt[g], in.capH);
+        }
+        if (ok) {
             const uint4 h0 = in.wire[i].q[0];        // dst, src, type word, seq
             // (FIX, k_bucket_hist: a long head's tail index becomes the
-            // index among every received tail)
-            if (FIX && wire_long(h0.z)) in.wire[i].q[1].w += in.seg[in.nseg + 1 + wire_source(in, i)];
+            // index among every received tail -- in the fixed layout kept
+            // inside its source's region: a sender past its tail capacity
+            // aborted the round, exchange_fixed)
+            if (FIX && wire_long(h0.z)) {
+                if (in.capH) in.wire[i].q[1].w = min(in.wire[i].q[1].w, in.capT - 1) + g * in.capT;
+                else in.wire[i].q[1].w += in.seg[in.nseg + 1 + wire_source(in, i)];
+            }
             f(i, h0.x - in.lo, in.pl ? 0u : max_emit(h0.z & 0xFF));
         }
         return;
@@ -518,11 +546,17 @@ __global__ void __launch_bounds__(RB_STEP) k_bucket_scatter(RouteIn in, uint32_t
 // A wave walks its 64 nodes' records in slot order, 64 at a time; the rank
 // within a batch is a ballot over the lanes of the same owner, one ballot
 // per distinct owner in the batch (<= G).
+// A batched rank round (capH > 0, exchange_fixed) writes the fixed layout
+// instead: owner q's heads at [q capH, (q + 1) capH), its tails at G capH +
+// [q capT, (q + 1) capT); a record past its owner's capacity is not written
+// (k_owner_offsets aborts the round, code 3).
 template <bool WRITE>
 __global__ void __launch_bounds__(RB_STEP) k_owner_part(RouteIn in, uint32_t nsteps, uint32_t spb, uint32_t G,
                                                         uint32_t per, uint32_t* hist,
                                                         const uint32_t* __restrict__ off, Wire* __restrict__ out,
-                                                        unsigned long long* mark) {
+                                                        unsigned long long* mark, uint32_t capH, uint32_t capT,
+                                                        const uint32_t* ctl) {
+    if (*ctl) return;                                 // an aborted batch (run_batch_ranked)
     if (mark && blockIdx.x == 0 && threadIdx.x == 0) *mark = __builtin_amdgcn_s_memrealtime();   // (phase end)
     __shared__ uint32_t spre[RB_WAVES][65];
     __shared__ uint64_t sbase[RB_WAVES][64];
@@ -531,10 +565,17 @@ __global__ void __launch_bounds__(RB_STEP) k_owner_part(RouteIn in, uint32_t nst
     __shared__ uint32_t tb[64];                       // per owner: its first tail (WRITE)
     const uint32_t w = threadIdx.x >> 6, l = threadIdx.x & 63, nblk = gridDim.x;
     if (threadIdx.x < 64) {
-        const bool q = WRITE && threadIdx.x < G;
-        run[threadIdx.x] = q ? off[threadIdx.x * nblk + blockIdx.x] : 0u;
-        runl[threadIdx.x] = q ? off[(G + threadIdx.x) * nblk + blockIdx.x] : 0u;
-        tb[threadIdx.x] = q ? off[(G + threadIdx.x) * nblk] : 0u;
+        const uint32_t o = threadIdx.x;
+        const bool q = WRITE && o < G;
+        if (capH) {                                   // (each owner's region starts at its fixed base)
+            run[o] = q ? o * capH + off[o * nblk + blockIdx.x] - off[o * nblk] : 0u;
+            runl[o] = q ? G * capH + o * capT + off[(G + o) * nblk + blockIdx.x] - off[(G + o) * nblk] : 0u;
+            tb[o] = q ? G * capH + o * capT : 0u;
+        } else {
+            run[o] = q ? off[o * nblk + blockIdx.x] : 0u;
+            runl[o] = q ? off[(G + o) * nblk + blockIdx.x] : 0u;
+            tb[o] = q ? off[(G + o) * nblk] : 0u;
+        }
     }
     if (!WRITE && blockIdx.x == 0 && threadIdx.x == 0) hist[2 * G * nblk] = 0;
     const uint32_t s_end = min(nsteps, (blockIdx.x + 1) * spb);
@@ -612,11 +653,15 @@ __global__ void __launch_bounds__(RB_STEP) k_owner_part(RouteIn in, uint32_t nst
                 if (o != 0xFFFFFFFFu) {
                     if (lg) {
                         x1.w = lpos - tb[o];          // the tail's index among owner o's tails
-                        out[lpos].q[0] = x2;
-                        out[lpos].q[1] = x3;
+                        if (!capH || x1.w < capT) {
+                            out[lpos].q[0] = x2;
+                            out[lpos].q[1] = x3;
+                        }
                     }
-                    out[pos].q[0] = x0;
-                    out[pos].q[1] = x1;
+                    if (!capH || pos < (o + 1) * capH) {
+                        out[pos].q[0] = x0;
+                        out[pos].q[1] = x1;
+                    }
                 }
             }
         }
@@ -638,12 +683,42 @@ __global__ void __launch_bounds__(RB_STEP) k_owner_part(RouteIn in, uint32_t nst
 // ranks, each owner's record count | its long records' count << 32 straight
 // into the send half of the count all-to-all (so the round reads both back
 // at once)
-__global__ void k_owner_offsets(const uint32_t* hoff, uint32_t nblk, uint32_t G, uint64_t* d_off, uint64_t* cnt) {
+// Also, for the rank path: the largest per-owner head and tail counts into
+// the x-words (xw[1], xw[2]: all-reduced with the round's stats, they size
+// the next batch's fixed exchange), and in a batched round (capH > 0) an
+// owner past its capacity aborts the round (code 3, ctl[1] = round).  An
+// aborted round sends counts of 0 (its send buffer was not written).
+__global__ void k_owner_offsets(const uint32_t* hoff, uint32_t nblk, uint32_t G, uint64_t* d_off, uint64_t* cnt,
+                                uint64_t* xw, uint32_t capH, uint32_t capT, uint32_t* ctl, uint32_t round) {
     const uint32_t q = threadIdx.x;
+    const bool dead = *ctl != 0;
     if (q <= 2 * G) d_off[q] = hoff[q * nblk];
     if (cnt && q < G)
-        cnt[q] = (uint64_t)(hoff[(q + 1) * nblk] - hoff[q * nblk]) |
-                 ((uint64_t)(hoff[(G + q + 1) * nblk] - hoff[(G + q) * nblk]) << 32);
+        cnt[q] = dead ? 0ull
+                      : (uint64_t)(hoff[(q + 1) * nblk] - hoff[q * nblk]) |
+                            ((uint64_t)(hoff[(G + q + 1) * nblk] - hoff[(G + q) * nblk]) << 32);
+    if (xw && q == 0) {
+        uint32_t mh = 0, mt = 0;
+        for (uint32_t o = 0; o < G && !dead; o++) {
+            mh = max(mh, hoff[(o + 1) * nblk] - hoff[o * nblk]);
+            mt = max(mt, hoff[(G + o + 1) * nblk] - hoff[(G + o) * nblk]);
+        }
+        xw[1] = mh;
+        xw[2] = mt;
+        if (capH && !dead && (mh > capH || mt > capT)) { ctl[1] = round; __threadfence(); ctl[0] = 3; }
+    }
+}
+
+// the rank path's abort word into the round's x-words, before their
+// all-reduce (every rank, whatever its own state: ranks > 0 of the sum mean
+// some rank's round did not finish); after it, a rank whose own round went
+// through stops its later ones too (code 4), so every rank of a batch stops
+// at the same round
+__global__ void k_xabort(const uint32_t* ctl, uint64_t* xw) {
+    if (threadIdx.x == 0) xw[0] = *ctl != 0 ? 1u : 0u;
+}
+__global__ void k_abort_sync(const uint64_t* xw, uint32_t* ctl, uint32_t round) {
+    if (threadIdx.x == 0 && xw[0] && !*ctl) { ctl[1] = round; __threadfence(); ctl[0] = 4; }
 }
 
 
@@ -820,6 +895,7 @@ __global__ void __launch_bounds__(RR_THREADS) k_bucket_route(
     if (b == gridDim.x - 1 && threadIdx.x == 0) {   // the record count
         in_beg[n] = s1;
         *hm = s1;
+        if (s1 > hm[PIN_MMAX - PIN_M]) hm[PIN_MMAX - PIN_M] = s1;
     }
     if (inreg) {
 #pragma unroll
@@ -1142,6 +1218,7 @@ __device__ __forceinline__ void desc_entry(const RoundArgs& a, uint32_t li, uint
         *nact = (uint32_t)P;
         obase[li] = tot;
         hout[PIN_TOTAL] = tot;                        // the host's one mid-round read
+        if (tot > hout[PIN_TMAX]) hout[PIN_TMAX] = tot;
         // a batch (cap > 0) checks the outbox here instead: a total past its
         // capacity stops the rest of the batch (code 1, this round)
         if (cap && tot + 1 > cap) { ctl[1] = a.round; __threadfence(); ctl[0] = 1; }
@@ -1556,6 +1633,14 @@ struct Shard {
     uint32_t batch_round1 = 0;
     uint32_t stat_slot = 0;
     bool outx_short = false;            // the outstanding pool failed to grow (reported once per shard)
+    // the rank path's batches (run_batch_ranked): the fixed per-owner
+    // capacities of the exchange (heads, tails; 0 = not known yet: no batch),
+    // identical on every rank (set from all-reduced counts), and the next
+    // batch's length (1 after an abort, doubling up to BATCH_MAX)
+    uint32_t xcap_h = 0, xcap_t = 0;
+    uint32_t xbatch = 1;
+    uint64_t xmax_host[2] = {0, 0};     // (the host side of the exact round's max all-reduce)
+    uint64_t trace_tmax = 0, trace_mmax = 0;   // PSIM_TRACE_BOUND's high-water marks
 };
 
 }  // namespace
@@ -2121,7 +2206,7 @@ unsigned long long* phase_end_mark(psim_handle* h, Shard* s) {
                                                     : reinterpret_cast<unsigned long long*>(s->stat_out.p + NST) + 1;
 }
 
-int route_group(psim_handle* h, Shard* s, bool dense, uint32_t m) {
+int route_group(psim_handle* h, Shard* s, bool dense, uint32_t m, bool fixed = false) {
     const uint32_t n = s->n;
     // buckets of 2^wshift destinations, one k_bucket_route block each, at
     // most 16 K of them (the two passes' LDS histograms: 4 B per bucket).
@@ -2138,7 +2223,8 @@ int route_group(psim_handle* h, Shard* s, bool dense, uint32_t m) {
     const uint32_t W = 1u << wshift, nb = (n + W - 1) >> wshift;
     const RouteIn in{s->outbox.p, s->okey.p, s->obase.p, s->ocnt.p, dense ? m : n, s->lo,
                      h->cfg.manager == PSIM_MANAGER_PLUGGABLE, dense ? s->recvh.p : nullptr,
-                     dense ? s->recvt.p : nullptr, dense ? s->wseg.p : nullptr, dense ? h->G : 0u};
+                     dense ? s->recvt.p : nullptr, dense && !fixed ? s->wseg.p : nullptr, dense ? h->G : 0u,
+                     fixed ? s->xcap_h : 0u, fixed ? s->xcap_t : 0u, fixed ? h->comm_cnt.p + h->G : nullptr};
     const uint32_t nsteps = std::max<uint32_t>(1, (in.n_src + RB_STEP - 1) / RB_STEP);
     const uint32_t nblk = std::min<uint32_t>(nsteps, h->rb_blocks);
     const size_t nh = (size_t)nb * nblk;
@@ -2204,7 +2290,10 @@ void send_counts(Shard* s, uint32_t G);
 
 // G > 1, sender side: the outbox partitioned by owner shard into the send
 // buffer in the wire format (k_owner_part); per-owner counts/offsets on the host
-int phase_partition(psim_handle* h, Shard* s) {
+// fixed: a batched rank round (run_batch_ranked) -- the fixed layout of
+// s->xcap_h / xcap_t per owner, nothing read back (the buffers were sized for
+// the batch)
+int phase_partition(psim_handle* h, Shard* s, bool fixed = false) {
     const uint32_t G = h->G;
     RouteIn in{};
     in.rec = s->outbox.p; in.okey = s->okey.p; in.obase = s->obase.p; in.ocnt = s->ocnt.p; in.n_src = s->n;
@@ -2214,19 +2303,22 @@ int phase_partition(psim_handle* h, Shard* s) {
     const size_t nh = (size_t)2 * G * nblk + 1;
     TRY(s->hist.ensure(nh));
     TRY(s->hoff.ensure(nh));
-    TRY(s->sendbuf.ensure(2 * (s->pin[PIN_TOTAL] + 1), 2));   // (the outbox bound bounds the records)
+    if (!fixed) TRY(s->sendbuf.ensure(2 * (s->pin[PIN_TOTAL] + 1), 2));   // (the outbox bound bounds the records)
     TRY(s->d_off.ensure(2 * G + 1));
     const bool rccl = h->ranked;
-    if (rccl) TRY(h->comm_cnt.ensure(2 * G));
+    if (rccl) TRY(h->comm_cnt.ensure(2 * G + 2));   // (send and receive counts, then 2 words of phase_stats)
     s->soff.assign(2 * G + 1, 0);
+    const uint32_t capH = fixed ? s->xcap_h : 0u, capT = fixed ? s->xcap_t : 0u;
     {
         KTimer t(h, s, KT_SORT);
         k_owner_part<false><<<nblk, RB_STEP, 0, s->stream>>>(in, nsteps, spb, G, h->per, s->hist.p, nullptr,
-                                                              nullptr, phase_end_mark(h, s));
+                                                              nullptr, phase_end_mark(h, s), capH, capT, s->ctl.p);
         TRY(scan_excl(s, s->hist.p, s->hoff.p, (uint32_t)nh));
         k_owner_part<true><<<nblk, RB_STEP, 0, s->stream>>>(in, nsteps, spb, G, h->per, nullptr, s->hoff.p,
-                                                             s->sendbuf.p, nullptr);
-        k_owner_offsets<<<1, 256, 0, s->stream>>>(s->hoff.p, nblk, G, s->d_off.p, rccl ? h->comm_cnt.p : nullptr);
+                                                             s->sendbuf.p, nullptr, capH, capT, s->ctl.p);
+        k_owner_offsets<<<1, 256, 0, s->stream>>>(s->hoff.p, nblk, G, s->d_off.p, rccl ? h->comm_cnt.p : nullptr,
+                                                  rccl ? s->stat_out.p + STAT_OUT_X : nullptr, capH, capT, s->ctl.p,
+                                                  (uint32_t)h->round);
         HIP_TRY(hipGetLastError());
         // an RCCL rank reads the offsets back with the received counts, after
         // the count all-to-all (exchange_rccl): one host wait a round, not two
@@ -2368,16 +2460,81 @@ int exchange_rccl(psim_handle* h) {
     return phase_receive(h, s, hc, lc);
 }
 
+// A batched rank round (run_batch_ranked): no host wait.  The counts go
+// through the all-to-all as always, but the records travel in fixed-size
+// messages -- per peer xcap_h heads and xcap_t tails, identical on every rank
+// -- so nothing is sized on the host; the receiver's route reads each
+// source's region up to the count it received (the fixed layout of RouteIn).
+// A sender whose owner count passed a capacity aborted the round
+// (k_owner_offsets, code 3) and every rank redoes it exactly
+// (run_batch_ranked).  The padding crosses the link too: a capacity is the
+// largest per-owner count seen so far, 1.25x (xcaps_update).
+int exchange_fixed(psim_handle* h) {
+    Shard* s = h->shards[0];
+    const uint32_t G = h->G, capH = s->xcap_h, capT = s->xcap_t;
+    KTimer t(h, s, KT_EXCHANGE);
+    TRY(h->comm->all_to_all_u64(h->comm_cnt.p, h->comm_cnt.p + G, 1, s->stream));
+    std::vector<Xfer> sends, recvs;
+    const bool self_comm = h->world == 1;
+    for (uint32_t g = 0; g < G; g++) {
+        if (g == s->idx && !self_comm) continue;
+        sends.push_back({(int)g, s->sendbuf.p + (size_t)g * capH, (size_t)capH * sizeof(Wire)});
+        sends.push_back({(int)g, s->sendbuf.p + (size_t)G * capH + (size_t)g * capT, (size_t)capT * sizeof(Wire)});
+        recvs.push_back({(int)g, s->recvh.p + (size_t)g * capH, (size_t)capH * sizeof(Wire)});
+        recvs.push_back({(int)g, s->recvt.p + (size_t)g * capT, (size_t)capT * sizeof(Wire)});
+    }
+    TRY(h->comm->exchange(sends, recvs, s->stream));
+    if (!self_comm) {
+        const uint32_t g = s->idx;
+        HIP_TRY(hipMemcpyAsync(s->recvh.p + (size_t)g * capH, s->sendbuf.p + (size_t)g * capH, (size_t)capH * sizeof(Wire),
+                               hipMemcpyDeviceToDevice, s->stream));
+        HIP_TRY(hipMemcpyAsync(s->recvt.p + (size_t)g * capT, s->sendbuf.p + (size_t)G * capH + (size_t)g * capT,
+                               (size_t)capT * sizeof(Wire), hipMemcpyDeviceToDevice, s->stream));
+    }
+    return route_group(h, s, true, G * capH, true);
+}
+
+// the fixed capacities of the next batch after an exact rank round: the
+// largest per-owner head / tail counts of any rank this round (an all-reduce
+// max of the exact round, phase_stats, into pinned slot 0), 1.25x and 1024
+// more, never below the current ones -- the same on every rank
+void xcaps_update(Shard* s) {
+    const uint64_t mh = s->pin[PIN_XMH], mt = s->pin[PIN_XMT];
+    const uint64_t ch = std::min<uint64_t>(mh + mh / 4 + 1024, 0x7FFFFFFFull);
+    const uint64_t ct = std::min<uint64_t>(mt + mt / 4 + 1024, 0x7FFFFFFFull);
+    s->xcap_h = std::max<uint32_t>(s->xcap_h, (uint32_t)ch);
+    s->xcap_t = std::max<uint32_t>(s->xcap_t, (uint32_t)ct);
+}
+
 // the round's end after its route (which summed the stats: StatsIn)
-int phase_stats(psim_handle* h, Shard* s, const std::vector<uint32_t>& crashed) {
+// exact_caps: an exact rank round -- also the ranks' largest per-owner
+// counts (all-reduce max) for the next batch's capacities (xcaps_update)
+int phase_stats(psim_handle* h, Shard* s, const std::vector<uint32_t>& crashed, bool exact_caps = false) {
     KTimer t(h, s, KT_STATS);
     if (h->ranked) {
         // the ranks' sums reduced on the device, on the shard's stream, and
         // stored over the pinned words: the end of the round waits once
-        // (a host copy, an all-reduce and a second wait after it before)
-        TRY(h->comm->all_reduce(s->stat_out.p, NST, CType::U64, COp::SUM, s->stream));
-        HIP_TRY(hipMemcpyAsync(s->pin_dev + (size_t)s->stat_slot * PIN_STRIDE, s->stat_out.p, NST * 8,
-                               hipMemcpyDeviceToDevice, s->stream));
+        // (a host copy, an all-reduce and a second wait after it before).
+        // The x-words go with them: whether a rank's round aborted (a batch),
+        // the largest per-owner counts (the next batch's capacities)
+        uint64_t* pw = s->pin_dev + (size_t)s->stat_slot * PIN_STRIDE;
+        k_xabort<<<1, 64, 0, s->stream>>>(s->ctl.p, s->stat_out.p + STAT_OUT_X);
+        TRY(h->comm->all_reduce(s->stat_out.p, STAT_OUT_N, CType::U64, COp::SUM, s->stream));
+        HIP_TRY(hipMemcpyAsync(pw, s->stat_out.p, NST * 8, hipMemcpyDeviceToDevice, s->stream));
+        HIP_TRY(hipMemcpyAsync(pw + PIN_XAB, s->stat_out.p + STAT_OUT_X, 3 * 8, hipMemcpyDeviceToDevice, s->stream));
+        HIP_TRY(hipMemcpyAsync(pw + PIN_XCNT, h->comm_cnt.p, h->G * 8, hipMemcpyDeviceToDevice, s->stream));
+        k_abort_sync<<<1, 64, 0, s->stream>>>(s->stat_out.p + STAT_OUT_X, s->ctl.p, (uint32_t)h->round);
+        if (exact_caps) {
+            s->xmax_host[0] = s->xmax_host[1] = 0;
+            for (uint32_t g = 0; g < h->G; g++) {
+                s->xmax_host[0] = std::max<uint64_t>(s->xmax_host[0], s->scnt[g]);
+                s->xmax_host[1] = std::max<uint64_t>(s->xmax_host[1], s->lcnt[g]);
+            }
+            uint64_t* xm = h->comm_cnt.p + 2 * h->G;       // (phase_partition sized it)
+            HIP_TRY(hipMemcpyAsync(xm, s->xmax_host, 16, hipMemcpyHostToDevice, s->stream));
+            TRY(h->comm->all_reduce(xm, 2, CType::U64, COp::MAX, s->stream));
+            HIP_TRY(hipMemcpyAsync(pw + PIN_XMH, xm, 16, hipMemcpyDeviceToDevice, s->stream));
+        }
     }
     if (!crashed.empty()) {
         TRY(upload(s, s->ev_ids, crashed));
@@ -2406,7 +2563,10 @@ void bcast_slots(psim_handle* h, RoundCtl& ctl) {
 // One round, waited for.  events_applied: the pending events went to the
 // device already (the redo of an aborted batch round): only their
 // round-end halves run (crash-round EXIT checks, k_uncrash, origins spent).
-int run_round(psim_handle* h, uint64_t* st, bool events_applied = false) {
+// from_partition: the node-round phase ran already (a rank's redo of an
+// aborted batch round, run_batch_ranked): the round goes on from its owner
+// partition, over the outbox that phase left.
+int run_round(psim_handle* h, uint64_t* st, bool events_applied = false, bool from_partition = false) {
     RoundCtl ctl;
     ctl.crashes = !h->pend_crash.empty();
     if (!events_applied) bcast_slots(h, ctl);
@@ -2418,7 +2578,7 @@ int run_round(psim_handle* h, uint64_t* st, bool events_applied = false) {
     }
     for (Shard* s : h->shards) s->tn = 0;        // (timers of a round that failed)
     std::vector<RoundArgs> args(h->shards.size());   // (consume fills the payload arena fields)
-    for (size_t i = 0; i < h->shards.size(); i++)
+    for (size_t i = 0; i < h->shards.size() && !from_partition; i++)
         TRY(phase_events_prepare(h, h->shards[i], ctl, args[i], !events_applied));
     // (test hook: this round fails half-way, after its events went to the
     // device, as an allocation failure inside a round would)
@@ -2427,7 +2587,7 @@ int run_round(psim_handle* h, uint64_t* st, bool events_applied = false) {
         for (Shard* s : h->shards) (void)hipStreamSynchronize(s->stream);
         return PSIM_ENOMEM;
     }
-    for (size_t i = 0; i < h->shards.size(); i++) TRY(phase_consume(h, h->shards[i], args[i]));
+    for (size_t i = 0; i < h->shards.size() && !from_partition; i++) TRY(phase_consume(h, h->shards[i], args[i]));
     if (local_route(h)) {
         TRY(phase_route_local(h, h->shards[0]));
     } else {
@@ -2436,7 +2596,7 @@ int run_round(psim_handle* h, uint64_t* st, bool events_applied = false) {
         else TRY(exchange_local(h));
     }
     for (Shard* s : h->shards) {
-        TRY(phase_stats(h, s, h->pend_crash));
+        TRY(phase_stats(h, s, h->pend_crash, h->ranked));
         if (!h->pend_b_root.empty())        // this round's origins are spent
             k_origin<<<grid_for(h->pend_b_root.size()), BLK, 0, s->stream>>>(
                 s->origin.p, s->lo, s->n, s->bc_roots.p, s->bc_msgs.p, (uint32_t)h->pend_b_root.size(), s->flags.p,
@@ -2463,6 +2623,7 @@ int run_round(psim_handle* h, uint64_t* st, bool events_applied = false) {
             TRY(stream_wait(s));
         }
         if (local_route(h)) s->m_in = (uint32_t)s->pin[PIN_M];   // routed this round
+        if (h->ranked) xcaps_update(s);           // (the next batch's exchange capacities)
         static const bool trace_relay = getenv("PSIM_TRACE_RELAY") != nullptr;
         if (trace_relay && s->rgrid)
         {
@@ -2556,11 +2717,15 @@ void fill_stats(const uint64_t* s, uint64_t round, psim_round_stats* o) {
 bool batchable(psim_handle* h) {
     static const bool trace = getenv("PSIM_TRACE_RELAY") != nullptr;
     static const bool off = getenv("PSIM_NO_BATCH") != nullptr || getenv("PSIM_TEST_FAIL_ROUND") != nullptr;
-    if (off || trace || h->G != 1 || h->ranked || h->phase_timers || h->cfg.strict ||
-        h->cfg.manager == PSIM_MANAGER_PLUGGABLE || !h->pend_lv_a.empty())
+    static const bool off_ranked = getenv("PSIM_NO_RANK_BATCH") != nullptr;
+    if (off || trace || h->phase_timers || h->cfg.strict || h->cfg.manager == PSIM_MANAGER_PLUGGABLE ||
+        !h->pend_lv_a.empty())
         return false;
     Shard* s = h->shards[0];
-    return s->reserved && s->rcap && s->outbox.n;
+    // a rank batches once an exact round has set the exchange capacities
+    // (every rank decides alike: the same events, the same all-reduced caps)
+    if (h->ranked) return !off_ranked && s->reserved && s->rcap && s->outbox.n && s->xcap_h && s->xcap_t;
+    return h->G == 1 && s->reserved && s->rcap && s->outbox.n;
 }
 
 // Up to BATCH_MAX rounds enqueued back to back with no host wait between
@@ -2685,6 +2850,118 @@ int run_batch(psim_handle* h, uint32_t nb, psim_round_stats* st_out, uint32_t* d
     return PSIM_OK;
 }
 
+// The rank path's batch (RCCL ranks, or loopback): up to nb rounds enqueued
+// back to back with no host wait -- the outbox checked against its capacity by
+// k_desc (code 1), the exchange in fixed-size messages (exchange_fixed; an
+// owner past its capacity, code 3), the route's capacity G * xcap_h records
+// (never short) -- then one wait.  Every round all-reduces whether any rank
+// aborted it (phase_stats: k_xabort, k_abort_sync), so all ranks stop at the
+// same round r; its records are then exchanged again exactly by every rank
+// (run_round from its owner partition; a rank whose outbox was short grows it
+// and runs the round's node phase again first -- nothing of it ran past
+// k_desc).  Rounds after r returned at once from every kernel; their
+// collectives moved nothing anyone reads.
+int run_batch_ranked(psim_handle* h, uint32_t nb, psim_round_stats* st_out, uint32_t* done_out) {
+    Shard* s = h->shards[0];
+    const uint32_t G = h->G, capH = s->xcap_h, capT = s->xcap_t;
+    const uint64_t r0 = h->round;
+    TRY(s->sendbuf.ensure((size_t)G * (capH + capT) + 1));
+    TRY(s->recvh.ensure((size_t)G * capH + 1));
+    TRY(s->recvt.ensure((size_t)G * capT + 1));
+    TRY(h->comm_cnt.ensure(2 * G + 2));
+    s->rcap = std::max<uint64_t>(s->rcap, (uint64_t)G * capH);    // (the route never overflows)
+    TRY(route_buffers(s, false));
+    RoundCtl ctl0;
+    ctl0.crashes = !h->pend_crash.empty();
+    bcast_slots(h, ctl0);
+    const std::vector<uint32_t> crashed0 = h->pend_crash;
+    const std::vector<uint32_t> none;
+    const bool bc0 = !h->pend_b_root.empty();
+    s->tn = 0;
+    s->desc_cap = std::min<uint64_t>(s->outbox.n, s->okey.n);
+    for (uint32_t j = 0; j < nb; j++) {
+        s->stat_slot = j + 1;
+        s->batch_round1 = (uint32_t)h->round + 1;
+        RoundArgs a;
+        const RoundCtl ctl = j == 0 ? ctl0 : RoundCtl{};
+        TRY(phase_events_prepare(h, s, ctl, a, j == 0, true));
+        TRY(phase_consume(h, s, a));
+        TRY(phase_partition(h, s, true));
+        TRY(exchange_fixed(h));
+        TRY(phase_stats(h, s, j == 0 ? crashed0 : none));
+        if (j == 0 && bc0)                  // the first round's origins are spent
+            k_origin<<<grid_for(h->pend_b_root.size()), BLK, 0, s->stream>>>(
+                s->origin.p, s->lo, s->n, s->bc_roots.p, s->bc_msgs.p, (uint32_t)h->pend_b_root.size(), s->flags.p,
+                true, s->ctl.p);
+        HIP_TRY(hipGetLastError());
+        h->round++;
+    }
+    s->stat_slot = 0; s->batch_round1 = 0; s->desc_cap = 0;
+    uint32_t cw[2] = {0, 0};
+    HIP_TRY(hipMemcpyAsync(cw, s->ctl.p, sizeof cw, hipMemcpyDeviceToHost, s->stream));
+    TRY(stream_wait(s));
+    if (s->pin[PIN_BIGIN]) {                          // a node's inbox count must fit 27 bits
+        s->pin[PIN_BIGIN] = 0;
+        HIP_TRY(hipMemsetAsync(s->ctl.p, 0, sizeof cw, s->stream));
+        return PSIM_ENOMEM;
+    }
+    // the first round some rank aborted (the all-reduced x-word: every rank
+    // finds the same one)
+    uint32_t done = nb;
+    for (uint32_t j = 0; j < nb; j++)
+        if (s->pin[(size_t)(j + 1) * PIN_STRIDE + PIN_XAB]) { done = j; break; }
+    if (done == nb && cw[0]) return PSIM_EDEVICE;     // (an abort no round reported)
+    const bool self_comm = h->world == 1;
+    for (uint32_t j = 0; j < done; j++) {
+        const uint64_t* p = s->pin + (size_t)(j + 1) * PIN_STRIDE;
+        if (p[ST_BOUND]) {
+            std::fprintf(stderr, "psim: round %llu: %llu nodes emitted past their outbox bound (engine bug)\n",
+                         (unsigned long long)(r0 + j), (unsigned long long)p[ST_BOUND]);
+            return PSIM_EDEVICE;
+        }
+        if (st_out) fill_stats(p, r0 + j, &st_out[j]);
+        if (p[NST] != ~0ull && p[NST + 1] > p[NST]) {     // 100 MHz ticks
+            h->kt_ms[KT_CONSUME] += (double)(p[NST + 1] - p[NST]) * 1e-5;
+            h->kt_n[KT_CONSUME]++;
+        }
+        for (uint32_t g = 0; g < G; g++) {            // (the padded messages cross the links)
+            if (g == s->idx && !self_comm) continue;
+            h->x_records += p[PIN_XCNT + g] & 0xFFFFFFFFull;
+            h->x_bytes += (uint64_t)(capH + capT) * sizeof(Wire);
+        }
+    }
+    if (done > 0) {                           // the first round's events are spent
+        for (uint32_t j : h->pend_join) h->pend_join_mark[j] = 0;
+        h->pend_crash.clear(); h->pend_join.clear(); h->pend_contact.clear();
+        h->pend_part_set = h->pend_part_clear = false;
+        h->pend_b_root.clear(); h->pend_b_msg.clear();
+        h->faults_dirty = false;
+    }
+    s->m_in = (uint32_t)s->pin[PIN_M];         // (the last route that ran)
+    *done_out = done;
+    if (done == nb) {
+        h->round = r0 + nb;
+        s->xbatch = std::min<uint32_t>(2 * s->xbatch, BATCH_MAX);
+        return PSIM_OK;
+    }
+    // round r0 + done stopped the batch on some rank: every rank redoes it
+    // exactly (a rank whose own outbox was short from its node phase)
+    s->xbatch = 1;
+    HIP_TRY(hipMemsetAsync(s->ctl.p, 0, sizeof cw, s->stream));
+    h->round = r0 + done;
+    const bool short_outbox = cw[0] == 1 && cw[1] == (uint32_t)h->round;
+    uint64_t st[NST];
+    if (short_outbox) {
+        std::fprintf(stderr, "psim: round %llu: outbox grows past its capacity (%zu -> %llu slots)\n",
+                     (unsigned long long)h->round, s->outbox.n, (unsigned long long)s->pin[PIN_TOTAL] + 1);
+        TRY(stream_wait(s));
+    }
+    TRY(run_round(h, st, done == 0, !short_outbox));
+    if (st_out) fill_stats(st, r0 + done, &st_out[done]);
+    *done_out = done + 1;
+    return PSIM_OK;
+}
+
 int shard_alloc(psim_handle* h, Shard* s) {
     HIP_TRY(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
     HIP_TRY(hipEventCreateWithFlags(&s->wait_ev, hipEventDisableTiming));
@@ -2753,7 +3030,7 @@ int shard_alloc(psim_handle* h, Shard* s) {
     rc |= s->desc_lite.alloc(2 * n); rc |= s->n_lite.alloc(4);
     rc |= s->desc_ptl.alloc(n); rc |= s->n_ptl.alloc(2);
     if (h->cfg.manager == PSIM_MANAGER_PLUGGABLE) { rc |= s->stop_ids.alloc(n); rc |= s->n_stop.alloc(1); }
-    rc |= s->stat_out.alloc(NST + 2);   // + the consume span
+    rc |= s->stat_out.alloc(STAT_OUT_N);   // + the consume span, the rank path's x-words
     rc |= s->ctl.alloc(2);
     rc |= s->stat_tile.alloc((size_t)STAT_TILES * NST);
     rc |= s->ikeys.alloc(1024); rc |= s->ivals.alloc(1024);
@@ -3209,7 +3486,9 @@ int psim_step(psim_handle* h, uint32_t n_rounds, psim_round_stats* stats) {
     for (uint32_t i = 0; i < n_rounds;) {
         if (batchable(h)) {                   // rounds back to back, one wait per batch
             uint32_t done = 0;
-            int rc = run_batch(h, std::min<uint32_t>(n_rounds - i, BATCH_MAX), stats ? stats + i : nullptr, &done);
+            int rc = h->ranked ? run_batch_ranked(h, std::min<uint32_t>(n_rounds - i, h->shards[0]->xbatch),
+                                                  stats ? stats + i : nullptr, &done)
+                               : run_batch(h, std::min<uint32_t>(n_rounds - i, BATCH_MAX), stats ? stats + i : nullptr, &done);
             if (rc) { h->failed = true; return rc; }
             for (Shard* s : h->shards)
                 if ((rc = grow_outx(s))) { h->failed = true; return rc; }
@@ -3226,6 +3505,18 @@ int psim_step(psim_handle* h, uint32_t n_rounds, psim_round_stats* stats) {
         if (h->cfg.strict && st[ST_OVF]) return PSIM_ECAPACITY;   // cfg.strict: fail loudly
         i++;
     }
+    // (diagnostic: the buffers' high-water marks, printed as they rise)
+    static const bool trace = getenv("PSIM_TRACE_BOUND") != nullptr;
+    if (trace)
+        for (Shard* s : h->shards)
+            if (s->pin[PIN_TMAX] > s->trace_tmax || s->pin[PIN_MMAX] > s->trace_mmax) {
+                s->trace_tmax = std::max<uint64_t>(s->trace_tmax, s->pin[PIN_TMAX]);
+                s->trace_mmax = std::max<uint64_t>(s->trace_mmax, s->pin[PIN_MMAX]);
+                std::fprintf(stderr, "psim: round %llu shard %u: outbox total max %llu of %zu slots, routed max %llu "
+                             "of %llu records\n", (unsigned long long)h->round, s->idx,
+                             (unsigned long long)s->trace_tmax, s->outbox.n, (unsigned long long)s->trace_mmax,
+                             (unsigned long long)s->rcap);
+            }
     return PSIM_OK;
 }
 

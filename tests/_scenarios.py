@@ -55,6 +55,32 @@ def doubling(make, n, seed, rounds, bcast_period=None, bcast_first=None, **cfg):
     return sim, st
 
 
+def multistep(make, n=4096, seed=9):
+    """Rounds run several at a time between events (psim_step(k), k > 1),
+    so the rank path runs batches of rounds (run_batch_ranked) whose
+    fixed-size exchange was sized by quieter rounds: a broadcast after a
+    quiet stretch, a crash wave, a partition -- each a step in the message
+    counts that overflows a capacity and makes every rank redo that round
+    exactly.  Doubling bootstrap, then 40 quiet rounds, a broadcast and 30
+    rounds, 5 % crashes and 20 rounds, a half/half partition for 12 rounds,
+    a broadcast and 25 rounds."""
+    sim = make(default_config(n_nodes=n, seed=seed))
+    st = [sim.run_schedule(W.doubling_join(n, seed), 20)]
+    st.append(sim.step(40))
+    sim.broadcast(0, 1)
+    st.append(sim.step(30))
+    rng = np.random.Generator(np.random.PCG64([seed, 77]))
+    victims = np.sort(rng.choice(np.arange(1, n, dtype=np.uint32), size=n // 20, replace=False)).astype(np.uint32)
+    sim.crash(victims)
+    st.append(sim.step(20))
+    sim.set_partition(W.half_partition(n))
+    st.append(sim.step(12))
+    sim.clear_partition()
+    sim.broadcast(1, 2)
+    st.append(sim.step(25))
+    return sim, np.concatenate(st)
+
+
 def churn_partition(make, n=2048, seed=5, rounds=140, **cfg):
     """Config E in miniature: doubling bootstrap, 20% churn over rounds
     40-79, a half/half partition for rounds 90-99, a broadcast every 10."""

@@ -92,14 +92,25 @@ def main():
     bad = [i for i, (a, b) in enumerate(zip(h1, h8)) if a != b]
     assert not bad, f"strategy rows differ in chunks {bad[:8]}"
     log("strategy rows equal (", len(h1), "chunks )")
-    # D's properties: every live node holds a partial view (SCAMP's
-    # log-sized views: (c + 1) ln N scale), nothing overflowed, messages
-    # conserved round to round
+    # D's properties: nothing overflowed, messages conserved round to round,
+    # and the view sizes the oracle shows on this schedule at every size it
+    # can run: mean partial view 2.987 / 2.993 / 2.991 and mean in-view
+    # 0.950 / 0.946 / 0.946 at 2^12 / 2^14 / 2^16 -- size-independent, not
+    # SCAMP's (c + 1) ln N (the reference's v2 keeps a forwarded subscription
+    # with probability 0.4 whatever the view size: random_0_or_1/0 is 1 when
+    # rand:uniform(10) >= 5, sv2:353-360, so Keep = trunc((|View| + 1) *
+    # Random) is 0 exactly when it is 0, sv2:293-294, App. A Q12).  The two means
+    # differ by ~2 because a partial view gets entries the in-views never
+    # see: its own node (init/1, sv2:57-61) and the joiner its contact adds
+    # in join/3 (sv2:64-72, no keep_subscription back); an in-view entry
+    # comes only from a keep_subscription (sv2:328-336), sent once per kept
+    # forwarded subscription (sv2:296-312)
     assert int(st1["overflow"].sum()) == 0
     em = st1["emitted"].sum(axis=1)
     got = st1["delivered"].sum(axis=1) + st1["dropped"] + st1["omitted"]
     assert np.array_equal(em[:-1], got[1:]), "messages not conserved"
-    assert 1.0 < props["view_mean"] < 6 * np.log(N), props
+    assert 2.95 < props["view_mean"] < 3.03 and 0.93 < props["in_mean"] < 0.96, props
+    assert abs(props["view_mean"] - props["in_mean"] - 2.0) < 0.1, props
     print("D24 OK", {"nodes": N, "ranks": RANKS, "rounds": len(st1), **props,
                      "msgs": int(st1["emitted"].sum()), "seconds": round(time.time() - T0, 1)}, flush=True)
 

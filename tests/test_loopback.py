@@ -38,6 +38,17 @@ def test_loopback_churn_partition_parity(world):
     gs.close()
 
 
+@pytest.mark.parametrize("world", [2, 3])
+def test_loopback_multistep_parity(world):
+    """rounds several at a time: batches of fixed-size exchanges on every
+    rank, stopping together at the round any rank overflowed"""
+    gs, gst = S.multistep(_ranks(world))
+    os_, ost = S.multistep(Oracle)
+    S.compare_stats(gst, ost)
+    S.compare_nodes(gs.nodes(), os_.nodes())
+    gs.close()
+
+
 def test_loopback_e_miniature_parity():
     """bench.py's sharding-check schedule (config E in miniature, 2^14 nodes)
     over 3 ranks: uneven shards (2^14 / 3)."""

@@ -44,6 +44,17 @@ def test_rccl1_churn_partition_parity():
     gs.close()
 
 
+def test_rccl1_multistep_parity():
+    """rounds several at a time (the rank path's batches of fixed-size
+    exchanges, run_batch_ranked), with the steps in traffic that overflow a
+    batch's capacities and make it redo a round exactly"""
+    gs, gst = S.multistep(_rccl1)
+    os_, ost = S.multistep(Oracle)
+    S.compare_stats(gst, ost)
+    S.compare_nodes(gs.nodes(), os_.nodes())
+    gs.close()
+
+
 def test_rccl1_e_miniature_parity():
     """bench.py's sharding-check schedule (config E in miniature, 2^14 nodes)"""
     gs, gst = S.e_miniature(_rccl1)
