@@ -527,6 +527,50 @@ __global__ void __launch_bounds__(RB_STEP) k_bucket_scatter(RouteIn in, uint32_t
         });
 }
 
+// The fused route pass of one shard's own outbox (G == 1; route_group
+// `fused`): k_bucket_hist, k_bucket_offsets and k_bucket_scatter in one
+// launch.  Each block counts its records per bucket in LDS, reserves its
+// share of every bucket it touches with one global atomic per bucket
+// (gcnt, zeroed by k_node_prep), and scatters its pairs into the bucket's
+// fixed region [b capb, (b + 1) capb) of `pairs`.  The order of a bucket's
+// pairs then depends on the atomics' timing -- which k_bucket_route never
+// relied on: it ranks each destination's records by LDS atomics and sorts
+// every run by source index.  A bucket past capb (a join storm on a few
+// destinations) stops the fused route: k_bucket_route returns, the round's
+// records are routed again by the four-pass route (flag in ctl[2]).
+template <bool DENSE>
+__global__ void __launch_bounds__(RB_STEP) k_bucket_fill(RouteIn in, uint32_t nsteps, uint32_t nb, uint32_t wshift,
+                                                         uint32_t* gcnt, uint32_t capb, uint2* pairs, uint32_t* ctl,
+                                                         unsigned long long* mark, StatsIn st) {
+    if (*ctl) return;                                 // an aborted batch (run_batch)
+    if (mark && blockIdx.x == 0 && threadIdx.x == 0) *mark = __builtin_amdgcn_s_memrealtime();   // (phase end)
+    extern __shared__ uint32_t hcnt[];                // nb bucket counters, then this block's bases
+    __shared__ uint32_t spre[RB_WAVES][65];
+    __shared__ uint64_t sbase[RB_WAVES][64];
+    if (blockIdx.x < st.nt) stats_tile(st, blockIdx.x, sbase);   // (uniform)
+    for (uint32_t j = threadIdx.x; j < nb; j += blockDim.x) hcnt[j] = 0;
+    __syncthreads();
+    for (uint32_t step = blockIdx.x; step < nsteps; step += gridDim.x)
+        route_step<DENSE>(in, step, spre, sbase,
+                          [&](uint32_t, uint32_t d, uint32_t) { atomicAdd(&hcnt[d >> wshift], 1u); });
+    __syncthreads();
+    bool over = false;
+    for (uint32_t j = threadIdx.x; j < nb; j += blockDim.x) {
+        const uint32_t c = hcnt[j];
+        const uint32_t b0 = c ? atomicAdd(&gcnt[j], c) : 0u;
+        over |= b0 + c > capb;
+        hcnt[j] = j * capb + b0;
+    }
+    if (over) ctl[2] = 1;                             // (read by k_bucket_route, a later launch)
+    __syncthreads();
+    const uint32_t wmask = (1u << wshift) - 1;
+    for (uint32_t step = blockIdx.x; step < nsteps; step += gridDim.x)
+        route_step<DENSE>(in, step, spre, sbase, [&](uint32_t g, uint32_t d, uint32_t cls) {
+            const uint32_t j = d >> wshift, q = atomicAdd(&hcnt[j], 1u);
+            if (q < (j + 1) * capb) pairs[q] = make_uint2((d & wmask) | (cls << 16), g);
+        });
+}
+
 // G > 1, sender side: this shard's outbox runs stably partitioned by owner
 // shard (owner = dst / per) straight into the send buffer in the wire format
 // (Wire: the heads of every owner, then the tails of every owner), so each
@@ -815,7 +859,7 @@ __global__ void __launch_bounds__(RR_THREADS) k_bucket_route(
     const uint2* __restrict__ pairs, const Msg* __restrict__ rec, const Wire* __restrict__ heads,
     const Wire* __restrict__ tails, uint32_t* rank, unsigned long long* cb,
     unsigned long long* bmask, uint32_t* in_beg, uint32_t* idx, uint32_t* tmp, Msg* __restrict__ inbox, uint64_t* hm,
-    uint64_t cap, const uint32_t* ctl) {
+    uint64_t cap, uint32_t* ctl, const uint32_t* gcnt, uint32_t capb, uint32_t round1, StatsIn st) {
     if (*ctl) return;                                 // an aborted batch (run_batch)
     // (the dynamic words hold 64-bit masks: 8-byte aligned -- a 4-byte static
     // word in front of them misaligned ds_or_b64 and faulted; the long-run
@@ -828,8 +872,40 @@ __global__ void __launch_bounds__(RR_THREADS) k_bucket_route(
     uint32_t* bs = sm + W;
     unsigned long long* mk = reinterpret_cast<unsigned long long*>(sm + 2 * W);
     uint32_t* pre = bs;                               // (after the bound sums are written out)
-    const uint32_t s0 = base[b], s1 = base[b + 1];
-    if (base[gridDim.x] > cap) return;                // overflow (k_bucket_scatter flagged it)
+    // the bucket's records: [s0, s1) of the inbox, from its pairs at q0 ..
+    uint32_t s0, s1, q0;
+    if (gcnt) {
+        // the fused route (k_bucket_fill): the round's stats from its tiles,
+        // then every block scans the bucket totals itself
+        if (b == 0) stats_final(st, reinterpret_cast<uint64_t(*)[64]>(sm));
+        const uint32_t nb = gridDim.x, per_t = (nb + blockDim.x - 1) / blockDim.x;
+        const uint32_t t0 = min(nb, threadIdx.x * per_t), t1 = min(nb, t0 + per_t);
+        uint32_t v = 0;
+        for (uint32_t j = t0; j < t1; j++) v += gcnt[j];
+        uint32_t m;
+        const uint32_t run = block_excl<uint32_t, RR_THREADS>(v, &m);
+        if (b >= t0 && b < t1) {
+            uint32_t x = run;
+            for (uint32_t j = t0; j < b; j++) x += gcnt[j];
+            spart[RR_THREADS + 1] = x;
+        }
+        __syncthreads();
+        s0 = spart[RR_THREADS + 1];
+        s1 = s0 + gcnt[b];
+        q0 = b * capb;
+        if (ctl[2] || m > cap) {                      // a bucket past capb, or the records past the buffers
+            if (b == 0 && threadIdx.x == 0) {         // (the host routes them again: four passes)
+                *(hm + (PIN_OVF - PIN_M)) = max(m, 1u);
+                if (round1) { ctl[1] = round1 - 1; __threadfence(); ctl[0] = 2; }
+            }
+            return;
+        }
+    } else {
+        s0 = base[b]; s1 = base[b + 1]; q0 = s0;
+        if (base[gridDim.x] > cap) return;            // overflow (k_bucket_scatter flagged it)
+    }
+    pairs += q0;                                      // (pair i of the bucket at pairs[i], its rank at rank[i])
+    rank += q0;
     for (uint32_t j = threadIdx.x; j < 4 * W; j += blockDim.x) sm[j] = 0;
     if (threadIdx.x == 0) s_nl = 0;
     __syncthreads();
@@ -849,20 +925,21 @@ __global__ void __launch_bounds__(RR_THREADS) k_bucket_route(
         }
         return r;
     };
-    const bool inreg = s1 - s0 <= regcap * blockDim.x;   // (uniform; regcap <= RR_REG)
+    const uint32_t np = s1 - s0;
+    const bool inreg = np <= regcap * blockDim.x;     // (uniform; regcap <= RR_REG)
     uint2 px[RR_REG];
     uint32_t pr[RR_REG];
     if (inreg) {
 #pragma unroll
         for (uint32_t k = 0; k < RR_REG; k++) {
-            const uint32_t p = s0 + threadIdx.x + k * blockDim.x;
-            px[k] = p < s1 ? pairs[p] : make_uint2(0, 0);
+            const uint32_t p = threadIdx.x + k * blockDim.x;
+            px[k] = p < np ? pairs[p] : make_uint2(0, 0);
         }
 #pragma unroll
         for (uint32_t k = 0; k < RR_REG; k++)
-            if (s0 + threadIdx.x + k * blockDim.x < s1) pr[k] = count(px[k]);
+            if (threadIdx.x + k * blockDim.x < np) pr[k] = count(px[k]);
     } else {
-        for (uint32_t p = s0 + threadIdx.x; p < s1; p += blockDim.x) rank[p] = count(pairs[p]);
+        for (uint32_t p = threadIdx.x; p < np; p += blockDim.x) rank[p] = count(pairs[p]);
     }
     __syncthreads();
     // run starts: each thread scans W / RR_THREADS consecutive counts, then
@@ -900,9 +977,9 @@ __global__ void __launch_bounds__(RR_THREADS) k_bucket_route(
     if (inreg) {
 #pragma unroll
         for (uint32_t k = 0; k < RR_REG; k++)
-            if (s0 + threadIdx.x + k * blockDim.x < s1) idx[s0 + pre[px[k].x & wmask] + pr[k]] = px[k].y;
+            if (threadIdx.x + k * blockDim.x < np) idx[s0 + pre[px[k].x & wmask] + pr[k]] = px[k].y;
     } else {
-        for (uint32_t p = s0 + threadIdx.x; p < s1; p += blockDim.x) {
+        for (uint32_t p = threadIdx.x; p < np; p += blockDim.x) {
             const uint2 x = pairs[p];
             idx[s0 + pre[x.x & wmask] + rank[p]] = x.y;
         }
@@ -978,8 +1055,12 @@ __device__ __forceinline__ bool due(uint32_t period, uint32_t r, uint32_t start)
 // messages addressed to dead ones.
 __global__ void __launch_bounds__(BLK) k_node_prep(RoundArgs a, const unsigned long long* bmask, uint64_t* packed,
                                                    uint64_t* part, uint32_t* ocnt, unsigned long long* btot,
-                                                   uint32_t per, uint64_t* tiles) {
+                                                   uint32_t per, uint64_t* tiles, uint32_t* gcnt, uint32_t ngcnt) {
     if (*a.ctl) return;                               // an aborted batch (run_batch)
+    // the fused route's bucket counters and its overflow flag, for this
+    // round's route (k_bucket_fill)
+    for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < ngcnt; j += gridDim.x * blockDim.x) gcnt[j] = 0;
+    if (gcnt && blockIdx.x == 0 && threadIdx.x == 0) const_cast<uint32_t*>(a.ctl)[2] = 0;
     __shared__ unsigned long long s_up, s_drop, s_b, s_w;
     if (threadIdx.x == 0) { s_up = 0; s_drop = 0; s_b = 0; s_w = 0; }
     if (blockIdx.x == 0 && threadIdx.x == 0) {
@@ -1583,6 +1664,7 @@ struct Shard {
     DBuf<uint32_t> okey, ocnt, in_beg,
         d_nact, n_slow, n_pt, n_shuf, n_lite, n_ptl, rank, tmp, hist, hoff;
     DBuf<uint32_t> rtot, rbase;         // route: per bucket its record count, and its first pair
+    DBuf<uint32_t> gcnt;                // fused route: per bucket its record count (k_bucket_fill's atomics)
     DBuf<unsigned long long> bmask;     // per local node: message slots of its BROADCAST records
     DBuf<uint2> pairs;                  // route: (destination in bucket | class, source index)
     DBuf<unsigned long long> cb;        // per local node: inbox count | bound sum << 32 (n + 1)
@@ -1705,6 +1787,10 @@ struct psim_handle {
     // hook, PSIM_ROUTE_BLOCKS, lowers it so small runs take several steps per block)
     uint32_t rb_blocks = RB_BLOCKS;
     uint32_t rr_reg = RR_REG;           // k_bucket_route: pairs a thread may hold (PSIM_ROUTE_REG=0: the array path)
+    // one shard's own outbox routed by the fused pass (k_bucket_fill) instead
+    // of k_bucket_hist + k_bucket_offsets + k_bucket_scatter
+    // (PSIM_ROUTE_FUSED=0: the four passes, for A/B; reroutes take them too)
+    bool route_fused = true;
 };
 
 namespace {
@@ -2037,7 +2123,7 @@ int phase_events_prepare(psim_handle* h, Shard* s, const RoundCtl& ctl, RoundArg
         TRY(s->stat_part.ensure((size_t)(s->pgrid + s->cgrid + s->rgrid + s->tgrid + s->sgrid + s->lgrid + s->qgrid) *
                                 NST));
         k_node_prep<<<s->pgrid, BLK, 0, s->stream>>>(a, s->bmask.p, s->bound.p, s->stat_part.p, s->ocnt.p,
-                                                     s->btot.p, s->pper, s->pscan.p);
+                                                     s->btot.p, s->pper, s->pscan.p, s->gcnt.p, (uint32_t)s->gcnt.n);
         // (pscan: the ranges' sums of packed words; k_desc's last block sums them all)
         // obase[n] = the exact total (btot, summed by k_desc's last block)
         TRY(scan_desc(s, a));
@@ -2206,7 +2292,7 @@ unsigned long long* phase_end_mark(psim_handle* h, Shard* s) {
                                                     : reinterpret_cast<unsigned long long*>(s->stat_out.p + NST) + 1;
 }
 
-int route_group(psim_handle* h, Shard* s, bool dense, uint32_t m, bool fixed = false) {
+int route_group(psim_handle* h, Shard* s, bool dense, uint32_t m, bool fixed = false, bool exact = false) {
     const uint32_t n = s->n;
     // buckets of 2^wshift destinations, one k_bucket_route block each, at
     // most 16 K of them (the two passes' LDS histograms: 4 B per bucket).
@@ -2240,6 +2326,27 @@ int route_group(psim_handle* h, Shard* s, bool dense, uint32_t m, bool fixed = f
                      s->stat_tile.p, s->stat_out.p, s->pin_dev + (size_t)s->stat_slot * PIN_STRIDE,
                      s->outx.p ? s->outx_top.p : nullptr, s->pin_dev};
     KTimer t(h, s, KT_SORT);
+    if (!dense && !exact && h->route_fused) {
+        // a bucket's fixed region holds 1.5x its share of the route's
+        // capacity: only a hot spot (a join storm) overflows one, and that
+        // round goes through the four passes again (run_round, run_batch)
+        const uint64_t capb64 = (s->rcap + nb - 1) / nb * 3 / 2 + 64;
+        const uint32_t capb = (uint32_t)std::min<uint64_t>(capb64, 0xFFFFFFFFull / nb);
+        if (s->gcnt.n < nb) {
+            TRY(s->gcnt.ensure(nb));
+            HIP_TRY(hipMemsetAsync(s->gcnt.p, 0, s->gcnt.n * 4, s->stream));
+        }
+        TRY(s->pairs.ensure((size_t)nb * capb));
+        TRY(s->rank.ensure((size_t)nb * capb));
+        k_bucket_fill<false><<<nblk, RB_STEP, lds_h, s->stream>>>(in, nsteps, nb, wshift, s->gcnt.p, capb, s->pairs.p,
+                                                                  s->ctl.p, phase_end_mark(h, s), st);
+        k_bucket_route<false><<<nb, RR_THREADS, lds_r, s->stream>>>(
+            n, wshift, h->rr_reg, nullptr, s->pairs.p, in.rec, nullptr, nullptr, s->rank.p, s->cb.p, s->bmask.p,
+            s->in_beg.p, s->ivals.p, s->tmp.p, s->inbox.p, s->pin_dev + PIN_M, s->rcap, s->ctl.p, s->gcnt.p, capb,
+            s->batch_round1, st);
+        HIP_TRY(hipGetLastError());
+        return PSIM_OK;
+    }
     if (dense)
         k_bucket_hist<true><<<nblk, RB_STEP, lds_h, s->stream>>>(in, nsteps, nb, wshift, s->hist.p, s->ctl.p,
                                                                  nullptr, st);
@@ -2260,11 +2367,13 @@ int route_group(psim_handle* h, Shard* s, bool dense, uint32_t m, bool fixed = f
     if (dense)
         k_bucket_route<true><<<nb, RR_THREADS, lds_r, s->stream>>>(
             n, wshift, h->rr_reg, s->rbase.p, s->pairs.p, nullptr, in.wire, in.tails, s->rank.p, s->cb.p, s->bmask.p,
-            s->in_beg.p, s->ivals.p, s->tmp.p, s->inbox.p, s->pin_dev + PIN_M, s->rcap, s->ctl.p);
+            s->in_beg.p, s->ivals.p, s->tmp.p, s->inbox.p, s->pin_dev + PIN_M, s->rcap, s->ctl.p, nullptr, 0u,
+            s->batch_round1, st);
     else
         k_bucket_route<false><<<nb, RR_THREADS, lds_r, s->stream>>>(
             n, wshift, h->rr_reg, s->rbase.p, s->pairs.p, in.rec, nullptr, nullptr, s->rank.p, s->cb.p, s->bmask.p,
-            s->in_beg.p, s->ivals.p, s->tmp.p, s->inbox.p, s->pin_dev + PIN_M, s->rcap, s->ctl.p);
+            s->in_beg.p, s->ivals.p, s->tmp.p, s->inbox.p, s->pin_dev + PIN_M, s->rcap, s->ctl.p, nullptr, 0u,
+            s->batch_round1, st);
     HIP_TRY(hipGetLastError());
     return PSIM_OK;
 }
@@ -2284,7 +2393,8 @@ int route_buffers(Shard* s, bool both_inboxes) {
 // G == 1: the outbox runs grouped by destination are the whole route
 // (m_in: read back with the round's stats; ivals, pairs, rank, tmp and the
 // inbox were sized in prepare by the outbox total, which bounds it)
-int phase_route_local(psim_handle* h, Shard* s) { return route_group(h, s, false, 0); }
+// exact: the four-pass route (a reroute after an overflow of the fused one)
+int phase_route_local(psim_handle* h, Shard* s, bool exact = false) { return route_group(h, s, false, 0, false, exact); }
 
 void send_counts(Shard* s, uint32_t G);
 
@@ -2619,7 +2729,7 @@ int run_round(psim_handle* h, uint64_t* st, bool events_applied = false, bool fr
                 else s->rcap = (want + (1ull << 20) - 1) >> 20 << 20;
             }
             TRY(route_buffers(s, false));
-            TRY(phase_route_local(h, s));
+            TRY(phase_route_local(h, s, true));
             TRY(stream_wait(s));
         }
         if (local_route(h)) s->m_in = (uint32_t)s->pin[PIN_M];   // routed this round
@@ -2722,9 +2832,11 @@ bool batchable(psim_handle* h) {
         !h->pend_lv_a.empty())
         return false;
     Shard* s = h->shards[0];
-    // a rank batches once an exact round has set the exchange capacities
-    // (every rank decides alike: the same events, the same all-reduced caps)
-    if (h->ranked) return !off_ranked && s->reserved && s->rcap && s->outbox.n && s->xcap_h && s->xcap_t;
+    // a rank batches once an exact round has set the exchange capacities.
+    // Every rank must decide alike, so nothing local enters here (a rank that
+    // has received no record yet has no route capacity: run_batch_ranked
+    // sizes it) -- only the events, the config and the all-reduced caps
+    if (h->ranked) return !off_ranked && s->reserved && s->outbox.n && s->xcap_h && s->xcap_t;
     return h->G == 1 && s->reserved && s->rcap && s->outbox.n;
 }
 
@@ -2822,7 +2934,7 @@ int run_batch(psim_handle* h, uint32_t nb, psim_round_stats* st_out, uint32_t* d
         if (want <= (1ull << 26)) while (s->rcap < want) s->rcap <<= 1;
         else s->rcap = (want + (1ull << 20) - 1) >> 20 << 20;
         TRY(route_buffers(s, false));
-        TRY(phase_route_local(h, s));
+        TRY(phase_route_local(h, s, true));
         TRY(phase_stats(h, s, done == 0 ? crashed0 : none));
         if (done == 0 && bc0)
             k_origin<<<grid_for(h->pend_b_root.size()), BLK, 0, s->stream>>>(
@@ -3031,7 +3143,7 @@ int shard_alloc(psim_handle* h, Shard* s) {
     rc |= s->desc_ptl.alloc(n); rc |= s->n_ptl.alloc(2);
     if (h->cfg.manager == PSIM_MANAGER_PLUGGABLE) { rc |= s->stop_ids.alloc(n); rc |= s->n_stop.alloc(1); }
     rc |= s->stat_out.alloc(STAT_OUT_N);   // + the consume span, the rank path's x-words
-    rc |= s->ctl.alloc(2);
+    rc |= s->ctl.alloc(4);   // (the abort word: code, round; then the fused route's overflow flag)
     rc |= s->stat_tile.alloc((size_t)STAT_TILES * NST);
     rc |= s->ikeys.alloc(1024); rc |= s->ivals.alloc(1024);
     rc |= s->recvh.alloc(1024); rc |= s->recvt.alloc(1024); rc |= s->wseg.alloc(130); rc |= s->inbox.alloc(1024); rc |= s->outbox.alloc(1024);
@@ -3212,6 +3324,8 @@ int psim_create(const psim_config* cfg, psim_handle** out) {
         if (b && *b) h->rb_blocks = std::max<uint32_t>(1, std::min<uint32_t>(RB_MAX_BLOCKS, (uint32_t)atoi(b)));
         const char* g = getenv("PSIM_ROUTE_REG");     // (test hook: the large-bucket path everywhere)
         if (g && *g) h->rr_reg = std::min<uint32_t>(RR_REG, (uint32_t)atoi(g));
+        const char* f = getenv("PSIM_ROUTE_FUSED");   // (0: the four-pass route every round, A/B)
+        if (f && *f) h->route_fused = atoi(f) != 0;
     }
     h->device = dev;
     for (uint32_t g = 0; g < G; g++) {

@@ -139,8 +139,13 @@ def test_crash_revive_parity():
     S.compare_nodes(gs.nodes(), os_.nodes())
 
 
-def test_star_hotspot_parity():
-    (gs, gst), (os_, ost) = _both(S.star, n=512)
+@pytest.mark.parametrize("n", [512, 1 << 16])
+def test_star_hotspot_parity(n):
+    """every node joins node 0 in one round; at 2^16 the JOINs overflow
+    their route bucket's fixed region (k_bucket_fill: 1.5x the bucket's
+    share of the route capacity) and that round goes through the four-pass
+    route again"""
+    (gs, gst), (os_, ost) = _both(S.star, n=n)
     S.compare_stats(gst, ost)
     S.compare_nodes(gs.nodes(), os_.nodes())
 
