@@ -56,15 +56,19 @@ enum { PIN_TOTAL = NST + 2, PIN_M = NST + 3, PIN_OVF = NST + 4, PIN_BIGIN = NST 
 // checks, exchange_fixed), PIN_XMH / PIN_XMT the ranks' largest per-owner head
 // / tail counts, summed; then this rank's per-owner send counts (G words)
 enum { PIN_XAB = NST + 8, PIN_XMH = NST + 9, PIN_XMT = NST + 10, PIN_XCNT = NST + 16 };
+// ... then every rank's largest per-owner head count (word PIN_XRANK + r)
+// and tail count (PIN_XRANK + 64 + r): each rank fills its own words and
+// zeros the others', so the sum all-reduce leaves the exact maxima
+constexpr uint32_t PIN_XRANK = PIN_XCNT + 64;
 // slot 0 only: the largest outbox total (k_desc) and routed count (the
 // route) since the host last cleared them (PSIM_TRACE_BOUND, psim_step)
 enum { PIN_TMAX = NST + 7, PIN_MMAX = NST + 11 };
 // stat_out: NST sums, the node-round span (2), the three x-words of the
 // rank path (all-reduced with the sums)
-constexpr uint32_t STAT_OUT_X = NST + 2, STAT_OUT_N = NST + 5;
+constexpr uint32_t STAT_OUT_X = NST + 2, STAT_OUT_R = NST + 5, STAT_OUT_N = NST + 5 + 128;
 // the pinned words: slot 0 holds the above (and a single round's stats);
 // slot j + 1 the stats and node-round span of round j of a batch (run_batch)
-constexpr uint32_t PIN_STRIDE = PIN_XCNT + 64;
+constexpr uint32_t PIN_STRIDE = PIN_XRANK + 128;
 constexpr uint32_t BATCH_MAX = 64;
 
 #define HIP_TRY(x)                                                       \
@@ -732,8 +736,12 @@ __global__ void __launch_bounds__(RB_STEP) k_owner_part(RouteIn in, uint32_t nst
 // the next batch's fixed exchange), and in a batched round (capH > 0) an
 // owner past its capacity aborts the round (code 3, ctl[1] = round).  An
 // aborted round sends counts of 0 (its send buffer was not written).
+// (xw[3 + r] / xw[3 + 64 + r]: rank r's largest head / tail count, every
+// other rank's word 0: the all-reduce sum keeps each rank's own)
 __global__ void k_owner_offsets(const uint32_t* hoff, uint32_t nblk, uint32_t G, uint64_t* d_off, uint64_t* cnt,
-                                uint64_t* xw, uint32_t capH, uint32_t capT, uint32_t* ctl, uint32_t round) {
+                                uint64_t* xw, uint32_t capH, uint32_t capT, uint32_t* ctl, uint32_t round,
+                                uint32_t rank) {
+    __shared__ uint32_t smh, smt;
     const uint32_t q = threadIdx.x;
     const bool dead = *ctl != 0;
     if (q <= 2 * G) d_off[q] = hoff[q * nblk];
@@ -741,7 +749,8 @@ __global__ void k_owner_offsets(const uint32_t* hoff, uint32_t nblk, uint32_t G,
         cnt[q] = dead ? 0ull
                       : (uint64_t)(hoff[(q + 1) * nblk] - hoff[q * nblk]) |
                             ((uint64_t)(hoff[(G + q + 1) * nblk] - hoff[(G + q) * nblk]) << 32);
-    if (xw && q == 0) {
+    if (!xw) return;                                  // (uniform)
+    if (q == 0) {
         uint32_t mh = 0, mt = 0;
         for (uint32_t o = 0; o < G && !dead; o++) {
             mh = max(mh, hoff[(o + 1) * nblk] - hoff[o * nblk]);
@@ -749,8 +758,11 @@ __global__ void k_owner_offsets(const uint32_t* hoff, uint32_t nblk, uint32_t G,
         }
         xw[1] = mh;
         xw[2] = mt;
+        smh = mh; smt = mt;
         if (capH && !dead && (mh > capH || mt > capT)) { ctl[1] = round; __threadfence(); ctl[0] = 3; }
     }
+    __syncthreads();
+    if (q < 128) xw[3 + q] = q == rank ? smh : q == 64 + rank ? smt : 0u;
 }
 
 // the rank path's abort word into the round's x-words, before their
@@ -1721,7 +1733,6 @@ struct Shard {
     // batch's length (1 after an abort, doubling up to BATCH_MAX)
     uint32_t xcap_h = 0, xcap_t = 0;
     uint32_t xbatch = 1;
-    uint64_t xmax_host[2] = {0, 0};     // (the host side of the exact round's max all-reduce)
     uint64_t trace_tmax = 0, trace_mmax = 0;   // PSIM_TRACE_BOUND's high-water marks
 };
 
@@ -2428,7 +2439,7 @@ int phase_partition(psim_handle* h, Shard* s, bool fixed = false) {
                                                              s->sendbuf.p, nullptr, capH, capT, s->ctl.p);
         k_owner_offsets<<<1, 256, 0, s->stream>>>(s->hoff.p, nblk, G, s->d_off.p, rccl ? h->comm_cnt.p : nullptr,
                                                   rccl ? s->stat_out.p + STAT_OUT_X : nullptr, capH, capT, s->ctl.p,
-                                                  (uint32_t)h->round);
+                                                  (uint32_t)h->round, s->idx);
         HIP_TRY(hipGetLastError());
         // an RCCL rank reads the offsets back with the received counts, after
         // the count all-to-all (exchange_rccl): one host wait a round, not two
@@ -2604,12 +2615,16 @@ int exchange_fixed(psim_handle* h) {
     return route_group(h, s, true, G * capH, true);
 }
 
-// the fixed capacities of the next batch after an exact rank round: the
-// largest per-owner head / tail counts of any rank this round (an all-reduce
-// max of the exact round, phase_stats, into pinned slot 0), 1.25x and 1024
-// more, never below the current ones -- the same on every rank
-void xcaps_update(Shard* s) {
-    const uint64_t mh = s->pin[PIN_XMH], mt = s->pin[PIN_XMT];
+// the fixed capacities of the next batch from a rank round's pinned slot p:
+// the largest per-owner head / tail count of any rank (every rank's own, in
+// the all-reduced stats), 1.25x and 1024 more, never below the current ones
+// -- the same on every rank
+void xcaps_update(psim_handle* h, Shard* s, const uint64_t* p) {
+    uint64_t mh = 0, mt = 0;
+    for (int r = 0; r < h->world && r < 64; r++) {
+        mh = std::max<uint64_t>(mh, p[PIN_XRANK + r]);
+        mt = std::max<uint64_t>(mt, p[PIN_XRANK + 64 + r]);
+    }
     const uint64_t ch = std::min<uint64_t>(mh + mh / 4 + 1024, 0x7FFFFFFFull);
     const uint64_t ct = std::min<uint64_t>(mt + mt / 4 + 1024, 0x7FFFFFFFull);
     s->xcap_h = std::max<uint32_t>(s->xcap_h, (uint32_t)ch);
@@ -2617,9 +2632,7 @@ void xcaps_update(Shard* s) {
 }
 
 // the round's end after its route (which summed the stats: StatsIn)
-// exact_caps: an exact rank round -- also the ranks' largest per-owner
-// counts (all-reduce max) for the next batch's capacities (xcaps_update)
-int phase_stats(psim_handle* h, Shard* s, const std::vector<uint32_t>& crashed, bool exact_caps = false) {
+int phase_stats(psim_handle* h, Shard* s, const std::vector<uint32_t>& crashed) {
     KTimer t(h, s, KT_STATS);
     if (h->ranked) {
         // the ranks' sums reduced on the device, on the shard's stream, and
@@ -2633,18 +2646,8 @@ int phase_stats(psim_handle* h, Shard* s, const std::vector<uint32_t>& crashed, 
         HIP_TRY(hipMemcpyAsync(pw, s->stat_out.p, NST * 8, hipMemcpyDeviceToDevice, s->stream));
         HIP_TRY(hipMemcpyAsync(pw + PIN_XAB, s->stat_out.p + STAT_OUT_X, 3 * 8, hipMemcpyDeviceToDevice, s->stream));
         HIP_TRY(hipMemcpyAsync(pw + PIN_XCNT, h->comm_cnt.p, h->G * 8, hipMemcpyDeviceToDevice, s->stream));
+        HIP_TRY(hipMemcpyAsync(pw + PIN_XRANK, s->stat_out.p + STAT_OUT_R, 128 * 8, hipMemcpyDeviceToDevice, s->stream));
         k_abort_sync<<<1, 64, 0, s->stream>>>(s->stat_out.p + STAT_OUT_X, s->ctl.p, (uint32_t)h->round);
-        if (exact_caps) {
-            s->xmax_host[0] = s->xmax_host[1] = 0;
-            for (uint32_t g = 0; g < h->G; g++) {
-                s->xmax_host[0] = std::max<uint64_t>(s->xmax_host[0], s->scnt[g]);
-                s->xmax_host[1] = std::max<uint64_t>(s->xmax_host[1], s->lcnt[g]);
-            }
-            uint64_t* xm = h->comm_cnt.p + 2 * h->G;       // (phase_partition sized it)
-            HIP_TRY(hipMemcpyAsync(xm, s->xmax_host, 16, hipMemcpyHostToDevice, s->stream));
-            TRY(h->comm->all_reduce(xm, 2, CType::U64, COp::MAX, s->stream));
-            HIP_TRY(hipMemcpyAsync(pw + PIN_XMH, xm, 16, hipMemcpyDeviceToDevice, s->stream));
-        }
     }
     if (!crashed.empty()) {
         TRY(upload(s, s->ev_ids, crashed));
@@ -2706,7 +2709,7 @@ int run_round(psim_handle* h, uint64_t* st, bool events_applied = false, bool fr
         else TRY(exchange_local(h));
     }
     for (Shard* s : h->shards) {
-        TRY(phase_stats(h, s, h->pend_crash, h->ranked));
+        TRY(phase_stats(h, s, h->pend_crash));
         if (!h->pend_b_root.empty())        // this round's origins are spent
             k_origin<<<grid_for(h->pend_b_root.size()), BLK, 0, s->stream>>>(
                 s->origin.p, s->lo, s->n, s->bc_roots.p, s->bc_msgs.p, (uint32_t)h->pend_b_root.size(), s->flags.p,
@@ -2733,7 +2736,7 @@ int run_round(psim_handle* h, uint64_t* st, bool events_applied = false, bool fr
             TRY(stream_wait(s));
         }
         if (local_route(h)) s->m_in = (uint32_t)s->pin[PIN_M];   // routed this round
-        if (h->ranked) xcaps_update(s);           // (the next batch's exchange capacities)
+        if (h->ranked) xcaps_update(h, s, s->pin);   // (the next batch's exchange capacities)
         static const bool trace_relay = getenv("PSIM_TRACE_RELAY") != nullptr;
         if (trace_relay && s->rgrid)
         {
@@ -3023,6 +3026,14 @@ int run_batch_ranked(psim_handle* h, uint32_t nb, psim_round_stats* st_out, uint
     for (uint32_t j = 0; j < nb; j++)
         if (s->pin[(size_t)(j + 1) * PIN_STRIDE + PIN_XAB]) { done = j; break; }
     if (done == nb && cw[0]) return PSIM_EDEVICE;     // (an abort no round reported)
+    // the capacities grow with the largest counts the batch met -- the
+    // stopped round's included, which is what the redo will need
+    for (uint32_t j = 0; j <= done && j < nb; j++) xcaps_update(h, s, s->pin + (size_t)(j + 1) * PIN_STRIDE);
+    static const bool trace_batch = getenv("PSIM_TRACE_BATCH") != nullptr;
+    if (trace_batch)
+        std::fprintf(stderr, "psim: rank %d: batch of %u from round %llu: %u done%s; caps %u heads, %u tails\n",
+                     h->rank, nb, (unsigned long long)r0, done, done < nb ? " (one redone exactly)" : "", s->xcap_h,
+                     s->xcap_t);
     const bool self_comm = h->world == 1;
     for (uint32_t j = 0; j < done; j++) {
         const uint64_t* p = s->pin + (size_t)(j + 1) * PIN_STRIDE;
