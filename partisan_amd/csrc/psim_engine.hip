@@ -306,13 +306,21 @@ struct RouteIn {
     const Wire* tails;         // dense: the tails
     const uint32_t* seg;       // dense: per source shard its first head, then its first tail (2 (nseg + 1))
     uint32_t nseg;
-    // dense, a batched rank round (exchange_fixed): source g's heads at
-    // [g capH, g capH + its count), its tails at [g capT, ..), the counts
-    // (heads | tails << 32) received by the count all-to-all; capH = 0: the
-    // packed layout above
+    // dense, a batched rank round (exchange_fixed): source g's message is
+    // XHDR header slots (xhdr_*: its counts, abort flag, largest counts and
+    // stats) then its heads, at [g (XHDR + capH), ..); its tails at
+    // [g capT, ..); capH = 0: the packed layout above
     uint32_t capH, capT;
-    const uint64_t* rcnt;
+    uint32_t round;            // (the abort word's round, k_bucket_hist's header pass)
 };
+
+// The header of a batched rank round's message to one owner (XHDR wire
+// slots, read as 64-bit words): the record counts (heads | tails << 32), the
+// sender's abort flag, its largest per-owner head and tail counts, then its
+// NST stats sums -- the round's count all-to-all and stats all-reduce ride
+// with the records (one grouped send / receive a round)
+enum { XH_CNT = 0, XH_ABORT = 1, XH_MH = 2, XH_MT = 3, XH_STATS = 4 };
+constexpr uint32_t XHDR = (XH_STATS + NST + 3) / 4;
 
 // the source shard of received head i (seg: nseg + 1 increasing starts)
 __device__ __forceinline__ uint32_t wire_source(const RouteIn& in, uint32_t i) {
@@ -337,9 +345,12 @@ __device__ __forceinline__ void route_step(const RouteIn& in, uint32_t step, uin
     if (DENSE) {
         uint32_t g = 0;
         bool ok = i < in.n_src;
-        if (in.capH && ok) {                          // (the fixed layout: a slot past its source's count is empty)
-            g = i / in.capH;
-            ok = i - g * in.capH < min((uint32_t)in.rcnt[g], in.capH);
+        if (in.capH && ok) {                          // (the fixed layout: a header slot, or one past its
+            const uint32_t xs = XHDR + in.capH;       //  source's count, holds no record)
+            g = i / xs;
+            const uint32_t j = i - g * xs;
+            const uint32_t c = (uint32_t)reinterpret_cast<const uint64_t*>(in.wire + (size_t)g * xs)[XH_CNT];
+            ok = j >= XHDR && j - XHDR < min(c, in.capH);
         }
         if (ok) {
             const uint4 h0 = in.wire[i].q[0];        // dst, src, type word, seq
@@ -442,16 +453,44 @@ __device__ __forceinline__ void stats_final(const StatsIn& st, uint64_t (*red)[6
     __syncthreads();
 }
 
+// a batched rank round's received headers (block 0 of k_bucket_hist, the
+// first kernel after the exchange, whatever the abort word says): the
+// sources' stats summed into the round's pinned words, the ranks' abort flags
+// (PIN_XAB) and largest counts (PIN_XRANK); a round any rank aborted stops
+// this rank's later kernels too (code 4)
+__device__ __forceinline__ void xhdr_reduce(const RouteIn& in, const StatsIn& st, uint32_t* ctl) {
+    const uint32_t c = threadIdx.x, xs = XHDR + in.capH;
+    auto hw = [&](uint32_t g, uint32_t k) { return reinterpret_cast<const uint64_t*>(in.wire + (size_t)g * xs)[k]; };
+    if (c < NST) {
+        uint64_t v = 0;
+        for (uint32_t g = 0; g < in.nseg; g++) v += hw(g, XH_STATS + c);
+        st.hout[c] = v;
+    } else if (c >= 64 && c < 64 + in.nseg) {
+        st.hout[PIN_XRANK + (c - 64)] = hw(c - 64, XH_MH);
+        st.hout[PIN_XRANK + 64 + (c - 64)] = hw(c - 64, XH_MT);
+    } else if (c == 256) {
+        uint64_t ab = 0;
+        for (uint32_t g = 0; g < in.nseg; g++) ab += hw(g, XH_ABORT);
+        st.hout[PIN_XAB] = ab;
+        if (ab && !ctl[0]) { ctl[1] = in.round; __threadfence(); ctl[0] = 4; }
+    }
+}
+
 template <bool DENSE>
 __global__ void __launch_bounds__(RB_STEP) k_bucket_hist(RouteIn in, uint32_t nsteps, uint32_t nb,
-                                                         uint32_t wshift, uint32_t* hist, const uint32_t* ctl,
+                                                         uint32_t wshift, uint32_t* hist, uint32_t* ctl,
                                                          unsigned long long* mark, StatsIn st) {
-    if (*ctl) return;                                 // an aborted batch (run_batch)
+    __shared__ uint32_t s_dead;
+    if (DENSE && in.capH && blockIdx.x == 0) xhdr_reduce(in, st, ctl);
+    // (read once a block: block 0 above may be writing it)
+    if (threadIdx.x == 0) s_dead = *ctl;
+    __syncthreads();
+    if (s_dead) return;                               // an aborted batch (run_batch)
     if (mark && blockIdx.x == 0 && threadIdx.x == 0) *mark = __builtin_amdgcn_s_memrealtime();   // (phase end)
     extern __shared__ uint32_t hcnt[];                // nb bucket counters
     __shared__ uint32_t spre[RB_WAVES][65];
     __shared__ uint64_t sbase[RB_WAVES][64];
-    if (blockIdx.x < st.nt) stats_tile(st, blockIdx.x, sbase);   // (uniform)
+    if (blockIdx.x < st.nt) stats_tile(st, blockIdx.x, sbase);   // (uniform; nt = 0: the headers')
     for (uint32_t j = threadIdx.x; j < nb; j += blockDim.x) hcnt[j] = 0;
     __syncthreads();
     for (uint32_t step = blockIdx.x; step < nsteps; step += gridDim.x)
@@ -490,7 +529,7 @@ __global__ void __launch_bounds__(RB_STEP) k_bucket_scatter(RouteIn in, uint32_t
     extern __shared__ uint32_t hcnt[];                // nb rank counters
     __shared__ uint32_t spre[RB_WAVES][65];
     __shared__ uint64_t sbase[RB_WAVES][64];
-    if (blockIdx.x == 0) stats_final(st, sbase);      // (the tiles are k_bucket_hist's; before any return)
+    if (blockIdx.x == 0 && st.nt) stats_final(st, sbase);   // (the tiles are k_bucket_hist's; before any return)
     // the buckets' bases: the totals through LDS (coalesced), a run of them a
     // thread, one block scan of the run sums
     for (uint32_t j = threadIdx.x; j < nb; j += blockDim.x) hcnt[j] = tot[j];
@@ -595,19 +634,23 @@ __global__ void __launch_bounds__(RB_STEP) k_bucket_fill(RouteIn in, uint32_t ns
 // within a batch is a ballot over the lanes of the same owner, one ballot
 // per distinct owner in the batch (<= G).
 // A batched rank round (capH > 0, exchange_fixed) writes the fixed layout
-// instead: owner q's heads at [q capH, (q + 1) capH), its tails at G capH +
-// [q capT, (q + 1) capT); a record past its owner's capacity is not written
-// (k_owner_offsets aborts the round, code 3).
+// instead: owner q's message -- XHDR header slots (k_owner_offsets), then its
+// heads -- at [q (XHDR + capH), (q + 1) (XHDR + capH)), its tails at
+// G (XHDR + capH) + [q capT, (q + 1) capT); a record past its owner's
+// capacity is not written (k_owner_offsets aborts the round, code 3).  The
+// count pass's first blocks also sum the round's stats rows into tiles
+// (st.nt > 0: the stats travel in the headers instead of an all-reduce).
 template <bool WRITE>
 __global__ void __launch_bounds__(RB_STEP) k_owner_part(RouteIn in, uint32_t nsteps, uint32_t spb, uint32_t G,
                                                         uint32_t per, uint32_t* hist,
                                                         const uint32_t* __restrict__ off, Wire* __restrict__ out,
                                                         unsigned long long* mark, uint32_t capH, uint32_t capT,
-                                                        const uint32_t* ctl) {
+                                                        const uint32_t* ctl, StatsIn st) {
     if (*ctl) return;                                 // an aborted batch (run_batch_ranked)
     if (mark && blockIdx.x == 0 && threadIdx.x == 0) *mark = __builtin_amdgcn_s_memrealtime();   // (phase end)
     __shared__ uint32_t spre[RB_WAVES][65];
     __shared__ uint64_t sbase[RB_WAVES][64];
+    if (!WRITE && blockIdx.x < st.nt) stats_tile(st, blockIdx.x, sbase);   // (uniform)
     __shared__ uint32_t wc[RB_WAVES][64], wl[RB_WAVES][64];   // per wave and owner: records / long ones this step
     __shared__ uint32_t run[64], runl[64];            // per owner: the block's next head / tail position
     __shared__ uint32_t tb[64];                       // per owner: its first tail (WRITE)
@@ -616,9 +659,10 @@ __global__ void __launch_bounds__(RB_STEP) k_owner_part(RouteIn in, uint32_t nst
         const uint32_t o = threadIdx.x;
         const bool q = WRITE && o < G;
         if (capH) {                                   // (each owner's region starts at its fixed base)
-            run[o] = q ? o * capH + off[o * nblk + blockIdx.x] - off[o * nblk] : 0u;
-            runl[o] = q ? G * capH + o * capT + off[(G + o) * nblk + blockIdx.x] - off[(G + o) * nblk] : 0u;
-            tb[o] = q ? G * capH + o * capT : 0u;
+            const uint32_t xs = XHDR + capH;
+            run[o] = q ? o * xs + XHDR + off[o * nblk + blockIdx.x] - off[o * nblk] : 0u;
+            runl[o] = q ? G * xs + o * capT + off[(G + o) * nblk + blockIdx.x] - off[(G + o) * nblk] : 0u;
+            tb[o] = q ? G * xs + o * capT : 0u;
         } else {
             run[o] = q ? off[o * nblk + blockIdx.x] : 0u;
             runl[o] = q ? off[(G + o) * nblk + blockIdx.x] : 0u;
@@ -706,7 +750,7 @@ __global__ void __launch_bounds__(RB_STEP) k_owner_part(RouteIn in, uint32_t nst
                             out[lpos].q[1] = x3;
                         }
                     }
-                    if (!capH || pos < (o + 1) * capH) {
+                    if (!capH || pos < (o + 1) * (XHDR + capH)) {
                         out[pos].q[0] = x0;
                         out[pos].q[1] = x1;
                     }
@@ -738,12 +782,48 @@ __global__ void __launch_bounds__(RB_STEP) k_owner_part(RouteIn in, uint32_t nst
 // aborted round sends counts of 0 (its send buffer was not written).
 // (xw[3 + r] / xw[3 + 64 + r]: rank r's largest head / tail count, every
 // other rank's word 0: the all-reduce sum keeps each rank's own)
+// A batched round (capH > 0) writes each owner's message header instead:
+// the counts, this rank's abort flag and largest counts, and the round's
+// stats summed from the count pass's tiles; and the round's span, its own
+// send counts (PIN_XCNT) and the outstanding pool's top into the pinned words
 __global__ void k_owner_offsets(const uint32_t* hoff, uint32_t nblk, uint32_t G, uint64_t* d_off, uint64_t* cnt,
                                 uint64_t* xw, uint32_t capH, uint32_t capT, uint32_t* ctl, uint32_t round,
-                                uint32_t rank) {
+                                uint32_t rank, Wire* sendbuf, StatsIn st) {
     __shared__ uint32_t smh, smt;
+    __shared__ uint64_t ssum[64];
     const uint32_t q = threadIdx.x;
     const bool dead = *ctl != 0;
+    if (capH) {
+        const uint32_t xs = XHDR + capH;
+        uint32_t mh = 0, mt = 0;
+        for (uint32_t o = 0; o < G && !dead; o++) {
+            mh = max(mh, hoff[(o + 1) * nblk] - hoff[o * nblk]);
+            mt = max(mt, hoff[(G + o + 1) * nblk] - hoff[(G + o) * nblk]);
+        }
+        const bool over = !dead && (mh > capH || mt > capT);
+        if (q < NST) {
+            uint64_t v = 0;
+            for (uint32_t b = 0; b < st.nt; b++) v += st.tiles[(size_t)b * NST + q];
+            ssum[q] = v;
+        }
+        __syncthreads();
+        for (uint32_t o = 0; o < G; o++) {
+            uint64_t* hw = reinterpret_cast<uint64_t*>(sendbuf + (size_t)o * xs);
+            const uint64_t c = dead ? 0ull
+                                    : (uint64_t)(hoff[(o + 1) * nblk] - hoff[o * nblk]) |
+                                          ((uint64_t)(hoff[(G + o + 1) * nblk] - hoff[(G + o) * nblk]) << 32);
+            if (q == 0) { hw[XH_CNT] = c; hw[XH_ABORT] = dead || over ? 1u : 0u; hw[XH_MH] = mh; hw[XH_MT] = mt; }
+            if (q < NST) hw[XH_STATS + q] = ssum[q];
+            if (q == 1) st.hout[PIN_XCNT + o] = c;
+        }
+        if (q == 0) {
+            st.hout[NST] = st.out[NST];               // (the node-round span)
+            st.hout[NST + 1] = st.out[NST + 1];
+            if (st.outx_top) st.hout0[PIN_OUTX] = *st.outx_top;
+            if (over) { ctl[1] = round; __threadfence(); ctl[0] = 3; }
+        }
+        return;
+    }
     if (q <= 2 * G) d_off[q] = hoff[q * nblk];
     if (cnt && q < G)
         cnt[q] = dead ? 0ull
@@ -765,17 +845,7 @@ __global__ void k_owner_offsets(const uint32_t* hoff, uint32_t nblk, uint32_t G,
     if (q < 128) xw[3 + q] = q == rank ? smh : q == 64 + rank ? smt : 0u;
 }
 
-// the rank path's abort word into the round's x-words, before their
-// all-reduce (every rank, whatever its own state: ranks > 0 of the sum mean
-// some rank's round did not finish); after it, a rank whose own round went
-// through stops its later ones too (code 4), so every rank of a batch stops
-// at the same round
-__global__ void k_xabort(const uint32_t* ctl, uint64_t* xw) {
-    if (threadIdx.x == 0) xw[0] = *ctl != 0 ? 1u : 0u;
-}
-__global__ void k_abort_sync(const uint64_t* xw, uint32_t* ctl, uint32_t round) {
-    if (threadIdx.x == 0 && xw[0] && !*ctl) { ctl[1] = round; __threadfence(); ctl[0] = 4; }
-}
+
 
 
 // bitonic sort of p[0..k) (k <= RUN_LDS) through LDS, whole block
@@ -2165,13 +2235,19 @@ int phase_events_prepare(psim_handle* h, Shard* s, const RoundCtl& ctl, RoundArg
                 const uint64_t per_slot = sizeof(Msg) + sizeof(uint32_t);
                 // (memory the current buffers hold comes back when they regrow)
                 uint64_t avail = fr + (uint64_t)s->outbox.n * sizeof(Msg) + (uint64_t)s->okey.n * 4;
+                // (PSIM_RESERVE_PER_NODE / PSIM_RCAP_RESERVE: other reservations,
+                // for measurements of the memory a workload needs)
+                static const uint64_t res_pn = getenv("PSIM_RESERVE_PER_NODE")
+                                                   ? strtoull(getenv("PSIM_RESERVE_PER_NODE"), nullptr, 10) : RESERVE_PER_NODE;
+                static const uint64_t rcap_pn = getenv("PSIM_RCAP_RESERVE")
+                                                    ? strtoull(getenv("PSIM_RCAP_RESERVE"), nullptr, 10) : RCAP_RESERVE;
                 if (local_route(h) && !rcap_init) {
-                    const uint64_t rc = (uint64_t)n * RCAP_RESERVE;
+                    const uint64_t rc = (uint64_t)n * rcap_pn;
                     if (rc > s->rcap && (double)(rc * per_rec) <= RCAP_FREE_FRAC * (double)avail) s->rcap = rc;
                     const uint64_t held = s->rcap * per_rec;
                     avail = avail > held ? avail - held : 0;
                 }
-                const uint64_t r = std::min<uint64_t>((uint64_t)n * RESERVE_PER_NODE,
+                const uint64_t r = std::min<uint64_t>((uint64_t)n * res_pn,
                                                       (uint64_t)((1.0 - OUTBOX_SPARE) * (double)avail) / per_slot);
                 if (r > want) {
                     want = r;
@@ -2321,7 +2397,7 @@ int route_group(psim_handle* h, Shard* s, bool dense, uint32_t m, bool fixed = f
     const RouteIn in{s->outbox.p, s->okey.p, s->obase.p, s->ocnt.p, dense ? m : n, s->lo,
                      h->cfg.manager == PSIM_MANAGER_PLUGGABLE, dense ? s->recvh.p : nullptr,
                      dense ? s->recvt.p : nullptr, dense && !fixed ? s->wseg.p : nullptr, dense ? h->G : 0u,
-                     fixed ? s->xcap_h : 0u, fixed ? s->xcap_t : 0u, fixed ? h->comm_cnt.p + h->G : nullptr};
+                     fixed ? s->xcap_h : 0u, fixed ? s->xcap_t : 0u, (uint32_t)h->round};
     const uint32_t nsteps = std::max<uint32_t>(1, (in.n_src + RB_STEP - 1) / RB_STEP);
     const uint32_t nblk = std::min<uint32_t>(nsteps, h->rb_blocks);
     const size_t nh = (size_t)nb * nblk;
@@ -2332,8 +2408,10 @@ int route_group(psim_handle* h, Shard* s, bool dense, uint32_t m, bool fixed = f
     const size_t lds_h = (size_t)nb * 4, lds_r = (size_t)W * 16;
     // the round's stats rows (every node-phase kernel's blocks) are complete
     const uint32_t rows = s->pgrid + s->cgrid + s->rgrid + s->tgrid + s->sgrid + s->lgrid + s->qgrid;
+    // (a batched rank round, fixed: the stats came summed in the message
+    // headers -- k_bucket_hist's block 0 adds them up, no tiles here)
     const StatsIn st{s->stat_part.p, rows,
-                     std::min<uint32_t>(nblk, std::min<uint32_t>(STAT_TILES, std::max<uint32_t>(1, rows / 32))),
+                     fixed ? 0u : std::min<uint32_t>(nblk, std::min<uint32_t>(STAT_TILES, std::max<uint32_t>(1, rows / 32))),
                      s->stat_tile.p, s->stat_out.p, s->pin_dev + (size_t)s->stat_slot * PIN_STRIDE,
                      s->outx.p ? s->outx_top.p : nullptr, s->pin_dev};
     KTimer t(h, s, KT_SORT);
@@ -2430,16 +2508,26 @@ int phase_partition(psim_handle* h, Shard* s, bool fixed = false) {
     if (rccl) TRY(h->comm_cnt.ensure(2 * G + 2));   // (send and receive counts, then 2 words of phase_stats)
     s->soff.assign(2 * G + 1, 0);
     const uint32_t capH = fixed ? s->xcap_h : 0u, capT = fixed ? s->xcap_t : 0u;
+    // a batched round's stats: tiles from the count pass, summed into the
+    // message headers by k_owner_offsets (the route sums the received ones)
+    StatsIn st{};
+    if (fixed) {
+        const uint32_t rows = s->pgrid + s->cgrid + s->rgrid + s->tgrid + s->sgrid + s->lgrid + s->qgrid;
+        st = StatsIn{s->stat_part.p, rows,
+                     std::min<uint32_t>(nblk, std::min<uint32_t>(STAT_TILES, std::max<uint32_t>(1, rows / 32))),
+                     s->stat_tile.p, s->stat_out.p, s->pin_dev + (size_t)s->stat_slot * PIN_STRIDE,
+                     s->outx.p ? s->outx_top.p : nullptr, s->pin_dev};
+    }
     {
         KTimer t(h, s, KT_SORT);
         k_owner_part<false><<<nblk, RB_STEP, 0, s->stream>>>(in, nsteps, spb, G, h->per, s->hist.p, nullptr,
-                                                              nullptr, phase_end_mark(h, s), capH, capT, s->ctl.p);
+                                                              nullptr, phase_end_mark(h, s), capH, capT, s->ctl.p, st);
         TRY(scan_excl(s, s->hist.p, s->hoff.p, (uint32_t)nh));
         k_owner_part<true><<<nblk, RB_STEP, 0, s->stream>>>(in, nsteps, spb, G, h->per, nullptr, s->hoff.p,
-                                                             s->sendbuf.p, nullptr, capH, capT, s->ctl.p);
+                                                             s->sendbuf.p, nullptr, capH, capT, s->ctl.p, StatsIn{});
         k_owner_offsets<<<1, 256, 0, s->stream>>>(s->hoff.p, nblk, G, s->d_off.p, rccl ? h->comm_cnt.p : nullptr,
                                                   rccl ? s->stat_out.p + STAT_OUT_X : nullptr, capH, capT, s->ctl.p,
-                                                  (uint32_t)h->round, s->idx);
+                                                  (uint32_t)h->round, s->idx, s->sendbuf.p, st);
         HIP_TRY(hipGetLastError());
         // an RCCL rank reads the offsets back with the received counts, after
         // the count all-to-all (exchange_rccl): one host wait a round, not two
@@ -2592,27 +2680,27 @@ int exchange_rccl(psim_handle* h) {
 // largest per-owner count seen so far, 1.25x (xcaps_update).
 int exchange_fixed(psim_handle* h) {
     Shard* s = h->shards[0];
-    const uint32_t G = h->G, capH = s->xcap_h, capT = s->xcap_t;
+    const uint32_t G = h->G, capT = s->xcap_t;
+    const size_t xs = XHDR + s->xcap_h;               // (a message: its header, then the heads)
     KTimer t(h, s, KT_EXCHANGE);
-    TRY(h->comm->all_to_all_u64(h->comm_cnt.p, h->comm_cnt.p + G, 1, s->stream));
     std::vector<Xfer> sends, recvs;
     const bool self_comm = h->world == 1;
     for (uint32_t g = 0; g < G; g++) {
         if (g == s->idx && !self_comm) continue;
-        sends.push_back({(int)g, s->sendbuf.p + (size_t)g * capH, (size_t)capH * sizeof(Wire)});
-        sends.push_back({(int)g, s->sendbuf.p + (size_t)G * capH + (size_t)g * capT, (size_t)capT * sizeof(Wire)});
-        recvs.push_back({(int)g, s->recvh.p + (size_t)g * capH, (size_t)capH * sizeof(Wire)});
+        sends.push_back({(int)g, s->sendbuf.p + g * xs, xs * sizeof(Wire)});
+        sends.push_back({(int)g, s->sendbuf.p + G * xs + (size_t)g * capT, (size_t)capT * sizeof(Wire)});
+        recvs.push_back({(int)g, s->recvh.p + g * xs, xs * sizeof(Wire)});
         recvs.push_back({(int)g, s->recvt.p + (size_t)g * capT, (size_t)capT * sizeof(Wire)});
     }
     TRY(h->comm->exchange(sends, recvs, s->stream));
     if (!self_comm) {
         const uint32_t g = s->idx;
-        HIP_TRY(hipMemcpyAsync(s->recvh.p + (size_t)g * capH, s->sendbuf.p + (size_t)g * capH, (size_t)capH * sizeof(Wire),
-                               hipMemcpyDeviceToDevice, s->stream));
-        HIP_TRY(hipMemcpyAsync(s->recvt.p + (size_t)g * capT, s->sendbuf.p + (size_t)G * capH + (size_t)g * capT,
+        HIP_TRY(hipMemcpyAsync(s->recvh.p + g * xs, s->sendbuf.p + g * xs, xs * sizeof(Wire), hipMemcpyDeviceToDevice,
+                               s->stream));
+        HIP_TRY(hipMemcpyAsync(s->recvt.p + (size_t)g * capT, s->sendbuf.p + G * xs + (size_t)g * capT,
                                (size_t)capT * sizeof(Wire), hipMemcpyDeviceToDevice, s->stream));
     }
-    return route_group(h, s, true, G * capH, true);
+    return route_group(h, s, true, (uint32_t)(G * xs), true);
 }
 
 // the fixed capacities of the next batch from a rank round's pinned slot p:
@@ -2632,22 +2720,19 @@ void xcaps_update(psim_handle* h, Shard* s, const uint64_t* p) {
 }
 
 // the round's end after its route (which summed the stats: StatsIn)
-int phase_stats(psim_handle* h, Shard* s, const std::vector<uint32_t>& crashed) {
+// batched: a batched rank round -- its stats came in the message headers
+int phase_stats(psim_handle* h, Shard* s, const std::vector<uint32_t>& crashed, bool batched = false) {
     KTimer t(h, s, KT_STATS);
-    if (h->ranked) {
+    if (h->ranked && !batched) {
         // the ranks' sums reduced on the device, on the shard's stream, and
         // stored over the pinned words: the end of the round waits once
         // (a host copy, an all-reduce and a second wait after it before).
         // The x-words go with them: whether a rank's round aborted (a batch),
         // the largest per-owner counts (the next batch's capacities)
         uint64_t* pw = s->pin_dev + (size_t)s->stat_slot * PIN_STRIDE;
-        k_xabort<<<1, 64, 0, s->stream>>>(s->ctl.p, s->stat_out.p + STAT_OUT_X);
         TRY(h->comm->all_reduce(s->stat_out.p, STAT_OUT_N, CType::U64, COp::SUM, s->stream));
         HIP_TRY(hipMemcpyAsync(pw, s->stat_out.p, NST * 8, hipMemcpyDeviceToDevice, s->stream));
-        HIP_TRY(hipMemcpyAsync(pw + PIN_XAB, s->stat_out.p + STAT_OUT_X, 3 * 8, hipMemcpyDeviceToDevice, s->stream));
-        HIP_TRY(hipMemcpyAsync(pw + PIN_XCNT, h->comm_cnt.p, h->G * 8, hipMemcpyDeviceToDevice, s->stream));
         HIP_TRY(hipMemcpyAsync(pw + PIN_XRANK, s->stat_out.p + STAT_OUT_R, 128 * 8, hipMemcpyDeviceToDevice, s->stream));
-        k_abort_sync<<<1, 64, 0, s->stream>>>(s->stat_out.p + STAT_OUT_X, s->ctl.p, (uint32_t)h->round);
     }
     if (!crashed.empty()) {
         TRY(upload(s, s->ev_ids, crashed));
@@ -2980,8 +3065,8 @@ int run_batch_ranked(psim_handle* h, uint32_t nb, psim_round_stats* st_out, uint
     Shard* s = h->shards[0];
     const uint32_t G = h->G, capH = s->xcap_h, capT = s->xcap_t;
     const uint64_t r0 = h->round;
-    TRY(s->sendbuf.ensure((size_t)G * (capH + capT) + 1));
-    TRY(s->recvh.ensure((size_t)G * capH + 1));
+    TRY(s->sendbuf.ensure((size_t)G * (XHDR + capH + capT) + 1));
+    TRY(s->recvh.ensure((size_t)G * (XHDR + capH) + 1));
     TRY(s->recvt.ensure((size_t)G * capT + 1));
     TRY(h->comm_cnt.ensure(2 * G + 2));
     s->rcap = std::max<uint64_t>(s->rcap, (uint64_t)G * capH);    // (the route never overflows)
@@ -3003,7 +3088,7 @@ int run_batch_ranked(psim_handle* h, uint32_t nb, psim_round_stats* st_out, uint
         TRY(phase_consume(h, s, a));
         TRY(phase_partition(h, s, true));
         TRY(exchange_fixed(h));
-        TRY(phase_stats(h, s, j == 0 ? crashed0 : none));
+        TRY(phase_stats(h, s, j == 0 ? crashed0 : none, true));
         if (j == 0 && bc0)                  // the first round's origins are spent
             k_origin<<<grid_for(h->pend_b_root.size()), BLK, 0, s->stream>>>(
                 s->origin.p, s->lo, s->n, s->bc_roots.p, s->bc_msgs.p, (uint32_t)h->pend_b_root.size(), s->flags.p,
@@ -3050,7 +3135,7 @@ int run_batch_ranked(psim_handle* h, uint32_t nb, psim_round_stats* st_out, uint
         for (uint32_t g = 0; g < G; g++) {            // (the padded messages cross the links)
             if (g == s->idx && !self_comm) continue;
             h->x_records += p[PIN_XCNT + g] & 0xFFFFFFFFull;
-            h->x_bytes += (uint64_t)(capH + capT) * sizeof(Wire);
+            h->x_bytes += (uint64_t)(XHDR + capH + capT) * sizeof(Wire);
         }
     }
     if (done > 0) {                           // the first round's events are spent
