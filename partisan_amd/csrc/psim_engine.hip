@@ -782,6 +782,7 @@ __global__ void __launch_bounds__(RB_STEP) k_owner_part(RouteIn in, uint32_t nst
 // aborted round sends counts of 0 (its send buffer was not written).
 // (xw[3 + r] / xw[3 + 64 + r]: rank r's largest head / tail count, every
 // other rank's word 0: the all-reduce sum keeps each rank's own)
+constexpr uint32_t OO_THREADS = 1024;   // k_owner_offsets' block
 // A batched round (capH > 0) writes each owner's message header instead:
 // the counts, this rank's abort flag and largest counts, and the round's
 // stats summed from the count pass's tiles; and the round's span, its own
@@ -791,6 +792,7 @@ __global__ void k_owner_offsets(const uint32_t* hoff, uint32_t nblk, uint32_t G,
                                 uint32_t rank, Wire* sendbuf, StatsIn st) {
     __shared__ uint32_t smh, smt;
     __shared__ uint64_t ssum[64];
+    __shared__ uint64_t sred[OO_THREADS / 64][64];
     const uint32_t q = threadIdx.x;
     const bool dead = *ctl != 0;
     if (capH) {
@@ -801,10 +803,20 @@ __global__ void k_owner_offsets(const uint32_t* hoff, uint32_t nblk, uint32_t G,
             mt = max(mt, hoff[(G + o + 1) * nblk] - hoff[(G + o) * nblk]);
         }
         const bool over = !dead && (mh > capH || mt > capT);
-        if (q < NST) {
+        {                                             // the stats tiles' sums: 16 tiles a thread at most
+            const uint32_t c = q & 63, g = q >> 6, ng = OO_THREADS / 64;
             uint64_t v = 0;
-            for (uint32_t b = 0; b < st.nt; b++) v += st.tiles[(size_t)b * NST + q];
-            ssum[q] = v;
+            if (c < NST) {
+#pragma unroll 4
+                for (uint32_t b = g; b < st.nt; b += ng) v += st.tiles[(size_t)b * NST + c];
+            }
+            sred[g][c] = v;
+            __syncthreads();
+            if (g == 0) {
+                uint64_t u = 0;
+                for (uint32_t k = 0; k < ng; k++) u += sred[k][c];
+                ssum[c] = u;
+            }
         }
         __syncthreads();
         for (uint32_t o = 0; o < G; o++) {
@@ -2525,7 +2537,7 @@ int phase_partition(psim_handle* h, Shard* s, bool fixed = false) {
         TRY(scan_excl(s, s->hist.p, s->hoff.p, (uint32_t)nh));
         k_owner_part<true><<<nblk, RB_STEP, 0, s->stream>>>(in, nsteps, spb, G, h->per, nullptr, s->hoff.p,
                                                              s->sendbuf.p, nullptr, capH, capT, s->ctl.p, StatsIn{});
-        k_owner_offsets<<<1, 256, 0, s->stream>>>(s->hoff.p, nblk, G, s->d_off.p, rccl ? h->comm_cnt.p : nullptr,
+        k_owner_offsets<<<1, OO_THREADS, 0, s->stream>>>(s->hoff.p, nblk, G, s->d_off.p, rccl ? h->comm_cnt.p : nullptr,
                                                   rccl ? s->stat_out.p + STAT_OUT_X : nullptr, capH, capT, s->ctl.p,
                                                   (uint32_t)h->round, s->idx, s->sendbuf.p, st);
         HIP_TRY(hipGetLastError());
@@ -2703,20 +2715,28 @@ int exchange_fixed(psim_handle* h) {
     return route_group(h, s, true, (uint32_t)(G * xs), true);
 }
 
-// the fixed capacities of the next batch from a rank round's pinned slot p:
-// the largest per-owner head / tail count of any rank (every rank's own, in
-// the all-reduced stats), 1.25x and 1024 more, never below the current ones
-// -- the same on every rank
-void xcaps_update(psim_handle* h, Shard* s, const uint64_t* p) {
-    uint64_t mh = 0, mt = 0;
+// the fixed capacities of the next batch from the largest per-owner head /
+// tail counts of any rank over a batch's rounds (every rank's own, in the
+// headers or the all-reduced stats: the same on every rank): 1.5x and 1024
+// more -- raised at once, lowered only once the batch's largest count falls
+// below half the capacity (the padding crosses the links: a broadcast's peak
+// should not fix it for good)
+void xcaps_set(Shard* s, uint64_t mh, uint64_t mt) {
+    const uint64_t ch = std::min<uint64_t>(mh + mh / 2 + 1024, 0x7FFFFFFFull);
+    const uint64_t ct = std::min<uint64_t>(mt + mt / 2 + 1024, 0x7FFFFFFFull);
+    if (ch > s->xcap_h || 2 * mh < s->xcap_h) s->xcap_h = (uint32_t)ch;
+    if (ct > s->xcap_t || 2 * mt < s->xcap_t) s->xcap_t = (uint32_t)ct;
+}
+void xcaps_max(psim_handle* h, const uint64_t* p, uint64_t& mh, uint64_t& mt) {
     for (int r = 0; r < h->world && r < 64; r++) {
         mh = std::max<uint64_t>(mh, p[PIN_XRANK + r]);
         mt = std::max<uint64_t>(mt, p[PIN_XRANK + 64 + r]);
     }
-    const uint64_t ch = std::min<uint64_t>(mh + mh / 4 + 1024, 0x7FFFFFFFull);
-    const uint64_t ct = std::min<uint64_t>(mt + mt / 4 + 1024, 0x7FFFFFFFull);
-    s->xcap_h = std::max<uint32_t>(s->xcap_h, (uint32_t)ch);
-    s->xcap_t = std::max<uint32_t>(s->xcap_t, (uint32_t)ct);
+}
+void xcaps_update(psim_handle* h, Shard* s, const uint64_t* p) {
+    uint64_t mh = 0, mt = 0;
+    xcaps_max(h, p, mh, mt);
+    xcaps_set(s, mh, mt);
 }
 
 // the round's end after its route (which summed the stats: StatsIn)
@@ -3113,7 +3133,11 @@ int run_batch_ranked(psim_handle* h, uint32_t nb, psim_round_stats* st_out, uint
     if (done == nb && cw[0]) return PSIM_EDEVICE;     // (an abort no round reported)
     // the capacities grow with the largest counts the batch met -- the
     // stopped round's included, which is what the redo will need
-    for (uint32_t j = 0; j <= done && j < nb; j++) xcaps_update(h, s, s->pin + (size_t)(j + 1) * PIN_STRIDE);
+    {
+        uint64_t mh = 0, mt = 0;
+        for (uint32_t j = 0; j <= done && j < nb; j++) xcaps_max(h, s->pin + (size_t)(j + 1) * PIN_STRIDE, mh, mt);
+        xcaps_set(s, mh, mt);
+    }
     static const bool trace_batch = getenv("PSIM_TRACE_BATCH") != nullptr;
     if (trace_batch)
         std::fprintf(stderr, "psim: rank %d: batch of %u from round %llu: %u done%s; caps %u heads, %u tails\n",
