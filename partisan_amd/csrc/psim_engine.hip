@@ -26,6 +26,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -2721,9 +2722,12 @@ int exchange_fixed(psim_handle* h) {
 // more -- raised at once, lowered only once the batch's largest count falls
 // below half the capacity (the padding crosses the links: a broadcast's peak
 // should not fix it for good)
-void xcaps_set(Shard* s, uint64_t mh, uint64_t mt) {
-    const uint64_t ch = std::min<uint64_t>(mh + mh / 2 + 1024, 0x7FFFFFFFull);
-    const uint64_t ct = std::min<uint64_t>(mt + mt / 2 + 1024, 0x7FFFFFFFull);
+// (grow: a batch stopped on a count past its capacity -- the traffic is
+// climbing, a broadcast's wave: 2x headroom, so the next batch is likelier to
+// get through)
+void xcaps_set(Shard* s, uint64_t mh, uint64_t mt, bool grow = false) {
+    const uint64_t ch = std::min<uint64_t>(grow ? 2 * mh + 1024 : mh + mh / 2 + 1024, 0x7FFFFFFFull);
+    const uint64_t ct = std::min<uint64_t>(grow ? 2 * mt + 1024 : mt + mt / 2 + 1024, 0x7FFFFFFFull);
     if (ch > s->xcap_h || 2 * mh < s->xcap_h) s->xcap_h = (uint32_t)ch;
     if (ct > s->xcap_t || 2 * mt < s->xcap_t) s->xcap_t = (uint32_t)ct;
 }
@@ -2967,6 +2971,7 @@ int run_batch(psim_handle* h, uint32_t nb, psim_round_stats* st_out, uint32_t* d
     const bool bc0 = !h->pend_b_root.empty();
     s->tn = 0;
     s->desc_cap = std::min<uint64_t>(s->outbox.n, s->okey.n);
+    const auto t_enq = std::chrono::steady_clock::now();
     for (uint32_t j = 0; j < nb; j++) {
         s->stat_slot = j + 1;
         s->batch_round1 = (uint32_t)h->round + 1;
@@ -2986,7 +2991,13 @@ int run_batch(psim_handle* h, uint32_t nb, psim_round_stats* st_out, uint32_t* d
     s->stat_slot = 0; s->batch_round1 = 0; s->desc_cap = 0;
     uint32_t cw[2] = {0, 0};
     HIP_TRY(hipMemcpyAsync(cw, s->ctl.p, sizeof cw, hipMemcpyDeviceToHost, s->stream));
+    const auto t_wait = std::chrono::steady_clock::now();
     TRY(stream_wait(s));
+    static const bool trace_batch = getenv("PSIM_TRACE_BATCH") != nullptr;
+    if (trace_batch)
+        std::fprintf(stderr, "psim: batch of %u from round %llu: enqueue %.3f ms, wait %.3f ms\n", nb,
+                     (unsigned long long)r0, std::chrono::duration<double, std::milli>(t_wait - t_enq).count(),
+                     std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_wait).count());
     if (s->pin[PIN_BIGIN]) {                          // a node's inbox count must fit 27 bits
         s->pin[PIN_BIGIN] = 0;
         HIP_TRY(hipMemsetAsync(s->ctl.p, 0, sizeof cw, s->stream));
@@ -3099,16 +3110,29 @@ int run_batch_ranked(psim_handle* h, uint32_t nb, psim_round_stats* st_out, uint
     const bool bc0 = !h->pend_b_root.empty();
     s->tn = 0;
     s->desc_cap = std::min<uint64_t>(s->outbox.n, s->okey.n);
+    const auto t_enq = std::chrono::steady_clock::now();
+    double tph[5] = {0, 0, 0, 0, 0};                  // (PSIM_TRACE_BATCH: host ms per phase)
+    auto tick = [](std::chrono::steady_clock::time_point& t0, double& acc) {
+        const auto t1 = std::chrono::steady_clock::now();
+        acc += std::chrono::duration<double, std::milli>(t1 - t0).count();
+        t0 = t1;
+    };
     for (uint32_t j = 0; j < nb; j++) {
         s->stat_slot = j + 1;
         s->batch_round1 = (uint32_t)h->round + 1;
         RoundArgs a;
         const RoundCtl ctl = j == 0 ? ctl0 : RoundCtl{};
+        auto t0 = std::chrono::steady_clock::now();
         TRY(phase_events_prepare(h, s, ctl, a, j == 0, true));
+        tick(t0, tph[0]);
         TRY(phase_consume(h, s, a));
+        tick(t0, tph[1]);
         TRY(phase_partition(h, s, true));
+        tick(t0, tph[2]);
         TRY(exchange_fixed(h));
+        tick(t0, tph[3]);
         TRY(phase_stats(h, s, j == 0 ? crashed0 : none, true));
+        tick(t0, tph[4]);
         if (j == 0 && bc0)                  // the first round's origins are spent
             k_origin<<<grid_for(h->pend_b_root.size()), BLK, 0, s->stream>>>(
                 s->origin.p, s->lo, s->n, s->bc_roots.p, s->bc_msgs.p, (uint32_t)h->pend_b_root.size(), s->flags.p,
@@ -3119,7 +3143,9 @@ int run_batch_ranked(psim_handle* h, uint32_t nb, psim_round_stats* st_out, uint
     s->stat_slot = 0; s->batch_round1 = 0; s->desc_cap = 0;
     uint32_t cw[2] = {0, 0};
     HIP_TRY(hipMemcpyAsync(cw, s->ctl.p, sizeof cw, hipMemcpyDeviceToHost, s->stream));
+    const auto t_wait = std::chrono::steady_clock::now();
     TRY(stream_wait(s));
+    const auto t_end = std::chrono::steady_clock::now();
     if (s->pin[PIN_BIGIN]) {                          // a node's inbox count must fit 27 bits
         s->pin[PIN_BIGIN] = 0;
         HIP_TRY(hipMemsetAsync(s->ctl.p, 0, sizeof cw, s->stream));
@@ -3136,13 +3162,16 @@ int run_batch_ranked(psim_handle* h, uint32_t nb, psim_round_stats* st_out, uint
     {
         uint64_t mh = 0, mt = 0;
         for (uint32_t j = 0; j <= done && j < nb; j++) xcaps_max(h, s->pin + (size_t)(j + 1) * PIN_STRIDE, mh, mt);
-        xcaps_set(s, mh, mt);
+        xcaps_set(s, mh, mt, done < nb);
     }
     static const bool trace_batch = getenv("PSIM_TRACE_BATCH") != nullptr;
     if (trace_batch)
-        std::fprintf(stderr, "psim: rank %d: batch of %u from round %llu: %u done%s; caps %u heads, %u tails\n",
+        std::fprintf(stderr, "psim: rank %d: batch of %u from round %llu: %u done%s; caps %u heads, %u tails; "
+                     "enqueue %.3f ms (prepare %.3f, node phase %.3f, partition %.3f, exchange + route %.3f, end "
+                     "%.3f), wait %.3f ms\n",
                      h->rank, nb, (unsigned long long)r0, done, done < nb ? " (one redone exactly)" : "", s->xcap_h,
-                     s->xcap_t);
+                     s->xcap_t, std::chrono::duration<double, std::milli>(t_wait - t_enq).count(), tph[0], tph[1],
+                     tph[2], tph[3], tph[4], std::chrono::duration<double, std::milli>(t_end - t_wait).count());
     const bool self_comm = h->world == 1;
     for (uint32_t j = 0; j < done; j++) {
         const uint64_t* p = s->pin + (size_t)(j + 1) * PIN_STRIDE;
@@ -3177,8 +3206,10 @@ int run_batch_ranked(psim_handle* h, uint32_t nb, psim_round_stats* st_out, uint
         return PSIM_OK;
     }
     // round r0 + done stopped the batch on some rank: every rank redoes it
-    // exactly (a rank whose own outbox was short from its node phase)
-    s->xbatch = 1;
+    // exactly (a rank whose own outbox was short from its node phase); the
+    // next batch is a quarter as long (its dead tail, every round's padded
+    // messages, is what a stop costs)
+    s->xbatch = std::max<uint32_t>(2, s->xbatch / 4);
     HIP_TRY(hipMemsetAsync(s->ctl.p, 0, sizeof cw, s->stream));
     h->round = r0 + done;
     const bool short_outbox = cw[0] == 1 && cw[1] == (uint32_t)h->round;
