@@ -2725,11 +2725,12 @@ int exchange_fixed(psim_handle* h) {
 // (grow: a batch stopped on a count past its capacity -- the traffic is
 // climbing, a broadcast's wave: 2x headroom, so the next batch is likelier to
 // get through)
-void xcaps_set(Shard* s, uint64_t mh, uint64_t mt, bool grow = false) {
+// (shrink = false: one exact round's counts only raise them)
+void xcaps_set(Shard* s, uint64_t mh, uint64_t mt, bool grow = false, bool shrink = true) {
     const uint64_t ch = std::min<uint64_t>(grow ? 2 * mh + 1024 : mh + mh / 2 + 1024, 0x7FFFFFFFull);
     const uint64_t ct = std::min<uint64_t>(grow ? 2 * mt + 1024 : mt + mt / 2 + 1024, 0x7FFFFFFFull);
-    if (ch > s->xcap_h || 2 * mh < s->xcap_h) s->xcap_h = (uint32_t)ch;
-    if (ct > s->xcap_t || 2 * mt < s->xcap_t) s->xcap_t = (uint32_t)ct;
+    if (ch > s->xcap_h || (shrink && 2 * mh < s->xcap_h)) s->xcap_h = (uint32_t)ch;
+    if (ct > s->xcap_t || (shrink && 2 * mt < s->xcap_t)) s->xcap_t = (uint32_t)ct;
 }
 void xcaps_max(psim_handle* h, const uint64_t* p, uint64_t& mh, uint64_t& mt) {
     for (int r = 0; r < h->world && r < 64; r++) {
@@ -2740,7 +2741,7 @@ void xcaps_max(psim_handle* h, const uint64_t* p, uint64_t& mh, uint64_t& mt) {
 void xcaps_update(psim_handle* h, Shard* s, const uint64_t* p) {
     uint64_t mh = 0, mt = 0;
     xcaps_max(h, p, mh, mt);
-    xcaps_set(s, mh, mt);
+    xcaps_set(s, mh, mt, false, false);
 }
 
 // the round's end after its route (which summed the stats: StatsIn)
