@@ -44,6 +44,8 @@ static ERL_NIF_TERM busy(ErlNifEnv *env) {
 
 /* normal-scheduler NIFs: take the handle's mutex only if it is free */
 #define LOCK_OR_BUSY(r) do { if (enif_mutex_trylock((r)->mu) != 0) return busy(env); } while (0)
+/* the same, releasing an enif_alloc'ed buffer on the busy path */
+#define LOCK_OR_BUSY_FREE(r, p) do { if (enif_mutex_trylock((r)->mu) != 0) { enif_free(p); return busy(env); } } while (0)
 
 static int get_u32(ErlNifEnv *env, ERL_NIF_TERM map, const char *k, uint32_t *out) {
     ERL_NIF_TERM v;
@@ -394,9 +396,15 @@ static ERL_NIF_TERM nif_set_phash_table(ErlNifEnv *env, int argc, const ERL_NIF_
     if (!enif_get_resource(env, argv[0], SIM_RT, (void **)&r) || !enif_inspect_binary(env, argv[1], &b) ||
         b.size != (size_t)r->n_nodes * 4)
         return enif_make_badarg(env);
-    LOCK_OR_BUSY(r);
-    int rc = psim_set_phash_table(r->h, (const uint32_t *)b.data, r->n_nodes);
+    /* (binary data -- a sub-binary's above all -- need not be 4-byte
+     * aligned: the hashes are copied into an aligned buffer first) */
+    uint32_t *ph = enif_alloc(b.size ? b.size : 4);
+    if (!ph) return enif_make_badarg(env);
+    memcpy(ph, b.data, b.size);
+    LOCK_OR_BUSY_FREE(r, ph);
+    int rc = psim_set_phash_table(r->h, ph, r->n_nodes);
     enif_mutex_unlock(r->mu);
+    enif_free(ph);
     return rc ? err(env, rc) : enif_make_atom(env, "ok");
 }
 
