@@ -2428,7 +2428,10 @@ int route_group(psim_handle* h, Shard* s, bool dense, uint32_t m, bool fixed = f
                      s->stat_tile.p, s->stat_out.p, s->pin_dev + (size_t)s->stat_slot * PIN_STRIDE,
                      s->outx.p ? s->outx_top.p : nullptr, s->pin_dev};
     KTimer t(h, s, KT_SORT);
-    if (!dense && !exact && h->route_fused) {
+    // (above 2^24 nodes the four passes: the fused route's fixed bucket
+    // regions hold 1.5x the route's pairs, ~3 GB more at 2^26 nodes, where
+    // the device is full -- E at 2^26 took 300 GB, profiles/r06/pass1)
+    if (!dense && !exact && h->route_fused && n <= (1u << 24)) {
         // a bucket's fixed region holds 1.5x its share of the route's
         // capacity: only a hot spot (a join storm) overflows one, and that
         // round goes through the four passes again (run_round, run_batch)
@@ -3727,7 +3730,7 @@ int psim_broadcast(psim_handle* h, uint32_t root, uint32_t msg_id) {
 // growth is reported once and leaves the pool as it is (a table that then
 // finds no row counts a PSIM_OVF_PT_OUT overflow; cfg.strict fails the step).
 int grow_outx(Shard* s) {
-    if (!s->outx.p) return PSIM_OK;
+    if (!s->outx.p || s->outx_short) return PSIM_OK;   // (a growth that failed is not retried every round)
     const uint64_t rows = s->outx.n / OUT_EXT, used = std::min<uint64_t>(s->pin[PIN_OUTX], rows);
     if (rows >= s->n || used * 2 < rows) return PSIM_OK;
     const uint64_t want = std::min<uint64_t>(std::max<uint64_t>(2 * rows, used + 1024), s->n);
