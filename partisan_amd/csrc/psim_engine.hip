@@ -582,22 +582,40 @@ __global__ void __launch_bounds__(RB_STEP) k_bucket_scatter(RouteIn in, uint32_t
 // every run by source index.  A bucket past capb (a join storm on a few
 // destinations) stops the fused route: k_bucket_route returns, the round's
 // records are routed again by the four-pass route (flag in ctl[2]).
+#ifndef PSIM_FILL_REG
+#define PSIM_FILL_REG 8
+#endif
+constexpr uint32_t FILL_REG = PSIM_FILL_REG;   // k_bucket_fill: records a thread keeps between its passes
 template <bool DENSE>
 __global__ void __launch_bounds__(RB_STEP) k_bucket_fill(RouteIn in, uint32_t nsteps, uint32_t nb, uint32_t wshift,
                                                          uint32_t* gcnt, uint32_t capb, uint2* pairs, uint32_t* ctl,
-                                                         unsigned long long* mark, StatsIn st) {
+                                                         unsigned long long* mark, StatsIn st, uint32_t walk) {
     if (*ctl) return;                                 // an aborted batch (run_batch)
     if (mark && blockIdx.x == 0 && threadIdx.x == 0) *mark = __builtin_amdgcn_s_memrealtime();   // (phase end)
     extern __shared__ uint32_t hcnt[];                // nb bucket counters, then this block's bases
     __shared__ uint32_t spre[RB_WAVES][65];
     __shared__ uint64_t sbase[RB_WAVES][64];
+    __shared__ uint32_t s_spill;
     if (blockIdx.x < st.nt) stats_tile(st, blockIdx.x, sbase);   // (uniform)
     for (uint32_t j = threadIdx.x; j < nb; j += blockDim.x) hcnt[j] = 0;
+    if (threadIdx.x == 0) s_spill = walk;             // (walk: the second pass walks the runs, A/B)
     __syncthreads();
+    // the first FILL_REG records a thread meets are kept in registers
+    // (destination | class << 27, source index), so the scatter below need not
+    // walk the outbox runs a second time; a block where some thread met more
+    // walks them again
+    uint32_t rk[FILL_REG], rg[FILL_REG], nr = 0;
     for (uint32_t step = blockIdx.x; step < nsteps; step += gridDim.x)
-        route_step<DENSE>(in, step, spre, sbase,
-                          [&](uint32_t, uint32_t d, uint32_t) { atomicAdd(&hcnt[d >> wshift], 1u); });
+        route_step<DENSE>(in, step, spre, sbase, [&](uint32_t g, uint32_t d, uint32_t cls) {
+            atomicAdd(&hcnt[d >> wshift], 1u);
+#pragma unroll
+            for (uint32_t k = 0; k < FILL_REG; k++)
+                if (k == nr) { rk[k] = d | (cls << KEY_DST_BITS); rg[k] = g; }
+            nr++;
+        });
+    if (nr > FILL_REG) s_spill = 1;
     __syncthreads();
+    const bool spill = s_spill != 0;                  // (uniform)
     bool over = false;
     for (uint32_t j = threadIdx.x; j < nb; j += blockDim.x) {
         const uint32_t c = hcnt[j];
@@ -608,11 +626,17 @@ __global__ void __launch_bounds__(RB_STEP) k_bucket_fill(RouteIn in, uint32_t ns
     if (over) ctl[2] = 1;                             // (read by k_bucket_route, a later launch)
     __syncthreads();
     const uint32_t wmask = (1u << wshift) - 1;
-    for (uint32_t step = blockIdx.x; step < nsteps; step += gridDim.x)
-        route_step<DENSE>(in, step, spre, sbase, [&](uint32_t g, uint32_t d, uint32_t cls) {
-            const uint32_t j = d >> wshift, q = atomicAdd(&hcnt[j], 1u);
-            if (q < (j + 1) * capb) pairs[q] = make_uint2((d & wmask) | (cls << 16), g);
-        });
+    auto put = [&](uint32_t g, uint32_t d, uint32_t cls) {
+        const uint32_t j = d >> wshift, q = atomicAdd(&hcnt[j], 1u);
+        if (q < (j + 1) * capb) pairs[q] = make_uint2((d & wmask) | (cls << 16), g);
+    };
+    if (!spill) {
+#pragma unroll
+        for (uint32_t k = 0; k < FILL_REG; k++)
+            if (k < nr) put(rg[k], rk[k] & KEY_DST_MASK, rk[k] >> KEY_DST_BITS);
+    } else {
+        for (uint32_t step = blockIdx.x; step < nsteps; step += gridDim.x) route_step<DENSE>(in, step, spre, sbase, put);
+    }
 }
 
 // G > 1, sender side: this shard's outbox runs stably partitioned by owner
@@ -2443,8 +2467,9 @@ int route_group(psim_handle* h, Shard* s, bool dense, uint32_t m, bool fixed = f
         }
         TRY(s->pairs.ensure((size_t)nb * capb));
         TRY(s->rank.ensure((size_t)nb * capb));
+        static const uint32_t walk = getenv("PSIM_FILL_WALK") && atoi(getenv("PSIM_FILL_WALK")) ? 1u : 0u;
         k_bucket_fill<false><<<nblk, RB_STEP, lds_h, s->stream>>>(in, nsteps, nb, wshift, s->gcnt.p, capb, s->pairs.p,
-                                                                  s->ctl.p, phase_end_mark(h, s), st);
+                                                                  s->ctl.p, phase_end_mark(h, s), st, walk);
         k_bucket_route<false><<<nb, RR_THREADS, lds_r, s->stream>>>(
             n, wshift, h->rr_reg, nullptr, s->pairs.p, in.rec, nullptr, nullptr, s->rank.p, s->cb.p, s->bmask.p,
             s->in_beg.p, s->ivals.p, s->tmp.p, s->inbox.p, s->pin_dev + PIN_M, s->rcap, s->ctl.p, s->gcnt.p, capb,
