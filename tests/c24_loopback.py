@@ -19,6 +19,11 @@ at 2^24 is ~28).
 
 Run directly (prints progress) or from tests/test_gpu_c24.py.  Exit 0 = equal."""
 import hashlib
+
+try:
+    import xxhash                    # (20 GB of node rows: a fast hash; sha1 took ~1 minute)
+except ImportError:
+    xxhash = None
 import os
 import sys
 import time
@@ -67,7 +72,7 @@ def row_hashes(sim, chunk=1 << 18):
     out = []
     for lo in range(0, N, chunk):
         v = sim.nodes(lo, min(chunk, N - lo))
-        out.append(hashlib.sha1(v.tobytes()).hexdigest())
+        out.append(xxhash.xxh3_128_hexdigest(v.tobytes()) if xxhash else hashlib.sha1(v.tobytes()).hexdigest())
     return out
 
 

@@ -11,6 +11,11 @@ node 5 rounds later), a half/half partition for 8 rounds, 8 more rounds.
 
 Run directly (prints progress) or from tests/test_gpu_d24.py.  Exit 0 = equal."""
 import hashlib
+
+try:
+    import xxhash                    # (20 GB of node rows: a fast hash; sha1 took ~1 minute)
+except ImportError:
+    xxhash = None
 import os
 import sys
 import time
@@ -68,7 +73,7 @@ def row_hashes(sim, chunk=1 << 18):
     out = []
     for lo in range(0, N, chunk):
         v = sim.strategy_nodes(lo, min(chunk, N - lo))
-        out.append(hashlib.sha1(v.tobytes()).hexdigest())
+        out.append(xxhash.xxh3_128_hexdigest(v.tobytes()) if xxhash else hashlib.sha1(v.tobytes()).hexdigest())
     return out
 
 
