@@ -45,8 +45,9 @@ CHECK_NODES = 1 << 14           # the built-in sharding check
 CHECK_ROUNDS = 90
 SCHEDULE_VERSION = 4            # bumps when the event schedule of a run changes (PMC keys)
 OVF_KINDS = ("idmap", "pt_outstanding", "pt_sets_roots_msgs", "strategy", "conn")   # PSIM_OVF_*
-ALG_FORMULA = ("B = N_proc * 2 * 416 + M_in * 64 + M_out * 68 per round, N_proc = nodes with work "
-               "(stats nodes_processed), M_in / M_out = delivered / emitted records.  Departs from "
+ALG_FORMULA = ("B = N_run * 2 * 416 + M_in * 64 + M_out * 68 per round, N_run = nodes the phase kernels "
+               "run (stats state_bytes / 832; nodes_processed less the quiet lazy ticks k_node_prep counts "
+               "without running the node), M_in / M_out = delivered / emitted records.  Departs from "
                "SURVEY 8(d) (every node's 416 B read, touched nodes' written, 32-B Plumtree records): "
                "idle nodes are not read by the kernels and are not counted; every record is the "
                "64-B record the engine moves, plus its 4-B route key")
@@ -712,7 +713,9 @@ def main():
     # roofline of the dominant kernel (the node-round phase): algorithmic
     # bytes per launch of this rank (global counters / world: equal ranges)
     per = world
-    proc = int(st["nodes_processed"].sum()) / per
+    # (state_bytes: the rows of the nodes the kernels ran, 2 * S_NODE each --
+    # nodes_processed also counts the quiet lazy ticks k_node_prep settles)
+    proc = int(st["state_bytes"].sum()) / (2 * S_NODE) / per
     deliv = int(st["delivered"].sum()) / per
     alg_bytes = proc * 2 * S_NODE + deliv * S_MSG + msgs / per * (S_MSG + 4)
     c_ms, c_n = kt.get("consume", (0.0, 0))
@@ -780,8 +783,10 @@ def main():
         # each node-round kernel's share of the algorithmic bytes (the formula
         # above, with the kernel's own counts: its nodes processed, records
         # delivered and emitted), per round
+        # (k_node_prep's entry: quiet lazy ticks, counted without reading
+        # the node -- no bytes)
         out["per_kernel_alg"] = {k: (v[0] * 2 * S_NODE + v[1] * S_MSG + v[2] * (S_MSG + 4)) / args.steps
-                                 for k, v in kc.items()}
+                                 for k, v in kc.items() if k != "k_node_prep"}
         out["per_kernel_counts"] = {k: [x / args.steps for x in v] for k, v in kc.items()}
     if world > 1 or args.vshards > 1 or args.rank_path:
         # the cross-shard exchange over the window, this rank's shards: records

@@ -511,7 +511,10 @@ int psim_wire_decode(const uint8_t *buf, size_t len, const psim_wire_names *name
  * k_lite_half, k_consume, k_ptl, k_pt; this process's first shard), 4 words
  * each: nodes processed, records delivered, records emitted, 0 -- the
  * kernel's share of the algorithmic bytes (bench.py --kernel-counts,
- * profiles/pmc_record.py).  Returns 6 (0 under the pluggable manager). */
+ * profiles/pmc_record.py).  With cap >= 28 a seventh entry, k_node_prep:
+ * the quiet lazy ticks it counted without running their nodes (processed,
+ * 0, 0, 0).  Returns 6 or 7 (0 under the pluggable
+ * manager). */
 int psim_debug_kernel_counts(psim_handle *h, uint64_t *out, int cap);
 
 /* Per-kernel device time (ms) accumulated over the last psim_step call:

@@ -115,6 +115,7 @@ struct Wv {
     uint32_t fl;         // flag byte at node start (writeback)
     uint32_t KM;         // magic_lanes(): the exact-modulo multipliers
     bool work;           // the node had work this round
+    bool lazy_quiet;     // its lazy tick ran and found no outstanding peer connected (flag_byte)
 };
 constexpr uint64_t NONE64 = ~0ull;
 constexpr uint32_t STAGE = 16;
@@ -1436,6 +1437,7 @@ DEV void begin_node(Wv& w, const NodeIn& x, const NodeX& y) {
     w.nlog_n = 0;
     w.dc_base = NONE64;                                // the cache holds another node's stream
     w.work = false;
+    w.lazy_quiet = false;
 }
 
 // The node's HyParView handlers in the order of round model R0, then the
@@ -1618,7 +1620,8 @@ DEV void out_ext(Wv& w) {
 }
 
 DEV uint8_t flag_byte(const Wv& w) {
-    return (uint8_t)((w.fl & (F_UP | F_CRASHED)) | (w.out_n ? F_LAZY : 0) | (min(w.out_n, 15u) << F_OUTN_SHIFT) |
+    return (uint8_t)((w.fl & (F_UP | F_CRASHED)) | (w.out_n && !w.lazy_quiet ? F_LAZY : 0) |
+                     (min(w.out_n, 15u) << F_OUTN_SHIFT) |
                      (w.act_n < kargs().min_active ? F_LOWACT : 0));
 }
 
@@ -1979,12 +1982,13 @@ DEV void begin_pt(Wv& w, const PtIn& x, const PtX& y) {
     w.CN = l < w.conn_n ? x.CN : 0u;
     load_pt_regs(w, y.PA, y.PG, y.PL, y.PO);
     w.pt_dirty = false;
+    w.lazy_quiet = false;
     w.seq = x.oc; w.flushed = x.oc;                  // after the HyParView phase's records
 }
 
 // the lazy tick's IHAVEs for the outstanding table's tail (entries
-// OUT_HEAD.., after the register's: the table's order)
-DEV void lazy_tick_tail(Wv& w) {
+// OUT_HEAD.., after the register's: the table's order); the entries sent
+DEV uint64_t lazy_tick_tail(Wv& w) {
     const uint32_t l = lane_id();
     const uint64_t T = load_out_tail(w);
     const uint32_t peer = (uint32_t)(T >> 32), msg = ((uint32_t)T >> 16) & 0xFFFFu;
@@ -1996,6 +2000,7 @@ DEV void lazy_tick_tail(Wv& w) {
     st_add(w, ST_OVF, dead);
     st_add(w, ST_OVF_BY + PSIM_OVF_PT, dead);
     emit_batch<true>(w, ok, PSIM_MSG_PT_IHAVE, peer & ~PSIM_MAP_BIT, msg, (uint32_t)T & 0xFFFFu, root);
+    return ok;
 }
 
 DEV void body_pt(Wv& w, const PtIn& x) {
@@ -2038,7 +2043,11 @@ DEV void body_pt(Wv& w, const PtIn& x) {
         st_add(w, ST_OVF, dead);
         st_add(w, ST_OVF_BY + PSIM_OVF_PT, dead);
         emit_batch<true>(w, ok, PSIM_MSG_PT_IHAVE, peer & ~PSIM_MAP_BIT, msg, (uint32_t)w.OUT & 0xFFFFu, root);
-        if (w.out_n > OUT_HEAD) lazy_tick_tail(w);
+        const uint64_t ok_tail = w.out_n > OUT_HEAD ? lazy_tick_tail(w) : 0ull;
+        // no entry's peer connected: the tick is the round's last handler, so
+        // until a handler or a partition change connects one, every later
+        // tick fails the same way (k_node_prep counts it without a wave)
+        w.lazy_quiet = (ok | ok_tail) == 0;
         STAMP(w, 22);
     }
 }
@@ -3180,7 +3189,9 @@ __global__ void PTL_BOUNDS k_ptl(RoundArgs) {
             }
         }
         PTL_STAMP(11);
+        bool quiet = false;                              // (flag_byte's lazy_quiet)
         if (((D.z >> 28) & DESC_LAZY) && n.on > 0) {   // the lazy tick (pt:341-345, :443-453)
+            const uint32_t seq0 = seq;
 #if PSIM_PTL_PF
             uint64_t o_nx = out_at(n, 0);
 #endif
@@ -3201,6 +3212,7 @@ __global__ void PTL_BOUNDS k_ptl(RoundArgs) {
                 seq++;
                 v[T_EMT + 2]++;
             }
+            quiet = seq == seq0;
         }
         PTL_STAMP(12);
         // write back: header words 5-8 and 11, the sets, the table, the flag byte
@@ -3235,7 +3247,8 @@ __global__ void PTL_BOUNDS k_ptl(RoundArgs) {
         }
         a.ocnt[li] = seq;
         v[T_BOUND] += seq > oend - D.w ? 1u : 0u;
-        a.flags[id] = (uint8_t)((fl0 & (F_UP | F_CRASHED)) | (n.on ? F_LAZY : 0) | (min(n.on, 15u) << F_OUTN_SHIFT) |
+        a.flags[id] = (uint8_t)((fl0 & (F_UP | F_CRASHED)) | (n.on && !quiet ? F_LAZY : 0) |
+                                (min(n.on, 15u) << F_OUTN_SHIFT) |
                                 (act_n < a.min_active ? F_LOWACT : 0));
         PTL_STAMP(13);
         }

@@ -43,10 +43,13 @@ struct __attribute__((aligned(16))) Msg {
 static_assert(sizeof(Msg) == 64, "Msg must be 64 B");
 
 // node flag byte
-// F_LAZY: outstanding lazy pushes; F_LOWACT: |active| < min_active_size (a due
-// promotion timer can act)
+// F_LAZY: outstanding lazy pushes that a lazy tick may send -- clear with
+// entries outstanding ("quiet") when the node's last lazy tick found none of
+// their peers connected (k_node_prep then counts the next ticks without
+// running the node, until a handler or a partition change can connect one);
+// F_LOWACT: |active| < min_active_size (a due promotion timer can act)
 // high nibble: the node's outstanding lazy pushes after its last round,
-// saturating at 15 (the next round's lazy-tick bound, k_node_prep)
+// saturating at 15 (the next round's lazy-tick bound, k_node_prep; 0 = none)
 enum : uint8_t { F_UP = 1, F_CRASHED = 2, F_LAZY = 4, F_LOWACT = 8 };
 constexpr uint32_t F_OUTN_SHIFT = 4;
 

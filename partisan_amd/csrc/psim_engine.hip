@@ -1164,9 +1164,23 @@ __global__ void __launch_bounds__(RR_THREADS) k_bucket_route(
     }
 }
 
+constexpr uint64_t NODE_STATE_BYTES = 416;   // HyParView 304 + Plumtree 112 per node
+
 __device__ __forceinline__ bool due(uint32_t period, uint32_t r, uint32_t start) {
     return period > 0 && r > start && ((r - start) % period) == 0;
 }
+
+#ifdef PSIM_BOUND_TERMS
+// diagnostic build (make evariant V=bterms X=-DPSIM_BOUND_TERMS): the outbox
+// bound's terms summed over the nodes of every round since psim_step last
+// printed them (PSIM_TRACE_BOUND)
+enum { BT_RESP, BT_TIMER, BT_PUSH, BT_PUSH_NE, BT_NPUSH, BT_LAZY, BT_ON, BT_NL, BT_LC, BT_CRASH, BT_XBOT,
+       BT_BUMP, BT_TOTAL, BT_C, BT_QUIET, BT_ROUNDS, BT_N };
+__device__ unsigned long long g_bterm[BT_N];
+#define BTERM(k, v) (bt[k] += (v))
+#else
+#define BTERM(k, v) ((void)0)
+#endif
 
 // Per local node: the upper bound of its emissions this round (sizes its
 // outbox region) and whether it has any work (inbox, join, timers, EXIT
@@ -1180,8 +1194,8 @@ __global__ void __launch_bounds__(BLK) k_node_prep(RoundArgs a, const unsigned l
     // round's route (k_bucket_fill)
     for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < ngcnt; j += gridDim.x * blockDim.x) gcnt[j] = 0;
     if (gcnt && blockIdx.x == 0 && threadIdx.x == 0) const_cast<uint32_t*>(a.ctl)[2] = 0;
-    __shared__ unsigned long long s_up, s_drop, s_b, s_w;
-    if (threadIdx.x == 0) { s_up = 0; s_drop = 0; s_b = 0; s_w = 0; }
+    __shared__ unsigned long long s_up, s_drop, s_b, s_w, s_qp, s_qf;
+    if (threadIdx.x == 0) { s_up = 0; s_drop = 0; s_b = 0; s_w = 0; s_qp = 0; s_qf = 0; }
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         a.ktime[0] = ~0ull; a.ktime[1] = 0; *a.n_slow = 0; *a.n_pt = 0;
         if (a.n_shuf) *a.n_shuf = 0;
@@ -1196,6 +1210,10 @@ __global__ void __launch_bounds__(BLK) k_node_prep(RoundArgs a, const unsigned l
         for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g < a.n_nodes; g += gridDim.x * blockDim.x)
             a.upart[g] = (a.flags[g] & F_UP) ? (upart_t)a.part[g] : UPART_DOWN;
     unsigned long long up = 0, drop = 0, bs = 0, ws = 0;   // this thread's sums (wave-summed below)
+    unsigned long long qp = 0, qf = 0;                     // quiet lazy ticks: nodes, failed sends
+#ifdef PSIM_BOUND_TERMS
+    unsigned long long bt[BT_N] = {};
+#endif
     // block b takes the nodes [b * per, (b + 1) * per), blockDim at a time
     // (coalesced), so that its sums are a contiguous tile of the scan below
     const uint32_t i0 = blockIdx.x * per, i1 = min(a.n_local, i0 + per);
@@ -1262,6 +1280,8 @@ __global__ void __launch_bounds__(BLK) k_node_prep(RoundArgs a, const unsigned l
                 const bool promo = a.random_promotion && due(a.promotion_period, r, st);
                 b = (cbi >> 32) + (st == r && x.join_contact != PSIM_NONE ? 1u : 0u) + (promo ? 1u : 0u) +
                     (due(a.shuffle_period, r, st) ? 1u : 0u);
+                BTERM(BT_RESP, cbi >> 32);
+                BTERM(BT_TIMER, b - (cbi >> 32));
                 // per BROADCAST message slot a first delivery's eager push
                 // and lazy adds (plus the origin's): at most the root's sets
                 // at round start -- or the common eagers of a new root or of a
@@ -1286,6 +1306,11 @@ __global__ void __launch_bounds__(BLK) k_node_prep(RoundArgs a, const unsigned l
                             }
                         b += min(2u * PSIM_ACTIVE_CAP, ne + c);
                         lazy_add += nl + c;
+                        BTERM(BT_PUSH, min(2u * PSIM_ACTIVE_CAP, ne + c));
+                        BTERM(BT_PUSH_NE, min(2u * PSIM_ACTIVE_CAP, ne));
+                        BTERM(BT_NPUSH, 1);
+                        BTERM(BT_NL, nl);
+                        BTERM(BT_LC, c);
                     };
                     for (unsigned long long m = bm; m; m &= m - 1) push(a.slots[PSIM_MSG_SLOTS + __ffsll(m) - 1]);
                     if (origin) push((a.lo + i) | PSIM_MAP_BIT);
@@ -1299,7 +1324,10 @@ __global__ void __launch_bounds__(BLK) k_node_prep(RoundArgs a, const unsigned l
                     const uint32_t fo = (uint32_t)f >> F_OUTN_SHIFT;
                     const uint32_t on = fo < 15 ? fo : (uint32_t)x.out_n;
                     b += min((uint32_t)PSIM_PT_OUT_CAP, on + lazy_add);
+                    BTERM(BT_LAZY, min((uint32_t)PSIM_PT_OUT_CAP, on + lazy_add));
+                    BTERM(BT_ON, on);
                 }
+                if (pushes) BTERM(BT_C, c);
                 // a crash round: a NEIGHBOR_REQUEST per crashed active member
                 // (bounded over every crashed member); EXIT work for a
                 // crashed member held over a connection -- an active member
@@ -1322,6 +1350,7 @@ __global__ void __launch_bounds__(BLK) k_node_prep(RoundArgs a, const unsigned l
                         if ((uint32_t)k < x.act_n && av[k] < a.n_nodes && av[k] != a.lo + i &&
                             crashed_now(a, av[k])) {
                             b++;
+                            BTERM(BT_CRASH, 1);
                             bool down = false;
 #pragma unroll
                             for (int j = 0; j < PSIM_CONN_CAP; j++) down |= (uint32_t)j < cn && cv[j] == (av[k] | PSIM_CONN_DOWN);
@@ -1331,7 +1360,15 @@ __global__ void __launch_bounds__(BLK) k_node_prep(RoundArgs a, const unsigned l
                     for (int j = 0; j < PSIM_CONN_CAP; j++)
                         exits |= (uint32_t)j < cn && !(cv[j] & PSIM_CONN_DOWN) && crashed_now(a, cv[j] & KEY_DST_MASK);
                 }
-                w = c > 0 || st == r || exits || (f & F_LAZY) || origin ||
+                // a quiet node (entries outstanding, F_LAZY clear: its last
+                // tick reached no peer) runs only for other work: its tick
+                // fails every entry again (pt:443-453 over send/3), counted
+                // here -- the node processed, a failed send per entry.  Only
+                // with a tick every round (else a round without one could
+                // connect a peer unseen) and no waking event
+                const uint32_t fon = (uint32_t)f >> F_OUTN_SHIFT;
+                const bool quiet_ok = a.lazy_tick_period == 1 && !a.lazy_wake && !(f & F_LAZY);
+                w = c > 0 || st == r || exits || (fon && !quiet_ok) || origin ||
                     (a.random_promotion && (f & F_LOWACT) && due(a.promotion_period, r, st)) ||
                     due(a.shuffle_period, r, st);
                 if (a.xbot) {
@@ -1341,11 +1378,18 @@ __global__ void __launch_bounds__(BLK) k_node_prep(RoundArgs a, const unsigned l
                     const bool xb = due(a.xbot_period, r, st);
                     const uint32_t cl = x.conn_cl;
                     b += (xb ? 2u : 0u) + cl;
+                    BTERM(BT_XBOT, (xb ? 2u : 0u) + cl);
                     w = w || xb || cl;
                 }
                 // a working node's first slot is reserved: a wave that emits
                 // nothing rewrites it (flush_recs' fixed store)
-                if (w && b == 0) b = 1;
+                if (w && b == 0) { b = 1; BTERM(BT_BUMP, 1); }
+                if (!w && fon && lazy) {
+                    qp++;
+                    qf += fon < 15 ? fon : (uint32_t)x.out_n;
+                    BTERM(BT_QUIET, 1);
+                    b = 0;
+                }
             }
             up++;
         } else {
@@ -1357,18 +1401,31 @@ __global__ void __launch_bounds__(BLK) k_node_prep(RoundArgs a, const unsigned l
         ocnt[i] = 0;               // consume writes the count of every node it runs
         bs += b;
         ws += w;
+        BTERM(BT_TOTAL, b);
     }
+#ifdef PSIM_BOUND_TERMS
+    if (blockIdx.x == 0 && threadIdx.x == 0) bt[BT_ROUNDS] = 1;
+    for (int k = 0; k < BT_N; k++) {
+        unsigned long long v = bt[k];
+        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+        if ((threadIdx.x & 63) == 0 && v) atomicAdd(&g_bterm[k], v);
+    }
+#endif
     for (int o = 32; o > 0; o >>= 1) {
         up += __shfl_xor(up, o);
         drop += __shfl_xor(drop, o);
         bs += __shfl_xor(bs, o);
         ws += __shfl_xor(ws, o);
+        qp += __shfl_xor(qp, o);
+        qf += __shfl_xor(qf, o);
     }
     if ((threadIdx.x & 63) == 0) {
         if (up) atomicAdd(&s_up, up);
         if (drop) atomicAdd(&s_drop, drop);
         if (bs) atomicAdd(&s_b, bs);
         if (ws) atomicAdd(&s_w, ws);
+        if (qp) atomicAdd(&s_qp, qp);
+        if (qf) atomicAdd(&s_qf, qf);
     }
     __syncthreads();
     // the tile's sum of the packed words (wrapping like them past 2^32
@@ -1383,7 +1440,11 @@ __global__ void __launch_bounds__(BLK) k_node_prep(RoundArgs a, const unsigned l
     // same-address atomic per block serialised 4096 adds at L2 every round)
     if (threadIdx.x == 0) btot[blockIdx.x] = s_b;
     if (threadIdx.x < NST) {
-        uint64_t v = threadIdx.x == ST_UP ? s_up : threadIdx.x == ST_DROPPED ? s_drop : 0ull;
+        // (state_bytes, R0: the rows of the nodes the phase kernels run, read
+        // and written once -- SURVEY 8(d)'s 416 B of HyParView + Plumtree state)
+        uint64_t v = threadIdx.x == ST_UP ? s_up : threadIdx.x == ST_DROPPED ? s_drop : threadIdx.x == ST_PROC ? s_qp
+                   : threadIdx.x == ST_FAIL ? s_qf : threadIdx.x == ST_BYTES && !a.pl ? s_w * (2 * NODE_STATE_BYTES)
+                   : 0ull;
         part[(size_t)blockIdx.x * NST + threadIdx.x] = v;
     }
 }
@@ -2177,6 +2238,10 @@ int phase_events_prepare(psim_handle* h, Shard* s, const RoundCtl& ctl, RoundArg
     // events (k_crash, k_join, the partition copy): rebuilt only then
     a.upart_dirty = !s->upart_valid ||
                     (events && (ctl.crashes || !h->pend_join.empty() || h->pend_part_set || h->pend_part_clear));
+    // (a crash only disconnects, and a restarted peer's holders dropped it
+    // in the EXIT of its crash round: neither wakes a quiet node)
+    a.lazy_wake = !s->upart_valid || (events && (h->pend_part_set || h->pend_part_clear || h->faults_dirty ||
+                                                 !h->pend_lv_a.empty()));
     s->upart_valid = true;
     if (events) {
         KTimer t(h, s, KT_EVENTS);
@@ -3801,6 +3866,20 @@ int psim_step(psim_handle* h, uint32_t n_rounds, psim_round_stats* stats) {
     }
     // (diagnostic: the buffers' high-water marks, printed as they rise)
     static const bool trace = getenv("PSIM_TRACE_BOUND") != nullptr;
+#ifdef PSIM_BOUND_TERMS
+    if (trace) {
+        unsigned long long v[BT_N];
+        if (hipMemcpyFromSymbol(v, HIP_SYMBOL(g_bterm), sizeof v) == hipSuccess) {
+            static const char* nm[BT_N] = {"resp", "timer", "push", "push_ne", "npush", "lazy", "on", "nl", "lc",
+                                           "crash", "xbot", "bump", "total", "c", "quiet", "rounds"};
+            std::fprintf(stderr, "psim: bound terms to round %llu:", (unsigned long long)h->round);
+            for (int k = 0; k < BT_N; k++) std::fprintf(stderr, " %s=%llu", nm[k], v[k]);
+            std::fprintf(stderr, "\n");
+            std::memset(v, 0, sizeof v);
+            (void)hipMemcpyToSymbol(HIP_SYMBOL(g_bterm), v, sizeof v);
+        }
+    }
+#endif
     if (trace)
         for (Shard* s : h->shards)
             if (s->pin[PIN_TMAX] > s->trace_tmax || s->pin[PIN_MMAX] > s->trace_mmax) {
@@ -4337,8 +4416,10 @@ int psim_kernel_times(psim_handle* h, const char** names, double* ms, uint64_t* 
 // stats rows every block leaves, before the route sums them), in the order
 // k_relay, k_shuf, k_lite_half / k_consume_lite, k_consume, k_ptl,
 // k_pt: out[4 k] nodes processed (stats nodes_processed), out[4 k + 1]
-// records delivered, out[4 k + 2] records emitted, out[4 k + 3] 0.  Returns
-// the number of kernels (6); 0 for the pluggable manager's one kernel.
+// records delivered, out[4 k + 2] records emitted, out[4 k + 3] 0; with cap
+// >= 28 then k_node_prep's quiet lazy ticks (nodes processed without a
+// kernel).  Returns the number of entries (6 or 7); 0 for the pluggable
+// manager's one kernel.
 int psim_debug_kernel_counts(psim_handle* h, uint64_t* out, int cap) {
     if (!h || !out || cap < 24) return PSIM_EINVAL;
     if (h->cfg.manager == PSIM_MANAGER_PLUGGABLE) return 0;
@@ -4350,8 +4431,10 @@ int psim_debug_kernel_counts(psim_handle* h, uint64_t* out, int cap) {
     // row ranges (make_args: prepare, consume, relay, pt, shuf, lite, ptl)
     const uint32_t b_cons = s->pgrid, b_rel = b_cons + s->cgrid, b_pt = b_rel + s->rgrid, b_sh = b_pt + s->tgrid,
                    b_li = b_sh + s->sgrid, b_pl = b_li + s->lgrid, b_end = b_pl + s->qgrid;
-    const uint32_t rng[6][2] = {{b_rel, b_pt}, {b_sh, b_li}, {b_li, b_pl}, {b_cons, b_rel}, {b_pl, b_end}, {b_pt, b_sh}};
-    for (int k = 0; k < 6; k++) {
+    const uint32_t rng[7][2] = {{b_rel, b_pt}, {b_sh, b_li}, {b_li, b_pl}, {b_cons, b_rel}, {b_pl, b_end}, {b_pt, b_sh},
+                                {0, b_cons}};
+    const int nk = cap >= 28 ? 7 : 6;
+    for (int k = 0; k < nk; k++) {
         uint64_t v[3] = {0, 0, 0};
         for (uint32_t r = rng[k][0]; r < rng[k][1]; r++) {
             const uint64_t* row = st.data() + (size_t)r * NST;
@@ -4360,7 +4443,7 @@ int psim_debug_kernel_counts(psim_handle* h, uint64_t* out, int cap) {
         }
         out[4 * k] = v[0]; out[4 * k + 1] = v[1]; out[4 * k + 2] = v[2]; out[4 * k + 3] = 0;
     }
-    return 6;
+    return nk;
 }
 
 // diagnostic: per-phase s_memtime sums of k_consume / k_pt, k_consume_lite and

@@ -31,6 +31,9 @@ struct RoundArgs {
     // per-round scalars
     uint32_t crash_round, tracked_msg;
     uint32_t upart_dirty;       // this round's events changed F_UP or a partition: k_node_prep rebuilds upart
+    uint32_t lazy_wake;         // this round's events may connect a quiet node's outstanding peers (a
+                                // partition change, faults, a leave, a fresh or restored state): every
+                                // quiet node runs its lazy tick (k_node_prep, F_LAZY)
     // node state: flags/part are replicated and indexed by global id;
     // every other row is local (index = id - lo)
     uint8_t* flags;

@@ -358,14 +358,15 @@ class Simulator(_Driver):
         self._check(self._extra["get_exchange_stats"](self._h, C.byref(r), C.byref(b)), "get_exchange_stats")
         return r.value, b.value
 
-    KERNELS = ("k_relay", "k_shuf", "k_lite_half", "k_consume", "k_ptl", "k_pt")
+    # (k_node_prep: the quiet lazy ticks it counts without running the node)
+    KERNELS = ("k_relay", "k_shuf", "k_lite_half", "k_consume", "k_ptl", "k_pt", "k_node_prep")
 
     def kernel_counts(self):
         """{kernel: (nodes processed, delivered, emitted)} of the last round,
         per node-round kernel (psim_debug_kernel_counts); {} under the
         pluggable manager."""
-        out = (C.c_uint64 * 24)()
-        k = self._extra["debug_kernel_counts"](self._h, out, 24)
+        out = (C.c_uint64 * 28)()
+        k = self._extra["debug_kernel_counts"](self._h, out, 28)
         self._check(min(k, 0), "debug_kernel_counts")
         return {self.KERNELS[i]: (out[4 * i], out[4 * i + 1], out[4 * i + 2]) for i in range(k)}
 
