@@ -2196,6 +2196,9 @@ DEV void block_append(bool go, const uint4& D, uint4* desc, uint32_t* cnt, uint3
 #ifndef PSIM_RELAY_WAVES       // (5: 95 VGPRs, no spills; 0.532 -> 0.527 ms a phase against 4, profiles/r04 ab6)
 #define PSIM_RELAY_WAVES 5
 #endif
+#ifndef PSIM_RELAY_FJ         // FORWARD_JOIN relays on k_relay's lanes (0: k_consume's waves, for A/B)
+#define PSIM_RELAY_FJ 1
+#endif
 #ifndef PSIM_PTL_BIN          // k_ptl's list binned by BROADCAST presence (0: one list, for A/B)
 #define PSIM_PTL_BIN 1
 #endif
@@ -2207,7 +2210,7 @@ __global__ void __launch_bounds__(256, PSIM_RELAY_WAVES) k_relay(RoundArgs) {
     // the node-round phase starts here: its span's first stamp (the last is
     // taken by the first kernel after the phase, RoundArgs::ktime)
     if (blockIdx.x == 0 && threadIdx.x == 0) kargs().ktime[0] = __builtin_amdgcn_s_memrealtime();
-    enum { R_PROC, R_DELIV, R_SHUF, R_FAIL, R_DIGEST, R_BOUND, R_N };
+    enum { R_PROC, R_DELIV, R_SHUF, R_FAIL, R_DIGEST, R_BOUND, R_DELIV_FJ, R_FJ, R_N };
     __shared__ unsigned long long sst[R_N];
     __shared__ uint32_t wc5[9][5];                    // per list: the wave counts, then the block's base
     if (threadIdx.x < R_N) sst[threadIdx.x] = 0;
@@ -2242,7 +2245,7 @@ __global__ void __launch_bounds__(256, PSIM_RELAY_WAVES) k_relay(RoundArgs) {
             // the inbox: how many HyParView messages, and whether each is a
             // SHUFFLE with TTL left (a relay while |active| > 1)
             uint32_t hvn = 0;
-            bool all_relay = true, all_shuf = true, term_out = false;
+            bool all_relay = true, all_shuf = true, term_out = false, fjn = false;
             bcast = false; term = false; extra = (tf & DESC_SHUFFLE) != 0;
             const uint32_t av[8] = {act0.x, act0.y, act0.z, act0.w, act1.x, act1.y, act1.z, act1.w};
             // (four records' first 16 B issued before any is waited on: a
@@ -2262,8 +2265,17 @@ __global__ void __launch_bounds__(256, PSIM_RELAY_WAVES) k_relay(RoundArgs) {
                     if (type < PSIM_MSG_PT_BROADCAST || type >= PSIM_MSG_XBOT_OPTIMIZATION) {   // (X-BOT's: heavy)
                         hvn++;
                         maps |= type <= PSIM_MSG_NEIGHBOR_ACCEPTED;   // id maps (hv:703-1089)
-                        const bool relays = ((tt >> 8) & 0xFF) > 0 && h.act_n > 1;
-                        all_relay &= type == PSIM_MSG_SHUFFLE && ((tt >> 8) & 0xFF) > 0;
+                        const uint32_t ttl = (tt >> 8) & 0xFF;
+                        const bool relays = ttl > 0 && h.act_n > 1;
+                        // a FORWARD_JOIN with TTL left, off the passive walk's
+                        // step (TTL == PRWL adds the joiner to the passive
+                        // view) and four active members or more (a pick
+                        // whatever its three omits): a relay like a
+                        // SHUFFLE's (hv:867-870, :899-906)
+                        const bool fj = PSIM_RELAY_FJ && !a.xbot && type == PSIM_MSG_FORWARD_JOIN && ttl > 0 &&
+                                        ttl != a.prwl && h.act_n >= 4;
+                        fjn |= fj;
+                        all_relay &= (type == PSIM_MSG_SHUFFLE && ttl > 0) || fj;
                         all_shuf &= type == PSIM_MSG_SHUFFLE || type == PSIM_MSG_SHUFFLE_REPLY;
                         // a walk that ends here replies to its Sender: maybe_connect
                         // (hv:1127) opens a lingering connection to a Sender outside
@@ -2307,8 +2319,25 @@ __global__ void __launch_bounds__(256, PSIM_RELAY_WAVES) k_relay(RoundArgs) {
             // X-BOT: a due xbot_execution, or connection pids stopped last
             // round (their 'EXIT's): k_consume
             const bool xwork = a.xbot && (h.conn_cl || (D.z & DESC_XBOT_BIT));
-            heavy = exits || fresh || ((tf & DESC_PROMO) && h.act_n < a.min_active) || (hvn && !all_shuf) ||
-                    term_out || cdown || xwork;
+            // (a FORWARD_JOIN relay ends in notify/1 (hv:921): a no-op only
+            // while Plumtree's all_members is the active view -- else its
+            // update belongs to k_consume)
+            bool fj_ok = true;
+            if (fjn && a.plumtree) {
+                const uint4* pr = reinterpret_cast<const uint4*>(a.pt_all + li * PSIM_PT_MEMBERS_CAP);
+                const uint4 p0 = pr[0], p1 = pr[1];
+                const uint32_t pv[8] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w};
+                fj_ok = h.all_n == h.act_n;
+#pragma unroll
+                for (int j = 0; j < 8; j++) {
+                    bool in = false;
+#pragma unroll
+                    for (int k = 0; k < 8; k++) in |= (uint32_t)k < h.all_n && pv[k] == av[j];
+                    fj_ok &= (uint32_t)j >= h.act_n || in;
+                }
+            }
+            heavy = exits || fresh || ((tf & DESC_PROMO) && h.act_n < a.min_active) ||
+                    (hvn && !all_shuf && !(all_relay && fj_ok)) || term_out || cdown || xwork;
             // SHUFFLE terminals and replies (with whatever relays and shuffle
             // start come with them): k_consume_lite
             lite = !heavy && hvn && !(all_relay && h.act_n > 1);
@@ -2400,16 +2429,21 @@ __global__ void __launch_bounds__(256, PSIM_RELAY_WAVES) k_relay(RoundArgs) {
         const uint32_t A[8] = {act0.x, act0.y, act0.z, act0.w, act1.x, act1.y, act1.z, act1.w};
         uint64_t rng = h.rng;
         uint32_t seq = 0;
-        for (uint32_t jr = 0; relay && jr < ik; jr++) {  // the SHUFFLE relays, in inbox order
+        for (uint32_t jr = 0; relay && jr < ik; jr++) {  // the SHUFFLE / FORWARD_JOIN relays, in inbox order
             const Msg* rp = a.rec_in + D.y + jr;
             const uint32_t tt = rp->tt;
             if ((tt & 0xFF) >= PSIM_MSG_PT_BROADCAST) continue;
+            const bool fj = (tt & 0xFF) == PSIM_MSG_FORWARD_JOIN;
             const uint32_t ttl = (tt >> 8) & 0xFF, nex = (tt >> 16) & 0xFF, src = rp->src;
-            v[R_DELIV]++;
-            // select_random(Active, [Sender, Myself]) (hv:1346-1356)
+            // (FORWARD_JOIN: the joiner and its epoch)
+            const uint32_t jq = fj ? rp->a0 : NONE, jpe = fj ? rp->a1 : 0u;
+            v[fj ? R_DELIV_FJ : R_DELIV]++;
+            // select_random(Active, [Sender, Myself]) (hv:1346-1356); a
+            // FORWARD_JOIN's omits the joiner too (hv:867-870)
             uint32_t elig = 0;
 #pragma unroll
-            for (int j = 0; j < 8; j++) elig |= (j < h.act_n && A[j] != src && A[j] != id) ? (1u << j) : 0u;
+            for (int j = 0; j < 8; j++)
+                elig |= (j < h.act_n && A[j] != src && A[j] != id && A[j] != jq) ? (1u << j) : 0u;
             const uint32_t cnt = __popc(elig);
             if (cnt) {
                 uint32_t k;
@@ -2430,15 +2464,20 @@ __global__ void __launch_bounds__(256, PSIM_RELAY_WAVES) k_relay(RoundArgs) {
                 // do_send_message: maybe_connect + find, then the dispatch draw
                 if (r < a.n_nodes && up == me_part) {
                     rng++;
-                    const uint4* ex = reinterpret_cast<const uint4*>(rp->ex);
-                    const uint4 e0 = ex[0], e1 = ex[1];
-                    uint32_t X[8] = {e0.x, e0.y, e0.z, e0.w, e1.x, e1.y, e1.z, e1.w};
+                    uint32_t X[8] = {};
+                    if (!fj) {
+                        const uint4* ex = reinterpret_cast<const uint4*>(rp->ex);
+                        const uint4 e0 = ex[0], e1 = ex[1];
+                        const uint32_t E[8] = {e0.x, e0.y, e0.z, e0.w, e1.x, e1.y, e1.z, e1.w};
 #pragma unroll
-                    for (int j = 0; j < 8; j++) X[j] = (uint32_t)j < nex ? X[j] : 0u;
-                    v[R_DIGEST] += relay_emit(a, D.w + seq, r, id, PSIM_MSG_SHUFFLE | ((ttl - 1) << 8) | (nex << 16),
-                                              seq, 0u, 0u, 0u, X);
+                        for (int j = 0; j < 8; j++) X[j] = (uint32_t)j < nex ? E[j] : 0u;
+                    }
+                    v[R_DIGEST] += relay_emit(a, D.w + seq, r, id,
+                                              fj ? PSIM_MSG_FORWARD_JOIN | ((ttl - 1) << 8)
+                                                 : PSIM_MSG_SHUFFLE | ((ttl - 1) << 8) | (nex << 16),
+                                              seq, fj ? jq : 0u, jpe, 0u, X);
                     seq++;
-                    v[R_SHUF]++;
+                    v[fj ? R_FJ : R_SHUF]++;
                 } else {
                     v[R_FAIL]++;
                 }
@@ -2466,6 +2505,7 @@ __global__ void __launch_bounds__(256, PSIM_RELAY_WAVES) k_relay(RoundArgs) {
     for (uint32_t k = threadIdx.x; k < NST; k += blockDim.x)
         row[k] = k == ST_PROC ? sst[R_PROC] : k == ST_DELIV + PSIM_MSG_SHUFFLE ? sst[R_DELIV]
                : k == ST_EMIT + PSIM_MSG_SHUFFLE ? sst[R_SHUF] : k == ST_FAIL ? sst[R_FAIL]
+               : k == ST_DELIV + PSIM_MSG_FORWARD_JOIN ? sst[R_DELIV_FJ] : k == ST_EMIT + PSIM_MSG_FORWARD_JOIN ? sst[R_FJ]
                : k == ST_DIGEST ? sst[R_DIGEST] : k == ST_BOUND ? sst[R_BOUND] : 0ull;
 }
 

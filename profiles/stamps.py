@@ -56,6 +56,7 @@ def main():
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--schedule", default="survey")
+    p.add_argument("--workload", default="C", choices=("C", "E"))
     a = p.parse_args()
     from partisan_amd import Simulator, _lib
     from partisan_amd import workloads as W
@@ -66,7 +67,7 @@ def main():
     lib.psim_debug_stamps.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
     buf = (C.c_ulonglong * 96)()
     sim = Simulator(default_config(n_nodes=a.nodes, seed=1))
-    sched = W.BenchSchedule("C", a.schedule, a.nodes, 1, a.warmup)
+    sched = W.BenchSchedule(a.workload, a.schedule, a.nodes, 1, a.warmup)
     boot, until = sched.bootstrap()
     sim.run_schedule(boot, until)
     for i in range(sched.t_start):
@@ -82,7 +83,7 @@ def main():
     lib.psim_debug_stamps(buf, 96)
     st = np.concatenate(st)
     v = np.array(buf[:], np.float64)
-    print(f"{a.schedule} schedule, {a.nodes} nodes, rounds {a.steps}: processed {int(st['nodes_processed'].sum())} "
+    print(f"{a.workload}, {a.schedule} schedule, {a.nodes} nodes, rounds {a.steps}: processed {int(st['nodes_processed'].sum())} "
           f"delivered {int(st['delivered'].sum())} emitted {int(st['emitted'].sum())} (s_memtime ticks)")
     dl = st["delivered"].sum(axis=0) / a.steps
     print("delivered/round: " + ", ".join(f"{n}={int(dl[i])}" for i, n in enumerate(HV + PT) if dl[i]))
