@@ -2229,6 +2229,10 @@ __global__ void __launch_bounds__(256, PSIM_RELAY_WAVES) k_relay(RoundArgs) {
         uint32_t ik = 0, oend = 0;
         uint4 act0 = make_uint4(0, 0, 0, 0), act1 = act0;
         uint32_t me_part = 0;
+        uint32_t hvm = 0;                             // the HyParView records among the first 32
+        uint8_t fl0 = 0;                              // (the flag byte, read with the rows: read after
+                                                      // the relays' stores, its wait drained them --
+                                                      // gfx9 counts loads and stores in one in-order counter)
         if (P < na) {
             D = a.desc[P];
             const uint32_t id = D.x, tf = D.z >> 28;
@@ -2242,9 +2246,11 @@ __global__ void __launch_bounds__(256, PSIM_RELAY_WAVES) k_relay(RoundArgs) {
             act0 = ar[0];
             act1 = ar[1];
             me_part = a.part[id];
+            fl0 = a.flags[id];
             // the inbox: how many HyParView messages, and whether each is a
             // SHUFFLE with TTL left (a relay while |active| > 1)
             uint32_t hvn = 0;
+            hvm = 0;
             bool all_relay = true, all_shuf = true, term_out = false, fjn = false;
             bcast = false; term = false; extra = (tf & DESC_SHUFFLE) != 0;
             const uint32_t av[8] = {act0.x, act0.y, act0.z, act0.w, act1.x, act1.y, act1.z, act1.w};
@@ -2264,6 +2270,7 @@ __global__ void __launch_bounds__(256, PSIM_RELAY_WAVES) k_relay(RoundArgs) {
                     bcast |= j + q < ik && type == PSIM_MSG_PT_BROADCAST;
                     if (type < PSIM_MSG_PT_BROADCAST || type >= PSIM_MSG_XBOT_OPTIMIZATION) {   // (X-BOT's: heavy)
                         hvn++;
+                        hvm |= j + q < 32 ? 1u << (j + q) : 0u;
                         maps |= type <= PSIM_MSG_NEIGHBOR_ACCEPTED;   // id maps (hv:703-1089)
                         const uint32_t ttl = (tt >> 8) & 0xFF;
                         const bool relays = ttl > 0 && h.act_n > 1;
@@ -2429,7 +2436,17 @@ __global__ void __launch_bounds__(256, PSIM_RELAY_WAVES) k_relay(RoundArgs) {
         const uint32_t A[8] = {act0.x, act0.y, act0.z, act0.w, act1.x, act1.y, act1.z, act1.w};
         uint64_t rng = h.rng;
         uint32_t seq = 0;
-        for (uint32_t jr = 0; relay && jr < ik; jr++) {  // the SHUFFLE / FORWARD_JOIN relays, in inbox order
+        // the SHUFFLE / FORWARD_JOIN relays, in inbox order: a relay lane's
+        // HyParView records (hvm; every record of an inbox past 32); a
+        // Plumtree record's type word is not read again -- each such load
+        // after a relay's stores waited for them (one in-order counter)
+        const bool big = ik > 32;
+        uint32_t rm = relay ? hvm : 0u;
+        for (uint32_t jr = 0; relay && (big ? jr < ik : rm != 0); jr++) {
+            if (!big) {
+                jr = (uint32_t)__ffs(rm) - 1;
+                rm &= rm - 1;
+            }
             const Msg* rp = a.rec_in + D.y + jr;
             const uint32_t tt = rp->tt;
             if ((tt & 0xFF) >= PSIM_MSG_PT_BROADCAST) continue;
@@ -2487,8 +2504,7 @@ __global__ void __launch_bounds__(256, PSIM_RELAY_WAVES) k_relay(RoundArgs) {
         a.ocnt[li] = seq;
         v[R_BOUND] += seq > oend - D.w ? 1u : 0u;
         if (!to_pt) {                                 // (k_ptl / k_pt write the byte of their nodes)
-            const uint8_t fl = a.flags[id];
-            a.flags[id] = (uint8_t)((fl & (F_UP | F_CRASHED)) | (h.out_n ? F_LAZY : 0) |
+            a.flags[id] = (uint8_t)((fl0 & (F_UP | F_CRASHED)) | (h.out_n ? F_LAZY : 0) |
                                     (min((uint32_t)h.out_n, 15u) << F_OUTN_SHIFT) |
                                     (h.act_n < a.min_active ? F_LOWACT : 0));
         }
