@@ -1288,24 +1288,33 @@ __global__ void __launch_bounds__(BLK) k_node_prep(RoundArgs a, const unsigned l
                 // reset -- plus one per message handled before; the push's
                 // sends need an active connection: at most two per active
                 // member (its atom and its node_spec identity, App. A Q6)
+                // (round 6: a slot's pushes and lazy adds together are at most
+                // the root's eager and lazy sets at round start -- or the
+                // common eagers of a new root or a reset -- plus one per
+                // message handled before: update_peers/5 (pt:593-609) adds one
+                // peer a message to their union, and the pushes go to the
+                // eager set, the adds to the lazy one (pt:374-378))
                 const unsigned long long bm = c ? bm_ : 0ull;
                 const uint32_t pushes = (uint32_t)__popcll(bm) + (origin ? 1u : 0u);
                 const bool lazy = a.plumtree && due(a.lazy_tick_period, r, st);
-                uint32_t lazy_add = 0;
+                uint32_t lazy_add = 0, push_sum = 0, union_sum = 0;
                 if (pushes) {
                     const uint4 r0 = *reinterpret_cast<const uint4*>(a.pt_rt + (size_t)i * RT_WORDS);
                     const uint2 cn = *reinterpret_cast<const uint2*>(a.pt_rt + (size_t)i * RT_WORDS + RT_EN);
                     const uint32_t rts[4] = {r0.x, r0.y, r0.z, r0.w};
                     auto push = [&](uint32_t root) {
-                        uint32_t ne = PSIM_PT_MEMBERS_CAP, nl = 0;
+                        uint32_t ne = PSIM_PT_MEMBERS_CAP, nl = 0, ne0 = 0;
 #pragma unroll
                         for (int k = 0; k < PSIM_PT_ROOTS; k++)
                             if (rts[k] == root) {
-                                ne = max(ne, (cn.x >> (8 * k)) & 0xFFu);
+                                ne0 = (cn.x >> (8 * k)) & 0xFFu;
+                                ne = max(ne, ne0);
                                 nl = (cn.y >> (8 * k)) & 0xFFu;
                             }
-                        b += min(2u * PSIM_ACTIVE_CAP, ne + c);
+                        const uint32_t pb = min(2u * PSIM_ACTIVE_CAP, ne + c);
+                        push_sum += pb;
                         lazy_add += nl + c;
+                        union_sum += min(pb + nl + c, max((uint32_t)PSIM_PT_MEMBERS_CAP, ne0 + nl) + c);
                         BTERM(BT_PUSH, min(2u * PSIM_ACTIVE_CAP, ne + c));
                         BTERM(BT_PUSH_NE, min(2u * PSIM_ACTIVE_CAP, ne));
                         BTERM(BT_NPUSH, 1);
@@ -1320,12 +1329,18 @@ __global__ void __launch_bounds__(BLK) k_node_prep(RoundArgs a, const unsigned l
                 // PT_OUT_CAP
                 // (the flag byte's nibble is min(out_n, 15) after the node's
                 // last round: the header only when it saturates)
+                // (with the tick: the pushes P and the tick's IHAVEs, at most
+                // min(PT_OUT_CAP, on + L), where P + L is at most the slots'
+                // union term)
                 if (lazy) {
                     const uint32_t fo = (uint32_t)f >> F_OUTN_SHIFT;
                     const uint32_t on = fo < 15 ? fo : (uint32_t)x.out_n;
-                    b += min((uint32_t)PSIM_PT_OUT_CAP, on + lazy_add);
-                    BTERM(BT_LAZY, min((uint32_t)PSIM_PT_OUT_CAP, on + lazy_add));
+                    const uint32_t pl = min(push_sum + min((uint32_t)PSIM_PT_OUT_CAP, on + lazy_add), on + union_sum);
+                    b += pl;
+                    BTERM(BT_LAZY, pl - push_sum);
                     BTERM(BT_ON, on);
+                } else {
+                    b += push_sum;
                 }
                 if (pushes) BTERM(BT_C, c);
                 // a crash round: a NEIGHBOR_REQUEST per crashed active member
@@ -1800,7 +1815,7 @@ int bits_for(uint64_t n) {
 //   RCAP_FREE_FRAC of the free memory (else RCAP_PER_NODE, growing);
 //   the outbox: RESERVE_PER_NODE slots per node, or what is left after the
 //   route, less OUTBOX_SPARE (a growth past it still works, slowly)
-constexpr uint64_t RESERVE_PER_NODE = 32;   // outbox slots per node reserved up front
+constexpr uint64_t RESERVE_PER_NODE = 24;   // outbox slots per node reserved up front (round 6: 32 before the union bound)
 constexpr uint64_t RCAP_PER_NODE = 4;       // initial route capacity (records) per node
 constexpr uint64_t RCAP_RESERVE = 8;        // ... reserved up front where it fits
 constexpr double RCAP_FREE_FRAC = 0.30;
