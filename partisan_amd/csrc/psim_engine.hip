@@ -271,6 +271,9 @@ constexpr uint32_t RR_REG = PSIM_RR_REG;   // k_bucket_route: pairs a thread hol
 // most W destinations), so W >= RUN_LDS; its run-start scan gives each
 // thread W / RR_THREADS counts
 constexpr uint32_t WSHIFT_MIN = 11, WSHIFT_MAX = 13;
+constexpr uint32_t ROUTE_LIDX = 8192;   // k_bucket_route: a bucket's source indices LDS holds (at W = 2^11)
+static_assert((1u << WSHIFT_MIN) * 16 + ROUTE_LIDX * 4 + (PSIM_RR_THREADS + 4) * 4 <= 80 * 1024,
+              "k_bucket_route at W = 2^11 with its indices in LDS: two blocks a CU");
 static_assert((1u << WSHIFT_MIN) >= RUN_LDS, "k_bucket_route: the sort buffer and the long-run list share 2 W words");
 static_assert((1u << WSHIFT_MIN) % RR_THREADS == 0, "k_bucket_route: W / RR_THREADS counts a thread");
 static_assert((1u << WSHIFT_MAX) * 16 <= 160 * 1024, "k_bucket_route: 16 W bytes of LDS");
@@ -978,7 +981,7 @@ __global__ void __launch_bounds__(RR_THREADS) k_bucket_route(
     const uint2* __restrict__ pairs, const Msg* __restrict__ rec, const Wire* __restrict__ heads,
     const Wire* __restrict__ tails, uint32_t* rank, unsigned long long* cb,
     unsigned long long* bmask, uint32_t* in_beg, uint32_t* idx, uint32_t* tmp, Msg* __restrict__ inbox, uint64_t* hm,
-    uint64_t cap, uint32_t* ctl, const uint32_t* gcnt, uint32_t capb, uint32_t round1, StatsIn st) {
+    uint64_t cap, uint32_t* ctl, const uint32_t* gcnt, uint32_t capb, uint32_t round1, StatsIn st, uint32_t lcap) {
     if (*ctl) return;                                 // an aborted batch (run_batch)
     // (the dynamic words hold 64-bit masks: 8-byte aligned -- a 4-byte static
     // word in front of them misaligned ds_or_b64 and faulted; the long-run
@@ -1025,6 +1028,12 @@ __global__ void __launch_bounds__(RR_THREADS) k_bucket_route(
     }
     pairs += q0;                                      // (pair i of the bucket at pairs[i], its rank at rank[i])
     rank += q0;
+    // the bucket's run-ordered source indices: in LDS after the 4 W words when
+    // they fit (lcap > 0: the host sized the dynamic LDS for them; round 6 --
+    // in memory, the runs' sorts and the gather each read back what the
+    // placement had just stored, every such load behind the block's stores),
+    // else in idx
+    uint32_t* const ix = lcap && s1 - s0 <= lcap ? sm + 4 * W : idx + s0;
     for (uint32_t j = threadIdx.x; j < 4 * W; j += blockDim.x) sm[j] = 0;
     if (threadIdx.x == 0) s_nl = 0;
     __syncthreads();
@@ -1096,11 +1105,11 @@ __global__ void __launch_bounds__(RR_THREADS) k_bucket_route(
     if (inreg) {
 #pragma unroll
         for (uint32_t k = 0; k < RR_REG; k++)
-            if (threadIdx.x + k * blockDim.x < np) idx[s0 + pre[px[k].x & wmask] + pr[k]] = px[k].y;
+            if (threadIdx.x + k * blockDim.x < np) ix[pre[px[k].x & wmask] + pr[k]] = px[k].y;
     } else {
         for (uint32_t p = threadIdx.x; p < np; p += blockDim.x) {
             const uint2 x = pairs[p];
-            idx[s0 + pre[x.x & wmask] + rank[p]] = x.y;
+            ix[pre[x.x & wmask] + rank[p]] = x.y;
         }
     }
     __syncthreads();                                  // the runs are in place (same block)
@@ -1115,7 +1124,7 @@ __global__ void __launch_bounds__(RR_THREADS) k_bucket_route(
             ll[atomicAdd(&s_nl, 1u)] = dl;
             continue;
         }
-        uint32_t* q = idx + s0 + pre[dl];
+        uint32_t* q = ix + pre[dl];
         uint32_t v[RUN_SHORT];
 #pragma unroll
         for (uint32_t t = 0; t < RUN_SHORT; t++) v[t] = t < k ? q[t] : 0xFFFFFFFFu;
@@ -1138,12 +1147,12 @@ __global__ void __launch_bounds__(RR_THREADS) k_bucket_route(
     const uint32_t nl = s_nl, wv = threadIdx.x >> 6, nwv = blockDim.x >> 6;
     for (uint32_t q = wv; q < nl; q += nwv) {
         const uint32_t dl = ll[q], k = cnt[dl];
-        if (k <= 64) wave_sort64(idx + s0 + pre[dl], k);
+        if (k <= 64) wave_sort64(ix + pre[dl], k);
     }
     __syncthreads();
     for (uint32_t q = 0; q < nl; q++) {               // (uniform)
         const uint32_t dl = ll[q], k = cnt[dl];
-        if (k > 64) sort_run_block(idx + s0 + pre[dl], k, tmp + s0 + pre[dl], sv);
+        if (k > 64) sort_run_block(ix + pre[dl], k, tmp + s0 + pre[dl], sv);
     }
     __syncthreads();
     // the bucket's records into the inbox in run order (16 B a lane; two
@@ -1153,11 +1162,11 @@ __global__ void __launch_bounds__(RR_THREADS) k_bucket_route(
         const uint32_t t2 = t + bd;
         uint4 a, c = make_uint4(0, 0, 0, 0);
         if (WIRE) {
-            a = wire_piece(heads, tails, idx[s0 + (t >> 2)], t & 3);
-            if (t2 < m4) c = wire_piece(heads, tails, idx[s0 + (t2 >> 2)], t2 & 3);
+            a = wire_piece(heads, tails, ix[t >> 2], t & 3);
+            if (t2 < m4) c = wire_piece(heads, tails, ix[t2 >> 2], t2 & 3);
         } else {
-            a = rec_piece(rec, idx[s0 + (t >> 2)], t & 3);
-            if (t2 < m4) c = rec_piece(rec, idx[s0 + (t2 >> 2)], t2 & 3);
+            a = rec_piece(rec, ix[t >> 2], t & 3);
+            if (t2 < m4) c = rec_piece(rec, ix[t2 >> 2], t2 & 3);
         }
         reinterpret_cast<uint4*>(&inbox[s0 + (t >> 2)])[t & 3] = a;
         if (t2 < m4) reinterpret_cast<uint4*>(&inbox[s0 + (t2 >> 2)])[t2 & 3] = c;
@@ -2522,7 +2531,12 @@ int route_group(psim_handle* h, Shard* s, bool dense, uint32_t m, bool fixed = f
     TRY(s->hoff.ensure(nh));
     TRY(s->rtot.ensure(nb));
     TRY(s->rbase.ensure(nb + 1));
-    const size_t lds_h = (size_t)nb * 4, lds_r = (size_t)W * 16;
+    // (k_bucket_route: 16 W bytes, and at W = 2^11 the bucket's source
+    // indices in LDS too when they fit -- 68 KiB a block, two blocks a CU;
+    // PSIM_ROUTE_LIDX=0: in memory, for A/B)
+    static const bool lidx_ok = !getenv("PSIM_ROUTE_LIDX") || atoi(getenv("PSIM_ROUTE_LIDX")) != 0;
+    const uint32_t lcap = lidx_ok && W == (1u << WSHIFT_MIN) ? ROUTE_LIDX : 0u;
+    const size_t lds_h = (size_t)nb * 4, lds_r = (size_t)W * 16 + (size_t)lcap * 4;
     // the round's stats rows (every node-phase kernel's blocks) are complete
     const uint32_t rows = s->pgrid + s->cgrid + s->rgrid + s->tgrid + s->sgrid + s->lgrid + s->qgrid;
     // (a batched rank round, fixed: the stats came summed in the message
@@ -2553,7 +2567,7 @@ int route_group(psim_handle* h, Shard* s, bool dense, uint32_t m, bool fixed = f
         k_bucket_route<false><<<nb, RR_THREADS, lds_r, s->stream>>>(
             n, wshift, h->rr_reg, nullptr, s->pairs.p, in.rec, nullptr, nullptr, s->rank.p, s->cb.p, s->bmask.p,
             s->in_beg.p, s->ivals.p, s->tmp.p, s->inbox.p, s->pin_dev + PIN_M, s->rcap, s->ctl.p, s->gcnt.p, capb,
-            s->batch_round1, st);
+            s->batch_round1, st, lcap);
         HIP_TRY(hipGetLastError());
         return PSIM_OK;
     }
@@ -2578,12 +2592,12 @@ int route_group(psim_handle* h, Shard* s, bool dense, uint32_t m, bool fixed = f
         k_bucket_route<true><<<nb, RR_THREADS, lds_r, s->stream>>>(
             n, wshift, h->rr_reg, s->rbase.p, s->pairs.p, nullptr, in.wire, in.tails, s->rank.p, s->cb.p, s->bmask.p,
             s->in_beg.p, s->ivals.p, s->tmp.p, s->inbox.p, s->pin_dev + PIN_M, s->rcap, s->ctl.p, nullptr, 0u,
-            s->batch_round1, st);
+            s->batch_round1, st, lcap);
     else
         k_bucket_route<false><<<nb, RR_THREADS, lds_r, s->stream>>>(
             n, wshift, h->rr_reg, s->rbase.p, s->pairs.p, in.rec, nullptr, nullptr, s->rank.p, s->cb.p, s->bmask.p,
             s->in_beg.p, s->ivals.p, s->tmp.p, s->inbox.p, s->pin_dev + PIN_M, s->rcap, s->ctl.p, nullptr, 0u,
-            s->batch_round1, st);
+            s->batch_round1, st, lcap);
     HIP_TRY(hipGetLastError());
     return PSIM_OK;
 }
