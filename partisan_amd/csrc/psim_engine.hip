@@ -2546,10 +2546,11 @@ int route_group(psim_handle* h, Shard* s, bool dense, uint32_t m, bool fixed = f
                      s->stat_tile.p, s->stat_out.p, s->pin_dev + (size_t)s->stat_slot * PIN_STRIDE,
                      s->outx.p ? s->outx_top.p : nullptr, s->pin_dev};
     KTimer t(h, s, KT_SORT);
-    // (above 2^24 nodes the four passes: the fused route's fixed bucket
-    // regions hold 1.5x the route's pairs, ~3 GB more at 2^26 nodes, where
-    // the device is full -- E at 2^26 took 300 GB, profiles/r06/pass1)
-    if (!dense && !exact && h->route_fused && n <= (1u << 24)) {
+    // (up to 2^26 nodes: the fused route's fixed bucket regions hold 1.5x the
+    // route's pairs, ~3 GB more than the four passes at 2^26 nodes -- room
+    // since round 6's tighter outbox bound, 296 -> 274 GB for E at 2^26;
+    // beyond, the four passes)
+    if (!dense && !exact && h->route_fused && n <= (1u << 26)) {
         // a bucket's fixed region holds 1.5x its share of the route's
         // capacity: only a hot spot (a join storm) overflows one, and that
         // round goes through the four passes again (run_round, run_batch)
