@@ -48,6 +48,10 @@ constexpr uint32_t PREP_BLK = 1024;   // k_desc blocks (at most PREP_BLK of them
 #define PSIM_PREP_NPT 4       // (2: step 0.620 -> 0.615 ms at 2^20 against 1 node a thread, profiles/r05/ab_log.txt r6m, r6n)
 #endif
 constexpr uint32_t PREP_NPT = PSIM_PREP_NPT;   // k_node_prep: nodes a thread (loads a node ahead)
+#ifndef PSIM_PREP_CHUNK
+#define PSIM_PREP_CHUNK 4
+#endif
+constexpr uint32_t PREP_CHUNK = PSIM_PREP_CHUNK;   // k_node_prep: nodes a thread loads, works and stores together
 constexpr uint32_t DESC_RANGES = 4;   // k_node_prep ranges a k_desc block takes (at most DESC_RANGES * PREP_BLK)
 // pinned host words per shard (Shard::pin): NST stats, the consume span, the
 // outbox total, the routed record count -- stored by kernels, read by the host
@@ -1247,10 +1251,11 @@ __global__ void __launch_bounds__(BLK) k_node_prep(RoundArgs a, const unsigned l
         }
         return q;
     };
-    PrepIn nx = prep_in(i0 + threadIdx.x);
-    for (uint32_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
-        const PrepIn cur = nx;
-        nx = prep_in(i + blockDim.x);
+    // one node's packed (bound << 32 | work) word (no stores: gfx9 counts
+    // loads and stores in one in-order counter, so a load issued after a
+    // store waits for it -- the node's row loads behind the last node's
+    // stores were a store latency per node, 64 nodes a thread at 2^26)
+    auto node = [&](uint32_t i, const PrepIn& cur) -> uint64_t {
         uint8_t f = cur.f;
         uint64_t b = 0;
         uint32_t w = 0;
@@ -1419,13 +1424,39 @@ __global__ void __launch_bounds__(BLK) k_node_prep(RoundArgs a, const unsigned l
         } else {
             drop += c;
         }
-        // one scan gives both the outbox base (high word: the bounds) and
-        // the position in the active list (low word: the work flags)
-        packed[i] = (b << 32) | w;
-        ocnt[i] = 0;               // consume writes the count of every node it runs
         bs += b;
         ws += w;
         BTERM(BT_TOTAL, b);
+        // one scan gives both the outbox base (high word: the bounds) and
+        // the position in the active list (low word: the work flags)
+        return (b << 32) | w;
+    };
+    // PREP_CHUNK nodes a thread at a time: their inputs loaded together (the
+    // next chunk's issued before this chunk's stores), their words and the
+    // consume counts stored together after the chunk's work
+    PrepIn q[PREP_CHUNK], qn[PREP_CHUNK];
+    const uint32_t cstep = PREP_CHUNK * blockDim.x;
+#pragma unroll
+    for (uint32_t k = 0; k < PREP_CHUNK; k++) q[k] = prep_in(i0 + threadIdx.x + k * blockDim.x);
+    for (uint32_t c0 = i0 + threadIdx.x; c0 < i1; c0 += cstep) {
+        uint64_t pk[PREP_CHUNK];
+#pragma unroll
+        for (uint32_t k = 0; k < PREP_CHUNK; k++) {
+            const uint32_t i = c0 + k * blockDim.x;
+            pk[k] = i < i1 ? node(i, q[k]) : 0ull;
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < PREP_CHUNK; k++) qn[k] = prep_in(c0 + cstep + k * blockDim.x);
+#pragma unroll
+        for (uint32_t k = 0; k < PREP_CHUNK; k++) {
+            const uint32_t i = c0 + k * blockDim.x;
+            if (i < i1) {
+                packed[i] = pk[k];
+                ocnt[i] = 0;       // consume writes the count of every node it runs
+            }
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < PREP_CHUNK; k++) q[k] = qn[k];
     }
 #ifdef PSIM_BOUND_TERMS
     if (blockIdx.x == 0 && threadIdx.x == 0) bt[BT_ROUNDS] = 1;
